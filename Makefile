@@ -1,0 +1,26 @@
+# Builds the product library (HIP, gfx950 only) and the CPU oracle (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH)
+CSRC := dragonboat_amd/csrc
+LIBDIR := dragonboat_amd/lib
+LIB := $(LIBDIR)/libhipquorum.so
+OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o
+DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
+
+all: $(LIB) oracle
+
+$(LIBDIR)/%.o: $(CSRC)/%.hip $(DEPS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(LIBDIR) oracle/build
+
+.PHONY: all oracle clean

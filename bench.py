@@ -1,0 +1,309 @@
+#!/usr/bin/env python3
+"""Quorum-decision throughput of the MI355X batched quorum engine (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4] [--no-cpu]
+
+A step is one pass of the hot path over one batch of synthetic groups resident in HBM: for the
+headline workload (BASELINE configs[1], "c2") one hq_commit_dev launch over 1,048,576 groups x 3
+voters in the term-start form. Inputs are generated on the device from splitmix64 seeds and rotate
+over >= 1.1 GiB of distinct batches so that the 256 MiB Infinity Cache cannot serve them.
+
+N > 1: one process per GPU (torch.distributed.run), groups sharded clusterID % N
+(internal/server/partition.go:38), weak scaling (fixed groups per GPU), no data-path collective;
+the barrier and the max-over-ranks time use torch.distributed.
+
+Rank 0 prints ONE JSON line. `roofline.achieved` = algorithmic bytes per launch / average kernel
+duration measured with HIP events on the launching stream over the timed region;
+`cpu_baseline` = the C restatement (oracle/qref.c, test infrastructure) timed on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+HBM_MEASURED_COPY_GBS = 6290.0  # measured float4 copy ceiling (same table)
+ROTATE_BYTES = int(1.1 * (1 << 30))
+SEED_BASE = 0x5EED0000
+
+WORKLOADS = {
+    "c2": dict(cfg=1, kind="commit", G=1 << 20, n=3, form=0, mixed=False,
+               desc="1M groups x 3 voters, batched commit-index kernel (term-start form)"),
+    "c3": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=1, mixed=False,
+               desc="1M groups x 5 voters (4 full + 1 witness; observers never packed), "
+                    "commit + term-ring gather R=16"),
+    "c4": dict(cfg=3, kind="bits", G=16 << 20, n=7,
+               desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
+}
+
+
+def algo_bytes_per_group(w):
+    """bytes the decision must move per group."""
+    if w["kind"] == "commit":
+        n = w["n"]
+        return 8 * n + 32 if w["form"] == 0 else 8 * n + 40 + (1 if w["mixed"] else 0)
+    return 4 + 3 / 8   # ack, granted, rejected, n (u8 each) in; confirmed bit + 2-bit outcome out
+
+
+def decisions_per_group(w):
+    return 1 if w["kind"] == "commit" else 2
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
+
+
+class Dist:
+    """Rank bookkeeping; torch.distributed only when launched with WORLD_SIZE > 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            self.torch, self.dist = torch, dist
+            if torch.cuda.is_available():
+                torch.cuda.set_device(self.local_rank)
+                backend = "nccl"   # RCCL on ROCm
+            else:
+                backend = "gloo"
+            dist.init_process_group(backend=backend)
+            self.backend = backend
+
+    def barrier(self):
+        if self.torch is not None:
+            self.dist.barrier()
+
+    def sync_device(self):
+        if self.torch is not None and self.torch.cuda.is_available():
+            self.torch.cuda.synchronize()
+
+    def max(self, x: float) -> float:
+        if self.torch is None:
+            return x
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if self.torch is None:
+            return x
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.torch is not None:
+            self.dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- GPU legs -------
+def build_sets(ctx, hq, shard, w, d: "Dist"):
+    """Device-generated input batches for this rank, enough to rotate over ROTATE_BYTES."""
+    G = w["G"]
+    per_set = algo_bytes_per_group(w) * G
+    nsets = max(4, int(np.ceil(ROTATE_BYTES / per_set)))
+    rng = shard.rank_shard(d.rank, d.world, G)
+    seed = SEED_BASE + w["cfg"]
+    sets = []
+    for s in range(nsets):
+        spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
+                             cid_stride=rng.cid_stride)
+        if w["kind"] == "commit":
+            b = hq.alloc_commit(ctx, G, w["n"], w["form"], 16)
+            ctx.synth_commit_dev(spec, b.args())
+            sets.append(b)
+        else:
+            arrs = [ctx.empty(G, np.uint8) for _ in range(4)]
+            ctx.synth_bitmaps_dev(spec, *arrs)
+            conf = ctx.empty(hq.words64(G), np.uint64)
+            outc = ctx.empty(hq.words32(G), np.uint64)
+            sets.append((arrs, conf, outc))
+    ctx.sync()
+    return sets, per_set
+
+
+def run_gpu(w, steps, warmup, d: Dist):
+    from dragonboat_amd import hipquorum as hq
+    from dragonboat_amd import shard
+
+    ctx = hq.Context(d.local_rank)
+    sets, per_set = build_sets(ctx, hq, shard, w, d)
+    G = w["G"]
+    if w["kind"] == "commit":
+        seq = hq.commit_batch_array([sets[i % len(sets)].args() for i in range(steps)])
+        wseq = hq.commit_batch_array([sets[i % len(sets)].args() for i in range(max(1, warmup))])
+
+        def run(batch):
+            ctx.commit_many_dev(batch)
+    else:
+        seq, wseq = list(range(steps)), list(range(max(1, warmup)))
+
+        def run(idx):
+            for i in idx:
+                (da, dg, dr, dn), conf, outc = sets[i % len(sets)]
+                ctx.readindex_vote_dev(G, da, dg, dr, dn, 0, conf, outc)
+
+    if warmup > 0:
+        run(wseq)
+    ctx.sync()
+    d.sync_device()
+    d.barrier()
+    ctx.timing_reset()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    run(seq)
+    ctx.sync()
+    d.sync_device()
+    d.barrier()
+    t1 = time.perf_counter()
+    ctx.timing(False)
+    kernel_ms, launches = ctx.timing_read()
+    elapsed = d.max(t1 - t0)
+    avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+    total_groups = d.sum(float(G * steps))
+    res = dict(
+        elapsed=elapsed, launches=launches, avg_kernel_s=avg_kernel_s,
+        decisions=total_groups * decisions_per_group(w), nsets=len(sets),
+        bytes_per_launch=per_set,
+    )
+    ctx.close()
+    return res
+
+
+# ----------------------------------------------------------------------------- CPU leg --------
+def cpu_baseline(w, budget_s=8.0):
+    """The oracle (C restatement of the reference path) on a bounded sample of the workload."""
+    from oracle import qref
+
+    host_threads = min(16, os.cpu_count() or 1)
+    G = min(w["G"], 1 << 20)
+    s = qref.spec(SEED_BASE + w["cfg"], G, w["n"])
+    out = {}
+    if w["kind"] == "commit":
+        inp = qref.CommitInputs(s)
+
+        def one(nt):
+            inp.run(w["form"], False, nthreads=nt)
+    else:
+        inp = qref.BitmapInputs(s)
+
+        def one(nt):
+            qref.readindex_batch(inp.ack, inp.n_voting, 0, nthreads=nt)
+            qref.vote_batch(inp.granted, inp.rejected, inp.n_voting, 0, nthreads=nt)
+    for nt in (1, host_threads):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            one(nt)
+            passes += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget_s / 2:
+                break
+        out[nt] = (passes * G * decisions_per_group(w) / dt, passes, dt)
+    rate, passes, dt = out[host_threads]
+    return {
+        "value": rate, "unit": "decisions/s", "cores": host_threads, "kind": "port",
+        "sample": (f"{G} groups of the same workload and generator, {passes} passes in {dt:.1f} s "
+                   f"on {host_threads} host threads (oracle/qref.c -O3, C restatement of the "
+                   f"reference Go path; Go toolchain unavailable)"),
+        "single_thread_value": out[1][0],
+    }
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(p))[workload]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--extra", default="c3,c4",
+                    help="comma list of extra workloads reported under 'extra' ('' for none)")
+    args = ap.parse_args()
+
+    d = Dist()
+    if args.gpus != d.world:
+        log(f"--gpus {args.gpus} but WORLD_SIZE={d.world}: launch N>1 with torch.distributed.run")
+        if d.world == 1 and args.gpus > 1:
+            sys.exit(2)
+    w = WORKLOADS[args.workload]
+    r = run_gpu(w, args.steps, args.warmup, d)
+    extras = []
+    for name in [x for x in args.extra.split(",") if x and x != args.workload]:
+        we = WORKLOADS[name]
+        re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
+        extras.append((name, we, re_))
+    cpu = None
+    if d.rank == 0 and d.world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(w)
+    if d.rank == 0:
+        achieved = r["bytes_per_launch"] / r["avg_kernel_s"] / 1e9
+        line = {
+            "metric": "quorum-commit decisions/sec (whole node) + % HBM roofline at 1/2/4/8 GPUs",
+            "value": r["decisions"] / r["elapsed"],
+            "unit": "decisions/s",
+            "n_gpus": d.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": r["elapsed"] / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: device-generated splitmix64 batches (DESIGN.md), "
+                    f"{r['nsets']} distinct batches per GPU rotated (>= 1.1 GiB)",
+            "config": {
+                "workload": f"{args.workload}: {w['desc']}",
+                "groups_per_gpu": w["G"], "voters": w["n"],
+                "form": ("term_start" if w.get("form") == 0 else "ring")
+                if w["kind"] == "commit" else "bitmaps",
+                "global_groups_per_step": w["G"] * d.world,
+                "parallelism": f"shard{d.world} (clusterID % {d.world})",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
+                "kernel_avg_us": r["avg_kernel_s"] * 1e6,
+                "algorithmic_bytes_per_launch": r["bytes_per_launch"],
+                "measured_copy_ceiling_gbs": HBM_MEASURED_COPY_GBS,
+            },
+            "cpu_baseline": cpu,
+            "extra": [
+                {
+                    "workload": f"{n}: {we['desc']}",
+                    "value": re_["decisions"] / re_["elapsed"], "unit": "decisions/s",
+                    "kernel_avg_us": re_["avg_kernel_s"] * 1e6,
+                    "roofline_achieved_gbs": re_["bytes_per_launch"] / re_["avg_kernel_s"] / 1e9,
+                    "roofline_frac": re_["bytes_per_launch"] / re_["avg_kernel_s"] / 1e9
+                    / HBM_PEAK_GBS,
+                }
+                for n, we, re_ in extras
+            ],
+        }
+        print(json.dumps(line), flush=True)
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

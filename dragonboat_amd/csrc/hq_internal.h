@@ -1,0 +1,41 @@
+// hq_internal.h — shared between the runtime (hq_runtime.hip) and the kernels (hq_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/hipquorum.h"
+
+struct hq_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // kernel timing (hq_timing_*): event pairs recorded around every launch
+    bool timing = false;
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    size_t ev_used = 0;
+    double timed_ms = 0.0;
+    uint64_t timed_launches = 0;
+    // device workspace for the host-pointer entry points
+    void *ws = nullptr;
+    size_t ws_bytes = 0;
+    // host readback of the fallback count (hq_commit etc.)
+};
+
+namespace hq {
+
+int fail(hq_ctx *ctx, int code, const std::string &msg);
+int check_hip(hq_ctx *ctx, hipError_t e, const char *what);
+// bracket a launch with timing events when enabled
+int pre_launch(hq_ctx *ctx);
+int post_launch(hq_ctx *ctx, const char *what);
+int ensure_workspace(hq_ctx *ctx, size_t bytes);
+
+inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline uint64_t words64(uint64_t G) { return (G + 63) / 64; }
+inline uint64_t words32(uint64_t G) { return (G + 31) / 32; }  // 2-bit outcome words
+
+}  // namespace hq

@@ -1,0 +1,650 @@
+// hq_kernels.hip — CDNA4 (gfx950) kernels of the batched quorum engine and their _dev launchers.
+//
+// Every kernel is an HBM stream over structure-of-arrays group state: one lane owns one or more
+// whole groups, loads are coalesced (consecutive lanes -> consecutive groups), decisions are
+// integer min/max networks and popcounts in registers, and bitmap outputs are assembled with
+// wave-wide __ballot (64-bit on wave64). No LDS and no MFMA: nothing here is reused or a
+// contraction (DESIGN.md "Kernels").
+#include "hq_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;           // 4 waves of 64
+constexpr int kMaxBlocks = 256 * 16;  // grid-stride beyond 16 workgroups per CU
+
+struct CommitK {
+    uint64_t G, stride, nwords;
+    uint32_t n_max, R;
+    const uint64_t *match;
+    const uint8_t *nv;
+    const uint64_t *cin;
+    uint64_t *cout;
+    const uint64_t *last;
+    const uint64_t *tstart;
+    const uint64_t *term;
+    const uint64_t *ring;
+    uint64_t *changed;
+    uint64_t *fallback;
+};
+
+// ---- compare-exchange networks over u64 held in registers --------------------------------
+__device__ __forceinline__ void ce(uint64_t &a, uint64_t &b) {
+    const uint64_t lo = a < b ? a : b;
+    const uint64_t hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// Ascending odd-even transposition network, fully unrolled; the compiler drops the
+// compare-exchanges that do not reach the selected element.
+template <int N>
+__device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+#pragma unroll
+        for (int i = r & 1; i + 1 < N; i += 2) ce(v[i], v[i + 1]);
+    }
+}
+
+// The quorum-th largest match = matched[n - quorum] after an ascending sort (raft.go:902-903).
+template <int N>
+__device__ __forceinline__ uint64_t quorum_match_uniform(uint64_t (&v)[N]) {
+    if constexpr (N == 1) {
+        return v[0];
+    } else if constexpr (N == 2) {
+        return v[0] < v[1] ? v[0] : v[1];
+    } else if constexpr (N == 3) {  // median of 3: 3 compare-exchanges
+        ce(v[0], v[1]);
+        ce(v[1], v[2]);
+        return v[0] > v[1] ? v[0] : v[1];
+    } else {
+        sort_net<N>(v);
+        return v[N - (N / 2 + 1)];
+    }
+}
+
+// Runtime n <= N: slots >= n are padded with 0 (the minimum), so the (n/2+1)-th largest of the
+// padded N values is the (n/2+1)-th largest of the n real ones.
+template <int N>
+__device__ __forceinline__ uint64_t quorum_match_pern(uint64_t (&v)[N], int n) {
+    sort_net<N>(v);
+    const int idx = N - (n / 2 + 1);
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) r = (k == idx) ? v[k] : r;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t spread32(uint32_t x) {  // bit i -> bit 2i
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+}
+
+// One group's decision given its packed matches. FORM 0 = term-start, 1 = ring gather.
+template <int N, int FORM, bool PERN>
+__device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&m)[N], int n,
+                                       uint64_t cin, uint64_t last, uint64_t aux,
+                                       uint64_t &cout, bool &chg, bool &fb) {
+    cout = cin;
+    chg = false;
+    fb = false;
+    if constexpr (PERN) {
+        if (n < 1 || n > N) {
+            fb = true;
+            return;
+        }
+#pragma unroll
+        for (int s = 0; s < N; ++s) m[s] = (s < n) ? m[s] : 0;
+    }
+    uint64_t q;
+    if constexpr (PERN) {
+        q = quorum_match_pern<N>(m, n);
+    } else {
+        q = quorum_match_uniform<N>(m);
+    }
+    if constexpr (FORM == HQ_FORM_TERM_START) {
+        // term(q) == term  <=>  term_start <= q <= last   (aux = term_start)
+        chg = (q > cin) & (q >= aux) & (q <= last);
+    } else {
+        // aux = the leader's term; the ring holds term(i) for i in (last - R, last]
+        fb = (aux == 0) | (cin > last) || (last - cin > a.R);
+        if (!fb && q > cin && q <= last) {
+            const uint64_t lterm = a.ring[g * a.R + (q & (uint64_t)(a.R - 1))];
+            chg = lterm == aux;
+        }
+    }
+    cout = chg ? q : cin;
+}
+
+// VEC = groups per lane (2: 16-byte loads of every SoA column; 1: 8-byte loads).
+template <int N, int FORM, int VEC, bool PERN>
+__global__ __launch_bounds__(kBlock) void k_commit(const CommitK a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * VEC;
+    const uint64_t *aux_col = (FORM == HQ_FORM_TERM_START) ? a.tstart : a.term;
+    for (uint64_t wbase = wave * 64 * VEC; wbase < a.G; wbase += step) {
+        const uint64_t g0 = wbase + (uint64_t)lane * VEC;
+        bool chg[VEC], fb[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) chg[j] = fb[j] = false;
+        if constexpr (VEC == 2) {
+            if (g0 + 1 < a.G) {
+                uint64_t m0[N], m1[N];
+#pragma unroll
+                for (int s = 0; s < N; ++s) {
+                    const ulong2 v = *reinterpret_cast<const ulong2 *>(a.match + s * a.stride + g0);
+                    m0[s] = v.x;
+                    m1[s] = v.y;
+                }
+                const ulong2 ci = *reinterpret_cast<const ulong2 *>(a.cin + g0);
+                const ulong2 la = *reinterpret_cast<const ulong2 *>(a.last + g0);
+                const ulong2 ax = *reinterpret_cast<const ulong2 *>(aux_col + g0);
+                int n0 = N, n1 = N;
+                if constexpr (PERN) {
+                    const uint16_t nn = *reinterpret_cast<const uint16_t *>(a.nv + g0);
+                    n0 = nn & 0xFF;
+                    n1 = nn >> 8;
+                }
+                ulong2 co;
+                decide<N, FORM, PERN>(a, g0, m0, n0, ci.x, la.x, ax.x, co.x, chg[0], fb[0]);
+                decide<N, FORM, PERN>(a, g0 + 1, m1, n1, ci.y, la.y, ax.y, co.y, chg[1], fb[1]);
+                *reinterpret_cast<ulong2 *>(a.cout + g0) = co;
+            } else if (g0 < a.G) {
+                uint64_t m0[N];
+#pragma unroll
+                for (int s = 0; s < N; ++s) m0[s] = a.match[s * a.stride + g0];
+                const int n0 = PERN ? (int)a.nv[g0] : N;
+                uint64_t co;
+                decide<N, FORM, PERN>(a, g0, m0, n0, a.cin[g0], a.last[g0], aux_col[g0], co,
+                                      chg[0], fb[0]);
+                a.cout[g0] = co;
+            }
+            const uint64_t b0 = __ballot(chg[0]), b1 = __ballot(chg[1]);
+            const uint64_t f0 = __ballot(fb[0]), f1 = __ballot(fb[1]);
+            if (lane == 0) {
+                const uint64_t w = wbase >> 6;
+                if (a.changed) {
+                    a.changed[w] = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
+                    if (w + 1 < a.nwords)
+                        a.changed[w + 1] = spread32((uint32_t)(b0 >> 32)) |
+                                           (spread32((uint32_t)(b1 >> 32)) << 1);
+                }
+                if (a.fallback) {
+                    a.fallback[w] = spread32((uint32_t)f0) | (spread32((uint32_t)f1) << 1);
+                    if (w + 1 < a.nwords)
+                        a.fallback[w + 1] = spread32((uint32_t)(f0 >> 32)) |
+                                            (spread32((uint32_t)(f1 >> 32)) << 1);
+                }
+            }
+        } else {
+            if (g0 < a.G) {
+                uint64_t m0[N];
+#pragma unroll
+                for (int s = 0; s < N; ++s) m0[s] = a.match[s * a.stride + g0];
+                const int n0 = PERN ? (int)a.nv[g0] : N;
+                uint64_t co;
+                decide<N, FORM, PERN>(a, g0, m0, n0, a.cin[g0], a.last[g0], aux_col[g0], co,
+                                      chg[0], fb[0]);
+                a.cout[g0] = co;
+            }
+            const uint64_t b0 = __ballot(chg[0]);
+            const uint64_t f0 = __ballot(fb[0]);
+            if (lane == 0) {
+                if (a.changed) a.changed[wbase >> 6] = b0;
+                if (a.fallback) a.fallback[wbase >> 6] = f0;
+            }
+        }
+    }
+}
+
+// ---- ReadIndex / vote / CheckQuorum over u8 bitmaps: 16 groups per lane ---------------------
+struct BitsK {
+    uint64_t G;
+    uint32_t n_uniform, self_slot;
+    const uint8_t *ack, *granted, *rejected;
+    uint8_t *active;
+    const uint8_t *nv;
+    uint64_t *confirmed, *outcome, *has_quorum, *fallback;
+    uint64_t n16;   // number of 16-group slots covered by the 64-group bitmap words
+    uint64_t n16o;  // number of 16-group slots covered by the 32-group outcome words
+};
+
+constexpr int kRI = 1, kVOTE = 2, kCHECKQ = 4;
+
+union V16 {
+    uint4 v;
+    uint8_t b[16];
+};
+
+__device__ __forceinline__ V16 load16(const uint8_t *p, uint64_t g, uint64_t G) {
+    V16 r;
+    if (g + 16 <= G) {
+        r.v = *reinterpret_cast<const uint4 *>(p + g);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r.b[k] = (g + k < G) ? p[g + k] : 0;
+    }
+    return r;
+}
+
+template <int MODE, bool PERN>
+__global__ __launch_bounds__(kBlock) void k_bits(const BitsK a) {
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * 16;
+    for (uint64_t g = tid * 16; g < a.n16o * 16 || g < a.n16 * 16; g += step) {
+        const uint64_t slot = g >> 4;
+        V16 nv, ack, gr, rj, ac;
+        if (g < a.G) {
+            if constexpr (PERN) nv = load16(a.nv, g, a.G);
+            if constexpr (MODE & kRI) ack = load16(a.ack, g, a.G);
+            if constexpr (MODE & kVOTE) {
+                gr = load16(a.granted, g, a.G);
+                rj = load16(a.rejected, g, a.G);
+            }
+            if constexpr (MODE & kCHECKQ) ac = load16(a.active, g, a.G);
+        }
+        uint32_t conf = 0, outc = 0, hq = 0, fb = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (g + k >= a.G) continue;
+            const uint32_t n = PERN ? nv.b[k] : a.n_uniform;
+            const bool bad = (n < 1) | (n > 8);
+            const uint32_t mask = bad ? 0u : ((1u << n) - 1u);
+            const uint32_t quorum = n / 2 + 1;
+            fb |= (uint32_t)bad << k;
+            if constexpr (MODE & kRI) {
+                // readindex.go:84: len(confirmed) + 1 >= quorum
+                const uint32_t c = __popc(ack.b[k] & mask) + 1;
+                conf |= (uint32_t)(!bad && c >= quorum) << k;
+            }
+            if constexpr (MODE & kVOTE) {
+                const uint32_t gm = gr.b[k] & mask;
+                const uint32_t rm = rj.b[k] & mask & ~gm;  // first response wins
+                uint32_t o = HQ_OUTCOME_CANDIDATE;
+                if (!bad) {
+                    if ((uint32_t)__popc(gm) >= quorum)
+                        o = HQ_OUTCOME_LEADER;
+                    else if ((uint32_t)__popc(rm) >= quorum)
+                        o = HQ_OUTCOME_FOLLOWER;
+                }
+                outc |= o << (2 * k);
+            }
+            if constexpr (MODE & kCHECKQ) {
+                const bool selfok = !bad && a.self_slot < n;
+                fb |= (uint32_t)(!selfok) << k;
+                const uint32_t c = __popc((ac.b[k] | (1u << a.self_slot)) & mask);
+                hq |= (uint32_t)(selfok && c >= quorum) << k;
+            }
+        }
+        // 64-group bitmap words viewed as 16-bit slots, 32-group outcome words as 32-bit slots
+        if (slot < a.n16) {
+            if constexpr (MODE & kRI) reinterpret_cast<uint16_t *>(a.confirmed)[slot] = conf;
+            if constexpr (MODE & kCHECKQ)
+                reinterpret_cast<uint16_t *>(a.has_quorum)[slot] = hq;
+            if (a.fallback) reinterpret_cast<uint16_t *>(a.fallback)[slot] = fb;
+        }
+        if constexpr (MODE & kVOTE) {
+            if (slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
+        }
+        if constexpr (MODE & kCHECKQ) {
+            // setNotActive for every voting member (raft.go:385, remote.go:196-198); groups left
+            // to the CPU path (fallback) keep their flags
+            V16 keep;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) keep.b[k] = ((fb >> k) & 1) ? ac.b[k] : 0;
+            if (g + 16 <= a.G) {
+                *reinterpret_cast<uint4 *>(a.active + g) = keep.v;
+            } else {
+                for (int k = 0; k < 16; ++k)
+                    if (g + k < a.G) a.active[g + k] = keep.b[k];
+            }
+        }
+    }
+}
+
+// ---- synthetic inputs (recipe: DESIGN.md "Synthetic inputs"; CPU twin oracle/qgen.c) --------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int synth_n(const hq_synth_spec &s, uint64_t cid) {
+    const uint32_t r = (uint32_t)(cid % 3);
+    return s.mixed_n ? (r == 0 ? 3 : r == 1 ? 5 : 7) : (int)s.n_max;
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, CommitK o) {
+    const uint64_t R = s.ring_len;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < s.G;
+         j += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t cid = s.cid_base + j * s.cid_stride;
+        uint64_t st = s.seed ^ cid;
+        const int n = synth_n(s, cid);
+        const uint64_t term = 2 + splitmix64(st) % ((1ull << 20) - 2);
+        const uint64_t last = (1ull << 20) + splitmix64(st) % (1ull << 40);
+        uint64_t committed = last - splitmix64(st) % R;
+        const uint64_t term_start = last - splitmix64(st) % R + 1;
+        if (s.parity_extras) {
+            const uint64_t x = splitmix64(st);
+            if (x % 100 == 0) committed = last;
+        }
+        for (int k = 0; k < (int)s.n_max; ++k) {
+            uint64_t m;
+            if (k >= n) {
+                m = 0;
+            } else if (k == 0) {
+                m = last;
+            } else {
+                const uint64_t x = splitmix64(st);
+                const uint64_t y = splitmix64(st);
+                m = committed - x % 4 + y % (last - committed + 4);
+                if (m > last) m = last;
+                if (s.parity_extras) {
+                    const uint64_t c = splitmix64(st);
+                    if (c % 100 == 0) m = last + 1 + (c / 100) % 3;
+                }
+            }
+            if (o.match) const_cast<uint64_t *>(o.match)[(uint64_t)k * o.stride + j] = m;
+        }
+        if (o.nv) const_cast<uint8_t *>(o.nv)[j] = (uint8_t)n;
+        if (o.cin) const_cast<uint64_t *>(o.cin)[j] = committed;
+        if (o.last) const_cast<uint64_t *>(o.last)[j] = last;
+        if (o.tstart) const_cast<uint64_t *>(o.tstart)[j] = term_start;
+        if (o.term) const_cast<uint64_t *>(o.term)[j] = term;
+        if (o.ring) {
+            uint64_t cur = term;
+            for (uint64_t k = 0; k < R; ++k) {
+                const uint64_t i = last - k;
+                uint64_t t;
+                if (i >= term_start) {
+                    t = term;
+                } else {
+                    const uint64_t x = splitmix64(st);
+                    const uint64_t dec = (i + 1 == term_start) ? 1 + (x & 1) : (x & 1);
+                    cur = cur > dec ? cur - dec : 1;
+                    t = cur;
+                }
+                const_cast<uint64_t *>(o.ring)[j * R + (i & (R - 1))] = t;
+            }
+        }
+    }
+}
+
+struct Bern {
+    uint64_t st, buf;
+    int avail;
+    __device__ __forceinline__ bool operator()(uint32_t thr16) {
+        if (avail == 0) {
+            buf = splitmix64(st);
+            avail = 4;
+        }
+        const uint32_t v = (uint32_t)(buf & 0xFFFF);
+        buf >>= 16;
+        --avail;
+        return v < thr16;
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void k_synth_bits(const hq_synth_spec s, uint8_t *ack,
+                                                       uint8_t *granted, uint8_t *rejected,
+                                                       uint8_t *nv) {
+    constexpr uint32_t P60 = 39322u, P30 = 19661u;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < s.G;
+         j += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t cid = s.cid_base + j * s.cid_stride;
+        Bern b{s.seed ^ cid, 0, 0};
+        const int n = synth_n(s, cid);
+        uint32_t a = 0, g = 1, r = 0;
+        for (int k = 1; k < n; ++k)
+            if (b(P60)) a |= 1u << k;
+        for (int k = 1; k < n; ++k)
+            if (b(P60)) g |= 1u << k;
+        for (int k = 1; k < n; ++k)
+            if (!((g >> k) & 1) && b(P30)) r |= 1u << k;
+        if (s.parity_extras) {
+            const uint64_t x = splitmix64(b.st);
+            if (x % 50 == 0) r |= g & ~1u;
+            if (x % 50 == 1) a |= 1u;
+            if (x % 50 == 2) a |= 0xFFu & ~((1u << n) - 1);
+        }
+        if (ack) ack[j] = (uint8_t)a;
+        if (granted) granted[j] = (uint8_t)g;
+        if (rejected) rejected[j] = (uint8_t)r;
+        if (nv) nv[j] = (uint8_t)n;
+    }
+}
+
+unsigned grid_for(uint64_t lanes_needed) {
+    uint64_t b = (lanes_needed + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    if (b > (uint64_t)kMaxBlocks) b = kMaxBlocks;
+    return (unsigned)b;
+}
+
+template <int N, int FORM, int VEC, bool PERN>
+int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
+    const unsigned grid = grid_for((k.G + VEC - 1) / VEC);
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       k);
+    return hq::post_launch(ctx, "k_commit");
+}
+
+template <int N>
+int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool pern) {
+#define HQ_DISPATCH(F)                                                                   \
+    if (vec2) return pern ? launch_commit_t<N, F, 2, true>(ctx, k)                       \
+                          : launch_commit_t<N, F, 2, false>(ctx, k);                     \
+    return pern ? launch_commit_t<N, F, 1, true>(ctx, k) : launch_commit_t<N, F, 1, false>(ctx, k);
+    if (form == HQ_FORM_TERM_START) {
+        HQ_DISPATCH(HQ_FORM_TERM_START)
+    } else {
+        HQ_DISPATCH(HQ_FORM_TERM_RING)
+    }
+#undef HQ_DISPATCH
+}
+
+int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
+    if (a->n_max < 1 || a->n_max > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit: n_max must be 1..8");
+    if (a->G == 0) return HQ_OK;
+    if (!a->match || !a->committed_in || !a->committed_out || !a->last_index)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit: NULL match/committed/last_index");
+    if (a->match_stride < a->G) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: match_stride < G");
+    if (a->form == HQ_FORM_TERM_START) {
+        if (!a->term_start) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term_start is NULL");
+    } else if (a->form == HQ_FORM_TERM_RING) {
+        if (!a->term || !a->ring) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term/ring NULL");
+        if (a->ring_len < 1 || a->ring_len > 1024 || (a->ring_len & (a->ring_len - 1)))
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: ring_len must be a power of two <= 1024");
+    } else {
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit: unknown form");
+    }
+    return HQ_OK;
+}
+
+}  // namespace
+
+extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
+    int rc = validate_commit(ctx, a);
+    if (rc || a->G == 0) return rc;
+    CommitK k;
+    k.G = a->G;
+    k.stride = a->match_stride;
+    k.nwords = hq::words64(a->G);
+    k.n_max = a->n_max;
+    k.R = a->ring_len;
+    k.match = a->match;
+    k.nv = a->n_voting;
+    k.cin = a->committed_in;
+    k.cout = a->committed_out;
+    k.last = a->last_index;
+    k.tstart = a->term_start;
+    k.term = a->term;
+    k.ring = a->ring;
+    k.changed = a->changed;
+    k.fallback = a->fallback;
+    const void *aux = a->form == HQ_FORM_TERM_START ? (const void *)a->term_start
+                                                     : (const void *)a->term;
+    const bool vec2 = hq::aligned16(a->match) && (a->match_stride % 2 == 0) &&
+                      hq::aligned16(a->committed_in) && hq::aligned16(a->committed_out) &&
+                      hq::aligned16(a->last_index) && hq::aligned16(aux) &&
+                      (!a->n_voting || (reinterpret_cast<uintptr_t>(a->n_voting) & 1) == 0);
+    const bool pern = a->n_voting != nullptr;
+    switch (a->n_max) {
+    case 1: return launch_commit_n<1>(ctx, k, a->form, vec2, pern);
+    case 2: return launch_commit_n<2>(ctx, k, a->form, vec2, pern);
+    case 3: return launch_commit_n<3>(ctx, k, a->form, vec2, pern);
+    case 4: return launch_commit_n<4>(ctx, k, a->form, vec2, pern);
+    case 5: return launch_commit_n<5>(ctx, k, a->form, vec2, pern);
+    case 6: return launch_commit_n<6>(ctx, k, a->form, vec2, pern);
+    case 7: return launch_commit_n<7>(ctx, k, a->form, vec2, pern);
+    default: return launch_commit_n<8>(ctx, k, a->form, vec2, pern);
+    }
+}
+
+extern "C" int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count && !args) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_many_dev: args is NULL");
+    for (uint32_t i = 0; i < count; ++i) {
+        int rc = hq_commit_dev(ctx, args + i);
+        if (rc) return rc;
+    }
+    return HQ_OK;
+}
+
+namespace {
+
+template <int MODE>
+int launch_bits(hq_ctx *ctx, BitsK &k, const char *what) {
+    if (!ctx) return HQ_E_INVAL;
+    if (k.G == 0) return HQ_OK;
+    if (!k.nv && (k.n_uniform < 1 || k.n_uniform > 8))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": n_uniform must be 1..8");
+    const uint8_t *ins[5] = {k.nv, k.ack, k.granted, k.rejected, k.active};
+    for (const uint8_t *p : ins)
+        if (p && !hq::aligned16(p))
+            return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": byte arrays must be 16-byte aligned");
+    k.n16 = hq::words64(k.G) * 4;
+    k.n16o = (MODE & kVOTE) ? hq::words32(k.G) * 2 : 0;
+    const uint64_t slots = k.n16 > k.n16o ? k.n16 : k.n16o;
+    const unsigned grid = grid_for(slots);
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    if (k.nv)
+        hipLaunchKernelGGL((k_bits<MODE, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    else
+        hipLaunchKernelGGL((k_bits<MODE, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    return hq::post_launch(ctx, what);
+}
+
+BitsK bits_args(uint64_t G, const uint8_t *nv, uint32_t nu, uint64_t *fallback) {
+    BitsK k{};
+    k.G = G;
+    k.nv = nv;
+    k.n_uniform = nu;
+    k.fallback = fallback;
+    return k;
+}
+
+}  // namespace
+
+extern "C" int hq_readindex_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,
+                                const uint8_t *n_voting, uint32_t n_uniform, uint64_t *confirmed,
+                                uint64_t *fallback) {
+    if (ctx && G && (!ack || !confirmed))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_readindex: NULL ack/confirmed");
+    BitsK k = bits_args(G, n_voting, n_uniform, fallback);
+    k.ack = ack;
+    k.confirmed = confirmed;
+    return launch_bits<kRI>(ctx, k, "hq_readindex");
+}
+
+extern "C" int hq_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *granted,
+                           const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
+                           uint64_t *outcome, uint64_t *fallback) {
+    if (ctx && G && (!granted || !rejected || !outcome))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_vote: NULL granted/rejected/outcome");
+    BitsK k = bits_args(G, n_voting, n_uniform, fallback);
+    k.granted = granted;
+    k.rejected = rejected;
+    k.outcome = outcome;
+    return launch_bits<kVOTE>(ctx, k, "hq_vote");
+}
+
+extern "C" int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,
+                                     const uint8_t *granted, const uint8_t *rejected,
+                                     const uint8_t *n_voting, uint32_t n_uniform,
+                                     uint64_t *confirmed, uint64_t *outcome, uint64_t *fallback) {
+    if (ctx && G && (!ack || !granted || !rejected || !confirmed || !outcome))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_vote: NULL argument");
+    BitsK k = bits_args(G, n_voting, n_uniform, fallback);
+    k.ack = ack;
+    k.granted = granted;
+    k.rejected = rejected;
+    k.confirmed = confirmed;
+    k.outcome = outcome;
+    return launch_bits<kRI | kVOTE>(ctx, k, "hq_readindex_vote");
+}
+
+extern "C" int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active,
+                                   const uint8_t *n_voting, uint32_t n_uniform,
+                                   uint32_t self_slot, uint64_t *has_quorum, uint64_t *fallback) {
+    if (ctx && G && (!active || !has_quorum))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_check_quorum: NULL active/has_quorum");
+    if (ctx && self_slot >= HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_check_quorum: self_slot must be < 8");
+    BitsK k = bits_args(G, n_voting, n_uniform, fallback);
+    k.active = active;
+    k.self_slot = self_slot;
+    k.has_quorum = has_quorum;
+    return launch_bits<kCHECKQ>(ctx, k, "hq_check_quorum");
+}
+
+extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,
+                                   const hq_commit_args *a) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!s || !a) return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit: NULL argument");
+    if (s->ring_len < 1 || (s->ring_len & (s->ring_len - 1)) || s->n_max < 1 || s->n_max > 8 ||
+        s->cid_stride < 1 || (s->mixed_n && s->n_max < 7) || (a->match && a->match_stride < s->G))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit: bad spec");
+    if (s->G == 0) return HQ_OK;
+    CommitK o{};
+    o.G = s->G;
+    o.stride = a->match_stride;
+    o.match = a->match;
+    o.nv = a->n_voting;
+    o.cin = a->committed_in;
+    o.last = a->last_index;
+    o.tstart = a->term_start;
+    o.term = a->term;
+    o.ring = a->ring;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_synth_commit, dim3(grid_for(s->G)), dim3(kBlock), 0, ctx->stream, *s, o);
+    return hq::post_launch(ctx, "k_synth_commit");
+}
+
+extern "C" int hq_synth_bitmaps_dev(hq_ctx *ctx, const hq_synth_spec *s, uint8_t *ack,
+                                    uint8_t *granted, uint8_t *rejected, uint8_t *n_voting) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!s || s->n_max < 1 || s->n_max > 8 || s->cid_stride < 1 || (s->mixed_n && s->n_max < 7))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_synth_bitmaps: bad spec");
+    if (s->G == 0) return HQ_OK;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_synth_bits, dim3(grid_for(s->G)), dim3(kBlock), 0, ctx->stream, *s, ack,
+                       granted, rejected, n_voting);
+    return hq::post_launch(ctx, "k_synth_bits");
+}

@@ -1,0 +1,357 @@
+// hq_runtime.hip — contexts, memory, timing and the host-pointer entry points of
+// libhipquorum.so. Kernels and their _dev launchers live in hq_kernels.hip.
+#include <cstring>
+#include <new>
+
+#include "hq_internal.h"
+
+namespace {
+thread_local std::string g_open_error;  // hq_open failures (no context yet)
+}
+
+namespace hq {
+
+int fail(hq_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    else g_open_error = msg;
+    return code;
+}
+
+int check_hip(hq_ctx *ctx, hipError_t e, const char *what) {
+    if (e == hipSuccess) return HQ_OK;
+    return fail(ctx, e == hipErrorOutOfMemory ? HQ_E_NOMEM : HQ_E_DEVICE,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int pre_launch(hq_ctx *ctx) {
+    int rc = check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (rc || !ctx->timing) return rc;
+    if (ctx->ev_used == ctx->ev_start.size()) {
+        hipEvent_t a, b;
+        rc = check_hip(ctx, hipEventCreate(&a), "hipEventCreate");
+        if (rc) return rc;
+        rc = check_hip(ctx, hipEventCreate(&b), "hipEventCreate");
+        if (rc) { (void)hipEventDestroy(a); return rc; }
+        ctx->ev_start.push_back(a);
+        ctx->ev_stop.push_back(b);
+    }
+    return check_hip(ctx, hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream),
+                     "hipEventRecord");
+}
+
+int post_launch(hq_ctx *ctx, const char *what) {
+    int rc = check_hip(ctx, hipGetLastError(), what);
+    if (rc) return rc;
+    if (ctx->timing) {
+        rc = check_hip(ctx, hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream),
+                       "hipEventRecord");
+        if (rc) return rc;
+        ctx->ev_used++;
+    }
+    return HQ_OK;
+}
+
+int ensure_workspace(hq_ctx *ctx, size_t bytes) {
+    if (ctx->ws_bytes >= bytes) return HQ_OK;
+    if (ctx->ws) {
+        int rc = check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+        if (rc) return rc;
+        (void)hipFree(ctx->ws);
+        ctx->ws = nullptr;
+        ctx->ws_bytes = 0;
+    }
+    int rc = check_hip(ctx, hipMalloc(&ctx->ws, bytes), "hipMalloc(workspace)");
+    if (rc) return rc;
+    ctx->ws_bytes = bytes;
+    return HQ_OK;
+}
+
+}  // namespace hq
+
+extern "C" {
+
+int hq_abi_version(void) { return HQ_ABI_VERSION; }
+
+int hq_device_count(int *out) {
+    if (!out) return HQ_E_INVAL;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return HQ_OK;
+}
+
+int hq_open(int device, uint32_t flags, hq_ctx **out) {
+    (void)flags;
+    if (!out) return hq::fail(nullptr, HQ_E_INVAL, "hq_open: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return hq::fail(nullptr, HQ_E_DEVICE, "hq_open: no HIP device visible");
+    if (device < 0 || device >= n)
+        return hq::fail(nullptr, HQ_E_INVAL, "hq_open: device index out of range");
+    hq_ctx *ctx = new (std::nothrow) hq_ctx();
+    if (!ctx) return hq::fail(nullptr, HQ_E_NOMEM, "hq_open: out of host memory");
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        std::string msg = std::string("hq_open: ") + hipGetErrorString(e);
+        delete ctx;
+        return hq::fail(nullptr, HQ_E_DEVICE, msg);
+    }
+    *out = ctx;
+    return HQ_OK;
+}
+
+void hq_close(hq_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (hipEvent_t e : ctx->ev_start) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->ev_stop) (void)hipEventDestroy(e);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *hq_last_error(const hq_ctx *ctx) {
+    return ctx ? ctx->err.c_str() : g_open_error.c_str();
+}
+
+int hq_sync(hq_ctx *ctx) {
+    if (!ctx) return HQ_E_INVAL;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (rc) return rc;
+    return hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+int hq_malloc_dev(hq_ctx *ctx, size_t bytes, void **out) {
+    if (!ctx || !out) return HQ_E_INVAL;
+    *out = nullptr;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (rc) return rc;
+    return hq::check_hip(ctx, hipMalloc(out, bytes ? bytes : 1), "hipMalloc");
+}
+
+int hq_free_dev(hq_ctx *ctx, void *p) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!p) return HQ_OK;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (rc) return rc;
+    return hq::check_hip(ctx, hipFree(p), "hipFree");
+}
+
+int hq_alloc_pinned(hq_ctx *ctx, size_t bytes, void **out) {
+    if (!ctx || !out) return HQ_E_INVAL;
+    *out = nullptr;
+    return hq::check_hip(ctx, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault),
+                         "hipHostMalloc");
+}
+
+int hq_free_pinned(hq_ctx *ctx, void *p) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!p) return HQ_OK;
+    return hq::check_hip(ctx, hipHostFree(p), "hipHostFree");
+}
+
+int hq_memcpy_async(hq_ctx *ctx, void *dst, const void *src, size_t bytes, int kind) {
+    if (!ctx) return HQ_E_INVAL;
+    if (bytes == 0) return HQ_OK;
+    if (!dst || !src) return hq::fail(ctx, HQ_E_INVAL, "hq_memcpy_async: NULL pointer");
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                    : kind == 1 ? hipMemcpyDeviceToHost
+                    : kind == 2 ? hipMemcpyDeviceToDevice
+                                : hipMemcpyDefault;
+    if (kind < 0 || kind > 2) return hq::fail(ctx, HQ_E_INVAL, "hq_memcpy_async: bad kind");
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (rc) return rc;
+    return hq::check_hip(ctx, hipMemcpyAsync(dst, src, bytes, k, ctx->stream), "hipMemcpyAsync");
+}
+
+int hq_memset_async(hq_ctx *ctx, void *dst, int value, size_t bytes) {
+    if (!ctx) return HQ_E_INVAL;
+    if (bytes == 0) return HQ_OK;
+    if (!dst) return hq::fail(ctx, HQ_E_INVAL, "hq_memset_async: NULL pointer");
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (rc) return rc;
+    return hq::check_hip(ctx, hipMemsetAsync(dst, value, bytes, ctx->stream), "hipMemsetAsync");
+}
+
+int hq_timing_enable(hq_ctx *ctx, int enable) {
+    if (!ctx) return HQ_E_INVAL;
+    ctx->timing = enable != 0;
+    return HQ_OK;
+}
+
+int hq_timing_read(hq_ctx *ctx, double *total_ms, uint64_t *launches) {
+    if (!ctx) return HQ_E_INVAL;
+    int rc = hq_sync(ctx);
+    if (rc) return rc;
+    for (size_t i = 0; i < ctx->ev_used; ++i) {
+        float ms = 0.f;
+        rc = hq::check_hip(ctx, hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]),
+                           "hipEventElapsedTime");
+        if (rc) return rc;
+        ctx->timed_ms += ms;
+        ctx->timed_launches++;
+    }
+    ctx->ev_used = 0;
+    if (total_ms) *total_ms = ctx->timed_ms;
+    if (launches) *launches = ctx->timed_launches;
+    return HQ_OK;
+}
+
+int hq_timing_reset(hq_ctx *ctx) {
+    if (!ctx) return HQ_E_INVAL;
+    int rc = hq_sync(ctx);
+    if (rc) return rc;
+    ctx->ev_used = 0;
+    ctx->timed_ms = 0.0;
+    ctx->timed_launches = 0;
+    return HQ_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- host-pointer entry points --
+// Stage host arrays through the context's device workspace: H2D, kernel, D2H, synchronise.
+
+namespace {
+
+struct Stage {
+    hq_ctx *ctx;
+    char *base;
+    size_t off = 0;
+    explicit Stage(hq_ctx *c) : ctx(c), base(static_cast<char *>(c->ws)) {}
+    static size_t pad(size_t b) { return (b + 255) & ~size_t(255); }
+    template <class T>
+    T *take(size_t bytes) {
+        T *p = reinterpret_cast<T *>(base + off);
+        off += pad(bytes);
+        return p;
+    }
+};
+
+int h2d(hq_ctx *ctx, void *d, const void *h, size_t b) { return hq_memcpy_async(ctx, d, h, b, 0); }
+int d2h(hq_ctx *ctx, void *h, const void *d, size_t b) { return hq_memcpy_async(ctx, h, d, b, 1); }
+
+}  // namespace
+
+extern "C" {
+
+int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
+    if (a->G == 0) return HQ_OK;
+    if (!a->match || !a->committed_in || !a->committed_out || !a->last_index ||
+        a->n_max < 1 || a->n_max > HQ_MAX_VOTERS || a->match_stride < a->G)
+        return hq_commit_dev(ctx, a);  // same validation and message
+    const uint64_t G = a->G, nw = hq::words64(G);
+    const bool ring = a->form == HQ_FORM_TERM_RING;
+    if (ring && (!a->ring || !a->term)) return hq_commit_dev(ctx, a);
+    if (!ring && !a->term_start) return hq_commit_dev(ctx, a);
+    const size_t col = G * 8;
+    size_t need = Stage::pad(col * a->n_max) + 4 * Stage::pad(col) + 2 * Stage::pad(nw * 8) +
+                  Stage::pad(G) + (ring ? Stage::pad(col * a->ring_len) : 0);
+    int rc = hq::ensure_workspace(ctx, need);
+    if (rc) return rc;
+    Stage s(ctx);
+    hq_commit_args d = *a;
+    uint64_t *dm = s.take<uint64_t>(col * a->n_max);
+    d.match = dm;
+    d.match_stride = G;
+    for (uint32_t k = 0; k < a->n_max && !rc; ++k)
+        rc = h2d(ctx, dm + (size_t)k * G, a->match + (size_t)k * a->match_stride, col);
+    uint64_t *dci = s.take<uint64_t>(col), *dco = s.take<uint64_t>(col);
+    uint64_t *dlast = s.take<uint64_t>(col), *daux = s.take<uint64_t>(col);
+    d.committed_in = dci;
+    d.committed_out = dco;
+    d.last_index = dlast;
+    if (!rc) rc = h2d(ctx, dci, a->committed_in, col);
+    if (!rc) rc = h2d(ctx, dlast, a->last_index, col);
+    if (ring) {
+        d.term = daux;
+        uint64_t *dring = s.take<uint64_t>(col * a->ring_len);
+        d.ring = dring;
+        if (!rc) rc = h2d(ctx, daux, a->term, col);
+        if (!rc) rc = h2d(ctx, dring, a->ring, col * a->ring_len);
+    } else {
+        d.term_start = daux;
+        if (!rc) rc = h2d(ctx, daux, a->term_start, col);
+    }
+    uint8_t *dnv = s.take<uint8_t>(G);
+    if (a->n_voting) {
+        d.n_voting = dnv;
+        if (!rc) rc = h2d(ctx, dnv, a->n_voting, G);
+    }
+    uint64_t *dchg = s.take<uint64_t>(nw * 8), *dfb = s.take<uint64_t>(nw * 8);
+    d.changed = a->changed ? dchg : nullptr;
+    d.fallback = a->fallback ? dfb : nullptr;
+    if (!rc) rc = hq_commit_dev(ctx, &d);
+    if (!rc) rc = d2h(ctx, a->committed_out, dco, col);
+    if (!rc && a->changed) rc = d2h(ctx, a->changed, dchg, nw * 8);
+    if (!rc && a->fallback) rc = d2h(ctx, a->fallback, dfb, nw * 8);
+    if (!rc) rc = hq_sync(ctx);
+    return rc;
+}
+
+static int bits_host(hq_ctx *ctx, uint64_t G, const uint8_t *const *ins, int nin,
+                     const uint8_t *nv, uint8_t **dins, uint8_t **dnv, uint64_t **dout,
+                     int nout, const size_t *out_bytes) {
+    size_t need = Stage::pad(G) * (nin + 1);
+    for (int i = 0; i < nout; ++i) need += Stage::pad(out_bytes[i]);
+    int rc = hq::ensure_workspace(ctx, need);
+    if (rc) return rc;
+    Stage s(ctx);
+    for (int i = 0; i < nin && !rc; ++i) {
+        dins[i] = s.take<uint8_t>(G);
+        rc = h2d(ctx, dins[i], ins[i], G);
+    }
+    *dnv = s.take<uint8_t>(G);
+    if (nv && !rc) rc = h2d(ctx, *dnv, nv, G);
+    if (!nv) *dnv = nullptr;
+    for (int i = 0; i < nout; ++i) dout[i] = s.take<uint64_t>(out_bytes[i]);
+    return rc;
+}
+
+int hq_readindex(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *n_voting,
+                 uint32_t n_uniform, uint64_t *confirmed, uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!ack || !confirmed) return hq::fail(ctx, HQ_E_INVAL, "hq_readindex: NULL ack/confirmed");
+    const size_t wb = hq::words64(G) * 8;
+    const uint8_t *ins[1] = {ack};
+    uint8_t *dins[1], *dnv;
+    uint64_t *dout[2];
+    size_t ob[2] = {wb, wb};
+    int rc = bits_host(ctx, G, ins, 1, n_voting, dins, &dnv, dout, 2, ob);
+    if (!rc) rc = hq_readindex_dev(ctx, G, dins[0], dnv, n_uniform, dout[0],
+                                   fallback ? dout[1] : nullptr);
+    if (!rc) rc = d2h(ctx, confirmed, dout[0], wb);
+    if (!rc && fallback) rc = d2h(ctx, fallback, dout[1], wb);
+    if (!rc) rc = hq_sync(ctx);
+    return rc;
+}
+
+int hq_vote(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *rejected,
+            const uint8_t *n_voting, uint32_t n_uniform, uint64_t *outcome, uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!granted || !rejected || !outcome)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_vote: NULL granted/rejected/outcome");
+    const size_t wb = hq::words64(G) * 8, ob2 = hq::words32(G) * 8;
+    const uint8_t *ins[2] = {granted, rejected};
+    uint8_t *dins[2], *dnv;
+    uint64_t *dout[2];
+    size_t ob[2] = {ob2, wb};
+    int rc = bits_host(ctx, G, ins, 2, n_voting, dins, &dnv, dout, 2, ob);
+    if (!rc) rc = hq_vote_dev(ctx, G, dins[0], dins[1], dnv, n_uniform, dout[0],
+                              fallback ? dout[1] : nullptr);
+    if (!rc) rc = d2h(ctx, outcome, dout[0], ob2);
+    if (!rc && fallback) rc = d2h(ctx, fallback, dout[1], wb);
+    if (!rc) rc = hq_sync(ctx);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,395 @@
+"""Python binding of libhipquorum.so (include/hipquorum.h) via ctypes.
+
+This is the harness-side caller of the C-ABI — the same entry points the Go cgo package
+``internal/hipquorum`` binds. It adds no computation of its own: every decision
+is made by the HIP kernels in ``dragonboat_amd/csrc``. There is no CPU fallback; if the shared
+library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libhipquorum.so")
+
+HQ_OK = 0
+HQ_E_INVAL = -1
+HQ_E_DEVICE = -2
+HQ_E_NOMEM = -3
+HQ_E_STATE = -4
+
+HQ_MAX_VOTERS = 8
+HQ_FORM_TERM_START = 0
+HQ_FORM_TERM_RING = 1
+
+OUTCOME_FOLLOWER = 0
+OUTCOME_CANDIDATE = 1
+OUTCOME_LEADER = 2
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+
+
+class CommitArgs(ctypes.Structure):
+    """Mirror of ``hq_commit_args``."""
+
+    _fields_ = [
+        ("G", ctypes.c_uint64),
+        ("n_max", ctypes.c_uint32),
+        ("form", ctypes.c_uint32),
+        ("ring_len", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("match_stride", ctypes.c_uint64),
+        ("match", _vp),
+        ("n_voting", _vp),
+        ("committed_in", _vp),
+        ("committed_out", _vp),
+        ("last_index", _vp),
+        ("term_start", _vp),
+        ("term", _vp),
+        ("ring", _vp),
+        ("changed", _vp),
+        ("fallback", _vp),
+    ]
+
+
+class SynthSpec(ctypes.Structure):
+    """Mirror of ``hq_synth_spec``."""
+
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("G", ctypes.c_uint64),
+        ("cid_base", ctypes.c_uint64),
+        ("cid_stride", ctypes.c_uint64),
+        ("n_max", ctypes.c_uint32),
+        ("mixed_n", ctypes.c_uint32),
+        ("ring_len", ctypes.c_uint32),
+        ("parity_extras", ctypes.c_uint32),
+    ]
+
+
+# name -> (restype, argtypes); the complete export list of include/hipquorum.h
+SIGNATURES = {
+    "hq_abi_version": (ctypes.c_int, []),
+    "hq_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "hq_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "hq_close": (None, [_vp]),
+    "hq_last_error": (ctypes.c_char_p, [_vp]),
+    "hq_sync": (ctypes.c_int, [_vp]),
+    "hq_malloc_dev": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "hq_free_dev": (ctypes.c_int, [_vp, _vp]),
+    "hq_alloc_pinned": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "hq_free_pinned": (ctypes.c_int, [_vp, _vp]),
+    "hq_memcpy_async": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int]),
+    "hq_memset_async": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t]),
+    "hq_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "hq_timing_read": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _u64p]),
+    "hq_timing_reset": (ctypes.c_int, [_vp]),
+    "hq_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs)]),
+    "hq_commit": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs)]),
+    "hq_commit_many_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
+    "hq_readindex_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
+    "hq_readindex": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
+    "hq_vote_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
+    "hq_vote": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
+    "hq_readindex_vote_dev": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp],
+    ),
+    "hq_check_quorum_dev": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp],
+    ),
+    "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
+    "hq_synth_bitmaps_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), _vp, _vp, _vp, _vp]),
+}
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libhipquorum.so and declare every exported signature. Raises if it is missing."""
+    if not os.path.exists(path):
+        raise ImportError(
+            f"libhipquorum.so not found at {path}: build it with `make` (or "
+            "__graft_entry__.build()); there is no CPU fallback for the quorum kernels"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = load_library()
+
+
+class HQError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hipquorum error {code}: {msg}")
+        self.code = code
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib.hq_device_count(ctypes.byref(n))
+    return n.value
+
+
+@dataclass
+class DeviceArray:
+    """A device allocation owned by a Context (freed with it or by ``free``)."""
+
+    ptr: int
+    nbytes: int
+    dtype: np.dtype
+    count: int
+
+    def at(self, elem_offset: int) -> int:
+        return self.ptr + elem_offset * self.dtype.itemsize
+
+
+class Context:
+    """One hq_ctx: one HIP stream on one GPU (a step worker's handle, execengine.go:675-690)."""
+
+    def __init__(self, device: int = 0):
+        h = _vp()
+        rc = lib.hq_open(device, 0, ctypes.byref(h))
+        if rc != HQ_OK:
+            raise HQError(rc, lib.hq_last_error(None).decode())
+        self.h = h
+        self.device = device
+        self._allocs: dict[int, DeviceArray] = {}
+
+    # -- lifetime ---------------------------------------------------------------------------
+    def close(self) -> None:
+        if self.h:
+            for a in list(self._allocs.values()):
+                lib.hq_free_dev(self.h, _vp(a.ptr))
+            self._allocs.clear()
+            lib.hq_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int) -> None:
+        if rc != HQ_OK:
+            raise HQError(rc, lib.hq_last_error(self.h).decode())
+
+    # -- memory -----------------------------------------------------------------------------
+    def empty(self, count: int, dtype) -> DeviceArray:
+        dtype = np.dtype(dtype)
+        p = _vp()
+        self._check(lib.hq_malloc_dev(self.h, max(1, count * dtype.itemsize), ctypes.byref(p)))
+        a = DeviceArray(p.value, count * dtype.itemsize, dtype, count)
+        self._allocs[a.ptr] = a
+        return a
+
+    def free(self, a: Optional[DeviceArray]) -> None:
+        if a is not None and a.ptr in self._allocs:
+            del self._allocs[a.ptr]
+            self._check(lib.hq_free_dev(self.h, _vp(a.ptr)))
+
+    def upload(self, host: np.ndarray) -> DeviceArray:
+        host = np.ascontiguousarray(host)
+        a = self.empty(host.size, host.dtype)
+        self._check(lib.hq_memcpy_async(self.h, _vp(a.ptr), host.ctypes.data_as(_vp), host.nbytes, 0))
+        self.sync()
+        return a
+
+    def download(self, a: DeviceArray, count: Optional[int] = None) -> np.ndarray:
+        count = a.count if count is None else count
+        out = np.empty(count, dtype=a.dtype)
+        self._check(lib.hq_memcpy_async(self.h, out.ctypes.data_as(_vp), _vp(a.ptr), out.nbytes, 1))
+        self.sync()
+        return out
+
+    def memset(self, a: DeviceArray, value: int = 0) -> None:
+        self._check(lib.hq_memset_async(self.h, _vp(a.ptr), value, a.nbytes))
+
+    def sync(self) -> None:
+        self._check(lib.hq_sync(self.h))
+
+    # -- timing -----------------------------------------------------------------------------
+    def timing(self, enable: bool) -> None:
+        self._check(lib.hq_timing_enable(self.h, int(enable)))
+
+    def timing_read(self) -> tuple[float, int]:
+        ms = ctypes.c_double(0)
+        n = ctypes.c_uint64(0)
+        self._check(lib.hq_timing_read(self.h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def timing_reset(self) -> None:
+        self._check(lib.hq_timing_reset(self.h))
+
+    # -- decisions (device pointers, asynchronous) -------------------------------------------
+    def commit_dev(self, args: CommitArgs) -> None:
+        self._check(lib.hq_commit_dev(self.h, ctypes.byref(args)))
+
+    def commit_many_dev(self, batch) -> None:
+        """batch: a ctypes array of CommitArgs (see ``commit_batch_array``)."""
+        self._check(lib.hq_commit_many_dev(self.h, batch, len(batch)))
+
+    def commit_host(self, args: CommitArgs) -> None:
+        self._check(lib.hq_commit(self.h, ctypes.byref(args)))
+
+    def readindex_dev(self, G, ack, n_voting, n_uniform, confirmed, fallback=None) -> None:
+        self._check(lib.hq_readindex_dev(self.h, G, _p(ack), _p(n_voting), n_uniform,
+                                         _p(confirmed), _p(fallback)))
+
+    def vote_dev(self, G, granted, rejected, n_voting, n_uniform, outcome, fallback=None) -> None:
+        self._check(lib.hq_vote_dev(self.h, G, _p(granted), _p(rejected), _p(n_voting), n_uniform,
+                                    _p(outcome), _p(fallback)))
+
+    def readindex_vote_dev(self, G, ack, granted, rejected, n_voting, n_uniform, confirmed,
+                           outcome, fallback=None) -> None:
+        self._check(lib.hq_readindex_vote_dev(self.h, G, _p(ack), _p(granted), _p(rejected),
+                                              _p(n_voting), n_uniform, _p(confirmed), _p(outcome),
+                                              _p(fallback)))
+
+    def check_quorum_dev(self, G, active, n_voting, n_uniform, self_slot, has_quorum,
+                         fallback=None) -> None:
+        self._check(lib.hq_check_quorum_dev(self.h, G, _p(active), _p(n_voting), n_uniform,
+                                            self_slot, _p(has_quorum), _p(fallback)))
+
+    def readindex_host(self, G, ack, n_voting, n_uniform, confirmed, fallback=None) -> None:
+        self._check(lib.hq_readindex(self.h, G, _p(ack), _p(n_voting), n_uniform, _p(confirmed),
+                                     _p(fallback)))
+
+    def vote_host(self, G, granted, rejected, n_voting, n_uniform, outcome, fallback=None) -> None:
+        self._check(lib.hq_vote(self.h, G, _p(granted), _p(rejected), _p(n_voting), n_uniform,
+                                _p(outcome), _p(fallback)))
+
+    def synth_commit_dev(self, spec: SynthSpec, args: CommitArgs) -> None:
+        self._check(lib.hq_synth_commit_dev(self.h, ctypes.byref(spec), ctypes.byref(args)))
+
+    def synth_bitmaps_dev(self, spec: SynthSpec, ack=None, granted=None, rejected=None,
+                          n_voting=None) -> None:
+        self._check(lib.hq_synth_bitmaps_dev(self.h, ctypes.byref(spec), _p(ack), _p(granted),
+                                             _p(rejected), _p(n_voting)))
+
+
+def _p(x) -> Optional[_vp]:
+    """Pointer argument from a DeviceArray, a numpy array (host) or None."""
+    if x is None:
+        return None
+    if isinstance(x, DeviceArray):
+        return _vp(x.ptr)
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data_as(_vp)
+    if isinstance(x, int):
+        return _vp(x)
+    raise TypeError(f"unsupported pointer argument {type(x)}")
+
+
+def commit_batch_array(args_list) -> ctypes.Array:
+    arr = (CommitArgs * len(args_list))()
+    for i, a in enumerate(args_list):
+        arr[i] = a
+    return arr
+
+
+def words64(G: int) -> int:
+    return (G + 63) // 64
+
+
+def words32(G: int) -> int:
+    return (G + 31) // 32
+
+
+# ------------------------------------------------------------------------------ device buffers
+@dataclass
+class CommitBuffers:
+    """SoA device state of one batch of G groups (DESIGN.md "Data layout in HBM")."""
+
+    G: int
+    n_max: int
+    form: int
+    ring_len: int
+    match: DeviceArray
+    committed_in: DeviceArray
+    committed_out: DeviceArray
+    last_index: DeviceArray
+    aux: DeviceArray            # term_start (term-start form) or term (ring form)
+    ring: Optional[DeviceArray]
+    n_voting: Optional[DeviceArray]
+    changed: DeviceArray
+    fallback: DeviceArray
+    term_start: Optional[DeviceArray] = None
+    term: Optional[DeviceArray] = None
+
+    def args(self) -> CommitArgs:
+        a = CommitArgs()
+        a.G = self.G
+        a.n_max = self.n_max
+        a.form = self.form
+        a.ring_len = self.ring_len
+        a.match_stride = self.G
+        a.match = self.match.ptr
+        a.n_voting = self.n_voting.ptr if self.n_voting else None
+        a.committed_in = self.committed_in.ptr
+        a.committed_out = self.committed_out.ptr
+        a.last_index = self.last_index.ptr
+        a.term_start = self.term_start.ptr if self.term_start else None
+        a.term = self.term.ptr if self.term else None
+        a.ring = self.ring.ptr if self.ring else None
+        a.changed = self.changed.ptr
+        a.fallback = self.fallback.ptr
+        return a
+
+    def arrays(self):
+        return [x for x in (self.match, self.committed_in, self.committed_out, self.last_index,
+                            self.term_start, self.term, self.ring, self.n_voting, self.changed,
+                            self.fallback) if x is not None]
+
+
+def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
+                 per_group_n: bool = False, with_both_aux: bool = False) -> CommitBuffers:
+    """Allocate the SoA columns of one commit batch (match is slot-major [n_max][G])."""
+    need_ts = form == HQ_FORM_TERM_START or with_both_aux
+    need_ring = form == HQ_FORM_TERM_RING or with_both_aux
+    ts = ctx.empty(G, np.uint64) if need_ts else None
+    term = ctx.empty(G, np.uint64) if need_ring else None
+    b = CommitBuffers(
+        G=G, n_max=n_max, form=form, ring_len=ring_len,
+        match=ctx.empty(G * n_max, np.uint64),
+        committed_in=ctx.empty(G, np.uint64),
+        committed_out=ctx.empty(G, np.uint64),
+        last_index=ctx.empty(G, np.uint64),
+        aux=ts if form == HQ_FORM_TERM_START else term,
+        ring=ctx.empty(G * ring_len, np.uint64) if need_ring else None,
+        n_voting=ctx.empty(G, np.uint8) if per_group_n else None,
+        changed=ctx.empty(words64(G), np.uint64),
+        fallback=ctx.empty(words64(G), np.uint64),
+        term_start=ts, term=term,
+    )
+    return b
+
+
+def synth_spec(seed: int, G: int, n_max: int, cid_base: int = 1, cid_stride: int = 1,
+               mixed_n: bool = False, ring_len: int = 16, parity_extras: bool = False) -> SynthSpec:
+    s = SynthSpec()
+    s.seed = seed
+    s.G = G
+    s.cid_base = cid_base
+    s.cid_stride = cid_stride
+    s.n_max = n_max
+    s.mixed_n = int(mixed_n)
+    s.ring_len = ring_len
+    s.parity_extras = int(parity_extras)
+    return s
+
+
+def free_commit(ctx: Context, b: CommitBuffers) -> None:
+    for a in b.arrays():
+        ctx.free(a)

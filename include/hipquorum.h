@@ -1,0 +1,228 @@
+/*
+ * hipquorum.h — C-ABI of libhipquorum.so, the MI355X (gfx950) batched quorum engine for
+ * dragonboat's multi-group Raft leader path.
+ *
+ * One call evaluates one quorum predicate for G independent Raft groups laid out as
+ * structure-of-arrays in HBM. The entry points replace these reference interfaces
+ * (paths relative to the dragonboat v3.3 tree):
+ *
+ *   hq_commit*        raft.tryCommit + sortMatchValues      internal/raft/raft.go:861-909
+ *                     entryLog.tryCommit / term / commitTo  internal/raft/logentry.go:143-160,323-332,378-393
+ *                     quorum / numVotingMembers             internal/raft/raft.go:368-378
+ *   hq_readindex*     readIndex.confirm (quorum test)       internal/raft/readindex.go:77-116 (:84)
+ *                     handleReadIndexLeaderConfirmation     internal/raft/raft.go:1740-1760
+ *   hq_vote*          handleVoteResp / handleCandidateRequestVoteResp
+ *                                                           internal/raft/raft.go:1062-1080,1968-1985
+ *   hq_check_quorum*  leaderHasQuorum                       internal/raft/raft.go:380-390
+ *
+ * The reference has no plugin/FFI for this path (the quorum code lives in unexported methods of
+ * the unexported raft struct, raft.go:198). The cgo binding a maintainer adds under
+ * internal/hipquorum is shown in INTEGRATION.md; it follows the gorocksdb cgo conventions
+ * (internal/logdb/kv/rocksdb/gorocksdb/db.go:3-9, errptr pattern db.go:241-253).
+ *
+ * Conventions
+ *   - Every function returns an int status: HQ_OK (0) or a negative HQ_E_* code. The message of
+ *     the last failure on a context is returned by hq_last_error(). Nothing aborts across the ABI.
+ *   - A context owns one HIP stream on one GPU. A context is not thread-safe; use one per step
+ *     worker (execengine.go:675-690). Different contexts may be used concurrently.
+ *   - *_dev functions take DEVICE pointers (from hq_malloc_dev) and are asynchronous on the
+ *     context's stream; call hq_sync() before reading results on the host.
+ *     The functions without _dev take HOST pointers (pinned memory from hq_alloc_pinned is
+ *     fastest), stage through the context's device workspace and return when results are on the
+ *     host.
+ *   - Bitmaps are arrays of uint64_t words, little-endian bit order: group g is bit (g % 64) of
+ *     word g / 64. Bits of groups >= G in the last word are written as 0.
+ *   - All arithmetic is unsigned 64-bit integer; results are bit-exact with the reference.
+ */
+#ifndef HIPQUORUM_H
+#define HIPQUORUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HQ_ABI_VERSION 1
+
+/* status codes */
+#define HQ_OK          0
+#define HQ_E_INVAL    -1   /* bad argument (null pointer, bad size, misaligned, bad form) */
+#define HQ_E_DEVICE   -2   /* HIP runtime error (launch failure, no device) */
+#define HQ_E_NOMEM    -3   /* allocation failed */
+#define HQ_E_STATE    -4   /* operation not valid in the context's current state */
+
+/* maximum packed voting slots per group in the bitmap kernels (u8 bitmaps) and commit kernels */
+#define HQ_MAX_VOTERS 8
+
+/* commit term-check forms (see hq_commit_args) */
+#define HQ_FORM_TERM_START 0  /* term(q)==term  <=>  term_start <= q <= last_index */
+#define HQ_FORM_TERM_RING  1  /* term(q) gathered from a per-group ring of the last R terms */
+
+/* vote outcomes, numerically equal to the reference State enum (internal/raft/raft.go:62-71) */
+#define HQ_OUTCOME_FOLLOWER  0u   /* rejections reached quorum: becomeFollower (raft.go:1981-1984) */
+#define HQ_OUTCOME_CANDIDATE 1u   /* undecided: stays candidate */
+#define HQ_OUTCOME_LEADER    2u   /* grants reached quorum: becomeLeader (raft.go:1977-1980) */
+
+typedef struct hq_ctx hq_ctx;
+
+/* ---------------------------------------------------------------- context / memory ---------- */
+
+/* Version of the ABI this library implements (HQ_ABI_VERSION). */
+int hq_abi_version(void);
+/* Number of visible GPUs. */
+int hq_device_count(int *out);
+/* Open a context (one HIP stream) on GPU `device`. flags: reserved, pass 0. */
+int hq_open(int device, uint32_t flags, hq_ctx **out);
+/* Destroy a context; waits for its stream. NULL is a no-op. */
+void hq_close(hq_ctx *ctx);
+/* Message of the last failure on ctx (never NULL; "" if none). ctx may be NULL for hq_open
+ * failures: then the thread's last open error is returned. */
+const char *hq_last_error(const hq_ctx *ctx);
+/* Wait for all work queued on the context's stream. */
+int hq_sync(hq_ctx *ctx);
+
+int hq_malloc_dev(hq_ctx *ctx, size_t bytes, void **out);
+int hq_free_dev(hq_ctx *ctx, void *p);
+int hq_alloc_pinned(hq_ctx *ctx, size_t bytes, void **out);
+int hq_free_pinned(hq_ctx *ctx, void *p);
+/* Asynchronous copies / fill on the context's stream. kind: 0 = H2D, 1 = D2H, 2 = D2D. */
+int hq_memcpy_async(hq_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
+int hq_memset_async(hq_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* Kernel timing: when enabled, every kernel the context launches is bracketed by HIP events on
+ * the context's stream. hq_timing_read() synchronises the stream and returns the summed kernel
+ * time (ms) and the number of timed launches since the last reset. */
+int hq_timing_enable(hq_ctx *ctx, int enable);
+int hq_timing_read(hq_ctx *ctx, double *total_ms, uint64_t *launches);
+int hq_timing_reset(hq_ctx *ctx);
+
+/* ---------------------------------------------------------------- commit ------------------- */
+
+/*
+ * Batched leader commit decision, one Raft group per index g in [0, G).
+ *
+ * For each group (raft.go:888-909 + logentry.go:378-393):
+ *   n  = n_voting ? n_voting[g] : n_max          voting members = remotes + witnesses
+ *                                                (self included, observers never packed)
+ *   q  = the (n/2+1)-th largest of match[0..n-1][g]     == matched[n - quorum] after sorting
+ *   lt = term(q)                                    (0 outside [first-1, last], logentry.go:144)
+ *   if q > committed_in[g] && lt == term[g]:  committed_out[g] = q, changed bit = 1
+ *   else                                       committed_out[g] = committed_in[g], changed = 0
+ *
+ * term(q) == term is evaluated in one of two exact forms:
+ *   HQ_FORM_TERM_START  term_start[g] = index of the leader's first entry of its current term (the
+ *       no-op appended by becomeLeader, raft.go:987). Because entries carry the leader's term
+ *       (raft.go:913-916) and log terms never decrease (entryutils.go:44-47):
+ *       term(q) == term  <=>  term_start[g] <= q <= last_index[g].  `term`/`ring` unused.
+ *   HQ_FORM_TERM_RING   ring[g * ring_len + (i % ring_len)] = term(i) for i in
+ *       (last_index - ring_len, last_index]. The gather happens only when q > committed; it is
+ *       exact when last_index[g] - committed_in[g] <= ring_len.
+ *
+ * Groups that violate the contract are NOT decided: committed_out = committed_in, changed = 0 and
+ * the fallback bit is set so the caller runs the CPU path (raft.go:888) for them:
+ *   n == 0 or n > n_max;  RING form only: term == 0, committed > last_index, or
+ *   last_index - committed > ring_len.
+ *
+ * Layout: match is slot-major, match[s * match_stride + g]; match_stride >= G.
+ * committed_out may alias committed_in. changed / fallback may be NULL.
+ */
+typedef struct hq_commit_args {
+    uint64_t G;               /* groups in this call */
+    uint32_t n_max;           /* packed slots per group, 1..HQ_MAX_VOTERS */
+    uint32_t form;            /* HQ_FORM_TERM_START or HQ_FORM_TERM_RING */
+    uint32_t ring_len;        /* R for HQ_FORM_TERM_RING: power of two, 1..1024 */
+    uint32_t reserved;        /* pass 0 */
+    uint64_t match_stride;    /* elements between slot rows of match, >= G */
+    const uint64_t *match;    /* [n_max][match_stride] */
+    const uint8_t *n_voting;  /* [G] voting members per group, or NULL: all groups have n_max */
+    const uint64_t *committed_in;   /* [G] */
+    uint64_t *committed_out;        /* [G] (may alias committed_in) */
+    const uint64_t *last_index;     /* [G] */
+    const uint64_t *term_start;     /* [G] HQ_FORM_TERM_START */
+    const uint64_t *term;           /* [G] HQ_FORM_TERM_RING: the leader's current term */
+    const uint64_t *ring;           /* [G][ring_len] HQ_FORM_TERM_RING */
+    uint64_t *changed;              /* [ceil(G/64)] or NULL */
+    uint64_t *fallback;             /* [ceil(G/64)] or NULL */
+} hq_commit_args;
+
+int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *args);
+int hq_commit(hq_ctx *ctx, const hq_commit_args *args);
+/* `count` independent batches back to back on the context's stream (e.g. a step worker's
+ * per-voter-count buckets of one step, or successive steps). Stops at the first invalid batch. */
+int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
+
+/* ---------------------------------------------------------------- ReadIndex / vote ----------- */
+
+/*
+ * ReadIndex heartbeat-ack quorum, one pending ctx per group (readindex.go:77-116):
+ *   confirmed bit = popcount(ack[g] & mask(n)) + 1 >= n/2 + 1     (the +1 is the leader, :84)
+ * ack[g] bit s = voting slot s acknowledged the pending SystemCtx (distinct `from`); bits >= n are
+ * ignored. n = n_voting ? n_voting[g] : n_uniform, valid 1..8; groups with an invalid n get
+ * confirmed = 0 and, if `fallback` is non-NULL, a fallback bit.
+ */
+int hq_readindex_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *n_voting,
+                     uint32_t n_uniform, uint64_t *confirmed, uint64_t *fallback);
+int hq_readindex(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *n_voting,
+                 uint32_t n_uniform, uint64_t *confirmed, uint64_t *fallback);
+
+/*
+ * Vote tally (raft.go:1062-1080, 1968-1985). granted[g] bit s = slot s granted (the candidate's
+ * own vote, campaign raft.go:1093, is a granted bit); rejected[g] bit s = slot s rejected.
+ * First response wins (raft.go:1071-1073): a slot present in both is counted as granted.
+ *   outcome = popcount(granted) >= q ? LEADER : popcount(rejected & ~granted) >= q ? FOLLOWER
+ *                                                                            : CANDIDATE
+ * Outcomes are 2-bit codes packed 32 per uint64_t word: group g at bits 2*(g%32) of word g/32.
+ * Invalid n gives CANDIDATE (+ fallback bit).
+ */
+int hq_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *rejected,
+                const uint8_t *n_voting, uint32_t n_uniform, uint64_t *outcome,
+                uint64_t *fallback);
+int hq_vote(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *rejected,
+            const uint8_t *n_voting, uint32_t n_uniform, uint64_t *outcome, uint64_t *fallback);
+
+/* ReadIndex confirmation and vote tally of the same groups in one pass over the shared n. */
+int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                          const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
+                          uint64_t *confirmed, uint64_t *outcome, uint64_t *fallback);
+
+/*
+ * CheckQuorum (raft.go:380-390): has_quorum bit = popcount(active[g] | 1 << self_slot) >= q,
+ * then every active flag is reset (remote.go:196-198): active[g] is written back as 0.
+ * self_slot is the leader's slot (the packer puts the leader in slot 0).
+ */
+int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active, const uint8_t *n_voting,
+                        uint32_t n_uniform, uint32_t self_slot, uint64_t *has_quorum,
+                        uint64_t *fallback);
+
+/* ---------------------------------------------------------------- synthetic inputs ---------- */
+
+/*
+ * Deterministic synthetic inputs generated on the device (benchmarks and parity tests; inputs
+ * never cross PCIe). Group j of the call has clusterID cid = cid_base + j * cid_stride and draws
+ * from splitmix64 seeded with (seed ^ cid). The byte-identical CPU generator is oracle/qgen.c;
+ * the recipe is DESIGN.md "Synthetic inputs".
+ */
+typedef struct hq_synth_spec {
+    uint64_t seed;
+    uint64_t G;
+    uint64_t cid_base;        /* clusterID of group 0 (>= 1; 0 is NoNode, raft.go:48) */
+    uint64_t cid_stride;      /* clusterID step between consecutive groups (>= 1) */
+    uint32_t n_max;           /* slots per group */
+    uint32_t mixed_n;         /* 0: every group has n_max voters; 1: n = {3,5,7}[cid % 3] */
+    uint32_t ring_len;        /* R: spread of committed/term_start below last, ring length */
+    uint32_t parity_extras;   /* 1: add the rare edge cases (q > last, committed == last) */
+} hq_synth_spec;
+
+/* Fills match (n_max rows at args->match_stride), n_voting (if non-NULL), committed_in,
+ * last_index, term_start, term and ring (each if non-NULL) of *args; args->form is ignored. */
+int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *spec, const hq_commit_args *args);
+/* Fills the ack / granted / rejected bitmaps and n_voting (each if non-NULL). */
+int hq_synth_bitmaps_dev(hq_ctx *ctx, const hq_synth_spec *spec, uint8_t *ack, uint8_t *granted,
+                         uint8_t *rejected, uint8_t *n_voting);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIPQUORUM_H */

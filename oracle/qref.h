@@ -1,0 +1,184 @@
+/*
+ * qref.h — CPU oracle for the hipquorum parity tests. TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of dragonboat's leader quorum arithmetic (reference tree
+ * /root/reference, Go module github.com/lni/dragonboat/v3, v3.3-dev). Each function cites the
+ * reference file:line it restates. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the CPU baseline — the
+ * product (libhipquorum.so) never links or calls it.
+ *
+ * Pinning: the reference is Go and no Go toolchain exists in this image, so the reference itself
+ * cannot be run. This restatement is pinned by the known-answer tables of the reference's own
+ * tests, transcribed as fixtures under tests/golden/ (see tests/golden/make_golden.py for the
+ * file:line of every table), plus an independent count-based definition of the commit quorum.
+ */
+#ifndef QREF_H
+#define QREF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QREF_MAX_NODES   64
+#define QREF_MAX_PENDING 256
+
+/* reference State enum values (internal/raft/raft.go:62-71) */
+#define QREF_FOLLOWER  0
+#define QREF_CANDIDATE 1
+#define QREF_LEADER    2
+
+/* status codes for reference panics (the Go code panics; the oracle reports) */
+#define QREF_OK            0
+#define QREF_PANIC        -100
+
+/* ---------------------------------------------------------------- quorum arithmetic ------- */
+int qref_num_voting_members(int n_remotes, int n_witnesses);   /* raft.go:368-370 */
+int qref_quorum(int n_voting);                                  /* raft.go:372-374 */
+int qref_is_single_node_quorum(int n_voting);                   /* raft.go:376-378 */
+void qref_sort_match_values(uint64_t *matched, int n);          /* raft.go:861-886 */
+
+/* ---------------------------------------------------------------- entry log term ---------- */
+/* Term source for indexes inside [first-1, last]: stands for inMemory.getTerm
+ * (inmemory.go:87-105) followed by ILogDB.Term (logentry.go:152-159). Returns the term. */
+typedef uint64_t (*qref_term_fn)(const void *ud, uint64_t index);
+
+typedef struct qref_log {
+    uint64_t first_minus_1;   /* termEntryRange() first (logentry.go:117-126) */
+    uint64_t last;            /* lastIndex() (logentry.go:107-115) */
+    uint64_t committed;       /* entryLog.committed */
+    qref_term_fn term_at;
+    const void *ud;
+} qref_log;
+
+uint64_t qref_log_term(const qref_log *l, uint64_t index);       /* logentry.go:143-160 */
+/* entryLog.tryCommit (logentry.go:378-393) incl. commitTo (:323-332). Returns 1 if committed
+ * advanced, 0 if not, QREF_PANIC where the reference panics (commitTo beyond lastIndex). */
+int qref_log_try_commit(qref_log *l, uint64_t index, uint64_t term);
+
+/* raft.tryCommit (raft.go:888-909): matched = remotes' match then witnesses' match; sort; q =
+ * matched[n - quorum]; log.tryCommit(q, term). *q_out (may be NULL) receives q. */
+int qref_try_commit(const uint64_t *remote_match, int n_remotes,
+                    const uint64_t *witness_match, int n_witnesses,
+                    qref_log *log, uint64_t term, uint64_t *q_out);
+
+/* Independent definition used to cross-check sort + index: q = max{x in match :
+ * |{i : match_i >= x}| >= quorum}. */
+uint64_t qref_quorum_match_by_count(const uint64_t *match, int n);
+
+/* ---------------------------------------------------------------- ReadIndex --------------- */
+typedef struct qref_sysctx { uint64_t low, high; } qref_sysctx;   /* raftpb/raft.go:46-49 */
+
+typedef struct qref_read_status {                                  /* readindex.go:21-26 */
+    uint64_t index;
+    uint64_t from;
+    qref_sysctx ctx;
+    int n_confirmed;
+    uint64_t confirmed[QREF_MAX_NODES];
+} qref_read_status;
+
+typedef struct qref_read_index {                                   /* readindex.go:31-34 */
+    qref_read_status pending[QREF_MAX_PENDING];  /* map keyed by ctx */
+    int n_pending;
+    qref_sysctx queue[QREF_MAX_PENDING];
+    int n_queue;
+} qref_read_index;
+
+void qref_ri_init(qref_read_index *r);
+/* readindex.go:43-67. Returns QREF_OK (also when the ctx was already pending: ignored) or
+ * QREF_PANIC ("index moved backward", "inconsistent pending and queue"). */
+int qref_ri_add_request(qref_read_index *r, uint64_t index, qref_sysctx ctx, uint64_t from);
+int qref_ri_has_pending(const qref_read_index *r);                 /* readindex.go:69-71 */
+/* readindex.go:77-116. Returns the number of released statuses (0 = nil) and copies them, in
+ * queue order with the rewritten index, into out[0..] (capacity QREF_MAX_PENDING); QREF_PANIC
+ * where the reference panics. */
+int qref_ri_confirm(qref_read_index *r, qref_sysctx ctx, uint64_t from, int quorum,
+                    qref_read_status *out);
+
+/* ---------------------------------------------------------------- votes ------------------- */
+typedef struct qref_votes {                                        /* raft.go:210 votes map */
+    int n;
+    uint64_t from[QREF_MAX_NODES];
+    int granted[QREF_MAX_NODES];
+} qref_votes;
+
+void qref_votes_reset(qref_votes *v);                              /* raft.go:999 */
+int qref_handle_vote_resp(qref_votes *v, uint64_t from, int rejected);   /* raft.go:1062-1080 */
+/* handleCandidateRequestVoteResp (raft.go:1968-1985) for a candidate; returns the state after
+ * the message (QREF_LEADER / QREF_FOLLOWER / QREF_CANDIDATE). Observer responses are dropped. */
+int qref_candidate_vote_resp(qref_votes *v, uint64_t from, int rejected, int from_is_observer,
+                             int quorum);
+
+/* leaderHasQuorum (raft.go:380-390): voting members with id == self or active count; every
+ * member's active flag is reset (remote.go:196-198). */
+int qref_leader_has_quorum(const uint64_t *ids, int *active, int n_voting, uint64_t self_id);
+
+/* ---------------------------------------------------------------- batched SoA forms ------- */
+/* Same memory layout and semantics as hq_commit_args in include/hipquorum.h (duplicated here so
+ * that the oracle does not depend on the product headers). */
+typedef struct qref_commit_args {
+    uint64_t G;
+    uint32_t n_max;
+    uint32_t form;            /* 0 = term-start, 1 = ring */
+    uint32_t ring_len;
+    uint32_t reserved;
+    uint64_t match_stride;
+    const uint64_t *match;
+    const uint8_t *n_voting;
+    const uint64_t *committed_in;
+    uint64_t *committed_out;
+    const uint64_t *last_index;
+    const uint64_t *term_start;
+    const uint64_t *term;
+    const uint64_t *ring;
+    uint64_t *changed;
+    uint64_t *fallback;
+} qref_commit_args;
+
+/* Batched commit: every group goes through qref_try_commit over a log view. Returns QREF_OK,
+ * -1 on bad arguments, QREF_PANIC if some group reached a reference panic. nthreads <= 1 runs
+ * single-threaded; otherwise groups are split over nthreads pthreads in contiguous 64-aligned
+ * blocks (bitmap words are never shared between threads). */
+int qref_commit_batch(const qref_commit_args *a, int nthreads);
+
+/* One pending ctx per group: addRequest + one confirm per acked slot in slot order
+ * (readindex.go:43-116); confirmed bit = some confirm released the ctx. */
+int qref_readindex_batch(uint64_t G, const uint8_t *ack, const uint8_t *n_voting,
+                         uint32_t n_uniform, uint64_t *confirmed, uint64_t *fallback,
+                         int nthreads);
+/* campaign self-vote (raft.go:1093) then one RequestVoteResp per responding slot in slot order
+ * through handleCandidateRequestVoteResp; outcome packed 2 bits per group. */
+int qref_vote_batch(uint64_t G, const uint8_t *granted, const uint8_t *rejected,
+                    const uint8_t *n_voting, uint32_t n_uniform, uint64_t *outcome,
+                    uint64_t *fallback, int nthreads);
+int qref_check_quorum_batch(uint64_t G, uint8_t *active, const uint8_t *n_voting,
+                            uint32_t n_uniform, uint32_t self_slot, uint64_t *has_quorum,
+                            uint64_t *fallback, int nthreads);
+
+/* ---------------------------------------------------------------- synthetic inputs -------- */
+/* Same layout as hq_synth_spec; CPU twin of the device generator. */
+typedef struct qgen_spec {
+    uint64_t seed;
+    uint64_t G;
+    uint64_t cid_base;
+    uint64_t cid_stride;
+    uint32_t n_max;
+    uint32_t mixed_n;
+    uint32_t ring_len;
+    uint32_t parity_extras;
+} qgen_spec;
+
+uint64_t qgen_splitmix64(uint64_t *state);
+int qgen_commit(const qgen_spec *s, const qref_commit_args *out);
+int qgen_bitmaps(const qgen_spec *s, uint8_t *ack, uint8_t *granted, uint8_t *rejected,
+                 uint8_t *n_voting);
+
+/* FNV-1a 64 over a byte range (fixture checksums). */
+uint64_t qref_fnv1a64(const void *p, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

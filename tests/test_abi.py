@@ -1,0 +1,96 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what include/hipquorum.h
+declares, the ctypes struct mirrors match the C layout, and argument validation fails cleanly."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hipquorum.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|void|const char \*)\s*\*?(hq_\w+)\(", text, re.M)))
+
+
+def test_exports_match_header(hq):
+    names = declared_functions()
+    assert len(names) >= 20
+    out = subprocess.run(["nm", "-D", "--defined-only", hq.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = sorted(set(re.findall(r" T (hq_\w+)$", out, re.M)))
+    assert exported == names
+    assert sorted(hq.SIGNATURES) == names   # the binding declares every entry point
+    for n in names:
+        assert getattr(hq.lib, n)
+
+
+def test_abi_version(hq):
+    assert hq.lib.hq_abi_version() == 1
+
+
+LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hipquorum.h"
+#define F(T, m) printf(#T "." #m " %zu\n", offsetof(T, m));
+int main(void) {
+  printf("hq_commit_args %zu\n", sizeof(hq_commit_args));
+  printf("hq_synth_spec %zu\n", sizeof(hq_synth_spec));
+  F(hq_commit_args, G) F(hq_commit_args, n_max) F(hq_commit_args, form)
+  F(hq_commit_args, ring_len) F(hq_commit_args, match_stride) F(hq_commit_args, match)
+  F(hq_commit_args, n_voting) F(hq_commit_args, committed_in) F(hq_commit_args, committed_out)
+  F(hq_commit_args, last_index) F(hq_commit_args, term_start) F(hq_commit_args, term)
+  F(hq_commit_args, ring) F(hq_commit_args, changed) F(hq_commit_args, fallback)
+  F(hq_synth_spec, seed) F(hq_synth_spec, G) F(hq_synth_spec, cid_base)
+  F(hq_synth_spec, cid_stride) F(hq_synth_spec, n_max) F(hq_synth_spec, mixed_n)
+  F(hq_synth_spec, ring_len) F(hq_synth_spec, parity_extras)
+  return 0;
+}
+"""
+
+
+def test_struct_layout_matches_c(hq, tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(LAYOUT_C)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", str(exe),
+                    str(src)], check=True)
+    lines = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    c = dict(l.rsplit(" ", 1) for l in lines if l)
+    assert int(c["hq_commit_args"]) == ctypes.sizeof(hq.CommitArgs)
+    assert int(c["hq_synth_spec"]) == ctypes.sizeof(hq.SynthSpec)
+    for key, val in c.items():
+        if "." in key:
+            t, m = key.split(".")
+            cls = hq.CommitArgs if t == "hq_commit_args" else hq.SynthSpec
+            assert getattr(cls, m).offset == int(val), key
+
+
+def test_null_context_is_invalid(hq):
+    a = hq.CommitArgs()
+    assert hq.lib.hq_commit_dev(None, ctypes.byref(a)) == hq.HQ_E_INVAL
+    assert hq.lib.hq_sync(None) == hq.HQ_E_INVAL
+    assert hq.lib.hq_readindex_dev(None, 0, None, None, 3, None, None) == hq.HQ_E_INVAL
+    assert hq.lib.hq_vote_dev(None, 0, None, None, None, 3, None, None) == hq.HQ_E_INVAL
+    hq.lib.hq_close(None)  # no-op
+    assert hq.lib.hq_last_error(None) is not None
+
+
+def test_open_without_gpu_fails_cleanly(hq):
+    if hq.device_count() > 0:
+        pytest.skip("a GPU is visible: covered by the gpu tests")
+    with pytest.raises(hq.HQError) as e:
+        hq.Context(0)
+    assert e.value.code == hq.HQ_E_DEVICE
+    assert "no HIP device" in str(e.value)
+
+
+def test_kernels_are_gfx950(hq):
+    """The fat binary carries gfx950 code objects only (no other offload target)."""
+    blob = open(hq.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-+(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
