@@ -38,6 +38,9 @@ WORKLOADS = {
     "c3": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=1, mixed=False,
                desc="1M groups x 5 voters (4 full + 1 witness; observers never packed), "
                     "commit + term-ring gather R=16"),
+    "c3m": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False,
+                desc="1M groups x 5 voters (4 full + 1 witness), commit + 16-bit current-term "
+                     "mask (exact replacement of the ring gather)"),
     "c4": dict(cfg=3, kind="bits", G=16 << 20, n=7,
                desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
 }
@@ -46,8 +49,9 @@ WORKLOADS = {
 def algo_bytes_per_group(w):
     """bytes the decision must move per group."""
     if w["kind"] == "commit":
-        n = w["n"]
-        return 8 * n + 32 if w["form"] == 0 else 8 * n + 40 + (1 if w["mixed"] else 0)
+        n, extra_n = w["n"], (1 if w["mixed"] else 0)
+        # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask)
+        return 8 * n + 24 + {0: 8, 1: 16, 2: 2}[w["form"]] + extra_n
     return 4 + 3 / 8   # ack, granted, rejected, n (u8 each) in; confirmed bit + 2-bit outcome out
 
 
@@ -238,7 +242,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c3,c4",
+    ap.add_argument("--extra", default="c3,c3m,c4",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -276,7 +280,7 @@ def main():
             "config": {
                 "workload": f"{args.workload}: {w['desc']}",
                 "groups_per_gpu": w["G"], "voters": w["n"],
-                "form": ("term_start" if w.get("form") == 0 else "ring")
+                "form": {0: "term_start", 1: "ring", 2: "term_mask"}[w["form"]]
                 if w["kind"] == "commit" else "bitmaps",
                 "global_groups_per_step": w["G"] * d.world,
                 "parallelism": f"shard{d.world} (clusterID % {d.world})",
@@ -285,6 +289,8 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
                 "kernel_avg_us": r["avg_kernel_s"] * 1e6,
+                "kernel_time": "HIP events bracketing the timed region on the launch stream / "
+                               "launches (kernel + dependent-launch boundary)",
                 "algorithmic_bytes_per_launch": r["bytes_per_launch"],
                 "measured_copy_ceiling_gbs": HBM_MEASURED_COPY_GBS,
             },

@@ -13,10 +13,13 @@ struct hq_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    // kernel timing (hq_timing_*): event pairs recorded around every launch
-    bool timing = false;
-    std::vector<hipEvent_t> ev_start, ev_stop;
-    size_t ev_used = 0;
+    // kernel timing (hq_timing_*): one event pair on the stream brackets a timed region; every
+    // launch inside it is counted. Per-launch event pairs are avoided on purpose: on gfx950 an
+    // event pair around a ~10 us kernel adds 3-6 us to the measured time and to the wall clock.
+    bool timing = false;      // a region is open (begin recorded, end not yet)
+    bool region_done = false; // a closed region awaits hq_timing_read
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    uint64_t region_launches = 0;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
     // device workspace for the host-pointer entry points

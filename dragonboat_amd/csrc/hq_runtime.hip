@@ -25,30 +25,12 @@ int check_hip(hq_ctx *ctx, hipError_t e, const char *what) {
 
 int pre_launch(hq_ctx *ctx) {
     int rc = check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    if (rc || !ctx->timing) return rc;
-    if (ctx->ev_used == ctx->ev_start.size()) {
-        hipEvent_t a, b;
-        rc = check_hip(ctx, hipEventCreate(&a), "hipEventCreate");
-        if (rc) return rc;
-        rc = check_hip(ctx, hipEventCreate(&b), "hipEventCreate");
-        if (rc) { (void)hipEventDestroy(a); return rc; }
-        ctx->ev_start.push_back(a);
-        ctx->ev_stop.push_back(b);
-    }
-    return check_hip(ctx, hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream),
-                     "hipEventRecord");
+    if (!rc && ctx->timing) ctx->region_launches++;
+    return rc;
 }
 
 int post_launch(hq_ctx *ctx, const char *what) {
-    int rc = check_hip(ctx, hipGetLastError(), what);
-    if (rc) return rc;
-    if (ctx->timing) {
-        rc = check_hip(ctx, hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream),
-                       "hipEventRecord");
-        if (rc) return rc;
-        ctx->ev_used++;
-    }
-    return HQ_OK;
+    return check_hip(ctx, hipGetLastError(), what);
 }
 
 int ensure_workspace(hq_ctx *ctx, size_t bytes) {
@@ -108,8 +90,8 @@ void hq_close(hq_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (hipEvent_t e : ctx->ev_start) (void)hipEventDestroy(e);
-    for (hipEvent_t e : ctx->ev_stop) (void)hipEventDestroy(e);
+    if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
+    if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -178,25 +160,52 @@ int hq_memset_async(hq_ctx *ctx, void *dst, int value, size_t bytes) {
     return hq::check_hip(ctx, hipMemsetAsync(dst, value, bytes, ctx->stream), "hipMemsetAsync");
 }
 
+static int timing_close(hq_ctx *ctx) {
+    if (!ctx->timing) return HQ_OK;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (!rc) rc = hq::check_hip(ctx, hipEventRecord(ctx->ev_end, ctx->stream), "hipEventRecord");
+    if (rc) return rc;
+    ctx->timing = false;
+    ctx->region_done = true;
+    return HQ_OK;
+}
+
+static int timing_fold(hq_ctx *ctx) {
+    if (!ctx->region_done) return HQ_OK;
+    int rc = hq::check_hip(ctx, hipEventSynchronize(ctx->ev_end), "hipEventSynchronize");
+    if (rc) return rc;
+    float ms = 0.f;
+    rc = hq::check_hip(ctx, hipEventElapsedTime(&ms, ctx->ev_begin, ctx->ev_end),
+                       "hipEventElapsedTime");
+    if (rc) return rc;
+    ctx->timed_ms += ms;
+    ctx->timed_launches += ctx->region_launches;
+    ctx->region_launches = 0;
+    ctx->region_done = false;
+    return HQ_OK;
+}
+
 int hq_timing_enable(hq_ctx *ctx, int enable) {
     if (!ctx) return HQ_E_INVAL;
-    ctx->timing = enable != 0;
+    if (!enable) return timing_close(ctx);
+    if (ctx->timing) return HQ_OK;
+    int rc = timing_fold(ctx);  // a previous region is accumulated before its events are reused
+    if (rc) return rc;
+    rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (!rc && !ctx->ev_begin) rc = hq::check_hip(ctx, hipEventCreate(&ctx->ev_begin), "hipEventCreate");
+    if (!rc && !ctx->ev_end) rc = hq::check_hip(ctx, hipEventCreate(&ctx->ev_end), "hipEventCreate");
+    if (!rc) rc = hq::check_hip(ctx, hipEventRecord(ctx->ev_begin, ctx->stream), "hipEventRecord");
+    if (rc) return rc;
+    ctx->timing = true;
+    ctx->region_launches = 0;
     return HQ_OK;
 }
 
 int hq_timing_read(hq_ctx *ctx, double *total_ms, uint64_t *launches) {
     if (!ctx) return HQ_E_INVAL;
-    int rc = hq_sync(ctx);
+    int rc = timing_close(ctx);
+    if (!rc) rc = timing_fold(ctx);
     if (rc) return rc;
-    for (size_t i = 0; i < ctx->ev_used; ++i) {
-        float ms = 0.f;
-        rc = hq::check_hip(ctx, hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]),
-                           "hipEventElapsedTime");
-        if (rc) return rc;
-        ctx->timed_ms += ms;
-        ctx->timed_launches++;
-    }
-    ctx->ev_used = 0;
     if (total_ms) *total_ms = ctx->timed_ms;
     if (launches) *launches = ctx->timed_launches;
     return HQ_OK;
@@ -204,9 +213,9 @@ int hq_timing_read(hq_ctx *ctx, double *total_ms, uint64_t *launches) {
 
 int hq_timing_reset(hq_ctx *ctx) {
     if (!ctx) return HQ_E_INVAL;
-    int rc = hq_sync(ctx);
+    int rc = timing_close(ctx);
+    if (!rc) rc = timing_fold(ctx);
     if (rc) return rc;
-    ctx->ev_used = 0;
     ctx->timed_ms = 0.0;
     ctx->timed_launches = 0;
     return HQ_OK;
@@ -249,8 +258,10 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
         return hq_commit_dev(ctx, a);  // same validation and message
     const uint64_t G = a->G, nw = hq::words64(G);
     const bool ring = a->form == HQ_FORM_TERM_RING;
+    const bool mask = a->form == HQ_FORM_TERM_MASK;
     if (ring && (!a->ring || !a->term)) return hq_commit_dev(ctx, a);
-    if (!ring && !a->term_start) return hq_commit_dev(ctx, a);
+    if (mask && !a->term_mask) return hq_commit_dev(ctx, a);
+    if (!ring && !mask && !a->term_start) return hq_commit_dev(ctx, a);
     const size_t col = G * 8;
     size_t need = Stage::pad(col * a->n_max) + 4 * Stage::pad(col) + 2 * Stage::pad(nw * 8) +
                   Stage::pad(G) + (ring ? Stage::pad(col * a->ring_len) : 0);
@@ -276,6 +287,9 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
         d.ring = dring;
         if (!rc) rc = h2d(ctx, daux, a->term, col);
         if (!rc) rc = h2d(ctx, dring, a->ring, col * a->ring_len);
+    } else if (mask) {
+        d.term_mask = reinterpret_cast<uint16_t *>(daux);
+        if (!rc) rc = h2d(ctx, daux, a->term_mask, G * 2);
     } else {
         d.term_start = daux;
         if (!rc) rc = h2d(ctx, daux, a->term_start, col);

@@ -26,6 +26,7 @@ HQ_E_STATE = -4
 HQ_MAX_VOTERS = 8
 HQ_FORM_TERM_START = 0
 HQ_FORM_TERM_RING = 1
+HQ_FORM_TERM_MASK = 2
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -56,6 +57,7 @@ class CommitArgs(ctypes.Structure):
         ("ring", _vp),
         ("changed", _vp),
         ("fallback", _vp),
+        ("term_mask", _vp),
     ]
 
 
@@ -320,13 +322,13 @@ class CommitBuffers:
     committed_in: DeviceArray
     committed_out: DeviceArray
     last_index: DeviceArray
-    aux: DeviceArray            # term_start (term-start form) or term (ring form)
     ring: Optional[DeviceArray]
     n_voting: Optional[DeviceArray]
     changed: DeviceArray
     fallback: DeviceArray
     term_start: Optional[DeviceArray] = None
     term: Optional[DeviceArray] = None
+    term_mask: Optional[DeviceArray] = None
 
     def args(self) -> CommitArgs:
         a = CommitArgs()
@@ -345,33 +347,35 @@ class CommitBuffers:
         a.ring = self.ring.ptr if self.ring else None
         a.changed = self.changed.ptr
         a.fallback = self.fallback.ptr
+        a.term_mask = self.term_mask.ptr if self.term_mask else None
         return a
 
     def arrays(self):
         return [x for x in (self.match, self.committed_in, self.committed_out, self.last_index,
-                            self.term_start, self.term, self.ring, self.n_voting, self.changed,
-                            self.fallback) if x is not None]
+                            self.term_start, self.term, self.ring, self.term_mask, self.n_voting,
+                            self.changed, self.fallback) if x is not None]
 
 
 def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
                  per_group_n: bool = False, with_both_aux: bool = False) -> CommitBuffers:
-    """Allocate the SoA columns of one commit batch (match is slot-major [n_max][G])."""
+    """Allocate the SoA columns of one commit batch (match is slot-major [n_max][G]).
+    with_both_aux allocates the columns of all three term forms (to compare them)."""
     need_ts = form == HQ_FORM_TERM_START or with_both_aux
     need_ring = form == HQ_FORM_TERM_RING or with_both_aux
-    ts = ctx.empty(G, np.uint64) if need_ts else None
-    term = ctx.empty(G, np.uint64) if need_ring else None
+    need_mask = form == HQ_FORM_TERM_MASK or (with_both_aux and ring_len <= 16)
     b = CommitBuffers(
         G=G, n_max=n_max, form=form, ring_len=ring_len,
         match=ctx.empty(G * n_max, np.uint64),
         committed_in=ctx.empty(G, np.uint64),
         committed_out=ctx.empty(G, np.uint64),
         last_index=ctx.empty(G, np.uint64),
-        aux=ts if form == HQ_FORM_TERM_START else term,
         ring=ctx.empty(G * ring_len, np.uint64) if need_ring else None,
         n_voting=ctx.empty(G, np.uint8) if per_group_n else None,
         changed=ctx.empty(words64(G), np.uint64),
         fallback=ctx.empty(words64(G), np.uint64),
-        term_start=ts, term=term,
+        term_start=ctx.empty(G, np.uint64) if need_ts else None,
+        term=ctx.empty(G, np.uint64) if need_ring else None,
+        term_mask=ctx.empty(G, np.uint16) if need_mask else None,
     )
     return b
 

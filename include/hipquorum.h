@@ -59,6 +59,7 @@ extern "C" {
 /* commit term-check forms (see hq_commit_args) */
 #define HQ_FORM_TERM_START 0  /* term(q)==term  <=>  term_start <= q <= last_index */
 #define HQ_FORM_TERM_RING  1  /* term(q) gathered from a per-group ring of the last R terms */
+#define HQ_FORM_TERM_MASK  2  /* term(q)==term read from a per-group bitmask over the last R */
 
 /* vote outcomes, numerically equal to the reference State enum (internal/raft/raft.go:62-71) */
 #define HQ_OUTCOME_FOLLOWER  0u   /* rejections reached quorum: becomeFollower (raft.go:1981-1984) */
@@ -91,9 +92,13 @@ int hq_free_pinned(hq_ctx *ctx, void *p);
 int hq_memcpy_async(hq_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 int hq_memset_async(hq_ctx *ctx, void *dst, int value, size_t bytes);
 
-/* Kernel timing: when enabled, every kernel the context launches is bracketed by HIP events on
- * the context's stream. hq_timing_read() synchronises the stream and returns the summed kernel
- * time (ms) and the number of timed launches since the last reset. */
+/* Kernel timing: hq_timing_enable(ctx, 1) records a HIP event on the context's stream and opens
+ * a timed region; every kernel launched in it is counted; hq_timing_enable(ctx, 0) (or
+ * hq_timing_read) records the closing event. hq_timing_read() waits for it and returns the GPU
+ * time of all closed regions (ms) and their launch count since the last reset, so
+ * total_ms / launches is the mean launch-to-launch kernel time on the stream (back-to-back
+ * kernels: kernel duration + the dependent-launch boundary). No per-launch events are recorded:
+ * on gfx950 they add several microseconds to a ~10 us kernel. */
 int hq_timing_enable(hq_ctx *ctx, int enable);
 int hq_timing_read(hq_ctx *ctx, double *total_ms, uint64_t *launches);
 int hq_timing_reset(hq_ctx *ctx);
@@ -119,10 +124,15 @@ int hq_timing_reset(hq_ctx *ctx);
  *   HQ_FORM_TERM_RING   ring[g * ring_len + (i % ring_len)] = term(i) for i in
  *       (last_index - ring_len, last_index]. The gather happens only when q > committed; it is
  *       exact when last_index[g] - committed_in[g] <= ring_len.
+ *   HQ_FORM_TERM_MASK   bit (i % ring_len) of term_mask[g] = (term(i) == the leader's term) for
+ *       i in (last_index - ring_len, last_index]; ring_len <= 16. The same per-index equality the
+ *       ring gather tests, without the term values (no monotonicity assumption); exact when
+ *       last_index[g] - committed_in[g] <= ring_len. `term`/`ring`/`term_start` unused.
  *
  * Groups that violate the contract are NOT decided: committed_out = committed_in, changed = 0 and
  * the fallback bit is set so the caller runs the CPU path (raft.go:888) for them:
- *   n == 0 or n > n_max;  RING form only: term == 0, committed > last_index, or
+ *   n == 0 or n > n_max;  RING form: term == 0, committed > last_index, or
+ *   last_index - committed > ring_len;  MASK form: committed > last_index or
  *   last_index - committed > ring_len.
  *
  * Layout: match is slot-major, match[s * match_stride + g]; match_stride >= G.
@@ -145,6 +155,7 @@ typedef struct hq_commit_args {
     const uint64_t *ring;           /* [G][ring_len] HQ_FORM_TERM_RING */
     uint64_t *changed;              /* [ceil(G/64)] or NULL */
     uint64_t *fallback;             /* [ceil(G/64)] or NULL */
+    const uint16_t *term_mask;      /* [G] HQ_FORM_TERM_MASK */
 } hq_commit_args;
 
 int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *args);
@@ -216,7 +227,8 @@ typedef struct hq_synth_spec {
 } hq_synth_spec;
 
 /* Fills match (n_max rows at args->match_stride), n_voting (if non-NULL), committed_in,
- * last_index, term_start, term and ring (each if non-NULL) of *args; args->form is ignored. */
+ * last_index, term_start, term, ring and term_mask (each if non-NULL) of *args; args->form is
+ * ignored. term_mask needs spec->ring_len <= 16. */
 int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *spec, const hq_commit_args *args);
 /* Fills the ack / granted / rejected bitmaps and n_voting (each if non-NULL). */
 int hq_synth_bitmaps_dev(hq_ctx *ctx, const hq_synth_spec *spec, uint8_t *ack, uint8_t *granted,

@@ -57,8 +57,9 @@ int qgen_commit(const qgen_spec *s, const qref_commit_args *o) {
         if (o->last_index) ((uint64_t *)o->last_index)[j] = last;
         if (o->term_start) ((uint64_t *)o->term_start)[j] = term_start;
         if (o->term) ((uint64_t *)o->term)[j] = term;
-        if (o->ring) {
+        if (o->ring || o->term_mask) {
             uint64_t cur = term;
+            uint32_t mask = 0;
             for (uint64_t k = 0; k < R; k++) {
                 const uint64_t i = last - k;
                 uint64_t t;
@@ -70,8 +71,10 @@ int qgen_commit(const qgen_spec *s, const qref_commit_args *o) {
                     cur = cur > dec ? cur - dec : 1;
                     t = cur;
                 }
-                ((uint64_t *)o->ring)[j * R + (i & (R - 1))] = t;
+                if (o->ring) ((uint64_t *)o->ring)[j * R + (i & (R - 1))] = t;
+                mask |= (uint32_t)(t == term) << (i & (R - 1));
             }
+            if (o->term_mask) ((uint16_t *)o->term_mask)[j] = (uint16_t)mask;
         }
     }
     return 0;

@@ -217,6 +217,13 @@ static uint64_t ring_term_at(const void *ud, uint64_t i) {
     return r->ring[i & r->mask];
 }
 
+typedef struct { uint32_t mask; uint64_t rmask; } mask_ud;
+/* Form 2: bit (i mod R) says whether entry i carries the leader's term (2) or not (1). */
+static uint64_t mask_term_at(const void *ud, uint64_t i) {
+    const mask_ud *m = (const mask_ud *)ud;
+    return ((m->mask >> (i & m->rmask)) & 1) ? 2 : 1;
+}
+
 typedef struct { uint64_t term_start; } tstart_ud;
 /* The leader's log under the monotone-term invariant (entryutils.go:44-47): entries at or after
  * the leader's first current-term entry carry the current term (2 here), older ones a lower
@@ -242,7 +249,19 @@ static void commit_range(const qref_commit_args *a, uint64_t g0, uint64_t g1, in
         uint64_t term;
         ring_ud rud;
         tstart_ud tud;
-        if (a->form == 1) {
+        mask_ud mud;
+        if (a->form == 2) {
+            term = 2;
+            if (cin > last || last - cin > R) {
+                if (a->fallback) bit_set(a->fallback, g);
+                continue;
+            }
+            mud.mask = a->term_mask[g];
+            mud.rmask = R - 1;
+            log.first_minus_1 = last >= R - 1 ? last - (R - 1) : 0;
+            log.term_at = mask_term_at;
+            log.ud = &mud;
+        } else if (a->form == 1) {
             term = a->term[g];
             if (term == 0 || cin > last || last - cin > R) {
                 if (a->fallback) bit_set(a->fallback, g);
@@ -403,6 +422,9 @@ int qref_commit_batch(const qref_commit_args *a, int nthreads) {
         if (!a->term || !a->ring || a->ring_len < 1 || (a->ring_len & (a->ring_len - 1))) return -1;
     } else if (a->form == 0) {
         if (!a->term_start) return -1;
+    } else if (a->form == 2) {
+        if (!a->term_mask || a->ring_len < 1 || a->ring_len > 16 ||
+            (a->ring_len & (a->ring_len - 1))) return -1;
     } else {
         return -1;
     }

@@ -121,7 +121,7 @@ int qref_leader_has_quorum(const uint64_t *ids, int *active, int n_voting, uint6
 typedef struct qref_commit_args {
     uint64_t G;
     uint32_t n_max;
-    uint32_t form;            /* 0 = term-start, 1 = ring */
+    uint32_t form;            /* 0 = term-start, 1 = ring, 2 = current-term mask */
     uint32_t ring_len;
     uint32_t reserved;
     uint64_t match_stride;
@@ -135,6 +135,7 @@ typedef struct qref_commit_args {
     const uint64_t *ring;
     uint64_t *changed;
     uint64_t *fallback;
+    const uint16_t *term_mask;   /* form 2 */
 } qref_commit_args;
 
 /* Batched commit: every group goes through qref_try_commit over a log view. Returns QREF_OK,

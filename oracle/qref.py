@@ -30,7 +30,7 @@ class QrefCommitArgs(ctypes.Structure):
         ("ring_len", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("match_stride", _u64),
         ("match", _vp), ("n_voting", _vp), ("committed_in", _vp), ("committed_out", _vp),
         ("last_index", _vp), ("term_start", _vp), ("term", _vp), ("ring", _vp),
-        ("changed", _vp), ("fallback", _vp),
+        ("changed", _vp), ("fallback", _vp), ("term_mask", _vp),
     ]
 
 
@@ -203,8 +203,9 @@ class PyVotes:
 # ------------------------------------------------------------------------ batched forms -----
 def commit_args(G, n_max, form, ring_len, match, committed_in, committed_out, last_index,
                 term_start=None, term=None, ring=None, n_voting=None, changed=None,
-                fallback=None, match_stride=None) -> QrefCommitArgs:
+                fallback=None, match_stride=None, term_mask=None) -> QrefCommitArgs:
     a = QrefCommitArgs()
+    a.term_mask = None if term_mask is None else term_mask.ctypes.data
     a.G, a.n_max, a.form, a.ring_len = G, n_max, form, ring_len
     a.match_stride = G if match_stride is None else match_stride
     a.match = match.ctypes.data
@@ -284,8 +285,10 @@ class CommitInputs:
         self.term_start = np.zeros(G, np.uint64)
         self.term = np.zeros(G, np.uint64)
         self.ring = np.zeros(G * s.ring_len, np.uint64)
+        self.term_mask = np.zeros(G, np.uint16) if s.ring_len <= 16 else None
         a = commit_args(G, n, 0, s.ring_len, self.match, self.committed_in, self.committed_in,
-                        self.last_index, self.term_start, self.term, self.ring, self.n_voting)
+                        self.last_index, self.term_start, self.term, self.ring, self.n_voting,
+                        term_mask=self.term_mask)
         rc = lib.qgen_commit(ctypes.byref(s), ctypes.byref(a))
         assert rc == 0, rc
 
@@ -297,7 +300,8 @@ class CommitInputs:
         fb = np.zeros(words64(G), np.uint64)
         a = commit_args(G, self.n_max, form, self.R, self.match, self.committed_in, out,
                         self.last_index, self.term_start, self.term, self.ring,
-                        self.n_voting if per_group_n else None, chg, fb)
+                        self.n_voting if per_group_n else None, chg, fb,
+                        term_mask=self.term_mask)
         rc = commit_batch(a, nthreads)
         return out, chg, fb, rc
 

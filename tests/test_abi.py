@@ -45,6 +45,7 @@ int main(void) {
   F(hq_commit_args, n_voting) F(hq_commit_args, committed_in) F(hq_commit_args, committed_out)
   F(hq_commit_args, last_index) F(hq_commit_args, term_start) F(hq_commit_args, term)
   F(hq_commit_args, ring) F(hq_commit_args, changed) F(hq_commit_args, fallback)
+  F(hq_commit_args, term_mask)
   F(hq_synth_spec, seed) F(hq_synth_spec, G) F(hq_synth_spec, cid_base)
   F(hq_synth_spec, cid_stride) F(hq_synth_spec, n_max) F(hq_synth_spec, mixed_n)
   F(hq_synth_spec, ring_len) F(hq_synth_spec, parity_extras)

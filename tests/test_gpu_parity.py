@@ -46,6 +46,8 @@ def upload_commit(ctx, hq, inp, form, per_group_n, stride_pad=0, offset_elems=0)
     a.term_start = up(inp.term_start)
     a.term = up(inp.term)
     a.ring = up(inp.ring)
+    if inp.term_mask is not None:
+        a.term_mask = up(inp.term_mask)
     if per_group_n:
         a.n_voting = up(inp.n_voting)
     chg = ctx.empty(hq.words64(G), np.uint64)
@@ -109,6 +111,7 @@ def test_synth_commit_matches_cpu_generator(gpu_ctx, hq, kw):
     np.testing.assert_array_equal(gpu_ctx.download(b.term_start), host.term_start)
     np.testing.assert_array_equal(gpu_ctx.download(b.term), host.term)
     np.testing.assert_array_equal(gpu_ctx.download(b.ring), host.ring)
+    np.testing.assert_array_equal(gpu_ctx.download(b.term_mask), host.term_mask)
     hq.free_commit(gpu_ctx, b)
 
 
@@ -126,7 +129,7 @@ def test_synth_bitmaps_matches_cpu_generator(gpu_ctx, hq, kw):
 
 
 # ----------------------------------------------------------------------- commit parity -------
-@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("n_max", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_commit_uniform_n(gpu_ctx, hq, form, n_max):
     inp = qref.CommitInputs(qref.spec(SEED + 1, 65_537, n_max, parity_extras=True))
@@ -135,14 +138,14 @@ def test_commit_uniform_n(gpu_ctx, hq, form, n_max):
         assert 0 < popcount(chg) < inp.G  # both outcomes exercised
 
 
-@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("n_max", [7, 8])
 def test_commit_per_group_n(gpu_ctx, hq, form, n_max):
     inp = qref.CommitInputs(qref.spec(SEED + 4, 99_999, n_max, mixed_n=True, parity_extras=True))
     check_commit(gpu_ctx, hq, inp, form, per_group_n=True)
 
 
-@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 def test_commit_vec1_paths(gpu_ctx, hq, form):
     inp = qref.CommitInputs(qref.spec(SEED + 5, 10_001, 5, parity_extras=True))
     check_commit(gpu_ctx, hq, inp, form, per_group_n=False, stride_pad=1)     # odd stride
@@ -153,7 +156,7 @@ def test_commit_vec1_paths(gpu_ctx, hq, form):
 
 @pytest.mark.parametrize("G", [1, 2, 3, 63, 64, 65, 127, 128, 129, 130, 1000, 4097])
 def test_commit_ragged_sizes(gpu_ctx, hq, G):
-    for form in (0, 1):
+    for form in (0, 1, 2):
         inp = qref.CommitInputs(qref.spec(SEED + G, G, 3, parity_extras=True))
         check_commit(gpu_ctx, hq, inp, form, per_group_n=False)
         inp8 = qref.CommitInputs(qref.spec(SEED + G, G, 8, mixed_n=True))
@@ -174,8 +177,11 @@ def _kat_inputs(cases, R=16):
         inp.last_index[g] = c["last"]
         inp.term[g] = c["term"]
         log = {int(k): v for k, v in c["log"].items()}
+        mask = 0
         for i in range(max(0, c["last"] - R + 1), c["last"] + 1):
             inp.ring[g * R + (i % R)] = log.get(i, 0)
+            mask |= int(log.get(i, 0) == c["term"]) << (i % R)
+        inp.term_mask[g] = mask
         # term-start form: first index carrying the current term (entryutils.go:44-47)
         cur = [i for i, t in log.items() if t == c["term"]]
         inp.term_start[g] = min(cur) if cur else c["last"] + 1
@@ -201,9 +207,10 @@ def test_commit_reference_kats_on_gpu(gpu_ctx, hq):
         cases += KATS[table]
     inp = _kat_inputs(cases)
     want = np.array([c["want_committed"] for c in cases], np.uint64)
-    out, chg, fb = run_commit(gpu_ctx, hq, inp, 1, per_group_n=True)
-    assert popcount(fb) == 0
-    np.testing.assert_array_equal(out, want)
+    for form in (1, 2):   # ring gather and current-term mask: every case representable
+        out, chg, fb = run_commit(gpu_ctx, hq, inp, form, per_group_n=True)
+        assert popcount(fb) == 0
+        np.testing.assert_array_equal(out, want)
     ok = np.array([_term_start_representable(c) for c in cases])
     assert ok.sum() >= len(cases) - 3
     out, chg, fb = run_commit(gpu_ctx, hq, inp, 0, per_group_n=True)
@@ -227,6 +234,7 @@ def test_commit_contract_fallbacks(gpu_ctx, hq):
     inp.n_voting[4] = 0                    # no voting member
     inp.n_voting[5] = 9                    # more than n_max
     inp.committed_in[6] = last - R         # exactly R behind: still exact
+    inp.term_mask[:] = 0xFFFF
     out, chg, fb = run_commit(gpu_ctx, hq, inp, 1, per_group_n=True)
     assert int(fb[0]) == 0b111110
     assert int(chg[0]) == 0b11000001
@@ -234,11 +242,19 @@ def test_commit_contract_fallbacks(gpu_ctx, hq):
     want_out, want_chg, want_fb, rc = inp.run(1, True)
     np.testing.assert_array_equal(out, want_out)
     np.testing.assert_array_equal(fb, want_fb)
+    # mask form: no term column, so group 1 (term 0) is decided normally
+    out, chg, fb = run_commit(gpu_ctx, hq, inp, 2, per_group_n=True)
+    assert int(fb[0]) == 0b111100
+    assert int(chg[0]) == 0b11000011
+    want_out, want_chg, want_fb, rc = inp.run(2, True)
+    np.testing.assert_array_equal(out, want_out)
+    np.testing.assert_array_equal(chg, want_chg)
+    np.testing.assert_array_equal(fb, want_fb)
 
 
 def test_commit_host_entry_point(gpu_ctx, hq):
     inp = qref.CommitInputs(qref.spec(SEED + 9, 30_001, 5, parity_extras=True))
-    for form in (0, 1):
+    for form in (0, 1, 2):
         out = np.zeros(inp.G, np.uint64)
         chg = np.zeros(hq.words64(inp.G), np.uint64)
         fb = np.zeros(hq.words64(inp.G), np.uint64)
@@ -248,6 +264,7 @@ def test_commit_host_entry_point(gpu_ctx, hq):
                                                     inp.committed_in.ctypes.data, out.ctypes.data)
         a.last_index, a.term_start = inp.last_index.ctypes.data, inp.term_start.ctypes.data
         a.term, a.ring = inp.term.ctypes.data, inp.ring.ctypes.data
+        a.term_mask = inp.term_mask.ctypes.data
         a.changed, a.fallback = chg.ctypes.data, fb.ctypes.data
         gpu_ctx.commit_host(a)
         want_out, want_chg, want_fb, _ = inp.run(form, False)
@@ -272,27 +289,31 @@ def test_commit_inplace_idempotent(gpu_ctx, hq):
     hq.free_commit(gpu_ctx, b)
 
 
-@pytest.mark.parametrize("n_max,form", [(3, 0), (5, 1)])
+@pytest.mark.parametrize("n_max,form", [(3, 0), (5, 1), (5, 2)])
 def test_commit_full_size_configs(gpu_ctx, hq, n_max, form):
     """BASELINE configs 2 and 3 at full size (1M groups): device-generated inputs, oracle on the
-    CPU generator's copy; also the two term forms agree on the same data."""
+    CPU generator's copy; the three term forms agree on the same data."""
     G = 1 << 20
     b = hq.alloc_commit(gpu_ctx, G, n_max, form, 16, with_both_aux=True)
     gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + n_max, G, n_max), b.args())
     gpu_ctx.commit_dev(b.args())
     gpu_ctx.sync()
     out, chg = gpu_ctx.download(b.committed_out), gpu_ctx.download(b.changed)
-    other = b.args()
-    other.form = 1 - form
-    other.committed_out = gpu_ctx.empty(G, np.uint64).ptr
     inp = qref.CommitInputs(qref.spec(SEED + n_max, G, n_max))
     want_out, want_chg, want_fb, rc = inp.run(form, False, nthreads=16)
     np.testing.assert_array_equal(out, want_out)
     np.testing.assert_array_equal(chg, want_chg)
     assert popcount(gpu_ctx.download(b.fallback)) == 0
-    gpu_ctx.commit_dev(other)
-    gpu_ctx.sync()
-    np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+    extra_out = gpu_ctx.empty(G, np.uint64)
+    for other_form in {0, 1, 2} - {form}:
+        other = b.args()
+        other.form = other_form
+        other.committed_out = extra_out.ptr
+        gpu_ctx.commit_dev(other)
+        gpu_ctx.sync()
+        np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+        np.testing.assert_array_equal(gpu_ctx.download(extra_out), want_out)
+    gpu_ctx.free(extra_out)
     hq.free_commit(gpu_ctx, b)
 
 
