@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Condense the rocprofv3 outputs of tools/profile_bench.sh into profiles/<round>/ and update
+profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of
+MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half of a wide (16 B/lane) coalesced streaming read;
+WRITE_SIZE is exact for 16 B/lane stores. Both counters are per-dispatch kilobytes.
+
+usage: python tools/summarize_profiles.py r01 c2 c3m ...
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = {"c2": "k_commit<3, 0, 2, false>", "c3": "k_commit<5, 1, 2, false>",
+          "c3m": "k_commit<5, 2, 2, false>", "c4": "k_bits<3, false>"}
+
+
+def counter(path, kernel):
+    rows = list(csv.DictReader(open(path)))
+    vals = [float(r["Counter_Value"]) for r in rows if kernel in r["Kernel_Name"]]
+    return statistics.median(vals), len(vals)
+
+
+def main():
+    rnd, workloads = sys.argv[1], sys.argv[2:]
+    dst = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    tj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    traffic = json.load(open(tj)) if os.path.exists(tj) else {}
+    for w in workloads:
+        src = os.path.join(ROOT, "gpurun_out", f"prof_{w}")
+        k = KERNEL[w]
+        shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                    os.path.join(dst, f"{w}_kernel_stats.csv"))
+        stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, f"{w}_kernel_stats.csv")))}
+        row = next(v for n, v in stats.items() if k in n)
+        fetch, nf = counter(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"), k)
+        write, nw = counter(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), k)
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            shutil.copy(os.path.join(src, f"pmc_{c}", "run_counter_collection.csv"),
+                        os.path.join(dst, f"{w}_pmc_{c}.csv"))
+        hbm = (2 * fetch + write) * 1024
+        traffic[w] = {
+            "kernel": k,
+            "rocprof_avg_ns": float(row["AverageNs"]),
+            "rocprof_calls": int(row["Calls"]),
+            "fetch_size_kb_median": fetch,
+            "write_size_kb_median": write,
+            "dispatches": min(nf, nw),
+            "hbm_bytes_per_launch": hbm,
+            "correction": "(2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE halves 16B/lane streams)",
+            "round": rnd,
+        }
+        print(w, json.dumps(traffic[w]))
+    json.dump(traffic, open(tj, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
