@@ -43,6 +43,12 @@ WORKLOADS = {
                      "mask (exact replacement of the ring gather)"),
     "c4": dict(cfg=3, kind="bits", G=16 << 20, n=7,
                desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
+    "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
+               desc="64M groups mixed 3/5/7 voters (n = {3,5,7}[clusterID % 3]) sharded "
+                    "clusterID % 8: 8M groups per GPU, one launch per voter-count bucket, "
+                    "current-term mask"),
+    "c5r": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=1, mixed=True,
+                desc="as c5 with the u64 term-ring gather (R = 16)"),
 }
 
 
@@ -115,21 +121,28 @@ class Dist:
 
 # ----------------------------------------------------------------------------- GPU legs -------
 def build_sets(ctx, hq, shard, w, d: "Dist"):
-    """Device-generated input batches for this rank, enough to rotate over ROTATE_BYTES."""
+    """Device-generated input batches for this rank, enough to rotate over ROTATE_BYTES.
+    Commit workloads: each set is a list of CommitBuffers launched back to back in one step
+    (one per voter-count bucket for the mixed-membership workload)."""
     G = w["G"]
-    per_set = algo_bytes_per_group(w) * G
+    per_set = algo_bytes_per_step(w)
     nsets = max(4, int(np.ceil(ROTATE_BYTES / per_set)))
-    rng = shard.rank_shard(d.rank, d.world, G)
     seed = SEED_BASE + w["cfg"]
     sets = []
     for s in range(nsets):
-        spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
-                             cid_stride=rng.cid_stride)
         if w["kind"] == "commit":
-            b = hq.alloc_commit(ctx, G, w["n"], w["form"], 16)
-            ctx.synth_commit_dev(spec, b.args())
-            sets.append(b)
+            buckets = []
+            for n, rng in commit_buckets(shard, w, d):
+                spec = hq.synth_spec(seed + (s << 40), rng.count, n, cid_base=rng.cid_base,
+                                     cid_stride=rng.cid_stride)
+                b = hq.alloc_commit(ctx, rng.count, n, w["form"], 16)
+                ctx.synth_commit_dev(spec, b.args())
+                buckets.append(b)
+            sets.append(buckets)
         else:
+            rng = shard.rank_shard(d.rank, d.world, G)
+            spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
+                                 cid_stride=rng.cid_stride)
             arrs = [ctx.empty(G, np.uint8) for _ in range(4)]
             ctx.synth_bitmaps_dev(spec, *arrs)
             conf = ctx.empty(hq.words64(G), np.uint64)
@@ -137,6 +150,25 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             sets.append((arrs, conf, outc))
     ctx.sync()
     return sets, per_set
+
+
+def commit_buckets(shard, w, d):
+    """(voters, clusterID progression) per launch of one step on this rank."""
+    if not w["mixed"]:
+        return [(w["n"], shard.rank_shard(d.rank, d.world, w["G"]))]
+    per = w["G"] // 3
+    return [(shard.MIXED_VOTERS[b], shard.rank_bucket(d.rank, d.world, b, per)) for b in range(3)]
+
+
+def algo_bytes_per_step(w):
+    if w["kind"] == "commit" and w["mixed"]:
+        per = w["G"] // 3
+        return sum(per * algo_bytes_per_group(dict(w, n=n, mixed=False)) for n in (3, 5, 7))
+    return algo_bytes_per_group(w) * w["G"]
+
+
+def groups_per_step(w):
+    return (w["G"] // 3) * 3 if w["kind"] == "commit" and w["mixed"] else w["G"]
 
 
 def run_gpu(w, steps, warmup, d: Dist):
@@ -147,8 +179,9 @@ def run_gpu(w, steps, warmup, d: Dist):
     sets, per_set = build_sets(ctx, hq, shard, w, d)
     G = w["G"]
     if w["kind"] == "commit":
-        seq = hq.commit_batch_array([sets[i % len(sets)].args() for i in range(steps)])
-        wseq = hq.commit_batch_array([sets[i % len(sets)].args() for i in range(max(1, warmup))])
+        def flat(k):
+            return hq.commit_batch_array([b.args() for i in range(k) for b in sets[i % len(sets)]])
+        seq, wseq = flat(steps), flat(max(1, warmup))
 
         def run(batch):
             ctx.commit_many_dev(batch)
@@ -177,11 +210,12 @@ def run_gpu(w, steps, warmup, d: Dist):
     kernel_ms, launches = ctx.timing_read()
     elapsed = d.max(t1 - t0)
     avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
-    total_groups = d.sum(float(G * steps))
+    total_groups = d.sum(float(groups_per_step(w) * steps))
     res = dict(
         elapsed=elapsed, launches=launches, avg_kernel_s=avg_kernel_s,
         decisions=total_groups * decisions_per_group(w), nsets=len(sets),
-        bytes_per_launch=per_set,
+        bytes_per_launch=per_set * steps / max(1, launches), steps=steps,
+        achieved_gbs=per_set * steps / (kernel_ms / 1e3) / 1e9,
     )
     ctx.close()
     return res
@@ -242,7 +276,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c3,c3m,c4",
+    ap.add_argument("--extra", default="c3,c3m,c4,c5,c5r",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -262,7 +296,7 @@ def main():
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(w)
     if d.rank == 0:
-        achieved = r["bytes_per_launch"] / r["avg_kernel_s"] / 1e9
+        achieved = r["achieved_gbs"]
         line = {
             "metric": "quorum-commit decisions/sec (whole node) + % HBM roofline at 1/2/4/8 GPUs",
             "value": r["decisions"] / r["elapsed"],
@@ -300,9 +334,9 @@ def main():
                     "workload": f"{n}: {we['desc']}",
                     "value": re_["decisions"] / re_["elapsed"], "unit": "decisions/s",
                     "kernel_avg_us": re_["avg_kernel_s"] * 1e6,
-                    "roofline_achieved_gbs": re_["bytes_per_launch"] / re_["avg_kernel_s"] / 1e9,
-                    "roofline_frac": re_["bytes_per_launch"] / re_["avg_kernel_s"] / 1e9
-                    / HBM_PEAK_GBS,
+                    "launches_per_step": re_["launches"] / max(1, re_["steps"]),
+                    "roofline_achieved_gbs": re_["achieved_gbs"],
+                    "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
             ],

@@ -264,13 +264,47 @@ __device__ __forceinline__ V16 load16(const uint8_t *p, uint64_t g, uint64_t G) 
     return r;
 }
 
+// ---- SWAR helpers: four groups per 32-bit word, one byte each -------------------------------
+constexpr uint32_t kB80 = 0x80808080u, kB01 = 0x01010101u;
+
+// per-byte popcount (each result byte 0..8)
+__device__ __forceinline__ uint32_t popc_bytes(uint32_t x) {
+    x = x - ((x >> 1) & 0x55555555u);
+    x = (x & 0x33333333u) + ((x >> 2) & 0x33333333u);
+    return (x + (x >> 4)) & 0x0F0F0F0Fu;
+}
+// bit 7 of each byte: a_byte >= b_byte, for bytes a, b < 128
+__device__ __forceinline__ uint32_t ge_bytes(uint32_t a, uint32_t b) {
+    return ((a | kB80) - b) & kB80;
+}
+// 4 flag bytes (0x80 / 0x00) -> 4 consecutive bits (group k -> bit k)
+__device__ __forceinline__ uint32_t pack4(uint32_t f) {
+    return (((f >> 7) & kB01) * 0x01020408u) >> 24;   // byte k's bit -> bit 24 + k
+}
+// 4 flag bytes -> bits 0, 2, 4, 6 (the low bit of 2-bit fields)
+__device__ __forceinline__ uint32_t pack4x2(uint32_t f) {
+    return (((f >> 7) & kB01) * 0x01041040u) >> 24;   // byte k's bit -> bit 24 + 2k
+}
+// per-byte valid n in [1, 8] -> 0x80
+__device__ __forceinline__ uint32_t valid_n(uint32_t n) {
+    const uint32_t lo = n & 0x0F0F0F0Fu, hi = (n >> 4) & 0x0F0F0F0Fu;
+    return (lo + 0x7F7F7F7Fu) & ~(lo + 0x77777777u) & ~(hi + 0x7F7F7F7Fu) & kB80;
+}
+// per-byte (1 << n) - 1 for n in [0, 8] with v_perm_b32 as a byte lookup table: selectors 0..7
+// pick masks 0x00..0x7F from {0x7F3F1F0F, 0x07030100}; selector 13 (n = 8) yields 0xFF
+__device__ __forceinline__ uint32_t mask_n(uint32_t n) {
+    const uint32_t sel = n | (((n >> 3) & kB01) * 0x0Du);
+    return __builtin_amdgcn_perm(0x7F3F1F0Fu, 0x07030100u, sel);
+}
+
 template <int MODE, bool PERN>
 __global__ __launch_bounds__(kBlock) void k_bits(const BitsK a) {
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * 16;
+    const uint32_t nu = a.n_uniform * kB01;  // n_uniform <= 8: no byte overflow
     for (uint64_t g = tid * 16; g < a.n16o * 16 || g < a.n16 * 16; g += step) {
         const uint64_t slot = g >> 4;
-        V16 nv, ack, gr, rj, ac;
+        V16 nv = {}, ack = {}, gr = {}, rj = {}, ac = {};
         if (g < a.G) {
             if constexpr (PERN) nv = load16(a.nv, g, a.G);
             if constexpr (MODE & kRI) ack = load16(a.ack, g, a.G);
@@ -281,37 +315,44 @@ __global__ __launch_bounds__(kBlock) void k_bits(const BitsK a) {
             if constexpr (MODE & kCHECKQ) ac = load16(a.active, g, a.G);
         }
         uint32_t conf = 0, outc = 0, hq = 0, fb = 0;
+        V16 keep;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (g + k >= a.G) continue;
-            const uint32_t n = PERN ? nv.b[k] : a.n_uniform;
-            const bool bad = (n < 1) | (n > 8);
-            const uint32_t mask = bad ? 0u : ((1u << n) - 1u);
-            const uint32_t quorum = n / 2 + 1;
-            fb |= (uint32_t)bad << k;
+        for (int w = 0; w < 4; ++w) {
+            // bytes of groups >= G are excluded (their output bits stay 0)
+            const uint64_t left = g < a.G ? a.G - g : 0;
+            const uint32_t inr = left >= (uint64_t)(4 * w + 4) ? kB80
+                                 : left <= (uint64_t)(4 * w) ? 0u
+                                 : (kB80 >> (8 * (4 - (uint32_t)(left - 4 * w))));
+            const uint32_t n = PERN ? nv.w[w] : nu;
+            const uint32_t ok = valid_n(n) & inr;
+            const uint32_t mask = mask_n(n);
+            const uint32_t quorum = ((n >> 1) & 0x7F7F7F7Fu) + kB01;  // n/2 + 1 (valid bytes)
+            uint32_t bad = ~ok & inr;
             if constexpr (MODE & kRI) {
-                // readindex.go:84: len(confirmed) + 1 >= quorum
-                const uint32_t c = __popc(ack.b[k] & mask) + 1;
-                conf |= (uint32_t)(!bad && c >= quorum) << k;
+                // readindex.go:84: len(confirmed) + 1 >= quorum  <=>  acks >= quorum - 1
+                const uint32_t c = popc_bytes(ack.w[w] & mask);
+                conf |= pack4(ge_bytes(c, quorum - kB01) & ok) << (4 * w);
             }
             if constexpr (MODE & kVOTE) {
-                const uint32_t gm = gr.b[k] & mask;
-                const uint32_t rm = rj.b[k] & mask & ~gm;  // first response wins
-                uint32_t o = HQ_OUTCOME_CANDIDATE;
-                if (!bad) {
-                    if ((uint32_t)__popc(gm) >= quorum)
-                        o = HQ_OUTCOME_LEADER;
-                    else if ((uint32_t)__popc(rm) >= quorum)
-                        o = HQ_OUTCOME_FOLLOWER;
-                }
-                outc |= o << (2 * k);
+                const uint32_t gm = gr.w[w] & mask;
+                const uint32_t rm = rj.w[w] & mask & ~gm;  // first response wins
+                const uint32_t lead = ge_bytes(popc_bytes(gm), quorum) & ok;
+                const uint32_t foll = ge_bytes(popc_bytes(rm), quorum) & ok & ~lead;
+                const uint32_t cand = inr & ~lead & ~foll;
+                // 2-bit codes: leader 2 (bit 1), candidate 1 (bit 0), follower 0
+                outc |= (pack4x2(cand) | (pack4x2(lead) << 1)) << (8 * w);
             }
             if constexpr (MODE & kCHECKQ) {
-                const bool selfok = !bad && a.self_slot < n;
-                fb |= (uint32_t)(!selfok) << k;
-                const uint32_t c = __popc((ac.b[k] | (1u << a.self_slot)) & mask);
-                hq |= (uint32_t)(selfok && c >= quorum) << k;
+                const uint32_t self = kB01 << a.self_slot;
+                const uint32_t selfok = ge_bytes(n, (a.self_slot + 1) * kB01) & ok;
+                bad = ~selfok & inr;
+                const uint32_t c = popc_bytes((ac.w[w] | self) & mask);
+                hq |= pack4(ge_bytes(c, quorum) & selfok) << (4 * w);
+                // setNotActive for every voting member (raft.go:385, remote.go:196-198);
+                // groups left to the CPU path keep their flags
+                keep.w[w] = ac.w[w] & ((bad >> 7) * 0xFFu);
             }
+            fb |= pack4(bad) << (4 * w);
         }
         // 64-group bitmap words viewed as 16-bit slots, 32-group outcome words as 32-bit slots
         if (slot < a.n16) {
@@ -324,11 +365,6 @@ __global__ __launch_bounds__(kBlock) void k_bits(const BitsK a) {
             if (slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
         }
         if constexpr (MODE & kCHECKQ) {
-            // setNotActive for every voting member (raft.go:385, remote.go:196-198); groups left
-            // to the CPU path (fallback) keep their flags
-            V16 keep;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) keep.b[k] = ((fb >> k) & 1) ? ac.b[k] : 0;
             if (g + 16 <= a.G) {
                 *reinterpret_cast<uint4 *>(a.active + g) = keep.v;
             } else {
