@@ -77,15 +77,22 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.torch = None
+        self.device = self.local_rank
+        self.backend = None
         if self.world > 1:
             import torch
             import torch.distributed as dist
 
             self.torch, self.dist = torch, dist
-            if torch.cuda.is_available():
-                torch.cuda.set_device(self.local_rank)
-                backend = "nccl"   # RCCL on ROCm
+            ngpu = torch.cuda.device_count() if torch.cuda.is_available() else 0
+            if ngpu >= self.world:
+                self.device = self.local_rank
+                torch.cuda.set_device(self.device)
+                backend = "nccl"   # RCCL on ROCm: barrier + MAX/SUM all-reduce only
             else:
+                # more ranks than GPUs (rehearsal on a small box): ranks share GPUs and the
+                # timing collectives run on the host
+                self.device = self.local_rank % max(1, ngpu)
                 backend = "gloo"
             dist.init_process_group(backend=backend)
             self.backend = backend
@@ -175,7 +182,7 @@ def run_gpu(w, steps, warmup, d: Dist):
     from dragonboat_amd import hipquorum as hq
     from dragonboat_amd import shard
 
-    ctx = hq.Context(d.local_rank)
+    ctx = hq.Context(d.device)
     sets, per_set = build_sets(ctx, hq, shard, w, d)
     G = w["G"]
     if w["kind"] == "commit":
@@ -219,6 +226,71 @@ def run_gpu(w, steps, warmup, d: Dist):
     )
     ctx.close()
     return res
+
+
+def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
+    """Host-fed end to end, PCIe included — never the headline `value`.
+    Per step: pinned H2D of G/4 leader appends + G follower match deltas (16 B each), append +
+    ingest kernels into the device-resident table, commit in place (term-mask form), D2H of the
+    changed bitmap and the committed column."""
+    from dragonboat_amd import hipquorum as hq
+    from dragonboat_amd import shard
+
+    ctx = hq.Context(d.device)
+    rng = shard.rank_shard(d.rank, d.world, G)
+    b = hq.alloc_commit(ctx, G, n, hq.HQ_FORM_TERM_MASK, 16)
+    ctx.synth_commit_dev(hq.synth_spec(SEED_BASE + 9, G, n, cid_base=rng.cid_base,
+                                       cid_stride=rng.cid_stride), b.args())
+    a = b.args()
+    a.committed_out = a.committed_in
+    last = ctx.download(b.last_index)
+    r = np.random.default_rng(d.rank)
+    nb = 4   # distinct host batches cycled through
+    apps, upds = [], []
+    for k in range(nb):
+        g = r.choice(G, G // 4, replace=False).astype(np.uint64)
+        app = ctx.pinned(2 * len(g), np.uint64)
+        app[0::2], app[1::2] = g, last[g] + np.uint64(k + 1)
+        apps.append(app)
+        gu = r.integers(0, G, G, dtype=np.uint64)
+        upd = ctx.pinned(2 * G, np.uint64)
+        upd[0::2] = (gu << np.uint64(8)) | r.integers(1, n, G, dtype=np.uint64)
+        upd[1::2] = last[gu] + np.uint64(k)
+        upds.append(upd)
+    dapp = ctx.empty(2 * (G // 4), np.uint64)
+    dupd = ctx.empty(2 * G, np.uint64)
+    out_chg = ctx.pinned(hq.words64(G), np.uint64)
+    out_com = ctx.pinned(G, np.uint64)
+
+    def step(i):
+        ctx.h2d_async(dapp, apps[i % nb])
+        ctx.h2d_async(dupd, upds[i % nb])
+        ctx.append_dev(dapp, G // 4, b.last_index, b.match, b.term_mask, 16, G)
+        ctx.ingest_match_dev(dupd, G, b.match, G, G, n)
+        ctx.commit_dev(a)
+        ctx.d2h_async(out_chg, b.changed)
+        ctx.d2h_async(out_com, b.committed_in)
+
+    for i in range(warmup):
+        step(i)
+    ctx.sync()
+    d.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    ctx.sync()
+    d.barrier()
+    elapsed = d.max(time.perf_counter() - t0)
+    pcie = (G // 4) * 16 + G * 16 + hq.words64(G) * 8 + G * 8
+    ctx.close()
+    return {
+        "workload": f"e2e: host-fed {G} groups x {n} voters per GPU per step: pinned H2D of "
+                    f"{G // 4} appends + {G} match deltas, ingest + commit kernels, D2H results",
+        "value": d.sum(float(G * steps)) / elapsed, "unit": "decisions/s",
+        "ms_per_step": elapsed / steps * 1e3,
+        "pcie_bytes_per_step": pcie,
+        "pcie_gbs": pcie * steps / elapsed / 1e9,
+    }
 
 
 # ----------------------------------------------------------------------------- CPU leg --------
@@ -276,7 +348,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c3,c3m,c4,c5,c5r",
+    ap.add_argument("--extra", default="c3,c3m,c4,c5,c5r,e2e",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -288,7 +360,11 @@ def main():
     w = WORKLOADS[args.workload]
     r = run_gpu(w, args.steps, args.warmup, d)
     extras = []
+    e2e = None
     for name in [x for x in args.extra.split(",") if x and x != args.workload]:
+        if name == "e2e":
+            e2e = run_e2e(max(20, args.steps // 20), 3, d)
+            continue
         we = WORKLOADS[name]
         re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
         extras.append((name, we, re_))
@@ -339,7 +415,7 @@ def main():
                     "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
-            ],
+            ] + ([e2e] if e2e else []),
         }
         print(json.dumps(line), flush=True)
     d.close()

@@ -729,3 +729,139 @@ extern "C" int hq_synth_bitmaps_dev(hq_ctx *ctx, const hq_synth_spec *s, uint8_t
                        granted, rejected, n_voting);
     return hq::post_launch(ctx, "k_synth_bits");
 }
+
+// ---- device-resident progress table: delta ingest ------------------------
+namespace {
+
+__device__ __forceinline__ void count_skip(uint64_t *n_skipped, bool skip) {
+    // one atomic per wave: the ballot's popcount of skipped lanes
+    const uint64_t m = __ballot(skip);
+    if (n_skipped && m && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)m) - 1))
+        atomicAdd(reinterpret_cast<unsigned long long *>(n_skipped),
+                  (unsigned long long)__popcll(m));
+}
+
+__global__ __launch_bounds__(kBlock) void k_ingest_match(const hq_match_update *u, uint64_t count,
+                                                         uint64_t *match, uint64_t stride,
+                                                         uint64_t G, uint32_t n_max,
+                                                         uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kBlock) {
+        bool skip = false;
+        if (i < count) {
+            const hq_match_update x = u[i];
+            const uint64_t g = x.group_slot >> 8;
+            const uint32_t s = (uint32_t)(x.group_slot & 0xFF);
+            skip = g >= G || s >= n_max;
+            // remote.tryUpdate (remote.go:127-131): match only rises
+            if (!skip)
+                atomicMax(reinterpret_cast<unsigned long long *>(match + s * stride + g),
+                          (unsigned long long)x.index);
+        }
+        count_skip(n_skipped, skip);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ingest_ack(const uint64_t *gs, uint64_t count,
+                                                       uint8_t *ack, uint64_t G, uint32_t n_max,
+                                                       uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kBlock) {
+        bool skip = false;
+        if (i < count) {
+            const uint64_t x = gs[i];
+            const uint64_t g = x >> 8;
+            const uint32_t s = (uint32_t)(x & 0xFF);
+            skip = g >= G || s >= n_max || s >= 8;
+            // readIndex.confirm: p.confirmed[from] = struct{}{} (readindex.go:83)
+            if (!skip)
+                atomicOr(reinterpret_cast<unsigned int *>(ack + (g & ~3ull)),
+                         1u << (s + 8 * (uint32_t)(g & 3)));
+        }
+        count_skip(n_skipped, skip);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_append(const hq_append_update *u, uint64_t count,
+                                                   uint64_t *last, uint64_t *match0,
+                                                   uint16_t *mask, uint32_t R, uint64_t G,
+                                                   uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kBlock) {
+        bool skip = false;
+        if (i < count) {
+            const hq_append_update x = u[i];
+            skip = x.group >= G;
+            if (!skip) {
+                const uint64_t g = x.group;
+                const uint64_t prev = atomicMax(reinterpret_cast<unsigned long long *>(last + g),
+                                                (unsigned long long)x.new_last);
+                if (x.new_last > prev) {
+                    // the leader's own remote follows its log (raft.go:918)
+                    atomicMax(reinterpret_cast<unsigned long long *>(match0 + g),
+                              (unsigned long long)x.new_last);
+                    if (mask) {
+                        // entries (prev, new_last] carry the leader's term (raft.go:913-916)
+                        const uint64_t n = x.new_last - prev;
+                        uint32_t bits = 0;
+                        if (n >= R) {
+                            bits = R >= 32 ? 0xFFFFFFFFu : ((1u << R) - 1u);
+                        } else {
+                            for (uint64_t k = 1; k <= n; ++k) bits |= 1u << ((prev + k) & (R - 1));
+                        }
+                        atomicOr(reinterpret_cast<unsigned int *>(mask + (g & ~1ull)),
+                                 (bits & 0xFFFFu) << (16 * (uint32_t)(g & 1)));
+                    }
+                }
+            }
+        }
+        count_skip(n_skipped, skip);
+    }
+}
+
+}  // namespace
+
+extern "C" int hq_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
+                                   uint64_t *match, uint64_t match_stride, uint64_t G,
+                                   uint32_t n_max, uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    if (!updates || !match || match_stride < G || n_max < 1 || n_max > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_ingest_match_dev: bad arguments");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_ingest_match, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
+                       updates, count, match, match_stride, G, n_max, n_skipped);
+    return hq::post_launch(ctx, "k_ingest_match");
+}
+
+extern "C" int hq_ingest_ack_dev(hq_ctx *ctx, const uint64_t *group_slot, uint64_t count,
+                                 uint8_t *ack, uint64_t G, uint32_t n_max, uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    if (!group_slot || !ack || (reinterpret_cast<uintptr_t>(ack) & 3) || n_max < 1 ||
+        n_max > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_ingest_ack_dev: bad arguments (ack must be 4-byte aligned)");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_ingest_ack, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
+                       group_slot, count, ack, G, n_max, n_skipped);
+    return hq::post_launch(ctx, "k_ingest_ack");
+}
+
+extern "C" int hq_append_dev(hq_ctx *ctx, const hq_append_update *updates, uint64_t count,
+                             uint64_t *last_index, uint64_t *match_slot0, uint16_t *term_mask,
+                             uint32_t ring_len, uint64_t G, uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    if (!updates || !last_index || !match_slot0 ||
+        (term_mask && ((reinterpret_cast<uintptr_t>(term_mask) & 3) || ring_len < 1 ||
+                       ring_len > 16 || (ring_len & (ring_len - 1)))))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_append_dev: bad arguments");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_append, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream, updates,
+                       count, last_index, match_slot0, term_mask, ring_len ? ring_len : 16u, G,
+                       n_skipped);
+    return hq::post_launch(ctx, "k_append");
+}

@@ -108,6 +108,12 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp],
     ),
+    "hq_ingest_match_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                           ctypes.c_uint64, ctypes.c_uint32, _vp]),
+    "hq_ingest_ack_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                         ctypes.c_uint32, _vp]),
+    "hq_append_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32,
+                                     ctypes.c_uint64, _vp]),
     "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
     "hq_synth_bitmaps_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), _vp, _vp, _vp, _vp]),
 }
@@ -167,13 +173,18 @@ class Context:
         self.h = h
         self.device = device
         self._allocs: dict[int, DeviceArray] = {}
+        self._pinned: list[int] = []
 
     # -- lifetime ---------------------------------------------------------------------------
     def close(self) -> None:
         if self.h:
+            lib.hq_sync(self.h)
             for a in list(self._allocs.values()):
                 lib.hq_free_dev(self.h, _vp(a.ptr))
             self._allocs.clear()
+            for p in self._pinned:
+                lib.hq_free_pinned(self.h, _vp(p))
+            self._pinned.clear()
             lib.hq_close(self.h)
             self.h = None
 
@@ -214,6 +225,21 @@ class Context:
         self._check(lib.hq_memcpy_async(self.h, out.ctypes.data_as(_vp), _vp(a.ptr), out.nbytes, 1))
         self.sync()
         return out
+
+    def pinned(self, count: int, dtype) -> np.ndarray:
+        """A numpy view of pinned host memory (hq_alloc_pinned), freed with the context."""
+        dtype = np.dtype(dtype)
+        p = _vp()
+        self._check(lib.hq_alloc_pinned(self.h, max(1, count * dtype.itemsize), ctypes.byref(p)))
+        self._pinned.append(p.value)
+        buf = (ctypes.c_char * (count * dtype.itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=dtype, count=count)
+
+    def h2d_async(self, dst: DeviceArray, src: np.ndarray) -> None:
+        self._check(lib.hq_memcpy_async(self.h, _vp(dst.ptr), src.ctypes.data_as(_vp), src.nbytes, 0))
+
+    def d2h_async(self, dst: np.ndarray, src: DeviceArray) -> None:
+        self._check(lib.hq_memcpy_async(self.h, dst.ctypes.data_as(_vp), _vp(src.ptr), dst.nbytes, 1))
 
     def memset(self, a: DeviceArray, value: int = 0) -> None:
         self._check(lib.hq_memset_async(self.h, _vp(a.ptr), value, a.nbytes))
@@ -271,6 +297,22 @@ class Context:
     def vote_host(self, G, granted, rejected, n_voting, n_uniform, outcome, fallback=None) -> None:
         self._check(lib.hq_vote(self.h, G, _p(granted), _p(rejected), _p(n_voting), n_uniform,
                                 _p(outcome), _p(fallback)))
+
+    def ingest_match_dev(self, updates, count, match, match_stride, G, n_max, n_skipped=None):
+        """updates: device array of hq_match_update (uint64 pairs: group << 8 | slot, index)."""
+        self._check(lib.hq_ingest_match_dev(self.h, _p(updates), count, _p(match), match_stride,
+                                            G, n_max, _p(n_skipped)))
+
+    def ingest_ack_dev(self, group_slot, count, ack, G, n_max, n_skipped=None):
+        self._check(lib.hq_ingest_ack_dev(self.h, _p(group_slot), count, _p(ack), G, n_max,
+                                          _p(n_skipped)))
+
+    def append_dev(self, updates, count, last_index, match_slot0, term_mask, ring_len, G,
+                   n_skipped=None):
+        """updates: device array of hq_append_update (uint64 pairs: group, new_last)."""
+        self._check(lib.hq_append_dev(self.h, _p(updates), count, _p(last_index),
+                                      _p(match_slot0), _p(term_mask), ring_len, G,
+                                      _p(n_skipped)))
 
     def synth_commit_dev(self, spec: SynthSpec, args: CommitArgs) -> None:
         self._check(lib.hq_synth_commit_dev(self.h, ctypes.byref(spec), ctypes.byref(args)))

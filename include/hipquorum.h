@@ -207,6 +207,44 @@ int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active, const uint8_t 
                         uint32_t n_uniform, uint32_t self_slot, uint64_t *has_quorum,
                         uint64_t *fallback);
 
+/* ---------------------------------------------------------------- device-resident state ----- */
+/*
+ * Delta ingest into a device-resident progress table: the host ships only what
+ * changed since the last step instead of re-packing whole batches over PCIe.
+ *
+ * hq_ingest_match_dev: for each update u, match[slot * match_stride + group] =
+ *   max(match[...], u.index) — remote.tryUpdate (remote.go:123-133) raises match only, so any
+ *   order of the batch (and duplicates) gives the sequential result. 64-bit atomic max.
+ * hq_ingest_ack_dev: ack[group] |= 1 << slot — the confirmed-set insert of readIndex.confirm
+ *   (readindex.go:83); idempotent, so duplicate acks never double count. ack must be 4-byte
+ *   aligned (32-bit atomic OR on the containing word).
+ * hq_append_dev: the leader appended entries at its current term up to new_last
+ *   (appendEntries, raft.go:911-922): last_index = new_last, the leader's own match (slot 0) =
+ *   new_last (raft.go:918), and the term-mask bits of (old_last, new_last] are set (ring_len <= 16).
+ *   new_last <= last_index leaves the group unchanged. term_mask may be NULL.
+ *
+ * Updates whose group >= G or slot >= n_max are skipped and counted into *n_skipped (a device
+ * uint64_t, may be NULL; accumulated, not reset).
+ */
+typedef struct hq_match_update {
+    uint64_t group_slot;   /* group << 8 | slot */
+    uint64_t index;        /* ReplicateResp LogIndex accepted by the leader */
+} hq_match_update;
+
+typedef struct hq_append_update {
+    uint64_t group;
+    uint64_t new_last;
+} hq_append_update;
+
+int hq_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
+                        uint64_t *match, uint64_t match_stride, uint64_t G, uint32_t n_max,
+                        uint64_t *n_skipped);
+int hq_ingest_ack_dev(hq_ctx *ctx, const uint64_t *group_slot, uint64_t count, uint8_t *ack,
+                      uint64_t G, uint32_t n_max, uint64_t *n_skipped);
+int hq_append_dev(hq_ctx *ctx, const hq_append_update *updates, uint64_t count,
+                  uint64_t *last_index, uint64_t *match_slot0, uint16_t *term_mask,
+                  uint32_t ring_len, uint64_t G, uint64_t *n_skipped);
+
 /* ---------------------------------------------------------------- synthetic inputs ---------- */
 
 /*

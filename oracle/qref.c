@@ -470,6 +470,51 @@ int qref_check_quorum_batch(uint64_t G, uint8_t *active, const uint8_t *n_voting
     return fan_out(j, G, nthreads, 64);
 }
 
+/* ================================================================ delta ingest ============= */
+
+/* remote.tryUpdate — remote.go:123-133: if r.match < index { r.match = index } */
+uint64_t qref_ingest_match(const uint64_t *u, uint64_t count, uint64_t *match, uint64_t stride,
+                           uint64_t G, uint32_t n_max) {
+    uint64_t skipped = 0;
+    for (uint64_t i = 0; i < count; i++) {
+        uint64_t g = u[2 * i] >> 8, s = u[2 * i] & 0xFF, index = u[2 * i + 1];
+        if (g >= G || s >= n_max) { skipped++; continue; }
+        uint64_t *m = &match[s * stride + g];
+        if (*m < index) *m = index;
+    }
+    return skipped;
+}
+
+/* readIndex.confirm — readindex.go:83: p.confirmed[from] = struct{}{} */
+uint64_t qref_ingest_ack(const uint64_t *gs, uint64_t count, uint8_t *ack, uint64_t G,
+                         uint32_t n_max) {
+    uint64_t skipped = 0;
+    for (uint64_t i = 0; i < count; i++) {
+        uint64_t g = gs[i] >> 8, s = gs[i] & 0xFF;
+        if (g >= G || s >= n_max || s >= 8) { skipped++; continue; }
+        ack[g] |= (uint8_t)(1u << s);
+    }
+    return skipped;
+}
+
+/* raft.appendEntries — raft.go:911-922: entries get r.term and indexes lastIndex+1.., then
+ * remotes[self].tryUpdate(lastIndex) */
+uint64_t qref_append(const uint64_t *u, uint64_t count, uint64_t *last_index,
+                     uint64_t *match_slot0, uint16_t *term_mask, uint32_t R, uint64_t G) {
+    uint64_t skipped = 0;
+    for (uint64_t i = 0; i < count; i++) {
+        uint64_t g = u[2 * i], new_last = u[2 * i + 1];
+        if (g >= G) { skipped++; continue; }
+        for (uint64_t idx = last_index[g] + 1; idx <= new_last; idx++) {
+            if (term_mask) term_mask[g] |= (uint16_t)(1u << (idx & (R - 1)));
+            if (new_last - idx >= R) idx = new_last - R;  /* older bits are overwritten anyway */
+        }
+        if (new_last > last_index[g]) last_index[g] = new_last;
+        if (match_slot0[g] < last_index[g]) match_slot0[g] = last_index[g];
+    }
+    return skipped;
+}
+
 uint64_t qref_fnv1a64(const void *p, size_t bytes) {
     const uint8_t *b = (const uint8_t *)p;
     uint64_t h = 0xcbf29ce484222325ull;

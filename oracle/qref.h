@@ -158,6 +158,18 @@ int qref_check_quorum_batch(uint64_t G, uint8_t *active, const uint8_t *n_voting
                             uint32_t n_uniform, uint32_t self_slot, uint64_t *has_quorum,
                             uint64_t *fallback, int nthreads);
 
+/* ---------------------------------------------------------------- delta ingest (§8f-1) ----- */
+/* Sequential restatements, applied in array order: remote.tryUpdate (remote.go:123-133) on
+ * match[slot*stride + group]; the confirmed-set insert (readindex.go:83) on ack[group]; and the
+ * leader's appendEntries (raft.go:911-922) on last_index / its own match / the term mask.
+ * Entries with group >= G or slot >= n_max are skipped; the return value is the skip count. */
+uint64_t qref_ingest_match(const uint64_t *group_slot_index, uint64_t count, uint64_t *match,
+                           uint64_t stride, uint64_t G, uint32_t n_max);
+uint64_t qref_ingest_ack(const uint64_t *group_slot, uint64_t count, uint8_t *ack, uint64_t G,
+                         uint32_t n_max);
+uint64_t qref_append(const uint64_t *group_newlast, uint64_t count, uint64_t *last_index,
+                     uint64_t *match_slot0, uint16_t *term_mask, uint32_t ring_len, uint64_t G);
+
 /* ---------------------------------------------------------------- synthetic inputs -------- */
 /* Same layout as hq_synth_spec; CPU twin of the device generator. */
 typedef struct qgen_spec {

@@ -108,6 +108,9 @@ def load() -> ctypes.CDLL:
         "qgen_commit": (ctypes.c_int, [ctypes.POINTER(QgenSpec), ctypes.POINTER(QrefCommitArgs)]),
         "qgen_bitmaps": (ctypes.c_int, [ctypes.POINTER(QgenSpec), _vp, _vp, _vp, _vp]),
         "qref_fnv1a64": (_u64, [_vp, ctypes.c_size_t]),
+        "qref_ingest_match": (_u64, [_vp, _u64, _vp, _u64, _u64, ctypes.c_uint32]),
+        "qref_ingest_ack": (_u64, [_vp, _u64, _vp, _u64, ctypes.c_uint32]),
+        "qref_append": (_u64, [_vp, _u64, _vp, _vp, _vp, ctypes.c_uint32, _u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -318,6 +321,27 @@ class BitmapInputs:
         rc = lib.qgen_bitmaps(ctypes.byref(s), _ptr(self.ack), _ptr(self.granted),
                               _ptr(self.rejected), _ptr(self.n_voting))
         assert rc == 0, rc
+
+
+def ingest_match(updates: np.ndarray, match: np.ndarray, stride: int, G: int, n_max: int) -> int:
+    """updates: uint64 [count, 2] rows (group << 8 | slot, index); match updated in place."""
+    u = np.ascontiguousarray(updates, np.uint64)
+    return int(lib.qref_ingest_match(u.ctypes.data_as(_vp), len(u), match.ctypes.data_as(_vp),
+                                     stride, G, n_max))
+
+
+def ingest_ack(group_slot: np.ndarray, ack: np.ndarray, G: int, n_max: int) -> int:
+    gs = np.ascontiguousarray(group_slot, np.uint64)
+    return int(lib.qref_ingest_ack(gs.ctypes.data_as(_vp), len(gs), ack.ctypes.data_as(_vp), G,
+                                   n_max))
+
+
+def append(updates: np.ndarray, last_index, match_slot0, term_mask, ring_len: int, G: int) -> int:
+    u = np.ascontiguousarray(updates, np.uint64)
+    return int(lib.qref_append(u.ctypes.data_as(_vp), len(u), last_index.ctypes.data_as(_vp),
+                               match_slot0.ctypes.data_as(_vp),
+                               None if term_mask is None else term_mask.ctypes.data_as(_vp),
+                               ring_len, G))
 
 
 def fnv1a64(a: np.ndarray) -> int:
