@@ -10,6 +10,9 @@
 namespace {
 
 constexpr int kBlock = 256;           // 4 waves of 64
+// The commit stream runs 512-thread blocks: ~5 % shorter than 256 on the 1M x 3 launch under
+// rocprofv3 (11.7 vs 12.4 us, tools/kexp2.hip); 4 groups per lane was slower.
+constexpr int kCommitBlock = 512;
 constexpr int kMaxBlocks = 256 * 16;  // grid-stride beyond 16 workgroups per CU
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -141,10 +144,10 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
 
 // VEC = groups per lane (2: 16-byte loads of every SoA column; 1: 8-byte loads).
 template <int N, int FORM, int VEC, bool PERN>
-__global__ __launch_bounds__(kBlock) void k_commit(const CommitK a) {
+__global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t step = (uint64_t)gridDim.x * kBlock * VEC;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kCommitBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = (uint64_t)gridDim.x * kCommitBlock * VEC;
     const uint64_t *aux_col = (FORM == HQ_FORM_TERM_START) ? a.tstart : a.term;
     // aux of group g: the u64 column (forms 0, 1) or the u16 term mask (form 2)
     auto aux1 = [&](uint64_t g) -> uint64_t {
@@ -492,20 +495,20 @@ __global__ __launch_bounds__(kBlock) void k_synth_bits(const hq_synth_spec s, ui
     }
 }
 
-unsigned grid_for(uint64_t lanes_needed) {
-    uint64_t b = (lanes_needed + kBlock - 1) / kBlock;
+unsigned grid_for(uint64_t lanes_needed, int block = kBlock, uint64_t max_blocks = kMaxBlocks) {
+    uint64_t b = (lanes_needed + block - 1) / block;
     if (b < 1) b = 1;
-    if (b > (uint64_t)kMaxBlocks) b = kMaxBlocks;
+    if (b > max_blocks) b = max_blocks;
     return (unsigned)b;
 }
 
 template <int N, int FORM, int VEC, bool PERN>
 int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
-    const unsigned grid = grid_for((k.G + VEC - 1) / VEC);
+    const unsigned grid = grid_for((k.G + VEC - 1) / VEC, kCommitBlock, kMaxBlocks / 2);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN>), dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       k);
+    hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN>), dim3(grid), dim3(kCommitBlock), 0,
+                       ctx->stream, k);
     return hq::post_launch(ctx, "k_commit");
 }
 
@@ -728,6 +731,117 @@ extern "C" int hq_synth_bitmaps_dev(hq_ctx *ctx, const hq_synth_spec *s, uint8_t
     hipLaunchKernelGGL(k_synth_bits, dim3(grid_for(s->G)), dim3(kBlock), 0, ctx->stream, *s, ack,
                        granted, rejected, n_voting);
     return hq::post_launch(ctx, "k_synth_bits");
+}
+
+// ---- general multi-ctx ReadIndex ------------------------------------------
+namespace {
+
+struct RiMultiK {
+    uint64_t G;
+    uint32_t K_max, n_max, n_uniform;
+    const uint16_t *ord;
+    const uint64_t *idx;
+    const uint8_t *np, *nv;
+    uint64_t *rel;
+    uint8_t *cnt;
+    uint64_t *fallback;
+};
+
+__device__ __forceinline__ void ce32(uint32_t &a, uint32_t &b) {
+    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+__device__ __forceinline__ void sort_net_u32(uint32_t (&v)[8]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+        for (int i = r & 1; i + 1 < 8; i += 2) ce32(v[i], v[i + 1]);
+    }
+}
+
+template <bool PERK, bool PERN>
+__global__ __launch_bounds__(kBlock) void k_ri_multi(const RiMultiK a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t wbase = wave * 64; wbase < a.G; wbase += step) {
+        const uint64_t g = wbase + lane;
+        bool fb = false;
+        if (g < a.G) {
+            const uint32_t K = PERK ? a.np[g] : a.K_max;
+            const uint32_t n = PERN ? a.nv[g] : a.n_uniform;
+            fb = n < 1 || n > a.n_max || K > a.K_max;
+            uint64_t idx[8];
+            uint32_t t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                idx[k] = 0;
+                t[k] = 0xFFFFu;
+                if (!fb && k < (int)K) {
+                    idx[k] = a.idx[(uint64_t)k * a.G + g];
+                    fb |= k > 0 && idx[k] < idx[k - 1];   // addRequest: index moved backward
+                    // reach time: the max(q-1, 1)-th smallest first-ack ordinal (readindex.go:84)
+                    uint32_t v[8];
+#pragma unroll
+                    for (int s = 0; s < 8; ++s)
+                        v[s] = (s < (int)n) ? a.ord[((uint64_t)k * a.n_max + s) * a.G + g] : 0xFFFFu;
+                    sort_net_u32(v);
+                    const int r = (int)(n / 2 + 1) - 1 > 1 ? (int)(n / 2 + 1) - 1 : 1;
+                    uint32_t tk = 0xFFFFu;
+#pragma unroll
+                    for (int s = 0; s < 8; ++s) tk = (s == r - 1) ? v[s] : tk;
+                    t[k] = tk;
+                }
+            }
+            // suffix-min scan: entry i goes with the first ctx k >= i to reach quorum
+            uint32_t best_t = 0xFFFFu;
+            uint64_t best_idx = 0;
+            uint32_t released = 0;
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+                if (!fb && k < (int)K && t[k] != 0xFFFFu && t[k] <= best_t) {
+                    best_t = t[k];
+                    best_idx = idx[k];
+                }
+                const bool rel = !fb && k < (int)K && best_t != 0xFFFFu;
+                released += rel;
+                if (k < (int)a.K_max) a.rel[(uint64_t)k * a.G + g] = rel ? best_idx : ~0ull;
+            }
+            a.cnt[g] = (uint8_t)released;
+        }
+        const uint64_t fw = __ballot(fb);
+        if (a.fallback && lane == 0) a.fallback[wbase >> 6] = fw;
+    }
+}
+
+}  // namespace
+
+extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
+                                      const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                                      const uint8_t *n_pending, const uint8_t *n_voting,
+                                      uint32_t n_uniform, uint64_t *released_index,
+                                      uint8_t *released_count, uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!ack_ordinal || !ctx_index || !released_index || !released_count || K_max < 1 ||
+        K_max > 8 || n_max < 1 || n_max > 8 || (!n_voting && (n_uniform < 1 || n_uniform > 8)))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_dev: bad arguments");
+    RiMultiK k{G, K_max, n_max, n_uniform, ack_ordinal, ctx_index, n_pending, n_voting,
+               released_index, released_count, fallback};
+    const unsigned grid = grid_for(G);
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    if (n_pending && n_voting)
+        hipLaunchKernelGGL((k_ri_multi<true, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    else if (n_pending)
+        hipLaunchKernelGGL((k_ri_multi<true, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    else if (n_voting)
+        hipLaunchKernelGGL((k_ri_multi<false, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    else
+        hipLaunchKernelGGL((k_ri_multi<false, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    return hq::post_launch(ctx, "k_ri_multi");
 }
 
 // ---- device-resident progress table: delta ingest ------------------------

@@ -108,6 +108,9 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp],
     ),
+    "hq_readindex_multi_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_uint32, _vp, _vp, _vp, _vp,
+                                              ctypes.c_uint32, _vp, _vp, _vp]),
     "hq_ingest_match_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                            ctypes.c_uint64, ctypes.c_uint32, _vp]),
     "hq_ingest_ack_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
@@ -297,6 +300,13 @@ class Context:
     def vote_host(self, G, granted, rejected, n_voting, n_uniform, outcome, fallback=None) -> None:
         self._check(lib.hq_vote(self.h, G, _p(granted), _p(rejected), _p(n_voting), n_uniform,
                                 _p(outcome), _p(fallback)))
+
+    def readindex_multi_dev(self, G, K_max, n_max, ack_ordinal, ctx_index, n_pending, n_voting,
+                            n_uniform, released_index, released_count, fallback=None):
+        self._check(lib.hq_readindex_multi_dev(self.h, G, K_max, n_max, _p(ack_ordinal),
+                                               _p(ctx_index), _p(n_pending), _p(n_voting),
+                                               n_uniform, _p(released_index),
+                                               _p(released_count), _p(fallback)))
 
     def ingest_match_dev(self, updates, count, match, match_stride, G, n_max, n_skipped=None):
         """updates: device array of hq_match_update (uint64 pairs: group << 8 | slot, index)."""

@@ -193,6 +193,27 @@ int hq_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *
 int hq_vote(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *rejected,
             const uint8_t *n_voting, uint32_t n_uniform, uint64_t *outcome, uint64_t *fallback);
 
+/*
+ * General ReadIndex with several pending ctxs per group (readindex.go:43-116).
+ * Per group g: K = n_pending ? n_pending[g] : K_max ctxs in queue order (oldest first) with
+ * indexes ctx_index[k * G + g] (non-decreasing, addRequest readindex.go:50-59); and
+ * ack_ordinal[(k * n_max + s) * G + g] = the arrival ordinal (message sequence number within the
+ * batch, 0 for acks carried over from earlier steps) of voting slot s's first HeartbeatResp for
+ * ctx k, 0xFFFF = none. Replaying the messages in ordinal order through confirm() releases queue
+ * prefixes; equivalently ctx k reaches quorum at t_k = the max(q-1, 1)-th smallest of its
+ * ordinals and entry i is released at min_{k >= i} t_k with the index of the (first) ctx
+ * attaining it (the rewrite of readindex.go:97-105).
+ * Out: released_index[k * G + g] = rewritten index of entry k, or UINT64_MAX if not released;
+ * released_count[g] = released prefix length. n outside [1, n_max], K > K_max or a decreasing
+ * ctx_index give fallback (nothing released). K_max <= 8, n_max <= 8; ordinals distinct per
+ * group except 0 (ties at equal ordinals resolve in queue order).
+ */
+int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
+                           const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                           const uint8_t *n_pending, const uint8_t *n_voting, uint32_t n_uniform,
+                           uint64_t *released_index, uint8_t *released_count,
+                           uint64_t *fallback);
+
 /* ReadIndex confirmation and vote tally of the same groups in one pass over the shared n. */
 int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
                           const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,

@@ -5,6 +5,7 @@
 #include "qref.h"
 
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* ================================================================ quorum arithmetic ======== */
@@ -468,6 +469,119 @@ int qref_check_quorum_batch(uint64_t G, uint8_t *active, const uint8_t *n_voting
     j.kind = JOB_CHECKQ; j.bw = active; j.nv = n_voting; j.nu = n_uniform; j.self_slot = self_slot;
     j.o0 = has_quorum; j.o1 = fallback;
     return fan_out(j, G, nthreads, 64);
+}
+
+/* ================================================================ multi-ctx ReadIndex ====== */
+
+typedef struct { uint32_t o, k, s; } ri_msg;
+
+static void ri_multi_range(uint64_t g0, uint64_t g1, uint32_t K_max, uint32_t n_max,
+                           const uint16_t *ord, const uint64_t *idx, const uint8_t *np,
+                           const uint8_t *nv, uint32_t nu, uint64_t *rel, uint8_t *cnt,
+                           uint64_t *fallback, uint64_t G) {
+    qref_read_index *ri = (qref_read_index *)malloc(sizeof *ri);
+    qref_read_status *out = (qref_read_status *)malloc(QREF_MAX_PENDING * sizeof *out);
+    ri_msg msgs[64 * 8];
+    for (uint64_t g = g0; g < g1; g++) {
+        uint32_t K = np ? np[g] : K_max;
+        int n = nv ? nv[g] : (int)nu;
+        for (uint32_t k = 0; k < K_max; k++) rel[(uint64_t)k * G + g] = UINT64_MAX;
+        cnt[g] = 0;
+        if (n < 1 || n > (int)n_max || K > K_max) {
+            if (fallback) bit_set(fallback, g);
+            continue;
+        }
+        int quorum = qref_quorum(n);
+        qref_ri_init(ri);
+        int bad = 0;
+        for (uint32_t k = 0; k < K && !bad; k++) {   /* handleLeaderReadIndex -> addRequest */
+            qref_sysctx c = {k + 1, k + 1};
+            bad = qref_ri_add_request(ri, idx[(uint64_t)k * G + g], c, 1) != QREF_OK;
+        }
+        if (bad) {                                     /* index moved backward: contract */
+            if (fallback) bit_set(fallback, g);
+            continue;
+        }
+        int nm = 0;
+        for (uint32_t k = 0; k < K; k++)
+            for (int s = 0; s < n; s++) {
+                uint16_t o = ord[((uint64_t)k * n_max + s) * G + g];
+                if (o != 0xFFFF) { msgs[nm].o = o; msgs[nm].k = k; msgs[nm].s = (uint32_t)s; nm++; }
+            }
+        /* arrival order: ordinal, then queue position (stable for equal ordinals) */
+        for (int i = 1; i < nm; i++) {
+            ri_msg v = msgs[i];
+            int j = i - 1;
+            while (j >= 0 && (msgs[j].o > v.o || (msgs[j].o == v.o && msgs[j].k > v.k))) {
+                msgs[j + 1] = msgs[j];
+                j--;
+            }
+            msgs[j + 1] = v;
+        }
+        uint8_t released = 0;
+        for (int i = 0; i < nm; i++) {                 /* HeartbeatResp -> confirm */
+            qref_sysctx c = {msgs[i].k + 1, msgs[i].k + 1};
+            int r = qref_ri_confirm(ri, c, (uint64_t)msgs[i].s + 1, quorum, out);
+            for (int j = 0; j < r; j++) {
+                rel[(out[j].ctx.low - 1) * G + g] = out[j].index;
+                released++;
+            }
+        }
+        cnt[g] = released;
+    }
+    free(ri);
+    free(out);
+}
+
+typedef struct {
+    uint64_t g0, g1, G;
+    uint32_t K_max, n_max, nu;
+    const uint16_t *ord;
+    const uint64_t *idx;
+    const uint8_t *np, *nv;
+    uint64_t *rel, *fb;
+    uint8_t *cnt;
+} ri_multi_job;
+
+static void *ri_multi_run(void *p) {
+    ri_multi_job *j = (ri_multi_job *)p;
+    ri_multi_range(j->g0, j->g1, j->K_max, j->n_max, j->ord, j->idx, j->np, j->nv, j->nu, j->rel,
+                   j->cnt, j->fb, j->G);
+    return NULL;
+}
+
+int qref_readindex_multi_batch(uint64_t G, uint32_t K_max, uint32_t n_max,
+                               const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                               const uint8_t *n_pending, const uint8_t *n_voting,
+                               uint32_t n_uniform, uint64_t *released_index,
+                               uint8_t *released_count, uint64_t *fallback, int nthreads) {
+    if (!ack_ordinal || !ctx_index || !released_index || !released_count || K_max < 1 ||
+        K_max > 64 || n_max < 1 || n_max > 8)
+        return -1;
+    if (fallback) memset(fallback, 0, words64(G, 64) * 8);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    ri_multi_job jobs[64];
+    pthread_t th[64];
+    uint64_t blocks = (G + 63) / 64, per = (blocks + nthreads - 1) / nthreads;
+    int started = 0;
+    for (int t = 0; t < nthreads; t++) {
+        uint64_t b0 = per * t, b1 = per * (t + 1);
+        if (b0 >= blocks) break;
+        if (b1 > blocks) b1 = blocks;
+        ri_multi_job j = {b0 * 64, b1 * 64 < G ? b1 * 64 : G, G, K_max, n_max, n_uniform,
+                          ack_ordinal, ctx_index, n_pending, n_voting, released_index, fallback,
+                          released_count};
+        jobs[t] = j;
+        if (nthreads == 1 || pthread_create(&th[t], NULL, ri_multi_run, &jobs[t]) != 0) {
+            ri_multi_run(&jobs[t]);
+            th[t] = 0;
+        }
+        started++;
+    }
+    for (int t = 0; t < started; t++)
+        if (th[t]) pthread_join(th[t], NULL);
+    return 0;
 }
 
 /* ================================================================ delta ingest ============= */

@@ -158,6 +158,19 @@ int qref_check_quorum_batch(uint64_t G, uint8_t *active, const uint8_t *n_voting
                             uint32_t n_uniform, uint32_t self_slot, uint64_t *has_quorum,
                             uint64_t *fallback, int nthreads);
 
+/* General multi-ctx ReadIndex. Per group: K pending ctxs in queue order with
+ * indexes ctx_index[k*G + g] (addRequest, readindex.go:43-67); ack_ordinal[(k*n_max + s)*G + g]
+ * = arrival ordinal of voting slot s's first HeartbeatResp for ctx k (0xFFFF = none). The
+ * messages are replayed in ordinal order through readIndex.confirm (readindex.go:77-116);
+ * released_index[k*G + g] = the rewritten index of entry k if it was released, else UINT64_MAX;
+ * released_count[g] = released prefix length. Groups with n outside [1, n_max] or K > K_max are
+ * fallback (nothing released). */
+int qref_readindex_multi_batch(uint64_t G, uint32_t K_max, uint32_t n_max,
+                               const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                               const uint8_t *n_pending, const uint8_t *n_voting,
+                               uint32_t n_uniform, uint64_t *released_index,
+                               uint8_t *released_count, uint64_t *fallback, int nthreads);
+
 /* ---------------------------------------------------------------- delta ingest (§8f-1) ----- */
 /* Sequential restatements, applied in array order: remote.tryUpdate (remote.go:123-133) on
  * match[slot*stride + group]; the confirmed-set insert (readindex.go:83) on ack[group]; and the

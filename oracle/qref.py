@@ -108,6 +108,9 @@ def load() -> ctypes.CDLL:
         "qgen_commit": (ctypes.c_int, [ctypes.POINTER(QgenSpec), ctypes.POINTER(QrefCommitArgs)]),
         "qgen_bitmaps": (ctypes.c_int, [ctypes.POINTER(QgenSpec), _vp, _vp, _vp, _vp]),
         "qref_fnv1a64": (_u64, [_vp, ctypes.c_size_t]),
+        "qref_readindex_multi_batch": (ctypes.c_int, [_u64, ctypes.c_uint32, ctypes.c_uint32, _vp,
+                                                      _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
+                                                      _vp, ctypes.c_int]),
         "qref_ingest_match": (_u64, [_vp, _u64, _vp, _u64, _u64, ctypes.c_uint32]),
         "qref_ingest_ack": (_u64, [_vp, _u64, _vp, _u64, ctypes.c_uint32]),
         "qref_append": (_u64, [_vp, _u64, _vp, _vp, _vp, ctypes.c_uint32, _u64]),
@@ -321,6 +324,21 @@ class BitmapInputs:
         rc = lib.qgen_bitmaps(ctypes.byref(s), _ptr(self.ack), _ptr(self.granted),
                               _ptr(self.rejected), _ptr(self.n_voting))
         assert rc == 0, rc
+
+
+def readindex_multi_batch(ack_ordinal, ctx_index, n_pending, n_voting, n_uniform, K_max, n_max,
+                          nthreads=1):
+    """General multi-ctx ReadIndex: returns (released_index [K_max*G], released_count [G],
+    fallback bitmap). ack_ordinal: uint16 [K_max][n_max][G]; ctx_index: uint64 [K_max][G]."""
+    G = len(ctx_index) // K_max
+    rel = np.zeros(K_max * G, np.uint64)
+    cnt = np.zeros(G, np.uint8)
+    fb = np.zeros(words64(G), np.uint64)
+    rc = lib.qref_readindex_multi_batch(G, K_max, n_max, _ptr(ack_ordinal), _ptr(ctx_index),
+                                        _ptr(n_pending), _ptr(n_voting), n_uniform, _ptr(rel),
+                                        _ptr(cnt), _ptr(fb), nthreads)
+    assert rc == 0, rc
+    return rel, cnt, fb
 
 
 def ingest_match(updates: np.ndarray, match: np.ndarray, stride: int, G: int, n_max: int) -> int:

@@ -1,0 +1,97 @@
+"""General multi-ctx ReadIndex (readindex.go:43-116).
+
+CPU: the oracle's message replay against the reference's own table
+(TestReadIndexLeaderCanBeConfirmed) and against the closed form the kernel uses (reach time =
+max(q-1, 1)-th smallest first-ack ordinal, suffix-min release). GPU: the kernel against the
+oracle, bit-exact, on random queues."""
+import numpy as np
+import pytest
+
+from oracle import qref
+
+NONE = 0xFFFF
+U64MAX = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def random_batch(rng, G, K_max, n_max, carried=True):
+    K = rng.integers(1, K_max + 1, G).astype(np.uint8)
+    n = rng.integers(1, n_max + 1, G).astype(np.uint8)
+    idx = np.cumsum(rng.integers(0, 3, (K_max, G)), axis=0).astype(np.uint64) + np.uint64(100)
+    ord_ = np.full((K_max, n_max, G), NONE, np.uint16)
+    for g in range(G):
+        cells = [(k, s) for k in range(K[g]) for s in range(n[g]) if rng.random() < 0.45]
+        perm = rng.permutation(len(cells)) + 1
+        for (k, s), o in zip(cells, perm):
+            ord_[k, s, g] = 0 if (carried and rng.random() < 0.1) else o
+    return ord_.reshape(-1), idx.reshape(-1), K, n
+
+
+def closed_form(ord_, idx, K, n, K_max, n_max, G):
+    ord_ = ord_.reshape(K_max, n_max, G)
+    idx = idx.reshape(K_max, G)
+    rel = np.full((K_max, G), U64MAX)
+    cnt = np.zeros(G, np.uint8)
+    for g in range(G):
+        q = int(n[g]) // 2 + 1
+        r = max(q - 1, 1)
+        t = []
+        for k in range(K[g]):
+            v = sorted(int(x) for x in ord_[k, :n[g], g] if x != NONE)
+            t.append(v[r - 1] if len(v) >= r else None)
+        best = None
+        for k in reversed(range(K[g])):
+            if t[k] is not None and (best is None or t[k] <= best[0]):
+                best = (t[k], k)
+            if best is not None:
+                rel[k, g] = idx[best[1], g]
+                cnt[g] += 1
+    return rel.reshape(-1), cnt
+
+
+def test_reference_table_as_batch():
+    # readindex_test.go:125-162: queue ctx2(3), ctx(4), ctx3(5); ctx confirmed by 1 and 3, q = 3
+    K_max, n_max, G = 3, 5, 1
+    ord_ = np.full((K_max, n_max, G), NONE, np.uint16)
+    ord_[1, 0, 0], ord_[1, 2, 0] = 1, 2          # from 1 -> slot 0, from 3 -> slot 2
+    idx = np.array([[3], [4], [5]], np.uint64)
+    rel, cnt, fb = qref.readindex_multi_batch(ord_.reshape(-1), idx.reshape(-1), None, None, 5,
+                                              K_max, n_max)
+    assert list(rel) == [4, 4, int(U64MAX)] and cnt[0] == 2 and fb[0] == 0
+
+
+def test_oracle_replay_equals_closed_form():
+    rng = np.random.default_rng(5)
+    G, K_max, n_max = 3000, 6, 7
+    ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
+    rel, cnt, fb = qref.readindex_multi_batch(ord_, idx, K, n, 0, K_max, n_max)
+    want_rel, want_cnt = closed_form(ord_, idx, K, n, K_max, n_max, G)
+    assert not fb.any()
+    np.testing.assert_array_equal(rel, want_rel)
+    np.testing.assert_array_equal(cnt, want_cnt)
+    assert 0 < cnt.astype(int).sum() < K.astype(int).sum()
+
+
+def test_decreasing_index_is_fallback():
+    ord_ = np.full(2 * 3, NONE, np.uint16)
+    rel, cnt, fb = qref.readindex_multi_batch(ord_, np.array([5, 4], np.uint64), None, None, 3, 2, 3)
+    assert fb[0] == 1 and cnt[0] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K_max,n_max,G", [(8, 8, 20_011), (3, 5, 4097), (1, 3, 65)])
+def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G):
+    rng = np.random.default_rng(K_max * 100 + n_max)
+    ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
+    n[::97] = 0                                   # invalid n -> fallback
+    idx.reshape(K_max, G)[:, 5] = np.arange(K_max, 0, -1)   # decreasing -> fallback
+    want_rel, want_cnt, want_fb = qref.readindex_multi_batch(ord_, idx, K, n, 0, K_max, n_max)
+    d = [gpu_ctx.upload(x) for x in (ord_, idx, K, n)]
+    rel = gpu_ctx.empty(K_max * G, np.uint64)
+    cnt = gpu_ctx.empty(G, np.uint8)
+    fb = gpu_ctx.empty(hq.words64(G), np.uint64)
+    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], 0, rel, cnt, fb)
+    np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
+    np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
+    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
+    for x in d + [rel, cnt, fb]:
+        gpu_ctx.free(x)
