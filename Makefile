@@ -5,14 +5,21 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH)
 CSRC := dragonboat_amd/csrc
 LIBDIR := dragonboat_amd/lib
 LIB := $(LIBDIR)/libhipquorum.so
-OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o
+OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o $(LIBDIR)/hq_pack.o
 DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
+CXX ?= g++
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra
 
 all: $(LIB) oracle
 
 $(LIBDIR)/%.o: $(CSRC)/%.hip $(DEPS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+# host-only sources (packers): plain C++
+$(LIBDIR)/%.o: $(CSRC)/%.cpp $(DEPS)
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
 
 $(LIB): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)

@@ -1,0 +1,138 @@
+// hq_pack.cpp — host-side packers of libhipquorum.so: a step worker's per-group membership and
+// step messages -> the kernels' structure-of-arrays inputs, with the reference's role rules
+// (include/hipquorum.h "host-side packers"). Plain C++ on the host; no GPU calls.
+#include <cstring>
+
+#include "../../include/hipquorum.h"
+
+namespace {
+
+// Voting slots of one group: slot 0 = the group's own node (must be a remote), then the other
+// remotes, then the witnesses, in member order. Observers get no slot (raft.go:368-370).
+struct Slots {
+    int n = 0;
+    int member[HQ_MAX_VOTERS];
+    bool ok = false;
+};
+
+Slots voting_slots(const hq_group_view &v, const hq_member *m, uint32_t n_max) {
+    Slots s;
+    const hq_member *mm = m + v.first_member;
+    int self = -1, count = 0;
+    for (uint32_t i = 0; i < v.n_members; ++i) {
+        if (mm[i].role == HQ_ROLE_OBSERVER) continue;
+        if (mm[i].role != HQ_ROLE_REMOTE && mm[i].role != HQ_ROLE_WITNESS) return s;  // unknown role
+        ++count;
+        if (mm[i].role == HQ_ROLE_REMOTE && mm[i].node_id == v.node_id) self = (int)i;
+    }
+    if (self < 0 || count > (int)n_max || count > HQ_MAX_VOTERS) return s;
+    s.member[s.n++] = self;
+    for (uint32_t pass = 0; pass < 2; ++pass) {
+        const uint32_t role = pass == 0 ? HQ_ROLE_REMOTE : HQ_ROLE_WITNESS;
+        for (uint32_t i = 0; i < v.n_members; ++i)
+            if (mm[i].role == role && (int)i != self) s.member[s.n++] = (int)i;
+    }
+    s.ok = true;
+    return s;
+}
+
+// slot of `from` among the voting members, -1 for observers and non-members
+int slot_of(const Slots &s, const hq_group_view &v, const hq_member *m, uint64_t from) {
+    for (int k = 0; k < s.n; ++k)
+        if (m[v.first_member + s.member[k]].node_id == from) return k;
+    return -1;
+}
+
+inline void set_bit(uint64_t *bm, uint64_t g) {
+    if (bm) bm[g >> 6] |= 1ull << (g & 63);
+}
+
+}  // namespace
+
+extern "C" int hq_pack_commit(const hq_group_view *groups, uint64_t G, const hq_member *members,
+                              hq_commit_args *a) {
+    if (G == 0) return HQ_OK;
+    if (!groups || !members || !a || !a->match || !a->committed_in || !a->last_index ||
+        !a->n_voting || a->G != G || a->match_stride < G || a->n_max < 1 ||
+        a->n_max > HQ_MAX_VOTERS)
+        return HQ_E_INVAL;
+    uint64_t *match = const_cast<uint64_t *>(a->match);
+    uint8_t *nv = const_cast<uint8_t *>(a->n_voting);
+    if (a->fallback) std::memset(a->fallback, 0, ((G + 63) / 64) * 8);
+    for (uint64_t g = 0; g < G; ++g) {
+        const hq_group_view &v = groups[g];
+        const Slots s = voting_slots(v, members, a->n_max);
+        for (uint32_t k = 0; k < a->n_max; ++k)
+            match[k * a->match_stride + g] =
+                (s.ok && (int)k < s.n) ? members[v.first_member + s.member[k]].match : 0;
+        nv[g] = s.ok ? (uint8_t)s.n : 0;
+        if (!s.ok) set_bit(a->fallback, g);
+        const_cast<uint64_t *>(a->committed_in)[g] = v.committed;
+        const_cast<uint64_t *>(a->last_index)[g] = v.last_index;
+        if (a->term_start) const_cast<uint64_t *>(a->term_start)[g] = v.term_start;
+        if (a->term) const_cast<uint64_t *>(a->term)[g] = v.term;
+        if (a->term_mask) const_cast<uint16_t *>(a->term_mask)[g] = v.term_mask;
+    }
+    return HQ_OK;
+}
+
+extern "C" int hq_pack_votes(const hq_group_view *groups, uint64_t G, const hq_member *members,
+                             const hq_msg *msgs, uint8_t *granted, uint8_t *rejected,
+                             uint8_t *n_voting, uint64_t *fallback) {
+    if (G == 0) return HQ_OK;
+    if (!groups || !members || !granted || !rejected || !n_voting) return HQ_E_INVAL;
+    if (fallback) std::memset(fallback, 0, ((G + 63) / 64) * 8);
+    for (uint64_t g = 0; g < G; ++g) {
+        const hq_group_view &v = groups[g];
+        const Slots s = voting_slots(v, members, HQ_MAX_VOTERS);
+        uint32_t gr = 0, rj = 0;
+        if (s.ok) {
+            gr = 1;  // campaign: the candidate votes for itself (raft.go:1093)
+            for (uint32_t i = 0; i < v.n_msgs; ++i) {
+                if (!msgs) return HQ_E_INVAL;
+                const hq_msg &mm = msgs[v.first_msg + i];
+                const int k = slot_of(s, v, members, mm.from);  // observers / non-members dropped
+                if (k < 0 || ((gr | rj) >> k) & 1) continue;    // first response wins
+                if (mm.reject) rj |= 1u << k;
+                else gr |= 1u << k;
+            }
+        } else {
+            set_bit(fallback, g);
+        }
+        granted[g] = (uint8_t)gr;
+        rejected[g] = (uint8_t)rj;
+        n_voting[g] = s.ok ? (uint8_t)s.n : 0;
+    }
+    return HQ_OK;
+}
+
+extern "C" int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *members,
+                            const hq_msg *msgs, uint8_t *ack, uint8_t *active, uint8_t *n_voting,
+                            uint32_t n_max, uint64_t *fallback) {
+    if (G == 0) return HQ_OK;
+    if (!groups || !members || !ack || !n_voting || n_max < 1 || n_max > HQ_MAX_VOTERS)
+        return HQ_E_INVAL;
+    if (fallback) std::memset(fallback, 0, ((G + 63) / 64) * 8);
+    for (uint64_t g = 0; g < G; ++g) {
+        const hq_group_view &v = groups[g];
+        const Slots s = voting_slots(v, members, n_max);
+        uint32_t a = 0, act = 0;
+        if (s.ok) {
+            for (uint32_t i = 0; i < v.n_msgs; ++i) {
+                if (!msgs) return HQ_E_INVAL;
+                const hq_msg &mm = msgs[v.first_msg + i];
+                if (mm.hint_low != v.ctx_low || mm.hint_high != v.ctx_high) continue;
+                const int k = slot_of(s, v, members, mm.from);
+                if (k >= 0) a |= 1u << k;   // the confirmed set (readindex.go:83)
+            }
+            for (int k = 0; k < s.n; ++k)
+                act |= (uint32_t)(members[v.first_member + s.member[k]].active != 0) << k;
+        } else {
+            set_bit(fallback, g);
+        }
+        ack[g] = (uint8_t)a;
+        if (active) active[g] = (uint8_t)act;
+        n_voting[g] = s.ok ? (uint8_t)s.n : 0;
+    }
+    return HQ_OK;
+}

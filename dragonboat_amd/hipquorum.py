@@ -76,6 +76,18 @@ class SynthSpec(ctypes.Structure):
     ]
 
 
+# numpy mirrors of the packer structs (hq_member, hq_group_view, hq_msg)
+ROLE_REMOTE, ROLE_OBSERVER, ROLE_WITNESS = 0, 1, 2
+MEMBER_DTYPE = np.dtype([("node_id", "<u8"), ("match", "<u8"), ("role", "<u4"),
+                         ("active", "<u4")], align=True)
+GROUP_DTYPE = np.dtype([("node_id", "<u8"), ("committed", "<u8"), ("last_index", "<u8"),
+                        ("term_start", "<u8"), ("term", "<u8"), ("ctx_low", "<u8"),
+                        ("ctx_high", "<u8"), ("term_mask", "<u2"), ("reserved0", "<u2"),
+                        ("reserved1", "<u4"), ("first_member", "<u4"), ("n_members", "<u4"),
+                        ("first_msg", "<u4"), ("n_msgs", "<u4")], align=True)
+MSG_DTYPE = np.dtype([("from", "<u8"), ("hint_low", "<u8"), ("hint_high", "<u8"),
+                      ("reject", "<u4"), ("reserved", "<u4")], align=True)
+
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
 SIGNATURES = {
     "hq_abi_version": (ctypes.c_int, []),
@@ -117,6 +129,10 @@ SIGNATURES = {
                                          ctypes.c_uint32, _vp]),
     "hq_append_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32,
                                      ctypes.c_uint64, _vp]),
+    "hq_pack_commit": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.POINTER(CommitArgs)]),
+    "hq_pack_votes": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hq_pack_acks": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
+                                    ctypes.c_uint32, _vp]),
     "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
     "hq_synth_bitmaps_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), _vp, _vp, _vp, _vp]),
 }
@@ -344,6 +360,46 @@ def _p(x) -> Optional[_vp]:
     if isinstance(x, int):
         return _vp(x)
     raise TypeError(f"unsupported pointer argument {type(x)}")
+
+
+def _chk(rc: int, what: str) -> None:
+    if rc != HQ_OK:
+        raise HQError(rc, what)
+
+
+def pack_commit(groups: np.ndarray, members: np.ndarray, n_max: int, ring_len: int = 16):
+    """hq_pack_commit into fresh host SoA arrays; returns (dict of columns, fallback bitmap)."""
+    G = len(groups)
+    cols = dict(match=np.zeros(n_max * G, np.uint64), n_voting=np.zeros(G, np.uint8),
+                committed_in=np.zeros(G, np.uint64), last_index=np.zeros(G, np.uint64),
+                term_start=np.zeros(G, np.uint64), term=np.zeros(G, np.uint64),
+                term_mask=np.zeros(G, np.uint16))
+    fb = np.zeros(words64(G), np.uint64)
+    a = CommitArgs()
+    a.G, a.n_max, a.ring_len, a.match_stride = G, n_max, ring_len, G
+    for k, v in cols.items():
+        setattr(a, k, v.ctypes.data)
+    a.fallback = fb.ctypes.data
+    _chk(lib.hq_pack_commit(_p(groups), G, _p(members), ctypes.byref(a)), "hq_pack_commit")
+    return cols, fb
+
+
+def pack_votes(groups: np.ndarray, members: np.ndarray, msgs: np.ndarray):
+    G = len(groups)
+    gr, rj, nv = (np.zeros(G, np.uint8) for _ in range(3))
+    fb = np.zeros(words64(G), np.uint64)
+    _chk(lib.hq_pack_votes(_p(groups), G, _p(members), _p(msgs), _p(gr), _p(rj), _p(nv), _p(fb)),
+         "hq_pack_votes")
+    return gr, rj, nv, fb
+
+
+def pack_acks(groups: np.ndarray, members: np.ndarray, msgs: np.ndarray, n_max: int = 8):
+    G = len(groups)
+    ack, act, nv = (np.zeros(G, np.uint8) for _ in range(3))
+    fb = np.zeros(words64(G), np.uint64)
+    _chk(lib.hq_pack_acks(_p(groups), G, _p(members), _p(msgs), _p(ack), _p(act), _p(nv), n_max,
+                          _p(fb)), "hq_pack_acks")
+    return ack, act, nv, fb
 
 
 def commit_batch_array(args_list) -> ctypes.Array:

@@ -266,6 +266,77 @@ int hq_append_dev(hq_ctx *ctx, const hq_append_update *updates, uint64_t count,
                   uint64_t *last_index, uint64_t *match_slot0, uint16_t *term_mask,
                   uint32_t ring_len, uint64_t G, uint64_t *n_skipped);
 
+/* ---------------------------------------------------------------- host-side packers --------- */
+/*
+ * The packers turn a step worker's per-group view — the membership maps r.remotes / r.observers
+ * / r.witnesses (raft.go:206-208) and the response messages of the step — into the kernels' SoA
+ * inputs, applying the reference's role rules. Host functions (no GPU); the caller owns every
+ * array. Slot 0 is always the group's own node (the leader / candidate); then the other remotes,
+ * then the witnesses, in member order; observers never get a slot (numVotingMembers,
+ * raft.go:368-370; tryCommit raft.go:894-901). A group with more than n_max voting members, or
+ * whose own node is not among its remotes, gets n_voting = 0 and a fallback bit, so the kernel
+ * leaves it to the CPU path.
+ */
+#define HQ_ROLE_REMOTE   0u   /* full member (r.remotes) */
+#define HQ_ROLE_OBSERVER 1u   /* non-voting member (r.observers) */
+#define HQ_ROLE_WITNESS  2u   /* witness (r.witnesses): votes and counts, holds no data */
+
+typedef struct hq_member {
+    uint64_t node_id;
+    uint64_t match;           /* remote.match (remote.go:62-69) */
+    uint32_t role;            /* HQ_ROLE_* */
+    uint32_t active;          /* remote.active (CheckQuorum) */
+} hq_member;
+
+typedef struct hq_group_view {
+    uint64_t node_id;         /* this node: the leader (commit, ReadIndex) or candidate (vote) */
+    uint64_t committed;       /* log.committed */
+    uint64_t last_index;      /* log.lastIndex() */
+    uint64_t term_start;      /* first index of the leader's term (term-start form) */
+    uint64_t term;            /* r.term (ring form) */
+    uint64_t ctx_low;         /* the pending ReadIndex SystemCtx (single-ctx form) */
+    uint64_t ctx_high;
+    uint16_t term_mask;       /* term-mask form */
+    uint16_t reserved0;
+    uint32_t reserved1;
+    uint32_t first_member;    /* this group's members: members[first_member .. +n_members) */
+    uint32_t n_members;
+    uint32_t first_msg;       /* this group's step messages: msgs[first_msg .. +n_msgs) */
+    uint32_t n_msgs;
+} hq_group_view;
+
+/* A response received in this step, in arrival order. RequestVoteResp: reject = m.Reject.
+ * HeartbeatResp: hint_low / hint_high = m.Hint / m.HintHigh (the echoed SystemCtx). */
+typedef struct hq_msg {
+    uint64_t from;
+    uint64_t hint_low;
+    uint64_t hint_high;
+    uint32_t reject;
+    uint32_t reserved;
+} hq_msg;
+
+/* Commit inputs: match rows (n_max rows at args->match_stride), n_voting, committed_in,
+ * last_index and, when non-NULL, term_start / term / term_mask of *args (host arrays).
+ * args->G must equal G; args->fallback (may be NULL) receives the packing fallbacks. */
+int hq_pack_commit(const hq_group_view *groups, uint64_t G, const hq_member *members,
+                   hq_commit_args *args);
+
+/* Vote bitmaps: slot 0 granted (campaign's self vote, raft.go:1093); then every message from a
+ * voting member sets its slot's granted or rejected bit if neither is set yet (first response
+ * wins, raft.go:1071-1073); responses from observers (raft.go:1969-1972) and non-members
+ * (Peer.Handle, peer.go:191-197) are dropped. */
+int hq_pack_votes(const hq_group_view *groups, uint64_t G, const hq_member *members,
+                  const hq_msg *msgs, uint8_t *granted, uint8_t *rejected, uint8_t *n_voting,
+                  uint64_t *fallback);
+
+/* ReadIndex ack bitmaps for the group's pending ctx: a HeartbeatResp from a voting member whose
+ * hint equals (ctx_low, ctx_high) sets that member's slot (readindex.go:83; heartbeats carrying
+ * a ctx go to voting members only, raft.go:836-848). Other hints, non-members and observers are
+ * ignored. Also fills `active` from the members' active flags when non-NULL. */
+int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *members,
+                 const hq_msg *msgs, uint8_t *ack, uint8_t *active, uint8_t *n_voting,
+                 uint32_t n_max, uint64_t *fallback);
+
 /* ---------------------------------------------------------------- synthetic inputs ---------- */
 
 /*

@@ -49,6 +49,17 @@ int main(void) {
   F(hq_synth_spec, seed) F(hq_synth_spec, G) F(hq_synth_spec, cid_base)
   F(hq_synth_spec, cid_stride) F(hq_synth_spec, n_max) F(hq_synth_spec, mixed_n)
   F(hq_synth_spec, ring_len) F(hq_synth_spec, parity_extras)
+  printf("hq_member %zu\n", sizeof(hq_member));
+  printf("hq_group_view %zu\n", sizeof(hq_group_view));
+  printf("hq_msg %zu\n", sizeof(hq_msg));
+  printf("hq_match_update %zu\n", sizeof(hq_match_update));
+  printf("hq_append_update %zu\n", sizeof(hq_append_update));
+  F(hq_member, node_id) F(hq_member, match) F(hq_member, role) F(hq_member, active)
+  F(hq_group_view, node_id) F(hq_group_view, committed) F(hq_group_view, last_index)
+  F(hq_group_view, term_start) F(hq_group_view, term) F(hq_group_view, ctx_low)
+  F(hq_group_view, ctx_high) F(hq_group_view, term_mask) F(hq_group_view, first_member)
+  F(hq_group_view, n_members) F(hq_group_view, first_msg) F(hq_group_view, n_msgs)
+  F(hq_msg, from) F(hq_msg, hint_low) F(hq_msg, hint_high) F(hq_msg, reject)
   return 0;
 }
 """
@@ -64,9 +75,17 @@ def test_struct_layout_matches_c(hq, tmp_path):
     c = dict(l.rsplit(" ", 1) for l in lines if l)
     assert int(c["hq_commit_args"]) == ctypes.sizeof(hq.CommitArgs)
     assert int(c["hq_synth_spec"]) == ctypes.sizeof(hq.SynthSpec)
+    dtypes = {"hq_member": hq.MEMBER_DTYPE, "hq_group_view": hq.GROUP_DTYPE,
+              "hq_msg": hq.MSG_DTYPE}
+    for name, dt in dtypes.items():
+        assert int(c[name]) == dt.itemsize, name
+    assert int(c["hq_match_update"]) == 16 and int(c["hq_append_update"]) == 16
     for key, val in c.items():
         if "." in key:
             t, m = key.split(".")
+            if t in dtypes:
+                assert dtypes[t].fields[m][1] == int(val), key
+                continue
             cls = hq.CommitArgs if t == "hq_commit_args" else hq.SynthSpec
             assert getattr(cls, m).offset == int(val), key
 
