@@ -22,6 +22,8 @@ struct hq_ctx {
     uint64_t region_launches = 0;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
+    // launch geometry of the bitmap kernels (256; HQ_BITS_BLOCK=512|1024 at hq_open)
+    int bits_block = 256;
     // device workspace for the host-pointer entry points
     void *ws = nullptr;
     size_t ws_bytes = 0;

@@ -300,10 +300,10 @@ __device__ __forceinline__ uint32_t mask_n(uint32_t n) {
     return __builtin_amdgcn_perm(0x7F3F1F0Fu, 0x07030100u, sel);
 }
 
-template <int MODE, bool PERN>
-__global__ __launch_bounds__(kBlock) void k_bits(const BitsK a) {
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t step = (uint64_t)gridDim.x * kBlock * 16;
+template <int MODE, bool PERN, int BLK>
+__global__ __launch_bounds__(BLK) void k_bits(const BitsK a) {
+    const uint64_t tid = (uint64_t)blockIdx.x * BLK + threadIdx.x;
+    const uint64_t step = (uint64_t)gridDim.x * BLK * 16;
     const uint32_t nu = a.n_uniform * kB01;  // n_uniform <= 8: no byte overflow
     for (uint64_t g = tid * 16; g < a.n16o * 16 || g < a.n16 * 16; g += step) {
         const uint64_t slot = g >> 4;
@@ -620,13 +620,21 @@ int launch_bits(hq_ctx *ctx, BitsK &k, const char *what) {
     k.n16 = hq::words64(k.G) * 4;
     k.n16o = (MODE & kVOTE) ? hq::words32(k.G) * 2 : 0;
     const uint64_t slots = k.n16 > k.n16o ? k.n16 : k.n16o;
-    const unsigned grid = grid_for(slots);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    if (k.nv)
-        hipLaunchKernelGGL((k_bits<MODE, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
-    else
-        hipLaunchKernelGGL((k_bits<MODE, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+    // block size: ctx->bits_block (256 default; HQ_BITS_BLOCK at hq_open, a tuning knob)
+#define HQ_BITS_LAUNCH(B)                                                                      \
+    {                                                                                          \
+        const unsigned grid = grid_for(slots, B, (uint64_t)kMaxBlocks * 256 / B);              \
+        if (k.nv)                                                                              \
+            hipLaunchKernelGGL((k_bits<MODE, true, B>), dim3(grid), dim3(B), 0, ctx->stream, k); \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_bits<MODE, false, B>), dim3(grid), dim3(B), 0, ctx->stream, k); \
+    }
+    if (ctx->bits_block == 512) HQ_BITS_LAUNCH(512)
+    else if (ctx->bits_block == 1024) HQ_BITS_LAUNCH(1024)
+    else HQ_BITS_LAUNCH(256)
+#undef HQ_BITS_LAUNCH
     return hq::post_launch(ctx, what);
 }
 

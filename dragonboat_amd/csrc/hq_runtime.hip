@@ -1,5 +1,6 @@
 // hq_runtime.hip — contexts, memory, timing and the host-pointer entry points of
 // libhipquorum.so. Kernels and their _dev launchers live in hq_kernels.hip.
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -75,6 +76,10 @@ int hq_open(int device, uint32_t flags, hq_ctx **out) {
     hq_ctx *ctx = new (std::nothrow) hq_ctx();
     if (!ctx) return hq::fail(nullptr, HQ_E_NOMEM, "hq_open: out of host memory");
     ctx->device = device;
+    if (const char *b = std::getenv("HQ_BITS_BLOCK")) {
+        const int v = std::atoi(b);
+        if (v == 256 || v == 512 || v == 1024) ctx->bits_block = v;
+    }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
