@@ -323,12 +323,20 @@ def cpu_baseline(w, budget_s=8.0):
                 break
         out[nt] = (passes * G * decisions_per_group(w) / dt, passes, dt)
     rate, passes, dt = out[host_threads]
+    # BASELINE config C1: the reference's own CPU case, one group x 3 voters, tryCommit per step
+    T = 4 << 20
+    match, last = qref.c1_stream(SEED_BASE, T, 1000, 1005)
+    t0 = time.perf_counter()
+    qref.c1_run(match, last, 1003, 1000)
+    c1_s = time.perf_counter() - t0
     return {
         "value": rate, "unit": "decisions/s", "cores": host_threads, "kind": "port",
         "sample": (f"{G} groups of the same workload and generator, {passes} passes in {dt:.1f} s "
                    f"on {host_threads} host threads (oracle/qref.c -O3, C restatement of the "
                    f"reference Go path; Go toolchain unavailable)"),
         "single_thread_value": out[1][0],
+        "c1_single_group_ns_per_trycommit": c1_s / T * 1e9,
+        "c1_sample": f"BASELINE config C1: 1 group x 3 voters, {T} sequential tryCommit steps",
     }
 
 

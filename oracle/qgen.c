@@ -80,6 +80,26 @@ int qgen_commit(const qgen_spec *s, const qref_commit_args *o) {
     return 0;
 }
 
+int qgen_c1_stream(uint64_t seed, uint64_t T, uint64_t committed0, uint64_t last0,
+                   uint64_t *match, uint64_t *last) {
+    uint64_t st = seed ^ 1;   /* clusterID 1 */
+    uint64_t m[3] = {last0, committed0, committed0};
+    uint64_t l = last0;
+    for (uint64_t t = 0; t < T; t++) {
+        uint64_t x = qgen_splitmix64(&st);
+        if (t % 8 == 7) {                          /* leader appends 1..4 entries */
+            l += 1 + (x >> 8) % 4;
+            m[0] = l;
+        }
+        int slot = 1 + (int)(x & 1);               /* one follower's ReplicateResp */
+        uint64_t nm = m[slot] + (x >> 1) % 4;
+        m[slot] = nm > l ? l : nm;
+        for (int s = 0; s < 3; s++) match[(uint64_t)s * T + t] = m[s];
+        last[t] = l;
+    }
+    return 0;
+}
+
 /* 16-bit Bernoulli draws carved from successive splitmix64 outputs */
 typedef struct { uint64_t st, buf; int avail; } bern_t;
 static int bern(bern_t *b, uint32_t thr16) {

@@ -584,6 +584,27 @@ int qref_readindex_multi_batch(uint64_t G, uint32_t K_max, uint32_t n_max,
     return 0;
 }
 
+/* ================================================================ config C1 stream ========= */
+
+int qref_c1_run(uint64_t T, const uint64_t *match, const uint64_t *last, uint64_t term_start,
+                uint64_t committed0, uint64_t *committed) {
+    tstart_ud tud = {term_start};
+    qref_log log;
+    log.first_minus_1 = committed0;
+    log.committed = committed0;
+    log.term_at = tstart_term_at;
+    log.ud = &tud;
+    uint64_t m[3];
+    for (uint64_t t = 0; t < T; t++) {
+        log.last = last[t];
+        for (int s = 0; s < 3; s++) m[s] = match[(uint64_t)s * T + t];
+        /* handleLeaderReplicateResp -> tryCommit once per message (raft.go:1678) */
+        if (qref_try_commit(m, 3, NULL, 0, &log, 2, NULL) == QREF_PANIC) return QREF_PANIC;
+        committed[t] = log.committed;
+    }
+    return 0;
+}
+
 /* ================================================================ delta ingest ============= */
 
 /* remote.tryUpdate — remote.go:123-133: if r.match < index { r.match = index } */

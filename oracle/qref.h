@@ -201,6 +201,17 @@ int qgen_commit(const qgen_spec *s, const qref_commit_args *out);
 int qgen_bitmaps(const qgen_spec *s, uint8_t *ack, uint8_t *granted, uint8_t *rejected,
                  uint8_t *n_voting);
 
+/* BASELINE config C1: one group x 3 voters, a stream of T ReplicateResp steps.
+ * qgen_c1_stream fills match (slot-major [3][T], the group's match vector after each step) and
+ * last (lastIndex after each step): each step raises one follower's match by 0..3 (clamped to
+ * last); every 8th step the leader appends 1..4 entries (its own match follows, raft.go:918).
+ * qref_c1_run replays the stream through raft.tryCommit one step at a time (term-start log
+ * view: entries >= term_start carry the leader's term) and writes committed after each step. */
+int qgen_c1_stream(uint64_t seed, uint64_t T, uint64_t committed0, uint64_t last0,
+                   uint64_t *match, uint64_t *last);
+int qref_c1_run(uint64_t T, const uint64_t *match, const uint64_t *last, uint64_t term_start,
+                uint64_t committed0, uint64_t *committed);
+
 /* FNV-1a 64 over a byte range (fixture checksums). */
 uint64_t qref_fnv1a64(const void *p, size_t bytes);
 

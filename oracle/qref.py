@@ -111,6 +111,8 @@ def load() -> ctypes.CDLL:
         "qref_readindex_multi_batch": (ctypes.c_int, [_u64, ctypes.c_uint32, ctypes.c_uint32, _vp,
                                                       _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                                       _vp, ctypes.c_int]),
+        "qgen_c1_stream": (ctypes.c_int, [_u64, _u64, _u64, _u64, _vp, _vp]),
+        "qref_c1_run": (ctypes.c_int, [_u64, _vp, _vp, _u64, _u64, _vp]),
         "qref_ingest_match": (_u64, [_vp, _u64, _vp, _u64, _u64, ctypes.c_uint32]),
         "qref_ingest_ack": (_u64, [_vp, _u64, _vp, _u64, ctypes.c_uint32]),
         "qref_append": (_u64, [_vp, _u64, _vp, _vp, _vp, ctypes.c_uint32, _u64]),
@@ -339,6 +341,22 @@ def readindex_multi_batch(ack_ordinal, ctx_index, n_pending, n_voting, n_uniform
                                         _ptr(cnt), _ptr(fb), nthreads)
     assert rc == 0, rc
     return rel, cnt, fb
+
+
+def c1_stream(seed: int, T: int, committed0: int, last0: int):
+    """BASELINE config C1 stream: (match [3*T] slot-major, last [T])."""
+    match = np.zeros(3 * T, np.uint64)
+    last = np.zeros(T, np.uint64)
+    assert lib.qgen_c1_stream(seed, T, committed0, last0, _ptr(match), _ptr(last)) == 0
+    return match, last
+
+
+def c1_run(match, last, term_start: int, committed0: int) -> np.ndarray:
+    """Sequential raft.tryCommit over the C1 stream: committed after every step."""
+    T = len(last)
+    out = np.zeros(T, np.uint64)
+    assert lib.qref_c1_run(T, _ptr(match), _ptr(last), term_start, committed0, _ptr(out)) == 0
+    return out
 
 
 def ingest_match(updates: np.ndarray, match: np.ndarray, stride: int, G: int, n_max: int) -> int:
