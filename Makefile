@@ -5,7 +5,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH)
 CSRC := dragonboat_amd/csrc
 LIBDIR := dragonboat_amd/lib
 LIB := $(LIBDIR)/libhipquorum.so
-OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o $(LIBDIR)/hq_pack.o
+OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o $(LIBDIR)/hq_pack.o $(LIBDIR)/hq_worker.o
 DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
 CXX ?= g++
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra

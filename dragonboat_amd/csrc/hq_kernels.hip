@@ -752,6 +752,7 @@ struct RiMultiK {
     const uint8_t *np, *nv;
     uint64_t *rel;
     uint8_t *cnt;
+    uint8_t *bend;
     uint64_t *fallback;
 };
 
@@ -804,20 +805,27 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi(const RiMultiK a) {
                 }
             }
             // suffix-min scan: entry i goes with the first ctx k >= i to reach quorum
+            // (ties at equal reach times go to the earlier ctx: the replay's queue order)
             uint32_t best_t = 0xFFFFu;
             uint64_t best_idx = 0;
-            uint32_t released = 0;
+            uint32_t released = 0, bend = 0;
 #pragma unroll
             for (int k = 7; k >= 0; --k) {
+                bool own = false;
                 if (!fb && k < (int)K && t[k] != 0xFFFFu && t[k] <= best_t) {
                     best_t = t[k];
                     best_idx = idx[k];
+                    own = true;
                 }
                 const bool rel = !fb && k < (int)K && best_t != 0xFFFFu;
                 released += rel;
+                // entry k closes its release batch: it is the ctx whose confirm() released
+                // the batch (readindex.go:96), whose ctx the ReadIndexResp hints carry
+                bend |= (uint32_t)(rel && own) << k;
                 if (k < (int)a.K_max) a.rel[(uint64_t)k * a.G + g] = rel ? best_idx : ~0ull;
             }
             a.cnt[g] = (uint8_t)released;
+            if (a.bend) a.bend[g] = (uint8_t)bend;
         }
         const uint64_t fw = __ballot(fb);
         if (a.fallback && lane == 0) a.fallback[wbase >> 6] = fw;
@@ -830,14 +838,15 @@ extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, u
                                       const uint16_t *ack_ordinal, const uint64_t *ctx_index,
                                       const uint8_t *n_pending, const uint8_t *n_voting,
                                       uint32_t n_uniform, uint64_t *released_index,
-                                      uint8_t *released_count, uint64_t *fallback) {
+                                      uint8_t *released_count, uint8_t *batch_end,
+                                      uint64_t *fallback) {
     if (!ctx) return HQ_E_INVAL;
     if (G == 0) return HQ_OK;
     if (!ack_ordinal || !ctx_index || !released_index || !released_count || K_max < 1 ||
         K_max > 8 || n_max < 1 || n_max > 8 || (!n_voting && (n_uniform < 1 || n_uniform > 8)))
         return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_dev: bad arguments");
     RiMultiK k{G, K_max, n_max, n_uniform, ack_ordinal, ctx_index, n_pending, n_voting,
-               released_index, released_count, fallback};
+               released_index, released_count, batch_end, fallback};
     const unsigned grid = grid_for(G);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;

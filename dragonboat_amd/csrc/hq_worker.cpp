@@ -1,0 +1,779 @@
+// hq_worker.cpp — the step worker of libhipquorum.so (include/hipquorum.h "step worker"): the
+// caller side of the quorum kernels, in the shape of dragonboat's execEngine.processSteps
+// (execengine.go:923-1000) driving node.handleEvents (node.go:1113-1157) for many groups.
+//
+// Host work per event is the reference's bookkeeping only — Peer.Handle's membership filter
+// (peer.go:186-198), onMessageTermNotMatched (raft.go:1416-1452), remote.tryUpdate
+// (remote.go:123-133), the ReadIndex confirmed-set insert (readindex.go:83) and the first-wins
+// vote insert (raft.go:1071-1073). Every quorum decision is a kernel launch through the C-ABI:
+// tryCommit (hq_commit_dev, term-start form), the ReadIndex release with its index rewrite
+// (hq_readindex_multi_dev), the vote outcome (hq_vote_dev) and leaderHasQuorum
+// (hq_check_quorum_dev). A group's events are taken in order until one needs a decision not
+// yet taken (a "run"); all runs of a pass are decided in one GPU batch, applied, and the next
+// pass continues where they stopped. Plain C++ (no HIP headers): the worker is a client of the
+// same ABI a cgo binding would use.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/hipquorum.h"
+
+namespace {
+
+constexpr uint32_t kMaxReads = 8;        // pending ReadIndex ctxs per group (k_ri_multi K_max)
+constexpr uint16_t kNoAck = 0xFFFF;
+constexpr uint16_t kMaxOrdinal = 0xFFF0;  // acks per run before a run is cut
+
+struct ReadStatus {                      // readStatus (readindex.go:21-26)
+    uint64_t index, from, low, high;
+    uint8_t confirmed;                   // slots confirmed in earlier runs (ordinal 0)
+    uint16_t ord[HQ_MAX_VOTERS];         // first-ack ordinal in the current run
+};
+
+struct Group {
+    uint64_t cluster_id = 0, node_id = 0, term = 0;
+    uint64_t committed = 0, last = 0, term_start = 0;
+    uint32_t state = HQ_STATE_FOLLOWER;
+    std::vector<hq_member> members;      // in the caller's order
+    std::vector<int8_t> slot_of;         // member -> voting slot, -1 for observers
+    int self = -1;                       // member index of this node
+    int n_voting = 0;
+    std::vector<ReadStatus> reads;       // readIndex.queue with its pending statuses
+    uint8_t granted = 0, rejected = 0;   // votes over voting slots
+    bool suspended = false;
+    // current step
+    uint64_t committed0 = 0;
+    bool touched = false;
+    size_t ev_begin = 0, ev_end = 0, cursor = 0;
+    // current run
+    bool commit_due = false, ri_due = false, vote_due = false, cq_due = false;
+    uint16_t ord = 0;
+    bool in_work = false;
+    bool pending() const { return commit_due || ri_due || vote_due || cq_due; }
+};
+
+enum Verdict { CONSUMED, BARRIER, FALLBACK };
+
+struct Event {
+    uint32_t array;                      // HQ_EVT_*
+    uint32_t group;
+    uint64_t index;
+};
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct hq_worker {
+    hq_ctx *ctx = nullptr;
+    uint32_t n_max = 0;
+    std::string err;
+    std::vector<Group> groups;
+    std::unordered_map<uint64_t, uint32_t> index;   // cluster_id -> group
+    // step scratch
+    const hq_step_input *in = nullptr;
+    std::vector<Event> events;
+    std::vector<uint32_t> counts;
+    std::vector<uint32_t> work, next_work, touched;
+    std::vector<uint32_t> l_commit, l_ri, l_vote, l_cq;
+    // outputs
+    std::vector<hq_commit_event> commits;
+    std::vector<hq_ready_to_read> ready;
+    std::vector<hq_read_index_resp> resps;
+    std::vector<hq_state_change> states;
+    std::vector<hq_dropped_read> dropped;
+    std::vector<hq_event_ref> deferred;
+    std::vector<uint64_t> fallback;
+    uint64_t decisions = 0;
+    // staging: one pinned host buffer mirrored by one device buffer per pass
+    void *host = nullptr, *dev = nullptr;
+    size_t cap = 0;
+
+    int fail(int code, const std::string &m) {
+        err = m;
+        return code;
+    }
+    int hq(int rc, const char *what) {
+        if (rc) err = std::string(what) + ": " + hq_last_error(ctx);
+        return rc;
+    }
+    int reserve(size_t bytes);
+    int load_group(Group &g, const hq_worker_group *src, const hq_member *m);
+    int step(const hq_step_input *in, hq_step_output *out);
+    Verdict handle(Group &g, uint32_t gi, const Event &e);
+    Verdict read_index(Group &g, uint64_t from, uint64_t low, uint64_t high, const Event &e);
+    void advance(Group &g, uint32_t gi);
+    int run_pass();
+    // reference state transitions (host bookkeeping of raft.go:949-1010)
+    void reset(Group &g, uint64_t term);
+    void become_follower(Group &g, uint64_t term, uint32_t reason);
+    void become_leader(Group &g);
+    void push_state(const Group &g, uint32_t reason) {
+        states.push_back({g.cluster_id, g.term, g.state, reason});
+    }
+    void defer(const Event &e) { deferred.push_back({e.array, 0, e.index}); }
+    int member_of(const Group &g, uint64_t id) const {
+        for (size_t i = 0; i < g.members.size(); ++i)
+            if (g.members[i].node_id == id) return (int)i;
+        return -1;
+    }
+};
+
+// ------------------------------------------------------------------------------ state ------
+int hq_worker::load_group(Group &g, const hq_worker_group *src, const hq_member *m) {
+    if (src->n_members < 1 || !m) return fail(HQ_E_INVAL, "group has no members");
+    if (src->state > HQ_STATE_LEADER) return fail(HQ_E_INVAL, "state must be follower, candidate or leader");
+    Group n;
+    n.cluster_id = src->cluster_id;
+    n.node_id = src->node_id;
+    n.term = src->term;
+    n.committed = src->committed;
+    n.last = src->last_index;
+    n.term_start = src->term_start;
+    n.state = src->state;
+    n.members.assign(m, m + src->n_members);
+    n.slot_of.assign(src->n_members, -1);
+    for (uint32_t i = 0; i < src->n_members; ++i) {
+        if (m[i].role > HQ_ROLE_WITNESS) return fail(HQ_E_INVAL, "unknown member role");
+        for (uint32_t j = 0; j < i; ++j)
+            if (m[j].node_id == m[i].node_id) return fail(HQ_E_INVAL, "duplicate member");
+        if (m[i].role == HQ_ROLE_REMOTE && m[i].node_id == src->node_id) n.self = (int)i;
+    }
+    if (n.self < 0) return fail(HQ_E_INVAL, "the node is not one of the group's remotes");
+    // voting slots: the node itself, the other remotes, then the witnesses (hq_pack_commit)
+    n.slot_of[n.self] = (int8_t)n.n_voting++;
+    for (uint32_t role : {HQ_ROLE_REMOTE, HQ_ROLE_WITNESS})
+        for (uint32_t i = 0; i < src->n_members; ++i)
+            if (m[i].role == role && (int)i != n.self) {
+                if (n.n_voting >= (int)n_max) return fail(HQ_E_INVAL, "more voting members than n_max");
+                n.slot_of[i] = (int8_t)n.n_voting++;
+            }
+    // a candidate holds its own vote (campaign, raft.go:1093)
+    if (n.state == HQ_STATE_CANDIDATE) n.granted = 1;
+    g = std::move(n);
+    return HQ_OK;
+}
+
+void hq_worker::reset(Group &g, uint64_t term) {   // raft.reset, raft.go:991-1010
+    g.term = term;
+    g.granted = g.rejected = 0;
+    g.reads.clear();
+    for (auto &m : g.members) {                     // resetRemotes/Observers/Witnesses
+        m.match = m.node_id == g.node_id ? g.last : 0;
+        m.active = 0;
+    }
+}
+
+void hq_worker::become_follower(Group &g, uint64_t term, uint32_t reason) {
+    g.state = HQ_STATE_FOLLOWER;                    // raft.go:949-957
+    reset(g, term);
+    push_state(g, reason);
+}
+
+void hq_worker::become_leader(Group &g) {
+    g.state = HQ_STATE_LEADER;                      // raft.go:977-989
+    reset(g, g.term);
+    push_state(g, HQ_REASON_VOTE);
+    // the no-op of p72: first entry of the new term; the node's own remote follows the log
+    g.term_start = g.last + 1;
+    g.last += 1;
+    g.members[g.self].match = g.last;
+    if (g.n_voting == 1) g.commit_due = true;       // appendEntries: single-node tryCommit
+}
+
+// ------------------------------------------------------------------------------ events -----
+Verdict hq_worker::read_index(Group &g, uint64_t from, uint64_t low, uint64_t high,
+                              const Event &e) {
+    if (g.state != HQ_STATE_LEADER) {
+        if (g.vote_due) return BARRIER;             // the vote may have made it leader
+        defer(e);                                   // forwarded / dropped (raft.go:1875, 1937)
+        return CONSUMED;
+    }
+    // handleLeaderReadIndex (raft.go:1636-1669)
+    const int fm = member_of(g, from);
+    if (fm >= 0 && g.members[fm].role == HQ_ROLE_WITNESS) {
+        dropped.push_back({g.cluster_id, low, high, from, HQ_DROP_WITNESS, 0});
+        return CONSUMED;
+    }
+    if (g.commit_due) return BARRIER;               // needs the committed index
+    if (g.n_voting == 1) {                          // isSingleNodeQuorum: quorum() == 1
+        ready.push_back({g.cluster_id, g.committed, low, high});
+        if (from != g.node_id && fm >= 0 && g.members[fm].role == HQ_ROLE_OBSERVER)
+            resps.push_back({g.cluster_id, from, g.committed, low, high});
+        return CONSUMED;
+    }
+    // hasCommittedEntryAtCurrentTerm (raft.go:1612-1621): term(committed) == r.term
+    if (!(g.committed >= g.term_start && g.committed <= g.last)) {
+        dropped.push_back({g.cluster_id, low, high, from, HQ_DROP_NOT_READY, 0});
+        return CONSUMED;
+    }
+    // readIndex.addRequest (readindex.go:43-67)
+    for (const auto &r : g.reads)
+        if (r.low == low && r.high == high) return g.ri_due ? BARRIER : CONSUMED;
+    if (!g.reads.empty() && g.committed < g.reads.back().index) return FALLBACK;
+    if (g.reads.size() >= kMaxReads) return g.ri_due ? BARRIER : FALLBACK;
+    ReadStatus s;
+    s.index = g.committed;
+    s.from = from;
+    s.low = low;
+    s.high = high;
+    s.confirmed = 0;
+    std::fill(std::begin(s.ord), std::end(s.ord), kNoAck);
+    g.reads.push_back(s);
+    return CONSUMED;
+}
+
+static bool is_response_type(uint32_t t) {   // isResponseMessageType (internal/raft/utils.go)
+    return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
+           t == HQ_MSG_HEARTBEAT_RESP || t == 20 /* ReadIndexResp */ ||
+           t == 8 /* SnapshotStatus */ || t == 9 /* Unreachable */;
+}
+
+Verdict hq_worker::handle(Group &g, uint32_t gi, const Event &e) {
+    (void)gi;
+    switch (e.array) {
+    case HQ_EVT_READ: {
+        const hq_read_request &r = in->reads[e.index];
+        return read_index(g, 0, r.ctx_low, r.ctx_high, e);
+    }
+    case HQ_EVT_TICK: {
+        const hq_tick &t = in->ticks[e.index];
+        if (t.kind == HQ_TICK_CHECK_QUORUM) {
+            if (g.state != HQ_STATE_LEADER) return g.vote_due ? BARRIER : CONSUMED;
+            if (g.cq_due) return BARRIER;
+            g.cq_due = true;
+            return CONSUMED;
+        }
+        if (t.kind == HQ_TICK_ELECTION) {
+            if (g.pending()) return BARRIER;
+            if (g.state == HQ_STATE_LEADER) return CONSUMED;   // leader ignores Election
+            // campaign: becomeCandidate + the self vote (raft.go:959-975, 1082-1095)
+            g.state = HQ_STATE_CANDIDATE;
+            reset(g, g.term + 1);
+            push_state(g, HQ_REASON_CAMPAIGN);
+            g.granted = 1;
+            g.vote_due = true;                      // isSingleNodeQuorum -> the vote kernel
+            return CONSUMED;
+        }
+        return FALLBACK;
+    }
+    case HQ_EVT_PROPOSAL: {
+        const hq_proposal &p = in->proposals[e.index];
+        if (g.pending() && (g.state != HQ_STATE_LEADER || g.cq_due)) return BARRIER;
+        if (g.state != HQ_STATE_LEADER) {
+            defer(e);                               // forwarded / dropped (raft.go:1845, 1932)
+            return CONSUMED;
+        }
+        // appendEntries (raft.go:911-922)
+        g.last += p.n_entries;
+        if (g.members[g.self].match < g.last) g.members[g.self].match = g.last;
+        if (g.n_voting == 1) g.commit_due = true;
+        return CONSUMED;
+    }
+    case HQ_EVT_MSG:
+        break;
+    default:
+        return FALLBACK;
+    }
+    const hq_message &m = in->msgs[e.index];
+    if (m.type != HQ_MSG_REPLICATE_RESP && m.type != HQ_MSG_HEARTBEAT_RESP &&
+        m.type != HQ_MSG_REQUEST_VOTE_RESP && m.type != HQ_MSG_READ_INDEX)
+        return FALLBACK;
+    const int mi = member_of(g, m.from);
+    if (is_response_type(m.type) && mi < 0) return CONSUMED;     // Peer.Handle drop
+    if (m.term != 0 && m.term != g.term) {                      // onMessageTermNotMatched
+        if (m.term < g.term) return CONSUMED;
+        if (g.pending()) return BARRIER;            // decisions of the run come first
+        become_follower(g, m.term, HQ_REASON_HIGHER_TERM);
+    }
+    if (g.state == HQ_STATE_LEADER) {
+        switch (m.type) {
+        case HQ_MSG_REPLICATE_RESP: {               // handleLeaderReplicateResp (:1671-1700)
+            hq_member &rp = g.members[mi];
+            if (!m.reject && rp.match < m.log_index) {
+                if (m.log_index > g.last) return FALLBACK;  // a follower can only ack what it got
+                rp.match = m.log_index;             // remote.tryUpdate
+                g.commit_due = true;                // -> tryCommit
+            }
+            rp.active = 1;
+            return CONSUMED;
+        }
+        case HQ_MSG_HEARTBEAT_RESP: {               // handleLeaderHeartbeatResp (:1702-1714)
+            if (m.hint != 0) {                      // handleReadIndexLeaderConfirmation
+                for (auto &r : g.reads) {
+                    if (r.low != m.hint || r.high != m.hint_high) continue;
+                    const int s = g.slot_of[mi];
+                    if (s < 0) return FALLBACK;     // an observer acking a ctx
+                    if (g.ord >= kMaxOrdinal) return BARRIER;
+                    if (!((r.confirmed >> s) & 1) && r.ord[s] == kNoAck) {
+                        r.ord[s] = ++g.ord;         // p.confirmed[from] = struct{}{}
+                        g.ri_due = true;
+                    }
+                    break;
+                }
+            }
+            g.members[mi].active = 1;
+            return CONSUMED;
+        }
+        case HQ_MSG_READ_INDEX:
+            return read_index(g, m.from, m.hint, m.hint_high, e);
+        default:
+            return CONSUMED;                        // RequestVoteResp: no leader handler
+        }
+    }
+    if (g.state == HQ_STATE_CANDIDATE) {
+        if (m.type == HQ_MSG_REQUEST_VOTE_RESP) {   // handleCandidateRequestVoteResp
+            const int s = g.slot_of[mi];
+            if (s < 0) return CONSUMED;             // observer vote dropped (:1969-1972)
+            if (!(((g.granted | g.rejected) >> s) & 1)) {   // first response wins
+                if (m.reject) g.rejected |= (uint8_t)(1u << s);
+                else g.granted |= (uint8_t)(1u << s);
+            }
+            g.vote_due = true;
+            return CONSUMED;
+        }
+        if (g.vote_due) return BARRIER;             // may be leader by now
+    }
+    if (m.type == HQ_MSG_READ_INDEX) return read_index(g, m.from, m.hint, m.hint_high, e);
+    return CONSUMED;                                // no handler in this state
+}
+
+void hq_worker::advance(Group &g, uint32_t gi) {
+    while (g.cursor < g.ev_end) {
+        const Event &e = events[g.cursor];
+        if (g.suspended) {
+            defer(e);
+            ++g.cursor;
+            continue;
+        }
+        const Verdict v = handle(g, gi, e);
+        if (v == BARRIER) return;
+        if (v == FALLBACK) {
+            g.suspended = true;
+            fallback.push_back(g.cluster_id);
+            continue;                               // this event and the rest are deferred
+        }
+        ++g.cursor;
+    }
+}
+
+// ------------------------------------------------------------------------------ GPU pass ---
+int hq_worker::reserve(size_t bytes) {
+    if (bytes <= cap) return HQ_OK;
+    size_t want = std::max(bytes, cap * 2);
+    want = std::max<size_t>(want, 1 << 20);
+    if (host) hq_free_pinned(ctx, host);
+    if (dev) hq_free_dev(ctx, dev);
+    host = dev = nullptr;
+    cap = 0;
+    int rc = hq(hq_alloc_pinned(ctx, want, &host), "hq_alloc_pinned");
+    if (!rc) rc = hq(hq_malloc_dev(ctx, want, &dev), "hq_malloc_dev");
+    if (rc) return rc;
+    cap = want;
+    return HQ_OK;
+}
+
+namespace {
+// Carves one staging region into aligned arrays; host and device share the offsets.
+struct Layout {
+    size_t off = 0;
+    size_t take(size_t bytes) {
+        const size_t o = off;
+        off = align_up(off + std::max<size_t>(bytes, 1), 256);
+        return o;
+    }
+};
+}  // namespace
+
+int hq_worker::run_pass() {
+    const uint64_t Gc = l_commit.size(), Gr = l_ri.size(), Gv = l_vote.size(), Gq = l_cq.size();
+    const uint32_t N = n_max;
+    uint32_t K = 1;
+    for (uint32_t gi : l_ri) K = std::max<uint32_t>(K, (uint32_t)groups[gi].reads.size());
+    const uint64_t sc = align_up(std::max<uint64_t>(Gc, 1), 2);   // even stride: 16-B loads
+    // inputs
+    Layout L;
+    const size_t c_match = L.take(8 * N * sc), c_nv = L.take(Gc), c_cin = L.take(8 * Gc),
+                 c_last = L.take(8 * Gc), c_ts = L.take(8 * Gc);
+    const size_t r_ord = L.take(2 * (size_t)K * N * Gr), r_idx = L.take(8 * (size_t)K * Gr),
+                 r_np = L.take(Gr), r_nv = L.take(Gr);
+    const size_t v_gr = L.take(Gv), v_rj = L.take(Gv), v_nv = L.take(Gv);
+    const size_t q_act = L.take(Gq), q_nv = L.take(Gq);
+    const size_t in_bytes = L.off;
+    // outputs
+    const size_t c_out = L.take(8 * Gc), c_chg = L.take(8 * ((Gc + 63) / 64)),
+                 c_fb = L.take(8 * ((Gc + 63) / 64));
+    const size_t r_rel = L.take(8 * (size_t)K * Gr), r_cnt = L.take(Gr), r_be = L.take(Gr),
+                 r_fb = L.take(8 * ((Gr + 63) / 64));
+    const size_t v_out = L.take(8 * ((Gv + 31) / 32)), v_fb = L.take(8 * ((Gv + 63) / 64));
+    const size_t q_hq = L.take(8 * ((Gq + 63) / 64)), q_fb = L.take(8 * ((Gq + 63) / 64));
+    const size_t total = L.off;
+    int rc = reserve(total);
+    if (rc) return rc;
+    auto H = [&](size_t o) { return static_cast<uint8_t *>(host) + o; };
+    auto D = [&](size_t o) { return static_cast<uint8_t *>(dev) + o; };
+
+    // pack (the SoA layout of DESIGN.md §2)
+    {
+        uint64_t *match = reinterpret_cast<uint64_t *>(H(c_match));
+        uint8_t *nv = H(c_nv);
+        uint64_t *cin = reinterpret_cast<uint64_t *>(H(c_cin));
+        uint64_t *last = reinterpret_cast<uint64_t *>(H(c_last));
+        uint64_t *ts = reinterpret_cast<uint64_t *>(H(c_ts));
+        for (uint64_t j = 0; j < Gc; ++j) {
+            const Group &g = groups[l_commit[j]];
+            for (uint32_t s = 0; s < N; ++s) match[s * sc + j] = 0;
+            for (size_t i = 0; i < g.members.size(); ++i)
+                if (g.slot_of[i] >= 0) match[(uint64_t)g.slot_of[i] * sc + j] = g.members[i].match;
+            nv[j] = (uint8_t)g.n_voting;
+            cin[j] = g.committed;
+            last[j] = g.last;
+            ts[j] = g.term_start;
+        }
+        uint16_t *ord = reinterpret_cast<uint16_t *>(H(r_ord));
+        uint64_t *idx = reinterpret_cast<uint64_t *>(H(r_idx));
+        uint8_t *np = H(r_np), *rnv = H(r_nv);
+        for (uint64_t j = 0; j < Gr; ++j) {
+            const Group &g = groups[l_ri[j]];
+            np[j] = (uint8_t)g.reads.size();
+            rnv[j] = (uint8_t)g.n_voting;
+            for (uint32_t k = 0; k < K; ++k) {
+                const ReadStatus *r = k < g.reads.size() ? &g.reads[k] : nullptr;
+                idx[(uint64_t)k * Gr + j] = r ? r->index : 0;
+                for (uint32_t s = 0; s < N; ++s)
+                    ord[((uint64_t)k * N + s) * Gr + j] =
+                        !r ? kNoAck : ((r->confirmed >> s) & 1) ? 0 : r->ord[s];
+            }
+        }
+        uint8_t *gr = H(v_gr), *rj = H(v_rj), *vnv = H(v_nv);
+        for (uint64_t j = 0; j < Gv; ++j) {
+            const Group &g = groups[l_vote[j]];
+            gr[j] = g.granted;
+            rj[j] = g.rejected;
+            vnv[j] = (uint8_t)g.n_voting;
+        }
+        uint8_t *act = H(q_act), *qnv = H(q_nv);
+        for (uint64_t j = 0; j < Gq; ++j) {
+            const Group &g = groups[l_cq[j]];
+            uint8_t a = 0;
+            for (size_t i = 0; i < g.members.size(); ++i)
+                if (g.slot_of[i] >= 0 && g.members[i].active) a |= (uint8_t)(1u << g.slot_of[i]);
+            act[j] = a;
+            qnv[j] = (uint8_t)g.n_voting;
+        }
+    }
+
+    // one H2D, the decisions, one D2H, one sync
+    rc = hq(hq_memcpy_async(ctx, dev, host, in_bytes, 0), "hq_memcpy_async(H2D)");
+    if (!rc && Gc) {
+        hq_commit_args a{};
+        a.G = Gc;
+        a.n_max = N;
+        a.form = HQ_FORM_TERM_START;
+        a.match_stride = sc;
+        a.match = reinterpret_cast<const uint64_t *>(D(c_match));
+        a.n_voting = D(c_nv);
+        a.committed_in = reinterpret_cast<const uint64_t *>(D(c_cin));
+        a.committed_out = reinterpret_cast<uint64_t *>(D(c_out));
+        a.last_index = reinterpret_cast<const uint64_t *>(D(c_last));
+        a.term_start = reinterpret_cast<const uint64_t *>(D(c_ts));
+        a.changed = reinterpret_cast<uint64_t *>(D(c_chg));
+        a.fallback = reinterpret_cast<uint64_t *>(D(c_fb));
+        rc = hq(hq_commit_dev(ctx, &a), "hq_commit_dev");
+    }
+    if (!rc && Gr)
+        rc = hq(hq_readindex_multi_dev(ctx, Gr, K, N, reinterpret_cast<const uint16_t *>(D(r_ord)),
+                                       reinterpret_cast<const uint64_t *>(D(r_idx)), D(r_np),
+                                       D(r_nv), 0, reinterpret_cast<uint64_t *>(D(r_rel)),
+                                       D(r_cnt), D(r_be), reinterpret_cast<uint64_t *>(D(r_fb))),
+                "hq_readindex_multi_dev");
+    if (!rc && Gv)
+        rc = hq(hq_vote_dev(ctx, Gv, D(v_gr), D(v_rj), D(v_nv), 0,
+                            reinterpret_cast<uint64_t *>(D(v_out)),
+                            reinterpret_cast<uint64_t *>(D(v_fb))),
+                "hq_vote_dev");
+    if (!rc && Gq)
+        rc = hq(hq_check_quorum_dev(ctx, Gq, D(q_act), D(q_nv), 0, 0,
+                                    reinterpret_cast<uint64_t *>(D(q_hq)),
+                                    reinterpret_cast<uint64_t *>(D(q_fb))),
+                "hq_check_quorum_dev");
+    if (!rc) rc = hq(hq_memcpy_async(ctx, H(in_bytes), D(in_bytes), total - in_bytes, 1),
+                     "hq_memcpy_async(D2H)");
+    if (!rc) rc = hq(hq_sync(ctx), "hq_sync");
+    if (rc) return rc;
+    decisions += Gc + Gr + Gv + Gq;
+
+    auto bit = [](const uint8_t *words, uint64_t j) {
+        return (reinterpret_cast<const uint64_t *>(words)[j >> 6] >> (j & 63)) & 1;
+    };
+    // every group handed to a kernel satisfies its contract; a fallback bit is an internal error
+    for (uint64_t j = 0; j < Gc; ++j)
+        if (bit(H(c_fb), j)) return fail(HQ_E_STATE, "commit kernel refused a packed group");
+    for (uint64_t j = 0; j < Gr; ++j)
+        if (bit(H(r_fb), j)) return fail(HQ_E_STATE, "ReadIndex kernel refused a packed group");
+    for (uint64_t j = 0; j < Gv; ++j)
+        if (bit(H(v_fb), j)) return fail(HQ_E_STATE, "vote kernel refused a packed group");
+    for (uint64_t j = 0; j < Gq; ++j)
+        if (bit(H(q_fb), j)) return fail(HQ_E_STATE, "CheckQuorum kernel refused a packed group");
+
+    // apply, per group in the reference's order: commit, ReadIndex release, vote, CheckQuorum
+    const uint64_t *cout = reinterpret_cast<const uint64_t *>(H(c_out));
+    for (uint64_t j = 0; j < Gc; ++j) {
+        Group &g = groups[l_commit[j]];
+        g.committed = cout[j];                      // commitTo (logentry.go:323-332)
+        g.commit_due = false;
+    }
+    const uint64_t *rel = reinterpret_cast<const uint64_t *>(H(r_rel));
+    const uint8_t *cnt = H(r_cnt), *be = H(r_be);
+    for (uint64_t j = 0; j < Gr; ++j) {
+        Group &g = groups[l_ri[j]];
+        const uint32_t c = cnt[j];
+        for (uint32_t i = 0; i < c; ++i) {
+            uint32_t k = i;                         // the ctx whose confirm() released entry i
+            while (k < c && !((be[j] >> k) & 1)) ++k;
+            if (k >= c) return fail(HQ_E_STATE, "ReadIndex release without a closing ctx");
+            const ReadStatus &s = g.reads[i];
+            const uint64_t index = rel[(uint64_t)i * Gr + j];
+            if (s.from == 0 || s.from == g.node_id)
+                ready.push_back({g.cluster_id, index, s.low, s.high});
+            else
+                resps.push_back({g.cluster_id, s.from, index, g.reads[k].low, g.reads[k].high});
+        }
+        g.reads.erase(g.reads.begin(), g.reads.begin() + c);
+        for (auto &r : g.reads) {                   // carry the run's confirmations over
+            for (uint32_t s = 0; s < HQ_MAX_VOTERS; ++s) {
+                if (r.ord[s] != kNoAck) r.confirmed |= (uint8_t)(1u << s);
+                r.ord[s] = kNoAck;
+            }
+        }
+        g.ord = 0;
+        g.ri_due = false;
+    }
+    const uint64_t *outc = reinterpret_cast<const uint64_t *>(H(v_out));
+    for (uint64_t j = 0; j < Gv; ++j) {
+        Group &g = groups[l_vote[j]];
+        g.vote_due = false;
+        const uint32_t o = (uint32_t)((outc[j >> 5] >> (2 * (j & 31))) & 3);
+        if (o == HQ_OUTCOME_LEADER) become_leader(g);
+        else if (o == HQ_OUTCOME_FOLLOWER) become_follower(g, g.term, HQ_REASON_VOTE);
+    }
+    for (uint64_t j = 0; j < Gq; ++j) {
+        Group &g = groups[l_cq[j]];
+        g.cq_due = false;
+        for (size_t i = 0; i < g.members.size(); ++i)   // setNotActive (remote.go:196-198)
+            if (g.slot_of[i] >= 0) g.members[i].active = 0;
+        if (!bit(H(q_hq), j)) become_follower(g, g.term, HQ_REASON_CHECK_QUORUM);
+    }
+    return HQ_OK;
+}
+
+// ------------------------------------------------------------------------------ step -------
+int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
+    in = inp;
+    commits.clear();
+    ready.clear();
+    resps.clear();
+    states.clear();
+    dropped.clear();
+    deferred.clear();
+    fallback.clear();
+    decisions = 0;
+    uint64_t passes = 0;
+
+    // bucket the step's events by group, in node.handleEvents phase order
+    events.clear();
+    touched.clear();
+    auto add = [&](uint32_t array, uint64_t i, uint64_t cid) {
+        auto it = index.find(cid);
+        if (it == index.end()) {                    // not one of this worker's groups
+            deferred.push_back({array, 0, i});
+            return;
+        }
+        events.push_back({array, it->second, i});
+    };
+    for (uint64_t i = 0; i < in->n_reads; ++i) add(HQ_EVT_READ, i, in->reads[i].cluster_id);
+    for (uint64_t i = 0; i < in->n_msgs; ++i) add(HQ_EVT_MSG, i, in->msgs[i].cluster_id);
+    for (uint64_t i = 0; i < in->n_ticks; ++i) add(HQ_EVT_TICK, i, in->ticks[i].cluster_id);
+    for (uint64_t i = 0; i < in->n_proposals; ++i)
+        add(HQ_EVT_PROPOSAL, i, in->proposals[i].cluster_id);
+    // stable counting sort by group
+    counts.assign(groups.size() + 1, 0);
+    for (const Event &e : events) counts[e.group + 1]++;
+    for (size_t i = 0; i < groups.size(); ++i) counts[i + 1] += counts[i];
+    {
+        std::vector<Event> sorted(events.size());
+        std::vector<uint32_t> pos(counts.begin(), counts.end() - 1);
+        for (const Event &e : events) sorted[pos[e.group]++] = e;
+        events.swap(sorted);
+    }
+    work.clear();
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        if (counts[gi + 1] == counts[gi]) continue;
+        Group &g = groups[gi];
+        g.ev_begin = g.cursor = counts[gi];
+        g.ev_end = counts[gi + 1];
+        g.committed0 = g.committed;
+        g.touched = true;
+        touched.push_back((uint32_t)gi);
+        work.push_back((uint32_t)gi);
+    }
+
+    while (!work.empty()) {
+        l_commit.clear();
+        l_ri.clear();
+        l_vote.clear();
+        l_cq.clear();
+        for (uint32_t gi : work) {
+            Group &g = groups[gi];
+            g.in_work = false;
+            advance(g, gi);
+            if (g.commit_due) l_commit.push_back(gi);
+            if (g.ri_due) l_ri.push_back(gi);
+            if (g.vote_due) l_vote.push_back(gi);
+            if (g.cq_due) l_cq.push_back(gi);
+        }
+        if (l_commit.empty() && l_ri.empty() && l_vote.empty() && l_cq.empty()) break;
+        int rc = run_pass();
+        if (rc) return rc;
+        ++passes;
+        next_work.clear();
+        for (const auto *l : {&l_commit, &l_ri, &l_vote, &l_cq})
+            for (uint32_t gi : *l) {
+                Group &g = groups[gi];
+                if (g.in_work) continue;
+                if (g.cursor < g.ev_end || g.pending()) {
+                    g.in_work = true;
+                    next_work.push_back(gi);
+                }
+            }
+        work.swap(next_work);
+    }
+    for (uint32_t gi : touched) {
+        Group &g = groups[gi];
+        g.touched = false;
+        if (g.committed != g.committed0) commits.push_back({g.cluster_id, g.committed});
+    }
+
+    out->commits = commits.data();
+    out->n_commits = commits.size();
+    out->ready = ready.data();
+    out->n_ready = ready.size();
+    out->read_resps = resps.data();
+    out->n_read_resps = resps.size();
+    out->state_changes = states.data();
+    out->n_state_changes = states.size();
+    out->dropped_reads = dropped.data();
+    out->n_dropped_reads = dropped.size();
+    out->deferred = deferred.data();
+    out->n_deferred = deferred.size();
+    out->fallback_groups = fallback.data();
+    out->n_fallback_groups = fallback.size();
+    out->gpu_passes = passes;
+    out->decisions = decisions;
+    return HQ_OK;
+}
+
+// ------------------------------------------------------------------------------ C-ABI ------
+extern "C" {
+
+int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
+    if (!out) return HQ_E_INVAL;
+    *out = nullptr;
+    if (n_max < 1 || n_max > HQ_MAX_VOTERS) return HQ_E_INVAL;
+    hq_worker *w = new (std::nothrow) hq_worker();
+    if (!w) return HQ_E_NOMEM;
+    int rc = hq_open(device, 0, &w->ctx);
+    if (rc) {
+        delete w;
+        return rc;   // message: hq_last_error(NULL)
+    }
+    w->n_max = n_max;
+    *out = w;
+    return HQ_OK;
+}
+
+void hq_worker_close(hq_worker *w) {
+    if (!w) return;
+    if (w->ctx) {
+        hq_sync(w->ctx);
+        if (w->host) hq_free_pinned(w->ctx, w->host);
+        if (w->dev) hq_free_dev(w->ctx, w->dev);
+        hq_close(w->ctx);
+    }
+    delete w;
+}
+
+const char *hq_worker_last_error(const hq_worker *w) {
+    return w ? w->err.c_str() : hq_last_error(nullptr);
+}
+
+int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member *members) {
+    if (!w) return HQ_E_INVAL;
+    if (!g) return w->fail(HQ_E_INVAL, "hq_worker_add_group: group is NULL");
+    if (w->index.count(g->cluster_id)) return w->fail(HQ_E_INVAL, "hq_worker_add_group: cluster exists");
+    Group n;
+    int rc = w->load_group(n, g, members);
+    if (rc) return rc;
+    w->index.emplace(g->cluster_id, (uint32_t)w->groups.size());
+    w->groups.push_back(std::move(n));
+    return HQ_OK;
+}
+
+int hq_worker_set_group(hq_worker *w, const hq_worker_group *g, const hq_member *members) {
+    if (!w) return HQ_E_INVAL;
+    if (!g) return w->fail(HQ_E_INVAL, "hq_worker_set_group: group is NULL");
+    auto it = w->index.find(g->cluster_id);
+    if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_set_group: unknown cluster");
+    Group n;
+    int rc = w->load_group(n, g, members);
+    if (rc) return rc;
+    w->groups[it->second] = std::move(n);
+    return HQ_OK;
+}
+
+int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *out,
+                        hq_member *members, uint32_t cap, hq_read_status *reads,
+                        uint32_t reads_cap) {
+    if (!w) return HQ_E_INVAL;
+    auto it = w->index.find(cluster_id);
+    if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_get_group: unknown cluster");
+    const Group &g = w->groups[it->second];
+    if (out) {
+        out->cluster_id = g.cluster_id;
+        out->node_id = g.node_id;
+        out->term = g.term;
+        out->committed = g.committed;
+        out->last_index = g.last;
+        out->term_start = g.term_start;
+        out->state = g.state;
+        out->n_members = (uint32_t)g.members.size();
+        out->n_pending_reads = (uint32_t)g.reads.size();
+        out->suspended = g.suspended;
+    }
+    if (members)
+        for (uint32_t i = 0; i < cap && i < g.members.size(); ++i) members[i] = g.members[i];
+    if (reads)
+        for (uint32_t i = 0; i < reads_cap && i < g.reads.size(); ++i) {
+            const ReadStatus &r = g.reads[i];
+            uint32_t n = 0;
+            for (uint32_t s = 0; s < HQ_MAX_VOTERS; ++s)
+                n += ((r.confirmed >> s) & 1) || r.ord[s] != kNoAck;
+            reads[i] = {r.index, r.from, r.low, r.high, n, 0};
+        }
+    return HQ_OK;
+}
+
+int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
+    if (!w) return HQ_E_INVAL;
+    if (!in || !out) return w->fail(HQ_E_INVAL, "hq_worker_step: NULL argument");
+    if ((in->n_reads && !in->reads) || (in->n_msgs && !in->msgs) ||
+        (in->n_ticks && !in->ticks) || (in->n_proposals && !in->proposals))
+        return w->fail(HQ_E_INVAL, "hq_worker_step: NULL event array");
+    std::memset(out, 0, sizeof *out);
+    return w->step(in, out);
+}
+
+}  // extern "C"

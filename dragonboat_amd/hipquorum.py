@@ -88,6 +88,62 @@ GROUP_DTYPE = np.dtype([("node_id", "<u8"), ("committed", "<u8"), ("last_index",
 MSG_DTYPE = np.dtype([("from", "<u8"), ("hint_low", "<u8"), ("hint_high", "<u8"),
                       ("reject", "<u4"), ("reserved", "<u4")], align=True)
 
+# step worker records (include/hipquorum.h "step worker")
+STATE_FOLLOWER, STATE_CANDIDATE, STATE_LEADER = 0, 1, 2
+MSG_REPLICATE_RESP, MSG_REQUEST_VOTE_RESP, MSG_HEARTBEAT_RESP, MSG_READ_INDEX = 13, 15, 18, 19
+TICK_CHECK_QUORUM, TICK_ELECTION = 1, 2
+REASON_VOTE, REASON_CHECK_QUORUM, REASON_HIGHER_TERM, REASON_CAMPAIGN = 1, 2, 3, 4
+DROP_WITNESS, DROP_NOT_READY = 1, 2
+EVT_READ, EVT_MSG, EVT_TICK, EVT_PROPOSAL = 1, 2, 3, 4
+MESSAGE_DTYPE = np.dtype([("cluster_id", "<u8"), ("from", "<u8"), ("term", "<u8"),
+                          ("log_index", "<u8"), ("hint", "<u8"), ("hint_high", "<u8"),
+                          ("type", "<u4"), ("reject", "<u4")], align=True)
+READ_REQUEST_DTYPE = np.dtype([("cluster_id", "<u8"), ("ctx_low", "<u8"), ("ctx_high", "<u8")],
+                              align=True)
+TICK_DTYPE = np.dtype([("cluster_id", "<u8"), ("kind", "<u4"), ("reserved", "<u4")], align=True)
+PROPOSAL_DTYPE = np.dtype([("cluster_id", "<u8"), ("n_entries", "<u8")], align=True)
+WORKER_GROUP_DTYPE = np.dtype([("cluster_id", "<u8"), ("node_id", "<u8"), ("term", "<u8"),
+                               ("committed", "<u8"), ("last_index", "<u8"), ("term_start", "<u8"),
+                               ("state", "<u4"), ("n_members", "<u4"),
+                               ("n_pending_reads", "<u4"), ("suspended", "<u4")], align=True)
+READ_STATUS_DTYPE = np.dtype([("index", "<u8"), ("from", "<u8"), ("ctx_low", "<u8"),
+                              ("ctx_high", "<u8"), ("n_confirmed", "<u4"), ("reserved", "<u4")],
+                             align=True)
+COMMIT_EVENT_DTYPE = np.dtype([("cluster_id", "<u8"), ("committed", "<u8")], align=True)
+READY_DTYPE = np.dtype([("cluster_id", "<u8"), ("index", "<u8"), ("ctx_low", "<u8"),
+                        ("ctx_high", "<u8")], align=True)
+READ_RESP_DTYPE = np.dtype([("cluster_id", "<u8"), ("to", "<u8"), ("log_index", "<u8"),
+                            ("hint", "<u8"), ("hint_high", "<u8")], align=True)
+STATE_CHANGE_DTYPE = np.dtype([("cluster_id", "<u8"), ("term", "<u8"), ("state", "<u4"),
+                               ("reason", "<u4")], align=True)
+DROPPED_READ_DTYPE = np.dtype([("cluster_id", "<u8"), ("ctx_low", "<u8"), ("ctx_high", "<u8"),
+                               ("from", "<u8"), ("reason", "<u4"), ("reserved", "<u4")],
+                              align=True)
+EVENT_REF_DTYPE = np.dtype([("array", "<u4"), ("reserved", "<u4"), ("index", "<u8")], align=True)
+
+
+class StepInput(ctypes.Structure):
+    """Mirror of ``hq_step_input``."""
+
+    _fields_ = [("reads", _vp), ("n_reads", ctypes.c_uint64), ("msgs", _vp),
+                ("n_msgs", ctypes.c_uint64), ("ticks", _vp), ("n_ticks", ctypes.c_uint64),
+                ("proposals", _vp), ("n_proposals", ctypes.c_uint64)]
+
+
+STEP_OUTPUT_LISTS = [("commits", COMMIT_EVENT_DTYPE), ("ready", READY_DTYPE),
+                     ("read_resps", READ_RESP_DTYPE), ("state_changes", STATE_CHANGE_DTYPE),
+                     ("dropped_reads", DROPPED_READ_DTYPE), ("deferred", EVENT_REF_DTYPE),
+                     ("fallback_groups", np.dtype("<u8"))]
+
+
+class StepOutput(ctypes.Structure):
+    """Mirror of ``hq_step_output``."""
+
+    _fields_ = [f for name, _ in STEP_OUTPUT_LISTS
+                for f in ((name, _vp), ("n_" + name, ctypes.c_uint64))] + \
+               [("gpu_passes", ctypes.c_uint64), ("decisions", ctypes.c_uint64)]
+
+
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
 SIGNATURES = {
     "hq_abi_version": (ctypes.c_int, []),
@@ -122,7 +178,7 @@ SIGNATURES = {
     ),
     "hq_readindex_multi_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32,
                                               ctypes.c_uint32, _vp, _vp, _vp, _vp,
-                                              ctypes.c_uint32, _vp, _vp, _vp]),
+                                              ctypes.c_uint32, _vp, _vp, _vp, _vp]),
     "hq_ingest_match_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                            ctypes.c_uint64, ctypes.c_uint32, _vp]),
     "hq_ingest_ack_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
@@ -133,6 +189,15 @@ SIGNATURES = {
     "hq_pack_votes": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hq_pack_acks": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_uint32, _vp]),
+    "hq_worker_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "hq_worker_close": (None, [_vp]),
+    "hq_worker_last_error": (ctypes.c_char_p, [_vp]),
+    "hq_worker_add_group": (ctypes.c_int, [_vp, _vp, _vp]),
+    "hq_worker_set_group": (ctypes.c_int, [_vp, _vp, _vp]),
+    "hq_worker_get_group": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp,
+                                           ctypes.c_uint32]),
+    "hq_worker_step": (ctypes.c_int, [_vp, ctypes.POINTER(StepInput),
+                                      ctypes.POINTER(StepOutput)]),
     "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
     "hq_synth_bitmaps_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), _vp, _vp, _vp, _vp]),
 }
@@ -318,11 +383,13 @@ class Context:
                                 _p(outcome), _p(fallback)))
 
     def readindex_multi_dev(self, G, K_max, n_max, ack_ordinal, ctx_index, n_pending, n_voting,
-                            n_uniform, released_index, released_count, fallback=None):
+                            n_uniform, released_index, released_count, fallback=None,
+                            batch_end=None):
         self._check(lib.hq_readindex_multi_dev(self.h, G, K_max, n_max, _p(ack_ordinal),
                                                _p(ctx_index), _p(n_pending), _p(n_voting),
                                                n_uniform, _p(released_index),
-                                               _p(released_count), _p(fallback)))
+                                               _p(released_count), _p(batch_end),
+                                               _p(fallback)))
 
     def ingest_match_dev(self, updates, count, match, match_stride, G, n_max, n_skipped=None):
         """updates: device array of hq_match_update (uint64 pairs: group << 8 | slot, index)."""
@@ -505,3 +572,85 @@ def synth_spec(seed: int, G: int, n_max: int, cid_base: int = 1, cid_stride: int
 def free_commit(ctx: Context, b: CommitBuffers) -> None:
     for a in b.arrays():
         ctx.free(a)
+
+
+class Worker:
+    """The step worker (hq_worker_*): one step's events in, the reference's step results out,
+    every quorum decision taken by the kernels."""
+
+    def __init__(self, device: int = 0, n_max: int = 8):
+        self.h = _vp()
+        rc = lib.hq_worker_open(device, n_max, ctypes.byref(self.h))
+        if rc != HQ_OK:
+            raise HQError(rc, "hq_worker_open: " + lib.hq_last_error(None).decode())
+        self.n_max = n_max
+
+    def close(self) -> None:
+        if self.h:
+            lib.hq_worker_close(self.h)
+            self.h = _vp()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != HQ_OK:
+            raise HQError(rc, f"{what}: {lib.hq_worker_last_error(self.h).decode()}")
+
+    @staticmethod
+    def _group(cluster_id, node_id, term, state, committed, last_index, term_start, members):
+        g = np.zeros(1, WORKER_GROUP_DTYPE)
+        g["cluster_id"], g["node_id"], g["term"], g["state"] = cluster_id, node_id, term, state
+        g["committed"], g["last_index"], g["term_start"] = committed, last_index, term_start
+        m = np.asarray(members, MEMBER_DTYPE)
+        g["n_members"] = len(m)
+        return g, m
+
+    def add_group(self, cluster_id, node_id, term, state, committed, last_index, term_start,
+                  members) -> None:
+        g, m = self._group(cluster_id, node_id, term, state, committed, last_index, term_start,
+                           members)
+        self._check(lib.hq_worker_add_group(self.h, _p(g), _p(m)), "hq_worker_add_group")
+
+    def set_group(self, cluster_id, node_id, term, state, committed, last_index, term_start,
+                  members) -> None:
+        g, m = self._group(cluster_id, node_id, term, state, committed, last_index, term_start,
+                           members)
+        self._check(lib.hq_worker_set_group(self.h, _p(g), _p(m)), "hq_worker_set_group")
+
+    def get_group(self, cluster_id):
+        """(group record, members, pending reads) of one group."""
+        g = np.zeros(1, WORKER_GROUP_DTYPE)
+        self._check(lib.hq_worker_get_group(self.h, cluster_id, _p(g), None, 0, None, 0),
+                    "hq_worker_get_group")
+        m = np.zeros(int(g["n_members"][0]), MEMBER_DTYPE)
+        r = np.zeros(int(g["n_pending_reads"][0]), READ_STATUS_DTYPE)
+        self._check(lib.hq_worker_get_group(self.h, cluster_id, _p(g), _p(m), len(m), _p(r),
+                                            len(r)), "hq_worker_get_group")
+        return g[0], m, r
+
+    def step(self, reads=None, msgs=None, ticks=None, proposals=None):
+        """One step; returns a dict of numpy record arrays (copies) plus gpu_passes/decisions."""
+        arrs = [np.ascontiguousarray(x if x is not None else np.zeros(0, dt), dt)
+                for x, dt in ((reads, READ_REQUEST_DTYPE), (msgs, MESSAGE_DTYPE),
+                              (ticks, TICK_DTYPE), (proposals, PROPOSAL_DTYPE))]
+        inp = StepInput(_p(arrs[0]), len(arrs[0]), _p(arrs[1]), len(arrs[1]), _p(arrs[2]),
+                        len(arrs[2]), _p(arrs[3]), len(arrs[3]))
+        out = StepOutput()
+        self._check(lib.hq_worker_step(self.h, ctypes.byref(inp), ctypes.byref(out)),
+                    "hq_worker_step")
+        res = {}
+        for name, dt in STEP_OUTPUT_LISTS:
+            n = getattr(out, "n_" + name)
+            ptr = getattr(out, name)
+            if n == 0:
+                res[name] = np.zeros(0, dt)
+                continue
+            buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
+            res[name] = np.frombuffer(buf, dt).copy()
+        res["gpu_passes"] = out.gpu_passes
+        res["decisions"] = out.decisions
+        return res

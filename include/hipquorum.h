@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 1
+#define HQ_ABI_VERSION 2
 
 /* status codes */
 #define HQ_OK          0
@@ -204,15 +204,18 @@ int hq_vote(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *reje
  * ordinals and entry i is released at min_{k >= i} t_k with the index of the (first) ctx
  * attaining it (the rewrite of readindex.go:97-105).
  * Out: released_index[k * G + g] = rewritten index of entry k, or UINT64_MAX if not released;
- * released_count[g] = released prefix length. n outside [1, n_max], K > K_max or a decreasing
- * ctx_index give fallback (nothing released). K_max <= 8, n_max <= 8; ordinals distinct per
- * group except 0 (ties at equal ordinals resolve in queue order).
+ * released_count[g] = released prefix length; batch_end[g] (may be NULL) bit k = entry k is the
+ * ctx whose confirm() released its batch — every released entry i belongs to the batch closed by
+ * the first k >= i with bit k set, and the ReadIndexResp messages of that batch carry ctx k as
+ * their hint (handleReadIndexLeaderConfirmation, raft.go:1740-1760). n outside [1, n_max],
+ * K > K_max or a decreasing ctx_index give fallback (nothing released). K_max <= 8, n_max <= 8;
+ * ordinals distinct per group except 0 (ties at equal ordinals resolve in queue order).
  */
 int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
                            const uint16_t *ack_ordinal, const uint64_t *ctx_index,
                            const uint8_t *n_pending, const uint8_t *n_voting, uint32_t n_uniform,
                            uint64_t *released_index, uint8_t *released_count,
-                           uint64_t *fallback);
+                           uint8_t *batch_end, uint64_t *fallback);
 
 /* ReadIndex confirmation and vote tally of the same groups in one pass over the shared n. */
 int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
@@ -336,6 +339,172 @@ int hq_pack_votes(const hq_group_view *groups, uint64_t G, const hq_member *memb
 int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *members,
                  const hq_msg *msgs, uint8_t *ack, uint8_t *active, uint8_t *n_voting,
                  uint32_t n_max, uint64_t *fallback);
+
+/* ---------------------------------------------------------------- step worker -------------- */
+/*
+ * The step worker is the caller side of the kernels: execEngine.processSteps (execengine.go:
+ * 923-1000) for the quorum part of many Raft groups at once. It holds each group's quorum state
+ * (raft.remotes / witnesses / observers, raft.go:206-208; entryLog committed / lastIndex and the
+ * first index of the leader's term; readIndex, readindex.go:31-34; votes, raft.go:210) and takes
+ * one step's events in node.handleEvents order (node.go:1113-1157):
+ *   1. local ReadIndex requests      node.handleReadIndex -> Peer.ReadIndex (peer.go:297-303)
+ *   2. received messages             handleReceivedMessages -> Peer.Handle (peer.go:186-198)
+ *   3. tick messages                 CheckQuorum (raft.go:1582) / Election (raft.go:1485)
+ *   4. proposals                     handleProposals -> handleLeaderPropose (raft.go:1590)
+ * Membership filtering (Peer.Handle), the term check (onMessageTermNotMatched, raft.go:1416),
+ * remote.tryUpdate, the confirmed-set inserts and first-response-wins votes are applied on the
+ * host as the events arrive; every quorum decision — tryCommit, the ReadIndex release with its
+ * index rewrite, the vote outcome, leaderHasQuorum — is taken by the kernels above at the end of
+ * a run of events. A run ends early only where a later event reads a decision (a ReadIndex
+ * needs the committed index; a state change needs the vote / CheckQuorum outcome; a higher-term
+ * message ends the group's leadership), so one step usually costs one GPU pass. Results equal
+ * the reference processing the events one by one (tests/test_gpu_worker.py against
+ * oracle/qref_step.c).
+ *
+ * Events the reference hands to code outside the quorum path without touching quorum state —
+ * a follower or candidate forwarding or dropping a ReadIndex or a proposal — are returned as
+ * `deferred`. Events the worker cannot take exactly suspend the group (`fallback`): an observer
+ * acknowledging a pending ReadIndex ctx, a ReplicateResp above the leader's lastIndex, more
+ * than 8 pending ReadIndex ctxs, an unknown message type. The group's events from that one on
+ * are returned as deferred, its state is as of the event before, and it stays suspended (its
+ * events deferred) until the caller re-syncs it with hq_worker_set_group.
+ *
+ * One worker per step worker goroutine; not thread-safe.
+ */
+#define HQ_STATE_FOLLOWER  0u
+#define HQ_STATE_CANDIDATE 1u
+#define HQ_STATE_LEADER    2u
+
+/* raftpb.MessageType values (raftpb/raft.proto:26-52) the worker consumes */
+#define HQ_MSG_REPLICATE_RESP    13u
+#define HQ_MSG_REQUEST_VOTE_RESP 15u
+#define HQ_MSG_HEARTBEAT_RESP    18u
+#define HQ_MSG_READ_INDEX        19u
+
+#define HQ_TICK_CHECK_QUORUM 1u   /* the leader tick's CheckQuorum message (raft.go:1582-1588) */
+#define HQ_TICK_ELECTION     2u   /* the election tick's Election message (raft.go:1485-1515);
+                                     issue it only when hasConfigChangeToApply() is false */
+
+/* hq_state_change.reason */
+#define HQ_REASON_VOTE         1u  /* vote outcome: became leader or follower */
+#define HQ_REASON_CHECK_QUORUM 2u  /* leader lost quorum */
+#define HQ_REASON_HIGHER_TERM  3u  /* a message with a higher term */
+#define HQ_REASON_CAMPAIGN     4u  /* became candidate */
+/* hq_dropped_read.reason (reportDroppedReadIndex) */
+#define HQ_DROP_WITNESS   1u      /* ReadIndex from a witness (raft.go:1642-1643) */
+#define HQ_DROP_NOT_READY 2u      /* no committed entry at the current term yet (:1645-1651) */
+
+typedef struct hq_message {      /* the pb.Message fields the path reads (raft.proto:154-168) */
+    uint64_t cluster_id;
+    uint64_t from;
+    uint64_t term;
+    uint64_t log_index;
+    uint64_t hint;               /* HeartbeatResp / ReadIndex: SystemCtx.Low */
+    uint64_t hint_high;          /* SystemCtx.High */
+    uint32_t type;               /* HQ_MSG_* */
+    uint32_t reject;
+} hq_message;
+
+typedef struct hq_read_request { /* local ReadIndex: Peer.ReadIndex(ctx), From = NoNode */
+    uint64_t cluster_id;
+    uint64_t ctx_low;
+    uint64_t ctx_high;
+} hq_read_request;
+
+typedef struct hq_tick {
+    uint64_t cluster_id;
+    uint32_t kind;               /* HQ_TICK_* */
+    uint32_t reserved;
+} hq_tick;
+
+typedef struct hq_proposal {
+    uint64_t cluster_id;
+    uint64_t n_entries;
+} hq_proposal;
+
+typedef struct hq_worker_group { /* a group's quorum state (add / set / get) */
+    uint64_t cluster_id;
+    uint64_t node_id;            /* this node; must be one of the group's remotes */
+    uint64_t term;
+    uint64_t committed;
+    uint64_t last_index;
+    uint64_t term_start;         /* leader: index of its first entry at `term` (its no-op) */
+    uint32_t state;              /* HQ_STATE_* */
+    uint32_t n_members;          /* remotes + witnesses + observers; at most 8 voting */
+    uint32_t n_pending_reads;    /* get only */
+    uint32_t suspended;          /* get only: 1 while the group is in fallback */
+} hq_worker_group;
+
+typedef struct hq_read_status {  /* readStatus (readindex.go:21-26), get only */
+    uint64_t index;
+    uint64_t from;
+    uint64_t ctx_low;
+    uint64_t ctx_high;
+    uint32_t n_confirmed;
+    uint32_t reserved;
+} hq_read_status;
+
+typedef struct hq_step_input {
+    const hq_read_request *reads;   uint64_t n_reads;
+    const hq_message *msgs;         uint64_t n_msgs;      /* arrival order */
+    const hq_tick *ticks;           uint64_t n_ticks;
+    const hq_proposal *proposals;   uint64_t n_proposals;
+} hq_step_input;
+
+typedef struct hq_commit_event { uint64_t cluster_id, committed; } hq_commit_event;
+typedef struct hq_ready_to_read {   /* pb.ReadyToRead (raftpb/raft.go:54-57) */
+    uint64_t cluster_id, index, ctx_low, ctx_high;
+} hq_ready_to_read;
+typedef struct hq_read_index_resp { /* ReadIndexResp to a remote requester (raft.go:1751-1757) */
+    uint64_t cluster_id, to, log_index, hint, hint_high;
+} hq_read_index_resp;
+typedef struct hq_state_change {
+    uint64_t cluster_id, term;
+    uint32_t state, reason;
+} hq_state_change;
+typedef struct hq_dropped_read {
+    uint64_t cluster_id, ctx_low, ctx_high, from;
+    uint32_t reason, reserved;
+} hq_dropped_read;
+/* an input event handed back to the caller: which array (HQ_EVT_*) and its index there */
+#define HQ_EVT_READ     1u
+#define HQ_EVT_MSG      2u
+#define HQ_EVT_TICK     3u
+#define HQ_EVT_PROPOSAL 4u
+typedef struct hq_event_ref { uint32_t array, reserved; uint64_t index; } hq_event_ref;
+
+/* Results of one step; the arrays are owned by the worker and valid until its next call. Per
+ * group, every list is in the order the reference produces it. */
+typedef struct hq_step_output {
+    const hq_commit_event *commits;        uint64_t n_commits;      /* committed index advanced */
+    const hq_ready_to_read *ready;         uint64_t n_ready;
+    const hq_read_index_resp *read_resps;  uint64_t n_read_resps;
+    const hq_state_change *state_changes;  uint64_t n_state_changes;
+    const hq_dropped_read *dropped_reads;  uint64_t n_dropped_reads;
+    const hq_event_ref *deferred;          uint64_t n_deferred;
+    const uint64_t *fallback_groups;       uint64_t n_fallback_groups;
+    uint64_t gpu_passes;        /* GPU passes (kernel batches + one sync each) of this step */
+    uint64_t decisions;         /* group decisions taken on the GPU in this step */
+} hq_step_output;
+
+typedef struct hq_worker hq_worker;
+
+/* n_max: voting slots per group (1..8). */
+int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
+void hq_worker_close(hq_worker *w);
+const char *hq_worker_last_error(const hq_worker *w);
+/* Add a group; members[0 .. g->n_members). Fails if the cluster exists, the node is not one of
+ * its remotes or it has more than n_max voting members. */
+int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member *members);
+/* Overwrite a group's state (re-sync after fallback); clears its read queue and votes and
+ * resumes it. */
+int hq_worker_set_group(hq_worker *w, const hq_worker_group *g, const hq_member *members);
+/* Read a group's state: members (up to cap) in the order given at add/set, and its pending
+ * ReadIndex queue (up to reads_cap) in queue order. Either array may be NULL. */
+int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *g,
+                        hq_member *members, uint32_t cap, hq_read_status *reads,
+                        uint32_t reads_cap);
+int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
 
 /* ---------------------------------------------------------------- synthetic inputs ---------- */
 

@@ -478,7 +478,7 @@ typedef struct { uint32_t o, k, s; } ri_msg;
 static void ri_multi_range(uint64_t g0, uint64_t g1, uint32_t K_max, uint32_t n_max,
                            const uint16_t *ord, const uint64_t *idx, const uint8_t *np,
                            const uint8_t *nv, uint32_t nu, uint64_t *rel, uint8_t *cnt,
-                           uint64_t *fallback, uint64_t G) {
+                           uint8_t *bend, uint64_t *fallback, uint64_t G) {
     qref_read_index *ri = (qref_read_index *)malloc(sizeof *ri);
     qref_read_status *out = (qref_read_status *)malloc(QREF_MAX_PENDING * sizeof *out);
     ri_msg msgs[64 * 8];
@@ -487,6 +487,7 @@ static void ri_multi_range(uint64_t g0, uint64_t g1, uint32_t K_max, uint32_t n_
         int n = nv ? nv[g] : (int)nu;
         for (uint32_t k = 0; k < K_max; k++) rel[(uint64_t)k * G + g] = UINT64_MAX;
         cnt[g] = 0;
+        if (bend) bend[g] = 0;
         if (n < 1 || n > (int)n_max || K > K_max) {
             if (fallback) bit_set(fallback, g);
             continue;
@@ -526,6 +527,8 @@ static void ri_multi_range(uint64_t g0, uint64_t g1, uint32_t K_max, uint32_t n_
                 rel[(out[j].ctx.low - 1) * G + g] = out[j].index;
                 released++;
             }
+            /* the confirming ctx is the last of the released batch (readindex.go:96) */
+            if (r > 0 && bend) bend[g] |= (uint8_t)(1u << (out[r - 1].ctx.low - 1));
         }
         cnt[g] = released;
     }
@@ -540,13 +543,13 @@ typedef struct {
     const uint64_t *idx;
     const uint8_t *np, *nv;
     uint64_t *rel, *fb;
-    uint8_t *cnt;
+    uint8_t *cnt, *bend;
 } ri_multi_job;
 
 static void *ri_multi_run(void *p) {
     ri_multi_job *j = (ri_multi_job *)p;
     ri_multi_range(j->g0, j->g1, j->K_max, j->n_max, j->ord, j->idx, j->np, j->nv, j->nu, j->rel,
-                   j->cnt, j->fb, j->G);
+                   j->cnt, j->bend, j->fb, j->G);
     return NULL;
 }
 
@@ -554,7 +557,8 @@ int qref_readindex_multi_batch(uint64_t G, uint32_t K_max, uint32_t n_max,
                                const uint16_t *ack_ordinal, const uint64_t *ctx_index,
                                const uint8_t *n_pending, const uint8_t *n_voting,
                                uint32_t n_uniform, uint64_t *released_index,
-                               uint8_t *released_count, uint64_t *fallback, int nthreads) {
+                               uint8_t *released_count, uint8_t *batch_end, uint64_t *fallback,
+                               int nthreads) {
     if (!ack_ordinal || !ctx_index || !released_index || !released_count || K_max < 1 ||
         K_max > 64 || n_max < 1 || n_max > 8)
         return -1;
@@ -571,7 +575,7 @@ int qref_readindex_multi_batch(uint64_t G, uint32_t K_max, uint32_t n_max,
         if (b1 > blocks) b1 = blocks;
         ri_multi_job j = {b0 * 64, b1 * 64 < G ? b1 * 64 : G, G, K_max, n_max, n_uniform,
                           ack_ordinal, ctx_index, n_pending, n_voting, released_index, fallback,
-                          released_count};
+                          released_count, batch_end};
         jobs[t] = j;
         if (nthreads == 1 || pthread_create(&th[t], NULL, ri_multi_run, &jobs[t]) != 0) {
             ri_multi_run(&jobs[t]);

@@ -22,8 +22,8 @@
 extern "C" {
 #endif
 
-#define QREF_MAX_NODES   64
-#define QREF_MAX_PENDING 256
+#define QREF_MAX_NODES   16
+#define QREF_MAX_PENDING 64
 
 /* reference State enum values (internal/raft/raft.go:62-71) */
 #define QREF_FOLLOWER  0
@@ -163,13 +163,15 @@ int qref_check_quorum_batch(uint64_t G, uint8_t *active, const uint8_t *n_voting
  * = arrival ordinal of voting slot s's first HeartbeatResp for ctx k (0xFFFF = none). The
  * messages are replayed in ordinal order through readIndex.confirm (readindex.go:77-116);
  * released_index[k*G + g] = the rewritten index of entry k if it was released, else UINT64_MAX;
- * released_count[g] = released prefix length. Groups with n outside [1, n_max] or K > K_max are
- * fallback (nothing released). */
+ * released_count[g] = released prefix length; batch_end[g] (may be NULL) bit k = entry k was the
+ * ctx of the confirm() call that released its batch. Groups with n outside [1, n_max] or
+ * K > K_max are fallback (nothing released). */
 int qref_readindex_multi_batch(uint64_t G, uint32_t K_max, uint32_t n_max,
                                const uint16_t *ack_ordinal, const uint64_t *ctx_index,
                                const uint8_t *n_pending, const uint8_t *n_voting,
                                uint32_t n_uniform, uint64_t *released_index,
-                               uint8_t *released_count, uint64_t *fallback, int nthreads);
+                               uint8_t *released_count, uint8_t *batch_end, uint64_t *fallback,
+                               int nthreads);
 
 /* ---------------------------------------------------------------- delta ingest (§8f-1) ----- */
 /* Sequential restatements, applied in array order: remote.tryUpdate (remote.go:123-133) on
@@ -211,6 +213,73 @@ int qgen_c1_stream(uint64_t seed, uint64_t T, uint64_t committed0, uint64_t last
                    uint64_t *match, uint64_t *last);
 int qref_c1_run(uint64_t T, const uint64_t *match, const uint64_t *last, uint64_t term_start,
                 uint64_t committed0, uint64_t *committed);
+
+/* ---------------------------------------------------------------- one step, event by event - */
+/* Sequential replay of one group's step (oracle/qref_step.c): the checker of the GPU step worker
+ * (hq_worker_step). Roles and members mirror hq_member of include/hipquorum.h. */
+#define QREF_ROLE_REMOTE   0
+#define QREF_ROLE_OBSERVER 1
+#define QREF_ROLE_WITNESS  2
+#define QREF_STEP_MAX_MEMBERS 16
+#define QREF_STEP_MAX_OUT     64
+
+#define QREF_EV_READ         1   /* local ReadIndex (node.handleReadIndex): hint/hint_high = ctx */
+#define QREF_EV_MSG          2   /* received message (type, from, term, log_index, hint, reject) */
+#define QREF_EV_CHECK_QUORUM 3   /* the leader tick's CheckQuorum message */
+#define QREF_EV_CAMPAIGN     4   /* the election tick's Election message */
+#define QREF_EV_PROPOSE      5   /* proposal of log_index entries */
+
+/* state-change reasons */
+#define QREF_REASON_VOTE         1
+#define QREF_REASON_CHECK_QUORUM 2
+#define QREF_REASON_HIGHER_TERM  3
+#define QREF_REASON_CAMPAIGN     4
+/* dropped-ReadIndex reasons (reportDroppedReadIndex) */
+#define QREF_DROP_WITNESS   1
+#define QREF_DROP_NOT_READY 2
+
+typedef struct qref_member {
+    uint64_t node_id;
+    uint64_t match;
+    uint32_t role;
+    uint32_t active;
+} qref_member;
+
+typedef struct qref_event {
+    uint32_t kind;
+    uint32_t type;
+    uint64_t from, term, log_index, hint, hint_high;
+    uint32_t reject;
+    uint32_t reserved;
+} qref_event;
+
+typedef struct qref_group {
+    uint64_t cluster_id, node_id, term;
+    int state;
+    int n_members;
+    uint64_t committed, last, term_start;
+    qref_member members[QREF_STEP_MAX_MEMBERS];
+    qref_read_index ri;
+    qref_votes votes;
+} qref_group;
+
+typedef struct qref_step_out {
+    uint64_t committed;
+    int commit_changed;
+    int n_ready, n_resps, n_states, n_dropped, n_deferred;
+    struct { uint64_t index, low, high; } ready[QREF_STEP_MAX_OUT];
+    struct { uint64_t to, index, hint, hint_high; } resps[QREF_STEP_MAX_OUT];
+    struct { uint64_t term; uint32_t state, reason; } states[QREF_STEP_MAX_OUT];
+    struct { uint64_t low, high, from; uint32_t reason, reserved; } dropped[QREF_STEP_MAX_OUT];
+    uint32_t deferred[QREF_STEP_MAX_OUT];   /* event indexes handed to the non-quorum CPU path */
+} qref_step_out;
+
+int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64_t term,
+                    int state, uint64_t committed, uint64_t last, uint64_t term_start,
+                    const qref_member *members, int n_members);
+/* Replays the events in order; returns 0, -1 on bad arguments or QREF_PANIC where the reference
+ * panics (or an output list overflows). */
+int qref_group_step(qref_group *g, const qref_event *ev, int n_events, qref_step_out *out);
 
 /* FNV-1a 64 over a byte range (fixture checksums). */
 uint64_t qref_fnv1a64(const void *p, size_t bytes);

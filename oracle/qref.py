@@ -17,8 +17,8 @@ LIB_PATH = os.path.join(_HERE, "build", "libqref.so")
 
 QREF_FOLLOWER, QREF_CANDIDATE, QREF_LEADER = 0, 1, 2
 QREF_PANIC = -100
-QREF_MAX_NODES = 64
-QREF_MAX_PENDING = 256
+QREF_MAX_NODES = 16
+QREF_MAX_PENDING = 64
 
 _vp = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -59,6 +59,55 @@ class ReadIndex(ctypes.Structure):
 class Votes(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("from_", _u64 * QREF_MAX_NODES),
                 ("granted", ctypes.c_int * QREF_MAX_NODES)]
+
+
+QREF_STEP_MAX_MEMBERS = 16
+QREF_STEP_MAX_OUT = 64
+EV_READ, EV_MSG, EV_CHECK_QUORUM, EV_CAMPAIGN, EV_PROPOSE = 1, 2, 3, 4, 5
+
+
+class Member(ctypes.Structure):
+    _fields_ = [("node_id", _u64), ("match", _u64), ("role", ctypes.c_uint32),
+                ("active", ctypes.c_uint32)]
+
+
+class Event(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("type", ctypes.c_uint32), ("from_", _u64),
+                ("term", _u64), ("log_index", _u64), ("hint", _u64), ("hint_high", _u64),
+                ("reject", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class Group(ctypes.Structure):
+    _fields_ = [("cluster_id", _u64), ("node_id", _u64), ("term", _u64), ("state", ctypes.c_int),
+                ("n_members", ctypes.c_int), ("committed", _u64), ("last", _u64),
+                ("term_start", _u64), ("members", Member * QREF_STEP_MAX_MEMBERS),
+                ("ri", ReadIndex), ("votes", Votes)]
+
+
+class _Ready(ctypes.Structure):
+    _fields_ = [("index", _u64), ("low", _u64), ("high", _u64)]
+
+
+class _Resp(ctypes.Structure):
+    _fields_ = [("to", _u64), ("index", _u64), ("hint", _u64), ("hint_high", _u64)]
+
+
+class _State(ctypes.Structure):
+    _fields_ = [("term", _u64), ("state", ctypes.c_uint32), ("reason", ctypes.c_uint32)]
+
+
+class _Dropped(ctypes.Structure):
+    _fields_ = [("low", _u64), ("high", _u64), ("from_", _u64), ("reason", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class StepOut(ctypes.Structure):
+    _fields_ = [("committed", _u64), ("commit_changed", ctypes.c_int), ("n_ready", ctypes.c_int),
+                ("n_resps", ctypes.c_int), ("n_states", ctypes.c_int), ("n_dropped", ctypes.c_int),
+                ("n_deferred", ctypes.c_int), ("ready", _Ready * QREF_STEP_MAX_OUT),
+                ("resps", _Resp * QREF_STEP_MAX_OUT), ("states", _State * QREF_STEP_MAX_OUT),
+                ("dropped", _Dropped * QREF_STEP_MAX_OUT),
+                ("deferred", ctypes.c_uint32 * QREF_STEP_MAX_OUT)]
 
 
 TERM_FN = ctypes.CFUNCTYPE(_u64, _vp, _u64)
@@ -110,8 +159,11 @@ def load() -> ctypes.CDLL:
         "qref_fnv1a64": (_u64, [_vp, ctypes.c_size_t]),
         "qref_readindex_multi_batch": (ctypes.c_int, [_u64, ctypes.c_uint32, ctypes.c_uint32, _vp,
                                                       _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
-                                                      _vp, ctypes.c_int]),
+                                                      _vp, _vp, ctypes.c_int]),
         "qgen_c1_stream": (ctypes.c_int, [_u64, _u64, _u64, _u64, _vp, _vp]),
+        "qref_group_init": (ctypes.c_int, [_vp, _u64, _u64, _u64, ctypes.c_int, _u64, _u64, _u64,
+                                           _vp, ctypes.c_int]),
+        "qref_group_step": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
         "qref_c1_run": (ctypes.c_int, [_u64, _vp, _vp, _u64, _u64, _vp]),
         "qref_ingest_match": (_u64, [_vp, _u64, _vp, _u64, _u64, ctypes.c_uint32]),
         "qref_ingest_ack": (_u64, [_vp, _u64, _vp, _u64, ctypes.c_uint32]),
@@ -331,16 +383,18 @@ class BitmapInputs:
 def readindex_multi_batch(ack_ordinal, ctx_index, n_pending, n_voting, n_uniform, K_max, n_max,
                           nthreads=1):
     """General multi-ctx ReadIndex: returns (released_index [K_max*G], released_count [G],
-    fallback bitmap). ack_ordinal: uint16 [K_max][n_max][G]; ctx_index: uint64 [K_max][G]."""
+    fallback bitmap, batch_end [G]). ack_ordinal: uint16 [K_max][n_max][G]; ctx_index: uint64
+    [K_max][G]."""
     G = len(ctx_index) // K_max
     rel = np.zeros(K_max * G, np.uint64)
     cnt = np.zeros(G, np.uint8)
+    bend = np.zeros(G, np.uint8)
     fb = np.zeros(words64(G), np.uint64)
     rc = lib.qref_readindex_multi_batch(G, K_max, n_max, _ptr(ack_ordinal), _ptr(ctx_index),
                                         _ptr(n_pending), _ptr(n_voting), n_uniform, _ptr(rel),
-                                        _ptr(cnt), _ptr(fb), nthreads)
+                                        _ptr(cnt), _ptr(bend), _ptr(fb), nthreads)
     assert rc == 0, rc
-    return rel, cnt, fb
+    return rel, cnt, fb, bend
 
 
 def c1_stream(seed: int, T: int, committed0: int, last0: int):
@@ -383,3 +437,65 @@ def append(updates: np.ndarray, last_index, match_slot0, term_mask, ring_len: in
 def fnv1a64(a: np.ndarray) -> int:
     a = np.ascontiguousarray(a)
     return int(lib.qref_fnv1a64(a.ctypes.data_as(_vp), a.nbytes))
+
+
+class StepGroup:
+    """One group replayed event by event through the reference's handlers (oracle/qref_step.c).
+    Events are tuples: ("read", low, high) | ("msg", type, from, term, log_index, hint,
+    hint_high, reject) | ("check_quorum",) | ("campaign",) | ("propose", n)."""
+
+    def __init__(self, cluster_id, node_id, term, state, committed, last, term_start, members):
+        self.c = Group()
+        m = (Member * len(members))(*[Member(int(a), int(b), int(c), int(d))
+                                      for a, b, c, d in members])
+        rc = lib.qref_group_init(ctypes.byref(self.c), cluster_id, node_id, term, state,
+                                 committed, last, term_start, m, len(members))
+        assert rc == 0, rc
+        self._out = StepOut()
+
+    def step(self, events):
+        ev = (Event * max(1, len(events)))()
+        for i, e in enumerate(events):
+            k = e[0]
+            if k == "read":
+                ev[i] = Event(EV_READ, 19, 0, 0, 0, e[1], e[2], 0, 0)
+            elif k == "msg":
+                ev[i] = Event(EV_MSG, e[1], e[2], e[3], e[4], e[5], e[6], e[7], 0)
+            elif k == "check_quorum":
+                ev[i] = Event(EV_CHECK_QUORUM, 0, 0, 0, 0, 0, 0, 0, 0)
+            elif k == "campaign":
+                ev[i] = Event(EV_CAMPAIGN, 0, 0, 0, 0, 0, 0, 0, 0)
+            elif k == "propose":
+                ev[i] = Event(EV_PROPOSE, 0, 0, 0, e[1], 0, 0, 0, 0)
+            else:
+                raise ValueError(k)
+        o = self._out
+        rc = lib.qref_group_step(ctypes.byref(self.c), ev, len(events), ctypes.byref(o))
+        if rc != 0:
+            return rc
+        return {
+            "committed": int(o.committed), "commit_changed": bool(o.commit_changed),
+            "ready": [(int(r.index), int(r.low), int(r.high)) for r in o.ready[:o.n_ready]],
+            "resps": [(int(r.to), int(r.index), int(r.hint), int(r.hint_high))
+                      for r in o.resps[:o.n_resps]],
+            "states": [(int(r.term), int(r.state), int(r.reason)) for r in o.states[:o.n_states]],
+            "dropped": [(int(r.low), int(r.high), int(r.from_), int(r.reason))
+                        for r in o.dropped[:o.n_dropped]],
+            "deferred": [int(x) for x in o.deferred[:o.n_deferred]],
+        }
+
+    def state(self):
+        """(term, state, committed, last, term_start, [(node_id, match, role, active)],
+        [(index, from, (low, high), n_confirmed)] in queue order)."""
+        c = self.c
+        members = [(int(m.node_id), int(m.match), int(m.role), int(m.active))
+                   for m in c.members[:c.n_members]]
+        reads = []
+        for qi in range(c.ri.n_queue):
+            q = c.ri.queue[qi]
+            for p in c.ri.pending[:c.ri.n_pending]:
+                if p.ctx.low == q.low and p.ctx.high == q.high:
+                    reads.append((int(p.index), int(p.from_), (int(q.low), int(q.high)),
+                                  int(p.n_confirmed)))
+        return (int(c.term), int(c.state), int(c.committed), int(c.last), int(c.term_start),
+                members, reads)

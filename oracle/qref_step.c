@@ -1,0 +1,330 @@
+/*
+ * qref_step.c — CPU oracle of one step of a Raft node's quorum-relevant event stream, replayed
+ * one event at a time exactly as the reference processes it. TEST INFRASTRUCTURE ONLY: it is the
+ * sequential checker of the step worker (hq_worker_step in include/hipquorum.h), which batches
+ * the same events and decides them on the GPU.
+ *
+ * Event order inside a step follows node.handleEvents (node.go:1113-1157): the local ReadIndex
+ * (handleReadIndex :1197-1206 -> Peer.ReadIndex, peer.go:297-303), the received messages
+ * (handleReceivedMessages :1257-1289 -> Peer.Handle, peer.go:186-198), the local tick's
+ * CheckQuorum / Election messages (handleLocalTick), then proposals (handleProposals
+ * :1184-1195). The caller lists the events of one group in that order.
+ */
+#include <string.h>
+
+#include "qref.h"
+
+/* raftpb message types (raftpb/raft.proto:26-52) */
+enum { MT_REPLICATE_RESP = 13, MT_REQUEST_VOTE_RESP = 15, MT_HEARTBEAT_RESP = 18, MT_READ_INDEX = 19 };
+
+static int is_response_type(uint32_t t) {   /* isResponseMessageType (raft/utils.go) */
+    return t == MT_REPLICATE_RESP || t == MT_REQUEST_VOTE_RESP || t == MT_HEARTBEAT_RESP ||
+           t == 20 /* ReadIndexResp */ || t == 8 /* SnapshotStatus */ || t == 9 /* Unreachable */;
+}
+
+static int find_member(const qref_group *g, uint64_t id) {
+    for (int i = 0; i < g->n_members; i++)
+        if (g->members[i].node_id == id) return i;
+    return -1;
+}
+
+static int role_of(const qref_group *g, uint64_t id) {
+    int i = find_member(g, id);
+    return i < 0 ? -1 : (int)g->members[i].role;
+}
+
+static int n_voting(const qref_group *g) {      /* numVotingMembers, raft.go:368-370 */
+    int n = 0;
+    for (int i = 0; i < g->n_members; i++) n += g->members[i].role != QREF_ROLE_OBSERVER;
+    return n;
+}
+
+static int quorum(const qref_group *g) { return qref_quorum(n_voting(g)); }
+
+typedef struct { uint64_t term, term_start; } leader_log_ud;
+/* the leader's log: entries from its first current-term entry on carry r.term; older entries a
+ * lower term (entryutils.go:44-47) */
+static uint64_t leader_term_at(const void *ud, uint64_t i) {
+    const leader_log_ud *l = (const leader_log_ud *)ud;
+    return i >= l->term_start ? l->term : l->term - 1;
+}
+
+static qref_log log_view(qref_group *g, leader_log_ud *ud) {
+    ud->term = g->term;
+    ud->term_start = g->term_start;
+    qref_log l;
+    l.first_minus_1 = 0;
+    l.last = g->last;
+    l.committed = g->committed;
+    l.term_at = leader_term_at;
+    l.ud = ud;
+    return l;
+}
+
+/* raft.tryCommit (raft.go:888-909) over the group's remotes then witnesses */
+static int try_commit(qref_group *g) {
+    uint64_t rm[QREF_STEP_MAX_MEMBERS], wm[QREF_STEP_MAX_MEMBERS];
+    int nr = 0, nw = 0;
+    for (int i = 0; i < g->n_members; i++) {
+        if (g->members[i].role == QREF_ROLE_REMOTE) rm[nr++] = g->members[i].match;
+        else if (g->members[i].role == QREF_ROLE_WITNESS) wm[nw++] = g->members[i].match;
+    }
+    leader_log_ud ud;
+    qref_log l = log_view(g, &ud);
+    int rc = qref_try_commit(rm, nr, wm, nw, &l, g->term, NULL);
+    if (rc == QREF_PANIC) return rc;
+    g->committed = l.committed;
+    return rc;
+}
+
+static int push_state(qref_group *g, qref_step_out *o, int reason) {
+    if (o->n_states >= QREF_STEP_MAX_OUT) return QREF_PANIC;
+    o->states[o->n_states].term = g->term;
+    o->states[o->n_states].state = (uint32_t)g->state;
+    o->states[o->n_states].reason = (uint32_t)reason;
+    o->n_states++;
+    return QREF_OK;
+}
+
+/* raft.reset (raft.go:991-1010): votes, readIndex and every remote (resetRemotes/Observers/
+ * Witnesses :1025-1059: match 0 except the node itself at lastIndex, active false) */
+static void reset(qref_group *g, uint64_t term) {
+    if (g->term != term) g->term = term;   /* vote = NoLeader: not modelled */
+    qref_votes_reset(&g->votes);
+    qref_ri_init(&g->ri);
+    for (int i = 0; i < g->n_members; i++) {
+        g->members[i].match = g->members[i].node_id == g->node_id ? g->last : 0;
+        g->members[i].active = 0;
+    }
+}
+
+static int become_follower(qref_group *g, uint64_t term, qref_step_out *o, int reason) {
+    g->state = QREF_FOLLOWER;                                        /* raft.go:949-957 */
+    reset(g, term);
+    return push_state(g, o, reason);
+}
+
+/* raft.appendEntries (raft.go:911-922): entries get r.term and follow lastIndex; the node's own
+ * remote follows the log; a single-node quorum commits at once */
+static int append_entries(qref_group *g, uint64_t n) {
+    g->last += n;
+    int self = find_member(g, g->node_id);
+    if (self >= 0 && g->members[self].match < g->last) g->members[self].match = g->last;
+    if (qref_is_single_node_quorum(n_voting(g))) {
+        int rc = try_commit(g);
+        if (rc == QREF_PANIC) return rc;
+    }
+    return QREF_OK;
+}
+
+static int become_leader(qref_group *g, qref_step_out *o) {
+    g->state = QREF_LEADER;                                          /* raft.go:977-989 */
+    reset(g, g->term);
+    int rc = push_state(g, o, QREF_REASON_VOTE);
+    if (rc) return rc;
+    g->term_start = g->last + 1;   /* the no-op of p72 is the first entry of the new term */
+    return append_entries(g, 1);
+}
+
+static int add_ready(qref_step_out *o, uint64_t index, uint64_t low, uint64_t high) {
+    if (o->n_ready >= QREF_STEP_MAX_OUT) return QREF_PANIC;
+    o->ready[o->n_ready].index = index;
+    o->ready[o->n_ready].low = low;
+    o->ready[o->n_ready].high = high;
+    o->n_ready++;
+    return QREF_OK;
+}
+
+static int add_resp(qref_step_out *o, uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
+    if (o->n_resps >= QREF_STEP_MAX_OUT) return QREF_PANIC;
+    o->resps[o->n_resps].to = to;
+    o->resps[o->n_resps].index = index;
+    o->resps[o->n_resps].hint = hint;
+    o->resps[o->n_resps].hint_high = high;
+    o->n_resps++;
+    return QREF_OK;
+}
+
+static int add_dropped(qref_step_out *o, const qref_event *e, int reason) {
+    if (o->n_dropped >= QREF_STEP_MAX_OUT) return QREF_PANIC;
+    o->dropped[o->n_dropped].low = e->hint;
+    o->dropped[o->n_dropped].high = e->hint_high;
+    o->dropped[o->n_dropped].from = e->from;
+    o->dropped[o->n_dropped].reason = (uint32_t)reason;
+    o->n_dropped++;
+    return QREF_OK;
+}
+
+static int defer_event(qref_step_out *o, int i) {
+    if (o->n_deferred >= QREF_STEP_MAX_OUT) return QREF_PANIC;
+    o->deferred[o->n_deferred++] = (uint32_t)i;
+    return QREF_OK;
+}
+
+/* raft.hasCommittedEntryAtCurrentTerm (raft.go:1612-1621) */
+static int has_committed_entry_at_current_term(qref_group *g) {
+    leader_log_ud ud;
+    qref_log l = log_view(g, &ud);
+    return qref_log_term(&l, g->committed) == g->term;
+}
+
+/* raft.handleLeaderReadIndex (raft.go:1636-1669) */
+static int leader_read_index(qref_group *g, const qref_event *e, qref_step_out *o) {
+    qref_sysctx ctx = {e->hint, e->hint_high};
+    if (role_of(g, e->from) == QREF_ROLE_WITNESS) return add_dropped(o, e, QREF_DROP_WITNESS);
+    if (!qref_is_single_node_quorum(n_voting(g))) {
+        if (!has_committed_entry_at_current_term(g)) return add_dropped(o, e, QREF_DROP_NOT_READY);
+        return qref_ri_add_request(&g->ri, g->committed, ctx, e->from);
+    }
+    int rc = add_ready(o, g->committed, ctx.low, ctx.high);
+    if (rc) return rc;
+    if (e->from != g->node_id && role_of(g, e->from) == QREF_ROLE_OBSERVER)
+        return add_resp(o, e->from, g->committed, e->hint, e->hint_high);
+    return QREF_OK;
+}
+
+/* raft.handleReadIndexLeaderConfirmation (raft.go:1740-1760) */
+static int read_index_confirmation(qref_group *g, const qref_event *e, qref_step_out *o) {
+    static qref_read_status out[QREF_MAX_PENDING];
+    qref_sysctx ctx = {e->hint, e->hint_high};
+    int r = qref_ri_confirm(&g->ri, ctx, e->from, quorum(g), out);
+    if (r < 0) return r;
+    for (int i = 0; i < r; i++) {
+        int rc = (out[i].from == 0 || out[i].from == g->node_id)
+                     ? add_ready(o, out[i].index, out[i].ctx.low, out[i].ctx.high)
+                     : add_resp(o, out[i].from, out[i].index, e->hint, e->hint_high);
+        if (rc) return rc;
+    }
+    return QREF_OK;
+}
+
+/* raft.campaign (raft.go:1082-1117) after becomeCandidate (:959-975) */
+static int campaign(qref_group *g, qref_step_out *o) {
+    g->state = QREF_CANDIDATE;
+    reset(g, g->term + 1);
+    int rc = push_state(g, o, QREF_REASON_CAMPAIGN);
+    if (rc) return rc;
+    qref_handle_vote_resp(&g->votes, g->node_id, 0);
+    if (qref_is_single_node_quorum(n_voting(g))) return become_leader(g, o);
+    return QREF_OK;
+}
+
+static int handle_message(qref_group *g, const qref_event *e, int i, qref_step_out *o) {
+    /* Peer.Handle (peer.go:186-198): responses from non-members are dropped */
+    if (is_response_type(e->type) && find_member(g, e->from) < 0) return QREF_OK;
+    /* raft.onMessageTermNotMatched (raft.go:1416-1452); none of the types here is a leader
+     * message, so a higher term makes the node a follower with no known leader */
+    if (e->term != 0 && e->term != g->term) {
+        if (e->term < g->term) return QREF_OK;                       /* ignored */
+        int rc = become_follower(g, e->term, o, QREF_REASON_HIGHER_TERM);
+        if (rc) return rc;
+    }
+    const int self_state = g->state;
+    int m = find_member(g, e->from);
+    if (self_state == QREF_LEADER) {
+        switch (e->type) {
+        case MT_REPLICATE_RESP: {                                    /* lw + :1671-1700 */
+            qref_member *rp = &g->members[m];
+            rp->active = 1;
+            if (!e->reject && rp->match < e->log_index) {            /* remote.tryUpdate */
+                rp->match = e->log_index;
+                int rc = try_commit(g);
+                if (rc == QREF_PANIC) return rc;
+            }
+            return QREF_OK;
+        }
+        case MT_HEARTBEAT_RESP:                                      /* lw + :1702-1714 */
+            g->members[m].active = 1;
+            if (e->hint != 0) return read_index_confirmation(g, e, o);
+            return QREF_OK;
+        case MT_READ_INDEX:
+            return leader_read_index(g, e, o);
+        default:
+            return QREF_OK;   /* no leader handler (RequestVoteResp) */
+        }
+    }
+    if (self_state == QREF_CANDIDATE && e->type == MT_REQUEST_VOTE_RESP) {
+        int st = qref_candidate_vote_resp(&g->votes, e->from, e->reject != 0,
+                                          role_of(g, e->from) == QREF_ROLE_OBSERVER, quorum(g));
+        if (st == QREF_LEADER) return become_leader(g, o);
+        if (st == QREF_FOLLOWER) return become_follower(g, g->term, o, QREF_REASON_VOTE);
+        return QREF_OK;
+    }
+    /* follower / candidate ReadIndex: forwarded to the leader or dropped outside the quorum
+     * path (raft.go:1875-1883, 1937-1945) */
+    if (e->type == MT_READ_INDEX) return defer_event(o, i);
+    return QREF_OK;
+}
+
+int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64_t term,
+                    int state, uint64_t committed, uint64_t last, uint64_t term_start,
+                    const qref_member *members, int n_members) {
+    if (!g || n_members < 1 || n_members > QREF_STEP_MAX_MEMBERS || (n_members && !members))
+        return -1;
+    memset(g, 0, sizeof *g);
+    g->cluster_id = cluster_id;
+    g->node_id = node_id;
+    g->term = term;
+    g->state = state;
+    g->committed = committed;
+    g->last = last;
+    g->term_start = term_start;
+    g->n_members = n_members;
+    memcpy(g->members, members, (size_t)n_members * sizeof *members);
+    qref_ri_init(&g->ri);
+    qref_votes_reset(&g->votes);
+    /* a candidate holds its own vote (campaign, raft.go:1093) */
+    if (state == QREF_CANDIDATE) qref_handle_vote_resp(&g->votes, node_id, 0);
+    return 0;
+}
+
+int qref_group_step(qref_group *g, const qref_event *ev, int n_events, qref_step_out *o) {
+    if (!g || !o || (n_events && !ev)) return -1;
+    memset(o, 0, sizeof *o);
+    const uint64_t committed0 = g->committed;
+    for (int i = 0; i < n_events; i++) {
+        const qref_event *e = &ev[i];
+        int rc = QREF_OK;
+        switch (e->kind) {
+        case QREF_EV_READ: {       /* Peer.ReadIndex: a ReadIndex message with From = NoNode */
+            qref_event m = *e;
+            m.type = MT_READ_INDEX;
+            m.from = 0;
+            m.term = 0;
+            rc = handle_message(g, &m, i, o);
+            break;
+        }
+        case QREF_EV_MSG:
+            rc = handle_message(g, e, i, o);
+            break;
+        case QREF_EV_CHECK_QUORUM:                                   /* raft.go:1582-1588 */
+            if (g->state == QREF_LEADER) {
+                uint64_t ids[QREF_STEP_MAX_MEMBERS];
+                int act[QREF_STEP_MAX_MEMBERS], idx[QREF_STEP_MAX_MEMBERS], n = 0;
+                for (int k = 0; k < g->n_members; k++) {
+                    if (g->members[k].role == QREF_ROLE_OBSERVER) continue;
+                    ids[n] = g->members[k].node_id;
+                    act[n] = g->members[k].active;
+                    idx[n++] = k;
+                }
+                int ok = qref_leader_has_quorum(ids, act, n, g->node_id);
+                for (int k = 0; k < n; k++) g->members[idx[k]].active = act[k];
+                if (!ok) rc = become_follower(g, g->term, o, QREF_REASON_CHECK_QUORUM);
+            }
+            break;
+        case QREF_EV_CAMPAIGN:                                       /* raft.go:1485-1515 */
+            if (g->state != QREF_LEADER) rc = campaign(g, o);
+            break;
+        case QREF_EV_PROPOSE:                                        /* raft.go:1590-1610 */
+            if (g->state == QREF_LEADER) rc = append_entries(g, e->log_index);
+            else rc = defer_event(o, i);   /* forwarded / dropped (raft.go:1845-1857, 1932) */
+            break;
+        default:
+            return -1;
+        }
+        if (rc < 0) return rc;
+    }
+    o->committed = g->committed;
+    o->commit_changed = g->committed != committed0;
+    return 0;
+}

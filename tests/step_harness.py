@@ -1,0 +1,146 @@
+"""Shared driver for step-level tests: the same per-group event streams run through the CPU oracle
+(oracle/qref_step.c, one event at a time as the reference does) or through the GPU step worker
+(hq_worker_step), with results split per group in one format.
+
+An event is a tuple, listed per group in node.handleEvents order (node.go:1113-1157):
+  ("read", ctx_low, ctx_high)                                     local ReadIndex
+  ("msg", type, from, term, log_index, hint, hint_high, reject)    received message
+  ("check_quorum",) / ("campaign",)                                tick messages
+  ("propose", n_entries)                                           proposal
+"""
+import numpy as np
+
+PHASE = {"read": 0, "msg": 1, "check_quorum": 2, "campaign": 2, "propose": 3}
+
+
+def check_phase_order(events):
+    ph = [PHASE[e[0]] for e in events]
+    assert ph == sorted(ph), events
+
+
+class OracleBackend:
+    def __init__(self):
+        from oracle import qref
+
+        self.qref = qref
+        self.groups = {}
+
+    def add_group(self, cid, node, term, state, committed, last, term_start, members):
+        self.groups[cid] = self.qref.StepGroup(cid, node, term, state, committed, last,
+                                               term_start, members)
+
+    def step(self, per_group):
+        out = {}
+        for cid, events in per_group.items():
+            check_phase_order(events)
+            r = self.groups[cid].step(events)
+            assert isinstance(r, dict), (cid, r, events)
+            out[cid] = r
+        return out
+
+    def state(self, cid):
+        return self.groups[cid].state()
+
+
+class WorkerBackend:
+    def __init__(self, hq, n_max=8, seed=0, worker=None):
+        self.hq = hq
+        self.w = worker if worker is not None else hq.Worker(0, n_max)
+        self.rng = np.random.default_rng(seed)
+        self.cids = []
+        self.last_passes = 0
+        self.last_decisions = 0
+
+    def close(self):
+        self.w.close()
+
+    def add_group(self, cid, node, term, state, committed, last, term_start, members):
+        self.w.add_group(cid, node, term, state, committed, last, term_start, members)
+        self.cids.append(cid)
+
+    def build_inputs(self, per_group):
+        """Arrays for hq_worker_step; messages of different groups are interleaved at random
+        (per-group order kept). Returns (arrays, refs) with refs[(array, index)] = (cid, pos)."""
+        hq = self.hq
+        reads, ticks, props, msg_lists = [], [], [], []
+        refs = {}
+        for cid, events in per_group.items():
+            check_phase_order(events)
+            ml = []
+            for pos, e in enumerate(events):
+                k = e[0]
+                if k == "read":
+                    refs[(hq.EVT_READ, len(reads))] = (cid, pos)
+                    reads.append((cid, e[1], e[2]))
+                elif k == "msg":
+                    ml.append((pos, (cid, e[2], e[3], e[4], e[5], e[6], e[1], e[7])))
+                elif k in ("check_quorum", "campaign"):
+                    refs[(hq.EVT_TICK, len(ticks))] = (cid, pos)
+                    kind = hq.TICK_CHECK_QUORUM if k == "check_quorum" else hq.TICK_ELECTION
+                    ticks.append((cid, kind, 0))
+                else:
+                    refs[(hq.EVT_PROPOSAL, len(props))] = (cid, pos)
+                    props.append((cid, e[1]))
+            if ml:
+                msg_lists.append(ml)
+        # random interleaving of the groups' message streams
+        order = np.concatenate([np.full(len(ml), i) for i, ml in enumerate(msg_lists)]) \
+            if msg_lists else np.zeros(0, int)
+        self.rng.shuffle(order)
+        cursors = [0] * len(msg_lists)
+        msgs = []
+        for i in order:
+            pos, rec = msg_lists[i][cursors[i]]
+            cursors[i] += 1
+            refs[(hq.EVT_MSG, len(msgs))] = (rec[0], pos)
+            msgs.append(rec)
+        arrs = (np.array(reads, hq.READ_REQUEST_DTYPE), np.array(msgs, hq.MESSAGE_DTYPE),
+                np.array(ticks, hq.TICK_DTYPE), np.array(props, hq.PROPOSAL_DTYPE))
+        return arrs, refs
+
+    def step(self, per_group):
+        arrs, refs = self.build_inputs(per_group)
+        res = self.w.step(*arrs)
+        self.last_passes, self.last_decisions = res["gpu_passes"], res["decisions"]
+        self.last_raw = res
+        out = {cid: {"ready": [], "resps": [], "states": [], "dropped": [], "deferred": [],
+                     "commit_changed": False} for cid in per_group}
+        for r in res["ready"]:
+            out[int(r["cluster_id"])]["ready"].append(
+                (int(r["index"]), int(r["ctx_low"]), int(r["ctx_high"])))
+        for r in res["read_resps"]:
+            out[int(r["cluster_id"])]["resps"].append(
+                (int(r["to"]), int(r["log_index"]), int(r["hint"]), int(r["hint_high"])))
+        for r in res["state_changes"]:
+            out[int(r["cluster_id"])]["states"].append(
+                (int(r["term"]), int(r["state"]), int(r["reason"])))
+        for r in res["dropped_reads"]:
+            out[int(r["cluster_id"])]["dropped"].append(
+                (int(r["ctx_low"]), int(r["ctx_high"]), int(r["from"]), int(r["reason"])))
+        for r in res["deferred"]:
+            cid, pos = refs[(int(r["array"]), int(r["index"]))]
+            out[cid]["deferred"].append(pos)
+        for cid in out:
+            out[cid]["deferred"].sort()
+        for r in res["commits"]:
+            out[int(r["cluster_id"])]["commit_changed"] = True
+        for cid in out:
+            out[cid]["committed"] = int(self.w.get_group(cid)[0]["committed"])
+        out["_fallback"] = [int(x) for x in res["fallback_groups"]]
+        return out
+
+    def state(self, cid):
+        g, m, r = self.w.get_group(cid)
+        members = [(int(x["node_id"]), int(x["match"]), int(x["role"]), int(x["active"]))
+                   for x in m]
+        reads = [(int(x["index"]), int(x["from"]), (int(x["ctx_low"]), int(x["ctx_high"])),
+                  int(x["n_confirmed"])) for x in r]
+        return (int(g["term"]), int(g["state"]), int(g["committed"]), int(g["last_index"]),
+                int(g["term_start"]), members, reads)
+
+
+def same_step(oracle_out, worker_out, cid):
+    """Per-group step results must be identical."""
+    o, w = oracle_out[cid], worker_out[cid]
+    for k in ("committed", "commit_changed", "ready", "resps", "states", "dropped", "deferred"):
+        assert o[k] == w[k], (cid, k, o[k], w[k])

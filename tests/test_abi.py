@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == 1
+    assert hq.lib.hq_abi_version() == 2
 
 
 LAYOUT_C = r"""
@@ -114,3 +114,14 @@ def test_kernels_are_gfx950(hq):
     blob = open(hq.LIB_PATH, "rb").read()
     targets = set(re.findall(rb"amdgcn-amd-amdhsa-+(gfx[0-9a-z]+)", blob))
     assert targets == {b"gfx950"}, targets
+
+
+def test_worker_without_gpu_fails_cleanly(hq):
+    if hq.device_count() > 0:
+        pytest.skip("a GPU is visible: covered by tests/test_gpu_worker.py")
+    with pytest.raises(hq.HQError) as e:
+        hq.Worker(0, 5)
+    assert e.value.code == hq.HQ_E_DEVICE
+    assert hq.lib.hq_worker_open(0, 0, ctypes.byref(ctypes.c_void_p())) == hq.HQ_E_INVAL
+    assert hq.lib.hq_worker_step(None, None, None) == hq.HQ_E_INVAL
+    hq.lib.hq_worker_close(None)   # no-op

@@ -1,0 +1,135 @@
+"""The GPU step worker (hq_worker_*, dragonboat_amd/csrc/hq_worker.cpp) against the sequential
+step oracle (oracle/qref_step.c): the reference's raft-level tests restated as step scenarios,
+then random multi-step differential runs over thousands of groups. Every quorum decision of the
+worker is a kernel launch; results must be identical to the reference processing the same events
+one at a time."""
+import numpy as np
+import pytest
+
+import step_random as sr
+import step_scenarios as sc
+from step_harness import OracleBackend, WorkerBackend, same_step
+
+pytestmark = pytest.mark.gpu
+CASES = list(sc.all_cases())
+
+
+@pytest.fixture(scope="module")
+def worker_backend(hq):
+    b = WorkerBackend(hq, n_max=8, seed=1)
+    yield b
+    b.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_reference_scenario_on_gpu(worker_backend, case):
+    outs, state = sc.run_case(worker_backend, case)
+    sc.check_case(case, outs, state)
+    want_outs, want_state = sc.run_case(OracleBackend(), case)
+    assert state == want_state, case["name"]
+    for w, o in zip(outs, want_outs):
+        for k in ("committed", "commit_changed", "ready", "resps", "states", "dropped",
+                  "deferred"):
+            assert w[k] == o[k], (case["name"], k, w[k], o[k])
+
+
+def test_one_gpu_pass_per_plain_step(hq):
+    """Commit + ReadIndex acks + CheckQuorum of many groups: one GPU batch per step."""
+    b = WorkerBackend(hq, n_max=5)
+    try:
+        for cid in range(1, 101):
+            b.add_group(cid, 1, 3, sc.LEADER, 10, 12, 10,
+                        [(i, 12 if i == 1 else 10, sc.REMOTE, 0) for i in range(1, 6)])
+        out = b.step({cid: [sc.msg(sc.RREP, 2, 3, 12), sc.msg(sc.RREP, 3, 3, 11),
+                            ("check_quorum",)] for cid in range(1, 101)})
+        assert b.last_passes == 1 and b.last_decisions == 200
+        assert all(out[cid]["committed"] == 11 for cid in range(1, 101))
+        assert all(out[cid]["states"] == [] for cid in range(1, 101))
+    finally:
+        b.close()
+
+
+@pytest.mark.parametrize("seed,G,steps", [(1, 3000, 6), (2, 1500, 10), (3, 400, 25)])
+def test_random_differential(hq, seed, G, steps):
+    rng = np.random.default_rng(seed)
+    groups = sr.random_groups(rng, G)
+    o, w = OracleBackend(), WorkerBackend(hq, n_max=8, seed=seed)
+    try:
+        for g in groups:
+            o.add_group(*g)
+            w.add_group(*g)
+        ctx_seq = [0]
+        seen = dict(ready=0, resps=0, states=0, dropped=0, deferred=0, commit=0)
+        passes = []
+        for s in range(steps):
+            per = {}
+            for g in groups:
+                if rng.random() < 0.85:
+                    per[g[0]] = sr.random_events(rng, o.state(g[0]), s + 1, ctx_seq)
+            want = o.step(per)
+            got = w.step(per)
+            passes.append(w.last_passes)
+            assert got["_fallback"] == []
+            for cid in per:
+                same_step(want, got, cid)
+                seen["commit"] += want[cid]["commit_changed"]
+                for k in ("ready", "resps", "states", "dropped", "deferred"):
+                    seen[k] += len(want[cid][k])
+            for g in groups:
+                assert w.state(g[0]) == o.state(g[0]), (s, g[0])
+        # the streams exercised every output kind, and runs cut by barriers (several passes)
+        assert all(v > 0 for v in seen.values()), seen
+        assert max(passes) >= 2, passes
+    finally:
+        w.close()
+
+
+def test_fallback_suspends_and_resync_resumes(hq):
+    """An observer acknowledging a pending ctx cannot be taken by the slot model: the group is
+    suspended from that event on (its tail deferred) and resumes after hq_worker_set_group."""
+    w = hq.Worker(0, 8)
+    try:
+        mem = [(i, 9, sc.REMOTE, 0) for i in range(1, 6)] + [(6, 0, sc.OBSERVER, 0)]
+        w.add_group(7, 1, 2, sc.LEADER, 9, 9, 9, mem)
+        b = WorkerBackend(hq, worker=w)
+        out = b.step({7: [("read", 5, 6), sc.msg(sc.HBRESP, 2, 2, hint=5, high=6),
+                          sc.msg(sc.HBRESP, 6, 2, hint=5, high=6), sc.msg(sc.RREP, 2, 2, 9),
+                          ("propose", 1)]})
+        assert out["_fallback"] == [7]
+        assert out[7]["deferred"] == [2, 3, 4]
+        g, m, r = w.get_group(7)
+        assert g["suspended"] == 1 and len(r) == 1 and r[0]["n_confirmed"] == 1
+        out = b.step({7: [("propose", 1)]})
+        assert out[7]["deferred"] == [0]       # still suspended
+        w.set_group(7, 1, 2, sc.LEADER, 9, 10, 9, [(1, 10, 0, 0), (2, 10, 0, 0), (3, 9, 0, 0),
+                                                   (4, 9, 0, 0), (5, 9, 0, 0), (6, 0, 1, 0)])
+        out = b.step({7: [sc.msg(sc.RREP, 3, 2, 10)]})
+        assert out["_fallback"] == [] and out[7]["committed"] == 10
+    finally:
+        w.close()
+
+
+def test_ack_above_last_index_is_fallback(hq):
+    w = hq.Worker(0, 4)
+    try:
+        w.add_group(1, 1, 2, sc.LEADER, 5, 6, 5, [(1, 6, 0, 0), (2, 5, 0, 0), (3, 5, 0, 0)])
+        b = WorkerBackend(hq, worker=w)
+        out = b.step({1: [sc.msg(sc.RREP, 2, 2, 6), sc.msg(sc.RREP, 3, 2, 7)]})
+        assert out["_fallback"] == [1] and out[1]["deferred"] == [1]
+        assert out[1]["committed"] == 6        # decided up to the offending message
+    finally:
+        w.close()
+
+
+def test_add_group_validation(hq):
+    w = hq.Worker(0, 3)
+    try:
+        with pytest.raises(hq.HQError, match="n_max"):
+            w.add_group(1, 1, 1, 0, 0, 0, 0, [(i, 0, 0, 0) for i in range(1, 5)])
+        with pytest.raises(hq.HQError, match="remotes"):
+            w.add_group(2, 9, 1, 0, 0, 0, 0, [(1, 0, 0, 0)])
+        w.add_group(3, 1, 1, 0, 0, 0, 0, [(1, 0, 0, 0)])
+        with pytest.raises(hq.HQError, match="exists"):
+            w.add_group(3, 1, 1, 0, 0, 0, 0, [(1, 0, 0, 0)])
+    finally:
+        w.close()

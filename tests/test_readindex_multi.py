@@ -31,6 +31,7 @@ def closed_form(ord_, idx, K, n, K_max, n_max, G):
     idx = idx.reshape(K_max, G)
     rel = np.full((K_max, G), U64MAX)
     cnt = np.zeros(G, np.uint8)
+    bend = np.zeros(G, np.uint8)
     for g in range(G):
         q = int(n[g]) // 2 + 1
         r = max(q - 1, 1)
@@ -45,7 +46,9 @@ def closed_form(ord_, idx, K, n, K_max, n_max, G):
             if best is not None:
                 rel[k, g] = idx[best[1], g]
                 cnt[g] += 1
-    return rel.reshape(-1), cnt
+                if best[1] == k:
+                    bend[g] |= 1 << k
+    return rel.reshape(-1), cnt, bend
 
 
 def test_reference_table_as_batch():
@@ -54,27 +57,30 @@ def test_reference_table_as_batch():
     ord_ = np.full((K_max, n_max, G), NONE, np.uint16)
     ord_[1, 0, 0], ord_[1, 2, 0] = 1, 2          # from 1 -> slot 0, from 3 -> slot 2
     idx = np.array([[3], [4], [5]], np.uint64)
-    rel, cnt, fb = qref.readindex_multi_batch(ord_.reshape(-1), idx.reshape(-1), None, None, 5,
-                                              K_max, n_max)
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ord_.reshape(-1), idx.reshape(-1), None, None,
+                                                    5, K_max, n_max)
     assert list(rel) == [4, 4, int(U64MAX)] and cnt[0] == 2 and fb[0] == 0
+    assert bend[0] == 0b010    # one confirm() released ctx2 and ctx: ctx closes the batch
 
 
 def test_oracle_replay_equals_closed_form():
     rng = np.random.default_rng(5)
     G, K_max, n_max = 3000, 6, 7
     ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
-    rel, cnt, fb = qref.readindex_multi_batch(ord_, idx, K, n, 0, K_max, n_max)
-    want_rel, want_cnt = closed_form(ord_, idx, K, n, K_max, n_max, G)
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ord_, idx, K, n, 0, K_max, n_max)
+    want_rel, want_cnt, want_bend = closed_form(ord_, idx, K, n, K_max, n_max, G)
     assert not fb.any()
     np.testing.assert_array_equal(rel, want_rel)
     np.testing.assert_array_equal(cnt, want_cnt)
+    np.testing.assert_array_equal(bend, want_bend)
     assert 0 < cnt.astype(int).sum() < K.astype(int).sum()
 
 
 def test_decreasing_index_is_fallback():
     ord_ = np.full(2 * 3, NONE, np.uint16)
-    rel, cnt, fb = qref.readindex_multi_batch(ord_, np.array([5, 4], np.uint64), None, None, 3, 2, 3)
-    assert fb[0] == 1 and cnt[0] == 0
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ord_, np.array([5, 4], np.uint64), None, None,
+                                                    3, 2, 3)
+    assert fb[0] == 1 and cnt[0] == 0 and bend[0] == 0
 
 
 @pytest.mark.gpu
@@ -84,14 +90,17 @@ def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G):
     ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
     n[::97] = 0                                   # invalid n -> fallback
     idx.reshape(K_max, G)[:, 5] = np.arange(K_max, 0, -1)   # decreasing -> fallback
-    want_rel, want_cnt, want_fb = qref.readindex_multi_batch(ord_, idx, K, n, 0, K_max, n_max)
+    want_rel, want_cnt, want_fb, want_bend = qref.readindex_multi_batch(ord_, idx, K, n, 0, K_max,
+                                                                        n_max)
     d = [gpu_ctx.upload(x) for x in (ord_, idx, K, n)]
     rel = gpu_ctx.empty(K_max * G, np.uint64)
     cnt = gpu_ctx.empty(G, np.uint8)
+    bend = gpu_ctx.empty(G, np.uint8)
     fb = gpu_ctx.empty(hq.words64(G), np.uint64)
-    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], 0, rel, cnt, fb)
+    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], 0, rel, cnt, fb, bend)
     np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
     np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
     np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
-    for x in d + [rel, cnt, fb]:
+    np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
+    for x in d + [rel, cnt, bend, fb]:
         gpu_ctx.free(x)
