@@ -17,6 +17,7 @@ duration measured with HIP events on the launching stream over the timed region;
 `cpu_baseline` = the C restatement (oracle/qref.c, test infrastructure) timed on this host.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -293,6 +294,123 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
     }
 
 
+def step_groups(hq, G, cid_base, cid_stride, last0=1000):
+    """Leader groups of the step workload: 3 voters (node 1 leads), term 5, all caught up."""
+    cids = np.uint64(cid_base) + np.arange(G, dtype=np.uint64) * np.uint64(cid_stride)
+    g = np.zeros(G, hq.WORKER_GROUP_DTYPE)
+    g["cluster_id"], g["node_id"], g["term"], g["state"] = cids, 1, 5, hq.STATE_LEADER
+    g["committed"], g["last_index"], g["term_start"], g["n_members"] = last0, last0, last0 - 10, 3
+    m = np.zeros(3 * G, hq.MEMBER_DTYPE)
+    m["node_id"] = np.tile(np.array([1, 2, 3], np.uint64), G)
+    m["match"] = last0
+    return g, m, cids
+
+
+def step_events(hq, G, s, last0=1000):
+    """Step s of the steady-state leader workload, as hq_step_input rows (every group, in
+    handle order): every 4th group serves a local ReadIndex; both followers ack the leader's
+    previous append (ReplicateResp) and answer a heartbeat (the ReadIndex groups' heartbeats
+    carry the ctx); every group proposes one entry. Per group: 4 messages, 1 proposal, 1/4 read
+    -> 1 commit decision and 1/4 ReadIndex decision."""
+    last_s = np.uint64(last0 + s)
+    has_read = (np.arange(G) % 4) == 0
+    per = 5 + has_read.astype(np.int64)
+    offsets = np.zeros(G + 1, np.uint64)
+    offsets[1:] = np.cumsum(per)
+    ev = np.zeros(int(offsets[-1]), hq.EVENT_DTYPE)
+    base = offsets[:-1].astype(np.int64)
+    ctx_low = (np.uint64(s + 1) << np.uint64(32)) | np.arange(G, dtype=np.uint64)
+    rd = np.nonzero(has_read)[0]
+    r = ev[base[rd]]                                   # node.handleReadIndex
+    r["kind"], r["hint"], r["hint_high"] = hq.EV_READ, ctx_low[rd], s + 1
+    ev[base[rd]] = r
+    first_msg = base + has_read
+    for k, (frm, typ) in enumerate(((2, 13), (3, 13), (2, 18), (3, 18))):
+        idx = first_msg + k
+        blk = ev[idx]
+        blk["kind"], blk["type"], blk["from"], blk["term"] = hq.EV_MESSAGE, typ, frm, 5
+        if typ == 13:
+            blk["log_index"] = last_s
+        else:
+            blk["hint"] = np.where(has_read, ctx_low, 0)
+            blk["hint_high"] = np.where(has_read, s + 1, 0)
+        ev[idx] = blk
+    p = ev[first_msg + 4]
+    p["kind"], p["log_index"] = hq.EV_PROPOSE, 1
+    ev[first_msg + 4] = p
+    return np.arange(G, dtype=np.uint32), offsets, ev
+
+
+def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
+    assert cpu_steps <= steps
+    """The step worker end to end (hq_worker_step): host bookkeeping of every event plus the
+    GPU passes, against the event-by-event C restatement of the reference (oracle, CPU) on the
+    same events; the committed sums of both must agree."""
+    from dragonboat_amd import hipquorum as hq
+    from dragonboat_amd import shard
+
+    rng = shard.rank_shard(d.rank, d.world, G)
+    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride)
+    w = hq.Worker(d.device, 3)
+    w.add_groups(g, m)                   # handles 0 .. G-1 in cids order
+    t_total, acc = 0.0, dict(handle_ns=0, pass_ns=0, gpu_passes=0, decisions=0)
+    n_events = 0
+    committed_gpu = None
+    for s in range(steps + 1):
+        ev = step_events(hq, G, s)
+        t0 = time.perf_counter()
+        res = w.step(*ev)
+        dt = time.perf_counter() - t0
+        if s == cpu_steps:   # state checked against the CPU replay of the same steps
+            committed_gpu = [int(w.get_group(int(c))[0]["committed"]) for c in cids[:4096]]
+        if s == 0:
+            continue                      # warm-up: allocations and first-touch
+        t_total += dt
+        n_events += len(ev[2])
+        for k in acc:
+            acc[k] += res[k]
+    w.close()
+    elapsed = d.max(t_total)
+    out = {
+        "workload": f"step: hq_worker_step over {G} leader groups x 3 voters per GPU; per group "
+                    f"and step 4 messages (2 ReplicateResp, 2 HeartbeatResp), 1 proposal, 1/4 "
+                    f"local ReadIndex; one worker (one host thread)",
+        "value": d.sum(float(n_events)) / elapsed, "unit": "events/s",
+        "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
+        "ms_per_step": elapsed / steps * 1e3,
+        "gpu_passes_per_step": acc["gpu_passes"] / steps,
+        "host_ms_per_step": acc["handle_ns"] / steps / 1e6,
+        "gpu_pass_ms_per_step": acc["pass_ns"] / steps / 1e6,
+    }
+    if with_cpu and d.rank == 0 and d.world == 1:
+        from oracle import qref
+
+        threads = min(16, os.cpu_count() or 1)
+        cpu = {}
+        for nt in (1, threads):
+            b = qref.StepBatch(g, m)
+            tc, ne = 0.0, 0
+            for s in range(cpu_steps + 1):
+                ev = step_events(hq, G, s)
+                t0 = time.perf_counter()
+                b.step(*ev, nthreads=nt)
+                if s > 0:
+                    tc += time.perf_counter() - t0
+                    ne += len(ev[2])
+            committed_cpu = [b.committed(i) for i in range(min(G, 4096))]
+            b.close()
+            cpu[nt] = ne / tc
+        out["cpu_reference"] = {
+            "value": cpu[threads], "unit": "events/s", "threads": threads,
+            "single_thread_value": cpu[1],
+            "sample": f"the same events of the first {cpu_steps} steps, replayed event by "
+                      f"event (oracle/qref_step.c, C restatement of the reference path)",
+        }
+        # the same events left the same committed indexes (first 4096 groups)
+        out["parity_committed"] = committed_gpu == committed_cpu
+    return out
+
+
 # ----------------------------------------------------------------------------- CPU leg --------
 def cpu_baseline(w, budget_s=8.0):
     """The oracle (C restatement of the reference path) on a bounded sample of the workload."""
@@ -355,8 +473,10 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--step-groups", type=int, default=1 << 20,
+                    help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c3,c3m,c4,c5,c5r,e2e",
+    ap.add_argument("--extra", default="c3,c3m,c4,c5,c5r,e2e,step",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -368,10 +488,13 @@ def main():
     w = WORKLOADS[args.workload]
     r = run_gpu(w, args.steps, args.warmup, d)
     extras = []
-    e2e = None
+    e2e = step_leg = None
     for name in [x for x in args.extra.split(",") if x and x != args.workload]:
         if name == "e2e":
             e2e = run_e2e(max(20, args.steps // 20), 3, d)
+            continue
+        if name == "step":
+            step_leg = run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu)
             continue
         we = WORKLOADS[name]
         re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
@@ -423,7 +546,7 @@ def main():
                     "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
-            ] + ([e2e] if e2e else []),
+            ] + ([e2e] if e2e else []) + ([step_leg] if step_leg else []),
         }
         print(json.dumps(line), flush=True)
     d.close()

@@ -13,6 +13,7 @@
 // pass continues where they stopped. Plain C++ (no HIP headers): the worker is a client of the
 // same ABI a cgo binding would use.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <new>
 #include <string>
@@ -47,7 +48,7 @@ struct Group {
     // current step
     uint64_t committed0 = 0;
     bool touched = false;
-    size_t ev_begin = 0, ev_end = 0, cursor = 0;
+    uint64_t ev_end = 0, cursor = 0;     // the group's events in the step input
     // current run
     bool commit_due = false, ri_due = false, vote_due = false, cq_due = false;
     uint16_t ord = 0;
@@ -56,12 +57,6 @@ struct Group {
 };
 
 enum Verdict { CONSUMED, BARRIER, FALLBACK };
-
-struct Event {
-    uint32_t array;                      // HQ_EVT_*
-    uint32_t group;
-    uint64_t index;
-};
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -75,8 +70,6 @@ struct hq_worker {
     std::unordered_map<uint64_t, uint32_t> index;   // cluster_id -> group
     // step scratch
     const hq_step_input *in = nullptr;
-    std::vector<Event> events;
-    std::vector<uint32_t> counts;
     std::vector<uint32_t> work, next_work, touched;
     std::vector<uint32_t> l_commit, l_ri, l_vote, l_cq;
     // outputs
@@ -85,7 +78,7 @@ struct hq_worker {
     std::vector<hq_read_index_resp> resps;
     std::vector<hq_state_change> states;
     std::vector<hq_dropped_read> dropped;
-    std::vector<hq_event_ref> deferred;
+    std::vector<uint64_t> deferred;
     std::vector<uint64_t> fallback;
     uint64_t decisions = 0;
     // staging: one pinned host buffer mirrored by one device buffer per pass
@@ -103,9 +96,9 @@ struct hq_worker {
     int reserve(size_t bytes);
     int load_group(Group &g, const hq_worker_group *src, const hq_member *m);
     int step(const hq_step_input *in, hq_step_output *out);
-    Verdict handle(Group &g, uint32_t gi, const Event &e);
-    Verdict read_index(Group &g, uint64_t from, uint64_t low, uint64_t high, const Event &e);
-    void advance(Group &g, uint32_t gi);
+    Verdict handle(Group &g, const hq_event &e, uint64_t ei);
+    Verdict read_index(Group &g, uint64_t from, uint64_t low, uint64_t high, uint64_t ei);
+    void advance(Group &g);
     int run_pass();
     // reference state transitions (host bookkeeping of raft.go:949-1010)
     void reset(Group &g, uint64_t term);
@@ -114,7 +107,7 @@ struct hq_worker {
     void push_state(const Group &g, uint32_t reason) {
         states.push_back({g.cluster_id, g.term, g.state, reason});
     }
-    void defer(const Event &e) { deferred.push_back({e.array, 0, e.index}); }
+    void defer(uint64_t ei) { deferred.push_back(ei); }
     int member_of(const Group &g, uint64_t id) const {
         for (size_t i = 0; i < g.members.size(); ++i)
             if (g.members[i].node_id == id) return (int)i;
@@ -186,10 +179,10 @@ void hq_worker::become_leader(Group &g) {
 
 // ------------------------------------------------------------------------------ events -----
 Verdict hq_worker::read_index(Group &g, uint64_t from, uint64_t low, uint64_t high,
-                              const Event &e) {
+                              uint64_t ei) {
     if (g.state != HQ_STATE_LEADER) {
         if (g.vote_due) return BARRIER;             // the vote may have made it leader
-        defer(e);                                   // forwarded / dropped (raft.go:1875, 1937)
+        defer(ei);                                  // forwarded / dropped (raft.go:1875, 1937)
         return CONSUMED;
     }
     // handleLeaderReadIndex (raft.go:1636-1669)
@@ -232,53 +225,42 @@ static bool is_response_type(uint32_t t) {   // isResponseMessageType (internal/
            t == 8 /* SnapshotStatus */ || t == 9 /* Unreachable */;
 }
 
-Verdict hq_worker::handle(Group &g, uint32_t gi, const Event &e) {
-    (void)gi;
-    switch (e.array) {
-    case HQ_EVT_READ: {
-        const hq_read_request &r = in->reads[e.index];
-        return read_index(g, 0, r.ctx_low, r.ctx_high, e);
-    }
-    case HQ_EVT_TICK: {
-        const hq_tick &t = in->ticks[e.index];
-        if (t.kind == HQ_TICK_CHECK_QUORUM) {
-            if (g.state != HQ_STATE_LEADER) return g.vote_due ? BARRIER : CONSUMED;
-            if (g.cq_due) return BARRIER;
-            g.cq_due = true;
-            return CONSUMED;
-        }
-        if (t.kind == HQ_TICK_ELECTION) {
-            if (g.pending()) return BARRIER;
-            if (g.state == HQ_STATE_LEADER) return CONSUMED;   // leader ignores Election
-            // campaign: becomeCandidate + the self vote (raft.go:959-975, 1082-1095)
-            g.state = HQ_STATE_CANDIDATE;
-            reset(g, g.term + 1);
-            push_state(g, HQ_REASON_CAMPAIGN);
-            g.granted = 1;
-            g.vote_due = true;                      // isSingleNodeQuorum -> the vote kernel
-            return CONSUMED;
-        }
-        return FALLBACK;
-    }
-    case HQ_EVT_PROPOSAL: {
-        const hq_proposal &p = in->proposals[e.index];
+Verdict hq_worker::handle(Group &g, const hq_event &e, uint64_t ei) {
+    switch (e.kind) {
+    case HQ_EV_READ:
+        return read_index(g, 0, e.hint, e.hint_high, ei);
+    case HQ_EV_CHECK_QUORUM:
+        if (g.state != HQ_STATE_LEADER) return g.vote_due ? BARRIER : CONSUMED;
+        if (g.cq_due) return BARRIER;
+        g.cq_due = true;
+        return CONSUMED;
+    case HQ_EV_ELECTION:
+        if (g.pending()) return BARRIER;
+        if (g.state == HQ_STATE_LEADER) return CONSUMED;   // leader ignores Election
+        // campaign: becomeCandidate + the self vote (raft.go:959-975, 1082-1095)
+        g.state = HQ_STATE_CANDIDATE;
+        reset(g, g.term + 1);
+        push_state(g, HQ_REASON_CAMPAIGN);
+        g.granted = 1;
+        g.vote_due = true;                          // isSingleNodeQuorum -> the vote kernel
+        return CONSUMED;
+    case HQ_EV_PROPOSE:
         if (g.pending() && (g.state != HQ_STATE_LEADER || g.cq_due)) return BARRIER;
         if (g.state != HQ_STATE_LEADER) {
-            defer(e);                               // forwarded / dropped (raft.go:1845, 1932)
+            defer(ei);                              // forwarded / dropped (raft.go:1845, 1932)
             return CONSUMED;
         }
         // appendEntries (raft.go:911-922)
-        g.last += p.n_entries;
+        g.last += e.log_index;
         if (g.members[g.self].match < g.last) g.members[g.self].match = g.last;
         if (g.n_voting == 1) g.commit_due = true;
         return CONSUMED;
-    }
-    case HQ_EVT_MSG:
+    case HQ_EV_MESSAGE:
         break;
     default:
         return FALLBACK;
     }
-    const hq_message &m = in->msgs[e.index];
+    const hq_event &m = e;
     if (m.type != HQ_MSG_REPLICATE_RESP && m.type != HQ_MSG_HEARTBEAT_RESP &&
         m.type != HQ_MSG_REQUEST_VOTE_RESP && m.type != HQ_MSG_READ_INDEX)
         return FALLBACK;
@@ -319,7 +301,7 @@ Verdict hq_worker::handle(Group &g, uint32_t gi, const Event &e) {
             return CONSUMED;
         }
         case HQ_MSG_READ_INDEX:
-            return read_index(g, m.from, m.hint, m.hint_high, e);
+            return read_index(g, m.from, m.hint, m.hint_high, ei);
         default:
             return CONSUMED;                        // RequestVoteResp: no leader handler
         }
@@ -337,19 +319,19 @@ Verdict hq_worker::handle(Group &g, uint32_t gi, const Event &e) {
         }
         if (g.vote_due) return BARRIER;             // may be leader by now
     }
-    if (m.type == HQ_MSG_READ_INDEX) return read_index(g, m.from, m.hint, m.hint_high, e);
+    if (m.type == HQ_MSG_READ_INDEX) return read_index(g, m.from, m.hint, m.hint_high, ei);
     return CONSUMED;                                // no handler in this state
 }
 
-void hq_worker::advance(Group &g, uint32_t gi) {
+void hq_worker::advance(Group &g) {
     while (g.cursor < g.ev_end) {
-        const Event &e = events[g.cursor];
+        const uint64_t ei = g.cursor;
         if (g.suspended) {
-            defer(e);
+            defer(ei);
             ++g.cursor;
             continue;
         }
-        const Verdict v = handle(g, gi, e);
+        const Verdict v = handle(g, in->events[ei], ei);
         if (v == BARRIER) return;
         if (v == FALLBACK) {
             g.suspended = true;
@@ -571,7 +553,17 @@ int hq_worker::run_pass() {
 }
 
 // ------------------------------------------------------------------------------ step -------
+namespace {
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+}  // namespace
+
 int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
+    const uint64_t t0 = now_ns();
+    uint64_t t_pass = 0;
     in = inp;
     commits.clear();
     ready.clear();
@@ -583,42 +575,29 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     decisions = 0;
     uint64_t passes = 0;
 
-    // bucket the step's events by group, in node.handleEvents phase order
-    events.clear();
-    touched.clear();
-    auto add = [&](uint32_t array, uint64_t i, uint64_t cid) {
-        auto it = index.find(cid);
-        if (it == index.end()) {                    // not one of this worker's groups
-            deferred.push_back({array, 0, i});
-            return;
-        }
-        events.push_back({array, it->second, i});
-    };
-    for (uint64_t i = 0; i < in->n_reads; ++i) add(HQ_EVT_READ, i, in->reads[i].cluster_id);
-    for (uint64_t i = 0; i < in->n_msgs; ++i) add(HQ_EVT_MSG, i, in->msgs[i].cluster_id);
-    for (uint64_t i = 0; i < in->n_ticks; ++i) add(HQ_EVT_TICK, i, in->ticks[i].cluster_id);
-    for (uint64_t i = 0; i < in->n_proposals; ++i)
-        add(HQ_EVT_PROPOSAL, i, in->proposals[i].cluster_id);
-    // stable counting sort by group
-    counts.assign(groups.size() + 1, 0);
-    for (const Event &e : events) counts[e.group + 1]++;
-    for (size_t i = 0; i < groups.size(); ++i) counts[i + 1] += counts[i];
-    {
-        std::vector<Event> sorted(events.size());
-        std::vector<uint32_t> pos(counts.begin(), counts.end() - 1);
-        for (const Event &e : events) sorted[pos[e.group]++] = e;
-        events.swap(sorted);
-    }
+    // the groups with events, each with its slice of the event array (node.mq per node)
     work.clear();
-    for (size_t gi = 0; gi < groups.size(); ++gi) {
-        if (counts[gi + 1] == counts[gi]) continue;
+    touched.clear();
+    int rc = HQ_OK;
+    for (uint64_t i = 0; i < in->n_groups; ++i) {
+        const uint32_t gi = in->groups[i];
+        const uint64_t b = in->offsets[i], e = in->offsets[i + 1];
+        if (gi >= groups.size()) { rc = fail(HQ_E_INVAL, "hq_worker_step: unknown group handle"); break; }
+        if (e < b) { rc = fail(HQ_E_INVAL, "hq_worker_step: offsets decrease"); break; }
         Group &g = groups[gi];
-        g.ev_begin = g.cursor = counts[gi];
-        g.ev_end = counts[gi + 1];
-        g.committed0 = g.committed;
+        if (g.touched) { rc = fail(HQ_E_INVAL, "hq_worker_step: a group is listed twice"); break; }
         g.touched = true;
-        touched.push_back((uint32_t)gi);
-        work.push_back((uint32_t)gi);
+        g.committed0 = g.committed;
+        touched.push_back(gi);
+        if (b == e) continue;
+        g.cursor = b;
+        g.ev_end = e;
+        g.in_work = true;
+        work.push_back(gi);
+    }
+    if (rc) {
+        for (uint32_t gi : touched) groups[gi].touched = groups[gi].in_work = false;
+        return rc;
     }
 
     while (!work.empty()) {
@@ -629,15 +608,17 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
         for (uint32_t gi : work) {
             Group &g = groups[gi];
             g.in_work = false;
-            advance(g, gi);
+            advance(g);
             if (g.commit_due) l_commit.push_back(gi);
             if (g.ri_due) l_ri.push_back(gi);
             if (g.vote_due) l_vote.push_back(gi);
             if (g.cq_due) l_cq.push_back(gi);
         }
         if (l_commit.empty() && l_ri.empty() && l_vote.empty() && l_cq.empty()) break;
-        int rc = run_pass();
-        if (rc) return rc;
+        const uint64_t tp = now_ns();
+        rc = run_pass();
+        t_pass += now_ns() - tp;
+        if (rc) break;
         ++passes;
         next_work.clear();
         for (const auto *l : {&l_commit, &l_ri, &l_vote, &l_cq})
@@ -653,9 +634,10 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     }
     for (uint32_t gi : touched) {
         Group &g = groups[gi];
-        g.touched = false;
+        g.touched = g.in_work = false;
         if (g.committed != g.committed0) commits.push_back({g.cluster_id, g.committed});
     }
+    if (rc) return rc;
 
     out->commits = commits.data();
     out->n_commits = commits.size();
@@ -673,6 +655,8 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     out->n_fallback_groups = fallback.size();
     out->gpu_passes = passes;
     out->decisions = decisions;
+    out->pass_ns = t_pass;
+    out->handle_ns = now_ns() - t0 - t_pass;
     return HQ_OK;
 }
 
@@ -710,15 +694,43 @@ const char *hq_worker_last_error(const hq_worker *w) {
     return w ? w->err.c_str() : hq_last_error(nullptr);
 }
 
-int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member *members) {
+int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member *members,
+                        uint32_t *handle) {
     if (!w) return HQ_E_INVAL;
     if (!g) return w->fail(HQ_E_INVAL, "hq_worker_add_group: group is NULL");
     if (w->index.count(g->cluster_id)) return w->fail(HQ_E_INVAL, "hq_worker_add_group: cluster exists");
+    if (w->groups.size() >= UINT32_MAX) return w->fail(HQ_E_NOMEM, "hq_worker_add_group: too many groups");
     Group n;
     int rc = w->load_group(n, g, members);
     if (rc) return rc;
-    w->index.emplace(g->cluster_id, (uint32_t)w->groups.size());
+    const uint32_t h = (uint32_t)w->groups.size();
+    w->index.emplace(g->cluster_id, h);
     w->groups.push_back(std::move(n));
+    if (handle) *handle = h;
+    return HQ_OK;
+}
+
+int hq_worker_find(hq_worker *w, uint64_t cluster_id, uint32_t *handle) {
+    if (!w) return HQ_E_INVAL;
+    auto it = w->index.find(cluster_id);
+    if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_find: unknown cluster");
+    if (handle) *handle = it->second;
+    return HQ_OK;
+}
+
+int hq_worker_add_groups(hq_worker *w, const hq_worker_group *groups, uint64_t count,
+                         const hq_member *members) {
+    if (!w) return HQ_E_INVAL;
+    if (count && (!groups || !members))
+        return w->fail(HQ_E_INVAL, "hq_worker_add_groups: NULL argument");
+    w->groups.reserve(w->groups.size() + count);
+    w->index.reserve(w->groups.size() + count);
+    uint64_t off = 0;
+    for (uint64_t i = 0; i < count; ++i) {
+        int rc = hq_worker_add_group(w, groups + i, members + off, nullptr);
+        if (rc) return rc;
+        off += groups[i].n_members;
+    }
     return HQ_OK;
 }
 
@@ -769,9 +781,10 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *out,
 int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
     if (!w) return HQ_E_INVAL;
     if (!in || !out) return w->fail(HQ_E_INVAL, "hq_worker_step: NULL argument");
-    if ((in->n_reads && !in->reads) || (in->n_msgs && !in->msgs) ||
-        (in->n_ticks && !in->ticks) || (in->n_proposals && !in->proposals))
-        return w->fail(HQ_E_INVAL, "hq_worker_step: NULL event array");
+    if (in->n_groups && (!in->groups || !in->offsets))
+        return w->fail(HQ_E_INVAL, "hq_worker_step: NULL groups/offsets");
+    if (in->n_groups && in->offsets[in->n_groups] > in->offsets[0] && !in->events)
+        return w->fail(HQ_E_INVAL, "hq_worker_step: NULL events");
     std::memset(out, 0, sizeof *out);
     return w->step(in, out);
 }

@@ -91,17 +91,12 @@ MSG_DTYPE = np.dtype([("from", "<u8"), ("hint_low", "<u8"), ("hint_high", "<u8")
 # step worker records (include/hipquorum.h "step worker")
 STATE_FOLLOWER, STATE_CANDIDATE, STATE_LEADER = 0, 1, 2
 MSG_REPLICATE_RESP, MSG_REQUEST_VOTE_RESP, MSG_HEARTBEAT_RESP, MSG_READ_INDEX = 13, 15, 18, 19
-TICK_CHECK_QUORUM, TICK_ELECTION = 1, 2
+EV_READ, EV_MESSAGE, EV_CHECK_QUORUM, EV_ELECTION, EV_PROPOSE = 1, 2, 3, 4, 5
 REASON_VOTE, REASON_CHECK_QUORUM, REASON_HIGHER_TERM, REASON_CAMPAIGN = 1, 2, 3, 4
 DROP_WITNESS, DROP_NOT_READY = 1, 2
-EVT_READ, EVT_MSG, EVT_TICK, EVT_PROPOSAL = 1, 2, 3, 4
-MESSAGE_DTYPE = np.dtype([("cluster_id", "<u8"), ("from", "<u8"), ("term", "<u8"),
-                          ("log_index", "<u8"), ("hint", "<u8"), ("hint_high", "<u8"),
-                          ("type", "<u4"), ("reject", "<u4")], align=True)
-READ_REQUEST_DTYPE = np.dtype([("cluster_id", "<u8"), ("ctx_low", "<u8"), ("ctx_high", "<u8")],
-                              align=True)
-TICK_DTYPE = np.dtype([("cluster_id", "<u8"), ("kind", "<u4"), ("reserved", "<u4")], align=True)
-PROPOSAL_DTYPE = np.dtype([("cluster_id", "<u8"), ("n_entries", "<u8")], align=True)
+EVENT_DTYPE = np.dtype([("kind", "<u4"), ("type", "<u4"), ("from", "<u8"), ("term", "<u8"),
+                        ("log_index", "<u8"), ("hint", "<u8"), ("hint_high", "<u8"),
+                        ("reject", "<u4"), ("reserved", "<u4")], align=True)
 WORKER_GROUP_DTYPE = np.dtype([("cluster_id", "<u8"), ("node_id", "<u8"), ("term", "<u8"),
                                ("committed", "<u8"), ("last_index", "<u8"), ("term_start", "<u8"),
                                ("state", "<u4"), ("n_members", "<u4"),
@@ -119,20 +114,18 @@ STATE_CHANGE_DTYPE = np.dtype([("cluster_id", "<u8"), ("term", "<u8"), ("state",
 DROPPED_READ_DTYPE = np.dtype([("cluster_id", "<u8"), ("ctx_low", "<u8"), ("ctx_high", "<u8"),
                                ("from", "<u8"), ("reason", "<u4"), ("reserved", "<u4")],
                               align=True)
-EVENT_REF_DTYPE = np.dtype([("array", "<u4"), ("reserved", "<u4"), ("index", "<u8")], align=True)
 
 
 class StepInput(ctypes.Structure):
     """Mirror of ``hq_step_input``."""
 
-    _fields_ = [("reads", _vp), ("n_reads", ctypes.c_uint64), ("msgs", _vp),
-                ("n_msgs", ctypes.c_uint64), ("ticks", _vp), ("n_ticks", ctypes.c_uint64),
-                ("proposals", _vp), ("n_proposals", ctypes.c_uint64)]
+    _fields_ = [("n_groups", ctypes.c_uint64), ("groups", _vp), ("offsets", _vp),
+                ("events", _vp)]
 
 
 STEP_OUTPUT_LISTS = [("commits", COMMIT_EVENT_DTYPE), ("ready", READY_DTYPE),
                      ("read_resps", READ_RESP_DTYPE), ("state_changes", STATE_CHANGE_DTYPE),
-                     ("dropped_reads", DROPPED_READ_DTYPE), ("deferred", EVENT_REF_DTYPE),
+                     ("dropped_reads", DROPPED_READ_DTYPE), ("deferred", np.dtype("<u8")),
                      ("fallback_groups", np.dtype("<u8"))]
 
 
@@ -141,7 +134,8 @@ class StepOutput(ctypes.Structure):
 
     _fields_ = [f for name, _ in STEP_OUTPUT_LISTS
                 for f in ((name, _vp), ("n_" + name, ctypes.c_uint64))] + \
-               [("gpu_passes", ctypes.c_uint64), ("decisions", ctypes.c_uint64)]
+               [("gpu_passes", ctypes.c_uint64), ("decisions", ctypes.c_uint64),
+                ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -192,8 +186,10 @@ SIGNATURES = {
     "hq_worker_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp)]),
     "hq_worker_close": (None, [_vp]),
     "hq_worker_last_error": (ctypes.c_char_p, [_vp]),
-    "hq_worker_add_group": (ctypes.c_int, [_vp, _vp, _vp]),
+    "hq_worker_add_group": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(ctypes.c_uint32)]),
     "hq_worker_set_group": (ctypes.c_int, [_vp, _vp, _vp]),
+    "hq_worker_add_groups": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp]),
+    "hq_worker_find": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]),
     "hq_worker_get_group": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp,
                                            ctypes.c_uint32]),
     "hq_worker_step": (ctypes.c_int, [_vp, ctypes.POINTER(StepInput),
@@ -610,10 +606,19 @@ class Worker:
         return g, m
 
     def add_group(self, cluster_id, node_id, term, state, committed, last_index, term_start,
-                  members) -> None:
+                  members) -> int:
+        """Adds a group; returns its handle."""
         g, m = self._group(cluster_id, node_id, term, state, committed, last_index, term_start,
                            members)
-        self._check(lib.hq_worker_add_group(self.h, _p(g), _p(m)), "hq_worker_add_group")
+        h = ctypes.c_uint32()
+        self._check(lib.hq_worker_add_group(self.h, _p(g), _p(m), ctypes.byref(h)),
+                    "hq_worker_add_group")
+        return h.value
+
+    def find(self, cluster_id) -> int:
+        h = ctypes.c_uint32()
+        self._check(lib.hq_worker_find(self.h, cluster_id, ctypes.byref(h)), "hq_worker_find")
+        return h.value
 
     def set_group(self, cluster_id, node_id, term, state, committed, last_index, term_start,
                   members) -> None:
@@ -632,13 +637,14 @@ class Worker:
                                             len(r)), "hq_worker_get_group")
         return g[0], m, r
 
-    def step(self, reads=None, msgs=None, ticks=None, proposals=None):
-        """One step; returns a dict of numpy record arrays (copies) plus gpu_passes/decisions."""
-        arrs = [np.ascontiguousarray(x if x is not None else np.zeros(0, dt), dt)
-                for x, dt in ((reads, READ_REQUEST_DTYPE), (msgs, MESSAGE_DTYPE),
-                              (ticks, TICK_DTYPE), (proposals, PROPOSAL_DTYPE))]
-        inp = StepInput(_p(arrs[0]), len(arrs[0]), _p(arrs[1]), len(arrs[1]), _p(arrs[2]),
-                        len(arrs[2]), _p(arrs[3]), len(arrs[3]))
+    def step(self, groups, offsets, events):
+        """One step: `groups` (uint32 handles), `offsets` (uint64, len(groups) + 1) and
+        `events` (EVENT_DTYPE). Returns a dict of numpy record arrays (copies) plus counters."""
+        groups = np.ascontiguousarray(groups, np.uint32)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        events = np.ascontiguousarray(events, EVENT_DTYPE)
+        assert len(offsets) == len(groups) + 1
+        inp = StepInput(len(groups), _p(groups), _p(offsets), _p(events))
         out = StepOutput()
         self._check(lib.hq_worker_step(self.h, ctypes.byref(inp), ctypes.byref(out)),
                     "hq_worker_step")
@@ -651,6 +657,14 @@ class Worker:
                 continue
             buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
             res[name] = np.frombuffer(buf, dt).copy()
-        res["gpu_passes"] = out.gpu_passes
-        res["decisions"] = out.decisions
+        for k in ("gpu_passes", "decisions", "handle_ns", "pass_ns"):
+            res[k] = getattr(out, k)
         return res
+
+    def add_groups(self, groups: np.ndarray, members: np.ndarray) -> None:
+        """Bulk add: WORKER_GROUP_DTYPE records, members of consecutive groups back to back."""
+        groups = np.ascontiguousarray(groups, WORKER_GROUP_DTYPE)
+        members = np.ascontiguousarray(members, MEMBER_DTYPE)
+        assert int(groups["n_members"].sum()) == len(members)
+        self._check(lib.hq_worker_add_groups(self.h, _p(groups), len(groups), _p(members)),
+                    "hq_worker_add_groups")

@@ -346,14 +346,17 @@ int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *membe
  * 923-1000) for the quorum part of many Raft groups at once. It holds each group's quorum state
  * (raft.remotes / witnesses / observers, raft.go:206-208; entryLog committed / lastIndex and the
  * first index of the leader's term; readIndex, readindex.go:31-34; votes, raft.go:210) and takes
- * one step's events in node.handleEvents order (node.go:1113-1157):
- *   1. local ReadIndex requests      node.handleReadIndex -> Peer.ReadIndex (peer.go:297-303)
+ * one step's events per group, in node.handleEvents order (node.go:1113-1157):
+ *   1. the local ReadIndex           node.handleReadIndex -> Peer.ReadIndex (peer.go:297-303)
  *   2. received messages             handleReceivedMessages -> Peer.Handle (peer.go:186-198)
  *   3. tick messages                 CheckQuorum (raft.go:1582) / Election (raft.go:1485)
  *   4. proposals                     handleProposals -> handleLeaderPropose (raft.go:1590)
+ * The input is laid out the way a step worker holds it: the groups that have events, each with
+ * its event list (a node's message queue, node.mq), i.e. compressed rows over one event array.
+ *
  * Membership filtering (Peer.Handle), the term check (onMessageTermNotMatched, raft.go:1416),
  * remote.tryUpdate, the confirmed-set inserts and first-response-wins votes are applied on the
- * host as the events arrive; every quorum decision — tryCommit, the ReadIndex release with its
+ * host as the events are read; every quorum decision — tryCommit, the ReadIndex release with its
  * index rewrite, the vote outcome, leaderHasQuorum — is taken by the kernels above at the end of
  * a run of events. A run ends early only where a later event reads a decision (a ReadIndex
  * needs the committed index; a state change needs the vote / CheckQuorum outcome; a higher-term
@@ -365,9 +368,9 @@ int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *membe
  * a follower or candidate forwarding or dropping a ReadIndex or a proposal — are returned as
  * `deferred`. Events the worker cannot take exactly suspend the group (`fallback`): an observer
  * acknowledging a pending ReadIndex ctx, a ReplicateResp above the leader's lastIndex, more
- * than 8 pending ReadIndex ctxs, an unknown message type. The group's events from that one on
- * are returned as deferred, its state is as of the event before, and it stays suspended (its
- * events deferred) until the caller re-syncs it with hq_worker_set_group.
+ * than 8 pending ReadIndex ctxs, an unknown message type or event kind. The group's events from
+ * that one on are returned as deferred, its state is as of the event before, and it stays
+ * suspended (its events deferred) until the caller re-syncs it with hq_worker_set_group.
  *
  * One worker per step worker goroutine; not thread-safe.
  */
@@ -381,9 +384,13 @@ int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *membe
 #define HQ_MSG_HEARTBEAT_RESP    18u
 #define HQ_MSG_READ_INDEX        19u
 
-#define HQ_TICK_CHECK_QUORUM 1u   /* the leader tick's CheckQuorum message (raft.go:1582-1588) */
-#define HQ_TICK_ELECTION     2u   /* the election tick's Election message (raft.go:1485-1515);
-                                     issue it only when hasConfigChangeToApply() is false */
+/* hq_event.kind */
+#define HQ_EV_READ         1u  /* local ReadIndex: Peer.ReadIndex(ctx), From = NoNode; ctx in hint */
+#define HQ_EV_MESSAGE      2u  /* a received pb.Message */
+#define HQ_EV_CHECK_QUORUM 3u  /* the leader tick's CheckQuorum message (raft.go:1582-1588) */
+#define HQ_EV_ELECTION     4u  /* the election tick's Election message (raft.go:1485-1515);
+                                  issue it only when hasConfigChangeToApply() is false */
+#define HQ_EV_PROPOSE      5u  /* a proposal of log_index entries (handleLeaderPropose) */
 
 /* hq_state_change.reason */
 #define HQ_REASON_VOTE         1u  /* vote outcome: became leader or follower */
@@ -394,33 +401,18 @@ int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_member *membe
 #define HQ_DROP_WITNESS   1u      /* ReadIndex from a witness (raft.go:1642-1643) */
 #define HQ_DROP_NOT_READY 2u      /* no committed entry at the current term yet (:1645-1651) */
 
-typedef struct hq_message {      /* the pb.Message fields the path reads (raft.proto:154-168) */
-    uint64_t cluster_id;
+typedef struct hq_event {        /* one event of a group's step; messages carry the pb.Message
+                                    fields the path reads (raft.proto:154-168) */
+    uint32_t kind;               /* HQ_EV_* */
+    uint32_t type;               /* HQ_EV_MESSAGE: HQ_MSG_* */
     uint64_t from;
     uint64_t term;
-    uint64_t log_index;
-    uint64_t hint;               /* HeartbeatResp / ReadIndex: SystemCtx.Low */
+    uint64_t log_index;          /* HQ_EV_PROPOSE: number of entries */
+    uint64_t hint;               /* HeartbeatResp / ReadIndex / HQ_EV_READ: SystemCtx.Low */
     uint64_t hint_high;          /* SystemCtx.High */
-    uint32_t type;               /* HQ_MSG_* */
     uint32_t reject;
-} hq_message;
-
-typedef struct hq_read_request { /* local ReadIndex: Peer.ReadIndex(ctx), From = NoNode */
-    uint64_t cluster_id;
-    uint64_t ctx_low;
-    uint64_t ctx_high;
-} hq_read_request;
-
-typedef struct hq_tick {
-    uint64_t cluster_id;
-    uint32_t kind;               /* HQ_TICK_* */
     uint32_t reserved;
-} hq_tick;
-
-typedef struct hq_proposal {
-    uint64_t cluster_id;
-    uint64_t n_entries;
-} hq_proposal;
+} hq_event;
 
 typedef struct hq_worker_group { /* a group's quorum state (add / set / get) */
     uint64_t cluster_id;
@@ -444,11 +436,13 @@ typedef struct hq_read_status {  /* readStatus (readindex.go:21-26), get only */
     uint32_t reserved;
 } hq_read_status;
 
+/* One step: group i of the list (a handle from hq_worker_add_group; each at most once) has the
+ * events events[offsets[i] .. offsets[i + 1]) in the order above. */
 typedef struct hq_step_input {
-    const hq_read_request *reads;   uint64_t n_reads;
-    const hq_message *msgs;         uint64_t n_msgs;      /* arrival order */
-    const hq_tick *ticks;           uint64_t n_ticks;
-    const hq_proposal *proposals;   uint64_t n_proposals;
+    uint64_t n_groups;
+    const uint32_t *groups;
+    const uint64_t *offsets;     /* [n_groups + 1], non-decreasing */
+    const hq_event *events;
 } hq_step_input;
 
 typedef struct hq_commit_event { uint64_t cluster_id, committed; } hq_commit_event;
@@ -466,25 +460,22 @@ typedef struct hq_dropped_read {
     uint64_t cluster_id, ctx_low, ctx_high, from;
     uint32_t reason, reserved;
 } hq_dropped_read;
-/* an input event handed back to the caller: which array (HQ_EVT_*) and its index there */
-#define HQ_EVT_READ     1u
-#define HQ_EVT_MSG      2u
-#define HQ_EVT_TICK     3u
-#define HQ_EVT_PROPOSAL 4u
-typedef struct hq_event_ref { uint32_t array, reserved; uint64_t index; } hq_event_ref;
 
 /* Results of one step; the arrays are owned by the worker and valid until its next call. Per
- * group, every list is in the order the reference produces it. */
+ * group, every list is in the order the reference produces it. `deferred` holds indexes into
+ * the input's events array. */
 typedef struct hq_step_output {
     const hq_commit_event *commits;        uint64_t n_commits;      /* committed index advanced */
     const hq_ready_to_read *ready;         uint64_t n_ready;
     const hq_read_index_resp *read_resps;  uint64_t n_read_resps;
     const hq_state_change *state_changes;  uint64_t n_state_changes;
     const hq_dropped_read *dropped_reads;  uint64_t n_dropped_reads;
-    const hq_event_ref *deferred;          uint64_t n_deferred;
-    const uint64_t *fallback_groups;       uint64_t n_fallback_groups;
+    const uint64_t *deferred;              uint64_t n_deferred;
+    const uint64_t *fallback_groups;       uint64_t n_fallback_groups;   /* cluster ids */
     uint64_t gpu_passes;        /* GPU passes (kernel batches + one sync each) of this step */
     uint64_t decisions;         /* group decisions taken on the GPU in this step */
+    uint64_t handle_ns;         /* wall time: the host bookkeeping of the events */
+    uint64_t pass_ns;           /* wall time: GPU passes (pack, copies, kernels, sync, apply) */
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;
@@ -493,9 +484,17 @@ typedef struct hq_worker hq_worker;
 int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
 void hq_worker_close(hq_worker *w);
 const char *hq_worker_last_error(const hq_worker *w);
-/* Add a group; members[0 .. g->n_members). Fails if the cluster exists, the node is not one of
+/* Add a group; members[0 .. g->n_members); *handle (may be NULL) receives its handle, the
+ * group's index in the order of addition. Fails if the cluster exists, the node is not one of
  * its remotes or it has more than n_max voting members. */
-int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member *members);
+int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member *members,
+                        uint32_t *handle);
+/* Add `count` groups (handles continue in order); group i's members follow group i-1's in
+ * `members`. Stops at the first group that fails (the groups before it stay added). */
+int hq_worker_add_groups(hq_worker *w, const hq_worker_group *groups, uint64_t count,
+                         const hq_member *members);
+/* The handle of a cluster. */
+int hq_worker_find(hq_worker *w, uint64_t cluster_id, uint32_t *handle);
 /* Overwrite a group's state (re-sync after fallback); clears its read queue and votes and
  * resumes it. */
 int hq_worker_set_group(hq_worker *w, const hq_worker_group *g, const hq_member *members);

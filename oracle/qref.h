@@ -259,7 +259,7 @@ typedef struct qref_group {
     int n_members;
     uint64_t committed, last, term_start;
     qref_member members[QREF_STEP_MAX_MEMBERS];
-    qref_read_index ri;
+    qref_read_index *ri;      /* allocated on the first ReadIndex; qref_group_free releases it */
     qref_votes votes;
 } qref_group;
 
@@ -277,6 +277,29 @@ typedef struct qref_step_out {
 int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64_t term,
                     int state, uint64_t committed, uint64_t last, uint64_t term_start,
                     const qref_member *members, int n_members);
+void qref_group_free(qref_group *g);
+
+/* Many groups, one step (the CPU baseline of the step worker): list[i] is an index into
+ * `groups` whose events are events[offsets[i] .. offsets[i + 1]) — the layout of hq_step_input
+ * (qref_event has hq_event's layout and kind values). Each listed group is replayed with
+ * qref_group_step; the list is split over nthreads threads. Totals of the outputs go to *tot. */
+typedef struct qref_step_totals {
+    uint64_t commits, ready, resps, states, dropped, deferred, committed_sum;
+} qref_step_totals;
+
+/* hq_worker_group layout: a group's initial state; members of consecutive groups back to back */
+typedef struct qref_group_rec {
+    uint64_t cluster_id, node_id, term, committed, last_index, term_start;
+    uint32_t state, n_members, n_pending_reads, suspended;
+} qref_group_rec;
+
+qref_group *qref_groups_new(uint64_t G);
+int qref_groups_init(qref_group *groups, uint64_t G, const qref_group_rec *recs,
+                     const qref_member *members);
+void qref_groups_free(qref_group *groups, uint64_t G);
+int qref_step_batch(qref_group *groups, uint64_t G, uint64_t n_list, const uint32_t *list,
+                    const uint64_t *offsets, const qref_event *events, int nthreads,
+                    qref_step_totals *tot);
 /* Replays the events in order; returns 0, -1 on bad arguments or QREF_PANIC where the reference
  * panics (or an output list overflows). */
 int qref_group_step(qref_group *g, const qref_event *ev, int n_events, qref_step_out *out);

@@ -81,7 +81,7 @@ class Group(ctypes.Structure):
     _fields_ = [("cluster_id", _u64), ("node_id", _u64), ("term", _u64), ("state", ctypes.c_int),
                 ("n_members", ctypes.c_int), ("committed", _u64), ("last", _u64),
                 ("term_start", _u64), ("members", Member * QREF_STEP_MAX_MEMBERS),
-                ("ri", ReadIndex), ("votes", Votes)]
+                ("ri", ctypes.POINTER(ReadIndex)), ("votes", Votes)]
 
 
 class _Ready(ctypes.Structure):
@@ -164,6 +164,11 @@ def load() -> ctypes.CDLL:
         "qref_group_init": (ctypes.c_int, [_vp, _u64, _u64, _u64, ctypes.c_int, _u64, _u64, _u64,
                                            _vp, ctypes.c_int]),
         "qref_group_step": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
+        "qref_group_free": (None, [_vp]),
+        "qref_groups_new": (_vp, [_u64]),
+        "qref_groups_free": (None, [_vp, _u64]),
+        "qref_groups_init": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
+        "qref_step_batch": (ctypes.c_int, [_vp, _u64, _u64, _vp, _vp, _vp, ctypes.c_int, _vp]),
         "qref_c1_run": (ctypes.c_int, [_u64, _vp, _vp, _u64, _u64, _vp]),
         "qref_ingest_match": (_u64, [_vp, _u64, _vp, _u64, _u64, ctypes.c_uint32]),
         "qref_ingest_ack": (_u64, [_vp, _u64, _vp, _u64, ctypes.c_uint32]),
@@ -453,6 +458,10 @@ class StepGroup:
         assert rc == 0, rc
         self._out = StepOut()
 
+    def __del__(self):
+        if lib is not None and getattr(self, "c", None) is not None:
+            lib.qref_group_free(ctypes.byref(self.c))
+
     def step(self, events):
         ev = (Event * max(1, len(events)))()
         for i, e in enumerate(events):
@@ -491,11 +500,45 @@ class StepGroup:
         members = [(int(m.node_id), int(m.match), int(m.role), int(m.active))
                    for m in c.members[:c.n_members]]
         reads = []
-        for qi in range(c.ri.n_queue):
-            q = c.ri.queue[qi]
-            for p in c.ri.pending[:c.ri.n_pending]:
+        ri = c.ri.contents if c.ri else None
+        for qi in range(ri.n_queue if ri else 0):
+            q = ri.queue[qi]
+            for p in ri.pending[:ri.n_pending]:
                 if p.ctx.low == q.low and p.ctx.high == q.high:
                     reads.append((int(p.index), int(p.from_), (int(q.low), int(q.high)),
                                   int(p.n_confirmed)))
         return (int(c.term), int(c.state), int(c.committed), int(c.last), int(c.term_start),
                 members, reads)
+
+
+class StepTotals(ctypes.Structure):
+    _fields_ = [(k, _u64) for k in ("commits", "ready", "resps", "states", "dropped", "deferred",
+                                    "committed_sum")]
+
+
+class StepBatch:
+    """Many groups replayed event by event (qref_step_batch): the CPU baseline of the step
+    worker, on the same compressed-row input (group index list, offsets, events) as
+    hq_worker_step. Group records / members use the worker's numpy dtypes."""
+
+    def __init__(self, groups: np.ndarray, members: np.ndarray):
+        self.G = len(groups)
+        self.h = lib.qref_groups_new(self.G)
+        assert self.h
+        rc = lib.qref_groups_init(self.h, self.G, _ptr(groups), _ptr(members))
+        assert rc == 0, rc
+
+    def close(self):
+        if self.h:
+            lib.qref_groups_free(self.h, self.G)
+            self.h = None
+
+    def committed(self, i: int) -> int:
+        return int(Group.from_address(self.h + i * ctypes.sizeof(Group)).committed)
+
+    def step(self, list_, offsets, events, nthreads=1):
+        t = StepTotals()
+        rc = lib.qref_step_batch(self.h, self.G, len(list_), _ptr(list_), _ptr(offsets),
+                                 _ptr(events), nthreads, ctypes.byref(t))
+        assert rc == 0, rc
+        return {k: int(getattr(t, k)) for k, _ in StepTotals._fields_}

@@ -10,6 +10,8 @@
  * CheckQuorum / Election messages (handleLocalTick), then proposals (handleProposals
  * :1184-1195). The caller lists the events of one group in that order.
  */
+#include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "qref.h"
@@ -91,7 +93,7 @@ static int push_state(qref_group *g, qref_step_out *o, int reason) {
 static void reset(qref_group *g, uint64_t term) {
     if (g->term != term) g->term = term;   /* vote = NoLeader: not modelled */
     qref_votes_reset(&g->votes);
-    qref_ri_init(&g->ri);
+    if (g->ri) qref_ri_init(g->ri);
     for (int i = 0; i < g->n_members; i++) {
         g->members[i].match = g->members[i].node_id == g->node_id ? g->last : 0;
         g->members[i].active = 0;
@@ -174,7 +176,12 @@ static int leader_read_index(qref_group *g, const qref_event *e, qref_step_out *
     if (role_of(g, e->from) == QREF_ROLE_WITNESS) return add_dropped(o, e, QREF_DROP_WITNESS);
     if (!qref_is_single_node_quorum(n_voting(g))) {
         if (!has_committed_entry_at_current_term(g)) return add_dropped(o, e, QREF_DROP_NOT_READY);
-        return qref_ri_add_request(&g->ri, g->committed, ctx, e->from);
+        if (!g->ri) {                      /* the queue is allocated on first use */
+            g->ri = (qref_read_index *)malloc(sizeof *g->ri);
+            if (!g->ri) return QREF_PANIC;
+            qref_ri_init(g->ri);
+        }
+        return qref_ri_add_request(g->ri, g->committed, ctx, e->from);
     }
     int rc = add_ready(o, g->committed, ctx.low, ctx.high);
     if (rc) return rc;
@@ -185,9 +192,10 @@ static int leader_read_index(qref_group *g, const qref_event *e, qref_step_out *
 
 /* raft.handleReadIndexLeaderConfirmation (raft.go:1740-1760) */
 static int read_index_confirmation(qref_group *g, const qref_event *e, qref_step_out *o) {
-    static qref_read_status out[QREF_MAX_PENDING];
+    qref_read_status out[QREF_MAX_PENDING];   /* 10.7 KB on the stack; thread-safe */
     qref_sysctx ctx = {e->hint, e->hint_high};
-    int r = qref_ri_confirm(&g->ri, ctx, e->from, quorum(g), out);
+    if (!g->ri) return QREF_OK;            /* nothing pending: confirm() returns nil */
+    int r = qref_ri_confirm(g->ri, ctx, e->from, quorum(g), out);
     if (r < 0) return r;
     for (int i = 0; i < r; i++) {
         int rc = (out[i].from == 0 || out[i].from == g->node_id)
@@ -256,6 +264,13 @@ static int handle_message(qref_group *g, const qref_event *e, int i, qref_step_o
     return QREF_OK;
 }
 
+void qref_group_free(qref_group *g) {
+    if (g && g->ri) {
+        free(g->ri);
+        g->ri = NULL;
+    }
+}
+
 int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64_t term,
                     int state, uint64_t committed, uint64_t last, uint64_t term_start,
                     const qref_member *members, int n_members) {
@@ -271,7 +286,7 @@ int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64
     g->term_start = term_start;
     g->n_members = n_members;
     memcpy(g->members, members, (size_t)n_members * sizeof *members);
-    qref_ri_init(&g->ri);
+    g->ri = NULL;
     qref_votes_reset(&g->votes);
     /* a candidate holds its own vote (campaign, raft.go:1093) */
     if (state == QREF_CANDIDATE) qref_handle_vote_resp(&g->votes, node_id, 0);
@@ -280,7 +295,10 @@ int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64
 
 int qref_group_step(qref_group *g, const qref_event *ev, int n_events, qref_step_out *o) {
     if (!g || !o || (n_events && !ev)) return -1;
-    memset(o, 0, sizeof *o);
+    /* only the counts: the lists are read up to them (the struct is ~7 KB) */
+    o->committed = 0;
+    o->commit_changed = 0;
+    o->n_ready = o->n_resps = o->n_states = o->n_dropped = o->n_deferred = 0;
     const uint64_t committed0 = g->committed;
     for (int i = 0; i < n_events; i++) {
         const qref_event *e = &ev[i];
@@ -326,5 +344,105 @@ int qref_group_step(qref_group *g, const qref_event *ev, int n_events, qref_step
     }
     o->committed = g->committed;
     o->commit_changed = g->committed != committed0;
+    return 0;
+}
+
+/* ================================================================ many groups, one step ==== */
+
+typedef struct {
+    qref_group *groups;
+    const uint32_t *list;
+    const uint64_t *offsets;
+    const qref_event *ev;
+    uint64_t i0, i1;
+    qref_step_totals tot;
+    int rc;
+} step_job;
+
+static void *step_run(void *p) {
+    step_job *j = (step_job *)p;
+    qref_step_out *o = (qref_step_out *)malloc(sizeof *o);
+    if (!o) { j->rc = QREF_PANIC; return NULL; }
+    for (uint64_t i = j->i0; i < j->i1; i++) {
+        uint64_t b = j->offsets[i], e = j->offsets[i + 1];
+        int rc = qref_group_step(&j->groups[j->list[i]], j->ev + b, (int)(e - b), o);
+        if (rc) { j->rc = rc; break; }
+        j->tot.commits += (uint64_t)o->commit_changed;
+        j->tot.ready += (uint64_t)o->n_ready;
+        j->tot.resps += (uint64_t)o->n_resps;
+        j->tot.states += (uint64_t)o->n_states;
+        j->tot.dropped += (uint64_t)o->n_dropped;
+        j->tot.deferred += (uint64_t)o->n_deferred;
+        j->tot.committed_sum += o->committed;
+    }
+    free(o);
+    return NULL;
+}
+
+int qref_step_batch(qref_group *groups, uint64_t G, uint64_t n_list, const uint32_t *list,
+                    const uint64_t *offsets, const qref_event *events, int nthreads,
+                    qref_step_totals *tot) {
+    if (!groups || !tot || nthreads < 1 || (n_list && (!list || !offsets))) return -1;
+    memset(tot, 0, sizeof *tot);
+    for (uint64_t i = 0; i < n_list; i++)
+        if (list[i] >= G || offsets[i + 1] < offsets[i]) return -1;
+    if (nthreads > 64) nthreads = 64;
+    step_job jobs[64];
+    pthread_t th[64];
+    uint64_t per = (n_list + (uint64_t)nthreads - 1) / (uint64_t)nthreads;
+    int started = 0, rc = 0;
+    for (int t = 0; t < nthreads; t++) {
+        uint64_t i0 = per * (uint64_t)t, i1 = i0 + per;
+        if (i0 >= n_list) break;
+        if (i1 > n_list) i1 = n_list;
+        memset(&jobs[t], 0, sizeof jobs[t]);
+        jobs[t].groups = groups;
+        jobs[t].list = list;
+        jobs[t].offsets = offsets;
+        jobs[t].ev = events;
+        jobs[t].i0 = i0;
+        jobs[t].i1 = i1;
+        if (nthreads == 1 || pthread_create(&th[t], NULL, step_run, &jobs[t]) != 0) {
+            step_run(&jobs[t]);
+            th[t] = 0;
+        }
+        started++;
+    }
+    for (int t = 0; t < started; t++) {
+        if (th[t]) pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+        tot->commits += jobs[t].tot.commits;
+        tot->ready += jobs[t].tot.ready;
+        tot->resps += jobs[t].tot.resps;
+        tot->states += jobs[t].tot.states;
+        tot->dropped += jobs[t].tot.dropped;
+        tot->deferred += jobs[t].tot.deferred;
+        tot->committed_sum += jobs[t].tot.committed_sum;
+    }
+    return rc;
+}
+
+qref_group *qref_groups_new(uint64_t G) {
+    return (qref_group *)calloc(G ? G : 1, sizeof(qref_group));
+}
+
+void qref_groups_free(qref_group *groups, uint64_t G) {
+    if (!groups) return;
+    for (uint64_t g = 0; g < G; g++) qref_group_free(&groups[g]);
+    free(groups);
+}
+
+int qref_groups_init(qref_group *groups, uint64_t G, const qref_group_rec *recs,
+                     const qref_member *members) {
+    if (!groups || (G && (!recs || !members))) return -1;
+    uint64_t off = 0;
+    for (uint64_t g = 0; g < G; g++) {
+        const qref_group_rec *r = &recs[g];
+        int rc = qref_group_init(&groups[g], r->cluster_id, r->node_id, r->term, (int)r->state,
+                                 r->committed, r->last_index, r->term_start, members + off,
+                                 (int)r->n_members);
+        if (rc) return rc;
+        off += r->n_members;
+    }
     return 0;
 }

@@ -18,6 +18,23 @@ def check_phase_order(events):
     assert ph == sorted(ph), events
 
 
+def event_record(hq, e):
+    """An event tuple as an hq_event record (kind, type, from, term, log_index, hint,
+    hint_high, reject, reserved)."""
+    k = e[0]
+    if k == "read":
+        return (hq.EV_READ, 0, 0, 0, 0, e[1], e[2], 0, 0)
+    if k == "msg":
+        return (hq.EV_MESSAGE, e[1], e[2], e[3], e[4], e[5], e[6], e[7], 0)
+    if k == "check_quorum":
+        return (hq.EV_CHECK_QUORUM, 0, 0, 0, 0, 0, 0, 0, 0)
+    if k == "campaign":
+        return (hq.EV_ELECTION, 0, 0, 0, 0, 0, 0, 0, 0)
+    if k == "propose":
+        return (hq.EV_PROPOSE, 0, 0, 0, e[1], 0, 0, 0, 0)
+    raise ValueError(k)
+
+
 class OracleBackend:
     def __init__(self):
         from oracle import qref
@@ -59,44 +76,22 @@ class WorkerBackend:
         self.cids.append(cid)
 
     def build_inputs(self, per_group):
-        """Arrays for hq_worker_step; messages of different groups are interleaved at random
-        (per-group order kept). Returns (arrays, refs) with refs[(array, index)] = (cid, pos)."""
+        """hq_worker_step input: the groups (in a random order) with their event lists.
+        Returns ((handles, offsets, events), refs) with refs[event index] = (cid, pos)."""
         hq = self.hq
-        reads, ticks, props, msg_lists = [], [], [], []
-        refs = {}
-        for cid, events in per_group.items():
+        cids = list(per_group)
+        self.rng.shuffle(cids)
+        handles, offsets, recs, refs = [], [0], [], {}
+        for cid in cids:
+            events = per_group[cid]
             check_phase_order(events)
-            ml = []
+            handles.append(self.w.find(cid))
             for pos, e in enumerate(events):
-                k = e[0]
-                if k == "read":
-                    refs[(hq.EVT_READ, len(reads))] = (cid, pos)
-                    reads.append((cid, e[1], e[2]))
-                elif k == "msg":
-                    ml.append((pos, (cid, e[2], e[3], e[4], e[5], e[6], e[1], e[7])))
-                elif k in ("check_quorum", "campaign"):
-                    refs[(hq.EVT_TICK, len(ticks))] = (cid, pos)
-                    kind = hq.TICK_CHECK_QUORUM if k == "check_quorum" else hq.TICK_ELECTION
-                    ticks.append((cid, kind, 0))
-                else:
-                    refs[(hq.EVT_PROPOSAL, len(props))] = (cid, pos)
-                    props.append((cid, e[1]))
-            if ml:
-                msg_lists.append(ml)
-        # random interleaving of the groups' message streams
-        order = np.concatenate([np.full(len(ml), i) for i, ml in enumerate(msg_lists)]) \
-            if msg_lists else np.zeros(0, int)
-        self.rng.shuffle(order)
-        cursors = [0] * len(msg_lists)
-        msgs = []
-        for i in order:
-            pos, rec = msg_lists[i][cursors[i]]
-            cursors[i] += 1
-            refs[(hq.EVT_MSG, len(msgs))] = (rec[0], pos)
-            msgs.append(rec)
-        arrs = (np.array(reads, hq.READ_REQUEST_DTYPE), np.array(msgs, hq.MESSAGE_DTYPE),
-                np.array(ticks, hq.TICK_DTYPE), np.array(props, hq.PROPOSAL_DTYPE))
-        return arrs, refs
+                refs[len(recs)] = (cid, pos)
+                recs.append(event_record(hq, e))
+            offsets.append(len(recs))
+        return (np.array(handles, np.uint32), np.array(offsets, np.uint64),
+                np.array(recs, hq.EVENT_DTYPE)), refs
 
     def step(self, per_group):
         arrs, refs = self.build_inputs(per_group)
@@ -118,7 +113,7 @@ class WorkerBackend:
             out[int(r["cluster_id"])]["dropped"].append(
                 (int(r["ctx_low"]), int(r["ctx_high"]), int(r["from"]), int(r["reason"])))
         for r in res["deferred"]:
-            cid, pos = refs[(int(r["array"]), int(r["index"]))]
+            cid, pos = refs[int(r)]
             out[cid]["deferred"].append(pos)
         for cid in out:
             out[cid]["deferred"].sort()
