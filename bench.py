@@ -341,53 +341,99 @@ def step_events(hq, G, s, last0=1000):
     return np.arange(G, dtype=np.uint32), offsets, ev
 
 
-def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
-    assert cpu_steps <= steps
-    """The step worker end to end (hq_worker_step): host bookkeeping of every event plus the
-    GPU passes, against the event-by-event C restatement of the reference (oracle, CPU) on the
-    same events; the committed sums of both must agree."""
-    from dragonboat_amd import hipquorum as hq
-    from dragonboat_amd import shard
+def _run_workers(hq, d: Dist, G, W, steps, cpu_steps):
+    """W workers (one host thread each, own HIP stream) over G groups split into W contiguous
+    partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
+    of the first 4096 groups after cpu_steps steps)."""
+    import threading
 
-    rng = shard.rank_shard(d.rank, d.world, G)
+    rng = _shard_of(d, G)
     g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride)
-    w = hq.Worker(d.device, 3)
-    w.add_groups(g, m)                   # handles 0 .. G-1 in cids order
-    t_total, acc = 0.0, dict(handle_ns=0, pass_ns=0, gpu_passes=0, decisions=0)
-    n_events = 0
-    committed_gpu = None
+    bounds = [G * i // W for i in range(W + 1)]
+    workers = []
+    for i in range(W):
+        w = hq.Worker(d.device, 3)
+        w.add_groups(g[bounds[i]:bounds[i + 1]], m[3 * bounds[i]:3 * bounds[i + 1]])
+        workers.append(w)
+    acc = dict(handle_ns=0, pass_ns=0, pack_ns=0, device_ns=0, apply_ns=0, gpu_passes=0,
+               decisions=0)
+    t_total, n_events, committed = 0.0, 0, None
     for s in range(steps + 1):
-        ev = step_events(hq, G, s)
+        evs = [step_events(hq, bounds[i + 1] - bounds[i], s) for i in range(W)]
+        res = [None] * W
+
+        def run(i):
+            res[i] = workers[i].step(*evs[i], copy=False)
+
+        threads = [threading.Thread(target=run, args=(i,)) for i in range(W)]
         t0 = time.perf_counter()
-        res = w.step(*ev)
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
         dt = time.perf_counter() - t0
         if s == cpu_steps:   # state checked against the CPU replay of the same steps
-            committed_gpu = [int(w.get_group(int(c))[0]["committed"]) for c in cids[:4096]]
+            committed = [int(workers[0].get_group(int(c))[0]["committed"])
+                         for c in cids[:min(4096, bounds[1])]]
         if s == 0:
             continue                      # warm-up: allocations and first-touch
         t_total += dt
-        n_events += len(ev[2])
-        for k in acc:
-            acc[k] += res[k]
-    w.close()
-    elapsed = d.max(t_total)
+        n_events += sum(len(e[2]) for e in evs)
+        for r in res:
+            for k in acc:
+                acc[k] += r[k]
+    for w in workers:
+        w.close()
+    return t_total, n_events, acc, committed, (g, m)
+
+
+def _shard_of(d, G):
+    from dragonboat_amd import shard
+
+    return shard.rank_shard(d.rank, d.world, G)
+
+
+def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
+    """The step worker end to end (hq_worker_step): host bookkeeping of every event plus the
+    GPU passes, against the event-by-event C restatement of the reference (oracle, CPU) on the
+    same events; the committed indexes of both must agree. Run with one worker (one step-worker
+    thread) and with T workers stepping concurrently (dragonboat runs 16 step workers,
+    internal/settings/hard.go:36), next to the CPU replay on 1 and T threads."""
+    from dragonboat_amd import hipquorum as hq
+
+    assert cpu_steps <= steps
+    T = min(16, os.cpu_count() or 1)
     out = {
         "workload": f"step: hq_worker_step over {G} leader groups x 3 voters per GPU; per group "
                     f"and step 4 messages (2 ReplicateResp, 2 HeartbeatResp), 1 proposal, 1/4 "
-                    f"local ReadIndex; one worker (one host thread)",
-        "value": d.sum(float(n_events)) / elapsed, "unit": "events/s",
-        "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
-        "ms_per_step": elapsed / steps * 1e3,
-        "gpu_passes_per_step": acc["gpu_passes"] / steps,
-        "host_ms_per_step": acc["handle_ns"] / steps / 1e6,
-        "gpu_pass_ms_per_step": acc["pass_ns"] / steps / 1e6,
+                    f"local ReadIndex",
+        "unit": "events/s",
     }
+    committed_gpu = None
+    for W in (1, T):
+        t, ne, acc, committed, gm = _run_workers(hq, d, G, W, steps, cpu_steps)
+        elapsed = d.max(t)
+        rec = {
+            "workers": W,
+            "value": d.sum(float(ne)) / elapsed,
+            "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
+            "ms_per_step": elapsed / steps * 1e3,
+            "gpu_passes_per_step": acc["gpu_passes"] / steps / W,
+            "host_ms_per_step_per_worker": acc["handle_ns"] / steps / W / 1e6,
+            "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
+                                         for k in ("pack", "device", "apply")},
+        }
+        if W == 1:
+            out.update(rec)
+            committed_gpu = committed
+        else:
+            out["concurrent_workers"] = rec
     if with_cpu and d.rank == 0 and d.world == 1:
         from oracle import qref
 
-        threads = min(16, os.cpu_count() or 1)
+        g, m = gm
         cpu = {}
-        for nt in (1, threads):
+        for nt in (1, T):
             b = qref.StepBatch(g, m)
             tc, ne = 0.0, 0
             for s in range(cpu_steps + 1):
@@ -397,16 +443,15 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
                 if s > 0:
                     tc += time.perf_counter() - t0
                     ne += len(ev[2])
-            committed_cpu = [b.committed(i) for i in range(min(G, 4096))]
+            committed_cpu = [b.committed(i) for i in range(len(committed_gpu))]
             b.close()
             cpu[nt] = ne / tc
         out["cpu_reference"] = {
-            "value": cpu[threads], "unit": "events/s", "threads": threads,
-            "single_thread_value": cpu[1],
+            "value": cpu[T], "unit": "events/s", "threads": T, "single_thread_value": cpu[1],
             "sample": f"the same events of the first {cpu_steps} steps, replayed event by "
                       f"event (oracle/qref_step.c, C restatement of the reference path)",
         }
-        # the same events left the same committed indexes (first 4096 groups)
+        # the same events left the same committed indexes
         out["parity_committed"] = committed_gpu == committed_cpu
     return out
 

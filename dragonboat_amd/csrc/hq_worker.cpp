@@ -12,6 +12,10 @@
 // yet taken (a "run"); all runs of a pass are decided in one GPU batch, applied, and the next
 // pass continues where they stopped. Plain C++ (no HIP headers): the worker is a client of the
 // same ABI a cgo binding would use.
+//
+// Storage is flat: one fixed-size record per group, its members in one pool (voting slots
+// first, in slot order, so packing a group's match row is a contiguous copy) and pending
+// ReadIndex queues in a pool of fixed 8-entry blocks.
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -24,41 +28,63 @@
 
 namespace {
 
-constexpr uint32_t kMaxReads = 8;        // pending ReadIndex ctxs per group (k_ri_multi K_max)
+constexpr uint32_t kMaxReads = 8;         // pending ReadIndex ctxs per group (k_ri_multi K_max)
 constexpr uint16_t kNoAck = 0xFFFF;
 constexpr uint16_t kMaxOrdinal = 0xFFF0;  // acks per run before a run is cut
+constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-struct ReadStatus {                      // readStatus (readindex.go:21-26)
+struct Member {                           // a remote, witness or observer of one group
+    uint64_t node_id, match;
+    uint8_t role, active;
+    uint8_t order;                        // position in the caller's member list
+    uint8_t pad[5];
+};
+
+struct ReadStatus {                       // readStatus (readindex.go:21-26)
     uint64_t index, from, low, high;
-    uint8_t confirmed;                   // slots confirmed in earlier runs (ordinal 0)
-    uint16_t ord[HQ_MAX_VOTERS];         // first-ack ordinal in the current run
+    uint16_t ord[HQ_MAX_VOTERS];          // first-ack ordinal in the current run
+    uint8_t confirmed;                    // slots confirmed in earlier runs (ordinal 0)
+};
+
+struct ReadQueue {                        // readIndex.queue with its pending statuses
+    uint32_t n;
+    ReadStatus r[kMaxReads];
+};
+
+enum : uint8_t {
+    kSuspended = 1, kTouched = 2, kInWork = 4,
+    kCommitDue = 8, kRiDue = 16, kVoteDue = 32, kCqDue = 64,
+    kDue = kCommitDue | kRiDue | kVoteDue | kCqDue,
 };
 
 struct Group {
-    uint64_t cluster_id = 0, node_id = 0, term = 0;
-    uint64_t committed = 0, last = 0, term_start = 0;
-    uint32_t state = HQ_STATE_FOLLOWER;
-    std::vector<hq_member> members;      // in the caller's order
-    std::vector<int8_t> slot_of;         // member -> voting slot, -1 for observers
-    int self = -1;                       // member index of this node
-    int n_voting = 0;
-    std::vector<ReadStatus> reads;       // readIndex.queue with its pending statuses
-    uint8_t granted = 0, rejected = 0;   // votes over voting slots
-    bool suspended = false;
-    // current step
-    uint64_t committed0 = 0;
-    bool touched = false;
-    uint64_t ev_end = 0, cursor = 0;     // the group's events in the step input
-    // current run
-    bool commit_due = false, ri_due = false, vote_due = false, cq_due = false;
-    uint16_t ord = 0;
-    bool in_work = false;
-    bool pending() const { return commit_due || ri_due || vote_due || cq_due; }
+    uint64_t cluster_id, node_id, term, committed, last, term_start;
+    uint64_t committed0, cursor, ev_end;  // current step
+    uint32_t mem;                         // first member in the pool; [0] is the node itself
+    uint32_t rq;                          // read queue block, kNone when empty
+    uint16_t ord;                         // acks recorded in the current run
+    uint8_t n_members, mem_cap, n_voting, state, granted, rejected, flags;
+    bool has(uint8_t f) const { return flags & f; }
+    void set(uint8_t f) { flags |= f; }
+    void clear(uint8_t f) { flags &= (uint8_t)~f; }
+    bool pending() const { return flags & kDue; }
 };
 
 enum Verdict { CONSUMED, BARRIER, FALLBACK };
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+bool is_response_type(uint32_t t) {       // isResponseMessageType (internal/raft/utils.go)
+    return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
+           t == HQ_MSG_HEARTBEAT_RESP || t == 20 /* ReadIndexResp */ ||
+           t == 8 /* SnapshotStatus */ || t == 9 /* Unreachable */;
+}
 
 }  // namespace
 
@@ -67,7 +93,10 @@ struct hq_worker {
     uint32_t n_max = 0;
     std::string err;
     std::vector<Group> groups;
-    std::unordered_map<uint64_t, uint32_t> index;   // cluster_id -> group
+    std::vector<Member> pool;
+    std::vector<ReadQueue> rqs;
+    std::vector<uint32_t> rq_free;
+    std::unordered_map<uint64_t, uint32_t> index;   // cluster_id -> handle
     // step scratch
     const hq_step_input *in = nullptr;
     std::vector<uint32_t> work, next_work, touched;
@@ -81,6 +110,7 @@ struct hq_worker {
     std::vector<uint64_t> deferred;
     std::vector<uint64_t> fallback;
     uint64_t decisions = 0;
+    uint64_t t_pack = 0, t_device = 0, t_apply = 0;
     // staging: one pinned host buffer mirrored by one device buffer per pass
     void *host = nullptr, *dev = nullptr;
     size_t cap = 0;
@@ -93,8 +123,31 @@ struct hq_worker {
         if (rc) err = std::string(what) + ": " + hq_last_error(ctx);
         return rc;
     }
+    Member *members(Group &g) { return pool.data() + g.mem; }
+    int member_of(const Group &g, uint64_t id) const {
+        const Member *m = pool.data() + g.mem;
+        for (int i = 0; i < g.n_members; ++i)
+            if (m[i].node_id == id) return i;
+        return -1;
+    }
+    ReadQueue *reads(const Group &g) { return g.rq == kNone ? nullptr : &rqs[g.rq]; }
+    uint32_t rq_alloc() {
+        if (!rq_free.empty()) {
+            const uint32_t i = rq_free.back();
+            rq_free.pop_back();
+            rqs[i].n = 0;
+            return i;
+        }
+        rqs.emplace_back();
+        rqs.back().n = 0;
+        return (uint32_t)rqs.size() - 1;
+    }
+    void rq_release(Group &g) {
+        if (g.rq != kNone) rq_free.push_back(g.rq);
+        g.rq = kNone;
+    }
     int reserve(size_t bytes);
-    int load_group(Group &g, const hq_worker_group *src, const hq_member *m);
+    int load_group(Group &g, const hq_worker_group *src, const hq_member *m, bool fresh);
     int step(const hq_step_input *in, hq_step_output *out);
     Verdict handle(Group &g, const hq_event &e, uint64_t ei);
     Verdict read_index(Group &g, uint64_t from, uint64_t low, uint64_t high, uint64_t ei);
@@ -108,55 +161,70 @@ struct hq_worker {
         states.push_back({g.cluster_id, g.term, g.state, reason});
     }
     void defer(uint64_t ei) { deferred.push_back(ei); }
-    int member_of(const Group &g, uint64_t id) const {
-        for (size_t i = 0; i < g.members.size(); ++i)
-            if (g.members[i].node_id == id) return (int)i;
-        return -1;
-    }
 };
 
 // ------------------------------------------------------------------------------ state ------
-int hq_worker::load_group(Group &g, const hq_worker_group *src, const hq_member *m) {
-    if (src->n_members < 1 || !m) return fail(HQ_E_INVAL, "group has no members");
+// Validates and loads a group; `fresh` groups get a new member range, others reuse theirs when
+// it is large enough.
+int hq_worker::load_group(Group &g, const hq_worker_group *src, const hq_member *m, bool fresh) {
+    const uint32_t n = src->n_members;
+    if (n < 1 || !m) return fail(HQ_E_INVAL, "group has no members");
+    if (n > 64) return fail(HQ_E_INVAL, "more than 64 members");
     if (src->state > HQ_STATE_LEADER) return fail(HQ_E_INVAL, "state must be follower, candidate or leader");
-    Group n;
-    n.cluster_id = src->cluster_id;
-    n.node_id = src->node_id;
-    n.term = src->term;
-    n.committed = src->committed;
-    n.last = src->last_index;
-    n.term_start = src->term_start;
-    n.state = src->state;
-    n.members.assign(m, m + src->n_members);
-    n.slot_of.assign(src->n_members, -1);
-    for (uint32_t i = 0; i < src->n_members; ++i) {
+    int self = -1, n_voting = 0;
+    for (uint32_t i = 0; i < n; ++i) {
         if (m[i].role > HQ_ROLE_WITNESS) return fail(HQ_E_INVAL, "unknown member role");
         for (uint32_t j = 0; j < i; ++j)
             if (m[j].node_id == m[i].node_id) return fail(HQ_E_INVAL, "duplicate member");
-        if (m[i].role == HQ_ROLE_REMOTE && m[i].node_id == src->node_id) n.self = (int)i;
+        if (m[i].role == HQ_ROLE_REMOTE && m[i].node_id == src->node_id) self = (int)i;
+        n_voting += m[i].role != HQ_ROLE_OBSERVER;
     }
-    if (n.self < 0) return fail(HQ_E_INVAL, "the node is not one of the group's remotes");
-    // voting slots: the node itself, the other remotes, then the witnesses (hq_pack_commit)
-    n.slot_of[n.self] = (int8_t)n.n_voting++;
-    for (uint32_t role : {HQ_ROLE_REMOTE, HQ_ROLE_WITNESS})
-        for (uint32_t i = 0; i < src->n_members; ++i)
-            if (m[i].role == role && (int)i != n.self) {
-                if (n.n_voting >= (int)n_max) return fail(HQ_E_INVAL, "more voting members than n_max");
-                n.slot_of[i] = (int8_t)n.n_voting++;
-            }
+    if (self < 0) return fail(HQ_E_INVAL, "the node is not one of the group's remotes");
+    if (n_voting > (int)n_max) return fail(HQ_E_INVAL, "more voting members than n_max");
+    if (fresh || g.mem_cap < n) {
+        g.mem = (uint32_t)pool.size();
+        g.mem_cap = (uint8_t)n;
+        pool.resize(pool.size() + n);
+    }
+    // pool order: the node itself, the other remotes, the witnesses (the voting slots of
+    // hq_pack_commit), then the observers
+    Member *dst = pool.data() + g.mem;
+    int k = 0;
+    auto put = [&](uint32_t i) {
+        dst[k] = Member{m[i].node_id, m[i].match, (uint8_t)m[i].role, (uint8_t)(m[i].active != 0),
+                        (uint8_t)i, {0, 0, 0, 0, 0}};
+        ++k;
+    };
+    put((uint32_t)self);
+    for (uint32_t role : {HQ_ROLE_REMOTE, HQ_ROLE_WITNESS, HQ_ROLE_OBSERVER})
+        for (uint32_t i = 0; i < n; ++i)
+            if (m[i].role == role && (int)i != self) put(i);
+    g.cluster_id = src->cluster_id;
+    g.node_id = src->node_id;
+    g.term = src->term;
+    g.committed = src->committed;
+    g.last = src->last_index;
+    g.term_start = src->term_start;
+    g.state = (uint8_t)src->state;
+    g.n_members = (uint8_t)n;
+    g.n_voting = (uint8_t)n_voting;
+    g.ord = 0;
+    g.flags = 0;
+    rq_release(g);
     // a candidate holds its own vote (campaign, raft.go:1093)
-    if (n.state == HQ_STATE_CANDIDATE) n.granted = 1;
-    g = std::move(n);
+    g.granted = g.state == HQ_STATE_CANDIDATE ? 1 : 0;
+    g.rejected = 0;
     return HQ_OK;
 }
 
 void hq_worker::reset(Group &g, uint64_t term) {   // raft.reset, raft.go:991-1010
     g.term = term;
     g.granted = g.rejected = 0;
-    g.reads.clear();
-    for (auto &m : g.members) {                     // resetRemotes/Observers/Witnesses
-        m.match = m.node_id == g.node_id ? g.last : 0;
-        m.active = 0;
+    rq_release(g);
+    Member *m = members(g);
+    for (int i = 0; i < g.n_members; ++i) {          // resetRemotes/Observers/Witnesses
+        m[i].match = m[i].node_id == g.node_id ? g.last : 0;
+        m[i].active = 0;
     }
 }
 
@@ -173,28 +241,29 @@ void hq_worker::become_leader(Group &g) {
     // the no-op of p72: first entry of the new term; the node's own remote follows the log
     g.term_start = g.last + 1;
     g.last += 1;
-    g.members[g.self].match = g.last;
-    if (g.n_voting == 1) g.commit_due = true;       // appendEntries: single-node tryCommit
+    members(g)[0].match = g.last;
+    if (g.n_voting == 1) g.set(kCommitDue);         // appendEntries: single-node tryCommit
 }
 
 // ------------------------------------------------------------------------------ events -----
 Verdict hq_worker::read_index(Group &g, uint64_t from, uint64_t low, uint64_t high,
                               uint64_t ei) {
     if (g.state != HQ_STATE_LEADER) {
-        if (g.vote_due) return BARRIER;             // the vote may have made it leader
+        if (g.has(kVoteDue)) return BARRIER;        // the vote may have made it leader
         defer(ei);                                  // forwarded / dropped (raft.go:1875, 1937)
         return CONSUMED;
     }
     // handleLeaderReadIndex (raft.go:1636-1669)
     const int fm = member_of(g, from);
-    if (fm >= 0 && g.members[fm].role == HQ_ROLE_WITNESS) {
+    const uint8_t role = fm >= 0 ? members(g)[fm].role : 0xFF;
+    if (role == HQ_ROLE_WITNESS) {
         dropped.push_back({g.cluster_id, low, high, from, HQ_DROP_WITNESS, 0});
         return CONSUMED;
     }
-    if (g.commit_due) return BARRIER;               // needs the committed index
+    if (g.has(kCommitDue)) return BARRIER;          // needs the committed index
     if (g.n_voting == 1) {                          // isSingleNodeQuorum: quorum() == 1
         ready.push_back({g.cluster_id, g.committed, low, high});
-        if (from != g.node_id && fm >= 0 && g.members[fm].role == HQ_ROLE_OBSERVER)
+        if (from != g.node_id && role == HQ_ROLE_OBSERVER)
             resps.push_back({g.cluster_id, from, g.committed, low, high});
         return CONSUMED;
     }
@@ -204,25 +273,25 @@ Verdict hq_worker::read_index(Group &g, uint64_t from, uint64_t low, uint64_t hi
         return CONSUMED;
     }
     // readIndex.addRequest (readindex.go:43-67)
-    for (const auto &r : g.reads)
-        if (r.low == low && r.high == high) return g.ri_due ? BARRIER : CONSUMED;
-    if (!g.reads.empty() && g.committed < g.reads.back().index) return FALLBACK;
-    if (g.reads.size() >= kMaxReads) return g.ri_due ? BARRIER : FALLBACK;
-    ReadStatus s;
+    ReadQueue *q = reads(g);
+    if (q) {
+        for (uint32_t i = 0; i < q->n; ++i)
+            if (q->r[i].low == low && q->r[i].high == high)
+                return g.has(kRiDue) ? BARRIER : CONSUMED;   // already pending (or released)
+        if (q->n && g.committed < q->r[q->n - 1].index) return FALLBACK;  // reference panics
+        if (q->n >= kMaxReads) return g.has(kRiDue) ? BARRIER : FALLBACK;
+    } else {
+        g.rq = rq_alloc();
+        q = &rqs[g.rq];
+    }
+    ReadStatus &s = q->r[q->n++];
     s.index = g.committed;
     s.from = from;
     s.low = low;
     s.high = high;
     s.confirmed = 0;
     std::fill(std::begin(s.ord), std::end(s.ord), kNoAck);
-    g.reads.push_back(s);
     return CONSUMED;
-}
-
-static bool is_response_type(uint32_t t) {   // isResponseMessageType (internal/raft/utils.go)
-    return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
-           t == HQ_MSG_HEARTBEAT_RESP || t == 20 /* ReadIndexResp */ ||
-           t == 8 /* SnapshotStatus */ || t == 9 /* Unreachable */;
 }
 
 Verdict hq_worker::handle(Group &g, const hq_event &e, uint64_t ei) {
@@ -230,9 +299,9 @@ Verdict hq_worker::handle(Group &g, const hq_event &e, uint64_t ei) {
     case HQ_EV_READ:
         return read_index(g, 0, e.hint, e.hint_high, ei);
     case HQ_EV_CHECK_QUORUM:
-        if (g.state != HQ_STATE_LEADER) return g.vote_due ? BARRIER : CONSUMED;
-        if (g.cq_due) return BARRIER;
-        g.cq_due = true;
+        if (g.state != HQ_STATE_LEADER) return g.has(kVoteDue) ? BARRIER : CONSUMED;
+        if (g.has(kCqDue)) return BARRIER;
+        g.set(kCqDue);
         return CONSUMED;
     case HQ_EV_ELECTION:
         if (g.pending()) return BARRIER;
@@ -242,91 +311,91 @@ Verdict hq_worker::handle(Group &g, const hq_event &e, uint64_t ei) {
         reset(g, g.term + 1);
         push_state(g, HQ_REASON_CAMPAIGN);
         g.granted = 1;
-        g.vote_due = true;                          // isSingleNodeQuorum -> the vote kernel
+        g.set(kVoteDue);                            // isSingleNodeQuorum -> the vote kernel
         return CONSUMED;
     case HQ_EV_PROPOSE:
-        if (g.pending() && (g.state != HQ_STATE_LEADER || g.cq_due)) return BARRIER;
+        if (g.pending() && (g.state != HQ_STATE_LEADER || g.has(kCqDue))) return BARRIER;
         if (g.state != HQ_STATE_LEADER) {
             defer(ei);                              // forwarded / dropped (raft.go:1845, 1932)
             return CONSUMED;
         }
         // appendEntries (raft.go:911-922)
         g.last += e.log_index;
-        if (g.members[g.self].match < g.last) g.members[g.self].match = g.last;
-        if (g.n_voting == 1) g.commit_due = true;
+        if (members(g)[0].match < g.last) members(g)[0].match = g.last;
+        if (g.n_voting == 1) g.set(kCommitDue);
         return CONSUMED;
     case HQ_EV_MESSAGE:
         break;
     default:
         return FALLBACK;
     }
-    const hq_event &m = e;
-    if (m.type != HQ_MSG_REPLICATE_RESP && m.type != HQ_MSG_HEARTBEAT_RESP &&
-        m.type != HQ_MSG_REQUEST_VOTE_RESP && m.type != HQ_MSG_READ_INDEX)
+    const uint32_t type = e.type;
+    if (type != HQ_MSG_REPLICATE_RESP && type != HQ_MSG_HEARTBEAT_RESP &&
+        type != HQ_MSG_REQUEST_VOTE_RESP && type != HQ_MSG_READ_INDEX)
         return FALLBACK;
-    const int mi = member_of(g, m.from);
-    if (is_response_type(m.type) && mi < 0) return CONSUMED;     // Peer.Handle drop
-    if (m.term != 0 && m.term != g.term) {                      // onMessageTermNotMatched
-        if (m.term < g.term) return CONSUMED;
+    const int mi = member_of(g, e.from);
+    if (mi < 0 && is_response_type(type)) return CONSUMED;      // Peer.Handle drop
+    if (e.term != 0 && e.term != g.term) {                      // onMessageTermNotMatched
+        if (e.term < g.term) return CONSUMED;
         if (g.pending()) return BARRIER;            // decisions of the run come first
-        become_follower(g, m.term, HQ_REASON_HIGHER_TERM);
+        become_follower(g, e.term, HQ_REASON_HIGHER_TERM);
     }
     if (g.state == HQ_STATE_LEADER) {
-        switch (m.type) {
+        switch (type) {
         case HQ_MSG_REPLICATE_RESP: {               // handleLeaderReplicateResp (:1671-1700)
-            hq_member &rp = g.members[mi];
-            if (!m.reject && rp.match < m.log_index) {
-                if (m.log_index > g.last) return FALLBACK;  // a follower can only ack what it got
-                rp.match = m.log_index;             // remote.tryUpdate
-                g.commit_due = true;                // -> tryCommit
+            Member &rp = members(g)[mi];
+            if (!e.reject && rp.match < e.log_index) {
+                if (e.log_index > g.last) return FALLBACK;  // a follower can only ack what it got
+                rp.match = e.log_index;             // remote.tryUpdate
+                g.set(kCommitDue);                  // -> tryCommit
             }
             rp.active = 1;
             return CONSUMED;
         }
         case HQ_MSG_HEARTBEAT_RESP: {               // handleLeaderHeartbeatResp (:1702-1714)
-            if (m.hint != 0) {                      // handleReadIndexLeaderConfirmation
-                for (auto &r : g.reads) {
-                    if (r.low != m.hint || r.high != m.hint_high) continue;
-                    const int s = g.slot_of[mi];
-                    if (s < 0) return FALLBACK;     // an observer acking a ctx
+            ReadQueue *q = e.hint != 0 ? reads(g) : nullptr;
+            if (q) {                                // handleReadIndexLeaderConfirmation
+                for (uint32_t i = 0; i < q->n; ++i) {
+                    ReadStatus &r = q->r[i];
+                    if (r.low != e.hint || r.high != e.hint_high) continue;
+                    if (mi >= g.n_voting) return FALLBACK;   // an observer acking a ctx
                     if (g.ord >= kMaxOrdinal) return BARRIER;
-                    if (!((r.confirmed >> s) & 1) && r.ord[s] == kNoAck) {
-                        r.ord[s] = ++g.ord;         // p.confirmed[from] = struct{}{}
-                        g.ri_due = true;
+                    if (!((r.confirmed >> mi) & 1) && r.ord[mi] == kNoAck) {
+                        r.ord[mi] = ++g.ord;        // p.confirmed[from] = struct{}{}
+                        g.set(kRiDue);
                     }
                     break;
                 }
             }
-            g.members[mi].active = 1;
+            members(g)[mi].active = 1;
             return CONSUMED;
         }
         case HQ_MSG_READ_INDEX:
-            return read_index(g, m.from, m.hint, m.hint_high, ei);
+            return read_index(g, e.from, e.hint, e.hint_high, ei);
         default:
             return CONSUMED;                        // RequestVoteResp: no leader handler
         }
     }
     if (g.state == HQ_STATE_CANDIDATE) {
-        if (m.type == HQ_MSG_REQUEST_VOTE_RESP) {   // handleCandidateRequestVoteResp
-            const int s = g.slot_of[mi];
-            if (s < 0) return CONSUMED;             // observer vote dropped (:1969-1972)
-            if (!(((g.granted | g.rejected) >> s) & 1)) {   // first response wins
-                if (m.reject) g.rejected |= (uint8_t)(1u << s);
-                else g.granted |= (uint8_t)(1u << s);
+        if (type == HQ_MSG_REQUEST_VOTE_RESP) {     // handleCandidateRequestVoteResp
+            if (mi >= g.n_voting) return CONSUMED;  // observer vote dropped (:1969-1972)
+            if (!(((g.granted | g.rejected) >> mi) & 1)) {   // first response wins
+                if (e.reject) g.rejected |= (uint8_t)(1u << mi);
+                else g.granted |= (uint8_t)(1u << mi);
             }
-            g.vote_due = true;
+            g.set(kVoteDue);
             return CONSUMED;
         }
-        if (g.vote_due) return BARRIER;             // may be leader by now
+        if (g.has(kVoteDue)) return BARRIER;        // may be leader by now
     }
-    if (m.type == HQ_MSG_READ_INDEX) return read_index(g, m.from, m.hint, m.hint_high, ei);
+    if (type == HQ_MSG_READ_INDEX) return read_index(g, e.from, e.hint, e.hint_high, ei);
     return CONSUMED;                                // no handler in this state
 }
 
 void hq_worker::advance(Group &g) {
     while (g.cursor < g.ev_end) {
         const uint64_t ei = g.cursor;
-        if (g.suspended) {
+        if (g.has(kSuspended)) {
             defer(ei);
             ++g.cursor;
             continue;
@@ -334,7 +403,7 @@ void hq_worker::advance(Group &g) {
         const Verdict v = handle(g, in->events[ei], ei);
         if (v == BARRIER) return;
         if (v == FALLBACK) {
-            g.suspended = true;
+            g.set(kSuspended);
             fallback.push_back(g.cluster_id);
             continue;                               // this event and the rest are deferred
         }
@@ -374,7 +443,7 @@ int hq_worker::run_pass() {
     const uint64_t Gc = l_commit.size(), Gr = l_ri.size(), Gv = l_vote.size(), Gq = l_cq.size();
     const uint32_t N = n_max;
     uint32_t K = 1;
-    for (uint32_t gi : l_ri) K = std::max<uint32_t>(K, (uint32_t)groups[gi].reads.size());
+    for (uint32_t gi : l_ri) K = std::max<uint32_t>(K, rqs[groups[gi].rq].n);
     const uint64_t sc = align_up(std::max<uint64_t>(Gc, 1), 2);   // even stride: 16-B loads
     // inputs
     Layout L;
@@ -398,7 +467,8 @@ int hq_worker::run_pass() {
     auto H = [&](size_t o) { return static_cast<uint8_t *>(host) + o; };
     auto D = [&](size_t o) { return static_cast<uint8_t *>(dev) + o; };
 
-    // pack (the SoA layout of DESIGN.md §2)
+    // pack (the SoA layout of DESIGN.md §2): voting slot s of a group is pool entry s
+    const uint64_t t0 = now_ns();
     {
         uint64_t *match = reinterpret_cast<uint64_t *>(H(c_match));
         uint8_t *nv = H(c_nv);
@@ -407,10 +477,11 @@ int hq_worker::run_pass() {
         uint64_t *ts = reinterpret_cast<uint64_t *>(H(c_ts));
         for (uint64_t j = 0; j < Gc; ++j) {
             const Group &g = groups[l_commit[j]];
-            for (uint32_t s = 0; s < N; ++s) match[s * sc + j] = 0;
-            for (size_t i = 0; i < g.members.size(); ++i)
-                if (g.slot_of[i] >= 0) match[(uint64_t)g.slot_of[i] * sc + j] = g.members[i].match;
-            nv[j] = (uint8_t)g.n_voting;
+            const Member *m = pool.data() + g.mem;
+            uint32_t s = 0;
+            for (; s < g.n_voting; ++s) match[s * sc + j] = m[s].match;
+            for (; s < N; ++s) match[s * sc + j] = 0;
+            nv[j] = g.n_voting;
             cin[j] = g.committed;
             last[j] = g.last;
             ts[j] = g.term_start;
@@ -420,10 +491,11 @@ int hq_worker::run_pass() {
         uint8_t *np = H(r_np), *rnv = H(r_nv);
         for (uint64_t j = 0; j < Gr; ++j) {
             const Group &g = groups[l_ri[j]];
-            np[j] = (uint8_t)g.reads.size();
-            rnv[j] = (uint8_t)g.n_voting;
+            const ReadQueue &q = rqs[g.rq];
+            np[j] = (uint8_t)q.n;
+            rnv[j] = g.n_voting;
             for (uint32_t k = 0; k < K; ++k) {
-                const ReadStatus *r = k < g.reads.size() ? &g.reads[k] : nullptr;
+                const ReadStatus *r = k < q.n ? &q.r[k] : nullptr;
                 idx[(uint64_t)k * Gr + j] = r ? r->index : 0;
                 for (uint32_t s = 0; s < N; ++s)
                     ord[((uint64_t)k * N + s) * Gr + j] =
@@ -435,20 +507,22 @@ int hq_worker::run_pass() {
             const Group &g = groups[l_vote[j]];
             gr[j] = g.granted;
             rj[j] = g.rejected;
-            vnv[j] = (uint8_t)g.n_voting;
+            vnv[j] = g.n_voting;
         }
         uint8_t *act = H(q_act), *qnv = H(q_nv);
         for (uint64_t j = 0; j < Gq; ++j) {
             const Group &g = groups[l_cq[j]];
+            const Member *m = pool.data() + g.mem;
             uint8_t a = 0;
-            for (size_t i = 0; i < g.members.size(); ++i)
-                if (g.slot_of[i] >= 0 && g.members[i].active) a |= (uint8_t)(1u << g.slot_of[i]);
+            for (uint32_t s = 0; s < g.n_voting; ++s) a |= (uint8_t)(m[s].active << s);
             act[j] = a;
-            qnv[j] = (uint8_t)g.n_voting;
+            qnv[j] = g.n_voting;
         }
     }
 
     // one H2D, the decisions, one D2H, one sync
+    const uint64_t t1 = now_ns();
+    t_pack += t1 - t0;
     rc = hq(hq_memcpy_async(ctx, dev, host, in_bytes, 0), "hq_memcpy_async(H2D)");
     if (!rc && Gc) {
         hq_commit_args a{};
@@ -487,80 +561,77 @@ int hq_worker::run_pass() {
     if (!rc) rc = hq(hq_sync(ctx), "hq_sync");
     if (rc) return rc;
     decisions += Gc + Gr + Gv + Gq;
+    const uint64_t t2 = now_ns();
+    t_device += t2 - t1;
 
-    auto bit = [](const uint8_t *words, uint64_t j) {
-        return (reinterpret_cast<const uint64_t *>(words)[j >> 6] >> (j & 63)) & 1;
-    };
     // every group handed to a kernel satisfies its contract; a fallback bit is an internal error
-    for (uint64_t j = 0; j < Gc; ++j)
-        if (bit(H(c_fb), j)) return fail(HQ_E_STATE, "commit kernel refused a packed group");
-    for (uint64_t j = 0; j < Gr; ++j)
-        if (bit(H(r_fb), j)) return fail(HQ_E_STATE, "ReadIndex kernel refused a packed group");
-    for (uint64_t j = 0; j < Gv; ++j)
-        if (bit(H(v_fb), j)) return fail(HQ_E_STATE, "vote kernel refused a packed group");
-    for (uint64_t j = 0; j < Gq; ++j)
-        if (bit(H(q_fb), j)) return fail(HQ_E_STATE, "CheckQuorum kernel refused a packed group");
+    auto any = [&](size_t o, uint64_t G) {
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(H(o));
+        for (uint64_t i = 0; i < (G + 63) / 64; ++i)
+            if (w[i]) return true;
+        return false;
+    };
+    if (any(c_fb, Gc) || any(r_fb, Gr) || any(v_fb, Gv) || any(q_fb, Gq))
+        return fail(HQ_E_STATE, "a kernel refused a packed group (worker contract bug)");
 
     // apply, per group in the reference's order: commit, ReadIndex release, vote, CheckQuorum
     const uint64_t *cout = reinterpret_cast<const uint64_t *>(H(c_out));
     for (uint64_t j = 0; j < Gc; ++j) {
         Group &g = groups[l_commit[j]];
         g.committed = cout[j];                      // commitTo (logentry.go:323-332)
-        g.commit_due = false;
+        g.clear(kCommitDue);
     }
     const uint64_t *rel = reinterpret_cast<const uint64_t *>(H(r_rel));
     const uint8_t *cnt = H(r_cnt), *be = H(r_be);
     for (uint64_t j = 0; j < Gr; ++j) {
         Group &g = groups[l_ri[j]];
+        ReadQueue &q = rqs[g.rq];
         const uint32_t c = cnt[j];
         for (uint32_t i = 0; i < c; ++i) {
             uint32_t k = i;                         // the ctx whose confirm() released entry i
             while (k < c && !((be[j] >> k) & 1)) ++k;
             if (k >= c) return fail(HQ_E_STATE, "ReadIndex release without a closing ctx");
-            const ReadStatus &s = g.reads[i];
+            const ReadStatus &s = q.r[i];
             const uint64_t index = rel[(uint64_t)i * Gr + j];
             if (s.from == 0 || s.from == g.node_id)
                 ready.push_back({g.cluster_id, index, s.low, s.high});
             else
-                resps.push_back({g.cluster_id, s.from, index, g.reads[k].low, g.reads[k].high});
+                resps.push_back({g.cluster_id, s.from, index, q.r[k].low, q.r[k].high});
         }
-        g.reads.erase(g.reads.begin(), g.reads.begin() + c);
-        for (auto &r : g.reads) {                   // carry the run's confirmations over
+        std::copy(q.r + c, q.r + q.n, q.r);         // r.queue = r.queue[done:]
+        q.n -= c;
+        for (uint32_t i = 0; i < q.n; ++i) {        // carry the run's confirmations over
+            ReadStatus &r = q.r[i];
             for (uint32_t s = 0; s < HQ_MAX_VOTERS; ++s) {
                 if (r.ord[s] != kNoAck) r.confirmed |= (uint8_t)(1u << s);
                 r.ord[s] = kNoAck;
             }
         }
+        if (q.n == 0) rq_release(g);
         g.ord = 0;
-        g.ri_due = false;
+        g.clear(kRiDue);
     }
     const uint64_t *outc = reinterpret_cast<const uint64_t *>(H(v_out));
     for (uint64_t j = 0; j < Gv; ++j) {
         Group &g = groups[l_vote[j]];
-        g.vote_due = false;
+        g.clear(kVoteDue);
         const uint32_t o = (uint32_t)((outc[j >> 5] >> (2 * (j & 31))) & 3);
         if (o == HQ_OUTCOME_LEADER) become_leader(g);
         else if (o == HQ_OUTCOME_FOLLOWER) become_follower(g, g.term, HQ_REASON_VOTE);
     }
+    const uint64_t *hqb = reinterpret_cast<const uint64_t *>(H(q_hq));
     for (uint64_t j = 0; j < Gq; ++j) {
         Group &g = groups[l_cq[j]];
-        g.cq_due = false;
-        for (size_t i = 0; i < g.members.size(); ++i)   // setNotActive (remote.go:196-198)
-            if (g.slot_of[i] >= 0) g.members[i].active = 0;
-        if (!bit(H(q_hq), j)) become_follower(g, g.term, HQ_REASON_CHECK_QUORUM);
+        g.clear(kCqDue);
+        Member *m = members(g);
+        for (uint32_t s = 0; s < g.n_voting; ++s) m[s].active = 0;   // setNotActive
+        if (!((hqb[j >> 6] >> (j & 63)) & 1)) become_follower(g, g.term, HQ_REASON_CHECK_QUORUM);
     }
+    t_apply += now_ns() - t2;
     return HQ_OK;
 }
 
 // ------------------------------------------------------------------------------ step -------
-namespace {
-uint64_t now_ns() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-}
-}  // namespace
-
 int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     const uint64_t t0 = now_ns();
     uint64_t t_pass = 0;
@@ -573,6 +644,7 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     deferred.clear();
     fallback.clear();
     decisions = 0;
+    t_pack = t_device = t_apply = 0;
     uint64_t passes = 0;
 
     // the groups with events, each with its slice of the event array (node.mq per node)
@@ -585,34 +657,30 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
         if (gi >= groups.size()) { rc = fail(HQ_E_INVAL, "hq_worker_step: unknown group handle"); break; }
         if (e < b) { rc = fail(HQ_E_INVAL, "hq_worker_step: offsets decrease"); break; }
         Group &g = groups[gi];
-        if (g.touched) { rc = fail(HQ_E_INVAL, "hq_worker_step: a group is listed twice"); break; }
-        g.touched = true;
+        if (g.has(kTouched)) { rc = fail(HQ_E_INVAL, "hq_worker_step: a group is listed twice"); break; }
+        g.set(kTouched);
         g.committed0 = g.committed;
         touched.push_back(gi);
         if (b == e) continue;
         g.cursor = b;
         g.ev_end = e;
-        g.in_work = true;
+        g.set(kInWork);
         work.push_back(gi);
     }
-    if (rc) {
-        for (uint32_t gi : touched) groups[gi].touched = groups[gi].in_work = false;
-        return rc;
-    }
 
-    while (!work.empty()) {
+    while (!rc && !work.empty()) {
         l_commit.clear();
         l_ri.clear();
         l_vote.clear();
         l_cq.clear();
         for (uint32_t gi : work) {
             Group &g = groups[gi];
-            g.in_work = false;
+            g.clear(kInWork);
             advance(g);
-            if (g.commit_due) l_commit.push_back(gi);
-            if (g.ri_due) l_ri.push_back(gi);
-            if (g.vote_due) l_vote.push_back(gi);
-            if (g.cq_due) l_cq.push_back(gi);
+            if (g.has(kCommitDue)) l_commit.push_back(gi);
+            if (g.has(kRiDue)) l_ri.push_back(gi);
+            if (g.has(kVoteDue)) l_vote.push_back(gi);
+            if (g.has(kCqDue)) l_cq.push_back(gi);
         }
         if (l_commit.empty() && l_ri.empty() && l_vote.empty() && l_cq.empty()) break;
         const uint64_t tp = now_ns();
@@ -624,9 +692,9 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
         for (const auto *l : {&l_commit, &l_ri, &l_vote, &l_cq})
             for (uint32_t gi : *l) {
                 Group &g = groups[gi];
-                if (g.in_work) continue;
+                if (g.has(kInWork)) continue;
                 if (g.cursor < g.ev_end || g.pending()) {
-                    g.in_work = true;
+                    g.set(kInWork);
                     next_work.push_back(gi);
                 }
             }
@@ -634,7 +702,7 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     }
     for (uint32_t gi : touched) {
         Group &g = groups[gi];
-        g.touched = g.in_work = false;
+        g.clear(kTouched | kInWork);
         if (g.committed != g.committed0) commits.push_back({g.cluster_id, g.committed});
     }
     if (rc) return rc;
@@ -656,6 +724,9 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     out->gpu_passes = passes;
     out->decisions = decisions;
     out->pass_ns = t_pass;
+    out->pack_ns = t_pack;
+    out->device_ns = t_device;
+    out->apply_ns = t_apply;
     out->handle_ns = now_ns() - t0 - t_pass;
     return HQ_OK;
 }
@@ -700,13 +771,36 @@ int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member 
     if (!g) return w->fail(HQ_E_INVAL, "hq_worker_add_group: group is NULL");
     if (w->index.count(g->cluster_id)) return w->fail(HQ_E_INVAL, "hq_worker_add_group: cluster exists");
     if (w->groups.size() >= UINT32_MAX) return w->fail(HQ_E_NOMEM, "hq_worker_add_group: too many groups");
-    Group n;
-    int rc = w->load_group(n, g, members);
-    if (rc) return rc;
+    Group n{};
+    n.rq = kNone;
+    const size_t pool0 = w->pool.size();
+    int rc = w->load_group(n, g, members, true);
+    if (rc) {
+        w->pool.resize(pool0);
+        return rc;
+    }
     const uint32_t h = (uint32_t)w->groups.size();
     w->index.emplace(g->cluster_id, h);
-    w->groups.push_back(std::move(n));
+    w->groups.push_back(n);
     if (handle) *handle = h;
+    return HQ_OK;
+}
+
+int hq_worker_add_groups(hq_worker *w, const hq_worker_group *groups, uint64_t count,
+                         const hq_member *members) {
+    if (!w) return HQ_E_INVAL;
+    if (count && (!groups || !members))
+        return w->fail(HQ_E_INVAL, "hq_worker_add_groups: NULL argument");
+    w->groups.reserve(w->groups.size() + count);
+    w->index.reserve(w->groups.size() + count);
+    uint64_t off = 0, nm = 0;
+    for (uint64_t i = 0; i < count; ++i) nm += groups[i].n_members;
+    w->pool.reserve(w->pool.size() + nm);
+    for (uint64_t i = 0; i < count; ++i) {
+        int rc = hq_worker_add_group(w, groups + i, members + off, nullptr);
+        if (rc) return rc;
+        off += groups[i].n_members;
+    }
     return HQ_OK;
 }
 
@@ -718,31 +812,15 @@ int hq_worker_find(hq_worker *w, uint64_t cluster_id, uint32_t *handle) {
     return HQ_OK;
 }
 
-int hq_worker_add_groups(hq_worker *w, const hq_worker_group *groups, uint64_t count,
-                         const hq_member *members) {
-    if (!w) return HQ_E_INVAL;
-    if (count && (!groups || !members))
-        return w->fail(HQ_E_INVAL, "hq_worker_add_groups: NULL argument");
-    w->groups.reserve(w->groups.size() + count);
-    w->index.reserve(w->groups.size() + count);
-    uint64_t off = 0;
-    for (uint64_t i = 0; i < count; ++i) {
-        int rc = hq_worker_add_group(w, groups + i, members + off, nullptr);
-        if (rc) return rc;
-        off += groups[i].n_members;
-    }
-    return HQ_OK;
-}
-
 int hq_worker_set_group(hq_worker *w, const hq_worker_group *g, const hq_member *members) {
     if (!w) return HQ_E_INVAL;
     if (!g) return w->fail(HQ_E_INVAL, "hq_worker_set_group: group is NULL");
     auto it = w->index.find(g->cluster_id);
     if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_set_group: unknown cluster");
-    Group n;
-    int rc = w->load_group(n, g, members);
+    Group n = w->groups[it->second];
+    int rc = w->load_group(n, g, members, false);
     if (rc) return rc;
-    w->groups[it->second] = std::move(n);
+    w->groups[it->second] = n;
     return HQ_OK;
 }
 
@@ -753,6 +831,7 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *out,
     auto it = w->index.find(cluster_id);
     if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_get_group: unknown cluster");
     const Group &g = w->groups[it->second];
+    const ReadQueue *q = g.rq == kNone ? nullptr : &w->rqs[g.rq];
     if (out) {
         out->cluster_id = g.cluster_id;
         out->node_id = g.node_id;
@@ -761,15 +840,19 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *out,
         out->last_index = g.last;
         out->term_start = g.term_start;
         out->state = g.state;
-        out->n_members = (uint32_t)g.members.size();
-        out->n_pending_reads = (uint32_t)g.reads.size();
-        out->suspended = g.suspended;
+        out->n_members = g.n_members;
+        out->n_pending_reads = q ? q->n : 0;
+        out->suspended = g.has(kSuspended);
     }
-    if (members)
-        for (uint32_t i = 0; i < cap && i < g.members.size(); ++i) members[i] = g.members[i];
-    if (reads)
-        for (uint32_t i = 0; i < reads_cap && i < g.reads.size(); ++i) {
-            const ReadStatus &r = g.reads[i];
+    if (members) {                                  // back in the caller's order
+        const Member *m = w->pool.data() + g.mem;
+        for (uint32_t i = 0; i < g.n_members; ++i)
+            if (m[i].order < cap)
+                members[m[i].order] = hq_member{m[i].node_id, m[i].match, m[i].role, m[i].active};
+    }
+    if (reads && q)
+        for (uint32_t i = 0; i < reads_cap && i < q->n; ++i) {
+            const ReadStatus &r = q->r[i];
             uint32_t n = 0;
             for (uint32_t s = 0; s < HQ_MAX_VOTERS; ++s)
                 n += ((r.confirmed >> s) & 1) || r.ord[s] != kNoAck;

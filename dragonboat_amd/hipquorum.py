@@ -135,7 +135,9 @@ class StepOutput(ctypes.Structure):
     _fields_ = [f for name, _ in STEP_OUTPUT_LISTS
                 for f in ((name, _vp), ("n_" + name, ctypes.c_uint64))] + \
                [("gpu_passes", ctypes.c_uint64), ("decisions", ctypes.c_uint64),
-                ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64)]
+                ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64),
+                ("pack_ns", ctypes.c_uint64), ("device_ns", ctypes.c_uint64),
+                ("apply_ns", ctypes.c_uint64)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -637,9 +639,10 @@ class Worker:
                                             len(r)), "hq_worker_get_group")
         return g[0], m, r
 
-    def step(self, groups, offsets, events):
+    def step(self, groups, offsets, events, copy=True):
         """One step: `groups` (uint32 handles), `offsets` (uint64, len(groups) + 1) and
-        `events` (EVENT_DTYPE). Returns a dict of numpy record arrays (copies) plus counters."""
+        `events` (EVENT_DTYPE). Returns a dict of numpy record arrays plus counters; with
+        copy=False the arrays are views of the worker's buffers, valid until its next call."""
         groups = np.ascontiguousarray(groups, np.uint32)
         offsets = np.ascontiguousarray(offsets, np.uint64)
         events = np.ascontiguousarray(events, EVENT_DTYPE)
@@ -656,8 +659,9 @@ class Worker:
                 res[name] = np.zeros(0, dt)
                 continue
             buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
-            res[name] = np.frombuffer(buf, dt).copy()
-        for k in ("gpu_passes", "decisions", "handle_ns", "pass_ns"):
+            res[name] = np.frombuffer(buf, dt).copy() if copy else np.frombuffer(buf, dt)
+        for k in ("gpu_passes", "decisions", "handle_ns", "pass_ns", "pack_ns", "device_ns",
+                  "apply_ns"):
             res[k] = getattr(out, k)
         return res
 

@@ -476,6 +476,9 @@ typedef struct hq_step_output {
     uint64_t decisions;         /* group decisions taken on the GPU in this step */
     uint64_t handle_ns;         /* wall time: the host bookkeeping of the events */
     uint64_t pass_ns;           /* wall time: GPU passes (pack, copies, kernels, sync, apply) */
+    uint64_t pack_ns;           /*   of which packing the kernels' SoA inputs */
+    uint64_t device_ns;         /*   of which H2D + kernels + D2H + sync */
+    uint64_t apply_ns;          /*   of which applying the decisions */
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;
