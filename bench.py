@@ -39,6 +39,9 @@ WORKLOADS = {
     "c3": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=1, mixed=False,
                desc="1M groups x 5 voters (4 full + 1 witness; observers never packed), "
                     "commit + term-ring gather R=16"),
+    "c3r32": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=3, mixed=False,
+                  desc="1M groups x 5 voters (4 full + 1 witness), commit + term-ring gather "
+                       "from a u32 ring (R = 16; two groups per gathered 128-B line)"),
     "c3m": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False,
                 desc="1M groups x 5 voters (4 full + 1 witness), commit + 16-bit current-term "
                      "mask (exact replacement of the ring gather)"),
@@ -46,10 +49,14 @@ WORKLOADS = {
                desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
                desc="64M groups mixed 3/5/7 voters (n = {3,5,7}[clusterID % 3]) sharded "
-                    "clusterID % 8: 8M groups per GPU, one launch per voter-count bucket, "
-                    "current-term mask"),
+                    "clusterID % 8: 8M groups per GPU, the three voter-count buckets in one "
+                    "fused launch, current-term mask"),
     "c5r": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=1, mixed=True,
                 desc="as c5 with the u64 term-ring gather (R = 16)"),
+    "c5r32": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=3, mixed=True,
+                  desc="as c5 with the u32 term-ring gather (R = 16)"),
+    "c5s": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True, separate=True,
+                desc="as c5 with one launch per voter-count bucket (3 launches per step)"),
 }
 
 
@@ -57,8 +64,9 @@ def algo_bytes_per_group(w):
     """bytes the decision must move per group."""
     if w["kind"] == "commit":
         n, extra_n = w["n"], (1 if w["mixed"] else 0)
-        # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask)
-        return 8 * n + 24 + {0: 8, 1: 16, 2: 2}[w["form"]] + extra_n
+        # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask
+        # | term + gathered u32 ring term)
+        return 8 * n + 24 + {0: 8, 1: 16, 2: 2, 3: 12}[w["form"]] + extra_n
     return 4 + 3 / 8   # ack, granted, rejected, n (u8 each) in; confirmed bit + 2-bit outcome out
 
 
@@ -186,7 +194,15 @@ def run_gpu(w, steps, warmup, d: Dist):
     ctx = hq.Context(d.device)
     sets, per_set = build_sets(ctx, hq, shard, w, d)
     G = w["G"]
-    if w["kind"] == "commit":
+    if w["kind"] == "commit" and w["mixed"] and not w.get("separate"):
+        # a step = the rank's voter-count buckets decided by one fused launch
+        per_step = [hq.commit_batch_array([b.args() for b in bs]) for bs in sets]
+        seq, wseq = list(range(steps)), list(range(max(1, warmup)))
+
+        def run(idx):
+            for i in idx:
+                ctx.commit_fused_dev(per_step[i % len(per_step)])
+    elif w["kind"] == "commit":
         def flat(k):
             return hq.commit_batch_array([b.args() for i in range(k) for b in sets[i % len(sets)]])
         seq, wseq = flat(steps), flat(max(1, warmup))
@@ -227,6 +243,51 @@ def run_gpu(w, steps, warmup, d: Dist):
     )
     ctx.close()
     return res
+
+
+def run_concurrent(w, steps, warmup, d: Dist, W=2):
+    """W step workers stepping the same workload concurrently, each with its own hq_ctx (= its
+    own HIP stream; dragonboat runs one goroutine per step worker, execengine.go:675-690, and
+    the boundary gives each its own context): step i runs on worker i % W, so one worker's
+    grid fill / drain overlaps another's stream. Kernels of different workers overlap, so only
+    the aggregate rate (bytes / wall time) is meaningful here, not a per-kernel duration."""
+    from dragonboat_amd import hipquorum as hq
+    from dragonboat_amd import shard
+
+    ctxs = [hq.Context(d.device) for _ in range(W)]
+    sets, per_set = build_sets(ctxs[0], hq, shard, w, d)
+
+    def seqs(k):
+        return [hq.commit_batch_array([b.args() for i in range(c, k, W)
+                                       for b in sets[i % len(sets)]]) for c in range(W)]
+
+    def run(arrs):
+        for c, a in zip(ctxs, arrs):
+            c.commit_many_dev(a)
+        for c in ctxs:
+            c.sync()
+
+    run(seqs(max(W, warmup)))
+    d.sync_device()
+    d.barrier()
+    timed = seqs(steps)
+    t0 = time.perf_counter()
+    run(timed)
+    d.sync_device()
+    d.barrier()
+    elapsed = d.max(time.perf_counter() - t0)
+    for c in ctxs:
+        c.close()
+    gbs = d.sum(float(per_set * steps)) / elapsed / 1e9
+    return {
+        "workload": f"w{W}: the headline workload ({w['G']} groups x {w['n']} voters per step, "
+                    f"term-start form) stepped by {W} concurrent step workers, one HIP stream "
+                    f"each, step i on worker i % {W}",
+        "value": d.sum(float(groups_per_step(w) * steps)) / elapsed, "unit": "decisions/s",
+        "ms_per_step": elapsed / steps * 1e3,
+        "aggregate_gbs": gbs, "aggregate_frac_of_peak": gbs / d.world / HBM_PEAK_GBS,
+        "note": "kernels of different workers overlap; rate = algorithmic bytes / wall time",
+    }
 
 
 def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
@@ -521,7 +582,7 @@ def main():
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c3,c3m,c4,c5,c5r,e2e,step",
+    ap.add_argument("--extra", default="c3,c3r32,c3m,c4,c5,c5s,c5r,c5r32,w2,e2e,step",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -534,12 +595,16 @@ def main():
     r = run_gpu(w, args.steps, args.warmup, d)
     extras = []
     e2e = step_leg = None
+    conc = []
     for name in [x for x in args.extra.split(",") if x and x != args.workload]:
         if name == "e2e":
             e2e = run_e2e(max(20, args.steps // 20), 3, d)
             continue
         if name == "step":
             step_leg = run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu)
+            continue
+        if name.startswith("w") and name[1:].isdigit():
+            conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))
             continue
         we = WORKLOADS[name]
         re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
@@ -566,7 +631,7 @@ def main():
             "config": {
                 "workload": f"{args.workload}: {w['desc']}",
                 "groups_per_gpu": w["G"], "voters": w["n"],
-                "form": {0: "term_start", 1: "ring", 2: "term_mask"}[w["form"]]
+                "form": {0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
                 if w["kind"] == "commit" else "bitmaps",
                 "global_groups_per_step": w["G"] * d.world,
                 "parallelism": f"shard{d.world} (clusterID % {d.world})",
@@ -591,7 +656,7 @@ def main():
                     "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
-            ] + ([e2e] if e2e else []) + ([step_leg] if step_leg else []),
+            ] + conc + ([e2e] if e2e else []) + ([step_leg] if step_leg else []),
         }
         print(json.dumps(line), flush=True)
     d.close()

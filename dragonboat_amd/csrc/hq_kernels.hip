@@ -18,13 +18,15 @@ constexpr int kMaxBlocks = 256 * 16;  // grid-stride beyond 16 workgroups per CU
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Streaming columns are read once and written once: nontemporal loads/stores (measured ~6 %
-// faster than plain ones on the 1M x 3 commit stream, tools/kexp.hip).
+// Streaming columns are read once: nontemporal loads (measured ~6 % faster than plain ones on
+// the 1M x 3 commit stream, tools/kexp.hip). The committed column is stored with plain stores:
+// 11.10 vs 11.45 us per 1M x 3 launch against nontemporal ones (tools/kexp3.hip; sc1
+// write-through 11.19, nt sc1 12.36).
 __device__ __forceinline__ u64x2 ld_stream2(const uint64_t *p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
 }
 __device__ __forceinline__ void st_stream2(uint64_t *p, u64x2 v) {
-    __builtin_nontemporal_store(v, reinterpret_cast<u64x2 *>(p));
+    *reinterpret_cast<u64x2 *>(p) = v;
 }
 
 struct CommitK {
@@ -41,6 +43,7 @@ struct CommitK {
     uint64_t *changed;
     uint64_t *fallback;
     const uint16_t *mask;
+    const uint32_t *ring32;
 };
 
 // ---- compare-exchange networks over u64 held in registers --------------------------------
@@ -102,7 +105,8 @@ __device__ __forceinline__ uint64_t spread32(uint32_t x) {  // bit i -> bit 2i
 }
 
 // One group's decision given its packed matches. FORM 0 = term-start, 1 = ring gather,
-// 2 = current-term mask. aux = term_start (0), the leader's term (1) or the mask (2).
+// 2 = current-term mask, 3 = u32 ring gather. aux = term_start (0), the leader's term (1, 3) or
+// the mask (2).
 template <int N, int FORM, bool PERN>
 __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&m)[N], int n,
                                        uint64_t cin, uint64_t last, uint64_t aux,
@@ -131,6 +135,15 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
         // bit (i mod R) of the mask = term(i) == term for i in (last - R, last]
         fb = (cin > last) || (last - cin > a.R);
         chg = !fb && q > cin && q <= last && ((aux >> (q & (uint64_t)(a.R - 1))) & 1);
+    } else if constexpr (FORM == HQ_FORM_TERM_RING32) {
+        // the same gather from a u32 ring (entries saturated at 0xFFFFFFFF by the packer): with
+        // the leader's term below 0xFFFFFFFF, ring32 == term <=> term(i) == term. Two groups'
+        // rings share one 128-B line, so a lane's pair of gathers costs one line, not two.
+        fb = (aux == 0) | (aux >= 0xFFFFFFFFull) | (cin > last) || (last - cin > a.R);
+        if (!fb && q > cin && q <= last) {
+            const uint32_t lterm = a.ring32[g * a.R + (q & (uint64_t)(a.R - 1))];
+            chg = lterm == (uint32_t)aux;
+        }
     } else {
         // aux = the leader's term; the ring holds term(i) for i in (last - R, last]
         fb = (aux == 0) | (cin > last) || (last - cin > a.R);
@@ -142,12 +155,14 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
     cout = chg ? q : cin;
 }
 
-// VEC = groups per lane (2: 16-byte loads of every SoA column; 1: 8-byte loads).
+// VEC = groups per lane (2: 16-byte loads of every SoA column; 1: 8-byte loads). The body of
+// one workgroup `blk` of `nblk` working on batch `a` (k_commit: the grid; k_commit_fused: the
+// workgroups one batch of the launch owns).
 template <int N, int FORM, int VEC, bool PERN>
-__global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
+__device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * (kCommitBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t step = (uint64_t)gridDim.x * kCommitBlock * VEC;
+    const uint64_t wave = blk * (kCommitBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = nblk * kCommitBlock * VEC;
     const uint64_t *aux_col = (FORM == HQ_FORM_TERM_START) ? a.tstart : a.term;
     // aux of group g: the u64 column (forms 0, 1) or the u16 term mask (form 2)
     auto aux1 = [&](uint64_t g) -> uint64_t {
@@ -236,6 +251,42 @@ __global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
     }
 }
 
+template <int N, int FORM, int VEC, bool PERN>
+__global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
+    commit_blocks<N, FORM, VEC, PERN>(a, blockIdx.x, gridDim.x);
+}
+
+// Several uniform-n batches of one step in ONE launch (a step worker's voter-count buckets):
+// batch i owns workgroups [first[i], first[i+1]); the batch index and its n are uniform per
+// workgroup, so the switch costs no divergence. Saves the dependent-launch boundary and the
+// grid fill / drain between buckets (MI355X_MICROARCH.md "boundary": 1.7-1.9 us each).
+constexpr int kMaxFused = 8;
+struct FusedK {
+    CommitK b[kMaxFused];
+    uint32_t first[kMaxFused + 1];
+    uint8_t n[kMaxFused];
+    uint32_t count;
+};
+
+template <int FORM>
+__global__ __launch_bounds__(kCommitBlock) void k_commit_fused(const FusedK f) {
+    const uint32_t blk = blockIdx.x;
+    uint32_t i = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
+    const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
+    switch (f.n[i]) {
+    case 1: commit_blocks<1, FORM, 2, false>(f.b[i], b, nb); break;
+    case 2: commit_blocks<2, FORM, 2, false>(f.b[i], b, nb); break;
+    case 3: commit_blocks<3, FORM, 2, false>(f.b[i], b, nb); break;
+    case 4: commit_blocks<4, FORM, 2, false>(f.b[i], b, nb); break;
+    case 5: commit_blocks<5, FORM, 2, false>(f.b[i], b, nb); break;
+    case 6: commit_blocks<6, FORM, 2, false>(f.b[i], b, nb); break;
+    case 7: commit_blocks<7, FORM, 2, false>(f.b[i], b, nb); break;
+    default: commit_blocks<8, FORM, 2, false>(f.b[i], b, nb); break;
+    }
+}
+
 // ---- ReadIndex / vote / CheckQuorum over u8 bitmaps: 16 groups per lane ---------------------
 struct BitsK {
     uint64_t G;
@@ -300,81 +351,101 @@ __device__ __forceinline__ uint32_t mask_n(uint32_t n) {
     return __builtin_amdgcn_perm(0x7F3F1F0Fu, 0x07030100u, sel);
 }
 
+// One 16-group slot starting at group g. FULL: all 16 groups exist (g + 16 <= G), so every load
+// is one unconditional 16-byte nontemporal load and no byte needs masking (the common case; the
+// ragged tail slot takes the guarded path).
+template <int MODE, bool PERN, bool FULL>
+__device__ __forceinline__ void bits_slot(const BitsK &a, uint64_t g, uint32_t nu) {
+    const uint64_t slot = g >> 4;
+    V16 nv = {}, ack = {}, gr = {}, rj = {}, ac = {};
+    auto ld = [&](const uint8_t *p) -> V16 {
+        if constexpr (FULL) {
+            V16 r;
+            r.w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + g));
+            return r;
+        }
+        return g < a.G ? load16(p, g, a.G) : V16{};
+    };
+    if constexpr (PERN) nv = ld(a.nv);
+    if constexpr (MODE & kRI) ack = ld(a.ack);
+    if constexpr (MODE & kVOTE) {
+        gr = ld(a.granted);
+        rj = ld(a.rejected);
+    }
+    if constexpr (MODE & kCHECKQ) ac = ld(a.active);
+    uint32_t conf = 0, outc = 0, hq = 0, fb = 0;
+    V16 keep;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        // bytes of groups >= G are excluded (their output bits stay 0)
+        uint32_t inr = kB80;
+        if constexpr (!FULL) {
+            const uint64_t left = g < a.G ? a.G - g : 0;
+            inr = left >= (uint64_t)(4 * w + 4) ? kB80
+                  : left <= (uint64_t)(4 * w)   ? 0u
+                                                : (kB80 >> (8 * (4 - (uint32_t)(left - 4 * w))));
+        }
+        const uint32_t n = PERN ? nv.w[w] : nu;
+        const uint32_t ok = valid_n(n) & inr;
+        const uint32_t mask = mask_n(n);
+        const uint32_t quorum = ((n >> 1) & 0x7F7F7F7Fu) + kB01;  // n/2 + 1 (valid bytes)
+        uint32_t bad = ~ok & inr;
+        if constexpr (MODE & kRI) {
+            // readindex.go:84: len(confirmed) + 1 >= quorum  <=>  acks >= quorum - 1
+            const uint32_t c = popc_bytes(ack.w[w] & mask);
+            conf |= pack4(ge_bytes(c, quorum - kB01) & ok) << (4 * w);
+        }
+        if constexpr (MODE & kVOTE) {
+            const uint32_t gm = gr.w[w] & mask;
+            const uint32_t rm = rj.w[w] & mask & ~gm;  // first response wins
+            const uint32_t lead = ge_bytes(popc_bytes(gm), quorum) & ok;
+            const uint32_t foll = ge_bytes(popc_bytes(rm), quorum) & ok & ~lead;
+            const uint32_t cand = inr & ~lead & ~foll;
+            // 2-bit codes: leader 2 (bit 1), candidate 1 (bit 0), follower 0
+            outc |= (pack4x2(cand) | (pack4x2(lead) << 1)) << (8 * w);
+        }
+        if constexpr (MODE & kCHECKQ) {
+            const uint32_t self = kB01 << a.self_slot;
+            const uint32_t selfok = ge_bytes(n, (a.self_slot + 1) * kB01) & ok;
+            bad = ~selfok & inr;
+            const uint32_t c = popc_bytes((ac.w[w] | self) & mask);
+            hq |= pack4(ge_bytes(c, quorum) & selfok) << (4 * w);
+            // setNotActive for every voting member (raft.go:385, remote.go:196-198);
+            // groups left to the CPU path keep their flags
+            keep.w[w] = ac.w[w] & ((bad >> 7) * 0xFFu);
+        }
+        fb |= pack4(bad) << (4 * w);
+    }
+    // 64-group bitmap words viewed as 16-bit slots, 32-group outcome words as 32-bit slots
+    // (a full slot lies below G / 16 <= n16, n16o)
+    if (FULL || slot < a.n16) {
+        if constexpr (MODE & kRI) reinterpret_cast<uint16_t *>(a.confirmed)[slot] = conf;
+        if constexpr (MODE & kCHECKQ) reinterpret_cast<uint16_t *>(a.has_quorum)[slot] = hq;
+        if (a.fallback) reinterpret_cast<uint16_t *>(a.fallback)[slot] = fb;
+    }
+    if constexpr (MODE & kVOTE) {
+        if (FULL || slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
+    }
+    if constexpr (MODE & kCHECKQ) {
+        if constexpr (FULL) {
+            *reinterpret_cast<uint4 *>(a.active + g) = keep.v;
+        } else {
+            for (int k = 0; k < 16; ++k)
+                if (g + k < a.G) a.active[g + k] = keep.b[k];
+        }
+    }
+}
+
 template <int MODE, bool PERN, int BLK>
 __global__ __launch_bounds__(BLK) void k_bits(const BitsK a) {
     const uint64_t tid = (uint64_t)blockIdx.x * BLK + threadIdx.x;
     const uint64_t step = (uint64_t)gridDim.x * BLK * 16;
     const uint32_t nu = a.n_uniform * kB01;  // n_uniform <= 8: no byte overflow
     for (uint64_t g = tid * 16; g < a.n16o * 16 || g < a.n16 * 16; g += step) {
-        const uint64_t slot = g >> 4;
-        V16 nv = {}, ack = {}, gr = {}, rj = {}, ac = {};
-        if (g < a.G) {
-            if constexpr (PERN) nv = load16(a.nv, g, a.G);
-            if constexpr (MODE & kRI) ack = load16(a.ack, g, a.G);
-            if constexpr (MODE & kVOTE) {
-                gr = load16(a.granted, g, a.G);
-                rj = load16(a.rejected, g, a.G);
-            }
-            if constexpr (MODE & kCHECKQ) ac = load16(a.active, g, a.G);
-        }
-        uint32_t conf = 0, outc = 0, hq = 0, fb = 0;
-        V16 keep;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            // bytes of groups >= G are excluded (their output bits stay 0)
-            const uint64_t left = g < a.G ? a.G - g : 0;
-            const uint32_t inr = left >= (uint64_t)(4 * w + 4) ? kB80
-                                 : left <= (uint64_t)(4 * w) ? 0u
-                                 : (kB80 >> (8 * (4 - (uint32_t)(left - 4 * w))));
-            const uint32_t n = PERN ? nv.w[w] : nu;
-            const uint32_t ok = valid_n(n) & inr;
-            const uint32_t mask = mask_n(n);
-            const uint32_t quorum = ((n >> 1) & 0x7F7F7F7Fu) + kB01;  // n/2 + 1 (valid bytes)
-            uint32_t bad = ~ok & inr;
-            if constexpr (MODE & kRI) {
-                // readindex.go:84: len(confirmed) + 1 >= quorum  <=>  acks >= quorum - 1
-                const uint32_t c = popc_bytes(ack.w[w] & mask);
-                conf |= pack4(ge_bytes(c, quorum - kB01) & ok) << (4 * w);
-            }
-            if constexpr (MODE & kVOTE) {
-                const uint32_t gm = gr.w[w] & mask;
-                const uint32_t rm = rj.w[w] & mask & ~gm;  // first response wins
-                const uint32_t lead = ge_bytes(popc_bytes(gm), quorum) & ok;
-                const uint32_t foll = ge_bytes(popc_bytes(rm), quorum) & ok & ~lead;
-                const uint32_t cand = inr & ~lead & ~foll;
-                // 2-bit codes: leader 2 (bit 1), candidate 1 (bit 0), follower 0
-                outc |= (pack4x2(cand) | (pack4x2(lead) << 1)) << (8 * w);
-            }
-            if constexpr (MODE & kCHECKQ) {
-                const uint32_t self = kB01 << a.self_slot;
-                const uint32_t selfok = ge_bytes(n, (a.self_slot + 1) * kB01) & ok;
-                bad = ~selfok & inr;
-                const uint32_t c = popc_bytes((ac.w[w] | self) & mask);
-                hq |= pack4(ge_bytes(c, quorum) & selfok) << (4 * w);
-                // setNotActive for every voting member (raft.go:385, remote.go:196-198);
-                // groups left to the CPU path keep their flags
-                keep.w[w] = ac.w[w] & ((bad >> 7) * 0xFFu);
-            }
-            fb |= pack4(bad) << (4 * w);
-        }
-        // 64-group bitmap words viewed as 16-bit slots, 32-group outcome words as 32-bit slots
-        if (slot < a.n16) {
-            if constexpr (MODE & kRI) reinterpret_cast<uint16_t *>(a.confirmed)[slot] = conf;
-            if constexpr (MODE & kCHECKQ)
-                reinterpret_cast<uint16_t *>(a.has_quorum)[slot] = hq;
-            if (a.fallback) reinterpret_cast<uint16_t *>(a.fallback)[slot] = fb;
-        }
-        if constexpr (MODE & kVOTE) {
-            if (slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
-        }
-        if constexpr (MODE & kCHECKQ) {
-            if (g + 16 <= a.G) {
-                *reinterpret_cast<uint4 *>(a.active + g) = keep.v;
-            } else {
-                for (int k = 0; k < 16; ++k)
-                    if (g + k < a.G) a.active[g + k] = keep.b[k];
-            }
-        }
+        if (g + 16 <= a.G)
+            bits_slot<MODE, PERN, true>(a, g, nu);
+        else
+            bits_slot<MODE, PERN, false>(a, g, nu);
     }
 }
 
@@ -429,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, 
         if (o.last) const_cast<uint64_t *>(o.last)[j] = last;
         if (o.tstart) const_cast<uint64_t *>(o.tstart)[j] = term_start;
         if (o.term) const_cast<uint64_t *>(o.term)[j] = term;
-        if (o.ring || o.mask) {
+        if (o.ring || o.mask || o.ring32) {
             uint64_t cur = term;
             uint32_t mask = 0;
             for (uint64_t k = 0; k < R; ++k) {
@@ -444,6 +515,9 @@ __global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, 
                     t = cur;
                 }
                 if (o.ring) const_cast<uint64_t *>(o.ring)[j * R + (i & (R - 1))] = t;
+                if (o.ring32)
+                    const_cast<uint32_t *>(o.ring32)[j * R + (i & (R - 1))] =
+                        t < 0xFFFFFFFFull ? (uint32_t)t : 0xFFFFFFFFu;
                 mask |= (uint32_t)(t == term) << (i & (R - 1));
             }
             if (o.mask) const_cast<uint16_t *>(o.mask)[j] = (uint16_t)mask;
@@ -522,6 +596,8 @@ int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool per
         HQ_DISPATCH(HQ_FORM_TERM_START)
     } else if (form == HQ_FORM_TERM_MASK) {
         HQ_DISPATCH(HQ_FORM_TERM_MASK)
+    } else if (form == HQ_FORM_TERM_RING32) {
+        HQ_DISPATCH(HQ_FORM_TERM_RING32)
     } else {
         HQ_DISPATCH(HQ_FORM_TERM_RING)
     }
@@ -539,8 +615,9 @@ int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (a->match_stride < a->G) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: match_stride < G");
     if (a->form == HQ_FORM_TERM_START) {
         if (!a->term_start) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term_start is NULL");
-    } else if (a->form == HQ_FORM_TERM_RING) {
-        if (!a->term || !a->ring) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term/ring NULL");
+    } else if (a->form == HQ_FORM_TERM_RING || a->form == HQ_FORM_TERM_RING32) {
+        if (!a->term || (a->form == HQ_FORM_TERM_RING ? !a->ring : !a->ring32))
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term/ring NULL");
         if (a->ring_len < 1 || a->ring_len > 1024 || (a->ring_len & (a->ring_len - 1)))
             return hq::fail(ctx, HQ_E_INVAL, "hq_commit: ring_len must be a power of two <= 1024");
     } else if (a->form == HQ_FORM_TERM_MASK) {
@@ -555,9 +632,9 @@ int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
 
 }  // namespace
 
-extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
-    int rc = validate_commit(ctx, a);
-    if (rc || a->G == 0) return rc;
+namespace {
+
+CommitK commit_k(const hq_commit_args *a) {
     CommitK k;
     k.G = a->G;
     k.stride = a->match_stride;
@@ -575,13 +652,29 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     k.changed = a->changed;
     k.fallback = a->fallback;
     k.mask = a->term_mask;
+    k.ring32 = a->ring32;
+    return k;
+}
+
+// every column of the batch can be read two groups per lane with 16-byte loads
+bool commit_vec2(const hq_commit_args *a) {
     const bool aux_ok = a->form == HQ_FORM_TERM_START ? hq::aligned16(a->term_start)
-                      : a->form == HQ_FORM_TERM_RING  ? hq::aligned16(a->term)
-                      : (reinterpret_cast<uintptr_t>(a->term_mask) & 3) == 0;
-    const bool vec2 = hq::aligned16(a->match) && (a->match_stride % 2 == 0) &&
-                      hq::aligned16(a->committed_in) && hq::aligned16(a->committed_out) &&
-                      hq::aligned16(a->last_index) && aux_ok &&
-                      (!a->n_voting || (reinterpret_cast<uintptr_t>(a->n_voting) & 1) == 0);
+                      : a->form == HQ_FORM_TERM_MASK
+                          ? (reinterpret_cast<uintptr_t>(a->term_mask) & 3) == 0
+                          : hq::aligned16(a->term);
+    return hq::aligned16(a->match) && (a->match_stride % 2 == 0) &&
+           hq::aligned16(a->committed_in) && hq::aligned16(a->committed_out) &&
+           hq::aligned16(a->last_index) && aux_ok &&
+           (!a->n_voting || (reinterpret_cast<uintptr_t>(a->n_voting) & 1) == 0);
+}
+
+}  // namespace
+
+extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
+    int rc = validate_commit(ctx, a);
+    if (rc || a->G == 0) return rc;
+    const CommitK k = commit_k(a);
+    const bool vec2 = commit_vec2(a);
     const bool pern = a->n_voting != nullptr;
     switch (a->n_max) {
     case 1: return launch_commit_n<1>(ctx, k, a->form, vec2, pern);
@@ -593,6 +686,53 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     case 7: return launch_commit_n<7>(ctx, k, a->form, vec2, pern);
     default: return launch_commit_n<8>(ctx, k, a->form, vec2, pern);
     }
+}
+
+extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count && !args) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_fused_dev: args is NULL");
+    for (uint32_t i = 0; i < count; ++i) {
+        int rc = validate_commit(ctx, args + i);
+        if (rc) return rc;
+    }
+    // batches that can share the launch: uniform n, 16-byte aligned columns, one form
+    bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
+    for (uint32_t i = 0; fusable && i < count; ++i)
+        fusable = args[i].G > 0 && !args[i].n_voting && commit_vec2(args + i) &&
+                  args[i].form == args[0].form;
+    if (!fusable) return hq_commit_many_dev(ctx, args, count);
+    FusedK f{};
+    f.count = count;
+    uint64_t blocks = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        f.b[i] = commit_k(args + i);
+        f.n[i] = (uint8_t)args[i].n_max;
+        f.first[i] = (uint32_t)blocks;
+        // the same workgroups per batch as its own launch would get (grid-stride beyond that)
+        blocks += grid_for((args[i].G + 1) / 2, kCommitBlock, kMaxBlocks / 2);
+    }
+    for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    switch (args[0].form) {
+    case HQ_FORM_TERM_START:
+        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_START>), dim3(blocks), dim3(kCommitBlock),
+                           0, ctx->stream, f);
+        break;
+    case HQ_FORM_TERM_MASK:
+        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_MASK>), dim3(blocks), dim3(kCommitBlock),
+                           0, ctx->stream, f);
+        break;
+    case HQ_FORM_TERM_RING32:
+        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_RING32>), dim3(blocks),
+                           dim3(kCommitBlock), 0, ctx->stream, f);
+        break;
+    default:
+        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_RING>), dim3(blocks), dim3(kCommitBlock),
+                           0, ctx->stream, f);
+        break;
+    }
+    return hq::post_launch(ctx, "k_commit_fused");
 }
 
 extern "C" int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count) {
@@ -720,6 +860,7 @@ extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,
     o.term = a->term;
     o.ring = a->ring;
     o.mask = a->term_mask;
+    o.ring32 = a->ring32;
     if (o.mask && s->ring_len > 16)
         return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit: term_mask needs ring_len <= 16");
     int rc = hq::pre_launch(ctx);

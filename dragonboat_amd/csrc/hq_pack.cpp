@@ -136,3 +136,12 @@ extern "C" int hq_pack_acks(const hq_group_view *groups, uint64_t G, const hq_me
     }
     return HQ_OK;
 }
+
+extern "C" int hq_pack_ring32(const uint64_t *ring, uint64_t count, uint32_t *ring32) {
+    if (count == 0) return HQ_OK;
+    if (!ring || !ring32) return HQ_E_INVAL;
+    // terms at or above 0xFFFFFFFF saturate: never equal to a term the kernel decides for
+    for (uint64_t i = 0; i < count; ++i)
+        ring32[i] = ring[i] < 0xFFFFFFFFull ? (uint32_t)ring[i] : 0xFFFFFFFFu;
+    return HQ_OK;
+}

@@ -263,13 +263,18 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
         return hq_commit_dev(ctx, a);  // same validation and message
     const uint64_t G = a->G, nw = hq::words64(G);
     const bool ring = a->form == HQ_FORM_TERM_RING;
+    const bool ring32 = a->form == HQ_FORM_TERM_RING32;
     const bool mask = a->form == HQ_FORM_TERM_MASK;
+    if (a->form > HQ_FORM_TERM_RING32) return hq_commit_dev(ctx, a);
     if (ring && (!a->ring || !a->term)) return hq_commit_dev(ctx, a);
+    if (ring32 && (!a->ring32 || !a->term)) return hq_commit_dev(ctx, a);
     if (mask && !a->term_mask) return hq_commit_dev(ctx, a);
-    if (!ring && !mask && !a->term_start) return hq_commit_dev(ctx, a);
+    if (!ring && !ring32 && !mask && !a->term_start) return hq_commit_dev(ctx, a);
+    if ((ring || ring32) && (a->ring_len < 1 || a->ring_len > 1024)) return hq_commit_dev(ctx, a);
     const size_t col = G * 8;
+    const size_t ring_bytes = ring ? col * a->ring_len : ring32 ? G * 4 * a->ring_len : 0;
     size_t need = Stage::pad(col * a->n_max) + 4 * Stage::pad(col) + 2 * Stage::pad(nw * 8) +
-                  Stage::pad(G) + (ring ? Stage::pad(col * a->ring_len) : 0);
+                  Stage::pad(G) + Stage::pad(ring_bytes);
     int rc = hq::ensure_workspace(ctx, need);
     if (rc) return rc;
     Stage s(ctx);
@@ -292,6 +297,12 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
         d.ring = dring;
         if (!rc) rc = h2d(ctx, daux, a->term, col);
         if (!rc) rc = h2d(ctx, dring, a->ring, col * a->ring_len);
+    } else if (ring32) {
+        d.term = daux;
+        uint32_t *dring = s.take<uint32_t>(ring_bytes);
+        d.ring32 = dring;
+        if (!rc) rc = h2d(ctx, daux, a->term, col);
+        if (!rc) rc = h2d(ctx, dring, a->ring32, ring_bytes);
     } else if (mask) {
         d.term_mask = reinterpret_cast<uint16_t *>(daux);
         if (!rc) rc = h2d(ctx, daux, a->term_mask, G * 2);

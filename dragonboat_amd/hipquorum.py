@@ -27,6 +27,7 @@ HQ_MAX_VOTERS = 8
 HQ_FORM_TERM_START = 0
 HQ_FORM_TERM_RING = 1
 HQ_FORM_TERM_MASK = 2
+HQ_FORM_TERM_RING32 = 3
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -58,6 +59,7 @@ class CommitArgs(ctypes.Structure):
         ("changed", _vp),
         ("fallback", _vp),
         ("term_mask", _vp),
+        ("ring32", _vp),
     ]
 
 
@@ -160,6 +162,7 @@ SIGNATURES = {
     "hq_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs)]),
     "hq_commit": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs)]),
     "hq_commit_many_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
+    "hq_commit_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
     "hq_readindex_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
     "hq_readindex": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
     "hq_vote_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
@@ -182,6 +185,7 @@ SIGNATURES = {
     "hq_append_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32,
                                      ctypes.c_uint64, _vp]),
     "hq_pack_commit": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.POINTER(CommitArgs)]),
+    "hq_pack_ring32": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp]),
     "hq_pack_votes": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hq_pack_acks": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_uint32, _vp]),
@@ -350,6 +354,11 @@ class Context:
         """batch: a ctypes array of CommitArgs (see ``commit_batch_array``)."""
         self._check(lib.hq_commit_many_dev(self.h, batch, len(batch)))
 
+    def commit_fused_dev(self, batch) -> None:
+        """The batches of ``batch`` (ctypes array of CommitArgs) in one launch when they can
+        share it (hq_commit_fused_dev)."""
+        self._check(lib.hq_commit_fused_dev(self.h, batch, len(batch)))
+
     def commit_host(self, args: CommitArgs) -> None:
         self._check(lib.hq_commit(self.h, ctypes.byref(args)))
 
@@ -449,6 +458,14 @@ def pack_commit(groups: np.ndarray, members: np.ndarray, n_max: int, ring_len: i
     return cols, fb
 
 
+def pack_ring32(ring: np.ndarray) -> np.ndarray:
+    """hq_pack_ring32: the u32 ring of HQ_FORM_TERM_RING32 from a u64 term ring."""
+    ring = np.ascontiguousarray(ring, np.uint64)
+    out = np.zeros(len(ring), np.uint32)
+    _chk(lib.hq_pack_ring32(_p(ring), len(ring), _p(out)), "hq_pack_ring32")
+    return out
+
+
 def pack_votes(groups: np.ndarray, members: np.ndarray, msgs: np.ndarray):
     G = len(groups)
     gr, rj, nv = (np.zeros(G, np.uint8) for _ in range(3))
@@ -502,6 +519,7 @@ class CommitBuffers:
     term_start: Optional[DeviceArray] = None
     term: Optional[DeviceArray] = None
     term_mask: Optional[DeviceArray] = None
+    ring32: Optional[DeviceArray] = None
 
     def args(self) -> CommitArgs:
         a = CommitArgs()
@@ -521,20 +539,22 @@ class CommitBuffers:
         a.changed = self.changed.ptr
         a.fallback = self.fallback.ptr
         a.term_mask = self.term_mask.ptr if self.term_mask else None
+        a.ring32 = self.ring32.ptr if self.ring32 else None
         return a
 
     def arrays(self):
         return [x for x in (self.match, self.committed_in, self.committed_out, self.last_index,
                             self.term_start, self.term, self.ring, self.term_mask, self.n_voting,
-                            self.changed, self.fallback) if x is not None]
+                            self.changed, self.fallback, self.ring32) if x is not None]
 
 
 def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
                  per_group_n: bool = False, with_both_aux: bool = False) -> CommitBuffers:
     """Allocate the SoA columns of one commit batch (match is slot-major [n_max][G]).
-    with_both_aux allocates the columns of all three term forms (to compare them)."""
+    with_both_aux allocates the columns of all four term forms (to compare them)."""
     need_ts = form == HQ_FORM_TERM_START or with_both_aux
     need_ring = form == HQ_FORM_TERM_RING or with_both_aux
+    need_ring32 = form == HQ_FORM_TERM_RING32 or with_both_aux
     need_mask = form == HQ_FORM_TERM_MASK or (with_both_aux and ring_len <= 16)
     b = CommitBuffers(
         G=G, n_max=n_max, form=form, ring_len=ring_len,
@@ -547,8 +567,9 @@ def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16
         changed=ctx.empty(words64(G), np.uint64),
         fallback=ctx.empty(words64(G), np.uint64),
         term_start=ctx.empty(G, np.uint64) if need_ts else None,
-        term=ctx.empty(G, np.uint64) if need_ring else None,
+        term=ctx.empty(G, np.uint64) if need_ring or need_ring32 else None,
         term_mask=ctx.empty(G, np.uint16) if need_mask else None,
+        ring32=ctx.empty(G * ring_len, np.uint32) if need_ring32 else None,
     )
     return b
 

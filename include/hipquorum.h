@@ -60,6 +60,7 @@ extern "C" {
 #define HQ_FORM_TERM_START 0  /* term(q)==term  <=>  term_start <= q <= last_index */
 #define HQ_FORM_TERM_RING  1  /* term(q) gathered from a per-group ring of the last R terms */
 #define HQ_FORM_TERM_MASK  2  /* term(q)==term read from a per-group bitmask over the last R */
+#define HQ_FORM_TERM_RING32 3 /* the ring gather from a u32 ring (terms saturated at 2^32-1) */
 
 /* vote outcomes, numerically equal to the reference State enum (internal/raft/raft.go:62-71) */
 #define HQ_OUTCOME_FOLLOWER  0u   /* rejections reached quorum: becomeFollower (raft.go:1981-1984) */
@@ -128,11 +129,15 @@ int hq_timing_reset(hq_ctx *ctx);
  *       i in (last_index - ring_len, last_index]; ring_len <= 16. The same per-index equality the
  *       ring gather tests, without the term values (no monotonicity assumption); exact when
  *       last_index[g] - committed_in[g] <= ring_len. `term`/`ring`/`term_start` unused.
+ *   HQ_FORM_TERM_RING32 the ring form over ring32[g * ring_len + (i % ring_len)] =
+ *       min(term(i), 0xFFFFFFFF) (hq_pack_ring32). For a leader's term below 0xFFFFFFFF the u32
+ *       equality is the u64 one; a 64-B ring (R = 16) lets two groups share each gathered 128-B
+ *       line. Groups whose term is >= 0xFFFFFFFF go to the fallback path.
  *
  * Groups that violate the contract are NOT decided: committed_out = committed_in, changed = 0 and
  * the fallback bit is set so the caller runs the CPU path (raft.go:888) for them:
  *   n == 0 or n > n_max;  RING form: term == 0, committed > last_index, or
- *   last_index - committed > ring_len;  MASK form: committed > last_index or
+ *   last_index - committed > ring_len;  RING32 form: as RING, and term >= 0xFFFFFFFF;  MASK form: committed > last_index or
  *   last_index - committed > ring_len.
  *
  * Layout: match is slot-major, match[s * match_stride + g]; match_stride >= G.
@@ -156,6 +161,7 @@ typedef struct hq_commit_args {
     uint64_t *changed;              /* [ceil(G/64)] or NULL */
     uint64_t *fallback;             /* [ceil(G/64)] or NULL */
     const uint16_t *term_mask;      /* [G] HQ_FORM_TERM_MASK */
+    const uint32_t *ring32;         /* [G][ring_len] HQ_FORM_TERM_RING32 */
 } hq_commit_args;
 
 int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *args);
@@ -163,6 +169,12 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *args);
 /* `count` independent batches back to back on the context's stream (e.g. a step worker's
  * per-voter-count buckets of one step, or successive steps). Stops at the first invalid batch. */
 int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
+/* The same `count` batches decided by ONE kernel launch when they can share it (2..8 batches,
+ * uniform n (n_voting NULL), one form, 16-byte aligned columns, G > 0): a step worker's
+ * voter-count buckets (groups bucketed by n for coalesced SoA, execengine.go:923 caller). Batch i
+ * owns its own workgroups; results are identical to hq_commit_many_dev, which is what runs
+ * when the batches cannot share a launch. */
+int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
 
 /* ---------------------------------------------------------------- ReadIndex / vote ----------- */
 
@@ -323,6 +335,10 @@ typedef struct hq_msg {
  * args->G must equal G; args->fallback (may be NULL) receives the packing fallbacks. */
 int hq_pack_commit(const hq_group_view *groups, uint64_t G, const hq_member *members,
                    hq_commit_args *args);
+
+/* The u32 ring of HQ_FORM_TERM_RING32 from the u64 term ring (logentry.go:143-160 values):
+ * ring32[i] = min(ring[i], 0xFFFFFFFF). `count` = G * ring_len entries. */
+int hq_pack_ring32(const uint64_t *ring, uint64_t count, uint32_t *ring32);
 
 /* Vote bitmaps: slot 0 granted (campaign's self vote, raft.go:1093); then every message from a
  * voting member sets its slot's granted or rejected bit if neither is set yet (first response

@@ -262,9 +262,13 @@ static void commit_range(const qref_commit_args *a, uint64_t g0, uint64_t g1, in
             log.first_minus_1 = last >= R - 1 ? last - (R - 1) : 0;
             log.term_at = mask_term_at;
             log.ud = &mud;
-        } else if (a->form == 1) {
+        } else if (a->form == 1 || a->form == 3) {
+            /* form 3 (the u32-ring packing of the same ring) decides from the u64 terms here:
+             * the product's narrowing is checked against the full-width restatement; its
+             * contract adds term >= 0xFFFFFFFF to the fallback set */
             term = a->term[g];
-            if (term == 0 || cin > last || last - cin > R) {
+            if (term == 0 || cin > last || last - cin > R ||
+                (a->form == 3 && term >= 0xFFFFFFFFull)) {
                 if (a->fallback) bit_set(a->fallback, g);
                 continue;
             }
@@ -419,7 +423,7 @@ static uint64_t words64(uint64_t G, uint64_t per_word) { return (G + per_word - 
 int qref_commit_batch(const qref_commit_args *a, int nthreads) {
     if (!a || !a->match || !a->committed_in || !a->committed_out || !a->last_index) return -1;
     if (a->n_max < 1 || a->n_max > QREF_MAX_NODES || a->match_stride < a->G) return -1;
-    if (a->form == 1) {
+    if (a->form == 1 || a->form == 3) {
         if (!a->term || !a->ring || a->ring_len < 1 || (a->ring_len & (a->ring_len - 1))) return -1;
     } else if (a->form == 0) {
         if (!a->term_start) return -1;

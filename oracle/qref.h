@@ -121,7 +121,8 @@ int qref_leader_has_quorum(const uint64_t *ids, int *active, int n_voting, uint6
 typedef struct qref_commit_args {
     uint64_t G;
     uint32_t n_max;
-    uint32_t form;            /* 0 = term-start, 1 = ring, 2 = current-term mask */
+    uint32_t form;            /* 0 = term-start, 1 = ring, 2 = current-term mask, 3 = ring
+                                 (u32-packed in the product; decided here from the u64 ring) */
     uint32_t ring_len;
     uint32_t reserved;
     uint64_t match_stride;

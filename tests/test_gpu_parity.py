@@ -46,6 +46,7 @@ def upload_commit(ctx, hq, inp, form, per_group_n, stride_pad=0, offset_elems=0)
     a.term_start = up(inp.term_start)
     a.term = up(inp.term)
     a.ring = up(inp.ring)
+    a.ring32 = up(hq.pack_ring32(inp.ring))
     if inp.term_mask is not None:
         a.term_mask = up(inp.term_mask)
     if per_group_n:
@@ -112,6 +113,7 @@ def test_synth_commit_matches_cpu_generator(gpu_ctx, hq, kw):
     np.testing.assert_array_equal(gpu_ctx.download(b.term), host.term)
     np.testing.assert_array_equal(gpu_ctx.download(b.ring), host.ring)
     np.testing.assert_array_equal(gpu_ctx.download(b.term_mask), host.term_mask)
+    np.testing.assert_array_equal(gpu_ctx.download(b.ring32), hq.pack_ring32(host.ring))
     hq.free_commit(gpu_ctx, b)
 
 
@@ -129,7 +131,10 @@ def test_synth_bitmaps_matches_cpu_generator(gpu_ctx, hq, kw):
 
 
 # ----------------------------------------------------------------------- commit parity -------
-@pytest.mark.parametrize("form", [0, 1, 2])
+FORMS = [0, 1, 2, 3]   # term-start, u64 ring gather, current-term mask, u32 ring gather
+
+
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("n_max", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_commit_uniform_n(gpu_ctx, hq, form, n_max):
     inp = qref.CommitInputs(qref.spec(SEED + 1, 65_537, n_max, parity_extras=True))
@@ -138,14 +143,14 @@ def test_commit_uniform_n(gpu_ctx, hq, form, n_max):
         assert 0 < popcount(chg) < inp.G  # both outcomes exercised
 
 
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("n_max", [7, 8])
 def test_commit_per_group_n(gpu_ctx, hq, form, n_max):
     inp = qref.CommitInputs(qref.spec(SEED + 4, 99_999, n_max, mixed_n=True, parity_extras=True))
     check_commit(gpu_ctx, hq, inp, form, per_group_n=True)
 
 
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", FORMS)
 def test_commit_vec1_paths(gpu_ctx, hq, form):
     inp = qref.CommitInputs(qref.spec(SEED + 5, 10_001, 5, parity_extras=True))
     check_commit(gpu_ctx, hq, inp, form, per_group_n=False, stride_pad=1)     # odd stride
@@ -156,7 +161,7 @@ def test_commit_vec1_paths(gpu_ctx, hq, form):
 
 @pytest.mark.parametrize("G", [1, 2, 3, 63, 64, 65, 127, 128, 129, 130, 1000, 4097])
 def test_commit_ragged_sizes(gpu_ctx, hq, G):
-    for form in (0, 1, 2):
+    for form in FORMS:
         inp = qref.CommitInputs(qref.spec(SEED + G, G, 3, parity_extras=True))
         check_commit(gpu_ctx, hq, inp, form, per_group_n=False)
         inp8 = qref.CommitInputs(qref.spec(SEED + G, G, 8, mixed_n=True))
@@ -207,7 +212,7 @@ def test_commit_reference_kats_on_gpu(gpu_ctx, hq):
         cases += KATS[table]
     inp = _kat_inputs(cases)
     want = np.array([c["want_committed"] for c in cases], np.uint64)
-    for form in (1, 2):   # ring gather and current-term mask: every case representable
+    for form in (1, 2, 3):   # ring gathers and current-term mask: every case representable
         out, chg, fb = run_commit(gpu_ctx, hq, inp, form, per_group_n=True)
         assert popcount(fb) == 0
         np.testing.assert_array_equal(out, want)
@@ -250,11 +255,107 @@ def test_commit_contract_fallbacks(gpu_ctx, hq):
     np.testing.assert_array_equal(out, want_out)
     np.testing.assert_array_equal(chg, want_chg)
     np.testing.assert_array_equal(fb, want_fb)
+    # u32 ring: the ring form's fallbacks, plus a term that does not fit below 0xFFFFFFFF
+    inp.term[7] = 1 << 32
+    out, chg, fb = run_commit(gpu_ctx, hq, inp, 3, per_group_n=True)
+    assert int(fb[0]) == 0b10111110
+    want_out, want_chg, want_fb, rc = inp.run(3, True)
+    np.testing.assert_array_equal(out, want_out)
+    np.testing.assert_array_equal(chg, want_chg)
+    np.testing.assert_array_equal(fb, want_fb)
+
+
+def test_commit_ring32_wide_terms(gpu_ctx, hq):
+    """Terms around 2^32: the u32 ring decides exactly what the u64 ring decides (entries at or
+    above 0xFFFFFFFF saturate and never equal a decidable term; larger terms fall back)."""
+    G, R = 4096, 16
+    inp = qref.CommitInputs(qref.spec(SEED + 11, G, 5))
+    rng = np.random.default_rng(5)
+    base = np.array([0xFFFFFFFE, 0xFFFFFFFF, 0x100000000, 0x1FFFFFFFE, 0xFFFFFFF0, 3],
+                    np.uint64)
+    inp.term[:] = base[rng.integers(0, len(base), G)]
+    # ring entries: the term itself, its low 32 bits with a high bit set (equal after
+    # truncation, not after saturation), or an older term
+    pick = rng.integers(0, 3, G * R)
+    t = np.repeat(inp.term, R)
+    inp.ring[:] = np.where(pick == 0, t, np.where(pick == 1, (t & np.uint64(0xFFFFFFFF)) |
+                                                   np.uint64(1 << 33), t // np.uint64(2)))
+    out, chg, fb = run_commit(gpu_ctx, hq, inp, 3, per_group_n=False)
+    want_out, want_chg, want_fb, rc = inp.run(3, False)
+    assert rc == 0
+    np.testing.assert_array_equal(out, want_out)
+    np.testing.assert_array_equal(chg, want_chg)
+    np.testing.assert_array_equal(fb, want_fb)
+    assert 0 < popcount(chg) and 0 < popcount(fb) < G
+    # groups the u32 form decides are decided as the u64 ring form decides them
+    out1, chg1, _ = run_commit(gpu_ctx, hq, inp, 1, per_group_n=False)
+    dec = inp.term < np.uint64(0xFFFFFFFF)
+    np.testing.assert_array_equal(out[dec], out1[dec])
+
+
+def _fused_buckets(ctx, hq, form, sizes):
+    """Device batches of several voter counts (a step worker's buckets) with their oracle
+    answers."""
+    bs, want = [], []
+    for k, (n, G) in enumerate(sizes):
+        inp = qref.CommitInputs(qref.spec(SEED + 40 + k, G, n, parity_extras=True))
+        # even row stride: 16-byte loads of every row (what a fused launch needs)
+        d = upload_commit(ctx, hq, inp, form, per_group_n=False, stride_pad=G % 2)
+        bs.append(d)
+        want.append(inp.run(form, False, nthreads=8)[:3])
+    return bs, want
+
+
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("sizes", [[(3, 100_001), (5, 99_999), (7, 100_003)],
+                                   [(3, 1), (5, 64), (7, 65), (1, 129), (8, 3000)],
+                                   [(5, 1 << 20), (3, 2049)]])
+def test_commit_fused_buckets(gpu_ctx, hq, form, sizes):
+    """One launch over several voter-count buckets equals the oracle on each bucket."""
+    bs, want = _fused_buckets(gpu_ctx, hq, form, sizes)
+    gpu_ctx.timing_reset()
+    gpu_ctx.timing(True)
+    gpu_ctx.commit_fused_dev(hq.commit_batch_array([d["args"] for d in bs]))
+    gpu_ctx.sync()
+    gpu_ctx.timing(False)
+    assert gpu_ctx.timing_read()[1] == 1          # one launch
+    for d, (wo, wc, wf) in zip(bs, want):
+        np.testing.assert_array_equal(gpu_ctx.download(d["out"])[:len(wo)], wo)
+        np.testing.assert_array_equal(gpu_ctx.download(d["chg"]), wc)
+        np.testing.assert_array_equal(gpu_ctx.download(d["fb"]), wf)
+        for b in d["bufs"]:
+            gpu_ctx.free(b)
+
+
+def test_commit_fused_unfusable_batches(gpu_ctx, hq):
+    """Batches that cannot share a launch (per-group n, more than 8, one batch) are launched
+    separately with the same results."""
+    sizes = [(3, 5000), (5, 4000), (7, 3000)] * 3            # 9 batches
+    bs, want = _fused_buckets(gpu_ctx, hq, 2, sizes)
+    gpu_ctx.commit_fused_dev(hq.commit_batch_array([d["args"] for d in bs]))
+    gpu_ctx.sync()
+    for d, (wo, wc, wf) in zip(bs, want):
+        np.testing.assert_array_equal(gpu_ctx.download(d["out"])[:len(wo)], wo)
+        np.testing.assert_array_equal(gpu_ctx.download(d["chg"]), wc)
+        for b in d["bufs"]:
+            gpu_ctx.free(b)
+    inp = qref.CommitInputs(qref.spec(SEED + 50, 7777, 7, mixed_n=True, parity_extras=True))
+    d0 = upload_commit(gpu_ctx, hq, inp, 1, per_group_n=True)
+    d1 = upload_commit(gpu_ctx, hq, inp, 1, per_group_n=False)
+    gpu_ctx.commit_fused_dev(hq.commit_batch_array([d0["args"], d1["args"]]))
+    gpu_ctx.sync()
+    for d, pern in ((d0, True), (d1, False)):
+        wo, wc, wf, _ = inp.run(1, pern)
+        np.testing.assert_array_equal(gpu_ctx.download(d["out"])[:len(wo)], wo)
+        np.testing.assert_array_equal(gpu_ctx.download(d["fb"]), wf)
+        for b in d["bufs"]:
+            gpu_ctx.free(b)
 
 
 def test_commit_host_entry_point(gpu_ctx, hq):
     inp = qref.CommitInputs(qref.spec(SEED + 9, 30_001, 5, parity_extras=True))
-    for form in (0, 1, 2):
+    ring32 = hq.pack_ring32(inp.ring)
+    for form in FORMS:
         out = np.zeros(inp.G, np.uint64)
         chg = np.zeros(hq.words64(inp.G), np.uint64)
         fb = np.zeros(hq.words64(inp.G), np.uint64)
@@ -265,6 +366,7 @@ def test_commit_host_entry_point(gpu_ctx, hq):
         a.last_index, a.term_start = inp.last_index.ctypes.data, inp.term_start.ctypes.data
         a.term, a.ring = inp.term.ctypes.data, inp.ring.ctypes.data
         a.term_mask = inp.term_mask.ctypes.data
+        a.ring32 = ring32.ctypes.data
         a.changed, a.fallback = chg.ctypes.data, fb.ctypes.data
         gpu_ctx.commit_host(a)
         want_out, want_chg, want_fb, _ = inp.run(form, False)
@@ -289,7 +391,7 @@ def test_commit_inplace_idempotent(gpu_ctx, hq):
     hq.free_commit(gpu_ctx, b)
 
 
-@pytest.mark.parametrize("n_max,form", [(3, 0), (5, 1), (5, 2)])
+@pytest.mark.parametrize("n_max,form", [(3, 0), (5, 1), (5, 2), (5, 3)])
 def test_commit_full_size_configs(gpu_ctx, hq, n_max, form):
     """BASELINE configs 2 and 3 at full size (1M groups): device-generated inputs, oracle on the
     CPU generator's copy; the three term forms agree on the same data."""
@@ -305,7 +407,7 @@ def test_commit_full_size_configs(gpu_ctx, hq, n_max, form):
     np.testing.assert_array_equal(chg, want_chg)
     assert popcount(gpu_ctx.download(b.fallback)) == 0
     extra_out = gpu_ctx.empty(G, np.uint64)
-    for other_form in {0, 1, 2} - {form}:
+    for other_form in set(FORMS) - {form}:
         other = b.args()
         other.form = other_form
         other.committed_out = extra_out.ptr
