@@ -24,6 +24,8 @@ struct hq_ctx {
     uint64_t timed_launches = 0;
     // launch geometry of the bitmap kernels (256; HQ_BITS_BLOCK=512|1024 at hq_open)
     int bits_block = 256;
+    // hq_wait_for: recorded on this context's stream when another context orders after it
+    hipEvent_t ev_order = nullptr;
     // device workspace for the host-pointer entry points
     void *ws = nullptr;
     size_t ws_bytes = 0;

@@ -97,6 +97,7 @@ void hq_close(hq_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
     if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
+    if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -111,6 +112,23 @@ int hq_sync(hq_ctx *ctx) {
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     if (rc) return rc;
     return hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+int hq_wait_for(hq_ctx *ctx, hq_ctx *other) {
+    if (!ctx || !other) return HQ_E_INVAL;
+    if (other == ctx) return HQ_OK;  // a stream is already ordered after itself
+    if (other->device != ctx->device)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_wait_for: contexts on different devices");
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (!rc && !other->ev_order)
+        rc = hq::check_hip(ctx, hipEventCreateWithFlags(&other->ev_order, hipEventDisableTiming),
+                           "hipEventCreateWithFlags");
+    // the wait captures the event as just recorded, so re-recording it later is safe
+    if (!rc) rc = hq::check_hip(ctx, hipEventRecord(other->ev_order, other->stream), "hipEventRecord");
+    if (!rc)
+        rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, other->ev_order, 0),
+                           "hipStreamWaitEvent");
+    return rc;
 }
 
 int hq_malloc_dev(hq_ctx *ctx, size_t bytes, void **out) {

@@ -150,6 +150,7 @@ SIGNATURES = {
     "hq_close": (None, [_vp]),
     "hq_last_error": (ctypes.c_char_p, [_vp]),
     "hq_sync": (ctypes.c_int, [_vp]),
+    "hq_wait_for": (ctypes.c_int, [_vp, _vp]),
     "hq_malloc_dev": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "hq_free_dev": (ctypes.c_int, [_vp, _vp]),
     "hq_alloc_pinned": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
@@ -332,6 +333,10 @@ class Context:
 
     def sync(self) -> None:
         self._check(lib.hq_sync(self.h))
+
+    def wait_for(self, other: "Context") -> None:
+        """Order this context's stream after the work queued on ``other``'s (hq_wait_for)."""
+        self._check(lib.hq_wait_for(self.h, other.h))
 
     # -- timing -----------------------------------------------------------------------------
     def timing(self, enable: bool) -> None:

@@ -85,6 +85,12 @@ const char *hq_last_error(const hq_ctx *ctx);
 /* Wait for all work queued on the context's stream. */
 int hq_sync(hq_ctx *ctx);
 
+/* Order ctx's stream after everything enqueued on other's stream so far (an event recorded on
+ * other's stream, waited on by ctx's; no host synchronisation). Both contexts must be on one
+ * device. Lets a step worker pipeline its steps over two contexts: step i+1's host-to-device
+ * copies overlap step i's kernels and readback, its kernels still run after step i's. */
+int hq_wait_for(hq_ctx *ctx, hq_ctx *other);
+
 int hq_malloc_dev(hq_ctx *ctx, size_t bytes, void **out);
 int hq_free_dev(hq_ctx *ctx, void *p);
 int hq_alloc_pinned(hq_ctx *ctx, size_t bytes, void **out);
