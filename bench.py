@@ -45,6 +45,12 @@ WORKLOADS = {
     "c3m": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False,
                 desc="1M groups x 5 voters (4 full + 1 witness), commit + 16-bit current-term "
                      "mask (exact replacement of the ring gather)"),
+    "c2l": dict(cfg=1, kind="lag", G=1 << 20, n=3, form=0, mixed=False,
+                desc="1M groups x 3 voters, commit over int32 lags below lastIndex (term-start "
+                     "form; 24 B per decision against 56 B)"),
+    "c3l": dict(cfg=2, kind="lag", G=1 << 20, n=5, form=2, mixed=False,
+                desc="1M groups x 5 voters (4 full + 1 witness), commit over int32 lags with the "
+                     "lag-indexed current-term mask (30 B per decision)"),
     "c4": dict(cfg=3, kind="bits", G=16 << 20, n=7,
                desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
@@ -62,6 +68,9 @@ WORKLOADS = {
 
 def algo_bytes_per_group(w):
     """bytes the decision must move per group."""
+    if w["kind"] == "lag":
+        # lag rows + cin_lag + cout_lag + (ts_lag | lag_mask)
+        return 4 * w["n"] + 8 + {0: 4, 2: 2}[w["form"]]
     if w["kind"] == "commit":
         n, extra_n = w["n"], (1 if w["mixed"] else 0)
         # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask
@@ -71,7 +80,7 @@ def algo_bytes_per_group(w):
 
 
 def decisions_per_group(w):
-    return 1 if w["kind"] == "commit" else 2
+    return 2 if w["kind"] == "bits" else 1
 
 
 def log(msg):
@@ -155,6 +164,13 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
                 ctx.synth_commit_dev(spec, b.args())
                 buckets.append(b)
             sets.append(buckets)
+        elif w["kind"] == "lag":
+            rng = shard.rank_shard(d.rank, d.world, G)
+            spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
+                                 cid_stride=rng.cid_stride)
+            b = hq.alloc_commit_lag(ctx, G, w["n"], w["form"], 16)
+            ctx.synth_commit_lag_dev(spec, b.args())
+            sets.append(b)
         else:
             rng = shard.rank_shard(d.rank, d.world, G)
             spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
@@ -202,6 +218,13 @@ def run_gpu(w, steps, warmup, d: Dist):
         def run(idx):
             for i in idx:
                 ctx.commit_fused_dev(per_step[i % len(per_step)])
+    elif w["kind"] == "lag":
+        lag_args = [b.args() for b in sets]
+        seq, wseq = list(range(steps)), list(range(max(1, warmup)))
+
+        def run(idx):
+            for i in idx:
+                ctx.commit_lag_dev(lag_args[i % len(lag_args)])
     elif w["kind"] == "commit":
         def flat(k):
             return hq.commit_batch_array([b.args() for i in range(k) for b in sets[i % len(sets)]])
@@ -518,7 +541,7 @@ def cpu_baseline(w, budget_s=8.0):
     G = min(w["G"], 1 << 20)
     s = qref.spec(SEED_BASE + w["cfg"], G, w["n"])
     out = {}
-    if w["kind"] == "commit":
+    if w["kind"] in ("commit", "lag"):   # the oracle decides the u64 layout
         inp = qref.CommitInputs(s)
 
         def one(nt):
@@ -574,7 +597,7 @@ def main():
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c3,c3r32,c3m,c4,c5,c5s,c5r,c5r32,w2,e2e,step",
+    ap.add_argument("--extra", default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5r,c5r32,w2,e2e,step",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -623,8 +646,9 @@ def main():
             "config": {
                 "workload": f"{args.workload}: {w['desc']}",
                 "groups_per_gpu": w["G"], "voters": w["n"],
-                "form": {0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
-                if w["kind"] == "commit" else "bitmaps",
+                "form": ({0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
+                         + ("_lag" if w["kind"] == "lag" else ""))
+                if w["kind"] in ("commit", "lag") else "bitmaps",
                 "global_groups_per_step": w["G"] * d.world,
                 "parallelism": f"shard{d.world} (clusterID % {d.world})",
             },

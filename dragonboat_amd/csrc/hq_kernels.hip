@@ -287,6 +287,187 @@ __global__ __launch_bounds__(kCommitBlock) void k_commit_fused(const FusedK f) {
     }
 }
 
+// ---- commit over lags (hq_commit_lag_dev): int32 distances below lastIndex -------------------
+// Four groups per lane: every column is read with 16-byte loads of four int32 (consecutive
+// lanes -> consecutive groups). The quorum-th largest match is the quorum-th SMALLEST lag.
+struct LagK {
+    uint64_t G, stride, nwords;
+    uint32_t n_max, R;
+    const int32_t *lag;
+    const uint8_t *nv;
+    const int32_t *cin;
+    int32_t *cout;
+    const int32_t *ts;
+    const uint16_t *mask;
+    uint64_t *changed, *fallback;
+};
+
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void ce_i32(int32_t &a, int32_t &b) {
+    const int32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// the (n/2+1)-th smallest of v[0..n); slots >= n are padded with INT32_MAX (the maximum), so
+// with a runtime n the (n/2+1)-th smallest of the padded N values is the same element
+template <int N, bool PERN>
+__device__ __forceinline__ int32_t lag_select(int32_t (&v)[N], int n) {
+    if constexpr (!PERN && N == 1) {
+        return v[0];
+    } else if constexpr (!PERN && N == 2) {
+        return v[0] > v[1] ? v[0] : v[1];   // quorum 2 of 2: the larger lag
+    } else if constexpr (!PERN && N == 3) {  // median of 3
+        ce_i32(v[0], v[1]);
+        ce_i32(v[1], v[2]);
+        return v[0] > v[1] ? v[0] : v[1];
+    } else {
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+#pragma unroll
+            for (int i = r & 1; i + 1 < N; i += 2) ce_i32(v[i], v[i + 1]);
+        }
+        if constexpr (!PERN) return v[N / 2];   // index quorum - 1 = N/2
+        const int idx = n / 2;
+        int32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) r = (k == idx) ? v[k] : r;
+        return r;
+    }
+}
+
+template <int N, int FORM, bool PERN>
+__device__ __forceinline__ void decide_lag(const LagK &a, int32_t (&l)[N], int n, int32_t c,
+                                           int32_t aux, int32_t &co, bool &chg, bool &fb) {
+    co = c;
+    chg = false;
+    if constexpr (PERN) {
+        fb = n < 1 || n > N;
+#pragma unroll
+        for (int s = 0; s < N; ++s) l[s] = (s < n) ? l[s] : INT32_MAX;
+    } else {
+        fb = false;
+    }
+    if constexpr (FORM == HQ_FORM_TERM_START) {
+        fb |= c == INT32_MAX || c == INT32_MIN;   // committed not representable as a lag
+    } else {
+        fb |= c < 0 || c > (int32_t)a.R;
+    }
+    const int32_t d = lag_select<N, PERN>(l, n);
+    if constexpr (FORM == HQ_FORM_TERM_START) {
+        // q > committed, q <= last, q >= term_start (aux = ts_lag)
+        chg = !fb & (d < c) & (d >= 0) & (d <= aux);
+    } else {
+        // bit d of the lag-indexed mask: term(last - d) == term (d < c <= R <= 16)
+        chg = !fb & (d < c) & (d >= 0) && ((aux >> (d & 31)) & 1);
+    }
+    co = chg ? d : c;
+}
+
+// bit i of x (16 bits) -> bit 4i
+__device__ __forceinline__ uint64_t spread16x4(uint32_t x) {
+    uint64_t v = x & 0xFFFFu;
+    v = (v | (v << 24)) & 0x000000FF000000FFull;
+    v = (v | (v << 12)) & 0x000F000F000F000Full;
+    v = (v | (v << 6)) & 0x0303030303030303ull;
+    v = (v | (v << 3)) & 0x1111111111111111ull;
+    return v;
+}
+
+// VEC = 4: lane owns groups g0..g0+3 (16-byte loads); VEC = 1: one group, 4-byte loads.
+template <int N, int FORM, int VEC, bool PERN>
+__global__ __launch_bounds__(kCommitBlock) void k_commit_lag(const LagK a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kCommitBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = (uint64_t)gridDim.x * kCommitBlock * VEC;
+    for (uint64_t wbase = wave * 64 * VEC; wbase < a.G; wbase += step) {
+        const uint64_t g0 = wbase + (uint64_t)lane * VEC;
+        bool chg[VEC], fb[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) chg[j] = fb[j] = false;
+        if (VEC == 4 && g0 + 3 < a.G) {
+            int32_t l[4][N];
+#pragma unroll
+            for (int s = 0; s < N; ++s) {
+                const i32x4 v = __builtin_nontemporal_load(
+                    reinterpret_cast<const i32x4 *>(a.lag + s * a.stride + g0));
+                l[0][s] = v.x;
+                l[1][s] = v.y;
+                l[2][s] = v.z;
+                l[3][s] = v.w;
+            }
+            const i32x4 ci = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(a.cin + g0));
+            i32x4 ax;
+            if constexpr (FORM == HQ_FORM_TERM_START) {
+                ax = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(a.ts + g0));
+            } else {
+                // the lane's 4 u16 masks: one aligned 8-byte load
+                const uint64_t m4 = __builtin_nontemporal_load(
+                    reinterpret_cast<const uint64_t *>(a.mask + g0));
+                ax = (i32x4){(int32_t)(m4 & 0xFFFF), (int32_t)((m4 >> 16) & 0xFFFF),
+                             (int32_t)((m4 >> 32) & 0xFFFF), (int32_t)(m4 >> 48)};
+            }
+            int n4[4] = {N, N, N, N};
+            if constexpr (PERN) {
+                const uint32_t nn = *reinterpret_cast<const uint32_t *>(a.nv + g0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) n4[j] = (nn >> (8 * j)) & 0xFF;
+            }
+            int32_t co[4];
+            const int32_t cv[4] = {ci.x, ci.y, ci.z, ci.w}, av[4] = {ax.x, ax.y, ax.z, ax.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                decide_lag<N, FORM, PERN>(a, l[j], n4[j], cv[j], av[j], co[j], chg[j], fb[j]);
+            *reinterpret_cast<i32x4 *>(a.cout + g0) = (i32x4){co[0], co[1], co[2], co[3]};
+        } else {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) {
+                const uint64_t g = g0 + j;
+                if (g < a.G) {
+                    int32_t l[N];
+#pragma unroll
+                    for (int s = 0; s < N; ++s) l[s] = a.lag[s * a.stride + g];
+                    const int n = PERN ? (int)a.nv[g] : N;
+                    const int32_t aux = FORM == HQ_FORM_TERM_START ? a.ts[g] : (int32_t)a.mask[g];
+                    int32_t co;
+                    decide_lag<N, FORM, PERN>(a, l, n, a.cin[g], aux, co, chg[j], fb[j]);
+                    a.cout[g] = co;
+                }
+            }
+        }
+        if constexpr (VEC == 4) {
+            // lane l owns groups 4l..4l+3 of the wave's 256: word k = lanes 16k..16k+15
+            const uint64_t b0 = __ballot(chg[0]), b1 = __ballot(chg[1]);
+            const uint64_t b2 = __ballot(chg[2]), b3 = __ballot(chg[3]);
+            const uint64_t f0 = __ballot(fb[0]), f1 = __ballot(fb[1]);
+            const uint64_t f2 = __ballot(fb[2]), f3 = __ballot(fb[3]);
+            if (lane < 4) {
+                const int sh = 16 * lane;
+                const uint64_t w = (wbase >> 6) + lane;
+                if (w < a.nwords) {
+                    if (a.changed)
+                        a.changed[w] = spread16x4((uint32_t)(b0 >> sh)) |
+                                       (spread16x4((uint32_t)(b1 >> sh)) << 1) |
+                                       (spread16x4((uint32_t)(b2 >> sh)) << 2) |
+                                       (spread16x4((uint32_t)(b3 >> sh)) << 3);
+                    if (a.fallback)
+                        a.fallback[w] = spread16x4((uint32_t)(f0 >> sh)) |
+                                        (spread16x4((uint32_t)(f1 >> sh)) << 1) |
+                                        (spread16x4((uint32_t)(f2 >> sh)) << 2) |
+                                        (spread16x4((uint32_t)(f3 >> sh)) << 3);
+                }
+            }
+        } else {
+            const uint64_t b0 = __ballot(chg[0]), f0 = __ballot(fb[0]);
+            if (lane == 0) {
+                if (a.changed) a.changed[wbase >> 6] = b0;
+                if (a.fallback) a.fallback[wbase >> 6] = f0;
+            }
+        }
+    }
+}
+
 // ---- ReadIndex / vote / CheckQuorum over u8 bitmaps: 16 groups per lane ---------------------
 struct BitsK {
     uint64_t G;
@@ -462,7 +643,26 @@ __device__ __forceinline__ int synth_n(const hq_synth_spec &s, uint64_t cid) {
     return s.mixed_n ? (r == 0 ? 3 : r == 1 ? 5 : 7) : (int)s.n_max;
 }
 
-__global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, CommitK o) {
+// lag-layout outputs of the generator (hq_synth_commit_lag_dev); all NULL for the u64 layout
+struct LagOut {
+    int32_t *lag;
+    uint64_t stride;
+    int32_t *cin, *ts;
+    uint16_t *mask;
+    uint64_t *last;
+};
+
+__device__ __forceinline__ int32_t lag_of(uint64_t last, uint64_t x) {  // clamp(last - x)
+    if (x <= last) {
+        const uint64_t d = last - x;
+        return d >= (uint64_t)INT32_MAX ? INT32_MAX : (int32_t)d;
+    }
+    const uint64_t d = x - last;
+    return d >= (uint64_t)INT32_MAX + 1 ? INT32_MIN : -(int32_t)d;
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, CommitK o,
+                                                         LagOut lo) {
     const uint64_t R = s.ring_len;
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < s.G;
          j += (uint64_t)gridDim.x * kBlock) {
@@ -494,15 +694,19 @@ __global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, 
                 }
             }
             if (o.match) const_cast<uint64_t *>(o.match)[(uint64_t)k * o.stride + j] = m;
+            if (lo.lag) lo.lag[(uint64_t)k * lo.stride + j] = k < n ? lag_of(last, m) : 0;
         }
+        if (lo.cin) lo.cin[j] = lag_of(last, committed);
+        if (lo.ts) lo.ts[j] = lag_of(last, term_start);
+        if (lo.last) lo.last[j] = last;
         if (o.nv) const_cast<uint8_t *>(o.nv)[j] = (uint8_t)n;
         if (o.cin) const_cast<uint64_t *>(o.cin)[j] = committed;
         if (o.last) const_cast<uint64_t *>(o.last)[j] = last;
         if (o.tstart) const_cast<uint64_t *>(o.tstart)[j] = term_start;
         if (o.term) const_cast<uint64_t *>(o.term)[j] = term;
-        if (o.ring || o.mask || o.ring32) {
+        if (o.ring || o.mask || o.ring32 || lo.mask) {
             uint64_t cur = term;
-            uint32_t mask = 0;
+            uint32_t mask = 0, lmask = 0;
             for (uint64_t k = 0; k < R; ++k) {
                 const uint64_t i = last - k;
                 uint64_t t;
@@ -519,8 +723,10 @@ __global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, 
                     const_cast<uint32_t *>(o.ring32)[j * R + (i & (R - 1))] =
                         t < 0xFFFFFFFFull ? (uint32_t)t : 0xFFFFFFFFu;
                 mask |= (uint32_t)(t == term) << (i & (R - 1));
+                lmask |= (uint32_t)(t == term) << k;   // indexed by lag k = last - i
             }
             if (o.mask) const_cast<uint16_t *>(o.mask)[j] = (uint16_t)mask;
+            if (lo.mask) lo.mask[j] = (uint16_t)lmask;
         }
     }
 }
@@ -735,6 +941,90 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     return hq::post_launch(ctx, "k_commit_fused");
 }
 
+namespace {
+
+template <int N, int FORM, int VEC, bool PERN>
+int launch_lag_t(hq_ctx *ctx, const LagK &k) {
+    const unsigned grid = grid_for((k.G + VEC - 1) / VEC, kCommitBlock, kMaxBlocks / 2);
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_commit_lag<N, FORM, VEC, PERN>), dim3(grid), dim3(kCommitBlock), 0,
+                       ctx->stream, k);
+    return hq::post_launch(ctx, "k_commit_lag");
+}
+
+template <int N>
+int launch_lag_n(hq_ctx *ctx, const LagK &k, int form, bool vec4, bool pern) {
+#define HQ_LAG_DISPATCH(F)                                                                   \
+    if (vec4) return pern ? launch_lag_t<N, F, 4, true>(ctx, k) : launch_lag_t<N, F, 4, false>(ctx, k); \
+    return pern ? launch_lag_t<N, F, 1, true>(ctx, k) : launch_lag_t<N, F, 1, false>(ctx, k);
+    if (form == HQ_FORM_TERM_START) {
+        HQ_LAG_DISPATCH(HQ_FORM_TERM_START)
+    } else {
+        HQ_LAG_DISPATCH(HQ_FORM_TERM_MASK)
+    }
+#undef HQ_LAG_DISPATCH
+}
+
+int validate_lag(hq_ctx *ctx, const hq_commit_lag_args *a) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: args is NULL");
+    if (a->n_max < 1 || a->n_max > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: n_max must be 1..8");
+    if (a->G == 0) return HQ_OK;
+    if (!a->lag || !a->cin_lag || !a->cout_lag)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: NULL lag/cin_lag/cout_lag");
+    if (a->lag_stride < a->G) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: lag_stride < G");
+    if (a->form == HQ_FORM_TERM_START) {
+        if (!a->ts_lag) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: ts_lag is NULL");
+    } else if (a->form == HQ_FORM_TERM_MASK) {
+        if (!a->lag_mask) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: lag_mask is NULL");
+        if (a->ring_len < 1 || a->ring_len > 16 || (a->ring_len & (a->ring_len - 1)))
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: mask form needs ring_len <= 16 (power of two)");
+    } else {
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: form must be TERM_START or TERM_MASK");
+    }
+    return HQ_OK;
+}
+
+}  // namespace
+
+extern "C" int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *a) {
+    int rc = validate_lag(ctx, a);
+    if (rc || a->G == 0) return rc;
+    LagK k;
+    k.G = a->G;
+    k.stride = a->lag_stride;
+    k.nwords = hq::words64(a->G);
+    k.n_max = a->n_max;
+    k.R = a->ring_len;
+    k.lag = a->lag;
+    k.nv = a->n_voting;
+    k.cin = a->cin_lag;
+    k.cout = a->cout_lag;
+    k.ts = a->ts_lag;
+    k.mask = a->lag_mask;
+    k.changed = a->changed;
+    k.fallback = a->fallback;
+    const bool aux_ok = a->form == HQ_FORM_TERM_START
+                            ? hq::aligned16(a->ts_lag)
+                            : (reinterpret_cast<uintptr_t>(a->lag_mask) & 7) == 0;
+    const bool vec4 = hq::aligned16(a->lag) && (a->lag_stride % 4 == 0) &&
+                      hq::aligned16(a->cin_lag) && hq::aligned16(a->cout_lag) && aux_ok &&
+                      (!a->n_voting || (reinterpret_cast<uintptr_t>(a->n_voting) & 3) == 0);
+    const bool pern = a->n_voting != nullptr;
+    switch (a->n_max) {
+    case 1: return launch_lag_n<1>(ctx, k, a->form, vec4, pern);
+    case 2: return launch_lag_n<2>(ctx, k, a->form, vec4, pern);
+    case 3: return launch_lag_n<3>(ctx, k, a->form, vec4, pern);
+    case 4: return launch_lag_n<4>(ctx, k, a->form, vec4, pern);
+    case 5: return launch_lag_n<5>(ctx, k, a->form, vec4, pern);
+    case 6: return launch_lag_n<6>(ctx, k, a->form, vec4, pern);
+    case 7: return launch_lag_n<7>(ctx, k, a->form, vec4, pern);
+    default: return launch_lag_n<8>(ctx, k, a->form, vec4, pern);
+    }
+}
+
 extern "C" int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count) {
     if (!ctx) return HQ_E_INVAL;
     if (count && !args) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_many_dev: args is NULL");
@@ -865,7 +1155,29 @@ extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,
         return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit: term_mask needs ring_len <= 16");
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_synth_commit, dim3(grid_for(s->G)), dim3(kBlock), 0, ctx->stream, *s, o);
+    hipLaunchKernelGGL(k_synth_commit, dim3(grid_for(s->G)), dim3(kBlock), 0, ctx->stream, *s, o,
+                       LagOut{});
+    return hq::post_launch(ctx, "k_synth_commit");
+}
+
+extern "C" int hq_synth_commit_lag_dev(hq_ctx *ctx, const hq_synth_spec *s,
+                                       const hq_commit_lag_args *a, uint64_t *last_index) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!s || !a) return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit_lag: NULL argument");
+    if (s->ring_len < 1 || (s->ring_len & (s->ring_len - 1)) || s->n_max < 1 || s->n_max > 8 ||
+        s->cid_stride < 1 || (s->mixed_n && s->n_max < 7) || (a->lag && a->lag_stride < s->G) ||
+        (a->lag_mask && s->ring_len > 16))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit_lag: bad spec");
+    if (s->G == 0) return HQ_OK;
+    CommitK o{};
+    o.G = s->G;
+    o.nv = a->n_voting;
+    LagOut lo{const_cast<int32_t *>(a->lag), a->lag_stride, const_cast<int32_t *>(a->cin_lag),
+              const_cast<int32_t *>(a->ts_lag), const_cast<uint16_t *>(a->lag_mask), last_index};
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_synth_commit, dim3(grid_for(s->G)), dim3(kBlock), 0, ctx->stream, *s, o,
+                       lo);
     return hq::post_launch(ctx, "k_synth_commit");
 }
 

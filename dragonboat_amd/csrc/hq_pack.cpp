@@ -145,3 +145,58 @@ extern "C" int hq_pack_ring32(const uint64_t *ring, uint64_t count, uint32_t *ri
         ring32[i] = ring[i] < 0xFFFFFFFFull ? (uint32_t)ring[i] : 0xFFFFFFFFu;
     return HQ_OK;
 }
+
+namespace {
+
+int32_t lag_of(uint64_t last, uint64_t x) {  // clamp(last - x) to int32
+    if (x <= last) {
+        const uint64_t d = last - x;
+        return d >= (uint64_t)INT32_MAX ? INT32_MAX : (int32_t)d;
+    }
+    const uint64_t d = x - last;
+    return d >= (uint64_t)INT32_MAX + 1 ? INT32_MIN : -(int32_t)d;
+}
+
+}  // namespace
+
+extern "C" int hq_pack_lags(uint64_t G, uint32_t n_max, const uint64_t *match,
+                            uint64_t match_stride, const uint64_t *committed,
+                            const uint64_t *last_index, const uint64_t *term_start,
+                            const uint16_t *term_mask, const hq_commit_lag_args *out) {
+    if (G == 0) return HQ_OK;
+    if (!match || !committed || !last_index || !out || !out->lag || !out->cin_lag ||
+        match_stride < G || out->lag_stride < G || n_max < 1 || n_max > out->n_max)
+        return HQ_E_INVAL;
+    const bool ts = out->form == HQ_FORM_TERM_START;
+    if (ts ? (!term_start || !out->ts_lag) : (!term_mask || !out->lag_mask)) return HQ_E_INVAL;
+    const uint32_t R = out->ring_len;
+    if (!ts && (R < 1 || R > 16 || (R & (R - 1)))) return HQ_E_INVAL;
+    int32_t *lag = const_cast<int32_t *>(out->lag);
+    for (uint32_t s = 0; s < n_max; ++s)
+        for (uint64_t g = 0; g < G; ++g)
+            lag[s * out->lag_stride + g] = lag_of(last_index[g], match[s * match_stride + g]);
+    for (uint64_t g = 0; g < G; ++g) {
+        const uint64_t last = last_index[g];
+        const_cast<int32_t *>(out->cin_lag)[g] = lag_of(last, committed[g]);
+        if (ts) {
+            const_cast<int32_t *>(out->ts_lag)[g] = lag_of(last, term_start[g]);
+        } else {
+            // bit (i % R) of the u64-layout mask -> bit k = last - i of the lag-indexed mask
+            uint32_t m = 0;
+            for (uint32_t k = 0; k < R; ++k) m |= ((term_mask[g] >> ((last - k) & (R - 1))) & 1u) << k;
+            const_cast<uint16_t *>(out->lag_mask)[g] = (uint16_t)m;
+        }
+    }
+    return HQ_OK;
+}
+
+extern "C" int hq_unpack_lags(uint64_t G, const uint64_t *last_index, const int32_t *cout_lag,
+                              const uint64_t *fallback, uint64_t *committed) {
+    if (G == 0) return HQ_OK;
+    if (!last_index || !cout_lag || !committed) return HQ_E_INVAL;
+    // a decided group's cout_lag is d (>= 0) or its own unclamped cin_lag: last - lag is exact
+    for (uint64_t g = 0; g < G; ++g)
+        if (!fallback || !((fallback[g >> 6] >> (g & 63)) & 1))
+            committed[g] = last_index[g] - (uint64_t)(int64_t)cout_lag[g];
+    return HQ_OK;
+}

@@ -63,6 +63,27 @@ class CommitArgs(ctypes.Structure):
     ]
 
 
+class LagArgs(ctypes.Structure):
+    """Mirror of ``hq_commit_lag_args``."""
+
+    _fields_ = [
+        ("G", ctypes.c_uint64),
+        ("n_max", ctypes.c_uint32),
+        ("form", ctypes.c_uint32),
+        ("ring_len", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("lag_stride", ctypes.c_uint64),
+        ("lag", _vp),
+        ("n_voting", _vp),
+        ("cin_lag", _vp),
+        ("cout_lag", _vp),
+        ("ts_lag", _vp),
+        ("lag_mask", _vp),
+        ("changed", _vp),
+        ("fallback", _vp),
+    ]
+
+
 class SynthSpec(ctypes.Structure):
     """Mirror of ``hq_synth_spec``."""
 
@@ -164,6 +185,10 @@ SIGNATURES = {
     "hq_commit": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs)]),
     "hq_commit_many_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
     "hq_commit_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
+    "hq_commit_lag_dev": (ctypes.c_int, [_vp, ctypes.POINTER(LagArgs)]),
+    "hq_pack_lags": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp,
+                                    _vp, _vp, _vp, ctypes.POINTER(LagArgs)]),
+    "hq_unpack_lags": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "hq_readindex_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
     "hq_readindex": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
     "hq_vote_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
@@ -202,6 +227,8 @@ SIGNATURES = {
     "hq_worker_step": (ctypes.c_int, [_vp, ctypes.POINTER(StepInput),
                                       ctypes.POINTER(StepOutput)]),
     "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
+    "hq_synth_commit_lag_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec),
+                                               ctypes.POINTER(LagArgs), _vp]),
     "hq_synth_bitmaps_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), _vp, _vp, _vp, _vp]),
 }
 
@@ -364,6 +391,9 @@ class Context:
         share it (hq_commit_fused_dev)."""
         self._check(lib.hq_commit_fused_dev(self.h, batch, len(batch)))
 
+    def commit_lag_dev(self, args: LagArgs) -> None:
+        self._check(lib.hq_commit_lag_dev(self.h, ctypes.byref(args)))
+
     def commit_host(self, args: CommitArgs) -> None:
         self._check(lib.hq_commit(self.h, ctypes.byref(args)))
 
@@ -422,6 +452,10 @@ class Context:
     def synth_commit_dev(self, spec: SynthSpec, args: CommitArgs) -> None:
         self._check(lib.hq_synth_commit_dev(self.h, ctypes.byref(spec), ctypes.byref(args)))
 
+    def synth_commit_lag_dev(self, spec: SynthSpec, args: LagArgs, last_index=None) -> None:
+        self._check(lib.hq_synth_commit_lag_dev(self.h, ctypes.byref(spec), ctypes.byref(args),
+                                                _p(last_index)))
+
     def synth_bitmaps_dev(self, spec: SynthSpec, ack=None, granted=None, rejected=None,
                           n_voting=None) -> None:
         self._check(lib.hq_synth_bitmaps_dev(self.h, ctypes.byref(spec), _p(ack), _p(granted),
@@ -469,6 +503,48 @@ def pack_ring32(ring: np.ndarray) -> np.ndarray:
     out = np.zeros(len(ring), np.uint32)
     _chk(lib.hq_pack_ring32(_p(ring), len(ring), _p(out)), "hq_pack_ring32")
     return out
+
+
+def lag_args(G, n_max, form, ring_len, lag, cin_lag, cout_lag, ts_lag=None, lag_mask=None,
+             n_voting=None, changed=None, fallback=None, lag_stride=None) -> LagArgs:
+    """LagArgs over device arrays / numpy arrays / raw pointers (see ``_p``)."""
+    a = LagArgs()
+    a.G, a.n_max, a.form, a.ring_len = G, n_max, form, ring_len
+    a.lag_stride = G if lag_stride is None else lag_stride
+    for name, v in (("lag", lag), ("cin_lag", cin_lag), ("cout_lag", cout_lag),
+                    ("ts_lag", ts_lag), ("lag_mask", lag_mask), ("n_voting", n_voting),
+                    ("changed", changed), ("fallback", fallback)):
+        ptr = _p(v)
+        setattr(a, name, ptr.value if ptr is not None else None)
+    return a
+
+
+def pack_lags(G, n_max, form, ring_len, match, committed, last_index, term_start=None,
+              term_mask=None, match_stride=None):
+    """hq_pack_lags into fresh host arrays: (lag [n_max*G] int32, cin_lag, ts_lag or lag_mask)."""
+    lag = np.zeros(n_max * G, np.int32)
+    cin = np.zeros(G, np.int32)
+    ts = np.zeros(G, np.int32) if form == HQ_FORM_TERM_START else None
+    lm = np.zeros(G, np.uint16) if form == HQ_FORM_TERM_MASK else None
+    out = lag_args(G, n_max, form, ring_len, lag, cin, cin, ts, lm)
+    _chk(lib.hq_pack_lags(G, n_max, _p(np.ascontiguousarray(match, np.uint64)),
+                          G if match_stride is None else match_stride,
+                          _p(np.ascontiguousarray(committed, np.uint64)),
+                          _p(np.ascontiguousarray(last_index, np.uint64)),
+                          _p(None if term_start is None else np.ascontiguousarray(term_start, np.uint64)),
+                          _p(None if term_mask is None else np.ascontiguousarray(term_mask, np.uint16)),
+                          ctypes.byref(out)), "hq_pack_lags")
+    return lag, cin, (ts if form == HQ_FORM_TERM_START else lm)
+
+
+def unpack_lags(last_index: np.ndarray, cout_lag: np.ndarray, committed: np.ndarray,
+                fallback: Optional[np.ndarray] = None) -> np.ndarray:
+    """hq_unpack_lags: committed' = lastIndex - cout_lag for the groups without a fallback bit
+    (updates ``committed`` in place and returns it)."""
+    _chk(lib.hq_unpack_lags(len(last_index), _p(np.ascontiguousarray(last_index, np.uint64)),
+                            _p(np.ascontiguousarray(cout_lag, np.int32)), _p(fallback),
+                            _p(committed)), "hq_unpack_lags")
+    return committed
 
 
 def pack_votes(groups: np.ndarray, members: np.ndarray, msgs: np.ndarray):
@@ -577,6 +653,44 @@ def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16
         ring32=ctx.empty(G * ring_len, np.uint32) if need_ring32 else None,
     )
     return b
+
+
+@dataclass
+class LagBuffers:
+    """Device lag-layout state of one batch (hq_commit_lag_args)."""
+
+    G: int
+    n_max: int
+    form: int
+    ring_len: int
+    lag: DeviceArray
+    cin_lag: DeviceArray
+    cout_lag: DeviceArray
+    aux: DeviceArray          # ts_lag (int32) or lag_mask (uint16)
+    changed: DeviceArray
+    fallback: DeviceArray
+    last_index: Optional[DeviceArray] = None
+
+    def args(self) -> LagArgs:
+        ts = self.aux if self.form == HQ_FORM_TERM_START else None
+        lm = self.aux if self.form == HQ_FORM_TERM_MASK else None
+        return lag_args(self.G, self.n_max, self.form, self.ring_len, self.lag, self.cin_lag,
+                        self.cout_lag, ts, lm, None, self.changed, self.fallback)
+
+    def arrays(self):
+        return [x for x in (self.lag, self.cin_lag, self.cout_lag, self.aux, self.changed,
+                            self.fallback, self.last_index) if x is not None]
+
+
+def alloc_commit_lag(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
+                     with_last: bool = False) -> LagBuffers:
+    return LagBuffers(
+        G=G, n_max=n_max, form=form, ring_len=ring_len,
+        lag=ctx.empty(G * n_max, np.int32), cin_lag=ctx.empty(G, np.int32),
+        cout_lag=ctx.empty(G, np.int32),
+        aux=ctx.empty(G, np.int32 if form == HQ_FORM_TERM_START else np.uint16),
+        changed=ctx.empty(words64(G), np.uint64), fallback=ctx.empty(words64(G), np.uint64),
+        last_index=ctx.empty(G, np.uint64) if with_last else None)
 
 
 def synth_spec(seed: int, G: int, n_max: int, cid_base: int = 1, cid_stride: int = 1,

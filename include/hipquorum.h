@@ -182,6 +182,60 @@ int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
  * when the batches cannot share a launch. */
 int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
 
+/* ---------------------------------------------------------------- commit over lags --------- */
+/*
+ * The same decision over a compact layout: every index is stored as its distance below the
+ * group's lastIndex, as int32 ("lag"). The decision depends only on the order of the match
+ * values, committed, term_start and lastIndex, and that order is kept by the lags:
+ *   lag[s][g] = clamp(last_index - match_s)      (negative when match > last_index)
+ *   cin_lag[g] = clamp(last_index - committed)
+ *   ts_lag[g]  = clamp(last_index - term_start)  (HQ_FORM_TERM_START)
+ *   lag_mask[g] bit k = (term(last_index - k) == the leader's term), k < ring_len
+ *                                                 (HQ_FORM_TERM_MASK; the mask indexed by lag)
+ * with clamp() saturating to [INT32_MIN, INT32_MAX]. Then (raft.go:888-909, logentry.go:378-393)
+ *   d  = the (n/2+1)-th SMALLEST lag                   (= lastIndex - the quorum-th largest match)
+ *   commit iff d < cin_lag && d >= 0 && (d <= ts_lag | bit d of lag_mask)
+ *   cout_lag[g] = commit ? d : cin_lag[g];     committed' = lastIndex - cout_lag (hq_unpack_lags)
+ * Saturation never changes a decision: a clamped lag is only ever compared against an unclamped
+ * cin_lag. Fallback (not decided, as in hq_commit_dev): n == 0 or n > n_max; TERM_START:
+ * cin_lag == INT32_MAX or INT32_MIN (committed not representable); TERM_MASK: cin_lag < 0 or
+ * cin_lag > ring_len (the mask form's contract). A decided group's cout_lag is exact.
+ * Bytes per group: 4n + 12 (term-start; 24 B at n = 3 against 56 B for hq_commit_dev) or
+ * 4n + 10 (mask). Packed from the u64 columns by hq_pack_lags (host) or generated on the device.
+ */
+typedef struct hq_commit_lag_args {
+    uint64_t G;
+    uint32_t n_max;           /* 1..HQ_MAX_VOTERS */
+    uint32_t form;            /* HQ_FORM_TERM_START or HQ_FORM_TERM_MASK */
+    uint32_t ring_len;        /* TERM_MASK: power of two <= 16 */
+    uint32_t reserved;
+    uint64_t lag_stride;      /* elements between slot rows of lag, >= G */
+    const int32_t *lag;       /* [n_max][lag_stride] */
+    const uint8_t *n_voting;  /* [G] or NULL (all groups have n_max) */
+    const int32_t *cin_lag;   /* [G] */
+    int32_t *cout_lag;        /* [G] (may alias cin_lag) */
+    const int32_t *ts_lag;    /* [G] TERM_START */
+    const uint16_t *lag_mask; /* [G] TERM_MASK */
+    uint64_t *changed;        /* [ceil(G/64)] or NULL */
+    uint64_t *fallback;       /* [ceil(G/64)] or NULL */
+} hq_commit_lag_args;
+
+int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *args);
+
+/* Host packer: the lag columns of *out (lag rows at out->lag_stride, cin_lag and ts_lag or
+ * lag_mask per out->form) from u64 columns laid out as in hq_commit_args (match rows at
+ * match_stride; term_start for TERM_START; term_mask (bit i % ring_len) for TERM_MASK).
+ * Slots >= n_max of the lag rows are not written. */
+int hq_pack_lags(uint64_t G, uint32_t n_max, const uint64_t *match, uint64_t match_stride,
+                 const uint64_t *committed, const uint64_t *last_index,
+                 const uint64_t *term_start, const uint16_t *term_mask,
+                 const hq_commit_lag_args *out);
+/* committed[g] = last_index[g] - cout_lag[g] (the host's commitTo, logentry.go:323-332) for
+ * every group whose fallback bit is clear (fallback may be NULL); fallback groups keep their
+ * committed value for the CPU path. */
+int hq_unpack_lags(uint64_t G, const uint64_t *last_index, const int32_t *cout_lag,
+                   const uint64_t *fallback, uint64_t *committed);
+
 /* ---------------------------------------------------------------- ReadIndex / vote ----------- */
 
 /*
@@ -554,6 +608,10 @@ typedef struct hq_synth_spec {
  * ignored. term_mask needs spec->ring_len <= 16. */
 int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *spec, const hq_commit_args *args);
 /* Fills the ack / granted / rejected bitmaps and n_voting (each if non-NULL). */
+/* The same generated batch in the lag layout (hq_commit_lag_args; lag rows, cin_lag, ts_lag and
+ * lag_mask, each if non-NULL); last_index (if non-NULL) receives the groups' lastIndex. */
+int hq_synth_commit_lag_dev(hq_ctx *ctx, const hq_synth_spec *spec,
+                            const hq_commit_lag_args *args, uint64_t *last_index);
 int hq_synth_bitmaps_dev(hq_ctx *ctx, const hq_synth_spec *spec, uint8_t *ack, uint8_t *granted,
                          uint8_t *rejected, uint8_t *n_voting);
 

@@ -528,3 +528,176 @@ def test_timing_counts_launches(gpu_ctx, hq):
     gpu_ctx.timing(False)
     assert n == 5 and ms > 0
     hq.free_commit(gpu_ctx, b)
+
+
+# ----------------------------------------------------------------------- lag layout ----------
+I32_MIN, I32_MAX = -(1 << 31), (1 << 31) - 1
+
+
+def run_commit_lag(ctx, hq, inp, form, per_group_n, stride_pad=0, offset_elems=0,
+                   lags=None):
+    """The oracle-generated u64 batch packed into lags on the host (hq_pack_lags), decided by
+    hq_commit_lag_dev; returns (committed' unpacked, changed, fallback)."""
+    G, n = inp.G, inp.n_max
+    lag, cin, aux = lags if lags is not None else hq.pack_lags(
+        G, n, form, inp.R, inp.match, inp.committed_in, inp.last_index, inp.term_start,
+        inp.term_mask)
+    stride = G + stride_pad
+    rows = np.zeros((n, stride), np.int32)
+    rows[:, :G] = lag.reshape(n, G)
+    bufs = []
+
+    def up(a):
+        full = np.concatenate([np.zeros(offset_elems, a.dtype), a]) if offset_elems else a
+        d = ctx.upload(full)
+        bufs.append(d)
+        return d.ptr + offset_elems * a.dtype.itemsize
+
+    out = ctx.empty(G + offset_elems + 4, np.int32)
+    chg = ctx.empty(hq.words64(G), np.uint64)
+    fb = ctx.empty(hq.words64(G), np.uint64)
+    ctx.memset(chg, 0xFF)
+    ctx.memset(fb, 0xFF)
+    bufs += [out, chg, fb]
+    a = hq.lag_args(G, n, form, inp.R, up(rows.reshape(-1)), up(cin),
+                    out.ptr + offset_elems * 4,
+                    up(aux) if form == 0 else None, up(aux) if form == 2 else None,
+                    up(inp.n_voting) if per_group_n else None, chg, fb, lag_stride=stride)
+    ctx.commit_lag_dev(a)
+    ctx.sync()
+    cout = ctx.download(out)[offset_elems:offset_elems + G]
+    c, f = ctx.download(chg), ctx.download(fb)
+    for b in bufs:
+        ctx.free(b)
+    com = inp.committed_in.copy()
+    hq.unpack_lags(inp.last_index, cout, com, f)
+    return com, c, f
+
+
+def check_commit_lag(ctx, hq, inp, form, per_group_n, **kw):
+    com, chg, fb = run_commit_lag(ctx, hq, inp, form, per_group_n, **kw)
+    want_out, want_chg, want_fb, rc = inp.run(form, per_group_n, nthreads=8)
+    assert rc == 0
+    bad = np.nonzero(com != want_out)[0]
+    assert bad.size == 0, f"{bad.size} groups differ, first {bad[:5]}"
+    np.testing.assert_array_equal(chg, want_chg)
+    np.testing.assert_array_equal(fb, want_fb)
+    return chg
+
+
+@pytest.mark.parametrize("form", [0, 2])
+@pytest.mark.parametrize("n_max", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_commit_lag_uniform_n(gpu_ctx, hq, form, n_max):
+    inp = qref.CommitInputs(qref.spec(SEED + 21, 65_537, n_max, parity_extras=True))
+    chg = check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False)
+    if n_max > 1:
+        assert 0 < popcount(chg) < inp.G
+
+
+@pytest.mark.parametrize("form", [0, 2])
+@pytest.mark.parametrize("n_max", [7, 8])
+def test_commit_lag_per_group_n(gpu_ctx, hq, form, n_max):
+    inp = qref.CommitInputs(qref.spec(SEED + 22, 99_999, n_max, mixed_n=True, parity_extras=True))
+    check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=True)
+
+
+@pytest.mark.parametrize("form", [0, 2])
+def test_commit_lag_vec1_and_ragged(gpu_ctx, hq, form):
+    inp = qref.CommitInputs(qref.spec(SEED + 23, 10_001, 5, parity_extras=True))
+    check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False, stride_pad=1)
+    check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False, offset_elems=1)
+    for G in (1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 1001):
+        inp = qref.CommitInputs(qref.spec(SEED + G, G, 3, parity_extras=True))
+        check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False)
+        inp8 = qref.CommitInputs(qref.spec(SEED + G, G, 8, mixed_n=True))
+        check_commit_lag(gpu_ctx, hq, inp8, form, per_group_n=True)
+
+
+def test_commit_lag_reference_kats(gpu_ctx, hq):
+    cases = []
+    for table in ("TestCommit", "TestLeaderOnlyCommitsLogFromCurrentTerm",
+                  "TestLeaderAcknowledgeCommit", "TestLeaderCommitPrecedingEntries",
+                  "TestSingleNodeCommit", "TestCannotCommitWithoutNewTermEntry",
+                  "TestCommitWithoutNewTermEntry", "TestLeaderAppResp",
+                  "TestFullMemberWithOneWitness", "TestVotingMemberLengthMismatch"):
+        cases += KATS[table]
+    inp = _kat_inputs(cases)
+    want = np.array([c["want_committed"] for c in cases], np.uint64)
+    com, chg, fb = run_commit_lag(gpu_ctx, hq, inp, 2, per_group_n=True)
+    assert popcount(fb) == 0
+    np.testing.assert_array_equal(com, want)
+    ok = np.array([_term_start_representable(c) for c in cases])
+    com, chg, fb = run_commit_lag(gpu_ctx, hq, inp, 0, per_group_n=True)
+    np.testing.assert_array_equal(com[ok], want[ok])
+
+
+def test_commit_lag_saturation_is_exact(gpu_ctx, hq):
+    """Indexes 2^31 and more away from lastIndex: saturated lags never change a decision; only
+    an unrepresentable committed falls back (term-start form)."""
+    G, n = 4096, 5
+    rng = np.random.default_rng(9)
+    inp = qref.CommitInputs(qref.spec(SEED + 24, G, n))
+    last = inp.last_index
+    m = inp.match.reshape(n, G).copy()
+    lastb = np.broadcast_to(last, (n, G))
+    far = rng.random((n, G)) < 0.25
+    m[far] = lastb[far] - np.uint64(1 << 35)                            # far behind
+    ahead = rng.random((n, G)) < 0.05
+    m[ahead] = lastb[ahead] + np.uint64((1 << 33) + 5)                  # far above last
+    inp.match[:] = m.reshape(-1)
+    cfar = rng.random(G) < 0.05
+    inp.committed_in[cfar] = last[cfar] - np.uint64((1 << 31) + 7)       # not representable
+    tsfar = rng.random(G) < 0.1
+    inp.term_start[tsfar] = last[tsfar] - np.uint64(1 << 34)            # far below: any q >= ts
+    com, chg, fb = run_commit_lag(gpu_ctx, hq, inp, 0, per_group_n=False)
+    want_out, want_chg, _, rc = inp.run(0, False)
+    fbits = np.unpackbits(fb.view(np.uint8), bitorder="little")[:G].astype(bool)
+    np.testing.assert_array_equal(fbits, cfar)
+    np.testing.assert_array_equal(com[~cfar], want_out[~cfar])
+    cbits = np.unpackbits(chg.view(np.uint8), bitorder="little")[:G].astype(bool)
+    wbits = np.unpackbits(want_chg.view(np.uint8), bitorder="little")[:G].astype(bool)
+    np.testing.assert_array_equal(cbits[~cfar], wbits[~cfar])
+    assert cbits.sum() > G // 10
+
+
+@pytest.mark.parametrize("kw", [dict(n_max=3), dict(n_max=5, parity_extras=True),
+                                dict(n_max=8, mixed_n=True, parity_extras=True)])
+def test_synth_commit_lag_matches_host_packer(gpu_ctx, hq, kw):
+    G = 50_003
+    host = qref.CommitInputs(qref.spec(SEED + 25, G, **kw))
+    spec = hq.synth_spec(SEED + 25, G, **kw)
+    for form in (0, 2):
+        lag, cin, aux = hq.pack_lags(G, kw["n_max"], form, 16, host.match, host.committed_in,
+                                     host.last_index, host.term_start, host.term_mask)
+        if kw.get("mixed_n"):   # the device generator writes 0 into slots >= n
+            rows = lag.reshape(kw["n_max"], G)
+            for s in range(kw["n_max"]):
+                rows[s][host.n_voting <= s] = 0
+        b = hq.alloc_commit_lag(gpu_ctx, G, kw["n_max"], form, 16, with_last=True)
+        gpu_ctx.synth_commit_lag_dev(spec, b.args(), b.last_index)
+        gpu_ctx.sync()
+        np.testing.assert_array_equal(gpu_ctx.download(b.lag), lag)
+        np.testing.assert_array_equal(gpu_ctx.download(b.cin_lag), cin)
+        np.testing.assert_array_equal(gpu_ctx.download(b.aux), aux)
+        np.testing.assert_array_equal(gpu_ctx.download(b.last_index), host.last_index)
+        hq.free_commit(gpu_ctx, b)
+
+
+@pytest.mark.parametrize("n_max,form", [(3, 0), (5, 2)])
+def test_commit_lag_full_size(gpu_ctx, hq, n_max, form):
+    """BASELINE configs 2 and 3 at full size in the lag layout: device-generated, decided,
+    unpacked, equal to the oracle's u64 decision on the CPU generator's copy."""
+    G = 1 << 20
+    b = hq.alloc_commit_lag(gpu_ctx, G, n_max, form, 16, with_last=True)
+    gpu_ctx.synth_commit_lag_dev(hq.synth_spec(SEED + n_max, G, n_max), b.args(), b.last_index)
+    gpu_ctx.commit_lag_dev(b.args())
+    gpu_ctx.sync()
+    inp = qref.CommitInputs(qref.spec(SEED + n_max, G, n_max))
+    want_out, want_chg, want_fb, rc = inp.run(form, False, nthreads=16)
+    com = inp.committed_in.copy()
+    hq.unpack_lags(inp.last_index, gpu_ctx.download(b.cout_lag), com,
+                   gpu_ctx.download(b.fallback))
+    np.testing.assert_array_equal(com, want_out)
+    np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+    assert popcount(gpu_ctx.download(b.fallback)) == 0
+    hq.free_commit(gpu_ctx, b)

@@ -18,7 +18,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {"c2": "k_commit<3, 0, 2, false>", "c3": "k_commit<5, 1, 2, false>",
           "c3m": "k_commit<5, 2, 2, false>", "c3r32": "k_commit<5, 3, 2, false>",
-          "c4": "k_bits<3, true", "c5": "k_commit_fused<2>", "c5s": "k_commit<7, 2, 2, false>"}
+          "c4": "k_bits<3, true", "c5": "k_commit_fused<2>", "c5s": "k_commit<7, 2, 2, false>",
+          "c2l": "k_commit_lag<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>"}
 
 
 def counter(path, kernel):
