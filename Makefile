@@ -27,7 +27,14 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# tuning variant: lag kernels with 2 groups per lane (8-byte loads), for A/B runs via HQ_LIB_PATH
+tools/lib_vec2/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(DEPS)
+	@mkdir -p tools/lib_vec2
+	$(HIPCC) $(HIPFLAGS) -DHQ_LAG_VEC=2 -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
+
+variants: tools/lib_vec2/libhipquorum.so
+
 clean:
 	rm -rf $(LIBDIR) oracle/build
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean variants

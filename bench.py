@@ -51,6 +51,9 @@ WORKLOADS = {
     "c3l": dict(cfg=2, kind="lag", G=1 << 20, n=5, form=2, mixed=False,
                 desc="1M groups x 5 voters (4 full + 1 witness), commit over int32 lags with the "
                      "lag-indexed current-term mask (30 B per decision)"),
+    "c5l": dict(cfg=4, kind="lag", G=8 << 20, n=5, form=2, mixed=True,
+                desc="as c5 in the int32 lag layout (lag-indexed mask), the three buckets in one "
+                     "fused launch"),
     "c4": dict(cfg=3, kind="bits", G=16 << 20, n=7,
                desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
@@ -165,12 +168,14 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
                 buckets.append(b)
             sets.append(buckets)
         elif w["kind"] == "lag":
-            rng = shard.rank_shard(d.rank, d.world, G)
-            spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
-                                 cid_stride=rng.cid_stride)
-            b = hq.alloc_commit_lag(ctx, G, w["n"], w["form"], 16)
-            ctx.synth_commit_lag_dev(spec, b.args())
-            sets.append(b)
+            buckets = []
+            for n, rng in commit_buckets(shard, w, d):
+                spec = hq.synth_spec(seed + (s << 40), rng.count, n, cid_base=rng.cid_base,
+                                     cid_stride=rng.cid_stride)
+                b = hq.alloc_commit_lag(ctx, rng.count, n, w["form"], 16)
+                ctx.synth_commit_lag_dev(spec, b.args())
+                buckets.append(b)
+            sets.append(buckets)
         else:
             rng = shard.rank_shard(d.rank, d.world, G)
             spec = hq.synth_spec(seed + (s << 40), G, w["n"], cid_base=rng.cid_base,
@@ -193,14 +198,14 @@ def commit_buckets(shard, w, d):
 
 
 def algo_bytes_per_step(w):
-    if w["kind"] == "commit" and w["mixed"]:
+    if w["kind"] in ("commit", "lag") and w["mixed"]:
         per = w["G"] // 3
         return sum(per * algo_bytes_per_group(dict(w, n=n, mixed=False)) for n in (3, 5, 7))
     return algo_bytes_per_group(w) * w["G"]
 
 
 def groups_per_step(w):
-    return (w["G"] // 3) * 3 if w["kind"] == "commit" and w["mixed"] else w["G"]
+    return (w["G"] // 3) * 3 if w["kind"] in ("commit", "lag") and w["mixed"] else w["G"]
 
 
 def run_gpu(w, steps, warmup, d: Dist):
@@ -219,12 +224,17 @@ def run_gpu(w, steps, warmup, d: Dist):
             for i in idx:
                 ctx.commit_fused_dev(per_step[i % len(per_step)])
     elif w["kind"] == "lag":
-        lag_args = [b.args() for b in sets]
+        # one launch per step: the bucket set's batches fused (a single batch: plain launch)
+        per_step = [hq.lag_batch_array([b.args() for b in bs]) for bs in sets]
         seq, wseq = list(range(steps)), list(range(max(1, warmup)))
 
         def run(idx):
             for i in idx:
-                ctx.commit_lag_dev(lag_args[i % len(lag_args)])
+                arr = per_step[i % len(per_step)]
+                if len(arr) == 1:
+                    ctx.commit_lag_dev(arr[0])
+                else:
+                    ctx.commit_lag_fused_dev(arr)
     elif w["kind"] == "commit":
         def flat(k):
             return hq.commit_batch_array([b.args() for i in range(k) for b in sets[i % len(sets)]])
@@ -597,7 +607,7 @@ def main():
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5r,c5r32,w2,e2e,step",
+    ap.add_argument("--extra", default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5l,c5r,c5r32,w2,e2e,step",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 

@@ -304,6 +304,12 @@ struct LagK {
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
+// groups per lane of the lag kernels (4: 16-byte loads, 2: 8-byte loads); HQ_LAG_VEC at build
+#ifndef HQ_LAG_VEC
+#define HQ_LAG_VEC 4
+#endif
+constexpr int kLagVec = HQ_LAG_VEC;
+
 __device__ __forceinline__ void ce_i32(int32_t &a, int32_t &b) {
     const int32_t lo = a < b ? a : b, hi = a < b ? b : a;
     a = lo;
@@ -375,96 +381,153 @@ __device__ __forceinline__ uint64_t spread16x4(uint32_t x) {
     return v;
 }
 
-// VEC = 4: lane owns groups g0..g0+3 (16-byte loads); VEC = 1: one group, 4-byte loads.
+template <int V> struct LagVec;   // VEC int32 lanes of one load
+template <> struct LagVec<4> { typedef i32x4 T; typedef uint64_t M; typedef uint32_t NV; };
+template <> struct LagVec<2> {
+    typedef int32_t T __attribute__((ext_vector_type(2)));
+    typedef uint32_t M;
+    typedef uint16_t NV;
+};
+
+// bit i of the V ballots' 64/V-bit slice -> bit V*i + j of a bitmap word
+template <int V>
+__device__ __forceinline__ uint64_t spread_v(uint32_t x) {
+    if constexpr (V == 4) return spread16x4(x);
+    else if constexpr (V == 2) return spread32(x);
+    else return x;
+}
+
+// VEC = 4 / 2: lane owns groups g0..g0+VEC-1 (16- / 8-byte loads of every column); VEC = 1: one
+// group, 4-byte loads. The body of workgroup `blk` of `nblk` on batch `a`.
 template <int N, int FORM, int VEC, bool PERN>
-__global__ __launch_bounds__(kCommitBlock) void k_commit_lag(const LagK a) {
+__device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t nblk) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * (kCommitBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t step = (uint64_t)gridDim.x * kCommitBlock * VEC;
+    const uint64_t wave = blk * (kCommitBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = nblk * kCommitBlock * VEC;
     for (uint64_t wbase = wave * 64 * VEC; wbase < a.G; wbase += step) {
         const uint64_t g0 = wbase + (uint64_t)lane * VEC;
         bool chg[VEC], fb[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) chg[j] = fb[j] = false;
-        if (VEC == 4 && g0 + 3 < a.G) {
-            int32_t l[4][N];
+        bool done = false;
+        if constexpr (VEC > 1) {
+            if (g0 + VEC <= a.G) {
+                done = true;
+                typedef typename LagVec<VEC>::T VT;
+                int32_t l[VEC][N];
 #pragma unroll
-            for (int s = 0; s < N; ++s) {
-                const i32x4 v = __builtin_nontemporal_load(
-                    reinterpret_cast<const i32x4 *>(a.lag + s * a.stride + g0));
-                l[0][s] = v.x;
-                l[1][s] = v.y;
-                l[2][s] = v.z;
-                l[3][s] = v.w;
-            }
-            const i32x4 ci = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(a.cin + g0));
-            i32x4 ax;
-            if constexpr (FORM == HQ_FORM_TERM_START) {
-                ax = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(a.ts + g0));
-            } else {
-                // the lane's 4 u16 masks: one aligned 8-byte load
-                const uint64_t m4 = __builtin_nontemporal_load(
-                    reinterpret_cast<const uint64_t *>(a.mask + g0));
-                ax = (i32x4){(int32_t)(m4 & 0xFFFF), (int32_t)((m4 >> 16) & 0xFFFF),
-                             (int32_t)((m4 >> 32) & 0xFFFF), (int32_t)(m4 >> 48)};
-            }
-            int n4[4] = {N, N, N, N};
-            if constexpr (PERN) {
-                const uint32_t nn = *reinterpret_cast<const uint32_t *>(a.nv + g0);
+                for (int s = 0; s < N; ++s) {
+                    const VT v = __builtin_nontemporal_load(
+                        reinterpret_cast<const VT *>(a.lag + s * a.stride + g0));
 #pragma unroll
-                for (int j = 0; j < 4; ++j) n4[j] = (nn >> (8 * j)) & 0xFF;
-            }
-            int32_t co[4];
-            const int32_t cv[4] = {ci.x, ci.y, ci.z, ci.w}, av[4] = {ax.x, ax.y, ax.z, ax.w};
+                    for (int j = 0; j < VEC; ++j) l[j][s] = v[j];
+                }
+                const VT ci = __builtin_nontemporal_load(reinterpret_cast<const VT *>(a.cin + g0));
+                int32_t av[VEC];
+                if constexpr (FORM == HQ_FORM_TERM_START) {
+                    const VT t = __builtin_nontemporal_load(reinterpret_cast<const VT *>(a.ts + g0));
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                decide_lag<N, FORM, PERN>(a, l[j], n4[j], cv[j], av[j], co[j], chg[j], fb[j]);
-            *reinterpret_cast<i32x4 *>(a.cout + g0) = (i32x4){co[0], co[1], co[2], co[3]};
-        } else {
+                    for (int j = 0; j < VEC; ++j) av[j] = t[j];
+                } else {
+                    // the lane's VEC u16 masks in one aligned load
+                    typedef typename LagVec<VEC>::M MT;
+                    const MT m = __builtin_nontemporal_load(reinterpret_cast<const MT *>(a.mask + g0));
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) av[j] = (int32_t)((m >> (16 * j)) & 0xFFFF);
+                }
+                int nn[VEC];
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) nn[j] = N;
+                if constexpr (PERN) {
+                    typedef typename LagVec<VEC>::NV NT;
+                    const NT x = *reinterpret_cast<const NT *>(a.nv + g0);
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) nn[j] = (x >> (8 * j)) & 0xFF;
+                }
+                VT co;
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    int32_t c;
+                    decide_lag<N, FORM, PERN>(a, l[j], nn[j], ci[j], av[j], c, chg[j], fb[j]);
+                    co[j] = c;
+                }
+                *reinterpret_cast<VT *>(a.cout + g0) = co;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            const uint64_t g = g0 + j;
+            if (!done && g < a.G) {
+                int32_t l[N];
+#pragma unroll
+                for (int s = 0; s < N; ++s) l[s] = a.lag[s * a.stride + g];
+                const int n = PERN ? (int)a.nv[g] : N;
+                const int32_t aux = FORM == HQ_FORM_TERM_START ? a.ts[g] : (int32_t)a.mask[g];
+                int32_t co;
+                decide_lag<N, FORM, PERN>(a, l, n, a.cin[g], aux, co, chg[j], fb[j]);
+                a.cout[g] = co;
+            }
+        }
+        {
+        // lane l owns groups VEC*l .. VEC*l+VEC-1 of the wave's 64*VEC: bitmap word k covers
+        // lanes (64/VEC)*k .. (64/VEC)*(k+1)-1
+        uint64_t bc[VEC], bf[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            bc[j] = __ballot(chg[j]);
+            bf[j] = __ballot(fb[j]);
+        }
+        if (lane < VEC) {
+            const int sh = (64 / VEC) * lane;
+            const uint64_t w = (wbase >> 6) + lane;
+            uint64_t wc = 0, wf = 0;
 #pragma unroll
             for (int j = 0; j < VEC; ++j) {
-                const uint64_t g = g0 + j;
-                if (g < a.G) {
-                    int32_t l[N];
+                wc |= spread_v<VEC>((uint32_t)(bc[j] >> sh)) << j;
+                wf |= spread_v<VEC>((uint32_t)(bf[j] >> sh)) << j;
+            }
+            if (VEC == 1) {
+                wc = bc[0];
+                wf = bf[0];
+            }
+            if (w < a.nwords) {
+                if (a.changed) a.changed[w] = wc;
+                if (a.fallback) a.fallback[w] = wf;
+            }
+        }
+    }
+    }
+}
+
+template <int N, int FORM, int VEC, bool PERN>
+__global__ __launch_bounds__(kCommitBlock) void k_commit_lag(const LagK a) {
+    lag_blocks<N, FORM, VEC, PERN>(a, blockIdx.x, gridDim.x);
+}
+
+// the lag twin of k_commit_fused: uniform-n lag batches of one step in one launch
+struct FusedLagK {
+    LagK b[kMaxFused];
+    uint32_t first[kMaxFused + 1];
+    uint8_t n[kMaxFused];
+    uint32_t count;
+};
+
+template <int FORM>
+__global__ __launch_bounds__(kCommitBlock) void k_commit_lag_fused(const FusedLagK f) {
+    const uint32_t blk = blockIdx.x;
+    uint32_t i = 0;
 #pragma unroll
-                    for (int s = 0; s < N; ++s) l[s] = a.lag[s * a.stride + g];
-                    const int n = PERN ? (int)a.nv[g] : N;
-                    const int32_t aux = FORM == HQ_FORM_TERM_START ? a.ts[g] : (int32_t)a.mask[g];
-                    int32_t co;
-                    decide_lag<N, FORM, PERN>(a, l, n, a.cin[g], aux, co, chg[j], fb[j]);
-                    a.cout[g] = co;
-                }
-            }
-        }
-        if constexpr (VEC == 4) {
-            // lane l owns groups 4l..4l+3 of the wave's 256: word k = lanes 16k..16k+15
-            const uint64_t b0 = __ballot(chg[0]), b1 = __ballot(chg[1]);
-            const uint64_t b2 = __ballot(chg[2]), b3 = __ballot(chg[3]);
-            const uint64_t f0 = __ballot(fb[0]), f1 = __ballot(fb[1]);
-            const uint64_t f2 = __ballot(fb[2]), f3 = __ballot(fb[3]);
-            if (lane < 4) {
-                const int sh = 16 * lane;
-                const uint64_t w = (wbase >> 6) + lane;
-                if (w < a.nwords) {
-                    if (a.changed)
-                        a.changed[w] = spread16x4((uint32_t)(b0 >> sh)) |
-                                       (spread16x4((uint32_t)(b1 >> sh)) << 1) |
-                                       (spread16x4((uint32_t)(b2 >> sh)) << 2) |
-                                       (spread16x4((uint32_t)(b3 >> sh)) << 3);
-                    if (a.fallback)
-                        a.fallback[w] = spread16x4((uint32_t)(f0 >> sh)) |
-                                        (spread16x4((uint32_t)(f1 >> sh)) << 1) |
-                                        (spread16x4((uint32_t)(f2 >> sh)) << 2) |
-                                        (spread16x4((uint32_t)(f3 >> sh)) << 3);
-                }
-            }
-        } else {
-            const uint64_t b0 = __ballot(chg[0]), f0 = __ballot(fb[0]);
-            if (lane == 0) {
-                if (a.changed) a.changed[wbase >> 6] = b0;
-                if (a.fallback) a.fallback[wbase >> 6] = f0;
-            }
-        }
+    for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
+    const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
+    switch (f.n[i]) {
+    case 1: lag_blocks<1, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 2: lag_blocks<2, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 3: lag_blocks<3, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 4: lag_blocks<4, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 5: lag_blocks<5, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 6: lag_blocks<6, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 7: lag_blocks<7, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    default: lag_blocks<8, FORM, kLagVec, false>(f.b[i], b, nb); break;
     }
 }
 
@@ -954,9 +1017,10 @@ int launch_lag_t(hq_ctx *ctx, const LagK &k) {
 }
 
 template <int N>
-int launch_lag_n(hq_ctx *ctx, const LagK &k, int form, bool vec4, bool pern) {
+int launch_lag_n(hq_ctx *ctx, const LagK &k, int form, bool vec, bool pern) {
 #define HQ_LAG_DISPATCH(F)                                                                   \
-    if (vec4) return pern ? launch_lag_t<N, F, 4, true>(ctx, k) : launch_lag_t<N, F, 4, false>(ctx, k); \
+    if (vec) return pern ? launch_lag_t<N, F, kLagVec, true>(ctx, k)                          \
+                         : launch_lag_t<N, F, kLagVec, false>(ctx, k);                        \
     return pern ? launch_lag_t<N, F, 1, true>(ctx, k) : launch_lag_t<N, F, 1, false>(ctx, k);
     if (form == HQ_FORM_TERM_START) {
         HQ_LAG_DISPATCH(HQ_FORM_TERM_START)
@@ -987,11 +1051,7 @@ int validate_lag(hq_ctx *ctx, const hq_commit_lag_args *a) {
     return HQ_OK;
 }
 
-}  // namespace
-
-extern "C" int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *a) {
-    int rc = validate_lag(ctx, a);
-    if (rc || a->G == 0) return rc;
+LagK lag_k(const hq_commit_lag_args *a) {
     LagK k;
     k.G = a->G;
     k.stride = a->lag_stride;
@@ -1006,12 +1066,25 @@ extern "C" int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *a) {
     k.mask = a->lag_mask;
     k.changed = a->changed;
     k.fallback = a->fallback;
-    const bool aux_ok = a->form == HQ_FORM_TERM_START
-                            ? hq::aligned16(a->ts_lag)
-                            : (reinterpret_cast<uintptr_t>(a->lag_mask) & 7) == 0;
-    const bool vec4 = hq::aligned16(a->lag) && (a->lag_stride % 4 == 0) &&
-                      hq::aligned16(a->cin_lag) && hq::aligned16(a->cout_lag) && aux_ok &&
-                      (!a->n_voting || (reinterpret_cast<uintptr_t>(a->n_voting) & 3) == 0);
+    return k;
+}
+
+// every column can be read kLagVec groups per lane with aligned vector loads
+bool lag_vec(const hq_commit_lag_args *a) {
+    const uintptr_t al = 4 * kLagVec;   // bytes of one lane's int32 load
+    auto ok = [&](const void *p, uintptr_t b) { return (reinterpret_cast<uintptr_t>(p) % b) == 0; };
+    const bool aux_ok = a->form == HQ_FORM_TERM_START ? ok(a->ts_lag, al) : ok(a->lag_mask, al / 2);
+    return ok(a->lag, al) && (a->lag_stride % kLagVec == 0) && ok(a->cin_lag, al) &&
+           ok(a->cout_lag, al) && aux_ok && (!a->n_voting || ok(a->n_voting, al / 4));
+}
+
+}  // namespace
+
+extern "C" int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *a) {
+    int rc = validate_lag(ctx, a);
+    if (rc || a->G == 0) return rc;
+    const LagK k = lag_k(a);
+    const bool vec4 = lag_vec(a);
     const bool pern = a->n_voting != nullptr;
     switch (a->n_max) {
     case 1: return launch_lag_n<1>(ctx, k, a->form, vec4, pern);
@@ -1023,6 +1096,46 @@ extern "C" int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *a) {
     case 7: return launch_lag_n<7>(ctx, k, a->form, vec4, pern);
     default: return launch_lag_n<8>(ctx, k, a->form, vec4, pern);
     }
+}
+
+extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *args,
+                                       uint32_t count) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count && !args) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag_fused_dev: args is NULL");
+    for (uint32_t i = 0; i < count; ++i) {
+        int rc = validate_lag(ctx, args + i);
+        if (rc) return rc;
+    }
+    bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
+    for (uint32_t i = 0; fusable && i < count; ++i)
+        fusable = args[i].G > 0 && !args[i].n_voting && lag_vec(args + i) &&
+                  args[i].form == args[0].form;
+    if (!fusable) {
+        for (uint32_t i = 0; i < count; ++i) {
+            int rc = hq_commit_lag_dev(ctx, args + i);
+            if (rc) return rc;
+        }
+        return HQ_OK;
+    }
+    FusedLagK f{};
+    f.count = count;
+    uint64_t blocks = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        f.b[i] = lag_k(args + i);
+        f.n[i] = (uint8_t)args[i].n_max;
+        f.first[i] = (uint32_t)blocks;
+        blocks += grid_for((args[i].G + kLagVec - 1) / kLagVec, kCommitBlock, kMaxBlocks / 2);
+    }
+    for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    if (args[0].form == HQ_FORM_TERM_START)
+        hipLaunchKernelGGL((k_commit_lag_fused<HQ_FORM_TERM_START>), dim3(blocks),
+                           dim3(kCommitBlock), 0, ctx->stream, f);
+    else
+        hipLaunchKernelGGL((k_commit_lag_fused<HQ_FORM_TERM_MASK>), dim3(blocks),
+                           dim3(kCommitBlock), 0, ctx->stream, f);
+    return hq::post_launch(ctx, "k_commit_lag_fused");
 }
 
 extern "C" int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count) {

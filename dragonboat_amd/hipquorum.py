@@ -15,7 +15,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libhipquorum.so")
+# HQ_LIB_PATH: an alternative build of the same library (tuning experiments, tools/)
+LIB_PATH = os.environ.get("HQ_LIB_PATH") or os.path.join(_HERE, "lib", "libhipquorum.so")
 
 HQ_OK = 0
 HQ_E_INVAL = -1
@@ -186,6 +187,7 @@ SIGNATURES = {
     "hq_commit_many_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
     "hq_commit_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
     "hq_commit_lag_dev": (ctypes.c_int, [_vp, ctypes.POINTER(LagArgs)]),
+    "hq_commit_lag_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(LagArgs), ctypes.c_uint32]),
     "hq_pack_lags": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp,
                                     _vp, _vp, _vp, ctypes.POINTER(LagArgs)]),
     "hq_unpack_lags": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
@@ -394,6 +396,10 @@ class Context:
     def commit_lag_dev(self, args: LagArgs) -> None:
         self._check(lib.hq_commit_lag_dev(self.h, ctypes.byref(args)))
 
+    def commit_lag_fused_dev(self, batch) -> None:
+        """batch: a ctypes array of LagArgs (``lag_batch_array``)."""
+        self._check(lib.hq_commit_lag_fused_dev(self.h, batch, len(batch)))
+
     def commit_host(self, args: CommitArgs) -> None:
         self._check(lib.hq_commit(self.h, ctypes.byref(args)))
 
@@ -572,6 +578,13 @@ def commit_batch_array(args_list) -> ctypes.Array:
     return arr
 
 
+def lag_batch_array(args_list) -> ctypes.Array:
+    arr = (LagArgs * len(args_list))()
+    for i, a in enumerate(args_list):
+        arr[i] = a
+    return arr
+
+
 def words64(G: int) -> int:
     return (G + 63) // 64
 
@@ -670,12 +683,14 @@ class LagBuffers:
     changed: DeviceArray
     fallback: DeviceArray
     last_index: Optional[DeviceArray] = None
+    stride: int = 0           # lag row stride (G rounded up to 4: 16-byte aligned rows)
 
     def args(self) -> LagArgs:
         ts = self.aux if self.form == HQ_FORM_TERM_START else None
         lm = self.aux if self.form == HQ_FORM_TERM_MASK else None
         return lag_args(self.G, self.n_max, self.form, self.ring_len, self.lag, self.cin_lag,
-                        self.cout_lag, ts, lm, None, self.changed, self.fallback)
+                        self.cout_lag, ts, lm, None, self.changed, self.fallback,
+                        lag_stride=self.stride or self.G)
 
     def arrays(self):
         return [x for x in (self.lag, self.cin_lag, self.cout_lag, self.aux, self.changed,
@@ -684,9 +699,10 @@ class LagBuffers:
 
 def alloc_commit_lag(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
                      with_last: bool = False) -> LagBuffers:
+    stride = (G + 3) & ~3
     return LagBuffers(
-        G=G, n_max=n_max, form=form, ring_len=ring_len,
-        lag=ctx.empty(G * n_max, np.int32), cin_lag=ctx.empty(G, np.int32),
+        G=G, n_max=n_max, form=form, ring_len=ring_len, stride=stride,
+        lag=ctx.empty(stride * n_max, np.int32), cin_lag=ctx.empty(G, np.int32),
         cout_lag=ctx.empty(G, np.int32),
         aux=ctx.empty(G, np.int32 if form == HQ_FORM_TERM_START else np.uint16),
         changed=ctx.empty(words64(G), np.uint64), fallback=ctx.empty(words64(G), np.uint64),

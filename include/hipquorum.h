@@ -221,6 +221,9 @@ typedef struct hq_commit_lag_args {
 } hq_commit_lag_args;
 
 int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *args);
+/* hq_commit_fused_dev for the lag layout: 2..8 uniform-n batches of one form, aligned columns,
+ * in one launch; otherwise one launch per batch, same results. */
+int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *args, uint32_t count);
 
 /* Host packer: the lag columns of *out (lag rows at out->lag_stride, cin_lag and ts_lag or
  * lag_mask per out->form) from u64 columns laid out as in hq_commit_args (match rows at

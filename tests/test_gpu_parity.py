@@ -676,7 +676,8 @@ def test_synth_commit_lag_matches_host_packer(gpu_ctx, hq, kw):
         b = hq.alloc_commit_lag(gpu_ctx, G, kw["n_max"], form, 16, with_last=True)
         gpu_ctx.synth_commit_lag_dev(spec, b.args(), b.last_index)
         gpu_ctx.sync()
-        np.testing.assert_array_equal(gpu_ctx.download(b.lag), lag)
+        dl = gpu_ctx.download(b.lag).reshape(kw["n_max"], b.stride)[:, :G].reshape(-1)
+        np.testing.assert_array_equal(dl, lag)
         np.testing.assert_array_equal(gpu_ctx.download(b.cin_lag), cin)
         np.testing.assert_array_equal(gpu_ctx.download(b.aux), aux)
         np.testing.assert_array_equal(gpu_ctx.download(b.last_index), host.last_index)
@@ -701,3 +702,35 @@ def test_commit_lag_full_size(gpu_ctx, hq, n_max, form):
     np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
     assert popcount(gpu_ctx.download(b.fallback)) == 0
     hq.free_commit(gpu_ctx, b)
+
+
+@pytest.mark.parametrize("form", [0, 2])
+@pytest.mark.parametrize("sizes", [[(3, 100_001), (5, 99_999), (7, 100_003)],
+                                   [(3, 1), (5, 64), (7, 65), (1, 129), (8, 3000)]])
+def test_commit_lag_fused_buckets(gpu_ctx, hq, form, sizes):
+    """One launch over several voter-count buckets in the lag layout (device generator) equals
+    the oracle's u64 decision on each bucket."""
+    bufs, want = [], []
+    for k, (n, G) in enumerate(sizes):
+        spec = qref.spec(SEED + 60 + k, G, n, parity_extras=True)
+        b = hq.alloc_commit_lag(gpu_ctx, G, n, form, 16, with_last=True)
+        gpu_ctx.synth_commit_lag_dev(hq.synth_spec(SEED + 60 + k, G, n, parity_extras=True),
+                                     b.args(), b.last_index)
+        inp = qref.CommitInputs(spec)
+        bufs.append((b, inp))
+        want.append(inp.run(form, False, nthreads=8)[:3])
+    gpu_ctx.sync()
+    gpu_ctx.timing_reset()
+    gpu_ctx.timing(True)
+    gpu_ctx.commit_lag_fused_dev(hq.lag_batch_array([b.args() for b, _ in bufs]))
+    gpu_ctx.sync()
+    gpu_ctx.timing(False)
+    assert gpu_ctx.timing_read()[1] == 1
+    for (b, inp), (wo, wc, wf) in zip(bufs, want):
+        fb = gpu_ctx.download(b.fallback)
+        com = inp.committed_in.copy()
+        hq.unpack_lags(inp.last_index, gpu_ctx.download(b.cout_lag), com, fb)
+        np.testing.assert_array_equal(com, wo)
+        np.testing.assert_array_equal(gpu_ctx.download(b.changed), wc)
+        np.testing.assert_array_equal(fb, wf)
+        hq.free_commit(gpu_ctx, b)
