@@ -278,6 +278,102 @@ def run_gpu(w, steps, warmup, d: Dist):
     return res
 
 
+def _timed(ctx, d, run, steps, warmup):
+    """Warm up, then time `steps` calls of run(i) with a barrier + sync on both sides; returns
+    (max-over-ranks seconds, average launch seconds from the HIP-event region)."""
+    for i in range(max(1, warmup)):
+        run(i)
+    ctx.sync()
+    d.sync_device()
+    d.barrier()
+    ctx.timing_reset()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run(i)
+    ctx.sync()
+    d.sync_device()
+    d.barrier()
+    t1 = time.perf_counter()
+    ctx.timing(False)
+    ms, launches = ctx.timing_read()
+    return d.max(t1 - t0), ms / 1e3 / max(1, launches), launches
+
+
+def run_kernel_leg(name, steps, warmup, d: Dist):
+    """The remaining decision kernels, each on its own BASELINE-shaped batch, device-resident and
+    rotated past the Infinity Cache like the commit legs:
+      rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
+      cq:  CheckQuorum (k_bits CHECKQ), 16M groups x 7 voters, active flags reset in place
+      ing: match-delta ingest (k_ingest_match), 4M ReplicateResp deltas into a 4M x 3 table"""
+    from dragonboat_amd import hipquorum as hq
+
+    ctx = hq.Context(d.device)
+    r = np.random.default_rng(SEED_BASE + d.rank)
+    if name == "rim":
+        G, K, n = 2 << 20, 4, 7
+        # first-ack ordinals: ~70 % of (ctx, voter) pairs acked, in arrival order 1..K*n
+        ordn = r.integers(1, K * n + 1, (K, n, G)).astype(np.uint16)
+        ordn[r.random((K, n, G)) < 0.3] = 0xFFFF
+        idx = (np.uint64(1 << 30) + np.arange(K, dtype=np.uint64)[:, None] * np.uint64(3)
+               + r.integers(0, 1 << 20, G, dtype=np.uint64)[None, :])
+        per = G * (2 * K * n + 8 * K + 8 * K + 2)      # ordinals + ctx index in; released out
+        nsets = max(4, int(np.ceil(ROTATE_BYTES / per)))
+        sets = [(ctx.upload(ordn.reshape(-1)), ctx.upload(idx.reshape(-1)),
+                 ctx.empty(K * G, np.uint64), ctx.empty(G, np.uint8), ctx.empty(G, np.uint8))
+                for _ in range(nsets)]
+
+        def run(i):
+            o, x, rel, cnt, bend = sets[i % nsets]
+            ctx.readindex_multi_dev(G, K, n, o, x, None, None, n, rel, cnt, batch_end=bend)
+        desc = (f"rim: general multi-ctx ReadIndex release (suffix-min), {G} groups x {K} pending "
+                f"ctxs x {n} voters")
+        units, unit = G, "releases/s"
+    elif name == "cq":
+        G, n = 16 << 20, 7
+        per = G * 2 + G // 8
+        nsets = max(4, int(np.ceil(ROTATE_BYTES / per)))
+        sets = []
+        for k in range(nsets):
+            act = ctx.empty(G, np.uint8)
+            ctx.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 3 + (k << 40), G, n), act)
+            sets.append((act, ctx.empty(hq.words64(G), np.uint64)))
+        ctx.sync()
+
+        def run(i):
+            act, hqb = sets[i % nsets]
+            ctx.check_quorum_dev(G, act, None, n, 0, hqb)
+        desc = f"cq: CheckQuorum (leaderHasQuorum + setNotActive), {G} groups x {n} voters"
+        units, unit = G, "decisions/s"
+    else:   # ing
+        G, n, U = 4 << 20, 3, 4 << 20
+        per = U * 16 + U * 16          # the update + the 8-byte read-modify-write of its match
+        nsets = max(4, int(np.ceil(ROTATE_BYTES / (U * 16))))
+        table = ctx.upload(np.full(n * G, 1 << 30, np.uint64))
+        ups = []
+        for k in range(nsets):
+            g = r.integers(0, G, U, dtype=np.uint64)
+            s = r.integers(1, n, U, dtype=np.uint64)
+            u = np.stack([(g << np.uint64(8)) | s,
+                          np.uint64(1 << 30) + np.uint64(k) + r.integers(0, 64, U, dtype=np.uint64)],
+                         axis=1)
+            ups.append(ctx.upload(u.reshape(-1)))
+
+        def run(i):
+            ctx.ingest_match_dev(ups[i % nsets], U, table, G, G, n)
+        desc = (f"ing: ReplicateResp match-delta ingest (remote.tryUpdate as 64-bit atomic max), "
+                f"{U} deltas into a {G} x {n} device table")
+        units, unit = U, "updates/s"
+    elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
+    ctx.close()
+    return {
+        "workload": desc, "value": d.sum(float(units * steps)) / elapsed, "unit": unit,
+        "kernel_avg_us": avg * 1e6, "launches_per_step": launches / max(1, steps),
+        "roofline_achieved_gbs": per / avg / 1e9, "roofline_frac": per / avg / 1e9 / HBM_PEAK_GBS,
+        "algorithmic_bytes_per_launch": per,
+    }
+
+
 def run_concurrent(w, steps, warmup, d: Dist, W=2):
     """W step workers stepping the same workload concurrently, each with its own hq_ctx (= its
     own HIP stream; dragonboat runs one goroutine per step worker, execengine.go:675-690, and
@@ -607,7 +703,8 @@ def main():
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5l,c5r,c5r32,w2,e2e,step",
+    ap.add_argument("--extra",
+                    default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5l,c5r,c5r32,rim,cq,ing,w2,e2e,step",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -620,13 +717,16 @@ def main():
     r = run_gpu(w, args.steps, args.warmup, d)
     extras = []
     e2e = step_leg = None
-    conc = []
+    conc, kern = [], []
     for name in [x for x in args.extra.split(",") if x and x != args.workload]:
         if name == "e2e":
             e2e = run_e2e(max(20, args.steps // 20), 3, d)
             continue
         if name == "step":
             step_leg = run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu)
+            continue
+        if name in ("rim", "cq", "ing"):
+            kern.append(run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d))
             continue
         if name.startswith("w") and name[1:].isdigit():
             conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))
@@ -682,7 +782,7 @@ def main():
                     "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
-            ] + conc + ([e2e] if e2e else []) + ([step_leg] if step_leg else []),
+            ] + kern + conc + ([e2e] if e2e else []) + ([step_leg] if step_leg else []),
         }
         print(json.dumps(line), flush=True)
     d.close()
