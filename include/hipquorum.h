@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 2
+#define HQ_ABI_VERSION 3
 
 /* status codes */
 #define HQ_OK          0

@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == 2
+    assert hq.lib.hq_abi_version() == 3
 
 
 LAYOUT_C = r"""
@@ -45,7 +45,13 @@ int main(void) {
   F(hq_commit_args, n_voting) F(hq_commit_args, committed_in) F(hq_commit_args, committed_out)
   F(hq_commit_args, last_index) F(hq_commit_args, term_start) F(hq_commit_args, term)
   F(hq_commit_args, ring) F(hq_commit_args, changed) F(hq_commit_args, fallback)
-  F(hq_commit_args, term_mask)
+  F(hq_commit_args, term_mask) F(hq_commit_args, ring32)
+  printf("hq_commit_lag_args %zu\n", sizeof(hq_commit_lag_args));
+  F(hq_commit_lag_args, G) F(hq_commit_lag_args, n_max) F(hq_commit_lag_args, form)
+  F(hq_commit_lag_args, ring_len) F(hq_commit_lag_args, lag_stride) F(hq_commit_lag_args, lag)
+  F(hq_commit_lag_args, n_voting) F(hq_commit_lag_args, cin_lag) F(hq_commit_lag_args, cout_lag)
+  F(hq_commit_lag_args, ts_lag) F(hq_commit_lag_args, lag_mask) F(hq_commit_lag_args, changed)
+  F(hq_commit_lag_args, fallback)
   F(hq_synth_spec, seed) F(hq_synth_spec, G) F(hq_synth_spec, cid_base)
   F(hq_synth_spec, cid_stride) F(hq_synth_spec, n_max) F(hq_synth_spec, mixed_n)
   F(hq_synth_spec, ring_len) F(hq_synth_spec, parity_extras)
@@ -75,6 +81,7 @@ def test_struct_layout_matches_c(hq, tmp_path):
     c = dict(l.rsplit(" ", 1) for l in lines if l)
     assert int(c["hq_commit_args"]) == ctypes.sizeof(hq.CommitArgs)
     assert int(c["hq_synth_spec"]) == ctypes.sizeof(hq.SynthSpec)
+    assert int(c["hq_commit_lag_args"]) == ctypes.sizeof(hq.LagArgs)
     dtypes = {"hq_member": hq.MEMBER_DTYPE, "hq_group_view": hq.GROUP_DTYPE,
               "hq_msg": hq.MSG_DTYPE}
     for name, dt in dtypes.items():
@@ -86,7 +93,8 @@ def test_struct_layout_matches_c(hq, tmp_path):
             if t in dtypes:
                 assert dtypes[t].fields[m][1] == int(val), key
                 continue
-            cls = hq.CommitArgs if t == "hq_commit_args" else hq.SynthSpec
+            cls = {"hq_commit_args": hq.CommitArgs, "hq_synth_spec": hq.SynthSpec,
+                   "hq_commit_lag_args": hq.LagArgs}[t]
             assert getattr(cls, m).offset == int(val), key
 
 
@@ -96,6 +104,10 @@ def test_null_context_is_invalid(hq):
     assert hq.lib.hq_sync(None) == hq.HQ_E_INVAL
     assert hq.lib.hq_readindex_dev(None, 0, None, None, 3, None, None) == hq.HQ_E_INVAL
     assert hq.lib.hq_vote_dev(None, 0, None, None, None, 3, None, None) == hq.HQ_E_INVAL
+    assert hq.lib.hq_commit_lag_dev(None, ctypes.byref(hq.LagArgs())) == hq.HQ_E_INVAL
+    assert hq.lib.hq_commit_fused_dev(None, None, 0) == hq.HQ_E_INVAL
+    assert hq.lib.hq_commit_lag_fused_dev(None, None, 0) == hq.HQ_E_INVAL
+    assert hq.lib.hq_wait_for(None, None) == hq.HQ_E_INVAL
     hq.lib.hq_close(None)  # no-op
     assert hq.lib.hq_last_error(None) is not None
 
