@@ -134,6 +134,17 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, xs) -> list:
+        """Every rank's list of floats, in rank order (all_gather; RCCL when each rank has its
+        own GPU)."""
+        if self.torch is None:
+            return [list(xs)]
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor(list(xs), dtype=self.torch.float64, device=dev)
+        out = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [o.cpu().tolist() for o in out]
+
     def sum(self, x: float) -> float:
         if self.torch is None:
             return x
@@ -265,14 +276,25 @@ def run_gpu(w, steps, warmup, d: Dist):
     t1 = time.perf_counter()
     ctx.timing(False)
     kernel_ms, launches = ctx.timing_read()
-    elapsed = d.max(t1 - t0)
+    local = t1 - t0
+    elapsed = d.max(local)
     avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+    # per-GPU numbers (SURVEY.md §8e reporting), gathered off the timed region
+    per_gpu = d.gather([groups_per_step(w) * steps * decisions_per_group(w) / local,
+                        avg_kernel_s * 1e6])
+    set0 = None
+    if w["kind"] == "commit" and not w["mixed"]:
+        # the decisions of batch 0 (its output column is rewritten identically every rotation),
+        # checked against the oracle by the cpu_baseline leg
+        b = sets[0][0]
+        set0 = (ctx.download(b.committed_out), ctx.download(b.changed))
     total_groups = d.sum(float(groups_per_step(w) * steps))
     res = dict(
         elapsed=elapsed, launches=launches, avg_kernel_s=avg_kernel_s,
         decisions=total_groups * decisions_per_group(w), nsets=len(sets),
         bytes_per_launch=per_set * steps / max(1, launches), steps=steps,
         achieved_gbs=per_set * steps / (kernel_ms / 1e3) / 1e9,
+        per_gpu=per_gpu, set0=set0,
     )
     ctx.close()
     return res
@@ -639,8 +661,10 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
 
 
 # ----------------------------------------------------------------------------- CPU leg --------
-def cpu_baseline(w, budget_s=8.0):
-    """The oracle (C restatement of the reference path) on a bounded sample of the workload."""
+def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
+    """The oracle (C restatement of the reference path) on a bounded sample of the workload.
+    gpu_set0: the GPU's (committed', changed) of batch 0 of the timed run, which is exactly this
+    sample's input; the oracle's answer for it is compared bit for bit (full-size parity)."""
     from oracle import qref
 
     host_threads = min(16, os.cpu_count() or 1)
@@ -668,6 +692,12 @@ def cpu_baseline(w, budget_s=8.0):
                 break
         out[nt] = (passes * G * decisions_per_group(w) / dt, passes, dt)
     rate, passes, dt = out[host_threads]
+    parity = None
+    if gpu_set0 is not None and w["kind"] == "commit":
+        want_out, want_chg, _, rc = inp.run(w["form"], False, nthreads=host_threads)
+        parity = {"groups": G, "oracle_rc": rc,
+                  "committed_equal": bool(np.array_equal(gpu_set0[0], want_out)),
+                  "changed_equal": bool(np.array_equal(gpu_set0[1], want_chg))}
     # BASELINE config C1: the reference's own CPU case, one group x 3 voters, tryCommit per step
     T = 4 << 20
     match, last = qref.c1_stream(SEED_BASE, T, 1000, 1005)
@@ -682,6 +712,7 @@ def cpu_baseline(w, budget_s=8.0):
         "single_thread_value": out[1][0],
         "c1_single_group_ns_per_trycommit": c1_s / T * 1e9,
         "c1_sample": f"BASELINE config C1: 1 group x 3 voters, {T} sequential tryCommit steps",
+        "parity_full_size": parity,
     }
 
 
@@ -736,7 +767,7 @@ def main():
         extras.append((name, we, re_))
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(w)
+        cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
     if d.rank == 0:
         achieved = r["achieved_gbs"]
         line = {
@@ -771,6 +802,8 @@ def main():
                 "algorithmic_bytes_per_launch": r["bytes_per_launch"],
                 "measured_copy_ceiling_gbs": HBM_MEASURED_COPY_GBS,
             },
+            "per_gpu": [{"rank": i, "decisions_per_s": v, "kernel_avg_us": k}
+                        for i, (v, k) in enumerate(r["per_gpu"])],
             "cpu_baseline": cpu,
             "extra": [
                 {

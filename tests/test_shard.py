@@ -66,6 +66,8 @@ def _worker(rank, world, port, G, q):
     d.barrier()
     total = d.sum(float(np.unpackbits(chg.view(np.uint8)).sum()))
     slowest = d.max(float(rank + 1))
+    gathered = d.gather([float(rank), float(len(out))])   # per-GPU numbers, rank order
+    assert gathered == [[float(r), float(G)] for r in range(world)]
     q.put((rank, list(rng.cids()), out.tolist(), total, slowest))
     d.close()
 
