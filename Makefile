@@ -32,7 +32,12 @@ tools/lib_vec2/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(
 	@mkdir -p tools/lib_vec2
 	$(HIPCC) $(HIPFLAGS) -DHQ_LAG_VEC=2 -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
 
-variants: tools/lib_vec2/libhipquorum.so
+# tuning variant: every commit kernel with 512-thread blocks (the pre-1024 geometry)
+tools/lib_b512/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(DEPS)
+	@mkdir -p tools/lib_b512
+	$(HIPCC) $(HIPFLAGS) -DHQ_COMMIT_BLOCK_BIG=512 -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
+
+variants: tools/lib_vec2/libhipquorum.so tools/lib_b512/libhipquorum.so
 
 clean:
 	rm -rf $(LIBDIR) oracle/build

@@ -13,6 +13,22 @@ constexpr int kBlock = 256;           // 4 waves of 64
 // The commit stream runs 512-thread blocks: ~5 % shorter than 256 on the 1M x 3 launch under
 // rocprofv3 (11.7 vs 12.4 us, tools/kexp2.hip); 4 groups per lane was slower.
 constexpr int kCommitBlock = 512;
+// Kernels that fit 64 VGPRs (occupancy 8) run 1024-thread blocks: 10.57 vs 11.1 us per 1M x 3
+// launch (tools/kexp3.hip: fewer workgroups to dispatch for the same waves); the others keep
+// 512 so that two or more blocks still fit a CU. HQ_COMMIT_BLOCK_BIG=512 restores one size.
+#ifndef HQ_COMMIT_BLOCK_BIG
+#define HQ_COMMIT_BLOCK_BIG 1024
+#endif
+template <int N, int FORM, bool PERN>
+constexpr int commit_blk() {
+    return !PERN && (N <= 4 || (N == 5 && (FORM == HQ_FORM_TERM_START || FORM == HQ_FORM_TERM_MASK)))
+               ? HQ_COMMIT_BLOCK_BIG
+               : kCommitBlock;
+}
+template <int N, bool PERN>
+constexpr int lag_blk() {
+    return !PERN && N <= 4 ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
+}
 constexpr int kMaxBlocks = 256 * 16;  // grid-stride beyond 16 workgroups per CU
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -158,11 +174,11 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
 // VEC = groups per lane (2: 16-byte loads of every SoA column; 1: 8-byte loads). The body of
 // one workgroup `blk` of `nblk` working on batch `a` (k_commit: the grid; k_commit_fused: the
 // workgroups one batch of the launch owns).
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, int BLK>
 __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = blk * (kCommitBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t step = nblk * kCommitBlock * VEC;
+    const uint64_t wave = blk * (BLK / 64) + (threadIdx.x >> 6);
+    const uint64_t step = nblk * BLK * VEC;
     const uint64_t *aux_col = (FORM == HQ_FORM_TERM_START) ? a.tstart : a.term;
     // aux of group g: the u64 column (forms 0, 1) or the u16 term mask (form 2)
     auto aux1 = [&](uint64_t g) -> uint64_t {
@@ -253,7 +269,12 @@ __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, ui
 
 template <int N, int FORM, int VEC, bool PERN>
 __global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
-    commit_blocks<N, FORM, VEC, PERN>(a, blockIdx.x, gridDim.x);
+    commit_blocks<N, FORM, VEC, PERN, kCommitBlock>(a, blockIdx.x, gridDim.x);
+}
+// the 1024-thread twin: two blocks per CU need occupancy 8 (<= 64 VGPRs), so it is asked for
+template <int N, int FORM, int VEC, bool PERN>
+__global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_big(const CommitK a) {
+    commit_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG>(a, blockIdx.x, gridDim.x);
 }
 
 // Several uniform-n batches of one step in ONE launch (a step worker's voter-count buckets):
@@ -268,22 +289,22 @@ struct FusedK {
     uint32_t count;
 };
 
-template <int FORM>
-__global__ __launch_bounds__(kCommitBlock) void k_commit_fused(const FusedK f) {
+template <int FORM, int BLK>
+__global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_fused(const FusedK f) {
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
 #pragma unroll
     for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
     const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
     switch (f.n[i]) {
-    case 1: commit_blocks<1, FORM, 2, false>(f.b[i], b, nb); break;
-    case 2: commit_blocks<2, FORM, 2, false>(f.b[i], b, nb); break;
-    case 3: commit_blocks<3, FORM, 2, false>(f.b[i], b, nb); break;
-    case 4: commit_blocks<4, FORM, 2, false>(f.b[i], b, nb); break;
-    case 5: commit_blocks<5, FORM, 2, false>(f.b[i], b, nb); break;
-    case 6: commit_blocks<6, FORM, 2, false>(f.b[i], b, nb); break;
-    case 7: commit_blocks<7, FORM, 2, false>(f.b[i], b, nb); break;
-    default: commit_blocks<8, FORM, 2, false>(f.b[i], b, nb); break;
+    case 1: commit_blocks<1, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 2: commit_blocks<2, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 3: commit_blocks<3, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 4: commit_blocks<4, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 5: commit_blocks<5, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 6: commit_blocks<6, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 7: commit_blocks<7, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    default: commit_blocks<8, FORM, 2, false, BLK>(f.b[i], b, nb); break;
     }
 }
 
@@ -399,11 +420,11 @@ __device__ __forceinline__ uint64_t spread_v(uint32_t x) {
 
 // VEC = 4 / 2: lane owns groups g0..g0+VEC-1 (16- / 8-byte loads of every column); VEC = 1: one
 // group, 4-byte loads. The body of workgroup `blk` of `nblk` on batch `a`.
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, int BLK>
 __device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t nblk) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = blk * (kCommitBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t step = nblk * kCommitBlock * VEC;
+    const uint64_t wave = blk * (BLK / 64) + (threadIdx.x >> 6);
+    const uint64_t step = nblk * BLK * VEC;
     for (uint64_t wbase = wave * 64 * VEC; wbase < a.G; wbase += step) {
         const uint64_t g0 = wbase + (uint64_t)lane * VEC;
         bool chg[VEC], fb[VEC];
@@ -501,7 +522,11 @@ __device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t
 
 template <int N, int FORM, int VEC, bool PERN>
 __global__ __launch_bounds__(kCommitBlock) void k_commit_lag(const LagK a) {
-    lag_blocks<N, FORM, VEC, PERN>(a, blockIdx.x, gridDim.x);
+    lag_blocks<N, FORM, VEC, PERN, kCommitBlock>(a, blockIdx.x, gridDim.x);
+}
+template <int N, int FORM, int VEC, bool PERN>
+__global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_lag_big(const LagK a) {
+    lag_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG>(a, blockIdx.x, gridDim.x);
 }
 
 // the lag twin of k_commit_fused: uniform-n lag batches of one step in one launch
@@ -512,22 +537,22 @@ struct FusedLagK {
     uint32_t count;
 };
 
-template <int FORM>
-__global__ __launch_bounds__(kCommitBlock) void k_commit_lag_fused(const FusedLagK f) {
+template <int FORM, int BLK>
+__global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_lag_fused(const FusedLagK f) {
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
 #pragma unroll
     for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
     const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
     switch (f.n[i]) {
-    case 1: lag_blocks<1, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    case 2: lag_blocks<2, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    case 3: lag_blocks<3, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    case 4: lag_blocks<4, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    case 5: lag_blocks<5, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    case 6: lag_blocks<6, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    case 7: lag_blocks<7, FORM, kLagVec, false>(f.b[i], b, nb); break;
-    default: lag_blocks<8, FORM, kLagVec, false>(f.b[i], b, nb); break;
+    case 1: lag_blocks<1, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 2: lag_blocks<2, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 3: lag_blocks<3, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 4: lag_blocks<4, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 5: lag_blocks<5, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 6: lag_blocks<6, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 7: lag_blocks<7, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    default: lag_blocks<8, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
     }
 }
 
@@ -847,11 +872,15 @@ unsigned grid_for(uint64_t lanes_needed, int block = kBlock, uint64_t max_blocks
 
 template <int N, int FORM, int VEC, bool PERN>
 int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
-    const unsigned grid = grid_for((k.G + VEC - 1) / VEC, kCommitBlock, kMaxBlocks / 2);
+    constexpr int B = commit_blk<N, FORM, PERN>();
+    const unsigned grid = grid_for((k.G + VEC - 1) / VEC, B, kMaxBlocks * 256 / B);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN>), dim3(grid), dim3(kCommitBlock), 0,
-                       ctx->stream, k);
+    if constexpr (B == kCommitBlock)
+        hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0, ctx->stream, k);
+    else
+        hipLaunchKernelGGL((k_commit_big<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0,
+                           ctx->stream, k);
     return hq::post_launch(ctx, "k_commit");
 }
 
@@ -972,35 +1001,45 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     if (!fusable) return hq_commit_many_dev(ctx, args, count);
     FusedK f{};
     f.count = count;
+    // one block size for the launch: the big one only if every batch's kernel body fits it
+    bool big = true;
+    // (the fused kernel's bodies fit 64 VGPRs without spilling for these two forms only)
+    for (uint32_t i = 0; i < count; ++i)
+        big &= args[i].n_max <= 5 &&
+               (args[i].form == HQ_FORM_TERM_START || args[i].form == HQ_FORM_TERM_MASK);
+    const int B = big ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
     uint64_t blocks = 0;
     for (uint32_t i = 0; i < count; ++i) {
         f.b[i] = commit_k(args + i);
         f.n[i] = (uint8_t)args[i].n_max;
         f.first[i] = (uint32_t)blocks;
-        // the same workgroups per batch as its own launch would get (grid-stride beyond that)
-        blocks += grid_for((args[i].G + 1) / 2, kCommitBlock, kMaxBlocks / 2);
+        // the same lanes per batch as its own launch would get (grid-stride beyond that)
+        blocks += grid_for((args[i].G + 1) / 2, B, (uint64_t)kMaxBlocks * 256 / B);
     }
     for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
+#define HQ_FUSED(F, BLK)                                                                       \
+    hipLaunchKernelGGL((k_commit_fused<F, BLK>), dim3(blocks), dim3(BLK), 0, ctx->stream, f);
     switch (args[0].form) {
     case HQ_FORM_TERM_START:
-        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_START>), dim3(blocks), dim3(kCommitBlock),
-                           0, ctx->stream, f);
+        if (big) {
+            HQ_FUSED(HQ_FORM_TERM_START, HQ_COMMIT_BLOCK_BIG)
+        } else {
+            HQ_FUSED(HQ_FORM_TERM_START, kCommitBlock)
+        }
         break;
     case HQ_FORM_TERM_MASK:
-        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_MASK>), dim3(blocks), dim3(kCommitBlock),
-                           0, ctx->stream, f);
+        if (big) {
+            HQ_FUSED(HQ_FORM_TERM_MASK, HQ_COMMIT_BLOCK_BIG)
+        } else {
+            HQ_FUSED(HQ_FORM_TERM_MASK, kCommitBlock)
+        }
         break;
-    case HQ_FORM_TERM_RING32:
-        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_RING32>), dim3(blocks),
-                           dim3(kCommitBlock), 0, ctx->stream, f);
-        break;
-    default:
-        hipLaunchKernelGGL((k_commit_fused<HQ_FORM_TERM_RING>), dim3(blocks), dim3(kCommitBlock),
-                           0, ctx->stream, f);
-        break;
+    case HQ_FORM_TERM_RING32: HQ_FUSED(HQ_FORM_TERM_RING32, kCommitBlock) break;
+    default: HQ_FUSED(HQ_FORM_TERM_RING, kCommitBlock) break;
     }
+#undef HQ_FUSED
     return hq::post_launch(ctx, "k_commit_fused");
 }
 
@@ -1008,11 +1047,16 @@ namespace {
 
 template <int N, int FORM, int VEC, bool PERN>
 int launch_lag_t(hq_ctx *ctx, const LagK &k) {
-    const unsigned grid = grid_for((k.G + VEC - 1) / VEC, kCommitBlock, kMaxBlocks / 2);
+    constexpr int B = lag_blk<N, PERN>();
+    const unsigned grid = grid_for((k.G + VEC - 1) / VEC, B, kMaxBlocks * 256 / B);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_commit_lag<N, FORM, VEC, PERN>), dim3(grid), dim3(kCommitBlock), 0,
-                       ctx->stream, k);
+    if constexpr (B == kCommitBlock)
+        hipLaunchKernelGGL((k_commit_lag<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0, ctx->stream,
+                           k);
+    else
+        hipLaunchKernelGGL((k_commit_lag_big<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0,
+                           ctx->stream, k);
     return hq::post_launch(ctx, "k_commit_lag");
 }
 
@@ -1119,22 +1163,32 @@ extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *ar
     }
     FusedLagK f{};
     f.count = count;
+    bool big = true;
+    for (uint32_t i = 0; i < count; ++i) big &= args[i].n_max <= 4;
+    const int B = big ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
     uint64_t blocks = 0;
     for (uint32_t i = 0; i < count; ++i) {
         f.b[i] = lag_k(args + i);
         f.n[i] = (uint8_t)args[i].n_max;
         f.first[i] = (uint32_t)blocks;
-        blocks += grid_for((args[i].G + kLagVec - 1) / kLagVec, kCommitBlock, kMaxBlocks / 2);
+        blocks += grid_for((args[i].G + kLagVec - 1) / kLagVec, B, (uint64_t)kMaxBlocks * 256 / B);
     }
     for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    if (args[0].form == HQ_FORM_TERM_START)
-        hipLaunchKernelGGL((k_commit_lag_fused<HQ_FORM_TERM_START>), dim3(blocks),
+#define HQ_LAG_FUSED(F)                                                                        \
+    if (big)                                                                                   \
+        hipLaunchKernelGGL((k_commit_lag_fused<F, HQ_COMMIT_BLOCK_BIG>), dim3(blocks),         \
+                           dim3(HQ_COMMIT_BLOCK_BIG), 0, ctx->stream, f);                      \
+    else                                                                                       \
+        hipLaunchKernelGGL((k_commit_lag_fused<F, kCommitBlock>), dim3(blocks),                \
                            dim3(kCommitBlock), 0, ctx->stream, f);
-    else
-        hipLaunchKernelGGL((k_commit_lag_fused<HQ_FORM_TERM_MASK>), dim3(blocks),
-                           dim3(kCommitBlock), 0, ctx->stream, f);
+    if (args[0].form == HQ_FORM_TERM_START) {
+        HQ_LAG_FUSED(HQ_FORM_TERM_START)
+    } else {
+        HQ_LAG_FUSED(HQ_FORM_TERM_MASK)
+    }
+#undef HQ_LAG_FUSED
     return hq::post_launch(ctx, "k_commit_lag_fused");
 }
 

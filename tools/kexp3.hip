@@ -56,11 +56,11 @@ __device__ __forceinline__ u64 spread32(unsigned x) {
 
 struct C2 { const u64 *m; u64 stride; const u64 *cin, *last, *ts; u64 *cout, *chg; u64 G, nwords; };
 
-template <int ST>
-__global__ __launch_bounds__(512) void c2(C2 a) {
+template <int ST, int BLK = 512>
+__global__ __launch_bounds__(BLK) void c2(C2 a) {
     const int lane = threadIdx.x & 63;
-    const u64 wave = (u64)blockIdx.x * 8 + (threadIdx.x >> 6);
-    const u64 step = (u64)gridDim.x * 512 * 2;
+    const u64 wave = (u64)blockIdx.x * (BLK / 64) + (threadIdx.x >> 6);
+    const u64 step = (u64)gridDim.x * BLK * 2;
     for (u64 wb = wave * 128; wb < a.G; wb += step) {
         const u64 g = wb + 2 * (u64)lane;
         bool c0 = false, c1 = false;
@@ -114,10 +114,16 @@ int main() {
         return C2{a.match, G, a.committed_in, a.last_index, a.term_start, a.committed_out, a.changed, G, nw};
     };
     typedef void (*KF)(C2);
-    struct V { const char *name; KF k; };
-    V vs[] = {{"nt", c2<ST_NT>}, {"plain", c2<ST_PLAIN>}, {"sc1", c2<ST_SC1>},
-              {"sc0 sc1", c2<ST_SC0SC1>}, {"nt sc1", c2<ST_NTSC1>}, {"sc0", c2<ST_SC0>}};
-    const unsigned grid = (unsigned)(G / 2 / 512);
+    struct V { const char *name; KF k; int blk; unsigned grid; };
+    const unsigned g512 = (unsigned)(G / 2 / 512);
+    V vs[] = {{"plain b512", c2<ST_PLAIN, 512>, 512, g512},
+              {"plain b256", c2<ST_PLAIN, 256>, 256, 2 * g512},
+              {"plain b1024", c2<ST_PLAIN, 1024>, 1024, g512 / 2},
+              {"plain b512 g768", c2<ST_PLAIN, 512>, 512, 768},
+              {"plain b512 g512", c2<ST_PLAIN, 512>, 512, 512},
+              {"plain b256 g1024", c2<ST_PLAIN, 256>, 256, 1024},
+              {"plain b512 g2048", c2<ST_PLAIN, 512>, 512, 2048},
+              {"sc0", c2<ST_SC0, 512>, 512, g512}};
     for (int rep = 0; rep < 2; ++rep) {
         // library kernel for reference
         {
@@ -135,16 +141,16 @@ int main() {
         for (const V &v : vs) {
             CK(hipMemsetAsync((void *)s2[0].committed_out, 0, G * 8, st));
             CK(hipMemsetAsync((void *)s2[0].changed, 0, nw * 8, st));
-            hipLaunchKernelGGL(v.k, grid, 512, 0, st, mk(0));
+            hipLaunchKernelGGL(v.k, v.grid, v.blk, 0, st, mk(0));
             CK(hipStreamSynchronize(st));
             CK(hipMemcpy(out.data(), s2[0].committed_out, G * 8, hipMemcpyDeviceToHost));
             CK(hipMemcpy(chg.data(), s2[0].changed, nw * 8, hipMemcpyDeviceToHost));
             const bool ok = out == ref_out && chg == ref_chg;
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-            for (int i = 0; i < 40; ++i) hipLaunchKernelGGL(v.k, grid, 512, 0, st, mk(i % nsets));
+            for (int i = 0; i < 40; ++i) hipLaunchKernelGGL(v.k, v.grid, v.blk, 0, st, mk(i % nsets));
             CK(hipEventRecord(e0, st));
-            for (int i = 0; i < 400; ++i) hipLaunchKernelGGL(v.k, grid, 512, 0, st, mk(i % nsets));
+            for (int i = 0; i < 400; ++i) hipLaunchKernelGGL(v.k, v.grid, v.blk, 0, st, mk(i % nsets));
             CK(hipEventRecord(e1, st));
             CK(hipEventSynchronize(e1));
             float ms;
