@@ -145,6 +145,29 @@ class Dist:
         self.dist.all_gather(out, t)
         return [o.cpu().tolist() for o in out]
 
+    def gather_words(self, ctx, dev_words, nwords: int):
+        """All ranks' device uint64 words (an hq DeviceArray) on every rank, rank-major: one
+        all_gather over RCCL (xGMI) when each rank has its own GPU, over gloo from host copies
+        otherwise. Returns (numpy [world, nwords], seconds spent in the collective)."""
+        torch = self.torch
+        if self.backend == "nccl":
+            t = torch.empty(nwords, dtype=torch.int64, device=f"cuda:{self.device}")
+            ctx.copy_to_ptr(t.data_ptr(), dev_words, nwords * 8)   # device to device
+            ctx.sync()
+            out = torch.empty(self.world * nwords, dtype=torch.int64, device=t.device)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            self.dist.all_gather_into_tensor(out, t)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            return out.view(self.world, nwords).cpu().numpy().view(np.uint64), dt
+        t = torch.from_numpy(ctx.download(dev_words).view(np.int64).copy())
+        outs = [torch.zeros_like(t) for _ in range(self.world)]
+        t0 = time.perf_counter()
+        self.dist.all_gather(outs, t)
+        dt = time.perf_counter() - t0
+        return np.stack([o.numpy() for o in outs]).view(np.uint64), dt
+
     def sum(self, x: float) -> float:
         if self.torch is None:
             return x
@@ -288,13 +311,22 @@ def run_gpu(w, steps, warmup, d: Dist):
         # checked against the oracle by the cpu_baseline leg
         b = sets[0][0]
         set0 = (ctx.download(b.committed_out), ctx.download(b.changed))
+    gather = None
+    if d.world > 1 and w["kind"] == "commit" and not w["mixed"]:
+        # optional result gather: every GPU's changed bits of batch 0 to every
+        # rank, in clusterID order; off the timed region
+        nw = hq.words64(G)
+        words, dt = d.gather_words(ctx, sets[0][0].changed, nw)
+        node = shard.interleave_bitmaps(list(words), G)
+        gather = {"bytes": int(words.nbytes), "ms": dt * 1e3, "backend": d.backend,
+                  "node_changed": int(np.unpackbits(node.view(np.uint8)).sum())}
     total_groups = d.sum(float(groups_per_step(w) * steps))
     res = dict(
         elapsed=elapsed, launches=launches, avg_kernel_s=avg_kernel_s,
         decisions=total_groups * decisions_per_group(w), nsets=len(sets),
         bytes_per_launch=per_set * steps / max(1, launches), steps=steps,
         achieved_gbs=per_set * steps / (kernel_ms / 1e3) / 1e9,
-        per_gpu=per_gpu, set0=set0,
+        per_gpu=per_gpu, set0=set0, gather=gather,
     )
     ctx.close()
     return res
@@ -804,6 +836,7 @@ def main():
             },
             "per_gpu": [{"rank": i, "decisions_per_s": v, "kernel_avg_us": k}
                         for i, (v, k) in enumerate(r["per_gpu"])],
+            "result_gather": r["gather"],
             "cpu_baseline": cpu,
             "extra": [
                 {

@@ -354,6 +354,11 @@ class Context:
     def h2d_async(self, dst: DeviceArray, src: np.ndarray) -> None:
         self._check(lib.hq_memcpy_async(self.h, _vp(dst.ptr), src.ctypes.data_as(_vp), src.nbytes, 0))
 
+    def copy_to_ptr(self, dst_ptr: int, src: DeviceArray, nbytes: int) -> None:
+        """Device-to-device copy into memory this context does not own (e.g. a torch tensor
+        that a collective reads), asynchronous on the context's stream."""
+        self._check(lib.hq_memcpy_async(self.h, _vp(dst_ptr), _vp(src.ptr), nbytes, 2))
+
     def d2h_async(self, dst: np.ndarray, src: DeviceArray) -> None:
         self._check(lib.hq_memcpy_async(self.h, dst.ctypes.data_as(_vp), _vp(src.ptr), dst.nbytes, 1))
 

@@ -58,3 +58,23 @@ def rank_bucket(rank: int, world: int, bucket: int, groups: int) -> ShardRange:
         if c % world == rank and c % 3 == bucket:
             return ShardRange(c, stride, groups)
     raise AssertionError("unreachable")
+
+
+def interleave_bitmaps(rank_bitmaps, groups_per_rank: int):
+    """The node's bitmap in clusterID order from the per-GPU bitmaps of ``rank_shard``.
+
+    Rank r's bit j is clusterID ``world + r + j * world`` (rank_shard, world > 1), i.e. node
+    position ``j * world + r`` of the clusterIDs world .. world * (G + 1) - 1; for world == 1 the
+    rank's bitmap is the node's. Used after the optional result gather: changed /
+    confirmed bits of every GPU collected over xGMI for the host that applies them.
+    """
+    import numpy as np
+
+    world = len(rank_bitmaps)
+    G = groups_per_rank
+    bits = np.stack([np.unpackbits(np.ascontiguousarray(b, np.uint64).view(np.uint8),
+                                   bitorder="little")[:G] for b in rank_bitmaps])
+    node = bits.T.reshape(-1)                       # position j * world + r
+    pad = (-node.size) % 64
+    node = np.concatenate([node, np.zeros(pad, np.uint8)])
+    return np.packbits(node, bitorder="little").view(np.uint64)

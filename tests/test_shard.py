@@ -68,7 +68,13 @@ def _worker(rank, world, port, G, q):
     slowest = d.max(float(rank + 1))
     gathered = d.gather([float(rank), float(len(out))])   # per-GPU numbers, rank order
     assert gathered == [[float(r), float(G)] for r in range(world)]
-    q.put((rank, list(rng.cids()), out.tolist(), total, slowest))
+
+    class _Host:   # the gloo path of Dist.gather_words reads the rank's words via download()
+        def download(self, a):
+            return a
+    words, _ = d.gather_words(_Host(), chg, len(chg))
+    node = shard.interleave_bitmaps(list(words), G)
+    q.put((rank, list(rng.cids()), out.tolist(), total, slowest, node.tolist()))
     d.close()
 
 
@@ -90,10 +96,12 @@ def test_gloo_world2_sharded_equals_single_process():
 
     by_cid = {}
     totals = set()
-    for rank, cids, out, total, slowest in res:
+    nodes = []
+    for rank, cids, out, total, slowest, node in res:
         assert slowest == world  # max over ranks
         totals.add(total)
         by_cid.update(zip(cids, out))
+        nodes.append(node)
     assert len(totals) == 1      # every rank sees the same all-reduced sum
     # single process over the union of clusterIDs: world + r, 2*world + r, ... == 2 .. 2G+1
     single = qref.CommitInputs(qref.spec(0x5EED0001, G * world, 5, cid_base=world, cid_stride=1,
@@ -102,3 +110,23 @@ def test_gloo_world2_sharded_equals_single_process():
     cids = range(world, world + G * world)
     assert [by_cid[c] for c in cids] == s_out.tolist()
     assert totals.pop() == float(np.unpackbits(s_chg.view(np.uint8)).sum())
+    # the gathered per-GPU changed bits, interleaved by clusterID, are the single-process bitmap
+    for node in nodes:
+        assert node == s_chg.tolist()
+
+
+@pytest.mark.parametrize("world,G", [(1, 100), (2, 64), (4, 1000), (8, 77)])
+def test_interleave_bitmaps_orders_by_cluster_id(world, G):
+    rng = np.random.default_rng(world * G)
+    node_bits = rng.integers(0, 2, world * G).astype(np.uint8)   # bit k <-> cid k + base
+    ranks = []
+    for r in range(world):
+        mine = node_bits[r::world] if world > 1 else node_bits
+        ranks.append(np.packbits(np.concatenate([mine, np.zeros((-len(mine)) % 64, np.uint8)]),
+                                 bitorder="little").view(np.uint64))
+    node = shard.interleave_bitmaps(ranks, G)
+    got = np.unpackbits(node.view(np.uint8), bitorder="little")[:world * G]
+    np.testing.assert_array_equal(got, node_bits)
+    if world > 1:   # rank r's group j is cid world + r + j * world
+        cids = [list(shard.rank_shard(r, world, G).cids()) for r in range(world)]
+        assert cids[1][2] - world == 2 * world + 1
