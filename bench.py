@@ -303,8 +303,13 @@ def run_gpu(w, steps, warmup, d: Dist):
     elapsed = d.max(local)
     avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
     # per-GPU numbers (SURVEY.md §8e reporting), gathered off the timed region
-    per_gpu = d.gather([groups_per_step(w) * steps * decisions_per_group(w) / local,
-                        avg_kernel_s * 1e6])
+    try:
+        per_gpu = d.gather([groups_per_step(w) * steps * decisions_per_group(w) / local,
+                            avg_kernel_s * 1e6])
+    except Exception as e:  # a diagnostic must never cost the benchmark line
+        log(f"per-GPU gather failed: {e!r}")
+        per_gpu = [[groups_per_step(w) * steps * decisions_per_group(w) / local,
+                    avg_kernel_s * 1e6]]
     set0 = None
     if w["kind"] == "commit" and not w["mixed"]:
         # the decisions of batch 0 (its output column is rewritten identically every rotation),
@@ -315,11 +320,15 @@ def run_gpu(w, steps, warmup, d: Dist):
     if d.world > 1 and w["kind"] == "commit" and not w["mixed"]:
         # optional result gather: every GPU's changed bits of batch 0 to every
         # rank, in clusterID order; off the timed region
-        nw = hq.words64(G)
-        words, dt = d.gather_words(ctx, sets[0][0].changed, nw)
-        node = shard.interleave_bitmaps(list(words), G)
-        gather = {"bytes": int(words.nbytes), "ms": dt * 1e3, "backend": d.backend,
-                  "node_changed": int(np.unpackbits(node.view(np.uint8)).sum())}
+        try:
+            nw = hq.words64(G)
+            words, dt = d.gather_words(ctx, sets[0][0].changed, nw)
+            node = shard.interleave_bitmaps(list(words), G)
+            gather = {"bytes": int(words.nbytes), "ms": dt * 1e3, "backend": d.backend,
+                      "node_changed": int(np.unpackbits(node.view(np.uint8)).sum())}
+        except Exception as e:   # optional: report, never abort the bench
+            log(f"result gather failed: {e!r}")
+            gather = {"error": repr(e)}
     total_groups = d.sum(float(groups_per_step(w) * steps))
     res = dict(
         elapsed=elapsed, launches=launches, avg_kernel_s=avg_kernel_s,
