@@ -56,10 +56,14 @@ __device__ __forceinline__ u64 spread32(unsigned x) {
 
 struct C2 { const u64 *m; u64 stride; const u64 *cin, *last, *ts; u64 *cout, *chg; u64 G, nwords; };
 
-template <int ST, int BLK = 512>
+template <int ST, int BLK = 512, bool XCD = false>
 __global__ __launch_bounds__(BLK) void c2(C2 a) {
     const int lane = threadIdx.x & 63;
-    const u64 wave = (u64)blockIdx.x * (BLK / 64) + (threadIdx.x >> 6);
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8); remap so that
+    // each XCD streams one contiguous eighth of the batch
+    const u64 nb = gridDim.x;
+    const u64 bid = XCD && nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+    const u64 wave = bid * (BLK / 64) + (threadIdx.x >> 6);
     const u64 step = (u64)gridDim.x * BLK * 2;
     for (u64 wb = wave * 128; wb < a.G; wb += step) {
         const u64 g = wb + 2 * (u64)lane;
@@ -116,7 +120,10 @@ int main() {
     typedef void (*KF)(C2);
     struct V { const char *name; KF k; int blk; unsigned grid; };
     const unsigned g512 = (unsigned)(G / 2 / 512);
-    V vs[] = {{"plain b512", c2<ST_PLAIN, 512>, 512, g512},
+    V vs[] = {{"plain b1024", c2<ST_PLAIN, 1024>, 1024, g512 / 2},
+              {"plain b1024 xcd", c2<ST_PLAIN, 1024, true>, 1024, g512 / 2},
+              {"plain b512 xcd", c2<ST_PLAIN, 512, true>, 512, g512},
+              {"plain b512", c2<ST_PLAIN, 512>, 512, g512},
               {"plain b256", c2<ST_PLAIN, 256>, 256, 2 * g512},
               {"plain b1024", c2<ST_PLAIN, 1024>, 1024, g512 / 2},
               {"plain b512 g768", c2<ST_PLAIN, 512>, 512, 768},
