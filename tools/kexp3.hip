@@ -85,6 +85,22 @@ __global__ __launch_bounds__(BLK) void c2(C2 a) {
     }
 }
 
+// the same bytes with no decision: 6 x 16-B loads per lane, one 16-B store (xor of the loads so
+// nothing is dead) — the floor for one 1M-group launch of this footprint
+template <int BLK>
+__global__ __launch_bounds__(BLK) void copy_like(C2 a) {
+    const u64 wave = (u64)blockIdx.x * (BLK / 64) + (threadIdx.x >> 6);
+    const u64 step = (u64)gridDim.x * BLK * 2;
+    for (u64 wb = wave * 128; wb < a.G; wb += step) {
+        const u64 g = wb + 2 * (u64)(threadIdx.x & 63);
+        if (g + 2 <= a.G) {
+            const u64x2 m0 = ld2(a.m + g), m1 = ld2(a.m + a.stride + g), m2 = ld2(a.m + 2 * a.stride + g);
+            const u64x2 ci = ld2(a.cin + g), la = ld2(a.last + g), ts = ld2(a.ts + g);
+            *reinterpret_cast<u64x2 *>(a.cout + g) = m0 ^ m1 ^ m2 ^ ci ^ la ^ ts;
+        }
+    }
+}
+
 int main() {
     const u64 G = 1ull << 20, nw = G / 64;
     hq_ctx *ctx = nullptr;
@@ -120,7 +136,9 @@ int main() {
     typedef void (*KF)(C2);
     struct V { const char *name; KF k; int blk; unsigned grid; };
     const unsigned g512 = (unsigned)(G / 2 / 512);
-    V vs[] = {{"plain b1024", c2<ST_PLAIN, 1024>, 1024, g512 / 2},
+    V vs[] = {{"copy-like b1024", copy_like<1024>, 1024, g512 / 2},
+              {"copy-like b512", copy_like<512>, 512, g512},
+              {"plain b1024", c2<ST_PLAIN, 1024>, 1024, g512 / 2},
               {"plain b1024 xcd", c2<ST_PLAIN, 1024, true>, 1024, g512 / 2},
               {"plain b512 xcd", c2<ST_PLAIN, 512, true>, 512, g512},
               {"plain b512", c2<ST_PLAIN, 512>, 512, g512},
@@ -162,7 +180,7 @@ int main() {
             CK(hipEventSynchronize(e1));
             float ms;
             CK(hipEventElapsedTime(&ms, e0, e1));
-            printf("%-10s per launch %.2f us  (%.0f GB/s)  %s\n", v.name, ms * 1e3 / 400, G * 56.0 / (ms * 1e-3 / 400) / 1e9, ok ? "exact" : "MISMATCH");
+            printf("%-10s per launch %.2f us  (%.0f GB/s)  %s\n", v.name, ms * 1e3 / 400, G * 56.0 / (ms * 1e-3 / 400) / 1e9, ok ? "exact" : (strncmp(v.name, "copy", 4) == 0 ? "(no decision)" : "MISMATCH"));
         }
     }
     hq_close(ctx);
