@@ -790,22 +790,29 @@ def main():
     extras = []
     e2e = step_leg = None
     conc, kern = [], []
+    failed = []
     for name in [x for x in args.extra.split(",") if x and x != args.workload]:
-        if name == "e2e":
-            e2e = run_e2e(max(20, args.steps // 20), 3, d)
+        we = WORKLOADS.get(name)
+        if we is not None and we.get("mixed") and d.world % 3 == 0:
+            # voter-count buckets need gcd(3, world) == 1 (shard.rank_bucket); same on every rank
+            failed.append({"workload": name, "skipped": "world size divisible by 3"})
             continue
-        if name == "step":
-            step_leg = run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu)
-            continue
-        if name in ("rim", "cq", "ing"):
-            kern.append(run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d))
-            continue
-        if name.startswith("w") and name[1:].isdigit():
-            conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))
-            continue
-        we = WORKLOADS[name]
-        re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
-        extras.append((name, we, re_))
+        try:
+            if name == "e2e":
+                e2e = run_e2e(max(20, args.steps // 20), 3, d)
+            elif name == "step":
+                step_leg = run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu)
+            elif name in ("rim", "cq", "ing"):
+                kern.append(run_kernel_leg(name, max(50, args.steps // 4),
+                                           max(5, args.warmup // 4), d))
+            elif name.startswith("w") and name[1:].isdigit():
+                conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))
+            else:
+                re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
+                extras.append((name, we, re_))
+        except Exception as e:   # an extra leg never costs the headline line
+            log(f"extra leg {name} failed: {e!r}")
+            failed.append({"workload": name, "error": repr(e)})
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
@@ -857,7 +864,7 @@ def main():
                     "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
-            ] + kern + conc + ([e2e] if e2e else []) + ([step_leg] if step_leg else []),
+            ] + kern + conc + ([e2e] if e2e else []) + ([step_leg] if step_leg else []) + failed,
         }
         print(json.dumps(line), flush=True)
     d.close()
