@@ -21,9 +21,7 @@ constexpr int kCommitBlock = 512;
 #endif
 template <int N, int FORM, bool PERN>
 constexpr int commit_blk() {
-    return !PERN && (N <= 4 || (N == 5 && (FORM == HQ_FORM_TERM_START || FORM == HQ_FORM_TERM_MASK)))
-               ? HQ_COMMIT_BLOCK_BIG
-               : kCommitBlock;
+    return !PERN && N <= 5 ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
 }
 template <int N, bool PERN>
 constexpr int lag_blk() {
