@@ -484,34 +484,41 @@ def run_concurrent(w, steps, warmup, d: Dist, W=2):
 
 def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
     """Host-fed end to end, PCIe included — never the headline `value`.
-    Per step: pinned H2D of G/4 leader appends + G follower match deltas (16 B each), append +
-    ingest kernels into the device-resident table, commit in place (term-mask form), D2H of the
-    changed bitmap and the committed column (dragonboat_amd/pipeline.py). Serial (one stream)
-    and pipelined over two contexts (the next step's copies overlap this step's kernels and
-    readback; the kernels stay in step order)."""
+    Per step: pinned H2D of G/4 leader appends + G follower match deltas, append + ingest kernels
+    into the device-resident table, commit in place (term-mask form), D2H of the changed bitmap
+    and the committed column (dragonboat_amd/pipeline.py). Reported: 8-byte records (append
+    counts, acks as lags below lastIndex) pipelined over 2 contexts; beside it the 16-byte
+    records pipelined and on one stream."""
     from dragonboat_amd import hipquorum as hq
     from dragonboat_amd import shard
     from dragonboat_amd.pipeline import HostFedPipeline
 
     rng = shard.rank_shard(d.rank, d.world, G)
     spec = hq.synth_spec(SEED_BASE + 9, G, n, cid_base=rng.cid_base, cid_stride=rng.cid_stride)
-    r = np.random.default_rng(d.rank)
     nb = 4   # distinct host batches cycled through
     out = {}
-    for depth in (1, 2):
-        p = HostFedPipeline(d.device, G, n, G // 4, G, depth=depth)
+    for depth, compact in ((1, False), (2, False), (2, True)):
+        r = np.random.default_rng(d.rank)
+        p = HostFedPipeline(d.device, G, n, G // 4, G, depth=depth, compact=compact)
         p.synth(spec)
         last = p.ctxs[0].download(p.table.last_index)
         apps, upds = [], []
         for k in range(nb):
             g = r.choice(G, G // 4, replace=False).astype(np.uint64)
-            app = p.ctxs[0].pinned(2 * len(g), np.uint64)
-            app[0::2], app[1::2] = g, last[g] + np.uint64(k + 1)
-            apps.append(app)
             gu = r.integers(0, G, G, dtype=np.uint64)
-            upd = p.ctxs[0].pinned(2 * G, np.uint64)
-            upd[0::2] = (gu << np.uint64(8)) | r.integers(1, n, G, dtype=np.uint64)
-            upd[1::2] = last[gu] + np.uint64(k)
+            su = r.integers(1, n, G, dtype=np.uint64)
+            if compact:
+                app = p.ctxs[0].pinned(len(g), np.uint64)
+                app[:] = hq.pack_append_counts(g, np.full(len(g), k + 1, np.uint64))
+                upd = p.ctxs[0].pinned(G, np.uint64)
+                upd[:] = hq.pack_lag_updates(gu, su, r.integers(0, 4, G, dtype=np.uint64))
+            else:
+                app = p.ctxs[0].pinned(2 * len(g), np.uint64)
+                app[0::2], app[1::2] = g, last[g] + np.uint64(k + 1)
+                upd = p.ctxs[0].pinned(2 * G, np.uint64)
+                upd[0::2] = (gu << np.uint64(8)) | su
+                upd[1::2] = last[gu] + np.uint64(k)
+            apps.append(app)
             upds.append(upd)
         for i in range(warmup):
             p.step(i, apps[i % nb], G // 4, upds[i % nb], G)
@@ -522,21 +529,26 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
             p.step(i, apps[i % nb], G // 4, upds[i % nb], G)
         p.sync()
         d.barrier()
-        out[depth] = d.max(time.perf_counter() - t0)
+        out[(depth, compact)] = d.max(time.perf_counter() - t0)
         p.close()
-    pcie = (G // 4) * 16 + G * 16 + hq.words64(G) * 8 + G * 8
-    elapsed = out[2]
-    return {
+
+    def pcie(w):   # H2D records + D2H changed bitmap and committed column, bytes per step
+        return (G // 4) * w + G * w + hq.words64(G) * 8 + G * 8
+
+    def rec(key, w):
+        return {"value": d.sum(float(G * steps)) / out[key], "ms_per_step": out[key] / steps * 1e3,
+                "pcie_bytes_per_step": pcie(w), "pcie_gbs": pcie(w) * steps / out[key] / 1e9}
+
+    res = {
         "workload": f"e2e: host-fed {G} groups x {n} voters per GPU per step: pinned H2D of "
-                    f"{G // 4} appends + {G} match deltas, ingest + commit kernels, D2H results; "
-                    f"steps pipelined over 2 contexts",
-        "value": d.sum(float(G * steps)) / elapsed, "unit": "decisions/s",
-        "ms_per_step": elapsed / steps * 1e3,
-        "pcie_bytes_per_step": pcie,
-        "pcie_gbs": pcie * steps / elapsed / 1e9,
-        "serial_one_stream": {"value": d.sum(float(G * steps)) / out[1],
-                              "ms_per_step": out[1] / steps * 1e3},
+                    f"{G // 4} appends + {G} match deltas (8-byte records), ingest + commit "
+                    f"kernels, D2H results; steps pipelined over 2 contexts",
+        "unit": "decisions/s",
     }
+    res.update(rec((2, True), 8))
+    res["records_16B_pipelined"] = rec((2, False), 16)
+    res["records_16B_one_stream"] = rec((1, False), 16)
+    return res
 
 
 def step_groups(hq, G, cid_base, cid_stride, last0=1000):

@@ -1570,6 +1570,106 @@ __global__ __launch_bounds__(kBlock) void k_append(const hq_append_update *u, ui
 
 }  // namespace
 
+// ---- compact 8-byte deltas (hq_ingest_lag_dev / hq_append_count_dev) ------------------------
+namespace {
+
+// the term-mask bits of the entries (prev, prev + n] (appendEntries at the leader's term)
+__device__ __forceinline__ uint32_t append_bits(uint64_t prev, uint64_t n, uint32_t R) {
+    if (n >= R) return R >= 32 ? 0xFFFFFFFFu : ((1u << R) - 1u);
+    uint32_t bits = 0;
+    for (uint64_t k = 1; k <= n; ++k) bits |= 1u << ((prev + k) & (R - 1));
+    return bits;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ingest_lag(const uint64_t *u, uint64_t count,
+                                                       uint64_t *match, uint64_t stride,
+                                                       const uint64_t *last, uint64_t G,
+                                                       uint32_t n_max, uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kBlock) {
+        bool skip = false;
+        if (i < count) {
+            const uint64_t x = __builtin_nontemporal_load(u + i);
+            const uint64_t g = x >> 32;
+            const uint32_t s = (uint32_t)(x >> 28) & 0xFu;
+            const uint64_t lag = x & 0x0FFFFFFFull;
+            skip = g >= G || s >= n_max;
+            if (!skip) {
+                const uint64_t l = last[g];
+                skip = lag > l;
+                // remote.tryUpdate (remote.go:127-131) of the acknowledged index lastIndex - lag
+                if (!skip)
+                    atomicMax(reinterpret_cast<unsigned long long *>(match + s * stride + g),
+                              (unsigned long long)(l - lag));
+            }
+        }
+        count_skip(n_skipped, skip);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_append_count(const uint64_t *u, uint64_t count,
+                                                         uint64_t *last, uint64_t *match0,
+                                                         uint16_t *mask, uint32_t R, uint64_t G,
+                                                         uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kBlock) {
+        bool skip = false;
+        if (i < count) {
+            const uint64_t x = __builtin_nontemporal_load(u + i);
+            const uint64_t g = x >> 32, n = x & 0xFFFFFFFFull;
+            skip = g >= G || n == 0;
+            if (!skip) {
+                // appendEntries (raft.go:911-922): lastIndex += len(entries); additions commute,
+                // so several appends of one group in a batch land in any order
+                const uint64_t prev = atomicAdd(reinterpret_cast<unsigned long long *>(last + g),
+                                                (unsigned long long)n);
+                atomicMax(reinterpret_cast<unsigned long long *>(match0 + g),
+                          (unsigned long long)(prev + n));          // raft.go:918
+                if (mask)
+                    atomicOr(reinterpret_cast<unsigned int *>(mask + (g & ~1ull)),
+                             (append_bits(prev, n, R) & 0xFFFFu) << (16 * (uint32_t)(g & 1)));
+            }
+        }
+        count_skip(n_skipped, skip);
+    }
+}
+
+}  // namespace
+
+extern "C" int hq_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                                 uint64_t *match, uint64_t match_stride,
+                                 const uint64_t *last_index, uint64_t G, uint32_t n_max,
+                                 uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    if (!updates || !match || !last_index || match_stride < G || n_max < 1 ||
+        n_max > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_ingest_lag_dev: bad arguments");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_ingest_lag, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
+                       updates, count, match, match_stride, last_index, G, n_max, n_skipped);
+    return hq::post_launch(ctx, "k_ingest_lag");
+}
+
+extern "C" int hq_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                                   uint64_t *last_index, uint64_t *match_slot0,
+                                   uint16_t *term_mask, uint32_t ring_len, uint64_t G,
+                                   uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    if (!updates || !last_index || !match_slot0 ||
+        (term_mask && ((reinterpret_cast<uintptr_t>(term_mask) & 3) || ring_len < 1 ||
+                       ring_len > 16 || (ring_len & (ring_len - 1)))))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_append_count_dev: bad arguments");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_append_count, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
+                       updates, count, last_index, match_slot0, term_mask,
+                       ring_len ? ring_len : 16u, G, n_skipped);
+    return hq::post_launch(ctx, "k_append_count");
+}
+
 extern "C" int hq_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
                                    uint64_t *match, uint64_t match_stride, uint64_t G,
                                    uint32_t n_max, uint64_t *n_skipped) {

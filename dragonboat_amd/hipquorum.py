@@ -212,6 +212,10 @@ SIGNATURES = {
                                          ctypes.c_uint32, _vp]),
     "hq_append_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint32,
                                      ctypes.c_uint64, _vp]),
+    "hq_ingest_lag_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp,
+                                         ctypes.c_uint64, ctypes.c_uint32, _vp]),
+    "hq_append_count_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
+                                           ctypes.c_uint32, ctypes.c_uint64, _vp]),
     "hq_pack_commit": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.POINTER(CommitArgs)]),
     "hq_pack_ring32": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp]),
     "hq_pack_votes": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -460,6 +464,19 @@ class Context:
                                       _p(match_slot0), _p(term_mask), ring_len, G,
                                       _p(n_skipped)))
 
+    def ingest_lag_dev(self, updates, count, match, match_stride, last_index, G, n_max,
+                       n_skipped=None):
+        """updates: device uint64 array of group << 32 | slot << 28 | lag."""
+        self._check(lib.hq_ingest_lag_dev(self.h, _p(updates), count, _p(match), match_stride,
+                                          _p(last_index), G, n_max, _p(n_skipped)))
+
+    def append_count_dev(self, updates, count, last_index, match_slot0, term_mask, ring_len, G,
+                         n_skipped=None):
+        """updates: device uint64 array of group << 32 | n_entries."""
+        self._check(lib.hq_append_count_dev(self.h, _p(updates), count, _p(last_index),
+                                            _p(match_slot0), _p(term_mask), ring_len, G,
+                                            _p(n_skipped)))
+
     def synth_commit_dev(self, spec: SynthSpec, args: CommitArgs) -> None:
         self._check(lib.hq_synth_commit_dev(self.h, ctypes.byref(spec), ctypes.byref(args)))
 
@@ -581,6 +598,19 @@ def commit_batch_array(args_list) -> ctypes.Array:
     for i, a in enumerate(args_list):
         arr[i] = a
     return arr
+
+
+def pack_lag_updates(group, slot, lag) -> np.ndarray:
+    """8-byte match deltas for hq_ingest_lag_dev (lag < 2^28, slot < 16)."""
+    g, s, l = (np.asarray(x, np.uint64) for x in (group, slot, lag))
+    if (l >= np.uint64(1 << 28)).any() or (s >= np.uint64(16)).any():
+        raise ValueError("lag >= 2^28 or slot >= 16: use the 16-byte hq_match_update form")
+    return (g << np.uint64(32)) | (s << np.uint64(28)) | l
+
+
+def pack_append_counts(group, n) -> np.ndarray:
+    """8-byte appends for hq_append_count_dev (n entries, 1 <= n < 2^32)."""
+    return (np.asarray(group, np.uint64) << np.uint64(32)) | np.asarray(n, np.uint64)
 
 
 def lag_batch_array(args_list) -> ctypes.Array:

@@ -27,10 +27,15 @@ from . import hipquorum as hq
 
 class HostFedPipeline:
     def __init__(self, device: int, G: int, n: int, max_appends: int, max_updates: int,
-                 depth: int = 2, ring_len: int = 16):
+                 depth: int = 2, ring_len: int = 16, compact: bool = False):
+        """compact: 8-byte records (hq_append_count_dev: group << 32 | entries;
+        hq_ingest_lag_dev: group << 32 | slot << 28 | lastIndex - index) instead of the 16-byte
+        hq_append_update / hq_match_update pairs — half the PCIe bytes per step."""
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.G, self.n, self.R, self.depth = G, n, ring_len, depth
+        self.compact = compact
+        w = 1 if compact else 2     # uint64 words per record
         self.ctxs = [hq.Context(device) for _ in range(depth)]
         c0 = self.ctxs[0]
         self.table = hq.alloc_commit(c0, G, n, hq.HQ_FORM_TERM_MASK, ring_len)
@@ -39,8 +44,8 @@ class HostFedPipeline:
         self.args = a
         self.max_appends, self.max_updates = max_appends, max_updates
         # per context: device staging for the step's inputs, pinned buffers for its results
-        self.dapp = [c.empty(2 * max(1, max_appends), np.uint64) for c in self.ctxs]
-        self.dupd = [c.empty(2 * max(1, max_updates), np.uint64) for c in self.ctxs]
+        self.dapp = [c.empty(w * max(1, max_appends), np.uint64) for c in self.ctxs]
+        self.dupd = [c.empty(w * max(1, max_updates), np.uint64) for c in self.ctxs]
         self.out_chg = [c.pinned(hq.words64(G), np.uint64) for c in self.ctxs]
         self.out_com = [c.pinned(G, np.uint64) for c in self.ctxs]
         self._last = None
@@ -62,24 +67,35 @@ class HostFedPipeline:
     def step(self, i: int, appends: np.ndarray, n_appends: int, updates: np.ndarray,
              n_updates: int) -> int:
         """Enqueue step i (asynchronous). appends / updates: flat pinned uint64 arrays of
-        (group, new_last) and (group << 8 | slot, index) pairs. Returns the index of the result
-        buffers the step reads back into (``results``)."""
+        (group, new_last) and (group << 8 | slot, index) pairs, or in the compact form one word
+        each (``hipquorum.pack_append_counts`` / ``pack_lag_updates``; lags relative to lastIndex
+        after this step's appends). Returns the index of the result buffers the step reads back
+        into (``results``)."""
         if n_appends > self.max_appends or n_updates > self.max_updates:
             raise ValueError("step larger than the staging buffers")
+        w = 1 if self.compact else 2
         k = i % self.depth
         x = self.ctxs[k]
         if n_appends:
-            x.h2d_async(self.dapp[k], appends[:2 * n_appends])
+            x.h2d_async(self.dapp[k], appends[:w * n_appends])
         if n_updates:
-            x.h2d_async(self.dupd[k], updates[:2 * n_updates])
+            x.h2d_async(self.dupd[k], updates[:w * n_updates])
         if self._last is not None and self._last is not x:
             x.wait_for(self._last)        # kernels after the previous step (and its readback)
         t = self.table
-        if n_appends:
-            x.append_dev(self.dapp[k], n_appends, t.last_index, t.match, t.term_mask, self.R,
-                         self.G)
-        if n_updates:
-            x.ingest_match_dev(self.dupd[k], n_updates, t.match, self.G, self.G, self.n)
+        if self.compact:
+            if n_appends:
+                x.append_count_dev(self.dapp[k], n_appends, t.last_index, t.match, t.term_mask,
+                                   self.R, self.G)
+            if n_updates:
+                x.ingest_lag_dev(self.dupd[k], n_updates, t.match, self.G, t.last_index, self.G,
+                                 self.n)
+        else:
+            if n_appends:
+                x.append_dev(self.dapp[k], n_appends, t.last_index, t.match, t.term_mask,
+                             self.R, self.G)
+            if n_updates:
+                x.ingest_match_dev(self.dupd[k], n_updates, t.match, self.G, self.G, self.n)
         x.commit_dev(self.args)
         x.d2h_async(self.out_chg[k], t.changed)
         x.d2h_async(self.out_com[k], t.committed_in)

@@ -344,6 +344,25 @@ int hq_append_dev(hq_ctx *ctx, const hq_append_update *updates, uint64_t count,
                   uint64_t *last_index, uint64_t *match_slot0, uint16_t *term_mask,
                   uint32_t ring_len, uint64_t G, uint64_t *n_skipped);
 
+/*
+ * The same two updates in 8 bytes each, for host-fed steps (PCIe is the bound there):
+ * hq_ingest_lag_dev: update = group << 32 | slot << 28 | lag (28 bits): the follower in `slot`
+ *   acknowledged index last_index[group] - lag, last_index as it stands when the kernel runs (after
+ *   the step's appends); match = max(match, that index) as in hq_ingest_match_dev. A lag above
+ *   last_index, group >= G or slot >= n_max is skipped and counted. Acks 2^28 or more below
+ *   lastIndex need the 16-byte form.
+ * hq_append_count_dev: update = group << 32 | n (n >= 1 entries appended at the leader's term):
+ *   last_index += n (64-bit atomic add, so several appends of a group in one batch commute),
+ *   the leader's match = the new last, term-mask bits of the n new indexes set. n == 0 or
+ *   group >= G is skipped and counted.
+ */
+int hq_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count, uint64_t *match,
+                      uint64_t match_stride, const uint64_t *last_index, uint64_t G,
+                      uint32_t n_max, uint64_t *n_skipped);
+int hq_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                        uint64_t *last_index, uint64_t *match_slot0, uint16_t *term_mask,
+                        uint32_t ring_len, uint64_t G, uint64_t *n_skipped);
+
 /* ---------------------------------------------------------------- host-side packers --------- */
 /*
  * The packers turn a step worker's per-group view — the membership maps r.remotes / r.observers

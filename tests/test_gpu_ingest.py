@@ -135,8 +135,9 @@ def test_device_resident_leader_pipeline(gpu_ctx, hq):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("depth", [1, 2, 3])
-def test_host_fed_pipeline_matches_oracle(hq, depth):
+@pytest.mark.parametrize("depth,compact", [(1, False), (2, False), (3, False), (1, True),
+                                           (2, True)])
+def test_host_fed_pipeline_matches_oracle(hq, depth, compact):
     """dragonboat_amd.pipeline: host-fed steps (pinned appends + match deltas -> append, ingest,
     commit in place -> readback) over `depth` contexts. Every step's read-back changed bitmap and
     committed column equal the oracle's sequential run, whatever the pipelining."""
@@ -147,17 +148,19 @@ def test_host_fed_pipeline_matches_oracle(hq, depth):
     inp = qref.CommitInputs(qref.spec(SEED + 4, G, n))
     host = dict(match=inp.match.copy(), last=inp.last_index.copy(), mask=inp.term_mask.copy(),
                 committed=inp.committed_in.copy())
-    p = HostFedPipeline(0, G, n, G // 2, G, depth=depth, ring_len=R)
+    p = HostFedPipeline(0, G, n, G // 2, G, depth=depth, ring_len=R, compact=compact)
     p.upload(host["match"], host["committed"], host["last"], host["mask"])
     want, slots = [], []
     for step in range(T):
         gsel = rng.choice(G, G // 3, replace=False).astype(np.uint64)
         app = np.stack([gsel, host["last"][gsel] + rng.integers(1, 4, len(gsel), dtype=np.uint64)],
                        axis=1).astype(np.uint64)
+        counts = app[:, 1] - host["last"][gsel]           # entries appended (gsel distinct)
         qref.append(app, host["last"], host["match"][:G], host["mask"], R, G)
         g = rng.integers(0, G, G, dtype=np.uint64)
         s = rng.integers(1, n, G, dtype=np.uint64)
-        idx = host["last"][g] - rng.integers(0, 6, G, dtype=np.uint64)
+        lag = rng.integers(0, 6, G, dtype=np.uint64)
+        idx = host["last"][g] - lag                       # lastIndex after the step's appends
         upd = np.stack([(g << np.uint64(8)) | s, idx], axis=1).astype(np.uint64)
         qref.ingest_match(upd, host["match"], G, G, n)
         out = np.zeros(G, np.uint64)
@@ -167,10 +170,12 @@ def test_host_fed_pipeline_matches_oracle(hq, depth):
         assert qref.commit_batch(qa, 8) == 0
         host["committed"] = out
         want.append((wchg, out))
-        pa = p.ctxs[step % depth].pinned(app.size, np.uint64)
-        pa[:] = app.reshape(-1)
-        pu = p.ctxs[step % depth].pinned(upd.size, np.uint64)
-        pu[:] = upd.reshape(-1)
+        wire_app = hq.pack_append_counts(gsel, counts) if compact else app.reshape(-1)
+        wire_upd = hq.pack_lag_updates(g, s, lag) if compact else upd.reshape(-1)
+        pa = p.ctxs[step % depth].pinned(wire_app.size, np.uint64)
+        pa[:] = wire_app
+        pu = p.ctxs[step % depth].pinned(wire_upd.size, np.uint64)
+        pu[:] = wire_upd
         slots.append(p.step(step, pa, len(app), pu, G))
         if step % depth == depth - 1 or step == T - 1:
             # read back the steps whose result buffers are about to be reused
@@ -181,3 +186,57 @@ def test_host_fed_pipeline_matches_oracle(hq, depth):
     np.testing.assert_array_equal(p.ctxs[0].download(p.table.match), host["match"])
     assert sum(int(np.unpackbits(w[0].view(np.uint8)).sum()) for w in want) > G
     p.close()
+
+
+@pytest.mark.gpu
+def test_compact_deltas_equal_the_16_byte_forms(gpu_ctx, hq):
+    """hq_append_count_dev / hq_ingest_lag_dev against the sequential restatements of the
+    16-byte forms: repeated appends of one group in a batch add up, acks are relative to the
+    post-append lastIndex, out-of-range records are skipped and counted."""
+    rng = np.random.default_rng(SEED + 5)
+    G, n, R = 30_011, 5, 16
+    inp = qref.CommitInputs(qref.spec(SEED + 5, G, n))
+    last, match, mask = inp.last_index.copy(), inp.match.copy(), inp.term_mask.copy()
+    dl, dm, dk = gpu_ctx.upload(last), gpu_ctx.upload(match), gpu_ctx.upload(mask)
+    skip = gpu_ctx.upload(np.zeros(1, np.uint64))
+    # appends: 20 000 records over 8 000 groups (duplicates), 1..20 entries, + 2 bad records
+    ga = rng.integers(0, 8000, 20_000, dtype=np.uint64)
+    na = rng.integers(1, 21, 20_000, dtype=np.uint64)
+    seq = []
+    cur = last.copy()
+    for gg, nn in zip(ga, na):                           # the sequential meaning: += n
+        cur[gg] += nn
+        seq.append((gg, cur[gg]))
+    want_last, want_match, want_mask = last.copy(), match.copy(), mask.copy()
+    qref.append(np.array(seq, np.uint64), want_last, want_match[:G], want_mask, R, G)
+    wire = np.concatenate([hq.pack_append_counts(ga, na),
+                           hq.pack_append_counts([G + 5, 3], [1, 0])])
+    du = gpu_ctx.upload(wire)
+    gpu_ctx.append_count_dev(du, len(wire), dl, dm, dk, R, G, skip)
+    np.testing.assert_array_equal(gpu_ctx.download(dl), want_last)
+    np.testing.assert_array_equal(gpu_ctx.download(dk), want_mask)
+    np.testing.assert_array_equal(gpu_ctx.download(dm)[:G], want_match[:G])
+    assert int(gpu_ctx.download(skip)[0]) == 2
+    # acks: lags relative to the new lastIndex, + records beyond G / n_max / lastIndex
+    g = rng.integers(0, G, 100_000, dtype=np.uint64)
+    s = rng.integers(1, n, 100_000, dtype=np.uint64)
+    lag = rng.integers(0, 40, 100_000, dtype=np.uint64)
+    upd = np.stack([(g << np.uint64(8)) | s, want_last[g] - lag], axis=1).astype(np.uint64)
+    # the two valid records among the edge cases below, in the 16-byte form
+    extra = [((1 << 8) | 1, int(want_last[1]))]
+    if (1 << 28) - 1 <= int(want_last[2]):
+        extra.append(((2 << 8) | 1, int(want_last[2]) - ((1 << 28) - 1)))
+    upd = np.concatenate([upd, np.array(extra, np.uint64)])
+    qref.ingest_match(upd, want_match, G, G, n)
+    wire = np.concatenate([hq.pack_lag_updates(g, s, lag),
+                           hq.pack_lag_updates([G, 0, 1], [1, 7, 1], [0, 0, 0]),
+                           hq.pack_lag_updates([2], [1], [(1 << 28) - 1])])
+    du2 = gpu_ctx.upload(wire)
+    gpu_ctx.ingest_lag_dev(du2, len(wire), dm, G, dl, G, n, skip)
+    np.testing.assert_array_equal(gpu_ctx.download(dm), want_match)
+    skipped = int(gpu_ctx.download(skip)[0]) - 2
+    assert skipped == 2 + int((1 << 28) - 1 > int(want_last[2]))
+    with pytest.raises(ValueError):
+        hq.pack_lag_updates([1], [1], [1 << 28])
+    for x in (dl, dm, dk, skip, du, du2):
+        gpu_ctx.free(x)
