@@ -16,11 +16,11 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {"c2": "k_commit<3, 0, 2, false>", "c3": "k_commit<5, 1, 2, false>",
-          "c3m": "k_commit<5, 2, 2, false>", "c3r32": "k_commit<5, 3, 2, false>",
-          "c4": "k_bits<3, true", "c5": "k_commit_fused<2>", "c5s": "k_commit<7, 2, 2, false>",
-          "c2l": "k_commit_lag<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
-          "c5l": "k_commit_lag_fused<2>", "rim": "k_ri_multi<false, false>",
+KERNEL = {"c2": "k_commit_big<3, 0, 2, false>", "c3": "k_commit_big<5, 1, 2, false>",
+          "c3m": "k_commit_big<5, 2, 2, false>", "c3r32": "k_commit_big<5, 3, 2, false>",
+          "c4": "k_bits<3, true", "c5": "k_commit_fused<2, 512>", "c5s": "k_commit<7, 2, 2, false>",
+          "c2l": "k_commit_lag_big<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
+          "c5l": "k_commit_lag_fused<2, 512>", "rim": "k_ri_multi<false, false>",
           "cq": "k_bits<4, false", "ing": "k_ingest_match"}
 
 
