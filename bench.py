@@ -551,27 +551,43 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
     return res
 
 
-def step_groups(hq, G, cid_base, cid_stride, last0=1000):
-    """Leader groups of the step workload: 3 voters (node 1 leads), term 5, all caught up."""
+STEP_ROLES = {
+    # node 1 leads; the rest follow in member order
+    "step": ("remote",) * 3,
+    # BASELINE config 3's membership: 4 full members (leader included), 1 witness, 2 observers
+    "step5": ("remote",) * 4 + ("witness",) + ("observer",) * 2,
+}
+
+
+def step_groups(hq, G, cid_base, cid_stride, roles=STEP_ROLES["step"], last0=1000):
+    """Leader groups of the step workload (node 1 leads, term 5, all caught up); member k has
+    node id k + 1 and role roles[k]."""
+    role_code = {"remote": hq.ROLE_REMOTE, "witness": hq.ROLE_WITNESS,
+                 "observer": hq.ROLE_OBSERVER}
+    nm = len(roles)
     cids = np.uint64(cid_base) + np.arange(G, dtype=np.uint64) * np.uint64(cid_stride)
     g = np.zeros(G, hq.WORKER_GROUP_DTYPE)
     g["cluster_id"], g["node_id"], g["term"], g["state"] = cids, 1, 5, hq.STATE_LEADER
-    g["committed"], g["last_index"], g["term_start"], g["n_members"] = last0, last0, last0 - 10, 3
-    m = np.zeros(3 * G, hq.MEMBER_DTYPE)
-    m["node_id"] = np.tile(np.array([1, 2, 3], np.uint64), G)
+    g["committed"], g["last_index"], g["term_start"], g["n_members"] = last0, last0, last0 - 10, nm
+    m = np.zeros(nm * G, hq.MEMBER_DTYPE)
+    m["node_id"] = np.tile(np.arange(1, nm + 1, dtype=np.uint64), G)
+    m["role"] = np.tile(np.array([role_code[r] for r in roles], np.uint32), G)
     m["match"] = last0
     return g, m, cids
 
 
-def step_events(hq, G, s, last0=1000):
+def step_events(hq, G, s, roles=STEP_ROLES["step"], last0=1000):
     """Step s of the steady-state leader workload, as hq_step_input rows (every group, in
-    handle order): every 4th group serves a local ReadIndex; both followers ack the leader's
-    previous append (ReplicateResp) and answer a heartbeat (the ReadIndex groups' heartbeats
-    carry the ctx); every group proposes one entry. Per group: 4 messages, 1 proposal, 1/4 read
-    -> 1 commit decision and 1/4 ReadIndex decision."""
+    handle order): every 4th group serves a local ReadIndex; every other member acks the
+    leader's previous append (ReplicateResp, witnesses and observers included) and answers a
+    heartbeat (the ReadIndex groups' heartbeats to voting members carry the ctx, observers get
+    ctx-less ones, raft.go:836-848); every group proposes one entry. Per group: 2 (m - 1)
+    messages, 1 proposal, 1/4 read -> 1 commit decision and 1/4 ReadIndex decision."""
+    others = [(k + 1, r) for k, r in enumerate(roles)][1:]
+    nmsg = 2 * len(others)
     last_s = np.uint64(last0 + s)
     has_read = (np.arange(G) % 4) == 0
-    per = 5 + has_read.astype(np.int64)
+    per = nmsg + 1 + has_read.astype(np.int64)
     offsets = np.zeros(G + 1, np.uint64)
     offsets[1:] = np.cumsum(per)
     ev = np.zeros(int(offsets[-1]), hq.EVENT_DTYPE)
@@ -582,41 +598,44 @@ def step_events(hq, G, s, last0=1000):
     r["kind"], r["hint"], r["hint_high"] = hq.EV_READ, ctx_low[rd], s + 1
     ev[base[rd]] = r
     first_msg = base + has_read
-    for k, (frm, typ) in enumerate(((2, 13), (3, 13), (2, 18), (3, 18))):
+    msgs = [(frm, 13, role) for frm, role in others] + [(frm, 18, role) for frm, role in others]
+    for k, (frm, typ, role) in enumerate(msgs):
         idx = first_msg + k
         blk = ev[idx]
         blk["kind"], blk["type"], blk["from"], blk["term"] = hq.EV_MESSAGE, typ, frm, 5
         if typ == 13:
             blk["log_index"] = last_s
-        else:
+        elif role != "observer":
             blk["hint"] = np.where(has_read, ctx_low, 0)
             blk["hint_high"] = np.where(has_read, s + 1, 0)
         ev[idx] = blk
-    p = ev[first_msg + 4]
+    p = ev[first_msg + nmsg]
     p["kind"], p["log_index"] = hq.EV_PROPOSE, 1
-    ev[first_msg + 4] = p
+    ev[first_msg + nmsg] = p
     return np.arange(G, dtype=np.uint32), offsets, ev
 
 
-def _run_workers(hq, d: Dist, G, W, steps, cpu_steps):
+def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles):
     """W workers (one host thread each, own HIP stream) over G groups split into W contiguous
     partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
     of the first 4096 groups after cpu_steps steps)."""
     import threading
 
     rng = _shard_of(d, G)
-    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride)
+    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
+    nm = len(roles)
+    n_voting = sum(r != "observer" for r in roles)
     bounds = [G * i // W for i in range(W + 1)]
     workers = []
     for i in range(W):
-        w = hq.Worker(d.device, 3)
-        w.add_groups(g[bounds[i]:bounds[i + 1]], m[3 * bounds[i]:3 * bounds[i + 1]])
+        w = hq.Worker(d.device, n_voting)
+        w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
         workers.append(w)
     acc = dict(handle_ns=0, pass_ns=0, pack_ns=0, device_ns=0, apply_ns=0, gpu_passes=0,
                decisions=0)
     t_total, n_events, committed = 0.0, 0, None
     for s in range(steps + 1):
-        evs = [step_events(hq, bounds[i + 1] - bounds[i], s) for i in range(W)]
+        evs = [step_events(hq, bounds[i + 1] - bounds[i], s, roles) for i in range(W)]
         res = [None] * W
 
         def run(i):
@@ -650,7 +669,7 @@ def _shard_of(d, G):
     return shard.rank_shard(d.rank, d.world, G)
 
 
-def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
+def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="step"):
     """The step worker end to end (hq_worker_step): host bookkeeping of every event plus the
     GPU passes, against the event-by-event C restatement of the reference (oracle, CPU) on the
     same events; the committed indexes of both must agree. Run with one worker (one step-worker
@@ -660,15 +679,19 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
 
     assert cpu_steps <= steps
     T = min(16, os.cpu_count() or 1)
+    roles = STEP_ROLES[name]
+    nmsg = 2 * (len(roles) - 1)
+    members = ", ".join(f"{roles.count(r)} {r}" for r in ("remote", "witness", "observer")
+                        if roles.count(r))
     out = {
-        "workload": f"step: hq_worker_step over {G} leader groups x 3 voters per GPU; per group "
-                    f"and step 4 messages (2 ReplicateResp, 2 HeartbeatResp), 1 proposal, 1/4 "
-                    f"local ReadIndex",
+        "workload": f"{name}: hq_worker_step over {G} leader groups per GPU ({members}); per group "
+                    f"and step {nmsg} messages ({nmsg // 2} ReplicateResp, {nmsg // 2} "
+                    f"HeartbeatResp), 1 proposal, 1/4 local ReadIndex",
         "unit": "events/s",
     }
     committed_gpu = None
     for W in (1, T):
-        t, ne, acc, committed, gm = _run_workers(hq, d, G, W, steps, cpu_steps)
+        t, ne, acc, committed, gm = _run_workers(hq, d, G, W, steps, cpu_steps, roles)
         elapsed = d.max(t)
         rec = {
             "workers": W,
@@ -694,7 +717,7 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True):
             b = qref.StepBatch(g, m)
             tc, ne = 0.0, 0
             for s in range(cpu_steps + 1):
-                ev = step_events(hq, G, s)
+                ev = step_events(hq, G, s, roles)
                 t0 = time.perf_counter()
                 b.step(*ev, nthreads=nt)
                 if s > 0:
@@ -788,7 +811,7 @@ def main():
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
-                    default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5l,c5r,c5r32,rim,cq,ing,w2,e2e,step",
+                    default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5l,c5r,c5r32,rim,cq,ing,w2,e2e,step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -800,7 +823,8 @@ def main():
     w = WORKLOADS[args.workload]
     r = run_gpu(w, args.steps, args.warmup, d)
     extras = []
-    e2e = step_leg = None
+    e2e = None
+    steps_legs = []
     conc, kern = [], []
     failed = []
     for name in [x for x in args.extra.split(",") if x and x != args.workload]:
@@ -812,8 +836,9 @@ def main():
         try:
             if name == "e2e":
                 e2e = run_e2e(max(20, args.steps // 20), 3, d)
-            elif name == "step":
-                step_leg = run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu)
+            elif name in STEP_ROLES:
+                steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
+                                               name=name))
             elif name in ("rim", "cq", "ing"):
                 kern.append(run_kernel_leg(name, max(50, args.steps // 4),
                                            max(5, args.warmup // 4), d))
@@ -876,7 +901,7 @@ def main():
                     "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
                 }
                 for n, we, re_ in extras
-            ] + kern + conc + ([e2e] if e2e else []) + ([step_leg] if step_leg else []) + failed,
+            ] + kern + conc + ([e2e] if e2e else []) + steps_legs + failed,
         }
         print(json.dumps(line), flush=True)
     d.close()
