@@ -36,6 +36,17 @@ SEED_BASE = 0x5EED0000
 WORKLOADS = {
     "c2": dict(cfg=1, kind="commit", G=1 << 20, n=3, form=0, mixed=False,
                desc="1M groups x 3 voters, batched commit-index kernel (term-start form)"),
+    "c2t": dict(cfg=1, kind="commit", G=1 << 20, n=3, form=0, mixed=False, tiled=True,
+                desc="1M groups x 3 voters, batched commit-index kernel (term-start form) over "
+                     "128-group tiles (HQ_LAYOUT_TILES: one contiguous stream per wave)"),
+    "c3mt": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False, tiled=True,
+                 desc="1M groups x 5 voters (4 full + 1 witness), current-term mask, "
+                      "128-group tiles"),
+    "c3r32t": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=3, mixed=False, tiled=True,
+                   desc="1M groups x 5 voters (4 full + 1 witness), u32 term-ring gather, "
+                        "128-group tiles"),
+    "c5t": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True, tiled=True,
+                desc="as c5 over 128-group tiles (the three buckets in one fused launch)"),
     "c3": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=1, mixed=False,
                desc="1M groups x 5 voters (4 full + 1 witness; observers never packed), "
                     "commit + term-ring gather R=16"),
@@ -56,6 +67,9 @@ WORKLOADS = {
                      "fused launch"),
     "c4": dict(cfg=3, kind="bits", G=16 << 20, n=7,
                desc="16M groups x 7 voters, fused ReadIndex ack quorum + vote tally"),
+    "c4u": dict(cfg=3, kind="bits", G=16 << 20, n=7, uniform=True,
+                desc="as c4 with the voter count uniform over the batch (a step worker's "
+                     "7-voter bucket): no per-group n column"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
                desc="64M groups mixed 3/5/7 voters (n = {3,5,7}[clusterID % 3]) sharded "
                     "clusterID % 8: 8M groups per GPU, the three voter-count buckets in one "
@@ -79,7 +93,8 @@ def algo_bytes_per_group(w):
         # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask
         # | term + gathered u32 ring term)
         return 8 * n + 24 + {0: 8, 1: 16, 2: 2, 3: 12}[w["form"]] + extra_n
-    return 4 + 3 / 8   # ack, granted, rejected, n (u8 each) in; confirmed bit + 2-bit outcome out
+    # ack, granted, rejected (+ n unless uniform) u8 each in; confirmed bit + 2-bit outcome out
+    return (3 if w.get("uniform") else 4) + 3 / 8
 
 
 def decisions_per_group(w):
@@ -197,8 +212,10 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             for n, rng in commit_buckets(shard, w, d):
                 spec = hq.synth_spec(seed + (s << 40), rng.count, n, cid_base=rng.cid_base,
                                      cid_stride=rng.cid_stride)
-                b = hq.alloc_commit(ctx, rng.count, n, w["form"], 16)
+                b = hq.alloc_commit(ctx, rng.count, n, w["form"], 16, tiled=w.get("tiled", False))
                 ctx.synth_commit_dev(spec, b.args())
+                if b.tiles is not None:
+                    ctx.tile_commit_dev(b.args(), b.tiles)
                 buckets.append(b)
             sets.append(buckets)
         elif w["kind"] == "lag":
@@ -221,6 +238,11 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             sets.append((arrs, conf, outc))
     ctx.sync()
     return sets, per_set
+
+
+def batch_args(b):
+    """The launch arguments of one commit batch: its tiles when it has them."""
+    return b.tile_args() if b.tiles is not None else b.args()
 
 
 def commit_buckets(shard, w, d):
@@ -251,7 +273,7 @@ def run_gpu(w, steps, warmup, d: Dist):
     G = w["G"]
     if w["kind"] == "commit" and w["mixed"] and not w.get("separate"):
         # a step = the rank's voter-count buckets decided by one fused launch
-        per_step = [hq.commit_batch_array([b.args() for b in bs]) for bs in sets]
+        per_step = [hq.commit_batch_array([batch_args(b) for b in bs]) for bs in sets]
         seq, wseq = list(range(steps)), list(range(max(1, warmup)))
 
         def run(idx):
@@ -271,7 +293,8 @@ def run_gpu(w, steps, warmup, d: Dist):
                     ctx.commit_lag_fused_dev(arr)
     elif w["kind"] == "commit":
         def flat(k):
-            return hq.commit_batch_array([b.args() for i in range(k) for b in sets[i % len(sets)]])
+            return hq.commit_batch_array([batch_args(b) for i in range(k)
+                                          for b in sets[i % len(sets)]])
         seq, wseq = flat(steps), flat(max(1, warmup))
 
         def run(batch):
@@ -282,7 +305,10 @@ def run_gpu(w, steps, warmup, d: Dist):
         def run(idx):
             for i in idx:
                 (da, dg, dr, dn), conf, outc = sets[i % len(sets)]
-                ctx.readindex_vote_dev(G, da, dg, dr, dn, 0, conf, outc)
+                if w.get("uniform"):
+                    ctx.readindex_vote_dev(G, da, dg, dr, None, w["n"], conf, outc)
+                else:
+                    ctx.readindex_vote_dev(G, da, dg, dr, dn, 0, conf, outc)
 
     if warmup > 0:
         run(wseq)
@@ -368,7 +394,8 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
     rotated past the Infinity Cache like the commit legs:
       rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
       cq:  CheckQuorum (k_bits CHECKQ), 16M groups x 7 voters, active flags reset in place
-      ing: match-delta ingest (k_ingest_match), 4M ReplicateResp deltas into a 4M x 3 table"""
+      ing: match-delta ingest (k_ingest_match), 4M ReplicateResp deltas into a 4M x 3 table
+      ingo: the same deltas in group order, the order a step worker emits them"""
     from dragonboat_amd import hipquorum as hq
 
     ctx = hq.Context(d.device)
@@ -420,12 +447,17 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
             u = np.stack([(g << np.uint64(8)) | s,
                           np.uint64(1 << 30) + np.uint64(k) + r.integers(0, 64, U, dtype=np.uint64)],
                          axis=1)
+            if name == "ingo":
+                # the order a step worker emits them: node by node (execengine.go:923-1000)
+                u = u[np.argsort(u[:, 0], kind="stable")]
             ups.append(ctx.upload(u.reshape(-1)))
 
         def run(i):
             ctx.ingest_match_dev(ups[i % nsets], U, table, G, G, n)
-        desc = (f"ing: ReplicateResp match-delta ingest (remote.tryUpdate as 64-bit atomic max), "
-                f"{U} deltas into a {G} x {n} device table")
+        desc = (f"{name}: ReplicateResp match-delta ingest (remote.tryUpdate as 64-bit atomic "
+                f"max), {U} deltas into a {G} x {n} device table, "
+                + ("in group order (as a step worker emits them)" if name == "ingo"
+                   else "in random order"))
         units, unit = U, "updates/s"
     elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
     ctx.close()
@@ -811,7 +843,8 @@ def main():
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
-                    default="c2l,c3,c3r32,c3m,c3l,c4,c5,c5s,c5l,c5r,c5r32,rim,cq,ing,w2,e2e,step,step5",
+                    default="c2l,c3,c3r32,c3m,c3l,c4,c4u,c5,c5s,c5l,c5r,c5r32,rim,cq,ing,ingo,w2,e2e,"
+                            "step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -839,7 +872,7 @@ def main():
             elif name in STEP_ROLES:
                 steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
                                                name=name))
-            elif name in ("rim", "cq", "ing"):
+            elif name in ("rim", "cq", "ing", "ingo"):
                 kern.append(run_kernel_leg(name, max(50, args.steps // 4),
                                            max(5, args.warmup // 4), d))
             elif name.startswith("w") and name[1:].isdigit():
@@ -875,6 +908,7 @@ def main():
                 "form": ({0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
                          + ("_lag" if w["kind"] == "lag" else ""))
                 if w["kind"] in ("commit", "lag") else "bitmaps",
+                "layout": "tiles" if w.get("tiled") else "columns",
                 "global_groups_per_step": w["G"] * d.world,
                 "parallelism": f"shard{d.world} (clusterID % {d.world})",
             },

@@ -43,7 +43,8 @@ __device__ __forceinline__ void st_stream2(uint64_t *p, u64x2 v) {
     *reinterpret_cast<u64x2 *>(p) = v;
 }
 
-struct CommitK {
+// Every field of a column batch (the generator and the tile packer write / read them all).
+struct CommitCols {
     uint64_t G, stride, nwords;
     uint32_t n_max, R;
     const uint64_t *match;
@@ -58,7 +59,26 @@ struct CommitK {
     uint64_t *fallback;
     const uint16_t *mask;
     const uint32_t *ring32;
+    uint64_t tile_words;   // HQ_LAYOUT_TILES: u64 words per tile
 };
+
+// The decision kernels' argument: only what one form reads, 96 bytes. Kernel arguments past
+// that cost the 1M-group launch 0.25 us (a 160-byte twin of the same kernel: 10.55 vs 10.30 us,
+// tools/kexp6.hip), so the form-specific columns share the `aux` and `ring` slots.
+struct CommitK {
+    uint64_t G;
+    uint64_t stride;        // columns: elements between match rows; tiles: u64 words per tile
+    const uint64_t *match;  // columns: slot 0's row; tiles: tile 0
+    const uint64_t *cin;    // columns only (tiles carry it)
+    uint64_t *cout;
+    const uint64_t *last;   // columns only
+    const void *aux;        // term_start (TERM_START) | term (RING, RING32) | u16 mask (MASK)
+    const void *ring;       // u64 ring (RING) | u32 ring (RING32)
+    uint64_t *changed, *fallback;
+    const uint8_t *nv;
+    uint32_t R, reserved;
+};
+static_assert(sizeof(CommitK) == 96, "keep the decision kernels' argument at 96 bytes");
 
 // ---- compare-exchange networks over u64 held in registers --------------------------------
 __device__ __forceinline__ void ce(uint64_t &a, uint64_t &b) {
@@ -155,14 +175,14 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
         // rings share one 128-B line, so a lane's pair of gathers costs one line, not two.
         fb = (aux == 0) | (aux >= 0xFFFFFFFFull) | (cin > last) || (last - cin > a.R);
         if (!fb && q > cin && q <= last) {
-            const uint32_t lterm = a.ring32[g * a.R + (q & (uint64_t)(a.R - 1))];
+            const uint32_t lterm = static_cast<const uint32_t *>(a.ring)[g * a.R + (q & (uint64_t)(a.R - 1))];
             chg = lterm == (uint32_t)aux;
         }
     } else {
         // aux = the leader's term; the ring holds term(i) for i in (last - R, last]
         fb = (aux == 0) | (cin > last) || (last - cin > a.R);
         if (!fb && q > cin && q <= last) {
-            const uint64_t lterm = a.ring[g * a.R + (q & (uint64_t)(a.R - 1))];
+            const uint64_t lterm = static_cast<const uint64_t *>(a.ring)[g * a.R + (q & (uint64_t)(a.R - 1))];
             chg = lterm == aux;
         }
     }
@@ -171,41 +191,71 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
 
 // VEC = groups per lane (2: 16-byte loads of every SoA column; 1: 8-byte loads). The body of
 // one workgroup `blk` of `nblk` working on batch `a` (k_commit: the grid; k_commit_fused: the
-// workgroups one batch of the launch owns).
-template <int N, int FORM, int VEC, bool PERN, int BLK>
+// workgroups one batch of the launch owns). TILED (HQ_LAYOUT_TILES, VEC = 2 only): a wave's 128
+// groups are one tile, so its loads walk one contiguous 128·(n+3)·8-byte block instead of n + 3
+// column streams.
+template <int N, int FORM, int VEC, bool PERN, int BLK, bool TILED = false>
 __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
+    static_assert(!TILED || VEC == 2, "tiles are read two groups per lane");
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = blk * (BLK / 64) + (threadIdx.x >> 6);
+    // the wave index is wave-uniform: read it into a scalar so the loop bound and the full-wave
+    // test below are scalar branches, not exec masks (10.4 vs 10.9 us per 1M x 3 tiled launch,
+    // tools/kexp6.hip)
+    const uint64_t wave = blk * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = nblk * BLK * VEC;
-    const uint64_t *aux_col = (FORM == HQ_FORM_TERM_START) ? a.tstart : a.term;
-    // aux of group g: the u64 column (forms 0, 1) or the u16 term mask (form 2)
-    auto aux1 = [&](uint64_t g) -> uint64_t {
-        if constexpr (FORM == HQ_FORM_TERM_MASK) return a.mask[g];
-        return aux_col[g];
-    };
     for (uint64_t wbase = wave * 64 * VEC; wbase < a.G; wbase += step) {
         const uint64_t g0 = wbase + (uint64_t)lane * VEC;
+        // every input field as a wave-uniform base + this lane's element offset `off` (scalar
+        // base + vector offset addressing, no 64-bit address per lane and field): slot s of
+        // match at bm[s * ms + off], then committed_in, last_index and aux (term_start / term
+        // as u64, or the u16 mask)
+        const uint64_t *bm, *bcin, *blast, *baux;
+        const uint16_t *bmask;
+        uint64_t ms, off;
+        if constexpr (TILED) {
+            const uint64_t *t = a.match + (wbase / HQ_TILE_GROUPS) * a.stride;
+            bm = t;
+            ms = HQ_TILE_GROUPS;
+            bcin = t + N * HQ_TILE_GROUPS;
+            blast = t + (N + 1) * HQ_TILE_GROUPS;
+            baux = t + (N + 2) * HQ_TILE_GROUPS;
+            bmask = reinterpret_cast<const uint16_t *>(baux);
+            off = (uint64_t)lane * 2;
+        } else {
+            bm = a.match;
+            ms = a.stride;
+            bcin = a.cin;
+            blast = a.last;
+            baux = static_cast<const uint64_t *>(a.aux);
+            bmask = static_cast<const uint16_t *>(a.aux);
+            off = g0;
+        }
+        auto aux1 = [&]() -> uint64_t {
+            if constexpr (FORM == HQ_FORM_TERM_MASK) return bmask[off];
+            return baux[off];
+        };
         bool chg[VEC], fb[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) chg[j] = fb[j] = false;
         if constexpr (VEC == 2) {
-            if (g0 + 1 < a.G) {
+            // both groups of the lane: 16-byte loads of every field
+            auto pair = [&]() {
                 uint64_t m0[N], m1[N];
 #pragma unroll
                 for (int s = 0; s < N; ++s) {
-                    const u64x2 v = ld_stream2(a.match + s * a.stride + g0);
+                    const u64x2 v = ld_stream2(bm + s * ms + off);
                     m0[s] = v.x;
                     m1[s] = v.y;
                 }
-                const u64x2 ci = ld_stream2(a.cin + g0);
-                const u64x2 la = ld_stream2(a.last + g0);
+                const u64x2 ci = ld_stream2(bcin + off);
+                const u64x2 la = ld_stream2(blast + off);
                 u64x2 ax;
                 if constexpr (FORM == HQ_FORM_TERM_MASK) {
                     const uint32_t mm = __builtin_nontemporal_load(
-                        reinterpret_cast<const uint32_t *>(a.mask + g0));
+                        reinterpret_cast<const uint32_t *>(bmask + off));
                     ax = (u64x2){mm & 0xFFFFu, mm >> 16};
                 } else {
-                    ax = ld_stream2(aux_col + g0);
+                    ax = ld_stream2(baux + off);
                 }
                 int n0 = N, n1 = N;
                 if constexpr (PERN) {
@@ -217,44 +267,55 @@ __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, ui
                 decide<N, FORM, PERN>(a, g0, m0, n0, ci.x, la.x, ax.x, co0, chg[0], fb[0]);
                 decide<N, FORM, PERN>(a, g0 + 1, m1, n1, ci.y, la.y, ax.y, co1, chg[1], fb[1]);
                 st_stream2(a.cout + g0, (u64x2){co0, co1});
-            } else if (g0 < a.G) {
-                uint64_t m0[N];
+            };
+            if (wbase + 64 * VEC <= a.G) {   // scalar: the whole wave is inside the batch
+                pair();
+            } else {                         // the batch's last, partial wave: group by group
+                for (int j = 0; j < 2; ++j) {
+                    if (g0 + j < a.G) {
+                        uint64_t m0[N];
 #pragma unroll
-                for (int s = 0; s < N; ++s) m0[s] = a.match[s * a.stride + g0];
-                const int n0 = PERN ? (int)a.nv[g0] : N;
-                uint64_t co;
-                decide<N, FORM, PERN>(a, g0, m0, n0, a.cin[g0], a.last[g0], aux1(g0), co,
-                                      chg[0], fb[0]);
-                a.cout[g0] = co;
+                        for (int s = 0; s < N; ++s) m0[s] = bm[s * ms + off + j];
+                        const int n0 = PERN ? (int)a.nv[g0 + j] : N;
+                        const uint64_t ax = FORM == HQ_FORM_TERM_MASK ? (uint64_t)bmask[off + j]
+                                                                      : baux[off + j];
+                        uint64_t co;
+                        bool c, f;
+                        decide<N, FORM, PERN>(a, g0 + j, m0, n0, bcin[off + j], blast[off + j], ax,
+                                              co, c, f);
+                        a.cout[g0 + j] = co;
+                        chg[j] = c;
+                        fb[j] = f;
+                    }
+                }
             }
+            // the wave's 128 groups are two bitmap words: lane k < 2 writes word k (lane i's
+            // groups are bits 2i, 2i+1: the two ballots interleaved)
             const uint64_t b0 = __ballot(chg[0]), b1 = __ballot(chg[1]);
             const uint64_t f0 = __ballot(fb[0]), f1 = __ballot(fb[1]);
-            if (lane == 0) {
-                const uint64_t w = wbase >> 6;
-                if (a.changed) {
-                    a.changed[w] = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
-                    if (w + 1 < a.nwords)
-                        a.changed[w + 1] = spread32((uint32_t)(b0 >> 32)) |
-                                           (spread32((uint32_t)(b1 >> 32)) << 1);
-                }
-                if (a.fallback) {
-                    a.fallback[w] = spread32((uint32_t)f0) | (spread32((uint32_t)f1) << 1);
-                    if (w + 1 < a.nwords)
-                        a.fallback[w + 1] = spread32((uint32_t)(f0 >> 32)) |
-                                            (spread32((uint32_t)(f1 >> 32)) << 1);
-                }
+            const uint64_t w = (wbase >> 6) + lane;
+            if (lane < 2 && w < ((a.G + 63) >> 6)) {
+                const int sh = 32 * lane;
+                if (a.changed)
+                    a.changed[w] = spread32((uint32_t)(b0 >> sh)) |
+                                   (spread32((uint32_t)(b1 >> sh)) << 1);
+                if (a.fallback)
+                    a.fallback[w] = spread32((uint32_t)(f0 >> sh)) |
+                                    (spread32((uint32_t)(f1 >> sh)) << 1);
             }
         } else {
-            if (g0 < a.G) {
+            auto one = [&]() {
                 uint64_t m0[N];
 #pragma unroll
-                for (int s = 0; s < N; ++s) m0[s] = a.match[s * a.stride + g0];
+                for (int s = 0; s < N; ++s) m0[s] = bm[s * ms + off];
                 const int n0 = PERN ? (int)a.nv[g0] : N;
                 uint64_t co;
-                decide<N, FORM, PERN>(a, g0, m0, n0, a.cin[g0], a.last[g0], aux1(g0), co,
-                                      chg[0], fb[0]);
+                decide<N, FORM, PERN>(a, g0, m0, n0, bcin[off], blast[off], aux1(), co, chg[0],
+                                      fb[0]);
                 a.cout[g0] = co;
-            }
+            };
+            if (wbase + 64 <= a.G) one();
+            else if (g0 < a.G) one();
             const uint64_t b0 = __ballot(chg[0]);
             const uint64_t f0 = __ballot(fb[0]);
             if (lane == 0) {
@@ -265,14 +326,14 @@ __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, ui
     }
 }
 
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, bool TILED>
 __global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
-    commit_blocks<N, FORM, VEC, PERN, kCommitBlock>(a, blockIdx.x, gridDim.x);
+    commit_blocks<N, FORM, VEC, PERN, kCommitBlock, TILED>(a, blockIdx.x, gridDim.x);
 }
 // the 1024-thread twin: two blocks per CU need occupancy 8 (<= 64 VGPRs), so it is asked for
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, bool TILED>
 __global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_big(const CommitK a) {
-    commit_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG>(a, blockIdx.x, gridDim.x);
+    commit_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG, TILED>(a, blockIdx.x, gridDim.x);
 }
 
 // Several uniform-n batches of one step in ONE launch (a step worker's voter-count buckets):
@@ -287,7 +348,7 @@ struct FusedK {
     uint32_t count;
 };
 
-template <int FORM, int BLK>
+template <int FORM, int BLK, bool TILED>
 __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_fused(const FusedK f) {
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
@@ -295,14 +356,14 @@ __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_fuse
     for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
     const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
     switch (f.n[i]) {
-    case 1: commit_blocks<1, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    case 2: commit_blocks<2, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    case 3: commit_blocks<3, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    case 4: commit_blocks<4, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    case 5: commit_blocks<5, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    case 6: commit_blocks<6, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    case 7: commit_blocks<7, FORM, 2, false, BLK>(f.b[i], b, nb); break;
-    default: commit_blocks<8, FORM, 2, false, BLK>(f.b[i], b, nb); break;
+    case 1: commit_blocks<1, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    case 2: commit_blocks<2, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    case 3: commit_blocks<3, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    case 4: commit_blocks<4, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    case 5: commit_blocks<5, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    case 6: commit_blocks<6, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    case 7: commit_blocks<7, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
+    default: commit_blocks<8, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
     }
 }
 
@@ -747,7 +808,7 @@ __device__ __forceinline__ int32_t lag_of(uint64_t last, uint64_t x) {  // clamp
     return d >= (uint64_t)INT32_MAX + 1 ? INT32_MIN : -(int32_t)d;
 }
 
-__global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, CommitK o,
+__global__ __launch_bounds__(kBlock) void k_synth_commit(const hq_synth_spec s, CommitCols o,
                                                          LagOut lo) {
     const uint64_t R = s.ring_len;
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < s.G;
@@ -868,23 +929,27 @@ unsigned grid_for(uint64_t lanes_needed, int block = kBlock, uint64_t max_blocks
     return (unsigned)b;
 }
 
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, bool TILED = false>
 int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
     constexpr int B = commit_blk<N, FORM, PERN>();
     const unsigned grid = grid_for((k.G + VEC - 1) / VEC, B, kMaxBlocks * 256 / B);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     if constexpr (B == kCommitBlock)
-        hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0, ctx->stream, k);
+        hipLaunchKernelGGL((k_commit<N, FORM, VEC, PERN, TILED>), dim3(grid), dim3(B), 0,
+                           ctx->stream, k);
     else
-        hipLaunchKernelGGL((k_commit_big<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0,
+        hipLaunchKernelGGL((k_commit_big<N, FORM, VEC, PERN, TILED>), dim3(grid), dim3(B), 0,
                            ctx->stream, k);
     return hq::post_launch(ctx, "k_commit");
 }
 
+// tiles are always read two groups per lane (the validation requires a 16-byte aligned base)
 template <int N>
-int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool pern) {
+int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool pern, bool tiled) {
 #define HQ_DISPATCH(F)                                                                   \
+    if (tiled) return pern ? launch_commit_t<N, F, 2, true, true>(ctx, k)         \
+                                  : launch_commit_t<N, F, 2, false, true>(ctx, k);       \
     if (vec2) return pern ? launch_commit_t<N, F, 2, true>(ctx, k)                       \
                           : launch_commit_t<N, F, 2, false>(ctx, k);                     \
     return pern ? launch_commit_t<N, F, 1, true>(ctx, k) : launch_commit_t<N, F, 1, false>(ctx, k);
@@ -905,19 +970,35 @@ int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
     if (a->n_max < 1 || a->n_max > HQ_MAX_VOTERS)
         return hq::fail(ctx, HQ_E_INVAL, "hq_commit: n_max must be 1..8");
+    if (a->layout != HQ_LAYOUT_COLUMNS && a->layout != HQ_LAYOUT_TILES)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit: unknown layout");
     if (a->G == 0) return HQ_OK;
-    if (!a->match || !a->committed_in || !a->committed_out || !a->last_index)
-        return hq::fail(ctx, HQ_E_INVAL, "hq_commit: NULL match/committed/last_index");
-    if (a->match_stride < a->G) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: match_stride < G");
+    const bool tiles = a->layout == HQ_LAYOUT_TILES;
+    if (tiles) {
+        if (!a->match || !a->committed_out)
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: NULL tiles (match) / committed_out");
+        if (!hq::aligned16(a->match) || !hq::aligned16(a->committed_out) ||
+            (a->n_voting && (reinterpret_cast<uintptr_t>(a->n_voting) & 1)))
+            return hq::fail(ctx, HQ_E_INVAL,
+                            "hq_commit: tiles and committed_out must be 16-byte aligned, "
+                            "n_voting 2-byte aligned");
+    } else {
+        if (!a->match || !a->committed_in || !a->committed_out || !a->last_index)
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: NULL match/committed/last_index");
+        if (a->match_stride < a->G)
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: match_stride < G");
+    }
     if (a->form == HQ_FORM_TERM_START) {
-        if (!a->term_start) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term_start is NULL");
+        if (!tiles && !a->term_start)
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term_start is NULL");
     } else if (a->form == HQ_FORM_TERM_RING || a->form == HQ_FORM_TERM_RING32) {
-        if (!a->term || (a->form == HQ_FORM_TERM_RING ? !a->ring : !a->ring32))
+        if ((!tiles && !a->term) || (a->form == HQ_FORM_TERM_RING ? !a->ring : !a->ring32))
             return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term/ring NULL");
         if (a->ring_len < 1 || a->ring_len > 1024 || (a->ring_len & (a->ring_len - 1)))
             return hq::fail(ctx, HQ_E_INVAL, "hq_commit: ring_len must be a power of two <= 1024");
     } else if (a->form == HQ_FORM_TERM_MASK) {
-        if (!a->term_mask) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term_mask is NULL");
+        if (!tiles && !a->term_mask)
+            return hq::fail(ctx, HQ_E_INVAL, "hq_commit: term_mask is NULL");
         if (a->ring_len < 1 || a->ring_len > 16 || (a->ring_len & (a->ring_len - 1)))
             return hq::fail(ctx, HQ_E_INVAL, "hq_commit: mask form needs ring_len <= 16 (power of two)");
     } else {
@@ -931,7 +1012,29 @@ int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
 namespace {
 
 CommitK commit_k(const hq_commit_args *a) {
-    CommitK k;
+    CommitK k{};
+    const bool tiles = a->layout == HQ_LAYOUT_TILES;
+    k.G = a->G;
+    k.stride = tiles ? hq_commit_tile_words(a->n_max, a->form) : a->match_stride;
+    k.R = a->ring_len;
+    k.match = a->match;
+    k.nv = a->n_voting;
+    k.cin = a->committed_in;
+    k.cout = a->committed_out;
+    k.last = a->last_index;
+    k.aux = a->form == HQ_FORM_TERM_START ? static_cast<const void *>(a->term_start)
+          : a->form == HQ_FORM_TERM_MASK  ? static_cast<const void *>(a->term_mask)
+                                          : static_cast<const void *>(a->term);
+    k.ring = a->form == HQ_FORM_TERM_RING32 ? static_cast<const void *>(a->ring32)
+                                            : static_cast<const void *>(a->ring);
+    k.changed = a->changed;
+    k.fallback = a->fallback;
+    return k;
+}
+
+// every field of a column batch (generator, tile packer)
+CommitCols commit_cols(const hq_commit_args *a) {
+    CommitCols k{};
     k.G = a->G;
     k.stride = a->match_stride;
     k.nwords = hq::words64(a->G);
@@ -949,11 +1052,13 @@ CommitK commit_k(const hq_commit_args *a) {
     k.fallback = a->fallback;
     k.mask = a->term_mask;
     k.ring32 = a->ring32;
+    k.tile_words = hq_commit_tile_words(a->n_max, a->form);
     return k;
 }
 
 // every column of the batch can be read two groups per lane with 16-byte loads
 bool commit_vec2(const hq_commit_args *a) {
+    if (a->layout == HQ_LAYOUT_TILES) return true;   // alignment checked by validate_commit
     const bool aux_ok = a->form == HQ_FORM_TERM_START ? hq::aligned16(a->term_start)
                       : a->form == HQ_FORM_TERM_MASK
                           ? (reinterpret_cast<uintptr_t>(a->term_mask) & 3) == 0
@@ -972,15 +1077,16 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     const CommitK k = commit_k(a);
     const bool vec2 = commit_vec2(a);
     const bool pern = a->n_voting != nullptr;
+    const bool tiled = a->layout == HQ_LAYOUT_TILES;
     switch (a->n_max) {
-    case 1: return launch_commit_n<1>(ctx, k, a->form, vec2, pern);
-    case 2: return launch_commit_n<2>(ctx, k, a->form, vec2, pern);
-    case 3: return launch_commit_n<3>(ctx, k, a->form, vec2, pern);
-    case 4: return launch_commit_n<4>(ctx, k, a->form, vec2, pern);
-    case 5: return launch_commit_n<5>(ctx, k, a->form, vec2, pern);
-    case 6: return launch_commit_n<6>(ctx, k, a->form, vec2, pern);
-    case 7: return launch_commit_n<7>(ctx, k, a->form, vec2, pern);
-    default: return launch_commit_n<8>(ctx, k, a->form, vec2, pern);
+    case 1: return launch_commit_n<1>(ctx, k, a->form, vec2, pern, tiled);
+    case 2: return launch_commit_n<2>(ctx, k, a->form, vec2, pern, tiled);
+    case 3: return launch_commit_n<3>(ctx, k, a->form, vec2, pern, tiled);
+    case 4: return launch_commit_n<4>(ctx, k, a->form, vec2, pern, tiled);
+    case 5: return launch_commit_n<5>(ctx, k, a->form, vec2, pern, tiled);
+    case 6: return launch_commit_n<6>(ctx, k, a->form, vec2, pern, tiled);
+    case 7: return launch_commit_n<7>(ctx, k, a->form, vec2, pern, tiled);
+    default: return launch_commit_n<8>(ctx, k, a->form, vec2, pern, tiled);
     }
 }
 
@@ -995,7 +1101,7 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
     for (uint32_t i = 0; fusable && i < count; ++i)
         fusable = args[i].G > 0 && !args[i].n_voting && commit_vec2(args + i) &&
-                  args[i].form == args[0].form;
+                  args[i].form == args[0].form && args[i].layout == args[0].layout;
     if (!fusable) return hq_commit_many_dev(ctx, args, count);
     FusedK f{};
     f.count = count;
@@ -1018,7 +1124,12 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
 #define HQ_FUSED(F, BLK)                                                                       \
-    hipLaunchKernelGGL((k_commit_fused<F, BLK>), dim3(blocks), dim3(BLK), 0, ctx->stream, f);
+    if (args[0].layout == HQ_LAYOUT_TILES)                                                     \
+        hipLaunchKernelGGL((k_commit_fused<F, BLK, true>), dim3(blocks), dim3(BLK), 0,         \
+                           ctx->stream, f);                                                    \
+    else                                                                                       \
+        hipLaunchKernelGGL((k_commit_fused<F, BLK, false>), dim3(blocks), dim3(BLK), 0,        \
+                           ctx->stream, f);
     switch (args[0].form) {
     case HQ_FORM_TERM_START:
         if (big) {
@@ -1304,7 +1415,7 @@ extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,
         s->cid_stride < 1 || (s->mixed_n && s->n_max < 7) || (a->match && a->match_stride < s->G))
         return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit: bad spec");
     if (s->G == 0) return HQ_OK;
-    CommitK o{};
+    CommitCols o{};
     o.G = s->G;
     o.stride = a->match_stride;
     o.match = a->match;
@@ -1325,6 +1436,49 @@ extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,
     return hq::post_launch(ctx, "k_synth_commit");
 }
 
+// Columns -> HQ_LAYOUT_TILES tiles, one thread per tile word (include/hipquorum.h). Builds
+// tiled inputs from column batches on the device (benchmark inputs, device-side packers).
+__global__ __launch_bounds__(kBlock) void k_tile_commit(const CommitCols c, uint64_t *tiles,
+                                                        uint64_t ntiles, uint32_t n, int form) {
+    const uint64_t tw = c.tile_words, total = ntiles * tw;
+    for (uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x; w < total;
+         w += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t t = w / tw, r = w % tw, row = r / HQ_TILE_GROUPS;
+        uint64_t v = 0;
+        if (form == HQ_FORM_TERM_MASK && row >= n + 2) {   // 4 u16 masks per word
+            const uint64_t g = t * HQ_TILE_GROUPS + 4 * (r - (uint64_t)(n + 2) * HQ_TILE_GROUPS);
+            for (int k = 3; k >= 0; --k) v = (v << 16) | (g + k < c.G ? c.mask[g + k] : 0);
+        } else {
+            const uint64_t g = t * HQ_TILE_GROUPS + r % HQ_TILE_GROUPS;
+            if (g < c.G) {
+                v = row < n       ? c.match[row * c.stride + g]
+                  : row == n      ? c.cin[g]
+                  : row == n + 1  ? c.last[g]
+                  : form == HQ_FORM_TERM_START ? c.tstart[g] : c.term[g];
+            }
+        }
+        tiles[w] = v;
+    }
+}
+
+extern "C" int hq_tile_commit_dev(hq_ctx *ctx, const hq_commit_args *a, uint64_t *tiles) {
+    if (!ctx) return HQ_E_INVAL;
+    if (!a || !tiles) return hq::fail(ctx, HQ_E_INVAL, "hq_tile_commit: NULL argument");
+    if (a->layout != HQ_LAYOUT_COLUMNS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_commit: input must be the column layout");
+    hq_commit_args chk = *a;
+    chk.committed_out = chk.committed_out ? chk.committed_out : tiles;  // not written here
+    int rc = validate_commit(ctx, &chk);
+    if (rc || a->G == 0) return rc;
+    const CommitCols k = commit_cols(a);
+    const uint64_t ntiles = hq_commit_tiles(a->G);
+    rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_commit, dim3(grid_for(ntiles * k.tile_words)), dim3(kBlock), 0,
+                       ctx->stream, k, tiles, ntiles, a->n_max, (int)a->form);
+    return hq::post_launch(ctx, "k_tile_commit");
+}
+
 extern "C" int hq_synth_commit_lag_dev(hq_ctx *ctx, const hq_synth_spec *s,
                                        const hq_commit_lag_args *a, uint64_t *last_index) {
     if (!ctx) return HQ_E_INVAL;
@@ -1334,7 +1488,7 @@ extern "C" int hq_synth_commit_lag_dev(hq_ctx *ctx, const hq_synth_spec *s,
         (a->lag_mask && s->ring_len > 16))
         return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit_lag: bad spec");
     if (s->G == 0) return HQ_OK;
-    CommitK o{};
+    CommitCols o{};
     o.G = s->G;
     o.nv = a->n_voting;
     LagOut lo{const_cast<int32_t *>(a->lag), a->lag_stride, const_cast<int32_t *>(a->cin_lag),

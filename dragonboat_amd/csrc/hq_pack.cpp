@@ -200,3 +200,33 @@ extern "C" int hq_unpack_lags(uint64_t G, const uint64_t *last_index, const int3
             committed[g] = last_index[g] - (uint64_t)(int64_t)cout_lag[g];
     return HQ_OK;
 }
+
+// Columns -> HQ_LAYOUT_TILES tiles on the host (the twin of k_tile_commit): a step worker that
+// packs columns can hand the kernel one contiguous staging block per 128 groups instead.
+extern "C" int hq_tile_commit_host(const hq_commit_args *a, uint64_t *tiles) {
+    if (!a || !tiles || a->layout != HQ_LAYOUT_COLUMNS || a->n_max < 1 ||
+        a->n_max > HQ_MAX_VOTERS || a->form > HQ_FORM_TERM_RING32)
+        return HQ_E_INVAL;
+    if (a->G == 0) return HQ_OK;
+    const bool mask = a->form == HQ_FORM_TERM_MASK;
+    const uint64_t *aux = a->form == HQ_FORM_TERM_START ? a->term_start : a->term;
+    if (!a->match || !a->committed_in || !a->last_index || a->match_stride < a->G ||
+        (mask ? !a->term_mask : !aux))
+        return HQ_E_INVAL;
+    const uint32_t n = a->n_max;
+    const uint64_t tw = hq_commit_tile_words(n, a->form), T = HQ_TILE_GROUPS;
+    for (uint64_t t = 0; t < hq_commit_tiles(a->G); ++t) {
+        uint64_t *tile = tiles + t * tw;
+        std::memset(tile, 0, tw * 8);
+        const uint64_t g0 = t * T, cnt = a->G - g0 < T ? a->G - g0 : T;
+        for (uint32_t s = 0; s < n; ++s)
+            std::memcpy(tile + s * T, a->match + s * a->match_stride + g0, cnt * 8);
+        std::memcpy(tile + n * T, a->committed_in + g0, cnt * 8);
+        std::memcpy(tile + (n + 1) * T, a->last_index + g0, cnt * 8);
+        if (mask)
+            std::memcpy(tile + (n + 2) * T, a->term_mask + g0, cnt * 2);
+        else
+            std::memcpy(tile + (n + 2) * T, aux + g0, cnt * 8);
+    }
+    return HQ_OK;
+}

@@ -268,6 +268,50 @@ struct Stage {
 int h2d(hq_ctx *ctx, void *d, const void *h, size_t b) { return hq_memcpy_async(ctx, d, h, b, 0); }
 int d2h(hq_ctx *ctx, void *h, const void *d, size_t b) { return hq_memcpy_async(ctx, h, d, b, 1); }
 
+// HQ_LAYOUT_TILES from host memory: the tiles are one block, so the whole input is one H2D copy
+int commit_tiles_host(hq_ctx *ctx, const hq_commit_args *a) {
+    if (!a->match || !a->committed_out || a->n_max < 1 || a->n_max > HQ_MAX_VOTERS ||
+        a->form > HQ_FORM_TERM_RING32)
+        return hq_commit_dev(ctx, a);  // same validation and message
+    const bool ring = a->form == HQ_FORM_TERM_RING, ring32 = a->form == HQ_FORM_TERM_RING32;
+    if ((ring && !a->ring) || (ring32 && !a->ring32)) return hq_commit_dev(ctx, a);
+    if ((ring || ring32) && (a->ring_len < 1 || a->ring_len > 1024)) return hq_commit_dev(ctx, a);
+    const uint64_t G = a->G, nw = hq::words64(G);
+    const size_t tiles = hq_commit_tiles(G) * hq_commit_tile_words(a->n_max, a->form) * 8;
+    const size_t ring_bytes = ring ? G * 8 * a->ring_len : ring32 ? G * 4 * a->ring_len : 0;
+    const size_t need = Stage::pad(tiles) + Stage::pad(G * 8) + 2 * Stage::pad(nw * 8) +
+                        Stage::pad(G) + Stage::pad(ring_bytes);
+    int rc = hq::ensure_workspace(ctx, need);
+    if (rc) return rc;
+    Stage s(ctx);
+    hq_commit_args d = *a;
+    uint64_t *dt = s.take<uint64_t>(tiles), *dco = s.take<uint64_t>(G * 8);
+    d.match = dt;
+    d.committed_out = dco;
+    rc = h2d(ctx, dt, a->match, tiles);
+    if (ring || ring32) {
+        void *dr = s.take<char>(ring_bytes);
+        if (ring) d.ring = static_cast<const uint64_t *>(dr);
+        else d.ring32 = static_cast<const uint32_t *>(dr);
+        if (!rc) rc = h2d(ctx, dr, ring ? (const void *)a->ring : (const void *)a->ring32,
+                          ring_bytes);
+    }
+    uint8_t *dnv = s.take<uint8_t>(G);
+    if (a->n_voting) {
+        d.n_voting = dnv;
+        if (!rc) rc = h2d(ctx, dnv, a->n_voting, G);
+    }
+    uint64_t *dchg = s.take<uint64_t>(nw * 8), *dfb = s.take<uint64_t>(nw * 8);
+    d.changed = a->changed ? dchg : nullptr;
+    d.fallback = a->fallback ? dfb : nullptr;
+    if (!rc) rc = hq_commit_dev(ctx, &d);
+    if (!rc) rc = d2h(ctx, a->committed_out, dco, G * 8);
+    if (!rc && a->changed) rc = d2h(ctx, a->changed, dchg, nw * 8);
+    if (!rc && a->fallback) rc = d2h(ctx, a->fallback, dfb, nw * 8);
+    if (!rc) rc = hq_sync(ctx);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -276,6 +320,7 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (!ctx) return HQ_E_INVAL;
     if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
     if (a->G == 0) return HQ_OK;
+    if (a->layout == HQ_LAYOUT_TILES) return commit_tiles_host(ctx, a);
     if (!a->match || !a->committed_in || !a->committed_out || !a->last_index ||
         a->n_max < 1 || a->n_max > HQ_MAX_VOTERS || a->match_stride < a->G)
         return hq_commit_dev(ctx, a);  // same validation and message

@@ -29,6 +29,10 @@ HQ_FORM_TERM_START = 0
 HQ_FORM_TERM_RING = 1
 HQ_FORM_TERM_MASK = 2
 HQ_FORM_TERM_RING32 = 3
+HQ_LAYOUT_COLUMNS = 0
+HQ_LAYOUT_TILES = 1
+HQ_TILE_GROUPS = 128
+HQ_ABI_VERSION = 4
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -47,7 +51,7 @@ class CommitArgs(ctypes.Structure):
         ("n_max", ctypes.c_uint32),
         ("form", ctypes.c_uint32),
         ("ring_len", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("layout", ctypes.c_uint32),
         ("match_stride", ctypes.c_uint64),
         ("match", _vp),
         ("n_voting", _vp),
@@ -218,6 +222,8 @@ SIGNATURES = {
                                            ctypes.c_uint32, ctypes.c_uint64, _vp]),
     "hq_pack_commit": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.POINTER(CommitArgs)]),
     "hq_pack_ring32": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp]),
+    "hq_tile_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), _vp]),
+    "hq_tile_commit_host": (ctypes.c_int, [ctypes.POINTER(CommitArgs), _vp]),
     "hq_pack_votes": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hq_pack_acks": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_uint32, _vp]),
@@ -411,6 +417,10 @@ class Context:
 
     def commit_host(self, args: CommitArgs) -> None:
         self._check(lib.hq_commit(self.h, ctypes.byref(args)))
+
+    def tile_commit_dev(self, columns: CommitArgs, tiles) -> None:
+        """hq_tile_commit_dev: the column batch's inputs cut into HQ_LAYOUT_TILES tiles."""
+        self._check(lib.hq_tile_commit_dev(self.h, ctypes.byref(columns), _p(tiles)))
 
     def readindex_dev(self, G, ack, n_voting, n_uniform, confirmed, fallback=None) -> None:
         self._check(lib.hq_readindex_dev(self.h, G, _p(ack), _p(n_voting), n_uniform,
@@ -624,6 +634,26 @@ def words64(G: int) -> int:
     return (G + 63) // 64
 
 
+def commit_tile_words(n_max: int, form: int) -> int:
+    """hq_commit_tile_words: u64 words of one tile of HQ_TILE_GROUPS groups."""
+    if form == HQ_FORM_TERM_MASK:
+        return (n_max + 2) * HQ_TILE_GROUPS + 32
+    return (n_max + 3) * HQ_TILE_GROUPS
+
+
+def commit_tiles(G: int) -> int:
+    return (G + HQ_TILE_GROUPS - 1) // HQ_TILE_GROUPS
+
+
+def tile_commit_host(columns: CommitArgs) -> np.ndarray:
+    """hq_tile_commit_host over host column arrays (pointers in ``columns``): the tiles as a
+    uint64 array."""
+    out = np.zeros(commit_tiles(columns.G) * commit_tile_words(columns.n_max, columns.form),
+                   np.uint64)
+    _chk(lib.hq_tile_commit_host(ctypes.byref(columns), _p(out)), "hq_tile_commit_host")
+    return out
+
+
 def words32(G: int) -> int:
     return (G + 31) // 32
 
@@ -649,6 +679,7 @@ class CommitBuffers:
     term: Optional[DeviceArray] = None
     term_mask: Optional[DeviceArray] = None
     ring32: Optional[DeviceArray] = None
+    tiles: Optional[DeviceArray] = None    # HQ_LAYOUT_TILES copy of the input columns
 
     def args(self) -> CommitArgs:
         a = CommitArgs()
@@ -671,16 +702,29 @@ class CommitBuffers:
         a.ring32 = self.ring32.ptr if self.ring32 else None
         return a
 
+    def tile_args(self) -> CommitArgs:
+        """The same batch in HQ_LAYOUT_TILES: the inputs from ``tiles`` (filled by
+        ``Context.tile_commit_dev(b.args(), b.tiles)``), outputs as in ``args``."""
+        a = self.args()
+        a.layout = HQ_LAYOUT_TILES
+        a.match = self.tiles.ptr
+        a.match_stride = 0
+        a.committed_in = a.last_index = a.term_start = a.term = a.term_mask = None
+        return a
+
     def arrays(self):
         return [x for x in (self.match, self.committed_in, self.committed_out, self.last_index,
                             self.term_start, self.term, self.ring, self.term_mask, self.n_voting,
-                            self.changed, self.fallback, self.ring32) if x is not None]
+                            self.changed, self.fallback, self.ring32, self.tiles)
+                if x is not None]
 
 
 def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
-                 per_group_n: bool = False, with_both_aux: bool = False) -> CommitBuffers:
+                 per_group_n: bool = False, with_both_aux: bool = False,
+                 tiled: bool = False) -> CommitBuffers:
     """Allocate the SoA columns of one commit batch (match is slot-major [n_max][G]).
-    with_both_aux allocates the columns of all four term forms (to compare them)."""
+    with_both_aux allocates the columns of all four term forms (to compare them); tiled adds
+    the HQ_LAYOUT_TILES buffer of the form."""
     need_ts = form == HQ_FORM_TERM_START or with_both_aux
     need_ring = form == HQ_FORM_TERM_RING or with_both_aux
     need_ring32 = form == HQ_FORM_TERM_RING32 or with_both_aux
@@ -699,6 +743,8 @@ def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16
         term=ctx.empty(G, np.uint64) if need_ring or need_ring32 else None,
         term_mask=ctx.empty(G, np.uint16) if need_mask else None,
         ring32=ctx.empty(G * ring_len, np.uint32) if need_ring32 else None,
+        tiles=ctx.empty(commit_tiles(G) * commit_tile_words(n_max, form), np.uint64)
+        if tiled else None,
     )
     return b
 

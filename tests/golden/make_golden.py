@@ -136,6 +136,35 @@ def kats():
         commit_case("raft_test.go:2791-2806", [1, 1, 0], [0], {0: 0, 1: 1}, 1, 0, 0,
                     note="witness 4 added after the no-op: n = 4, quorum 3 -> no commit"),
     ]
+    # TestCommitAfterRemoveNode — raft_etcd_test.go:2611-2668 (derived). Two voters; leader at
+    # term 1 writes its no-op (1), the RemoveNode entry (2) and "hello" (3). Node 2 acks the
+    # config change: matched {self 3, node 2: 2} -> 2 commits, entries 1-2 ("two committed
+    # entries", :2653-2656). removeNode(2) re-runs tryCommit over the one remaining voter
+    # (raft.go:1194-1198): q = 3 commits "hello" (:2666-2671).
+    log_rm = {0: 0, 1: 1, 2: 1, 3: 1}
+    out["TestCommitAfterRemoveNode"] = [
+        commit_case("raft_etcd_test.go:2646-2656", [3, 2], [], log_rm, 1, 0, 2,
+                    note="node 2 acks the config-change entry"),
+        commit_case("raft_etcd_test.go:2663-2671", [3], [], log_rm, 1, 2, 3,
+                    note="after removeNode(2): one voter, quorum 1"),
+    ]
+    # TestCommitTo — logentry_etcd_test.go:374-406 (derived): previous entries {1:t1, 2:t2,
+    # 3:t3}, committed 2. commitTo(3) -> 3; commitTo(1) -> 2 (never decreases); commitTo(4)
+    # panics, which tryCommit never reaches: an index above lastIndex has term 0
+    # (logentry.go:144-147), so q = 4 fails the term check and committed stays 2.
+    log_ct = {0: 0, 1: 1, 2: 2, 3: 3}
+    out["TestCommitTo"] = [
+        commit_case("logentry_etcd_test.go:379", [3], [], log_ct, 3, 2, 3),
+        commit_case("logentry_etcd_test.go:380", [3, 1, 1], [], log_ct, 3, 2, 2,
+                    note="q = 1 <= committed: never decrease"),
+        commit_case("logentry_etcd_test.go:381", [3, 4, 4], [], log_ct, 3, 2, 2,
+                    note="q = 4 > lastIndex: term(4) = 0, the commitTo panic is unreachable"),
+    ]
+    # TestTryCommitResetsMatchArray — raft_test.go:136-145 (derived): a fresh 3-voter leader at
+    # term 1 (no-op at 1, no acks): tryCommit sizes matched to 3 voters; q = 0, nothing commits
+    out["TestTryCommitResetsMatchArray"] = [
+        commit_case("raft_test.go:137-144", [1, 0, 0], [], {0: 0, 1: 1}, 1, 0, 0),
+    ]
 
     # ---- sortMatchValues / quorum — raft_test.go:2033-2055, :1525-1549 ---------------------
     out["TestUnrolledBubbleSortMatchValue"] = [

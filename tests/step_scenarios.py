@@ -1,14 +1,10 @@
 """Step-level scenarios restating the reference's own raft tests (file:line on each). Every
 scenario runs on any backend of tests/step_harness.py: the CPU oracle (test_oracle_step.py pins
 it against these) and the GPU step worker (test_gpu_worker.py)."""
-import json
-import os
-
+from kats import COMMIT_TABLES, KATS
 from oracle.qref import QREF_CANDIDATE as CANDIDATE
 from oracle.qref import QREF_FOLLOWER as FOLLOWER
 from oracle.qref import QREF_LEADER as LEADER
-
-KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
 
 REMOTE, OBSERVER, WITNESS = 0, 1, 2
 RREP, VRESP, HBRESP, READIDX = 13, 15, 18, 19
@@ -74,14 +70,10 @@ def _term_start(case):
 def commit_cases():
     """The commit tables of tests/golden (TestLeaderAcknowledgeCommit, TestLeaderOnlyCommits-
     LogFromCurrentTerm, TestLeaderCommitPrecedingEntries, TestCommitWithoutNewTermEntry,
-    TestFullMemberWithOneWitness, TestLeaderAppResp ...): the leader's followers report their
-    match in ReplicateResp messages of one step."""
-    tables = ["TestLeaderAcknowledgeCommit", "TestLeaderOnlyCommitsLogFromCurrentTerm",
-              "TestLeaderCommitPrecedingEntries", "TestCommitWithoutNewTermEntry",
-              "TestCannotCommitWithoutNewTermEntry", "TestFullMemberWithOneWitness",
-              "TestLeaderAppResp", "TestCommit"]
+    TestFullMemberWithOneWitness, TestLeaderAppResp, TestCommitAfterRemoveNode ...): the leader's
+    followers report their match in ReplicateResp messages of one step."""
     k = 0
-    for t in tables:
+    for t in COMMIT_TABLES:
         for c in KATS[t]:
             ts, mono = _term_start(c)
             rem, wit = c["remotes"], c["witnesses"]
@@ -148,6 +140,61 @@ def readindex_cases():
                        msg(HBRESP, 5, 2, hint=8, high=80)]],
                want_committed=4, want_resps=[(2, 4, 8, 80), (4, 4, 8, 80)], want_pending=0,
                src="readindex_test.go:125-162, raft.go:1740-1760")
+    yield _read_only_option_safe()
+    # TestObserverCanReadIndexQuorum2 (raft_test.go:500-535): voters 1 (leader) and 2, observer
+    # 3. Ten proposals; the observer's ReplicateResp alone commits nothing (observers are not
+    # voting members, raft.go:888-909), node 2's commits all ten; the observer's ReadIndex is
+    # forwarded to the leader, confirmed by node 2's heartbeat ack (observers never ack a ctx,
+    # raft.go:843-847) and answered with the committed index.
+    obs = [(1, 1, REMOTE, 0), (2, 1, REMOTE, 0), (3, 1, OBSERVER, 0)]
+    yield dict(name="ri_observer2_noack", group=(507, 1, 1, LEADER, 1, 1, 1, obs),
+               steps=[[("propose", 10)], [msg(RREP, 3, 1, 11)]], want_committed=1,
+               src="raft_test.go:500-535")
+    yield dict(name="ri_observer2", group=(508, 1, 1, LEADER, 1, 1, 1, obs),
+               steps=[[("propose", 10)], [msg(RREP, 3, 1, 11)], [msg(RREP, 2, 1, 11)],
+                      [msg(READIDX, 3, 1, hint=12345), msg(HBRESP, 2, 1, hint=12345)]],
+               want_committed=11, want_resps=[(3, 11, 12345, 0)], want_pending=0,
+               src="raft_test.go:500-535")
+    # TestHasCommittedEntryAtCurrentTerm (raft_test.go:1863-1881): a new 2-voter leader has no
+    # committed entry at its term until node 2 acks the no-op (hasCommittedEntryAtCurrentTerm,
+    # raft.go:1612-1621), so a ReadIndex before that ack is dropped and one after it is queued
+    yield dict(name="ri_committed_at_term", group=(509, 1, 0, FOLLOWER, 0, 0, 0, members(2)),
+               steps=[[("campaign",)], [msg(VRESP, 2, 1)], [("read", 101, 1002)],
+                      [msg(RREP, 2, 1, 1)], [("read", 103, 1004)]],
+               want_state=LEADER, want_committed=1, want_dropped=[(101, 1002, 0, D_NOT_READY)],
+               want_pending=1, src="raft_test.go:1863-1881")
+    # TestReadIndexIsResetAfterRaftStateChange (readindex_test.go:164-175): a pending request
+    # is dropped by reset() when a higher-term message turns the leader into a follower
+    yield dict(name="ri_reset", group=(510, 1, 1, LEADER, 1, 1, 1,
+                                       [(1, 1, REMOTE, 0), (2, 1, REMOTE, 0), (3, 1, REMOTE, 0)]),
+               steps=[[("read", 10001, 10002)], [msg(HBRESP, 2, 2)]],
+               want_state=FOLLOWER, want_pending=0, src="readindex_test.go:164-175")
+
+
+def _read_only_option_safe():
+    """TestReadOnlyOptionSafe (raft_etcd_test.go:1847-1899): leader 1 of voters {1, 2, 3} at term
+    1 with its no-op committed. Six rounds of ten proposals, each committed by both followers'
+    acks, then a ReadIndex at node 1 (local), 2 or 3 (forwarded to the leader), confirmed by the
+    heartbeat acks: the read index is the committed index 11, 21, ..., 61 with the request's ctx
+    (getTestSystemCtx(v) = {v, v + 1}, readindex_test.go:23-28); a follower's read comes back
+    as the ReadIndexResp of raft.go:1751-1757."""
+    table = [(1, 11, 10001), (2, 21, 10002), (3, 31, 10003),
+             (1, 41, 10004), (2, 51, 10005), (3, 61, 10006)]
+    steps, ready, resps = [], [], []
+    for who, wri, v in table:
+        steps.append([("propose", 10)])
+        steps.append([msg(RREP, 2, 1, wri), msg(RREP, 3, 1, wri)])
+        acks = [msg(HBRESP, 2, 1, hint=v, high=v + 1), msg(HBRESP, 3, 1, hint=v, high=v + 1)]
+        if who == 1:
+            steps.append([("read", v, v + 1)] + acks)
+            ready.append((wri, v, v + 1))
+        else:
+            steps.append([msg(READIDX, who, 1, hint=v, high=v + 1)] + acks)
+            resps.append((who, wri, v, v + 1))
+    return dict(name="ri_read_only_safe", group=(511, 1, 1, LEADER, 1, 1, 1,
+                                                 [(i, 1, REMOTE, 0) for i in (1, 2, 3)]),
+                steps=steps, want_committed=61, want_ready=ready, want_resps=resps,
+                want_pending=0, src="raft_etcd_test.go:1847-1899")
 
 
 def single_node_commit_cases():

@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == 3
+    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 4
 
 
 LAYOUT_C = r"""
@@ -45,7 +45,11 @@ int main(void) {
   F(hq_commit_args, n_voting) F(hq_commit_args, committed_in) F(hq_commit_args, committed_out)
   F(hq_commit_args, last_index) F(hq_commit_args, term_start) F(hq_commit_args, term)
   F(hq_commit_args, ring) F(hq_commit_args, changed) F(hq_commit_args, fallback)
-  F(hq_commit_args, term_mask) F(hq_commit_args, ring32)
+  F(hq_commit_args, term_mask) F(hq_commit_args, ring32) F(hq_commit_args, layout)
+  for (unsigned n = 1; n <= 8; ++n)
+    for (unsigned f = 0; f <= 3; ++f)
+      printf("tile_words_%u_%u %llu\n", n, f, (unsigned long long)hq_commit_tile_words(n, f));
+  printf("tiles_129 %llu\n", (unsigned long long)hq_commit_tiles(129));
   printf("hq_commit_lag_args %zu\n", sizeof(hq_commit_lag_args));
   F(hq_commit_lag_args, G) F(hq_commit_lag_args, n_max) F(hq_commit_lag_args, form)
   F(hq_commit_lag_args, ring_len) F(hq_commit_lag_args, lag_stride) F(hq_commit_lag_args, lag)
@@ -87,6 +91,10 @@ def test_struct_layout_matches_c(hq, tmp_path):
     for name, dt in dtypes.items():
         assert int(c[name]) == dt.itemsize, name
     assert int(c["hq_match_update"]) == 16 and int(c["hq_append_update"]) == 16
+    for n in range(1, 9):
+        for f in range(4):
+            assert int(c[f"tile_words_{n}_{f}"]) == hq.commit_tile_words(n, f)
+    assert int(c["tiles_129"]) == hq.commit_tiles(129) == 2
     for key, val in c.items():
         if "." in key:
             t, m = key.split(".")

@@ -3,17 +3,15 @@
 Bar: bit-exact — committed', changed and fallback bitmaps, confirmed bits, 2-bit vote outcomes,
 has-quorum bits and the rewritten active flags must equal the oracle's for every group.
 """
-import json
-import os
 
 import numpy as np
 import pytest
 
+from kats import KATS, commit_cases
 from oracle import qref
 
 pytestmark = pytest.mark.gpu
 
-KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
 SEED = 0x5EED0000
 
 
@@ -203,13 +201,7 @@ def _term_start_representable(c):
 
 
 def test_commit_reference_kats_on_gpu(gpu_ctx, hq):
-    cases = []
-    for table in ("TestCommit", "TestLeaderOnlyCommitsLogFromCurrentTerm",
-                  "TestLeaderAcknowledgeCommit", "TestLeaderCommitPrecedingEntries",
-                  "TestSingleNodeCommit", "TestCannotCommitWithoutNewTermEntry",
-                  "TestCommitWithoutNewTermEntry", "TestLeaderAppResp",
-                  "TestFullMemberWithOneWitness", "TestVotingMemberLengthMismatch"):
-        cases += KATS[table]
+    cases = commit_cases()
     inp = _kat_inputs(cases)
     want = np.array([c["want_committed"] for c in cases], np.uint64)
     for form in (1, 2, 3):   # ring gathers and current-term mask: every case representable
@@ -614,13 +606,7 @@ def test_commit_lag_vec1_and_ragged(gpu_ctx, hq, form):
 
 
 def test_commit_lag_reference_kats(gpu_ctx, hq):
-    cases = []
-    for table in ("TestCommit", "TestLeaderOnlyCommitsLogFromCurrentTerm",
-                  "TestLeaderAcknowledgeCommit", "TestLeaderCommitPrecedingEntries",
-                  "TestSingleNodeCommit", "TestCannotCommitWithoutNewTermEntry",
-                  "TestCommitWithoutNewTermEntry", "TestLeaderAppResp",
-                  "TestFullMemberWithOneWitness", "TestVotingMemberLengthMismatch"):
-        cases += KATS[table]
+    cases = commit_cases()
     inp = _kat_inputs(cases)
     want = np.array([c["want_committed"] for c in cases], np.uint64)
     com, chg, fb = run_commit_lag(gpu_ctx, hq, inp, 2, per_group_n=True)

@@ -1,0 +1,150 @@
+"""HQ_LAYOUT_TILES commit decisions on the GPU, bit-exact with the CPU oracle: every term form,
+voter counts 1-8, uniform and per-group n, ragged last tiles, the fused multi-bucket launch, the
+host-staged entry point, and the full BASELINE size. The device tile packer is checked word for
+word against the host one first."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import qref
+from test_gpu_parity import popcount, upload_commit
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0000
+
+
+def tiled_args(hq, cols, tiles):
+    a = hq.CommitArgs.from_buffer_copy(cols)
+    a.layout = hq.HQ_LAYOUT_TILES
+    a.match = tiles.ptr
+    a.match_stride = 0
+    a.committed_in = a.last_index = a.term_start = a.term = a.term_mask = None
+    return a
+
+
+def host_tiles(hq, inp, form):
+    a = hq.CommitArgs()
+    a.G, a.n_max, a.form, a.ring_len = inp.G, inp.n_max, form, inp.R
+    a.match_stride = inp.G
+    a.match = inp.match.ctypes.data
+    a.committed_in = inp.committed_in.ctypes.data
+    a.last_index = inp.last_index.ctypes.data
+    a.term_start = inp.term_start.ctypes.data
+    a.term = inp.term.ctypes.data
+    if inp.term_mask is not None:
+        a.term_mask = inp.term_mask.ctypes.data
+    return hq.tile_commit_host(a)
+
+
+def run_tiled(ctx, hq, inp, form, per_group_n):
+    """Columns uploaded, tiled on the device (checked against the host packer), decided from
+    the tiles. Returns (committed_out, changed, fallback)."""
+    d = upload_commit(ctx, hq, inp, form, per_group_n)
+    words = hq.commit_tiles(inp.G) * hq.commit_tile_words(inp.n_max, form)
+    tiles = ctx.empty(words, np.uint64)
+    ctx.tile_commit_dev(d["args"], tiles)
+    ctx.sync()
+    np.testing.assert_array_equal(ctx.download(tiles), host_tiles(hq, inp, form))
+    ctx.commit_dev(tiled_args(hq, d["args"], tiles))
+    ctx.sync()
+    out = ctx.download(d["out"])[:inp.G]
+    chg, fb = ctx.download(d["chg"]), ctx.download(d["fb"])
+    for b in d["bufs"] + [tiles]:
+        ctx.free(b)
+    return out, chg, fb
+
+
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", range(1, 9))
+def test_tiled_commit_every_form_and_n(gpu_ctx, hq, form, n):
+    for G, pern in ((1, False), (129, True), (20_011, False), (20_011, True)):
+        inp = qref.CommitInputs(qref.spec(SEED + 7 * n + G, G, n, mixed_n=pern and n >= 7,
+                                          parity_extras=True))
+        out, chg, fb = run_tiled(gpu_ctx, hq, inp, form, pern)
+        want_out, want_chg, want_fb, rc = inp.run(form, pern, nthreads=8)
+        assert rc == 0
+        np.testing.assert_array_equal(out, want_out)
+        np.testing.assert_array_equal(chg, want_chg)
+        np.testing.assert_array_equal(fb, want_fb)
+
+
+def test_tiled_full_size_c2(gpu_ctx, hq):
+    """BASELINE config 2 (1M groups x 3 voters, term-start) in tiles, device-generated."""
+    G, n = 1 << 20, 3
+    b = hq.alloc_commit(gpu_ctx, G, n, hq.HQ_FORM_TERM_START, 16, tiled=True)
+    gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + 1, G, n), b.args())
+    gpu_ctx.tile_commit_dev(b.args(), b.tiles)
+    gpu_ctx.commit_dev(b.tile_args())
+    gpu_ctx.sync()
+    inp = qref.CommitInputs(qref.spec(SEED + 1, G, n))
+    want_out, want_chg, want_fb, rc = inp.run(hq.HQ_FORM_TERM_START, False, nthreads=8)
+    assert rc == 0
+    np.testing.assert_array_equal(gpu_ctx.download(b.committed_out), want_out)
+    np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+    assert popcount(gpu_ctx.download(b.fallback)) == 0
+    hq.free_commit(gpu_ctx, b)
+
+
+@pytest.mark.parametrize("form", [0, 2, 1, 3])
+def test_tiled_fused_buckets_equal_separate(gpu_ctx, hq, form):
+    """Voter-count buckets of one step in one tiled launch = each bucket decided alone."""
+    sizes = [(3, 70_001), (5, 40_000), (7, 33_333), (1, 5)]
+    bufs = []
+    for k, (n, G) in enumerate(sizes):
+        b = hq.alloc_commit(gpu_ctx, G, n, form, 16, tiled=True)
+        gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + 40 + k, G, n, parity_extras=True),
+                                 b.args())
+        gpu_ctx.tile_commit_dev(b.args(), b.tiles)
+        bufs.append(b)
+    gpu_ctx.commit_fused_dev(hq.commit_batch_array([b.tile_args() for b in bufs]))
+    gpu_ctx.sync()
+    for k, (b, (n, G)) in enumerate(zip(bufs, sizes)):
+        inp = qref.CommitInputs(qref.spec(SEED + 40 + k, G, n, parity_extras=True))
+        want_out, want_chg, want_fb, rc = inp.run(form, False, nthreads=8)
+        assert rc == 0
+        np.testing.assert_array_equal(gpu_ctx.download(b.committed_out), want_out)
+        np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+        np.testing.assert_array_equal(gpu_ctx.download(b.fallback), want_fb)
+        hq.free_commit(gpu_ctx, b)
+
+
+def test_tiled_host_entry_point(gpu_ctx, hq):
+    """hq_commit with host tiles: one H2D block, same decisions."""
+    G, n, form = 10_007, 5, hq.HQ_FORM_TERM_RING32
+    inp = qref.CommitInputs(qref.spec(SEED + 99, G, n, parity_extras=True))
+    tiles = host_tiles(hq, inp, form)
+    ring32 = hq.pack_ring32(inp.ring)
+    out = np.zeros(G, np.uint64)
+    chg = np.zeros(hq.words64(G), np.uint64)
+    fb = np.zeros(hq.words64(G), np.uint64)
+    a = hq.CommitArgs()
+    a.G, a.n_max, a.form, a.ring_len, a.layout = G, n, form, 16, hq.HQ_LAYOUT_TILES
+    a.match = tiles.ctypes.data
+    a.ring32 = ring32.ctypes.data
+    a.committed_out = out.ctypes.data
+    a.changed, a.fallback = chg.ctypes.data, fb.ctypes.data
+    gpu_ctx.commit_host(a)
+    want_out, want_chg, want_fb, rc = inp.run(form, False, nthreads=8)
+    np.testing.assert_array_equal(out, want_out)
+    np.testing.assert_array_equal(chg, want_chg)
+    np.testing.assert_array_equal(fb, want_fb)
+
+
+def test_tiled_validation(gpu_ctx, hq):
+    a = hq.CommitArgs()
+    a.G, a.n_max, a.form, a.layout = 1000, 3, 0, hq.HQ_LAYOUT_TILES
+    with pytest.raises(hq.HQError):
+        gpu_ctx.commit_dev(a)                       # no tiles
+    t = gpu_ctx.empty(4096, np.uint64)
+    o = gpu_ctx.empty(1001, np.uint64)
+    a.match, a.committed_out = t.ptr + 8, o.ptr      # misaligned tiles
+    with pytest.raises(hq.HQError):
+        gpu_ctx.commit_dev(a)
+    a.layout = 7
+    with pytest.raises(hq.HQError):
+        gpu_ctx.commit_dev(a)
+    assert hq.lib.hq_commit_dev(gpu_ctx.h, ctypes.byref(a)) == hq.HQ_E_INVAL
+    gpu_ctx.free(t)
+    gpu_ctx.free(o)

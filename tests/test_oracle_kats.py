@@ -2,22 +2,14 @@
 
 These pin oracle/qref.c before it is trusted as the parity checker for the HIP kernels.
 """
-import json
-import os
 
 import numpy as np
 import pytest
 
 from oracle import qref
 
-KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
+from kats import COMMIT_TABLES, KATS
 
-COMMIT_TABLES = [
-    "TestCommit", "TestLeaderOnlyCommitsLogFromCurrentTerm", "TestLeaderAcknowledgeCommit",
-    "TestLeaderCommitPrecedingEntries", "TestSingleNodeCommit",
-    "TestCannotCommitWithoutNewTermEntry", "TestCommitWithoutNewTermEntry", "TestLeaderAppResp",
-    "TestFullMemberWithOneWitness", "TestVotingMemberLengthMismatch",
-]
 
 
 def _log(case, committed=None):

@@ -1,0 +1,61 @@
+"""HQ_LAYOUT_TILES on the host (no GPU): hq_tile_commit_host cuts the input columns of a commit
+batch into 128-group tiles exactly as include/hipquorum.h lays them out."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import qref
+
+T = 128
+
+
+def column_args(hq, inp, form, n):
+    """CommitArgs over the host columns of a qref.CommitInputs (kept alive by the caller)."""
+    a = hq.CommitArgs()
+    a.G, a.n_max, a.form, a.ring_len, a.layout = inp.G, n, form, 16, hq.HQ_LAYOUT_COLUMNS
+    a.match_stride = inp.G
+    a.match = inp.match.ctypes.data
+    a.committed_in = inp.committed_in.ctypes.data
+    a.last_index = inp.last_index.ctypes.data
+    a.term_start = inp.term_start.ctypes.data
+    a.term = inp.term.ctypes.data
+    a.term_mask = inp.term_mask.ctypes.data
+    return a
+
+
+def expected_tiles(hq, inp, form, n):
+    G = inp.G
+    nt = hq.commit_tiles(G)
+    rows = []
+    pad = nt * T - G
+    for s in range(n):
+        rows.append(inp.match[s * G:(s + 1) * G])
+    rows += [inp.committed_in, inp.last_index]
+    rows = [np.concatenate([r, np.zeros(pad, np.uint64)]).reshape(nt, T) for r in rows]
+    if form == hq.HQ_FORM_TERM_MASK:
+        m = np.concatenate([inp.term_mask, np.zeros(pad, np.uint16)]).reshape(nt, T)
+        rows.append(m.view(np.uint64).reshape(nt, T // 4))
+    else:
+        aux = inp.term_start if form == hq.HQ_FORM_TERM_START else inp.term
+        rows.append(np.concatenate([aux, np.zeros(pad, np.uint64)]).reshape(nt, T))
+    return np.concatenate(rows, axis=1).reshape(-1)
+
+
+@pytest.mark.parametrize("G", [1, 127, 128, 129, 1000])
+@pytest.mark.parametrize("n", [1, 3, 5, 8])
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
+def test_tile_commit_host(hq, G, n, form):
+    inp = qref.CommitInputs(qref.spec(0x5EED0100 + G, G, n, parity_extras=True))
+    a = column_args(hq, inp, form, n)
+    tiles = hq.tile_commit_host(a)
+    assert tiles.size == hq.commit_tiles(G) * hq.commit_tile_words(n, form)
+    np.testing.assert_array_equal(tiles, expected_tiles(hq, inp, form, n))
+
+
+def test_tile_commit_host_rejects_bad_input(hq):
+    a = hq.CommitArgs()
+    assert hq.lib.hq_tile_commit_host(ctypes.byref(a), None) == hq.HQ_E_INVAL
+    a.G, a.n_max, a.layout = 4, 3, hq.HQ_LAYOUT_TILES
+    out = np.zeros(1024, np.uint64)
+    assert hq.lib.hq_tile_commit_host(ctypes.byref(a), out.ctypes.data) == hq.HQ_E_INVAL
