@@ -194,42 +194,23 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
 // workgroups one batch of the launch owns). TILED (HQ_LAYOUT_TILES, VEC = 2 only): a wave's 128
 // groups are one tile, so its loads walk one contiguous 128·(n+3)·8-byte block instead of n + 3
 // column streams.
-template <int N, int FORM, int VEC, bool PERN, int BLK, bool TILED = false>
-__device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
-    static_assert(!TILED || VEC == 2, "tiles are read two groups per lane");
+template <int N, int FORM, bool PERN, int BLK>
+__device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk);
+
+template <int N, int FORM, int VEC, bool PERN, int BLK>
+__device__ __forceinline__ void column_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     const int lane = threadIdx.x & 63;
-    // the wave index is wave-uniform: read it into a scalar so the loop bound and the full-wave
-    // test below are scalar branches, not exec masks (10.4 vs 10.9 us per 1M x 3 tiled launch,
-    // tools/kexp6.hip)
-    const uint64_t wave = blk * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t wave = blk * (BLK / 64) + (threadIdx.x >> 6);
     const uint64_t step = nblk * BLK * VEC;
     for (uint64_t wbase = wave * 64 * VEC; wbase < a.G; wbase += step) {
         const uint64_t g0 = wbase + (uint64_t)lane * VEC;
-        // every input field as a wave-uniform base + this lane's element offset `off` (scalar
-        // base + vector offset addressing, no 64-bit address per lane and field): slot s of
-        // match at bm[s * ms + off], then committed_in, last_index and aux (term_start / term
-        // as u64, or the u16 mask)
-        const uint64_t *bm, *bcin, *blast, *baux;
-        const uint16_t *bmask;
-        uint64_t ms, off;
-        if constexpr (TILED) {
-            const uint64_t *t = a.match + (wbase / HQ_TILE_GROUPS) * a.stride;
-            bm = t;
-            ms = HQ_TILE_GROUPS;
-            bcin = t + N * HQ_TILE_GROUPS;
-            blast = t + (N + 1) * HQ_TILE_GROUPS;
-            baux = t + (N + 2) * HQ_TILE_GROUPS;
-            bmask = reinterpret_cast<const uint16_t *>(baux);
-            off = (uint64_t)lane * 2;
-        } else {
-            bm = a.match;
-            ms = a.stride;
-            bcin = a.cin;
-            blast = a.last;
-            baux = static_cast<const uint64_t *>(a.aux);
-            bmask = static_cast<const uint16_t *>(a.aux);
-            off = g0;
-        }
+        // every input field as a base + this lane's element offset: slot s of match at
+        // bm[s * ms + off], then committed_in, last_index and aux (term_start / term as u64, or
+        // the u16 mask)
+        const uint64_t *bm = a.match, *bcin = a.cin, *blast = a.last;
+        const uint64_t *baux = static_cast<const uint64_t *>(a.aux);
+        const uint16_t *bmask = static_cast<const uint16_t *>(a.aux);
+        const uint64_t ms = a.stride, off = g0;
         auto aux1 = [&]() -> uint64_t {
             if constexpr (FORM == HQ_FORM_TERM_MASK) return bmask[off];
             return baux[off];
@@ -268,27 +249,21 @@ __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, ui
                 decide<N, FORM, PERN>(a, g0 + 1, m1, n1, ci.y, la.y, ax.y, co1, chg[1], fb[1]);
                 st_stream2(a.cout + g0, (u64x2){co0, co1});
             };
-            if (wbase + 64 * VEC <= a.G) {   // scalar: the whole wave is inside the batch
-                pair();
-            } else {                         // the batch's last, partial wave: group by group
-                for (int j = 0; j < 2; ++j) {
-                    if (g0 + j < a.G) {
-                        uint64_t m0[N];
+            // one group (the other of the lane's pair is outside the batch)
+            auto single = [&](int j) {
+                uint64_t m0[N];
 #pragma unroll
-                        for (int s = 0; s < N; ++s) m0[s] = bm[s * ms + off + j];
-                        const int n0 = PERN ? (int)a.nv[g0 + j] : N;
-                        const uint64_t ax = FORM == HQ_FORM_TERM_MASK ? (uint64_t)bmask[off + j]
-                                                                      : baux[off + j];
-                        uint64_t co;
-                        bool c, f;
-                        decide<N, FORM, PERN>(a, g0 + j, m0, n0, bcin[off + j], blast[off + j], ax,
-                                              co, c, f);
-                        a.cout[g0 + j] = co;
-                        chg[j] = c;
-                        fb[j] = f;
-                    }
-                }
-            }
+                for (int s = 0; s < N; ++s) m0[s] = bm[s * ms + off + j];
+                const int n0 = PERN ? (int)a.nv[g0 + j] : N;
+                const uint64_t ax = FORM == HQ_FORM_TERM_MASK ? (uint64_t)bmask[off + j]
+                                                              : baux[off + j];
+                uint64_t co;
+                decide<N, FORM, PERN>(a, g0 + j, m0, n0, bcin[off + j], blast[off + j], ax, co,
+                                      chg[j], fb[j]);
+                a.cout[g0 + j] = co;
+            };
+            if (g0 + 1 < a.G) pair();
+            else if (g0 < a.G) single(0);
             // the wave's 128 groups are two bitmap words: lane k < 2 writes word k (lane i's
             // groups are bits 2i, 2i+1: the two ballots interleaved)
             const uint64_t b0 = __ballot(chg[0]), b1 = __ballot(chg[1]);
@@ -314,14 +289,86 @@ __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, ui
                                       fb[0]);
                 a.cout[g0] = co;
             };
-            if (wbase + 64 <= a.G) one();
-            else if (g0 < a.G) one();
+            if (g0 < a.G) one();
             const uint64_t b0 = __ballot(chg[0]);
             const uint64_t f0 = __ballot(fb[0]);
             if (lane == 0) {
                 if (a.changed) a.changed[wbase >> 6] = b0;
                 if (a.fallback) a.fallback[wbase >> 6] = f0;
             }
+        }
+    }
+}
+
+// HQ_LAYOUT_TILES: one wave per 128-group tile. Row position 2i holds group i of the tile and
+// position 2i + 1 group i + 64, so lane i's 16-byte load of a row brings groups i and i + 64:
+// every field of the wave is ONE contiguous block of (n + 3) KiB, and the two ballots are the
+// tile's two bitmap words as they are (no bit interleave). The full-tile test is scalar (the
+// wave index is read into an SGPR), so full tiles carry no per-lane guard.
+template <int N, int FORM, int VEC, bool PERN, int BLK, bool TILED = false>
+__device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
+    static_assert(!TILED || VEC == 2, "tiles are read two groups per lane");
+    if constexpr (TILED) tile_blocks<N, FORM, PERN, BLK>(a, blk, nblk);
+    else column_blocks<N, FORM, VEC, PERN, BLK>(a, blk, nblk);
+}
+
+template <int N, int FORM, bool PERN, int BLK>
+__device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
+    constexpr uint64_t T = HQ_TILE_GROUPS, H = T / 2;
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = blk * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = nblk * BLK * 2;
+    for (uint64_t wbase = wave * T; wbase < a.G; wbase += step) {
+        const uint64_t *t = a.match + (wbase / T) * a.stride + lane * 2;
+        const uint64_t ga = wbase + lane, gb = ga + H;
+        bool ca = false, cb = false, fa = false, fb = false;
+        if (wbase + T <= a.G) {
+            uint64_t m0[N], m1[N];
+#pragma unroll
+            for (int s = 0; s < N; ++s) {
+                const u64x2 v = ld_stream2(t + s * T);
+                m0[s] = v.x;
+                m1[s] = v.y;
+            }
+            const u64x2 ci = ld_stream2(t + N * T), la = ld_stream2(t + (N + 1) * T);
+            u64x2 ax;
+            if constexpr (FORM == HQ_FORM_TERM_MASK) {
+                const uint32_t mm = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
+                    reinterpret_cast<const uint16_t *>(t - lane * 2 + (N + 2) * T) + lane * 2));
+                ax = (u64x2){mm & 0xFFFFu, mm >> 16};
+            } else {
+                ax = ld_stream2(t + (N + 2) * T);
+            }
+            const int na = PERN ? (int)a.nv[ga] : N, nb = PERN ? (int)a.nv[gb] : N;
+            uint64_t coa, cob;
+            decide<N, FORM, PERN>(a, ga, m0, na, ci.x, la.x, ax.x, coa, ca, fa);
+            decide<N, FORM, PERN>(a, gb, m1, nb, ci.y, la.y, ax.y, cob, cb, fb);
+            a.cout[ga] = coa;
+            a.cout[gb] = cob;
+        } else {   // the batch's last, partial tile: group by group
+            auto single = [&](int j, bool &c, bool &f) {
+                const uint64_t g = ga + H * j;
+                uint64_t m[N];
+#pragma unroll
+                for (int s = 0; s < N; ++s) m[s] = t[s * T + j];
+                const uint64_t ax =
+                    FORM == HQ_FORM_TERM_MASK
+                        ? (uint64_t)reinterpret_cast<const uint16_t *>(t - lane * 2 + (N + 2) * T)[lane * 2 + j]
+                        : t[(N + 2) * T + j];
+                uint64_t co;
+                decide<N, FORM, PERN>(a, g, m, PERN ? (int)a.nv[g] : N, t[N * T + j],
+                                      t[(N + 1) * T + j], ax, co, c, f);
+                a.cout[g] = co;
+            };
+            if (ga < a.G) single(0, ca, fa);
+            if (gb < a.G) single(1, cb, fb);
+        }
+        const uint64_t ba = __ballot(ca), bb = __ballot(cb);
+        const uint64_t xa = __ballot(fa), xb = __ballot(fb);
+        const uint64_t w = (wbase >> 6) + lane;
+        if (lane < 2 && w < ((a.G + 63) >> 6)) {
+            if (a.changed) a.changed[w] = lane ? bb : ba;
+            if (a.fallback) a.fallback[w] = lane ? xb : xa;
         }
     }
 }
@@ -1445,11 +1492,16 @@ __global__ __launch_bounds__(kBlock) void k_tile_commit(const CommitCols c, uint
          w += (uint64_t)gridDim.x * kBlock) {
         const uint64_t t = w / tw, r = w % tw, row = r / HQ_TILE_GROUPS;
         uint64_t v = 0;
+        // row position p holds group (p >> 1) + 64 * (p & 1) of the tile (include/hipquorum.h)
+        auto group = [&](uint64_t p) { return t * HQ_TILE_GROUPS + (p >> 1) + (HQ_TILE_GROUPS / 2) * (p & 1); };
         if (form == HQ_FORM_TERM_MASK && row >= n + 2) {   // 4 u16 masks per word
-            const uint64_t g = t * HQ_TILE_GROUPS + 4 * (r - (uint64_t)(n + 2) * HQ_TILE_GROUPS);
-            for (int k = 3; k >= 0; --k) v = (v << 16) | (g + k < c.G ? c.mask[g + k] : 0);
+            const uint64_t p0 = 4 * (r - (uint64_t)(n + 2) * HQ_TILE_GROUPS);
+            for (int k = 3; k >= 0; --k) {
+                const uint64_t g = group(p0 + k);
+                v = (v << 16) | (g < c.G ? c.mask[g] : 0);
+            }
         } else {
-            const uint64_t g = t * HQ_TILE_GROUPS + r % HQ_TILE_GROUPS;
+            const uint64_t g = group(r % HQ_TILE_GROUPS);
             if (g < c.G) {
                 v = row < n       ? c.match[row * c.stride + g]
                   : row == n      ? c.cin[g]

@@ -1,6 +1,7 @@
 // hq_pack.cpp — host-side packers of libhipquorum.so: a step worker's per-group membership and
 // step messages -> the kernels' structure-of-arrays inputs, with the reference's role rules
 // (include/hipquorum.h "host-side packers"). Plain C++ on the host; no GPU calls.
+#include <cstdint>
 #include <cstring>
 
 #include "../../include/hipquorum.h"
@@ -218,15 +219,17 @@ extern "C" int hq_tile_commit_host(const hq_commit_args *a, uint64_t *tiles) {
     for (uint64_t t = 0; t < hq_commit_tiles(a->G); ++t) {
         uint64_t *tile = tiles + t * tw;
         std::memset(tile, 0, tw * 8);
-        const uint64_t g0 = t * T, cnt = a->G - g0 < T ? a->G - g0 : T;
-        for (uint32_t s = 0; s < n; ++s)
-            std::memcpy(tile + s * T, a->match + s * a->match_stride + g0, cnt * 8);
-        std::memcpy(tile + n * T, a->committed_in + g0, cnt * 8);
-        std::memcpy(tile + (n + 1) * T, a->last_index + g0, cnt * 8);
-        if (mask)
-            std::memcpy(tile + (n + 2) * T, a->term_mask + g0, cnt * 2);
-        else
-            std::memcpy(tile + (n + 2) * T, aux + g0, cnt * 8);
+        uint16_t *mrow = reinterpret_cast<uint16_t *>(tile + (n + 2) * T);
+        // row position p holds group (p >> 1) + 64 * (p & 1) of the tile
+        for (uint64_t p = 0; p < T; ++p) {
+            const uint64_t g = t * T + (p >> 1) + (T / 2) * (p & 1);
+            if (g >= a->G) continue;
+            for (uint32_t s = 0; s < n; ++s) tile[s * T + p] = a->match[s * a->match_stride + g];
+            tile[n * T + p] = a->committed_in[g];
+            tile[(n + 1) * T + p] = a->last_index[g];
+            if (mask) mrow[p] = a->term_mask[g];
+            else tile[(n + 2) * T + p] = aux[g];
+        }
     }
     return HQ_OK;
 }
