@@ -482,7 +482,7 @@ def run_concurrent(w, steps, warmup, d: Dist, W=2):
     sets, per_set = build_sets(ctxs[0], hq, shard, w, d)
 
     def seqs(k):
-        return [hq.commit_batch_array([b.args() for i in range(c, k, W)
+        return [hq.commit_batch_array([batch_args(b) for i in range(c, k, W)
                                        for b in sets[i % len(sets)]]) for c in range(W)]
 
     def run(arrs):
@@ -838,13 +838,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c2t", choices=sorted(WORKLOADS))
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
-                    default="c2l,c3,c3r32,c3m,c3l,c4,c4u,c5,c5s,c5l,c5r,c5r32,rim,cq,ing,ingo,w2,e2e,"
-                            "step,step5",
+                    default="c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c4,c4u,c5,c5t,c5s,c5l,c5r,c5r32,rim,"
+                            "cq,ing,ingo,w2,e2e,step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 

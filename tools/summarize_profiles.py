@@ -16,12 +16,16 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {"c2": "k_commit_big<3, 0, 2, false>", "c3": "k_commit_big<5, 1, 2, false>",
-          "c3m": "k_commit_big<5, 2, 2, false>", "c3r32": "k_commit_big<5, 3, 2, false>",
-          "c4": "k_bits<3, true", "c5": "k_commit_fused<2, 512>", "c5s": "k_commit<7, 2, 2, false>",
+KERNEL = {"c2": "k_commit_big<3, 0, 2, false, false>", "c2t": "k_commit_big<3, 0, 2, false, true>",
+          "c3": "k_commit_big<5, 1, 2, false, false>", "c3m": "k_commit_big<5, 2, 2, false, false>",
+          "c3mt": "k_commit_big<5, 2, 2, false, true>",
+          "c3r32": "k_commit_big<5, 3, 2, false, false>",
+          "c3r32t": "k_commit_big<5, 3, 2, false, true>",
+          "c4": "k_bits<3, true", "c4u": "k_bits<3, false", "c5": "k_commit_fused<2, 512, false>",
+          "c5t": "k_commit_fused<2, 512, true>", "c5s": "k_commit<7, 2, 2, false, false>",
           "c2l": "k_commit_lag_big<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
           "c5l": "k_commit_lag_fused<2, 512>", "rim": "k_ri_multi<false, false>",
-          "cq": "k_bits<4, false", "ing": "k_ingest_match"}
+          "cq": "k_bits<4, false", "ing": "k_ingest_match", "ingo": "k_ingest_match"}
 
 
 def counter(path, kernel):
