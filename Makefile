@@ -37,6 +37,11 @@ tools/lib_b512/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(
 	@mkdir -p tools/lib_b512
 	$(HIPCC) $(HIPFLAGS) -DHQ_COMMIT_BLOCK_BIG=512 -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
 
+# tuning variants: grid cap (in 256-thread units) raised 2x / 4x / 8x
+tools/lib_mb%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(DEPS)
+	@mkdir -p tools/lib_mb$*
+	$(HIPCC) $(HIPFLAGS) -DHQ_MAX_BLOCKS=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
+
 variants: tools/lib_vec2/libhipquorum.so tools/lib_b512/libhipquorum.so
 
 clean:

@@ -47,6 +47,12 @@ WORKLOADS = {
                         "128-group tiles"),
     "c5t": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True, tiled=True,
                 desc="as c5 over 128-group tiles (the three buckets in one fused launch)"),
+    "c5v5t": dict(cfg=2, kind="commit", G=8 << 20, n=5, form=2, mixed=False, tiled=True,
+                  desc="8M groups x 5 voters (4 full + 1 witness) per GPU, the per-GPU share of "
+                       "64M 5-voter groups on 8 GPUs: current-term mask, 128-group tiles"),
+    "c5v5r32t": dict(cfg=2, kind="commit", G=8 << 20, n=5, form=3, mixed=False, tiled=True,
+                     desc="8M groups x 5 voters (4 full + 1 witness) per GPU, u32 term-ring "
+                          "gather, 128-group tiles"),
     "c3": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=1, mixed=False,
                desc="1M groups x 5 voters (4 full + 1 witness; observers never packed), "
                     "commit + term-ring gather R=16"),
@@ -843,7 +849,8 @@ def main():
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
-                    default="c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c4,c4u,c5,c5t,c5s,c5l,c5r,c5r32,rim,"
+                    default="c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5r32t,c4,c4u,c5,c5t,c5s,c5l,"
+                            "c5r,c5r32,rim,"
                             "cq,ing,ingo,w2,e2e,step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()

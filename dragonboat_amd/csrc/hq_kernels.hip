@@ -27,7 +27,13 @@ template <int N, bool PERN>
 constexpr int lag_blk() {
     return !PERN && N <= 4 ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
 }
-constexpr int kMaxBlocks = 256 * 16;  // grid-stride beyond 16 workgroups per CU
+// Grid cap in 256-thread units (64 per CU), grid-stride beyond. An 8M-group x 5 launch then runs
+// one tile per wave: 92-94 vs 96-98 us with the earlier cap of 16 per CU, neutral at 1M groups
+// (profiles/r01e/ab_maxblocks.log).
+#ifndef HQ_MAX_BLOCKS
+#define HQ_MAX_BLOCKS (256 * 64)
+#endif
+constexpr int kMaxBlocks = HQ_MAX_BLOCKS;
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

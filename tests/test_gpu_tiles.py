@@ -148,3 +148,26 @@ def test_tiled_validation(gpu_ctx, hq):
     assert hq.lib.hq_commit_dev(gpu_ctx.h, ctypes.byref(a)) == hq.HQ_E_INVAL
     gpu_ctx.free(t)
     gpu_ctx.free(o)
+
+
+@pytest.mark.parametrize("tiled", [False, True])
+def test_commit_grid_stride_beyond_cap(gpu_ctx, hq, tiled):
+    """More groups than one capped grid covers (HQ_MAX_BLOCKS x 256 threads, two groups per
+    lane = 8M groups): the grid-stride loop's second iteration, columns and tiles, bit-exact."""
+    G, n = (8 << 20) + 4099, 5
+    form = hq.HQ_FORM_TERM_MASK
+    b = hq.alloc_commit(gpu_ctx, G, n, form, 16, tiled=tiled)
+    gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + 11, G, n), b.args())
+    if tiled:
+        gpu_ctx.tile_commit_dev(b.args(), b.tiles)
+        gpu_ctx.commit_dev(b.tile_args())
+    else:
+        gpu_ctx.commit_dev(b.args())
+    gpu_ctx.sync()
+    inp = qref.CommitInputs(qref.spec(SEED + 11, G, n))
+    want_out, want_chg, want_fb, rc = inp.run(form, False, nthreads=16)
+    assert rc == 0
+    np.testing.assert_array_equal(gpu_ctx.download(b.committed_out), want_out)
+    np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+    assert popcount(gpu_ctx.download(b.fallback)) == 0
+    hq.free_commit(gpu_ctx, b)
