@@ -76,6 +76,11 @@ WORKLOADS = {
     "c4u": dict(cfg=3, kind="bits", G=16 << 20, n=7, uniform=True,
                 desc="as c4 with the voter count uniform over the batch (a step worker's "
                      "7-voter bucket): no per-group n column"),
+    "c4t": dict(cfg=3, kind="bits", G=16 << 20, n=7, tiled=True,
+                desc="as c4 over 1024-group bitmap tiles (rows n, ack, granted, rejected: one "
+                     "contiguous stream per wave)"),
+    "c4ut": dict(cfg=3, kind="bits", G=16 << 20, n=7, uniform=True, tiled=True,
+                 desc="as c4u over 1024-group bitmap tiles (rows ack, granted, rejected)"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
                desc="64M groups mixed 3/5/7 voters (n = {3,5,7}[clusterID % 3]) sharded "
                     "clusterID % 8: 8M groups per GPU, the three voter-count buckets in one "
@@ -241,7 +246,16 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             ctx.synth_bitmaps_dev(spec, *arrs)
             conf = ctx.empty(hq.words64(G), np.uint64)
             outc = ctx.empty(hq.words32(G), np.uint64)
-            sets.append((arrs, conf, outc))
+            tiles = None
+            if w.get("tiled"):
+                pern = not w.get("uniform")
+                tiles = ctx.empty(hq.bits_tile_bytes(G, pern), np.uint8)
+                ctx.tile_bits_dev(G, *arrs[:3], arrs[3] if pern else None, tiles)
+                ctx.sync()
+                for a in arrs:
+                    ctx.free(a)
+                arrs = None
+            sets.append((arrs, conf, outc, tiles))
     ctx.sync()
     return sets, per_set
 
@@ -310,7 +324,13 @@ def run_gpu(w, steps, warmup, d: Dist):
 
         def run(idx):
             for i in idx:
-                (da, dg, dr, dn), conf, outc = sets[i % len(sets)]
+                arrs, conf, outc, tiles = sets[i % len(sets)]
+                if tiles is not None:
+                    uni = w.get("uniform", False)
+                    ctx.readindex_vote_tiles_dev(G, tiles, not uni, w["n"] if uni else 0, conf,
+                                                 outc)
+                    continue
+                da, dg, dr, dn = arrs
                 if w.get("uniform"):
                     ctx.readindex_vote_dev(G, da, dg, dr, None, w["n"], conf, outc)
                 else:
@@ -849,7 +869,7 @@ def main():
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
-                    default="c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5r32t,c4,c4u,c5,c5t,c5s,c5l,"
+                    default="c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5r32t,c4,c4t,c4u,c4ut,c5,c5t,c5s,c5l,"
                             "c5r,c5r32,rim,"
                             "cq,ing,ingo,w2,e2e,step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")

@@ -678,6 +678,8 @@ struct BitsK {
     uint64_t *confirmed, *outcome, *has_quorum, *fallback;
     uint64_t n16;   // number of 16-group slots covered by the 64-group bitmap words
     uint64_t n16o;  // number of 16-group slots covered by the 32-group outcome words
+    const uint8_t *tiles;  // HQ_LAYOUT_TILES: 1024-group tiles of rows [n] ack granted rejected
+    uint32_t tile_rows;    // 4 with the per-group n row, else 3
 };
 
 constexpr int kRI = 1, kVOTE = 2, kCHECKQ = 4;
@@ -735,23 +737,31 @@ __device__ __forceinline__ uint32_t mask_n(uint32_t n) {
 // One 16-group slot starting at group g. FULL: all 16 groups exist (g + 16 <= G), so every load
 // is one unconditional 16-byte nontemporal load and no byte needs masking (the common case; the
 // ragged tail slot takes the guarded path).
-template <int MODE, bool PERN, bool FULL>
-__device__ __forceinline__ void bits_slot(const BitsK &a, uint64_t g, uint32_t nu) {
+// TILED: the inputs are the slot's tile rows, loaded by the caller before it branches on the full
+// tile test (so the four loads issue together); every tile is padded to 1024 groups, so even the
+// ragged last slot holds 16 loaded bytes (the padding bytes are masked by `inr` like any byte
+// beyond G).
+template <int MODE, bool PERN, bool FULL, bool TILED = false, bool FB = true>
+__device__ __forceinline__ void bits_slot(const BitsK &a, uint64_t g, uint32_t nu,
+                                          const V16 *trow = nullptr) {
     const uint64_t slot = g >> 4;
     V16 nv = {}, ack = {}, gr = {}, rj = {}, ac = {};
-    auto ld = [&](const uint8_t *p) -> V16 {
-        if constexpr (FULL) {
+    auto ld = [&](const uint8_t *p, uint32_t row = 0) -> V16 {
+        if constexpr (TILED) {
+            return trow[row];
+        } else if constexpr (FULL) {
             V16 r;
             r.w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + g));
             return r;
         }
         return g < a.G ? load16(p, g, a.G) : V16{};
     };
-    if constexpr (PERN) nv = ld(a.nv);
-    if constexpr (MODE & kRI) ack = ld(a.ack);
+    constexpr uint32_t r0 = PERN ? 1 : 0;   // tile rows: [n] ack granted rejected
+    if constexpr (PERN) nv = ld(a.nv, 0);
+    if constexpr (MODE & kRI) ack = ld(a.ack, r0);
     if constexpr (MODE & kVOTE) {
-        gr = ld(a.granted);
-        rj = ld(a.rejected);
+        gr = ld(a.granted, r0 + 1);
+        rj = ld(a.rejected, r0 + 2);
     }
     if constexpr (MODE & kCHECKQ) ac = ld(a.active);
     uint32_t conf = 0, outc = 0, hq = 0, fb = 0;
@@ -795,14 +805,14 @@ __device__ __forceinline__ void bits_slot(const BitsK &a, uint64_t g, uint32_t n
             // groups left to the CPU path keep their flags
             keep.w[w] = ac.w[w] & ((bad >> 7) * 0xFFu);
         }
-        fb |= pack4(bad) << (4 * w);
+        if constexpr (FB) fb |= pack4(bad) << (4 * w);
     }
     // 64-group bitmap words viewed as 16-bit slots, 32-group outcome words as 32-bit slots
     // (a full slot lies below G / 16 <= n16, n16o)
     if (FULL || slot < a.n16) {
         if constexpr (MODE & kRI) reinterpret_cast<uint16_t *>(a.confirmed)[slot] = conf;
         if constexpr (MODE & kCHECKQ) reinterpret_cast<uint16_t *>(a.has_quorum)[slot] = hq;
-        if (a.fallback) reinterpret_cast<uint16_t *>(a.fallback)[slot] = fb;
+        if (FB && a.fallback) reinterpret_cast<uint16_t *>(a.fallback)[slot] = fb;
     }
     if constexpr (MODE & kVOTE) {
         if (FULL || slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
@@ -817,16 +827,42 @@ __device__ __forceinline__ void bits_slot(const BitsK &a, uint64_t g, uint32_t n
     }
 }
 
-template <int MODE, bool PERN, int BLK>
+// FB = false (no fallback bitmap requested) drops the fallback bits' arithmetic (tiles only)
+template <int MODE, bool PERN, int BLK, bool TILED = false, bool FB = true>
 __global__ __launch_bounds__(BLK) void k_bits(const BitsK a) {
     const uint64_t tid = (uint64_t)blockIdx.x * BLK + threadIdx.x;
     const uint64_t step = (uint64_t)gridDim.x * BLK * 16;
     const uint32_t nu = a.n_uniform * kB01;  // n_uniform <= 8: no byte overflow
+    if constexpr (TILED) {
+        // one wave per 1024-group tile: the tile base is wave-uniform (scalar), lane i reads
+        // bytes [16 i, 16 i + 16) of every row
+        constexpr uint64_t R = PERN ? 4 : 3;
+        const uint64_t lane = threadIdx.x & 63;
+        const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) +
+                              __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const uint64_t nw = (uint64_t)gridDim.x * (BLK / 64);
+        const uint64_t slots = a.n16o > a.n16 ? a.n16o : a.n16;
+        const uint64_t ntiles = (slots * 16 + 1023) >> 10;
+        for (uint64_t t = wave; t < ntiles; t += nw) {
+            const uint8_t *base = a.tiles + t * (R << 10) + lane * 16;
+            V16 rows[R];
+#pragma unroll
+            for (uint64_t r = 0; r < R; ++r)
+                rows[r].w = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4 *>(base + (r << 10)));
+            const uint64_t g = (t << 10) + lane * 16;
+            if ((t << 10) + 1024 <= a.G)
+                bits_slot<MODE, PERN, true, true, FB>(a, g, nu, rows);
+            else
+                bits_slot<MODE, PERN, false, true, FB>(a, g, nu, rows);
+        }
+        return;
+    }
     for (uint64_t g = tid * 16; g < a.n16o * 16 || g < a.n16 * 16; g += step) {
         if (g + 16 <= a.G)
-            bits_slot<MODE, PERN, true>(a, g, nu);
+            bits_slot<MODE, PERN, true, TILED>(a, g, nu);
         else
-            bits_slot<MODE, PERN, false>(a, g, nu);
+            bits_slot<MODE, PERN, false, TILED>(a, g, nu);
     }
 }
 
@@ -1370,8 +1406,10 @@ template <int MODE>
 int launch_bits(hq_ctx *ctx, BitsK &k, const char *what) {
     if (!ctx) return HQ_E_INVAL;
     if (k.G == 0) return HQ_OK;
-    if (!k.nv && (k.n_uniform < 1 || k.n_uniform > 8))
+    if (!k.nv && !(k.tiles && k.tile_rows == 4) && (k.n_uniform < 1 || k.n_uniform > 8))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": n_uniform must be 1..8");
+    if (k.tiles && (k.nv || !hq::aligned16(k.tiles) || (k.tile_rows != 3 && k.tile_rows != 4)))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": bad tiles");
     const uint8_t *ins[5] = {k.nv, k.ack, k.granted, k.rejected, k.active};
     for (const uint8_t *p : ins)
         if (p && !hq::aligned16(p))
@@ -1385,7 +1423,22 @@ int launch_bits(hq_ctx *ctx, BitsK &k, const char *what) {
 #define HQ_BITS_LAUNCH(B)                                                                      \
     {                                                                                          \
         const unsigned grid = grid_for(slots, B, (uint64_t)kMaxBlocks * 256 / B);              \
-        if (k.nv)                                                                              \
+        if constexpr (MODE == (kRI | kVOTE)) {                                                 \
+            if (k.tiles && k.tile_rows == 4 && k.fallback)                                     \
+                hipLaunchKernelGGL((k_bits<MODE, true, B, true>), dim3(grid), dim3(B), 0,      \
+                                   ctx->stream, k);                                            \
+            else if (k.tiles && k.tile_rows == 4)                                              \
+                hipLaunchKernelGGL((k_bits<MODE, true, B, true, false>), dim3(grid), dim3(B),  \
+                                   0, ctx->stream, k);                                         \
+            else if (k.tiles && k.fallback)                                                    \
+                hipLaunchKernelGGL((k_bits<MODE, false, B, true>), dim3(grid), dim3(B), 0,     \
+                                   ctx->stream, k);                                            \
+            else if (k.tiles)                                                                  \
+                hipLaunchKernelGGL((k_bits<MODE, false, B, true, false>), dim3(grid), dim3(B), \
+                                   0, ctx->stream, k);                                         \
+        }                                                                                      \
+        if (k.tiles) {                                                                         \
+        } else if (k.nv)                                                                       \
             hipLaunchKernelGGL((k_bits<MODE, true, B>), dim3(grid), dim3(B), 0, ctx->stream, k); \
         else                                                                                   \
             hipLaunchKernelGGL((k_bits<MODE, false, B>), dim3(grid), dim3(B), 0, ctx->stream, k); \
@@ -1444,6 +1497,57 @@ extern "C" int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack
     k.confirmed = confirmed;
     k.outcome = outcome;
     return launch_bits<kRI | kVOTE>(ctx, k, "hq_readindex_vote");
+}
+
+extern "C" int hq_readindex_vote_tiles_dev(hq_ctx *ctx, uint64_t G, const uint8_t *tiles,
+                                           uint32_t per_group_n, uint32_t n_uniform,
+                                           uint64_t *confirmed, uint64_t *outcome,
+                                           uint64_t *fallback) {
+    if (ctx && G && (!tiles || !confirmed || !outcome))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_vote_tiles: NULL argument");
+    BitsK k = bits_args(G, nullptr, n_uniform, fallback);
+    k.tiles = tiles;
+    k.tile_rows = per_group_n ? 4 : 3;
+    k.confirmed = confirmed;
+    k.outcome = outcome;
+    return launch_bits<kRI | kVOTE>(ctx, k, "hq_readindex_vote_tiles");
+}
+
+namespace {
+// one lane per 16 groups: 16-byte column loads (guarded at G) into the tile rows (padding zeroed)
+__global__ __launch_bounds__(kBlock) void k_tile_bits(uint64_t G, const uint8_t *nv,
+                                                      const uint8_t *ack, const uint8_t *gr,
+                                                      const uint8_t *rj, uint8_t *tiles,
+                                                      uint32_t rows) {
+    const uint64_t slots = (G + HQ_BITS_TILE_GROUPS - 1) / HQ_BITS_TILE_GROUPS * (HQ_BITS_TILE_GROUPS / 16);
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < slots;
+         t += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t g = t * 16;
+        uint8_t *row = tiles + (g >> 10) * ((uint64_t)rows << 10) + (g & 1023);
+        const uint8_t *cols[4] = {nv, ack, gr, rj};
+        for (uint32_t r = 0; r < rows; ++r) {
+            const uint8_t *c = cols[r + 4 - rows];
+            *reinterpret_cast<uint4 *>(row + (r << 10)) = load16(c, g, G).v;
+        }
+    }
+}
+}  // namespace
+
+extern "C" int hq_tile_bits_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,
+                                const uint8_t *granted, const uint8_t *rejected,
+                                const uint8_t *n_voting, uint8_t *tiles) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!ack || !granted || !rejected || !tiles || !hq::aligned16(tiles) || !hq::aligned16(ack) ||
+        !hq::aligned16(granted) || !hq::aligned16(rejected) ||
+        (n_voting && !hq::aligned16(n_voting)))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_bits_dev: NULL or misaligned argument");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_bits, dim3(grid_for(hq_bits_tiles(G) * (HQ_BITS_TILE_GROUPS / 16))),
+                       dim3(kBlock), 0, ctx->stream, G, n_voting, ack, granted, rejected, tiles,
+                       n_voting ? 4u : 3u);
+    return hq::post_launch(ctx, "k_tile_bits");
 }
 
 extern "C" int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active,

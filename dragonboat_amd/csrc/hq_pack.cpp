@@ -233,3 +233,23 @@ extern "C" int hq_tile_commit_host(const hq_commit_args *a, uint64_t *tiles) {
     }
     return HQ_OK;
 }
+
+// Bitmap columns -> 1024-group tiles on the host (the twin of k_tile_bits).
+extern "C" int hq_tile_bits_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                                 const uint8_t *rejected, const uint8_t *n_voting,
+                                 uint8_t *tiles) {
+    if (G == 0) return HQ_OK;
+    if (!ack || !granted || !rejected || !tiles) return HQ_E_INVAL;
+    const uint8_t *cols[4] = {n_voting, ack, granted, rejected};
+    const uint32_t rows = n_voting ? 4 : 3;
+    const uint64_t T = HQ_BITS_TILE_GROUPS;
+    for (uint64_t t = 0; t < hq_bits_tiles(G); ++t) {
+        const uint64_t g0 = t * T, cnt = G - g0 < T ? G - g0 : T;
+        uint8_t *tile = tiles + t * rows * T;
+        for (uint32_t r = 0; r < rows; ++r) {
+            std::memcpy(tile + r * T, cols[r + 4 - rows] + g0, cnt);
+            std::memset(tile + r * T + cnt, 0, T - cnt);
+        }
+    }
+    return HQ_OK;
+}

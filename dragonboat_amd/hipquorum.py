@@ -32,7 +32,7 @@ HQ_FORM_TERM_RING32 = 3
 HQ_LAYOUT_COLUMNS = 0
 HQ_LAYOUT_TILES = 1
 HQ_TILE_GROUPS = 128
-HQ_ABI_VERSION = 4
+HQ_ABI_VERSION = 5
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -203,6 +203,12 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp],
     ),
+    "hq_readindex_vote_tiles_dev": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp],
+    ),
+    "hq_tile_bits_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
+    "hq_tile_bits_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
     "hq_check_quorum_dev": (
         ctypes.c_int,
         [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp],
@@ -436,6 +442,18 @@ class Context:
                                               _p(n_voting), n_uniform, _p(confirmed), _p(outcome),
                                               _p(fallback)))
 
+    def readindex_vote_tiles_dev(self, G, tiles, per_group_n, n_uniform, confirmed, outcome,
+                                 fallback=None) -> None:
+        """hq_readindex_vote_tiles_dev: the fused pass over HQ_BITS_TILE_GROUPS-group tiles."""
+        self._check(lib.hq_readindex_vote_tiles_dev(self.h, G, _p(tiles), int(per_group_n),
+                                                    n_uniform, _p(confirmed), _p(outcome),
+                                                    _p(fallback)))
+
+    def tile_bits_dev(self, G, ack, granted, rejected, n_voting, tiles) -> None:
+        """hq_tile_bits_dev: bitmap columns cut into tiles (rows [n] ack granted rejected)."""
+        self._check(lib.hq_tile_bits_dev(self.h, G, _p(ack), _p(granted), _p(rejected),
+                                         _p(n_voting), _p(tiles)))
+
     def check_quorum_dev(self, G, active, n_voting, n_uniform, self_slot, has_quorum,
                          fallback=None) -> None:
         self._check(lib.hq_check_quorum_dev(self.h, G, _p(active), _p(n_voting), n_uniform,
@@ -651,6 +669,28 @@ def tile_commit_host(columns: CommitArgs) -> np.ndarray:
     out = np.zeros(commit_tiles(columns.G) * commit_tile_words(columns.n_max, columns.form),
                    np.uint64)
     _chk(lib.hq_tile_commit_host(ctypes.byref(columns), _p(out)), "hq_tile_commit_host")
+    return out
+
+
+HQ_BITS_TILE_GROUPS = 1024
+
+
+def bits_tiles(G: int) -> int:
+    return (G + HQ_BITS_TILE_GROUPS - 1) // HQ_BITS_TILE_GROUPS
+
+
+def bits_tile_bytes(G: int, per_group_n: bool) -> int:
+    """Bytes of the bitmap tiles of G groups (rows [n] ack granted rejected, 1024 bytes each)."""
+    return bits_tiles(G) * (4 if per_group_n else 3) * HQ_BITS_TILE_GROUPS
+
+
+def tile_bits_host(ack, granted, rejected, n_voting=None) -> np.ndarray:
+    """hq_tile_bits_host over host uint8 columns: the tiles as a uint8 array."""
+    G = len(ack)
+    cols = [np.ascontiguousarray(a, np.uint8) if a is not None else None
+            for a in (ack, granted, rejected, n_voting)]
+    out = np.empty(bits_tile_bytes(G, n_voting is not None), np.uint8)
+    _chk(lib.hq_tile_bits_host(G, *[_p(c) for c in cols], _p(out)), "hq_tile_bits_host")
     return out
 
 

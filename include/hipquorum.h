@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 4
+#define HQ_ABI_VERSION 5
 
 /* status codes */
 #define HQ_OK          0
@@ -334,6 +334,32 @@ int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_m
 int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
                           const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
                           uint64_t *confirmed, uint64_t *outcome, uint64_t *fallback);
+
+/*
+ * The same fused pass over a tiled bitmap layout: the bitmaps of 1024 consecutive groups (one
+ * wave, 16 groups per lane) stored as one contiguous block of 1024-byte rows
+ *   [n_voting (per_group_n only)] [ack] [granted] [rejected]
+ * so a wave reads ONE stream instead of 3-4 columns (tools/kexp8.hip: 14.5 vs 15.5 us per
+ * 16M x 7 launch, 11.1 vs 11.9 us with uniform n). Tile t starts at tiles + t * rows * 1024,
+ * byte (g & 1023) of each row is group g; the last tile is padded to 1024 groups (padding is
+ * never decided). Outputs are the columns of hq_readindex_vote_dev. Same decisions as
+ * readIndex.confirm's quorum test (readindex.go:84) and handleVoteResp / the candidate's tally
+ * (raft.go:1062-1080, 1968-1985).
+ */
+#define HQ_BITS_TILE_GROUPS 1024
+static inline uint64_t hq_bits_tiles(uint64_t G) {
+    return (G + HQ_BITS_TILE_GROUPS - 1) / HQ_BITS_TILE_GROUPS;
+}
+int hq_readindex_vote_tiles_dev(hq_ctx *ctx, uint64_t G, const uint8_t *tiles,
+                                uint32_t per_group_n, uint32_t n_uniform, uint64_t *confirmed,
+                                uint64_t *outcome, uint64_t *fallback);
+/* Columns -> bitmap tiles (hq_bits_tiles(G) * (n_voting ? 4 : 3) * 1024 bytes, padding zeroed).
+ * _dev: device pointers, 16-byte aligned, async on the context's stream; _host: host pointers
+ * (a step worker packing its staging buffer). */
+int hq_tile_bits_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                     const uint8_t *rejected, const uint8_t *n_voting, uint8_t *tiles);
+int hq_tile_bits_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                      const uint8_t *rejected, const uint8_t *n_voting, uint8_t *tiles);
 
 /*
  * CheckQuorum (raft.go:380-390): has_quorum bit = popcount(active[g] | 1 << self_slot) >= q,

@@ -171,3 +171,93 @@ def test_commit_grid_stride_beyond_cap(gpu_ctx, hq, tiled):
     np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
     assert popcount(gpu_ctx.download(b.fallback)) == 0
     hq.free_commit(gpu_ctx, b)
+
+
+# ---- bitmap tiles: fused ReadIndex + vote over 1024-group tiles ------------------------------
+def _bits_tiled(ctx, hq, inp, G, pern, n_uniform):
+    """Columns uploaded, tiled on the device (checked against the host packer), decided from
+    the tiles. Returns (confirmed, outcome, fallback) words."""
+    nv = inp.n_voting if pern else None
+    cols = [ctx.upload(np.ascontiguousarray(a)) if a is not None else None
+            for a in (inp.ack, inp.granted, inp.rejected, nv)]
+    tiles = ctx.empty(hq.bits_tile_bytes(G, pern), np.uint8)
+    ctx.memset(tiles, 0xAB)
+    ctx.tile_bits_dev(G, *cols, tiles)
+    ctx.sync()
+    np.testing.assert_array_equal(ctx.download(tiles),
+                                  hq.tile_bits_host(inp.ack, inp.granted, inp.rejected, nv))
+    conf = ctx.empty(hq.words64(G), np.uint64)
+    outc = ctx.empty(hq.words32(G), np.uint64)
+    fb = ctx.empty(hq.words64(G), np.uint64)
+    for x in (conf, outc, fb):
+        ctx.memset(x, 0xFF)
+    ctx.readindex_vote_tiles_dev(G, tiles, pern, n_uniform, conf, outc, fb)
+    ctx.sync()
+    res = [ctx.download(x) for x in (conf, outc, fb)]
+    for x in [c for c in cols if c is not None] + [tiles, conf, outc, fb]:
+        ctx.free(x)
+    return res
+
+
+@pytest.mark.parametrize("G", [1, 16, 17, 63, 65, 1023, 1024, 1025, 5000, 20_011])
+@pytest.mark.parametrize("pern", [True, False])
+def test_tiled_bits_equal_oracle(gpu_ctx, hq, G, pern):
+    n = 8 if pern else 7
+    inp = qref.BitmapInputs(qref.spec(SEED + G + pern, G, n, mixed_n=pern, parity_extras=True))
+    nu = 0 if pern else n
+    conf, outc, fb = _bits_tiled(gpu_ctx, hq, inp, G, pern, nu)
+    nv = inp.n_voting if pern else None
+    want_conf, want_fb = qref.readindex_batch(inp.ack, nv, nu)
+    want_out, want_fb2 = qref.vote_batch(inp.granted, inp.rejected, nv, nu)
+    np.testing.assert_array_equal(conf, want_conf)
+    np.testing.assert_array_equal(outc, want_out)
+    np.testing.assert_array_equal(fb, want_fb)
+    np.testing.assert_array_equal(fb, want_fb2)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 6, 8])
+def test_tiled_bits_uniform_n(gpu_ctx, hq, n):
+    G = 3000
+    inp = qref.BitmapInputs(qref.spec(SEED + 100 + n, G, n, parity_extras=True))
+    conf, outc, fb = _bits_tiled(gpu_ctx, hq, inp, G, False, n)
+    np.testing.assert_array_equal(conf, qref.readindex_batch(inp.ack, None, n)[0])
+    np.testing.assert_array_equal(outc, qref.vote_batch(inp.granted, inp.rejected, None, n)[0])
+    assert popcount(fb) == 0
+
+
+def test_tiled_bits_validation(gpu_ctx, hq):
+    G = 100
+    tiles = gpu_ctx.empty(hq.bits_tile_bytes(G, False), np.uint8)
+    conf = gpu_ctx.empty(hq.words64(G), np.uint64)
+    outc = gpu_ctx.empty(hq.words32(G), np.uint64)
+    with pytest.raises(hq.HQError):
+        gpu_ctx.readindex_vote_tiles_dev(G, tiles, False, 0, conf, outc)   # n_uniform 0
+    with pytest.raises(hq.HQError):
+        gpu_ctx.readindex_vote_tiles_dev(G, tiles.ptr + 1, False, 7, conf, outc)   # misaligned
+    with pytest.raises(hq.HQError):
+        gpu_ctx.readindex_vote_tiles_dev(G, None, False, 7, conf, outc)
+    for x in (tiles, conf, outc):
+        gpu_ctx.free(x)
+
+
+@pytest.mark.parametrize("pern", [True, False])
+def test_tiled_bits_full_size_config4(gpu_ctx, hq, pern):
+    """BASELINE config 4 at full size (16M groups x 7 voters) over tiles, device-generated."""
+    G = 16 << 20
+    arrs = [gpu_ctx.empty(G, np.uint8) for _ in range(4)]
+    da, dg, dr, dn = arrs
+    gpu_ctx.synth_bitmaps_dev(hq.synth_spec(SEED + 3, G, 7), da, dg, dr, dn)
+    tiles = gpu_ctx.empty(hq.bits_tile_bytes(G, pern), np.uint8)
+    gpu_ctx.tile_bits_dev(G, da, dg, dr, dn if pern else None, tiles)
+    conf = gpu_ctx.empty(hq.words64(G), np.uint64)
+    outc = gpu_ctx.empty(hq.words32(G), np.uint64)
+    gpu_ctx.readindex_vote_tiles_dev(G, tiles, pern, 0 if pern else 7, conf, outc)
+    inp = qref.BitmapInputs(qref.spec(SEED + 3, G, 7))
+    nv = inp.n_voting if pern else None
+    nu = 0 if pern else 7
+    want_conf, _ = qref.readindex_batch(inp.ack, nv, nu, nthreads=16)
+    want_out, _ = qref.vote_batch(inp.granted, inp.rejected, nv, nu, nthreads=16)
+    np.testing.assert_array_equal(gpu_ctx.download(conf), want_conf)
+    np.testing.assert_array_equal(gpu_ctx.download(outc), want_out)
+    for x in arrs + [tiles, conf, outc]:
+        gpu_ctx.free(x)

@@ -73,3 +73,23 @@ def test_tile_commit_host_rejects_bad_input(hq):
     a.G, a.n_max, a.layout = 4, 3, hq.HQ_LAYOUT_TILES
     out = np.zeros(1024, np.uint64)
     assert hq.lib.hq_tile_commit_host(ctypes.byref(a), out.ctypes.data) == hq.HQ_E_INVAL
+
+
+# ---- bitmap tiles (hq_tile_bits_host) ------------------------------------------------------
+@pytest.mark.parametrize("G,pern", [(1, False), (1023, True), (1024, False), (2049, True)])
+def test_tile_bits_host_layout(hq, G, pern):
+    """Tile t holds rows [n] ack granted rejected of groups [1024 t, 1024 t + 1024), 1024 bytes
+    each, byte (g & 1023) = group g; the last tile's padding is zero."""
+    rng = np.random.default_rng(G)
+    cols = [rng.integers(0, 256, G, dtype=np.uint8) for _ in range(4)]
+    ack, gr, rj, nv = cols
+    t = hq.tile_bits_host(ack, gr, rj, nv if pern else None)
+    rows = 4 if pern else 3
+    T = hq.HQ_BITS_TILE_GROUPS
+    assert t.size == hq.bits_tiles(G) * rows * T
+    tiles = t.reshape(hq.bits_tiles(G), rows, T)
+    want = ([nv] if pern else []) + [ack, gr, rj]
+    for r, col in enumerate(want):
+        flat = tiles[:, r, :].reshape(-1)
+        np.testing.assert_array_equal(flat[:G], col)
+        assert not flat[G:].any()
