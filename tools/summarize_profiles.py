@@ -23,8 +23,8 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, false>", "c2t": "k_commit_big<3, 0
           "c3r32t": "k_commit_big<5, 3, 2, false, true>",
           "c5v5t": "k_commit_big<5, 2, 2, false, true>",
           "c5v5r32t": "k_commit_big<5, 3, 2, false, true>",
-          "c4": "k_bits<3, true, 256, false>", "c4u": "k_bits<3, false, 256, false>",
-          "c4t": "k_bits<3, true, 256, true>", "c4ut": "k_bits<3, false, 256, true>", "c5": "k_commit_fused<2, 512, false>",
+          "c4": "k_bits<3, true, 256, false, true>", "c4u": "k_bits<3, false, 256, false, true>",
+          "c4t": "k_bits<3, true, 256, true, false>", "c4ut": "k_bits<3, false, 256, true, false>", "c5": "k_commit_fused<2, 512, false>",
           "c5t": "k_commit_fused<2, 512, true>", "c5s": "k_commit<7, 2, 2, false, false>",
           "c2l": "k_commit_lag_big<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
           "c5l": "k_commit_lag_fused<2, 512>", "rim": "k_ri_multi<false, false>",
