@@ -24,6 +24,8 @@ struct hq_ctx {
     uint64_t timed_launches = 0;
     // launch geometry of the bitmap kernels (256; HQ_BITS_BLOCK=512|1024 at hq_open)
     int bits_block = 256;
+    // multi-ctx ReadIndex two groups per lane when the batch allows it (HQ_RI_PAIRS=0: off, A/B)
+    bool ri_pairs = true;
     // hq_wait_for: recorded on this context's stream when another context orders after it
     hipEvent_t ev_order = nullptr;
     // device workspace for the host-pointer entry points

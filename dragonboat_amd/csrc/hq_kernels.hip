@@ -1766,6 +1766,116 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi(const RiMultiK a) {
     }
 }
 
+
+// Two adjacent groups per lane (even G, aligned columns): the u16 first-ack ordinals of both
+// groups travel packed in one 32-bit register, so one 4-byte load reads a (ctx, voter) pair and
+// the sorting network runs on both groups at once with packed u16 min / max (v_pk_min_u16 /
+// v_pk_max_u16); the ctx indexes and released indexes move as 16-byte pairs. Same decisions as
+// k_ri_multi (the suffix-min release of readindex.go:77-116).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void ce_pk(uint32_t &a, uint32_t &b) {
+    const u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
+    a = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
+    b = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+
+template <bool PERK, bool PERN>
+__global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * 2;
+    for (uint64_t wbase = wave * 128; wbase < a.G; wbase += step) {
+        const uint64_t g = wbase + 2 * (uint64_t)lane;
+        bool fb0 = false, fb1 = false;
+        if (g < a.G) {   // G is even: g + 1 < G too
+            uint32_t K0 = a.K_max, K1 = a.K_max, n0 = a.n_uniform, n1 = a.n_uniform;
+            if constexpr (PERK) {
+                const uint32_t kk = *reinterpret_cast<const uint16_t *>(a.np + g);
+                K0 = kk & 0xFF;
+                K1 = kk >> 8;
+            }
+            if constexpr (PERN) {
+                const uint32_t nn = *reinterpret_cast<const uint16_t *>(a.nv + g);
+                n0 = nn & 0xFF;
+                n1 = nn >> 8;
+            }
+            fb0 = n0 < 1 || n0 > a.n_max || K0 > a.K_max;
+            fb1 = n1 < 1 || n1 > a.n_max || K1 > a.K_max;
+            const uint32_t kmax = K0 > K1 ? K0 : K1;
+            // padding of the voters >= n, per half (0xFFFF = never acked)
+            const int r0 = n0 / 2 > 1 ? (int)(n0 / 2) : 1, r1 = n1 / 2 > 1 ? (int)(n1 / 2) : 1;
+            u64x2 idx[8];
+            uint32_t t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                idx[k] = (u64x2){0, 0};
+                t[k] = 0xFFFFFFFFu;
+                if (k < (int)kmax && k < (int)a.K_max) {
+                    idx[k] = __builtin_nontemporal_load(
+                        reinterpret_cast<const u64x2 *>(a.idx + (uint64_t)k * a.G + g));
+                    if (k > 0) {   // addRequest: index moved backward
+                        fb0 |= k < (int)K0 && idx[k].x < idx[k - 1].x;
+                        fb1 |= k < (int)K1 && idx[k].y < idx[k - 1].y;
+                    }
+                    uint32_t v[8];
+#pragma unroll
+                    for (int sl = 0; sl < 8; ++sl) {
+                        uint32_t x = 0xFFFFFFFFu;
+                        if (sl < (int)a.n_max)
+                            x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
+                                a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g));
+                        x |= (sl < (int)n0 ? 0u : 0xFFFFu) | (sl < (int)n1 ? 0u : 0xFFFF0000u);
+                        v[sl] = x;
+                    }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+                        for (int i = r & 1; i + 1 < 8; i += 2) ce_pk(v[i], v[i + 1]);
+                    }
+                    // reach time: the max(q-1, 1)-th smallest first-ack ordinal (readindex.go:84)
+                    uint32_t tk = 0;
+#pragma unroll
+                    for (int sl = 0; sl < 8; ++sl) {
+                        const uint32_t m = (sl == r0 - 1 ? 0xFFFFu : 0u) |
+                                           (sl == r1 - 1 ? 0xFFFF0000u : 0u);
+                        tk |= v[sl] & m;
+                    }
+                    t[k] = tk;
+                }
+            }
+            // suffix-min scan per group (ties go to the earlier ctx, as in k_ri_multi)
+            uint32_t bt0 = 0xFFFFu, bt1 = 0xFFFFu, rel0 = 0, rel1 = 0, be0 = 0, be1 = 0;
+            uint64_t bi0 = 0, bi1 = 0;
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+                const uint32_t t0 = t[k] & 0xFFFFu, t1 = t[k] >> 16;
+                const bool in0 = !fb0 && k < (int)K0, in1 = !fb1 && k < (int)K1;
+                bool own0 = false, own1 = false;
+                if (in0 && t0 != 0xFFFFu && t0 <= bt0) { bt0 = t0; bi0 = idx[k].x; own0 = true; }
+                if (in1 && t1 != 0xFFFFu && t1 <= bt1) { bt1 = t1; bi1 = idx[k].y; own1 = true; }
+                const bool rl0 = in0 && bt0 != 0xFFFFu, rl1 = in1 && bt1 != 0xFFFFu;
+                rel0 += rl0;
+                rel1 += rl1;
+                be0 |= (uint32_t)(rl0 && own0) << k;
+                be1 |= (uint32_t)(rl1 && own1) << k;
+                if (k < (int)a.K_max)
+                    *reinterpret_cast<u64x2 *>(a.rel + (uint64_t)k * a.G + g) =
+                        (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
+            }
+            *reinterpret_cast<uint16_t *>(a.cnt + g) = (uint16_t)(rel0 | (rel1 << 8));
+            if (a.bend) *reinterpret_cast<uint16_t *>(a.bend + g) = (uint16_t)(be0 | (be1 << 8));
+        }
+        const uint64_t f0 = __ballot(fb0), f1 = __ballot(fb1);
+        if (a.fallback && lane < 2) {
+            const uint32_t sh = 32 * lane;
+            const uint64_t w = (wbase >> 6) + lane;
+            if (w < (a.G + 63) >> 6)
+                a.fallback[w] = spread32((uint32_t)(f0 >> sh)) | (spread32((uint32_t)(f1 >> sh)) << 1);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
@@ -1781,9 +1891,24 @@ extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, u
         return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_dev: bad arguments");
     RiMultiK k{G, K_max, n_max, n_uniform, ack_ordinal, ctx_index, n_pending, n_voting,
                released_index, released_count, batch_end, fallback};
-    const unsigned grid = grid_for(G);
+    auto al = [](const void *p, uintptr_t m) { return ((uintptr_t)p & (m - 1)) == 0; };
+    const bool pairs = ctx->ri_pairs && G % 2 == 0 && al(ack_ordinal, 4) && al(ctx_index, 16) &&
+                       al(released_index, 16) && al(released_count, 2) && al(batch_end, 2) &&
+                       al(n_pending, 2) && al(n_voting, 2);
+    const unsigned grid = pairs ? grid_for(G / 2) : grid_for(G);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
+    if (pairs) {
+        if (n_pending && n_voting)
+            hipLaunchKernelGGL((k_ri_multi2<true, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+        else if (n_pending)
+            hipLaunchKernelGGL((k_ri_multi2<true, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+        else if (n_voting)
+            hipLaunchKernelGGL((k_ri_multi2<false, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+        else
+            hipLaunchKernelGGL((k_ri_multi2<false, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+        return hq::post_launch(ctx, "k_ri_multi2");
+    }
     if (n_pending && n_voting)
         hipLaunchKernelGGL((k_ri_multi<true, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
     else if (n_pending)

@@ -80,6 +80,7 @@ int hq_open(int device, uint32_t flags, hq_ctx **out) {
         const int v = std::atoi(b);
         if (v == 256 || v == 512 || v == 1024) ctx->bits_block = v;
     }
+    if (const char *r = std::getenv("HQ_RI_PAIRS")) ctx->ri_pairs = std::atoi(r) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {

@@ -104,3 +104,39 @@ def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G):
     np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
     for x in d + [rel, cnt, bend, fb]:
         gpu_ctx.free(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K_max,n_max,G,perk,pern", [(8, 8, 20_010, True, True),
+                                                     (4, 7, 4096, False, False),
+                                                     (4, 7, 4098, True, False),
+                                                     (3, 5, 130, False, True),
+                                                     (2, 3, 2, True, True),
+                                                     (1, 1, 64, False, False)])
+def test_kernel_pairs_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
+    """Even G with aligned columns takes the two-groups-per-lane kernel (packed u16 sorting):
+    every combination of per-group / uniform pending count and voter count, bit-exact."""
+    rng = np.random.default_rng(K_max * 1000 + n_max + G)
+    ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
+    if pern:
+        n[::97] = 0
+    if G > 5:
+        idx.reshape(K_max, G)[:, 5] = np.arange(K_max, 0, -1)
+    Kp = K if perk else None
+    nv = n if pern else None
+    nu = 0 if pern else n_max
+    want_rel, want_cnt, want_fb, want_bend = qref.readindex_multi_batch(ord_, idx, Kp, nv, nu,
+                                                                        K_max, n_max)
+    d = [gpu_ctx.upload(x) if x is not None else None for x in (ord_, idx, Kp, nv)]
+    rel = gpu_ctx.empty(K_max * G, np.uint64)
+    cnt = gpu_ctx.empty(G, np.uint8)
+    bend = gpu_ctx.empty(G, np.uint8)
+    fb = gpu_ctx.empty(hq.words64(G), np.uint64)
+    gpu_ctx.memset(fb, 0xFF)
+    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], nu, rel, cnt, fb, bend)
+    np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
+    np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
+    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
+    np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
+    for x in [x for x in d if x is not None] + [rel, cnt, bend, fb]:
+        gpu_ctx.free(x)
