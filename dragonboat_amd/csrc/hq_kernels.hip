@@ -1179,6 +1179,9 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     }
 }
 
+#ifndef HQ_FUSED_BIG_NMAX
+#define HQ_FUSED_BIG_NMAX 5
+#endif
 extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count) {
     if (!ctx) return HQ_E_INVAL;
     if (count && !args) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_fused_dev: args is NULL");
@@ -1198,7 +1201,7 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     bool big = true;
     // (the fused kernel's bodies fit 64 VGPRs without spilling for these two forms only)
     for (uint32_t i = 0; i < count; ++i)
-        big &= args[i].n_max <= 5 &&
+        big &= args[i].n_max <= HQ_FUSED_BIG_NMAX &&
                (args[i].form == HQ_FORM_TERM_START || args[i].form == HQ_FORM_TERM_MASK);
     const int B = big ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
     uint64_t blocks = 0;
