@@ -714,13 +714,15 @@ __device__ __forceinline__ uint32_t popc_bytes(uint32_t x) {
 __device__ __forceinline__ uint32_t ge_bytes(uint32_t a, uint32_t b) {
     return ((a | kB80) - b) & kB80;
 }
-// 4 flag bytes (0x80 / 0x00) -> 4 consecutive bits (group k -> bit k)
+// 4 flag bytes (0x80 / 0x00) -> 4 consecutive bits (group k -> bit k): a byte dot product with
+// weights 1, 2, 4, 8 (v_dot4_u32_u8, full rate; the multiply it replaces is quarter rate)
 __device__ __forceinline__ uint32_t pack4(uint32_t f) {
-    return (((f >> 7) & kB01) * 0x01020408u) >> 24;   // byte k's bit -> bit 24 + k
+    return __builtin_amdgcn_udot4(f, 0x08040201u, 0u, false) >> 7;
 }
-// 4 flag bytes -> bits 0, 2, 4, 6 (the low bit of 2-bit fields)
-__device__ __forceinline__ uint32_t pack4x2(uint32_t f) {
-    return (((f >> 7) & kB01) * 0x01041040u) >> 24;   // byte k's bit -> bit 24 + 2k
+// 4 flag bytes -> bits 0, 2, 4, 6 (the low bit of 2-bit fields); `hi` flags -> bits 1, 3, 5, 7
+__device__ __forceinline__ uint32_t pack4x2(uint32_t f, uint32_t hi = 0) {
+    return __builtin_amdgcn_udot4(f, 0x40100401u, __builtin_amdgcn_udot4(hi, 0x80200802u, 0u, false),
+                                  false) >> 7;
 }
 // per-byte valid n in [1, 8] -> 0x80
 __device__ __forceinline__ uint32_t valid_n(uint32_t n) {
@@ -793,7 +795,7 @@ __device__ __forceinline__ void bits_slot(const BitsK &a, uint64_t g, uint32_t n
             const uint32_t foll = ge_bytes(popc_bytes(rm), quorum) & ok & ~lead;
             const uint32_t cand = inr & ~lead & ~foll;
             // 2-bit codes: leader 2 (bit 1), candidate 1 (bit 0), follower 0
-            outc |= (pack4x2(cand) | (pack4x2(lead) << 1)) << (8 * w);
+            outc |= pack4x2(cand, lead) << (8 * w);
         }
         if constexpr (MODE & kCHECKQ) {
             const uint32_t self = kB01 << a.self_slot;
