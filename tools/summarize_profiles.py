@@ -28,7 +28,7 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, false>", "c2t": "k_commit_big<3, 0
           "c5t": "k_commit_fused<2, 512, true>", "c5s": "k_commit<7, 2, 2, false, false>",
           "c2l": "k_commit_lag_big<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
           "c5l": "k_commit_lag_fused<2, 512>", "rim": "k_ri_multi2<false, false>",
-          "cq": "k_bits<4, false", "ing": "k_ingest_match", "ingo": "k_ingest_match", "rim2": "k_ri_multi2"}
+          "cq": "k_bits<4, false, 256, false, true>", "ing": "k_ingest_match", "ingo": "k_ingest_match", "rim2": "k_ri_multi2"}
 
 
 def counter(path, kernel):
