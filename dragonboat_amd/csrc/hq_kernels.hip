@@ -732,7 +732,8 @@ __device__ __forceinline__ uint32_t valid_n(uint32_t n) {
 // per-byte (1 << n) - 1 for n in [0, 8] with v_perm_b32 as a byte lookup table: selectors 0..7
 // pick masks 0x00..0x7F from {0x7F3F1F0F, 0x07030100}; selector 13 (n = 8) yields 0xFF
 __device__ __forceinline__ uint32_t mask_n(uint32_t n) {
-    const uint32_t sel = n | (((n >> 3) & kB01) * 0x0Du);
+    const uint32_t b3 = n & 0x08080808u;   // n = 8 -> selector 8 | 4 | 1 = 13 (no multiply)
+    const uint32_t sel = n | (b3 >> 1) | (b3 >> 3);
     return __builtin_amdgcn_perm(0x7F3F1F0Fu, 0x07030100u, sel);
 }
 
