@@ -1182,6 +1182,9 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     }
 }
 
+#ifndef HQ_FUSED_HEAVY_FIRST
+#define HQ_FUSED_HEAVY_FIRST 1
+#endif
 #ifndef HQ_FUSED_BIG_NMAX
 #define HQ_FUSED_BIG_NMAX 5
 #endif
@@ -1208,12 +1211,26 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
                (args[i].form == HQ_FORM_TERM_START || args[i].form == HQ_FORM_TERM_MASK);
     const int B = big ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
     uint64_t blocks = 0;
-    for (uint32_t i = 0; i < count; ++i) {
-        f.b[i] = commit_k(args + i);
-        f.n[i] = (uint8_t)args[i].n_max;
+    // workgroup ranges in launch order, the widest batches first (their waves are dispatched
+    // first, so the tail is made of the light ones: c5t 96-97 -> 93-94 us,
+    // profiles/r01f/ab_heavy_first.log; HQ_FUSED_HEAVY_FIRST=0 keeps the argument order)
+    uint32_t order[kMaxFused];
+    for (uint32_t i = 0; i < count; ++i) order[i] = i;
+#if HQ_FUSED_HEAVY_FIRST
+    for (uint32_t i = 1; i < count; ++i)
+        for (uint32_t j = i; j > 0 && args[order[j]].n_max > args[order[j - 1]].n_max; --j) {
+            const uint32_t t = order[j];
+            order[j] = order[j - 1];
+            order[j - 1] = t;
+        }
+#endif
+    for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t i = k;
+        f.b[i] = commit_k(args + order[k]);
+        f.n[i] = (uint8_t)args[order[k]].n_max;
         f.first[i] = (uint32_t)blocks;
         // the same lanes per batch as its own launch would get (grid-stride beyond that)
-        blocks += grid_for((args[i].G + 1) / 2, B, (uint64_t)kMaxBlocks * 256 / B);
+        blocks += grid_for((args[order[k]].G + 1) / 2, B, (uint64_t)kMaxBlocks * 256 / B);
     }
     for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
     int rc = hq::pre_launch(ctx);
