@@ -1182,6 +1182,9 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     }
 }
 
+#ifndef HQ_LAG_HEAVY_FIRST
+#define HQ_LAG_HEAVY_FIRST 1
+#endif
 #ifndef HQ_FUSED_HEAVY_FIRST
 #define HQ_FUSED_HEAVY_FIRST 1
 #endif
@@ -1388,11 +1391,22 @@ extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *ar
     for (uint32_t i = 0; i < count; ++i) big &= args[i].n_max <= 4;
     const int B = big ? HQ_COMMIT_BLOCK_BIG : kCommitBlock;
     uint64_t blocks = 0;
+    uint32_t order[kMaxFused];
+    for (uint32_t i = 0; i < count; ++i) order[i] = i;
+#if HQ_LAG_HEAVY_FIRST
+    for (uint32_t i = 1; i < count; ++i)   // the widest batches first, as in hq_commit_fused_dev
+        for (uint32_t j = i; j > 0 && args[order[j]].n_max > args[order[j - 1]].n_max; --j) {
+            const uint32_t t = order[j];
+            order[j] = order[j - 1];
+            order[j - 1] = t;
+        }
+#endif
     for (uint32_t i = 0; i < count; ++i) {
-        f.b[i] = lag_k(args + i);
-        f.n[i] = (uint8_t)args[i].n_max;
+        const hq_commit_lag_args *b = args + order[i];
+        f.b[i] = lag_k(b);
+        f.n[i] = (uint8_t)b->n_max;
         f.first[i] = (uint32_t)blocks;
-        blocks += grid_for((args[i].G + kLagVec - 1) / kLagVec, B, (uint64_t)kMaxBlocks * 256 / B);
+        blocks += grid_for((b->G + kLagVec - 1) / kLagVec, B, (uint64_t)kMaxBlocks * 256 / B);
     }
     for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
     int rc = hq::pre_launch(ctx);
