@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Quorum-decision throughput of the MI355X batched quorum engine (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2tl|c2t|c3mt|c4t|...] [--no-cpu]
 
 A step is one pass of the hot path over one batch of synthetic groups resident in HBM: for the
-headline workload (BASELINE configs[1], "c2") one hq_commit_dev launch over 1,048,576 groups x 3
-voters in the term-start form. Inputs are generated on the device from splitmix64 seeds and rotate
+headline workload (BASELINE configs[1], "c2tl") one hq_commit_dev launch over 1,048,576 groups x 3
+voters in the term-start form, read from 128-group tiles that carry the leader's match as its
+lastIndex (HQ_LAYOUT_TILES_LEADER, raft.go:918; 48 B per decision). Inputs are generated on the device from splitmix64 seeds and rotate
 over >= 1.1 GiB of distinct batches so that the 256 MiB Infinity Cache cannot serve them.
 
 N > 1: one process per GPU (torch.distributed.run), groups sharded clusterID % N
@@ -39,6 +40,18 @@ WORKLOADS = {
     "c2t": dict(cfg=1, kind="commit", G=1 << 20, n=3, form=0, mixed=False, tiled=True,
                 desc="1M groups x 3 voters, batched commit-index kernel (term-start form) over "
                      "128-group tiles (HQ_LAYOUT_TILES: one contiguous stream per wave)"),
+    "c2tl": dict(cfg=1, kind="commit", G=1 << 20, n=3, form=0, mixed=False, tiled=True, lead=True,
+                 desc="1M groups x 3 voters, batched commit-index kernel (term-start form) over "
+                      "128-group tiles without the leader's match row (HQ_LAYOUT_TILES_LEADER: "
+                      "slot 0 = lastIndex, raft.go:918; 48 B per decision)"),
+    "c3mtl": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False, tiled=True,
+                  lead=True, desc="1M groups x 5 voters (4 full + 1 witness), current-term mask, "
+                                  "128-group tiles without the leader's match row"),
+    "c5v5tl": dict(cfg=2, kind="commit", G=8 << 20, n=5, form=2, mixed=False, tiled=True,
+                   lead=True, desc="as c5v5t without the leader's match row "
+                                   "(HQ_LAYOUT_TILES_LEADER)"),
+    "c5tl": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True, tiled=True, lead=True,
+                 desc="as c5t without the leader's match row (HQ_LAYOUT_TILES_LEADER)"),
     "c3mt": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False, tiled=True,
                  desc="1M groups x 5 voters (4 full + 1 witness), current-term mask, "
                       "128-group tiles"),
@@ -103,7 +116,9 @@ def algo_bytes_per_group(w):
         n, extra_n = w["n"], (1 if w["mixed"] else 0)
         # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask
         # | term + gathered u32 ring term)
-        return 8 * n + 24 + {0: 8, 1: 16, 2: 2, 3: 12}[w["form"]] + extra_n
+        # (the leader-row tile layout carries slot 0 as last_index: 8 bytes less)
+        return (8 * (n - 1 if w.get("lead") else n) + 24 + {0: 8, 1: 16, 2: 2, 3: 12}[w["form"]]
+                + extra_n)
     # ack, granted, rejected (+ n unless uniform) u8 each in; confirmed bit + 2-bit outcome out
     return (3 if w.get("uniform") else 4) + 3 / 8
 
@@ -223,10 +238,12 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             for n, rng in commit_buckets(shard, w, d):
                 spec = hq.synth_spec(seed + (s << 40), rng.count, n, cid_base=rng.cid_base,
                                      cid_stride=rng.cid_stride)
-                b = hq.alloc_commit(ctx, rng.count, n, w["form"], 16, tiled=w.get("tiled", False))
+                lay = hq.HQ_LAYOUT_TILES_LEADER if w.get("lead") else hq.HQ_LAYOUT_TILES
+                b = hq.alloc_commit(ctx, rng.count, n, w["form"], 16,
+                                    tiled=w.get("tiled", False), tile_layout=lay)
                 ctx.synth_commit_dev(spec, b.args())
                 if b.tiles is not None:
-                    ctx.tile_commit_dev(b.args(), b.tiles)
+                    ctx.tile_commit_dev(b.args(), b.tiles, lay)
                 buckets.append(b)
             sets.append(buckets)
         elif w["kind"] == "lag":
@@ -864,12 +881,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", default="c2t", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c2tl", choices=sorted(WORKLOADS))
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
-                    default="c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5r32t,c4,c4t,c4u,c4ut,c5,c5t,c5s,c5l,"
+                    default="c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3mtl,c3l,c5v5t,c5v5tl,c5v5r32t,"
+                            "c4,c4t,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,"
                             "c5r,c5r32,rim,"
                             "cq,ing,ingo,w2,e2e,step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
@@ -935,7 +953,8 @@ def main():
                 "form": ({0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
                          + ("_lag" if w["kind"] == "lag" else ""))
                 if w["kind"] in ("commit", "lag") else "bitmaps",
-                "layout": "tiles" if w.get("tiled") else "columns",
+                "layout": ("tiles_leader" if w.get("lead") else "tiles") if w.get("tiled")
+                else "columns",
                 "global_groups_per_step": w["G"] * d.world,
                 "parallelism": f"shard{d.world} (clusterID % {d.world})",
             },

@@ -199,8 +199,9 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
 // one workgroup `blk` of `nblk` working on batch `a` (k_commit: the grid; k_commit_fused: the
 // workgroups one batch of the launch owns). TILED (HQ_LAYOUT_TILES, VEC = 2 only): a wave's 128
 // groups are one tile, so its loads walk one contiguous 128·(n+3)·8-byte block instead of n + 3
-// column streams.
-template <int N, int FORM, bool PERN, int BLK>
+// column streams. TILED = 2 (HQ_LAYOUT_TILES_LEADER): the same tiles without the leader's match
+// row; slot 0 is last_index (the leader's own match, raft.go:918, 1031).
+template <int N, int FORM, bool PERN, int BLK, int LEAD>
 __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk);
 
 template <int N, int FORM, int VEC, bool PERN, int BLK>
@@ -311,16 +312,19 @@ __device__ __forceinline__ void column_blocks(const CommitK &a, uint64_t blk, ui
 // every field of the wave is ONE contiguous block of (n + 3) KiB, and the two ballots are the
 // tile's two bitmap words as they are (no bit interleave). The full-tile test is scalar (the
 // wave index is read into an SGPR), so full tiles carry no per-lane guard.
-template <int N, int FORM, int VEC, bool PERN, int BLK, bool TILED = false>
+template <int N, int FORM, int VEC, bool PERN, int BLK, int TILED = 0>
 __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     static_assert(!TILED || VEC == 2, "tiles are read two groups per lane");
-    if constexpr (TILED) tile_blocks<N, FORM, PERN, BLK>(a, blk, nblk);
+    if constexpr (TILED) tile_blocks<N, FORM, PERN, BLK, TILED == 2 ? 1 : 0>(a, blk, nblk);
     else column_blocks<N, FORM, VEC, PERN, BLK>(a, blk, nblk);
 }
 
-template <int N, int FORM, bool PERN, int BLK>
+// LEAD = 1: rows start at slot 1 (row s - 1 holds slot s) and m[0] = last_index, so the wave's
+// block is (n + 2) KiB: 8 bytes less per group.
+template <int N, int FORM, bool PERN, int BLK, int LEAD>
 __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     constexpr uint64_t T = HQ_TILE_GROUPS, H = T / 2;
+    constexpr int NR = N - LEAD;   // match rows in the tile
     const uint64_t lane = threadIdx.x & 63;
     const uint64_t wave = blk * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = nblk * BLK * 2;
@@ -331,19 +335,23 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
         if (wbase + T <= a.G) {
             uint64_t m0[N], m1[N];
 #pragma unroll
-            for (int s = 0; s < N; ++s) {
-                const u64x2 v = ld_stream2(t + s * T);
+            for (int s = LEAD; s < N; ++s) {
+                const u64x2 v = ld_stream2(t + (s - LEAD) * T);
                 m0[s] = v.x;
                 m1[s] = v.y;
             }
-            const u64x2 ci = ld_stream2(t + N * T), la = ld_stream2(t + (N + 1) * T);
+            const u64x2 ci = ld_stream2(t + NR * T), la = ld_stream2(t + (NR + 1) * T);
+            if constexpr (LEAD) {
+                m0[0] = la.x;
+                m1[0] = la.y;
+            }
             u64x2 ax;
             if constexpr (FORM == HQ_FORM_TERM_MASK) {
                 const uint32_t mm = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
-                    reinterpret_cast<const uint16_t *>(t - lane * 2 + (N + 2) * T) + lane * 2));
+                    reinterpret_cast<const uint16_t *>(t - lane * 2 + (NR + 2) * T) + lane * 2));
                 ax = (u64x2){mm & 0xFFFFu, mm >> 16};
             } else {
-                ax = ld_stream2(t + (N + 2) * T);
+                ax = ld_stream2(t + (NR + 2) * T);
             }
             const int na = PERN ? (int)a.nv[ga] : N, nb = PERN ? (int)a.nv[gb] : N;
             uint64_t coa, cob;
@@ -355,15 +363,17 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
             auto single = [&](int j, bool &c, bool &f) {
                 const uint64_t g = ga + H * j;
                 uint64_t m[N];
+                const uint64_t last = t[(NR + 1) * T + j];
 #pragma unroll
-                for (int s = 0; s < N; ++s) m[s] = t[s * T + j];
+                for (int s = LEAD; s < N; ++s) m[s] = t[(s - LEAD) * T + j];
+                if constexpr (LEAD) m[0] = last;
                 const uint64_t ax =
                     FORM == HQ_FORM_TERM_MASK
-                        ? (uint64_t)reinterpret_cast<const uint16_t *>(t - lane * 2 + (N + 2) * T)[lane * 2 + j]
-                        : t[(N + 2) * T + j];
+                        ? (uint64_t)reinterpret_cast<const uint16_t *>(t - lane * 2 + (NR + 2) * T)[lane * 2 + j]
+                        : t[(NR + 2) * T + j];
                 uint64_t co;
-                decide<N, FORM, PERN>(a, g, m, PERN ? (int)a.nv[g] : N, t[N * T + j],
-                                      t[(N + 1) * T + j], ax, co, c, f);
+                decide<N, FORM, PERN>(a, g, m, PERN ? (int)a.nv[g] : N, t[NR * T + j], last, ax,
+                                      co, c, f);
                 a.cout[g] = co;
             };
             if (ga < a.G) single(0, ca, fa);
@@ -379,12 +389,12 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
     }
 }
 
-template <int N, int FORM, int VEC, bool PERN, bool TILED>
+template <int N, int FORM, int VEC, bool PERN, int TILED>
 __global__ __launch_bounds__(kCommitBlock) void k_commit(const CommitK a) {
     commit_blocks<N, FORM, VEC, PERN, kCommitBlock, TILED>(a, blockIdx.x, gridDim.x);
 }
 // the 1024-thread twin: two blocks per CU need occupancy 8 (<= 64 VGPRs), so it is asked for
-template <int N, int FORM, int VEC, bool PERN, bool TILED>
+template <int N, int FORM, int VEC, bool PERN, int TILED>
 __global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_big(const CommitK a) {
     commit_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG, TILED>(a, blockIdx.x, gridDim.x);
 }
@@ -401,7 +411,7 @@ struct FusedK {
     uint32_t count;
 };
 
-template <int FORM, int BLK, bool TILED>
+template <int FORM, int BLK, int TILED>
 __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_fused(const FusedK f) {
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
@@ -1021,7 +1031,7 @@ unsigned grid_for(uint64_t lanes_needed, int block = kBlock, uint64_t max_blocks
     return (unsigned)b;
 }
 
-template <int N, int FORM, int VEC, bool PERN, bool TILED = false>
+template <int N, int FORM, int VEC, bool PERN, int TILED = 0>
 int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
     constexpr int B = commit_blk<N, FORM, PERN>();
     const unsigned grid = grid_for((k.G + VEC - 1) / VEC, B, kMaxBlocks * 256 / B);
@@ -1036,12 +1046,15 @@ int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
     return hq::post_launch(ctx, "k_commit");
 }
 
-// tiles are always read two groups per lane (the validation requires a 16-byte aligned base)
+// tiles are always read two groups per lane (the validation requires a 16-byte aligned base);
+// tiled: 0 columns, 1 HQ_LAYOUT_TILES, 2 HQ_LAYOUT_TILES_LEADER
 template <int N>
-int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool pern, bool tiled) {
+int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool pern, int tiled) {
 #define HQ_DISPATCH(F)                                                                   \
-    if (tiled) return pern ? launch_commit_t<N, F, 2, true, true>(ctx, k)         \
-                                  : launch_commit_t<N, F, 2, false, true>(ctx, k);       \
+    if (tiled == 2) return pern ? launch_commit_t<N, F, 2, true, 2>(ctx, k)              \
+                                : launch_commit_t<N, F, 2, false, 2>(ctx, k);            \
+    if (tiled) return pern ? launch_commit_t<N, F, 2, true, 1>(ctx, k)                   \
+                           : launch_commit_t<N, F, 2, false, 1>(ctx, k);                 \
     if (vec2) return pern ? launch_commit_t<N, F, 2, true>(ctx, k)                       \
                           : launch_commit_t<N, F, 2, false>(ctx, k);                     \
     return pern ? launch_commit_t<N, F, 1, true>(ctx, k) : launch_commit_t<N, F, 1, false>(ctx, k);
@@ -1062,10 +1075,11 @@ int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
     if (a->n_max < 1 || a->n_max > HQ_MAX_VOTERS)
         return hq::fail(ctx, HQ_E_INVAL, "hq_commit: n_max must be 1..8");
-    if (a->layout != HQ_LAYOUT_COLUMNS && a->layout != HQ_LAYOUT_TILES)
+    if (a->layout != HQ_LAYOUT_COLUMNS && a->layout != HQ_LAYOUT_TILES &&
+        a->layout != HQ_LAYOUT_TILES_LEADER)
         return hq::fail(ctx, HQ_E_INVAL, "hq_commit: unknown layout");
     if (a->G == 0) return HQ_OK;
-    const bool tiles = a->layout == HQ_LAYOUT_TILES;
+    const bool tiles = a->layout != HQ_LAYOUT_COLUMNS;
     if (tiles) {
         if (!a->match || !a->committed_out)
             return hq::fail(ctx, HQ_E_INVAL, "hq_commit: NULL tiles (match) / committed_out");
@@ -1105,9 +1119,9 @@ namespace {
 
 CommitK commit_k(const hq_commit_args *a) {
     CommitK k{};
-    const bool tiles = a->layout == HQ_LAYOUT_TILES;
+    const bool tiles = a->layout != HQ_LAYOUT_COLUMNS;
     k.G = a->G;
-    k.stride = tiles ? hq_commit_tile_words(a->n_max, a->form) : a->match_stride;
+    k.stride = tiles ? hq_commit_tile_words_for(a->n_max, a->form, a->layout) : a->match_stride;
     k.R = a->ring_len;
     k.match = a->match;
     k.nv = a->n_voting;
@@ -1150,7 +1164,7 @@ CommitCols commit_cols(const hq_commit_args *a) {
 
 // every column of the batch can be read two groups per lane with 16-byte loads
 bool commit_vec2(const hq_commit_args *a) {
-    if (a->layout == HQ_LAYOUT_TILES) return true;   // alignment checked by validate_commit
+    if (a->layout != HQ_LAYOUT_COLUMNS) return true;   // alignment checked by validate_commit
     const bool aux_ok = a->form == HQ_FORM_TERM_START ? hq::aligned16(a->term_start)
                       : a->form == HQ_FORM_TERM_MASK
                           ? (reinterpret_cast<uintptr_t>(a->term_mask) & 3) == 0
@@ -1169,7 +1183,7 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     const CommitK k = commit_k(a);
     const bool vec2 = commit_vec2(a);
     const bool pern = a->n_voting != nullptr;
-    const bool tiled = a->layout == HQ_LAYOUT_TILES;
+    const int tiled = a->layout == HQ_LAYOUT_TILES_LEADER ? 2 : a->layout == HQ_LAYOUT_TILES ? 1 : 0;
     switch (a->n_max) {
     case 1: return launch_commit_n<1>(ctx, k, a->form, vec2, pern, tiled);
     case 2: return launch_commit_n<2>(ctx, k, a->form, vec2, pern, tiled);
@@ -1239,11 +1253,14 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
 #define HQ_FUSED(F, BLK)                                                                       \
-    if (args[0].layout == HQ_LAYOUT_TILES)                                                     \
-        hipLaunchKernelGGL((k_commit_fused<F, BLK, true>), dim3(blocks), dim3(BLK), 0,         \
+    if (args[0].layout == HQ_LAYOUT_TILES_LEADER)                                              \
+        hipLaunchKernelGGL((k_commit_fused<F, BLK, 2>), dim3(blocks), dim3(BLK), 0,            \
+                           ctx->stream, f);                                                    \
+    else if (args[0].layout == HQ_LAYOUT_TILES)                                                \
+        hipLaunchKernelGGL((k_commit_fused<F, BLK, 1>), dim3(blocks), dim3(BLK), 0,            \
                            ctx->stream, f);                                                    \
     else                                                                                       \
-        hipLaunchKernelGGL((k_commit_fused<F, BLK, false>), dim3(blocks), dim3(BLK), 0,        \
+        hipLaunchKernelGGL((k_commit_fused<F, BLK, 0>), dim3(blocks), dim3(BLK), 0,            \
                            ctx->stream, f);
     switch (args[0].form) {
     case HQ_FORM_TERM_START:
@@ -1630,10 +1647,12 @@ extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,
     return hq::post_launch(ctx, "k_synth_commit");
 }
 
-// Columns -> HQ_LAYOUT_TILES tiles, one thread per tile word (include/hipquorum.h). Builds
-// tiled inputs from column batches on the device (benchmark inputs, device-side packers).
+// Columns -> HQ_LAYOUT_TILES(_LEADER) tiles, one thread per tile word (include/hipquorum.h).
+// Builds tiled inputs from column batches on the device (benchmark inputs, device-side packers).
+// lead = 1 drops slot 0's row: tile row r < n holds match slot r + 1.
 __global__ __launch_bounds__(kBlock) void k_tile_commit(const CommitCols c, uint64_t *tiles,
-                                                        uint64_t ntiles, uint32_t n, int form) {
+                                                        uint64_t ntiles, uint32_t n, int form,
+                                                        int lead) {
     const uint64_t tw = c.tile_words, total = ntiles * tw;
     for (uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x; w < total;
          w += (uint64_t)gridDim.x * kBlock) {
@@ -1650,7 +1669,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_commit(const CommitCols c, uint
         } else {
             const uint64_t g = group(r % HQ_TILE_GROUPS);
             if (g < c.G) {
-                v = row < n       ? c.match[row * c.stride + g]
+                v = row < n       ? c.match[(row + lead) * c.stride + g]
                   : row == n      ? c.cin[g]
                   : row == n + 1  ? c.last[g]
                   : form == HQ_FORM_TERM_START ? c.tstart[g] : c.term[g];
@@ -1661,20 +1680,29 @@ __global__ __launch_bounds__(kBlock) void k_tile_commit(const CommitCols c, uint
 }
 
 extern "C" int hq_tile_commit_dev(hq_ctx *ctx, const hq_commit_args *a, uint64_t *tiles) {
+    return hq_tile_commit_as_dev(ctx, a, tiles, HQ_LAYOUT_TILES);
+}
+
+extern "C" int hq_tile_commit_as_dev(hq_ctx *ctx, const hq_commit_args *a, uint64_t *tiles,
+                                     uint32_t layout) {
     if (!ctx) return HQ_E_INVAL;
     if (!a || !tiles) return hq::fail(ctx, HQ_E_INVAL, "hq_tile_commit: NULL argument");
     if (a->layout != HQ_LAYOUT_COLUMNS)
         return hq::fail(ctx, HQ_E_INVAL, "hq_tile_commit: input must be the column layout");
+    if (layout != HQ_LAYOUT_TILES && layout != HQ_LAYOUT_TILES_LEADER)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_commit: target must be a tile layout");
     hq_commit_args chk = *a;
     chk.committed_out = chk.committed_out ? chk.committed_out : tiles;  // not written here
     int rc = validate_commit(ctx, &chk);
     if (rc || a->G == 0) return rc;
-    const CommitCols k = commit_cols(a);
+    const int lead = layout == HQ_LAYOUT_TILES_LEADER ? 1 : 0;
+    CommitCols k = commit_cols(a);
+    k.tile_words = hq_commit_tile_words_for(a->n_max, a->form, layout);
     const uint64_t ntiles = hq_commit_tiles(a->G);
     rc = hq::pre_launch(ctx);
     if (rc) return rc;
     hipLaunchKernelGGL(k_tile_commit, dim3(grid_for(ntiles * k.tile_words)), dim3(kBlock), 0,
-                       ctx->stream, k, tiles, ntiles, a->n_max, (int)a->form);
+                       ctx->stream, k, tiles, ntiles, a->n_max - lead, (int)a->form, lead);
     return hq::post_launch(ctx, "k_tile_commit");
 }
 

@@ -205,8 +205,16 @@ extern "C" int hq_unpack_lags(uint64_t G, const uint64_t *last_index, const int3
 // Columns -> HQ_LAYOUT_TILES tiles on the host (the twin of k_tile_commit): a step worker that
 // packs columns can hand the kernel one contiguous staging block per 128 groups instead.
 extern "C" int hq_tile_commit_host(const hq_commit_args *a, uint64_t *tiles) {
+    return hq_tile_commit_as_host(a, tiles, HQ_LAYOUT_TILES);
+}
+
+// HQ_LAYOUT_TILES_LEADER drops slot 0's row, which the layout defines as last_index (the
+// leader's own match, raft.go:918 appendEntries / :1031 reset). A group with n >= 1 whose
+// slot 0 differs is refused (HQ_E_INVAL): the layout cannot carry it.
+extern "C" int hq_tile_commit_as_host(const hq_commit_args *a, uint64_t *tiles, uint32_t layout) {
     if (!a || !tiles || a->layout != HQ_LAYOUT_COLUMNS || a->n_max < 1 ||
-        a->n_max > HQ_MAX_VOTERS || a->form > HQ_FORM_TERM_RING32)
+        a->n_max > HQ_MAX_VOTERS || a->form > HQ_FORM_TERM_RING32 ||
+        (layout != HQ_LAYOUT_TILES && layout != HQ_LAYOUT_TILES_LEADER))
         return HQ_E_INVAL;
     if (a->G == 0) return HQ_OK;
     const bool mask = a->form == HQ_FORM_TERM_MASK;
@@ -214,8 +222,13 @@ extern "C" int hq_tile_commit_host(const hq_commit_args *a, uint64_t *tiles) {
     if (!a->match || !a->committed_in || !a->last_index || a->match_stride < a->G ||
         (mask ? !a->term_mask : !aux))
         return HQ_E_INVAL;
-    const uint32_t n = a->n_max;
-    const uint64_t tw = hq_commit_tile_words(n, a->form), T = HQ_TILE_GROUPS;
+    const uint32_t lead = layout == HQ_LAYOUT_TILES_LEADER ? 1 : 0;
+    if (lead)
+        for (uint64_t g = 0; g < a->G; ++g)
+            if ((!a->n_voting || a->n_voting[g] >= 1) && a->match[g] != a->last_index[g])
+                return HQ_E_INVAL;
+    const uint32_t n = a->n_max - lead;   // match rows per tile
+    const uint64_t tw = hq_commit_tile_words_for(a->n_max, a->form, layout), T = HQ_TILE_GROUPS;
     for (uint64_t t = 0; t < hq_commit_tiles(a->G); ++t) {
         uint64_t *tile = tiles + t * tw;
         std::memset(tile, 0, tw * 8);
@@ -224,7 +237,8 @@ extern "C" int hq_tile_commit_host(const hq_commit_args *a, uint64_t *tiles) {
         for (uint64_t p = 0; p < T; ++p) {
             const uint64_t g = t * T + (p >> 1) + (T / 2) * (p & 1);
             if (g >= a->G) continue;
-            for (uint32_t s = 0; s < n; ++s) tile[s * T + p] = a->match[s * a->match_stride + g];
+            for (uint32_t s = 0; s < n; ++s)
+                tile[s * T + p] = a->match[(s + lead) * a->match_stride + g];
             tile[n * T + p] = a->committed_in[g];
             tile[(n + 1) * T + p] = a->last_index[g];
             if (mask) mrow[p] = a->term_mask[g];

@@ -269,7 +269,8 @@ struct Stage {
 int h2d(hq_ctx *ctx, void *d, const void *h, size_t b) { return hq_memcpy_async(ctx, d, h, b, 0); }
 int d2h(hq_ctx *ctx, void *h, const void *d, size_t b) { return hq_memcpy_async(ctx, h, d, b, 1); }
 
-// HQ_LAYOUT_TILES from host memory: the tiles are one block, so the whole input is one H2D copy
+// HQ_LAYOUT_TILES(_LEADER) from host memory: the tiles are one block, so the whole input is one
+// H2D copy
 int commit_tiles_host(hq_ctx *ctx, const hq_commit_args *a) {
     if (!a->match || !a->committed_out || a->n_max < 1 || a->n_max > HQ_MAX_VOTERS ||
         a->form > HQ_FORM_TERM_RING32)
@@ -278,7 +279,8 @@ int commit_tiles_host(hq_ctx *ctx, const hq_commit_args *a) {
     if ((ring && !a->ring) || (ring32 && !a->ring32)) return hq_commit_dev(ctx, a);
     if ((ring || ring32) && (a->ring_len < 1 || a->ring_len > 1024)) return hq_commit_dev(ctx, a);
     const uint64_t G = a->G, nw = hq::words64(G);
-    const size_t tiles = hq_commit_tiles(G) * hq_commit_tile_words(a->n_max, a->form) * 8;
+    const size_t tiles =
+        hq_commit_tiles(G) * hq_commit_tile_words_for(a->n_max, a->form, a->layout) * 8;
     const size_t ring_bytes = ring ? G * 8 * a->ring_len : ring32 ? G * 4 * a->ring_len : 0;
     const size_t need = Stage::pad(tiles) + Stage::pad(G * 8) + 2 * Stage::pad(nw * 8) +
                         Stage::pad(G) + Stage::pad(ring_bytes);
@@ -321,7 +323,8 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (!ctx) return HQ_E_INVAL;
     if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
     if (a->G == 0) return HQ_OK;
-    if (a->layout == HQ_LAYOUT_TILES) return commit_tiles_host(ctx, a);
+    if (a->layout == HQ_LAYOUT_TILES || a->layout == HQ_LAYOUT_TILES_LEADER)
+        return commit_tiles_host(ctx, a);
     if (!a->match || !a->committed_in || !a->committed_out || !a->last_index ||
         a->n_max < 1 || a->n_max > HQ_MAX_VOTERS || a->match_stride < a->G)
         return hq_commit_dev(ctx, a);  // same validation and message

@@ -31,8 +31,9 @@ HQ_FORM_TERM_MASK = 2
 HQ_FORM_TERM_RING32 = 3
 HQ_LAYOUT_COLUMNS = 0
 HQ_LAYOUT_TILES = 1
+HQ_LAYOUT_TILES_LEADER = 2   # tiles without the leader row: slot 0 = last_index
 HQ_TILE_GROUPS = 128
-HQ_ABI_VERSION = 5
+HQ_ABI_VERSION = 6
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -230,6 +231,8 @@ SIGNATURES = {
     "hq_pack_ring32": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp]),
     "hq_tile_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), _vp]),
     "hq_tile_commit_host": (ctypes.c_int, [ctypes.POINTER(CommitArgs), _vp]),
+    "hq_tile_commit_as_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), _vp, ctypes.c_uint32]),
+    "hq_tile_commit_as_host": (ctypes.c_int, [ctypes.POINTER(CommitArgs), _vp, ctypes.c_uint32]),
     "hq_pack_votes": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hq_pack_acks": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_uint32, _vp]),
@@ -424,9 +427,14 @@ class Context:
     def commit_host(self, args: CommitArgs) -> None:
         self._check(lib.hq_commit(self.h, ctypes.byref(args)))
 
-    def tile_commit_dev(self, columns: CommitArgs, tiles) -> None:
-        """hq_tile_commit_dev: the column batch's inputs cut into HQ_LAYOUT_TILES tiles."""
-        self._check(lib.hq_tile_commit_dev(self.h, ctypes.byref(columns), _p(tiles)))
+    def tile_commit_dev(self, columns: CommitArgs, tiles, layout: int = HQ_LAYOUT_TILES) -> None:
+        """hq_tile_commit_dev / hq_tile_commit_as_dev: the column batch's inputs cut into
+        HQ_LAYOUT_TILES (or HQ_LAYOUT_TILES_LEADER) tiles."""
+        if layout == HQ_LAYOUT_TILES:
+            self._check(lib.hq_tile_commit_dev(self.h, ctypes.byref(columns), _p(tiles)))
+        else:
+            self._check(lib.hq_tile_commit_as_dev(self.h, ctypes.byref(columns), _p(tiles),
+                                                  layout))
 
     def readindex_dev(self, G, ack, n_voting, n_uniform, confirmed, fallback=None) -> None:
         self._check(lib.hq_readindex_dev(self.h, G, _p(ack), _p(n_voting), n_uniform,
@@ -652,8 +660,10 @@ def words64(G: int) -> int:
     return (G + 63) // 64
 
 
-def commit_tile_words(n_max: int, form: int) -> int:
-    """hq_commit_tile_words: u64 words of one tile of HQ_TILE_GROUPS groups."""
+def commit_tile_words(n_max: int, form: int, layout: int = HQ_LAYOUT_TILES) -> int:
+    """hq_commit_tile_words(_for): u64 words of one tile of HQ_TILE_GROUPS groups."""
+    if layout == HQ_LAYOUT_TILES_LEADER:
+        n_max -= 1
     if form == HQ_FORM_TERM_MASK:
         return (n_max + 2) * HQ_TILE_GROUPS + 32
     return (n_max + 3) * HQ_TILE_GROUPS
@@ -663,12 +673,16 @@ def commit_tiles(G: int) -> int:
     return (G + HQ_TILE_GROUPS - 1) // HQ_TILE_GROUPS
 
 
-def tile_commit_host(columns: CommitArgs) -> np.ndarray:
-    """hq_tile_commit_host over host column arrays (pointers in ``columns``): the tiles as a
-    uint64 array."""
-    out = np.zeros(commit_tiles(columns.G) * commit_tile_words(columns.n_max, columns.form),
-                   np.uint64)
-    _chk(lib.hq_tile_commit_host(ctypes.byref(columns), _p(out)), "hq_tile_commit_host")
+def tile_commit_host(columns: CommitArgs, layout: int = HQ_LAYOUT_TILES) -> np.ndarray:
+    """hq_tile_commit_host / hq_tile_commit_as_host over host column arrays (pointers in
+    ``columns``): the tiles as a uint64 array."""
+    out = np.zeros(commit_tiles(columns.G) *
+                   commit_tile_words(columns.n_max, columns.form, layout), np.uint64)
+    if layout == HQ_LAYOUT_TILES:
+        _chk(lib.hq_tile_commit_host(ctypes.byref(columns), _p(out)), "hq_tile_commit_host")
+    else:
+        _chk(lib.hq_tile_commit_as_host(ctypes.byref(columns), _p(out), layout),
+             "hq_tile_commit_as_host")
     return out
 
 
@@ -719,7 +733,8 @@ class CommitBuffers:
     term: Optional[DeviceArray] = None
     term_mask: Optional[DeviceArray] = None
     ring32: Optional[DeviceArray] = None
-    tiles: Optional[DeviceArray] = None    # HQ_LAYOUT_TILES copy of the input columns
+    tiles: Optional[DeviceArray] = None    # HQ_LAYOUT_TILES(_LEADER) copy of the input columns
+    tile_layout: int = HQ_LAYOUT_TILES
 
     def args(self) -> CommitArgs:
         a = CommitArgs()
@@ -743,10 +758,10 @@ class CommitBuffers:
         return a
 
     def tile_args(self) -> CommitArgs:
-        """The same batch in HQ_LAYOUT_TILES: the inputs from ``tiles`` (filled by
-        ``Context.tile_commit_dev(b.args(), b.tiles)``), outputs as in ``args``."""
+        """The same batch in its tile layout: the inputs from ``tiles`` (filled by
+        ``Context.tile_commit_dev(b.args(), b.tiles, b.tile_layout)``), outputs as in ``args``."""
         a = self.args()
-        a.layout = HQ_LAYOUT_TILES
+        a.layout = self.tile_layout
         a.match = self.tiles.ptr
         a.match_stride = 0
         a.committed_in = a.last_index = a.term_start = a.term = a.term_mask = None
@@ -761,10 +776,10 @@ class CommitBuffers:
 
 def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16,
                  per_group_n: bool = False, with_both_aux: bool = False,
-                 tiled: bool = False) -> CommitBuffers:
+                 tiled: bool = False, tile_layout: int = HQ_LAYOUT_TILES) -> CommitBuffers:
     """Allocate the SoA columns of one commit batch (match is slot-major [n_max][G]).
     with_both_aux allocates the columns of all four term forms (to compare them); tiled adds
-    the HQ_LAYOUT_TILES buffer of the form."""
+    the tile buffer of the form in ``tile_layout`` (HQ_LAYOUT_TILES or _TILES_LEADER)."""
     need_ts = form == HQ_FORM_TERM_START or with_both_aux
     need_ring = form == HQ_FORM_TERM_RING or with_both_aux
     need_ring32 = form == HQ_FORM_TERM_RING32 or with_both_aux
@@ -783,8 +798,9 @@ def alloc_commit(ctx: Context, G: int, n_max: int, form: int, ring_len: int = 16
         term=ctx.empty(G, np.uint64) if need_ring or need_ring32 else None,
         term_mask=ctx.empty(G, np.uint16) if need_mask else None,
         ring32=ctx.empty(G * ring_len, np.uint32) if need_ring32 else None,
-        tiles=ctx.empty(commit_tiles(G) * commit_tile_words(n_max, form), np.uint64)
+        tiles=ctx.empty(commit_tiles(G) * commit_tile_words(n_max, form, tile_layout), np.uint64)
         if tiled else None,
+        tile_layout=tile_layout,
     )
     return b
 

@@ -15,16 +15,16 @@ pytestmark = pytest.mark.gpu
 SEED = 0x5EED0000
 
 
-def tiled_args(hq, cols, tiles):
+def tiled_args(hq, cols, tiles, layout=None):
     a = hq.CommitArgs.from_buffer_copy(cols)
-    a.layout = hq.HQ_LAYOUT_TILES
+    a.layout = hq.HQ_LAYOUT_TILES if layout is None else layout
     a.match = tiles.ptr
     a.match_stride = 0
     a.committed_in = a.last_index = a.term_start = a.term = a.term_mask = None
     return a
 
 
-def host_tiles(hq, inp, form):
+def host_tiles(hq, inp, form, layout=None):
     a = hq.CommitArgs()
     a.G, a.n_max, a.form, a.ring_len = inp.G, inp.n_max, form, inp.R
     a.match_stride = inp.G
@@ -35,19 +35,20 @@ def host_tiles(hq, inp, form):
     a.term = inp.term.ctypes.data
     if inp.term_mask is not None:
         a.term_mask = inp.term_mask.ctypes.data
-    return hq.tile_commit_host(a)
+    return hq.tile_commit_host(a, hq.HQ_LAYOUT_TILES if layout is None else layout)
 
 
-def run_tiled(ctx, hq, inp, form, per_group_n):
+def run_tiled(ctx, hq, inp, form, per_group_n, layout=None):
     """Columns uploaded, tiled on the device (checked against the host packer), decided from
     the tiles. Returns (committed_out, changed, fallback)."""
+    layout = hq.HQ_LAYOUT_TILES if layout is None else layout
     d = upload_commit(ctx, hq, inp, form, per_group_n)
-    words = hq.commit_tiles(inp.G) * hq.commit_tile_words(inp.n_max, form)
+    words = hq.commit_tiles(inp.G) * hq.commit_tile_words(inp.n_max, form, layout)
     tiles = ctx.empty(words, np.uint64)
-    ctx.tile_commit_dev(d["args"], tiles)
+    ctx.tile_commit_dev(d["args"], tiles, layout)
     ctx.sync()
-    np.testing.assert_array_equal(ctx.download(tiles), host_tiles(hq, inp, form))
-    ctx.commit_dev(tiled_args(hq, d["args"], tiles))
+    np.testing.assert_array_equal(ctx.download(tiles), host_tiles(hq, inp, form, layout))
+    ctx.commit_dev(tiled_args(hq, d["args"], tiles, layout))
     ctx.sync()
     out = ctx.download(d["out"])[:inp.G]
     chg, fb = ctx.download(d["chg"]), ctx.download(d["fb"])
@@ -70,12 +71,28 @@ def test_tiled_commit_every_form_and_n(gpu_ctx, hq, form, n):
         np.testing.assert_array_equal(fb, want_fb)
 
 
-def test_tiled_full_size_c2(gpu_ctx, hq):
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", range(1, 9))
+def test_leader_tiles_every_form_and_n(gpu_ctx, hq, form, n):
+    """HQ_LAYOUT_TILES_LEADER (slot 0 taken from last_index): the same decisions."""
+    for G, pern in ((1, False), (129, True), (20_011, False), (20_011, True)):
+        inp = qref.CommitInputs(qref.spec(SEED + 11 * n + G, G, n, mixed_n=pern and n >= 7,
+                                          parity_extras=True))
+        out, chg, fb = run_tiled(gpu_ctx, hq, inp, form, pern, hq.HQ_LAYOUT_TILES_LEADER)
+        want_out, want_chg, want_fb, rc = inp.run(form, pern, nthreads=8)
+        assert rc == 0
+        np.testing.assert_array_equal(out, want_out)
+        np.testing.assert_array_equal(chg, want_chg)
+        np.testing.assert_array_equal(fb, want_fb)
+
+
+@pytest.mark.parametrize("layout", [1, 2])
+def test_tiled_full_size_c2(gpu_ctx, hq, layout):
     """BASELINE config 2 (1M groups x 3 voters, term-start) in tiles, device-generated."""
     G, n = 1 << 20, 3
-    b = hq.alloc_commit(gpu_ctx, G, n, hq.HQ_FORM_TERM_START, 16, tiled=True)
+    b = hq.alloc_commit(gpu_ctx, G, n, hq.HQ_FORM_TERM_START, 16, tiled=True, tile_layout=layout)
     gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + 1, G, n), b.args())
-    gpu_ctx.tile_commit_dev(b.args(), b.tiles)
+    gpu_ctx.tile_commit_dev(b.args(), b.tiles, layout)
     gpu_ctx.commit_dev(b.tile_args())
     gpu_ctx.sync()
     inp = qref.CommitInputs(qref.spec(SEED + 1, G, n))
@@ -87,16 +104,17 @@ def test_tiled_full_size_c2(gpu_ctx, hq):
     hq.free_commit(gpu_ctx, b)
 
 
+@pytest.mark.parametrize("layout", [1, 2])
 @pytest.mark.parametrize("form", [0, 2, 1, 3])
-def test_tiled_fused_buckets_equal_separate(gpu_ctx, hq, form):
+def test_tiled_fused_buckets_equal_separate(gpu_ctx, hq, form, layout):
     """Voter-count buckets of one step in one tiled launch = each bucket decided alone."""
-    sizes = [(3, 70_001), (5, 40_000), (7, 33_333), (1, 5)]
+    sizes = [(3, 70_001), (5, 40_000), (7, 33_333), (1, 5), (8, 1_000)]
     bufs = []
     for k, (n, G) in enumerate(sizes):
-        b = hq.alloc_commit(gpu_ctx, G, n, form, 16, tiled=True)
+        b = hq.alloc_commit(gpu_ctx, G, n, form, 16, tiled=True, tile_layout=layout)
         gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + 40 + k, G, n, parity_extras=True),
                                  b.args())
-        gpu_ctx.tile_commit_dev(b.args(), b.tiles)
+        gpu_ctx.tile_commit_dev(b.args(), b.tiles, layout)
         bufs.append(b)
     gpu_ctx.commit_fused_dev(hq.commit_batch_array([b.tile_args() for b in bufs]))
     gpu_ctx.sync()
@@ -110,17 +128,18 @@ def test_tiled_fused_buckets_equal_separate(gpu_ctx, hq, form):
         hq.free_commit(gpu_ctx, b)
 
 
-def test_tiled_host_entry_point(gpu_ctx, hq):
+@pytest.mark.parametrize("layout", [1, 2])
+def test_tiled_host_entry_point(gpu_ctx, hq, layout):
     """hq_commit with host tiles: one H2D block, same decisions."""
     G, n, form = 10_007, 5, hq.HQ_FORM_TERM_RING32
     inp = qref.CommitInputs(qref.spec(SEED + 99, G, n, parity_extras=True))
-    tiles = host_tiles(hq, inp, form)
+    tiles = host_tiles(hq, inp, form, layout)
     ring32 = hq.pack_ring32(inp.ring)
     out = np.zeros(G, np.uint64)
     chg = np.zeros(hq.words64(G), np.uint64)
     fb = np.zeros(hq.words64(G), np.uint64)
     a = hq.CommitArgs()
-    a.G, a.n_max, a.form, a.ring_len, a.layout = G, n, form, 16, hq.HQ_LAYOUT_TILES
+    a.G, a.n_max, a.form, a.ring_len, a.layout = G, n, form, 16, layout
     a.match = tiles.ctypes.data
     a.ring32 = ring32.ctypes.data
     a.committed_out = out.ctypes.data

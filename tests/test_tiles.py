@@ -24,12 +24,13 @@ def column_args(hq, inp, form, n):
     return a
 
 
-def expected_tiles(hq, inp, form, n):
+def expected_tiles(hq, inp, form, n, lead=0):
+    """lead = 1: HQ_LAYOUT_TILES_LEADER, the same tiles without match slot 0's row."""
     G = inp.G
     nt = hq.commit_tiles(G)
     rows = []
     pad = nt * T - G
-    for s in range(n):
+    for s in range(lead, n):
         rows.append(inp.match[s * G:(s + 1) * G])
     rows += [inp.committed_in, inp.last_index]
     rows = [np.concatenate([r, np.zeros(pad, np.uint64)]).reshape(nt, T) for r in rows]
@@ -45,7 +46,7 @@ def expected_tiles(hq, inp, form, n):
     perm[0::2] = np.arange(T // 2)
     perm[1::2] = np.arange(T // 2) + T // 2
     out = np.empty_like(tiles)
-    nrow = n + 2
+    nrow = n - lead + 2
     for r in range(nrow):
         out[:, r * T:(r + 1) * T] = tiles[:, r * T:(r + 1) * T][:, perm]
     if form == hq.HQ_FORM_TERM_MASK:
@@ -65,6 +66,37 @@ def test_tile_commit_host(hq, G, n, form):
     tiles = hq.tile_commit_host(a)
     assert tiles.size == hq.commit_tiles(G) * hq.commit_tile_words(n, form)
     np.testing.assert_array_equal(tiles, expected_tiles(hq, inp, form, n))
+
+
+@pytest.mark.parametrize("G", [1, 129, 1000])
+@pytest.mark.parametrize("n", [1, 3, 5, 8])
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
+def test_tile_commit_host_leader(hq, G, n, form):
+    """HQ_LAYOUT_TILES_LEADER: rows of match slots 1..n-1, then committed_in, last_index, term."""
+    inp = qref.CommitInputs(qref.spec(0x5EED0200 + G, G, n, parity_extras=True))
+    assert (inp.match[:G] == inp.last_index).all()   # the generator's leader slot (raft.go:918)
+    a = column_args(hq, inp, form, n)
+    tiles = hq.tile_commit_host(a, hq.HQ_LAYOUT_TILES_LEADER)
+    assert tiles.size == hq.commit_tiles(G) * hq.commit_tile_words(n - 1, form)
+    np.testing.assert_array_equal(tiles, expected_tiles(hq, inp, form, n, lead=1))
+
+
+def test_tile_commit_host_leader_refuses_other_slot0(hq):
+    """A group whose slot 0 is not its lastIndex cannot be carried by the leader layout."""
+    G, n = 300, 3
+    inp = qref.CommitInputs(qref.spec(0x5EED0300, G, n))
+    inp.match[17] -= 1
+    a = column_args(hq, inp, 0, n)
+    out = np.zeros(hq.commit_tiles(G) * hq.commit_tile_words(n - 1, 0), np.uint64)
+    assert hq.lib.hq_tile_commit_as_host(ctypes.byref(a), out.ctypes.data,
+                                         hq.HQ_LAYOUT_TILES_LEADER) == hq.HQ_E_INVAL
+    assert hq.lib.hq_tile_commit_as_host(ctypes.byref(a), out.ctypes.data, 7) == hq.HQ_E_INVAL
+    # per-group n = 0 groups carry no slot 0 and are not checked
+    nv = np.full(G, n, np.uint8)
+    nv[17] = 0
+    a.n_voting = nv.ctypes.data
+    assert hq.lib.hq_tile_commit_as_host(ctypes.byref(a), out.ctypes.data,
+                                         hq.HQ_LAYOUT_TILES_LEADER) == 0
 
 
 def test_tile_commit_host_rejects_bad_input(hq):

@@ -16,16 +16,18 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {"c2": "k_commit_big<3, 0, 2, false, false>", "c2t": "k_commit_big<3, 0, 2, false, true>",
-          "c3": "k_commit_big<5, 1, 2, false, false>", "c3m": "k_commit_big<5, 2, 2, false, false>",
-          "c3mt": "k_commit_big<5, 2, 2, false, true>",
-          "c3r32": "k_commit_big<5, 3, 2, false, false>",
-          "c3r32t": "k_commit_big<5, 3, 2, false, true>",
-          "c5v5t": "k_commit_big<5, 2, 2, false, true>",
-          "c5v5r32t": "k_commit_big<5, 3, 2, false, true>",
+KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2, false, 1>",
+          "c3": "k_commit_big<5, 1, 2, false, 0>", "c3m": "k_commit_big<5, 2, 2, false, 0>",
+          "c3mt": "k_commit_big<5, 2, 2, false, 1>",
+          "c2tl": "k_commit_big<3, 0, 2, false, 2>", "c3mtl": "k_commit_big<5, 2, 2, false, 2>",
+          "c5v5tl": "k_commit_big<5, 2, 2, false, 2>", "c5tl": "k_commit_fused<2, 512, 2>",
+          "c3r32": "k_commit_big<5, 3, 2, false, 0>",
+          "c3r32t": "k_commit_big<5, 3, 2, false, 1>",
+          "c5v5t": "k_commit_big<5, 2, 2, false, 1>",
+          "c5v5r32t": "k_commit_big<5, 3, 2, false, 1>",
           "c4": "k_bits<3, true, 256, false, true>", "c4u": "k_bits<3, false, 256, false, true>",
-          "c4t": "k_bits<3, true, 256, true, false>", "c4ut": "k_bits<3, false, 256, true, false>", "c5": "k_commit_fused<2, 512, false>",
-          "c5t": "k_commit_fused<2, 512, true>", "c5s": "k_commit<7, 2, 2, false, false>",
+          "c4t": "k_bits<3, true, 256, true, false>", "c4ut": "k_bits<3, false, 256, true, false>", "c5": "k_commit_fused<2, 512, 0>",
+          "c5t": "k_commit_fused<2, 512, 1>", "c5s": "k_commit<7, 2, 2, false, 0>",
           "c2l": "k_commit_lag_big<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
           "c5l": "k_commit_lag_fused<2, 512>", "rim": "k_ri_multi2<false, false>",
           "cq": "k_bits<4, false, 256, false, true>", "ing": "k_ingest_match", "ingo": "k_ingest_match", "rim2": "k_ri_multi2"}
