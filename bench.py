@@ -81,6 +81,11 @@ WORKLOADS = {
     "c3l": dict(cfg=2, kind="lag", G=1 << 20, n=5, form=2, mixed=False,
                 desc="1M groups x 5 voters (4 full + 1 witness), commit over int32 lags with the "
                      "lag-indexed current-term mask (30 B per decision)"),
+    "c2ll": dict(cfg=1, kind="lag", G=1 << 20, n=3, form=0, mixed=False, lead=True,
+                 desc="as c2l without the leader's lag row (HQ_LAG_LEADER_IMPLICIT: slot 0 = "
+                      "lastIndex, raft.go:918; 20 B per decision)"),
+    "c5ll": dict(cfg=4, kind="lag", G=8 << 20, n=5, form=2, mixed=True, lead=True,
+                 desc="as c5l without the leader's lag row (HQ_LAG_LEADER_IMPLICIT)"),
     "c5l": dict(cfg=4, kind="lag", G=8 << 20, n=5, form=2, mixed=True,
                 desc="as c5 in the int32 lag layout (lag-indexed mask), the three buckets in one "
                      "fused launch"),
@@ -111,7 +116,8 @@ def algo_bytes_per_group(w):
     """bytes the decision must move per group."""
     if w["kind"] == "lag":
         # lag rows + cin_lag + cout_lag + (ts_lag | lag_mask)
-        return 4 * w["n"] + 8 + {0: 4, 2: 2}[w["form"]]
+        # (HQ_LAG_LEADER_IMPLICIT: no row for the leader's lag, always 0)
+        return 4 * (w["n"] - 1 if w.get("lead") else w["n"]) + 8 + {0: 4, 2: 2}[w["form"]]
     if w["kind"] == "commit":
         n, extra_n = w["n"], (1 if w["mixed"] else 0)
         # match + committed in/out + last + (term_start | term + gathered ring term | u16 mask
@@ -318,7 +324,7 @@ def run_gpu(w, steps, warmup, d: Dist):
                 ctx.commit_fused_dev(per_step[i % len(per_step)])
     elif w["kind"] == "lag":
         # one launch per step: the bucket set's batches fused (a single batch: plain launch)
-        per_step = [hq.lag_batch_array([b.args() for b in bs]) for bs in sets]
+        per_step = [hq.lag_batch_array([b.args(bool(w.get("lead"))) for b in bs]) for bs in sets]
         seq, wseq = list(range(steps)), list(range(max(1, warmup)))
 
         def run(idx):
@@ -887,7 +893,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extra",
                     default="c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3mtl,c3l,c5v5t,c5v5tl,c5v5r32t,"
-                            "c4,c4t,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,"
+                            "c4,c4t,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,"
                             "c5r,c5r32,rim,"
                             "cq,ing,ingo,w2,e2e,step,step5",
                     help="comma list of extra workloads reported under 'extra' ('' for none)")

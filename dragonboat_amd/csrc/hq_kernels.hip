@@ -542,7 +542,9 @@ __device__ __forceinline__ uint64_t spread_v(uint32_t x) {
 
 // VEC = 4 / 2: lane owns groups g0..g0+VEC-1 (16- / 8-byte loads of every column); VEC = 1: one
 // group, 4-byte loads. The body of workgroup `blk` of `nblk` on batch `a`.
-template <int N, int FORM, int VEC, bool PERN, int BLK>
+// LEAD = 1 (HQ_LAG_LEADER_IMPLICIT): lag row s - 1 holds slot s, slot 0's lag is 0 (the
+// leader's own match is lastIndex, raft.go:918, 1031): 4 bytes less per group.
+template <int N, int FORM, int VEC, bool PERN, int BLK, int LEAD = 0>
 __device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t nblk) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = blk * (BLK / 64) + (threadIdx.x >> 6);
@@ -559,11 +561,15 @@ __device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t
                 typedef typename LagVec<VEC>::T VT;
                 int32_t l[VEC][N];
 #pragma unroll
-                for (int s = 0; s < N; ++s) {
+                for (int s = LEAD; s < N; ++s) {
                     const VT v = __builtin_nontemporal_load(
-                        reinterpret_cast<const VT *>(a.lag + s * a.stride + g0));
+                        reinterpret_cast<const VT *>(a.lag + (s - LEAD) * a.stride + g0));
 #pragma unroll
                     for (int j = 0; j < VEC; ++j) l[j][s] = v[j];
+                }
+                if constexpr (LEAD) {
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) l[j][0] = 0;
                 }
                 const VT ci = __builtin_nontemporal_load(reinterpret_cast<const VT *>(a.cin + g0));
                 int32_t av[VEC];
@@ -603,7 +609,8 @@ __device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t
             if (!done && g < a.G) {
                 int32_t l[N];
 #pragma unroll
-                for (int s = 0; s < N; ++s) l[s] = a.lag[s * a.stride + g];
+                for (int s = LEAD; s < N; ++s) l[s] = a.lag[(s - LEAD) * a.stride + g];
+                if constexpr (LEAD) l[0] = 0;
                 const int n = PERN ? (int)a.nv[g] : N;
                 const int32_t aux = FORM == HQ_FORM_TERM_START ? a.ts[g] : (int32_t)a.mask[g];
                 int32_t co;
@@ -642,13 +649,13 @@ __device__ __forceinline__ void lag_blocks(const LagK &a, uint64_t blk, uint64_t
     }
 }
 
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, int LEAD>
 __global__ __launch_bounds__(kCommitBlock) void k_commit_lag(const LagK a) {
-    lag_blocks<N, FORM, VEC, PERN, kCommitBlock>(a, blockIdx.x, gridDim.x);
+    lag_blocks<N, FORM, VEC, PERN, kCommitBlock, LEAD>(a, blockIdx.x, gridDim.x);
 }
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, int LEAD>
 __global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_lag_big(const LagK a) {
-    lag_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG>(a, blockIdx.x, gridDim.x);
+    lag_blocks<N, FORM, VEC, PERN, HQ_COMMIT_BLOCK_BIG, LEAD>(a, blockIdx.x, gridDim.x);
 }
 
 // the lag twin of k_commit_fused: uniform-n lag batches of one step in one launch
@@ -659,7 +666,7 @@ struct FusedLagK {
     uint32_t count;
 };
 
-template <int FORM, int BLK>
+template <int FORM, int BLK, int LEAD>
 __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_lag_fused(const FusedLagK f) {
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
@@ -667,14 +674,14 @@ __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_lag_
     for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
     const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
     switch (f.n[i]) {
-    case 1: lag_blocks<1, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    case 2: lag_blocks<2, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    case 3: lag_blocks<3, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    case 4: lag_blocks<4, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    case 5: lag_blocks<5, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    case 6: lag_blocks<6, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    case 7: lag_blocks<7, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
-    default: lag_blocks<8, FORM, kLagVec, false, BLK>(f.b[i], b, nb); break;
+    case 1: lag_blocks<1, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    case 2: lag_blocks<2, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    case 3: lag_blocks<3, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    case 4: lag_blocks<4, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    case 5: lag_blocks<5, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    case 6: lag_blocks<6, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    case 7: lag_blocks<7, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
+    default: lag_blocks<8, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
     }
 }
 
@@ -1286,33 +1293,39 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
 
 namespace {
 
-template <int N, int FORM, int VEC, bool PERN>
+template <int N, int FORM, int VEC, bool PERN, int LEAD>
 int launch_lag_t(hq_ctx *ctx, const LagK &k) {
     constexpr int B = lag_blk<N, PERN>();
     const unsigned grid = grid_for((k.G + VEC - 1) / VEC, B, kMaxBlocks * 256 / B);
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     if constexpr (B == kCommitBlock)
-        hipLaunchKernelGGL((k_commit_lag<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0, ctx->stream,
-                           k);
+        hipLaunchKernelGGL((k_commit_lag<N, FORM, VEC, PERN, LEAD>), dim3(grid), dim3(B), 0,
+                           ctx->stream, k);
     else
-        hipLaunchKernelGGL((k_commit_lag_big<N, FORM, VEC, PERN>), dim3(grid), dim3(B), 0,
+        hipLaunchKernelGGL((k_commit_lag_big<N, FORM, VEC, PERN, LEAD>), dim3(grid), dim3(B), 0,
                            ctx->stream, k);
     return hq::post_launch(ctx, "k_commit_lag");
 }
 
-template <int N>
-int launch_lag_n(hq_ctx *ctx, const LagK &k, int form, bool vec, bool pern) {
+template <int N, int LEAD>
+int launch_lag_nl(hq_ctx *ctx, const LagK &k, int form, bool vec, bool pern) {
 #define HQ_LAG_DISPATCH(F)                                                                   \
-    if (vec) return pern ? launch_lag_t<N, F, kLagVec, true>(ctx, k)                          \
-                         : launch_lag_t<N, F, kLagVec, false>(ctx, k);                        \
-    return pern ? launch_lag_t<N, F, 1, true>(ctx, k) : launch_lag_t<N, F, 1, false>(ctx, k);
+    if (vec) return pern ? launch_lag_t<N, F, kLagVec, true, LEAD>(ctx, k)                    \
+                         : launch_lag_t<N, F, kLagVec, false, LEAD>(ctx, k);                  \
+    return pern ? launch_lag_t<N, F, 1, true, LEAD>(ctx, k)                                   \
+                : launch_lag_t<N, F, 1, false, LEAD>(ctx, k);
     if (form == HQ_FORM_TERM_START) {
         HQ_LAG_DISPATCH(HQ_FORM_TERM_START)
     } else {
         HQ_LAG_DISPATCH(HQ_FORM_TERM_MASK)
     }
 #undef HQ_LAG_DISPATCH
+}
+template <int N>
+int launch_lag_n(hq_ctx *ctx, const LagK &k, int form, bool vec, bool pern, bool lead) {
+    return lead ? launch_lag_nl<N, 1>(ctx, k, form, vec, pern)
+                : launch_lag_nl<N, 0>(ctx, k, form, vec, pern);
 }
 
 int validate_lag(hq_ctx *ctx, const hq_commit_lag_args *a) {
@@ -1324,6 +1337,8 @@ int validate_lag(hq_ctx *ctx, const hq_commit_lag_args *a) {
     if (!a->lag || !a->cin_lag || !a->cout_lag)
         return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: NULL lag/cin_lag/cout_lag");
     if (a->lag_stride < a->G) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: lag_stride < G");
+    if (a->flags & ~(uint32_t)HQ_LAG_LEADER_IMPLICIT)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: unknown flags");
     if (a->form == HQ_FORM_TERM_START) {
         if (!a->ts_lag) return hq::fail(ctx, HQ_E_INVAL, "hq_commit_lag: ts_lag is NULL");
     } else if (a->form == HQ_FORM_TERM_MASK) {
@@ -1371,15 +1386,16 @@ extern "C" int hq_commit_lag_dev(hq_ctx *ctx, const hq_commit_lag_args *a) {
     const LagK k = lag_k(a);
     const bool vec4 = lag_vec(a);
     const bool pern = a->n_voting != nullptr;
+    const bool lead = (a->flags & HQ_LAG_LEADER_IMPLICIT) != 0;
     switch (a->n_max) {
-    case 1: return launch_lag_n<1>(ctx, k, a->form, vec4, pern);
-    case 2: return launch_lag_n<2>(ctx, k, a->form, vec4, pern);
-    case 3: return launch_lag_n<3>(ctx, k, a->form, vec4, pern);
-    case 4: return launch_lag_n<4>(ctx, k, a->form, vec4, pern);
-    case 5: return launch_lag_n<5>(ctx, k, a->form, vec4, pern);
-    case 6: return launch_lag_n<6>(ctx, k, a->form, vec4, pern);
-    case 7: return launch_lag_n<7>(ctx, k, a->form, vec4, pern);
-    default: return launch_lag_n<8>(ctx, k, a->form, vec4, pern);
+    case 1: return launch_lag_n<1>(ctx, k, a->form, vec4, pern, lead);
+    case 2: return launch_lag_n<2>(ctx, k, a->form, vec4, pern, lead);
+    case 3: return launch_lag_n<3>(ctx, k, a->form, vec4, pern, lead);
+    case 4: return launch_lag_n<4>(ctx, k, a->form, vec4, pern, lead);
+    case 5: return launch_lag_n<5>(ctx, k, a->form, vec4, pern, lead);
+    case 6: return launch_lag_n<6>(ctx, k, a->form, vec4, pern, lead);
+    case 7: return launch_lag_n<7>(ctx, k, a->form, vec4, pern, lead);
+    default: return launch_lag_n<8>(ctx, k, a->form, vec4, pern, lead);
     }
 }
 
@@ -1394,7 +1410,7 @@ extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *ar
     bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
     for (uint32_t i = 0; fusable && i < count; ++i)
         fusable = args[i].G > 0 && !args[i].n_voting && lag_vec(args + i) &&
-                  args[i].form == args[0].form;
+                  args[i].form == args[0].form && args[i].flags == args[0].flags;
     if (!fusable) {
         for (uint32_t i = 0; i < count; ++i) {
             int rc = hq_commit_lag_dev(ctx, args + i);
@@ -1428,17 +1444,26 @@ extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *ar
     for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
-#define HQ_LAG_FUSED(F)                                                                        \
+#define HQ_LAG_FUSED(F, L)                                                                     \
     if (big)                                                                                   \
-        hipLaunchKernelGGL((k_commit_lag_fused<F, HQ_COMMIT_BLOCK_BIG>), dim3(blocks),         \
+        hipLaunchKernelGGL((k_commit_lag_fused<F, HQ_COMMIT_BLOCK_BIG, L>), dim3(blocks),      \
                            dim3(HQ_COMMIT_BLOCK_BIG), 0, ctx->stream, f);                      \
     else                                                                                       \
-        hipLaunchKernelGGL((k_commit_lag_fused<F, kCommitBlock>), dim3(blocks),                \
+        hipLaunchKernelGGL((k_commit_lag_fused<F, kCommitBlock, L>), dim3(blocks),             \
                            dim3(kCommitBlock), 0, ctx->stream, f);
+    const bool lead = (args[0].flags & HQ_LAG_LEADER_IMPLICIT) != 0;
     if (args[0].form == HQ_FORM_TERM_START) {
-        HQ_LAG_FUSED(HQ_FORM_TERM_START)
+        if (lead) {
+            HQ_LAG_FUSED(HQ_FORM_TERM_START, 1)
+        } else {
+            HQ_LAG_FUSED(HQ_FORM_TERM_START, 0)
+        }
     } else {
-        HQ_LAG_FUSED(HQ_FORM_TERM_MASK)
+        if (lead) {
+            HQ_LAG_FUSED(HQ_FORM_TERM_MASK, 1)
+        } else {
+            HQ_LAG_FUSED(HQ_FORM_TERM_MASK, 0)
+        }
     }
 #undef HQ_LAG_FUSED
     return hq::post_launch(ctx, "k_commit_lag_fused");
@@ -1714,6 +1739,8 @@ extern "C" int hq_synth_commit_lag_dev(hq_ctx *ctx, const hq_synth_spec *s,
         s->cid_stride < 1 || (s->mixed_n && s->n_max < 7) || (a->lag && a->lag_stride < s->G) ||
         (a->lag_mask && s->ring_len > 16))
         return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit_lag: bad spec");
+    if (a->flags)   // the generator writes every slot's row; view rows 1.. with lag + lag_stride
+        return hq::fail(ctx, HQ_E_INVAL, "hq_synth_commit_lag: generate with flags = 0");
     if (s->G == 0) return HQ_OK;
     CommitCols o{};
     o.G = s->G;

@@ -173,9 +173,18 @@ extern "C" int hq_pack_lags(uint64_t G, uint32_t n_max, const uint64_t *match,
     const uint32_t R = out->ring_len;
     if (!ts && (R < 1 || R > 16 || (R & (R - 1)))) return HQ_E_INVAL;
     int32_t *lag = const_cast<int32_t *>(out->lag);
-    for (uint32_t s = 0; s < n_max; ++s)
+    if (out->flags & ~HQ_LAG_LEADER_IMPLICIT) return HQ_E_INVAL;
+    // HQ_LAG_LEADER_IMPLICIT: slot 0 is not stored; it must be the leader's lastIndex
+    // (raft.go:918, 1031) for every group that has a slot 0
+    const uint32_t lead = (out->flags & HQ_LAG_LEADER_IMPLICIT) ? 1 : 0;
+    if (lead)
         for (uint64_t g = 0; g < G; ++g)
-            lag[s * out->lag_stride + g] = lag_of(last_index[g], match[s * match_stride + g]);
+            if ((!out->n_voting || out->n_voting[g] >= 1) && match[g] != last_index[g])
+                return HQ_E_INVAL;
+    for (uint32_t s = lead; s < n_max; ++s)
+        for (uint64_t g = 0; g < G; ++g)
+            lag[(s - lead) * out->lag_stride + g] =
+                lag_of(last_index[g], match[s * match_stride + g]);
     for (uint64_t g = 0; g < G; ++g) {
         const uint64_t last = last_index[g];
         const_cast<int32_t *>(out->cin_lag)[g] = lag_of(last, committed[g]);

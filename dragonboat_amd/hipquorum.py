@@ -32,6 +32,7 @@ HQ_FORM_TERM_RING32 = 3
 HQ_LAYOUT_COLUMNS = 0
 HQ_LAYOUT_TILES = 1
 HQ_LAYOUT_TILES_LEADER = 2   # tiles without the leader row: slot 0 = last_index
+HQ_LAG_LEADER_IMPLICIT = 1   # hq_commit_lag_args.flags: lag rows start at slot 1
 HQ_TILE_GROUPS = 128
 HQ_ABI_VERSION = 6
 
@@ -77,7 +78,7 @@ class LagArgs(ctypes.Structure):
         ("n_max", ctypes.c_uint32),
         ("form", ctypes.c_uint32),
         ("ring_len", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
         ("lag_stride", ctypes.c_uint64),
         ("lag", _vp),
         ("n_voting", _vp),
@@ -584,13 +585,15 @@ def lag_args(G, n_max, form, ring_len, lag, cin_lag, cout_lag, ts_lag=None, lag_
 
 
 def pack_lags(G, n_max, form, ring_len, match, committed, last_index, term_start=None,
-              term_mask=None, match_stride=None):
-    """hq_pack_lags into fresh host arrays: (lag [n_max*G] int32, cin_lag, ts_lag or lag_mask)."""
-    lag = np.zeros(n_max * G, np.int32)
+              term_mask=None, match_stride=None, flags=0):
+    """hq_pack_lags into fresh host arrays: (lag [rows*G] int32, cin_lag, ts_lag or lag_mask);
+    rows = n_max, or n_max - 1 with flags = HQ_LAG_LEADER_IMPLICIT."""
+    lag = np.zeros((n_max - (1 if flags & HQ_LAG_LEADER_IMPLICIT else 0)) * G, np.int32)
     cin = np.zeros(G, np.int32)
     ts = np.zeros(G, np.int32) if form == HQ_FORM_TERM_START else None
     lm = np.zeros(G, np.uint16) if form == HQ_FORM_TERM_MASK else None
-    out = lag_args(G, n_max, form, ring_len, lag, cin, cin, ts, lm)
+    out = lag_args(G, n_max, form, ring_len, lag if lag.size else cin, cin, cin, ts, lm)
+    out.flags = flags
     _chk(lib.hq_pack_lags(G, n_max, _p(np.ascontiguousarray(match, np.uint64)),
                           G if match_stride is None else match_stride,
                           _p(np.ascontiguousarray(committed, np.uint64)),
@@ -822,12 +825,18 @@ class LagBuffers:
     last_index: Optional[DeviceArray] = None
     stride: int = 0           # lag row stride (G rounded up to 4: 16-byte aligned rows)
 
-    def args(self) -> LagArgs:
+    def args(self, leader_implicit: bool = False) -> LagArgs:
+        """leader_implicit: the same batch with HQ_LAG_LEADER_IMPLICIT, the lag rows viewed
+        from slot 1 (the generator writes every row; slot 0's lag is 0 by construction)."""
         ts = self.aux if self.form == HQ_FORM_TERM_START else None
         lm = self.aux if self.form == HQ_FORM_TERM_MASK else None
-        return lag_args(self.G, self.n_max, self.form, self.ring_len, self.lag, self.cin_lag,
-                        self.cout_lag, ts, lm, None, self.changed, self.fallback,
-                        lag_stride=self.stride or self.G)
+        stride = self.stride or self.G
+        a = lag_args(self.G, self.n_max, self.form, self.ring_len, self.lag, self.cin_lag,
+                     self.cout_lag, ts, lm, None, self.changed, self.fallback, lag_stride=stride)
+        if leader_implicit:
+            a.flags = HQ_LAG_LEADER_IMPLICIT
+            a.lag = self.lag.ptr + stride * 4
+        return a
 
     def arrays(self):
         return [x for x in (self.lag, self.cin_lag, self.cout_lag, self.aux, self.changed,

@@ -258,13 +258,18 @@ int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count)
  * cin_lag > ring_len (the mask form's contract). A decided group's cout_lag is exact.
  * Bytes per group: 4n + 12 (term-start; 24 B at n = 3 against 56 B for hq_commit_dev) or
  * 4n + 10 (mask). Packed from the u64 columns by hq_pack_lags (host) or generated on the device.
+ *
+ * flags & HQ_LAG_LEADER_IMPLICIT: the lag rows start at slot 1 (row s - 1 = slot s) and slot 0's
+ * lag is 0 — slot 0 is the leader, whose own match is its lastIndex at every step (reset,
+ * raft.go:1031; appendEntries, raft.go:918). 4 bytes less per group (20 B at n = 3).
  */
+#define HQ_LAG_LEADER_IMPLICIT 1u
 typedef struct hq_commit_lag_args {
     uint64_t G;
     uint32_t n_max;           /* 1..HQ_MAX_VOTERS */
     uint32_t form;            /* HQ_FORM_TERM_START or HQ_FORM_TERM_MASK */
     uint32_t ring_len;        /* TERM_MASK: power of two <= 16 */
-    uint32_t reserved;
+    uint32_t flags;           /* 0 or HQ_LAG_LEADER_IMPLICIT */
     uint64_t lag_stride;      /* elements between slot rows of lag, >= G */
     const int32_t *lag;       /* [n_max][lag_stride] */
     const uint8_t *n_voting;  /* [G] or NULL (all groups have n_max) */
@@ -284,7 +289,9 @@ int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *args, uint32_
 /* Host packer: the lag columns of *out (lag rows at out->lag_stride, cin_lag and ts_lag or
  * lag_mask per out->form) from u64 columns laid out as in hq_commit_args (match rows at
  * match_stride; term_start for TERM_START; term_mask (bit i % ring_len) for TERM_MASK).
- * Slots >= n_max of the lag rows are not written. */
+ * Slots >= n_max of the lag rows are not written. With out->flags = HQ_LAG_LEADER_IMPLICIT slot 0
+ * is not written (row s - 1 = slot s) and a group with n >= 1 (out->n_voting, if given) whose
+ * match[0] != last_index is refused (HQ_E_INVAL). */
 int hq_pack_lags(uint64_t G, uint32_t n_max, const uint64_t *match, uint64_t match_stride,
                  const uint64_t *committed, const uint64_t *last_index,
                  const uint64_t *term_start, const uint16_t *term_mask,

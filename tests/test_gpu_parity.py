@@ -527,16 +527,18 @@ I32_MIN, I32_MAX = -(1 << 31), (1 << 31) - 1
 
 
 def run_commit_lag(ctx, hq, inp, form, per_group_n, stride_pad=0, offset_elems=0,
-                   lags=None):
+                   lags=None, lead=False):
     """The oracle-generated u64 batch packed into lags on the host (hq_pack_lags), decided by
     hq_commit_lag_dev; returns (committed' unpacked, changed, fallback)."""
     G, n = inp.G, inp.n_max
+    flags = hq.HQ_LAG_LEADER_IMPLICIT if lead else 0
     lag, cin, aux = lags if lags is not None else hq.pack_lags(
         G, n, form, inp.R, inp.match, inp.committed_in, inp.last_index, inp.term_start,
-        inp.term_mask)
+        inp.term_mask, flags=flags)
+    nr = n - 1 if lead else n   # lag rows (lead: slots 1..n-1)
     stride = G + stride_pad
-    rows = np.zeros((n, stride), np.int32)
-    rows[:, :G] = lag.reshape(n, G)
+    rows = np.zeros((max(nr, 1), stride), np.int32)
+    rows[:nr, :G] = lag.reshape(nr, G)
     bufs = []
 
     def up(a):
@@ -555,6 +557,7 @@ def run_commit_lag(ctx, hq, inp, form, per_group_n, stride_pad=0, offset_elems=0
                     out.ptr + offset_elems * 4,
                     up(aux) if form == 0 else None, up(aux) if form == 2 else None,
                     up(inp.n_voting) if per_group_n else None, chg, fb, lag_stride=stride)
+    a.flags = flags
     ctx.commit_lag_dev(a)
     ctx.sync()
     cout = ctx.download(out)[offset_elems:offset_elems + G]
@@ -591,6 +594,23 @@ def test_commit_lag_uniform_n(gpu_ctx, hq, form, n_max):
 def test_commit_lag_per_group_n(gpu_ctx, hq, form, n_max):
     inp = qref.CommitInputs(qref.spec(SEED + 22, 99_999, n_max, mixed_n=True, parity_extras=True))
     check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=True)
+
+
+@pytest.mark.parametrize("form", [0, 2])
+@pytest.mark.parametrize("n_max", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_commit_lag_leader_implicit(gpu_ctx, hq, form, n_max):
+    """HQ_LAG_LEADER_IMPLICIT: rows from slot 1, slot 0's lag 0 (the leader's own match is its
+    lastIndex, raft.go:918): the same decisions, vector and scalar paths, per-group n."""
+    inp = qref.CommitInputs(qref.spec(SEED + 26 + n_max, 65_537, n_max, parity_extras=True))
+    check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False, lead=True)
+    check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False, lead=True, offset_elems=1)
+    for G in (1, 5, 65, 257):
+        inp = qref.CommitInputs(qref.spec(SEED + G + n_max, G, n_max, parity_extras=True))
+        check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=False, lead=True)
+    if n_max >= 7:
+        inp = qref.CommitInputs(qref.spec(SEED + 27, 30_001, n_max, mixed_n=True,
+                                          parity_extras=True))
+        check_commit_lag(gpu_ctx, hq, inp, form, per_group_n=True, lead=True)
 
 
 @pytest.mark.parametrize("form", [0, 2])
@@ -690,10 +710,11 @@ def test_commit_lag_full_size(gpu_ctx, hq, n_max, form):
     hq.free_commit(gpu_ctx, b)
 
 
+@pytest.mark.parametrize("lead", [False, True])
 @pytest.mark.parametrize("form", [0, 2])
 @pytest.mark.parametrize("sizes", [[(3, 100_001), (5, 99_999), (7, 100_003)],
                                    [(3, 1), (5, 64), (7, 65), (1, 129), (8, 3000)]])
-def test_commit_lag_fused_buckets(gpu_ctx, hq, form, sizes):
+def test_commit_lag_fused_buckets(gpu_ctx, hq, form, sizes, lead):
     """One launch over several voter-count buckets in the lag layout (device generator) equals
     the oracle's u64 decision on each bucket."""
     bufs, want = [], []
@@ -708,7 +729,7 @@ def test_commit_lag_fused_buckets(gpu_ctx, hq, form, sizes):
     gpu_ctx.sync()
     gpu_ctx.timing_reset()
     gpu_ctx.timing(True)
-    gpu_ctx.commit_lag_fused_dev(hq.lag_batch_array([b.args() for b, _ in bufs]))
+    gpu_ctx.commit_lag_fused_dev(hq.lag_batch_array([b.args(lead) for b, _ in bufs]))
     gpu_ctx.sync()
     gpu_ctx.timing(False)
     assert gpu_ctx.timing_read()[1] == 1

@@ -45,6 +45,29 @@ def test_pack_lags_generator_data(hq, form):
     np.testing.assert_array_equal(out, inp.committed_in)
 
 
+@pytest.mark.parametrize("form", [0, 2])
+def test_pack_lags_leader_implicit(hq, form):
+    """HQ_LAG_LEADER_IMPLICIT: rows of slots 1..n-1 only; a slot 0 other than lastIndex refused."""
+    G, n = 3001, 5
+    inp = qref.CommitInputs(qref.spec(SEED + 1, G, n, parity_extras=True))
+    full = hq.pack_lags(G, n, form, 16, inp.match, inp.committed_in, inp.last_index,
+                        inp.term_start, inp.term_mask)
+    lead = hq.pack_lags(G, n, form, 16, inp.match, inp.committed_in, inp.last_index,
+                        inp.term_start, inp.term_mask, flags=hq.HQ_LAG_LEADER_IMPLICIT)
+    assert not full[0].reshape(n, G)[0].any()        # the leader's lag is 0
+    np.testing.assert_array_equal(lead[0], full[0].reshape(n, G)[1:].reshape(-1))
+    np.testing.assert_array_equal(lead[1], full[1])
+    np.testing.assert_array_equal(lead[2], full[2])
+    bad = inp.match.copy()
+    bad[7] += 1
+    with pytest.raises(hq.HQError):
+        hq.pack_lags(G, n, form, 16, bad, inp.committed_in, inp.last_index, inp.term_start,
+                     inp.term_mask, flags=hq.HQ_LAG_LEADER_IMPLICIT)
+    with pytest.raises(hq.HQError):
+        hq.pack_lags(G, n, form, 16, inp.match, inp.committed_in, inp.last_index,
+                     inp.term_start, inp.term_mask, flags=2)
+
+
 def test_pack_lags_saturates(hq):
     last = np.array([1 << 40, 1 << 40, 5, 1 << 40, 100], np.uint64)
     match = np.array([0, (1 << 40) + (1 << 33), 9, (1 << 40) - I32_MAX, 100], np.uint64)

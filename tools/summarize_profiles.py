@@ -28,8 +28,9 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2,
           "c4": "k_bits<3, true, 256, false, true>", "c4u": "k_bits<3, false, 256, false, true>",
           "c4t": "k_bits<3, true, 256, true, false>", "c4ut": "k_bits<3, false, 256, true, false>", "c5": "k_commit_fused<2, 512, 0>",
           "c5t": "k_commit_fused<2, 512, 1>", "c5s": "k_commit<7, 2, 2, false, 0>",
-          "c2l": "k_commit_lag_big<3, 0, 4, false>", "c3l": "k_commit_lag<5, 2, 4, false>",
-          "c5l": "k_commit_lag_fused<2, 512>", "rim": "k_ri_multi2<false, false>",
+          "c2l": "k_commit_lag_big<3, 0, 4, false, 0>", "c3l": "k_commit_lag<5, 2, 4, false, 0>",
+          "c2ll": "k_commit_lag_big<3, 0, 4, false, 1>", "c5ll": "k_commit_lag_fused<2, 512, 1>",
+          "c5l": "k_commit_lag_fused<2, 512, 0>", "rim": "k_ri_multi2<false, false>",
           "cq": "k_bits<4, false, 256, false, true>", "ing": "k_ingest_match", "ingo": "k_ingest_match", "rim2": "k_ri_multi2"}
 
 
