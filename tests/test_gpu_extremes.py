@@ -1,7 +1,8 @@
 """Commit decisions at the edges of the u64 range, bit-exact with the oracle: indexes and terms
 next to 0 and 2^64 - 1, matches above lastIndex (the term() = 0 branch), committed above
 lastIndex, terms at 0 and around 2^32 (the u32 ring's saturation), random masks and rings, voter
-counts 0..n_max + 1 — in every term form, columns and tiles, uniform and per-group n."""
+counts 0..n_max + 1 — in every term form, columns, tiles and leader-row tiles, uniform and
+per-group n."""
 import numpy as np
 import pytest
 
@@ -93,6 +94,22 @@ def test_commit_extremes_tiles(gpu_ctx, hq, form, n, pern):
     G = 4099
     inp = adversarial(G, n, 31 * n + form + 100 * pern)
     out, chg, fb = run_tiled(gpu_ctx, hq, inp, form, pern)
+    want_out, want_chg, want_fb, rc = inp.run(form, pern)
+    np.testing.assert_array_equal(out, want_out)
+    np.testing.assert_array_equal(chg, want_chg)
+    np.testing.assert_array_equal(fb, want_fb)
+
+
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", [1, 3, 5, 8])
+@pytest.mark.parametrize("pern", [False, True])
+def test_commit_extremes_leader_tiles(gpu_ctx, hq, form, n, pern):
+    """HQ_LAYOUT_TILES_LEADER at the edges: slot 0 = lastIndex (the layout's precondition, the
+    leader's own match, raft.go:918), everything else adversarial."""
+    G = 4099
+    inp = adversarial(G, n, 43 * n + form + 100 * pern)
+    inp.match[:G] = inp.last_index
+    out, chg, fb = run_tiled(gpu_ctx, hq, inp, form, pern, hq.HQ_LAYOUT_TILES_LEADER)
     want_out, want_chg, want_fb, rc = inp.run(form, pern)
     np.testing.assert_array_equal(out, want_out)
     np.testing.assert_array_equal(chg, want_chg)
