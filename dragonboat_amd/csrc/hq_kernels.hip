@@ -307,6 +307,9 @@ __device__ __forceinline__ void column_blocks(const CommitK &a, uint64_t blk, ui
     }
 }
 
+#ifndef HQ_TILE_SCHED_BARRIER
+#define HQ_TILE_SCHED_BARRIER 1
+#endif
 // HQ_LAYOUT_TILES: one wave per 128-group tile. Row position 2i holds group i of the tile and
 // position 2i + 1 group i + 64, so lane i's 16-byte load of a row brings groups i and i + 64:
 // every field of the wave is ONE contiguous block of (n + 3) KiB, and the two ballots are the
@@ -353,6 +356,13 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
             } else {
                 ax = ld_stream2(t + (NR + 2) * T);
             }
+#if HQ_TILE_SCHED_BARRIER
+            // every row load of the tile is issued before the first compare: otherwise the
+            // scheduler starts the network after two rows and issues the rows past the 4-KiB
+            // immediate-offset range behind an s_waitcnt, one memory latency later (n <= 5: the
+            // wider bodies would spill inside the 64-VGPR fused kernel)
+            if constexpr (N <= 5) __builtin_amdgcn_sched_barrier(0);
+#endif
             const int na = PERN ? (int)a.nv[ga] : N, nb = PERN ? (int)a.nv[gb] : N;
             uint64_t coa, cob;
             decide<N, FORM, PERN>(a, ga, m0, na, ci.x, la.x, ax.x, coa, ca, fa);
