@@ -417,7 +417,7 @@ constexpr int kMaxFused = 8;
 struct FusedK {
     CommitK b[kMaxFused];
     uint32_t first[kMaxFused + 1];
-    uint8_t n[kMaxFused];
+    uint32_t n[kMaxFused];   // dwords: a scalar load (a byte array is read with a vector load + wait)
     uint32_t count;
 };
 
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_lag_big(const
 struct FusedLagK {
     LagK b[kMaxFused];
     uint32_t first[kMaxFused + 1];
-    uint8_t n[kMaxFused];
+    uint32_t n[kMaxFused];   // dwords: a scalar load (a byte array is read with a vector load + wait)
     uint32_t count;
 };
 
@@ -1261,7 +1261,7 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     for (uint32_t k = 0; k < count; ++k) {
         const uint32_t i = k;
         f.b[i] = commit_k(args + order[k]);
-        f.n[i] = (uint8_t)args[order[k]].n_max;
+        f.n[i] = args[order[k]].n_max;
         f.first[i] = (uint32_t)blocks;
         // the same lanes per batch as its own launch would get (grid-stride beyond that)
         blocks += grid_for((args[order[k]].G + 1) / 2, B, (uint64_t)kMaxBlocks * 256 / B);
@@ -1447,7 +1447,7 @@ extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *ar
     for (uint32_t i = 0; i < count; ++i) {
         const hq_commit_lag_args *b = args + order[i];
         f.b[i] = lag_k(b);
-        f.n[i] = (uint8_t)b->n_max;
+        f.n[i] = b->n_max;
         f.first[i] = (uint32_t)blocks;
         blocks += grid_for((b->G + kLagVec - 1) / kLagVec, B, (uint64_t)kMaxBlocks * 256 / B);
     }
