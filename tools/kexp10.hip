@@ -64,8 +64,11 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const char *names[] = {"c2tl library (48 B)", "floor 5 rows + store (48 B)",
-                           "c2t library (56 B)", "floor 6 rows + store (56 B)"};
-    const int NV = 4;
+                           "c2t library (56 B)", "floor 6 rows + store (56 B)",
+                           "c2tl 512-thread twin (48 B)", "c2tl 1024, 2 tiles/wave (48 B)"};
+    const int NV = 6;
+    std::vector<CommitK> k2(nsets);
+    for (int s = 0; s < nsets; ++s) k2[s] = commit_k(&t2[s]);
     std::vector<double> us[NV];
     for (int rep = 0; rep < reps; ++rep) {
         for (int v = 0; v < NV; ++v) {
@@ -76,9 +79,15 @@ int main() {
                 else if (v == 1)
                     hipLaunchKernelGGL(floor_tile<5>, dim3(G / 2048), dim3(1024), 0, ctx->stream,
                                        t2[s].match, t2[s].committed_out);
-                else
+                else if (v == 3)
                     hipLaunchKernelGGL(floor_tile<6>, dim3(G / 2048), dim3(1024), 0, ctx->stream,
                                        t1[s].match, t1[s].committed_out);
+                else if (v == 4)
+                    hipLaunchKernelGGL((k_commit<3, 0, 2, false, 2>), dim3(G / 1024), dim3(512), 0,
+                                       ctx->stream, k2[s]);
+                else
+                    hipLaunchKernelGGL((k_commit_big<3, 0, 2, false, 2>), dim3(G / 4096), dim3(1024),
+                                       0, ctx->stream, k2[s]);
             };
             for (int i = 0; i < 40; ++i) launch(i);
             CK(hipEventRecord(e0, ctx->stream));
@@ -92,7 +101,7 @@ int main() {
     }
     for (int v = 0; v < NV; ++v) {
         std::sort(us[v].begin(), us[v].end());
-        const double bytes = (v < 2 ? 48.0 : 56.0) * G;
+        const double bytes = (v == 2 || v == 3 ? 56.0 : 48.0) * G;
         printf("%-30s median %6.2f us  min %6.2f  (%5.0f GB/s at the median)\n", names[v],
                us[v][reps / 2], us[v][0], bytes / (us[v][reps / 2] * 1e3));
     }
