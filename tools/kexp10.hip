@@ -29,6 +29,19 @@ __global__ __launch_bounds__(1024, 8) void floor_tile(const u64 *tiles, u64 *out
     *reinterpret_cast<u64x2 *>(out + wave * 128 + lane * 2) = x;
 }
 
+// the same loads, the output as the library writes it: two 8-B stores, groups i and i + 64
+__global__ __launch_bounds__(1024, 8) void floor_tile_split(const u64 *tiles, u64 *out) {
+    const u64 wave = (u64)blockIdx.x * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const u64 lane = threadIdx.x & 63;
+    const u64 *t = tiles + wave * (5 * 128) + lane * 2;
+    u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(t));
+#pragma unroll
+    for (int r = 1; r < 5; ++r)
+        x ^= __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(t + r * 128));
+    out[wave * 128 + lane] = x.x;
+    out[wave * 128 + lane + 64] = x.y;
+}
+
 int main() {
     const uint64_t G = 1ull << 20, nw = G / 64;
     const int nsets = 24, steps = 400, reps = 12;
@@ -65,10 +78,17 @@ int main() {
     CK(hipEventCreate(&e1));
     const char *names[] = {"c2tl library (48 B)", "floor 5 rows + store (48 B)",
                            "c2t library (56 B)", "floor 6 rows + store (56 B)",
-                           "c2tl 512-thread twin (48 B)", "c2tl 1024, 2 tiles/wave (48 B)"};
-    const int NV = 6;
+                           "c2tl 512-thread twin (48 B)", "c2tl 1024, 2 tiles/wave (48 B)",
+                           "floor 5 rows, two 8-B stores", "c2tl, no changed/fallback",
+                           "c2tl, changed only"};
+    const int NV = 9;
     std::vector<CommitK> k2(nsets);
     for (int s = 0; s < nsets; ++s) k2[s] = commit_k(&t2[s]);
+    std::vector<CommitK> k3 = k2, k4 = k2;
+    for (int s = 0; s < nsets; ++s) {
+        k3[s].changed = k3[s].fallback = nullptr;
+        k4[s].fallback = nullptr;
+    }
     std::vector<double> us[NV];
     for (int rep = 0; rep < reps; ++rep) {
         for (int v = 0; v < NV; ++v) {
@@ -85,9 +105,18 @@ int main() {
                 else if (v == 4)
                     hipLaunchKernelGGL((k_commit<3, 0, 2, false, 2>), dim3(G / 1024), dim3(512), 0,
                                        ctx->stream, k2[s]);
-                else
+                else if (v == 5)
                     hipLaunchKernelGGL((k_commit_big<3, 0, 2, false, 2>), dim3(G / 4096), dim3(1024),
                                        0, ctx->stream, k2[s]);
+                else if (v == 7)
+                    hipLaunchKernelGGL((k_commit_big<3, 0, 2, false, 2>), dim3(G / 2048), dim3(1024),
+                                       0, ctx->stream, k3[s]);
+                else if (v == 8)
+                    hipLaunchKernelGGL((k_commit_big<3, 0, 2, false, 2>), dim3(G / 2048), dim3(1024),
+                                       0, ctx->stream, k4[s]);
+                else
+                    hipLaunchKernelGGL(floor_tile_split, dim3(G / 2048), dim3(1024), 0, ctx->stream,
+                                       t2[s].match, t2[s].committed_out);
             };
             for (int i = 0; i < 40; ++i) launch(i);
             CK(hipEventRecord(e0, ctx->stream));
