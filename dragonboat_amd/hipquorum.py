@@ -592,6 +592,8 @@ def pack_lags(G, n_max, form, ring_len, match, committed, last_index, term_start
     cin = np.zeros(G, np.int32)
     ts = np.zeros(G, np.int32) if form == HQ_FORM_TERM_START else None
     lm = np.zeros(G, np.uint16) if form == HQ_FORM_TERM_MASK else None
+    # (n_max = 1 with the leader flag has no lag row; the packer still wants a non-NULL lag
+    # pointer and writes nothing through it)
     out = lag_args(G, n_max, form, ring_len, lag if lag.size else cin, cin, cin, ts, lm)
     out.flags = flags
     _chk(lib.hq_pack_lags(G, n_max, _p(np.ascontiguousarray(match, np.uint64)),
