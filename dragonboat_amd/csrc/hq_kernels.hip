@@ -307,6 +307,8 @@ __device__ __forceinline__ void column_blocks(const CommitK &a, uint64_t blk, ui
     }
 }
 
+// 1: the tile bodies issue every row load before the first compare (tile_blocks); 0 is the
+// A/B baseline of profiles/r01i/kexp10_sched_barrier_ab.log
 #ifndef HQ_TILE_SCHED_BARRIER
 #define HQ_TILE_SCHED_BARRIER 1
 #endif
