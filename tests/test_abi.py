@@ -48,11 +48,16 @@ int main(void) {
   F(hq_commit_args, term_mask) F(hq_commit_args, ring32) F(hq_commit_args, layout)
   for (unsigned n = 1; n <= 8; ++n)
     for (unsigned f = 0; f <= 3; ++f)
-      printf("tile_words_%u_%u %llu\n", n, f, (unsigned long long)hq_commit_tile_words(n, f));
+      printf("tile_words_%u_%u %llu\nlead_words_%u_%u %llu\n", n, f,
+             (unsigned long long)hq_commit_tile_words(n, f), n, f,
+             (unsigned long long)hq_commit_tile_words_for(n, f, HQ_LAYOUT_TILES_LEADER));
   printf("tiles_129 %llu\n", (unsigned long long)hq_commit_tiles(129));
   printf("hq_commit_lag_args %zu\n", sizeof(hq_commit_lag_args));
   F(hq_commit_lag_args, G) F(hq_commit_lag_args, n_max) F(hq_commit_lag_args, form)
-  F(hq_commit_lag_args, ring_len) F(hq_commit_lag_args, lag_stride) F(hq_commit_lag_args, lag)
+  F(hq_commit_lag_args, ring_len) F(hq_commit_lag_args, flags)
+  F(hq_commit_lag_args, lag_stride) F(hq_commit_lag_args, lag)
+  printf("lag_leader_flag %u\nlayout_leader %u\n", (unsigned)HQ_LAG_LEADER_IMPLICIT,
+         (unsigned)HQ_LAYOUT_TILES_LEADER);
   F(hq_commit_lag_args, n_voting) F(hq_commit_lag_args, cin_lag) F(hq_commit_lag_args, cout_lag)
   F(hq_commit_lag_args, ts_lag) F(hq_commit_lag_args, lag_mask) F(hq_commit_lag_args, changed)
   F(hq_commit_lag_args, fallback)
@@ -94,6 +99,10 @@ def test_struct_layout_matches_c(hq, tmp_path):
     for n in range(1, 9):
         for f in range(4):
             assert int(c[f"tile_words_{n}_{f}"]) == hq.commit_tile_words(n, f)
+            assert int(c[f"lead_words_{n}_{f}"]) == hq.commit_tile_words(
+                n, f, hq.HQ_LAYOUT_TILES_LEADER)
+    assert int(c["lag_leader_flag"]) == hq.HQ_LAG_LEADER_IMPLICIT
+    assert int(c["layout_leader"]) == hq.HQ_LAYOUT_TILES_LEADER
     assert int(c["tiles_129"]) == hq.commit_tiles(129) == 2
     for key, val in c.items():
         if "." in key:

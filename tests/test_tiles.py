@@ -125,3 +125,16 @@ def test_tile_bits_host_layout(hq, G, pern):
         flat = tiles[:, r, :].reshape(-1)
         np.testing.assert_array_equal(flat[:G], col)
         assert not flat[G:].any()
+
+
+def test_bench_byte_accounting():
+    """bench.py's algorithmic bytes per decision for the headline layouts:
+    56 B (tiles), 48 B (leader-row tiles), 24 B (lags), 20 B (lags without the leader row)."""
+    import bench
+
+    w = bench.WORKLOADS
+    assert bench.algo_bytes_per_group(w["c2t"]) == 56
+    assert bench.algo_bytes_per_group(w["c2tl"]) == 48
+    assert bench.algo_bytes_per_group(w["c2l"]) == 24
+    assert bench.algo_bytes_per_group(w["c2ll"]) == 20
+    assert bench.algo_bytes_per_group(w["c5v5tl"]) == 58
