@@ -45,8 +45,12 @@ WORKLOADS = {
                       "128-group tiles without the leader's match row (HQ_LAYOUT_TILES_LEADER: "
                       "slot 0 = lastIndex, raft.go:918; 48 B per decision)"),
     "c3mtl": dict(cfg=2, kind="commit", G=1 << 20, n=5, form=2, mixed=False, tiled=True,
-                  lead=True, desc="1M groups x 5 voters (4 full + 1 witness), current-term mask, "
-                                  "128-group tiles without the leader's match row"),
+                  lead=True,
+                  desc="BASELINE config 3: 1M groups x 5 voting members (4 full incl. the leader "
+                       "+ 1 witness; the 2 observers are never packed, raft.go:894-901), commit "
+                       "+ current-term check (16-bit term mask over the last 16 indexes, exact "
+                       "twin of the term-ring gather), 128-group tiles without the leader's match "
+                       "row (slot 0 = lastIndex, raft.go:918; 58 B per decision)"),
     "c5v5tl": dict(cfg=2, kind="commit", G=8 << 20, n=5, form=2, mixed=False, tiled=True,
                    lead=True, desc="as c5v5t without the leader's match row "
                                    "(HQ_LAYOUT_TILES_LEADER)"),
@@ -110,6 +114,17 @@ WORKLOADS = {
     "c5s": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True, separate=True,
                 desc="as c5 with one launch per voter-count bucket (3 launches per step)"),
 }
+
+
+# BASELINE.json configs[2] (1M x 5 voters + witness/observers, commit + term check): the largest
+# single-GPU commit config and the north star's 5-voter bar
+HEADLINE = "c3mtl"
+DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
+                  "c4,c4t,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
+                  "cq,ing,ingo,w2,e2e,step,step5")
+# the same generated groups decided with the other exact term-check forms (same cfg, n, G)
+SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
+                   "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
 
 
 def algo_bytes_per_group(w):
@@ -314,40 +329,45 @@ def run_gpu(w, steps, warmup, d: Dist):
     ctx = hq.Context(d.device)
     sets, per_set = build_sets(ctx, hq, shard, w, d)
     G = w["G"]
+    nsets = len(sets)
+    # Warm-up decides sets 0 .. W-1; the timed steps continue the rotation at set W, so no timed
+    # launch re-reads a batch touched less than (nsets - 1) batches (>= 1.1 GiB) earlier: the
+    # 256 MiB Infinity Cache cannot hold it (MI355X_MICROARCH.md "Infinity Cache").
+    first = max(1, warmup) % nsets
+    launches_per_step = 1
     if w["kind"] == "commit" and w["mixed"] and not w.get("separate"):
         # a step = the rank's voter-count buckets decided by one fused launch
         per_step = [hq.commit_batch_array([batch_args(b) for b in bs]) for bs in sets]
-        seq, wseq = list(range(steps)), list(range(max(1, warmup)))
 
         def run(idx):
             for i in idx:
-                ctx.commit_fused_dev(per_step[i % len(per_step)])
+                ctx.commit_fused_dev(per_step[i % nsets])
     elif w["kind"] == "lag":
         # one launch per step: the bucket set's batches fused (a single batch: plain launch)
         per_step = [hq.lag_batch_array([b.args(bool(w.get("lead"))) for b in bs]) for bs in sets]
-        seq, wseq = list(range(steps)), list(range(max(1, warmup)))
 
         def run(idx):
             for i in idx:
-                arr = per_step[i % len(per_step)]
+                arr = per_step[i % nsets]
                 if len(arr) == 1:
                     ctx.commit_lag_dev(arr[0])
                 else:
                     ctx.commit_lag_fused_dev(arr)
     elif w["kind"] == "commit":
-        def flat(k):
-            return hq.commit_batch_array([batch_args(b) for i in range(k)
-                                          for b in sets[i % len(sets)]])
-        seq, wseq = flat(steps), flat(max(1, warmup))
+        # every launch of the sequence enqueued by one C call (hq_commit_many_dev)
+        launches_per_step = len(sets[0])
+        cache = {}
 
-        def run(batch):
-            ctx.commit_many_dev(batch)
-    else:
-        seq, wseq = list(range(steps)), list(range(max(1, warmup)))
+        def prepare(idx):   # the argument array of a sequence, built outside the timed region
+            cache[(idx.start, idx.stop)] = hq.commit_batch_array(
+                [batch_args(b) for i in idx for b in sets[i % nsets]])
 
         def run(idx):
+            ctx.commit_many_dev(cache[(idx.start, idx.stop)])
+    else:
+        def run(idx):
             for i in idx:
-                arrs, conf, outc, tiles = sets[i % len(sets)]
+                arrs, conf, outc, tiles = sets[i % nsets]
                 if tiles is not None:
                     uni = w.get("uniform", False)
                     ctx.readindex_vote_tiles_dev(G, tiles, not uni, w["n"] if uni else 0, conf,
@@ -359,38 +379,59 @@ def run_gpu(w, steps, warmup, d: Dist):
                 else:
                     ctx.readindex_vote_dev(G, da, dg, dr, dn, 0, conf, outc)
 
+    wseq, seq = range(0, max(1, warmup)), range(first, first + steps)
+    if w["kind"] == "commit" and not (w["mixed"] and not w.get("separate")):
+        prepare(wseq)
+        prepare(seq)
+        prepare(range(0, 1))
     if warmup > 0:
         run(wseq)
     ctx.sync()
     d.sync_device()
     d.barrier()
     ctx.timing_reset()
-    ctx.timing(True)
+    # The HIP-event region opens behind the first timed launch (in stream order: when it ends,
+    # with the second one already queued) and closes right behind the last one, so it holds
+    # back-to-back kernels only: no host launch latency at its start, no host sync at its end.
+    ctx.timing_begin_after(1 if steps * launches_per_step > 1 else 0)
     t0 = time.perf_counter()
     run(seq)
+    ctx.timing(False)
     ctx.sync()
     d.sync_device()
     d.barrier()
     t1 = time.perf_counter()
-    ctx.timing(False)
     kernel_ms, launches = ctx.timing_read()
     local = t1 - t0
     elapsed = d.max(local)
     avg_kernel_s = kernel_ms / 1e3 / max(1, launches)
+    bytes_per_launch = per_set / launches_per_step
+    achieved_local = bytes_per_launch / avg_kernel_s / 1e9 if launches else 0.0
     # per-GPU numbers (SURVEY.md §8e reporting), gathered off the timed region
     try:
         per_gpu = d.gather([groups_per_step(w) * steps * decisions_per_group(w) / local,
-                            avg_kernel_s * 1e6])
+                            avg_kernel_s * 1e6, achieved_local])
     except Exception as e:  # a diagnostic must never cost the benchmark line
         log(f"per-GPU gather failed: {e!r}")
         per_gpu = [[groups_per_step(w) * steps * decisions_per_group(w) / local,
-                    avg_kernel_s * 1e6]]
+                    avg_kernel_s * 1e6, achieved_local]]
+    # node-level roofline: every GPU's achieved bytes/s over N x the peak
+    achieved_node = d.sum(achieved_local)
+    # The decisions of set 0, taken once more after the timed region, for the full-size parity
+    # check of the cpu_baseline leg (every bucket of the step; outputs only, no timing).
     set0 = None
-    if w["kind"] == "commit" and not w["mixed"]:
-        # the decisions of batch 0 (its output column is rewritten identically every rotation),
-        # checked against the oracle by the cpu_baseline leg
-        b = sets[0][0]
-        set0 = (ctx.download(b.committed_out), ctx.download(b.changed))
+    if w["kind"] in ("commit", "lag"):
+        if w["kind"] == "commit" and w["mixed"] and not w.get("separate"):
+            ctx.commit_fused_dev(per_step[0])
+        else:
+            run(range(0, 1))
+        ctx.sync()
+        set0 = []
+        for (n, rng), b in zip(commit_buckets(shard, w, d), sets[0]):
+            outs = (b.cout_lag if w["kind"] == "lag" else b.committed_out, b.changed,
+                    b.fallback)
+            set0.append(dict(n=n, cid_base=rng.cid_base, cid_stride=rng.cid_stride,
+                             count=rng.count, out=[ctx.download(a) for a in outs]))
     gather = None
     if d.world > 1 and w["kind"] == "commit" and not w["mixed"]:
         # optional result gather: every GPU's changed bits of batch 0 to every
@@ -407,9 +448,9 @@ def run_gpu(w, steps, warmup, d: Dist):
     total_groups = d.sum(float(groups_per_step(w) * steps))
     res = dict(
         elapsed=elapsed, launches=launches, avg_kernel_s=avg_kernel_s,
-        decisions=total_groups * decisions_per_group(w), nsets=len(sets),
-        bytes_per_launch=per_set * steps / max(1, launches), steps=steps,
-        achieved_gbs=per_set * steps / (kernel_ms / 1e3) / 1e9,
+        decisions=total_groups * decisions_per_group(w), nsets=nsets, first_timed_set=first,
+        bytes_per_launch=bytes_per_launch, launches_per_step=launches_per_step, steps=steps,
+        achieved_gbs=achieved_local, achieved_node_gbs=achieved_node,
         per_gpu=per_gpu, set0=set0, gather=gather,
     )
     ctx.close()
@@ -419,21 +460,22 @@ def run_gpu(w, steps, warmup, d: Dist):
 def _timed(ctx, d, run, steps, warmup):
     """Warm up, then time `steps` calls of run(i) with a barrier + sync on both sides; returns
     (max-over-ranks seconds, average launch seconds from the HIP-event region)."""
-    for i in range(max(1, warmup)):
+    w0 = max(1, warmup)
+    for i in range(w0):
         run(i)
     ctx.sync()
     d.sync_device()
     d.barrier()
     ctx.timing_reset()
-    ctx.timing(True)
+    ctx.timing_begin_after(1 if steps > 1 else 0)   # as in run_gpu: back-to-back kernels only
     t0 = time.perf_counter()
-    for i in range(steps):
+    for i in range(w0, w0 + steps):    # the rotation continues past the warm-up's batches
         run(i)
+    ctx.timing(False)
     ctx.sync()
     d.sync_device()
     d.barrier()
     t1 = time.perf_counter()
-    ctx.timing(False)
     ms, launches = ctx.timing_read()
     return d.max(t1 - t0), ms / 1e3 / max(1, launches), launches
 
@@ -484,11 +526,15 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
             ctx.check_quorum_dev(G, act, None, n, 0, hqb)
         desc = f"cq: CheckQuorum (leaderHasQuorum + setNotActive), {G} groups x {n} voters"
         units, unit = G, "decisions/s"
-    else:   # ing
+    else:   # ing / ingo: the device table in the headline layout (leader-row tiles)
         G, n, U = 4 << 20, 3, 4 << 20
+        form = hq.HQ_FORM_TERM_MASK
         per = U * 16 + U * 16          # the update + the 8-byte read-modify-write of its match
         nsets = max(4, int(np.ceil(ROTATE_BYTES / (U * 16))))
-        table = ctx.upload(np.full(n * G, 1 << 30, np.uint64))
+        table = ctx.empty(hq.commit_tiles(G) * hq.commit_tile_words(n, form,
+                                                                    hq.HQ_LAYOUT_TILES_LEADER),
+                          np.uint64)
+        ctx.memset(table, 0)
         ups = []
         for k in range(nsets):
             g = r.integers(0, G, U, dtype=np.uint64)
@@ -500,13 +546,15 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                 # the order a step worker emits them: node by node (execengine.go:923-1000)
                 u = u[np.argsort(u[:, 0], kind="stable")]
             ups.append(ctx.upload(u.reshape(-1)))
+        flags = hq.HQ_INGEST_GROUPED if name == "ingo" else 0
 
         def run(i):
-            ctx.ingest_match_dev(ups[i % nsets], U, table, G, G, n)
-        desc = (f"{name}: ReplicateResp match-delta ingest (remote.tryUpdate as 64-bit atomic "
-                f"max), {U} deltas into a {G} x {n} device table, "
-                + ("in group order (as a step worker emits them)" if name == "ingo"
-                   else "in random order"))
+            ctx.table_ingest_match_dev(ups[i % nsets], U, table, G, n, form, flags)
+        desc = (f"{name}: ReplicateResp match-delta ingest (remote.tryUpdate) into a {G} x {n} "
+                f"device table in the headline layout (leader-row tiles), {U} deltas "
+                + ("in group order (as a step worker emits them): runs reduced in registers, "
+                   "plain read-modify-write, atomics only at wave edges (HQ_INGEST_GROUPED)"
+                   if name == "ingo" else "in random order: one 64-bit atomic max each"))
         units, unit = U, "updates/s"
     elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
     ctx.close()
@@ -554,7 +602,7 @@ def run_concurrent(w, steps, warmup, d: Dist, W=2):
     gbs = d.sum(float(per_set * steps)) / elapsed / 1e9
     return {
         "workload": f"w{W}: the headline workload ({w['G']} groups x {w['n']} voters per step, "
-                    f"term-start form) stepped by {W} concurrent step workers, one HIP stream "
+                    f"{w['desc'].split(',')[0]}) stepped by {W} concurrent step workers, one HIP stream "
                     f"each, step i on worker i % {W}",
         "value": d.sum(float(groups_per_step(w) * steps)) / elapsed, "unit": "decisions/s",
         "ms_per_step": elapsed / steps * 1e3,
@@ -563,13 +611,14 @@ def run_concurrent(w, steps, warmup, d: Dist, W=2):
     }
 
 
-def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
+def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=5):
     """Host-fed end to end, PCIe included — never the headline `value`.
     Per step: pinned H2D of G/4 leader appends + G follower match deltas, append + ingest kernels
-    into the device-resident table, commit in place (term-mask form), D2H of the changed bitmap
-    and the committed column (dragonboat_amd/pipeline.py). Reported: 8-byte records (append
-    counts, acks as lags below lastIndex) pipelined over 2 contexts; beside it the 16-byte
-    records pipelined and on one stream."""
+    into the device-resident table held in the headline layout (leader-row tiles, term mask), the
+    headline kernel deciding it in place, then D2H of the changed and fallback bitmaps and the
+    committed column (dragonboat_amd/pipeline.py). Reported: 8-byte records in group order
+    (grouped ingest, no atomics) pipelined over 2 contexts; beside it the 16-byte records, the
+    atomic ingest of unsorted records, and one stream."""
     from dragonboat_amd import hipquorum as hq
     from dragonboat_amd import shard
     from dragonboat_amd.pipeline import HostFedPipeline
@@ -578,16 +627,23 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
     spec = hq.synth_spec(SEED_BASE + 9, G, n, cid_base=rng.cid_base, cid_stride=rng.cid_stride)
     nb = 4   # distinct host batches cycled through
     out = {}
-    for depth, compact in ((1, False), (2, False), (2, True)):
+    variants = ((2, True, True), (2, False, True), (2, True, False), (2, False, False),
+                (1, False, False))
+    for depth, compact, grouped in variants:
         r = np.random.default_rng(d.rank)
-        p = HostFedPipeline(d.device, G, n, G // 4, G, depth=depth, compact=compact)
+        p = HostFedPipeline(d.device, G, n, G // 4, G, depth=depth, compact=compact,
+                            grouped=grouped)
         p.synth(spec)
-        last = p.ctxs[0].download(p.table.last_index)
+        last = hq.tile_view(p.ctxs[0].download(p.tiles), G, n, p.form,
+                            p.layout).row("last_index")
         apps, upds = [], []
         for k in range(nb):
-            g = r.choice(G, G // 4, replace=False).astype(np.uint64)
+            g = np.sort(r.choice(G, G // 4, replace=False)).astype(np.uint64)
             gu = r.integers(0, G, G, dtype=np.uint64)
             su = r.integers(1, n, G, dtype=np.uint64)
+            if grouped:   # node by node, as a step worker emits them
+                o = np.lexsort((su, gu))
+                gu, su = gu[o], su[o]
             if compact:
                 app = p.ctxs[0].pinned(len(g), np.uint64)
                 app[:] = hq.pack_append_counts(g, np.full(len(g), k + 1, np.uint64))
@@ -610,25 +666,30 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=3):
             p.step(i, apps[i % nb], G // 4, upds[i % nb], G)
         p.sync()
         d.barrier()
-        out[(depth, compact)] = d.max(time.perf_counter() - t0)
+        out[(depth, compact, grouped)] = d.max(time.perf_counter() - t0)
         p.close()
 
-    def pcie(w):   # H2D records + D2H changed bitmap and committed column, bytes per step
-        return (G // 4) * w + G * w + hq.words64(G) * 8 + G * 8
+    def pcie(w):   # H2D records + D2H changed / fallback bitmaps and committed column per step
+        return (G // 4) * w + G * w + 2 * hq.words64(G) * 8 + G * 8
 
-    def rec(key, w):
+    def rec(key):
+        w = 8 if key[1] else 16
         return {"value": d.sum(float(G * steps)) / out[key], "ms_per_step": out[key] / steps * 1e3,
                 "pcie_bytes_per_step": pcie(w), "pcie_gbs": pcie(w) * steps / out[key] / 1e9}
 
     res = {
-        "workload": f"e2e: host-fed {G} groups x {n} voters per GPU per step: pinned H2D of "
-                    f"{G // 4} appends + {G} match deltas (8-byte records), ingest + commit "
-                    f"kernels, D2H results; steps pipelined over 2 contexts",
+        "workload": f"e2e: host-fed {G} groups x {n} voters per GPU per step into the device "
+                    f"table in the headline layout (leader-row tiles, term mask): pinned H2D of "
+                    f"{G // 4} appends + {G} match deltas (8-byte records, group order), append "
+                    f"+ grouped ingest kernels, the headline kernel deciding in place, D2H "
+                    f"results; steps pipelined over 2 contexts",
         "unit": "decisions/s",
     }
-    res.update(rec((2, True), 8))
-    res["records_16B_pipelined"] = rec((2, False), 16)
-    res["records_16B_one_stream"] = rec((1, False), 16)
+    res.update(rec((2, True, True)))
+    res["records_16B_grouped_pipelined"] = rec((2, False, True))
+    res["records_8B_atomic_pipelined"] = rec((2, True, False))
+    res["records_16B_atomic_pipelined"] = rec((2, False, False))
+    res["records_16B_atomic_one_stream"] = rec((1, False, False))
     return res
 
 
@@ -818,10 +879,41 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
 
 
 # ----------------------------------------------------------------------------- CPU leg --------
+def full_size_parity(w, set0, nthreads):
+    """The GPU's decisions of batch set 0 (every voter-count bucket of the step, at the
+    workload's full size) against the oracle (oracle/qref.c, test infrastructure) on the same
+    generated inputs: committed', changed and fallback bit for bit. Lag workloads are unpacked
+    with the oracle-side lastIndex (committed' = lastIndex - cout_lag for decided groups,
+    hq_unpack_lags) and compared with the oracle's u64 decision."""
+    from oracle import qref
+
+    t0 = time.perf_counter()
+    res = {"groups": 0, "buckets": [], "equal": True}
+    for b in set0:
+        s = qref.spec(SEED_BASE + w["cfg"], b["count"], b["n"], cid_base=b["cid_base"],
+                      cid_stride=b["cid_stride"])
+        inp = qref.CommitInputs(s)
+        want_out, want_chg, want_fb, rc = inp.run(w["form"], False, nthreads=nthreads)
+        out, chg, fb = b["out"]
+        if w["kind"] == "lag":
+            fbit = np.unpackbits(fb.view(np.uint8), bitorder="little")[:b["count"]].astype(bool)
+            out = np.where(fbit, inp.committed_in,
+                           inp.last_index - out.astype(np.int64).astype(np.uint64))
+        eq = dict(committed=bool(np.array_equal(out, want_out)),
+                  changed=bool(np.array_equal(chg, want_chg)),
+                  fallback=bool(np.array_equal(fb, want_fb)), oracle_rc=int(rc))
+        ok = eq["committed"] and eq["changed"] and eq["fallback"] and rc == 0
+        res["buckets"].append(dict(voters=b["n"], groups=b["count"], **eq))
+        res["groups"] += b["count"]
+        res["equal"] &= ok
+    res["check_s"] = time.perf_counter() - t0
+    return res
+
+
 def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
     """The oracle (C restatement of the reference path) on a bounded sample of the workload.
-    gpu_set0: the GPU's (committed', changed) of batch 0 of the timed run, which is exactly this
-    sample's input; the oracle's answer for it is compared bit for bit (full-size parity)."""
+    gpu_set0: the GPU's decisions of batch set 0 (run_gpu), compared bit for bit with the
+    oracle's on the same inputs at full size (full_size_parity)."""
     from oracle import qref
 
     host_threads = min(16, os.cpu_count() or 1)
@@ -849,12 +941,7 @@ def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
                 break
         out[nt] = (passes * G * decisions_per_group(w) / dt, passes, dt)
     rate, passes, dt = out[host_threads]
-    parity = None
-    if gpu_set0 is not None and w["kind"] == "commit":
-        want_out, want_chg, _, rc = inp.run(w["form"], False, nthreads=host_threads)
-        parity = {"groups": G, "oracle_rc": rc,
-                  "committed_equal": bool(np.array_equal(gpu_set0[0], want_out)),
-                  "changed_equal": bool(np.array_equal(gpu_set0[1], want_chg))}
+    parity = full_size_parity(w, gpu_set0, host_threads) if gpu_set0 else None
     # BASELINE config C1: the reference's own CPU case, one group x 3 voters, tryCommit per step
     T = 4 << 20
     match, last = qref.c1_stream(SEED_BASE, T, 1000, 1005)
@@ -874,12 +961,38 @@ def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
 
 
 def pmc_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload (the
+    (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB gfx950 reading, MI355X_MICROARCH.md "HBM"), with the
+    profile it comes from; None if no PMC pass of this workload is committed."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(p))[workload]["hbm_bytes_per_launch"]
+        e = json.load(open(p))[workload]
+        return e["hbm_bytes_per_launch"], e.get("source")
     except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def extra_record(name, we, re_, parity=None):
+    rec = {
+        "workload": f"{name}: {we['desc']}",
+        "value": re_["decisions"] / re_["elapsed"], "unit": "decisions/s",
+        "kernel_avg_us": re_["avg_kernel_s"] * 1e6,
+        "launches_per_step": re_["launches_per_step"],
+        "roofline_achieved_gbs": re_["achieved_node_gbs"],
+        "roofline_frac": re_["achieved_node_gbs"] / (HBM_PEAK_GBS * re_["world"]),
+        "algorithmic_bytes_per_launch": re_["bytes_per_launch"],
+    }
+    if parity is not None:
+        rec["parity_full_size"] = parity
+    return rec
+
+
+def same_decisions(a, b):
+    """Two runs' set-0 decisions (committed', changed, fallback of every bucket) are equal."""
+    if not a or not b or len(a) != len(b):
         return None
+    return all(all(np.array_equal(x, y) for x, y in zip(p["out"], q["out"]))
+               for p, q in zip(a, b))
 
 
 def main():
@@ -887,15 +1000,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", default="c2tl", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker leg (extra 'step')")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra",
-                    default="c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3mtl,c3l,c5v5t,c5v5tl,c5v5r32t,"
-                            "c4,c4t,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,"
-                            "c5r,c5r32,rim,"
-                            "cq,ing,ingo,w2,e2e,step,step5",
+    ap.add_argument("--no-extra-parity", action="store_true",
+                    help="skip the full-size oracle check of the commit / lag extras")
+    ap.add_argument("--extra", default=DEFAULT_EXTRAS,
                     help="comma list of extra workloads reported under 'extra' ('' for none)")
     args = ap.parse_args()
 
@@ -906,7 +1017,10 @@ def main():
             sys.exit(2)
     w = WORKLOADS[args.workload]
     r = run_gpu(w, args.steps, args.warmup, d)
-    extras = []
+    r["world"] = d.world
+    host_threads = min(16, os.cpu_count() or 1)
+    oracle_here = d.rank == 0 and d.world == 1 and not args.no_cpu
+    extras, extra_runs = [], {}
     e2e = None
     steps_legs = []
     conc, kern = [], []
@@ -930,15 +1044,34 @@ def main():
                 conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))
             else:
                 re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
-                extras.append((name, we, re_))
+                re_["world"] = d.world
+                par = None
+                if oracle_here and re_.get("set0") and not args.no_extra_parity:
+                    par = full_size_parity(we, re_["set0"], host_threads)
+                extras.append(extra_record(name, we, re_, par))
+                extra_runs[name] = re_
         except Exception as e:   # an extra leg never costs the headline line
             log(f"extra leg {name} failed: {e!r}")
             failed.append({"workload": name, "error": repr(e)})
     cpu = None
-    if d.rank == 0 and d.world == 1 and not args.no_cpu:
+    if oracle_here:
         cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
+    # the term check of the same groups in its other exact forms (the ring gathers the north
+    # star names, the mask the headline streams): rate and whether every decision is identical
+    forms_same_data = []
+    for name in SAME_DATA_FORMS.get(args.workload, ()):
+        if name in extra_runs:
+            re_ = extra_runs[name]
+            forms_same_data.append({
+                "workload": name, "form": WORKLOADS[name]["desc"],
+                "value": re_["decisions"] / re_["elapsed"],
+                "roofline_frac": re_["achieved_node_gbs"] / (HBM_PEAK_GBS * d.world),
+                "decisions_equal_to_headline": same_decisions(r.get("set0"), re_.get("set0")),
+            })
     if d.rank == 0:
-        achieved = r["achieved_gbs"]
+        traffic, traffic_src = pmc_traffic(args.workload)
+        peak = HBM_PEAK_GBS * d.world
+        achieved = r["achieved_node_gbs"]
         line = {
             "metric": "quorum-commit decisions/sec (whole node) + % HBM roofline at 1/2/4/8 GPUs",
             "value": r["decisions"] / r["elapsed"],
@@ -952,7 +1085,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic: device-generated splitmix64 batches (DESIGN.md), "
-                    f"{r['nsets']} distinct batches per GPU rotated (>= 1.1 GiB)",
+                    f"{r['nsets']} distinct batches per GPU rotated (>= 1.1 GiB); the timed "
+                    f"steps start at batch {r['first_timed_set']}, after the warm-up's",
             "config": {
                 "workload": f"{args.workload}: {w['desc']}",
                 "groups_per_gpu": w["G"], "voters": w["n"],
@@ -963,31 +1097,29 @@ def main():
                 else "columns",
                 "global_groups_per_step": w["G"] * d.world,
                 "parallelism": f"shard{d.world} (clusterID % {d.world})",
+                "world_size": d.world,
+                "backend": d.backend or "none (one process)",
             },
             "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
+                "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                "frac": achieved / peak, "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_avg_us": r["avg_kernel_s"] * 1e6,
-                "kernel_time": "HIP events bracketing the timed region on the launch stream / "
-                               "launches (kernel + dependent-launch boundary)",
+                "kernel_time": "HIP events on the launch stream: a region opened behind the first "
+                               "timed launch and closed behind the last one, / the launches in "
+                               "it (back-to-back kernels: duration + dependent-launch boundary)",
                 "algorithmic_bytes_per_launch": r["bytes_per_launch"],
-                "measured_copy_ceiling_gbs": HBM_MEASURED_COPY_GBS,
+                "achieved_scope": f"node: sum over {d.world} GPU(s) of bytes per launch / "
+                                  "kernel time; peak = 8 TB/s x GPUs",
+                "measured_copy_ceiling_gbs": HBM_MEASURED_COPY_GBS * d.world,
             },
-            "per_gpu": [{"rank": i, "decisions_per_s": v, "kernel_avg_us": k}
-                        for i, (v, k) in enumerate(r["per_gpu"])],
+            "per_gpu": [{"rank": i, "decisions_per_s": v, "kernel_avg_us": k,
+                         "achieved_gbs": a, "frac": a / HBM_PEAK_GBS}
+                        for i, (v, k, a) in enumerate(r["per_gpu"])],
             "result_gather": r["gather"],
             "cpu_baseline": cpu,
-            "extra": [
-                {
-                    "workload": f"{n}: {we['desc']}",
-                    "value": re_["decisions"] / re_["elapsed"], "unit": "decisions/s",
-                    "kernel_avg_us": re_["avg_kernel_s"] * 1e6,
-                    "launches_per_step": re_["launches"] / max(1, re_["steps"]),
-                    "roofline_achieved_gbs": re_["achieved_gbs"],
-                    "roofline_frac": re_["achieved_gbs"] / HBM_PEAK_GBS,
-                }
-                for n, we, re_ in extras
-            ] + kern + conc + ([e2e] if e2e else []) + steps_legs + failed,
+            "term_check_forms_same_data": forms_same_data,
+            "extra": extras + kern + conc + ([e2e] if e2e else []) + steps_legs + failed,
         }
         print(json.dumps(line), flush=True)
     d.close()

@@ -20,6 +20,8 @@ struct hq_ctx {
     bool region_done = false; // a closed region awaits hq_timing_read
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     uint64_t region_launches = 0;
+    // hq_timing_begin_after: launches still to go before the begin event is recorded
+    uint64_t begin_after = 0;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
     // launch geometry of the bitmap kernels (256; HQ_BITS_BLOCK=512|1024 at hq_open)

@@ -201,7 +201,7 @@ __device__ __forceinline__ void decide(const CommitK &a, uint64_t g, uint64_t (&
 // groups are one tile, so its loads walk one contiguous 128·(n+3)·8-byte block instead of n + 3
 // column streams. TILED = 2 (HQ_LAYOUT_TILES_LEADER): the same tiles without the leader's match
 // row; slot 0 is last_index (the leader's own match, raft.go:918, 1031).
-template <int N, int FORM, bool PERN, int BLK, int LEAD>
+template <int N, int FORM, bool PERN, int BLK, int LEAD, bool INPLACE = false>
 __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk);
 
 template <int N, int FORM, int VEC, bool PERN, int BLK>
@@ -317,16 +317,18 @@ __device__ __forceinline__ void column_blocks(const CommitK &a, uint64_t blk, ui
 // every field of the wave is ONE contiguous block of (n + 3) KiB, and the two ballots are the
 // tile's two bitmap words as they are (no bit interleave). The full-tile test is scalar (the
 // wave index is read into an SGPR), so full tiles carry no per-lane guard.
+// TILED = 3: HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE, the device-resident table decided in
+// place (committed' written into the tile's committed row)
 template <int N, int FORM, int VEC, bool PERN, int BLK, int TILED = 0>
 __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     static_assert(!TILED || VEC == 2, "tiles are read two groups per lane");
-    if constexpr (TILED) tile_blocks<N, FORM, PERN, BLK, TILED == 2 ? 1 : 0>(a, blk, nblk);
+    if constexpr (TILED) tile_blocks<N, FORM, PERN, BLK, TILED >= 2 ? 1 : 0, TILED == 3>(a, blk, nblk);
     else column_blocks<N, FORM, VEC, PERN, BLK>(a, blk, nblk);
 }
 
 // LEAD = 1: rows start at slot 1 (row s - 1 holds slot s) and m[0] = last_index, so the wave's
 // block is (n + 2) KiB: 8 bytes less per group.
-template <int N, int FORM, bool PERN, int BLK, int LEAD>
+template <int N, int FORM, bool PERN, int BLK, int LEAD, bool INPLACE>
 __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
     constexpr uint64_t T = HQ_TILE_GROUPS, H = T / 2;
     constexpr int NR = N - LEAD;   // match rows in the tile
@@ -369,8 +371,13 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
             uint64_t coa, cob;
             decide<N, FORM, PERN>(a, ga, m0, na, ci.x, la.x, ax.x, coa, ca, fa);
             decide<N, FORM, PERN>(a, gb, m1, nb, ci.y, la.y, ax.y, cob, cb, fb);
-            a.cout[ga] = coa;
-            a.cout[gb] = cob;
+            if constexpr (INPLACE) {
+                // the lane's 16 bytes of the committed row it has just read (groups ga, gb)
+                st_stream2(const_cast<uint64_t *>(t) + NR * T, (u64x2){coa, cob});
+            } else {
+                a.cout[ga] = coa;
+                a.cout[gb] = cob;
+            }
         } else {   // the batch's last, partial tile: group by group
             auto single = [&](int j, bool &c, bool &f) {
                 const uint64_t g = ga + H * j;
@@ -386,7 +393,8 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
                 uint64_t co;
                 decide<N, FORM, PERN>(a, g, m, PERN ? (int)a.nv[g] : N, t[NR * T + j], last, ax,
                                       co, c, f);
-                a.cout[g] = co;
+                if constexpr (INPLACE) const_cast<uint64_t *>(t)[NR * T + j] = co;
+                else a.cout[g] = co;
             };
             if (ga < a.G) single(0, ca, fa);
             if (gb < a.G) single(1, cb, fb);
@@ -1070,6 +1078,8 @@ int launch_commit_t(hq_ctx *ctx, const CommitK &k) {
 template <int N>
 int launch_commit_n(hq_ctx *ctx, const CommitK &k, int form, bool vec2, bool pern, int tiled) {
 #define HQ_DISPATCH(F)                                                                   \
+    if (tiled == 3) return pern ? launch_commit_t<N, F, 2, true, 3>(ctx, k)              \
+                                : launch_commit_t<N, F, 2, false, 3>(ctx, k);            \
     if (tiled == 2) return pern ? launch_commit_t<N, F, 2, true, 2>(ctx, k)              \
                                 : launch_commit_t<N, F, 2, false, 2>(ctx, k);            \
     if (tiled) return pern ? launch_commit_t<N, F, 2, true, 1>(ctx, k)                   \
@@ -1094,15 +1104,19 @@ int validate_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
     if (a->n_max < 1 || a->n_max > HQ_MAX_VOTERS)
         return hq::fail(ctx, HQ_E_INVAL, "hq_commit: n_max must be 1..8");
+    const bool in_place = a->layout == (HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE);
     if (a->layout != HQ_LAYOUT_COLUMNS && a->layout != HQ_LAYOUT_TILES &&
-        a->layout != HQ_LAYOUT_TILES_LEADER)
+        a->layout != HQ_LAYOUT_TILES_LEADER && !in_place)
         return hq::fail(ctx, HQ_E_INVAL, "hq_commit: unknown layout");
+    if (in_place && a->form != HQ_FORM_TERM_START && a->form != HQ_FORM_TERM_MASK)
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_commit: an in-place table holds the term-start or term-mask form");
     if (a->G == 0) return HQ_OK;
     const bool tiles = a->layout != HQ_LAYOUT_COLUMNS;
     if (tiles) {
-        if (!a->match || !a->committed_out)
+        if (!a->match || (!a->committed_out && !in_place))
             return hq::fail(ctx, HQ_E_INVAL, "hq_commit: NULL tiles (match) / committed_out");
-        if (!hq::aligned16(a->match) || !hq::aligned16(a->committed_out) ||
+        if (!hq::aligned16(a->match) || (!in_place && !hq::aligned16(a->committed_out)) ||
             (a->n_voting && (reinterpret_cast<uintptr_t>(a->n_voting) & 1)))
             return hq::fail(ctx, HQ_E_INVAL,
                             "hq_commit: tiles and committed_out must be 16-byte aligned, "
@@ -1202,7 +1216,10 @@ extern "C" int hq_commit_dev(hq_ctx *ctx, const hq_commit_args *a) {
     const CommitK k = commit_k(a);
     const bool vec2 = commit_vec2(a);
     const bool pern = a->n_voting != nullptr;
-    const int tiled = a->layout == HQ_LAYOUT_TILES_LEADER ? 2 : a->layout == HQ_LAYOUT_TILES ? 1 : 0;
+    const int tiled = a->layout == (HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE) ? 3
+                    : a->layout == HQ_LAYOUT_TILES_LEADER                       ? 2
+                    : a->layout == HQ_LAYOUT_TILES                              ? 1
+                                                                                : 0;
     switch (a->n_max) {
     case 1: return launch_commit_n<1>(ctx, k, a->form, vec2, pern, tiled);
     case 2: return launch_commit_n<2>(ctx, k, a->form, vec2, pern, tiled);
@@ -1235,7 +1252,8 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
     for (uint32_t i = 0; fusable && i < count; ++i)
         fusable = args[i].G > 0 && !args[i].n_voting && commit_vec2(args + i) &&
-                  args[i].form == args[0].form && args[i].layout == args[0].layout;
+                  args[i].form == args[0].form && args[i].layout == args[0].layout &&
+                  !(args[i].layout & HQ_LAYOUT_IN_PLACE);
     if (!fusable) return hq_commit_many_dev(ctx, args, count);
     FusedK f{};
     f.count = count;

@@ -31,7 +31,17 @@ int pre_launch(hq_ctx *ctx) {
 }
 
 int post_launch(hq_ctx *ctx, const char *what) {
-    return check_hip(ctx, hipGetLastError(), what);
+    int rc = check_hip(ctx, hipGetLastError(), what);
+    // hq_timing_begin_after: the region opens behind the n-th launch, in stream order, so the
+    // begin event fires when that launch ends and the next one is already queued
+    if (!rc && ctx->begin_after && --ctx->begin_after == 0) {
+        rc = check_hip(ctx, hipEventRecord(ctx->ev_begin, ctx->stream), "hipEventRecord");
+        if (!rc) {
+            ctx->timing = true;
+            ctx->region_launches = 0;
+        }
+    }
+    return rc;
 }
 
 int ensure_workspace(hq_ctx *ctx, size_t bytes) {
@@ -185,6 +195,7 @@ int hq_memset_async(hq_ctx *ctx, void *dst, int value, size_t bytes) {
 }
 
 static int timing_close(hq_ctx *ctx) {
+    ctx->begin_after = 0;   // a region that never opened records nothing
     if (!ctx->timing) return HQ_OK;
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     if (!rc) rc = hq::check_hip(ctx, hipEventRecord(ctx->ev_end, ctx->stream), "hipEventRecord");
@@ -222,6 +233,21 @@ int hq_timing_enable(hq_ctx *ctx, int enable) {
     if (rc) return rc;
     ctx->timing = true;
     ctx->region_launches = 0;
+    return HQ_OK;
+}
+
+int hq_timing_begin_after(hq_ctx *ctx, uint64_t launches) {
+    if (!ctx) return HQ_E_INVAL;
+    if (launches == 0) return hq_timing_enable(ctx, 1);
+    if (ctx->timing || ctx->begin_after)
+        return hq::fail(ctx, HQ_E_STATE, "hq_timing_begin_after: a timed region is already open");
+    int rc = timing_fold(ctx);
+    if (rc) return rc;
+    rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (!rc && !ctx->ev_begin) rc = hq::check_hip(ctx, hipEventCreate(&ctx->ev_begin), "hipEventCreate");
+    if (!rc && !ctx->ev_end) rc = hq::check_hip(ctx, hipEventCreate(&ctx->ev_end), "hipEventCreate");
+    if (rc) return rc;
+    ctx->begin_after = launches;
     return HQ_OK;
 }
 
@@ -323,6 +349,9 @@ int hq_commit(hq_ctx *ctx, const hq_commit_args *a) {
     if (!ctx) return HQ_E_INVAL;
     if (!a) return hq::fail(ctx, HQ_E_INVAL, "hq_commit: args is NULL");
     if (a->G == 0) return HQ_OK;
+    if (a->layout & HQ_LAYOUT_IN_PLACE)
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_commit: HQ_LAYOUT_IN_PLACE is a device-resident table (hq_commit_dev)");
     if (a->layout == HQ_LAYOUT_TILES || a->layout == HQ_LAYOUT_TILES_LEADER)
         return commit_tiles_host(ctx, a);
     if (!a->match || !a->committed_in || !a->committed_out || !a->last_index ||

@@ -1,0 +1,384 @@
+// hq_table.hip — the device-resident progress table in the headline layout.
+//
+// The table IS the commit kernel's input: HQ_LAYOUT_TILES_LEADER tiles (128 groups per tile; rows
+// match slot 1 .. n-1, committed, lastIndex, then term_start (u64) or the u16 term mask; row
+// position 2i holds group i of the tile and 2i + 1 group i + 64), decided in place by
+// hq_commit_dev with HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE. The kernels here apply a step's
+// deltas to it:
+//   hq_table_ingest_match_dev / _lag_dev   remote.tryUpdate per accepted ReplicateResp
+//                                          (remote.go:123-133, raft.go:1671-1700): match only rises
+//   hq_table_append_dev / _append_count_dev appendEntries (raft.go:911-922): lastIndex, the term
+//                                          bits of the new entries (the leader's own match is
+//                                          lastIndex by construction of the layout, raft.go:918)
+//   hq_table_committed_dev                 the committed row back in group order (readback)
+//
+// Every update is a max (match, lastIndex) or a sum (appended counts) per key, so the batch can
+// be applied in any order. Default: one 64-bit atomic per record. HQ_INGEST_GROUPED (the
+// records of one key adjacent in the batch, as a step worker emits them node by node): a wave
+// reduces each run of equal keys with a segmented scan over shuffles and the run's last lane
+// applies it with a plain read-modify-write; only the runs that touch the wave's first or last
+// lane (they may continue in the neighbouring wave) use an atomic.
+#include "hq_internal.h"
+
+namespace {
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kTBlock = 256;
+constexpr uint64_t kT = HQ_TILE_GROUPS;
+
+unsigned tgrid(uint64_t lanes) {
+    uint64_t b = (lanes + kTBlock - 1) / kTBlock;
+    if (b < 1) b = 1;
+    if (b > 256 * 64) b = 256 * 64;   // grid-stride beyond 64 workgroups per CU
+    return (unsigned)b;
+}
+
+// The table of one launch: rows of 128 u64 per tile, tw words per tile.
+struct TableK {
+    uint64_t *tiles;
+    uint64_t G, tw;
+    uint32_t nr;     // match rows = n_max - 1 (slots 1 .. n_max - 1)
+    uint32_t R;      // ring_len of the term mask
+    uint32_t mask;   // 1: term-mask form (u16 row), 0: term-start form (u64 row, untouched)
+    uint32_t flags;
+};
+
+// word offset of group g inside its tile's rows
+__device__ __forceinline__ uint64_t tpos(uint64_t g) {
+    const uint64_t i = g & (kT - 1);
+    return 2 * (i & 63) + (i >> 6);
+}
+__device__ __forceinline__ uint64_t *trow(const TableK &t, uint64_t g, uint32_t row) {
+    return t.tiles + (g / kT) * t.tw + (uint64_t)row * kT + tpos(g);
+}
+__device__ __forceinline__ uint16_t *tmask(const TableK &t, uint64_t g) {
+    return reinterpret_cast<uint16_t *>(t.tiles + (g / kT) * t.tw + (uint64_t)(t.nr + 2) * kT) +
+           tpos(g);
+}
+
+__device__ __forceinline__ void count_skip(uint64_t *n_skipped, bool skip) {
+    const uint64_t m = __ballot(skip);
+    if (n_skipped && m && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)m) - 1))
+        atomicAdd(reinterpret_cast<unsigned long long *>(n_skipped),
+                  (unsigned long long)__popcll(m));
+}
+
+// Inclusive segmented scan over the wave: v = op(v of every earlier lane with the same key),
+// valid because equal keys are adjacent (HQ_INGEST_GROUPED): if lane - off has this key, so has
+// every lane in between.
+template <bool SUM>
+__device__ __forceinline__ uint64_t seg_scan(uint64_t key, uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t ko = __shfl_up(key, off);
+        const uint64_t vo = __shfl_up(v, off);
+        if (lane >= off && ko == key) v = SUM ? v + vo : (vo > v ? vo : v);
+    }
+    return v;
+}
+
+// The lane that applies its key's run (the run's last lane) and whether the run may continue in
+// a neighbouring wave (then an atomic applies it).
+struct RunTail {
+    bool tail, edge;
+};
+__device__ __forceinline__ RunTail run_tail(uint64_t key) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t next = __shfl_down(key, 1);
+    RunTail r;
+    r.tail = lane == 63 || next != key;
+    r.edge = key == __shfl(key, 0) || key == __shfl(key, 63);
+    return r;
+}
+
+// the term-mask bits of the entries (prev, prev + n] (appendEntries at the leader's term)
+__device__ __forceinline__ uint32_t append_bits(uint64_t prev, uint64_t n, uint32_t R) {
+    if (n >= R) return R >= 32 ? 0xFFFFFFFFu : ((1u << R) - 1u);
+    uint32_t bits = 0;
+    for (uint64_t k = 1; k <= n; ++k) bits |= 1u << ((prev + k) & (R - 1));
+    return bits;
+}
+
+// OR the u16 mask bits of group g: plain (the lane owns the u16) or atomic on the 32-bit word
+// that holds it (positions 2i, 2i + 1 share a word)
+__device__ __forceinline__ void or_mask(const TableK &t, uint64_t g, uint32_t bits, bool atomic) {
+    uint16_t *m = tmask(t, g);
+    if (atomic) {
+        const uint64_t p = tpos(g);
+        atomicOr(reinterpret_cast<unsigned int *>(m - (p & 1)), (bits & 0xFFFFu) << (16 * (p & 1)));
+    } else {
+        *m = (uint16_t)(*m | bits);
+    }
+}
+
+// the raise of one match word: atomicMax, or a plain read-max-write by the run's owner
+__device__ __forceinline__ void raise(uint64_t *p, uint64_t v, bool atomic) {
+    if (atomic) {
+        atomicMax(reinterpret_cast<unsigned long long *>(p), (unsigned long long)v);
+    } else {
+        const uint64_t old = *p;
+        if (v > old) *p = v;
+    }
+}
+
+template <bool GROUPED>
+__global__ __launch_bounds__(kTBlock) void k_table_ingest_match(const hq_match_update *u,
+                                                                uint64_t count, TableK t,
+                                                                uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kTBlock) {
+        uint64_t key = ~0ull, v = 0;
+        bool ok = false;
+        if (i < count) {
+            const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u) + i);
+            key = x.x;
+            v = x.y;
+            const uint64_t g = key >> 8, s = key & 0xFF;
+            // slot 0 is the leader: its match is lastIndex, no ReplicateResp comes from self
+            ok = g < t.G && s >= 1 && s <= t.nr;
+        }
+        const uint64_t g = key >> 8;
+        const uint32_t s = (uint32_t)(key & 0xFF);
+        if constexpr (GROUPED) {
+            v = seg_scan<false>(key, v);
+            const RunTail r = run_tail(key);
+            if (ok && r.tail) raise(trow(t, g, s - 1), v, r.edge);
+        } else {
+            if (ok) raise(trow(t, g, s - 1), v, true);
+        }
+        count_skip(n_skipped, i < count && !ok);
+    }
+}
+
+// 8-byte records: group << 32 | slot << 28 | lag, the acknowledged index lastIndex - lag
+template <bool GROUPED>
+__global__ __launch_bounds__(kTBlock) void k_table_ingest_lag(const uint64_t *u, uint64_t count,
+                                                              TableK t, uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kTBlock) {
+        uint64_t key = ~0ull, v = 0;
+        bool ok = false, skip = false;
+        if (i < count) {
+            const uint64_t x = __builtin_nontemporal_load(u + i);
+            key = x >> 28;   // group << 4 | slot
+            const uint64_t g = x >> 32, s = (x >> 28) & 0xF, lag = x & 0x0FFFFFFFull;
+            ok = g < t.G && s >= 1 && s <= t.nr;
+            if (ok) {
+                const uint64_t last = *trow(t, g, t.nr + 1);
+                // an ack above lastIndex is skipped (its value 0 leaves the run's max alone)
+                if (lag <= last) v = last - lag;
+                else skip = true;
+            } else {
+                skip = true;
+            }
+        }
+        const uint64_t g = key >> 4;
+        const uint32_t s = (uint32_t)(key & 0xF);
+        if constexpr (GROUPED) {
+            v = seg_scan<false>(key, v);
+            const RunTail r = run_tail(key);
+            if (ok && r.tail && v) raise(trow(t, g, s - 1), v, r.edge);
+        } else {
+            if (ok && !skip) raise(trow(t, g, s - 1), v, true);
+        }
+        count_skip(n_skipped, skip);
+    }
+}
+
+// one group's append of its run: lastIndex raised to new_last (16-byte form) or advanced by n
+// (count form); the term-mask bits of the new entries set
+template <bool COUNT>
+__device__ __forceinline__ void apply_append(const TableK &t, uint64_t g, uint64_t v, bool atomic) {
+    uint64_t *lp = trow(t, g, t.nr + 1);
+    uint64_t prev, n;
+    if (COUNT) {
+        prev = atomic ? (uint64_t)atomicAdd(reinterpret_cast<unsigned long long *>(lp),
+                                            (unsigned long long)v)
+                      : *lp;
+        if (!atomic) *lp = prev + v;
+        n = v;
+    } else {
+        prev = atomic ? (uint64_t)atomicMax(reinterpret_cast<unsigned long long *>(lp),
+                                            (unsigned long long)v)
+                      : *lp;
+        if (v <= prev) return;   // a stale append leaves the group unchanged
+        if (!atomic) *lp = v;
+        n = v - prev;
+    }
+    if (t.mask) or_mask(t, g, append_bits(prev, n, t.R), atomic);
+}
+
+// COUNT = 0: hq_append_update (group, new_last); 1: 8-byte group << 32 | n
+template <bool COUNT, bool GROUPED>
+__global__ __launch_bounds__(kTBlock) void k_table_append(const uint64_t *u, uint64_t count,
+                                                          TableK t, uint64_t *n_skipped) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
+         i += (uint64_t)gridDim.x * kTBlock) {
+        uint64_t key = ~0ull, v = 0;
+        bool ok = false;
+        if (i < count) {
+            if (COUNT) {
+                const uint64_t x = __builtin_nontemporal_load(u + i);
+                key = x >> 32;
+                v = x & 0xFFFFFFFFull;
+                ok = key < t.G && v != 0;
+            } else {
+                const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u + 2 * i));
+                key = x.x;
+                v = x.y;
+                ok = key < t.G;
+            }
+        }
+        if constexpr (GROUPED) {
+            // a skipped record keeps its key but adds nothing (0 is the sum's and max's identity)
+            const bool keyok = key < t.G;
+            if (!ok) v = 0;
+            v = seg_scan<COUNT>(key, v);
+            const RunTail r = run_tail(key);
+            if (keyok && r.tail && v) apply_append<COUNT>(t, key, v, r.edge);
+        } else {
+            if (ok) apply_append<COUNT>(t, key, v, true);
+        }
+        count_skip(n_skipped, i < count && !ok);
+    }
+}
+
+// the committed row of every tile back in group order: lane i of a wave reads the 16 bytes of
+// groups i and i + 64 and writes them to their two column positions
+__global__ __launch_bounds__(kTBlock) void k_table_committed(TableK t, uint64_t *out) {
+    const uint64_t ntiles = (t.G + kT - 1) / kT;
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (kTBlock / 64);
+    for (uint64_t tile = (uint64_t)blockIdx.x * (kTBlock / 64) + (threadIdx.x >> 6); tile < ntiles;
+         tile += nw) {
+        const u64x2 v = __builtin_nontemporal_load(
+            reinterpret_cast<const u64x2 *>(t.tiles + tile * t.tw + (uint64_t)t.nr * kT + 2 * lane));
+        const uint64_t ga = tile * kT + lane, gb = ga + 64;
+        if (ga < t.G) out[ga] = v.x;
+        if (gb < t.G) out[gb] = v.y;
+    }
+}
+
+int table_k(hq_ctx *ctx, const char *what, uint64_t *tiles, uint64_t G, uint32_t n_max,
+            uint32_t form, uint32_t ring_len, uint32_t flags, TableK &t) {
+    if (!tiles || !hq::aligned16(tiles))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": tiles NULL or not 16-byte aligned");
+    if (n_max < 1 || n_max > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": n_max must be 1..8");
+    if (form != HQ_FORM_TERM_START && form != HQ_FORM_TERM_MASK)
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": the table holds the term-start or "
+                                                              "term-mask form");
+    if (form == HQ_FORM_TERM_MASK &&
+        (ring_len < 1 || ring_len > 16 || (ring_len & (ring_len - 1))))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": ring_len must be a power of two <= 16");
+    if (flags & ~HQ_INGEST_GROUPED)
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": unknown flags");
+    t.tiles = tiles;
+    t.G = G;
+    t.tw = hq_commit_tile_words_for(n_max, form, HQ_LAYOUT_TILES_LEADER);
+    t.nr = n_max - 1;
+    t.R = ring_len ? ring_len : 16;
+    t.mask = form == HQ_FORM_TERM_MASK;
+    t.flags = flags;
+    return HQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
+                              uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                              uint32_t flags, uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    TableK t;
+    int rc = table_k(ctx, "hq_table_ingest_match_dev", tiles, G, n_max, form, 16, flags, t);
+    if (rc) return rc;
+    if (!updates || !hq::aligned16(updates))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_match_dev: updates NULL or misaligned");
+    if ((rc = hq::pre_launch(ctx))) return rc;
+    if (flags & HQ_INGEST_GROUPED)
+        hipLaunchKernelGGL(k_table_ingest_match<true>, dim3(tgrid(count)), dim3(kTBlock), 0,
+                           ctx->stream, updates, count, t, n_skipped);
+    else
+        hipLaunchKernelGGL(k_table_ingest_match<false>, dim3(tgrid(count)), dim3(kTBlock), 0,
+                           ctx->stream, updates, count, t, n_skipped);
+    return hq::post_launch(ctx, "k_table_ingest_match");
+}
+
+int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                            uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                            uint32_t flags, uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    TableK t;
+    int rc = table_k(ctx, "hq_table_ingest_lag_dev", tiles, G, n_max, form, 16, flags, t);
+    if (rc) return rc;
+    if (!updates) return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_lag_dev: updates NULL");
+    if ((rc = hq::pre_launch(ctx))) return rc;
+    if (flags & HQ_INGEST_GROUPED)
+        hipLaunchKernelGGL(k_table_ingest_lag<true>, dim3(tgrid(count)), dim3(kTBlock), 0,
+                           ctx->stream, updates, count, t, n_skipped);
+    else
+        hipLaunchKernelGGL(k_table_ingest_lag<false>, dim3(tgrid(count)), dim3(kTBlock), 0,
+                           ctx->stream, updates, count, t, n_skipped);
+    return hq::post_launch(ctx, "k_table_ingest_lag");
+}
+
+static int table_append(hq_ctx *ctx, const char *what, const uint64_t *updates, uint64_t count,
+                        bool counts, uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                        uint32_t ring_len, uint32_t flags, uint64_t *n_skipped) {
+    if (!ctx) return HQ_E_INVAL;
+    if (count == 0) return HQ_OK;
+    TableK t;
+    int rc = table_k(ctx, what, tiles, G, n_max, form, ring_len, flags, t);
+    if (rc) return rc;
+    if (!updates || (!counts && !hq::aligned16(updates)))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": updates NULL or misaligned");
+    if ((rc = hq::pre_launch(ctx))) return rc;
+    const bool grouped = flags & HQ_INGEST_GROUPED;
+    const dim3 grid(tgrid(count)), blk(kTBlock);
+    if (counts) {
+        if (grouped) hipLaunchKernelGGL((k_table_append<true, true>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
+        else hipLaunchKernelGGL((k_table_append<true, false>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
+    } else {
+        if (grouped) hipLaunchKernelGGL((k_table_append<false, true>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
+        else hipLaunchKernelGGL((k_table_append<false, false>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
+    }
+    return hq::post_launch(ctx, "k_table_append");
+}
+
+int hq_table_append_dev(hq_ctx *ctx, const hq_append_update *updates, uint64_t count,
+                        uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                        uint32_t ring_len, uint32_t flags, uint64_t *n_skipped) {
+    return table_append(ctx, "hq_table_append_dev", reinterpret_cast<const uint64_t *>(updates),
+                        count, false, tiles, G, n_max, form, ring_len, flags, n_skipped);
+}
+
+int hq_table_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                              uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                              uint32_t ring_len, uint32_t flags, uint64_t *n_skipped) {
+    return table_append(ctx, "hq_table_append_count_dev", updates, count, true, tiles, G, n_max,
+                        form, ring_len, flags, n_skipped);
+}
+
+int hq_table_committed_dev(hq_ctx *ctx, const uint64_t *tiles, uint64_t G, uint32_t n_max,
+                           uint32_t form, uint64_t *committed) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    TableK t;
+    int rc = table_k(ctx, "hq_table_committed_dev", const_cast<uint64_t *>(tiles), G, n_max, form,
+                     16, 0, t);
+    if (rc) return rc;
+    if (!committed) return hq::fail(ctx, HQ_E_INVAL, "hq_table_committed_dev: committed NULL");
+    if ((rc = hq::pre_launch(ctx))) return rc;
+    const uint64_t ntiles = (G + kT - 1) / kT;
+    hipLaunchKernelGGL(k_table_committed, dim3(tgrid(ntiles * 64)), dim3(kTBlock), 0, ctx->stream,
+                       t, committed);
+    return hq::post_launch(ctx, "k_table_committed");
+}
+
+}  // extern "C"

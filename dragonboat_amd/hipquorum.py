@@ -34,7 +34,9 @@ HQ_LAYOUT_TILES = 1
 HQ_LAYOUT_TILES_LEADER = 2   # tiles without the leader row: slot 0 = last_index
 HQ_LAG_LEADER_IMPLICIT = 1   # hq_commit_lag_args.flags: lag rows start at slot 1
 HQ_TILE_GROUPS = 128
-HQ_ABI_VERSION = 6
+HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table decided in place
+HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
+HQ_ABI_VERSION = 7
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -186,6 +188,7 @@ SIGNATURES = {
     "hq_memcpy_async": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int]),
     "hq_memset_async": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t]),
     "hq_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "hq_timing_begin_after": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "hq_timing_read": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _u64p]),
     "hq_timing_reset": (ctypes.c_int, [_vp]),
     "hq_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs)]),
@@ -228,6 +231,20 @@ SIGNATURES = {
                                          ctypes.c_uint64, ctypes.c_uint32, _vp]),
     "hq_append_count_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
                                            ctypes.c_uint32, ctypes.c_uint64, _vp]),
+    "hq_table_ingest_match_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 _vp]),
+    "hq_table_ingest_lag_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                               _vp]),
+    "hq_table_append_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_uint32, _vp]),
+    "hq_table_append_count_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, _vp]),
+    "hq_table_committed_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_uint32, _vp]),
     "hq_pack_commit": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.POINTER(CommitArgs)]),
     "hq_pack_ring32": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp]),
     "hq_tile_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), _vp]),
@@ -396,6 +413,10 @@ class Context:
     def timing(self, enable: bool) -> None:
         self._check(lib.hq_timing_enable(self.h, int(enable)))
 
+    def timing_begin_after(self, launches: int) -> None:
+        """Open a timed region behind the next ``launches`` launches (hq_timing_begin_after)."""
+        self._check(lib.hq_timing_begin_after(self.h, launches))
+
     def timing_read(self) -> tuple[float, int]:
         ms = ctypes.c_double(0)
         n = ctypes.c_uint64(0)
@@ -513,6 +534,30 @@ class Context:
         self._check(lib.hq_append_count_dev(self.h, _p(updates), count, _p(last_index),
                                             _p(match_slot0), _p(term_mask), ring_len, G,
                                             _p(n_skipped)))
+
+    # -- device-resident progress table (HQ_LAYOUT_TILES_LEADER, decided in place) ----------
+    def table_ingest_match_dev(self, updates, count, tiles, G, n_max, form, flags=0,
+                               n_skipped=None):
+        self._check(lib.hq_table_ingest_match_dev(self.h, _p(updates), count, _p(tiles), G, n_max,
+                                                  form, flags, _p(n_skipped)))
+
+    def table_ingest_lag_dev(self, updates, count, tiles, G, n_max, form, flags=0,
+                             n_skipped=None):
+        self._check(lib.hq_table_ingest_lag_dev(self.h, _p(updates), count, _p(tiles), G, n_max,
+                                                form, flags, _p(n_skipped)))
+
+    def table_append_dev(self, updates, count, tiles, G, n_max, form, ring_len=16, flags=0,
+                         n_skipped=None):
+        self._check(lib.hq_table_append_dev(self.h, _p(updates), count, _p(tiles), G, n_max, form,
+                                            ring_len, flags, _p(n_skipped)))
+
+    def table_append_count_dev(self, updates, count, tiles, G, n_max, form, ring_len=16, flags=0,
+                               n_skipped=None):
+        self._check(lib.hq_table_append_count_dev(self.h, _p(updates), count, _p(tiles), G, n_max,
+                                                  form, ring_len, flags, _p(n_skipped)))
+
+    def table_committed_dev(self, tiles, G, n_max, form, committed):
+        self._check(lib.hq_table_committed_dev(self.h, _p(tiles), G, n_max, form, _p(committed)))
 
     def synth_commit_dev(self, spec: SynthSpec, args: CommitArgs) -> None:
         self._check(lib.hq_synth_commit_dev(self.h, ctypes.byref(spec), ctypes.byref(args)))
@@ -689,6 +734,59 @@ def tile_commit_host(columns: CommitArgs, layout: int = HQ_LAYOUT_TILES) -> np.n
         _chk(lib.hq_tile_commit_as_host(ctypes.byref(columns), _p(out), layout),
              "hq_tile_commit_as_host")
     return out
+
+
+class TileView:
+    """Group-order access to the rows of HQ_LAYOUT_TILES(_LEADER) tiles held in a host uint64
+    array (tests and host-side re-syncs; the kernels read the tiles directly). Row position 2i of
+    tile t holds group 128 t + i, position 2i + 1 group 128 t + 64 + i (include/hipquorum.h)."""
+
+    def __init__(self, tiles: np.ndarray, G: int, n_max: int, form: int, layout: int):
+        lay = layout & 0xFF
+        self.tiles, self.G, self.n_max, self.form = tiles, G, n_max, form
+        self.lead = lay == HQ_LAYOUT_TILES_LEADER
+        self.nr = n_max - 1 if self.lead else n_max      # match rows
+        self.tw = commit_tile_words(n_max, form, lay)
+        g = np.arange(G, dtype=np.int64)
+        i = g % HQ_TILE_GROUPS
+        self.base = (g // HQ_TILE_GROUPS) * self.tw
+        self.pos = 2 * (i % 64) + i // 64
+        self.rows = {"committed": self.nr, "last_index": self.nr + 1, "aux": self.nr + 2}
+
+    def _idx(self, row: int, groups=None):
+        b = self.base if groups is None else self.base[groups]
+        p = self.pos if groups is None else self.pos[groups]
+        return b + row * HQ_TILE_GROUPS + p
+
+    def row(self, name: str) -> np.ndarray:
+        """committed / last_index (u64) or aux (term_start / term u64, or the u16 term mask)."""
+        r = self.rows[name]
+        if name == "aux" and self.form == HQ_FORM_TERM_MASK:
+            return self.tiles.view(np.uint16)[4 * (self.base + r * HQ_TILE_GROUPS) + self.pos]
+        return self.tiles[self._idx(r)]
+
+    def match(self) -> np.ndarray:
+        """match slot-major [n_max][G]; with the leader layout slot 0 is lastIndex."""
+        out = np.empty((self.n_max, self.G), np.uint64)
+        s0 = 0
+        if self.lead:
+            out[0] = self.row("last_index")
+            s0 = 1
+        for s in range(s0, self.n_max):
+            out[s] = self.tiles[self._idx(s - s0)]
+        return out
+
+    def set_row(self, name: str, groups, values) -> None:
+        r = self.rows[name]
+        if name == "aux" and self.form == HQ_FORM_TERM_MASK:
+            self.tiles.view(np.uint16)[4 * (self.base[groups] + r * HQ_TILE_GROUPS)
+                                       + self.pos[groups]] = values
+        else:
+            self.tiles[self._idx(r, groups)] = values
+
+
+def tile_view(tiles: np.ndarray, G: int, n_max: int, form: int, layout: int) -> TileView:
+    return TileView(tiles, G, n_max, form, layout)
 
 
 HQ_BITS_TILE_GROUPS = 1024

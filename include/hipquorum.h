@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 6
+#define HQ_ABI_VERSION 7
 
 /* status codes */
 #define HQ_OK          0
@@ -67,6 +67,10 @@ extern "C" {
 #define HQ_LAYOUT_TILES   1   /* the same arrays cut into tiles of HQ_TILE_GROUPS groups */
 #define HQ_LAYOUT_TILES_LEADER 2  /* tiles without the leader's match row (slot 0 = last_index) */
 #define HQ_TILE_GROUPS  128   /* groups per tile: one wave64, two groups per lane */
+/* flag OR-ed into HQ_LAYOUT_TILES_LEADER: the tiles are a device-resident progress table decided
+ * in place — committed' is written into each tile's committed_in row (committed_out unused, may be
+ * NULL; the tiles must be writable). Term-start and term-mask forms, hq_commit_dev only. */
+#define HQ_LAYOUT_IN_PLACE 0x100u
 
 /* vote outcomes, numerically equal to the reference State enum (internal/raft/raft.go:62-71) */
 #define HQ_OUTCOME_FOLLOWER  0u   /* rejections reached quorum: becomeFollower (raft.go:1981-1984) */
@@ -113,6 +117,11 @@ int hq_memset_async(hq_ctx *ctx, void *dst, int value, size_t bytes);
  * kernels: kernel duration + the dependent-launch boundary). No per-launch events are recorded:
  * on gfx950 they add several microseconds to a ~10 us kernel. */
 int hq_timing_enable(hq_ctx *ctx, int enable);
+/* Open a timed region behind the next `launches` kernel launches on the context's stream: the
+ * begin event is recorded right after the launches-th one (in stream order it fires when that
+ * kernel ends), so a region over back-to-back launches enqueued in one go starts with the next
+ * kernel already queued and measures no host launch latency. 0 = hq_timing_enable(ctx, 1). */
+int hq_timing_begin_after(hq_ctx *ctx, uint64_t launches);
 int hq_timing_read(hq_ctx *ctx, double *total_ms, uint64_t *launches);
 int hq_timing_reset(hq_ctx *ctx);
 
@@ -210,7 +219,8 @@ static inline uint64_t hq_commit_tile_words(uint32_t n_max, uint32_t form) {
 }
 /* words of one tile in `layout` (HQ_LAYOUT_TILES or HQ_LAYOUT_TILES_LEADER) */
 static inline uint64_t hq_commit_tile_words_for(uint32_t n_max, uint32_t form, uint32_t layout) {
-    return hq_commit_tile_words(layout == HQ_LAYOUT_TILES_LEADER ? n_max - 1 : n_max, form);
+    return hq_commit_tile_words((layout & 0xFFu) == HQ_LAYOUT_TILES_LEADER ? n_max - 1 : n_max,
+                                form);
 }
 static inline uint64_t hq_commit_tiles(uint64_t G) {
     return (G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
@@ -224,7 +234,10 @@ int hq_tile_commit_dev(hq_ctx *ctx, const hq_commit_args *columns, uint64_t *til
 int hq_tile_commit_host(const hq_commit_args *columns, uint64_t *tiles);
 /* The same into `layout` = HQ_LAYOUT_TILES or HQ_LAYOUT_TILES_LEADER (tiles of
  * hq_commit_tile_words_for(n_max, form, layout) words; the leader layout drops match slot 0,
- * and the host packer returns HQ_E_INVAL if a group with n >= 1 has match[0] != last_index). */
+ * and the host packer returns HQ_E_INVAL if a group with n >= 1 has match[0] != last_index; the
+ * device packer does not check it: it is meant for generated inputs whose slot 0 is lastIndex by
+ * construction, and a real table must be cut by the host packer or kept in the leader layout
+ * from the start, hq_table_* below). */
 int hq_tile_commit_as_dev(hq_ctx *ctx, const hq_commit_args *columns, uint64_t *tiles,
                           uint32_t layout);
 int hq_tile_commit_as_host(const hq_commit_args *columns, uint64_t *tiles, uint32_t layout);
@@ -413,6 +426,11 @@ int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active, const uint8_t 
  *
  * Updates whose group >= G or slot >= n_max are skipped and counted into *n_skipped (a device
  * uint64_t, may be NULL; accumulated, not reset).
+ *
+ * Padding: the ack and term_mask updates are 32-bit atomic ORs on the word that holds the target
+ * byte / u16, so the ack array must be allocated to a multiple of 4 bytes and term_mask to an
+ * even number of entries (hq_malloc_dev's rounding does it; a caller sub-allocating these arrays
+ * must pad them itself). The bytes beyond G in that last word are never changed (OR with 0).
  */
 typedef struct hq_match_update {
     uint64_t group_slot;   /* group << 8 | slot */
@@ -451,6 +469,49 @@ int hq_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count, uint
 int hq_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
                         uint64_t *last_index, uint64_t *match_slot0, uint16_t *term_mask,
                         uint32_t ring_len, uint64_t G, uint64_t *n_skipped);
+
+/* ---------------------------------------------------------------- progress table (tiles) ---- */
+/*
+ * The device-resident progress table in the headline layout: the commit kernel's own
+ * HQ_LAYOUT_TILES_LEADER tiles of (n_max, form) — form HQ_FORM_TERM_START or HQ_FORM_TERM_MASK —
+ * kept on the GPU across steps and decided in place (hq_commit_dev with layout
+ * HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE), so a step ships only its deltas and the decision
+ * streams the same 8(n-1) + 26 or 8(n-1) + 32 bytes per group as the headline kernel. Build it
+ * from columns with hq_tile_commit_as_host / _dev (HQ_LAYOUT_TILES_LEADER).
+ *   hq_table_ingest_match_dev  remote.tryUpdate per ReplicateResp (remote.go:123-133):
+ *                              match[slot] = max(match[slot], index); records as hq_match_update
+ *                              (16-byte aligned); slot 0 (the leader, whose match is lastIndex)
+ *                              and slot >= n_max are skipped and counted
+ *   hq_table_ingest_lag_dev    the same from 8-byte records group << 32 | slot << 28 | lag
+ *                              (index = lastIndex - lag as the table holds it when the kernel runs)
+ *   hq_table_append_dev        appendEntries (raft.go:911-922): lastIndex = max(lastIndex,
+ *                              new_last) and the term-mask bits of the new entries; records as
+ *                              hq_append_update (16-byte aligned)
+ *   hq_table_append_count_dev  the same from 8-byte records group << 32 | n: lastIndex += n
+ *   hq_table_committed_dev     the committed row of every tile into committed[G], group order
+ * flags: 0 = any batch (one 64-bit atomic per record); HQ_INGEST_GROUPED = the caller guarantees
+ * that the records of one key — (group, slot) for the ingests, group for the appends — are
+ * adjacent in the batch (a step worker emitting node by node; a batch with unique keys is
+ * grouped). Each wave then reduces its runs of equal keys with a segmented scan and applies a
+ * run with one plain read-modify-write; runs that reach the wave's first or last lane (they may
+ * continue in the next wave) use one atomic. Results equal the sequential application in any
+ * order; a batch that is not grouped must not carry the flag.
+ */
+#define HQ_INGEST_GROUPED 1u
+int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
+                              uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                              uint32_t flags, uint64_t *n_skipped);
+int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                            uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                            uint32_t flags, uint64_t *n_skipped);
+int hq_table_append_dev(hq_ctx *ctx, const hq_append_update *updates, uint64_t count,
+                        uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                        uint32_t ring_len, uint32_t flags, uint64_t *n_skipped);
+int hq_table_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
+                              uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
+                              uint32_t ring_len, uint32_t flags, uint64_t *n_skipped);
+int hq_table_committed_dev(hq_ctx *ctx, const uint64_t *tiles, uint64_t G, uint32_t n_max,
+                           uint32_t form, uint64_t *committed);
 
 /* ---------------------------------------------------------------- host-side packers --------- */
 /*

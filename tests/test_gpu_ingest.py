@@ -1,6 +1,7 @@
 """Device-resident progress table against the oracle's sequential restatements:
 match ingest (remote.tryUpdate), ack ingest (confirmed-set insert), leader append, and a
-multi-step pipeline (append -> acks -> commit in place) that must track the oracle step by step."""
+multi-step pipeline (append -> acks -> commit in place) that must track the oracle step by step.
+The same kernels over the headline tile layout, and the host-fed pipeline: tests/test_gpu_table.py."""
 import numpy as np
 import pytest
 
@@ -132,60 +133,6 @@ def test_device_resident_leader_pipeline(gpu_ctx, hq):
     assert total_changed > G  # commits advanced on many groups across the steps
     for x in list(d.values()) + [chg, fb]:
         gpu_ctx.free(x)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("depth,compact", [(1, False), (2, False), (3, False), (1, True),
-                                           (2, True)])
-def test_host_fed_pipeline_matches_oracle(hq, depth, compact):
-    """dragonboat_amd.pipeline: host-fed steps (pinned appends + match deltas -> append, ingest,
-    commit in place -> readback) over `depth` contexts. Every step's read-back changed bitmap and
-    committed column equal the oracle's sequential run, whatever the pipelining."""
-    from dragonboat_amd.pipeline import HostFedPipeline
-
-    rng = np.random.default_rng(SEED + 4)
-    G, n, R, T = 40_009, 3, 16, 7
-    inp = qref.CommitInputs(qref.spec(SEED + 4, G, n))
-    host = dict(match=inp.match.copy(), last=inp.last_index.copy(), mask=inp.term_mask.copy(),
-                committed=inp.committed_in.copy())
-    p = HostFedPipeline(0, G, n, G // 2, G, depth=depth, ring_len=R, compact=compact)
-    p.upload(host["match"], host["committed"], host["last"], host["mask"])
-    want, slots = [], []
-    for step in range(T):
-        gsel = rng.choice(G, G // 3, replace=False).astype(np.uint64)
-        app = np.stack([gsel, host["last"][gsel] + rng.integers(1, 4, len(gsel), dtype=np.uint64)],
-                       axis=1).astype(np.uint64)
-        counts = app[:, 1] - host["last"][gsel]           # entries appended (gsel distinct)
-        qref.append(app, host["last"], host["match"][:G], host["mask"], R, G)
-        g = rng.integers(0, G, G, dtype=np.uint64)
-        s = rng.integers(1, n, G, dtype=np.uint64)
-        lag = rng.integers(0, 6, G, dtype=np.uint64)
-        idx = host["last"][g] - lag                       # lastIndex after the step's appends
-        upd = np.stack([(g << np.uint64(8)) | s, idx], axis=1).astype(np.uint64)
-        qref.ingest_match(upd, host["match"], G, G, n)
-        out = np.zeros(G, np.uint64)
-        wchg = np.zeros(hq.words64(G), np.uint64)
-        qa = qref.commit_args(G, n, 2, R, host["match"], host["committed"], out, host["last"],
-                              changed=wchg, term_mask=host["mask"])
-        assert qref.commit_batch(qa, 8) == 0
-        host["committed"] = out
-        want.append((wchg, out))
-        wire_app = hq.pack_append_counts(gsel, counts) if compact else app.reshape(-1)
-        wire_upd = hq.pack_lag_updates(g, s, lag) if compact else upd.reshape(-1)
-        pa = p.ctxs[step % depth].pinned(wire_app.size, np.uint64)
-        pa[:] = wire_app
-        pu = p.ctxs[step % depth].pinned(wire_upd.size, np.uint64)
-        pu[:] = wire_upd
-        slots.append(p.step(step, pa, len(app), pu, G))
-        if step % depth == depth - 1 or step == T - 1:
-            # read back the steps whose result buffers are about to be reused
-            for j in range(step - step % depth, step + 1):
-                chg, com = p.results(slots[j])
-                np.testing.assert_array_equal(chg, want[j][0])
-                np.testing.assert_array_equal(com, want[j][1])
-    np.testing.assert_array_equal(p.ctxs[0].download(p.table.match), host["match"])
-    assert sum(int(np.unpackbits(w[0].view(np.uint8)).sum()) for w in want) > G
-    p.close()
 
 
 @pytest.mark.gpu

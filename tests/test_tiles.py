@@ -138,3 +138,28 @@ def test_bench_byte_accounting():
     assert bench.algo_bytes_per_group(w["c2l"]) == 24
     assert bench.algo_bytes_per_group(w["c2ll"]) == 20
     assert bench.algo_bytes_per_group(w["c5v5tl"]) == 58
+    # the headline: BASELINE config 3, 1M x 5 voters, mask form, leader rows
+    assert bench.HEADLINE == "c3mtl"
+    assert bench.algo_bytes_per_group(w["c3mtl"]) == 58
+    assert w["c3mtl"]["G"] == 1 << 20 and w["c3mtl"]["n"] == 5 and w["c3mtl"]["cfg"] == 2
+
+
+@pytest.mark.parametrize("form,lead", [(2, 1), (0, 1), (2, 0), (0, 0)])
+def test_tile_view_reads_back_the_columns(hq, form, lead):
+    """hipquorum.TileView (the host-side view of a device table's tiles) recovers every column
+    the host packer put into the tiles, and set_row writes one group's field in place."""
+    G, n = 1000 + 37, 5
+    inp = qref.CommitInputs(qref.spec(0x5EED3000, G, n))
+    lay = hq.HQ_LAYOUT_TILES_LEADER if lead else hq.HQ_LAYOUT_TILES
+    tiles = hq.tile_commit_host(column_args(hq, inp, form, n), lay)
+    v = hq.tile_view(tiles, G, n, form, lay)
+    np.testing.assert_array_equal(v.match().reshape(-1), inp.match)
+    np.testing.assert_array_equal(v.row("committed"), inp.committed_in)
+    np.testing.assert_array_equal(v.row("last_index"), inp.last_index)
+    np.testing.assert_array_equal(v.row("aux"), inp.term_mask if form == 2 else inp.term_start)
+    g = np.array([0, 63, 64, 127, 128, G - 1])
+    v.set_row("committed", g, np.arange(6, dtype=np.uint64) + 7)
+    got = hq.tile_view(tiles, G, n, form, lay).row("committed")
+    np.testing.assert_array_equal(got[g], np.arange(6, dtype=np.uint64) + 7)
+    keep = np.setdiff1d(np.arange(G), g)
+    np.testing.assert_array_equal(got[keep], inp.committed_in[keep])

@@ -69,6 +69,8 @@ def main():
             "hbm_bytes_per_launch": hbm,
             "correction": "(2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE halves 16B/lane streams)",
             "round": rnd,
+            "source": f"profiles/{rnd}/{w}_pmc_FETCH_SIZE.csv + {w}_pmc_WRITE_SIZE.csv "
+                      f"(kernel time: {w}_kernel_stats.csv)",
         }
         print(w, json.dumps(traffic[w]))
     json.dump(traffic, open(tj, "w"), indent=1, sort_keys=True)
