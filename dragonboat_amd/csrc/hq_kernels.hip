@@ -312,12 +312,11 @@ __device__ __forceinline__ void column_blocks(const CommitK &a, uint64_t blk, ui
 #ifndef HQ_TILE_SCHED_BARRIER
 #define HQ_TILE_SCHED_BARRIER 1
 #endif
-// HQ_LAYOUT_TILES: one wave per 128-group tile. Row position p holds group p of the tile, so lane
-// i's 16-byte load of a row brings groups 2i and 2i + 1: every field of the wave is ONE contiguous
-// block of (n + 3) KiB, the lane's committed' pair is one 16-byte store, and a tile's rows are in
-// group order (a delta ingest in group order touches whole lines, hq_table.hip). The two ballots
-// are bit-interleaved into the tile's two bitmap words. The full-tile test is scalar (the wave
-// index is read into an SGPR), so full tiles carry no per-lane guard.
+// HQ_LAYOUT_TILES: one wave per 128-group tile. Row position 2i holds group i of the tile and
+// position 2i + 1 group i + 64, so lane i's 16-byte load of a row brings groups i and i + 64:
+// every field of the wave is ONE contiguous block of (n + 3) KiB, and the two ballots are the
+// tile's two bitmap words as they are (no bit interleave). The full-tile test is scalar (the
+// wave index is read into an SGPR), so full tiles carry no per-lane guard.
 // TILED = 3: HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE, the device-resident table decided in
 // place (committed' written into the tile's committed row)
 template <int N, int FORM, int VEC, bool PERN, int BLK, int TILED = 0>
@@ -331,14 +330,14 @@ __device__ __forceinline__ void commit_blocks(const CommitK &a, uint64_t blk, ui
 // block is (n + 2) KiB: 8 bytes less per group.
 template <int N, int FORM, bool PERN, int BLK, int LEAD, bool INPLACE>
 __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint64_t nblk) {
-    constexpr uint64_t T = HQ_TILE_GROUPS;
+    constexpr uint64_t T = HQ_TILE_GROUPS, H = T / 2;
     constexpr int NR = N - LEAD;   // match rows in the tile
     const uint64_t lane = threadIdx.x & 63;
     const uint64_t wave = blk * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = nblk * BLK * 2;
     for (uint64_t wbase = wave * T; wbase < a.G; wbase += step) {
         const uint64_t *t = a.match + (wbase / T) * a.stride + lane * 2;
-        const uint64_t ga = wbase + 2 * lane, gb = ga + 1;
+        const uint64_t ga = wbase + lane, gb = ga + H;
         bool ca = false, cb = false, fa = false, fb = false;
         if (wbase + T <= a.G) {
             uint64_t m0[N], m1[N];
@@ -376,11 +375,12 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
                 // the lane's 16 bytes of the committed row it has just read (groups ga, gb)
                 st_stream2(const_cast<uint64_t *>(t) + NR * T, (u64x2){coa, cob});
             } else {
-                st_stream2(a.cout + ga, (u64x2){coa, cob});
+                a.cout[ga] = coa;
+                a.cout[gb] = cob;
             }
         } else {   // the batch's last, partial tile: group by group
             auto single = [&](int j, bool &c, bool &f) {
-                const uint64_t g = ga + j;
+                const uint64_t g = ga + H * j;
                 uint64_t m[N];
                 const uint64_t last = t[(NR + 1) * T + j];
 #pragma unroll
@@ -399,17 +399,12 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
             if (ga < a.G) single(0, ca, fa);
             if (gb < a.G) single(1, cb, fb);
         }
-        // the tile's two bitmap words: word k covers lanes 32k .. 32k + 31, lane i's groups
-        // are bits 2i, 2i + 1 (the two ballots interleaved)
         const uint64_t ba = __ballot(ca), bb = __ballot(cb);
         const uint64_t xa = __ballot(fa), xb = __ballot(fb);
         const uint64_t w = (wbase >> 6) + lane;
         if (lane < 2 && w < ((a.G + 63) >> 6)) {
-            const int sh = 32 * (int)lane;
-            if (a.changed)
-                a.changed[w] = spread32((uint32_t)(ba >> sh)) | (spread32((uint32_t)(bb >> sh)) << 1);
-            if (a.fallback)
-                a.fallback[w] = spread32((uint32_t)(xa >> sh)) | (spread32((uint32_t)(xb >> sh)) << 1);
+            if (a.changed) a.changed[w] = lane ? bb : ba;
+            if (a.fallback) a.fallback[w] = lane ? xb : xa;
         }
     }
 }
@@ -1718,8 +1713,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_commit(const CommitCols c, uint
          w += (uint64_t)gridDim.x * kBlock) {
         const uint64_t t = w / tw, r = w % tw, row = r / HQ_TILE_GROUPS;
         uint64_t v = 0;
-        // row position p holds group p of the tile (include/hipquorum.h)
-        auto group = [&](uint64_t p) { return t * HQ_TILE_GROUPS + p; };
+        // row position p holds group (p >> 1) + 64 * (p & 1) of the tile (include/hipquorum.h)
+        auto group = [&](uint64_t p) { return t * HQ_TILE_GROUPS + (p >> 1) + (HQ_TILE_GROUPS / 2) * (p & 1); };
         if (form == HQ_FORM_TERM_MASK && row >= n + 2) {   // 4 u16 masks per word
             const uint64_t p0 = 4 * (r - (uint64_t)(n + 2) * HQ_TILE_GROUPS);
             for (int k = 3; k >= 0; --k) {

@@ -242,9 +242,9 @@ extern "C" int hq_tile_commit_as_host(const hq_commit_args *a, uint64_t *tiles, 
         uint64_t *tile = tiles + t * tw;
         std::memset(tile, 0, tw * 8);
         uint16_t *mrow = reinterpret_cast<uint16_t *>(tile + (n + 2) * T);
-        // row position p holds group p of the tile
+        // row position p holds group (p >> 1) + 64 * (p & 1) of the tile
         for (uint64_t p = 0; p < T; ++p) {
-            const uint64_t g = t * T + p;
+            const uint64_t g = t * T + (p >> 1) + (T / 2) * (p & 1);
             if (g >= a->G) continue;
             for (uint32_t s = 0; s < n; ++s)
                 tile[s * T + p] = a->match[(s + lead) * a->match_stride + g];

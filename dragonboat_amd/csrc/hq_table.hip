@@ -2,7 +2,7 @@
 //
 // The table IS the commit kernel's input: HQ_LAYOUT_TILES_LEADER tiles (128 groups per tile; rows
 // match slot 1 .. n-1, committed, lastIndex, then term_start (u64) or the u16 term mask; row
-// position p holds group p of the tile), decided in place by
+// position 2i holds group i of the tile and 2i + 1 group i + 64), decided in place by
 // hq_commit_dev with HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE. The kernels here apply a step's
 // deltas to it:
 //   hq_table_ingest_match_dev / _lag_dev   remote.tryUpdate per accepted ReplicateResp
@@ -45,7 +45,10 @@ struct TableK {
 };
 
 // word offset of group g inside its tile's rows
-__device__ __forceinline__ uint64_t tpos(uint64_t g) { return g & (kT - 1); }
+__device__ __forceinline__ uint64_t tpos(uint64_t g) {
+    const uint64_t i = g & (kT - 1);
+    return 2 * (i & 63) + (i >> 6);
+}
 __device__ __forceinline__ uint64_t *trow(const TableK &t, uint64_t g, uint32_t row) {
     return t.tiles + (g / kT) * t.tw + (uint64_t)row * kT + tpos(g);
 }
@@ -99,7 +102,7 @@ __device__ __forceinline__ uint32_t append_bits(uint64_t prev, uint64_t n, uint3
 }
 
 // OR the u16 mask bits of group g: plain (the lane owns the u16) or atomic on the 32-bit word
-// that holds it (groups 2i, 2i + 1 share a word)
+// that holds it (positions 2i, 2i + 1 share a word)
 __device__ __forceinline__ void or_mask(const TableK &t, uint64_t g, uint32_t bits, bool atomic) {
     uint16_t *m = tmask(t, g);
     if (atomic) {
@@ -242,8 +245,8 @@ __global__ __launch_bounds__(kTBlock) void k_table_append(const uint64_t *u, uin
     }
 }
 
-// the committed row of every tile into a column: lane i of a wave moves the 16 bytes of groups
-// 2i and 2i + 1
+// the committed row of every tile back in group order: lane i of a wave reads the 16 bytes of
+// groups i and i + 64 and writes them to their two column positions
 __global__ __launch_bounds__(kTBlock) void k_table_committed(TableK t, uint64_t *out) {
     const uint64_t ntiles = (t.G + kT - 1) / kT;
     const uint64_t lane = threadIdx.x & 63;
@@ -252,9 +255,9 @@ __global__ __launch_bounds__(kTBlock) void k_table_committed(TableK t, uint64_t 
          tile += nw) {
         const u64x2 v = __builtin_nontemporal_load(
             reinterpret_cast<const u64x2 *>(t.tiles + tile * t.tw + (uint64_t)t.nr * kT + 2 * lane));
-        const uint64_t ga = tile * kT + 2 * lane, gb = ga + 1;
-        if (gb < t.G) *reinterpret_cast<u64x2 *>(out + ga) = v;
-        else if (ga < t.G) out[ga] = v.x;
+        const uint64_t ga = tile * kT + lane, gb = ga + 64;
+        if (ga < t.G) out[ga] = v.x;
+        if (gb < t.G) out[gb] = v.y;
     }
 }
 

@@ -738,8 +738,8 @@ def tile_commit_host(columns: CommitArgs, layout: int = HQ_LAYOUT_TILES) -> np.n
 
 class TileView:
     """Group-order access to the rows of HQ_LAYOUT_TILES(_LEADER) tiles held in a host uint64
-    array (tests and host-side re-syncs; the kernels read the tiles directly). Row position p of
-    tile t holds group 128 t + p (include/hipquorum.h)."""
+    array (tests and host-side re-syncs; the kernels read the tiles directly). Row position 2i of
+    tile t holds group 128 t + i, position 2i + 1 group 128 t + 64 + i (include/hipquorum.h)."""
 
     def __init__(self, tiles: np.ndarray, G: int, n_max: int, form: int, layout: int):
         lay = layout & 0xFF
@@ -750,7 +750,7 @@ class TileView:
         g = np.arange(G, dtype=np.int64)
         i = g % HQ_TILE_GROUPS
         self.base = (g // HQ_TILE_GROUPS) * self.tw
-        self.pos = i
+        self.pos = 2 * (i % 64) + i // 64
         self.rows = {"committed": self.nr, "last_index": self.nr + 1, "aux": self.nr + 2}
 
     def _idx(self, row: int, groups=None):

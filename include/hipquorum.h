@@ -168,8 +168,9 @@ int hq_timing_reset(hq_ctx *ctx);
  * one contiguous tile, so a wave reads its groups as ONE stream instead of n + 3 column streams
  * (6 % less time for the same bytes at 1 M groups x 3 voters, tools/kexp5.hip). `match` points
  * to tile 0 (16-byte aligned); tile t = match + t * hq_commit_tile_words(n_max, form) holds
- * groups [128 t, 128 t + 128), each row 128 entries of one field in group order, position p
- * holding group 128 t + p (lane i of a wave reads groups 2i and 2i + 1 with one 16-byte load):
+ * groups [128 t, 128 t + 128), each row 128 entries of one field, position 2i holding group
+ * 128 t + i and position 2i + 1 group 128 t + 64 + i (lane i of a wave reads both with one
+ * 16-byte load; its two ballots are then the tile's two bitmap words):
  *   rows 0 .. n_max-1   match of slot s (u64)
  *   row  n_max          committed_in (u64)
  *   row  n_max+1        last_index (u64)

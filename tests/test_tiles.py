@@ -41,8 +41,20 @@ def expected_tiles(hq, inp, form, n, lead=0):
         aux = inp.term_start if form == hq.HQ_FORM_TERM_START else inp.term
         rows.append(np.concatenate([aux, np.zeros(pad, np.uint64)]).reshape(nt, T))
     tiles = np.concatenate(rows, axis=1)
-    # row position p = group p of the tile (include/hipquorum.h)
-    return tiles.reshape(-1)
+    # row position 2i = group i of the tile, 2i + 1 = group 64 + i (include/hipquorum.h)
+    perm = np.empty(T, np.int64)
+    perm[0::2] = np.arange(T // 2)
+    perm[1::2] = np.arange(T // 2) + T // 2
+    out = np.empty_like(tiles)
+    nrow = n - lead + 2
+    for r in range(nrow):
+        out[:, r * T:(r + 1) * T] = tiles[:, r * T:(r + 1) * T][:, perm]
+    if form == hq.HQ_FORM_TERM_MASK:
+        m = tiles[:, nrow * T:].copy().view(np.uint16)
+        out[:, nrow * T:] = np.ascontiguousarray(m[:, perm]).view(np.uint64)
+    else:
+        out[:, nrow * T:] = tiles[:, nrow * T:][:, perm]
+    return out.reshape(-1)
 
 
 @pytest.mark.parametrize("G", [1, 127, 128, 129, 1000])
