@@ -43,6 +43,11 @@ tools/lib_mb%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSR
 	@mkdir -p tools/lib_mb$*
 	$(HIPCC) $(HIPFLAGS) -DHQ_MAX_BLOCKS=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
 
+# tuning variants: records per lane of the table ingest kernels
+tools/lib_iv%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(DEPS)
+	@mkdir -p tools/lib_iv$*
+	$(HIPCC) $(HIPFLAGS) -DHQ_INGEST_V=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp
+
 variants: tools/lib_vec2/libhipquorum.so tools/lib_b512/libhipquorum.so
 
 clean:

@@ -113,77 +113,98 @@ __device__ __forceinline__ void or_mask(const TableK &t, uint64_t g, uint32_t bi
     }
 }
 
-// the raise of one match word: atomicMax, or a plain read-max-write by the run's owner
-__device__ __forceinline__ void raise(uint64_t *p, uint64_t v, bool atomic) {
-    if (atomic) {
-        atomicMax(reinterpret_cast<unsigned long long *>(p), (unsigned long long)v);
-    } else {
-        const uint64_t old = *p;
-        if (v > old) *p = v;
-    }
-}
+// Records per lane of the ingest kernels: a wave takes V consecutive chunks of 64 records per
+// iteration (lane l holds record l of each chunk) and issues every chunk's loads before the
+// first dependent step, so a wave keeps V record loads and then V table loads in flight instead
+// of one (the grouped ingest is a chain of dependent steps: record load -> scan -> table load
+// -> store; with one record per lane its memory latency, not bandwidth, set the rate).
+#ifndef HQ_INGEST_V
+#define HQ_INGEST_V 4
+#endif
+constexpr int kIV = HQ_INGEST_V;
 
-template <bool GROUPED>
-__global__ __launch_bounds__(kTBlock) void k_table_ingest_match(const hq_match_update *u,
-                                                                uint64_t count, TableK t,
-                                                                uint64_t *n_skipped) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
-         i += (uint64_t)gridDim.x * kTBlock) {
-        uint64_t key = ~0ull, v = 0;
-        bool ok = false;
-        if (i < count) {
-            const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u) + i);
-            key = x.x;
-            v = x.y;
-            const uint64_t g = key >> 8, s = key & 0xFF;
-            // slot 0 is the leader: its match is lastIndex, no ReplicateResp comes from self
-            ok = g < t.G && s >= 1 && s <= t.nr;
-        }
-        const uint64_t g = key >> 8;
-        const uint32_t s = (uint32_t)(key & 0xFF);
-        if constexpr (GROUPED) {
-            v = seg_scan<false>(key, v);
-            const RunTail r = run_tail(key);
-            if (ok && r.tail) raise(trow(t, g, s - 1), v, r.edge);
-        } else {
-            if (ok) raise(trow(t, g, s - 1), v, true);
-        }
-        count_skip(n_skipped, i < count && !ok);
-    }
-}
-
-// 8-byte records: group << 32 | slot << 28 | lag, the acknowledged index lastIndex - lag
-template <bool GROUPED>
-__global__ __launch_bounds__(kTBlock) void k_table_ingest_lag(const uint64_t *u, uint64_t count,
-                                                              TableK t, uint64_t *n_skipped) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
-         i += (uint64_t)gridDim.x * kTBlock) {
-        uint64_t key = ~0ull, v = 0;
-        bool ok = false, skip = false;
-        if (i < count) {
-            const uint64_t x = __builtin_nontemporal_load(u + i);
-            key = x >> 28;   // group << 4 | slot
-            const uint64_t g = x >> 32, s = (x >> 28) & 0xF, lag = x & 0x0FFFFFFFull;
-            ok = g < t.G && s >= 1 && s <= t.nr;
-            if (ok) {
-                const uint64_t last = *trow(t, g, t.nr + 1);
-                // an ack above lastIndex is skipped (its value 0 leaves the run's max alone)
-                if (lag <= last) v = last - lag;
-                else skip = true;
-            } else {
-                skip = true;
+// One launch applies match raises: key = group << 8 | slot (match form) or group << 4 | slot
+// (lag form), value = the acknowledged index. LAG: 8-byte records, index = lastIndex - lag.
+template <bool GROUPED, bool LAG>
+__global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uint64_t count,
+                                                          TableK t, uint64_t *n_skipped) {
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kTBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kTBlock / 64);
+    constexpr int SH = LAG ? 4 : 8;   // slot bits of the key
+    for (uint64_t base = wave * 64 * kIV; base < count; base += nwaves * 64 * kIV) {
+        uint64_t key[kIV], v[kIV], lag[kIV];
+        bool in[kIV], ok[kIV];
+#pragma unroll
+        for (int c = 0; c < kIV; ++c) {
+            const uint64_t i = base + 64 * c + lane;
+            in[c] = i < count;
+            key[c] = ~0ull;
+            v[c] = lag[c] = 0;
+            if (in[c]) {
+                if constexpr (LAG) {
+                    const uint64_t x = __builtin_nontemporal_load(u + i);
+                    key[c] = x >> 28;   // group << 4 | slot
+                    lag[c] = x & 0x0FFFFFFFull;
+                } else {
+                    const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u) + i);
+                    key[c] = x.x;
+                    v[c] = x.y;
+                }
             }
         }
-        const uint64_t g = key >> 4;
-        const uint32_t s = (uint32_t)(key & 0xF);
-        if constexpr (GROUPED) {
-            v = seg_scan<false>(key, v);
-            const RunTail r = run_tail(key);
-            if (ok && r.tail && v) raise(trow(t, g, s - 1), v, r.edge);
-        } else {
-            if (ok && !skip) raise(trow(t, g, s - 1), v, true);
+        bool skip[kIV];
+#pragma unroll
+        for (int c = 0; c < kIV; ++c) {
+            const uint64_t g = key[c] >> SH, s = key[c] & ((1u << SH) - 1);
+            // slot 0 is the leader: its match is lastIndex, no ReplicateResp comes from self
+            ok[c] = in[c] && g < t.G && s >= 1 && s <= t.nr;
+            skip[c] = in[c] && !ok[c];
         }
-        count_skip(n_skipped, skip);
+        if constexpr (LAG) {
+            uint64_t last[kIV];
+#pragma unroll
+            for (int c = 0; c < kIV; ++c) last[c] = ok[c] ? *trow(t, key[c] >> 4, t.nr + 1) : 0;
+#pragma unroll
+            for (int c = 0; c < kIV; ++c) {
+                // an ack above lastIndex is skipped; its value 0 leaves the run's max alone
+                const bool above = ok[c] && lag[c] > last[c];
+                v[c] = ok[c] && !above ? last[c] - lag[c] : 0;
+                skip[c] |= above;
+            }
+        }
+        if constexpr (GROUPED) {
+            bool tail[kIV], edge[kIV];
+            uint64_t *p[kIV], old[kIV];
+#pragma unroll
+            for (int c = 0; c < kIV; ++c) {
+                v[c] = seg_scan<false>(key[c], v[c]);
+                const RunTail r = run_tail(key[c]);
+                tail[c] = ok[c] && r.tail;
+                edge[c] = r.edge;
+            }
+#pragma unroll
+            for (int c = 0; c < kIV; ++c) {
+                p[c] = trow(t, key[c] >> SH, (uint32_t)(key[c] & ((1u << SH) - 1)) - 1);
+                old[c] = tail[c] && !edge[c] ? *p[c] : 0;
+            }
+#pragma unroll
+            for (int c = 0; c < kIV; ++c) {
+                if (!tail[c]) continue;
+                if (edge[c]) atomicMax(reinterpret_cast<unsigned long long *>(p[c]),
+                                       (unsigned long long)v[c]);
+                else if (v[c] > old[c]) *p[c] = v[c];
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < kIV; ++c)
+                if (ok[c] && !skip[c])
+                    atomicMax(reinterpret_cast<unsigned long long *>(
+                                  trow(t, key[c] >> SH, (uint32_t)(key[c] & ((1u << SH) - 1)) - 1)),
+                              (unsigned long long)v[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < kIV; ++c) count_skip(n_skipped, skip[c]);
     }
 }
 
@@ -300,13 +321,15 @@ int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint6
     if (!updates || !hq::aligned16(updates))
         return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_match_dev: updates NULL or misaligned");
     if ((rc = hq::pre_launch(ctx))) return rc;
+    const uint64_t *u = reinterpret_cast<const uint64_t *>(updates);
+    const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
     if (flags & HQ_INGEST_GROUPED)
-        hipLaunchKernelGGL(k_table_ingest_match<true>, dim3(tgrid(count)), dim3(kTBlock), 0,
-                           ctx->stream, updates, count, t, n_skipped);
+        hipLaunchKernelGGL((k_table_ingest<true, false>), grid, blk, 0, ctx->stream, u, count, t,
+                           n_skipped);
     else
-        hipLaunchKernelGGL(k_table_ingest_match<false>, dim3(tgrid(count)), dim3(kTBlock), 0,
-                           ctx->stream, updates, count, t, n_skipped);
-    return hq::post_launch(ctx, "k_table_ingest_match");
+        hipLaunchKernelGGL((k_table_ingest<false, false>), grid, blk, 0, ctx->stream, u, count, t,
+                           n_skipped);
+    return hq::post_launch(ctx, "k_table_ingest");
 }
 
 int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
@@ -319,13 +342,14 @@ int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count
     if (rc) return rc;
     if (!updates) return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_lag_dev: updates NULL");
     if ((rc = hq::pre_launch(ctx))) return rc;
+    const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
     if (flags & HQ_INGEST_GROUPED)
-        hipLaunchKernelGGL(k_table_ingest_lag<true>, dim3(tgrid(count)), dim3(kTBlock), 0,
-                           ctx->stream, updates, count, t, n_skipped);
+        hipLaunchKernelGGL((k_table_ingest<true, true>), grid, blk, 0, ctx->stream, updates, count,
+                           t, n_skipped);
     else
-        hipLaunchKernelGGL(k_table_ingest_lag<false>, dim3(tgrid(count)), dim3(kTBlock), 0,
-                           ctx->stream, updates, count, t, n_skipped);
-    return hq::post_launch(ctx, "k_table_ingest_lag");
+        hipLaunchKernelGGL((k_table_ingest<false, true>), grid, blk, 0, ctx->stream, updates, count,
+                           t, n_skipped);
+    return hq::post_launch(ctx, "k_table_ingest");
 }
 
 static int table_append(hq_ctx *ctx, const char *what, const uint64_t *updates, uint64_t count,

@@ -74,12 +74,14 @@ def test_table_ingest_lag(gpu_ctx, hq, grouped):
     G, n = 50_003, 4
     form = hq.HQ_FORM_TERM_MASK
     inp = qref.CommitInputs(qref.spec(SEED + 2, G, n))
+    # five groups near the start of the log, so that acks above their lastIndex fit a lag
+    inp.last_index[:5] = inp.match[:5] = inp.committed_in[:5] = 10
     dt = _table(gpu_ctx, hq, inp, form)
     cnt = 300_000
     g = rng.integers(0, G, cnt, dtype=np.uint64)
     s = rng.integers(0, n + 1, cnt, dtype=np.uint64)
     lag = rng.integers(0, 40, cnt, dtype=np.uint64)
-    lag[:5] = inp.last_index[g[:5]] + np.uint64(1)             # above lastIndex: skipped
+    g[:5], s[:5], lag[:5] = np.arange(5), 1, 11                # above lastIndex: skipped
     g[5:9] = np.uint64(G + 3)                                  # out of range: skipped
     wire = hq.pack_lag_updates(g, s, lag)
     if grouped:
