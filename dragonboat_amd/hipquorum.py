@@ -148,6 +148,25 @@ DROPPED_READ_DTYPE = np.dtype([("cluster_id", "<u8"), ("ctx_low", "<u8"), ("ctx_
                               align=True)
 
 
+# wire decode (include/hipquorum.h "wire decode")
+HQ_RPC_BIN_VERSION = 210
+WIRE_MESSAGE_DTYPE = np.dtype([("ev", EVENT_DTYPE), ("cluster_id", "<u8"), ("to", "<u8"),
+                               ("log_term", "<u8"), ("commit", "<u8"), ("n_entries", "<u4"),
+                               ("has_snapshot", "<u4")], align=True)
+
+
+class WireBatchInfo(ctypes.Structure):
+    _fields_ = [("n_messages", ctypes.c_uint64), ("deployment_id", ctypes.c_uint64),
+                ("source_address_len", ctypes.c_uint64), ("bin_ver", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class WireStats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in
+                ("batches", "bytes", "messages", "entries", "snapshot_received",
+                 "dropped_batches", "dropped_messages", "dropped_no_cluster")]
+
+
 class StepInput(ctypes.Structure):
     """Mirror of ``hq_step_input``."""
 
@@ -265,6 +284,16 @@ SIGNATURES = {
                                            ctypes.c_uint32]),
     "hq_worker_step": (ctypes.c_int, [_vp, ctypes.POINTER(StepInput),
                                       ctypes.POINTER(StepOutput)]),
+    "hq_wire_decode_batch": (ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_uint64, _u64p,
+                                            ctypes.POINTER(WireBatchInfo)]),
+    "hq_wire_open": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(_vp)]),
+    "hq_wire_close": (None, [_vp]),
+    "hq_wire_last_error": (ctypes.c_char_p, [_vp]),
+    "hq_wire_reset": (ctypes.c_int, [_vp]),
+    "hq_wire_add_local": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64]),
+    "hq_wire_add_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    "hq_wire_step_input": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepInput),
+                                          ctypes.POINTER(WireStats)]),
     "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
     "hq_synth_commit_lag_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec),
                                                ctypes.POINTER(LagArgs), _vp]),
@@ -1074,3 +1103,62 @@ class Worker:
         assert int(groups["n_members"].sum()) == len(members)
         self._check(lib.hq_worker_add_groups(self.h, _p(groups), len(groups), _p(members)),
                     "hq_worker_add_groups")
+
+
+# ------------------------------------------------------------------------------ wire decode ----
+def decode_batch(data: bytes):
+    """hq_wire_decode_batch: (WIRE_MESSAGE_DTYPE array, WireBatchInfo) of one MessageBatch."""
+    buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+    n = ctypes.c_uint64(0)
+    info = WireBatchInfo()
+    _chk(lib.hq_wire_decode_batch(_p(buf), len(data), None, 0, ctypes.byref(n),
+                                  ctypes.byref(info)), "hq_wire_decode_batch")
+    out = np.zeros(max(1, n.value), WIRE_MESSAGE_DTYPE)
+    _chk(lib.hq_wire_decode_batch(_p(buf), len(data), _p(out), n.value, ctypes.byref(n),
+                                  ctypes.byref(info)), "hq_wire_decode_batch")
+    return out[:n.value], info
+
+
+class Wire:
+    """hq_wire: a step's input assembled from received MessageBatch bytes and local events."""
+
+    def __init__(self, deployment_id: int = 0):
+        self.h = _vp()
+        _chk(lib.hq_wire_open(deployment_id, ctypes.byref(self.h)), "hq_wire_open")
+        self._inp = StepInput()
+
+    def close(self) -> None:
+        if self.h:
+            lib.hq_wire_close(self.h)
+            self.h = None
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != HQ_OK:
+            raise HQError(rc, f"{what}: {lib.hq_wire_last_error(self.h).decode()}")
+
+    def reset(self) -> None:
+        self._check(lib.hq_wire_reset(self.h), "hq_wire_reset")
+
+    def add_local(self, cluster_id: int, events: np.ndarray) -> None:
+        ev = np.ascontiguousarray(events, EVENT_DTYPE)
+        self._check(lib.hq_wire_add_local(self.h, cluster_id, _p(ev), len(ev)),
+                    "hq_wire_add_local")
+
+    def add_batch(self, data: bytes) -> None:
+        buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+        self._check(lib.hq_wire_add_batch(self.h, _p(buf), len(data)), "hq_wire_add_batch")
+
+    def step_input(self, worker: "Worker"):
+        """(groups, offsets, events) numpy views of the assembled hq_step_input (owned by the
+        Wire until its next reset), and the WireStats."""
+        st = WireStats()
+        self._check(lib.hq_wire_step_input(self.h, worker.h, ctypes.byref(self._inp),
+                                           ctypes.byref(st)), "hq_wire_step_input")
+        n = self._inp.n_groups
+        grp = np.ctypeslib.as_array((ctypes.c_uint32 * max(1, n)).from_address(self._inp.groups))[:n] \
+            if n else np.zeros(0, np.uint32)
+        off = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(self._inp.offsets))
+        ne = int(off[-1]) if n else 0
+        ev = np.frombuffer((ctypes.c_char * (ne * EVENT_DTYPE.itemsize)).from_address(
+            self._inp.events), EVENT_DTYPE) if ne else np.zeros(0, EVENT_DTYPE)
+        return grp.copy(), off.copy(), ev.copy(), st

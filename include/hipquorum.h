@@ -756,6 +756,75 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *g,
                         uint32_t reads_cap);
 int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
 
+/* ---------------------------------------------------------------- wire decode --------------- */
+/*
+ * The step worker's input from the wire. A host receives raftpb.MessageBatch bytes (the protobuf
+ * encoding of raftpb/raft.proto:154-168 Message and :191-196 MessageBatch, marshalled by
+ * raft.pb.go Message.MarshalTo :2232 / MessageBatch.MarshalTo :2417) over the reference's TCP
+ * transport; these functions turn them into hq_step_input rows the way the reference turns them
+ * into Peer.Handle calls:
+ *   Transport.handleRequest (internal/transport/transport.go:289-300): a batch whose
+ *     deployment_id is not this host's or whose bin_ver is not HQ_RPC_BIN_VERSION is dropped;
+ *   messageHandler.HandleMessageBatch (nodehost.go:2021-2061): SnapshotReceived messages are
+ *     handled aside (not queued), messages of clusters this worker does not run are dropped,
+ *     the rest are queued per cluster in arrival order;
+ *   node.handleEvents (node.go:1113-1157) / handleReceivedMessages (:1257-1287): per cluster, the
+ *     local ReadIndex first, then the received messages in arrival order, then the ticks
+ *     (CheckQuorum / Election), then the proposals.
+ * Any valid proto2 encoding is accepted (fields in any order, unknown fields skipped, entries and
+ * snapshots counted but not decoded — the quorum path reads Type, From, Term, LogIndex, Reject,
+ * Hint, HintHigh). A malformed batch (truncated, bad varint, wrong wire type of a known field)
+ * is rejected whole with HQ_E_INVAL.
+ */
+#define HQ_RPC_BIN_VERSION 210u   /* raftio.RPCBinVersion (raftio/binversion.go:30) */
+
+typedef struct hq_wire_message {  /* one decoded pb.Message */
+    hq_event ev;                  /* kind HQ_EV_MESSAGE; type, from, term, log_index, hint,
+                                     hint_high, reject */
+    uint64_t cluster_id;
+    uint64_t to;
+    uint64_t log_term;
+    uint64_t commit;
+    uint32_t n_entries;           /* entries carried (field 11), not decoded */
+    uint32_t has_snapshot;        /* field 12 present */
+} hq_wire_message;
+
+typedef struct hq_wire_batch_info {
+    uint64_t n_messages;
+    uint64_t deployment_id;
+    uint64_t source_address_len;
+    uint32_t bin_ver;
+    uint32_t reserved;
+} hq_wire_batch_info;
+
+typedef struct hq_wire_stats {    /* counters since the last hq_wire_reset */
+    uint64_t batches, bytes, messages, entries;
+    uint64_t snapshot_received;   /* SnapshotReceived messages (handled aside by the host) */
+    uint64_t dropped_batches;     /* foreign deployment id / binary version */
+    uint64_t dropped_messages;    /* the messages of those batches */
+    uint64_t dropped_no_cluster;  /* events of clusters the worker does not run */
+} hq_wire_stats;
+
+/* Stateless: decode one MessageBatch into out[0 .. min(count, cap)) (out may be NULL to count).
+ * *count = messages in the batch; HQ_E_STATE if they do not fit cap. */
+int hq_wire_decode_batch(const uint8_t *bytes, size_t len, hq_wire_message *out, uint64_t cap,
+                         uint64_t *count, hq_wire_batch_info *info);
+
+typedef struct hq_wire hq_wire;
+int hq_wire_open(uint64_t deployment_id, hq_wire **out);
+void hq_wire_close(hq_wire *w);
+const char *hq_wire_last_error(const hq_wire *w);
+/* Start a step: forget every queued event. */
+int hq_wire_reset(hq_wire *w);
+/* Local events of a cluster for this step (HQ_EV_READ, HQ_EV_CHECK_QUORUM, HQ_EV_ELECTION,
+ * HQ_EV_PROPOSE), in their order within each kind. */
+int hq_wire_add_local(hq_wire *w, uint64_t cluster_id, const hq_event *events, uint64_t count);
+/* Decode one received MessageBatch and queue its messages. */
+int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len);
+/* The step's hq_step_input for `worker`: clusters in order of first appearance, each with its
+ * events in node.handleEvents order. Arrays owned by w until its next reset / step_input. */
+int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wire_stats *stats);
+
 /* ---------------------------------------------------------------- synthetic inputs ---------- */
 
 /*

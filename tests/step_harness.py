@@ -139,3 +139,78 @@ def same_step(oracle_out, worker_out, cid):
     o, w = oracle_out[cid], worker_out[cid]
     for k in ("committed", "commit_changed", "ready", "resps", "states", "dropped", "deferred"):
         assert o[k] == w[k], (cid, k, o[k], w[k])
+
+
+class WireBackend(WorkerBackend):
+    """The step worker fed from the wire: every received message of the step is marshalled into
+    raftpb.MessageBatch bytes (tests/wire_encode.py, the gogo layout), the clusters' queues
+    interleaved in arrival order and cut into several batches, plus batches and messages the
+    reference drops before Peer.Handle (a foreign deployment id, SnapshotReceived, a cluster this
+    host does not run); hq_wire decodes them and assembles the step input (local events via
+    hq_wire_add_local). Results must equal the event-row path's."""
+
+    DEPLOYMENT = 0x5EED
+
+    def __init__(self, hq, n_max=8, seed=0, worker=None):
+        super().__init__(hq, n_max, seed, worker)
+        self.wire = hq.Wire(self.DEPLOYMENT)
+        self.last_stats = None
+
+    def close(self):
+        self.wire.close()
+        super().close()
+
+    def build_inputs(self, per_group):
+        import wire_encode as we
+
+        hq, rng, wire = self.hq, self.rng, self.wire
+        wire.reset()
+        cids = list(per_group)
+        rng.shuffle(cids)
+        queues = {}
+        for cid in cids:
+            events = per_group[cid]
+            check_phase_order(events)
+            local = [event_record(hq, e) for e in events if e[0] != "msg"]
+            if local:
+                wire.add_local(cid, np.array(local, hq.EVENT_DTYPE))
+            queues[cid] = [we.message(type=e[1], to=1, frm=e[2], cluster_id=cid, term=e[3],
+                                      log_index=e[4], hint=e[5], hint_high=e[6],
+                                      reject=bool(e[7]))
+                           for e in events if e[0] == "msg"]
+        # arrival order: a random merge of the clusters' queues (each kept in order), with
+        # messages the reference drops before the queue mixed in
+        stream, heads = [], {c: 0 for c in cids}
+        live = [c for c in cids if queues[c]]
+        while live:
+            c = live[int(rng.integers(len(live)))]
+            stream.append(queues[c][heads[c]])
+            heads[c] += 1
+            if heads[c] == len(queues[c]):
+                live.remove(c)
+            r = rng.random()
+            if r < 0.02:   # SnapshotReceived: handled aside (nodehost.go:2039-2044)
+                stream.append(we.message(type=22, frm=2, cluster_id=c))
+            elif r < 0.04:  # a cluster this worker does not run: dropped (nodehost.go:2045)
+                stream.append(we.message(type=13, frm=2, cluster_id=(1 << 62) + c, term=1,
+                                         log_index=5))
+        cut = sorted(set(int(x) for x in rng.integers(0, len(stream) + 1, 3)))
+        parts = [stream[a:b] for a, b in zip([0] + cut, cut + [len(stream)])]
+        for i, p in enumerate(parts):
+            wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT, source_address=b"n2:1"))
+            if i == 0:   # a foreign deployment's batch: dropped whole (transport.go:291-295)
+                wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT + 1))
+        grp, off, ev, st = wire.step_input(self.w)
+        self.last_stats = st
+        # event index -> (cluster, position in its per_group list): the assembled rows keep
+        # node.handleEvents order, as the per_group lists do
+        refs = {}
+        handle_cid = {self.w.find(c): c for c in cids}
+        for i, h in enumerate(grp):
+            cid = handle_cid[int(h)]
+            for pos, k in enumerate(range(int(off[i]), int(off[i + 1]))):
+                refs[k] = (cid, pos)
+            assert int(off[i + 1]) - int(off[i]) == len(per_group[cid])
+        assert sorted(handle_cid[int(h)] for h in grp) == sorted(c for c in cids
+                                                                 if per_group[c])
+        return (grp, off, ev), refs

@@ -75,6 +75,13 @@ int main(void) {
   F(hq_group_view, ctx_high) F(hq_group_view, term_mask) F(hq_group_view, first_member)
   F(hq_group_view, n_members) F(hq_group_view, first_msg) F(hq_group_view, n_msgs)
   F(hq_msg, from) F(hq_msg, hint_low) F(hq_msg, hint_high) F(hq_msg, reject)
+  printf("hq_wire_message %zu\n", sizeof(hq_wire_message));
+  F(hq_wire_message, ev) F(hq_wire_message, cluster_id) F(hq_wire_message, to)
+  F(hq_wire_message, log_term) F(hq_wire_message, commit) F(hq_wire_message, n_entries)
+  F(hq_wire_message, has_snapshot)
+  printf("hq_wire_batch_info %zu\nhq_wire_stats %zu\nbin_ver %u\n", sizeof(hq_wire_batch_info),
+         sizeof(hq_wire_stats), (unsigned)HQ_RPC_BIN_VERSION);
+  printf("in_place %u\ngrouped %u\n", (unsigned)HQ_LAYOUT_IN_PLACE, (unsigned)HQ_INGEST_GROUPED);
   return 0;
 }
 """
@@ -92,7 +99,12 @@ def test_struct_layout_matches_c(hq, tmp_path):
     assert int(c["hq_synth_spec"]) == ctypes.sizeof(hq.SynthSpec)
     assert int(c["hq_commit_lag_args"]) == ctypes.sizeof(hq.LagArgs)
     dtypes = {"hq_member": hq.MEMBER_DTYPE, "hq_group_view": hq.GROUP_DTYPE,
-              "hq_msg": hq.MSG_DTYPE}
+              "hq_msg": hq.MSG_DTYPE, "hq_wire_message": hq.WIRE_MESSAGE_DTYPE}
+    assert int(c["hq_wire_batch_info"]) == ctypes.sizeof(hq.WireBatchInfo)
+    assert int(c["hq_wire_stats"]) == ctypes.sizeof(hq.WireStats)
+    assert int(c["bin_ver"]) == hq.HQ_RPC_BIN_VERSION
+    assert int(c["in_place"]) == hq.HQ_LAYOUT_IN_PLACE
+    assert int(c["grouped"]) == hq.HQ_INGEST_GROUPED
     for name, dt in dtypes.items():
         assert int(c[name]) == dt.itemsize, name
     assert int(c["hq_match_update"]) == 16 and int(c["hq_append_update"]) == 16

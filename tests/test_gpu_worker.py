@@ -133,3 +133,58 @@ def test_add_group_validation(hq):
             w.add_group(3, 1, 1, 0, 0, 0, 0, [(1, 0, 0, 0)])
     finally:
         w.close()
+
+
+# ---- the same worker driven from wire bytes (raftpb.MessageBatch, hq_wire) --------------------
+@pytest.fixture(scope="module")
+def wire_backend(hq):
+    from step_harness import WireBackend
+
+    b = WireBackend(hq, n_max=8, seed=5)
+    yield b
+    b.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_reference_scenario_from_wire_bytes(wire_backend, case):
+    outs, state = sc.run_case(wire_backend, case)
+    sc.check_case(case, outs, state)
+    want_outs, want_state = sc.run_case(OracleBackend(), case)
+    assert state == want_state, case["name"]
+    for w, o in zip(outs, want_outs):
+        for k in ("committed", "commit_changed", "ready", "resps", "states", "dropped",
+                  "deferred"):
+            assert w[k] == o[k], (case["name"], k, w[k], o[k])
+
+
+@pytest.mark.parametrize("seed,G,steps", [(11, 1500, 6), (12, 300, 15)])
+def test_random_differential_from_wire_bytes(hq, seed, G, steps):
+    from step_harness import WireBackend
+
+    rng = np.random.default_rng(seed)
+    groups = sr.random_groups(rng, G)
+    o, w = OracleBackend(), WireBackend(hq, n_max=8, seed=seed)
+    try:
+        for g in groups:
+            o.add_group(*g)
+            w.add_group(*g)
+        ctx_seq = [0]
+        dropped = 0
+        for s in range(steps):
+            per = {}
+            for g in groups:
+                if rng.random() < 0.85:
+                    per[g[0]] = sr.random_events(rng, o.state(g[0]), s + 1, ctx_seq)
+            want = o.step(per)
+            got = w.step(per)
+            st = w.last_stats
+            assert st.dropped_batches == 1 and st.batches >= 2
+            dropped += st.dropped_no_cluster + st.snapshot_received
+            assert got["_fallback"] == []
+            for cid in per:
+                same_step(want, got, cid)
+            for g in groups:
+                assert w.state(g[0]) == o.state(g[0]), (s, g[0])
+        assert dropped > 0
+    finally:
+        w.close()
