@@ -627,8 +627,10 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=5):
     spec = hq.synth_spec(SEED_BASE + 9, G, n, cid_base=rng.cid_base, cid_stride=rng.cid_stride)
     nb = 4   # distinct host batches cycled through
     out = {}
-    variants = ((2, True, True), (2, False, True), (2, True, False), (2, False, False),
-                (1, False, False))
+    # the first pipeline of a process pays one-time costs (first touch of pinned staging, the
+    # copy engines' first mappings): a throwaway run of the headline variant goes first
+    variants = ((2, True, True), (2, True, True), (2, False, True), (2, True, False),
+                (2, False, False), (1, False, False))
     for depth, compact, grouped in variants:
         r = np.random.default_rng(d.rank)
         p = HostFedPipeline(d.device, G, n, G // 4, G, depth=depth, compact=compact,
