@@ -103,6 +103,10 @@ WORKLOADS = {
                      "contiguous stream per wave)"),
     "c4ut": dict(cfg=3, kind="bits", G=16 << 20, n=7, uniform=True, tiled=True,
                  desc="as c4u over 1024-group bitmap tiles (rows ack, granted, rejected)"),
+    "c4t3": dict(cfg=3, kind="bits", G=16 << 20, n=7, tiled3=True,
+                 desc="as c4t over 3-byte tiles: the leader's own slot implicit (never acks its "
+                      "ctx, always grants its vote), 7 bits per bitmap + 3 bits of n - 1 "
+                      "(3.375 B per group instead of 4.375)"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
                desc="64M groups mixed 3/5/7 voters (n = {3,5,7}[clusterID % 3]) sharded "
                     "clusterID % 8: 8M groups per GPU, the three voter-count buckets in one "
@@ -120,7 +124,7 @@ WORKLOADS = {
 # single-GPU commit config and the north star's 5-voter bar
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
-                  "c4,c4t,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
+                  "c4,c4t,c4t3,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
                   "cq,ing,ingo,w2,e2e,step,step5")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
@@ -140,8 +144,9 @@ def algo_bytes_per_group(w):
         # (the leader-row tile layout carries slot 0 as last_index: 8 bytes less)
         return (8 * (n - 1 if w.get("lead") else n) + 24 + {0: 8, 1: 16, 2: 2, 3: 12}[w["form"]]
                 + extra_n)
-    # ack, granted, rejected (+ n unless uniform) u8 each in; confirmed bit + 2-bit outcome out
-    return (3 if w.get("uniform") else 4) + 3 / 8
+    # ack, granted, rejected (+ n unless uniform or packed into the 3-byte tiles) u8 each in;
+    # confirmed bit + 2-bit outcome out
+    return (3 if w.get("uniform") or w.get("tiled3") else 4) + 3 / 8
 
 
 def decisions_per_group(w):
@@ -285,7 +290,14 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             conf = ctx.empty(hq.words64(G), np.uint64)
             outc = ctx.empty(hq.words32(G), np.uint64)
             tiles = None
-            if w.get("tiled"):
+            if w.get("tiled3"):
+                tiles = ctx.empty(hq.bits_tiles(G) * 3 * hq.HQ_BITS_TILE_GROUPS, np.uint8)
+                ctx.tile_bits3_dev(G, *arrs, 0, tiles)
+                ctx.sync()
+                for a in arrs:
+                    ctx.free(a)
+                arrs = None
+            elif w.get("tiled"):
                 pern = not w.get("uniform")
                 tiles = ctx.empty(hq.bits_tile_bytes(G, pern), np.uint8)
                 ctx.tile_bits_dev(G, *arrs[:3], arrs[3] if pern else None, tiles)
@@ -368,6 +380,9 @@ def run_gpu(w, steps, warmup, d: Dist):
         def run(idx):
             for i in idx:
                 arrs, conf, outc, tiles = sets[i % nsets]
+                if w.get("tiled3"):
+                    ctx.readindex_vote_tiles3_dev(G, tiles, conf, outc)
+                    continue
                 if tiles is not None:
                     uni = w.get("uniform", False)
                     ctx.readindex_vote_tiles_dev(G, tiles, not uni, w["n"] if uni else 0, conf,

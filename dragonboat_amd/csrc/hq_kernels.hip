@@ -906,6 +906,95 @@ __global__ __launch_bounds__(BLK) void k_bits(const BitsK a) {
     }
 }
 
+// ---- 3-byte bitmap tiles (hq_readindex_vote_tiles3_dev) -------------------------------------
+// The leader's / candidate's own slot 0 carries no information: it never acks its own ReadIndex
+// ctx (readindex.go:84 counts it as the +1), always grants its own vote (campaign, raft.go:1093)
+// and never rejects it. So each of the three rows keeps the 7 bits of slots 1..7 (bit k = slot
+// k + 1) and its bit 7 holds one bit of n - 1: ack row bit 0 of n - 1, granted row bit 1,
+// rejected row bit 2. 3 bytes per group instead of 4 (rows [n] ack granted rejected), n always
+// in [1, 8]: nothing to fall back on.
+template <bool FULL>
+__device__ __forceinline__ void bits3_slot(const BitsK &a, uint64_t g, const V16 *rows) {
+    const uint64_t slot = g >> 4;
+    uint32_t conf = 0, outc = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t inr = kB80;
+        if constexpr (!FULL) {
+            const uint64_t left = g < a.G ? a.G - g : 0;
+            inr = left >= (uint64_t)(4 * w + 4) ? kB80
+                  : left <= (uint64_t)(4 * w)   ? 0u
+                                                : (kB80 >> (8 * (4 - (uint32_t)(left - 4 * w))));
+        }
+        const uint32_t A = rows[0].w[w], Gr = rows[1].w[w], Rj = rows[2].w[w];
+        const uint32_t nm1 = ((A >> 7) & kB01) | ((Gr >> 6) & 0x02020202u) | ((Rj >> 5) & 0x04040404u);
+        const uint32_t mask = mask_n(nm1);                 // the other voters' bits 0 .. n-2
+        const uint32_t half = ((nm1 + kB01) >> 1) & 0x7F7F7F7Fu;   // n/2 = quorum - 1
+        // readindex.go:84: acks + 1 >= quorum <=> acks >= n/2
+        conf |= pack4(ge_bytes(popc_bytes(A & mask), half) & inr) << (4 * w);
+        // handleVoteResp: granted (self included) / rejected (first response wins) >= quorum
+        const uint32_t gm = Gr & mask, rm = Rj & mask & ~gm;
+        const uint32_t lead = ge_bytes(popc_bytes(gm), half) & inr;          // gm + 1 >= n/2 + 1
+        const uint32_t foll = ge_bytes(popc_bytes(rm), half + kB01) & inr & ~lead;
+        outc |= pack4x2(inr & ~lead & ~foll, lead) << (8 * w);
+    }
+    if (FULL || slot < a.n16) reinterpret_cast<uint16_t *>(a.confirmed)[slot] = conf;
+    if (FULL || slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
+}
+
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_bits3(const BitsK a) {
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (BLK / 64);
+    const uint64_t slots = a.n16o > a.n16 ? a.n16o : a.n16;
+    const uint64_t ntiles = (slots * 16 + 1023) >> 10;
+    for (uint64_t t = wave; t < ntiles; t += nw) {
+        const uint8_t *base = a.tiles + t * (3 << 10) + lane * 16;
+        V16 rows[3];
+#pragma unroll
+        for (uint64_t r = 0; r < 3; ++r)
+            rows[r].w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + (r << 10)));
+        const uint64_t g = (t << 10) + lane * 16;
+        if ((t << 10) + 1024 <= a.G) bits3_slot<true>(a, g, rows);
+        else bits3_slot<false>(a, g, rows);
+    }
+}
+
+// columns -> 3-byte tiles: one thread per group; a group outside the contract (n not in
+// [1, 8], its own slot acked / not granted / rejected) gets a fallback bit and zero bytes
+__global__ __launch_bounds__(kBlock) void k_tile_bits3(uint64_t G, const uint8_t *nv, uint32_t nu,
+                                                       const uint8_t *ack, const uint8_t *gr,
+                                                       const uint8_t *rj, uint8_t *tiles,
+                                                       uint64_t *fallback) {
+    const uint64_t total = (G + 1023) / 1024 * 1024;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kBlock; g0 < total; g0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t g = g0 + threadIdx.x;
+        uint32_t A = 0, Gr = 0, Rj = 0;
+        bool bad = false;
+        if (g < G) {
+            const uint32_t n = nv ? nv[g] : nu;
+            const uint32_t a = ack[g], x = gr[g], r = rj[g];
+            bad = n < 1 || n > 8 || (a & 1) || !(x & 1) || (r & 1);
+            if (!bad) {
+                const uint32_t keep = (1u << n) - 2u, m = n - 1;   // slots 1 .. n-1
+                A = ((a & keep) >> 1) | ((m & 1) << 7);
+                Gr = ((x & keep) >> 1) | (((m >> 1) & 1) << 7);
+                Rj = ((r & keep) >> 1) | (((m >> 2) & 1) << 7);
+            }
+        }
+        if (g < total) {
+            uint8_t *row = tiles + (g >> 10) * (3 << 10) + (g & 1023);
+            row[0] = (uint8_t)A;
+            row[1024] = (uint8_t)Gr;
+            row[2048] = (uint8_t)Rj;
+        }
+        const uint64_t b = __ballot(bad);
+        if (fallback && (threadIdx.x & 63) == 0 && g < ((G + 63) & ~63ull)) fallback[g >> 6] = b;
+    }
+}
+
 // ---- synthetic inputs (recipe: DESIGN.md "Synthetic inputs"; CPU twin oracle/qgen.c) --------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -1620,6 +1709,44 @@ extern "C" int hq_readindex_vote_tiles_dev(hq_ctx *ctx, uint64_t G, const uint8_
     k.confirmed = confirmed;
     k.outcome = outcome;
     return launch_bits<kRI | kVOTE>(ctx, k, "hq_readindex_vote_tiles");
+}
+
+extern "C" int hq_readindex_vote_tiles3_dev(hq_ctx *ctx, uint64_t G, const uint8_t *tiles,
+                                            uint64_t *confirmed, uint64_t *outcome) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!tiles || !confirmed || !outcome || !hq::aligned16(tiles))
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_readindex_vote_tiles3: NULL argument or tiles not 16-byte aligned");
+    BitsK k = bits_args(G, nullptr, 0, nullptr);
+    k.tiles = tiles;
+    k.tile_rows = 3;
+    k.confirmed = confirmed;
+    k.outcome = outcome;
+    k.n16 = hq::words64(G) * 4;
+    k.n16o = hq::words32(G) * 2;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    const uint64_t ntiles = (G + 1023) / 1024;
+    hipLaunchKernelGGL(k_bits3<256>, dim3(grid_for(ntiles * 64, 256)), dim3(256), 0, ctx->stream,
+                       k);
+    return hq::post_launch(ctx, "hq_readindex_vote_tiles3");
+}
+
+extern "C" int hq_tile_bits3_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,
+                                 const uint8_t *granted, const uint8_t *rejected,
+                                 const uint8_t *n_voting, uint32_t n_uniform, uint8_t *tiles,
+                                 uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!ack || !granted || !rejected || !tiles)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_bits3: NULL argument");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_bits3, dim3(grid_for((G + 1023) / 1024 * 1024)), dim3(kBlock), 0,
+                       ctx->stream, G, n_voting, n_uniform, ack, granted, rejected, tiles,
+                       fallback);
+    return hq::post_launch(ctx, "k_tile_bits3");
 }
 
 namespace {

@@ -276,3 +276,35 @@ extern "C" int hq_tile_bits_host(uint64_t G, const uint8_t *ack, const uint8_t *
     }
     return HQ_OK;
 }
+
+// Bitmap columns -> 3-byte tiles on the host (the twin of k_tile_bits3): rows ack, granted,
+// rejected of 1024 groups, bits of slots 1..7 in bits 0..6 and one bit of n - 1 in bit 7
+// (include/hipquorum.h hq_readindex_vote_tiles3_dev). Groups outside the contract get a fallback
+// bit and zero bytes.
+extern "C" int hq_tile_bits3_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                                  const uint8_t *rejected, const uint8_t *n_voting,
+                                  uint32_t n_uniform, uint8_t *tiles, uint64_t *fallback) {
+    if (G && (!ack || !granted || !rejected || !tiles)) return HQ_E_INVAL;
+    const uint64_t total = (G + 1023) / 1024 * 1024;
+    if (fallback) std::memset(fallback, 0, ((G + 63) / 64) * 8);
+    for (uint64_t g = 0; g < total; ++g) {
+        uint32_t A = 0, Gr = 0, Rj = 0;
+        if (g < G) {
+            const uint32_t n = n_voting ? n_voting[g] : n_uniform;
+            const uint32_t a = ack[g], x = granted[g], r = rejected[g];
+            if (n < 1 || n > 8 || (a & 1) || !(x & 1) || (r & 1)) {
+                if (fallback) set_bit(fallback, g);
+            } else {
+                const uint32_t keep = (1u << n) - 2u, m = n - 1;
+                A = ((a & keep) >> 1) | ((m & 1) << 7);
+                Gr = ((x & keep) >> 1) | (((m >> 1) & 1) << 7);
+                Rj = ((r & keep) >> 1) | (((m >> 2) & 1) << 7);
+            }
+        }
+        uint8_t *row = tiles + (g >> 10) * 3072 + (g & 1023);
+        row[0] = (uint8_t)A;
+        row[1024] = (uint8_t)Gr;
+        row[2048] = (uint8_t)Rj;
+    }
+    return HQ_OK;
+}

@@ -232,6 +232,11 @@ SIGNATURES = {
         [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp],
     ),
     "hq_tile_bits_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
+    "hq_readindex_vote_tiles3_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "hq_tile_bits3_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
+                                         ctypes.c_uint32, _vp, _vp]),
+    "hq_tile_bits3_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+                                          _vp, _vp]),
     "hq_tile_bits_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
     "hq_check_quorum_dev": (
         ctypes.c_int,
@@ -512,6 +517,15 @@ class Context:
         """hq_tile_bits_dev: bitmap columns cut into tiles (rows [n] ack granted rejected)."""
         self._check(lib.hq_tile_bits_dev(self.h, G, _p(ack), _p(granted), _p(rejected),
                                          _p(n_voting), _p(tiles)))
+
+    def readindex_vote_tiles3_dev(self, G, tiles, confirmed, outcome) -> None:
+        self._check(lib.hq_readindex_vote_tiles3_dev(self.h, G, _p(tiles), _p(confirmed),
+                                                     _p(outcome)))
+
+    def tile_bits3_dev(self, G, ack, granted, rejected, n_voting, n_uniform, tiles,
+                       fallback=None) -> None:
+        self._check(lib.hq_tile_bits3_dev(self.h, G, _p(ack), _p(granted), _p(rejected),
+                                          _p(n_voting), n_uniform, _p(tiles), _p(fallback)))
 
     def check_quorum_dev(self, G, active, n_voting, n_uniform, self_slot, has_quorum,
                          fallback=None) -> None:
@@ -838,6 +852,18 @@ def tile_bits_host(ack, granted, rejected, n_voting=None) -> np.ndarray:
     out = np.empty(bits_tile_bytes(G, n_voting is not None), np.uint8)
     _chk(lib.hq_tile_bits_host(G, *[_p(c) for c in cols], _p(out)), "hq_tile_bits_host")
     return out
+
+
+def tile_bits3_host(ack, granted, rejected, n_voting=None, n_uniform=0):
+    """hq_tile_bits3_host over host uint8 columns: (tiles uint8 array, fallback words)."""
+    G = len(ack)
+    cols = [np.ascontiguousarray(a, np.uint8) if a is not None else None
+            for a in (ack, granted, rejected, n_voting)]
+    out = np.empty(bits_tiles(G) * 3 * HQ_BITS_TILE_GROUPS, np.uint8)
+    fb = np.zeros(words64(G), np.uint64)
+    _chk(lib.hq_tile_bits3_host(G, *[_p(c) for c in cols], n_uniform, _p(out), _p(fb)),
+         "hq_tile_bits3_host")
+    return out, fb
 
 
 def words32(G: int) -> int:

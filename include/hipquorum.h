@@ -400,6 +400,27 @@ int hq_tile_bits_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
                       const uint8_t *rejected, const uint8_t *n_voting, uint8_t *tiles);
 
 /*
+ * The same fused pass over 3-byte tiles: the leader's / candidate's own slot 0 carries no
+ * information (it never acks its own ctx — readindex.go:84 counts it as the +1 — always grants
+ * its own vote, campaign raft.go:1093, and never rejects it), so each group is 3 bytes instead
+ * of 4: 1024-group tiles of rows [ack] [granted] [rejected], byte bits 0..6 = slots 1..7 and
+ * bit 7 = one bit of n - 1 (ack row: bit 0, granted row: bit 1, rejected row: bit 2), n in
+ * [1, 8]. Tile t starts at tiles + t * 3072. Same decisions as hq_readindex_vote_dev on groups
+ * whose slot 0 is not acked, granted and not rejected; the packers give every other group (and
+ * n outside [1, 8]) a fallback bit and zero bytes, and its decision must be ignored.
+ */
+int hq_readindex_vote_tiles3_dev(hq_ctx *ctx, uint64_t G, const uint8_t *tiles,
+                                 uint64_t *confirmed, uint64_t *outcome);
+/* Columns (n_voting, or n_uniform when NULL) -> 3-byte tiles (hq_bits_tiles(G) * 3072 bytes,
+ * padding zeroed); fallback (may be NULL) receives the contract violations. */
+int hq_tile_bits3_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                      const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
+                      uint8_t *tiles, uint64_t *fallback);
+int hq_tile_bits3_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                       const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
+                       uint8_t *tiles, uint64_t *fallback);
+
+/*
  * CheckQuorum (raft.go:380-390): has_quorum bit = popcount(active[g] | 1 << self_slot) >= q,
  * then every active flag is reset (remote.go:196-198): active[g] is written back as 0.
  * self_slot is the leader's slot (the packer puts the leader in slot 0).
