@@ -48,6 +48,11 @@ tools/lib_iv%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSR
 	@mkdir -p tools/lib_iv$*
 	$(HIPCC) $(HIPFLAGS) -DHQ_INGEST_V=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp
 
+# tuning variants: tiles per wave of the 3-byte bitmap kernel
+tools/lib_b3tpw%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(DEPS)
+	@mkdir -p tools/lib_b3tpw$*
+	$(HIPCC) $(HIPFLAGS) -DHQ_BITS3_TPW=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp
+
 variants: tools/lib_vec2/libhipquorum.so tools/lib_b512/libhipquorum.so
 
 clean:

@@ -942,6 +942,14 @@ __device__ __forceinline__ void bits3_slot(const BitsK &a, uint64_t g, const V16
     if (FULL || slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
 }
 
+// TPW tiles per wave and iteration, every row load of them issued before the first decision
+// (HQ_BITS3_TPW: 2 took 12.6-12.7 vs 13.4-13.6 us per 16M-group launch on one box, 4 no
+// better than 1; tools/ab_libs.sh with tools/lib_b3tpw{2,4})
+#ifndef HQ_BITS3_TPW
+#define HQ_BITS3_TPW 2
+#endif
+constexpr int kB3TPW = HQ_BITS3_TPW;
+
 template <int BLK>
 __global__ __launch_bounds__(BLK) void k_bits3(const BitsK a) {
     const uint64_t lane = threadIdx.x & 63;
@@ -950,15 +958,25 @@ __global__ __launch_bounds__(BLK) void k_bits3(const BitsK a) {
     const uint64_t nw = (uint64_t)gridDim.x * (BLK / 64);
     const uint64_t slots = a.n16o > a.n16 ? a.n16o : a.n16;
     const uint64_t ntiles = (slots * 16 + 1023) >> 10;
-    for (uint64_t t = wave; t < ntiles; t += nw) {
-        const uint8_t *base = a.tiles + t * (3 << 10) + lane * 16;
-        V16 rows[3];
+    for (uint64_t t0 = wave * kB3TPW; t0 < ntiles; t0 += nw * kB3TPW) {
+        V16 rows[kB3TPW][3];
 #pragma unroll
-        for (uint64_t r = 0; r < 3; ++r)
-            rows[r].w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + (r << 10)));
-        const uint64_t g = (t << 10) + lane * 16;
-        if ((t << 10) + 1024 <= a.G) bits3_slot<true>(a, g, rows);
-        else bits3_slot<false>(a, g, rows);
+        for (int j = 0; j < kB3TPW; ++j) {
+            const uint64_t t = t0 + j < ntiles ? t0 + j : t0;   // wave-uniform
+            const uint8_t *base = a.tiles + t * (3 << 10) + lane * 16;
+#pragma unroll
+            for (uint64_t r = 0; r < 3; ++r)
+                rows[j][r].w = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4 *>(base + (r << 10)));
+        }
+#pragma unroll
+        for (int j = 0; j < kB3TPW; ++j) {
+            const uint64_t t = t0 + j;
+            if (t >= ntiles) break;
+            const uint64_t g = (t << 10) + lane * 16;
+            if ((t << 10) + 1024 <= a.G) bits3_slot<true>(a, g, rows[j]);
+            else bits3_slot<false>(a, g, rows[j]);
+        }
     }
 }
 
@@ -1728,8 +1746,8 @@ extern "C" int hq_readindex_vote_tiles3_dev(hq_ctx *ctx, uint64_t G, const uint8
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     const uint64_t ntiles = (G + 1023) / 1024;
-    hipLaunchKernelGGL(k_bits3<256>, dim3(grid_for(ntiles * 64, 256)), dim3(256), 0, ctx->stream,
-                       k);
+    hipLaunchKernelGGL(k_bits3<256>, dim3(grid_for((ntiles + kB3TPW - 1) / kB3TPW * 64, 256)),
+                       dim3(256), 0, ctx->stream, k);
     return hq::post_launch(ctx, "hq_readindex_vote_tiles3");
 }
 
