@@ -1,0 +1,60 @@
+// hq_dstep.h — the device step engine of the step worker (hq_worker_open_ex with
+// HQ_WORKER_ON_DEVICE), shared between hq_worker.cpp (plain C++, the host side: state mirror,
+// validation, outputs) and hq_dstep.hip (the kernels). Internal to libhipquorum.so.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/hipquorum.h"
+
+// device-resident group state: one record per group handle
+struct hq_dgroup {
+    uint64_t cluster_id, node_id, term, committed, last, term_start;
+    uint32_t mem;                     // first member in the member pool
+    uint8_t n_members, n_voting, state, granted;
+    uint8_t rejected, flags, n_reads, pad0;
+    uint32_t pad1;
+};
+static_assert(sizeof(hq_dgroup) == 64, "one 64-byte record per group");
+
+struct hq_dmember {                   // pool order per group: self, remotes, witnesses, observers
+    uint64_t node_id, match;
+    uint8_t role, active, order, pad[5];
+};
+static_assert(sizeof(hq_dmember) == 24, "24-byte member records");
+
+struct hq_dread {                     // a pending ReadIndex (readStatus, readindex.go:21-26)
+    uint64_t index, from, low, high;
+    uint8_t confirmed, pad[7];        // voting slots that acknowledged it
+};
+static_assert(sizeof(hq_dread) == 40, "40-byte read records");
+
+constexpr uint32_t kDReads = 8;       // pending ReadIndex ctxs per group
+constexpr uint32_t kDMembers = 16;    // members per group on the device path
+constexpr uint8_t kDSuspended = 1;
+
+struct hq_dstep;                      // device buffers of one worker
+
+struct hq_dstep_out {                 // the lists of one step, in input group order
+    std::vector<hq_commit_event> commits;
+    std::vector<hq_ready_to_read> ready;
+    std::vector<hq_read_index_resp> resps;
+    std::vector<hq_state_change> states;
+    std::vector<hq_dropped_read> dropped;
+    std::vector<uint64_t> deferred;
+    std::vector<uint64_t> fallback;
+    uint64_t decisions = 0;
+    uint64_t h2d_ns = 0, kernel_ns = 0, d2h_ns = 0;
+};
+
+int hq_dstep_open(hq_ctx *ctx, hq_dstep **out);
+void hq_dstep_close(hq_dstep *d);
+// copy group records [g0, g0 + ng) with their reads (kDReads per group) and member records
+// [m0, m0 + nm) to the device, growing the device arrays to hold them
+int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, const hq_dread *r,
+                 uint64_t m0, uint64_t nm, const hq_dmember *m);
+// copy the first ng group records (with their reads) and nm member records back
+int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t nm, hq_dmember *m);
+// one step over the device state (the input is already validated)
+int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out);

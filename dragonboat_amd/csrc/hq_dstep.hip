@@ -1,0 +1,571 @@
+// hq_dstep.hip — the step worker's device engine (hq_worker_open_ex, HQ_WORKER_ON_DEVICE): the
+// whole quorum side of execEngine.processSteps / node.handleEvents (execengine.go:923-1000,
+// node.go:1113-1157) for many Raft groups in one launch, their state resident in HBM.
+//
+// One thread owns one group of the step and takes its events in order, exactly as the reference
+// takes a node's queue one message at a time: Peer.Handle's membership filter (peer.go:186-198),
+// onMessageTermNotMatched (raft.go:1416-1452), remote.tryUpdate + tryCommit per ReplicateResp
+// (remote.go:123-133, raft.go:888-909, 1671-1700), the confirmed-set insert and readIndex.confirm
+// per HeartbeatResp (readindex.go:77-116, raft.go:1702-1760), handleLeaderReadIndex
+// (raft.go:1636-1669), the first-wins vote tally (raft.go:1062-1080, 1968-1985), CheckQuorum
+// (raft.go:380-390, 1582-1588), campaign (raft.go:1082-1117), appendEntries (raft.go:911-922)
+// and the state transitions (raft.go:949-1010). Every decision is taken at the event that
+// triggers it, so no event waits for another's decision and a step is one launch, whatever the
+// events (the host worker cuts runs at such barriers and needs several passes).
+//
+// The outputs are lists whose lengths are not known in advance: the kernel runs twice over the
+// same state, first counting each group's records (on a private copy of the state), then, after
+// an exclusive scan of the counts, writing every record at its place — in input group order, as
+// the host worker lists them — and writing the new state back.
+#include <algorithm>
+#include <chrono>
+#include <new>
+
+#include <hipcub/hipcub.hpp>
+
+#include "hq_dstep.h"
+#include "hq_internal.h"
+
+namespace {
+
+enum List { kCommits, kReady, kResps, kStates, kDropped, kDeferred, kFallback, kDecisions,
+            kLists };
+
+struct StepK {
+    hq_dgroup *groups;
+    hq_dmember *members;
+    hq_dread *reads;
+    uint64_t n;                   // groups listed in this step
+    const uint32_t *handles;
+    const uint64_t *offsets;
+    const hq_event *events;
+    uint32_t *counts;             // [kLists][n] (+1): pass A output
+    const uint32_t *scan;         // exclusive scan of counts: pass B input
+    hq_commit_event *commits;
+    hq_ready_to_read *ready;
+    hq_read_index_resp *resps;
+    hq_state_change *states;
+    hq_dropped_read *dropped;
+    uint64_t *deferred;
+    uint64_t *fallback;
+};
+
+__device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
+    return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
+           t == HQ_MSG_HEARTBEAT_RESP || t == 20 || t == 8 || t == 9;
+}
+
+// One group's state and its output cursor. WRITE = false: counting pass on a private copy;
+// WRITE = true: the same sequence writing records and, at the end, the new state.
+template <bool WRITE>
+struct Engine {
+    const StepK &a;
+    uint64_t i;                   // position of the group in the step's list
+    hq_dgroup g;
+    const hq_dmember *gm;         // the group's member records (node ids and roles read-only)
+    uint64_t match[kDMembers];
+    uint32_t active;              // bit s = member s active
+    hq_dread rd[kDReads];
+    uint32_t cnt[kLists];
+    uint32_t base[kLists];
+
+    __device__ Engine(const StepK &k, uint64_t idx, uint32_t h) : a(k), i(idx) {
+        g = k.groups[h];
+        gm = k.members + g.mem;
+        active = 0;
+        for (uint32_t s = 0; s < g.n_members; ++s) {
+            match[s] = gm[s].match;
+            active |= (uint32_t)(gm[s].active != 0) << s;
+        }
+        for (uint32_t r = 0; r < g.n_reads; ++r) rd[r] = k.reads[(uint64_t)h * kDReads + r];
+        for (int l = 0; l < kLists; ++l) {
+            cnt[l] = 0;
+            base[l] = WRITE ? k.scan[(uint64_t)l * k.n + idx] - k.scan[(uint64_t)l * k.n] : 0;
+        }
+    }
+
+    __device__ uint32_t quorum() const { return g.n_voting / 2 + 1; }   // raft.go:372-374
+    __device__ int member_of(uint64_t id) const {
+        for (uint32_t s = 0; s < g.n_members; ++s)
+            if (gm[s].node_id == id) return (int)s;
+        return -1;
+    }
+    __device__ uint32_t slot(int l) { return base[l] + cnt[l]++; }
+
+    // -- outputs ----------------------------------------------------------------------------
+    __device__ void ready(uint64_t index, uint64_t low, uint64_t high) {
+        const uint32_t p = slot(kReady);
+        if (WRITE) a.ready[p] = hq_ready_to_read{g.cluster_id, index, low, high};
+    }
+    __device__ void resp(uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
+        const uint32_t p = slot(kResps);
+        if (WRITE) a.resps[p] = hq_read_index_resp{g.cluster_id, to, index, hint, high};
+    }
+    __device__ void state_change(uint32_t reason) {
+        const uint32_t p = slot(kStates);
+        if (WRITE) a.states[p] = hq_state_change{g.cluster_id, g.term, g.state, reason};
+    }
+    __device__ void dropped(uint64_t low, uint64_t high, uint64_t from, uint32_t reason) {
+        const uint32_t p = slot(kDropped);
+        if (WRITE) a.dropped[p] = hq_dropped_read{g.cluster_id, low, high, from, reason, 0};
+    }
+    __device__ void defer(uint64_t e) {
+        const uint32_t p = slot(kDeferred);
+        if (WRITE) a.deferred[p] = e;
+    }
+
+    // -- reference state transitions (raft.go:949-1010) --------------------------------------
+    __device__ void reset(uint64_t term) {
+        g.term = term;
+        g.granted = g.rejected = 0;
+        g.n_reads = 0;                                   // r.readIndex = newReadIndex()
+        for (uint32_t s = 0; s < g.n_members; ++s)       // resetRemotes/Observers/Witnesses
+            match[s] = gm[s].node_id == g.node_id ? g.last : 0;
+        active = 0;
+    }
+    __device__ void become_follower(uint64_t term, uint32_t reason) {
+        g.state = HQ_STATE_FOLLOWER;
+        reset(term);
+        state_change(reason);
+    }
+    __device__ void become_leader() {
+        g.state = HQ_STATE_LEADER;
+        reset(g.term);
+        state_change(HQ_REASON_VOTE);
+        // the no-op of p72: the first entry of the new term; the node's own remote follows it
+        g.term_start = g.last + 1;
+        g.last += 1;
+        match[0] = g.last;
+        if (g.n_voting == 1) try_commit();               // appendEntries: single-node tryCommit
+    }
+
+    // raft.tryCommit (raft.go:888-909): the quorum-th largest match of the voting members, then
+    // entryLog.tryCommit (logentry.go:378-393) with term(q) == term <=> term_start <= q <= last
+    // (the leader's entries carry its term and terms never decrease, entryutils.go:44-47)
+    __device__ void try_commit() {
+        cnt[kDecisions]++;
+        const uint32_t n = g.n_voting, q = quorum();
+        uint64_t best = 0;
+        for (uint32_t s = 0; s < n; ++s) {
+            uint32_t ge = 0;
+            for (uint32_t t = 0; t < n; ++t) ge += match[t] >= match[s];
+            if (ge >= q && match[s] > best) best = match[s];
+        }
+        if (best > g.committed && best >= g.term_start && best <= g.last)
+            g.committed = best;                          // commitTo (logentry.go:323-332)
+    }
+
+    // handleLeaderReadIndex (raft.go:1636-1669) and readIndex.addRequest (readindex.go:43-67);
+    // returns false for the worker's fallback contract (see include/hipquorum.h)
+    __device__ bool read_index(uint64_t from, uint64_t low, uint64_t high, uint64_t e) {
+        if (g.state != HQ_STATE_LEADER) {
+            defer(e);                                    // forwarded / dropped (raft.go:1875, 1937)
+            return true;
+        }
+        const int fm = member_of(from);
+        const uint32_t role = fm >= 0 ? gm[fm].role : 0xFF;
+        if (role == HQ_ROLE_WITNESS) {
+            dropped(low, high, from, HQ_DROP_WITNESS);
+            return true;
+        }
+        if (g.n_voting == 1) {                           // isSingleNodeQuorum
+            ready(g.committed, low, high);
+            if (from != g.node_id && role == HQ_ROLE_OBSERVER) resp(from, g.committed, low, high);
+            return true;
+        }
+        // hasCommittedEntryAtCurrentTerm (raft.go:1612-1621)
+        if (!(g.committed >= g.term_start && g.committed <= g.last)) {
+            dropped(low, high, from, HQ_DROP_NOT_READY);
+            return true;
+        }
+        for (uint32_t k = 0; k < g.n_reads; ++k)
+            if (rd[k].low == low && rd[k].high == high) return true;   // already pending
+        if (g.n_reads && g.committed < rd[g.n_reads - 1].index) return false;  // reference panics
+        if (g.n_reads >= kDReads) return false;
+        hq_dread &r = rd[g.n_reads++];
+        r = hq_dread{};
+        r.index = g.committed;
+        r.from = from;
+        r.low = low;
+        r.high = high;
+        return true;
+    }
+
+    // readIndex.confirm (readindex.go:77-116) + handleReadIndexLeaderConfirmation
+    // (raft.go:1740-1760) for the ack of voting slot mi
+    __device__ bool confirm(uint64_t hint, uint64_t high, int mi) {
+        uint32_t k = 0;
+        while (k < g.n_reads && !(rd[k].low == hint && rd[k].high == high)) ++k;
+        if (k == g.n_reads) return true;                 // not pending
+        if (mi >= (int)g.n_voting) return false;         // an observer acking a ctx
+        rd[k].confirmed |= (uint8_t)(1u << mi);          // p.confirmed[from] = struct{}{}
+        cnt[kDecisions]++;
+        if ((uint32_t)__popc(rd[k].confirmed) + 1 < quorum()) return true;
+        const uint64_t index = rd[k].index;              // the rewrite of readindex.go:97-105
+        for (uint32_t r = 0; r <= k; ++r) {
+            if (rd[r].from == 0 || rd[r].from == g.node_id) ready(index, rd[r].low, rd[r].high);
+            else resp(rd[r].from, index, hint, high);
+        }
+        for (uint32_t r = k + 1; r < g.n_reads; ++r) rd[r - k - 1] = rd[r];
+        g.n_reads -= (uint8_t)(k + 1);
+        return true;
+    }
+
+    // one event; false: the group leaves the device path at this event (fallback)
+    __device__ bool handle(const hq_event &ev, uint64_t e) {
+        switch (ev.kind) {
+        case HQ_EV_READ:
+            return read_index(0, ev.hint, ev.hint_high, e);
+        case HQ_EV_CHECK_QUORUM: {                       // raft.go:1582-1588, 380-390
+            if (g.state != HQ_STATE_LEADER) return true;
+            cnt[kDecisions]++;
+            const uint32_t vm = (1u << g.n_voting) - 1u;
+            const bool has = (uint32_t)__popc((active | 1u) & vm) >= quorum();
+            active &= ~vm;                               // setNotActive (remote.go:196-198)
+            if (!has) become_follower(g.term, HQ_REASON_CHECK_QUORUM);
+            return true;
+        }
+        case HQ_EV_ELECTION:                             // raft.go:1485-1515, campaign 1082-1117
+            if (g.state == HQ_STATE_LEADER) return true;
+            g.state = HQ_STATE_CANDIDATE;
+            reset(g.term + 1);
+            state_change(HQ_REASON_CAMPAIGN);
+            g.granted = 1;                               // the self vote
+            cnt[kDecisions]++;
+            if (g.n_voting == 1) become_leader();        // isSingleNodeQuorum
+            return true;
+        case HQ_EV_PROPOSE:                              // handleLeaderPropose -> appendEntries
+            if (g.state != HQ_STATE_LEADER) {
+                defer(e);                                // forwarded / dropped (raft.go:1845, 1932)
+                return true;
+            }
+            g.last += ev.log_index;
+            if (match[0] < g.last) match[0] = g.last;
+            if (g.n_voting == 1) try_commit();
+            return true;
+        case HQ_EV_MESSAGE:
+            break;
+        default:
+            return false;
+        }
+        const uint32_t type = ev.type;
+        if (type != HQ_MSG_REPLICATE_RESP && type != HQ_MSG_HEARTBEAT_RESP &&
+            type != HQ_MSG_REQUEST_VOTE_RESP && type != HQ_MSG_READ_INDEX)
+            return false;
+        const int mi = member_of(ev.from);
+        if (mi < 0 && is_response(type)) return true;    // Peer.Handle drop (peer.go:191-197)
+        if (ev.term != 0 && ev.term != g.term) {         // onMessageTermNotMatched
+            if (ev.term < g.term) return true;
+            become_follower(ev.term, HQ_REASON_HIGHER_TERM);
+        }
+        if (g.state == HQ_STATE_LEADER) {
+            switch (type) {
+            case HQ_MSG_REPLICATE_RESP:                  // handleLeaderReplicateResp
+                if (!ev.reject && match[mi] < ev.log_index) {
+                    if (ev.log_index > g.last) return false;   // a follower acks only what it got
+                    match[mi] = ev.log_index;            // remote.tryUpdate
+                    try_commit();
+                }
+                active |= 1u << mi;
+                return true;
+            case HQ_MSG_HEARTBEAT_RESP:                  // handleLeaderHeartbeatResp
+                if (ev.hint != 0 && !confirm(ev.hint, ev.hint_high, mi)) return false;
+                active |= 1u << mi;
+                return true;
+            case HQ_MSG_READ_INDEX:
+                return read_index(ev.from, ev.hint, ev.hint_high, e);
+            default:
+                return true;                             // RequestVoteResp: no leader handler
+            }
+        }
+        if (g.state == HQ_STATE_CANDIDATE && type == HQ_MSG_REQUEST_VOTE_RESP) {
+            if (mi >= (int)g.n_voting) return true;      // observer vote dropped (:1969-1972)
+            const uint8_t bit = (uint8_t)(1u << mi);
+            if (!((g.granted | g.rejected) & bit)) {     // first response wins (:1071-1073)
+                if (ev.reject) g.rejected |= bit;
+                else g.granted |= bit;
+            }
+            cnt[kDecisions]++;
+            const uint32_t q = quorum();
+            if ((uint32_t)__popc(g.granted) == q) become_leader();            // :1977-1980
+            else if ((uint32_t)__popc(g.rejected) == q)                      // :1981-1984
+                become_follower(g.term, HQ_REASON_VOTE);
+            return true;
+        }
+        if (type == HQ_MSG_READ_INDEX) return read_index(ev.from, ev.hint, ev.hint_high, e);
+        return true;                                     // no handler in this state
+    }
+
+    __device__ void run(uint64_t e0, uint64_t e1) {
+        const uint64_t committed0 = g.committed;
+        for (uint64_t e = e0; e < e1; ++e) {
+            if (g.flags & kDSuspended) {
+                defer(e);
+                continue;
+            }
+            const hq_event ev = a.events[e];
+            if (!handle(ev, e)) {                        // this event and the rest are deferred
+                g.flags |= kDSuspended;
+                const uint32_t p = slot(kFallback);
+                if (WRITE) a.fallback[p] = g.cluster_id;
+                defer(e);
+            }
+        }
+        if (g.committed != committed0) {
+            const uint32_t p = slot(kCommits);
+            if (WRITE) a.commits[p] = hq_commit_event{g.cluster_id, g.committed};
+        }
+    }
+
+    __device__ void store(uint32_t h) {
+        a.groups[h] = g;
+        hq_dmember *m = a.members + g.mem;
+        for (uint32_t s = 0; s < g.n_members; ++s) {
+            m[s].match = match[s];
+            m[s].active = (uint8_t)((active >> s) & 1);
+        }
+        for (uint32_t r = 0; r < g.n_reads; ++r) a.reads[(uint64_t)h * kDReads + r] = rd[r];
+    }
+};
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_step(const StepK a) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t h = a.handles[i];
+    Engine<WRITE> eng(a, i, h);
+    eng.run(a.offsets[i], a.offsets[i + 1]);
+    if (WRITE) {
+        eng.store(h);
+    } else {
+        for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
+    }
+}
+
+// the start of every list in the scanned counts, and the grand total
+__global__ void k_list_bases(const uint32_t *scan, uint64_t n, uint32_t *bases) {
+    const int l = threadIdx.x;
+    if (l <= kLists) bases[l] = scan[(uint64_t)l * n];
+}
+
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+}  // namespace
+
+struct hq_dstep {
+    hq_ctx *ctx = nullptr;
+    hq_dgroup *groups = nullptr;
+    hq_dread *reads = nullptr;
+    hq_dmember *members = nullptr;
+    uint64_t gcap = 0, mcap = 0;
+    // step staging
+    void *in = nullptr;
+    size_t in_cap = 0;
+    uint32_t *counts = nullptr, *scan = nullptr, *bases = nullptr;
+    size_t cnt_cap = 0;
+    void *scan_tmp = nullptr;
+    size_t scan_tmp_cap = 0;
+    void *out = nullptr;
+    size_t out_cap = 0;
+};
+
+namespace {
+
+int grow(hq_ctx *ctx, void **p, size_t *cap, size_t need, bool keep, const char *what) {
+    if (need <= *cap) return HQ_OK;
+    size_t want = need + need / 2;
+    void *n = nullptr;
+    int rc = hq::check_hip(ctx, hipMalloc(&n, want), what);
+    if (rc) return rc;
+    if (*p && keep) rc = hq::check_hip(ctx, hipMemcpyAsync(n, *p, *cap, hipMemcpyDeviceToDevice,
+                                                           ctx->stream), what);
+    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), what);
+    if (*p) (void)hipFree(*p);
+    *p = n;
+    *cap = want;
+    return rc;
+}
+
+}  // namespace
+
+int hq_dstep_open(hq_ctx *ctx, hq_dstep **out) {
+    *out = new (std::nothrow) hq_dstep();
+    if (!*out) return HQ_E_NOMEM;
+    (*out)->ctx = ctx;
+    return HQ_OK;
+}
+
+void hq_dstep_close(hq_dstep *d) {
+    if (!d) return;
+    (void)hipSetDevice(d->ctx->device);
+    (void)hipStreamSynchronize(d->ctx->stream);
+    for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, d->in,
+                    (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp, d->out})
+        if (p) (void)hipFree(p);
+    delete d;
+}
+
+int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, const hq_dread *r,
+                 uint64_t m0, uint64_t nm, const hq_dmember *m) {
+    hq_ctx *ctx = d->ctx;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    size_t gc = d->gcap * sizeof(hq_dgroup), rcap = d->gcap * kDReads * sizeof(hq_dread),
+           mc = d->mcap * sizeof(hq_dmember);
+    if (!rc && (g0 + ng) > d->gcap) {
+        rc = grow(ctx, reinterpret_cast<void **>(&d->groups), &gc, (g0 + ng) * sizeof(hq_dgroup),
+                  true, "hq_dstep groups");
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->reads), &rcap,
+                      (g0 + ng) * kDReads * sizeof(hq_dread), true, "hq_dstep reads");
+        if (!rc) d->gcap = std::min(gc / sizeof(hq_dgroup), rcap / (kDReads * sizeof(hq_dread)));
+    }
+    if (!rc && (m0 + nm) > d->mcap) {
+        rc = grow(ctx, reinterpret_cast<void **>(&d->members), &mc,
+                  (m0 + nm) * sizeof(hq_dmember), true, "hq_dstep members");
+        if (!rc) d->mcap = mc / sizeof(hq_dmember);
+    }
+    if (!rc && ng)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(d->groups + g0, g, ng * sizeof(hq_dgroup),
+                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
+    if (!rc && ng)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(d->reads + g0 * kDReads, r,
+                                               ng * kDReads * sizeof(hq_dread),
+                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
+    if (!rc && nm)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(d->members + m0, m, nm * sizeof(hq_dmember),
+                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
+    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep_put");
+    return rc;
+}
+
+int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t nm, hq_dmember *m) {
+    hq_ctx *ctx = d->ctx;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (!rc && ng)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(g, d->groups, ng * sizeof(hq_dgroup),
+                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
+    if (!rc && ng)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(r, d->reads, ng * kDReads * sizeof(hq_dread),
+                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
+    if (!rc && nm)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(m, d->members, nm * sizeof(hq_dmember),
+                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
+    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep_get");
+    return rc;
+}
+
+int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out) {
+    hq_ctx *ctx = d->ctx;
+    const uint64_t n = in->n_groups;
+    const uint64_t ne = n ? in->offsets[n] : 0;
+    if (n == 0) return HQ_OK;
+    const uint64_t t0 = now_ns();
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    // the step's input: handles, offsets and events, one device region
+    const size_t o_off = (n * 4 + 255) & ~size_t(255);
+    const size_t o_ev = o_off + (((n + 1) * 8 + 255) & ~size_t(255));
+    const size_t in_bytes = o_ev + ne * sizeof(hq_event);
+    if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
+    char *din = static_cast<char *>(d->in);
+    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(din, in->groups, n * 4, hipMemcpyHostToDevice,
+                                                    ctx->stream), "hq_dstep H2D");
+    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(din + o_off, in->offsets, (n + 1) * 8,
+                                                    hipMemcpyHostToDevice, ctx->stream), "hq_dstep H2D");
+    if (!rc && ne)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(din + o_ev, in->events, ne * sizeof(hq_event),
+                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep H2D");
+    // counts [kLists][n] + 1 (zero: the scan's last element is the grand total)
+    const size_t cn = (size_t)kLists * n + 1;
+    size_t cc = d->cnt_cap * 4, sc = d->cnt_cap * 4, bc = d->cnt_cap ? 64 : 0;
+    if (!rc && cn > d->cnt_cap) {
+        rc = grow(ctx, reinterpret_cast<void **>(&d->counts), &cc, cn * 4, false, "hq_dstep counts");
+        if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->scan), &sc, cn * 4, false, "hq_dstep scan");
+        if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 64, false, "hq_dstep bases");
+        if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
+    }
+    size_t tmp = 0;
+    if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d->counts,
+                                                                       d->scan, cn, ctx->stream),
+                                "hipcub scan size");
+    if (!rc) rc = grow(ctx, &d->scan_tmp, &d->scan_tmp_cap, tmp, false, "hq_dstep scan tmp");
+    if (rc) return rc;
+    StepK k{};
+    k.groups = d->groups;
+    k.members = d->members;
+    k.reads = d->reads;
+    k.n = n;
+    k.handles = reinterpret_cast<const uint32_t *>(din);
+    k.offsets = reinterpret_cast<const uint64_t *>(din + o_off);
+    k.events = reinterpret_cast<const hq_event *>(din + o_ev);
+    k.counts = d->counts;
+    k.scan = d->scan;
+    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+    rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
+    if (!rc) rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_step<false>, grid, blk, 0, ctx->stream, k);
+    rc = hq::post_launch(ctx, "k_step<count>");
+    if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
+                                                                       d->scan, cn, ctx->stream),
+                                "hipcub scan");
+    if (!rc) {
+        hipLaunchKernelGGL(k_list_bases, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, d->bases);
+        rc = hq::check_hip(ctx, hipGetLastError(), "k_list_bases");
+    }
+    uint32_t bases[kLists + 1];
+    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(bases, d->bases, sizeof bases,
+                                                    hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
+    if (rc) return rc;
+    const uint64_t t1 = now_ns();
+    uint64_t len[kLists];
+    for (int l = 0; l < kLists; ++l) len[l] = bases[l + 1] - bases[l];
+    // the output lists in one device region
+    const size_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
+                                sizeof(hq_read_index_resp), sizeof(hq_state_change),
+                                sizeof(hq_dropped_read), 8, 8, 0};
+    size_t off[kLists], total = 0;
+    for (int l = 0; l < kLists; ++l) {
+        off[l] = total;
+        total += (len[l] * rec[l] + 255) & ~size_t(255);
+    }
+    rc = grow(ctx, &d->out, &d->out_cap, total + 256, false, "hq_dstep output");
+    if (rc) return rc;
+    char *o = static_cast<char *>(d->out);
+    k.commits = reinterpret_cast<hq_commit_event *>(o + off[kCommits]);
+    k.ready = reinterpret_cast<hq_ready_to_read *>(o + off[kReady]);
+    k.resps = reinterpret_cast<hq_read_index_resp *>(o + off[kResps]);
+    k.states = reinterpret_cast<hq_state_change *>(o + off[kStates]);
+    k.dropped = reinterpret_cast<hq_dropped_read *>(o + off[kDropped]);
+    k.deferred = reinterpret_cast<uint64_t *>(o + off[kDeferred]);
+    k.fallback = reinterpret_cast<uint64_t *>(o + off[kFallback]);
+    rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_step<true>, grid, blk, 0, ctx->stream, k);
+    rc = hq::post_launch(ctx, "k_step<write>");
+    out->commits.resize(len[kCommits]);
+    out->ready.resize(len[kReady]);
+    out->resps.resize(len[kResps]);
+    out->states.resize(len[kStates]);
+    out->dropped.resize(len[kDropped]);
+    out->deferred.resize(len[kDeferred]);
+    out->fallback.resize(len[kFallback]);
+    out->decisions = len[kDecisions];
+    void *dst[kLists - 1] = {out->commits.data(), out->ready.data(), out->resps.data(),
+                             out->states.data(), out->dropped.data(), out->deferred.data(),
+                             out->fallback.data()};
+    for (int l = 0; l < kLists - 1 && !rc; ++l)
+        if (len[l])
+            rc = hq::check_hip(ctx, hipMemcpyAsync(dst[l], o + off[l], len[l] * rec[l],
+                                                   hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
+    const uint64_t t2 = now_ns();
+    out->h2d_ns = 0;
+    out->kernel_ns = t1 - t0;
+    out->d2h_ns = t2 - t1;
+    return rc;
+}

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/hipquorum.h"
+#include "hq_dstep.h"
 
 namespace {
 
@@ -91,6 +92,15 @@ bool is_response_type(uint32_t t) {       // isResponseMessageType (internal/raf
 struct hq_worker {
     hq_ctx *ctx = nullptr;
     uint32_t n_max = 0;
+    // HQ_WORKER_ON_DEVICE: the group state lives on the GPU (hq_dstep.hip) and a step is one
+    // launch pair; the host records below are a mirror, refreshed from the device on demand
+    hq_dstep *dstep = nullptr;
+    bool host_stale = false;              // the device holds newer state than the mirror
+    uint64_t dev_groups = 0, dev_members = 0;   // records already on the device
+    std::vector<uint32_t> dirty;          // handles changed on the host since the last upload
+    std::vector<uint64_t> stamp;          // step stamp per handle (a group listed twice)
+    uint64_t step_no = 0;
+    hq_dstep_out dout;
     std::string err;
     std::vector<Group> groups;
     std::vector<Member> pool;
@@ -147,6 +157,11 @@ struct hq_worker {
         g.rq = kNone;
     }
     int reserve(size_t bytes);
+    // device mode
+    void to_device_record(const Group &g, hq_dgroup &d, hq_dread *r) const;
+    int sync_to_device();
+    int sync_from_device();
+    int step_on_device(const hq_step_input *in, hq_step_output *out);
     int load_group(Group &g, const hq_worker_group *src, const hq_member *m, bool fresh);
     int step(const hq_step_input *in, hq_step_output *out);
     Verdict handle(Group &g, const hq_event &e, uint64_t ei);
@@ -181,6 +196,8 @@ int hq_worker::load_group(Group &g, const hq_worker_group *src, const hq_member 
     }
     if (self < 0) return fail(HQ_E_INVAL, "the node is not one of the group's remotes");
     if (n_voting > (int)n_max) return fail(HQ_E_INVAL, "more voting members than n_max");
+    if (dstep && n > kDMembers)
+        return fail(HQ_E_INVAL, "more than 16 members on the device path (HQ_WORKER_ON_DEVICE)");
     if (fresh || g.mem_cap < n) {
         g.mem = (uint32_t)pool.size();
         g.mem_cap = (uint8_t)n;
@@ -731,11 +748,185 @@ int hq_worker::step(const hq_step_input *inp, hq_step_output *out) {
     return HQ_OK;
 }
 
+// ------------------------------------------------------------------------------ device mode ---
+void hq_worker::to_device_record(const Group &g, hq_dgroup &d, hq_dread *r) const {
+    d = hq_dgroup{};
+    d.cluster_id = g.cluster_id;
+    d.node_id = g.node_id;
+    d.term = g.term;
+    d.committed = g.committed;
+    d.last = g.last;
+    d.term_start = g.term_start;
+    d.mem = g.mem;
+    d.n_members = g.n_members;
+    d.n_voting = g.n_voting;
+    d.state = g.state;
+    d.granted = g.granted;
+    d.rejected = g.rejected;
+    d.flags = g.has(kSuspended) ? kDSuspended : 0;
+    const ReadQueue *q = g.rq == kNone ? nullptr : &rqs[g.rq];
+    d.n_reads = q ? (uint8_t)q->n : 0;
+    for (uint32_t k = 0; k < kDReads; ++k) {
+        r[k] = hq_dread{};
+        if (q && k < q->n) {
+            const ReadStatus &s = q->r[k];
+            r[k].index = s.index;
+            r[k].from = s.from;
+            r[k].low = s.low;
+            r[k].high = s.high;
+            uint8_t c = s.confirmed;
+            for (uint32_t v = 0; v < HQ_MAX_VOTERS; ++v)
+                if (s.ord[v] != kNoAck) c |= (uint8_t)(1u << v);
+            r[k].confirmed = c;
+        }
+    }
+}
+
+// new groups (and their members) in one upload; groups changed by set_group one by one
+int hq_worker::sync_to_device() {
+    const uint64_t G = groups.size();
+    if (dev_groups < G || dev_members < pool.size()) {
+        const uint64_t ng = G - dev_groups, nm = pool.size() - dev_members;
+        std::vector<hq_dgroup> dg(ng);
+        std::vector<hq_dread> dr(ng * kDReads);
+        for (uint64_t i = 0; i < ng; ++i)
+            to_device_record(groups[dev_groups + i], dg[i], dr.data() + i * kDReads);
+        std::vector<hq_dmember> dm(nm);
+        for (uint64_t i = 0; i < nm; ++i) {
+            const Member &m = pool[dev_members + i];
+            dm[i] = hq_dmember{m.node_id, m.match, m.role, m.active, m.order, {0, 0, 0, 0, 0}};
+        }
+        int rc = hq(hq_dstep_put(dstep, dev_groups, ng, dg.data(), dr.data(), dev_members, nm,
+                                 dm.data()), "hq_dstep_put");
+        if (rc) return rc;
+        dev_groups = G;
+        dev_members = pool.size();
+    }
+    for (uint32_t h : dirty) {
+        const Group &g = groups[h];
+        hq_dgroup dg;
+        hq_dread dr[kDReads];
+        to_device_record(g, dg, dr);
+        std::vector<hq_dmember> dm(g.n_members);
+        for (uint32_t i = 0; i < g.n_members; ++i) {
+            const Member &m = pool[g.mem + i];
+            dm[i] = hq_dmember{m.node_id, m.match, m.role, m.active, m.order, {0, 0, 0, 0, 0}};
+        }
+        int rc = hq(hq_dstep_put(dstep, h, 1, &dg, dr, g.mem, g.n_members, dm.data()),
+                    "hq_dstep_put");
+        if (rc) return rc;
+    }
+    dirty.clear();
+    return HQ_OK;
+}
+
+// the whole device state back into the host records
+int hq_worker::sync_from_device() {
+    if (!host_stale) return HQ_OK;
+    const uint64_t G = dev_groups, M = dev_members;
+    std::vector<hq_dgroup> dg(G);
+    std::vector<hq_dread> dr(G * kDReads);
+    std::vector<hq_dmember> dm(M);
+    int rc = hq(hq_dstep_get(dstep, G, dg.data(), dr.data(), M, dm.data()), "hq_dstep_get");
+    if (rc) return rc;
+    for (uint64_t h = 0; h < G; ++h) {
+        Group &g = groups[h];
+        const hq_dgroup &d = dg[h];
+        g.term = d.term;
+        g.committed = d.committed;
+        g.last = d.last;
+        g.term_start = d.term_start;
+        g.state = d.state;
+        g.granted = d.granted;
+        g.rejected = d.rejected;
+        if (d.flags & kDSuspended) g.set(kSuspended);
+        else g.clear(kSuspended);
+        if (d.n_reads == 0) {
+            rq_release(g);
+        } else {
+            if (g.rq == kNone) g.rq = rq_alloc();
+            ReadQueue &q = rqs[g.rq];
+            q.n = d.n_reads;
+            for (uint32_t k = 0; k < q.n; ++k) {
+                const hq_dread &r = dr[h * kDReads + k];
+                ReadStatus &s = q.r[k];
+                s.index = r.index;
+                s.from = r.from;
+                s.low = r.low;
+                s.high = r.high;
+                s.confirmed = r.confirmed;
+                std::fill(std::begin(s.ord), std::end(s.ord), kNoAck);
+            }
+        }
+    }
+    for (uint64_t i = 0; i < M; ++i) {
+        pool[i].match = dm[i].match;
+        pool[i].active = dm[i].active;
+    }
+    host_stale = false;
+    return HQ_OK;
+}
+
+int hq_worker::step_on_device(const hq_step_input *inp, hq_step_output *out) {
+    const uint64_t t0 = now_ns();
+    if (stamp.size() < groups.size()) stamp.resize(groups.size(), 0);
+    ++step_no;
+    for (uint64_t i = 0; i < inp->n_groups; ++i) {   // the host worker's input checks
+        const uint32_t gi = inp->groups[i];
+        if (gi >= groups.size()) return fail(HQ_E_INVAL, "hq_worker_step: unknown group handle");
+        if (inp->offsets[i + 1] < inp->offsets[i])
+            return fail(HQ_E_INVAL, "hq_worker_step: offsets decrease");
+        if (stamp[gi] == step_no) return fail(HQ_E_INVAL, "hq_worker_step: a group is listed twice");
+        stamp[gi] = step_no;
+    }
+    int rc = sync_to_device();
+    if (rc) return rc;
+    const uint64_t t1 = now_ns();
+    rc = hq(hq_dstep_run(dstep, inp, &dout), "hq_dstep_run");
+    if (rc) return rc;
+    host_stale = true;
+    const uint64_t t2 = now_ns();
+    commits.swap(dout.commits);
+    ready.swap(dout.ready);
+    resps.swap(dout.resps);
+    states.swap(dout.states);
+    dropped.swap(dout.dropped);
+    deferred.swap(dout.deferred);
+    fallback.swap(dout.fallback);
+    out->commits = commits.data();
+    out->n_commits = commits.size();
+    out->ready = ready.data();
+    out->n_ready = ready.size();
+    out->read_resps = resps.data();
+    out->n_read_resps = resps.size();
+    out->state_changes = states.data();
+    out->n_state_changes = states.size();
+    out->dropped_reads = dropped.data();
+    out->n_dropped_reads = dropped.size();
+    out->deferred = deferred.data();
+    out->n_deferred = deferred.size();
+    out->fallback_groups = fallback.data();
+    out->n_fallback_groups = fallback.size();
+    out->gpu_passes = inp->n_groups ? 1 : 0;
+    out->decisions = dout.decisions;
+    out->pass_ns = t2 - t1;
+    out->pack_ns = 0;
+    out->device_ns = t2 - t1;
+    out->apply_ns = 0;
+    out->handle_ns = (t1 - t0) + (now_ns() - t2);
+    return HQ_OK;
+}
+
 // ------------------------------------------------------------------------------ C-ABI ------
 extern "C" {
 
 int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
+    return hq_worker_open_ex(device, n_max, 0, out);
+}
+
+int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out) {
     if (!out) return HQ_E_INVAL;
+    if (flags & ~HQ_WORKER_ON_DEVICE) return HQ_E_INVAL;
     *out = nullptr;
     if (n_max < 1 || n_max > HQ_MAX_VOTERS) return HQ_E_INVAL;
     hq_worker *w = new (std::nothrow) hq_worker();
@@ -746,12 +937,21 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
         return rc;   // message: hq_last_error(NULL)
     }
     w->n_max = n_max;
+    if (flags & HQ_WORKER_ON_DEVICE) {
+        rc = hq_dstep_open(w->ctx, &w->dstep);
+        if (rc) {
+            hq_close(w->ctx);
+            delete w;
+            return rc;
+        }
+    }
     *out = w;
     return HQ_OK;
 }
 
 void hq_worker_close(hq_worker *w) {
     if (!w) return;
+    if (w->dstep) hq_dstep_close(w->dstep);
     if (w->ctx) {
         hq_sync(w->ctx);
         if (w->host) hq_free_pinned(w->ctx, w->host);
@@ -770,6 +970,10 @@ int hq_worker_add_group(hq_worker *w, const hq_worker_group *g, const hq_member 
     if (!w) return HQ_E_INVAL;
     if (!g) return w->fail(HQ_E_INVAL, "hq_worker_add_group: group is NULL");
     if (w->index.count(g->cluster_id)) return w->fail(HQ_E_INVAL, "hq_worker_add_group: cluster exists");
+    if (w->host_stale) {                            // new pool entries append to a fresh mirror
+        int rc = w->sync_from_device();
+        if (rc) return rc;
+    }
     if (w->groups.size() >= UINT32_MAX) return w->fail(HQ_E_NOMEM, "hq_worker_add_group: too many groups");
     Group n{};
     n.rq = kNone;
@@ -817,10 +1021,13 @@ int hq_worker_set_group(hq_worker *w, const hq_worker_group *g, const hq_member 
     if (!g) return w->fail(HQ_E_INVAL, "hq_worker_set_group: group is NULL");
     auto it = w->index.find(g->cluster_id);
     if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_set_group: unknown cluster");
+    int rc = w->sync_from_device();
+    if (rc) return rc;
     Group n = w->groups[it->second];
-    int rc = w->load_group(n, g, members, false);
+    rc = w->load_group(n, g, members, false);
     if (rc) return rc;
     w->groups[it->second] = n;
+    if (w->dstep && it->second < w->dev_groups) w->dirty.push_back(it->second);
     return HQ_OK;
 }
 
@@ -830,6 +1037,8 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *out,
     if (!w) return HQ_E_INVAL;
     auto it = w->index.find(cluster_id);
     if (it == w->index.end()) return w->fail(HQ_E_INVAL, "hq_worker_get_group: unknown cluster");
+    int rc = w->sync_from_device();
+    if (rc) return rc;
     const Group &g = w->groups[it->second];
     const ReadQueue *q = g.rq == kNone ? nullptr : &w->rqs[g.rq];
     if (out) {
@@ -869,6 +1078,7 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
     if (in->n_groups && in->offsets[in->n_groups] > in->offsets[0] && !in->events)
         return w->fail(HQ_E_INVAL, "hq_worker_step: NULL events");
     std::memset(out, 0, sizeof *out);
+    if (w->dstep) return w->step_on_device(in, out);
     return w->step(in, out);
 }
 

@@ -36,7 +36,8 @@ HQ_LAG_LEADER_IMPLICIT = 1   # hq_commit_lag_args.flags: lag rows start at slot 
 HQ_TILE_GROUPS = 128
 HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table decided in place
 HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
-HQ_ABI_VERSION = 7
+HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
+HQ_ABI_VERSION = 8
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -279,6 +280,8 @@ SIGNATURES = {
     "hq_pack_acks": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_uint32, _vp]),
     "hq_worker_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "hq_worker_open_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.POINTER(_vp)]),
     "hq_worker_close": (None, [_vp]),
     "hq_worker_last_error": (ctypes.c_char_p, [_vp]),
     "hq_worker_add_group": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(ctypes.c_uint32)]),
@@ -1033,12 +1036,17 @@ class Worker:
     """The step worker (hq_worker_*): one step's events in, the reference's step results out,
     every quorum decision taken by the kernels."""
 
-    def __init__(self, device: int = 0, n_max: int = 8):
+    def __init__(self, device: int = 0, n_max: int = 8, on_device: bool = False):
+        """on_device: HQ_WORKER_ON_DEVICE, the group state resident on the GPU and every event
+        taken there (hq_dstep.hip); otherwise the host worker (events on the host, decisions
+        in GPU passes)."""
         self.h = _vp()
-        rc = lib.hq_worker_open(device, n_max, ctypes.byref(self.h))
+        rc = lib.hq_worker_open_ex(device, n_max, HQ_WORKER_ON_DEVICE if on_device else 0,
+                                   ctypes.byref(self.h))
         if rc != HQ_OK:
             raise HQError(rc, "hq_worker_open: " + lib.hq_last_error(None).decode())
         self.n_max = n_max
+        self.on_device = on_device
 
     def close(self) -> None:
         if self.h:

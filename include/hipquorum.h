@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 7
+#define HQ_ABI_VERSION 8
 
 /* status codes */
 #define HQ_OK          0
@@ -754,6 +754,16 @@ typedef struct hq_worker hq_worker;
 
 /* n_max: voting slots per group (1..8). */
 int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
+/* flags: 0 (= hq_worker_open) or HQ_WORKER_ON_DEVICE — the groups' quorum state stays on the GPU
+ * and hq_worker_step takes every event there: one thread per group handles its events one at a
+ * time as the reference does (membership filter, term check, tryUpdate + tryCommit, the
+ * confirmed-set insert + readIndex.confirm, handleLeaderReadIndex, the vote tally, CheckQuorum,
+ * campaign, appendEntries, the state transitions), each decision at the event that triggers
+ * it; the host ships the step's event rows and reads the result lists back (one launch pair,
+ * two synchronisations). Same results as the host worker; groups of at most 16 members.
+ * add/set/get_group work on a host mirror refreshed from the device when needed. */
+#define HQ_WORKER_ON_DEVICE 1u
+int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out);
 void hq_worker_close(hq_worker *w);
 const char *hq_worker_last_error(const hq_worker *w);
 /* Add a group; members[0 .. g->n_members); *handle (may be NULL) receives its handle, the

@@ -60,9 +60,9 @@ class OracleBackend:
 
 
 class WorkerBackend:
-    def __init__(self, hq, n_max=8, seed=0, worker=None):
+    def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False):
         self.hq = hq
-        self.w = worker if worker is not None else hq.Worker(0, n_max)
+        self.w = worker if worker is not None else hq.Worker(0, n_max, on_device=on_device)
         self.rng = np.random.default_rng(seed)
         self.cids = []
         self.last_passes = 0
@@ -151,8 +151,8 @@ class WireBackend(WorkerBackend):
 
     DEPLOYMENT = 0x5EED
 
-    def __init__(self, hq, n_max=8, seed=0, worker=None):
-        super().__init__(hq, n_max, seed, worker)
+    def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False):
+        super().__init__(hq, n_max, seed, worker, on_device)
         self.wire = hq.Wire(self.DEPLOYMENT)
         self.last_stats = None
 

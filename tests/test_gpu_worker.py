@@ -14,9 +14,13 @@ pytestmark = pytest.mark.gpu
 CASES = list(sc.all_cases())
 
 
-@pytest.fixture(scope="module")
-def worker_backend(hq):
-    b = WorkerBackend(hq, n_max=8, seed=1)
+MODES = [False, True]
+MODE_IDS = ["host", "device"]      # the host worker / HQ_WORKER_ON_DEVICE (hq_dstep.hip)
+
+
+@pytest.fixture(scope="module", params=MODES, ids=MODE_IDS)
+def worker_backend(hq, request):
+    b = WorkerBackend(hq, n_max=8, seed=1, on_device=request.param)
     yield b
     b.close()
 
@@ -33,27 +37,31 @@ def test_reference_scenario_on_gpu(worker_backend, case):
             assert w[k] == o[k], (case["name"], k, w[k], o[k])
 
 
-def test_one_gpu_pass_per_plain_step(hq):
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_one_gpu_pass_per_plain_step(hq, on_device):
     """Commit + ReadIndex acks + CheckQuorum of many groups: one GPU batch per step."""
-    b = WorkerBackend(hq, n_max=5)
+    b = WorkerBackend(hq, n_max=5, on_device=on_device)
     try:
         for cid in range(1, 101):
             b.add_group(cid, 1, 3, sc.LEADER, 10, 12, 10,
                         [(i, 12 if i == 1 else 10, sc.REMOTE, 0) for i in range(1, 6)])
         out = b.step({cid: [sc.msg(sc.RREP, 2, 3, 12), sc.msg(sc.RREP, 3, 3, 11),
                             ("check_quorum",)] for cid in range(1, 101)})
-        assert b.last_passes == 1 and b.last_decisions == 200
+        # host: one commit + one CheckQuorum decision per group in one pass; device: every
+        # ReplicateResp's tryCommit and the CheckQuorum, in one launch pair
+        assert b.last_passes == 1 and b.last_decisions == (300 if on_device else 200)
         assert all(out[cid]["committed"] == 11 for cid in range(1, 101))
         assert all(out[cid]["states"] == [] for cid in range(1, 101))
     finally:
         b.close()
 
 
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
 @pytest.mark.parametrize("seed,G,steps", [(1, 3000, 6), (2, 1500, 10), (3, 400, 25)])
-def test_random_differential(hq, seed, G, steps):
+def test_random_differential(hq, seed, G, steps, on_device):
     rng = np.random.default_rng(seed)
     groups = sr.random_groups(rng, G)
-    o, w = OracleBackend(), WorkerBackend(hq, n_max=8, seed=seed)
+    o, w = OracleBackend(), WorkerBackend(hq, n_max=8, seed=seed, on_device=on_device)
     try:
         for g in groups:
             o.add_group(*g)
@@ -79,15 +87,17 @@ def test_random_differential(hq, seed, G, steps):
                 assert w.state(g[0]) == o.state(g[0]), (s, g[0])
         # the streams exercised every output kind, and runs cut by barriers (several passes)
         assert all(v > 0 for v in seen.values()), seen
-        assert max(passes) >= 2, passes
+        # host: runs cut by barriers take several passes; device: every step is one launch pair
+        assert max(passes) == 1 if on_device else max(passes) >= 2, passes
     finally:
         w.close()
 
 
-def test_fallback_suspends_and_resync_resumes(hq):
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_fallback_suspends_and_resync_resumes(hq, on_device):
     """An observer acknowledging a pending ctx cannot be taken by the slot model: the group is
     suspended from that event on (its tail deferred) and resumes after hq_worker_set_group."""
-    w = hq.Worker(0, 8)
+    w = hq.Worker(0, 8, on_device=on_device)
     try:
         mem = [(i, 9, sc.REMOTE, 0) for i in range(1, 6)] + [(6, 0, sc.OBSERVER, 0)]
         w.add_group(7, 1, 2, sc.LEADER, 9, 9, 9, mem)
@@ -109,8 +119,9 @@ def test_fallback_suspends_and_resync_resumes(hq):
         w.close()
 
 
-def test_ack_above_last_index_is_fallback(hq):
-    w = hq.Worker(0, 4)
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_ack_above_last_index_is_fallback(hq, on_device):
+    w = hq.Worker(0, 4, on_device=on_device)
     try:
         w.add_group(1, 1, 2, sc.LEADER, 5, 6, 5, [(1, 6, 0, 0), (2, 5, 0, 0), (3, 5, 0, 0)])
         b = WorkerBackend(hq, worker=w)
@@ -121,8 +132,9 @@ def test_ack_above_last_index_is_fallback(hq):
         w.close()
 
 
-def test_add_group_validation(hq):
-    w = hq.Worker(0, 3)
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_add_group_validation(hq, on_device):
+    w = hq.Worker(0, 3, on_device=on_device)
     try:
         with pytest.raises(hq.HQError, match="n_max"):
             w.add_group(1, 1, 1, 0, 0, 0, 0, [(i, 0, 0, 0) for i in range(1, 5)])
@@ -136,11 +148,11 @@ def test_add_group_validation(hq):
 
 
 # ---- the same worker driven from wire bytes (raftpb.MessageBatch, hq_wire) --------------------
-@pytest.fixture(scope="module")
-def wire_backend(hq):
+@pytest.fixture(scope="module", params=MODES, ids=MODE_IDS)
+def wire_backend(hq, request):
     from step_harness import WireBackend
 
-    b = WireBackend(hq, n_max=8, seed=5)
+    b = WireBackend(hq, n_max=8, seed=5, on_device=request.param)
     yield b
     b.close()
 
@@ -157,13 +169,14 @@ def test_reference_scenario_from_wire_bytes(wire_backend, case):
             assert w[k] == o[k], (case["name"], k, w[k], o[k])
 
 
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
 @pytest.mark.parametrize("seed,G,steps", [(11, 1500, 6), (12, 300, 15)])
-def test_random_differential_from_wire_bytes(hq, seed, G, steps):
+def test_random_differential_from_wire_bytes(hq, seed, G, steps, on_device):
     from step_harness import WireBackend
 
     rng = np.random.default_rng(seed)
     groups = sr.random_groups(rng, G)
-    o, w = OracleBackend(), WireBackend(hq, n_max=8, seed=seed)
+    o, w = OracleBackend(), WireBackend(hq, n_max=8, seed=seed, on_device=on_device)
     try:
         for g in groups:
             o.add_group(*g)
@@ -186,5 +199,18 @@ def test_random_differential_from_wire_bytes(hq, seed, G, steps):
             for g in groups:
                 assert w.state(g[0]) == o.state(g[0]), (s, g[0])
         assert dropped > 0
+    finally:
+        w.close()
+
+
+def test_device_worker_member_cap(hq):
+    """The device path holds at most 16 members per group (8 voting + observers)."""
+    w = hq.Worker(0, 8, on_device=True)
+    try:
+        mem = [(i, 0, sc.REMOTE, 0) for i in range(1, 4)] + \
+              [(i, 0, sc.OBSERVER, 0) for i in range(4, 18)]
+        with pytest.raises(hq.HQError, match="16 members"):
+            w.add_group(1, 1, 1, 0, 0, 0, 0, mem)
+        w.add_group(2, 1, 1, 0, 0, 0, 0, mem[:16])
     finally:
         w.close()
