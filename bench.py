@@ -774,10 +774,12 @@ def step_events(hq, G, s, roles=STEP_ROLES["step"], last0=1000):
     return np.arange(G, dtype=np.uint32), offsets, ev
 
 
-def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles):
+def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False):
     """W workers (one host thread each, own HIP stream) over G groups split into W contiguous
     partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
-    of the first 4096 groups after cpu_steps steps)."""
+    of the first 4096 groups after cpu_steps steps). on_device: HQ_WORKER_ON_DEVICE workers, the
+    step's event rows in pinned host memory (a step worker's receive buffers) so that they cross
+    PCIe at the link's rate."""
     import threading
 
     rng = _shard_of(d, G)
@@ -787,14 +789,23 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles):
     bounds = [G * i // W for i in range(W + 1)]
     workers = []
     for i in range(W):
-        w = hq.Worker(d.device, n_voting)
+        w = hq.Worker(d.device, n_voting, on_device=on_device)
         w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
         workers.append(w)
+    pin_ctx = hq.Context(d.device) if on_device else None
+    pinned = [None] * W
     acc = dict(handle_ns=0, pass_ns=0, pack_ns=0, device_ns=0, apply_ns=0, gpu_passes=0,
                decisions=0)
     t_total, n_events, committed = 0.0, 0, None
     for s in range(steps + 1):
         evs = [step_events(hq, bounds[i + 1] - bounds[i], s, roles) for i in range(W)]
+        if pin_ctx is not None:      # copied into pinned buffers outside the timed region
+            for i, e in enumerate(evs):
+                if pinned[i] is None or pinned[i][2].size < e[2].size:
+                    pinned[i] = tuple(pin_ctx.pinned(x.size, x.dtype) for x in e)
+                for dst, src in zip(pinned[i], e):
+                    dst[:src.size] = src
+            evs = [tuple(p[k][:e[k].size] for k in range(3)) for p, e in zip(pinned, evs)]
         res = [None] * W
 
         def run(i):
@@ -819,6 +830,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles):
                 acc[k] += r[k]
     for w in workers:
         w.close()
+    if pin_ctx is not None:
+        pin_ctx.close()
     return t_total, n_events, acc, committed, (g, m)
 
 
@@ -843,17 +856,20 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
     members = ", ".join(f"{roles.count(r)} {r}" for r in ("remote", "witness", "observer")
                         if roles.count(r))
     out = {
-        "workload": f"{name}: hq_worker_step over {G} leader groups per GPU ({members}); per group "
+        "workload": f"{name}: hq_worker_step (device engine; host worker beside it) over {G} "
+                    f"leader groups per GPU ({members}); per group "
                     f"and step {nmsg} messages ({nmsg // 2} ReplicateResp, {nmsg // 2} "
                     f"HeartbeatResp), 1 proposal, 1/4 local ReadIndex",
         "unit": "events/s",
     }
-    committed_gpu = None
-    for W in (1, T):
-        t, ne, acc, committed, gm = _run_workers(hq, d, G, W, steps, cpu_steps, roles)
+    committed_gpu = committed_host = None
+    for on_device, W in ((True, 1), (True, T), (False, 1), (False, T)):
+        t, ne, acc, committed, gm = _run_workers(hq, d, G, W, steps, cpu_steps, roles, on_device)
         elapsed = d.max(t)
         rec = {
             "workers": W,
+            "mode": "device (HQ_WORKER_ON_DEVICE: every event on the GPU)" if on_device else
+                    "host worker (events on the host, decisions in GPU passes)",
             "value": d.sum(float(ne)) / elapsed,
             "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
             "ms_per_step": elapsed / steps * 1e3,
@@ -862,11 +878,16 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
                                          for k in ("pack", "device", "apply")},
         }
-        if W == 1:
+        if on_device and W == 1:
             out.update(rec)
             committed_gpu = committed
-        else:
+        elif on_device:
             out["concurrent_workers"] = rec
+        elif W == 1:
+            out["host_worker"] = rec
+            committed_host = committed
+        else:
+            out["host_worker_concurrent"] = rec
     if with_cpu and d.rank == 0 and d.world == 1:
         from oracle import qref
 
@@ -891,7 +912,12 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
                       f"event (oracle/qref_step.c, C restatement of the reference path)",
         }
         # the same events left the same committed indexes
-        out["parity_committed"] = committed_gpu == committed_cpu
+        out["parity_committed"] = committed_gpu == committed_cpu == committed_host
+        for k in ("value", "concurrent_workers", "host_worker", "host_worker_concurrent"):
+            v = out.get(k)
+            v = v["value"] if isinstance(v, dict) else v
+            if v:
+                out.setdefault("vs_cpu_replay", {})[k] = v / cpu[T]
     return out
 
 

@@ -462,6 +462,14 @@ int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out) {
     hq_ctx *ctx = d->ctx;
     const uint64_t n = in->n_groups;
     const uint64_t ne = n ? in->offsets[n] : 0;
+    out->commits.clear();
+    out->ready.clear();
+    out->resps.clear();
+    out->states.clear();
+    out->dropped.clear();
+    out->deferred.clear();
+    out->fallback.clear();
+    out->decisions = 0;
     if (n == 0) return HQ_OK;
     const uint64_t t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
