@@ -6,7 +6,9 @@ CSRC := dragonboat_amd/csrc
 LIBDIR := dragonboat_amd/lib
 LIB := $(LIBDIR)/libhipquorum.so
 OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o $(LIBDIR)/hq_table.o $(LIBDIR)/hq_pack.o \
-        $(LIBDIR)/hq_worker.o $(LIBDIR)/hq_wire.o $(LIBDIR)/hq_dstep.o
+        $(LIBDIR)/hq_worker.o $(LIBDIR)/hq_wire.o $(LIBDIR)/hq_stream.o $(LIBDIR)/hq_dstep.o
+SRCS := $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp \
+        $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_stream.cpp $(CSRC)/hq_dstep.hip
 DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
 CXX ?= g++
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra
@@ -28,17 +30,28 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
-# tuning variant: lag kernels with 2 groups per lane (8-byte loads), for A/B runs via HQ_LIB_PATH
-tools/lib_vec2/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)
-	@mkdir -p tools/lib_vec2
-	$(HIPCC) $(HIPFLAGS) -DHQ_LAG_VEC=2 -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip
+# tuning variants (one library each, for A/B runs via HQ_LIB_PATH, tools/ab_libs.sh):
+#   lib_vec2   lag kernels with 2 groups per lane (8-byte loads)
+#   lib_b512   every commit kernel with 512-thread blocks
+#   lib_mbN    grid cap (in 256-thread units) raised N x
+#   lib_ivN    records per lane of the table ingest kernels
+#   lib_b3tpwN tiles per wave of the 3-byte bitmap kernel
+define variant
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(1) -shared -o $@ $(SRCS)
+endef
+tools/lib_vec2/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_LAG_VEC=2)
+tools/lib_b512/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_COMMIT_BLOCK_BIG=512)
+tools/lib_mb%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_MAX_BLOCKS=$*)
+tools/lib_iv%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_INGEST_V=$*)
+tools/lib_b3tpw%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_BITS3_TPW=$*)
 
-# tuning variant: every commit kernel with 512-thread blocks (the pre-1024 geometry)
-tools/lib_b512/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)
-	@mkdir -p tools/lib_b512
-	$(HIPCC) $(HIPFLAGS) -DHQ_COMMIT_BLOCK_BIG=512 -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip
-
-# tuning variants: grid cap (in 256-thread units) raised 2x / 4x / 8x
+variants: grid cap (in 256-thread units) raised 2x / 4x / 8x
 tools/lib_mb%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)
 	@mkdir -p tools/lib_mb$*
 	$(HIPCC) $(HIPFLAGS) -DHQ_MAX_BLOCKS=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip

@@ -774,12 +774,14 @@ def step_events(hq, G, s, roles=STEP_ROLES["step"], last0=1000):
     return np.arange(G, dtype=np.uint32), offsets, ev
 
 
-def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False):
+def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, stream=False):
     """W workers (one host thread each, own HIP stream) over G groups split into W contiguous
     partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
-    of the first 4096 groups after cpu_steps steps). on_device: HQ_WORKER_ON_DEVICE workers, the
-    step's event rows in pinned host memory (a step worker's receive buffers) so that they cross
-    PCIe at the link's rate."""
+    of the first 4096 groups after cpu_steps steps, ..., encode seconds). on_device:
+    HQ_WORKER_ON_DEVICE workers, the step's input in pinned host memory (a step worker's receive
+    buffers) so that it crosses PCIe at the link's rate. stream: the input is the event stream
+    (hq_worker_step_stream), written by the producer — here hq_events_encode over the rows,
+    outside the timed region and timed on its own (encode seconds)."""
     import threading
 
     rng = _shard_of(d, G)
@@ -796,20 +798,32 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False):
     pinned = [None] * W
     acc = dict(handle_ns=0, pass_ns=0, pack_ns=0, device_ns=0, apply_ns=0, gpu_passes=0,
                decisions=0)
-    t_total, n_events, committed = 0.0, 0, None
+    t_total, n_events, committed, t_enc, nb_total = 0.0, 0, None, 0.0, 0
     for s in range(steps + 1):
         evs = [step_events(hq, bounds[i + 1] - bounds[i], s, roles) for i in range(W)]
+        n_step = sum(len(e[2]) for e in evs)
+        if stream:
+            t0 = time.perf_counter()
+            enc = [hq.encode_events(e[1], e[2]) for e in evs]
+            if s > 0:
+                t_enc += time.perf_counter() - t0
+                nb_total += sum(len(data) for data, _ in enc)
+            evs = [(e[0], e[1], b, data) for e, (data, b) in zip(evs, enc)]
         if pin_ctx is not None:      # copied into pinned buffers outside the timed region
             for i, e in enumerate(evs):
-                if pinned[i] is None or pinned[i][2].size < e[2].size:
-                    pinned[i] = tuple(pin_ctx.pinned(x.size, x.dtype) for x in e)
+                if pinned[i] is None or any(p.size < x.size for p, x in zip(pinned[i], e)):
+                    pinned[i] = tuple(pin_ctx.pinned(x.size + x.size // 4 + 1, x.dtype)
+                                      for x in e)
                 for dst, src in zip(pinned[i], e):
                     dst[:src.size] = src
-            evs = [tuple(p[k][:e[k].size] for k in range(3)) for p, e in zip(pinned, evs)]
+            evs = [tuple(p[k][:e[k].size] for k in range(len(e))) for p, e in zip(pinned, evs)]
         res = [None] * W
 
         def run(i):
-            res[i] = workers[i].step(*evs[i], copy=False)
+            if stream:
+                res[i] = workers[i].step_stream(*evs[i], copy=False)
+            else:
+                res[i] = workers[i].step(*evs[i], copy=False)
 
         threads = [threading.Thread(target=run, args=(i,)) for i in range(W)]
         t0 = time.perf_counter()
@@ -824,7 +838,7 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False):
         if s == 0:
             continue                      # warm-up: allocations and first-touch
         t_total += dt
-        n_events += sum(len(e[2]) for e in evs)
+        n_events += n_step
         for r in res:
             for k in acc:
                 acc[k] += r[k]
@@ -832,7 +846,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False):
         w.close()
     if pin_ctx is not None:
         pin_ctx.close()
-    return t_total, n_events, acc, committed, (g, m)
+    acc["stream_bytes"] = nb_total
+    return t_total, n_events, acc, committed, (g, m), t_enc
 
 
 def _shard_of(d, G):
@@ -862,14 +877,19 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
                     f"HeartbeatResp), 1 proposal, 1/4 local ReadIndex",
         "unit": "events/s",
     }
-    committed_gpu = committed_host = None
-    for on_device, W in ((True, 1), (True, T), (False, 1), (False, T)):
-        t, ne, acc, committed, gm = _run_workers(hq, d, G, W, steps, cpu_steps, roles, on_device)
+    committed = {}
+    modes = {"device_stream": "device worker (HQ_WORKER_ON_DEVICE: every event on the GPU), "
+                              "events as the event stream (hq_worker_step_stream)",
+             "device_rows": "device worker, events as 56-byte hq_event rows (hq_worker_step)",
+             "host": "host worker (events on the host, decisions in GPU passes), rows"}
+    for mode, W in (("device_stream", 1), ("device_stream", T), ("device_rows", 1),
+                    ("device_rows", T), ("host", 1), ("host", T)):
+        t, ne, acc, committed[mode], gm, t_enc = _run_workers(
+            hq, d, G, W, steps, cpu_steps, roles, mode != "host", mode == "device_stream")
         elapsed = d.max(t)
         rec = {
             "workers": W,
-            "mode": "device (HQ_WORKER_ON_DEVICE: every event on the GPU)" if on_device else
-                    "host worker (events on the host, decisions in GPU passes)",
+            "mode": modes[mode],
             "value": d.sum(float(ne)) / elapsed,
             "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
             "ms_per_step": elapsed / steps * 1e3,
@@ -878,16 +898,16 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
                                          for k in ("pack", "device", "apply")},
         }
-        if on_device and W == 1:
+        if mode == "device_stream":
+            rec["stream_bytes_per_event"] = acc.get("stream_bytes", 0) / max(1, ne)
+            rec["producer_encode_ns_per_event"] = t_enc / max(1, ne) * 1e9
+        key = {("device_stream", 1): None, ("device_stream", T): "concurrent_workers",
+               ("device_rows", 1): "device_rows", ("device_rows", T): "device_rows_concurrent",
+               ("host", 1): "host_worker", ("host", T): "host_worker_concurrent"}[(mode, W)]
+        if key is None:
             out.update(rec)
-            committed_gpu = committed
-        elif on_device:
-            out["concurrent_workers"] = rec
-        elif W == 1:
-            out["host_worker"] = rec
-            committed_host = committed
         else:
-            out["host_worker_concurrent"] = rec
+            out[key] = rec
     if with_cpu and d.rank == 0 and d.world == 1:
         from oracle import qref
 
@@ -903,7 +923,7 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
                 if s > 0:
                     tc += time.perf_counter() - t0
                     ne += len(ev[2])
-            committed_cpu = [b.committed(i) for i in range(len(committed_gpu))]
+            committed_cpu = [b.committed(i) for i in range(len(committed["host"]))]
             b.close()
             cpu[nt] = ne / tc
         out["cpu_reference"] = {
@@ -912,8 +932,9 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
                       f"event (oracle/qref_step.c, C restatement of the reference path)",
         }
         # the same events left the same committed indexes
-        out["parity_committed"] = committed_gpu == committed_cpu == committed_host
-        for k in ("value", "concurrent_workers", "host_worker", "host_worker_concurrent"):
+        out["parity_committed"] = all(c == committed_cpu for c in committed.values())
+        for k in ("value", "concurrent_workers", "device_rows", "device_rows_concurrent",
+                  "host_worker", "host_worker_concurrent"):
             v = out.get(k)
             v = v["value"] if isinstance(v, dict) else v
             if v:

@@ -4,7 +4,6 @@
 #pragma once
 
 #include <cstdint>
-#include <vector>
 
 #include "../../include/hipquorum.h"
 
@@ -36,16 +35,27 @@ constexpr uint8_t kDSuspended = 1;
 
 struct hq_dstep;                      // device buffers of one worker
 
-struct hq_dstep_out {                 // the lists of one step, in input group order
-    std::vector<hq_commit_event> commits;
-    std::vector<hq_ready_to_read> ready;
-    std::vector<hq_read_index_resp> resps;
-    std::vector<hq_state_change> states;
-    std::vector<hq_dropped_read> dropped;
-    std::vector<uint64_t> deferred;
-    std::vector<uint64_t> fallback;
-    uint64_t decisions = 0;
-    uint64_t h2d_ns = 0, kernel_ns = 0, d2h_ns = 0;
+struct hq_dstep_out {                 // the lists of one step, in input group order, in the
+    const hq_commit_event *commits;   // engine's pinned host buffer (valid until its next step)
+    const hq_ready_to_read *ready;
+    const hq_read_index_resp *resps;
+    const hq_state_change *states;
+    const hq_dropped_read *dropped;
+    const uint64_t *deferred;
+    const uint64_t *fallback;
+    uint64_t n_commits, n_ready, n_resps, n_states, n_dropped, n_deferred, n_fallback;
+    uint64_t decisions;
+    uint64_t kernel_ns, d2h_ns;       // wall time: H2D + pass A + scan + bases; pass B + D2H
+};
+
+// one step's input: rows (events) or an event stream (bytes + boffsets)
+struct hq_dstep_in {
+    uint64_t n;
+    const uint32_t *groups;
+    const uint64_t *offsets;
+    const hq_event *events;
+    const uint64_t *boffsets;
+    const uint8_t *bytes;
 };
 
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out);
@@ -57,4 +67,4 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
 // copy the first ng group records (with their reads) and nm member records back
 int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t nm, hq_dmember *m);
 // one step over the device state (the input is already validated)
-int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out);
+int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out);

@@ -38,7 +38,9 @@ struct StepK {
     uint64_t n;                   // groups listed in this step
     const uint32_t *handles;
     const uint64_t *offsets;
-    const hq_event *events;
+    const hq_event *events;       // rows, or
+    const uint64_t *boffsets;     // an event stream (include/hipquorum.h "event streams")
+    const uint8_t *bytes;
     uint32_t *counts;             // [kLists][n] (+1): pass A output
     const uint32_t *scan;         // exclusive scan of counts: pass B input
     hq_commit_event *commits;
@@ -53,6 +55,42 @@ struct StepK {
 __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
     return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
            t == HQ_MSG_HEARTBEAT_RESP || t == 20 || t == 8 || t == 9;
+}
+
+// the device twin of hq_stream.cpp's decoder: one LEB128 varint
+__device__ __forceinline__ bool dvar(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
+    v = 0;
+    for (int sh = 0; sh < 64; sh += 7) {
+        if (p >= end) return false;
+        const uint32_t b = *p++;
+        v |= (uint64_t)(b & 0x7F) << sh;
+        if (b < 0x80) return true;
+    }
+    return false;
+}
+
+// one event of a group's stream; term: the group's previous message term in the stream
+__device__ bool decode_event(const uint8_t *&p, const uint8_t *end, uint64_t &term,
+                             hq_event &v) {
+    v = hq_event{};
+    if (p >= end) return false;
+    const uint32_t h = *p++;
+    v.kind = h & 7;
+    if (v.kind == HQ_EV_READ) return dvar(p, end, v.hint) && dvar(p, end, v.hint_high);
+    if (v.kind == HQ_EV_PROPOSE) return dvar(p, end, v.log_index);
+    if (v.kind != HQ_EV_MESSAGE) return true;
+    const uint32_t code = (h >> 3) & 7;
+    uint64_t t = code == 0 ? HQ_MSG_REPLICATE_RESP : code == 1 ? HQ_MSG_REQUEST_VOTE_RESP
+               : code == 2 ? HQ_MSG_HEARTBEAT_RESP : code == 3 ? HQ_MSG_READ_INDEX : 0;
+    if (code == 7 && !dvar(p, end, t)) return false;
+    v.type = (uint32_t)t;
+    v.reject = (h >> 6) & 1;
+    if (!dvar(p, end, v.from)) return false;
+    if (!(h & 0x80) && !dvar(p, end, term)) return false;
+    v.term = term;
+    if ((code == 0 || code == 7) && !dvar(p, end, v.log_index)) return false;
+    if (code >= 2 && !(dvar(p, end, v.hint) && dvar(p, end, v.hint_high))) return false;
+    return true;
 }
 
 // One group's state and its output cursor. WRITE = false: counting pass on a private copy;
@@ -296,15 +334,26 @@ struct Engine {
         return true;                                     // no handler in this state
     }
 
-    __device__ void run(uint64_t e0, uint64_t e1) {
+    // the group's events: rows (STREAM = false) or its bytes [p, end) of the stream; an event
+    // that does not decode is a fallback like one the path does not take
+    template <bool STREAM>
+    __device__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
         const uint64_t committed0 = g.committed;
+        uint64_t term = 0;
         for (uint64_t e = e0; e < e1; ++e) {
             if (g.flags & kDSuspended) {
                 defer(e);
                 continue;
             }
-            const hq_event ev = a.events[e];
-            if (!handle(ev, e)) {                        // this event and the rest are deferred
+            bool ok;
+            if (STREAM) {
+                hq_event ev;
+                ok = decode_event(p, end, term, ev) && handle(ev, e);
+            } else {
+                const hq_event ev = a.events[e];
+                ok = handle(ev, e);
+            }
+            if (!ok) {                                   // this event and the rest are deferred
                 g.flags |= kDSuspended;
                 const uint32_t p = slot(kFallback);
                 if (WRITE) a.fallback[p] = g.cluster_id;
@@ -328,13 +377,17 @@ struct Engine {
     }
 };
 
-template <bool WRITE>
+template <bool WRITE, bool STREAM>
 __global__ __launch_bounds__(256) void k_step(const StepK a) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t h = a.handles[i];
     Engine<WRITE> eng(a, i, h);
-    eng.run(a.offsets[i], a.offsets[i + 1]);
+    if (STREAM)
+        eng.template run<true>(a.offsets[i], a.offsets[i + 1], a.bytes + a.boffsets[i],
+                               a.bytes + a.boffsets[i + 1]);
+    else
+        eng.template run<false>(a.offsets[i], a.offsets[i + 1], nullptr, nullptr);
     if (WRITE) {
         eng.store(h);
     } else {
@@ -371,6 +424,8 @@ struct hq_dstep {
     size_t scan_tmp_cap = 0;
     void *out = nullptr;
     size_t out_cap = 0;
+    void *host_out = nullptr;     // pinned: the lists come back in one copy
+    size_t host_out_cap = 0;
 };
 
 namespace {
@@ -406,6 +461,7 @@ void hq_dstep_close(hq_dstep *d) {
     for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, d->in,
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp, d->out})
         if (p) (void)hipFree(p);
+    if (d->host_out) (void)hipHostFree(d->host_out);
     delete d;
 }
 
@@ -458,34 +514,37 @@ int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t n
     return rc;
 }
 
-int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out) {
+int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     hq_ctx *ctx = d->ctx;
-    const uint64_t n = in->n_groups;
+    const uint64_t n = in->n;
     const uint64_t ne = n ? in->offsets[n] : 0;
-    out->commits.clear();
-    out->ready.clear();
-    out->resps.clear();
-    out->states.clear();
-    out->dropped.clear();
-    out->deferred.clear();
-    out->fallback.clear();
-    out->decisions = 0;
+    const bool stream = in->bytes != nullptr;
+    const uint64_t nb = stream && n ? in->boffsets[n] : 0;
+    *out = hq_dstep_out{};
     if (n == 0) return HQ_OK;
     const uint64_t t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    // the step's input: handles, offsets and events, one device region
-    const size_t o_off = (n * 4 + 255) & ~size_t(255);
-    const size_t o_ev = o_off + (((n + 1) * 8 + 255) & ~size_t(255));
-    const size_t in_bytes = o_ev + ne * sizeof(hq_event);
+    // the step's input in one device region: handles, offsets, [boffsets,] events or bytes
+    auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t o_off = up(n * 4);
+    const size_t o_boff = o_off + up((n + 1) * 8);
+    const size_t o_ev = o_boff + (stream ? up((n + 1) * 8) : 0);
+    const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event));
     if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
     char *din = static_cast<char *>(d->in);
-    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(din, in->groups, n * 4, hipMemcpyHostToDevice,
-                                                    ctx->stream), "hq_dstep H2D");
-    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(din + o_off, in->offsets, (n + 1) * 8,
-                                                    hipMemcpyHostToDevice, ctx->stream), "hq_dstep H2D");
-    if (!rc && ne)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(din + o_ev, in->events, ne * sizeof(hq_event),
-                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep H2D");
+    auto h2d = [&](size_t off, const void *src, size_t bytes) {
+        if (!rc && bytes)
+            rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
+                                                   ctx->stream), "hq_dstep H2D");
+    };
+    h2d(0, in->groups, n * 4);
+    h2d(o_off, in->offsets, (n + 1) * 8);
+    if (stream) {
+        h2d(o_boff, in->boffsets, (n + 1) * 8);
+        h2d(o_ev, in->bytes, nb);
+    } else {
+        h2d(o_ev, in->events, ne * sizeof(hq_event));
+    }
     // counts [kLists][n] + 1 (zero: the scan's last element is the grand total)
     const size_t cn = (size_t)kLists * n + 1;
     size_t cc = d->cnt_cap * 4, sc = d->cnt_cap * 4, bc = d->cnt_cap ? 64 : 0;
@@ -508,14 +567,20 @@ int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out) {
     k.n = n;
     k.handles = reinterpret_cast<const uint32_t *>(din);
     k.offsets = reinterpret_cast<const uint64_t *>(din + o_off);
-    k.events = reinterpret_cast<const hq_event *>(din + o_ev);
+    if (stream) {
+        k.boffsets = reinterpret_cast<const uint64_t *>(din + o_boff);
+        k.bytes = reinterpret_cast<const uint8_t *>(din + o_ev);
+    } else {
+        k.events = reinterpret_cast<const hq_event *>(din + o_ev);
+    }
     k.counts = d->counts;
     k.scan = d->scan;
     const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
     rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
     if (!rc) rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_step<false>, grid, blk, 0, ctx->stream, k);
+    if (stream) hipLaunchKernelGGL((k_step<false, true>), grid, blk, 0, ctx->stream, k);
+    else hipLaunchKernelGGL((k_step<false, false>), grid, blk, 0, ctx->stream, k);
     rc = hq::post_launch(ctx, "k_step<count>");
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
@@ -532,16 +597,25 @@ int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out) {
     const uint64_t t1 = now_ns();
     uint64_t len[kLists];
     for (int l = 0; l < kLists; ++l) len[l] = bases[l + 1] - bases[l];
-    // the output lists in one device region
+    // the output lists in one device region, mirrored by one pinned host region
     const size_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
                                 sizeof(hq_read_index_resp), sizeof(hq_state_change),
                                 sizeof(hq_dropped_read), 8, 8, 0};
     size_t off[kLists], total = 0;
     for (int l = 0; l < kLists; ++l) {
         off[l] = total;
-        total += (len[l] * rec[l] + 255) & ~size_t(255);
+        total += up(len[l] * rec[l]);
     }
     rc = grow(ctx, &d->out, &d->out_cap, total + 256, false, "hq_dstep output");
+    if (!rc && total + 256 > d->host_out_cap) {
+        if (d->host_out) (void)hipHostFree(d->host_out);
+        d->host_out = nullptr;
+        d->host_out_cap = 0;
+        const size_t want = (total + 256) + (total + 256) / 2;
+        rc = hq::check_hip(ctx, hipHostMalloc(&d->host_out, want, hipHostMallocDefault),
+                           "hq_dstep pinned output");
+        if (!rc) d->host_out_cap = want;
+    }
     if (rc) return rc;
     char *o = static_cast<char *>(d->out);
     k.commits = reinterpret_cast<hq_commit_event *>(o + off[kCommits]);
@@ -553,27 +627,31 @@ int hq_dstep_run(hq_dstep *d, const hq_step_input *in, hq_dstep_out *out) {
     k.fallback = reinterpret_cast<uint64_t *>(o + off[kFallback]);
     rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_step<true>, grid, blk, 0, ctx->stream, k);
+    if (stream) hipLaunchKernelGGL((k_step<true, true>), grid, blk, 0, ctx->stream, k);
+    else hipLaunchKernelGGL((k_step<true, false>), grid, blk, 0, ctx->stream, k);
     rc = hq::post_launch(ctx, "k_step<write>");
-    out->commits.resize(len[kCommits]);
-    out->ready.resize(len[kReady]);
-    out->resps.resize(len[kResps]);
-    out->states.resize(len[kStates]);
-    out->dropped.resize(len[kDropped]);
-    out->deferred.resize(len[kDeferred]);
-    out->fallback.resize(len[kFallback]);
-    out->decisions = len[kDecisions];
-    void *dst[kLists - 1] = {out->commits.data(), out->ready.data(), out->resps.data(),
-                             out->states.data(), out->dropped.data(), out->deferred.data(),
-                             out->fallback.data()};
-    for (int l = 0; l < kLists - 1 && !rc; ++l)
-        if (len[l])
-            rc = hq::check_hip(ctx, hipMemcpyAsync(dst[l], o + off[l], len[l] * rec[l],
-                                                   hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    if (!rc && total)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(d->host_out, o, total, hipMemcpyDeviceToHost,
+                                               ctx->stream), "D2H");
     if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
-    const uint64_t t2 = now_ns();
-    out->h2d_ns = 0;
+    if (rc) return rc;
+    const char *ho = static_cast<const char *>(d->host_out);
+    out->commits = reinterpret_cast<const hq_commit_event *>(ho + off[kCommits]);
+    out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + off[kReady]);
+    out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + off[kResps]);
+    out->states = reinterpret_cast<const hq_state_change *>(ho + off[kStates]);
+    out->dropped = reinterpret_cast<const hq_dropped_read *>(ho + off[kDropped]);
+    out->deferred = reinterpret_cast<const uint64_t *>(ho + off[kDeferred]);
+    out->fallback = reinterpret_cast<const uint64_t *>(ho + off[kFallback]);
+    out->n_commits = len[kCommits];
+    out->n_ready = len[kReady];
+    out->n_resps = len[kResps];
+    out->n_states = len[kStates];
+    out->n_dropped = len[kDropped];
+    out->n_deferred = len[kDeferred];
+    out->n_fallback = len[kFallback];
+    out->decisions = len[kDecisions];
     out->kernel_ns = t1 - t0;
-    out->d2h_ns = t2 - t1;
-    return rc;
+    out->d2h_ns = now_ns() - t1;
+    return HQ_OK;
 }

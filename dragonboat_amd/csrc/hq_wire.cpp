@@ -154,6 +154,8 @@ struct hq_wire {
     std::vector<uint32_t> groups;
     std::vector<uint64_t> offsets;
     std::vector<hq_event> events;
+    std::vector<uint64_t> boffsets;    // hq_wire_step_stream
+    std::vector<uint8_t> bytes;
 
     int fail(int code, const std::string &m) {
         err = m;
@@ -325,6 +327,24 @@ int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wir
     out->offsets = w->offsets.data();
     out->events = w->events.data();
     if (stats) *stats = w->stats;
+    return HQ_OK;
+}
+
+int hq_wire_step_stream(hq_wire *w, hq_worker *worker, hq_step_stream *out, hq_wire_stats *stats) {
+    if (!w || !out) return HQ_E_INVAL;
+    hq_step_input in;
+    int rc = hq_wire_step_input(w, worker, &in, stats);
+    if (rc) return rc;
+    w->boffsets.resize(in.n_groups + 1);
+    w->bytes.resize((size_t)w->events.size() * HQ_EVENT_STREAM_MAX);
+    rc = hq_events_encode(in.n_groups, in.offsets, in.events, w->bytes.data(), w->bytes.size(),
+                          w->boffsets.data());
+    if (rc) return w->fail(rc, "hq_wire_step_stream: encode");
+    out->n_groups = in.n_groups;
+    out->groups = in.groups;
+    out->offsets = in.offsets;
+    out->boffsets = w->boffsets.data();
+    out->bytes = w->bytes.data();
     return HQ_OK;
 }
 

@@ -100,7 +100,8 @@ struct hq_worker {
     std::vector<uint32_t> dirty;          // handles changed on the host since the last upload
     std::vector<uint64_t> stamp;          // step stamp per handle (a group listed twice)
     uint64_t step_no = 0;
-    hq_dstep_out dout;
+    hq_dstep_out dout{};
+    std::vector<hq_event> decoded;        // host worker: a stream step's rows
     std::string err;
     std::vector<Group> groups;
     std::vector<Member> pool;
@@ -161,7 +162,7 @@ struct hq_worker {
     void to_device_record(const Group &g, hq_dgroup &d, hq_dread *r) const;
     int sync_to_device();
     int sync_from_device();
-    int step_on_device(const hq_step_input *in, hq_step_output *out);
+    int step_on_device(const hq_dstep_in &in, hq_step_output *out);
     int load_group(Group &g, const hq_worker_group *src, const hq_member *m, bool fresh);
     int step(const hq_step_input *in, hq_step_output *out);
     Verdict handle(Group &g, const hq_event &e, uint64_t ei);
@@ -867,53 +868,48 @@ int hq_worker::sync_from_device() {
     return HQ_OK;
 }
 
-int hq_worker::step_on_device(const hq_step_input *inp, hq_step_output *out) {
+int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     const uint64_t t0 = now_ns();
     if (stamp.size() < groups.size()) stamp.resize(groups.size(), 0);
     ++step_no;
-    for (uint64_t i = 0; i < inp->n_groups; ++i) {   // the host worker's input checks
-        const uint32_t gi = inp->groups[i];
+    for (uint64_t i = 0; i < inp.n; ++i) {           // the host worker's input checks
+        const uint32_t gi = inp.groups[i];
         if (gi >= groups.size()) return fail(HQ_E_INVAL, "hq_worker_step: unknown group handle");
-        if (inp->offsets[i + 1] < inp->offsets[i])
+        if (inp.offsets[i + 1] < inp.offsets[i])
             return fail(HQ_E_INVAL, "hq_worker_step: offsets decrease");
+        if (inp.boffsets && inp.boffsets[i + 1] < inp.boffsets[i])
+            return fail(HQ_E_INVAL, "hq_worker_step_stream: boffsets decrease");
         if (stamp[gi] == step_no) return fail(HQ_E_INVAL, "hq_worker_step: a group is listed twice");
         stamp[gi] = step_no;
     }
     int rc = sync_to_device();
     if (rc) return rc;
     const uint64_t t1 = now_ns();
-    rc = hq(hq_dstep_run(dstep, inp, &dout), "hq_dstep_run");
+    rc = hq(hq_dstep_run(dstep, &inp, &dout), "hq_dstep_run");
     if (rc) return rc;
     host_stale = true;
     const uint64_t t2 = now_ns();
-    commits.swap(dout.commits);
-    ready.swap(dout.ready);
-    resps.swap(dout.resps);
-    states.swap(dout.states);
-    dropped.swap(dout.dropped);
-    deferred.swap(dout.deferred);
-    fallback.swap(dout.fallback);
-    out->commits = commits.data();
-    out->n_commits = commits.size();
-    out->ready = ready.data();
-    out->n_ready = ready.size();
-    out->read_resps = resps.data();
-    out->n_read_resps = resps.size();
-    out->state_changes = states.data();
-    out->n_state_changes = states.size();
-    out->dropped_reads = dropped.data();
-    out->n_dropped_reads = dropped.size();
-    out->deferred = deferred.data();
-    out->n_deferred = deferred.size();
-    out->fallback_groups = fallback.data();
-    out->n_fallback_groups = fallback.size();
-    out->gpu_passes = inp->n_groups ? 1 : 0;
+    out->commits = dout.commits;
+    out->n_commits = dout.n_commits;
+    out->ready = dout.ready;
+    out->n_ready = dout.n_ready;
+    out->read_resps = dout.resps;
+    out->n_read_resps = dout.n_resps;
+    out->state_changes = dout.states;
+    out->n_state_changes = dout.n_states;
+    out->dropped_reads = dout.dropped;
+    out->n_dropped_reads = dout.n_dropped;
+    out->deferred = dout.deferred;
+    out->n_deferred = dout.n_deferred;
+    out->fallback_groups = dout.fallback;
+    out->n_fallback_groups = dout.n_fallback;
+    out->gpu_passes = inp.n ? 1 : 0;
     out->decisions = dout.decisions;
     out->pass_ns = t2 - t1;
     out->pack_ns = 0;
     out->device_ns = t2 - t1;
     out->apply_ns = 0;
-    out->handle_ns = (t1 - t0) + (now_ns() - t2);
+    out->handle_ns = t1 - t0;
     return HQ_OK;
 }
 
@@ -1078,8 +1074,31 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
     if (in->n_groups && in->offsets[in->n_groups] > in->offsets[0] && !in->events)
         return w->fail(HQ_E_INVAL, "hq_worker_step: NULL events");
     std::memset(out, 0, sizeof *out);
-    if (w->dstep) return w->step_on_device(in, out);
+    if (w->dstep)
+        return w->step_on_device(hq_dstep_in{in->n_groups, in->groups, in->offsets, in->events,
+                                             nullptr, nullptr}, out);
     return w->step(in, out);
+}
+
+int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output *out) {
+    if (!w) return HQ_E_INVAL;
+    if (!in || !out) return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL argument");
+    if (in->n_groups && (!in->groups || !in->offsets || !in->boffsets))
+        return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL groups/offsets/boffsets");
+    if (in->n_groups && in->boffsets[in->n_groups] > in->boffsets[0] && !in->bytes)
+        return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL bytes");
+    std::memset(out, 0, sizeof *out);
+    static const uint8_t none = 0;
+    if (w->dstep)
+        return w->step_on_device(hq_dstep_in{in->n_groups, in->groups, in->offsets, nullptr,
+                                             in->boffsets, in->bytes ? in->bytes : &none}, out);
+    const uint64_t ne = in->n_groups ? in->offsets[in->n_groups] : 0;
+    w->decoded.resize(ne);
+    if (in->n_groups && hq_events_decode(in->n_groups, in->offsets, in->boffsets, in->bytes,
+                                         w->decoded.data()) != HQ_OK)
+        return w->fail(HQ_E_INVAL, "hq_worker_step_stream: malformed event stream");
+    const hq_step_input rows{in->n_groups, in->groups, in->offsets, w->decoded.data()};
+    return w->step(&rows, out);
 }
 
 }  // extern "C"

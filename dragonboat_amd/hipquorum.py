@@ -37,7 +37,7 @@ HQ_TILE_GROUPS = 128
 HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table decided in place
 HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
-HQ_ABI_VERSION = 8
+HQ_ABI_VERSION = 9
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -175,6 +175,15 @@ class StepInput(ctypes.Structure):
                 ("events", _vp)]
 
 
+class StepStream(ctypes.Structure):
+    """Mirror of ``hq_step_stream``."""
+
+    _fields_ = [("n_groups", ctypes.c_uint64), ("groups", _vp), ("offsets", _vp),
+                ("boffsets", _vp), ("bytes", _vp)]
+
+
+HQ_EVENT_STREAM_MAX = 64
+
 STEP_OUTPUT_LISTS = [("commits", COMMIT_EVENT_DTYPE), ("ready", READY_DTYPE),
                      ("read_resps", READ_RESP_DTYPE), ("state_changes", STATE_CHANGE_DTYPE),
                      ("dropped_reads", DROPPED_READ_DTYPE), ("deferred", np.dtype("<u8")),
@@ -292,6 +301,12 @@ SIGNATURES = {
                                            ctypes.c_uint32]),
     "hq_worker_step": (ctypes.c_int, [_vp, ctypes.POINTER(StepInput),
                                       ctypes.POINTER(StepOutput)]),
+    "hq_worker_step_stream": (ctypes.c_int, [_vp, ctypes.POINTER(StepStream),
+                                             ctypes.POINTER(StepOutput)]),
+    "hq_events_encode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
+    "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
+                                           ctypes.POINTER(WireStats)]),
     "hq_wire_decode_batch": (ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_uint64, _u64p,
                                             ctypes.POINTER(WireBatchInfo)]),
     "hq_wire_open": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(_vp)]),
@@ -1116,6 +1131,24 @@ class Worker:
         out = StepOutput()
         self._check(lib.hq_worker_step(self.h, ctypes.byref(inp), ctypes.byref(out)),
                     "hq_worker_step")
+        return self._results(out, copy)
+
+    def step_stream(self, groups, offsets, boffsets, data, copy=True):
+        """hq_worker_step_stream: the step's events as an event stream (encode_events)."""
+        groups = np.ascontiguousarray(groups, np.uint32)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        boffsets = np.ascontiguousarray(boffsets, np.uint64)
+        data = np.ascontiguousarray(data, np.uint8)
+        assert len(offsets) == len(groups) + 1 == len(boffsets)
+        inp = StepStream(len(groups), _p(groups), _p(offsets), _p(boffsets),
+                         _p(data) if len(data) else None)
+        out = StepOutput()
+        self._check(lib.hq_worker_step_stream(self.h, ctypes.byref(inp), ctypes.byref(out)),
+                    "hq_worker_step_stream")
+        return self._results(out, copy)
+
+    @staticmethod
+    def _results(out, copy):
         res = {}
         for name, dt in STEP_OUTPUT_LISTS:
             n = getattr(out, "n_" + name)
@@ -1137,6 +1170,32 @@ class Worker:
         assert int(groups["n_members"].sum()) == len(members)
         self._check(lib.hq_worker_add_groups(self.h, _p(groups), len(groups), _p(members)),
                     "hq_worker_add_groups")
+
+
+def encode_events(offsets, events):
+    """hq_events_encode: (stream bytes as uint8, boffsets) of rows grouped by `offsets`."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    events = np.ascontiguousarray(events, EVENT_DTYPE)
+    n = len(offsets) - 1
+    ne = int(offsets[-1] - offsets[0]) if n > 0 else 0
+    out = np.zeros(max(1, ne * HQ_EVENT_STREAM_MAX), np.uint8)
+    boff = np.zeros(n + 1, np.uint64)
+    _chk(lib.hq_events_encode(n, _p(offsets), _p(events) if len(events) else None, _p(out),
+                              len(out), _p(boff)), "hq_events_encode")
+    return out[:int(boff[-1])].copy(), boff
+
+
+def decode_events(offsets, boffsets, data):
+    """hq_events_decode: the rows of an event stream (fields it does not carry are 0)."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    boffsets = np.ascontiguousarray(boffsets, np.uint64)
+    data = np.ascontiguousarray(data, np.uint8)
+    n = len(offsets) - 1
+    ev = np.zeros(max(1, int(offsets[-1]) if n > 0 else 0), EVENT_DTYPE)
+    _chk(lib.hq_events_decode(n, _p(offsets), _p(boffsets),
+                              _p(data) if len(data) else _p(np.zeros(1, np.uint8)), _p(ev)),
+         "hq_events_decode")
+    return ev[:int(offsets[-1]) if n > 0 else 0]
 
 
 # ------------------------------------------------------------------------------ wire decode ----
@@ -1196,3 +1255,20 @@ class Wire:
         ev = np.frombuffer((ctypes.c_char * (ne * EVENT_DTYPE.itemsize)).from_address(
             self._inp.events), EVENT_DTYPE) if ne else np.zeros(0, EVENT_DTYPE)
         return grp.copy(), off.copy(), ev.copy(), st
+
+    def step_stream(self, worker: "Worker"):
+        """(groups, offsets, boffsets, bytes) copies of hq_wire_step_stream's output, and the
+        WireStats."""
+        st = WireStats()
+        inp = StepStream()
+        self._check(lib.hq_wire_step_stream(self.h, worker.h, ctypes.byref(inp),
+                                            ctypes.byref(st)), "hq_wire_step_stream")
+        n = inp.n_groups
+        grp = np.ctypeslib.as_array((ctypes.c_uint32 * max(1, n)).from_address(inp.groups))[:n] \
+            if n else np.zeros(0, np.uint32)
+        off = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(inp.offsets))
+        boff = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(inp.boffsets))
+        nb = int(boff[-1]) if n else 0
+        data = np.frombuffer((ctypes.c_char * nb).from_address(inp.bytes), np.uint8) if nb \
+            else np.zeros(0, np.uint8)
+        return grp.copy(), off.copy(), boff.copy(), data.copy(), st

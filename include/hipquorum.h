@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 8
+#define HQ_ABI_VERSION 9
 
 /* status codes */
 #define HQ_OK          0
@@ -787,6 +787,52 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *g,
                         uint32_t reads_cap);
 int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
 
+/* ---------------------------------------------------------------- event streams ------------- */
+/*
+ * The same step as a compact byte stream: group i's events are bytes[boffsets[i] ..
+ * boffsets[i + 1]), one after another, each a header byte and LEB128 varints of exactly the
+ * fields its handler reads. A steady-state leader step (ReplicateResp / HeartbeatResp /
+ * proposals at the group's term) takes 3-7 bytes per event instead of the 56-byte row, so a
+ * device worker's step crosses PCIe ~10x faster; the producer (a transport decoder, the caller's
+ * own event queue, hq_wire_step_stream) writes it directly, or hq_events_encode turns rows into it.
+ *
+ *   header  bits 0-2  kind (HQ_EV_*; 0, 6, 7: not a valid kind -> the group falls back)
+ *           bits 3-5  HQ_EV_MESSAGE: type code 0 ReplicateResp, 1 RequestVoteResp,
+ *                     2 HeartbeatResp, 3 ReadIndex, 7 another type (its varint follows)
+ *           bit 6     reject
+ *           bit 7     term repeats the group's previous message term in the stream (0 before
+ *                     its first message): the term varint is left out
+ *   READ: hint, hint_high      PROPOSE: log_index      CHECK_QUORUM, ELECTION: nothing
+ *   MESSAGE: [type], from, [term], then ReplicateResp: log_index; RequestVoteResp: nothing;
+ *            HeartbeatResp, ReadIndex: hint, hint_high; another type: log_index, hint, hint_high
+ * Fields a handler does not read are not carried (hq_events_decode returns them as 0). Event
+ * indexes (offsets, deferred) count events as in hq_step_input.
+ */
+#define HQ_EVENT_STREAM_MAX 64u   /* bytes one event takes at most */
+
+typedef struct hq_step_stream {
+    uint64_t n_groups;
+    const uint32_t *groups;
+    const uint64_t *offsets;     /* [n_groups + 1] event index prefix, as hq_step_input */
+    const uint64_t *boffsets;    /* [n_groups + 1] byte prefix into bytes, non-decreasing */
+    const uint8_t *bytes;
+} hq_step_stream;
+
+/* Encode rows (offsets as in hq_step_input) into out[0 .. cap) and boffsets[0 .. n_groups];
+ * HQ_E_STATE when fewer than HQ_EVENT_STREAM_MAX bytes are left before an event (size out for
+ * HQ_EVENT_STREAM_MAX per event to never hit it). */
+int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
+                     uint8_t *out, uint64_t cap, uint64_t *boffsets);
+/* Decode a stream back into rows events[offsets[0] .. offsets[n_groups]); HQ_E_INVAL when a
+ * group's bytes do not hold exactly its events. */
+int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t *boffsets,
+                     const uint8_t *bytes, hq_event *events);
+/* hq_worker_step over a stream. An HQ_WORKER_ON_DEVICE worker ships the bytes and its device
+ * engine decodes them (a group whose bytes are malformed falls back at the event that fails to
+ * decode); a host worker decodes them into rows first (HQ_E_INVAL on malformed bytes). Inputs in
+ * pinned memory (hq_alloc_pinned) copy fastest. */
+int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output *out);
+
 /* ---------------------------------------------------------------- wire decode --------------- */
 /*
  * The step worker's input from the wire. A host receives raftpb.MessageBatch bytes (the protobuf
@@ -855,6 +901,8 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len);
 /* The step's hq_step_input for `worker`: clusters in order of first appearance, each with its
  * events in node.handleEvents order. Arrays owned by w until its next reset / step_input. */
 int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wire_stats *stats);
+/* The same step as an event stream (see "event streams" above); arrays owned by w likewise. */
+int hq_wire_step_stream(hq_wire *w, hq_worker *worker, hq_step_stream *out, hq_wire_stats *stats);
 
 /* ---------------------------------------------------------------- synthetic inputs ---------- */
 

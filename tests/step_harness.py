@@ -60,8 +60,12 @@ class OracleBackend:
 
 
 class WorkerBackend:
-    def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False):
+    """stream=True: the step's events go in as an event stream (hq_events_encode ->
+    hq_worker_step_stream) instead of rows."""
+
+    def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False, stream=False):
         self.hq = hq
+        self.stream = stream
         self.w = worker if worker is not None else hq.Worker(0, n_max, on_device=on_device)
         self.rng = np.random.default_rng(seed)
         self.cids = []
@@ -90,12 +94,16 @@ class WorkerBackend:
                 refs[len(recs)] = (cid, pos)
                 recs.append(event_record(hq, e))
             offsets.append(len(recs))
-        return (np.array(handles, np.uint32), np.array(offsets, np.uint64),
-                np.array(recs, hq.EVENT_DTYPE)), refs
+        grp, off = np.array(handles, np.uint32), np.array(offsets, np.uint64)
+        ev = np.array(recs, hq.EVENT_DTYPE)
+        if self.stream:
+            data, boff = hq.encode_events(off, ev)
+            return (grp, off, boff, data), refs
+        return (grp, off, ev), refs
 
     def step(self, per_group):
         arrs, refs = self.build_inputs(per_group)
-        res = self.w.step(*arrs)
+        res = self.w.step(*arrs) if len(arrs) == 3 else self.w.step_stream(*arrs)
         self.last_passes, self.last_decisions = res["gpu_passes"], res["decisions"]
         self.last_raw = res
         out = {cid: {"ready": [], "resps": [], "states": [], "dropped": [], "deferred": [],
@@ -151,8 +159,8 @@ class WireBackend(WorkerBackend):
 
     DEPLOYMENT = 0x5EED
 
-    def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False):
-        super().__init__(hq, n_max, seed, worker, on_device)
+    def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False, stream=False):
+        super().__init__(hq, n_max, seed, worker, on_device, stream)
         self.wire = hq.Wire(self.DEPLOYMENT)
         self.last_stats = None
 
@@ -200,7 +208,10 @@ class WireBackend(WorkerBackend):
             wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT, source_address=b"n2:1"))
             if i == 0:   # a foreign deployment's batch: dropped whole (transport.go:291-295)
                 wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT + 1))
-        grp, off, ev, st = wire.step_input(self.w)
+        if self.stream:                       # hq_wire_step_stream
+            grp, off, boff, data, st = wire.step_stream(self.w)
+        else:
+            grp, off, ev, st = wire.step_input(self.w)
         self.last_stats = st
         # event index -> (cluster, position in its per_group list): the assembled rows keep
         # node.handleEvents order, as the per_group lists do
@@ -213,4 +224,4 @@ class WireBackend(WorkerBackend):
             assert int(off[i + 1]) - int(off[i]) == len(per_group[cid])
         assert sorted(handle_cid[int(h)] for h in grp) == sorted(c for c in cids
                                                                  if per_group[c])
-        return (grp, off, ev), refs
+        return ((grp, off, boff, data) if self.stream else (grp, off, ev)), refs

@@ -16,11 +16,14 @@ CASES = list(sc.all_cases())
 
 MODES = [False, True]
 MODE_IDS = ["host", "device"]      # the host worker / HQ_WORKER_ON_DEVICE (hq_dstep.hip)
+# (on_device, stream): events as rows or as an event stream (hq_worker_step_stream)
+FEEDS = [(False, False), (True, False), (True, True), (False, True)]
+FEED_IDS = ["host", "device", "device-stream", "host-stream"]
 
 
-@pytest.fixture(scope="module", params=MODES, ids=MODE_IDS)
+@pytest.fixture(scope="module", params=FEEDS, ids=FEED_IDS)
 def worker_backend(hq, request):
-    b = WorkerBackend(hq, n_max=8, seed=1, on_device=request.param)
+    b = WorkerBackend(hq, n_max=8, seed=1, on_device=request.param[0], stream=request.param[1])
     yield b
     b.close()
 
@@ -56,12 +59,14 @@ def test_one_gpu_pass_per_plain_step(hq, on_device):
         b.close()
 
 
-@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+@pytest.mark.parametrize("feed", FEEDS, ids=FEED_IDS)
 @pytest.mark.parametrize("seed,G,steps", [(1, 3000, 6), (2, 1500, 10), (3, 400, 25)])
-def test_random_differential(hq, seed, G, steps, on_device):
+def test_random_differential(hq, seed, G, steps, feed):
+    on_device, stream = feed
     rng = np.random.default_rng(seed)
     groups = sr.random_groups(rng, G)
-    o, w = OracleBackend(), WorkerBackend(hq, n_max=8, seed=seed, on_device=on_device)
+    o, w = OracleBackend(), WorkerBackend(hq, n_max=8, seed=seed, on_device=on_device,
+                                          stream=stream)
     try:
         for g in groups:
             o.add_group(*g)
@@ -148,11 +153,11 @@ def test_add_group_validation(hq, on_device):
 
 
 # ---- the same worker driven from wire bytes (raftpb.MessageBatch, hq_wire) --------------------
-@pytest.fixture(scope="module", params=MODES, ids=MODE_IDS)
+@pytest.fixture(scope="module", params=FEEDS, ids=FEED_IDS)
 def wire_backend(hq, request):
     from step_harness import WireBackend
 
-    b = WireBackend(hq, n_max=8, seed=5, on_device=request.param)
+    b = WireBackend(hq, n_max=8, seed=5, on_device=request.param[0], stream=request.param[1])
     yield b
     b.close()
 
@@ -169,14 +174,15 @@ def test_reference_scenario_from_wire_bytes(wire_backend, case):
             assert w[k] == o[k], (case["name"], k, w[k], o[k])
 
 
-@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+@pytest.mark.parametrize("feed", FEEDS, ids=FEED_IDS)
 @pytest.mark.parametrize("seed,G,steps", [(11, 1500, 6), (12, 300, 15)])
-def test_random_differential_from_wire_bytes(hq, seed, G, steps, on_device):
+def test_random_differential_from_wire_bytes(hq, seed, G, steps, feed):
     from step_harness import WireBackend
 
     rng = np.random.default_rng(seed)
     groups = sr.random_groups(rng, G)
-    o, w = OracleBackend(), WireBackend(hq, n_max=8, seed=seed, on_device=on_device)
+    o, w = OracleBackend(), WireBackend(hq, n_max=8, seed=seed, on_device=feed[0],
+                                        stream=feed[1])
     try:
         for g in groups:
             o.add_group(*g)
@@ -212,5 +218,36 @@ def test_device_worker_member_cap(hq):
         with pytest.raises(hq.HQError, match="16 members"):
             w.add_group(1, 1, 1, 0, 0, 0, 0, mem)
         w.add_group(2, 1, 1, 0, 0, 0, 0, mem[:16])
+    finally:
+        w.close()
+
+
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_malformed_stream(hq, on_device):
+    """A device worker falls the group back at the event that does not decode (the events
+    before it taken); a host worker rejects the step."""
+    w = hq.Worker(0, 4, on_device=on_device)
+    try:
+        w.add_group(1, 1, 2, sc.LEADER, 5, 6, 5, [(1, 6, 0, 0), (2, 5, 0, 0), (3, 5, 0, 0)])
+        w.add_group(2, 1, 2, sc.LEADER, 5, 6, 5, [(1, 6, 0, 0), (2, 5, 0, 0), (3, 5, 0, 0)])
+        ev = np.array([(hq.EV_MESSAGE, sc.RREP, 2, 2, 6, 0, 0, 0, 0),
+                       (hq.EV_MESSAGE, sc.RREP, 3, 2, 6, 0, 0, 0, 0),
+                       (hq.EV_MESSAGE, sc.RREP, 2, 2, 6, 0, 0, 0, 0)], hq.EVENT_DTYPE)
+        off = np.array([0, 2, 3], np.uint64)
+        data, boff = hq.encode_events(off, ev)
+        # group 0's second event cut short: its last varint loses its final byte
+        cut = np.concatenate([data[:int(boff[1]) - 1], data[int(boff[1]):]])
+        boff2 = boff.copy()
+        boff2[1:] -= 1
+        grp = np.array([w.find(1), w.find(2)], np.uint32)
+        if not on_device:
+            with pytest.raises(hq.HQError, match="malformed"):
+                w.step_stream(grp, off, boff2, cut)
+            return
+        res = w.step_stream(grp, off, boff2, cut)
+        assert list(res["fallback_groups"]) == [1] and list(res["deferred"]) == [1]
+        assert w.get_group(2)[0]["committed"] == 6       # the other group is unaffected
+        g1 = w.get_group(1)[0]                            # its first ack was taken
+        assert g1["committed"] == 6 and g1["suspended"] == 1
     finally:
         w.close()

@@ -1,0 +1,119 @@
+"""The event stream (include/hipquorum.h "event streams", dragonboat_amd/csrc/hq_stream.cpp):
+rows -> bytes -> rows keeps every field a handler reads (the others come back 0), steady-state
+events take a few bytes, and malformed streams are rejected. CPU only (host encoder/decoder);
+the device decoder is checked against these bytes through the step worker in
+tests/test_gpu_worker.py (device-stream feeds)."""
+import numpy as np
+import pytest
+
+RREP, VRESP, HBRESP, READIDX = 13, 15, 18, 19
+
+
+def carried(hq, ev):
+    """The fields the stream carries for each row (the rest zeroed), as the decoder returns."""
+    out = np.zeros_like(ev)
+    kind = ev["kind"].copy()
+    kind[(kind < 1) | (kind > 5)] = 0
+    out["kind"] = kind
+    rd = kind == hq.EV_READ
+    pr = kind == hq.EV_PROPOSE
+    ms = kind == hq.EV_MESSAGE
+    out["hint"][rd], out["hint_high"][rd] = ev["hint"][rd], ev["hint_high"][rd]
+    out["log_index"][pr] = ev["log_index"][pr]
+    t = ev["type"]
+    known = np.isin(t, [RREP, VRESP, HBRESP, READIDX])
+    out["type"][ms] = t[ms]
+    out["reject"][ms] = ev["reject"][ms] != 0
+    out["from"][ms], out["term"][ms] = ev["from"][ms], ev["term"][ms]
+    li = ms & ((t == RREP) | ~known)
+    out["log_index"][li] = ev["log_index"][li]
+    hh = ms & (((t == HBRESP) | (t == READIDX)) | ~known)
+    out["hint"][hh], out["hint_high"][hh] = ev["hint"][hh], ev["hint_high"][hh]
+    return out
+
+
+def random_rows(rng, ne):
+    ev = np.zeros(ne, dtype=[("kind", "<u4"), ("type", "<u4"), ("from", "<u8"),
+                             ("term", "<u8"), ("log_index", "<u8"), ("hint", "<u8"),
+                             ("hint_high", "<u8"), ("reject", "<u4"), ("reserved", "<u4")])
+    ev["kind"] = rng.choice([0, 1, 2, 2, 2, 2, 3, 4, 5, 6, 9], ne)
+    ev["type"] = rng.choice([RREP, VRESP, HBRESP, READIDX, 1, 22, 1 << 31], ne)
+    big = lambda: np.where(rng.random(ne) < 0.2, rng.integers(0, 2**63, ne, dtype=np.uint64) * 2
+                           + 1, rng.integers(0, 300, ne).astype(np.uint64))
+    for k in ("from", "log_index", "hint", "hint_high"):
+        ev[k] = big()
+    ev["term"] = np.where(rng.random(ne) < 0.7, 7, big())        # mostly repeating
+    ev["reject"] = rng.choice([0, 0, 1, 5], ne)
+    ev["reserved"] = rng.integers(0, 9, ne)
+    return ev
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_round_trip(hq, seed):
+    rng = np.random.default_rng(seed)
+    n = 500
+    counts = rng.integers(0, 12, n)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    ev = random_rows(rng, int(off[-1])).view(hq.EVENT_DTYPE)
+    data, boff = hq.encode_events(off, ev)
+    assert boff[0] == 0 and np.all(np.diff(boff.astype(np.int64)) >= 0)
+    assert len(data) <= len(ev) * hq.HQ_EVENT_STREAM_MAX
+    back = hq.decode_events(off, boff, data)
+    want = carried(hq, ev)
+    for k in ("kind", "type", "from", "term", "log_index", "hint", "hint_high", "reject"):
+        np.testing.assert_array_equal(back[k], want[k], err_msg=k)
+    assert (back["reserved"] == 0).all()
+
+
+def test_steady_state_sizes(hq):
+    """A leader's steady step: ReplicateResp / HeartbeatResp at the group's term, a proposal."""
+    ev = np.zeros(6, hq.EVENT_DTYPE)
+    ev[0] = (hq.EV_MESSAGE, RREP, 2, 41, 1_000_000, 0, 0, 0, 0)     # first message: the term
+    ev[1] = (hq.EV_MESSAGE, RREP, 3, 41, 1_000_001, 0, 0, 0, 0)     # same term: 1 + 1 + 3
+    ev[2] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 0, 0, 0, 0)           # ctx-less heartbeat ack
+    ev[3] = (hq.EV_CHECK_QUORUM, 0, 0, 0, 0, 0, 0, 0, 0)
+    ev[4] = (hq.EV_PROPOSE, 0, 0, 0, 3, 0, 0, 0, 0)
+    ev[5] = (hq.EV_READ, 0, 0, 0, 0, 77, 0, 0, 0)
+    off = np.array([0, 6], np.uint64)
+    data, boff = hq.encode_events(off, ev)
+    sizes = []
+    for i in range(6):                     # per-event sizes from prefixes
+        d, _ = hq.encode_events(np.array([0, i + 1], np.uint64), ev[:i + 1])
+        sizes.append(len(d))
+    sizes = np.diff([0] + sizes)
+    assert list(sizes) == [1 + 1 + 1 + 3, 1 + 1 + 3, 1 + 1 + 1 + 1, 1, 2, 3]
+    assert len(data) == sum(sizes) and int(boff[1]) == len(data)
+
+
+def test_empty_and_groups_without_events(hq):
+    off = np.array([0, 0, 0], np.uint64)
+    data, boff = hq.encode_events(off, np.zeros(0, hq.EVENT_DTYPE))
+    assert len(data) == 0 and list(boff) == [0, 0, 0]
+    assert len(hq.decode_events(off, boff, data)) == 0
+
+
+def test_malformed_rejected(hq):
+    ev = np.zeros(2, hq.EVENT_DTYPE)
+    ev[0] = (hq.EV_MESSAGE, RREP, 2, 41, 1_000_000, 0, 0, 0, 0)
+    ev[1] = (hq.EV_READ, 0, 0, 0, 0, 5, 6, 0, 0)
+    off = np.array([0, 2], np.uint64)
+    data, boff = hq.encode_events(off, ev)
+    with pytest.raises(hq.HQError):                          # truncated
+        hq.decode_events(off, np.array([0, len(data) - 1], np.uint64), data[:-1])
+    with pytest.raises(hq.HQError):                          # trailing bytes
+        hq.decode_events(off, np.array([0, len(data) + 1], np.uint64),
+                         np.concatenate([data, [0]]).astype(np.uint8))
+    over = np.concatenate([data[:1], [0xFF] * 11, data[1:]]).astype(np.uint8)
+    with pytest.raises(hq.HQError):                          # a varint over 64 bits
+        hq.decode_events(off, np.array([0, len(over)], np.uint64), over)
+
+
+def test_encode_capacity(hq):
+    ev = np.zeros(3, hq.EVENT_DTYPE)
+    ev["kind"] = hq.EV_CHECK_QUORUM
+    off = np.array([0, 3], np.uint64)
+    out = np.zeros(hq.HQ_EVENT_STREAM_MAX + 1, np.uint8)     # room checked per event
+    boff = np.zeros(2, np.uint64)
+    rc = hq.lib.hq_events_encode(1, off.ctypes.data, ev.ctypes.data, out.ctypes.data,
+                                 len(out), boff.ctypes.data)
+    assert rc == hq.HQ_E_STATE
