@@ -45,6 +45,8 @@ struct hq_dstep_out {                 // the lists of one step, in input group o
     const uint64_t *fallback;
     uint64_t n_commits, n_ready, n_resps, n_states, n_dropped, n_deferred, n_fallback;
     uint64_t decisions;
+    uint32_t input_error;             // HQ_E_INVAL: bit 1 unknown handle, 2 offsets, 4 boffsets,
+                                      // 8 a group listed twice (no group state written)
     uint64_t kernel_ns, d2h_ns;       // wall time: H2D + pass A + scan + bases; pass B + D2H
 };
 
@@ -66,5 +68,5 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
                  uint64_t m0, uint64_t nm, const hq_dmember *m);
 // copy the first ng group records (with their reads) and nm member records back
 int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t nm, hq_dmember *m);
-// one step over the device state (the input is already validated)
+// one step over the device state; the kernels check the input (out->input_error)
 int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out);

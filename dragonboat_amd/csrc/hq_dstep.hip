@@ -30,12 +30,19 @@ namespace {
 
 enum List { kCommits, kReady, kResps, kStates, kDropped, kDeferred, kFallback, kDecisions,
             kLists };
+// the worker's input checks, taken by pass A (which writes no group state) before pass B runs
+enum InputError : uint32_t { kErrHandle = 1, kErrOffsets = 2, kErrBoffsets = 4, kErrTwice = 8 };
 
 struct StepK {
     hq_dgroup *groups;
     hq_dmember *members;
     hq_dread *reads;
     uint64_t n;                   // groups listed in this step
+    uint64_t n_handles;           // groups on the device (valid handles)
+    uint64_t n_events, n_bytes;   // input sizes (rows or stream bytes)
+    uint32_t *stamp;              // per handle: the last step that listed it
+    uint32_t step_no;
+    uint32_t *error;              // pass A: input errors (kErr* bits)
     const uint32_t *handles;
     const uint64_t *offsets;
     const hq_event *events;       // rows, or
@@ -382,6 +389,21 @@ __global__ __launch_bounds__(256) void k_step(const StepK a) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t h = a.handles[i];
+    if (!WRITE) {                 // validate this group's entry; a bad one is not stepped
+        uint32_t err = 0;
+        if (h >= a.n_handles) err |= kErrHandle;
+        if (a.offsets[i + 1] < a.offsets[i] || (!STREAM && a.offsets[i + 1] > a.n_events))
+            err |= kErrOffsets;
+        if (STREAM && (a.boffsets[i + 1] < a.boffsets[i] || a.boffsets[i + 1] > a.n_bytes))
+            err |= kErrBoffsets;
+        if (!(err & kErrHandle) && atomicExch(a.stamp + h, a.step_no) == a.step_no)
+            err |= kErrTwice;
+        if (err) {
+            atomicOr(a.error, err);
+            for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = 0;
+            return;
+        }
+    }
     Engine<WRITE> eng(a, i, h);
     if (STREAM)
         eng.template run<true>(a.offsets[i], a.offsets[i + 1], a.bytes + a.boffsets[i],
@@ -395,10 +417,12 @@ __global__ __launch_bounds__(256) void k_step(const StepK a) {
     }
 }
 
-// the start of every list in the scanned counts, and the grand total
-__global__ void k_list_bases(const uint32_t *scan, uint64_t n, uint32_t *bases) {
+// the start of every list in the scanned counts, the grand total, and the input errors
+__global__ void k_list_bases(const uint32_t *scan, uint64_t n, const uint32_t *error,
+                             uint32_t *bases) {
     const int l = threadIdx.x;
     if (l <= kLists) bases[l] = scan[(uint64_t)l * n];
+    if (l == kLists + 1) bases[l] = *error;
 }
 
 uint64_t now_ns() {
@@ -414,7 +438,10 @@ struct hq_dstep {
     hq_dgroup *groups = nullptr;
     hq_dread *reads = nullptr;
     hq_dmember *members = nullptr;
+    uint32_t *stamp = nullptr;    // [gcap] step stamps (duplicate handles)
     uint64_t gcap = 0, mcap = 0;
+    uint64_t n_groups = 0;        // group records uploaded (valid handles)
+    uint32_t step_no = 0;
     // step staging
     void *in = nullptr;
     size_t in_cap = 0;
@@ -458,7 +485,7 @@ void hq_dstep_close(hq_dstep *d) {
     if (!d) return;
     (void)hipSetDevice(d->ctx->device);
     (void)hipStreamSynchronize(d->ctx->stream);
-    for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, d->in,
+    for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, (void *)d->stamp, d->in,
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp, d->out})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
@@ -477,7 +504,16 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
         if (!rc)
             rc = grow(ctx, reinterpret_cast<void **>(&d->reads), &rcap,
                       (g0 + ng) * kDReads * sizeof(hq_dread), true, "hq_dstep reads");
-        if (!rc) d->gcap = std::min(gc / sizeof(hq_dgroup), rcap / (kDReads * sizeof(hq_dread)));
+        size_t sc = d->gcap * 4;
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->stamp), &sc, (g0 + ng) * 4, true,
+                      "hq_dstep stamps");
+        if (!rc) d->gcap = std::min({gc / sizeof(hq_dgroup), rcap / (kDReads * sizeof(hq_dread)),
+                                     sc / 4});
+    }
+    if (!rc && ng) {              // new stamps start at 0 (no step has listed them)
+        rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp + g0, 0, ng * 4, ctx->stream), "memset");
+        if (!rc && g0 + ng > d->n_groups) d->n_groups = g0 + ng;
     }
     if (!rc && (m0 + nm) > d->mcap) {
         rc = grow(ctx, reinterpret_cast<void **>(&d->members), &mc,
@@ -575,8 +611,20 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     }
     k.counts = d->counts;
     k.scan = d->scan;
+    k.n_handles = d->n_groups;
+    k.n_events = ne;
+    k.n_bytes = nb;
+    k.stamp = d->stamp;
+    if (++d->step_no == 0) {      // stamps wrap: forget them
+        rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp, 0, d->gcap * 4, ctx->stream), "memset");
+        d->step_no = 1;
+        if (rc) return rc;
+    }
+    k.step_no = d->step_no;
+    k.error = d->bases + kLists + 2;
     const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
     rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
+    if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(k.error, 0, 4, ctx->stream), "memset");
     if (!rc) rc = hq::pre_launch(ctx);
     if (rc) return rc;
     if (stream) hipLaunchKernelGGL((k_step<false, true>), grid, blk, 0, ctx->stream, k);
@@ -586,14 +634,19 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
                                                                        d->scan, cn, ctx->stream),
                                 "hipcub scan");
     if (!rc) {
-        hipLaunchKernelGGL(k_list_bases, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, d->bases);
+        hipLaunchKernelGGL(k_list_bases, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, k.error,
+                           d->bases);
         rc = hq::check_hip(ctx, hipGetLastError(), "k_list_bases");
     }
-    uint32_t bases[kLists + 1];
+    uint32_t bases[kLists + 2];
     if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(bases, d->bases, sizeof bases,
                                                     hipMemcpyDeviceToHost, ctx->stream), "D2H");
     if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
     if (rc) return rc;
+    if (bases[kLists + 1]) {      // no group state was written
+        out->input_error = bases[kLists + 1];
+        return HQ_E_INVAL;
+    }
     const uint64_t t1 = now_ns();
     uint64_t len[kLists];
     for (int l = 0; l < kLists; ++l) len[l] = bases[l + 1] - bases[l];

@@ -98,8 +98,6 @@ struct hq_worker {
     bool host_stale = false;              // the device holds newer state than the mirror
     uint64_t dev_groups = 0, dev_members = 0;   // records already on the device
     std::vector<uint32_t> dirty;          // handles changed on the host since the last upload
-    std::vector<uint64_t> stamp;          // step stamp per handle (a group listed twice)
-    uint64_t step_no = 0;
     hq_dstep_out dout{};
     std::vector<hq_event> decoded;        // host worker: a stream step's rows
     std::string err;
@@ -870,22 +868,20 @@ int hq_worker::sync_from_device() {
 
 int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     const uint64_t t0 = now_ns();
-    if (stamp.size() < groups.size()) stamp.resize(groups.size(), 0);
-    ++step_no;
-    for (uint64_t i = 0; i < inp.n; ++i) {           // the host worker's input checks
-        const uint32_t gi = inp.groups[i];
-        if (gi >= groups.size()) return fail(HQ_E_INVAL, "hq_worker_step: unknown group handle");
-        if (inp.offsets[i + 1] < inp.offsets[i])
-            return fail(HQ_E_INVAL, "hq_worker_step: offsets decrease");
-        if (inp.boffsets && inp.boffsets[i + 1] < inp.boffsets[i])
-            return fail(HQ_E_INVAL, "hq_worker_step_stream: boffsets decrease");
-        if (stamp[gi] == step_no) return fail(HQ_E_INVAL, "hq_worker_step: a group is listed twice");
-        stamp[gi] = step_no;
-    }
+    // the per-group input checks (handles, offsets, a group listed twice) run in the engine's
+    // first kernel, before any group state is written
     int rc = sync_to_device();
     if (rc) return rc;
     const uint64_t t1 = now_ns();
-    rc = hq(hq_dstep_run(dstep, &inp, &dout), "hq_dstep_run");
+    rc = hq_dstep_run(dstep, &inp, &dout);
+    if (rc == HQ_E_INVAL && dout.input_error) {
+        const uint32_t e = dout.input_error;
+        return fail(HQ_E_INVAL, e & 1 ? "hq_worker_step: unknown group handle"
+                                : e & 8 ? "hq_worker_step: a group is listed twice"
+                                : e & 2 ? "hq_worker_step: offsets decrease"
+                                        : "hq_worker_step_stream: boffsets decrease");
+    }
+    rc = hq(rc, "hq_dstep_run");
     if (rc) return rc;
     host_stale = true;
     const uint64_t t2 = now_ns();
@@ -1092,6 +1088,9 @@ int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output
     if (w->dstep)
         return w->step_on_device(hq_dstep_in{in->n_groups, in->groups, in->offsets, nullptr,
                                              in->boffsets, in->bytes ? in->bytes : &none}, out);
+    for (uint64_t i = 0; i < in->n_groups; ++i)
+        if (in->offsets[i + 1] < in->offsets[i])
+            return w->fail(HQ_E_INVAL, "hq_worker_step: offsets decrease");
     const uint64_t ne = in->n_groups ? in->offsets[in->n_groups] : 0;
     w->decoded.resize(ne);
     if (in->n_groups && hq_events_decode(in->n_groups, in->offsets, in->boffsets, in->bytes,

@@ -251,3 +251,33 @@ def test_malformed_stream(hq, on_device):
         assert g1["committed"] == 6 and g1["suspended"] == 1
     finally:
         w.close()
+
+
+@pytest.mark.parametrize("feed", FEEDS, ids=FEED_IDS)
+def test_step_input_errors_leave_state(hq, feed):
+    """Bad step inputs are rejected whole (HQ_E_INVAL) with no group state changed: an unknown
+    handle, a group listed twice, decreasing offsets."""
+    on_device, stream = feed
+    w = hq.Worker(0, 4, on_device=on_device)
+    try:
+        for cid in (1, 2):
+            w.add_group(cid, 1, 2, sc.LEADER, 5, 6, 5, [(1, 6, 0, 0), (2, 5, 0, 0), (3, 5, 0, 0)])
+        ev = np.array([(hq.EV_MESSAGE, sc.RREP, 2, 2, 6, 0, 0, 0, 0)] * 2, hq.EVENT_DTYPE)
+
+        def step(grp, off):
+            grp, off = np.array(grp, np.uint32), np.array(off, np.uint64)
+            if stream:                   # each group's one event: 4 bytes
+                data, boff = hq.encode_events(np.array([0, 1, 2], np.uint64), ev)
+                return w.step_stream(grp, off, boff, data)
+            return w.step(grp, off, ev)
+
+        for grp, off, msg in (([0, 7], [0, 1, 2], "unknown group handle"),
+                              ([1, 1], [0, 1, 2], "listed twice"),
+                              ([0, 1], [0, 2, 1], "offsets decrease")):
+            with pytest.raises(hq.HQError, match=msg):
+                step(grp, off)
+            assert w.get_group(1)[0]["committed"] == 5 and w.get_group(2)[0]["committed"] == 5
+        res = step([1, 0], [0, 1, 2])                        # and the worker still steps
+        assert sorted(int(c["cluster_id"]) for c in res["commits"]) == [1, 2]
+    finally:
+        w.close()
