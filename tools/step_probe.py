@@ -1,38 +1,62 @@
-"""Probe: the device step engine on the bench's step workload (1M leader groups), one worker,
-events in pinned memory (FEED=stream: as the event stream, FEED=rows: as hq_event rows); prints
-per-step wall time. Run under rocprofv3 --kernel-trace --stats for the kernels' share."""
+"""Probe: the device step engine on the bench's step workload (G = 1M leader groups), W workers
+(one thread each, G / W groups each), events in pinned memory (FEED=stream: as the event
+stream, FEED=rows: as hq_event rows); prints per-step wall time. Run under rocprofv3
+--kernel-trace --stats for the kernels' share."""
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
 from dragonboat_amd import hipquorum as hq  # noqa: E402
 
 G = int(os.environ.get("G", 1 << 20))
+W = int(os.environ.get("W", 1))
+STEPS = int(os.environ.get("STEPS", 6))
 roles = bench.STEP_ROLES[os.environ.get("LEG", "step")]
-g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
-w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True)
-w.add_groups(g, m)
-pc = hq.Context(0)
 stream = os.environ.get("FEED", "stream") == "stream"
-for s in range(6):
-    e = bench.step_events(hq, G, s, roles)
-    ne = len(e[2])
-    if stream:
-        data, boff = hq.encode_events(e[1], e[2])
-        e = (e[0], e[1], boff, data)
-    p = tuple(pc.pinned(x.size, x.dtype) for x in e)
-    for dst, src in zip(p, e):
-        dst[:] = src
+bounds = [G * i // W for i in range(W + 1)]
+g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
+nm = len(roles)
+workers = []
+for i in range(W):
+    w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True)
+    w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
+    workers.append(w)
+pc = hq.Context(0)
+for s in range(STEPS):
+    inputs, ne = [], 0
+    for i in range(W):
+        e = bench.step_events(hq, bounds[i + 1] - bounds[i], s, roles)
+        ne += len(e[2])
+        if stream:
+            data, boff = hq.encode_events(e[1], e[2])
+            e = (e[0], e[1], boff, data)
+        p = tuple(pc.pinned(x.size, x.dtype) for x in e)
+        for dst, src in zip(p, e):
+            dst[:] = src
+        inputs.append(p)
+    res = [None] * W
+
+    def run(i):
+        w = workers[i]
+        res[i] = w.step_stream(*inputs[i], copy=False) if stream else \
+            w.step(*inputs[i], copy=False)
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(W)]
     t0 = time.perf_counter()
-    r = w.step_stream(*p, copy=False) if stream else w.step(*p, copy=False)
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
     dt = time.perf_counter() - t0
-    print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, "
-          f"device {r['device_ns'] / 1e6:.2f} ms, input {sum(x.nbytes for x in p) / 1e6:.1f} MB",
+    dev = max(r["device_ns"] for r in res) / 1e6
+    print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, W={W}, "
+          f"max device {dev:.2f} ms, input {sum(x.nbytes for p in inputs for x in p) / 1e6:.1f} MB",
           flush=True)
-w.close()
+for w in workers:
+    w.close()
 pc.close()
