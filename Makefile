@@ -6,12 +6,12 @@ CSRC := dragonboat_amd/csrc
 LIBDIR := dragonboat_amd/lib
 LIB := $(LIBDIR)/libhipquorum.so
 OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o $(LIBDIR)/hq_table.o $(LIBDIR)/hq_pack.o \
-        $(LIBDIR)/hq_worker.o $(LIBDIR)/hq_wire.o $(LIBDIR)/hq_stream.o $(LIBDIR)/hq_dstep.o
+        $(LIBDIR)/hq_worker.o $(LIBDIR)/hq_wire.o $(LIBDIR)/hq_stream.o $(LIBDIR)/hq_jobs.o $(LIBDIR)/hq_dstep.o
 SRCS := $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp \
-        $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_stream.cpp $(CSRC)/hq_dstep.hip
+        $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_stream.cpp $(CSRC)/hq_jobs.cpp $(CSRC)/hq_dstep.hip
 DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
 CXX ?= g++
-CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -pthread -Wall -Wextra
 
 all: $(LIB) oracle
 
@@ -25,7 +25,7 @@ $(LIBDIR)/%.o: $(CSRC)/%.cpp $(DEPS)
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
 
 $(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -pthread -o $@ $(OBJS)
 
 oracle:
 	$(MAKE) -C oracle

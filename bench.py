@@ -775,15 +775,13 @@ def step_events(hq, G, s, roles=STEP_ROLES["step"], last0=1000):
 
 
 def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, stream=False):
-    """W workers (one host thread each, own HIP stream) over G groups split into W contiguous
+    """W workers (one native thread each, own HIP stream) over G groups split into W contiguous
     partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
     of the first 4096 groups after cpu_steps steps, ..., encode seconds). on_device:
     HQ_WORKER_ON_DEVICE workers, the step's input in pinned host memory (a step worker's receive
     buffers) so that it crosses PCIe at the link's rate. stream: the input is the event stream
     (hq_worker_step_stream), written by the producer — here hq_events_encode over the rows,
     outside the timed region and timed on its own (encode seconds)."""
-    import threading
-
     rng = _shard_of(d, G)
     g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
     nm = len(roles)
@@ -818,20 +816,11 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
                 for dst, src in zip(pinned[i], e):
                     dst[:src.size] = src
             evs = [tuple(p[k][:e[k].size] for k in range(len(e))) for p, e in zip(pinned, evs)]
-        res = [None] * W
-
-        def run(i):
-            if stream:
-                res[i] = workers[i].step_stream(*evs[i], copy=False)
-            else:
-                res[i] = workers[i].step(*evs[i], copy=False)
-
-        threads = [threading.Thread(target=run, args=(i,)) for i in range(W)]
+        # the W workers stepped at once on native threads (hq_worker_step_jobs), as W step-
+        # worker goroutines each calling its own worker
+        jobs = hq.StepJobs(list(zip(workers, evs)))
         t0 = time.perf_counter()
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
+        res = jobs.run(copy=False)
         dt = time.perf_counter() - t0
         if s == cpu_steps:   # state checked against the CPU replay of the same steps
             committed = [int(workers[0].get_group(int(c))[0]["committed"])

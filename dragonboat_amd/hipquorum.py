@@ -184,6 +184,13 @@ class StepStream(ctypes.Structure):
 
 HQ_EVENT_STREAM_MAX = 64
 
+
+class StepJob(ctypes.Structure):
+    """Mirror of ``hq_step_job``."""
+
+    _fields_ = [("worker", _vp), ("rows", _vp), ("stream", _vp), ("out", _vp),
+                ("rc", ctypes.c_int), ("reserved", ctypes.c_int)]
+
 STEP_OUTPUT_LISTS = [("commits", COMMIT_EVENT_DTYPE), ("ready", READY_DTYPE),
                      ("read_resps", READ_RESP_DTYPE), ("state_changes", STATE_CHANGE_DTYPE),
                      ("dropped_reads", DROPPED_READ_DTYPE), ("deferred", np.dtype("<u8")),
@@ -303,6 +310,7 @@ SIGNATURES = {
                                       ctypes.POINTER(StepOutput)]),
     "hq_worker_step_stream": (ctypes.c_int, [_vp, ctypes.POINTER(StepStream),
                                              ctypes.POINTER(StepOutput)]),
+    "hq_worker_step_jobs": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "hq_events_encode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
@@ -1170,6 +1178,49 @@ class Worker:
         assert int(groups["n_members"].sum()) == len(members)
         self._check(lib.hq_worker_add_groups(self.h, _p(groups), len(groups), _p(members)),
                     "hq_worker_add_groups")
+
+
+class StepJobs:
+    """hq_worker_step_jobs over prepared jobs: jobs = [(worker, (groups, offsets, events))]
+    (rows) or [(worker, (groups, offsets, boffsets, bytes))] (event stream). run() steps them
+    at once on native threads and returns one result dict per job (as Worker.step)."""
+
+    def __init__(self, jobs):
+        self.jobs = jobs
+        self.keep, self.arr = [], (StepJob * len(jobs))()
+        self.outs = [StepOutput() for _ in jobs]
+        for j, (w, a) in enumerate(jobs):
+            if len(a) == 3:
+                g, o, e = (np.ascontiguousarray(a[0], np.uint32),
+                           np.ascontiguousarray(a[1], np.uint64),
+                           np.ascontiguousarray(a[2], EVENT_DTYPE))
+                inp = StepInput(len(g), _p(g), _p(o), _p(e))
+                self.arr[j].rows = ctypes.cast(ctypes.pointer(inp), _vp)
+                self.keep += [g, o, e, inp]
+            else:
+                g, o, b, d = (np.ascontiguousarray(a[0], np.uint32),
+                              np.ascontiguousarray(a[1], np.uint64),
+                              np.ascontiguousarray(a[2], np.uint64),
+                              np.ascontiguousarray(a[3], np.uint8))
+                inp = StepStream(len(g), _p(g), _p(o), _p(b), _p(d) if len(d) else None)
+                self.arr[j].stream = ctypes.cast(ctypes.pointer(inp), _vp)
+                self.keep += [g, o, b, d, inp]
+            self.arr[j].worker = w.h
+            self.arr[j].out = ctypes.cast(ctypes.pointer(self.outs[j]), _vp)
+
+    def run(self, copy=True):
+        rc = lib.hq_worker_step_jobs(self.arr, len(self.jobs))
+        if rc != HQ_OK:
+            bad = [j for j in range(len(self.jobs)) if self.arr[j].rc != HQ_OK]
+            msg = lib.hq_worker_last_error(self.jobs[bad[0]][0].h).decode() if bad \
+                else "a worker listed twice"
+            raise HQError(rc, f"hq_worker_step_jobs: {msg}")
+        return [Worker._results(o, copy) for o in self.outs]
+
+
+def step_jobs(jobs, copy=True):
+    """StepJobs(jobs).run(copy)."""
+    return StepJobs(jobs).run(copy)
 
 
 def encode_events(offsets, events):

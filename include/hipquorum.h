@@ -833,6 +833,20 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
  * pinned memory (hq_alloc_pinned) copy fastest. */
 int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output *out);
 
+/* Several workers stepped at once, one native thread each (job 0 on the calling thread, the rest
+ * on a process-wide pool): what a host's step-worker goroutines do when each calls its own
+ * worker (execengine.go:923-1000). Each job names one of rows / stream. Every job's rc is set;
+ * returns the first failing rc (HQ_E_INVAL, nothing run, if a worker appears twice). */
+typedef struct hq_step_job {
+    hq_worker *worker;
+    const hq_step_input *rows;
+    const hq_step_stream *stream;
+    hq_step_output *out;
+    int rc;
+    int reserved;
+} hq_step_job;
+int hq_worker_step_jobs(hq_step_job *jobs, uint32_t count);
+
 /* ---------------------------------------------------------------- wire decode --------------- */
 /*
  * The step worker's input from the wire. A host receives raftpb.MessageBatch bytes (the protobuf

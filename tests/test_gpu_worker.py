@@ -281,3 +281,47 @@ def test_step_input_errors_leave_state(hq, feed):
         assert sorted(int(c["cluster_id"]) for c in res["commits"]) == [1, 2]
     finally:
         w.close()
+
+
+def test_step_jobs_equal_sequential_steps(hq):
+    """hq_worker_step_jobs: several workers (device and host, rows and streams) stepped at once
+    on native threads end in the same results and state as stepping them one by one."""
+    import bench
+
+    G = 3000
+    roles = bench.STEP_ROLES["step5"]
+    g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
+    nm, nv = len(roles), sum(r != "observer" for r in roles)
+    kinds = [(True, True), (True, False), (False, False), (True, True)]
+    bounds = [G * i // len(kinds) for i in range(len(kinds) + 1)]
+
+    def make():
+        ws = []
+        for i, (dev, _) in enumerate(kinds):
+            w = hq.Worker(0, nv, on_device=dev)
+            w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
+            ws.append(w)
+        return ws
+
+    a, b = make(), make()
+    try:
+        for s in range(3):
+            jobs = []
+            for i, (_, stream) in enumerate(kinds):
+                e = bench.step_events(hq, bounds[i + 1] - bounds[i], s, roles)
+                if stream:
+                    data, boff = hq.encode_events(e[1], e[2])
+                    e = (e[0], e[1], boff, data)
+                jobs.append(e)
+            got = hq.step_jobs(list(zip(a, jobs)))
+            for i, (w, e) in enumerate(zip(b, jobs)):
+                want = w.step(*e) if len(e) == 3 else w.step_stream(*e)
+                for k in ("commits", "ready", "read_resps", "state_changes", "dropped_reads",
+                          "deferred", "fallback_groups"):
+                    np.testing.assert_array_equal(got[i][k], want[k], err_msg=k)
+                assert len(want["commits"]) == (bounds[i + 1] - bounds[i] if s else 0)
+        with pytest.raises(hq.HQError):
+            hq.step_jobs([(a[0], jobs[0]), (a[0], jobs[0])])      # a worker twice
+    finally:
+        for w in a + b:
+            w.close()

@@ -1,10 +1,9 @@
 """Probe: the device step engine on the bench's step workload (G = 1M leader groups), W workers
-(one thread each, G / W groups each), events in pinned memory (FEED=stream: as the event
+(one native thread each via hq_worker_step_jobs, G / W groups each), events in pinned memory (FEED=stream: as the event
 stream, FEED=rows: as hq_event rows); prints per-step wall time. Run under rocprofv3
 --kernel-trace --stats for the kernels' share."""
 import os
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -39,19 +38,9 @@ for s in range(STEPS):
         for dst, src in zip(p, e):
             dst[:] = src
         inputs.append(p)
-    res = [None] * W
-
-    def run(i):
-        w = workers[i]
-        res[i] = w.step_stream(*inputs[i], copy=False) if stream else \
-            w.step(*inputs[i], copy=False)
-
-    threads = [threading.Thread(target=run, args=(i,)) for i in range(W)]
+    jobs = hq.StepJobs(list(zip(workers, inputs)))
     t0 = time.perf_counter()
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
+    res = jobs.run(copy=False)
     dt = time.perf_counter() - t0
     dev = max(r["device_ns"] for r in res) / 1e6
     print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, W={W}, "
