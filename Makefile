@@ -36,6 +36,8 @@ oracle:
 #   lib_mbN    grid cap (in 256-thread units) raised N x
 #   lib_ivN    records per lane of the table ingest kernels
 #   lib_b3tpwN tiles per wave of the 3-byte bitmap kernel
+#   lib_pltpwN tiles per wave of the bit-plane kernel
+#   lib_b3copy the 3-byte bitmap kernel's loads and stores without the decision (its floor)
 define variant
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(1) -shared -o $@ $(SRCS)
@@ -50,6 +52,10 @@ tools/lib_iv%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_INGEST_V=$*)
 tools/lib_b3tpw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_BITS3_TPW=$*)
+tools/lib_pltpw%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_PLANES_TPW=$*)
+tools/lib_b3copy/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_BITS3_COPY)
 
 variants: grid cap (in 256-thread units) raised 2x / 4x / 8x
 tools/lib_mb%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)

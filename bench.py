@@ -107,6 +107,10 @@ WORKLOADS = {
                  desc="as c4t over 3-byte tiles: the leader's own slot implicit (never acks its "
                       "ctx, always grants its vote), 7 bits per bitmap + 3 bits of n - 1 "
                       "(3.375 B per group instead of 4.375)"),
+    "c4p": dict(cfg=3, kind="bits", G=16 << 20, n=7, planes=True,
+                desc="as c4t3 over bit-plane tiles (the 3-byte tiles' bits transposed, 2048 "
+                     "groups per tile): 32 groups per lane decided with bitwise adders "
+                     "(3.375 B per group)"),
     "c5": dict(cfg=4, kind="commit", G=8 << 20, n=5, form=2, mixed=True,
                desc="64M groups mixed 3/5/7 voters (n = {3,5,7}[clusterID % 3]) sharded "
                     "clusterID % 8: 8M groups per GPU, the three voter-count buckets in one "
@@ -124,7 +128,7 @@ WORKLOADS = {
 # single-GPU commit config and the north star's 5-voter bar
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
-                  "c4,c4t,c4t3,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
+                  "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
                   "cq,ing,ingo,w2,e2e,step,step5")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
@@ -146,7 +150,7 @@ def algo_bytes_per_group(w):
                 + extra_n)
     # ack, granted, rejected (+ n unless uniform or packed into the 3-byte tiles) u8 each in;
     # confirmed bit + 2-bit outcome out
-    return (3 if w.get("uniform") or w.get("tiled3") else 4) + 3 / 8
+    return (3 if w.get("uniform") or w.get("tiled3") or w.get("planes") else 4) + 3 / 8
 
 
 def decisions_per_group(w):
@@ -290,7 +294,14 @@ def build_sets(ctx, hq, shard, w, d: "Dist"):
             conf = ctx.empty(hq.words64(G), np.uint64)
             outc = ctx.empty(hq.words32(G), np.uint64)
             tiles = None
-            if w.get("tiled3"):
+            if w.get("planes"):
+                tiles = ctx.empty(hq.plane_tiles(G) * 3 * hq.HQ_PLANE_TILE_GROUPS, np.uint8)
+                ctx.tile_planes_dev(G, *arrs, 0, tiles)
+                ctx.sync()
+                for a in arrs:
+                    ctx.free(a)
+                arrs = None
+            elif w.get("tiled3"):
                 tiles = ctx.empty(hq.bits_tiles(G) * 3 * hq.HQ_BITS_TILE_GROUPS, np.uint8)
                 ctx.tile_bits3_dev(G, *arrs, 0, tiles)
                 ctx.sync()
@@ -380,6 +391,9 @@ def run_gpu(w, steps, warmup, d: Dist):
         def run(idx):
             for i in idx:
                 arrs, conf, outc, tiles = sets[i % nsets]
+                if w.get("planes"):
+                    ctx.readindex_vote_planes_dev(G, tiles, conf, outc)
+                    continue
                 if w.get("tiled3"):
                     ctx.readindex_vote_tiles3_dev(G, tiles, conf, outc)
                     continue

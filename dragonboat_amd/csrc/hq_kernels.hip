@@ -917,6 +917,15 @@ template <bool FULL>
 __device__ __forceinline__ void bits3_slot(const BitsK &a, uint64_t g, const V16 *rows) {
     const uint64_t slot = g >> 4;
     uint32_t conf = 0, outc = 0;
+#ifdef HQ_BITS3_COPY   // tuning floor: the same loads and stores, no decision (wrong results)
+    for (int w = 0; w < 4; ++w) {
+        conf ^= rows[0].w[w] ^ rows[1].w[w];
+        outc += rows[2].w[w];
+    }
+    if (FULL || slot < a.n16) reinterpret_cast<uint16_t *>(a.confirmed)[slot] = conf ^ (conf >> 16);
+    if (FULL || slot < a.n16o) reinterpret_cast<uint32_t *>(a.outcome)[slot] = outc;
+    return;
+#endif
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         uint32_t inr = kB80;
@@ -1010,6 +1019,164 @@ __global__ __launch_bounds__(kBlock) void k_tile_bits3(uint64_t G, const uint8_t
         }
         const uint64_t b = __ballot(bad);
         if (fallback && (threadIdx.x & 63) == 0 && g < ((G + 63) & ~63ull)) fallback[g >> 6] = b;
+    }
+}
+
+// ---- bit-plane tiles (hq_readindex_vote_planes_dev) -----------------------------------------
+// The 3-byte tiles transposed: a 2048-group tile holds 24 planes of 256 bytes, plane 8r + b =
+// bit b of row r's byte (rows ack, granted, rejected) for the tile's groups, bit j of dword k =
+// group 32k + j. A lane takes 32 groups: one dword of every plane, and decides them with
+// bitwise full adders and comparators over the planes (bit-sliced: ~6 instructions per group
+// for both decisions, against ~15 for the byte-SWAR form of k_bits3). The confirmed plane is
+// the confirmed bitmap word as it is; the outcome codes interleave the candidate and leader
+// planes.
+constexpr uint32_t kPlaneTile = HQ_PLANE_TILE_GROUPS;   // 2048
+#ifndef HQ_PLANES_TPW
+#define HQ_PLANES_TPW 2
+#endif
+constexpr int kPlTPW = HQ_PLANES_TPW;
+
+__device__ __forceinline__ void full_add(uint32_t a, uint32_t b, uint32_t c, uint32_t &s,
+                                         uint32_t &co) {
+    const uint32_t t = a ^ b;
+    s = t ^ c;
+    co = (a & b) | (c & t);
+}
+
+// popcount of 7 planes as a 3-bit bit-sliced number (c0 + 2 c1 + 4 c2)
+__device__ __forceinline__ void count7(const uint32_t *x, uint32_t &c0, uint32_t &c1,
+                                       uint32_t &c2) {
+    uint32_t s1, k1, s2, k2, k3;
+    full_add(x[0], x[1], x[2], s1, k1);
+    full_add(x[3], x[4], x[5], s2, k2);
+    full_add(s1, s2, x[6], c0, k3);
+    full_add(k1, k2, k3, c1, c2);
+}
+
+// (a2 a1 a0) >= (b2 b1 b0), bit-sliced
+__device__ __forceinline__ uint32_t ge3(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t b0,
+                                        uint32_t b1, uint32_t b2) {
+    const uint32_t lt = (~a2 & b2) | (~(a2 ^ b2) & ((~a1 & b1) | (~(a1 ^ b1) & (~a0 & b0))));
+    return ~lt;
+}
+
+// 2-bit codes of 32 groups: bit 2j = lo_j, bit 2j + 1 = hi_j (byte zip, then a perfect shuffle
+// of each 16-bit unit)
+__device__ __forceinline__ uint32_t shuffle16(uint32_t x) {
+    x = (x & 0xF00FF00Fu) | ((x & 0x00F000F0u) << 4) | ((x >> 4) & 0x00F000F0u);
+    x = (x & 0xC3C3C3C3u) | ((x & 0x0C0C0C0Cu) << 2) | ((x >> 2) & 0x0C0C0C0Cu);
+    x = (x & 0x99999999u) | ((x & 0x22222222u) << 1) | ((x >> 1) & 0x22222222u);
+    return x;
+}
+
+template <bool FULL>
+__device__ __forceinline__ void planes_slot(const BitsK &a, uint64_t g, const uint32_t *p) {
+    const uint32_t n0 = p[7], n1 = p[15], n2 = p[23];     // n - 1
+    uint32_t m[7];                                        // slot k + 1 votes: n - 1 > k
+    m[0] = n0 | n1 | n2;
+    m[1] = n1 | n2;
+    m[2] = n2 | (n1 & n0);
+    m[3] = n2;
+    m[4] = n2 & (n1 | n0);
+    m[5] = n2 & n1;
+    m[6] = n2 & n1 & n0;
+    const uint32_t c = n1 & n0;                           // n / 2 = (n - 1 + 1) >> 1
+    const uint32_t h0 = n1 ^ n0, h1 = n2 ^ c, h2 = n2 & c;
+    uint32_t x[7], y[7], z[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        x[k] = p[k] & m[k];
+        y[k] = p[8 + k] & m[k];
+        z[k] = p[16 + k] & m[k] & ~y[k];                  // first response wins
+    }
+    uint32_t a0, a1, a2, g0, g1, g2, r0, r1, r2;
+    count7(x, a0, a1, a2);
+    count7(y, g0, g1, g2);
+    count7(z, r0, r1, r2);
+    uint32_t inr = ~0u;
+    if constexpr (!FULL) {
+        const uint64_t left = a.G - g;                    // g < G
+        inr = left >= 32 ? ~0u : (1u << left) - 1u;
+    }
+    // readindex.go:84: acks + 1 >= quorum <=> acks >= n/2; handleVoteResp: granted + 1 >=
+    // quorum, rejected >= quorum <=> rejected > n/2
+    const uint32_t conf = ge3(a0, a1, a2, h0, h1, h2) & inr;
+    const uint32_t lead = ge3(g0, g1, g2, h0, h1, h2) & inr;
+    const uint32_t foll = ~ge3(h0, h1, h2, r0, r1, r2) & inr & ~lead;
+    const uint32_t cand = inr & ~lead & ~foll;
+    reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = conf;
+    const uint32_t w0 = shuffle16(__builtin_amdgcn_perm(lead, cand, 0x05010400u));
+    const uint32_t w1 = shuffle16(__builtin_amdgcn_perm(lead, cand, 0x07030602u));
+    *reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(a.outcome) + (g >> 4)) =
+        make_uint2(w0, w1);
+}
+
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_planes(const BitsK a) {
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (BLK / 64);
+    const uint64_t ntiles = (a.G + kPlaneTile - 1) / kPlaneTile;
+    for (uint64_t t0 = wave * kPlTPW; t0 < ntiles; t0 += nw * kPlTPW) {
+        uint32_t p[kPlTPW][24];
+#pragma unroll
+        for (int j = 0; j < kPlTPW; ++j) {
+            const uint64_t t = t0 + j < ntiles ? t0 + j : t0;   // wave-uniform
+            const uint32_t *base =
+                reinterpret_cast<const uint32_t *>(a.tiles + t * (kPlaneTile * 3)) + lane;
+#pragma unroll
+            for (int q = 0; q < 24; ++q) p[j][q] = __builtin_nontemporal_load(base + q * 64);
+        }
+#pragma unroll
+        for (int j = 0; j < kPlTPW; ++j) {
+            const uint64_t t = t0 + j;
+            if (t >= ntiles) break;
+            const uint64_t g = t * kPlaneTile + lane * 32;
+            if (t * kPlaneTile + kPlaneTile <= a.G) planes_slot<true>(a, g, p[j]);
+            else if (g < a.G) planes_slot<false>(a, g, p[j]);
+            else if (g < ((a.G + 63) & ~63ull))           // the rest of the last bitmap word
+                reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = 0;
+        }
+    }
+}
+
+// columns -> bit-plane tiles: one thread per group computes its 3 bytes (as k_tile_bits3), the
+// wave's 64 groups become 24 ballots, lane q < 24 stores plane q's 8 bytes
+__global__ __launch_bounds__(kBlock) void k_tile_planes(uint64_t G, const uint8_t *nv,
+                                                        uint32_t nu, const uint8_t *ack,
+                                                        const uint8_t *gr, const uint8_t *rj,
+                                                        uint8_t *planes, uint64_t *fallback) {
+    const uint64_t total = (G + kPlaneTile - 1) / kPlaneTile * kPlaneTile;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kBlock; g0 < total;
+         g0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t g = g0 + threadIdx.x;
+        uint32_t bytes = 0;
+        bool bad = false;
+        if (g < G) {
+            const uint32_t n = nv ? nv[g] : nu;
+            const uint32_t av = ack[g], x = gr[g], r = rj[g];
+            bad = n < 1 || n > 8 || (av & 1) || !(x & 1) || (r & 1);
+            if (!bad) {
+                const uint32_t keep = (1u << n) - 2u, m = n - 1;
+                bytes = (((av & keep) >> 1) | ((m & 1) << 7)) |
+                        ((((x & keep) >> 1) | (((m >> 1) & 1) << 7)) << 8) |
+                        ((((r & keep) >> 1) | (((m >> 2) & 1) << 7)) << 16);
+            }
+        }
+        uint64_t mine = 0;
+#pragma unroll
+        for (int q = 0; q < 24; ++q) {
+            const uint64_t b = __ballot((bytes >> q) & 1);
+            if (lane == (uint32_t)q) mine = b;
+        }
+        const uint64_t gw = g - lane;                     // the wave's first group
+        if (gw < total && lane < 24)
+            *reinterpret_cast<uint64_t *>(planes + (gw / kPlaneTile) * (kPlaneTile * 3) +
+                                          lane * (kPlaneTile / 8) + (gw % kPlaneTile) / 8) = mine;
+        const uint64_t b = __ballot(bad);
+        if (fallback && lane == 0 && gw < ((G + 63) & ~63ull)) fallback[gw >> 6] = b;
     }
 }
 
@@ -1749,6 +1916,41 @@ extern "C" int hq_readindex_vote_tiles3_dev(hq_ctx *ctx, uint64_t G, const uint8
     hipLaunchKernelGGL(k_bits3<256>, dim3(grid_for((ntiles + kB3TPW - 1) / kB3TPW * 64, 256)),
                        dim3(256), 0, ctx->stream, k);
     return hq::post_launch(ctx, "hq_readindex_vote_tiles3");
+}
+
+extern "C" int hq_readindex_vote_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *planes,
+                                            uint64_t *confirmed, uint64_t *outcome) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!planes || !confirmed || !outcome || !hq::aligned16(planes))
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_readindex_vote_planes: NULL argument or planes not 16-byte aligned");
+    BitsK k = bits_args(G, nullptr, 0, nullptr);
+    k.tiles = planes;
+    k.confirmed = confirmed;
+    k.outcome = outcome;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    const uint64_t ntiles = (G + kPlaneTile - 1) / kPlaneTile;
+    hipLaunchKernelGGL(k_planes<256>, dim3(grid_for((ntiles + kPlTPW - 1) / kPlTPW * 64, 256)),
+                       dim3(256), 0, ctx->stream, k);
+    return hq::post_launch(ctx, "hq_readindex_vote_planes");
+}
+
+extern "C" int hq_tile_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,
+                                  const uint8_t *granted, const uint8_t *rejected,
+                                  const uint8_t *n_voting, uint32_t n_uniform, uint8_t *planes,
+                                  uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!ack || !granted || !rejected || !planes || (reinterpret_cast<uintptr_t>(planes) & 7))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_planes: NULL argument or planes misaligned");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_planes, dim3(grid_for((G + kPlaneTile - 1) / kPlaneTile * kPlaneTile)),
+                       dim3(kBlock), 0, ctx->stream, G, n_voting, n_uniform, ack, granted,
+                       rejected, planes, fallback);
+    return hq::post_launch(ctx, "k_tile_planes");
 }
 
 extern "C" int hq_tile_bits3_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,

@@ -308,3 +308,32 @@ extern "C" int hq_tile_bits3_host(uint64_t G, const uint8_t *ack, const uint8_t 
     }
     return HQ_OK;
 }
+
+// Bitmap columns -> bit-plane tiles on the host (the twin of k_tile_planes): each group's three
+// bytes as in hq_tile_bits3_host, bit b of row r set in plane 8 r + b.
+extern "C" int hq_tile_planes_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                                   const uint8_t *rejected, const uint8_t *n_voting,
+                                   uint32_t n_uniform, uint8_t *planes, uint64_t *fallback) {
+    if (G && (!ack || !granted || !rejected || !planes)) return HQ_E_INVAL;
+    constexpr uint64_t T = HQ_PLANE_TILE_GROUPS;
+    const uint64_t total = (G + T - 1) / T * T;
+    std::memset(planes, 0, total * 3);
+    if (fallback) std::memset(fallback, 0, ((G + 63) / 64) * 8);
+    for (uint64_t g = 0; g < G; ++g) {
+        const uint32_t n = n_voting ? n_voting[g] : n_uniform;
+        const uint32_t a = ack[g], x = granted[g], r = rejected[g];
+        if (n < 1 || n > 8 || (a & 1) || !(x & 1) || (r & 1)) {
+            if (fallback) set_bit(fallback, g);
+            continue;
+        }
+        const uint32_t keep = (1u << n) - 2u, m = n - 1;
+        const uint32_t bytes = (((a & keep) >> 1) | ((m & 1) << 7)) |
+                               ((((x & keep) >> 1) | (((m >> 1) & 1) << 7)) << 8) |
+                               ((((r & keep) >> 1) | (((m >> 2) & 1) << 7)) << 16);
+        uint8_t *tile = planes + (g / T) * (3 * T);
+        const uint64_t j = g % T;
+        for (uint32_t q = 0; q < 24; ++q)
+            if ((bytes >> q) & 1) tile[q * (T / 8) + j / 8] |= (uint8_t)(1u << (j % 8));
+    }
+    return HQ_OK;
+}

@@ -252,6 +252,11 @@ SIGNATURES = {
     "hq_readindex_vote_tiles3_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "hq_tile_bits3_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
                                          ctypes.c_uint32, _vp, _vp]),
+    "hq_readindex_vote_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "hq_tile_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
+                                          ctypes.c_uint32, _vp, _vp]),
+    "hq_tile_planes_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+                                           _vp, _vp]),
     "hq_tile_bits3_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
                                           _vp, _vp]),
     "hq_tile_bits_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
@@ -552,6 +557,15 @@ class Context:
                        fallback=None) -> None:
         self._check(lib.hq_tile_bits3_dev(self.h, G, _p(ack), _p(granted), _p(rejected),
                                           _p(n_voting), n_uniform, _p(tiles), _p(fallback)))
+
+    def readindex_vote_planes_dev(self, G, planes, confirmed, outcome) -> None:
+        self._check(lib.hq_readindex_vote_planes_dev(self.h, G, _p(planes), _p(confirmed),
+                                                     _p(outcome)))
+
+    def tile_planes_dev(self, G, ack, granted, rejected, n_voting, n_uniform, planes,
+                        fallback=None) -> None:
+        self._check(lib.hq_tile_planes_dev(self.h, G, _p(ack), _p(granted), _p(rejected),
+                                           _p(n_voting), n_uniform, _p(planes), _p(fallback)))
 
     def check_quorum_dev(self, G, active, n_voting, n_uniform, self_slot, has_quorum,
                          fallback=None) -> None:
@@ -889,6 +903,25 @@ def tile_bits3_host(ack, granted, rejected, n_voting=None, n_uniform=0):
     fb = np.zeros(words64(G), np.uint64)
     _chk(lib.hq_tile_bits3_host(G, *[_p(c) for c in cols], n_uniform, _p(out), _p(fb)),
          "hq_tile_bits3_host")
+    return out, fb
+
+
+HQ_PLANE_TILE_GROUPS = 2048
+
+
+def plane_tiles(G: int) -> int:
+    return (G + HQ_PLANE_TILE_GROUPS - 1) // HQ_PLANE_TILE_GROUPS
+
+
+def tile_planes_host(ack, granted, rejected, n_voting=None, n_uniform=0):
+    """hq_tile_planes_host over host uint8 columns: (planes uint8 array, fallback words)."""
+    G = len(ack)
+    cols = [np.ascontiguousarray(a, np.uint8) if a is not None else None
+            for a in (ack, granted, rejected, n_voting)]
+    out = np.empty(plane_tiles(G) * 3 * HQ_PLANE_TILE_GROUPS, np.uint8)
+    fb = np.zeros(words64(G), np.uint64)
+    _chk(lib.hq_tile_planes_host(G, *[_p(c) for c in cols], n_uniform, _p(out), _p(fb)),
+         "hq_tile_planes_host")
     return out, fb
 
 

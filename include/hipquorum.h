@@ -421,6 +421,29 @@ int hq_tile_bits3_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
                        uint8_t *tiles, uint64_t *fallback);
 
 /*
+ * The same pass over bit-plane tiles: the 3-byte tiles' bits transposed so that the kernel
+ * decides 32 groups per lane with bitwise adders (bit-sliced). A tile holds
+ * HQ_PLANE_TILE_GROUPS groups as 24 planes of HQ_PLANE_TILE_GROUPS / 8 bytes: plane 8 r + b =
+ * bit b of row r's byte of the 3-byte layout (r = 0 ack, 1 granted, 2 rejected), bit j of byte k
+ * of a plane = the tile's group 8 k + j. Tile t starts at planes + t * 3 * HQ_PLANE_TILE_GROUPS.
+ * Same decisions and contract as hq_readindex_vote_tiles3_dev.
+ */
+#define HQ_PLANE_TILE_GROUPS 2048
+static inline uint64_t hq_plane_tiles(uint64_t G) {
+    return (G + HQ_PLANE_TILE_GROUPS - 1) / HQ_PLANE_TILE_GROUPS;
+}
+int hq_readindex_vote_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *planes,
+                                 uint64_t *confirmed, uint64_t *outcome);
+/* Columns -> bit-plane tiles (hq_plane_tiles(G) * 3 * HQ_PLANE_TILE_GROUPS bytes, padding
+ * zeroed, 8-byte aligned); fallback (may be NULL) receives the contract violations. */
+int hq_tile_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                       const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
+                       uint8_t *planes, uint64_t *fallback);
+int hq_tile_planes_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
+                        const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,
+                        uint8_t *planes, uint64_t *fallback);
+
+/*
  * CheckQuorum (raft.go:380-390): has_quorum bit = popcount(active[g] | 1 << self_slot) >= q,
  * then every active flag is reset (remote.go:196-198): active[g] is written back as 0.
  * self_slot is the leader's slot (the packer puts the leader in slot 0).

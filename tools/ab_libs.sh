@@ -11,7 +11,7 @@ for r in $(seq 1 $ROUNDS); do
   for v in A B; do
     if [ $v = A ]; then unset HQ_LIB_PATH; else export HQ_LIB_PATH=$B; fi
     timeout -k 10 120 python3 bench.py --workload $HEAD --extra=$LEGS --no-cpu --steps 400 \
-      --warmup 20 > gpurun_out/ab/$v$r.log 2>&1 || exit $?
+      --warmup 20 ${EXTRA_ARGS:-} > gpurun_out/ab/$v$r.log 2>&1 || exit $?
     python3 - gpurun_out/ab/$v$r.log $v <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
