@@ -36,7 +36,7 @@ oracle:
 #   lib_mbN    grid cap (in 256-thread units) raised N x
 #   lib_ivN    records per lane of the table ingest kernels
 #   lib_b3tpwN tiles per wave of the 3-byte bitmap kernel
-#   lib_pltpwN tiles per wave of the bit-plane kernel
+#   lib_pltpwN tiles per wave of the bit-plane kernel, lib_plblkN its block size
 #   lib_b3copy the 3-byte bitmap kernel's loads and stores without the decision (its floor)
 define variant
 	@mkdir -p $(dir $@)
@@ -54,6 +54,10 @@ tools/lib_b3tpw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_BITS3_TPW=$*)
 tools/lib_pltpw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLANES_TPW=$*)
+tools/lib_plblk%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_PLANES_BLK=$*)
+tools/lib_plplain/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_PLANES_PLAIN)
 tools/lib_b3copy/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_BITS3_COPY)
 

@@ -1031,8 +1031,13 @@ __global__ __launch_bounds__(kBlock) void k_tile_bits3(uint64_t G, const uint8_t
 // the confirmed bitmap word as it is; the outcome codes interleave the candidate and leader
 // planes.
 constexpr uint32_t kPlaneTile = HQ_PLANE_TILE_GROUPS;   // 2048
+// HQ_PLANES_TPW tiles per wave and iteration (1: 10.3 us per 16M-group launch, 2: 10.7 us — 103
+// VGPRs, half the occupancy — tools/ab_libs.sh), HQ_PLANES_BLK threads per block
 #ifndef HQ_PLANES_TPW
-#define HQ_PLANES_TPW 2
+#define HQ_PLANES_TPW 1
+#endif
+#ifndef HQ_PLANES_BLK
+#define HQ_PLANES_BLK 256
 #endif
 constexpr int kPlTPW = HQ_PLANES_TPW;
 
@@ -1126,7 +1131,13 @@ __global__ __launch_bounds__(BLK) void k_planes(const BitsK a) {
             const uint32_t *base =
                 reinterpret_cast<const uint32_t *>(a.tiles + t * (kPlaneTile * 3)) + lane;
 #pragma unroll
-            for (int q = 0; q < 24; ++q) p[j][q] = __builtin_nontemporal_load(base + q * 64);
+            for (int q = 0; q < 24; ++q) {
+#ifdef HQ_PLANES_PLAIN
+                p[j][q] = base[q * 64];
+#else
+                p[j][q] = __builtin_nontemporal_load(base + q * 64);
+#endif
+            }
         }
 #pragma unroll
         for (int j = 0; j < kPlTPW; ++j) {
@@ -1932,8 +1943,9 @@ extern "C" int hq_readindex_vote_planes_dev(hq_ctx *ctx, uint64_t G, const uint8
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     const uint64_t ntiles = (G + kPlaneTile - 1) / kPlaneTile;
-    hipLaunchKernelGGL(k_planes<256>, dim3(grid_for((ntiles + kPlTPW - 1) / kPlTPW * 64, 256)),
-                       dim3(256), 0, ctx->stream, k);
+    hipLaunchKernelGGL(k_planes<HQ_PLANES_BLK>,
+                       dim3(grid_for((ntiles + kPlTPW - 1) / kPlTPW * 64, HQ_PLANES_BLK)),
+                       dim3(HQ_PLANES_BLK), 0, ctx->stream, k);
     return hq::post_launch(ctx, "hq_readindex_vote_planes");
 }
 
