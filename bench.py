@@ -888,6 +888,8 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
              "host": "host worker (events on the host, decisions in GPU passes), rows"}
     for mode, W in (("device_stream", 1), ("device_stream", T), ("device_rows", 1),
                     ("device_rows", T), ("host", 1), ("host", T)):
+        if d.rank == 0:
+            log(f"  step leg {name}: {mode}, {W} worker(s)")
         t, ne, acc, committed[mode], gm, t_enc = _run_workers(
             hq, d, G, W, steps, cpu_steps, roles, mode != "host", mode == "device_stream")
         elapsed = d.max(t)
@@ -1084,6 +1086,13 @@ def main():
         if d.world == 1 and args.gpus > 1:
             sys.exit(2)
     w = WORKLOADS[args.workload]
+    t_start = time.perf_counter()
+
+    def progress(msg):          # one line per phase (a long run must keep writing)
+        if d.rank == 0:
+            log(f"[bench {time.perf_counter() - t_start:7.1f} s] {msg}")
+
+    progress(f"headline {args.workload}: {args.steps} steps, {args.warmup} warmup")
     r = run_gpu(w, args.steps, args.warmup, d)
     r["world"] = d.world
     host_threads = min(16, os.cpu_count() or 1)
@@ -1099,6 +1108,7 @@ def main():
             # voter-count buckets need gcd(3, world) == 1 (shard.rank_bucket); same on every rank
             failed.append({"workload": name, "skipped": "world size divisible by 3"})
             continue
+        progress(f"extra {name}")
         try:
             if name == "e2e":
                 e2e = run_e2e(max(20, args.steps // 20), 3, d)
@@ -1123,6 +1133,7 @@ def main():
             failed.append({"workload": name, "error": repr(e)})
     cpu = None
     if oracle_here:
+        progress("cpu baseline")
         cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
     # the term check of the same groups in its other exact forms (the ring gathers the north
     # star names, the mask the headline streams): rate and whether every decision is identical
