@@ -788,14 +788,24 @@ def step_events(hq, G, s, roles=STEP_ROLES["step"], last0=1000):
     return np.arange(G, dtype=np.uint32), offsets, ev
 
 
-def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, stream=False):
+def _partition(ev_full, b0, b1):
+    """The step input of groups [b0, b1) of a full step_events() input, as its own worker's
+    (handles 0 .. b1 - b0 - 1)."""
+    _, off, ev = ev_full
+    o = off[b0:b1 + 1]
+    return (np.arange(b1 - b0, dtype=np.uint32), o - o[0], ev[int(o[0]):int(o[-1])])
+
+
+def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, stream=False,
+                 events=None):
     """W workers (one native thread each, own HIP stream) over G groups split into W contiguous
     partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
     of the first 4096 groups after cpu_steps steps, ..., encode seconds). on_device:
     HQ_WORKER_ON_DEVICE workers, the step's input in pinned host memory (a step worker's receive
     buffers) so that it crosses PCIe at the link's rate. stream: the input is the event stream
     (hq_worker_step_stream), written by the producer — here hq_events_encode over the rows,
-    outside the timed region and timed on its own (encode seconds)."""
+    outside the timed region and timed on its own (encode seconds). events(s): the full step s
+    input (cached by the caller across modes)."""
     rng = _shard_of(d, G)
     g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
     nm = len(roles)
@@ -813,7 +823,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
     t_total, n_events, committed, t_enc, nb_total = 0.0, 0, None, 0.0, 0
     warm = 2       # untimed: allocations, first touch, and the first step with commits (its
     for s in range(steps + warm):   # output lists size the pinned result buffers)
-        evs = [step_events(hq, bounds[i + 1] - bounds[i], s, roles) for i in range(W)]
+        full = events(s) if events else step_events(hq, G, s, roles)
+        evs = [_partition(full, bounds[i], bounds[i + 1]) for i in range(W)]
         n_step = sum(len(e[2]) for e in evs)
         if stream:
             t0 = time.perf_counter()
@@ -882,6 +893,13 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
         "unit": "events/s",
     }
     committed = {}
+    cache = {}
+
+    def events(s):            # one generation per step index, shared by every mode
+        if s not in cache:
+            cache[s] = step_events(hq, G, s, roles)
+        return cache[s]
+
     modes = {"device_stream": "device worker (HQ_WORKER_ON_DEVICE: every event on the GPU), "
                               "events as the event stream (hq_worker_step_stream)",
              "device_rows": "device worker, events as 56-byte hq_event rows (hq_worker_step)",
@@ -891,7 +909,7 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
         if d.rank == 0:
             log(f"  step leg {name}: {mode}, {W} worker(s)")
         t, ne, acc, committed[mode], gm, t_enc = _run_workers(
-            hq, d, G, W, steps, cpu_steps, roles, mode != "host", mode == "device_stream")
+            hq, d, G, W, steps, cpu_steps, roles, mode != "host", mode == "device_stream", events)
         elapsed = d.max(t)
         rec = {
             "workers": W,
@@ -923,7 +941,7 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             b = qref.StepBatch(g, m)
             tc, ne = 0.0, 0
             for s in range(cpu_steps + 1):
-                ev = step_events(hq, G, s, roles)
+                ev = events(s)
                 t0 = time.perf_counter()
                 b.step(*ev, nthreads=nt)
                 if s > 0:
