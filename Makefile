@@ -37,7 +37,8 @@ oracle:
 #   lib_ivN    records per lane of the table ingest kernels
 #   lib_b3tpwN tiles per wave of the 3-byte bitmap kernel
 #   lib_pltpwN tiles per wave of the bit-plane kernel, lib_plblkN its block size
-#   lib_b3copy the 3-byte bitmap kernel's loads and stores without the decision (its floor)
+#   lib_b3copy / lib_plcopy the 3-byte / bit-plane kernel's loads and stores without the
+#              decision (their floors)
 define variant
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(1) -shared -o $@ $(SRCS)
@@ -58,6 +59,8 @@ tools/lib_plblk%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLANES_BLK=$*)
 tools/lib_plplain/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLANES_PLAIN)
+tools/lib_plcopy/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_PLANES_COPY)
 tools/lib_b3copy/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_BITS3_COPY)
 

@@ -1076,6 +1076,18 @@ __device__ __forceinline__ uint32_t shuffle16(uint32_t x) {
 
 template <bool FULL>
 __device__ __forceinline__ void planes_slot(const BitsK &a, uint64_t g, const uint32_t *p) {
+#ifdef HQ_PLANES_COPY   // tuning floor: the same loads and stores, no decision (wrong results)
+    uint32_t x0 = 0, x1 = 0, x2 = 0;
+    for (int q = 0; q < 8; ++q) {
+        x0 ^= p[q];
+        x1 += p[8 + q];
+        x2 |= p[16 + q];
+    }
+    reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = x0;
+    *reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(a.outcome) + (g >> 4)) =
+        make_uint2(x1, x2);
+    return;
+#endif
     const uint32_t n0 = p[7], n1 = p[15], n2 = p[23];     // n - 1
     uint32_t m[7];                                        // slot k + 1 votes: n - 1 > k
     m[0] = n0 | n1 | n2;
