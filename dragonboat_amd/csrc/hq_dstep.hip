@@ -102,25 +102,36 @@ __device__ bool decode_event(const uint8_t *&p, const uint8_t *end, uint64_t &te
 
 // One group's state and its output cursor. WRITE = false: counting pass on a private copy;
 // WRITE = true: the same sequence writing records and, at the end, the new state.
-template <bool WRITE>
+template <bool WRITE, int MC>   // MC: member slots held in registers (8 or MC)
 struct Engine {
     const StepK &a;
     uint64_t i;                   // position of the group in the step's list
     hq_dgroup g;
     const hq_dmember *gm;         // the group's member records (node ids and roles read-only)
-    uint64_t match[kDMembers];
+    // member state in registers: every index below is a compile-time constant (unrolled loops,
+    // selects), so nothing of it lives in scratch; only the pending reads (rd) are indexed at run
+    // time, and they are touched only while a group has reads pending
+    uint64_t match[MC];
+    uint64_t ids[MC];
     uint32_t active;              // bit s = member s active
-    hq_dread rd[kDReads];
+    hq_dread *rd;                 // the pending reads: a separate local array (run-time indexed)
     uint32_t cnt[kLists];
     uint32_t base[kLists];
 
-    __device__ Engine(const StepK &k, uint64_t idx, uint32_t h) : a(k), i(idx) {
+    __device__ __forceinline__ Engine(const StepK &k, uint64_t idx, uint32_t h, hq_dread *reads)
+        : a(k), i(idx), rd(reads) {
         g = k.groups[h];
         gm = k.members + g.mem;
         active = 0;
-        for (uint32_t s = 0; s < g.n_members; ++s) {
-            match[s] = gm[s].match;
-            active |= (uint32_t)(gm[s].active != 0) << s;
+#pragma unroll
+        for (uint32_t s = 0; s < MC; ++s) {
+            match[s] = 0;
+            ids[s] = 0;
+            if (s < g.n_members) {
+                match[s] = gm[s].match;
+                ids[s] = gm[s].node_id;
+                active |= (uint32_t)(gm[s].active != 0) << s;
+            }
         }
         for (uint32_t r = 0; r < g.n_reads; ++r) rd[r] = k.reads[(uint64_t)h * kDReads + r];
         for (int l = 0; l < kLists; ++l) {
@@ -129,51 +140,64 @@ struct Engine {
         }
     }
 
-    __device__ uint32_t quorum() const { return g.n_voting / 2 + 1; }   // raft.go:372-374
-    __device__ int member_of(uint64_t id) const {
-        for (uint32_t s = 0; s < g.n_members; ++s)
-            if (gm[s].node_id == id) return (int)s;
-        return -1;
+    __device__ __forceinline__ uint32_t quorum() const { return g.n_voting / 2 + 1; }   // raft.go:372-374
+    __device__ __forceinline__ int member_of(uint64_t id) const {
+        int m = -1;
+#pragma unroll
+        for (int s = MC - 1; s >= 0; --s)           // the first match wins
+            m = (s < (int)g.n_members && ids[s] == id) ? s : m;
+        return m;
     }
-    __device__ uint32_t slot(int l) { return base[l] + cnt[l]++; }
+    __device__ __forceinline__ uint64_t match_of(int mi) const {
+        uint64_t v = 0;
+#pragma unroll
+        for (int s = 0; s < (int)MC; ++s) v = s == mi ? match[s] : v;
+        return v;
+    }
+    __device__ __forceinline__ void set_match(int mi, uint64_t v) {
+#pragma unroll
+        for (int s = 0; s < (int)MC; ++s) match[s] = s == mi ? v : match[s];
+    }
+    __device__ __forceinline__ uint32_t slot(int l) { return base[l] + cnt[l]++; }
 
     // -- outputs ----------------------------------------------------------------------------
-    __device__ void ready(uint64_t index, uint64_t low, uint64_t high) {
+    __device__ __forceinline__ void ready(uint64_t index, uint64_t low, uint64_t high) {
         const uint32_t p = slot(kReady);
         if (WRITE) a.ready[p] = hq_ready_to_read{g.cluster_id, index, low, high};
     }
-    __device__ void resp(uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
+    __device__ __forceinline__ void resp(uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
         const uint32_t p = slot(kResps);
         if (WRITE) a.resps[p] = hq_read_index_resp{g.cluster_id, to, index, hint, high};
     }
-    __device__ void state_change(uint32_t reason) {
+    __device__ __forceinline__ void state_change(uint32_t reason) {
         const uint32_t p = slot(kStates);
         if (WRITE) a.states[p] = hq_state_change{g.cluster_id, g.term, g.state, reason};
     }
-    __device__ void dropped(uint64_t low, uint64_t high, uint64_t from, uint32_t reason) {
+    __device__ __forceinline__ void dropped(uint64_t low, uint64_t high, uint64_t from, uint32_t reason) {
         const uint32_t p = slot(kDropped);
         if (WRITE) a.dropped[p] = hq_dropped_read{g.cluster_id, low, high, from, reason, 0};
     }
-    __device__ void defer(uint64_t e) {
+    __device__ __forceinline__ void defer(uint64_t e) {
         const uint32_t p = slot(kDeferred);
         if (WRITE) a.deferred[p] = e;
     }
 
     // -- reference state transitions (raft.go:949-1010) --------------------------------------
-    __device__ void reset(uint64_t term) {
+    __device__ __forceinline__ void reset(uint64_t term) {
         g.term = term;
         g.granted = g.rejected = 0;
         g.n_reads = 0;                                   // r.readIndex = newReadIndex()
-        for (uint32_t s = 0; s < g.n_members; ++s)       // resetRemotes/Observers/Witnesses
-            match[s] = gm[s].node_id == g.node_id ? g.last : 0;
+#pragma unroll
+        for (uint32_t s = 0; s < MC; ++s)         // resetRemotes/Observers/Witnesses
+            match[s] = s < g.n_members && ids[s] == g.node_id ? g.last : 0;
         active = 0;
     }
-    __device__ void become_follower(uint64_t term, uint32_t reason) {
+    __device__ __forceinline__ void become_follower(uint64_t term, uint32_t reason) {
         g.state = HQ_STATE_FOLLOWER;
         reset(term);
         state_change(reason);
     }
-    __device__ void become_leader() {
+    __device__ __forceinline__ void become_leader() {
         g.state = HQ_STATE_LEADER;
         reset(g.term);
         state_change(HQ_REASON_VOTE);
@@ -187,14 +211,16 @@ struct Engine {
     // raft.tryCommit (raft.go:888-909): the quorum-th largest match of the voting members, then
     // entryLog.tryCommit (logentry.go:378-393) with term(q) == term <=> term_start <= q <= last
     // (the leader's entries carry its term and terms never decrease, entryutils.go:44-47)
-    __device__ void try_commit() {
+    __device__ __forceinline__ void try_commit() {
         cnt[kDecisions]++;
         const uint32_t n = g.n_voting, q = quorum();
         uint64_t best = 0;
-        for (uint32_t s = 0; s < n; ++s) {
+#pragma unroll
+        for (uint32_t s = 0; s < HQ_MAX_VOTERS; ++s) {
             uint32_t ge = 0;
-            for (uint32_t t = 0; t < n; ++t) ge += match[t] >= match[s];
-            if (ge >= q && match[s] > best) best = match[s];
+#pragma unroll
+            for (uint32_t t = 0; t < HQ_MAX_VOTERS; ++t) ge += t < n && match[t] >= match[s];
+            if (s < n && ge >= q && match[s] > best) best = match[s];
         }
         if (best > g.committed && best >= g.term_start && best <= g.last)
             g.committed = best;                          // commitTo (logentry.go:323-332)
@@ -202,7 +228,7 @@ struct Engine {
 
     // handleLeaderReadIndex (raft.go:1636-1669) and readIndex.addRequest (readindex.go:43-67);
     // returns false for the worker's fallback contract (see include/hipquorum.h)
-    __device__ bool read_index(uint64_t from, uint64_t low, uint64_t high, uint64_t e) {
+    __device__ __forceinline__ bool read_index(uint64_t from, uint64_t low, uint64_t high, uint64_t e) {
         if (g.state != HQ_STATE_LEADER) {
             defer(e);                                    // forwarded / dropped (raft.go:1875, 1937)
             return true;
@@ -238,7 +264,7 @@ struct Engine {
 
     // readIndex.confirm (readindex.go:77-116) + handleReadIndexLeaderConfirmation
     // (raft.go:1740-1760) for the ack of voting slot mi
-    __device__ bool confirm(uint64_t hint, uint64_t high, int mi) {
+    __device__ __forceinline__ bool confirm(uint64_t hint, uint64_t high, int mi) {
         uint32_t k = 0;
         while (k < g.n_reads && !(rd[k].low == hint && rd[k].high == high)) ++k;
         if (k == g.n_reads) return true;                 // not pending
@@ -257,7 +283,7 @@ struct Engine {
     }
 
     // one event; false: the group leaves the device path at this event (fallback)
-    __device__ bool handle(const hq_event &ev, uint64_t e) {
+    __device__ __forceinline__ bool handle(const hq_event &ev, uint64_t e) {
         switch (ev.kind) {
         case HQ_EV_READ:
             return read_index(0, ev.hint, ev.hint_high, e);
@@ -306,9 +332,9 @@ struct Engine {
         if (g.state == HQ_STATE_LEADER) {
             switch (type) {
             case HQ_MSG_REPLICATE_RESP:                  // handleLeaderReplicateResp
-                if (!ev.reject && match[mi] < ev.log_index) {
+                if (!ev.reject && match_of(mi) < ev.log_index) {
                     if (ev.log_index > g.last) return false;   // a follower acks only what it got
-                    match[mi] = ev.log_index;            // remote.tryUpdate
+                    set_match(mi, ev.log_index);         // remote.tryUpdate
                     try_commit();
                 }
                 active |= 1u << mi;
@@ -344,7 +370,7 @@ struct Engine {
     // the group's events: rows (STREAM = false) or its bytes [p, end) of the stream; an event
     // that does not decode is a fallback like one the path does not take
     template <bool STREAM>
-    __device__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
+    __device__ __forceinline__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
         const uint64_t committed0 = g.committed;
         uint64_t term = 0;
         for (uint64_t e = e0; e < e1; ++e) {
@@ -373,18 +399,21 @@ struct Engine {
         }
     }
 
-    __device__ void store(uint32_t h) {
+    __device__ __forceinline__ void store(uint32_t h) {
         a.groups[h] = g;
         hq_dmember *m = a.members + g.mem;
-        for (uint32_t s = 0; s < g.n_members; ++s) {
-            m[s].match = match[s];
-            m[s].active = (uint8_t)((active >> s) & 1);
+#pragma unroll
+        for (uint32_t s = 0; s < MC; ++s) {
+            if (s < g.n_members) {
+                m[s].match = match[s];
+                m[s].active = (uint8_t)((active >> s) & 1);
+            }
         }
         for (uint32_t r = 0; r < g.n_reads; ++r) a.reads[(uint64_t)h * kDReads + r] = rd[r];
     }
 };
 
-template <bool WRITE, bool STREAM>
+template <bool WRITE, bool STREAM, int MC>
 __global__ __launch_bounds__(256) void k_step(const StepK a) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
@@ -404,7 +433,8 @@ __global__ __launch_bounds__(256) void k_step(const StepK a) {
             return;
         }
     }
-    Engine<WRITE> eng(a, i, h);
+    hq_dread reads[kDReads];
+    Engine<WRITE, MC> eng(a, i, h, reads);
     if (STREAM)
         eng.template run<true>(a.offsets[i], a.offsets[i + 1], a.bytes + a.boffsets[i],
                                a.bytes + a.boffsets[i + 1]);
@@ -441,6 +471,7 @@ struct hq_dstep {
     uint32_t *stamp = nullptr;    // [gcap] step stamps (duplicate handles)
     uint64_t gcap = 0, mcap = 0;
     uint64_t n_groups = 0;        // group records uploaded (valid handles)
+    uint32_t max_members = 0;     // the most members of any uploaded group
     uint32_t step_no = 0;
     // step staging
     void *in = nullptr;
@@ -511,6 +542,8 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
         if (!rc) d->gcap = std::min({gc / sizeof(hq_dgroup), rcap / (kDReads * sizeof(hq_dread)),
                                      sc / 4});
     }
+    for (uint64_t i = 0; i < ng; ++i)
+        if (g[i].n_members > d->max_members) d->max_members = g[i].n_members;
     if (!rc && ng) {              // new stamps start at 0 (no step has listed them)
         rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp + g0, 0, ng * 4, ctx->stream), "memset");
         if (!rc && g0 + ng > d->n_groups) d->n_groups = g0 + ng;
@@ -627,8 +660,11 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(k.error, 0, 4, ctx->stream), "memset");
     if (!rc) rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    if (stream) hipLaunchKernelGGL((k_step<false, true>), grid, blk, 0, ctx->stream, k);
-    else hipLaunchKernelGGL((k_step<false, false>), grid, blk, 0, ctx->stream, k);
+    const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
+    if (stream && small) hipLaunchKernelGGL((k_step<false, true, 8>), grid, blk, 0, ctx->stream, k);
+    else if (stream) hipLaunchKernelGGL((k_step<false, true, kDMembers>), grid, blk, 0, ctx->stream, k);
+    else if (small) hipLaunchKernelGGL((k_step<false, false, 8>), grid, blk, 0, ctx->stream, k);
+    else hipLaunchKernelGGL((k_step<false, false, kDMembers>), grid, blk, 0, ctx->stream, k);
     rc = hq::post_launch(ctx, "k_step<count>");
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
@@ -680,8 +716,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.fallback = reinterpret_cast<uint64_t *>(o + off[kFallback]);
     rc = hq::pre_launch(ctx);
     if (rc) return rc;
-    if (stream) hipLaunchKernelGGL((k_step<true, true>), grid, blk, 0, ctx->stream, k);
-    else hipLaunchKernelGGL((k_step<true, false>), grid, blk, 0, ctx->stream, k);
+    if (stream && small) hipLaunchKernelGGL((k_step<true, true, 8>), grid, blk, 0, ctx->stream, k);
+    else if (stream) hipLaunchKernelGGL((k_step<true, true, kDMembers>), grid, blk, 0, ctx->stream, k);
+    else if (small) hipLaunchKernelGGL((k_step<true, false, 8>), grid, blk, 0, ctx->stream, k);
+    else hipLaunchKernelGGL((k_step<true, false, kDMembers>), grid, blk, 0, ctx->stream, k);
     rc = hq::post_launch(ctx, "k_step<write>");
     if (!rc && total)
         rc = hq::check_hip(ctx, hipMemcpyAsync(d->host_out, o, total, hipMemcpyDeviceToHost,

@@ -2273,7 +2273,10 @@ __device__ __forceinline__ void ce_pk(uint32_t &a, uint32_t &b) {
     b = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
 }
 
-template <bool PERK, bool PERN>
+// KM >= K_max ctx slots in registers: every (ctx, voter) load of the lane is issued before the
+// first sorting network (K_max and n_max are uniform, so the guards are scalar branches; with the
+// loads inside the per-ctx branches each ctx waited for its own round trip)
+template <bool PERK, bool PERN, int KM>
 __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
@@ -2295,32 +2298,42 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
             }
             fb0 = n0 < 1 || n0 > a.n_max || K0 > a.K_max;
             fb1 = n1 < 1 || n1 > a.n_max || K1 > a.K_max;
-            const uint32_t kmax = K0 > K1 ? K0 : K1;
             // padding of the voters >= n, per half (0xFFFF = never acked)
             const int r0 = n0 / 2 > 1 ? (int)(n0 / 2) : 1, r1 = n1 / 2 > 1 ? (int)(n1 / 2) : 1;
             u64x2 idx[8];
+            uint32_t ov[KM][8];
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+                idx[k] = (u64x2){0, 0};
+                if (k < (int)a.K_max) {
+                    idx[k] = __builtin_nontemporal_load(
+                        reinterpret_cast<const u64x2 *>(a.idx + (uint64_t)k * a.G + g));
+#pragma unroll
+                    for (int sl = 0; sl < 8; ++sl) {
+                        ov[k][sl] = 0xFFFFFFFFu;
+                        if (sl < (int)a.n_max)
+                            ov[k][sl] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
+                                a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g));
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = KM; k < 8; ++k) idx[k] = (u64x2){0, 0};
+            const uint32_t kmax = K0 > K1 ? K0 : K1;
             uint32_t t[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                idx[k] = (u64x2){0, 0};
                 t[k] = 0xFFFFFFFFu;
-                if (k < (int)kmax && k < (int)a.K_max) {
-                    idx[k] = __builtin_nontemporal_load(
-                        reinterpret_cast<const u64x2 *>(a.idx + (uint64_t)k * a.G + g));
+                if (k < KM && k < (int)kmax && k < (int)a.K_max) {
                     if (k > 0) {   // addRequest: index moved backward
                         fb0 |= k < (int)K0 && idx[k].x < idx[k - 1].x;
                         fb1 |= k < (int)K1 && idx[k].y < idx[k - 1].y;
                     }
                     uint32_t v[8];
 #pragma unroll
-                    for (int sl = 0; sl < 8; ++sl) {
-                        uint32_t x = 0xFFFFFFFFu;
-                        if (sl < (int)a.n_max)
-                            x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
-                                a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g));
-                        x |= (sl < (int)n0 ? 0u : 0xFFFFu) | (sl < (int)n1 ? 0u : 0xFFFF0000u);
-                        v[sl] = x;
-                    }
+                    for (int sl = 0; sl < 8; ++sl)
+                        v[sl] = ov[k < KM ? k : 0][sl] | (sl < (int)n0 ? 0u : 0xFFFFu) |
+                                (sl < (int)n1 ? 0u : 0xFFFF0000u);
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
 #pragma unroll
@@ -2392,14 +2405,24 @@ extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, u
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     if (pairs) {
-        if (n_pending && n_voting)
-            hipLaunchKernelGGL((k_ri_multi2<true, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
-        else if (n_pending)
-            hipLaunchKernelGGL((k_ri_multi2<true, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
-        else if (n_voting)
-            hipLaunchKernelGGL((k_ri_multi2<false, true>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
-        else
-            hipLaunchKernelGGL((k_ri_multi2<false, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
+        const int km = K_max <= 2 ? 2 : K_max <= 4 ? 4 : 8;
+#define HQ_RIM2(PK, PN)                                                                         \
+        do {                                                                                    \
+            if (km == 2)                                                                        \
+                hipLaunchKernelGGL((k_ri_multi2<PK, PN, 2>), dim3(grid), dim3(kBlock), 0,       \
+                                   ctx->stream, k);                                             \
+            else if (km == 4)                                                                   \
+                hipLaunchKernelGGL((k_ri_multi2<PK, PN, 4>), dim3(grid), dim3(kBlock), 0,       \
+                                   ctx->stream, k);                                             \
+            else                                                                                \
+                hipLaunchKernelGGL((k_ri_multi2<PK, PN, 8>), dim3(grid), dim3(kBlock), 0,       \
+                                   ctx->stream, k);                                             \
+        } while (0)
+        if (n_pending && n_voting) HQ_RIM2(true, true);
+        else if (n_pending) HQ_RIM2(true, false);
+        else if (n_voting) HQ_RIM2(false, true);
+        else HQ_RIM2(false, false);
+#undef HQ_RIM2
         return hq::post_launch(ctx, "k_ri_multi2");
     }
     if (n_pending && n_voting)
