@@ -38,6 +38,7 @@ struct StepK {
     hq_dmember *members;
     hq_dread *reads;
     uint64_t n;                   // groups listed in this step
+    uint64_t i_begin, i_end;      // the chunk of them this launch takes
     uint64_t n_handles;           // groups on the device (valid handles)
     uint64_t n_events, n_bytes;   // input sizes (rows or stream bytes)
     uint32_t *stamp;              // per handle: the last step that listed it
@@ -415,8 +416,8 @@ struct Engine {
 
 template <bool WRITE, bool STREAM, int MC>
 __global__ __launch_bounds__(256) void k_step(const StepK a) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n) return;
+    const uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.i_end) return;
     const uint32_t h = a.handles[i];
     if (!WRITE) {                 // validate this group's entry; a bad one is not stepped
         uint32_t err = 0;
@@ -447,12 +448,18 @@ __global__ __launch_bounds__(256) void k_step(const StepK a) {
     }
 }
 
-// the start of every list in the scanned counts, the grand total, and the input errors
-__global__ void k_list_bases(const uint32_t *scan, uint64_t n, const uint32_t *error,
-                             uint32_t *bases) {
-    const int l = threadIdx.x;
-    if (l <= kLists) bases[l] = scan[(uint64_t)l * n];
-    if (l == kLists + 1) bases[l] = *error;
+// the scanned counts at every chunk boundary (row c: scan[l * n + bound[c]] for every list l;
+// the last row holds the ends of the lists, its last entry the grand total) and the input errors
+constexpr int kMaxChunks = 4;
+struct Bounds { uint64_t b[kMaxChunks + 1]; };
+__global__ void k_list_bases(const uint32_t *scan, uint64_t n, Bounds bd, int chunks,
+                             const uint32_t *error, uint32_t *bases) {
+    const int t = threadIdx.x;
+    if (t < (chunks + 1) * kLists) {
+        const int c = t / kLists, l = t % kLists;
+        bases[t] = scan[(uint64_t)l * n + bd.b[c]];
+    }
+    if (t == 63) bases[(chunks + 1) * kLists] = *error;
 }
 
 uint64_t now_ns() {
@@ -482,8 +489,12 @@ struct hq_dstep {
     size_t scan_tmp_cap = 0;
     void *out = nullptr;
     size_t out_cap = 0;
-    void *host_out = nullptr;     // pinned: the lists come back in one copy
+    void *host_out = nullptr;     // pinned: the lists come back into it
     size_t host_out_cap = 0;
+    // a large step runs in chunks of groups: chunk c's input copy (copy stream) overlaps pass A
+    // of chunk c - 1, and its result copy overlaps pass B of chunk c + 1 (compute stream)
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_in[kMaxChunks] = {}, ev_b[kMaxChunks] = {};
 };
 
 namespace {
@@ -508,8 +519,20 @@ int grow(hq_ctx *ctx, void **p, size_t *cap, size_t need, bool keep, const char 
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out) {
     *out = new (std::nothrow) hq_dstep();
     if (!*out) return HQ_E_NOMEM;
-    (*out)->ctx = ctx;
-    return HQ_OK;
+    hq_dstep *d = *out;
+    d->ctx = ctx;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    if (!rc) rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
+                                "hq_dstep copy stream");
+    for (int c = 0; c < kMaxChunks && !rc; ++c) {
+        rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_in[c], hipEventDisableTiming), "event");
+        if (!rc) rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_b[c], hipEventDisableTiming), "event");
+    }
+    if (rc) {
+        hq_dstep_close(d);
+        *out = nullptr;
+    }
+    return rc;
 }
 
 void hq_dstep_close(hq_dstep *d) {
@@ -520,6 +543,14 @@ void hq_dstep_close(hq_dstep *d) {
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp, d->out})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
+    if (d->copy) {
+        (void)hipStreamSynchronize(d->copy);
+        (void)hipStreamDestroy(d->copy);
+    }
+    for (int c = 0; c < kMaxChunks; ++c) {
+        if (d->ev_in[c]) (void)hipEventDestroy(d->ev_in[c]);
+        if (d->ev_b[c]) (void)hipEventDestroy(d->ev_b[c]);
+    }
     delete d;
 }
 
@@ -593,7 +624,12 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     if (n == 0) return HQ_OK;
     const uint64_t t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    // the step's input in one device region: handles, offsets, [boffsets,] events or bytes
+    // chunks of groups (at least 64 Ki each): copies overlap the passes of neighbouring chunks
+    const int chunks = n >= 4 * 65536 ? 4 : n >= 2 * 65536 ? 2 : 1;
+    Bounds bd{};
+    for (int c = 0; c <= chunks; ++c) bd.b[c] = n * c / chunks;
+    // the step's input in one device region: handles, offsets, [boffsets,] events or bytes, each
+    // at the offsets it has on the host
     auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t o_off = up(n * 4);
     const size_t o_boff = o_off + up((n + 1) * 8);
@@ -604,23 +640,15 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     auto h2d = [&](size_t off, const void *src, size_t bytes) {
         if (!rc && bytes)
             rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
-                                                   ctx->stream), "hq_dstep H2D");
+                                                   d->copy), "hq_dstep H2D");
     };
-    h2d(0, in->groups, n * 4);
-    h2d(o_off, in->offsets, (n + 1) * 8);
-    if (stream) {
-        h2d(o_boff, in->boffsets, (n + 1) * 8);
-        h2d(o_ev, in->bytes, nb);
-    } else {
-        h2d(o_ev, in->events, ne * sizeof(hq_event));
-    }
     // counts [kLists][n] + 1 (zero: the scan's last element is the grand total)
     const size_t cn = (size_t)kLists * n + 1;
-    size_t cc = d->cnt_cap * 4, sc = d->cnt_cap * 4, bc = d->cnt_cap ? 64 : 0;
+    size_t cc = d->cnt_cap * 4, sc = d->cnt_cap * 4, bc = d->cnt_cap ? 256 : 0;
     if (!rc && cn > d->cnt_cap) {
         rc = grow(ctx, reinterpret_cast<void **>(&d->counts), &cc, cn * 4, false, "hq_dstep counts");
         if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->scan), &sc, cn * 4, false, "hq_dstep scan");
-        if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 64, false, "hq_dstep bases");
+        if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 256, false, "hq_dstep bases");
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
     }
     size_t tmp = 0;
@@ -654,38 +682,72 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (rc) return rc;
     }
     k.step_no = d->step_no;
-    k.error = d->bases + kLists + 2;
-    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+    k.error = d->bases + 63;
     rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
     if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(k.error, 0, 4, ctx->stream), "memset");
-    if (!rc) rc = hq::pre_launch(ctx);
-    if (rc) return rc;
     const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
-    if (stream && small) hipLaunchKernelGGL((k_step<false, true, 8>), grid, blk, 0, ctx->stream, k);
-    else if (stream) hipLaunchKernelGGL((k_step<false, true, kDMembers>), grid, blk, 0, ctx->stream, k);
-    else if (small) hipLaunchKernelGGL((k_step<false, false, 8>), grid, blk, 0, ctx->stream, k);
-    else hipLaunchKernelGGL((k_step<false, false, kDMembers>), grid, blk, 0, ctx->stream, k);
-    rc = hq::post_launch(ctx, "k_step<count>");
+    auto launch = [&](bool write, uint64_t i0, uint64_t i1) {
+        k.i_begin = i0;
+        k.i_end = i1;
+        const dim3 grid((unsigned)((i1 - i0 + 255) / 256)), blk(256);
+        if (rc || i1 == i0) return;
+        rc = hq::pre_launch(ctx);
+        if (rc) return;
+#define HQ_STEP_LAUNCH(W)                                                                        \
+        if (stream && small) hipLaunchKernelGGL((k_step<W, true, 8>), grid, blk, 0, ctx->stream, k); \
+        else if (stream) hipLaunchKernelGGL((k_step<W, true, kDMembers>), grid, blk, 0, ctx->stream, k); \
+        else if (small) hipLaunchKernelGGL((k_step<W, false, 8>), grid, blk, 0, ctx->stream, k); \
+        else hipLaunchKernelGGL((k_step<W, false, kDMembers>), grid, blk, 0, ctx->stream, k);
+        if (write) {
+            HQ_STEP_LAUNCH(true)
+        } else {
+            HQ_STEP_LAUNCH(false)
+        }
+#undef HQ_STEP_LAUNCH
+        rc = hq::post_launch(ctx, write ? "k_step<write>" : "k_step<count>");
+    };
+    // inputs chunk by chunk on the copy stream, pass A of each chunk once it has landed
+    for (int c = 0; c < chunks && !rc; ++c) {
+        const uint64_t i0 = bd.b[c], i1 = bd.b[c + 1];
+        h2d(i0 * 4, in->groups + i0, (i1 - i0) * 4);
+        h2d(o_off + i0 * 8, in->offsets + i0, (i1 - i0 + 1) * 8);
+        if (stream) {
+            h2d(o_boff + i0 * 8, in->boffsets + i0, (i1 - i0 + 1) * 8);
+            // the chunk's bytes (garbage offsets are the kernel's to reject: clamp the copy)
+            const uint64_t lo = std::min(in->boffsets[i0], nb);
+            const uint64_t hi = std::min(std::max(in->boffsets[i1], lo), nb);
+            h2d(o_ev + lo, in->bytes + lo, hi - lo);
+        } else {
+            const uint64_t lo = std::min(in->offsets[i0], ne);
+            const uint64_t hi = std::min(std::max(in->offsets[i1], lo), ne);
+            h2d(o_ev + lo * sizeof(hq_event), in->events + lo, (hi - lo) * sizeof(hq_event));
+        }
+        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], d->copy), "event");
+        if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
+        launch(false, i0, i1);
+    }
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
                                 "hipcub scan");
     if (!rc) {
-        hipLaunchKernelGGL(k_list_bases, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, k.error,
-                           d->bases);
+        hipLaunchKernelGGL(k_list_bases, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, bd,
+                           chunks, k.error, d->bases);
         rc = hq::check_hip(ctx, hipGetLastError(), "k_list_bases");
     }
-    uint32_t bases[kLists + 2];
-    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(bases, d->bases, sizeof bases,
+    uint32_t bases[(kMaxChunks + 1) * kLists + 1];
+    const size_t nbases = (size_t)(chunks + 1) * kLists + 1;
+    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(bases, d->bases, nbases * 4,
                                                     hipMemcpyDeviceToHost, ctx->stream), "D2H");
     if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
     if (rc) return rc;
-    if (bases[kLists + 1]) {      // no group state was written
-        out->input_error = bases[kLists + 1];
+    if (bases[nbases - 1]) {      // no group state was written
+        out->input_error = bases[nbases - 1];
         return HQ_E_INVAL;
     }
     const uint64_t t1 = now_ns();
+    const uint32_t *first = bases, *last = bases + (size_t)chunks * kLists;
     uint64_t len[kLists];
-    for (int l = 0; l < kLists; ++l) len[l] = bases[l + 1] - bases[l];
+    for (int l = 0; l < kLists; ++l) len[l] = last[l] - first[l];
     // the output lists in one device region, mirrored by one pinned host region
     const size_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
                                 sizeof(hq_read_index_resp), sizeof(hq_state_change),
@@ -707,6 +769,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     }
     if (rc) return rc;
     char *o = static_cast<char *>(d->out);
+    char *ho = static_cast<char *>(d->host_out);
     k.commits = reinterpret_cast<hq_commit_event *>(o + off[kCommits]);
     k.ready = reinterpret_cast<hq_ready_to_read *>(o + off[kReady]);
     k.resps = reinterpret_cast<hq_read_index_resp *>(o + off[kResps]);
@@ -714,19 +777,23 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.dropped = reinterpret_cast<hq_dropped_read *>(o + off[kDropped]);
     k.deferred = reinterpret_cast<uint64_t *>(o + off[kDeferred]);
     k.fallback = reinterpret_cast<uint64_t *>(o + off[kFallback]);
-    rc = hq::pre_launch(ctx);
-    if (rc) return rc;
-    if (stream && small) hipLaunchKernelGGL((k_step<true, true, 8>), grid, blk, 0, ctx->stream, k);
-    else if (stream) hipLaunchKernelGGL((k_step<true, true, kDMembers>), grid, blk, 0, ctx->stream, k);
-    else if (small) hipLaunchKernelGGL((k_step<true, false, 8>), grid, blk, 0, ctx->stream, k);
-    else hipLaunchKernelGGL((k_step<true, false, kDMembers>), grid, blk, 0, ctx->stream, k);
-    rc = hq::post_launch(ctx, "k_step<write>");
-    if (!rc && total)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(d->host_out, o, total, hipMemcpyDeviceToHost,
-                                               ctx->stream), "D2H");
+    // pass B chunk by chunk; each chunk's records go back on the copy stream behind it
+    for (int c = 0; c < chunks && !rc; ++c) {
+        launch(true, bd.b[c], bd.b[c + 1]);
+        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_b[c], ctx->stream), "event");
+        if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(d->copy, d->ev_b[c], 0), "wait");
+        const uint32_t *cb = bases + (size_t)c * kLists, *ce = cb + kLists;
+        for (int l = 0; l < kLists - 1 && !rc; ++l) {
+            const size_t a = off[l] + (size_t)(cb[l] - first[l]) * rec[l];
+            const size_t bytes = (size_t)(ce[l] - cb[l]) * rec[l];
+            if (bytes)
+                rc = hq::check_hip(ctx, hipMemcpyAsync(ho + a, o + a, bytes, hipMemcpyDeviceToHost,
+                                                       d->copy), "D2H");
+        }
+    }
+    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(d->copy), "hq_dstep sync");
     if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
     if (rc) return rc;
-    const char *ho = static_cast<const char *>(d->host_out);
     out->commits = reinterpret_cast<const hq_commit_event *>(ho + off[kCommits]);
     out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + off[kReady]);
     out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + off[kResps]);

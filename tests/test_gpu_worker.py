@@ -325,3 +325,37 @@ def test_step_jobs_equal_sequential_steps(hq):
     finally:
         for w in a + b:
             w.close()
+
+
+@pytest.mark.parametrize("stream", [True, False], ids=["stream", "rows"])
+def test_chunked_device_step_equals_host_worker(hq, stream):
+    """A step of >= 256 Ki groups runs in 4 chunks whose copies overlap the neighbouring chunks'
+    passes (hq_dstep.hip); its lists equal the host worker's on the same events (the host
+    worker is checked against the oracle above), in the same order."""
+    import bench
+
+    G = 4 * 65536 + 5
+    roles = bench.STEP_ROLES["step5"]
+    g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
+    nv = sum(r != "observer" for r in roles)
+    dev, host = hq.Worker(0, nv, on_device=True), hq.Worker(0, nv)
+    try:
+        dev.add_groups(g, m)
+        host.add_groups(g, m)
+        for s in range(3):
+            e = bench.step_events(hq, G, s, roles)
+            want = host.step(*e)
+            if stream:
+                data, boff = hq.encode_events(e[1], e[2])
+                got = dev.step_stream(e[0], e[1], boff, data)
+            else:
+                got = dev.step(*e)
+            for k in ("commits", "ready", "read_resps", "state_changes", "dropped_reads",
+                      "deferred", "fallback_groups"):
+                np.testing.assert_array_equal(got[k], want[k], err_msg=f"step {s} {k}")
+            assert len(want["commits"]) == (G if s else 0) and len(want["ready"]) > G // 5
+        for cid in (1, 65537, 131073, 4 * 65536 + 5):
+            assert dev.get_group(cid)[0]["committed"] == host.get_group(cid)[0]["committed"]
+    finally:
+        dev.close()
+        host.close()
