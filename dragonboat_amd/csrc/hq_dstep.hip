@@ -492,9 +492,11 @@ struct hq_dstep {
     void *host_out = nullptr;     // pinned: the lists come back into it
     size_t host_out_cap = 0;
     // a large step runs in chunks of groups: chunk c's input copy (copy stream) overlaps pass A
-    // of chunk c - 1, and its result copy overlaps pass B of chunk c + 1 (compute stream)
+    // of chunk c - 1, and its result copy overlaps pass B of chunk c + 1 (compute stream); the
+    // copy stream is created by the first such step
     hipStream_t copy = nullptr;
     hipEvent_t ev_in[kMaxChunks] = {}, ev_b[kMaxChunks] = {};
+    hipEvent_t ev_sync = nullptr;  // blocking-sync event: a waiting worker thread sleeps
 };
 
 namespace {
@@ -516,14 +518,37 @@ int grow(hq_ctx *ctx, void **p, size_t *cap, size_t need, bool keep, const char 
 
 }  // namespace
 
+namespace {
+
+// Wait for a stream: poll briefly (a one-worker step's sync is short), then sleep on a
+// blocking-sync event, so that 16 workers waiting at once do not spin 16 host cores (a spinning
+// wait under a CPU quota stalls every thread of the process for the rest of the period)
+int wait_stream(hq_dstep *d, hipStream_t s, const char *what) {
+    hq_ctx *ctx = d->ctx;
+    int rc = hq::check_hip(ctx, hipEventRecord(d->ev_sync, s), what);
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(d->ev_sync);
+        if (q == hipSuccess) return HQ_OK;
+        if (q != hipErrorNotReady) return hq::check_hip(ctx, q, what);
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) break;
+    }
+    return hq::check_hip(ctx, hipEventSynchronize(d->ev_sync), what);
+}
+
+}  // namespace
+
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out) {
     *out = new (std::nothrow) hq_dstep();
     if (!*out) return HQ_E_NOMEM;
     hq_dstep *d = *out;
     d->ctx = ctx;
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    if (!rc) rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
-                                "hq_dstep copy stream");
+    if (!rc)
+        rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming |
+                                                                          hipEventBlockingSync),
+                           "event");
     for (int c = 0; c < kMaxChunks && !rc; ++c) {
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_in[c], hipEventDisableTiming), "event");
         if (!rc) rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_b[c], hipEventDisableTiming), "event");
@@ -547,6 +572,7 @@ void hq_dstep_close(hq_dstep *d) {
         (void)hipStreamSynchronize(d->copy);
         (void)hipStreamDestroy(d->copy);
     }
+    if (d->ev_sync) (void)hipEventDestroy(d->ev_sync);
     for (int c = 0; c < kMaxChunks; ++c) {
         if (d->ev_in[c]) (void)hipEventDestroy(d->ev_in[c]);
         if (d->ev_b[c]) (void)hipEventDestroy(d->ev_b[c]);
@@ -637,10 +663,15 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event));
     if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
     char *din = static_cast<char *>(d->in);
+    // one chunk: every copy on the compute stream (nothing to overlap, no cross-stream waits)
+    if (!rc && chunks > 1 && !d->copy)       // the copy stream of the first chunked step
+        rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
+                           "hq_dstep copy stream");
+    hipStream_t cs = chunks > 1 ? d->copy : ctx->stream;
     auto h2d = [&](size_t off, const void *src, size_t bytes) {
         if (!rc && bytes)
             rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
-                                                   d->copy), "hq_dstep H2D");
+                                                   cs), "hq_dstep H2D");
     };
     // counts [kLists][n] + 1 (zero: the scan's last element is the grand total)
     const size_t cn = (size_t)kLists * n + 1;
@@ -722,8 +753,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
             const uint64_t hi = std::min(std::max(in->offsets[i1], lo), ne);
             h2d(o_ev + lo * sizeof(hq_event), in->events + lo, (hi - lo) * sizeof(hq_event));
         }
-        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], d->copy), "event");
-        if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
+        if (chunks > 1) {
+            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
+            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
+        }
         launch(false, i0, i1);
     }
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
@@ -738,7 +771,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const size_t nbases = (size_t)(chunks + 1) * kLists + 1;
     if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(bases, d->bases, nbases * 4,
                                                     hipMemcpyDeviceToHost, ctx->stream), "D2H");
-    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
+    if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
     if (rc) return rc;
     if (bases[nbases - 1]) {      // no group state was written
         out->input_error = bases[nbases - 1];
@@ -780,19 +813,21 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     // pass B chunk by chunk; each chunk's records go back on the copy stream behind it
     for (int c = 0; c < chunks && !rc; ++c) {
         launch(true, bd.b[c], bd.b[c + 1]);
-        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_b[c], ctx->stream), "event");
-        if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(d->copy, d->ev_b[c], 0), "wait");
+        if (chunks > 1) {
+            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_b[c], ctx->stream), "event");
+            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(cs, d->ev_b[c], 0), "wait");
+        }
         const uint32_t *cb = bases + (size_t)c * kLists, *ce = cb + kLists;
         for (int l = 0; l < kLists - 1 && !rc; ++l) {
             const size_t a = off[l] + (size_t)(cb[l] - first[l]) * rec[l];
             const size_t bytes = (size_t)(ce[l] - cb[l]) * rec[l];
             if (bytes)
                 rc = hq::check_hip(ctx, hipMemcpyAsync(ho + a, o + a, bytes, hipMemcpyDeviceToHost,
-                                                       d->copy), "D2H");
+                                                       cs), "D2H");
         }
     }
-    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(d->copy), "hq_dstep sync");
-    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep sync");
+    if (!rc && chunks > 1) rc = wait_stream(d, cs, "hq_dstep sync");
+    if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
     if (rc) return rc;
     out->commits = reinterpret_cast<const hq_commit_event *>(ho + off[kCommits]);
     out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + off[kReady]);
