@@ -129,7 +129,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "cq,ing,ingo,w2,e2e,step,step5")
+                  "rimt,cq,ing,ingo,w2,e2e,step,step5")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -520,7 +520,7 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
 
     ctx = hq.Context(d.device)
     r = np.random.default_rng(SEED_BASE + d.rank)
-    if name == "rim":
+    if name in ("rim", "rimt"):
         G, K, n = 2 << 20, 4, 7
         # first-ack ordinals: ~70 % of (ctx, voter) pairs acked, in arrival order 1..K*n
         ordn = r.integers(1, K * n + 1, (K, n, G)).astype(np.uint16)
@@ -532,12 +532,26 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
         sets = [(ctx.upload(ordn.reshape(-1)), ctx.upload(idx.reshape(-1)),
                  ctx.empty(K * G, np.uint64), ctx.empty(G, np.uint8), ctx.empty(G, np.uint8))
                 for _ in range(nsets)]
+        if name == "rimt":     # the same inputs as 128-group tiles (one block per wave)
+            tb = hq.ri_tile_bytes(K, n, 0)
+            tiled = []
+            for o, x, rel, cnt, bend in sets:
+                t = ctx.empty((G // 128) * tb, np.uint8)
+                ctx.tile_ri_multi_dev(G, K, n, o, x, None, None, t)
+                ctx.sync()
+                ctx.free(o)
+                ctx.free(x)
+                tiled.append((t, rel, cnt, bend))
 
-        def run(i):
-            o, x, rel, cnt, bend = sets[i % nsets]
-            ctx.readindex_multi_dev(G, K, n, o, x, None, None, n, rel, cnt, batch_end=bend)
-        desc = (f"rim: general multi-ctx ReadIndex release (suffix-min), {G} groups x {K} pending "
-                f"ctxs x {n} voters")
+            def run(i):
+                t, rel, cnt, bend = tiled[i % nsets]
+                ctx.readindex_multi_tiles_dev(G, K, n, t, 0, n, rel, cnt, batch_end=bend)
+        else:
+            def run(i):
+                o, x, rel, cnt, bend = sets[i % nsets]
+                ctx.readindex_multi_dev(G, K, n, o, x, None, None, n, rel, cnt, batch_end=bend)
+        desc = (f"{name}: general multi-ctx ReadIndex release (suffix-min), {G} groups x {K} "
+                f"pending ctxs x {n} voters" + (", 128-group tiles" if name == "rimt" else ""))
         units, unit = G, "releases/s"
     elif name == "cq":
         G, n = 16 << 20, 7
@@ -1133,7 +1147,7 @@ def main():
             elif name in STEP_ROLES:
                 steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
                                                name=name))
-            elif name in ("rim", "cq", "ing", "ingo"):
+            elif name in ("rim", "rimt", "cq", "ing", "ingo"):
                 kern.append(run_kernel_leg(name, max(50, args.steps // 4),
                                            max(5, args.warmup // 4), d))
             elif name.startswith("w") and name[1:].isdigit():

@@ -2174,6 +2174,8 @@ namespace {
 struct RiMultiK {
     uint64_t G;
     uint32_t K_max, n_max, n_uniform;
+    const uint8_t *tiles;         // tiled layout (hq_readindex_multi_tiles_dev), else columns
+    uint64_t tile_bytes;
     const uint16_t *ord;
     const uint64_t *idx;
     const uint8_t *np, *nv;
@@ -2276,23 +2278,32 @@ __device__ __forceinline__ void ce_pk(uint32_t &a, uint32_t &b) {
 // KM >= K_max ctx slots in registers: every (ctx, voter) load of the lane is issued before the
 // first sorting network (K_max and n_max are uniform, so the guards are scalar branches; with the
 // loads inside the per-ctx branches each ctx waited for its own round trip)
-template <bool PERK, bool PERN, int KM>
+template <bool PERK, bool PERN, int KM, bool TILED = false>
 __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint64_t step = (uint64_t)gridDim.x * kBlock * 2;
     for (uint64_t wbase = wave * 128; wbase < a.G; wbase += step) {
         const uint64_t g = wbase + 2 * (uint64_t)lane;
+        // TILED: the wave's 128 groups are one tile (wbase is a multiple of 128); rows of 128
+        // entries, this lane's two groups at entries 2 lane, 2 lane + 1
+        const uint8_t *tb = TILED ? a.tiles + (wbase >> 7) * a.tile_bytes : nullptr;
+        const uint64_t ord_bytes = (uint64_t)a.K_max * a.n_max * 256;
         bool fb0 = false, fb1 = false;
-        if (g < a.G) {   // G is even: g + 1 < G too
+        if (g < a.G) {   // columns: G is even, g + 1 < G too; tiles: padded rows
             uint32_t K0 = a.K_max, K1 = a.K_max, n0 = a.n_uniform, n1 = a.n_uniform;
             if constexpr (PERK) {
-                const uint32_t kk = *reinterpret_cast<const uint16_t *>(a.np + g);
+                const uint32_t kk = TILED ? *reinterpret_cast<const uint16_t *>(
+                                                tb + ord_bytes + a.K_max * 1024ull + 2 * lane)
+                                          : *reinterpret_cast<const uint16_t *>(a.np + g);
                 K0 = kk & 0xFF;
                 K1 = kk >> 8;
             }
             if constexpr (PERN) {
-                const uint32_t nn = *reinterpret_cast<const uint16_t *>(a.nv + g);
+                const uint32_t nn =
+                    TILED ? *reinterpret_cast<const uint16_t *>(tb + ord_bytes + a.K_max * 1024ull +
+                                                               (PERK ? 128 : 0) + 2 * lane)
+                          : *reinterpret_cast<const uint16_t *>(a.nv + g);
                 n0 = nn & 0xFF;
                 n1 = nn >> 8;
             }
@@ -2306,14 +2317,17 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
             for (int k = 0; k < KM; ++k) {
                 idx[k] = (u64x2){0, 0};
                 if (k < (int)a.K_max) {
-                    idx[k] = __builtin_nontemporal_load(
-                        reinterpret_cast<const u64x2 *>(a.idx + (uint64_t)k * a.G + g));
+                    idx[k] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(
+                        TILED ? tb + ord_bytes + k * 1024ull + 16 * lane
+                              : reinterpret_cast<const uint8_t *>(a.idx + (uint64_t)k * a.G + g)));
 #pragma unroll
                     for (int sl = 0; sl < 8; ++sl) {
                         ov[k][sl] = 0xFFFFFFFFu;
                         if (sl < (int)a.n_max)
                             ov[k][sl] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
-                                a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g));
+                                TILED ? tb + ((uint64_t)k * a.n_max + sl) * 256 + 4 * lane
+                                      : reinterpret_cast<const uint8_t *>(
+                                            a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g)));
                     }
                 }
             }
@@ -2365,12 +2379,23 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
                 rel1 += rl1;
                 be0 |= (uint32_t)(rl0 && own0) << k;
                 be1 |= (uint32_t)(rl1 && own1) << k;
-                if (k < (int)a.K_max)
-                    *reinterpret_cast<u64x2 *>(a.rel + (uint64_t)k * a.G + g) =
-                        (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
+                if (k < (int)a.K_max) {
+                    uint64_t *r = a.rel + (uint64_t)k * a.G + g;
+                    if (!TILED || g + 1 < a.G) {
+                        *reinterpret_cast<u64x2 *>(r) = (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
+                    } else {
+                        r[0] = rl0 ? bi0 : ~0ull;   // odd G: the tile's padding group has no slot
+                    }
+                }
             }
-            *reinterpret_cast<uint16_t *>(a.cnt + g) = (uint16_t)(rel0 | (rel1 << 8));
-            if (a.bend) *reinterpret_cast<uint16_t *>(a.bend + g) = (uint16_t)(be0 | (be1 << 8));
+            if (!TILED || g + 1 < a.G) {
+                *reinterpret_cast<uint16_t *>(a.cnt + g) = (uint16_t)(rel0 | (rel1 << 8));
+                if (a.bend) *reinterpret_cast<uint16_t *>(a.bend + g) = (uint16_t)(be0 | (be1 << 8));
+            } else {
+                a.cnt[g] = (uint8_t)rel0;
+                if (a.bend) a.bend[g] = (uint8_t)be0;
+                fb1 = false;
+            }
         }
         const uint64_t f0 = __ballot(fb0), f1 = __ballot(fb1);
         if (a.fallback && lane < 2) {
@@ -2395,8 +2420,8 @@ extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, u
     if (!ack_ordinal || !ctx_index || !released_index || !released_count || K_max < 1 ||
         K_max > 8 || n_max < 1 || n_max > 8 || (!n_voting && (n_uniform < 1 || n_uniform > 8)))
         return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_dev: bad arguments");
-    RiMultiK k{G, K_max, n_max, n_uniform, ack_ordinal, ctx_index, n_pending, n_voting,
-               released_index, released_count, batch_end, fallback};
+    RiMultiK k{G, K_max, n_max, n_uniform, nullptr, 0, ack_ordinal, ctx_index, n_pending,
+               n_voting, released_index, released_count, batch_end, fallback};
     auto al = [](const void *p, uintptr_t m) { return ((uintptr_t)p & (m - 1)) == 0; };
     const bool pairs = ctx->ri_pairs && G % 2 == 0 && al(ack_ordinal, 4) && al(ctx_index, 16) &&
                        al(released_index, 16) && al(released_count, 2) && al(batch_end, 2) &&
@@ -2434,6 +2459,119 @@ extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, u
     else
         hipLaunchKernelGGL((k_ri_multi<false, false>), dim3(grid), dim3(kBlock), 0, ctx->stream, k);
     return hq::post_launch(ctx, "k_ri_multi");
+}
+
+namespace {
+
+// columns -> multi-ctx ReadIndex tiles: one thread per (tile, row, 16-byte chunk)
+__global__ __launch_bounds__(kBlock) void k_tile_ri_multi(uint64_t G, uint32_t K_max,
+                                                          uint32_t n_max, const uint16_t *ord,
+                                                          const uint64_t *idx, const uint8_t *np,
+                                                          const uint8_t *nv, uint8_t *tiles,
+                                                          uint64_t tile_bytes) {
+    const uint64_t ntiles = (G + HQ_RI_TILE_GROUPS - 1) / HQ_RI_TILE_GROUPS;
+    const uint64_t chunks = tile_bytes / 16;
+    const uint64_t ord_rows = (uint64_t)K_max * n_max, ord_bytes = ord_rows * 256;
+    for (uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q < ntiles * chunks;
+         q += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t t = q / chunks, off = (q % chunks) * 16;
+        const uint64_t g0 = t * HQ_RI_TILE_GROUPS;
+        uint8_t v[16];
+        if (off < ord_bytes) {                           // 8 u16 entries of row off / 256
+            const uint64_t row = off / 256, j = (off % 256) / 2;
+            for (int e = 0; e < 8; ++e) {
+                const uint64_t g = g0 + j + e;
+                const uint16_t x = g < G ? ord[row * G + g] : 0xFFFFu;
+                v[2 * e] = (uint8_t)x;
+                v[2 * e + 1] = (uint8_t)(x >> 8);
+            }
+        } else if (off < ord_bytes + K_max * 1024ull) {  // 2 u64 entries of ctx row
+            const uint64_t o = off - ord_bytes, k = o / 1024, j = (o % 1024) / 8;
+            for (int e = 0; e < 2; ++e) {
+                const uint64_t g = g0 + j + e;
+                const uint64_t x = g < G ? idx[k * G + g] : 0;
+                for (int b = 0; b < 8; ++b) v[8 * e + b] = (uint8_t)(x >> (8 * b));
+            }
+        } else {                                         // the u8 rows: n_pending, n_voting
+            const uint64_t o = off - ord_bytes - K_max * 1024ull;
+            const uint8_t *src = (np && o < 128) ? np : nv;
+            const uint64_t j = o % 128;
+            for (int e = 0; e < 16; ++e) {
+                const uint64_t g = g0 + j + e;
+                v[e] = g < G && src ? src[g] : 0;
+            }
+        }
+        uint4 w;
+        memcpy(&w, v, 16);
+        *reinterpret_cast<uint4 *>(tiles + t * tile_bytes + off) = w;
+    }
+}
+
+}  // namespace
+
+extern "C" int hq_readindex_multi_tiles_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max,
+                                            uint32_t n_max, const uint8_t *tiles, uint32_t flags,
+                                            uint32_t n_uniform, uint64_t *released_index,
+                                            uint8_t *released_count, uint8_t *batch_end,
+                                            uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    const bool perk = flags & HQ_RI_TILE_PER_K, pern = flags & HQ_RI_TILE_PER_N;
+    if (!tiles || !released_index || !released_count || K_max < 1 || K_max > 8 || n_max < 1 ||
+        n_max > 8 || (flags & ~(HQ_RI_TILE_PER_K | HQ_RI_TILE_PER_N)) ||
+        (!pern && (n_uniform < 1 || n_uniform > 8)) || !hq::aligned16(tiles) ||
+        (reinterpret_cast<uintptr_t>(released_index) & 15) ||
+        (reinterpret_cast<uintptr_t>(released_count) & 1) ||
+        (batch_end && (reinterpret_cast<uintptr_t>(batch_end) & 1)))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_tiles_dev: bad arguments");
+    RiMultiK k{G, K_max, n_max, n_uniform, tiles, hq_ri_tile_bytes(K_max, n_max, flags),
+               nullptr, nullptr, nullptr, nullptr, released_index, released_count, batch_end,
+               fallback};
+    // the pair kernel's column stores need 16-byte rows: G even keeps k * G + g aligned
+    if (G % 2)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_tiles_dev: G must be even");
+    const unsigned grid = grid_for(G / 2);
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    const int km = K_max <= 2 ? 2 : K_max <= 4 ? 4 : 8;
+#define HQ_RIM2T(PK, PN)                                                                        \
+    do {                                                                                        \
+        if (km == 2)                                                                            \
+            hipLaunchKernelGGL((k_ri_multi2<PK, PN, 2, true>), dim3(grid), dim3(kBlock), 0,     \
+                               ctx->stream, k);                                                 \
+        else if (km == 4)                                                                       \
+            hipLaunchKernelGGL((k_ri_multi2<PK, PN, 4, true>), dim3(grid), dim3(kBlock), 0,     \
+                               ctx->stream, k);                                                 \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_ri_multi2<PK, PN, 8, true>), dim3(grid), dim3(kBlock), 0,     \
+                               ctx->stream, k);                                                 \
+    } while (0)
+    if (perk && pern) HQ_RIM2T(true, true);
+    else if (perk) HQ_RIM2T(true, false);
+    else if (pern) HQ_RIM2T(false, true);
+    else HQ_RIM2T(false, false);
+#undef HQ_RIM2T
+    return hq::post_launch(ctx, "k_ri_multi2<tiles>");
+}
+
+extern "C" int hq_tile_ri_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
+                                    const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                                    const uint8_t *n_pending, const uint8_t *n_voting,
+                                    uint8_t *tiles) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!ack_ordinal || !ctx_index || !tiles || K_max < 1 || K_max > 8 || n_max < 1 ||
+        n_max > 8 || !hq::aligned16(tiles))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_ri_multi_dev: bad arguments");
+    const uint32_t flags = (n_pending ? HQ_RI_TILE_PER_K : 0) | (n_voting ? HQ_RI_TILE_PER_N : 0);
+    const uint64_t tb = hq_ri_tile_bytes(K_max, n_max, flags);
+    const uint64_t ntiles = (G + HQ_RI_TILE_GROUPS - 1) / HQ_RI_TILE_GROUPS;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_ri_multi, dim3(grid_for(ntiles * (tb / 16))), dim3(kBlock), 0,
+                       ctx->stream, G, K_max, n_max, ack_ordinal, ctx_index, n_pending, n_voting,
+                       tiles, tb);
+    return hq::post_launch(ctx, "k_tile_ri_multi");
 }
 
 // ---- device-resident progress table: delta ingest ------------------------

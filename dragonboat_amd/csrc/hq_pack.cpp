@@ -337,3 +337,38 @@ extern "C" int hq_tile_planes_host(uint64_t G, const uint8_t *ack, const uint8_t
     }
     return HQ_OK;
 }
+
+// Multi-ctx ReadIndex columns -> 128-group tiles on the host (the twin of k_tile_ri_multi;
+// include/hipquorum.h hq_readindex_multi_tiles_dev).
+extern "C" int hq_tile_ri_multi_host(uint64_t G, uint32_t K_max, uint32_t n_max,
+                                     const uint16_t *ord, const uint64_t *idx, const uint8_t *np,
+                                     const uint8_t *nv, uint8_t *tiles) {
+    if (G && (!ord || !idx || !tiles)) return HQ_E_INVAL;
+    if (K_max < 1 || K_max > 8 || n_max < 1 || n_max > 8) return HQ_E_INVAL;
+    constexpr uint64_t T = HQ_RI_TILE_GROUPS;
+    const uint32_t flags = (np ? HQ_RI_TILE_PER_K : 0) | (nv ? HQ_RI_TILE_PER_N : 0);
+    const uint64_t tb = hq_ri_tile_bytes(K_max, n_max, flags);
+    const uint64_t ntiles = (G + T - 1) / T, rows = (uint64_t)K_max * n_max;
+    for (uint64_t t = 0; t < ntiles; ++t) {
+        uint8_t *b = tiles + t * tb;
+        for (uint64_t j = 0; j < T; ++j) {
+            const uint64_t g = t * T + j;
+            const bool in = g < G;
+            for (uint64_t r = 0; r < rows; ++r) {
+                const uint16_t x = in ? ord[r * G + g] : 0xFFFFu;
+                std::memcpy(b + r * 256 + 2 * j, &x, 2);
+            }
+            for (uint64_t k = 0; k < K_max; ++k) {
+                const uint64_t x = in ? idx[k * G + g] : 0;
+                std::memcpy(b + rows * 256 + k * 1024 + 8 * j, &x, 8);
+            }
+            uint8_t *u = b + rows * 256 + K_max * 1024ull;   // the u8 rows
+            if (np) {
+                u[j] = in ? np[g] : 0;
+                u += T;
+            }
+            if (nv) u[j] = in ? nv[g] : 0;
+        }
+    }
+    return HQ_OK;
+}

@@ -267,6 +267,13 @@ SIGNATURES = {
     "hq_readindex_multi_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32,
                                               ctypes.c_uint32, _vp, _vp, _vp, _vp,
                                               ctypes.c_uint32, _vp, _vp, _vp, _vp]),
+    "hq_readindex_multi_tiles_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32,
+                                                    ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                                    ctypes.c_uint32, _vp, _vp, _vp, _vp]),
+    "hq_tile_ri_multi_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                            _vp, _vp, _vp, _vp, _vp]),
+    "hq_tile_ri_multi_host": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                             _vp, _vp, _vp, _vp, _vp]),
     "hq_ingest_match_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                            ctypes.c_uint64, ctypes.c_uint32, _vp]),
     "hq_ingest_ack_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
@@ -589,6 +596,20 @@ class Context:
                                                _p(released_count), _p(batch_end),
                                                _p(fallback)))
 
+    def readindex_multi_tiles_dev(self, G, K_max, n_max, tiles, flags, n_uniform, released_index,
+                                  released_count, fallback=None, batch_end=None):
+        """hq_readindex_multi_tiles_dev over 128-group tiles (tile_ri_multi_*)."""
+        self._check(lib.hq_readindex_multi_tiles_dev(self.h, G, K_max, n_max, _p(tiles), flags,
+                                                     n_uniform, _p(released_index),
+                                                     _p(released_count), _p(batch_end),
+                                                     _p(fallback)))
+
+    def tile_ri_multi_dev(self, G, K_max, n_max, ack_ordinal, ctx_index, n_pending, n_voting,
+                          tiles) -> None:
+        self._check(lib.hq_tile_ri_multi_dev(self.h, G, K_max, n_max, _p(ack_ordinal),
+                                             _p(ctx_index), _p(n_pending), _p(n_voting),
+                                             _p(tiles)))
+
     def ingest_match_dev(self, updates, count, match, match_stride, G, n_max, n_skipped=None):
         """updates: device array of hq_match_update (uint64 pairs: group << 8 | slot, index)."""
         self._check(lib.hq_ingest_match_dev(self.h, _p(updates), count, _p(match), match_stride,
@@ -907,6 +928,28 @@ def tile_bits3_host(ack, granted, rejected, n_voting=None, n_uniform=0):
 
 
 HQ_PLANE_TILE_GROUPS = 2048
+HQ_RI_TILE_GROUPS = 128
+HQ_RI_TILE_PER_K = 1
+HQ_RI_TILE_PER_N = 2
+
+
+def ri_tile_bytes(K_max: int, n_max: int, flags: int) -> int:
+    return K_max * n_max * 256 + K_max * 1024 + (128 if flags & HQ_RI_TILE_PER_K else 0) + \
+        (128 if flags & HQ_RI_TILE_PER_N else 0)
+
+
+def tile_ri_multi_host(G, K_max, n_max, ack_ordinal, ctx_index, n_pending=None, n_voting=None):
+    """hq_tile_ri_multi_host: (tiles uint8 array, flags) of host columns."""
+    flags = (HQ_RI_TILE_PER_K if n_pending is not None else 0) | \
+        (HQ_RI_TILE_PER_N if n_voting is not None else 0)
+    ntiles = (G + HQ_RI_TILE_GROUPS - 1) // HQ_RI_TILE_GROUPS
+    out = np.zeros(ntiles * ri_tile_bytes(K_max, n_max, flags), np.uint8)
+    cols = [np.ascontiguousarray(ack_ordinal, np.uint16), np.ascontiguousarray(ctx_index, np.uint64),
+            None if n_pending is None else np.ascontiguousarray(n_pending, np.uint8),
+            None if n_voting is None else np.ascontiguousarray(n_voting, np.uint8)]
+    _chk(lib.hq_tile_ri_multi_host(G, K_max, n_max, *[_p(c) for c in cols], _p(out)),
+         "hq_tile_ri_multi_host")
+    return out, flags
 
 
 def plane_tiles(G: int) -> int:

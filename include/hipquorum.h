@@ -368,6 +368,35 @@ int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_m
                            uint64_t *released_index, uint8_t *released_count,
                            uint8_t *batch_end, uint64_t *fallback);
 
+/*
+ * The same release over 128-group tiles: tile t starts at tiles + t * hq_ri_tile_bytes(K_max,
+ * n_max, flags) and holds the rows ack_ordinal[k][s] (k < K_max, s < n_max; 128 u16 each, k-major),
+ * ctx_index[k] (k < K_max; 128 u64 each), then with HQ_RI_TILE_PER_K n_pending (128 u8) and with
+ * HQ_RI_TILE_PER_N n_voting (128 u8); group 128 t + j at entry j of every row (padding: ordinal
+ * 0xFFFF, index 0, counts 0). One contiguous block per wave instead of K_max * (n_max + 1) column
+ * streams. Outputs (columns) and semantics as hq_readindex_multi_dev; G even, released_index
+ * 16-byte and released_count / batch_end 2-byte aligned.
+ */
+#define HQ_RI_TILE_GROUPS 128
+#define HQ_RI_TILE_PER_K 1u
+#define HQ_RI_TILE_PER_N 2u
+static inline uint64_t hq_ri_tile_bytes(uint32_t K_max, uint32_t n_max, uint32_t flags) {
+    return (uint64_t)K_max * n_max * 256 + (uint64_t)K_max * 1024 +
+           ((flags & HQ_RI_TILE_PER_K) ? 128 : 0) + ((flags & HQ_RI_TILE_PER_N) ? 128 : 0);
+}
+int hq_readindex_multi_tiles_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
+                                 const uint8_t *tiles, uint32_t flags, uint32_t n_uniform,
+                                 uint64_t *released_index, uint8_t *released_count,
+                                 uint8_t *batch_end, uint64_t *fallback);
+/* Columns (as hq_readindex_multi_dev; n_pending / n_voting may be NULL, setting the flags) ->
+ * tiles (ceil(G / 128) * hq_ri_tile_bytes(...) bytes, 16-byte aligned). _host: host pointers. */
+int hq_tile_ri_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max,
+                         const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                         const uint8_t *n_pending, const uint8_t *n_voting, uint8_t *tiles);
+int hq_tile_ri_multi_host(uint64_t G, uint32_t K_max, uint32_t n_max,
+                          const uint16_t *ack_ordinal, const uint64_t *ctx_index,
+                          const uint8_t *n_pending, const uint8_t *n_voting, uint8_t *tiles);
+
 /* ReadIndex confirmation and vote tally of the same groups in one pass over the shared n. */
 int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,
                           const uint8_t *rejected, const uint8_t *n_voting, uint32_t n_uniform,

@@ -140,3 +140,75 @@ def test_kernel_pairs_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
     np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
     for x in [x for x in d if x is not None] + [rel, cnt, bend, fb]:
         gpu_ctx.free(x)
+
+
+def tiles_reference(ord_, idx, Kp, nv, K_max, n_max, G):
+    """numpy restatement of the 128-group tile layout (include/hipquorum.h)."""
+    T = 128
+    nt = (G + T - 1) // T
+    o = np.full((K_max * n_max, nt * T), NONE, np.uint16)
+    o[:, :G] = ord_.reshape(K_max * n_max, G)
+    x = np.zeros((K_max, nt * T), np.uint64)
+    x[:, :G] = idx.reshape(K_max, G)
+    parts = [o.reshape(K_max * n_max, nt, T).transpose(1, 0, 2).reshape(nt, -1).view(np.uint8),
+             x.reshape(K_max, nt, T).transpose(1, 0, 2).reshape(nt, -1).view(np.uint8)]
+    for c in (Kp, nv):
+        if c is not None:
+            u = np.zeros(nt * T, np.uint8)
+            u[:G] = c
+            parts.append(u.reshape(nt, T))
+    return np.concatenate(parts, axis=1).reshape(-1)
+
+
+@pytest.mark.parametrize("K_max,n_max,G,perk,pern", [(4, 7, 300, False, False),
+                                                     (3, 5, 129, True, True),
+                                                     (8, 8, 128, True, False)])
+def test_tile_packer_layout(hq, K_max, n_max, G, perk, pern):
+    rng = np.random.default_rng(G)
+    ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
+    Kp, nv = (K if perk else None), (n if pern else None)
+    tiles, flags = hq.tile_ri_multi_host(G, K_max, n_max, ord_, idx, Kp, nv)
+    assert flags == (hq.HQ_RI_TILE_PER_K if perk else 0) | (hq.HQ_RI_TILE_PER_N if pern else 0)
+    assert len(tiles) == (G + 127) // 128 * hq.ri_tile_bytes(K_max, n_max, flags)
+    np.testing.assert_array_equal(tiles, tiles_reference(ord_, idx, Kp, nv, K_max, n_max, G))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K_max,n_max,G,perk,pern", [(8, 8, 20_010, True, True),
+                                                     (4, 7, 4096, False, False),
+                                                     (4, 7, 4098, True, False),
+                                                     (3, 5, 130, False, True),
+                                                     (2, 3, 2, True, True),
+                                                     (1, 1, 64, False, False)])
+def test_kernel_tiles_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
+    """The 128-group tile layout: the device packer equals the host packer, and the kernel over
+    tiles is bit-exact with the oracle (every per-group / uniform combination)."""
+    rng = np.random.default_rng(K_max * 1000 + n_max + G + 7)
+    ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
+    if pern:
+        n[::97] = 0
+    if G > 5:
+        idx.reshape(K_max, G)[:, 5] = np.arange(K_max, 0, -1)
+    Kp = K if perk else None
+    nv = n if pern else None
+    nu = 0 if pern else n_max
+    want_rel, want_cnt, want_fb, want_bend = qref.readindex_multi_batch(ord_, idx, Kp, nv, nu,
+                                                                        K_max, n_max)
+    tiles_h, flags = hq.tile_ri_multi_host(G, K_max, n_max, ord_, idx, Kp, nv)
+    d = [gpu_ctx.upload(x) if x is not None else None for x in (ord_, idx, Kp, nv)]
+    dt = gpu_ctx.empty(len(tiles_h), np.uint8)
+    gpu_ctx.memset(dt, 0xAB)
+    gpu_ctx.tile_ri_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], dt)
+    np.testing.assert_array_equal(gpu_ctx.download(dt), tiles_h)
+    rel = gpu_ctx.empty(K_max * G, np.uint64)
+    cnt = gpu_ctx.empty(G, np.uint8)
+    bend = gpu_ctx.empty(G, np.uint8)
+    fb = gpu_ctx.empty(hq.words64(G), np.uint64)
+    gpu_ctx.memset(fb, 0xFF)
+    gpu_ctx.readindex_multi_tiles_dev(G, K_max, n_max, dt, flags, nu, rel, cnt, fb, bend)
+    np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
+    np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
+    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
+    np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
+    for x in [x for x in d if x is not None] + [dt, rel, cnt, bend, fb]:
+        gpu_ctx.free(x)
