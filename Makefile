@@ -37,7 +37,7 @@ oracle:
 #   lib_ivN    records per lane of the table ingest kernels
 #   lib_b3tpwN tiles per wave of the 3-byte bitmap kernel
 #   lib_pltpwN tiles per wave of the bit-plane kernel, lib_plblkN its block size
-#   lib_b3copy / lib_plcopy the 3-byte / bit-plane kernel's loads and stores without the
+#   lib_tilecopy / lib_b3copy / lib_plcopy the commit tile / 3-byte / bit-plane kernel's loads and stores without the
 #              decision (their floors)
 define variant
 	@mkdir -p $(dir $@)
@@ -61,6 +61,8 @@ tools/lib_plplain/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLANES_PLAIN)
 tools/lib_plcopy/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLANES_COPY)
+tools/lib_tilecopy/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_TILE_COPY)
 tools/lib_b3copy/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_BITS3_COPY)
 

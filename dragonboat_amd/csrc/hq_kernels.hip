@@ -369,8 +369,22 @@ __device__ __forceinline__ void tile_blocks(const CommitK &a, uint64_t blk, uint
 #endif
             const int na = PERN ? (int)a.nv[ga] : N, nb = PERN ? (int)a.nv[gb] : N;
             uint64_t coa, cob;
+#ifdef HQ_TILE_COPY   // tuning floor: the same loads and stores, no decision (wrong results)
+            coa = ci.x ^ la.x ^ ax.x;
+            cob = ci.y ^ la.y ^ ax.y;
+#pragma unroll
+            for (int s = LEAD; s < N; ++s) {
+                coa ^= m0[s];
+                cob ^= m1[s];
+            }
+            ca = coa & 1;
+            cb = cob & 1;
+            (void)na;
+            (void)nb;
+#else
             decide<N, FORM, PERN>(a, ga, m0, na, ci.x, la.x, ax.x, coa, ca, fa);
             decide<N, FORM, PERN>(a, gb, m1, nb, ci.y, la.y, ax.y, cob, cb, fb);
+#endif
             if constexpr (INPLACE) {
                 // the lane's 16 bytes of the committed row it has just read (groups ga, gb)
                 st_stream2(const_cast<uint64_t *>(t) + NR * T, (u64x2){coa, cob});
