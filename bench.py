@@ -835,6 +835,7 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
     acc = dict(handle_ns=0, pass_ns=0, pack_ns=0, device_ns=0, apply_ns=0, gpu_passes=0,
                decisions=0)
     t_total, n_events, committed, t_enc, nb_total = 0.0, 0, None, 0.0, 0
+    step_ms = []
     warm = 2       # untimed: allocations, first touch, and the first step with commits (its
     for s in range(steps + warm):   # output lists size the pinned result buffers)
         full = events(s) if events else step_events(hq, G, s, roles)
@@ -866,6 +867,7 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
                          for c in cids[:min(4096, bounds[1])]]
         if s < warm:
             continue
+        step_ms.append(round(dt * 1e3, 3))
         t_total += dt
         n_events += n_step
         for r in res:
@@ -876,6 +878,7 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
     if pin_ctx is not None:
         pin_ctx.close()
     acc["stream_bytes"] = nb_total
+    acc["step_ms"] = step_ms
     return t_total, n_events, acc, committed, (g, m), t_enc
 
 
@@ -931,6 +934,7 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             "value": d.sum(float(ne)) / elapsed,
             "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
             "ms_per_step": elapsed / steps * 1e3,
+            "step_ms": acc["step_ms"],
             "gpu_passes_per_step": acc["gpu_passes"] / steps / W,
             "host_ms_per_step_per_worker": acc["handle_ns"] / steps / W / 1e6,
             "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
