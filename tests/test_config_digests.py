@@ -1,0 +1,108 @@
+"""Golden digests of the BASELINE configs at full size (tests/golden/config_digests.json, made
+by tests/golden/make_config_digests.py from the oracle's decisions on the generator's inputs).
+
+CPU: the oracle and the CPU generator still reproduce them (1 M-group configs; the ring and mask
+forms of C3 have one digest). GPU: the kernels, fed by the device generator, produce the same
+bytes in the headline layouts — leader-row tiles (term-start, mask), the ring gather in
+columns, the bit-plane and 4-byte bitmap paths, and C5's fused three-bucket launch."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import qref
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "config_digests.json")))
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_ring_and_mask_forms_share_one_digest():
+    for k in ("committed", "changed", "fallback"):
+        assert GOLD["C3_ring"][k] == GOLD["C3_mask"][k]
+
+
+@pytest.mark.parametrize("name", ["C2", "C3_mask"])
+def test_oracle_reproduces_digest(name):
+    c = GOLD[name]
+    inp = qref.CommitInputs(qref.spec(c["seed"], c["G"], c["n"], cid_base=c["cid_base"],
+                                      cid_stride=c["cid_stride"]))
+    out, chg, fb, rc = inp.run(c["form"], False, nthreads=os.cpu_count() or 1)
+    assert rc == 0
+    assert (digest(out), digest(chg), digest(fb)) == (c["committed"], c["changed"], c["fallback"])
+
+
+def _commit_on_gpu(ctx, hq, cases, layout):
+    """Generate every case on the device, decide them (one fused launch when several), return
+    each case's (committed, changed, fallback) digests."""
+    bufs = []
+    for c in cases:
+        tiled = layout is not None
+        b = hq.alloc_commit(ctx, c["G"], c["n"], c["form"], 16, tiled=tiled,
+                            tile_layout=layout if tiled else hq.HQ_LAYOUT_TILES)
+        ctx.synth_commit_dev(hq.synth_spec(c["seed"], c["G"], c["n"], cid_base=c["cid_base"],
+                                           cid_stride=c["cid_stride"]), b.args())
+        if tiled:
+            ctx.tile_commit_dev(b.args(), b.tiles, layout)
+        bufs.append(b)
+    ctx.sync()
+    if len(bufs) > 1:
+        ctx.commit_fused_dev(hq.commit_batch_array([b.tile_args() for b in bufs]))
+    else:
+        ctx.commit_dev(bufs[0].tile_args() if layout is not None else bufs[0].args())
+    ctx.sync()
+    res = []
+    for c, b in zip(cases, bufs):
+        res.append((digest(ctx.download(b.committed_out)[:c["G"]]), digest(ctx.download(b.changed)),
+                    digest(ctx.download(b.fallback))))
+        hq.free_commit(ctx, b)
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,layout", [("C2", "leader"), ("C3_mask", "leader"),
+                                         ("C3_mask", "tiles"), ("C3_ring", None)])
+def test_gpu_commit_digest(gpu_ctx, hq, name, layout):
+    c = GOLD[name]
+    lay = {"leader": hq.HQ_LAYOUT_TILES_LEADER, "tiles": hq.HQ_LAYOUT_TILES, None: None}[layout]
+    got = _commit_on_gpu(gpu_ctx, hq, [c], lay)[0]
+    assert got == (c["committed"], c["changed"], c["fallback"])
+
+
+@pytest.mark.gpu
+def test_gpu_c5_fused_digest(gpu_ctx, hq):
+    cases = [GOLD[f"C5_bucket{b}"] for b in range(3)]
+    got = _commit_on_gpu(gpu_ctx, hq, cases, hq.HQ_LAYOUT_TILES_LEADER)
+    for c, g in zip(cases, got):
+        assert g == (c["committed"], c["changed"], c["fallback"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["planes", "columns"])
+def test_gpu_c4_digest(gpu_ctx, hq, path):
+    c = GOLD["C4"]
+    G, n = c["G"], c["n"]
+    cols = [gpu_ctx.empty(G, np.uint8) for _ in range(4)]      # ack, granted, rejected, n
+    gpu_ctx.synth_bitmaps_dev(hq.synth_spec(c["seed"], G, n), *cols)
+    conf = gpu_ctx.empty(hq.words64(G), np.uint64)
+    outc = gpu_ctx.empty(hq.words32(G), np.uint64)
+    extra = []
+    if path == "planes":
+        planes = gpu_ctx.empty(hq.plane_tiles(G) * 3 * hq.HQ_PLANE_TILE_GROUPS, np.uint8)
+        fb = gpu_ctx.empty(hq.words64(G), np.uint64)
+        gpu_ctx.tile_planes_dev(G, *cols, 0, planes, fb)
+        gpu_ctx.readindex_vote_planes_dev(G, planes, conf, outc)
+        gpu_ctx.sync()
+        assert not gpu_ctx.download(fb).any()      # every generated group is in the contract
+        extra = [planes, fb]
+    else:
+        gpu_ctx.readindex_vote_dev(G, cols[0], cols[1], cols[2], cols[3], 0, conf, outc)
+        gpu_ctx.sync()
+    assert digest(gpu_ctx.download(conf)) == c["confirmed"]
+    assert digest(gpu_ctx.download(outc)) == c["outcome"]
+    for x in cols + [conf, outc] + extra:
+        gpu_ctx.free(x)

@@ -43,6 +43,9 @@ for s in range(STEPS):
     res = jobs.run(copy=False)
     dt = time.perf_counter() - t0
     dev = max(r["device_ns"] for r in res) / 1e6
+    if os.environ.get("PER_WORKER") and W > 1:
+        print("  device ms per worker:", " ".join(f"{r['device_ns'] / 1e6:.2f}" for r in res),
+              "| host ms:", " ".join(f"{r['handle_ns'] / 1e6:.2f}" for r in res), flush=True)
     print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, W={W}, "
           f"max device {dev:.2f} ms, input {sum(x.nbytes for p in inputs for x in p) / 1e6:.1f} MB",
           flush=True)
