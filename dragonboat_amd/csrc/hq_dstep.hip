@@ -51,13 +51,17 @@ struct StepK {
     const uint8_t *bytes;
     uint32_t *counts;             // [kLists][n] (+1): pass A output
     const uint32_t *scan;         // exclusive scan of counts: pass B input
-    hq_commit_event *commits;
-    hq_ready_to_read *ready;
-    hq_read_index_resp *resps;
-    hq_state_change *states;
-    hq_dropped_read *dropped;
-    uint64_t *deferred;
-    uint64_t *fallback;
+    char *out;                    // pass B: the lists, written straight into pinned host memory
+    const struct Layout *layout;  //   at layout->off[list]
+};
+
+// where the lists go in the host output region (k_layout, from the scanned counts); a step with
+// an input error or a region too small has pass B write nothing, not even state
+struct Layout {
+    uint64_t off[kLists];
+    uint32_t len[kLists];
+    uint64_t total;
+    uint32_t error, overflow;
 };
 
 __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
@@ -160,27 +164,33 @@ struct Engine {
         for (int s = 0; s < (int)MC; ++s) match[s] = s == mi ? v : match[s];
     }
     __device__ __forceinline__ uint32_t slot(int l) { return base[l] + cnt[l]++; }
+    template <class T>
+    __device__ __forceinline__ T *list(int l) const {   // (uniform: scalar loads of the layout)
+        return reinterpret_cast<T *>(a.out + a.layout->off[l]);
+    }
 
     // -- outputs ----------------------------------------------------------------------------
     __device__ __forceinline__ void ready(uint64_t index, uint64_t low, uint64_t high) {
         const uint32_t p = slot(kReady);
-        if (WRITE) a.ready[p] = hq_ready_to_read{g.cluster_id, index, low, high};
+        if (WRITE) list<hq_ready_to_read>(kReady)[p] = hq_ready_to_read{g.cluster_id, index, low, high};
     }
     __device__ __forceinline__ void resp(uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
         const uint32_t p = slot(kResps);
-        if (WRITE) a.resps[p] = hq_read_index_resp{g.cluster_id, to, index, hint, high};
+        if (WRITE)
+            list<hq_read_index_resp>(kResps)[p] = hq_read_index_resp{g.cluster_id, to, index, hint, high};
     }
     __device__ __forceinline__ void state_change(uint32_t reason) {
         const uint32_t p = slot(kStates);
-        if (WRITE) a.states[p] = hq_state_change{g.cluster_id, g.term, g.state, reason};
+        if (WRITE) list<hq_state_change>(kStates)[p] = hq_state_change{g.cluster_id, g.term, g.state, reason};
     }
     __device__ __forceinline__ void dropped(uint64_t low, uint64_t high, uint64_t from, uint32_t reason) {
         const uint32_t p = slot(kDropped);
-        if (WRITE) a.dropped[p] = hq_dropped_read{g.cluster_id, low, high, from, reason, 0};
+        if (WRITE)
+            list<hq_dropped_read>(kDropped)[p] = hq_dropped_read{g.cluster_id, low, high, from, reason, 0};
     }
     __device__ __forceinline__ void defer(uint64_t e) {
         const uint32_t p = slot(kDeferred);
-        if (WRITE) a.deferred[p] = e;
+        if (WRITE) list<uint64_t>(kDeferred)[p] = e;
     }
 
     // -- reference state transitions (raft.go:949-1010) --------------------------------------
@@ -390,13 +400,13 @@ struct Engine {
             if (!ok) {                                   // this event and the rest are deferred
                 g.flags |= kDSuspended;
                 const uint32_t p = slot(kFallback);
-                if (WRITE) a.fallback[p] = g.cluster_id;
+                if (WRITE) list<uint64_t>(kFallback)[p] = g.cluster_id;
                 defer(e);
             }
         }
         if (g.committed != committed0) {
             const uint32_t p = slot(kCommits);
-            if (WRITE) a.commits[p] = hq_commit_event{g.cluster_id, g.committed};
+            if (WRITE) list<hq_commit_event>(kCommits)[p] = hq_commit_event{g.cluster_id, g.committed};
         }
     }
 
@@ -418,6 +428,7 @@ template <bool WRITE, bool STREAM, int MC>
 __global__ __launch_bounds__(256) void k_step(const StepK a) {
     const uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.i_end) return;
+    if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
     const uint32_t h = a.handles[i];
     if (!WRITE) {                 // validate this group's entry; a bad one is not stepped
         uint32_t err = 0;
@@ -448,18 +459,26 @@ __global__ __launch_bounds__(256) void k_step(const StepK a) {
     }
 }
 
-// the scanned counts at every chunk boundary (row c: scan[l * n + bound[c]] for every list l;
-// the last row holds the ends of the lists, its last entry the grand total) and the input errors
+// the lists' place in the host output region (of cap bytes) from the scanned counts, and the
+// input errors of pass A (reset for the next step)
 constexpr int kMaxChunks = 4;
-struct Bounds { uint64_t b[kMaxChunks + 1]; };
-__global__ void k_list_bases(const uint32_t *scan, uint64_t n, Bounds bd, int chunks,
-                             const uint32_t *error, uint32_t *bases) {
-    const int t = threadIdx.x;
-    if (t < (chunks + 1) * kLists) {
-        const int c = t / kLists, l = t % kLists;
-        bases[t] = scan[(uint64_t)l * n + bd.b[c]];
+__global__ void k_layout(const uint32_t *scan, uint64_t n, uint32_t *error, uint64_t cap,
+                         Layout *lay) {
+    if (threadIdx.x != 0) return;
+    const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
+                                  sizeof(hq_read_index_resp), sizeof(hq_state_change),
+                                  sizeof(hq_dropped_read), 8, 8, 0};
+    uint64_t total = 0;
+    for (int l = 0; l < kLists; ++l) {
+        const uint32_t len = scan[(uint64_t)(l + 1) * n] - scan[(uint64_t)l * n];
+        lay->off[l] = total;
+        lay->len[l] = len;
+        total += (len * rec[l] + 255) & ~uint64_t(255);
     }
-    if (t == 63) bases[(chunks + 1) * kLists] = *error;
+    lay->total = total;
+    lay->error = *error;
+    lay->overflow = total > cap;
+    *error = 0;
 }
 
 uint64_t now_ns() {
@@ -487,15 +506,15 @@ struct hq_dstep {
     size_t cnt_cap = 0;
     void *scan_tmp = nullptr;
     size_t scan_tmp_cap = 0;
-    void *out = nullptr;
-    size_t out_cap = 0;
-    void *host_out = nullptr;     // pinned: the lists come back into it
+    void *host_out = nullptr;     // pinned host region pass B writes the lists into
     size_t host_out_cap = 0;
+    Layout *layout = nullptr;     // device: the lists' places (k_layout)
+    Layout *host_layout = nullptr;  // pinned mirror, copied back at the end of the step
     // a large step runs in chunks of groups: chunk c's input copy (copy stream) overlaps pass A
     // of chunk c - 1, and its result copy overlaps pass B of chunk c + 1 (compute stream); the
     // copy stream is created by the first such step
     hipStream_t copy = nullptr;
-    hipEvent_t ev_in[kMaxChunks] = {}, ev_b[kMaxChunks] = {};
+    hipEvent_t ev_in[kMaxChunks] = {};
     hipEvent_t ev_sync = nullptr;  // blocking-sync event: a waiting worker thread sleeps
 };
 
@@ -551,8 +570,11 @@ int hq_dstep_open(hq_ctx *ctx, hq_dstep **out) {
                            "event");
     for (int c = 0; c < kMaxChunks && !rc; ++c) {
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_in[c], hipEventDisableTiming), "event");
-        if (!rc) rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_b[c], hipEventDisableTiming), "event");
     }
+    if (!rc) rc = hq::check_hip(ctx, hipMalloc(&d->layout, sizeof(Layout)), "hq_dstep layout");
+    if (!rc)
+        rc = hq::check_hip(ctx, hipHostMalloc(&d->host_layout, sizeof(Layout), hipHostMallocDefault),
+                           "hq_dstep layout");
     if (rc) {
         hq_dstep_close(d);
         *out = nullptr;
@@ -565,9 +587,11 @@ void hq_dstep_close(hq_dstep *d) {
     (void)hipSetDevice(d->ctx->device);
     (void)hipStreamSynchronize(d->ctx->stream);
     for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, (void *)d->stamp, d->in,
-                    (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp, d->out})
+                    (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp,
+                    (void *)d->layout})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
+    if (d->host_layout) (void)hipHostFree(d->host_layout);
     if (d->copy) {
         (void)hipStreamSynchronize(d->copy);
         (void)hipStreamDestroy(d->copy);
@@ -575,7 +599,6 @@ void hq_dstep_close(hq_dstep *d) {
     if (d->ev_sync) (void)hipEventDestroy(d->ev_sync);
     for (int c = 0; c < kMaxChunks; ++c) {
         if (d->ev_in[c]) (void)hipEventDestroy(d->ev_in[c]);
-        if (d->ev_b[c]) (void)hipEventDestroy(d->ev_b[c]);
     }
     delete d;
 }
@@ -650,10 +673,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     if (n == 0) return HQ_OK;
     const uint64_t t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    // chunks of groups (at least 64 Ki each): copies overlap the passes of neighbouring chunks
+    // chunks of groups (at least 64 Ki each): chunk c's input copy overlaps pass A of chunk c - 1
     const int chunks = n >= 4 * 65536 ? 4 : n >= 2 * 65536 ? 2 : 1;
-    Bounds bd{};
-    for (int c = 0; c <= chunks; ++c) bd.b[c] = n * c / chunks;
+    uint64_t bound[kMaxChunks + 1];
+    for (int c = 0; c <= chunks; ++c) bound[c] = n * c / chunks;
     // the step's input in one device region: handles, offsets, [boffsets,] events or bytes, each
     // at the offsets it has on the host
     auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -662,12 +685,12 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const size_t o_ev = o_boff + (stream ? up((n + 1) * 8) : 0);
     const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event));
     if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
-    char *din = static_cast<char *>(d->in);
-    // one chunk: every copy on the compute stream (nothing to overlap, no cross-stream waits)
     if (!rc && chunks > 1 && !d->copy)       // the copy stream of the first chunked step
         rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
                            "hq_dstep copy stream");
+    // one chunk: every copy on the compute stream (nothing to overlap, no cross-stream waits)
     hipStream_t cs = chunks > 1 ? d->copy : ctx->stream;
+    char *din = static_cast<char *>(d->in);
     auto h2d = [&](size_t off, const void *src, size_t bytes) {
         if (!rc && bytes)
             rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
@@ -679,8 +702,19 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     if (!rc && cn > d->cnt_cap) {
         rc = grow(ctx, reinterpret_cast<void **>(&d->counts), &cc, cn * 4, false, "hq_dstep counts");
         if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->scan), &sc, cn * 4, false, "hq_dstep scan");
-        if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 256, false, "hq_dstep bases");
+        if (!rc && !d->bases) {
+            rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 256, false, "hq_dstep error");
+            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 4, ctx->stream), "memset");
+        }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
+    }
+    // the host region the lists go to: last step's size with room to spare (a step that needs
+    // more runs pass B again after growing it)
+    if (!rc && !d->host_out) {
+        const size_t want = std::max<size_t>(n * 64, 1 << 16);
+        rc = hq::check_hip(ctx, hipHostMalloc(&d->host_out, want, hipHostMallocDefault),
+                           "hq_dstep pinned output");
+        if (!rc) d->host_out_cap = want;
     }
     size_t tmp = 0;
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d->counts,
@@ -713,9 +747,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (rc) return rc;
     }
     k.step_no = d->step_no;
-    k.error = d->bases + 63;
+    k.error = d->bases;           // zero here: reset by the previous step's k_layout
+    k.out = static_cast<char *>(d->host_out);
+    k.layout = d->layout;
     rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
-    if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(k.error, 0, 4, ctx->stream), "memset");
     const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
     auto launch = [&](bool write, uint64_t i0, uint64_t i1) {
         k.i_begin = i0;
@@ -737,9 +772,9 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
 #undef HQ_STEP_LAUNCH
         rc = hq::post_launch(ctx, write ? "k_step<write>" : "k_step<count>");
     };
-    // inputs chunk by chunk on the copy stream, pass A of each chunk once it has landed
+    // inputs chunk by chunk, pass A of each chunk once it has landed
     for (int c = 0; c < chunks && !rc; ++c) {
-        const uint64_t i0 = bd.b[c], i1 = bd.b[c + 1];
+        const uint64_t i0 = bound[c], i1 = bound[c + 1];
         h2d(i0 * 4, in->groups + i0, (i1 - i0) * 4);
         h2d(o_off + i0 * 8, in->offsets + i0, (i1 - i0 + 1) * 8);
         if (stream) {
@@ -762,88 +797,56 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
                                 "hipcub scan");
-    if (!rc) {
-        hipLaunchKernelGGL(k_list_bases, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, bd,
-                           chunks, k.error, d->bases);
-        rc = hq::check_hip(ctx, hipGetLastError(), "k_list_bases");
-    }
-    uint32_t bases[(kMaxChunks + 1) * kLists + 1];
-    const size_t nbases = (size_t)(chunks + 1) * kLists + 1;
-    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(bases, d->bases, nbases * 4,
-                                                    hipMemcpyDeviceToHost, ctx->stream), "D2H");
-    if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
+    // layout, pass B (straight into the pinned region), the layout back: one wait per step
+    auto pass_b = [&]() {
+        if (!rc) {
+            hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, k.error,
+                               (uint64_t)d->host_out_cap, d->layout);
+            rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
+        }
+        launch(true, 0, n);
+        if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(d->host_layout, d->layout, sizeof(Layout),
+                                                        hipMemcpyDeviceToHost, ctx->stream), "D2H");
+        if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
+    };
+    pass_b();
+    const uint64_t t1 = now_ns();
     if (rc) return rc;
-    if (bases[nbases - 1]) {      // no group state was written
-        out->input_error = bases[nbases - 1];
+    const Layout &lay = *d->host_layout;
+    if (lay.error) {              // no group state was written
+        out->input_error = lay.error;
         return HQ_E_INVAL;
     }
-    const uint64_t t1 = now_ns();
-    const uint32_t *first = bases, *last = bases + (size_t)chunks * kLists;
-    uint64_t len[kLists];
-    for (int l = 0; l < kLists; ++l) len[l] = last[l] - first[l];
-    // the output lists in one device region, mirrored by one pinned host region
-    const size_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
-                                sizeof(hq_read_index_resp), sizeof(hq_state_change),
-                                sizeof(hq_dropped_read), 8, 8, 0};
-    size_t off[kLists], total = 0;
-    for (int l = 0; l < kLists; ++l) {
-        off[l] = total;
-        total += up(len[l] * rec[l]);
-    }
-    rc = grow(ctx, &d->out, &d->out_cap, total + 256, false, "hq_dstep output");
-    if (!rc && total + 256 > d->host_out_cap) {
+    if (lay.overflow) {           // grow the region and write the lists again
         if (d->host_out) (void)hipHostFree(d->host_out);
         d->host_out = nullptr;
         d->host_out_cap = 0;
-        const size_t want = (total + 256) + (total + 256) / 2;
+        const size_t want = lay.total + lay.total / 2;
         rc = hq::check_hip(ctx, hipHostMalloc(&d->host_out, want, hipHostMallocDefault),
                            "hq_dstep pinned output");
-        if (!rc) d->host_out_cap = want;
+        if (rc) return rc;
+        d->host_out_cap = want;
+        k.out = static_cast<char *>(d->host_out);
+        pass_b();
+        if (rc) return rc;
+        if (lay.overflow || lay.error) return hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout");
     }
-    if (rc) return rc;
-    char *o = static_cast<char *>(d->out);
-    char *ho = static_cast<char *>(d->host_out);
-    k.commits = reinterpret_cast<hq_commit_event *>(o + off[kCommits]);
-    k.ready = reinterpret_cast<hq_ready_to_read *>(o + off[kReady]);
-    k.resps = reinterpret_cast<hq_read_index_resp *>(o + off[kResps]);
-    k.states = reinterpret_cast<hq_state_change *>(o + off[kStates]);
-    k.dropped = reinterpret_cast<hq_dropped_read *>(o + off[kDropped]);
-    k.deferred = reinterpret_cast<uint64_t *>(o + off[kDeferred]);
-    k.fallback = reinterpret_cast<uint64_t *>(o + off[kFallback]);
-    // pass B chunk by chunk; each chunk's records go back on the copy stream behind it
-    for (int c = 0; c < chunks && !rc; ++c) {
-        launch(true, bd.b[c], bd.b[c + 1]);
-        if (chunks > 1) {
-            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_b[c], ctx->stream), "event");
-            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(cs, d->ev_b[c], 0), "wait");
-        }
-        const uint32_t *cb = bases + (size_t)c * kLists, *ce = cb + kLists;
-        for (int l = 0; l < kLists - 1 && !rc; ++l) {
-            const size_t a = off[l] + (size_t)(cb[l] - first[l]) * rec[l];
-            const size_t bytes = (size_t)(ce[l] - cb[l]) * rec[l];
-            if (bytes)
-                rc = hq::check_hip(ctx, hipMemcpyAsync(ho + a, o + a, bytes, hipMemcpyDeviceToHost,
-                                                       cs), "D2H");
-        }
-    }
-    if (!rc && chunks > 1) rc = wait_stream(d, cs, "hq_dstep sync");
-    if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
-    if (rc) return rc;
-    out->commits = reinterpret_cast<const hq_commit_event *>(ho + off[kCommits]);
-    out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + off[kReady]);
-    out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + off[kResps]);
-    out->states = reinterpret_cast<const hq_state_change *>(ho + off[kStates]);
-    out->dropped = reinterpret_cast<const hq_dropped_read *>(ho + off[kDropped]);
-    out->deferred = reinterpret_cast<const uint64_t *>(ho + off[kDeferred]);
-    out->fallback = reinterpret_cast<const uint64_t *>(ho + off[kFallback]);
-    out->n_commits = len[kCommits];
-    out->n_ready = len[kReady];
-    out->n_resps = len[kResps];
-    out->n_states = len[kStates];
-    out->n_dropped = len[kDropped];
-    out->n_deferred = len[kDeferred];
-    out->n_fallback = len[kFallback];
-    out->decisions = len[kDecisions];
+    const char *ho = static_cast<const char *>(d->host_out);
+    out->commits = reinterpret_cast<const hq_commit_event *>(ho + lay.off[kCommits]);
+    out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + lay.off[kReady]);
+    out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + lay.off[kResps]);
+    out->states = reinterpret_cast<const hq_state_change *>(ho + lay.off[kStates]);
+    out->dropped = reinterpret_cast<const hq_dropped_read *>(ho + lay.off[kDropped]);
+    out->deferred = reinterpret_cast<const uint64_t *>(ho + lay.off[kDeferred]);
+    out->fallback = reinterpret_cast<const uint64_t *>(ho + lay.off[kFallback]);
+    out->n_commits = lay.len[kCommits];
+    out->n_ready = lay.len[kReady];
+    out->n_resps = lay.len[kResps];
+    out->n_states = lay.len[kStates];
+    out->n_dropped = lay.len[kDropped];
+    out->n_deferred = lay.len[kDeferred];
+    out->n_fallback = lay.len[kFallback];
+    out->decisions = lay.len[kDecisions];
     out->kernel_ns = t1 - t0;
     out->d2h_ns = now_ns() - t1;
     return HQ_OK;
