@@ -129,7 +129,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,cq,ing,ingo,w2,e2e,step,step5")
+                  "rimt,cq,ing,ingo,ingu,w2,e2e,step,step5")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -515,7 +515,8 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
       rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
       cq:  CheckQuorum (k_bits CHECKQ), 16M groups x 7 voters, active flags reset in place
       ing: match-delta ingest (k_ingest_match), 4M ReplicateResp deltas into a 4M x 3 table
-      ingo: the same deltas in group order, the order a step worker emits them"""
+      ingo: the same deltas in group order, the order a step worker emits them
+      ingu: distinct (group, slot) keys in random order (HQ_INGEST_UNIQUE)"""
     from dragonboat_amd import hipquorum as hq
 
     ctx = hq.Context(d.device)
@@ -580,8 +581,12 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
         ctx.memset(table, 0)
         ups = []
         for k in range(nsets):
-            g = r.integers(0, G, U, dtype=np.uint64)
-            s = r.integers(1, n, U, dtype=np.uint64)
+            if name == "ingu":     # distinct (group, slot) keys: a step's final ack per member
+                keys = r.permutation(G * (n - 1))[:U].astype(np.uint64)
+                g, s = keys // np.uint64(n - 1), keys % np.uint64(n - 1) + np.uint64(1)
+            else:
+                g = r.integers(0, G, U, dtype=np.uint64)
+                s = r.integers(1, n, U, dtype=np.uint64)
             u = np.stack([(g << np.uint64(8)) | s,
                           np.uint64(1 << 30) + np.uint64(k) + r.integers(0, 64, U, dtype=np.uint64)],
                          axis=1)
@@ -589,15 +594,18 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                 # the order a step worker emits them: node by node (execengine.go:923-1000)
                 u = u[np.argsort(u[:, 0], kind="stable")]
             ups.append(ctx.upload(u.reshape(-1)))
-        flags = hq.HQ_INGEST_GROUPED if name == "ingo" else 0
+        flags = {"ingo": hq.HQ_INGEST_GROUPED, "ingu": hq.HQ_INGEST_UNIQUE}.get(name, 0)
 
         def run(i):
             ctx.table_ingest_match_dev(ups[i % nsets], U, table, G, n, form, flags)
         desc = (f"{name}: ReplicateResp match-delta ingest (remote.tryUpdate) into a {G} x {n} "
                 f"device table in the headline layout (leader-row tiles), {U} deltas "
-                + ("in group order (as a step worker emits them): runs reduced in registers, "
-                   "plain read-modify-write, atomics only at wave edges (HQ_INGEST_GROUPED)"
-                   if name == "ingo" else "in random order: one 64-bit atomic max each"))
+                + {"ingo": "in group order (as a step worker emits them): runs reduced in "
+                           "registers, plain read-modify-write, atomics only at wave edges "
+                           "(HQ_INGEST_GROUPED)",
+                   "ingu": "with distinct (group, slot) keys in random order: one plain "
+                           "read-modify-write each (HQ_INGEST_UNIQUE)"}.get(
+                       name, "in random order: one 64-bit atomic max each"))
         units, unit = U, "updates/s"
     elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
     ctx.close()
@@ -1151,7 +1159,7 @@ def main():
             elif name in STEP_ROLES:
                 steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
                                                name=name))
-            elif name in ("rim", "rimt", "cq", "ing", "ingo"):
+            elif name in ("rim", "rimt", "cq", "ing", "ingo", "ingu"):
                 kern.append(run_kernel_leg(name, max(50, args.steps // 4),
                                            max(5, args.warmup // 4), d))
             elif name.startswith("w") and name[1:].isdigit():

@@ -125,9 +125,13 @@ constexpr int kIV = HQ_INGEST_V;
 
 // One launch applies match raises: key = group << 8 | slot (match form) or group << 4 | slot
 // (lag form), value = the acknowledged index. LAG: 8-byte records, index = lastIndex - lag.
-template <bool GROUPED, bool LAG>
+// MODE: kAtomic (any batch), kGrouped (HQ_INGEST_GROUPED), kUnique (HQ_INGEST_UNIQUE: every key
+// at most once, so each record is a plain read-modify-write of its own word)
+enum IngestMode { kAtomic = 0, kGrouped = 1, kUnique = 2 };
+template <int MODE, bool LAG>
 __global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uint64_t count,
                                                           TableK t, uint64_t *n_skipped) {
+    constexpr bool GROUPED = MODE == kGrouped;
     const uint64_t lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * (kTBlock / 64) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kTBlock / 64);
@@ -195,6 +199,16 @@ __global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uin
                                        (unsigned long long)v[c]);
                 else if (v[c] > old[c]) *p[c] = v[c];
             }
+        } else if constexpr (MODE == kUnique) {
+            uint64_t *p[kIV], old[kIV];
+#pragma unroll
+            for (int c = 0; c < kIV; ++c) {        // every table load first, then the stores
+                p[c] = trow(t, key[c] >> SH, (uint32_t)(key[c] & ((1u << SH) - 1)) - 1);
+                old[c] = ok[c] && !skip[c] ? *p[c] : ~0ull;
+            }
+#pragma unroll
+            for (int c = 0; c < kIV; ++c)
+                if (ok[c] && !skip[c] && v[c] > old[c]) *p[c] = v[c];
         } else {
 #pragma unroll
             for (int c = 0; c < kIV; ++c)
@@ -232,9 +246,10 @@ __device__ __forceinline__ void apply_append(const TableK &t, uint64_t g, uint64
 }
 
 // COUNT = 0: hq_append_update (group, new_last); 1: 8-byte group << 32 | n
-template <bool COUNT, bool GROUPED>
+template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kTBlock) void k_table_append(const uint64_t *u, uint64_t count,
                                                           TableK t, uint64_t *n_skipped) {
+    constexpr bool GROUPED = MODE == kGrouped;
     for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
          i += (uint64_t)gridDim.x * kTBlock) {
         uint64_t key = ~0ull, v = 0;
@@ -260,7 +275,7 @@ __global__ __launch_bounds__(kTBlock) void k_table_append(const uint64_t *u, uin
             const RunTail r = run_tail(key);
             if (keyok && r.tail && v) apply_append<COUNT>(t, key, v, r.edge);
         } else {
-            if (ok) apply_append<COUNT>(t, key, v, true);
+            if (ok) apply_append<COUNT>(t, key, v, MODE == kAtomic);   // unique: plain
         }
         count_skip(n_skipped, i < count && !ok);
     }
@@ -294,7 +309,7 @@ int table_k(hq_ctx *ctx, const char *what, uint64_t *tiles, uint64_t G, uint32_t
     if (form == HQ_FORM_TERM_MASK &&
         (ring_len < 1 || ring_len > 16 || (ring_len & (ring_len - 1))))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": ring_len must be a power of two <= 16");
-    if (flags & ~HQ_INGEST_GROUPED)
+    if (flags & ~(HQ_INGEST_GROUPED | HQ_INGEST_UNIQUE))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": unknown flags");
     t.tiles = tiles;
     t.G = G;
@@ -323,12 +338,15 @@ int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint6
     if ((rc = hq::pre_launch(ctx))) return rc;
     const uint64_t *u = reinterpret_cast<const uint64_t *>(updates);
     const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
-    if (flags & HQ_INGEST_GROUPED)
-        hipLaunchKernelGGL((k_table_ingest<true, false>), grid, blk, 0, ctx->stream, u, count, t,
-                           n_skipped);
+    if (flags & HQ_INGEST_UNIQUE)
+        hipLaunchKernelGGL((k_table_ingest<kUnique, false>), grid, blk, 0, ctx->stream, u, count,
+                           t, n_skipped);
+    else if (flags & HQ_INGEST_GROUPED)
+        hipLaunchKernelGGL((k_table_ingest<kGrouped, false>), grid, blk, 0, ctx->stream, u, count,
+                           t, n_skipped);
     else
-        hipLaunchKernelGGL((k_table_ingest<false, false>), grid, blk, 0, ctx->stream, u, count, t,
-                           n_skipped);
+        hipLaunchKernelGGL((k_table_ingest<kAtomic, false>), grid, blk, 0, ctx->stream, u, count,
+                           t, n_skipped);
     return hq::post_launch(ctx, "k_table_ingest");
 }
 
@@ -343,12 +361,15 @@ int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count
     if (!updates) return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_lag_dev: updates NULL");
     if ((rc = hq::pre_launch(ctx))) return rc;
     const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
-    if (flags & HQ_INGEST_GROUPED)
-        hipLaunchKernelGGL((k_table_ingest<true, true>), grid, blk, 0, ctx->stream, updates, count,
-                           t, n_skipped);
+    if (flags & HQ_INGEST_UNIQUE)
+        hipLaunchKernelGGL((k_table_ingest<kUnique, true>), grid, blk, 0, ctx->stream, updates,
+                           count, t, n_skipped);
+    else if (flags & HQ_INGEST_GROUPED)
+        hipLaunchKernelGGL((k_table_ingest<kGrouped, true>), grid, blk, 0, ctx->stream, updates,
+                           count, t, n_skipped);
     else
-        hipLaunchKernelGGL((k_table_ingest<false, true>), grid, blk, 0, ctx->stream, updates, count,
-                           t, n_skipped);
+        hipLaunchKernelGGL((k_table_ingest<kAtomic, true>), grid, blk, 0, ctx->stream, updates,
+                           count, t, n_skipped);
     return hq::post_launch(ctx, "k_table_ingest");
 }
 
@@ -363,15 +384,21 @@ static int table_append(hq_ctx *ctx, const char *what, const uint64_t *updates, 
     if (!updates || (!counts && !hq::aligned16(updates)))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": updates NULL or misaligned");
     if ((rc = hq::pre_launch(ctx))) return rc;
-    const bool grouped = flags & HQ_INGEST_GROUPED;
+    const int mode = (flags & HQ_INGEST_UNIQUE) ? kUnique : (flags & HQ_INGEST_GROUPED) ? kGrouped
+                                                                                         : kAtomic;
     const dim3 grid(tgrid(count)), blk(kTBlock);
+#define HQ_APPEND(C, M) \
+    hipLaunchKernelGGL((k_table_append<C, M>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped)
     if (counts) {
-        if (grouped) hipLaunchKernelGGL((k_table_append<true, true>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
-        else hipLaunchKernelGGL((k_table_append<true, false>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
+        if (mode == kUnique) HQ_APPEND(true, kUnique);
+        else if (mode == kGrouped) HQ_APPEND(true, kGrouped);
+        else HQ_APPEND(true, kAtomic);
     } else {
-        if (grouped) hipLaunchKernelGGL((k_table_append<false, true>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
-        else hipLaunchKernelGGL((k_table_append<false, false>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped);
+        if (mode == kUnique) HQ_APPEND(false, kUnique);
+        else if (mode == kGrouped) HQ_APPEND(false, kGrouped);
+        else HQ_APPEND(false, kAtomic);
     }
+#undef HQ_APPEND
     return hq::post_launch(ctx, "k_table_append");
 }
 

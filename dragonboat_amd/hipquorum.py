@@ -36,6 +36,7 @@ HQ_LAG_LEADER_IMPLICIT = 1   # hq_commit_lag_args.flags: lag rows start at slot 
 HQ_TILE_GROUPS = 128
 HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table decided in place
 HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
+HQ_INGEST_UNIQUE = 2         # hq_table_*: every key at most once in the batch
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_ABI_VERSION = 9
 

@@ -568,9 +568,13 @@ int hq_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
  * grouped). Each wave then reduces its runs of equal keys with a segmented scan and applies a
  * run with one plain read-modify-write; runs that reach the wave's first or last lane (they may
  * continue in the next wave) use one atomic. Results equal the sequential application in any
- * order; a batch that is not grouped must not carry the flag.
+ * order; a batch that is not grouped must not carry the flag. HQ_INGEST_UNIQUE = the caller
+ * guarantees every key at most once in the batch (a step's final ack per (group, slot); one
+ * append per group): each record is one plain read-modify-write of its own table word, no scan
+ * and no atomic, in any order.
  */
 #define HQ_INGEST_GROUPED 1u
+#define HQ_INGEST_UNIQUE 2u
 int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
                               uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
                               uint32_t flags, uint64_t *n_skipped);

@@ -315,3 +315,72 @@ def test_pipeline_surfaces_fallback_groups(hq):
         p.set_committed(fbg, cpu)
         host["committed"] = out
     p.close()
+
+
+@pytest.mark.parametrize("lag", [False, True])
+def test_table_ingest_unique(gpu_ctx, hq, lag):
+    """HQ_INGEST_UNIQUE: every (group, slot) at most once, random order, plain read-modify-writes;
+    invalid records (slot 0, slot >= n, group out of range, ack above lastIndex) skipped."""
+    rng = np.random.default_rng(SEED + 40 + lag)
+    G, n = 60_007, 5
+    form = hq.HQ_FORM_TERM_MASK
+    inp = qref.CommitInputs(qref.spec(SEED + 4, G, n))
+    inp.last_index[:5] = inp.match[:5] = inp.committed_in[:5] = 10
+    dt = _table(gpu_ctx, hq, inp, form)
+    keys = rng.permutation(G * (n + 1))[:200_000].astype(np.uint64)   # distinct (g, s), s <= n
+    g, s = keys // np.uint64(n + 1), keys % np.uint64(n + 1)
+    g[:7] = np.uint64(G) + np.arange(7, dtype=np.uint64)              # out of range (distinct)
+    lg = rng.integers(0, 40, len(g), dtype=np.uint64)
+    gi = np.minimum(g, G - 1)
+    valid = (g < G) & (s >= 1) & (s < n)
+    if lag:
+        valid &= lg <= inp.last_index[gi]
+        wire = hq.pack_lag_updates(g, s, lg)
+        val = inp.last_index[gi] - np.minimum(lg, inp.last_index[gi])
+    else:
+        val = inp.last_index[gi] - lg
+        wire = np.stack([(g << np.uint64(8)) | s, val], axis=1).astype(np.uint64).reshape(-1)
+    want = inp.match.copy()
+    upd = np.stack([(g[valid] << np.uint64(8)) | s[valid], val[valid]], axis=1).astype(np.uint64)
+    qref.ingest_match(upd, want, G, G, n)
+    du = gpu_ctx.upload(wire)
+    skip = gpu_ctx.upload(np.zeros(1, np.uint64))
+    f = gpu_ctx.table_ingest_lag_dev if lag else gpu_ctx.table_ingest_match_dev
+    f(du, len(g), dt, G, n, form, hq.HQ_INGEST_UNIQUE, skip)
+    v = _view(gpu_ctx, hq, dt, G, n, form)
+    np.testing.assert_array_equal(v.match().reshape(-1), want)
+    assert int(gpu_ctx.download(skip)[0]) == int((~valid).sum())
+    for x in (dt, du, skip):
+        gpu_ctx.free(x)
+
+
+@pytest.mark.parametrize("counts", [False, True])
+def test_table_append_unique(gpu_ctx, hq, counts):
+    rng = np.random.default_rng(SEED + 50 + counts)
+    G, n, R = 40_009, 3, 16
+    form = hq.HQ_FORM_TERM_MASK
+    inp = qref.CommitInputs(qref.spec(SEED + 5, G, n))
+    dt = _table(gpu_ctx, hq, inp, form)
+    g = rng.permutation(G).astype(np.uint64)[:30_000]             # each group at most once
+    k = rng.choice(np.array([0, 1, 2, 3, 5, 15, 16, 17, 40], np.uint64), len(g))
+    last, match0, mask = inp.last_index.copy(), inp.match[:G].copy(), inp.term_mask.copy()
+    if counts:
+        app = np.stack([g[k > 0], last[g[k > 0]] + k[k > 0]], axis=1).astype(np.uint64)
+        wire = hq.pack_append_counts(g, k)
+        n_bad = int((k == 0).sum())
+    else:
+        newl = last[g] + k
+        app = np.stack([g, newl], axis=1).astype(np.uint64)
+        wire = app.reshape(-1)
+        n_bad = 0
+    qref.append(app, last, match0, mask, R, G)
+    du = gpu_ctx.upload(wire)
+    skip = gpu_ctx.upload(np.zeros(1, np.uint64))
+    f = gpu_ctx.table_append_count_dev if counts else gpu_ctx.table_append_dev
+    f(du, len(g), dt, G, n, form, R, hq.HQ_INGEST_UNIQUE, skip)
+    v = _view(gpu_ctx, hq, dt, G, n, form)
+    np.testing.assert_array_equal(v.row("last_index"), last)
+    np.testing.assert_array_equal(v.row("aux"), mask)
+    assert int(gpu_ctx.download(skip)[0]) == n_bad
+    for x in (dt, du, skip):
+        gpu_ctx.free(x)
