@@ -129,7 +129,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,cq,ing,ingo,ingu,w2,e2e,step,step5")
+                  "rimt,cq,ing,ingo,ingu,w2,e2e,step,step5,wire")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -992,6 +992,84 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
     return out
 
 
+def run_wire_leg(d: Dist, G=1 << 14, reps=20):
+    """The step worker's input from the wire (hq_wire.cpp), host side: the received messages of
+    a steady-state step of G leader groups (3 voters: a ReplicateResp and a HeartbeatResp from
+    each follower) marshalled as raftpb.MessageBatch bytes, one batch per sending node
+    (tests/wire_encode.py, the gogo layout), then per step: hq_wire_reset + hq_wire_add_batch of
+    every batch (protobuf decode, deployment / version check, per-cluster queues) +
+    hq_wire_step_stream (the step's event stream for the worker). One host thread; the bytes are
+    built outside the timed region. The stream it produces is then stepped on the device engine,
+    and its commits are checked against the same step fed as rows."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+    import wire_encode as we
+    from dragonboat_amd import hipquorum as hq
+
+    roles = STEP_ROLES["step"]
+    rng = _shard_of(d, G)
+    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
+    dep = 0x5EED
+    _, off, ev = step_events(hq, G, 1, roles)
+    msgs = {}
+    cols = {k: ev[k].tolist() for k in ("kind", "type", "from", "term", "log_index", "hint",
+                                        "hint_high")}
+    offl, cidl = off.tolist(), cids.tolist()
+    for i in range(G):
+        for j in range(offl[i], offl[i + 1]):
+            if cols["kind"][j] == hq.EV_MESSAGE:
+                msgs.setdefault(cols["from"][j], []).append(
+                    we.message(type=cols["type"][j], to=1, frm=cols["from"][j],
+                               cluster_id=cidl[i], term=cols["term"][j],
+                               log_index=cols["log_index"][j], hint=cols["hint"][j],
+                               hint_high=cols["hint_high"][j]))
+    batches = [we.batch(v, deployment_id=dep, source_address=b"n%d:63000" % k)
+               for k, v in sorted(msgs.items())]
+    n_msg = sum(len(v) for v in msgs.values())
+    n_bytes = sum(len(b) for b in batches)
+    w = hq.Worker(d.device, sum(r != "observer" for r in roles), on_device=True)
+    w.add_groups(g, m)
+    wire = hq.Wire(dep)
+    bufs = [np.frombuffer(b, np.uint8) for b in batches]
+    times = []
+    for r in range(reps + 2):
+        t0 = time.perf_counter()
+        wire.reset()
+        for b in bufs:
+            wire.add_batch(b)
+        grp, o, bo, data, st = wire.step_stream(w)
+        dt = time.perf_counter() - t0
+        if r >= 2:
+            times.append(dt)
+    assert st.messages == n_msg and st.dropped_messages == 0
+    # the stream from the wire decides like the same messages fed as rows
+    res = w.step_stream(grp, o, bo, data)
+    w2 = hq.Worker(d.device, sum(r != "observer" for r in roles), on_device=True)
+    w2.add_groups(g, m)
+    msg_only = ev[ev["kind"] == hq.EV_MESSAGE]
+    per = np.array([int(((ev["kind"][int(off[i]):int(off[i + 1])]) == hq.EV_MESSAGE).sum())
+                    for i in range(G)], np.int64)
+    moff = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
+    ref = w2.step(np.arange(G, dtype=np.uint32), moff, msg_only)
+    same = bool(np.array_equal(np.sort(res["commits"]["cluster_id"]),
+                               np.sort(ref["commits"]["cluster_id"])) and
+                np.array_equal(res["commits"]["committed"][np.argsort(res["commits"]["cluster_id"])],
+                               ref["commits"]["committed"][np.argsort(ref["commits"]["cluster_id"])]))
+    w.close()
+    w2.close()
+    wire.close()
+    t = float(np.median(times))
+    return {
+        "workload": f"wire: the received messages of one steady-state step of {G} leader groups "
+                    f"(3 voters), {n_msg} raftpb.Message in {len(batches)} MessageBatch "
+                    f"({n_bytes} bytes), decoded and assembled into the step's event stream "
+                    f"(hq_wire_add_batch + hq_wire_step_stream), one host thread",
+        "unit": "messages/s", "value": n_msg / t, "ms_per_step": t * 1e3,
+        "ns_per_message": t / n_msg * 1e9, "wire_mb_per_s": n_bytes / t / 1e6,
+        "stream_bytes_per_message": len(data) / n_msg,
+        "commits_equal_rows_path": same, "commits": int(len(res["commits"])),
+    }
+
+
 # ----------------------------------------------------------------------------- CPU leg --------
 def full_size_parity(w, set0, nthreads):
     """The GPU's decisions of batch set 0 (every voter-count bucket of the step, at the
@@ -1156,6 +1234,8 @@ def main():
         try:
             if name == "e2e":
                 e2e = run_e2e(max(20, args.steps // 20), 3, d)
+            elif name == "wire":
+                steps_legs.append(run_wire_leg(d))
             elif name in STEP_ROLES:
                 steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
                                                name=name))
