@@ -15,7 +15,6 @@
 #include <cstring>
 #include <new>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/hipquorum.h"
@@ -29,6 +28,10 @@ struct Reader {
     const char *err = nullptr;
 
     bool varint(uint64_t &v) {
+        if (p < end && *p < 0x80) {                   // the common one-byte varint
+            v = *p++;
+            return true;
+        }
         v = 0;
         for (int shift = 0; shift < 64; shift += 7) {
             if (p >= end) {
@@ -135,6 +138,119 @@ int decode_message(const uint8_t *b, size_t len, hq_wire_message *m, std::string
     return HQ_OK;
 }
 
+// MessageBatch (raft.proto:191-196): every Message handed to sink(bytes, len) in order (sink
+// returns an HQ_ status), the other fields into *bi. Any field order; unknown fields skipped.
+template <class Sink>
+int parse_batch(const uint8_t *bytes, size_t len, hq_wire_batch_info *bi, uint64_t *count,
+                Sink &&sink) {
+    *bi = hq_wire_batch_info{};
+    *count = 0;
+    Reader r{bytes, bytes + len};
+    while (r.p < r.end) {
+        uint64_t tag;
+        if (!r.varint(tag)) break;
+        const uint32_t field = (uint32_t)(tag >> 3), wt = (uint32_t)(tag & 7);
+        if (field == 1 && wt == 2) {                  // repeated Message requests
+            const uint8_t *m;
+            uint64_t n;
+            if (!r.bytes(m, n)) break;
+            const int rc = sink(m, (size_t)n);
+            if (rc) return rc;
+            ++*count;
+        } else if (field == 2 && wt == 0) {           // deployment_id
+            if (!r.varint(bi->deployment_id)) break;
+        } else if (field == 3 && wt == 2) {           // source_address
+            const uint8_t *a;
+            uint64_t n;
+            if (!r.bytes(a, n)) break;
+            bi->source_address_len = n;
+        } else if (field == 4 && wt == 0) {           // bin_ver
+            uint64_t v;
+            if (!r.varint(v)) break;
+            bi->bin_ver = (uint32_t)v;
+        } else if (field == 0) {
+            r.err = "illegal field number 0";
+            break;
+        } else if (field <= 4) {
+            r.err = "wrong wire type for a MessageBatch field";
+            break;
+        } else if (!r.skip(wt)) {
+            break;
+        }
+    }
+    if (r.err) return HQ_E_INVAL;
+    bi->n_messages = *count;
+    return HQ_OK;
+}
+
+// cluster id -> index in order of first appearance: open addressing, linear probing (a step
+// looks every message's cluster up once; a node-based map costs more than the decode)
+class ClusterIndex {
+  public:
+    void clear() {
+        for (uint32_t i : used_) keys_[i] = kEmpty;
+        used_.clear();
+        has_empty_ = false;
+    }
+    // the index of id, inserting next if new (*fresh = true)
+    uint32_t find_or_add(uint64_t id, uint32_t next, bool *fresh) {
+        if ((used_.size() + 1) * 2 > keys_.size()) rehash(keys_.empty() ? 1024 : keys_.size() * 2);
+        const uint64_t mask = keys_.size() - 1;
+        for (uint64_t i = hash(id) & mask;; i = (i + 1) & mask) {
+            if (keys_[i] == id && id != kEmpty) {
+                *fresh = false;
+                return vals_[i];
+            }
+            if (keys_[i] == kEmpty) {
+                if (id == kEmpty) {                   // the one key the table cannot hold
+                    if (!has_empty_) {
+                        has_empty_ = true;
+                        empty_val_ = next;
+                        *fresh = true;
+                        return next;
+                    }
+                    *fresh = false;
+                    return empty_val_;
+                }
+                keys_[i] = id;
+                vals_[i] = next;
+                used_.push_back((uint32_t)i);
+                *fresh = true;
+                return next;
+            }
+        }
+    }
+  private:
+    static constexpr uint64_t kEmpty = ~0ull;
+    static uint64_t hash(uint64_t x) {
+        x ^= x >> 33;
+        x *= 0xff51afd7ed558ccdull;
+        return x ^ (x >> 33);
+    }
+    void rehash(size_t cap) {
+        std::vector<uint64_t> k(cap, kEmpty);
+        std::vector<uint32_t> v(cap);
+        std::vector<uint32_t> u;
+        u.reserve(used_.size());
+        for (uint32_t i : used_) {
+            const uint64_t id = keys_[i];
+            uint64_t j = hash(id) & (cap - 1);
+            while (k[j] != kEmpty) j = (j + 1) & (cap - 1);
+            k[j] = id;
+            v[j] = vals_[i];
+            u.push_back((uint32_t)j);
+        }
+        keys_.swap(k);
+        vals_.swap(v);
+        used_.swap(u);
+    }
+    std::vector<uint64_t> keys_;
+    std::vector<uint32_t> vals_;
+    std::vector<uint32_t> used_;
+    bool has_empty_ = false;
+    uint32_t empty_val_ = 0;
+};
+
 }  // namespace
 
 struct hq_wire {
@@ -147,7 +263,7 @@ struct hq_wire {
     };
     std::vector<Rec> recs;
     std::vector<uint64_t> clusters;
-    std::unordered_map<uint64_t, uint32_t> cluster_index;
+    ClusterIndex cluster_index;
     std::vector<hq_wire_message> scratch;
     hq_wire_stats stats{};
     // the assembled step input (valid until the next reset)
@@ -162,11 +278,9 @@ struct hq_wire {
         return code;
     }
     uint32_t cluster(uint64_t id) {
-        auto it = cluster_index.find(id);
-        if (it != cluster_index.end()) return it->second;
-        const uint32_t k = (uint32_t)clusters.size();
-        cluster_index.emplace(id, k);
-        clusters.push_back(id);
+        bool fresh;
+        const uint32_t k = cluster_index.find_or_add(id, (uint32_t)clusters.size(), &fresh);
+        if (fresh) clusters.push_back(id);
         return k;
     }
 };
@@ -176,48 +290,16 @@ extern "C" {
 int hq_wire_decode_batch(const uint8_t *bytes, size_t len, hq_wire_message *out, uint64_t cap,
                          uint64_t *count, hq_wire_batch_info *info) {
     if ((!bytes && len) || !count) return HQ_E_INVAL;
-    *count = 0;
-    hq_wire_batch_info bi{};
-    Reader r{bytes, bytes + len};
     std::string err;
-    while (r.p < r.end) {
-        uint64_t tag;
-        if (!r.varint(tag)) break;
-        const uint32_t field = (uint32_t)(tag >> 3), wt = (uint32_t)(tag & 7);
-        if (field == 1 && wt == 2) {                  // repeated Message requests
-            const uint8_t *m;
-            uint64_t n;
-            if (!r.bytes(m, n)) break;
-            if (*count < cap && out) {
-                if (decode_message(m, n, out + *count, err) != HQ_OK) return HQ_E_INVAL;
-            } else {
-                hq_wire_message tmp;
-                if (decode_message(m, n, &tmp, err) != HQ_OK) return HQ_E_INVAL;
-            }
-            ++*count;
-        } else if (field == 2 && wt == 0) {           // deployment_id
-            if (!r.varint(bi.deployment_id)) break;
-        } else if (field == 3 && wt == 2) {           // source_address
-            const uint8_t *s;
-            uint64_t n;
-            if (!r.bytes(s, n)) break;
-            bi.source_address_len = n;
-        } else if (field == 4 && wt == 0) {           // bin_ver
-            uint64_t v;
-            if (!r.varint(v)) break;
-            bi.bin_ver = (uint32_t)v;
-        } else if (field == 0) {
-            r.err = "illegal field number 0";
-            break;
-        } else if (field <= 4) {
-            r.err = "wrong wire type for a MessageBatch field";
-            break;
-        } else if (!r.skip(wt)) {
-            break;
-        }
-    }
-    if (r.err) return HQ_E_INVAL;
-    bi.n_messages = *count;
+    hq_wire_batch_info bi;
+    uint64_t k = 0;
+    const int rc = parse_batch(bytes, len, &bi, count, [&](const uint8_t *m, size_t n) {
+        hq_wire_message tmp;
+        hq_wire_message *dst = out && k < cap ? out + k : &tmp;
+        ++k;
+        return decode_message(m, n, dst, err);
+    });
+    if (rc) return rc;
     if (info) *info = bi;
     return *count > cap && out ? HQ_E_STATE : HQ_OK;
 }
@@ -263,10 +345,19 @@ int hq_wire_add_local(hq_wire *w, uint64_t cluster_id, const hq_event *events, u
 
 int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
     if (!w) return HQ_E_INVAL;
-    uint64_t n = 0;
+    if (!bytes && len) return w->fail(HQ_E_INVAL, "hq_wire_add_batch: NULL bytes");
+    // one pass: every message decoded into the scratch list; the batch's own fields (they follow
+    // the messages in the marshalled order) decide afterwards whether it is kept
+    w->scratch.clear();
+    std::string err;
     hq_wire_batch_info bi;
-    if (hq_wire_decode_batch(bytes, len, nullptr, 0, &n, &bi) != HQ_OK)
-        return w->fail(HQ_E_INVAL, "hq_wire_add_batch: malformed MessageBatch");
+    uint64_t n = 0;
+    const int rc = parse_batch(bytes, len, &bi, &n, [&](const uint8_t *m, size_t k) {
+        w->scratch.emplace_back();
+        return decode_message(m, k, &w->scratch.back(), err);
+    });
+    if (rc) return w->fail(HQ_E_INVAL, "hq_wire_add_batch: malformed MessageBatch" +
+                                           (err.empty() ? std::string() : ": " + err));
     w->stats.batches++;
     w->stats.bytes += len;
     // Transport.handleRequest (transport.go:289-300): the whole batch is dropped on a foreign
@@ -276,12 +367,8 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
         w->stats.dropped_messages += n;
         return HQ_OK;
     }
-    w->scratch.resize(n);
-    uint64_t m = 0;
-    if (hq_wire_decode_batch(bytes, len, w->scratch.data(), n, &m, nullptr) != HQ_OK)
-        return w->fail(HQ_E_INVAL, "hq_wire_add_batch: malformed MessageBatch");
-    for (uint64_t i = 0; i < m; ++i) {
-        const hq_wire_message &x = w->scratch[i];
+    w->recs.reserve(w->recs.size() + n);
+    for (const hq_wire_message &x : w->scratch) {
         w->stats.messages++;
         w->stats.entries += x.n_entries;
         // HandleMessageBatch (nodehost.go:2039-2044): snapshot confirmations go aside
