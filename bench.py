@@ -129,7 +129,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,cq,ing,ingo,ingu,w2,e2e,step,step5,wire")
+                  "rimt,cq,cqp,ing,ingo,ingu,w2,sweep,e2e,step,step5,wire")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -486,6 +486,30 @@ def run_gpu(w, steps, warmup, d: Dist):
     return res
 
 
+def run_size_sweep(name, steps, warmup, d: Dist, sizes=(1 << 18, 1 << 19, 1 << 20, 1 << 21,
+                                                        1 << 22, 1 << 23)):
+    """The headline kernel at batch sizes 256K..8M groups per GPU (same generator, same
+    rotation past the Infinity Cache), and the least-squares line t(launch) = t0 + bytes / BW
+    over them: BW is the kernel's streaming rate, t0 what one launch costs whatever its size (the
+    dependent-launch boundary, fill and drain; MI355X_MICROARCH.md "boundary")."""
+    w = WORKLOADS[name]
+    pts = []
+    for g in sizes:
+        re_ = run_gpu(dict(w, G=g), steps, warmup, d)
+        pts.append({"groups": g, "bytes_per_launch": re_["bytes_per_launch"],
+                    "kernel_us": re_["avg_kernel_s"] * 1e6,
+                    "frac": re_["achieved_node_gbs"] / (HBM_PEAK_GBS * d.world)})
+    x = np.array([p["bytes_per_launch"] for p in pts], np.float64)
+    y = np.array([p["kernel_us"] for p in pts], np.float64)
+    slope, t0 = np.polyfit(x, y, 1)
+    resid = y - (t0 + slope * x)
+    return {"workload": f"sweep: {name} kernel vs batch size (t = t0 + bytes / BW)",
+            "points": pts, "fit_t0_us": float(t0),
+            "fit_stream_gbs": float(1e-3 / slope) if slope > 0 else None,
+            "fit_stream_frac_of_peak": float(1e-3 / slope / HBM_PEAK_GBS) if slope > 0 else None,
+            "fit_max_resid_us": float(np.abs(resid).max())}
+
+
 def _timed(ctx, d, run, steps, warmup):
     """Warm up, then time `steps` calls of run(i) with a barrier + sync on both sides; returns
     (max-over-ranks seconds, average launch seconds from the HIP-event region)."""
@@ -514,6 +538,7 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
     rotated past the Infinity Cache like the commit legs:
       rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
       cq:  CheckQuorum (k_bits CHECKQ), 16M groups x 7 voters, active flags reset in place
+      cqp: the same over active-flag planes (k_cq_planes)
       ing: match-delta ingest (k_ingest_match), 4M ReplicateResp deltas into a 4M x 3 table
       ingo: the same deltas in group order, the order a step worker emits them
       ingu: distinct (group, slot) keys in random order (HQ_INGEST_UNIQUE)"""
@@ -569,6 +594,28 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
             act, hqb = sets[i % nsets]
             ctx.check_quorum_dev(G, act, None, n, 0, hqb)
         desc = f"cq: CheckQuorum (leaderHasQuorum + setNotActive), {G} groups x {n} voters"
+        units, unit = G, "decisions/s"
+    elif name == "cqp":
+        G, n = 16 << 20, 7
+        pb = hq.cq_plane_bytes(G, n)
+        per = 2 * pb + G // 8          # active planes read + zeroed, has_quorum bits
+        nsets = max(4, int(np.ceil(ROTATE_BYTES / per)))
+        sets = []
+        for k in range(nsets):
+            act = ctx.empty(G, np.uint8)
+            ctx.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 3 + (k << 40), G, n), act)
+            pl = ctx.empty(pb, np.uint8)
+            ctx.tile_cq_planes_dev(G, act, None, n, 0, pl)
+            ctx.sync()
+            ctx.free(act)
+            sets.append((pl, ctx.empty(hq.words64(G), np.uint64)))
+
+        def run(i):
+            pl, hqb = sets[i % nsets]
+            ctx.check_quorum_planes_dev(G, pl, n, hqb)
+        desc = (f"cqp: CheckQuorum over active-flag planes (the leader's slot implicit, "
+                f"{n - 1} planes of 2048 groups; bit-sliced count, planes zeroed in place), "
+                f"{G} groups x {n} voters")
         units, unit = G, "decisions/s"
     else:   # ing / ingo: the device table in the headline layout (leader-row tiles)
         G, n, U = 4 << 20, 3, 4 << 20
@@ -1242,8 +1289,11 @@ def main():
             elif name in STEP_ROLES:
                 steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
                                                name=name))
-            elif name in ("rim", "rimt", "cq", "ing", "ingo", "ingu"):
+            elif name in ("rim", "rimt", "cq", "cqp", "ing", "ingo", "ingu"):
                 kern.append(run_kernel_leg(name, max(50, args.steps // 4),
+                                           max(5, args.warmup // 4), d))
+            elif name == "sweep":
+                conc.append(run_size_sweep(args.workload, max(50, args.steps // 4),
                                            max(5, args.warmup // 4), d))
             elif name.startswith("w") and name[1:].isdigit():
                 conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))

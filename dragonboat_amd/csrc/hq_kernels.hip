@@ -1217,6 +1217,105 @@ __global__ __launch_bounds__(kBlock) void k_tile_planes(uint64_t G, const uint8_
     }
 }
 
+// ---- CheckQuorum over active-flag planes (hq_check_quorum_planes_dev) -----------------------
+// The leader's own slot always counts (`nid == r.nodeID`, raft.go:384), so a group's CheckQuorum
+// state is the active flags of its other voting slots plus its voter count. Plane k < 7 holds the
+// active flag of the group's (k + 1)-th voting slot other than the leader, planes 7..9 the bits of
+// n - 1 (per-group n); a uniform-n batch keeps only its n - 1 active planes. 2048-group tiles as
+// the vote / ReadIndex planes, bit j of dword k of a plane = the tile's group 32 k + j. A lane
+// decides 32 groups: 1 + popcount(the active planes masked to the group's slots) >= n/2 + 1,
+// then zeroes the active planes it read (setNotActive of every voting member, raft.go:385,
+// remote.go:196-198).
+template <int P, bool PERN, int BLK>
+__global__ __launch_bounds__(BLK) void k_cq_planes(uint64_t G, uint8_t *planes,
+                                                   uint64_t *has_quorum) {
+    constexpr int NP = PERN ? 10 : P;   // planes per tile
+    constexpr int NA = PERN ? 7 : P;    // of which active planes
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (BLK / 64);
+    const uint64_t ntiles = (G + kPlaneTile - 1) / kPlaneTile;
+    uint32_t *out = reinterpret_cast<uint32_t *>(has_quorum);
+    for (uint64_t t = wave; t < ntiles; t += nw) {
+        uint32_t *base = reinterpret_cast<uint32_t *>(planes + t * (uint64_t)NP * (kPlaneTile / 8)) + lane;
+        uint32_t p[NP > 0 ? NP : 1];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) p[q] = __builtin_nontemporal_load(base + q * 64);
+        uint32_t x[7] = {0, 0, 0, 0, 0, 0, 0};
+        uint32_t h0, h1, h2;                              // n / 2, bit-sliced
+        if constexpr (PERN) {
+            const uint32_t n0 = p[7], n1 = p[8], n2 = p[9];
+            const uint32_t m[7] = {n0 | n1 | n2, n1 | n2, n2 | (n1 & n0), n2, n2 & (n1 | n0),
+                                   n2 & n1, n2 & n1 & n0};   // slot k + 1 votes: n - 1 > k
+#pragma unroll
+            for (int k = 0; k < 7; ++k) x[k] = p[k] & m[k];
+            const uint32_t c = n1 & n0;
+            h0 = n1 ^ n0;
+            h1 = n2 ^ c;
+            h2 = n2 & c;
+        } else {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) x[k] = p[k];
+            constexpr int h = (P + 1) / 2;
+            h0 = (h & 1) ? ~0u : 0u;
+            h1 = (h & 2) ? ~0u : 0u;
+            h2 = (h & 4) ? ~0u : 0u;
+        }
+        uint32_t c0, c1, c2;
+        count7(x, c0, c1, c2);
+        const uint32_t hq = ge3(c0, c1, c2, h0, h1, h2);
+        const uint64_t g = t * kPlaneTile + lane * 32;
+        if (g < G) {
+            const uint64_t left = G - g;
+            out[g >> 5] = left >= 32 ? hq : hq & ((1u << left) - 1u);
+        } else if (g < ((G + 63) & ~63ull)) {             // the rest of the last bitmap word
+            out[g >> 5] = 0;
+        }
+#pragma unroll
+        for (int q = 0; q < NA; ++q) __builtin_nontemporal_store(0u, base + q * 64);
+    }
+}
+
+// columns -> CheckQuorum planes: one thread per group packs the active flags of its voting slots
+// other than self_slot (in slot order) and n - 1, the wave's 64 groups become one ballot per
+// plane, lane q < NP stores plane q's 8 bytes
+__global__ __launch_bounds__(kBlock) void k_tile_cq_planes(uint64_t G, const uint8_t *active,
+                                                           const uint8_t *nv, uint32_t nu,
+                                                           uint32_t self_slot, uint8_t *planes,
+                                                           uint64_t *fallback) {
+    const uint64_t total = (G + kPlaneTile - 1) / kPlaneTile * kPlaneTile;
+    const uint32_t NP = nv ? 10u : nu - 1u;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kBlock; g0 < total;
+         g0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t g = g0 + threadIdx.x;
+        uint32_t bits = 0;
+        bool bad = false;
+        if (g < G) {
+            const uint32_t n = nv ? nv[g] : nu;
+            bad = n < 1 || n > 8 || self_slot >= n;
+            if (!bad) {
+                const uint32_t a = active[g] & ((1u << n) - 1u);
+                bits = (a & ((1u << self_slot) - 1u)) | ((a >> (self_slot + 1)) << self_slot);
+                if (nv) bits |= (n - 1) << 7;
+            }
+        }
+        uint64_t mine = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 10; ++q) {
+            const uint64_t b = __ballot((bits >> q) & 1);
+            if (lane == q) mine = b;
+        }
+        const uint64_t gw = g - lane;
+        if (gw < total && lane < NP)
+            *reinterpret_cast<uint64_t *>(planes + (gw / kPlaneTile) * (NP * (kPlaneTile / 8)) +
+                                          lane * (kPlaneTile / 8) + (gw % kPlaneTile) / 8) = mine;
+        const uint64_t b = __ballot(bad);
+        if (fallback && lane == 0 && gw < ((G + 63) & ~63ull)) fallback[gw >> 6] = b;
+    }
+}
+
 // ---- synthetic inputs (recipe: DESIGN.md "Synthetic inputs"; CPU twin oracle/qgen.c) --------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -2056,6 +2155,55 @@ extern "C" int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active,
     k.self_slot = self_slot;
     k.has_quorum = has_quorum;
     return launch_bits<kCHECKQ>(ctx, k, "hq_check_quorum");
+}
+
+extern "C" int hq_check_quorum_planes_dev(hq_ctx *ctx, uint64_t G, uint8_t *planes,
+                                          uint32_t n_uniform, uint64_t *has_quorum) {
+    if (!ctx) return HQ_E_INVAL;
+    if (n_uniform > HQ_MAX_VOTERS)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_check_quorum_planes: n_uniform must be 0 or 1..8");
+    if (G == 0) return HQ_OK;
+    if (!has_quorum || (n_uniform != 1 && (!planes || !hq::aligned16(planes))))
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_check_quorum_planes: NULL argument or planes not 16-byte aligned");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    constexpr int B = HQ_PLANES_BLK;
+    const dim3 grid(grid_for((G + kPlaneTile - 1) / kPlaneTile * 64, B));
+    switch (n_uniform) {
+    case 0: hipLaunchKernelGGL((k_cq_planes<0, true, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 1: hipLaunchKernelGGL((k_cq_planes<0, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 2: hipLaunchKernelGGL((k_cq_planes<1, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 3: hipLaunchKernelGGL((k_cq_planes<2, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 4: hipLaunchKernelGGL((k_cq_planes<3, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 5: hipLaunchKernelGGL((k_cq_planes<4, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 6: hipLaunchKernelGGL((k_cq_planes<5, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    case 7: hipLaunchKernelGGL((k_cq_planes<6, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    default: hipLaunchKernelGGL((k_cq_planes<7, false, B>), grid, dim3(B), 0, ctx->stream, G, planes, has_quorum); break;
+    }
+    return hq::post_launch(ctx, "hq_check_quorum_planes");
+}
+
+extern "C" int hq_tile_cq_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *active,
+                                     const uint8_t *n_voting, uint32_t n_uniform,
+                                     uint32_t self_slot, uint8_t *planes, uint64_t *fallback) {
+    if (!ctx) return HQ_E_INVAL;
+    if (n_voting ? n_uniform != 0 : (n_uniform < 1 || n_uniform > HQ_MAX_VOTERS))
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_tile_cq_planes: per-group n_voting with n_uniform 0, or n_uniform 1..8");
+    if (!n_voting && self_slot >= n_uniform)
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_cq_planes: self_slot >= n_uniform");
+    if (G == 0) return HQ_OK;
+    const bool no_planes = !n_voting && n_uniform == 1;   // a single-node batch has none
+    if (!active || (!no_planes && (!planes || (reinterpret_cast<uintptr_t>(planes) & 7))))
+        return hq::fail(ctx, HQ_E_INVAL, "hq_tile_cq_planes: NULL argument or planes misaligned");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_cq_planes,
+                       dim3(grid_for((G + kPlaneTile - 1) / kPlaneTile * kPlaneTile)),
+                       dim3(kBlock), 0, ctx->stream, G, active, n_voting, n_uniform, self_slot,
+                       planes, fallback);
+    return hq::post_launch(ctx, "k_tile_cq_planes");
 }
 
 extern "C" int hq_synth_commit_dev(hq_ctx *ctx, const hq_synth_spec *s,

@@ -338,6 +338,36 @@ extern "C" int hq_tile_planes_host(uint64_t G, const uint8_t *ack, const uint8_t
     return HQ_OK;
 }
 
+// Active flags -> CheckQuorum planes on the host (the twin of k_tile_cq_planes;
+// include/hipquorum.h hq_check_quorum_planes_dev).
+extern "C" int hq_tile_cq_planes_host(uint64_t G, const uint8_t *active, const uint8_t *n_voting,
+                                      uint32_t n_uniform, uint32_t self_slot, uint8_t *planes,
+                                      uint64_t *fallback) {
+    if (n_voting ? n_uniform != 0 : (n_uniform < 1 || n_uniform > HQ_MAX_VOTERS)) return HQ_E_INVAL;
+    if (!n_voting && self_slot >= n_uniform) return HQ_E_INVAL;
+    const uint64_t NP = n_voting ? 10 : n_uniform - 1;
+    if (G && (!active || (NP && !planes))) return HQ_E_INVAL;
+    constexpr uint64_t T = HQ_PLANE_TILE_GROUPS;
+    const uint64_t total = (G + T - 1) / T * T;
+    if (NP) std::memset(planes, 0, total / 8 * NP);
+    if (fallback) std::memset(fallback, 0, ((G + 63) / 64) * 8);
+    for (uint64_t g = 0; g < G; ++g) {
+        const uint32_t n = n_voting ? n_voting[g] : n_uniform;
+        if (n < 1 || n > 8 || self_slot >= n) {
+            if (fallback) set_bit(fallback, g);
+            continue;
+        }
+        const uint32_t a = active[g] & ((1u << n) - 1u);
+        uint32_t bits = (a & ((1u << self_slot) - 1u)) | ((a >> (self_slot + 1)) << self_slot);
+        if (n_voting) bits |= (n - 1) << 7;
+        uint8_t *tile = planes + (g / T) * (NP * T / 8);
+        const uint64_t j = g % T;
+        for (uint64_t q = 0; q < NP; ++q)
+            if ((bits >> q) & 1) tile[q * (T / 8) + j / 8] |= (uint8_t)(1u << (j % 8));
+    }
+    return HQ_OK;
+}
+
 // Multi-ctx ReadIndex columns -> 128-group tiles on the host (the twin of k_tile_ri_multi;
 // include/hipquorum.h hq_readindex_multi_tiles_dev).
 extern "C" int hq_tile_ri_multi_host(uint64_t G, uint32_t K_max, uint32_t n_max,

@@ -38,7 +38,7 @@ HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table
 HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
 HQ_INGEST_UNIQUE = 2         # hq_table_*: every key at most once in the batch
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
-HQ_ABI_VERSION = 9
+HQ_ABI_VERSION = 10
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -261,6 +261,12 @@ SIGNATURES = {
     "hq_tile_bits3_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
                                           _vp, _vp]),
     "hq_tile_bits_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
+    "hq_check_quorum_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
+                                                  _vp]),
+    "hq_tile_cq_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32,
+                                             ctypes.c_uint32, _vp, _vp]),
+    "hq_tile_cq_planes_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, ctypes.c_uint32,
+                                              ctypes.c_uint32, _vp, _vp]),
     "hq_check_quorum_dev": (
         ctypes.c_int,
         [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp],
@@ -579,6 +585,15 @@ class Context:
                          fallback=None) -> None:
         self._check(lib.hq_check_quorum_dev(self.h, G, _p(active), _p(n_voting), n_uniform,
                                             self_slot, _p(has_quorum), _p(fallback)))
+
+    def check_quorum_planes_dev(self, G, planes, n_uniform, has_quorum) -> None:
+        self._check(lib.hq_check_quorum_planes_dev(self.h, G, _p(planes), n_uniform,
+                                                   _p(has_quorum)))
+
+    def tile_cq_planes_dev(self, G, active, n_voting, n_uniform, self_slot, planes,
+                           fallback=None) -> None:
+        self._check(lib.hq_tile_cq_planes_dev(self.h, G, _p(active), _p(n_voting), n_uniform,
+                                              self_slot, _p(planes), _p(fallback)))
 
     def readindex_host(self, G, ack, n_voting, n_uniform, confirmed, fallback=None) -> None:
         self._check(lib.hq_readindex(self.h, G, _p(ack), _p(n_voting), n_uniform, _p(confirmed),
@@ -955,6 +970,23 @@ def tile_ri_multi_host(G, K_max, n_max, ack_ordinal, ctx_index, n_pending=None, 
 
 def plane_tiles(G: int) -> int:
     return (G + HQ_PLANE_TILE_GROUPS - 1) // HQ_PLANE_TILE_GROUPS
+
+
+def cq_plane_bytes(G: int, n_uniform: int) -> int:
+    """hq_cq_plane_bytes: CheckQuorum planes of G groups (n_uniform 0 = per-group n)."""
+    return plane_tiles(G) * (n_uniform - 1 if n_uniform else 10) * (HQ_PLANE_TILE_GROUPS // 8)
+
+
+def tile_cq_planes_host(active, n_voting=None, n_uniform=0, self_slot=0):
+    """hq_tile_cq_planes_host over a host uint8 active column: (planes uint8, fallback words)."""
+    G = len(active)
+    act = np.ascontiguousarray(active, np.uint8)
+    nv = None if n_voting is None else np.ascontiguousarray(n_voting, np.uint8)
+    out = np.empty(max(1, cq_plane_bytes(G, 0 if nv is not None else n_uniform)), np.uint8)
+    fb = np.zeros(words64(G), np.uint64)
+    _chk(lib.hq_tile_cq_planes_host(G, _p(act), _p(nv), n_uniform, self_slot, _p(out), _p(fb)),
+         "hq_tile_cq_planes_host")
+    return out[:cq_plane_bytes(G, 0 if nv is not None else n_uniform)], fb
 
 
 def tile_planes_host(ack, granted, rejected, n_voting=None, n_uniform=0):

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 9
+#define HQ_ABI_VERSION 10
 
 /* status codes */
 #define HQ_OK          0
@@ -480,6 +480,34 @@ int hq_tile_planes_host(uint64_t G, const uint8_t *ack, const uint8_t *granted,
 int hq_check_quorum_dev(hq_ctx *ctx, uint64_t G, uint8_t *active, const uint8_t *n_voting,
                         uint32_t n_uniform, uint32_t self_slot, uint64_t *has_quorum,
                         uint64_t *fallback);
+
+/*
+ * The same decision over active-flag planes (raft.go:380-390; the leader's own slot always
+ * counts, raft.go:384, so it is not stored). A tile holds HQ_PLANE_TILE_GROUPS groups as planes of
+ * HQ_PLANE_TILE_GROUPS / 8 bytes, bit j of byte k of a plane = the tile's group 8 k + j:
+ *   per-group n (n_uniform = 0): 10 planes — plane k < 7 = the active flag of the group's
+ *     (k + 1)-th voting slot other than the leader's (slot order), planes 7..9 = bits 0..2 of n - 1;
+ *   uniform n (n_uniform in 1..8): the n - 1 active planes only (none for n = 1).
+ * has_quorum bit = 1 + (active other voting slots) >= n/2 + 1; every active plane of the batch is
+ * then zeroed in place (setNotActive, remote.go:196-198). Planes 16-byte aligned, the tile size is
+ * hq_cq_plane_bytes(G, n_uniform) / hq_plane_tiles(G). Nothing falls back: the packers flag the
+ * groups whose columns break the contract (n outside 1..8, self_slot >= n), pack them as n = 1,
+ * and the caller decides those on the CPU from its columns.
+ */
+static inline uint64_t hq_cq_plane_bytes(uint64_t G, uint32_t n_uniform) {
+    return hq_plane_tiles(G) * (n_uniform ? n_uniform - 1 : 10) * (HQ_PLANE_TILE_GROUPS / 8);
+}
+int hq_check_quorum_planes_dev(hq_ctx *ctx, uint64_t G, uint8_t *planes, uint32_t n_uniform,
+                               uint64_t *has_quorum);
+/* Columns (active u8 bitmap per group, bit s = voting slot s; n_voting, or n_uniform when NULL;
+ * self_slot = the leader's slot) -> CheckQuorum planes (padding zeroed, 8-byte aligned);
+ * fallback (may be NULL) receives the contract violations. */
+int hq_tile_cq_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *active, const uint8_t *n_voting,
+                          uint32_t n_uniform, uint32_t self_slot, uint8_t *planes,
+                          uint64_t *fallback);
+int hq_tile_cq_planes_host(uint64_t G, const uint8_t *active, const uint8_t *n_voting,
+                           uint32_t n_uniform, uint32_t self_slot, uint8_t *planes,
+                           uint64_t *fallback);
 
 /* ---------------------------------------------------------------- device-resident state ----- */
 /*

@@ -31,7 +31,8 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2,
           "c2l": "k_commit_lag_big<3, 0, 4, false, 0>", "c3l": "k_commit_lag<5, 2, 4, false, 0>",
           "c2ll": "k_commit_lag_big<3, 0, 4, false, 1>", "c5ll": "k_commit_lag_fused<2, 512, 1>",
           "c5l": "k_commit_lag_fused<2, 512, 0>", "rim": "k_ri_multi2<false, false, 4, false>", "rimt": "k_ri_multi2<false, false, 4, true>",
-          "cq": "k_bits<4, false, 256, false, true>", "ing": "k_table_ingest<false, false>",
+          "cq": "k_bits<4, false, 256, false, true>", "cqp": "k_cq_planes<6, false, 256>",
+          "ing": "k_table_ingest<false, false>",
           "ingo": "k_table_ingest<true, false>", "rim2": "k_ri_multi2",
           "c4t3": "k_bits3<256>", "c4p": "k_planes<256>"}
 
