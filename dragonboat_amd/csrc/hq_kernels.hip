@@ -2353,12 +2353,35 @@ __device__ __forceinline__ void ce32(uint32_t &a, uint32_t &b) {
     b = hi;
 }
 
-__device__ __forceinline__ void sort_net_u32(uint32_t (&v)[8]) {
+// HQ_RI_NET 0: the transposition sort (A/B baseline, tools/ab_libs.sh)
+#ifndef HQ_RI_NET
+#define HQ_RI_NET 1
+#endif
+// Batcher's odd-even merge sort of 8 keys: 19 compare-exchanges in 6 layers (the transposition
+// sort it replaces takes 28); only the selected rank is read, so the compiler keeps just the
+// min / max halves on its path
+#if HQ_RI_NET
+constexpr int kNet8[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6},
+                              {5, 7}, {1, 2}, {5, 6}, {0, 4}, {1, 5}, {2, 6}, {3, 7},
+                              {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
+#endif
+
+template <typename CE>
+__device__ __forceinline__ void sort8(uint32_t (&v)[8], CE ce) {
+#if HQ_RI_NET
+#pragma unroll
+    for (int c = 0; c < 19; ++c) ce(v[kNet8[c][0]], v[kNet8[c][1]]);
+#else
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
 #pragma unroll
-        for (int i = r & 1; i + 1 < 8; i += 2) ce32(v[i], v[i + 1]);
+        for (int i = r & 1; i + 1 < 8; i += 2) ce(v[i], v[i + 1]);
     }
+#endif
+}
+
+__device__ __forceinline__ void sort_net_u32(uint32_t (&v)[8]) {
+    sort8(v, [](uint32_t &a, uint32_t &b) { ce32(a, b); });
 }
 
 template <bool PERK, bool PERN>
@@ -2510,11 +2533,7 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
                     for (int sl = 0; sl < 8; ++sl)
                         v[sl] = ov[k < KM ? k : 0][sl] | (sl < (int)n0 ? 0u : 0xFFFFu) |
                                 (sl < (int)n1 ? 0u : 0xFFFF0000u);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-#pragma unroll
-                        for (int i = r & 1; i + 1 < 8; i += 2) ce_pk(v[i], v[i + 1]);
-                    }
+                    sort8(v, [](uint32_t &a, uint32_t &b) { ce_pk(a, b); });
                     // reach time: the max(q-1, 1)-th smallest first-ack ordinal (readindex.go:84)
                     uint32_t tk = 0;
 #pragma unroll
