@@ -37,6 +37,7 @@ oracle:
 #   lib_ivN    records per lane of the table ingest kernels
 #   lib_b3tpwN tiles per wave of the 3-byte bitmap kernel
 #   lib_pltpwN tiles per wave of the bit-plane kernel, lib_plblkN its block size
+#   lib_swN    the device step engine's kernels asked for N waves per SIMD
 #   lib_rinet0 multi-ctx ReadIndex with the 28-CE transposition sort instead of Batcher's 19-CE network
 #   lib_tilecopy / lib_b3copy / lib_plcopy the commit tile / 3-byte / bit-plane kernel's loads and stores without the
 #              decision (their floors)
@@ -90,3 +91,5 @@ clean:
 .PHONY: all oracle clean variants
 tools/lib_rinet0/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_RI_NET=0)
+tools/lib_sw%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_STEP_WAVES=$*)

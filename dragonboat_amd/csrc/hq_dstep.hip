@@ -69,12 +69,32 @@ __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/uti
            t == HQ_MSG_HEARTBEAT_RESP || t == 20 || t == 8 || t == 9;
 }
 
+// A group's bytes read through one cached aligned 8-byte word: a varint byte costs a shift
+// instead of a dependent byte load (a group's ~24 bytes take 3-4 loads instead of ~24; the
+// input region keeps 8 bytes of slack past its last byte, so the aligned word never leaves it)
+struct ByteReader {
+    const uint8_t *p, *end;
+    uintptr_t wa = 1;             // address of the cached word (never a valid aligned one at start)
+    uint64_t w = 0;
+
+    __device__ __forceinline__ bool more() const { return p < end; }
+    __device__ __forceinline__ uint32_t next() {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        if ((a & ~uintptr_t(7)) != wa) {
+            wa = a & ~uintptr_t(7);
+            w = *reinterpret_cast<const uint64_t *>(wa);
+        }
+        ++p;
+        return (uint32_t)(w >> (8 * (a & 7))) & 0xFF;
+    }
+};
+
 // the device twin of hq_stream.cpp's decoder: one LEB128 varint
-__device__ __forceinline__ bool dvar(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
+__device__ __forceinline__ bool dvar(ByteReader &r, uint64_t &v) {
     v = 0;
     for (int sh = 0; sh < 64; sh += 7) {
-        if (p >= end) return false;
-        const uint32_t b = *p++;
+        if (!r.more()) return false;
+        const uint32_t b = r.next();
         v |= (uint64_t)(b & 0x7F) << sh;
         if (b < 0x80) return true;
     }
@@ -82,26 +102,25 @@ __device__ __forceinline__ bool dvar(const uint8_t *&p, const uint8_t *end, uint
 }
 
 // one event of a group's stream; term: the group's previous message term in the stream
-__device__ bool decode_event(const uint8_t *&p, const uint8_t *end, uint64_t &term,
-                             hq_event &v) {
+__device__ bool decode_event(ByteReader &r, uint64_t &term, hq_event &v) {
     v = hq_event{};
-    if (p >= end) return false;
-    const uint32_t h = *p++;
+    if (!r.more()) return false;
+    const uint32_t h = r.next();
     v.kind = h & 7;
-    if (v.kind == HQ_EV_READ) return dvar(p, end, v.hint) && dvar(p, end, v.hint_high);
-    if (v.kind == HQ_EV_PROPOSE) return dvar(p, end, v.log_index);
+    if (v.kind == HQ_EV_READ) return dvar(r, v.hint) && dvar(r, v.hint_high);
+    if (v.kind == HQ_EV_PROPOSE) return dvar(r, v.log_index);
     if (v.kind != HQ_EV_MESSAGE) return true;
     const uint32_t code = (h >> 3) & 7;
     uint64_t t = code == 0 ? HQ_MSG_REPLICATE_RESP : code == 1 ? HQ_MSG_REQUEST_VOTE_RESP
                : code == 2 ? HQ_MSG_HEARTBEAT_RESP : code == 3 ? HQ_MSG_READ_INDEX : 0;
-    if (code == 7 && !dvar(p, end, t)) return false;
+    if (code == 7 && !dvar(r, t)) return false;
     v.type = (uint32_t)t;
     v.reject = (h >> 6) & 1;
-    if (!dvar(p, end, v.from)) return false;
-    if (!(h & 0x80) && !dvar(p, end, term)) return false;
+    if (!dvar(r, v.from)) return false;
+    if (!(h & 0x80) && !dvar(r, term)) return false;
     v.term = term;
-    if ((code == 0 || code == 7) && !dvar(p, end, v.log_index)) return false;
-    if (code >= 2 && !(dvar(p, end, v.hint) && dvar(p, end, v.hint_high))) return false;
+    if ((code == 0 || code == 7) && !dvar(r, v.log_index)) return false;
+    if (code >= 2 && !(dvar(r, v.hint) && dvar(r, v.hint_high))) return false;
     return true;
 }
 
@@ -384,6 +403,7 @@ struct Engine {
     __device__ __forceinline__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
         const uint64_t committed0 = g.committed;
         uint64_t term = 0;
+        ByteReader br{p, end};
         for (uint64_t e = e0; e < e1; ++e) {
             if (g.flags & kDSuspended) {
                 defer(e);
@@ -392,7 +412,7 @@ struct Engine {
             bool ok;
             if (STREAM) {
                 hq_event ev;
-                ok = decode_event(p, end, term, ev) && handle(ev, e);
+                ok = decode_event(br, term, ev) && handle(ev, e);
             } else {
                 const hq_event ev = a.events[e];
                 ok = handle(ev, e);
@@ -425,7 +445,17 @@ struct Engine {
 };
 
 template <bool WRITE, bool STREAM, int MC>
-__global__ __launch_bounds__(256) void k_step(const StepK a) {
+// HQ_STEP_WAVES: waves per SIMD asked of the compiler (0: its own choice, 2-3 waves at 157-177
+// VGPRs); a group's events are one serial dependency chain, so resident waves hide its latency
+#ifndef HQ_STEP_WAVES
+#define HQ_STEP_WAVES 0
+#endif
+#if HQ_STEP_WAVES
+#define HQ_STEP_OCC __attribute__((amdgpu_waves_per_eu(HQ_STEP_WAVES)))
+#else
+#define HQ_STEP_OCC
+#endif
+__global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
     const uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.i_end) return;
     if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
@@ -683,7 +713,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const size_t o_off = up(n * 4);
     const size_t o_boff = o_off + up((n + 1) * 8);
     const size_t o_ev = o_boff + (stream ? up((n + 1) * 8) : 0);
-    const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event));
+    // + 8: slack for ByteReader's aligned word past the last byte
+    const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event)) + 8;
     if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
     if (!rc && chunks > 1 && !d->copy)       // the copy stream of the first chunked step
         rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
