@@ -896,13 +896,17 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
         full = events(s) if events else step_events(hq, G, s, roles)
         evs = [_partition(full, bounds[i], bounds[i + 1]) for i in range(W)]
         n_step = sum(len(e[2]) for e in evs)
+        n_ev = [len(e[2]) for e in evs]
         if stream:
             t0 = time.perf_counter()
-            enc = [hq.encode_events(e[1], e[2]) for e in evs]
+            enc = [hq.encode_events_sized(e[1], e[2]) if stream == "sized" else
+                   hq.encode_events(e[1], e[2]) for e in evs]
             if s >= warm:
                 t_enc += time.perf_counter() - t0
                 nb_total += sum(len(data) for data, _ in enc)
-            evs = [(e[0], e[1], b, data) for e, (data, b) in zip(evs, enc)]
+            # sized: (groups, size words, bytes); else (groups, offsets, boffsets, bytes)
+            evs = [(e[0], z, data) if stream == "sized" else (e[0], e[1], z, data)
+                   for e, (data, z) in zip(evs, enc)]
         if pin_ctx is not None:      # copied into pinned buffers outside the timed region
             for i, e in enumerate(evs):
                 if pinned[i] is None or any(p.size < x.size for p, x in zip(pinned[i], e)):
@@ -911,6 +915,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
                 for dst, src in zip(pinned[i], e):
                     dst[:src.size] = src
             evs = [tuple(p[k][:e[k].size] for k in range(len(e))) for p, e in zip(pinned, evs)]
+        if stream == "sized":
+            evs = [hq.SizedStream(e[0], e[1], ne, e[2]) for e, ne in zip(evs, n_ev)]
         # the W workers stepped at once on native threads (hq_worker_step_jobs), as W step-
         # worker goroutines each calling its own worker
         jobs = hq.StepJobs(list(zip(workers, evs)))
@@ -972,16 +978,21 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             cache[s] = step_events(hq, G, s, roles)
         return cache[s]
 
-    modes = {"device_stream": "device worker (HQ_WORKER_ON_DEVICE: every event on the GPU), "
-                              "events as the event stream (hq_worker_step_stream)",
+    modes = {"device_sized": "device worker (HQ_WORKER_ON_DEVICE: every event on the GPU), "
+                             "events as the event stream in the sized form (hq_worker_step_stream:"
+                             " 4-byte per-group size words, scanned on the device)",
+             "device_stream": "device worker, events as the event stream with the two 8-byte "
+                              "prefix arrays (hq_worker_step_stream)",
              "device_rows": "device worker, events as 56-byte hq_event rows (hq_worker_step)",
              "host": "host worker (events on the host, decisions in GPU passes), rows"}
-    for mode, W in (("device_stream", 1), ("device_stream", T), ("device_rows", 1),
-                    ("device_rows", T), ("host", 1), ("host", T)):
+    for mode, W in (("device_sized", 1), ("device_sized", T), ("device_stream", 1),
+                    ("device_stream", T), ("device_rows", 1), ("device_rows", T), ("host", 1),
+                    ("host", T)):
         if d.rank == 0:
             log(f"  step leg {name}: {mode}, {W} worker(s)")
         t, ne, acc, committed[mode], gm, t_enc = _run_workers(
-            hq, d, G, W, steps, cpu_steps, roles, mode != "host", mode == "device_stream", events)
+            hq, d, G, W, steps, cpu_steps, roles, mode != "host",
+            {"device_sized": "sized", "device_stream": True}.get(mode, False), events)
         elapsed = d.max(t)
         rec = {
             "workers": W,
@@ -995,10 +1006,11 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
                                          for k in ("pack", "device", "apply")},
         }
-        if mode == "device_stream":
+        if mode in ("device_sized", "device_stream"):
             rec["stream_bytes_per_event"] = acc.get("stream_bytes", 0) / max(1, ne)
             rec["producer_encode_ns_per_event"] = t_enc / max(1, ne) * 1e9
-        key = {("device_stream", 1): None, ("device_stream", T): "concurrent_workers",
+        key = {("device_sized", 1): None, ("device_sized", T): "concurrent_workers",
+               ("device_stream", 1): "device_stream", ("device_stream", T): "device_stream_concurrent",
                ("device_rows", 1): "device_rows", ("device_rows", T): "device_rows_concurrent",
                ("host", 1): "host_worker", ("host", T): "host_worker_concurrent"}[(mode, W)]
         if key is None:
@@ -1030,8 +1042,9 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
         }
         # the same events left the same committed indexes
         out["parity_committed"] = all(c == committed_cpu for c in committed.values())
-        for k in ("value", "concurrent_workers", "device_rows", "device_rows_concurrent",
-                  "host_worker", "host_worker_concurrent"):
+        for k in ("value", "concurrent_workers", "device_stream", "device_stream_concurrent",
+                  "device_rows", "device_rows_concurrent", "host_worker",
+                  "host_worker_concurrent"):
             v = out.get(k)
             v = v["value"] if isinstance(v, dict) else v
             if v:

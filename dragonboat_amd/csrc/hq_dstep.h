@@ -50,7 +50,8 @@ struct hq_dstep_out {                 // the lists of one step, in input group o
     uint64_t kernel_ns, d2h_ns;       // wall time: H2D + pass A + scan + bases; pass B + D2H
 };
 
-// one step's input: rows (events) or an event stream (bytes + boffsets)
+// one step's input: rows (events), an event stream (bytes + boffsets), or an event stream with
+// per-group sizes (sizes + the totals; offsets / boffsets unused: the engine scans the sizes)
 struct hq_dstep_in {
     uint64_t n;
     const uint32_t *groups;
@@ -58,6 +59,8 @@ struct hq_dstep_in {
     const hq_event *events;
     const uint64_t *boffsets;
     const uint8_t *bytes;
+    const uint32_t *sizes = nullptr;   // per group: events | bytes << 16
+    uint64_t n_events = 0, n_bytes = 0;
 };
 
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out);

@@ -49,10 +49,20 @@ struct StepK {
     const hq_event *events;       // rows, or
     const uint64_t *boffsets;     // an event stream (include/hipquorum.h "event streams")
     const uint8_t *bytes;
+    // sized streams: prefix[i] = events before group i << 32 | bytes before it (the scan of the
+    // sizes); pass A of byte chunk c takes the groups whose bytes end in [own_lo, own_hi)
+    const uint64_t *prefix;
+    uint64_t own_lo, own_hi;
     uint32_t *counts;             // [kLists][n] (+1): pass A output
     const uint32_t *scan;         // exclusive scan of counts: pass B input
     char *out;                    // pass B: the lists, written straight into pinned host memory
     const struct Layout *layout;  //   at layout->off[list]
+};
+
+struct PackSize {                 // per-group size word -> events << 32 | bytes
+    __host__ __device__ uint64_t operator()(uint32_t s) const {
+        return (uint64_t)(s & 0xFFFFu) << 32 | (s >> 16);
+    }
 };
 
 // where the lists go in the host output region (k_layout, from the scanned counts); a step with
@@ -459,14 +469,34 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
     const uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.i_end) return;
     if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
+    uint64_t e0, e1, b0 = 0, b1 = 0;
+    if (STREAM && a.prefix) {
+        const uint64_t x0 = a.prefix[i], x1 = a.prefix[i + 1];
+        e0 = x0 >> 32;
+        e1 = x1 >> 32;
+        b0 = x0 & 0xFFFFFFFFu;
+        b1 = x1 & 0xFFFFFFFFu;
+        if (!WRITE) {
+            // the sizes' totals must be the ones the copies were sized by (checked once)
+            if (i + 1 == a.n && a.own_lo == 0 && (e1 != a.n_events || b1 != a.n_bytes))
+                atomicOr(a.error, (uint32_t)kErrBoffsets);
+            if (b1 < a.own_lo || b1 >= a.own_hi) return;   // another chunk's group
+        }
+    } else {
+        e0 = a.offsets[i];
+        e1 = a.offsets[i + 1];
+        if (STREAM) {
+            b0 = a.boffsets[i];
+            b1 = a.boffsets[i + 1];
+        }
+    }
     const uint32_t h = a.handles[i];
     if (!WRITE) {                 // validate this group's entry; a bad one is not stepped
         uint32_t err = 0;
         if (h >= a.n_handles) err |= kErrHandle;
-        if (a.offsets[i + 1] < a.offsets[i] || (!STREAM && a.offsets[i + 1] > a.n_events))
+        if (e1 < e0 || (!STREAM && e1 > a.n_events) || (STREAM && a.prefix && e1 > a.n_events))
             err |= kErrOffsets;
-        if (STREAM && (a.boffsets[i + 1] < a.boffsets[i] || a.boffsets[i + 1] > a.n_bytes))
-            err |= kErrBoffsets;
+        if (STREAM && (b1 < b0 || b1 > a.n_bytes)) err |= kErrBoffsets;
         if (!(err & kErrHandle) && atomicExch(a.stamp + h, a.step_no) == a.step_no)
             err |= kErrTwice;
         if (err) {
@@ -478,10 +508,9 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
     hq_dread reads[kDReads];
     Engine<WRITE, MC> eng(a, i, h, reads);
     if (STREAM)
-        eng.template run<true>(a.offsets[i], a.offsets[i + 1], a.bytes + a.boffsets[i],
-                               a.bytes + a.boffsets[i + 1]);
+        eng.template run<true>(e0, e1, a.bytes + b0, a.bytes + b1);
     else
-        eng.template run<false>(a.offsets[i], a.offsets[i + 1], nullptr, nullptr);
+        eng.template run<false>(e0, e1, nullptr, nullptr);
     if (WRITE) {
         eng.store(h);
     } else {
@@ -696,9 +725,10 @@ int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t n
 int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     hq_ctx *ctx = d->ctx;
     const uint64_t n = in->n;
-    const uint64_t ne = n ? in->offsets[n] : 0;
     const bool stream = in->bytes != nullptr;
-    const uint64_t nb = stream && n ? in->boffsets[n] : 0;
+    const bool sized = stream && in->sizes != nullptr;   // per-group sizes, scanned here
+    const uint64_t ne = !n ? 0 : sized ? in->n_events : in->offsets[n];
+    const uint64_t nb = !n || !stream ? 0 : sized ? in->n_bytes : in->boffsets[n];
     *out = hq_dstep_out{};
     if (n == 0) return HQ_OK;
     const uint64_t t0 = now_ns();
@@ -708,11 +738,12 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     uint64_t bound[kMaxChunks + 1];
     for (int c = 0; c <= chunks; ++c) bound[c] = n * c / chunks;
     // the step's input in one device region: handles, offsets, [boffsets,] events or bytes, each
-    // at the offsets it has on the host
+    // at the offsets it has on the host; a sized stream: handles, sizes (+ a zero), their scan,
+    // bytes
     auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t o_off = up(n * 4);
     const size_t o_boff = o_off + up((n + 1) * 8);
-    const size_t o_ev = o_boff + (stream ? up((n + 1) * 8) : 0);
+    const size_t o_ev = o_boff + (stream ? up((n + 1) * 8) : 0);   // (sized: prefix at o_boff)
     // + 8: slack for ByteReader's aligned word past the last byte
     const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event)) + 8;
     if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
@@ -747,11 +778,19 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
                            "hq_dstep pinned output");
         if (!rc) d->host_out_cap = want;
     }
-    size_t tmp = 0;
+    size_t tmp = 0, tmp2 = 0;
+    const hipcub::TransformInputIterator<uint64_t, PackSize, const uint32_t *> packed_sizes(
+        reinterpret_cast<const uint32_t *>(din + o_off), PackSize{});
+    uint64_t *prefix = reinterpret_cast<uint64_t *>(din + o_boff);
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
                                 "hipcub scan size");
-    if (!rc) rc = grow(ctx, &d->scan_tmp, &d->scan_tmp_cap, tmp, false, "hq_dstep scan tmp");
+    if (!rc && sized)
+        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, packed_sizes,
+                                                                  prefix, n + 1, ctx->stream),
+                           "hipcub scan size");
+    if (!rc) rc = grow(ctx, &d->scan_tmp, &d->scan_tmp_cap, std::max(tmp, tmp2), false,
+                       "hq_dstep scan tmp");
     if (rc) return rc;
     StepK k{};
     k.groups = d->groups;
@@ -760,7 +799,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.n = n;
     k.handles = reinterpret_cast<const uint32_t *>(din);
     k.offsets = reinterpret_cast<const uint64_t *>(din + o_off);
-    if (stream) {
+    if (sized) {
+        k.prefix = prefix;
+        k.bytes = reinterpret_cast<const uint8_t *>(din + o_ev);
+    } else if (stream) {
         k.boffsets = reinterpret_cast<const uint64_t *>(din + o_boff);
         k.bytes = reinterpret_cast<const uint8_t *>(din + o_ev);
     } else {
@@ -803,8 +845,35 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
 #undef HQ_STEP_LAUNCH
         rc = hq::post_launch(ctx, write ? "k_step<write>" : "k_step<count>");
     };
+    if (sized) {
+        // handles and sizes (+ a zero: the scan's last element is the totals), their scan; then
+        // the bytes in equal byte chunks, each followed by pass A over the groups whose bytes end
+        // inside what has landed
+        h2d(0, in->groups, n * 4);
+        h2d(o_off, in->sizes, n * 4);
+        if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(din + o_off + n * 4, 0, 4, cs), "memset");
+        if (chunks > 1) {
+            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[0], cs), "event");
+            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[0], 0), "wait");
+        }
+        if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(
+                                              d->scan_tmp, tmp2, packed_sizes, prefix, n + 1,
+                                              ctx->stream),
+                                    "hipcub scan");
+        for (int c = 0; c < chunks && !rc; ++c) {
+            const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
+            h2d(o_ev + lo, in->bytes + lo, hi - lo);
+            if (chunks > 1) {
+                if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
+                if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
+            }
+            k.own_lo = c == 0 ? 0 : lo + 1;
+            k.own_hi = c + 1 == chunks ? UINT64_MAX : hi + 1;
+            launch(false, 0, n);
+        }
+    }
     // inputs chunk by chunk, pass A of each chunk once it has landed
-    for (int c = 0; c < chunks && !rc; ++c) {
+    for (int c = 0; c < chunks && !rc && !sized; ++c) {
         const uint64_t i0 = bound[c], i1 = bound[c + 1];
         h2d(i0 * 4, in->groups + i0, (i1 - i0) * 4);
         h2d(o_off + i0 * 8, in->offsets + i0, (i1 - i0 + 1) * 8);

@@ -97,6 +97,26 @@ int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event 
     return HQ_OK;
 }
 
+int hq_events_encode_sized(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
+                           uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_bytes) {
+    if (!offsets || !sizes || !n_bytes || (n_groups && offsets[n_groups] > offsets[0] && !events))
+        return HQ_E_INVAL;
+    uint8_t *p = out, *const end = out ? out + cap : nullptr;
+    for (uint64_t i = 0; i < n_groups; ++i) {
+        if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 0xFFFF) return HQ_E_INVAL;
+        uint8_t *const g0 = p;
+        uint64_t term_prev = 0;
+        for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
+            if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
+            p = encode(p, events[e], term_prev);
+        }
+        if (p - g0 > 0xFFFF) return HQ_E_INVAL;
+        sizes[i] = (uint32_t)(offsets[i + 1] - offsets[i]) | (uint32_t)(p - g0) << 16;
+    }
+    *n_bytes = (uint64_t)(p - out);
+    return HQ_OK;
+}
+
 int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t *boffsets,
                      const uint8_t *bytes, hq_event *events) {
     if (!offsets || !boffsets || !events) return HQ_E_INVAL;

@@ -432,6 +432,8 @@ int hq_wire_step_stream(hq_wire *w, hq_worker *worker, hq_step_stream *out, hq_w
     out->offsets = in.offsets;
     out->boffsets = w->boffsets.data();
     out->bytes = w->bytes.data();
+    out->sizes = nullptr;
+    out->n_events = out->n_bytes = 0;
     return HQ_OK;
 }
 

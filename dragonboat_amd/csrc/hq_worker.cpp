@@ -100,6 +100,7 @@ struct hq_worker {
     std::vector<uint32_t> dirty;          // handles changed on the host since the last upload
     hq_dstep_out dout{};
     std::vector<hq_event> decoded;        // host worker: a stream step's rows
+    std::vector<uint64_t> sized_off, sized_boff;   // host worker: a sized stream's prefixes
     std::string err;
     std::vector<Group> groups;
     std::vector<Member> pool;
@@ -879,7 +880,8 @@ int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
         return fail(HQ_E_INVAL, e & 1 ? "hq_worker_step: unknown group handle"
                                 : e & 8 ? "hq_worker_step: a group is listed twice"
                                 : e & 2 ? "hq_worker_step: offsets decrease"
-                                        : "hq_worker_step_stream: boffsets decrease");
+                                        : "hq_worker_step_stream: boffsets decrease or out of range, or sizes "
+                                          "not summing to the totals");
     }
     rc = hq(rc, "hq_dstep_run");
     if (rc) return rc;
@@ -1079,6 +1081,37 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
 int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output *out) {
     if (!w) return HQ_E_INVAL;
     if (!in || !out) return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL argument");
+    if (in->sizes || (in->n_groups && !in->offsets && !in->boffsets)) {
+        // the sized form: the device engine scans the sizes; a host worker (or a check) makes
+        // the prefix arrays here
+        if (in->n_groups && (!in->groups || !in->sizes))
+            return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL groups/sizes");
+        if (in->n_bytes && !in->bytes)
+            return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL bytes");
+        std::memset(out, 0, sizeof *out);
+        static const uint8_t none = 0;
+        if (w->dstep) {
+            hq_dstep_in d{in->n_groups, in->groups, nullptr, nullptr, nullptr,
+                          in->bytes ? in->bytes : &none};
+            d.sizes = in->sizes;
+            d.n_events = in->n_events;
+            d.n_bytes = in->n_bytes;
+            return w->step_on_device(d, out);
+        }
+        w->sized_off.resize(in->n_groups + 1);
+        w->sized_boff.resize(in->n_groups + 1);
+        w->sized_off[0] = w->sized_boff[0] = 0;
+        for (uint64_t i = 0; i < in->n_groups; ++i) {
+            w->sized_off[i + 1] = w->sized_off[i] + (in->sizes[i] & 0xFFFFu);
+            w->sized_boff[i + 1] = w->sized_boff[i] + (in->sizes[i] >> 16);
+        }
+        if (w->sized_off[in->n_groups] != in->n_events || w->sized_boff[in->n_groups] != in->n_bytes)
+            return w->fail(HQ_E_INVAL, "hq_worker_step_stream: sizes do not sum to the totals");
+        const hq_step_stream full{in->n_groups, in->groups, w->sized_off.data(),
+                                  w->sized_boff.data(), in->bytes ? in->bytes : &none,
+                                  nullptr, 0, 0};
+        return hq_worker_step_stream(w, &full, out);
+    }
     if (in->n_groups && (!in->groups || !in->offsets || !in->boffsets))
         return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL groups/offsets/boffsets");
     if (in->n_groups && in->boffsets[in->n_groups] > in->boffsets[0] && !in->bytes)

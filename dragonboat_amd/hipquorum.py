@@ -180,7 +180,16 @@ class StepStream(ctypes.Structure):
     """Mirror of ``hq_step_stream``."""
 
     _fields_ = [("n_groups", ctypes.c_uint64), ("groups", _vp), ("offsets", _vp),
-                ("boffsets", _vp), ("bytes", _vp)]
+                ("boffsets", _vp), ("bytes", _vp), ("sizes", _vp), ("n_events", ctypes.c_uint64),
+                ("n_bytes", ctypes.c_uint64)]
+
+
+class SizedStream(tuple):
+    """A step's event stream in the sized form of ``hq_step_stream``: (groups, sizes, n_events,
+    bytes), sizes[i] = events | bytes << 16 of group i (encode_events_sized)."""
+
+    def __new__(cls, groups, sizes, n_events, data):
+        return super().__new__(cls, (groups, sizes, n_events, data))
 
 
 HQ_EVENT_STREAM_MAX = 64
@@ -331,6 +340,8 @@ SIGNATURES = {
                                              ctypes.POINTER(StepOutput)]),
     "hq_worker_step_jobs": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "hq_events_encode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    "hq_events_encode_sized": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64,
+                                              _vp, _vp]),
     "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
                                            ctypes.POINTER(WireStats)]),
@@ -1264,6 +1275,16 @@ class Worker:
                     "hq_worker_step_stream")
         return self._results(out, copy)
 
+    def step_sized(self, groups, sizes, n_events, data, copy=True):
+        """hq_worker_step_stream in the sized form (encode_events_sized): per-group size words
+        instead of the two prefix arrays."""
+        inp, keep = _sized_input(groups, sizes, n_events, data)
+        out = StepOutput()
+        self._check(lib.hq_worker_step_stream(self.h, ctypes.byref(inp), ctypes.byref(out)),
+                    "hq_worker_step_stream")
+        del keep
+        return self._results(out, copy)
+
     @staticmethod
     def _results(out, copy):
         res = {}
@@ -1299,7 +1320,11 @@ class StepJobs:
         self.keep, self.arr = [], (StepJob * len(jobs))()
         self.outs = [StepOutput() for _ in jobs]
         for j, (w, a) in enumerate(jobs):
-            if len(a) == 3:
+            if isinstance(a, SizedStream):
+                inp, keep = _sized_input(*a)
+                self.arr[j].stream = ctypes.cast(ctypes.pointer(inp), _vp)
+                self.keep += keep + [inp]
+            elif len(a) == 3:
                 g, o, e = (np.ascontiguousarray(a[0], np.uint32),
                            np.ascontiguousarray(a[1], np.uint64),
                            np.ascontiguousarray(a[2], EVENT_DTYPE))
@@ -1343,6 +1368,32 @@ def encode_events(offsets, events):
     _chk(lib.hq_events_encode(n, _p(offsets), _p(events) if len(events) else None, _p(out),
                               len(out), _p(boff)), "hq_events_encode")
     return out[:int(boff[-1])].copy(), boff
+
+
+def _sized_input(groups, sizes, n_events, data):
+    g = np.ascontiguousarray(groups, np.uint32)
+    z = np.ascontiguousarray(sizes, np.uint32)
+    d = np.ascontiguousarray(data, np.uint8)
+    assert len(g) == len(z)
+    inp = StepStream(len(g), _p(g), None, None, _p(d) if len(d) else None, _p(z),
+                     int(n_events), len(d))
+    return inp, [g, z, d]
+
+
+def encode_events_sized(offsets, events):
+    """hq_events_encode_sized: (stream bytes as uint8, per-group size words) of rows grouped by
+    `offsets`."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    events = np.ascontiguousarray(events, EVENT_DTYPE)
+    n = len(offsets) - 1
+    ne = int(offsets[-1] - offsets[0]) if n > 0 else 0
+    out = np.zeros(max(1, ne * HQ_EVENT_STREAM_MAX), np.uint8)
+    sizes = np.zeros(max(0, n), np.uint32)
+    nb = ctypes.c_uint64(0)
+    _chk(lib.hq_events_encode_sized(n, _p(offsets), _p(events) if len(events) else None,
+                                    _p(out), len(out), _p(sizes), ctypes.byref(nb)),
+         "hq_events_encode_sized")
+    return out[:nb.value].copy(), sizes
 
 
 def decode_events(offsets, boffsets, data):

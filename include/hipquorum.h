@@ -900,6 +900,12 @@ typedef struct hq_step_stream {
     const uint64_t *offsets;     /* [n_groups + 1] event index prefix, as hq_step_input */
     const uint64_t *boffsets;    /* [n_groups + 1] byte prefix into bytes, non-decreasing */
     const uint8_t *bytes;
+    /* Sized form (sizes != NULL; offsets / boffsets are then not read): per group one word,
+     * events | bytes << 16 (each < 2^16), and the totals over the step — 4 bytes per group
+     * cross PCIe instead of the 16 of the two prefix arrays, and the device engine scans them.
+     * Event indexes (deferred) count from 0 in group order as with offsets[0] = 0. */
+    const uint32_t *sizes;
+    uint64_t n_events, n_bytes;
 } hq_step_stream;
 
 /* Encode rows (offsets as in hq_step_input) into out[0 .. cap) and boffsets[0 .. n_groups];
@@ -907,6 +913,11 @@ typedef struct hq_step_stream {
  * HQ_EVENT_STREAM_MAX per event to never hit it). */
 int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
                      uint8_t *out, uint64_t cap, uint64_t *boffsets);
+/* The same with per-group size words (sizes[i] = events | bytes << 16, the hq_step_stream sized
+ * form) and the byte total instead of boffsets; HQ_E_INVAL when a group has 2^16 or more events
+ * or bytes (use boffsets for such a step). */
+int hq_events_encode_sized(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
+                           uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_bytes);
 /* Decode a stream back into rows events[offsets[0] .. offsets[n_groups]); HQ_E_INVAL when a
  * group's bytes do not hold exactly its events. */
 int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t *boffsets,

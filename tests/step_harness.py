@@ -96,6 +96,9 @@ class WorkerBackend:
             offsets.append(len(recs))
         grp, off = np.array(handles, np.uint32), np.array(offsets, np.uint64)
         ev = np.array(recs, hq.EVENT_DTYPE)
+        if self.stream == "sized":
+            data, sizes = hq.encode_events_sized(off, ev)
+            return hq.SizedStream(grp, sizes, len(ev), data), refs
         if self.stream:
             data, boff = hq.encode_events(off, ev)
             return (grp, off, boff, data), refs
@@ -103,7 +106,10 @@ class WorkerBackend:
 
     def step(self, per_group):
         arrs, refs = self.build_inputs(per_group)
-        res = self.w.step(*arrs) if len(arrs) == 3 else self.w.step_stream(*arrs)
+        if isinstance(arrs, self.hq.SizedStream):
+            res = self.w.step_sized(*arrs)
+        else:
+            res = self.w.step(*arrs) if len(arrs) == 3 else self.w.step_stream(*arrs)
         self.last_passes, self.last_decisions = res["gpu_passes"], res["decisions"]
         self.last_raw = res
         out = {cid: {"ready": [], "resps": [], "states": [], "dropped": [], "deferred": [],
@@ -224,4 +230,7 @@ class WireBackend(WorkerBackend):
             assert int(off[i + 1]) - int(off[i]) == len(per_group[cid])
         assert sorted(handle_cid[int(h)] for h in grp) == sorted(c for c in cids
                                                                  if per_group[c])
+        if self.stream == "sized":
+            sizes = (np.diff(off) | (np.diff(boff) << np.uint64(16))).astype(np.uint32)
+            return self.hq.SizedStream(grp, sizes, int(off[-1]), data), refs
         return ((grp, off, boff, data) if self.stream else (grp, off, ev)), refs

@@ -17,8 +17,9 @@ CASES = list(sc.all_cases())
 MODES = [False, True]
 MODE_IDS = ["host", "device"]      # the host worker / HQ_WORKER_ON_DEVICE (hq_dstep.hip)
 # (on_device, stream): events as rows or as an event stream (hq_worker_step_stream)
-FEEDS = [(False, False), (True, False), (True, True), (False, True)]
-FEED_IDS = ["host", "device", "device-stream", "host-stream"]
+FEEDS = [(False, False), (True, False), (True, True), (False, True), (True, "sized"),
+         (False, "sized")]
+FEED_IDS = ["host", "device", "device-stream", "host-stream", "device-sized", "host-sized"]
 
 
 @pytest.fixture(scope="module", params=FEEDS, ids=FEED_IDS)
@@ -253,7 +254,7 @@ def test_malformed_stream(hq, on_device):
         w.close()
 
 
-@pytest.mark.parametrize("feed", FEEDS, ids=FEED_IDS)
+@pytest.mark.parametrize("feed", FEEDS[:4], ids=FEED_IDS[:4])
 def test_step_input_errors_leave_state(hq, feed):
     """Bad step inputs are rejected whole (HQ_E_INVAL) with no group state changed: an unknown
     handle, a group listed twice, decreasing offsets."""
@@ -283,6 +284,32 @@ def test_step_input_errors_leave_state(hq, feed):
         w.close()
 
 
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_sized_input_errors_leave_state(hq, on_device):
+    """The sized stream form: sizes that do not sum to the totals, an unknown handle or a group
+    listed twice reject the step whole, no group state changed."""
+    w = hq.Worker(0, 4, on_device=on_device)
+    try:
+        for cid in (1, 2):
+            w.add_group(cid, 1, 2, sc.LEADER, 5, 6, 5, [(1, 6, 0, 0), (2, 5, 0, 0), (3, 5, 0, 0)])
+        ev = np.array([(hq.EV_MESSAGE, sc.RREP, 2, 2, 6, 0, 0, 0, 0)] * 2, hq.EVENT_DTYPE)
+        data, sizes = hq.encode_events_sized(np.array([0, 1, 2], np.uint64), ev)
+        assert list(sizes) == [1 | 4 << 16, 1 | 4 << 16] and len(data) == 8
+        for grp, z, ne, d, msg in (
+                ([0, 7], sizes, 2, data, "unknown group handle"),
+                ([1, 1], sizes, 2, data, "listed twice"),
+                ([0, 1], sizes, 3, data, "sizes"),                        # events total
+                ([0, 1], sizes, 2, np.concatenate([data, data[:1]]), "sizes"),   # bytes total
+                ([0, 1], [1 | 4 << 16, 1 | 5 << 16], 2, data, "sizes")):
+            with pytest.raises(hq.HQError, match=msg):
+                w.step_sized(np.array(grp, np.uint32), np.array(z, np.uint32), ne, d)
+            assert w.get_group(1)[0]["committed"] == 5 and w.get_group(2)[0]["committed"] == 5
+        res = w.step_sized(np.array([1, 0], np.uint32), sizes, 2, data)
+        assert sorted(int(c["cluster_id"]) for c in res["commits"]) == [1, 2]
+    finally:
+        w.close()
+
+
 def test_step_jobs_equal_sequential_steps(hq):
     """hq_worker_step_jobs: several workers (device and host, rows and streams) stepped at once
     on native threads end in the same results and state as stepping them one by one."""
@@ -292,7 +319,7 @@ def test_step_jobs_equal_sequential_steps(hq):
     roles = bench.STEP_ROLES["step5"]
     g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
     nm, nv = len(roles), sum(r != "observer" for r in roles)
-    kinds = [(True, True), (True, False), (False, False), (True, True)]
+    kinds = [(True, True), (True, False), (False, False), (True, True), (True, "sized")]
     bounds = [G * i // len(kinds) for i in range(len(kinds) + 1)]
 
     def make():
@@ -309,13 +336,17 @@ def test_step_jobs_equal_sequential_steps(hq):
             jobs = []
             for i, (_, stream) in enumerate(kinds):
                 e = bench.step_events(hq, bounds[i + 1] - bounds[i], s, roles)
-                if stream:
+                if stream == "sized":
+                    data, sizes = hq.encode_events_sized(e[1], e[2])
+                    e = hq.SizedStream(e[0], sizes, len(e[2]), data)
+                elif stream:
                     data, boff = hq.encode_events(e[1], e[2])
                     e = (e[0], e[1], boff, data)
                 jobs.append(e)
             got = hq.step_jobs(list(zip(a, jobs)))
             for i, (w, e) in enumerate(zip(b, jobs)):
-                want = w.step(*e) if len(e) == 3 else w.step_stream(*e)
+                want = w.step_sized(*e) if isinstance(e, hq.SizedStream) else \
+                    w.step(*e) if len(e) == 3 else w.step_stream(*e)
                 for k in ("commits", "ready", "read_resps", "state_changes", "dropped_reads",
                           "deferred", "fallback_groups"):
                     np.testing.assert_array_equal(got[i][k], want[k], err_msg=k)
@@ -327,7 +358,7 @@ def test_step_jobs_equal_sequential_steps(hq):
             w.close()
 
 
-@pytest.mark.parametrize("stream", [True, False], ids=["stream", "rows"])
+@pytest.mark.parametrize("stream", [True, False, "sized"], ids=["stream", "rows", "sized"])
 def test_chunked_device_step_equals_host_worker(hq, stream):
     """A step of >= 256 Ki groups runs in 4 chunks whose copies overlap the neighbouring chunks'
     passes (hq_dstep.hip); its lists equal the host worker's on the same events (the host
@@ -345,7 +376,10 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
         for s in range(3):
             e = bench.step_events(hq, G, s, roles)
             want = host.step(*e)
-            if stream:
+            if stream == "sized":      # byte chunks, each group's pass A in the chunk its
+                data, sizes = hq.encode_events_sized(e[1], e[2])   # bytes end in
+                got = dev.step_sized(e[0], sizes, len(e[2]), data)
+            elif stream:
                 data, boff = hq.encode_events(e[1], e[2])
                 got = dev.step_stream(e[0], e[1], boff, data)
             else:

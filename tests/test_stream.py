@@ -117,3 +117,33 @@ def test_encode_capacity(hq):
     rc = hq.lib.hq_events_encode(1, off.ctypes.data, ev.ctypes.data, out.ctypes.data,
                                  len(out), boff.ctypes.data)
     assert rc == hq.HQ_E_STATE
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_sized_encoding_equals_prefix_encoding(hq, seed):
+    """hq_events_encode_sized: the same bytes as hq_events_encode, and size words = (events,
+    bytes) of each group = the differences of the two prefix arrays."""
+    rng = np.random.default_rng(seed)
+    n = 700
+    counts = rng.integers(0, 12, n)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    ev = random_rows(rng, int(off[-1])).view(hq.EVENT_DTYPE)
+    data, boff = hq.encode_events(off, ev)
+    sdata, sizes = hq.encode_events_sized(off, ev)
+    np.testing.assert_array_equal(sdata, data)
+    np.testing.assert_array_equal(sizes & 0xFFFF, np.diff(off))
+    np.testing.assert_array_equal(sizes >> 16, np.diff(boff))
+
+
+def test_sized_encoding_limits(hq):
+    """A group of 2^16 events (or bytes) does not fit a size word: HQ_E_INVAL."""
+    ev = np.zeros(1 << 16, hq.EVENT_DTYPE)
+    ev["kind"] = hq.EV_CHECK_QUORUM                           # 1 byte each
+    with pytest.raises(hq.HQError):
+        hq.encode_events_sized(np.array([0, 1 << 16], np.uint64), ev)
+    data, sizes = hq.encode_events_sized(np.array([0, (1 << 16) - 1], np.uint64), ev[:-1])
+    assert int(sizes[0]) == 0xFFFF | 0xFFFF << 16 and len(data) == 0xFFFF
+    big = np.zeros(9000, hq.EVENT_DTYPE)                     # ~10 bytes each: > 2^16 bytes
+    big["kind"], big["hint"], big["hint_high"] = hq.EV_READ, 1 << 40, 1 << 30
+    with pytest.raises(hq.HQError):
+        hq.encode_events_sized(np.array([0, 9000], np.uint64), big)

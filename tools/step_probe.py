@@ -1,6 +1,6 @@
 """Probe: the device step engine on the bench's step workload (G = 1M leader groups), W workers
-(one native thread each via hq_worker_step_jobs, G / W groups each), events in pinned memory (FEED=stream: as the event
-stream, FEED=rows: as hq_event rows); prints per-step wall time. Run under rocprofv3
+(one native thread each via hq_worker_step_jobs, G / W groups each), events in pinned memory (FEED=sized: the event
+stream with per-group size words, FEED=stream: with the two prefix arrays, FEED=rows: hq_event rows); prints per-step wall time. Run under rocprofv3
 --kernel-trace --stats for the kernels' share."""
 import os
 import sys
@@ -16,7 +16,8 @@ G = int(os.environ.get("G", 1 << 20))
 W = int(os.environ.get("W", 1))
 STEPS = int(os.environ.get("STEPS", 6))
 roles = bench.STEP_ROLES[os.environ.get("LEG", "step")]
-stream = os.environ.get("FEED", "stream") == "stream"
+feed = os.environ.get("FEED", "sized")      # sized | stream | rows
+stream = feed in ("stream", "sized")
 bounds = [G * i // W for i in range(W + 1)]
 g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
 nm = len(roles)
@@ -31,12 +32,18 @@ for s in range(STEPS):
     for i in range(W):
         e = bench.step_events(hq, bounds[i + 1] - bounds[i], s, roles)
         ne += len(e[2])
-        if stream:
+        nev = len(e[2])
+        if feed == "sized":
+            data, sizes = hq.encode_events_sized(e[1], e[2])
+            e = (e[0], sizes, data)
+        elif stream:
             data, boff = hq.encode_events(e[1], e[2])
             e = (e[0], e[1], boff, data)
         p = tuple(pc.pinned(x.size, x.dtype) for x in e)
         for dst, src in zip(p, e):
             dst[:] = src
+        if feed == "sized":
+            p = hq.SizedStream(p[0], p[1], nev, p[2])
         inputs.append(p)
     jobs = hq.StepJobs(list(zip(workers, inputs)))
     t0 = time.perf_counter()
@@ -47,7 +54,7 @@ for s in range(STEPS):
         print("  device ms per worker:", " ".join(f"{r['device_ns'] / 1e6:.2f}" for r in res),
               "| host ms:", " ".join(f"{r['handle_ns'] / 1e6:.2f}" for r in res), flush=True)
     print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, W={W}, "
-          f"max device {dev:.2f} ms, input {sum(x.nbytes for p in inputs for x in p) / 1e6:.1f} MB",
+          f"max device {dev:.2f} ms, input {sum(getattr(x, 'nbytes', 0) for p in inputs for x in p) / 1e6:.1f} MB",
           flush=True)
 for w in workers:
     w.close()
