@@ -865,11 +865,14 @@ def _partition(ev_full, b0, b1):
     return (np.arange(b1 - b0, dtype=np.uint32), o - o[0], ev[int(o[0]):int(o[-1])])
 
 
+STEP_WARM = 2
+
+
 def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, stream=False,
                  events=None):
     """W workers (one native thread each, own HIP stream) over G groups split into W contiguous
     partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
-    of the first 4096 groups after cpu_steps steps, ..., encode seconds). on_device:
+    of the first 4096 groups after the last step, ..., encode seconds). on_device:
     HQ_WORKER_ON_DEVICE workers, the step's input in pinned host memory (a step worker's receive
     buffers) so that it crosses PCIe at the link's rate. stream: the input is the event stream
     (hq_worker_step_stream), written by the producer — here hq_events_encode over the rows,
@@ -891,8 +894,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
                decisions=0)
     t_total, n_events, committed, t_enc, nb_total = 0.0, 0, None, 0.0, 0
     step_ms = []
-    warm = 2       # untimed: allocations, first touch, and the first step with commits (its
-    for s in range(steps + warm):   # output lists size the pinned result buffers)
+    warm = STEP_WARM   # untimed: allocations, first touch, and the first step with commits
+    for s in range(steps + warm):   # (its output lists size the pinned result buffers)
         full = events(s) if events else step_events(hq, G, s, roles)
         evs = [_partition(full, bounds[i], bounds[i + 1]) for i in range(W)]
         n_step = sum(len(e[2]) for e in evs)
@@ -923,9 +926,6 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
         t0 = time.perf_counter()
         res = jobs.run(copy=False)
         dt = time.perf_counter() - t0
-        if s == cpu_steps:   # state checked against the CPU replay of the same steps
-            committed = [int(workers[0].get_group(int(c))[0]["committed"])
-                         for c in cids[:min(4096, bounds[1])]]
         if s < warm:
             continue
         step_ms.append(round(dt * 1e3, 3))
@@ -934,6 +934,10 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
         for r in res:
             for k in acc:
                 acc[k] += r[k]
+    # the state after the last step, checked against the CPU replay of the same steps (read
+    # after the timed steps: reading a device worker's state downloads all of it)
+    committed = [int(workers[0].get_group(int(c))[0]["committed"])
+                 for c in cids[:min(4096, bounds[1])]]
     for w in workers:
         w.close()
     if pin_ctx is not None:
@@ -1025,11 +1029,11 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
         for nt in (1, T):
             b = qref.StepBatch(g, m)
             tc, ne = 0.0, 0
-            for s in range(cpu_steps + 1):
-                ev = events(s)
+            for s in range(steps + STEP_WARM):   # timed: steps 1 .. cpu_steps; the rest
+                ev = events(s)                       # replayed for the final state
                 t0 = time.perf_counter()
                 b.step(*ev, nthreads=nt)
-                if s > 0:
+                if 0 < s <= cpu_steps:
                     tc += time.perf_counter() - t0
                     ne += len(ev[2])
             committed_cpu = [b.committed(i) for i in range(len(committed["host"]))]
