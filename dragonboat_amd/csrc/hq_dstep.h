@@ -45,6 +45,8 @@ struct hq_dstep_out {                 // the lists of one step, in input group o
     const uint64_t *fallback;
     uint64_t n_commits, n_ready, n_resps, n_states, n_dropped, n_deferred, n_fallback;
     uint64_t decisions;
+    const uint64_t *commit_col;       // the commits as a column (hq_dstep_open's commit_column
+                                      // and more than half of the groups committing), else NULL
     uint32_t input_error;             // HQ_E_INVAL: bit 1 unknown handle, 2 offsets, 4 boffsets,
                                       // 8 a group listed twice (no group state written)
     uint64_t kernel_ns, d2h_ns;       // wall time: H2D + pass A + scan + bases; pass B + D2H
@@ -63,7 +65,8 @@ struct hq_dstep_in {
     uint64_t n_events = 0, n_bytes = 0;
 };
 
-int hq_dstep_open(hq_ctx *ctx, hq_dstep **out);
+// commit_column: a step may return its commits as a column (HQ_WORKER_COMMIT_COLUMN)
+int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, bool commit_column = false);
 void hq_dstep_close(hq_dstep *d);
 // copy group records [g0, g0 + ng) with their reads (kDReads per group) and member records
 // [m0, m0 + nm) to the device, growing the device arrays to hold them

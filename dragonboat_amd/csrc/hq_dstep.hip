@@ -72,6 +72,7 @@ struct Layout {
     uint32_t len[kLists];
     uint64_t total;
     uint32_t error, overflow;
+    uint32_t commit_column;       // the commits list is a column: one word per listed group
 };
 
 __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
@@ -434,7 +435,9 @@ struct Engine {
                 defer(e);
             }
         }
-        if (g.committed != committed0) {
+        if (WRITE && a.layout->commit_column) {          // every listed group writes its word
+            list<uint64_t>(kCommits)[i] = g.committed != committed0 ? g.committed : 0;
+        } else if (g.committed != committed0) {
             const uint32_t p = slot(kCommits);
             if (WRITE) list<hq_commit_event>(kCommits)[p] = hq_commit_event{g.cluster_id, g.committed};
         }
@@ -522,17 +525,21 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
 // input errors of pass A (reset for the next step)
 constexpr int kMaxChunks = 4;
 __global__ void k_layout(const uint32_t *scan, uint64_t n, uint32_t *error, uint64_t cap,
-                         Layout *lay) {
+                         uint32_t allow_column, Layout *lay) {
     if (threadIdx.x != 0) return;
     const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
                                   sizeof(hq_read_index_resp), sizeof(hq_state_change),
                                   sizeof(hq_dropped_read), 8, 8, 0};
     uint64_t total = 0;
+    const uint32_t commits = scan[n] - scan[0];
+    // the commits as a column when that moves fewer bytes (8 per group vs 16 per commit)
+    lay->commit_column = allow_column && 2 * (uint64_t)commits > n;
     for (int l = 0; l < kLists; ++l) {
         const uint32_t len = scan[(uint64_t)(l + 1) * n] - scan[(uint64_t)l * n];
         lay->off[l] = total;
         lay->len[l] = len;
-        total += (len * rec[l] + 255) & ~uint64_t(255);
+        const uint64_t bytes = l == kCommits && lay->commit_column ? n * 8 : len * rec[l];
+        total += (bytes + 255) & ~uint64_t(255);
     }
     lay->total = total;
     lay->error = *error;
@@ -558,6 +565,7 @@ struct hq_dstep {
     uint64_t n_groups = 0;        // group records uploaded (valid handles)
     uint32_t max_members = 0;     // the most members of any uploaded group
     uint32_t step_no = 0;
+    bool commit_column = false;   // HQ_WORKER_COMMIT_COLUMN
     // step staging
     void *in = nullptr;
     size_t in_cap = 0;
@@ -617,11 +625,12 @@ int wait_stream(hq_dstep *d, hipStream_t s, const char *what) {
 
 }  // namespace
 
-int hq_dstep_open(hq_ctx *ctx, hq_dstep **out) {
+int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, bool commit_column) {
     *out = new (std::nothrow) hq_dstep();
     if (!*out) return HQ_E_NOMEM;
     hq_dstep *d = *out;
     d->ctx = ctx;
+    d->commit_column = commit_column;
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     if (!rc)
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming |
@@ -901,7 +910,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     auto pass_b = [&]() {
         if (!rc) {
             hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, k.error,
-                               (uint64_t)d->host_out_cap, d->layout);
+                               (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout);
             rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
         }
         launch(true, 0, n);
@@ -932,7 +941,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (lay.overflow || lay.error) return hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout");
     }
     const char *ho = static_cast<const char *>(d->host_out);
-    out->commits = reinterpret_cast<const hq_commit_event *>(ho + lay.off[kCommits]);
+    out->commits = lay.commit_column ? nullptr
+                                     : reinterpret_cast<const hq_commit_event *>(ho + lay.off[kCommits]);
+    out->commit_col = lay.commit_column ? reinterpret_cast<const uint64_t *>(ho + lay.off[kCommits])
+                                        : nullptr;
     out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + lay.off[kReady]);
     out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + lay.off[kResps]);
     out->states = reinterpret_cast<const hq_state_change *>(ho + lay.off[kStates]);

@@ -889,6 +889,7 @@ int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     const uint64_t t2 = now_ns();
     out->commits = dout.commits;
     out->n_commits = dout.n_commits;
+    out->committed_column = dout.commit_col;
     out->ready = dout.ready;
     out->n_ready = dout.n_ready;
     out->read_resps = dout.resps;
@@ -920,7 +921,7 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
 
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out) {
     if (!out) return HQ_E_INVAL;
-    if (flags & ~HQ_WORKER_ON_DEVICE) return HQ_E_INVAL;
+    if (flags & ~(HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_COLUMN)) return HQ_E_INVAL;
     *out = nullptr;
     if (n_max < 1 || n_max > HQ_MAX_VOTERS) return HQ_E_INVAL;
     hq_worker *w = new (std::nothrow) hq_worker();
@@ -932,7 +933,7 @@ int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **ou
     }
     w->n_max = n_max;
     if (flags & HQ_WORKER_ON_DEVICE) {
-        rc = hq_dstep_open(w->ctx, &w->dstep);
+        rc = hq_dstep_open(w->ctx, &w->dstep, (flags & HQ_WORKER_COMMIT_COLUMN) != 0);
         if (rc) {
             hq_close(w->ctx);
             delete w;

@@ -38,6 +38,7 @@ HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table
 HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
 HQ_INGEST_UNIQUE = 2         # hq_table_*: every key at most once in the batch
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
+HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_ABI_VERSION = 10
 
 OUTCOME_FOLLOWER = 0
@@ -215,7 +216,7 @@ class StepOutput(ctypes.Structure):
                [("gpu_passes", ctypes.c_uint64), ("decisions", ctypes.c_uint64),
                 ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64),
                 ("pack_ns", ctypes.c_uint64), ("device_ns", ctypes.c_uint64),
-                ("apply_ns", ctypes.c_uint64)]
+                ("apply_ns", ctypes.c_uint64), ("committed_column", _vp)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -1179,13 +1180,16 @@ class Worker:
     """The step worker (hq_worker_*): one step's events in, the reference's step results out,
     every quorum decision taken by the kernels."""
 
-    def __init__(self, device: int = 0, n_max: int = 8, on_device: bool = False):
+    def __init__(self, device: int = 0, n_max: int = 8, on_device: bool = False,
+                 commit_column: bool = False):
         """on_device: HQ_WORKER_ON_DEVICE, the group state resident on the GPU and every event
         taken there (hq_dstep.hip); otherwise the host worker (events on the host, decisions
-        in GPU passes)."""
+        in GPU passes). commit_column: HQ_WORKER_COMMIT_COLUMN (results carry
+        'committed_column' instead of 'commits' when most listed groups commit)."""
         self.h = _vp()
-        rc = lib.hq_worker_open_ex(device, n_max, HQ_WORKER_ON_DEVICE if on_device else 0,
-                                   ctypes.byref(self.h))
+        flags = (HQ_WORKER_ON_DEVICE if on_device else 0) | \
+            (HQ_WORKER_COMMIT_COLUMN if commit_column else 0)
+        rc = lib.hq_worker_open_ex(device, n_max, flags, ctypes.byref(self.h))
         if rc != HQ_OK:
             raise HQError(rc, "hq_worker_open: " + lib.hq_last_error(None).decode())
         self.n_max = n_max
@@ -1259,7 +1263,7 @@ class Worker:
         out = StepOutput()
         self._check(lib.hq_worker_step(self.h, ctypes.byref(inp), ctypes.byref(out)),
                     "hq_worker_step")
-        return self._results(out, copy)
+        return self._results(out, copy, len(groups))
 
     def step_stream(self, groups, offsets, boffsets, data, copy=True):
         """hq_worker_step_stream: the step's events as an event stream (encode_events)."""
@@ -1273,7 +1277,7 @@ class Worker:
         out = StepOutput()
         self._check(lib.hq_worker_step_stream(self.h, ctypes.byref(inp), ctypes.byref(out)),
                     "hq_worker_step_stream")
-        return self._results(out, copy)
+        return self._results(out, copy, len(groups))
 
     def step_sized(self, groups, sizes, n_events, data, copy=True):
         """hq_worker_step_stream in the sized form (encode_events_sized): per-group size words
@@ -1283,15 +1287,15 @@ class Worker:
         self._check(lib.hq_worker_step_stream(self.h, ctypes.byref(inp), ctypes.byref(out)),
                     "hq_worker_step_stream")
         del keep
-        return self._results(out, copy)
+        return self._results(out, copy, len(groups))
 
     @staticmethod
-    def _results(out, copy):
+    def _results(out, copy, n_listed=0):
         res = {}
         for name, dt in STEP_OUTPUT_LISTS:
             n = getattr(out, "n_" + name)
             ptr = getattr(out, name)
-            if n == 0:
+            if n == 0 or (name == "commits" and out.committed_column):
                 res[name] = np.zeros(0, dt)
                 continue
             buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
@@ -1299,6 +1303,11 @@ class Worker:
         for k in ("gpu_passes", "decisions", "handle_ns", "pass_ns", "pack_ns", "device_ns",
                   "apply_ns"):
             res[k] = getattr(out, k)
+        if out.committed_column:
+            buf = (ctypes.c_char * (n_listed * 8)).from_address(out.committed_column)
+            col = np.frombuffer(buf, np.uint64)
+            res["committed_column"] = col.copy() if copy else col
+            res["n_commits"] = out.n_commits
         return res
 
     def add_groups(self, groups: np.ndarray, members: np.ndarray) -> None:
@@ -1349,7 +1358,7 @@ class StepJobs:
             msg = lib.hq_worker_last_error(self.jobs[bad[0]][0].h).decode() if bad \
                 else "a worker listed twice"
             raise HQError(rc, f"hq_worker_step_jobs: {msg}")
-        return [Worker._results(o, copy) for o in self.outs]
+        return [Worker._results(o, copy, len(a[0])) for o, (_, a) in zip(self.outs, self.jobs)]
 
 
 def step_jobs(jobs, copy=True):

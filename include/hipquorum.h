@@ -832,6 +832,10 @@ typedef struct hq_step_output {
     uint64_t pack_ns;           /*   of which packing the kernels' SoA inputs */
     uint64_t device_ns;         /*   of which H2D + kernels + D2H + sync */
     uint64_t apply_ns;          /*   of which applying the decisions */
+    /* HQ_WORKER_COMMIT_COLUMN workers only, else NULL: the step's commits as one word per
+     * listed group (input order), its new committed index or 0 (no commit: a commit never sets
+     * 0); `commits` is then NULL and n_commits counts the nonzero words */
+    const uint64_t *committed_column;
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;
@@ -847,6 +851,10 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
  * two synchronisations). Same results as the host worker; groups of at most 16 members.
  * add/set/get_group work on a host mirror refreshed from the device when needed. */
 #define HQ_WORKER_ON_DEVICE 1u
+/* with HQ_WORKER_ON_DEVICE: a step in which more than half of the listed groups commit returns
+ * its commits as hq_step_output.committed_column (8 bytes per listed group across PCIe instead
+ * of a 16-byte record per commit); other steps keep the list */
+#define HQ_WORKER_COMMIT_COLUMN 2u
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out);
 void hq_worker_close(hq_worker *w);
 const char *hq_worker_last_error(const hq_worker *w);

@@ -64,9 +64,12 @@ class WorkerBackend:
     hq_worker_step_stream) instead of rows."""
 
     def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False, stream=False):
+        """stream: False (rows), True (stream with prefix arrays), "sized" (size words) or
+        "sized-column" (size words in, commits as a column out: HQ_WORKER_COMMIT_COLUMN)."""
         self.hq = hq
         self.stream = stream
-        self.w = worker if worker is not None else hq.Worker(0, n_max, on_device=on_device)
+        self.w = worker if worker is not None else hq.Worker(
+            0, n_max, on_device=on_device, commit_column=stream == "sized-column")
         self.rng = np.random.default_rng(seed)
         self.cids = []
         self.last_passes = 0
@@ -94,9 +97,10 @@ class WorkerBackend:
                 refs[len(recs)] = (cid, pos)
                 recs.append(event_record(hq, e))
             offsets.append(len(recs))
+        self.last_cids = cids
         grp, off = np.array(handles, np.uint32), np.array(offsets, np.uint64)
         ev = np.array(recs, hq.EVENT_DTYPE)
-        if self.stream == "sized":
+        if str(self.stream).startswith("sized"):
             data, sizes = hq.encode_events_sized(off, ev)
             return hq.SizedStream(grp, sizes, len(ev), data), refs
         if self.stream:
@@ -133,8 +137,16 @@ class WorkerBackend:
             out[cid]["deferred"].sort()
         for r in res["commits"]:
             out[int(r["cluster_id"])]["commit_changed"] = True
+        col = res.get("committed_column")
+        if col is not None:             # one word per listed group, in input order
+            assert len(col) == len(self.last_cids) and res["n_commits"] == int((col != 0).sum())
+            for cid, v in zip(self.last_cids, col.tolist()):
+                if v:
+                    out[cid]["commit_changed"] = True
+                    out[cid]["_col"] = v
         for cid in out:
             out[cid]["committed"] = int(self.w.get_group(cid)[0]["committed"])
+            assert out[cid].pop("_col", out[cid]["committed"]) == out[cid]["committed"]
         out["_fallback"] = [int(x) for x in res["fallback_groups"]]
         return out
 
@@ -230,7 +242,8 @@ class WireBackend(WorkerBackend):
             assert int(off[i + 1]) - int(off[i]) == len(per_group[cid])
         assert sorted(handle_cid[int(h)] for h in grp) == sorted(c for c in cids
                                                                  if per_group[c])
-        if self.stream == "sized":
+        self.last_cids = [handle_cid[int(h)] for h in grp]
+        if str(self.stream).startswith("sized"):
             sizes = (np.diff(off) | (np.diff(boff) << np.uint64(16))).astype(np.uint32)
             return self.hq.SizedStream(grp, sizes, int(off[-1]), data), refs
         return ((grp, off, boff, data) if self.stream else (grp, off, ev)), refs

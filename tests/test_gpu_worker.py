@@ -18,8 +18,9 @@ MODES = [False, True]
 MODE_IDS = ["host", "device"]      # the host worker / HQ_WORKER_ON_DEVICE (hq_dstep.hip)
 # (on_device, stream): events as rows or as an event stream (hq_worker_step_stream)
 FEEDS = [(False, False), (True, False), (True, True), (False, True), (True, "sized"),
-         (False, "sized")]
-FEED_IDS = ["host", "device", "device-stream", "host-stream", "device-sized", "host-sized"]
+         (False, "sized"), (True, "sized-column")]
+FEED_IDS = ["host", "device", "device-stream", "host-stream", "device-sized", "host-sized",
+            "device-sized-column"]
 
 
 @pytest.fixture(scope="module", params=FEEDS, ids=FEED_IDS)
@@ -358,7 +359,8 @@ def test_step_jobs_equal_sequential_steps(hq):
             w.close()
 
 
-@pytest.mark.parametrize("stream", [True, False, "sized"], ids=["stream", "rows", "sized"])
+@pytest.mark.parametrize("stream", [True, False, "sized", "sized-column"],
+                         ids=["stream", "rows", "sized", "sized-column"])
 def test_chunked_device_step_equals_host_worker(hq, stream):
     """A step of >= 256 Ki groups runs in 4 chunks whose copies overlap the neighbouring chunks'
     passes (hq_dstep.hip); its lists equal the host worker's on the same events (the host
@@ -369,16 +371,26 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
     roles = bench.STEP_ROLES["step5"]
     g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
     nv = sum(r != "observer" for r in roles)
-    dev, host = hq.Worker(0, nv, on_device=True), hq.Worker(0, nv)
+    dev = hq.Worker(0, nv, on_device=True, commit_column=stream == "sized-column")
+    host = hq.Worker(0, nv)
     try:
         dev.add_groups(g, m)
         host.add_groups(g, m)
         for s in range(3):
             e = bench.step_events(hq, G, s, roles)
             want = host.step(*e)
-            if stream == "sized":      # byte chunks, each group's pass A in the chunk its
-                data, sizes = hq.encode_events_sized(e[1], e[2])   # bytes end in
+            if str(stream).startswith("sized"):   # byte chunks, each group's pass A in the
+                data, sizes = hq.encode_events_sized(e[1], e[2])   # chunk its bytes end in
                 got = dev.step_sized(e[0], sizes, len(e[2]), data)
+                if "committed_column" in got:     # every group commits from step 1 on
+                    assert s and stream == "sized-column" and got["n_commits"] == G
+                    want_col = np.zeros(G, np.uint64)
+                    want_col[want["commits"]["cluster_id"].astype(np.int64) - 1] = \
+                        want["commits"]["committed"]
+                    np.testing.assert_array_equal(got["committed_column"], want_col)
+                    got["commits"] = want["commits"]
+                else:
+                    assert not s or stream == "sized"
             elif stream:
                 data, boff = hq.encode_events(e[1], e[2])
                 got = dev.step_stream(e[0], e[1], boff, data)

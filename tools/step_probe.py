@@ -23,7 +23,8 @@ g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
 nm = len(roles)
 workers = []
 for i in range(W):
-    w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True)
+    w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True,
+                  commit_column=os.environ.get("COLUMN", "1") == "1")
     w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
     workers.append(w)
 pc = hq.Context(0)
