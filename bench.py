@@ -1301,7 +1301,7 @@ def main():
         progress(f"extra {name}")
         try:
             if name == "e2e":
-                e2e = run_e2e(max(20, args.steps // 20), 3, d)
+                e2e = run_e2e(max(100, args.steps // 4), 5, d)   # >= 30 ms timed per variant
             elif name == "wire":
                 steps_legs.append(run_wire_leg(d))
             elif name in STEP_ROLES:
