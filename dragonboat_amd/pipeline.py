@@ -22,9 +22,12 @@ fallback bitmap that ``results`` returns. The caller decides them with the CPU t
 
 With ``depth`` = 1 every step runs on one stream: the next step's host-to-device copies wait for
 the previous readback. With ``depth`` = 2 the steps alternate between two contexts; each step's
-kernels are ordered after the previous step (``hq_wait_for``), so the decisions are those of the
-serial run, while its copies overlap the previous step's kernels and readback (the copy engines
-run beside the compute queues; PCIe is full duplex). ``grouped``: the caller's records of one
+kernels are ordered after the previous step's kernels (``hq_wait_for``), so the decisions are
+those of the serial run, while its copies overlap the previous step's kernels and readback (the
+copy engines run beside the compute queues; PCIe is full duplex). The readback of a step runs on
+a context of its own, from result buffers of its own (one set per pipeline slot), so the next
+step's kernels need not wait for it: a slot's buffers are reused only after its readback of
+``depth`` steps earlier has finished. ``grouped``: the caller's records of one
 key are adjacent (node by node, as a step worker emits them), so the ingest kernels reduce runs
 in registers and write without atomics (HQ_INGEST_GROUPED). Every decision is a kernel of
 libhipquorum.so; nothing here computes.
@@ -56,14 +59,20 @@ class HostFedPipeline:
         self.layout = hq.HQ_LAYOUT_TILES_LEADER
         self.tiles = c0.empty(hq.commit_tiles(G) * hq.commit_tile_words(n, form, self.layout),
                               np.uint64)
-        self.changed = c0.empty(hq.words64(G), np.uint64)
-        self.fallback = c0.empty(hq.words64(G), np.uint64)
-        self.committed = c0.empty(G, np.uint64)
-        a = hq.CommitArgs()
-        a.G, a.n_max, a.form, a.ring_len = G, n, form, ring_len
-        a.layout = hq.HQ_LAYOUT_TILES_LEADER | hq.HQ_LAYOUT_IN_PLACE
-        a.match, a.changed, a.fallback = self.tiles.ptr, self.changed.ptr, self.fallback.ptr
-        self.args = a
+        # readback contexts (one stream per pipeline slot; the step's own with depth 1)
+        self.rbs = [hq.Context(device) for _ in range(depth)] if depth > 1 else self.ctxs
+        # per slot: the device result buffers the decision writes and the readback reads
+        self.changed = [c0.empty(hq.words64(G), np.uint64) for _ in range(depth)]
+        self.fallback = [c0.empty(hq.words64(G), np.uint64) for _ in range(depth)]
+        self.committed = [c0.empty(G, np.uint64) for _ in range(depth)]
+        self.args = []
+        for k in range(depth):
+            a = hq.CommitArgs()
+            a.G, a.n_max, a.form, a.ring_len = G, n, form, ring_len
+            a.layout = hq.HQ_LAYOUT_TILES_LEADER | hq.HQ_LAYOUT_IN_PLACE
+            a.match, a.changed, a.fallback = (self.tiles.ptr, self.changed[k].ptr,
+                                              self.fallback[k].ptr)
+            self.args.append(a)
         self.max_appends, self.max_updates = max_appends, max_updates
         # per context: device staging for the step's inputs, pinned buffers for its results
         self.dapp = [c.empty(w * max(1, max_appends), np.uint64) for c in self.ctxs]
@@ -132,8 +141,11 @@ class HostFedPipeline:
             x.h2d_async(self.dapp[k], appends[:w * n_appends])
         if n_updates:
             x.h2d_async(self.dupd[k], updates[:w * n_updates])
+        rb = self.rbs[k]
         if self._last is not None and self._last is not x:
-            x.wait_for(self._last)        # kernels after the previous step (and its readback)
+            x.wait_for(self._last)        # kernels after the previous step's kernels
+        if rb is not x:
+            x.wait_for(rb)                # slot k's result buffers read back (step i - depth)
         G, n, f = self.G, self.n, self.form
         if self.compact:
             if n_appends:
@@ -148,11 +160,13 @@ class HostFedPipeline:
             if n_updates:
                 x.table_ingest_match_dev(self.dupd[k], n_updates, self.tiles, G, n, f,
                                          self.flags)
-        x.commit_dev(self.args)
-        x.table_committed_dev(self.tiles, G, n, f, self.committed)
-        x.d2h_async(self.out_chg[k], self.changed)
-        x.d2h_async(self.out_fb[k], self.fallback)
-        x.d2h_async(self.out_com[k], self.committed)
+        x.commit_dev(self.args[k])
+        x.table_committed_dev(self.tiles, G, n, f, self.committed[k])
+        if rb is not x:
+            rb.wait_for(x)                # the readback after this step's kernels
+        rb.d2h_async(self.out_chg[k], self.changed[k])
+        rb.d2h_async(self.out_fb[k], self.fallback[k])
+        rb.d2h_async(self.out_com[k], self.committed[k])
         self._last = x
         return k
 
@@ -160,14 +174,18 @@ class HostFedPipeline:
         """(changed bitmap, committed column, fallback bitmap) of the last step that used
         result buffers k. Groups with a fallback bit were not decided (their committed index is
         the previous one): decide them on the CPU and write them back with set_committed."""
-        self.ctxs[k].sync()
+        self.rbs[k].sync()
         return self.out_chg[k], self.out_com[k], self.out_fb[k]
 
     def sync(self) -> None:
-        for c in self.ctxs:
+        for c in self.ctxs + (self.rbs if self.rbs is not self.ctxs else []):
             c.sync()
 
     def close(self) -> None:
+        self.sync()
+        if self.rbs is not self.ctxs:
+            for c in self.rbs:
+                c.close()
         for c in self.ctxs[1:]:
             c.close()
         self.ctxs[0].close()   # owns the table
