@@ -727,12 +727,15 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=5, variants=None):
     out = {}
     # the first pipeline of a process pays one-time costs (first touch of pinned staging, the
     # copy engines' first mappings): a throwaway run of the headline variant goes first
-    variants = variants or ((2, True, True), (2, True, True), (2, False, True), (2, True, False),
-                            (2, False, False), (1, False, False))
-    for depth, compact, grouped in variants:
+    variants = variants or ((2, True, True), (2, True, True), (2, True, True, True),
+                            (2, False, True), (2, True, False), (2, False, False),
+                            (1, False, False))
+    for v in variants:
+        depth, compact, grouped = v[:3]
+        zero_copy = len(v) > 3 and bool(v[3])
         r = np.random.default_rng(d.rank)
         p = HostFedPipeline(d.device, G, n, G // 4, G, depth=depth, compact=compact,
-                            grouped=grouped)
+                            grouped=grouped, zero_copy=zero_copy)
         p.synth(spec)
         last = hq.tile_view(p.ctxs[0].download(p.tiles), G, n, p.form,
                             p.layout).row("last_index")
@@ -766,7 +769,7 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=5, variants=None):
             p.step(i, apps[i % nb], G // 4, upds[i % nb], G)
         p.sync()
         d.barrier()
-        out[(depth, compact, grouped)] = d.max(time.perf_counter() - t0)
+        out[tuple(v)] = d.max(time.perf_counter() - t0)
         p.close()
 
     def pcie(w):   # H2D records + D2H changed / fallback bitmaps and committed column per step
@@ -787,7 +790,8 @@ def run_e2e(steps, warmup, d: Dist, G=1 << 20, n=5, variants=None):
     }
     if (2, True, True) in out:
         res.update(rec((2, True, True)))
-    for key, name in (((2, False, True), "records_16B_grouped_pipelined"),
+    for key, name in (((2, True, True, True), "records_8B_grouped_zero_copy"),
+                      ((2, False, True), "records_16B_grouped_pipelined"),
                       ((2, True, False), "records_8B_atomic_pipelined"),
                       ((2, False, False), "records_16B_atomic_pipelined"),
                       ((1, False, False), "records_16B_atomic_one_stream"),

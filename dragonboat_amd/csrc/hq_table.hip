@@ -245,39 +245,56 @@ __device__ __forceinline__ void apply_append(const TableK &t, uint64_t g, uint64
     if (t.mask) or_mask(t, g, append_bits(prev, n, t.R), atomic);
 }
 
-// COUNT = 0: hq_append_update (group, new_last); 1: 8-byte group << 32 | n
+// COUNT = 0: hq_append_update (group, new_last); 1: 8-byte group << 32 | n. Like the ingest, a
+// wave takes kIV chunks of 64 records and issues every record load before the first dependent
+// step (records read over PCIe from pinned host memory by the zero-copy pipeline would otherwise
+// cost one round trip per record and lane).
 template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kTBlock) void k_table_append(const uint64_t *u, uint64_t count,
                                                           TableK t, uint64_t *n_skipped) {
     constexpr bool GROUPED = MODE == kGrouped;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTBlock + threadIdx.x; i - threadIdx.x < count;
-         i += (uint64_t)gridDim.x * kTBlock) {
-        uint64_t key = ~0ull, v = 0;
-        bool ok = false;
-        if (i < count) {
-            if (COUNT) {
-                const uint64_t x = __builtin_nontemporal_load(u + i);
-                key = x >> 32;
-                v = x & 0xFFFFFFFFull;
-                ok = key < t.G && v != 0;
-            } else {
-                const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u + 2 * i));
-                key = x.x;
-                v = x.y;
-                ok = key < t.G;
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kTBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kTBlock / 64);
+    for (uint64_t base = wave * 64 * kIV; base < count; base += nwaves * 64 * kIV) {
+        uint64_t key[kIV], v[kIV];
+        bool in[kIV], ok[kIV];
+#pragma unroll
+        for (int c = 0; c < kIV; ++c) {
+            const uint64_t i = base + 64 * c + lane;
+            in[c] = i < count;
+            key[c] = ~0ull;
+            v[c] = 0;
+            ok[c] = false;
+            if (in[c]) {
+                if (COUNT) {
+                    const uint64_t x = __builtin_nontemporal_load(u + i);
+                    key[c] = x >> 32;
+                    v[c] = x & 0xFFFFFFFFull;
+                    ok[c] = key[c] < t.G && v[c] != 0;
+                } else {
+                    const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u + 2 * i));
+                    key[c] = x.x;
+                    v[c] = x.y;
+                    ok[c] = key[c] < t.G;
+                }
             }
         }
-        if constexpr (GROUPED) {
-            // a skipped record keeps its key but adds nothing (0 is the sum's and max's identity)
-            const bool keyok = key < t.G;
-            if (!ok) v = 0;
-            v = seg_scan<COUNT>(key, v);
-            const RunTail r = run_tail(key);
-            if (keyok && r.tail && v) apply_append<COUNT>(t, key, v, r.edge);
-        } else {
-            if (ok) apply_append<COUNT>(t, key, v, MODE == kAtomic);   // unique: plain
+#pragma unroll
+        for (int c = 0; c < kIV; ++c) {
+            if constexpr (GROUPED) {
+                // a skipped record keeps its key but adds nothing (0 is the sum's and max's
+                // identity); a run crossing a chunk edge is applied atomically like one crossing
+                // a wave edge
+                const bool keyok = key[c] < t.G;
+                const uint64_t x = seg_scan<COUNT>(key[c], ok[c] ? v[c] : 0);
+                const RunTail r = run_tail(key[c]);
+                if (keyok && r.tail && x) apply_append<COUNT>(t, key[c], x, r.edge);
+            } else {
+                if (ok[c]) apply_append<COUNT>(t, key[c], v[c], MODE == kAtomic);   // unique: plain
+            }
+            count_skip(n_skipped, in[c] && !ok[c]);
         }
-        count_skip(n_skipped, i < count && !ok);
     }
 }
 
@@ -386,7 +403,7 @@ static int table_append(hq_ctx *ctx, const char *what, const uint64_t *updates, 
     if ((rc = hq::pre_launch(ctx))) return rc;
     const int mode = (flags & HQ_INGEST_UNIQUE) ? kUnique : (flags & HQ_INGEST_GROUPED) ? kGrouped
                                                                                          : kAtomic;
-    const dim3 grid(tgrid(count)), blk(kTBlock);
+    const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
 #define HQ_APPEND(C, M) \
     hipLaunchKernelGGL((k_table_append<C, M>), grid, blk, 0, ctx->stream, updates, count, t, n_skipped)
     if (counts) {

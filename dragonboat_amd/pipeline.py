@@ -42,25 +42,35 @@ from . import hipquorum as hq
 class HostFedPipeline:
     def __init__(self, device: int, G: int, n: int, max_appends: int, max_updates: int,
                  depth: int = 2, ring_len: int = 16, compact: bool = False,
-                 form: int = hq.HQ_FORM_TERM_MASK, grouped: bool = False):
+                 form: int = hq.HQ_FORM_TERM_MASK, grouped: bool = False,
+                 zero_copy: bool = False):
         """compact: 8-byte records (hq_table_append_count_dev: group << 32 | entries;
         hq_table_ingest_lag_dev: group << 32 | slot << 28 | lastIndex - index) instead of the
-        16-byte hq_append_update / hq_match_update pairs — half the PCIe bytes per step."""
+        16-byte hq_append_update / hq_match_update pairs — half the PCIe bytes per step.
+        zero_copy: no copies at all — the append / ingest kernels read the caller's pinned records
+        over PCIe and the decision writes the changed / fallback bitmaps, and a second stream's
+        extraction the committed column, straight into this slot's pinned result buffers
+        (``depth`` result slots); the extraction's PCIe writes overlap the next step's appends and
+        ingests, no copy engine is involved."""
         if depth < 1:
             raise ValueError("depth must be >= 1")
+        self.zero_copy = zero_copy
         if form not in (hq.HQ_FORM_TERM_MASK, hq.HQ_FORM_TERM_START):
             raise ValueError("the table holds the term-mask or term-start form")
         self.G, self.n, self.R, self.depth, self.form = G, n, ring_len, depth, form
         self.compact = compact
         self.flags = hq.HQ_INGEST_GROUPED if grouped else 0
         w = 1 if compact else 2     # uint64 words per record
-        self.ctxs = [hq.Context(device) for _ in range(depth)]
+        # zero_copy: one stream for the appends, ingests and decisions, one for the committed
+        # column's extraction (its PCIe writes overlap the next step's PCIe reads)
+        self.ctxs = [hq.Context(device) for _ in range(2 if zero_copy else depth)]
         c0 = self.ctxs[0]
         self.layout = hq.HQ_LAYOUT_TILES_LEADER
         self.tiles = c0.empty(hq.commit_tiles(G) * hq.commit_tile_words(n, form, self.layout),
                               np.uint64)
         # readback contexts (one stream per pipeline slot; the step's own with depth 1)
-        self.rbs = [hq.Context(device) for _ in range(depth)] if depth > 1 else self.ctxs
+        self.rbs = [hq.Context(device) for _ in range(depth)] \
+            if depth > 1 and not zero_copy else self.ctxs
         # per slot: the device result buffers the decision writes and the readback reads
         self.changed = [c0.empty(hq.words64(G), np.uint64) for _ in range(depth)]
         self.fallback = [c0.empty(hq.words64(G), np.uint64) for _ in range(depth)]
@@ -74,12 +84,16 @@ class HostFedPipeline:
                                               self.fallback[k].ptr)
             self.args.append(a)
         self.max_appends, self.max_updates = max_appends, max_updates
-        # per context: device staging for the step's inputs, pinned buffers for its results
+        # per context: device staging for the step's inputs; per slot: pinned result buffers
         self.dapp = [c.empty(w * max(1, max_appends), np.uint64) for c in self.ctxs]
         self.dupd = [c.empty(w * max(1, max_updates), np.uint64) for c in self.ctxs]
-        self.out_chg = [c.pinned(hq.words64(G), np.uint64) for c in self.ctxs]
-        self.out_fb = [c.pinned(hq.words64(G), np.uint64) for c in self.ctxs]
-        self.out_com = [c.pinned(G, np.uint64) for c in self.ctxs]
+        self.out_chg = [c0.pinned(hq.words64(G), np.uint64) for _ in range(depth)]
+        self.out_fb = [c0.pinned(hq.words64(G), np.uint64) for _ in range(depth)]
+        self.out_com = [c0.pinned(G, np.uint64) for _ in range(depth)]
+        if zero_copy:   # the decision writes the results where the caller reads them
+            for k, a in enumerate(self.args):
+                a.changed = self.out_chg[k].ctypes.data
+                a.fallback = self.out_fb[k].ctypes.data
         self._last = None
 
     # -- setup ----------------------------------------------------------------------------
@@ -136,6 +150,29 @@ class HostFedPipeline:
             raise ValueError("step larger than the staging buffers")
         w = 1 if self.compact else 2
         k = i % self.depth
+        G, n, f = self.G, self.n, self.form
+        if self.zero_copy:
+            x = self.ctxs[0]
+            app, upd = appends[:w * n_appends], updates[:w * n_updates]
+            if self.compact:
+                if n_appends:
+                    x.table_append_count_dev(app, n_appends, self.tiles, G, n, f, self.R,
+                                             self.flags)
+                if n_updates:
+                    x.table_ingest_lag_dev(upd, n_updates, self.tiles, G, n, f, self.flags)
+            else:
+                if n_appends:
+                    x.table_append_dev(app, n_appends, self.tiles, G, n, f, self.R, self.flags)
+                if n_updates:
+                    x.table_ingest_match_dev(upd, n_updates, self.tiles, G, n, f, self.flags)
+            e = self.ctxs[1]
+            if self._last is not None:
+                x.wait_for(e)             # the previous committed row read out before this
+            x.commit_dev(self.args[k])    # decision rewrites it
+            e.wait_for(x)
+            e.table_committed_dev(self.tiles, G, n, f, self.out_com[k])
+            self._last = x
+            return k
         x = self.ctxs[k]
         if n_appends:
             x.h2d_async(self.dapp[k], appends[:w * n_appends])
@@ -146,7 +183,6 @@ class HostFedPipeline:
             x.wait_for(self._last)        # kernels after the previous step's kernels
         if rb is not x:
             x.wait_for(rb)                # slot k's result buffers read back (step i - depth)
-        G, n, f = self.G, self.n, self.form
         if self.compact:
             if n_appends:
                 x.table_append_count_dev(self.dapp[k], n_appends, self.tiles, G, n, f, self.R,
@@ -174,7 +210,10 @@ class HostFedPipeline:
         """(changed bitmap, committed column, fallback bitmap) of the last step that used
         result buffers k. Groups with a fallback bit were not decided (their committed index is
         the previous one): decide them on the CPU and write them back with set_committed."""
-        self.rbs[k].sync()
+        if self.zero_copy:
+            self.sync()
+        else:
+            self.rbs[k].sync()
         return self.out_chg[k], self.out_com[k], self.out_fb[k]
 
     def sync(self) -> None:

@@ -204,12 +204,17 @@ def test_table_validation(gpu_ctx, hq):
     gpu_ctx.free(u)
 
 
-@pytest.mark.parametrize("depth,compact,grouped", [(1, False, False), (2, False, True),
-                                                   (3, False, False), (1, True, True),
-                                                   (2, True, False), (2, True, True)])
-def test_host_fed_pipeline_matches_oracle(hq, depth, compact, grouped):
+@pytest.mark.parametrize("depth,compact,grouped,zero_copy",
+                         [(1, False, False, False), (2, False, True, False),
+                          (3, False, False, False), (1, True, True, False),
+                          (2, True, False, False), (2, True, True, False),
+                          (2, True, True, True), (1, False, False, True),
+                          (3, True, False, True)])
+def test_host_fed_pipeline_matches_oracle(hq, depth, compact, grouped, zero_copy):
     """dragonboat_amd.pipeline over the leader-row tile table: host-fed steps (pinned appends +
-    match deltas -> append, ingest, commit in place -> readback) over `depth` contexts. Every
+    match deltas -> append, ingest, commit in place -> readback) over `depth` contexts, or with
+    no copies at all (zero_copy: the kernels read the pinned records and write the pinned results
+    over PCIe). Every
     step's read-back changed / fallback bitmaps and committed column equal the oracle's
     sequential run, whatever the pipelining and the ingest path."""
     from dragonboat_amd.pipeline import HostFedPipeline
@@ -220,7 +225,7 @@ def test_host_fed_pipeline_matches_oracle(hq, depth, compact, grouped):
     host = dict(match=inp.match.copy(), last=inp.last_index.copy(), mask=inp.term_mask.copy(),
                 committed=inp.committed_in.copy())
     p = HostFedPipeline(0, G, n, G // 2, G, depth=depth, ring_len=R, compact=compact,
-                        grouped=grouped)
+                        grouped=grouped, zero_copy=zero_copy)
     p.upload(host["match"], host["committed"], host["last"], host["mask"])
     want, slots = [], []
     for step in range(T):
@@ -248,9 +253,9 @@ def test_host_fed_pipeline_matches_oracle(hq, depth, compact, grouped):
         want.append((wchg, out, wfb))
         wire_app = hq.pack_append_counts(gsel, counts) if compact else app.reshape(-1)
         wire_upd = hq.pack_lag_updates(g, s, lag) if compact else upd.reshape(-1)
-        pa = p.ctxs[step % depth].pinned(wire_app.size, np.uint64)
+        pa = p.ctxs[step % len(p.ctxs)].pinned(wire_app.size, np.uint64)
         pa[:] = wire_app
-        pu = p.ctxs[step % depth].pinned(wire_upd.size, np.uint64)
+        pu = p.ctxs[step % len(p.ctxs)].pinned(wire_upd.size, np.uint64)
         pu[:] = wire_upd
         slots.append(p.step(step, pa, len(app), pu, G))
         if step % depth == depth - 1 or step == T - 1:
