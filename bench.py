@@ -1020,6 +1020,9 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
             "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
             "ms_per_step": elapsed / steps * 1e3,
             "step_ms": acc["step_ms"],
+            # the copy-engine paths see occasional multi-ms idle gaps on these boxes:
+            # the median step beside the mean
+            "median_ms_per_step": float(np.median(acc["step_ms"])) if acc["step_ms"] else None,
             "gpu_passes_per_step": acc["gpu_passes"] / steps / W,
             "host_ms_per_step_per_worker": acc["handle_ns"] / steps / W / 1e6,
             "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
