@@ -14,6 +14,14 @@
  *   hq_vote*          handleVoteResp / handleCandidateRequestVoteResp
  *                                                           internal/raft/raft.go:1062-1080,1968-1985
  *   hq_check_quorum*  leaderHasQuorum                       internal/raft/raft.go:380-390
+ *   hq_readindex_multi*  readIndex.confirm prefix release   internal/raft/readindex.go:77-116
+ *   hq_table_*        remote.tryUpdate, appendEntries       internal/raft/remote.go:123-133
+ *                     (a device-resident progress table)    internal/raft/raft.go:911-922
+ *   hq_worker_*       execEngine.processSteps ->            internal/execengine.go:923-1000
+ *                     node.handleEvents -> raft.Handle      internal/node.go:1113-1157
+ *   hq_events_*       the step worker's compact event stream (no reference counterpart)
+ *   hq_wire_*         Transport.handleRequest,              internal/transport/transport.go:289-300
+ *                     HandleMessageBatch, MessageBatch      nodehost.go:2021-2061, raftpb/raft.proto:154-203
  *
  * The reference has no plugin/FFI for this path (the quorum code lives in unexported methods of
  * the unexported raft struct, raft.go:198). The cgo binding a maintainer adds under
