@@ -1004,9 +1004,12 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
                               "prefix arrays (hq_worker_step_stream)",
              "device_rows": "device worker, events as 56-byte hq_event rows (hq_worker_step)",
              "host": "host worker (events on the host, decisions in GPU passes), rows"}
-    for mode, W in (("device_sized", 1), ("device_sized", 2), ("device_sized", T),
-                    ("device_stream", 1), ("device_stream", T), ("device_rows", 1), ("device_rows", T), ("host", 1),
-                    ("host", T)):
+    all_modes = (("device_sized", 1), ("device_sized", 2), ("device_sized", T),
+                 ("device_stream", 1), ("device_stream", T), ("device_rows", 1),
+                 ("device_rows", T), ("host", 1), ("host", T))
+    # with several ranks (a node's GPUs, each with its own share) only the device engine's modes
+    # run: the comparison modes are host-bound and would share the node's cores
+    for mode, W in all_modes if d.world == 1 else all_modes[:3]:
         if d.rank == 0:
             log(f"  step leg {name}: {mode}, {W} worker(s)")
         t, ne, acc, committed[mode], gm, t_enc = _run_workers(
