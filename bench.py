@@ -931,8 +931,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
                 for dst, src in zip(pinned[i], e):
                     dst[:src.size] = src
             evs = [tuple(p[k][:e[k].size] for k in range(len(e))) for p, e in zip(pinned, evs)]
-        if stream == "sized":
-            evs = [hq.SizedStream(e[0], e[1], ne, e[2]) for e, ne in zip(evs, n_ev)]
+        if stream == "sized":   # every group in handle order: the handles stay implicit
+            evs = [hq.SizedStream(None, e[1], ne, e[2]) for e, ne in zip(evs, n_ev)]
         # the W workers stepped at once on native threads (hq_worker_step_jobs), as W step-
         # worker goroutines each calling its own worker
         jobs = hq.StepJobs(list(zip(workers, evs)))

@@ -493,7 +493,7 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
             b1 = a.boffsets[i + 1];
         }
     }
-    const uint32_t h = a.handles[i];
+    const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;   // NULL: handles 0 .. n - 1
     if (!WRITE) {                 // validate this group's entry; a bad one is not stepped
         uint32_t err = 0;
         if (h >= a.n_handles) err |= kErrHandle;
@@ -806,7 +806,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.members = d->members;
     k.reads = d->reads;
     k.n = n;
-    k.handles = reinterpret_cast<const uint32_t *>(din);
+    k.handles = sized && !in->groups ? nullptr : reinterpret_cast<const uint32_t *>(din);
     k.offsets = reinterpret_cast<const uint64_t *>(din + o_off);
     if (sized) {
         k.prefix = prefix;
@@ -858,7 +858,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         // handles and sizes (+ a zero: the scan's last element is the totals), their scan; then
         // the bytes in equal byte chunks, each followed by pass A over the groups whose bytes end
         // inside what has landed
-        h2d(0, in->groups, n * 4);
+        if (in->groups) h2d(0, in->groups, n * 4);   // NULL: the step lists handles 0 .. n - 1
         h2d(o_off, in->sizes, n * 4);
         if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(din + o_off + n * 4, 0, 4, cs), "memset");
         if (chunks > 1) {

@@ -101,6 +101,7 @@ struct hq_worker {
     hq_dstep_out dout{};
     std::vector<hq_event> decoded;        // host worker: a stream step's rows
     std::vector<uint64_t> sized_off, sized_boff;   // host worker: a sized stream's prefixes
+    std::vector<uint32_t> sized_groups;            // and its implicit handles
     std::string err;
     std::vector<Group> groups;
     std::vector<Member> pool;
@@ -1085,8 +1086,8 @@ int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output
     if (in->sizes || (in->n_groups && !in->offsets && !in->boffsets)) {
         // the sized form: the device engine scans the sizes; a host worker (or a check) makes
         // the prefix arrays here
-        if (in->n_groups && (!in->groups || !in->sizes))
-            return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL groups/sizes");
+        if (in->n_groups && !in->sizes)
+            return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL sizes");
         if (in->n_bytes && !in->bytes)
             return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL bytes");
         std::memset(out, 0, sizeof *out);
@@ -1099,6 +1100,12 @@ int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output
             d.n_bytes = in->n_bytes;
             return w->step_on_device(d, out);
         }
+        const uint32_t *groups = in->groups;
+        if (!groups) {                    // the step lists handles 0 .. n_groups - 1
+            w->sized_groups.resize(in->n_groups);
+            for (uint64_t i = 0; i < in->n_groups; ++i) w->sized_groups[i] = (uint32_t)i;
+            groups = w->sized_groups.data();
+        }
         w->sized_off.resize(in->n_groups + 1);
         w->sized_boff.resize(in->n_groups + 1);
         w->sized_off[0] = w->sized_boff[0] = 0;
@@ -1108,7 +1115,7 @@ int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output
         }
         if (w->sized_off[in->n_groups] != in->n_events || w->sized_boff[in->n_groups] != in->n_bytes)
             return w->fail(HQ_E_INVAL, "hq_worker_step_stream: sizes do not sum to the totals");
-        const hq_step_stream full{in->n_groups, in->groups, w->sized_off.data(),
+        const hq_step_stream full{in->n_groups, groups, w->sized_off.data(),
                                   w->sized_boff.data(), in->bytes ? in->bytes : &none,
                                   nullptr, 0, 0};
         return hq_worker_step_stream(w, &full, out);

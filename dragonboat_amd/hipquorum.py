@@ -1287,7 +1287,7 @@ class Worker:
         self._check(lib.hq_worker_step_stream(self.h, ctypes.byref(inp), ctypes.byref(out)),
                     "hq_worker_step_stream")
         del keep
-        return self._results(out, copy, len(groups))
+        return self._results(out, copy, len(sizes))
 
     @staticmethod
     def _results(out, copy, n_listed=0):
@@ -1358,7 +1358,8 @@ class StepJobs:
             msg = lib.hq_worker_last_error(self.jobs[bad[0]][0].h).decode() if bad \
                 else "a worker listed twice"
             raise HQError(rc, f"hq_worker_step_jobs: {msg}")
-        return [Worker._results(o, copy, len(a[0])) for o, (_, a) in zip(self.outs, self.jobs)]
+        return [Worker._results(o, copy, len(a[1]) if isinstance(a, SizedStream) else len(a[0]))
+                for o, (_, a) in zip(self.outs, self.jobs)]
 
 
 def step_jobs(jobs, copy=True):
@@ -1380,11 +1381,12 @@ def encode_events(offsets, events):
 
 
 def _sized_input(groups, sizes, n_events, data):
-    g = np.ascontiguousarray(groups, np.uint32)
+    """groups None: the step lists the worker's handles 0 .. len(sizes) - 1."""
     z = np.ascontiguousarray(sizes, np.uint32)
+    g = None if groups is None else np.ascontiguousarray(groups, np.uint32)
     d = np.ascontiguousarray(data, np.uint8)
-    assert len(g) == len(z)
-    inp = StepStream(len(g), _p(g), None, None, _p(d) if len(d) else None, _p(z),
+    assert g is None or len(g) == len(z)
+    inp = StepStream(len(z), _p(g), None, None, _p(d) if len(d) else None, _p(z),
                      int(n_events), len(d))
     return inp, [g, z, d]
 

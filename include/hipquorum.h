@@ -919,7 +919,9 @@ typedef struct hq_step_stream {
     /* Sized form (sizes != NULL; offsets / boffsets are then not read): per group one word,
      * events | bytes << 16 (each < 2^16), and the totals over the step — 4 bytes per group
      * cross PCIe instead of the 16 of the two prefix arrays, and the device engine scans them.
-     * Event indexes (deferred) count from 0 in group order as with offsets[0] = 0. */
+     * Event indexes (deferred) count from 0 in group order as with offsets[0] = 0. In this form
+     * `groups` may be NULL: the step lists the handles 0 .. n_groups - 1 in order (a worker
+     * that steps all its groups every time; a group without events has size 0). */
     const uint32_t *sizes;
     uint64_t n_events, n_bytes;
 } hq_step_stream;

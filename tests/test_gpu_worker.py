@@ -311,6 +311,37 @@ def test_sized_input_errors_leave_state(hq, on_device):
         w.close()
 
 
+@pytest.mark.parametrize("on_device", MODES, ids=MODE_IDS)
+def test_sized_stream_implicit_handles(hq, on_device):
+    """The sized form with groups NULL lists handles 0 .. n - 1: the same results and state as
+    the explicit list (step workload, 3 steps, every group committing from step 1 on)."""
+    import bench
+
+    G = 5000
+    roles = bench.STEP_ROLES["step5"]
+    g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
+    nv = sum(r != "observer" for r in roles)
+    a, b = hq.Worker(0, nv, on_device=on_device), hq.Worker(0, nv, on_device=on_device)
+    try:
+        a.add_groups(g, m)
+        b.add_groups(g, m)
+        for s in range(3):
+            grp, off, ev = bench.step_events(hq, G, s, roles)
+            data, sizes = hq.encode_events_sized(off, ev)
+            got = a.step_sized(None, sizes, len(ev), data)
+            want = b.step_sized(grp, sizes, len(ev), data)
+            for k in ("commits", "ready", "read_resps", "state_changes", "dropped_reads",
+                      "deferred", "fallback_groups"):
+                np.testing.assert_array_equal(got[k], want[k], err_msg=f"step {s} {k}")
+            assert len(got["commits"]) == (G if s else 0)
+        assert a.get_group(G)[0]["committed"] == b.get_group(G)[0]["committed"]
+        with pytest.raises(hq.HQError):                  # more sizes than groups on the worker
+            a.step_sized(None, np.zeros(G + 1, np.uint32), 0, np.zeros(0, np.uint8))
+    finally:
+        a.close()
+        b.close()
+
+
 def test_step_jobs_equal_sequential_steps(hq):
     """hq_worker_step_jobs: several workers (device and host, rows and streams) stepped at once
     on native threads end in the same results and state as stepping them one by one."""
