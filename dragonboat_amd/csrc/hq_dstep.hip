@@ -740,6 +740,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const uint64_t nb = !n || !stream ? 0 : sized ? in->n_bytes : in->boffsets[n];
     *out = hq_dstep_out{};
     if (n == 0) return HQ_OK;
+    if (sized && (ne >> 32 || nb >> 32))     // the scanned prefixes pack both totals in 64 bits
+        return hq::fail(ctx, HQ_E_INVAL, "hq_dstep: a sized step holds < 2^32 events and bytes");
     const uint64_t t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     // chunks of groups (at least 64 Ki each): chunk c's input copy overlaps pass A of chunk c - 1
