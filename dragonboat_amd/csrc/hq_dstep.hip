@@ -112,8 +112,10 @@ __device__ __forceinline__ bool dvar(ByteReader &r, uint64_t &v) {
     return false;
 }
 
-// one event of a group's stream; term: the group's previous message term in the stream
-__device__ bool decode_event(ByteReader &r, uint64_t &term, hq_event &v) {
+// one event of a group's stream; term: the group's previous message term in the stream; index /
+// have_index: its previous ReplicateResp's log_index (type code 4 repeats it)
+__device__ bool decode_event(ByteReader &r, uint64_t &term, uint64_t &index, bool &have_index,
+                             hq_event &v) {
     v = hq_event{};
     if (!r.more()) return false;
     const uint32_t h = r.next();
@@ -122,16 +124,24 @@ __device__ bool decode_event(ByteReader &r, uint64_t &term, hq_event &v) {
     if (v.kind == HQ_EV_PROPOSE) return dvar(r, v.log_index);
     if (v.kind != HQ_EV_MESSAGE) return true;
     const uint32_t code = (h >> 3) & 7;
-    uint64_t t = code == 0 ? HQ_MSG_REPLICATE_RESP : code == 1 ? HQ_MSG_REQUEST_VOTE_RESP
+    uint64_t t = code == 0 || code == 4 ? HQ_MSG_REPLICATE_RESP
+               : code == 1 ? HQ_MSG_REQUEST_VOTE_RESP
                : code == 2 ? HQ_MSG_HEARTBEAT_RESP : code == 3 ? HQ_MSG_READ_INDEX : 0;
     if (code == 7 && !dvar(r, t)) return false;
+    if (code == 4 && !have_index) return false;     // repeats an index the group has not sent
     v.type = (uint32_t)t;
     v.reject = (h >> 6) & 1;
     if (!dvar(r, v.from)) return false;
     if (!(h & 0x80) && !dvar(r, term)) return false;
     v.term = term;
     if ((code == 0 || code == 7) && !dvar(r, v.log_index)) return false;
-    if (code >= 2 && !(dvar(r, v.hint) && dvar(r, v.hint_high))) return false;
+    if (code == 4) v.log_index = index;
+    if ((code == 2 || code == 3 || code == 7) && !(dvar(r, v.hint) && dvar(r, v.hint_high)))
+        return false;
+    if (code == 0 || code == 4) {
+        index = v.log_index;
+        have_index = true;
+    }
     return true;
 }
 
@@ -413,7 +423,8 @@ struct Engine {
     template <bool STREAM>
     __device__ __forceinline__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
         const uint64_t committed0 = g.committed;
-        uint64_t term = 0;
+        uint64_t term = 0, index = 0;
+        bool have_index = false;
         ByteReader br{p, end};
         for (uint64_t e = e0; e < e1; ++e) {
             if (g.flags & kDSuspended) {
@@ -423,7 +434,7 @@ struct Engine {
             bool ok;
             if (STREAM) {
                 hq_event ev;
-                ok = decode_event(br, term, ev) && handle(ev, e);
+                ok = decode_event(br, term, index, have_index, ev) && handle(ev, e);
             } else {
                 const hq_event ev = a.events[e];
                 ok = handle(ev, e);

@@ -23,9 +23,10 @@ inline uint32_t type_code(uint32_t t) {
     }
 }
 inline uint32_t code_type(uint32_t c) {
-    static const uint32_t t[4] = {HQ_MSG_REPLICATE_RESP, HQ_MSG_REQUEST_VOTE_RESP,
-                                  HQ_MSG_HEARTBEAT_RESP, HQ_MSG_READ_INDEX};
-    return c < 4 ? t[c] : 0;
+    static const uint32_t t[5] = {HQ_MSG_REPLICATE_RESP, HQ_MSG_REQUEST_VOTE_RESP,
+                                  HQ_MSG_HEARTBEAT_RESP, HQ_MSG_READ_INDEX,
+                                  HQ_MSG_REPLICATE_RESP};
+    return c < 5 ? t[c] : 0;
 }
 
 inline uint8_t *put(uint8_t *p, uint64_t v) {
@@ -48,8 +49,10 @@ inline bool get(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
     return false;
 }
 
-// one event; returns the write position. term_prev: the group's previous message term
-inline uint8_t *encode(uint8_t *p, const hq_event &e, uint64_t &term_prev) {
+// one event; returns the write position. term_prev: the group's previous message term;
+// index_prev / have_index: its previous ReplicateResp's log_index (code 4 repeats it)
+inline uint8_t *encode(uint8_t *p, const hq_event &e, uint64_t &term_prev, uint64_t &index_prev,
+                       bool &have_index) {
     const uint32_t kind = e.kind >= 1 && e.kind <= 5 ? e.kind : 0;   // 0: not a valid kind
     if (kind != HQ_EV_MESSAGE) {
         *p++ = (uint8_t)kind;
@@ -61,7 +64,12 @@ inline uint8_t *encode(uint8_t *p, const hq_event &e, uint64_t &term_prev) {
         }
         return p;
     }
-    const uint32_t code = type_code(e.type);
+    uint32_t code = type_code(e.type);
+    if (code == 0) {
+        if (have_index && e.log_index == index_prev) code = 4;
+        index_prev = e.log_index;
+        have_index = true;
+    }
     const bool same = e.term == term_prev;
     *p++ = (uint8_t)(HQ_EV_MESSAGE | code << 3 | (e.reject ? 0x40 : 0) | (same ? 0x80 : 0));
     if (code == 7) p = put(p, e.type);
@@ -69,7 +77,7 @@ inline uint8_t *encode(uint8_t *p, const hq_event &e, uint64_t &term_prev) {
     if (!same) p = put(p, e.term);
     term_prev = e.term;
     if (code == 0 || code == 7) p = put(p, e.log_index);
-    if (code >= 2) {
+    if (code == 2 || code == 3 || code == 7) {
         p = put(p, e.hint);
         p = put(p, e.hint_high);
     }
@@ -87,10 +95,11 @@ int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event 
     uint8_t *p = out, *const end = out ? out + cap : nullptr;
     boffsets[0] = 0;
     for (uint64_t i = 0; i < n_groups; ++i) {
-        uint64_t term_prev = 0;
+        uint64_t term_prev = 0, index_prev = 0;
+        bool have_index = false;
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
-            p = encode(p, events[e], term_prev);
+            p = encode(p, events[e], term_prev, index_prev, have_index);
         }
         boffsets[i + 1] = (uint64_t)(p - out);
     }
@@ -105,10 +114,11 @@ int hq_events_encode_sized(uint64_t n_groups, const uint64_t *offsets, const hq_
     for (uint64_t i = 0; i < n_groups; ++i) {
         if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 0xFFFF) return HQ_E_INVAL;
         uint8_t *const g0 = p;
-        uint64_t term_prev = 0;
+        uint64_t term_prev = 0, index_prev = 0;
+        bool have_index = false;
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
-            p = encode(p, events[e], term_prev);
+            p = encode(p, events[e], term_prev, index_prev, have_index);
         }
         if (p - g0 > 0xFFFF) return HQ_E_INVAL;
         sizes[i] = (uint32_t)(offsets[i + 1] - offsets[i]) | (uint32_t)(p - g0) << 16;
@@ -122,7 +132,8 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
     if (!offsets || !boffsets || !events) return HQ_E_INVAL;
     for (uint64_t i = 0; i < n_groups; ++i) {
         const uint8_t *p = bytes + boffsets[i], *const end = bytes + boffsets[i + 1];
-        uint64_t term_prev = 0;
+        uint64_t term_prev = 0, index_prev = 0;
+        bool have_index = false;
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             hq_event &v = events[e];
             std::memset(&v, 0, sizeof v);
@@ -138,13 +149,20 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
                 const uint32_t code = (h >> 3) & 7;
                 uint64_t t = code_type(code);
                 if (code == 7) ok = get(p, end, t);
+                if (code == 4) ok = have_index;     // repeats an index the group has not sent
                 v.type = (uint32_t)t;
                 v.reject = (h >> 6) & 1;
                 ok = ok && get(p, end, v.from);
                 if (ok && !(h & 0x80)) ok = get(p, end, term_prev);
                 v.term = term_prev;
                 if (ok && (code == 0 || code == 7)) ok = get(p, end, v.log_index);
-                if (ok && code >= 2) ok = get(p, end, v.hint) && get(p, end, v.hint_high);
+                if (code == 4) v.log_index = index_prev;
+                if (ok && (code == 2 || code == 3 || code == 7))
+                    ok = get(p, end, v.hint) && get(p, end, v.hint_high);
+                if (ok && v.type == HQ_MSG_REPLICATE_RESP && code != 7) {
+                    index_prev = v.log_index;
+                    have_index = true;
+                }
             }
             if (!ok) return HQ_E_INVAL;
         }

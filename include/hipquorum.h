@@ -898,7 +898,10 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
  *
  *   header  bits 0-2  kind (HQ_EV_*; 0, 6, 7: not a valid kind -> the group falls back)
  *           bits 3-5  HQ_EV_MESSAGE: type code 0 ReplicateResp, 1 RequestVoteResp,
- *                     2 HeartbeatResp, 3 ReadIndex, 7 another type (its varint follows)
+ *                     2 HeartbeatResp, 3 ReadIndex, 4 ReplicateResp whose log_index repeats
+ *                     the group's previous ReplicateResp in the stream (its varint left out:
+ *                     the followers of a steady leader ack the same index), 7 another type
+ *                     (its varint follows)
  *           bit 6     reject
  *           bit 7     term repeats the group's previous message term in the stream (0 before
  *                     its first message): the term varint is left out

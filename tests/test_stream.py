@@ -147,3 +147,30 @@ def test_sized_encoding_limits(hq):
     big["kind"], big["hint"], big["hint_high"] = hq.EV_READ, 1 << 40, 1 << 30
     with pytest.raises(hq.HQError):
         hq.encode_events_sized(np.array([0, 9000], np.uint64), big)
+
+
+def test_repeated_replicate_index(hq):
+    """Type code 4: a ReplicateResp whose log_index repeats the group's previous ReplicateResp
+    (the followers of a steady leader ack the same index) leaves its index varint out; the
+    decoder restores it, per group; a code 4 before any ReplicateResp of the group is malformed."""
+    ev = np.zeros(5, hq.EVENT_DTYPE)
+    ev[0] = (hq.EV_MESSAGE, RREP, 2, 41, 1_000_000, 0, 0, 0, 0)   # 1 + 1 + 1 + 3
+    ev[1] = (hq.EV_MESSAGE, RREP, 3, 41, 1_000_000, 0, 0, 0, 0)   # 1 + 1: code 4
+    ev[2] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 0, 0, 0, 0)         # 1 + 1 + 1 + 1
+    ev[3] = (hq.EV_MESSAGE, RREP, 4, 41, 1_000_000, 0, 0, 1, 0)   # rejected, same index: code 4
+    ev[4] = (hq.EV_MESSAGE, RREP, 5, 41, 999, 0, 0, 0, 0)         # another index: code 0
+    off = np.array([0, 5], np.uint64)
+    data, boff = hq.encode_events(off, ev)
+    assert len(data) == 6 + 2 + 4 + 2 + (1 + 1 + 2)
+    assert (data[6] >> 3) & 7 == 4 and (data[12] >> 3) & 7 == 4
+    back = hq.decode_events(off, boff, data)
+    want = carried(hq, ev)
+    for k in ("kind", "type", "from", "term", "log_index", "hint", "hint_high", "reject"):
+        np.testing.assert_array_equal(back[k], want[k], err_msg=k)
+    # per group: the second group's first ReplicateResp is written in full
+    off2 = np.array([0, 1, 2], np.uint64)
+    d2, b2 = hq.encode_events(off2, ev[:2])
+    assert int(b2[1]) == 6 and int(b2[2]) == 12
+    bad = np.array([hq.EV_MESSAGE | 4 << 3 | 0x80, 2], np.uint8)
+    with pytest.raises(hq.HQError):
+        hq.decode_events(np.array([0, 1], np.uint64), np.array([0, 2], np.uint64), bad)
