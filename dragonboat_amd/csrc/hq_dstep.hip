@@ -112,10 +112,15 @@ __device__ __forceinline__ bool dvar(ByteReader &r, uint64_t &v) {
     return false;
 }
 
-// one event of a group's stream; term: the group's previous message term in the stream; index /
-// have_index: its previous ReplicateResp's log_index (type code 4 repeats it)
-__device__ bool decode_event(ByteReader &r, uint64_t &term, uint64_t &index, bool &have_index,
-                             hq_event &v) {
+// a group's stream state the codes refer back to (hq_stream.cpp's Prev): its previous message
+// term, its previous ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code 5)
+struct DPrev {
+    uint64_t term = 0, index = 0, hint = 0, high = 0;
+    bool have_index = false;
+};
+
+// one event of a group's stream
+__device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
     v = hq_event{};
     if (!r.more()) return false;
     const uint32_t h = r.next();
@@ -126,21 +131,30 @@ __device__ bool decode_event(ByteReader &r, uint64_t &term, uint64_t &index, boo
     const uint32_t code = (h >> 3) & 7;
     uint64_t t = code == 0 || code == 4 ? HQ_MSG_REPLICATE_RESP
                : code == 1 ? HQ_MSG_REQUEST_VOTE_RESP
-               : code == 2 ? HQ_MSG_HEARTBEAT_RESP : code == 3 ? HQ_MSG_READ_INDEX : 0;
+               : code == 2 || code == 5 ? HQ_MSG_HEARTBEAT_RESP
+               : code == 3 ? HQ_MSG_READ_INDEX : 0;
     if (code == 7 && !dvar(r, t)) return false;
-    if (code == 4 && !have_index) return false;     // repeats an index the group has not sent
+    if (code == 4 && !pv.have_index) return false;  // repeats an index the group has not sent
     v.type = (uint32_t)t;
     v.reject = (h >> 6) & 1;
     if (!dvar(r, v.from)) return false;
-    if (!(h & 0x80) && !dvar(r, term)) return false;
-    v.term = term;
+    if (!(h & 0x80) && !dvar(r, pv.term)) return false;
+    v.term = pv.term;
     if ((code == 0 || code == 7) && !dvar(r, v.log_index)) return false;
-    if (code == 4) v.log_index = index;
+    if (code == 4) v.log_index = pv.index;
     if ((code == 2 || code == 3 || code == 7) && !(dvar(r, v.hint) && dvar(r, v.hint_high)))
         return false;
+    if (code == 5) {
+        v.hint = pv.hint;
+        v.hint_high = pv.high;
+    }
     if (code == 0 || code == 4) {
-        index = v.log_index;
-        have_index = true;
+        pv.index = v.log_index;
+        pv.have_index = true;
+    }
+    if (code == 2 || code == 5) {
+        pv.hint = v.hint;
+        pv.high = v.hint_high;
     }
     return true;
 }
@@ -423,8 +437,7 @@ struct Engine {
     template <bool STREAM>
     __device__ __forceinline__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
         const uint64_t committed0 = g.committed;
-        uint64_t term = 0, index = 0;
-        bool have_index = false;
+        DPrev pv;
         ByteReader br{p, end};
         for (uint64_t e = e0; e < e1; ++e) {
             if (g.flags & kDSuspended) {
@@ -434,7 +447,7 @@ struct Engine {
             bool ok;
             if (STREAM) {
                 hq_event ev;
-                ok = decode_event(br, term, index, have_index, ev) && handle(ev, e);
+                ok = decode_event(br, pv, ev) && handle(ev, e);
             } else {
                 const hq_event ev = a.events[e];
                 ok = handle(ev, e);

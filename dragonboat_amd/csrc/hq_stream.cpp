@@ -23,10 +23,10 @@ inline uint32_t type_code(uint32_t t) {
     }
 }
 inline uint32_t code_type(uint32_t c) {
-    static const uint32_t t[5] = {HQ_MSG_REPLICATE_RESP, HQ_MSG_REQUEST_VOTE_RESP,
+    static const uint32_t t[6] = {HQ_MSG_REPLICATE_RESP, HQ_MSG_REQUEST_VOTE_RESP,
                                   HQ_MSG_HEARTBEAT_RESP, HQ_MSG_READ_INDEX,
-                                  HQ_MSG_REPLICATE_RESP};
-    return c < 5 ? t[c] : 0;
+                                  HQ_MSG_REPLICATE_RESP, HQ_MSG_HEARTBEAT_RESP};
+    return c < 6 ? t[c] : 0;
 }
 
 inline uint8_t *put(uint8_t *p, uint64_t v) {
@@ -49,10 +49,15 @@ inline bool get(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
     return false;
 }
 
-// one event; returns the write position. term_prev: the group's previous message term;
-// index_prev / have_index: its previous ReplicateResp's log_index (code 4 repeats it)
-inline uint8_t *encode(uint8_t *p, const hq_event &e, uint64_t &term_prev, uint64_t &index_prev,
-                       bool &have_index) {
+// a group's stream state the codes refer back to: its previous message term, its previous
+// ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code 5; 0 / 0 at first)
+struct Prev {
+    uint64_t term = 0, index = 0, hint = 0, high = 0;
+    bool have_index = false;
+};
+
+// one event; returns the write position
+inline uint8_t *encode(uint8_t *p, const hq_event &e, Prev &pv) {
     const uint32_t kind = e.kind >= 1 && e.kind <= 5 ? e.kind : 0;   // 0: not a valid kind
     if (kind != HQ_EV_MESSAGE) {
         *p++ = (uint8_t)kind;
@@ -66,16 +71,20 @@ inline uint8_t *encode(uint8_t *p, const hq_event &e, uint64_t &term_prev, uint6
     }
     uint32_t code = type_code(e.type);
     if (code == 0) {
-        if (have_index && e.log_index == index_prev) code = 4;
-        index_prev = e.log_index;
-        have_index = true;
+        if (pv.have_index && e.log_index == pv.index) code = 4;
+        pv.index = e.log_index;
+        pv.have_index = true;
+    } else if (code == 2) {
+        if (e.hint == pv.hint && e.hint_high == pv.high) code = 5;
+        pv.hint = e.hint;
+        pv.high = e.hint_high;
     }
-    const bool same = e.term == term_prev;
+    const bool same = e.term == pv.term;
     *p++ = (uint8_t)(HQ_EV_MESSAGE | code << 3 | (e.reject ? 0x40 : 0) | (same ? 0x80 : 0));
     if (code == 7) p = put(p, e.type);
     p = put(p, e.from);
     if (!same) p = put(p, e.term);
-    term_prev = e.term;
+    pv.term = e.term;
     if (code == 0 || code == 7) p = put(p, e.log_index);
     if (code == 2 || code == 3 || code == 7) {
         p = put(p, e.hint);
@@ -95,11 +104,10 @@ int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event 
     uint8_t *p = out, *const end = out ? out + cap : nullptr;
     boffsets[0] = 0;
     for (uint64_t i = 0; i < n_groups; ++i) {
-        uint64_t term_prev = 0, index_prev = 0;
-        bool have_index = false;
+        Prev pv;
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
-            p = encode(p, events[e], term_prev, index_prev, have_index);
+            p = encode(p, events[e], pv);
         }
         boffsets[i + 1] = (uint64_t)(p - out);
     }
@@ -114,11 +122,10 @@ int hq_events_encode_sized(uint64_t n_groups, const uint64_t *offsets, const hq_
     for (uint64_t i = 0; i < n_groups; ++i) {
         if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 0xFFFF) return HQ_E_INVAL;
         uint8_t *const g0 = p;
-        uint64_t term_prev = 0, index_prev = 0;
-        bool have_index = false;
+        Prev pv;
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
-            p = encode(p, events[e], term_prev, index_prev, have_index);
+            p = encode(p, events[e], pv);
         }
         if (p - g0 > 0xFFFF) return HQ_E_INVAL;
         sizes[i] = (uint32_t)(offsets[i + 1] - offsets[i]) | (uint32_t)(p - g0) << 16;
@@ -132,8 +139,7 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
     if (!offsets || !boffsets || !events) return HQ_E_INVAL;
     for (uint64_t i = 0; i < n_groups; ++i) {
         const uint8_t *p = bytes + boffsets[i], *const end = bytes + boffsets[i + 1];
-        uint64_t term_prev = 0, index_prev = 0;
-        bool have_index = false;
+        Prev pv;
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             hq_event &v = events[e];
             std::memset(&v, 0, sizeof v);
@@ -149,19 +155,27 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
                 const uint32_t code = (h >> 3) & 7;
                 uint64_t t = code_type(code);
                 if (code == 7) ok = get(p, end, t);
-                if (code == 4) ok = have_index;     // repeats an index the group has not sent
+                if (code == 4) ok = pv.have_index;  // repeats an index the group has not sent
                 v.type = (uint32_t)t;
                 v.reject = (h >> 6) & 1;
                 ok = ok && get(p, end, v.from);
-                if (ok && !(h & 0x80)) ok = get(p, end, term_prev);
-                v.term = term_prev;
+                if (ok && !(h & 0x80)) ok = get(p, end, pv.term);
+                v.term = pv.term;
                 if (ok && (code == 0 || code == 7)) ok = get(p, end, v.log_index);
-                if (code == 4) v.log_index = index_prev;
+                if (code == 4) v.log_index = pv.index;
                 if (ok && (code == 2 || code == 3 || code == 7))
                     ok = get(p, end, v.hint) && get(p, end, v.hint_high);
-                if (ok && v.type == HQ_MSG_REPLICATE_RESP && code != 7) {
-                    index_prev = v.log_index;
-                    have_index = true;
+                if (code == 5) {
+                    v.hint = pv.hint;
+                    v.hint_high = pv.high;
+                }
+                if (ok && (code == 0 || code == 4)) {
+                    pv.index = v.log_index;
+                    pv.have_index = true;
+                }
+                if (ok && (code == 2 || code == 5)) {
+                    pv.hint = v.hint;
+                    pv.high = v.hint_high;
                 }
             }
             if (!ok) return HQ_E_INVAL;

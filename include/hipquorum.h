@@ -900,14 +900,17 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
  *           bits 3-5  HQ_EV_MESSAGE: type code 0 ReplicateResp, 1 RequestVoteResp,
  *                     2 HeartbeatResp, 3 ReadIndex, 4 ReplicateResp whose log_index repeats
  *                     the group's previous ReplicateResp in the stream (its varint left out:
- *                     the followers of a steady leader ack the same index), 7 another type
- *                     (its varint follows)
+ *                     the followers of a steady leader ack the same index), 5 HeartbeatResp
+ *                     whose hint / hint_high repeat the group's previous HeartbeatResp in the
+ *                     stream (0 / 0 before the first: ctx-less acks and every follower's ack of
+ *                     the same ctx), 7 another type (its varint follows)
  *           bit 6     reject
  *           bit 7     term repeats the group's previous message term in the stream (0 before
  *                     its first message): the term varint is left out
  *   READ: hint, hint_high      PROPOSE: log_index      CHECK_QUORUM, ELECTION: nothing
  *   MESSAGE: [type], from, [term], then ReplicateResp: log_index; RequestVoteResp: nothing;
- *            HeartbeatResp, ReadIndex: hint, hint_high; another type: log_index, hint, hint_high
+ *            HeartbeatResp, ReadIndex: hint, hint_high; another type: log_index, hint, hint_high;
+ *            codes 4 and 5: nothing more
  * Fields a handler does not read are not carried (hq_events_decode returns them as 0). Event
  * indexes (offsets, deferred) count events as in hq_step_input.
  */

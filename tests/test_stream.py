@@ -70,7 +70,7 @@ def test_steady_state_sizes(hq):
     ev = np.zeros(6, hq.EVENT_DTYPE)
     ev[0] = (hq.EV_MESSAGE, RREP, 2, 41, 1_000_000, 0, 0, 0, 0)     # first message: the term
     ev[1] = (hq.EV_MESSAGE, RREP, 3, 41, 1_000_001, 0, 0, 0, 0)     # same term: 1 + 1 + 3
-    ev[2] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 0, 0, 0, 0)           # ctx-less heartbeat ack
+    ev[2] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 0, 0, 0, 0)           # ctx-less ack: code 5
     ev[3] = (hq.EV_CHECK_QUORUM, 0, 0, 0, 0, 0, 0, 0, 0)
     ev[4] = (hq.EV_PROPOSE, 0, 0, 0, 3, 0, 0, 0, 0)
     ev[5] = (hq.EV_READ, 0, 0, 0, 0, 77, 0, 0, 0)
@@ -81,7 +81,7 @@ def test_steady_state_sizes(hq):
         d, _ = hq.encode_events(np.array([0, i + 1], np.uint64), ev[:i + 1])
         sizes.append(len(d))
     sizes = np.diff([0] + sizes)
-    assert list(sizes) == [1 + 1 + 1 + 3, 1 + 1 + 3, 1 + 1 + 1 + 1, 1, 2, 3]
+    assert list(sizes) == [1 + 1 + 1 + 3, 1 + 1 + 3, 1 + 1, 1, 2, 3]
     assert len(data) == sum(sizes) and int(boff[1]) == len(data)
 
 
@@ -156,13 +156,13 @@ def test_repeated_replicate_index(hq):
     ev = np.zeros(5, hq.EVENT_DTYPE)
     ev[0] = (hq.EV_MESSAGE, RREP, 2, 41, 1_000_000, 0, 0, 0, 0)   # 1 + 1 + 1 + 3
     ev[1] = (hq.EV_MESSAGE, RREP, 3, 41, 1_000_000, 0, 0, 0, 0)   # 1 + 1: code 4
-    ev[2] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 0, 0, 0, 0)         # 1 + 1 + 1 + 1
+    ev[2] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 0, 0, 0, 0)         # ctx-less: 1 + 1, code 5
     ev[3] = (hq.EV_MESSAGE, RREP, 4, 41, 1_000_000, 0, 0, 1, 0)   # rejected, same index: code 4
     ev[4] = (hq.EV_MESSAGE, RREP, 5, 41, 999, 0, 0, 0, 0)         # another index: code 0
     off = np.array([0, 5], np.uint64)
     data, boff = hq.encode_events(off, ev)
-    assert len(data) == 6 + 2 + 4 + 2 + (1 + 1 + 2)
-    assert (data[6] >> 3) & 7 == 4 and (data[12] >> 3) & 7 == 4
+    assert len(data) == 6 + 2 + 2 + 2 + (1 + 1 + 2)
+    assert (data[6] >> 3) & 7 == 4 and (data[10] >> 3) & 7 == 4
     back = hq.decode_events(off, boff, data)
     want = carried(hq, ev)
     for k in ("kind", "type", "from", "term", "log_index", "hint", "hint_high", "reject"):
@@ -174,3 +174,34 @@ def test_repeated_replicate_index(hq):
     bad = np.array([hq.EV_MESSAGE | 4 << 3 | 0x80, 2], np.uint8)
     with pytest.raises(hq.HQError):
         hq.decode_events(np.array([0, 1], np.uint64), np.array([0, 2], np.uint64), bad)
+
+
+def test_repeated_heartbeat_ctx(hq):
+    """Type code 5: a HeartbeatResp whose hint / hint_high repeat the group's previous
+    HeartbeatResp (0 / 0 before the first: a ctx-less ack, or every follower acking the same
+    ReadIndex ctx) leaves both varints out; a ReadIndex between them does not reset it."""
+    ev = np.zeros(6, hq.EVENT_DTYPE)
+    ev[0] = (hq.EV_MESSAGE, HBRESP, 2, 41, 0, 0, 0, 0, 0)         # 1 + 1 + 1: code 5 (0 / 0)
+    ev[1] = (hq.EV_MESSAGE, HBRESP, 3, 41, 0, 900, 7, 0, 0)       # a ctx: 1 + 1 + 2 + 1, code 2
+    ev[2] = (hq.EV_MESSAGE, 19, 9, 41, 0, 5, 6, 0, 0)             # ReadIndex (code 3)
+    ev[3] = (hq.EV_MESSAGE, HBRESP, 4, 41, 0, 900, 7, 0, 0)       # same ctx: 1 + 1, code 5
+    ev[4] = (hq.EV_MESSAGE, HBRESP, 5, 41, 0, 900, 8, 1, 0)       # another high: code 2
+    ev[5] = (hq.EV_MESSAGE, HBRESP, 6, 41, 0, 0, 0, 0, 0)         # back to 0 / 0: code 2
+    off = np.array([0, 6], np.uint64)
+    data, boff = hq.encode_events(off, ev)
+    back = hq.decode_events(off, boff, data)
+    want = carried(hq, ev)
+    for k in ("kind", "type", "from", "term", "log_index", "hint", "hint_high", "reject"):
+        np.testing.assert_array_equal(back[k], want[k], err_msg=k)
+    codes = []
+    d, prev = None, 0
+    for i in range(6):
+        d, _ = hq.encode_events(np.array([0, i + 1], np.uint64), ev[:i + 1])
+        codes.append((int(d[prev]) >> 3) & 7)
+        prev = len(d)
+    assert codes == [5, 2, 3, 5, 2, 2]
+    assert len(data) == 3 + 5 + 4 + 2 + 5 + 4
+    # per group: a group's first ctx-ful ack is written in full even if the last group's matched
+    off2 = np.array([0, 2, 3], np.uint64)
+    d2, b2 = hq.encode_events(off2, ev[[0, 1, 3]])
+    assert (int(d2[int(b2[1])]) >> 3) & 7 == 2
