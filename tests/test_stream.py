@@ -32,7 +32,9 @@ def carried(hq, ev):
     return out
 
 
-def random_rows(rng, ne):
+def random_rows(rng, ne, small=False):
+    """Random rows; small: indexes and ctxs from {0, 1, 2}, so that the codes repeating a
+    group's previous index (4) or ctx (5) fire often."""
     ev = np.zeros(ne, dtype=[("kind", "<u4"), ("type", "<u4"), ("from", "<u8"),
                              ("term", "<u8"), ("log_index", "<u8"), ("hint", "<u8"),
                              ("hint_high", "<u8"), ("reject", "<u4"), ("reserved", "<u4")])
@@ -41,20 +43,21 @@ def random_rows(rng, ne):
     big = lambda: np.where(rng.random(ne) < 0.2, rng.integers(0, 2**63, ne, dtype=np.uint64) * 2
                            + 1, rng.integers(0, 300, ne).astype(np.uint64))
     for k in ("from", "log_index", "hint", "hint_high"):
-        ev[k] = big()
+        ev[k] = rng.integers(0, 3, ne).astype(np.uint64) if small and k != "from" else big()
     ev["term"] = np.where(rng.random(ne) < 0.7, 7, big())        # mostly repeating
     ev["reject"] = rng.choice([0, 0, 1, 5], ne)
     ev["reserved"] = rng.integers(0, 9, ne)
     return ev
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_round_trip(hq, seed):
+@pytest.mark.parametrize("seed,small", [(1, False), (2, False), (3, False), (4, True),
+                                        (5, True)])
+def test_round_trip(hq, seed, small):
     rng = np.random.default_rng(seed)
     n = 500
     counts = rng.integers(0, 12, n)
     off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
-    ev = random_rows(rng, int(off[-1])).view(hq.EVENT_DTYPE)
+    ev = random_rows(rng, int(off[-1]), small).view(hq.EVENT_DTYPE)
     data, boff = hq.encode_events(off, ev)
     assert boff[0] == 0 and np.all(np.diff(boff.astype(np.int64)) >= 0)
     assert len(data) <= len(ev) * hq.HQ_EVENT_STREAM_MAX
