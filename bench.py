@@ -898,7 +898,8 @@ def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, st
     bounds = [G * i // W for i in range(W + 1)]
     workers = []
     for i in range(W):
-        w = hq.Worker(d.device, n_voting, on_device=on_device, commit_column=stream == "sized")
+        w = hq.Worker(d.device, n_voting, on_device=on_device, commit_column=stream == "sized",
+                      commit_advance=stream == "sized")
         w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
         workers.append(w)
     pin_ctx = hq.Context(d.device) if on_device else None
@@ -999,7 +1000,8 @@ def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="
     modes = {"device_sized": "device worker (HQ_WORKER_ON_DEVICE: every event on the GPU), "
                              "events as the event stream in the sized form (hq_worker_step_stream:"
                              " 4-byte per-group size words, scanned on the device), commits as a "
-                             "column when most groups commit (HQ_WORKER_COMMIT_COLUMN)",
+                             "column of 4-byte advances when > 1/4 of the groups commit "
+                             "(HQ_WORKER_COMMIT_ADVANCE | _COLUMN)",
              "device_stream": "device worker, events as the event stream with the two 8-byte "
                               "prefix arrays (hq_worker_step_stream)",
              "device_rows": "device worker, events as 56-byte hq_event rows (hq_worker_step)",

@@ -47,6 +47,7 @@ struct hq_dstep_out {                 // the lists of one step, in input group o
     uint64_t decisions;
     const uint64_t *commit_col;       // the commits as a column (hq_dstep_open's commit_column
                                       // and more than half of the groups committing), else NULL
+    const uint32_t *commit_adv;       // the commits as advances (4 bytes per group), else NULL
     uint32_t input_error;             // HQ_E_INVAL: bit 1 unknown handle, 2 offsets, 4 boffsets,
                                       // 8 a group listed twice (no group state written)
     uint64_t kernel_ns, d2h_ns;       // wall time: H2D + pass A + scan + bases; pass B + D2H
@@ -65,8 +66,9 @@ struct hq_dstep_in {
     uint64_t n_events = 0, n_bytes = 0;
 };
 
-// commit_column: a step may return its commits as a column (HQ_WORKER_COMMIT_COLUMN)
-int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, bool commit_column = false);
+// commit_column: bit 1 a step may return its commits as a column (HQ_WORKER_COMMIT_COLUMN), bit 2
+// as a column of advances (HQ_WORKER_COMMIT_ADVANCE)
+int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column = 0);
 void hq_dstep_close(hq_dstep *d);
 // copy group records [g0, g0 + ng) with their reads (kDReads per group) and member records
 // [m0, m0 + nm) to the device, growing the device arrays to hold them

@@ -44,6 +44,7 @@ struct StepK {
     uint32_t *stamp;              // per handle: the last step that listed it
     uint32_t step_no;
     uint32_t *error;              // pass A: input errors (kErr* bits)
+    uint32_t *wide;               // pass A: a committed index advanced by 2^32 or more (or NULL)
     const uint32_t *handles;
     const uint64_t *offsets;
     const hq_event *events;       // rows, or
@@ -73,7 +74,9 @@ struct Layout {
     uint64_t total;
     uint32_t error, overflow;
     uint32_t commit_column;       // the commits list is a column: one word per listed group
+                                  // (kColumn64: the committed index, kColumn32: its advance)
 };
+constexpr uint32_t kColumn64 = 1, kColumn32 = 2;
 
 __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
     return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
@@ -459,7 +462,11 @@ struct Engine {
                 defer(e);
             }
         }
-        if (WRITE && a.layout->commit_column) {          // every listed group writes its word
+        if (!WRITE && g.committed - committed0 > 0xFFFFFFFFull && a.wide)
+            atomicOr(a.wide, 1u);                        // no 4-byte advance column this step
+        if (WRITE && a.layout->commit_column == kColumn32) {   // every listed group's word
+            list<uint32_t>(kCommits)[i] = (uint32_t)(g.committed - committed0);
+        } else if (WRITE && a.layout->commit_column) {
             list<uint64_t>(kCommits)[i] = g.committed != committed0 ? g.committed : 0;
         } else if (g.committed != committed0) {
             const uint32_t p = slot(kCommits);
@@ -550,19 +557,27 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
 constexpr int kMaxChunks = 4;
 __global__ void k_layout(const uint32_t *scan, uint64_t n, uint32_t *error, uint64_t cap,
                          uint32_t allow_column, Layout *lay) {
+    uint32_t *wide = error + 1;   // pass A: an advance of 2^32 or more
     if (threadIdx.x != 0) return;
     const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
                                   sizeof(hq_read_index_resp), sizeof(hq_state_change),
                                   sizeof(hq_dropped_read), 8, 8, 0};
     uint64_t total = 0;
     const uint32_t commits = scan[n] - scan[0];
-    // the commits as a column when that moves fewer bytes (8 per group vs 16 per commit)
-    lay->commit_column = allow_column && 2 * (uint64_t)commits > n;
+    // the commits as a column when that moves fewer bytes (16 per commit in the list against 8
+    // per listed group, or 4 when every advance fits)
+    // (allow_column: bit kColumn64 HQ_WORKER_COMMIT_COLUMN, bit kColumn32 _ADVANCE)
+    lay->commit_column = (allow_column & kColumn32) && !*wide && 4 * (uint64_t)commits > n
+                             ? kColumn32
+                         : (allow_column & kColumn64) && 2 * (uint64_t)commits > n ? kColumn64 : 0;
+    *wide = 0;
     for (int l = 0; l < kLists; ++l) {
         const uint32_t len = scan[(uint64_t)(l + 1) * n] - scan[(uint64_t)l * n];
         lay->off[l] = total;
         lay->len[l] = len;
-        const uint64_t bytes = l == kCommits && lay->commit_column ? n * 8 : len * rec[l];
+        const uint64_t bytes = l == kCommits && lay->commit_column
+                                   ? n * (lay->commit_column == kColumn32 ? 4 : 8)
+                                   : len * rec[l];
         total += (bytes + 255) & ~uint64_t(255);
     }
     lay->total = total;
@@ -589,7 +604,7 @@ struct hq_dstep {
     uint64_t n_groups = 0;        // group records uploaded (valid handles)
     uint32_t max_members = 0;     // the most members of any uploaded group
     uint32_t step_no = 0;
-    bool commit_column = false;   // HQ_WORKER_COMMIT_COLUMN
+    uint32_t commit_column = 0;   // bits: kColumn64 HQ_WORKER_COMMIT_COLUMN, kColumn32 _ADVANCE
     // step staging
     void *in = nullptr;
     size_t in_cap = 0;
@@ -649,7 +664,7 @@ int wait_stream(hq_dstep *d, hipStream_t s, const char *what) {
 
 }  // namespace
 
-int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, bool commit_column) {
+int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
     *out = new (std::nothrow) hq_dstep();
     if (!*out) return HQ_E_NOMEM;
     hq_dstep *d = *out;
@@ -801,7 +816,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->scan), &sc, cn * 4, false, "hq_dstep scan");
         if (!rc && !d->bases) {
             rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 256, false, "hq_dstep error");
-            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 4, ctx->stream), "memset");
+            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 8, ctx->stream), "memset");
         }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
     }
@@ -856,6 +871,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     }
     k.step_no = d->step_no;
     k.error = d->bases;           // zero here: reset by the previous step's k_layout
+    k.wide = d->commit_column & kColumn32 ? d->bases + 1 : nullptr;   // likewise
     k.out = static_cast<char *>(d->host_out);
     k.layout = d->layout;
     rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
@@ -969,8 +985,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const char *ho = static_cast<const char *>(d->host_out);
     out->commits = lay.commit_column ? nullptr
                                      : reinterpret_cast<const hq_commit_event *>(ho + lay.off[kCommits]);
-    out->commit_col = lay.commit_column ? reinterpret_cast<const uint64_t *>(ho + lay.off[kCommits])
-                                        : nullptr;
+    out->commit_col = lay.commit_column == kColumn64
+                          ? reinterpret_cast<const uint64_t *>(ho + lay.off[kCommits]) : nullptr;
+    out->commit_adv = lay.commit_column == kColumn32
+                          ? reinterpret_cast<const uint32_t *>(ho + lay.off[kCommits]) : nullptr;
     out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + lay.off[kReady]);
     out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + lay.off[kResps]);
     out->states = reinterpret_cast<const hq_state_change *>(ho + lay.off[kStates]);

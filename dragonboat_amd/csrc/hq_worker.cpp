@@ -891,6 +891,7 @@ int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     out->commits = dout.commits;
     out->n_commits = dout.n_commits;
     out->committed_column = dout.commit_col;
+    out->committed_advance = dout.commit_adv;
     out->ready = dout.ready;
     out->n_ready = dout.n_ready;
     out->read_resps = dout.resps;
@@ -922,7 +923,8 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
 
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out) {
     if (!out) return HQ_E_INVAL;
-    if (flags & ~(HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_COLUMN)) return HQ_E_INVAL;
+    if (flags & ~(HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_COLUMN | HQ_WORKER_COMMIT_ADVANCE))
+        return HQ_E_INVAL;
     *out = nullptr;
     if (n_max < 1 || n_max > HQ_MAX_VOTERS) return HQ_E_INVAL;
     hq_worker *w = new (std::nothrow) hq_worker();
@@ -934,7 +936,9 @@ int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **ou
     }
     w->n_max = n_max;
     if (flags & HQ_WORKER_ON_DEVICE) {
-        rc = hq_dstep_open(w->ctx, &w->dstep, (flags & HQ_WORKER_COMMIT_COLUMN) != 0);
+        rc = hq_dstep_open(w->ctx, &w->dstep,
+                           ((flags & HQ_WORKER_COMMIT_COLUMN) ? 1u : 0u) |
+                               ((flags & HQ_WORKER_COMMIT_ADVANCE) ? 2u : 0u));
         if (rc) {
             hq_close(w->ctx);
             delete w;

@@ -39,7 +39,8 @@ HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent i
 HQ_INGEST_UNIQUE = 2         # hq_table_*: every key at most once in the batch
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
-HQ_ABI_VERSION = 10
+HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
+HQ_ABI_VERSION = 11
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -216,7 +217,8 @@ class StepOutput(ctypes.Structure):
                [("gpu_passes", ctypes.c_uint64), ("decisions", ctypes.c_uint64),
                 ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64),
                 ("pack_ns", ctypes.c_uint64), ("device_ns", ctypes.c_uint64),
-                ("apply_ns", ctypes.c_uint64), ("committed_column", _vp)]
+                ("apply_ns", ctypes.c_uint64), ("committed_column", _vp),
+                ("committed_advance", _vp)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -1181,14 +1183,17 @@ class Worker:
     every quorum decision taken by the kernels."""
 
     def __init__(self, device: int = 0, n_max: int = 8, on_device: bool = False,
-                 commit_column: bool = False):
+                 commit_column: bool = False, commit_advance: bool = False):
         """on_device: HQ_WORKER_ON_DEVICE, the group state resident on the GPU and every event
         taken there (hq_dstep.hip); otherwise the host worker (events on the host, decisions
         in GPU passes). commit_column: HQ_WORKER_COMMIT_COLUMN (results carry
-        'committed_column' instead of 'commits' when most listed groups commit)."""
+        'committed_column' instead of 'commits' when most listed groups commit);
+        commit_advance: HQ_WORKER_COMMIT_ADVANCE ('committed_advance', u32 per listed group,
+        when more than a quarter of them commit)."""
         self.h = _vp()
         flags = (HQ_WORKER_ON_DEVICE if on_device else 0) | \
-            (HQ_WORKER_COMMIT_COLUMN if commit_column else 0)
+            (HQ_WORKER_COMMIT_COLUMN if commit_column else 0) | \
+            (HQ_WORKER_COMMIT_ADVANCE if commit_advance else 0)
         rc = lib.hq_worker_open_ex(device, n_max, flags, ctypes.byref(self.h))
         if rc != HQ_OK:
             raise HQError(rc, "hq_worker_open: " + lib.hq_last_error(None).decode())
@@ -1295,7 +1300,7 @@ class Worker:
         for name, dt in STEP_OUTPUT_LISTS:
             n = getattr(out, "n_" + name)
             ptr = getattr(out, name)
-            if n == 0 or (name == "commits" and out.committed_column):
+            if n == 0 or (name == "commits" and (out.committed_column or out.committed_advance)):
                 res[name] = np.zeros(0, dt)
                 continue
             buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
@@ -1307,6 +1312,11 @@ class Worker:
             buf = (ctypes.c_char * (n_listed * 8)).from_address(out.committed_column)
             col = np.frombuffer(buf, np.uint64)
             res["committed_column"] = col.copy() if copy else col
+            res["n_commits"] = out.n_commits
+        if out.committed_advance:
+            buf = (ctypes.c_char * (n_listed * 4)).from_address(out.committed_advance)
+            col = np.frombuffer(buf, np.uint32)
+            res["committed_advance"] = col.copy() if copy else col
             res["n_commits"] = out.n_commits
         return res
 

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 10
+#define HQ_ABI_VERSION 11
 
 /* status codes */
 #define HQ_OK          0
@@ -844,6 +844,12 @@ typedef struct hq_step_output {
      * listed group (input order), its new committed index or 0 (no commit: a commit never sets
      * 0); `commits` is then NULL and n_commits counts the nonzero words */
     const uint64_t *committed_column;
+    /* HQ_WORKER_COMMIT_ADVANCE workers only, else NULL: the step's commits as one 4-byte word per
+     * listed group (input order), how far its committed index advanced (new - previous; 0: no
+     * commit) — the host adds it to the committed index it already holds (entries (prev, prev +
+     * advance] are committed); `commits` and `committed_column` are then NULL and n_commits
+     * counts the nonzero words */
+    const uint32_t *committed_advance;
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;
@@ -863,6 +869,10 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
  * its commits as hq_step_output.committed_column (8 bytes per listed group across PCIe instead
  * of a 16-byte record per commit); other steps keep the list */
 #define HQ_WORKER_COMMIT_COLUMN 2u
+/* with HQ_WORKER_ON_DEVICE: a step in which more than a quarter of the listed groups commit
+ * returns its commits as hq_step_output.committed_advance (4 bytes per listed group); other steps,
+ * and a step in which some group's committed index advances by 2^32 or more, keep the list */
+#define HQ_WORKER_COMMIT_ADVANCE 4u
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out);
 void hq_worker_close(hq_worker *w);
 const char *hq_worker_last_error(const hq_worker *w);

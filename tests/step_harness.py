@@ -64,12 +64,14 @@ class WorkerBackend:
     hq_worker_step_stream) instead of rows."""
 
     def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False, stream=False):
-        """stream: False (rows), True (stream with prefix arrays), "sized" (size words) or
-        "sized-column" (size words in, commits as a column out: HQ_WORKER_COMMIT_COLUMN)."""
+        """stream: False (rows), True (stream with prefix arrays), "sized" (size words),
+        "sized-column" (size words in, commits as a column out: HQ_WORKER_COMMIT_COLUMN) or
+        "sized-advance" (commits as 4-byte advances: HQ_WORKER_COMMIT_ADVANCE)."""
         self.hq = hq
         self.stream = stream
         self.w = worker if worker is not None else hq.Worker(
-            0, n_max, on_device=on_device, commit_column=stream == "sized-column")
+            0, n_max, on_device=on_device, commit_column=stream == "sized-column",
+            commit_advance=stream == "sized-advance")
         self.rng = np.random.default_rng(seed)
         self.cids = []
         self.last_passes = 0
@@ -110,6 +112,9 @@ class WorkerBackend:
 
     def step(self, per_group):
         arrs, refs = self.build_inputs(per_group)
+        prev = {}                       # the committed indexes the advances add to
+        if self.stream == "sized-advance":
+            prev = {cid: int(self.w.get_group(cid)[0]["committed"]) for cid in self.last_cids}
         if isinstance(arrs, self.hq.SizedStream):
             res = self.w.step_sized(*arrs)
         else:
@@ -144,6 +149,13 @@ class WorkerBackend:
                 if v:
                     out[cid]["commit_changed"] = True
                     out[cid]["_col"] = v
+        adv = res.get("committed_advance")
+        if adv is not None:             # one advance per listed group, in input order
+            assert len(adv) == len(self.last_cids) and res["n_commits"] == int((adv != 0).sum())
+            for cid, v in zip(self.last_cids, adv.tolist()):
+                if v:
+                    out[cid]["commit_changed"] = True
+                    out[cid]["_col"] = prev[cid] + v
         for cid in out:
             out[cid]["committed"] = int(self.w.get_group(cid)[0]["committed"])
             assert out[cid].pop("_col", out[cid]["committed"]) == out[cid]["committed"]

@@ -18,9 +18,9 @@ MODES = [False, True]
 MODE_IDS = ["host", "device"]      # the host worker / HQ_WORKER_ON_DEVICE (hq_dstep.hip)
 # (on_device, stream): events as rows or as an event stream (hq_worker_step_stream)
 FEEDS = [(False, False), (True, False), (True, True), (False, True), (True, "sized"),
-         (False, "sized"), (True, "sized-column")]
+         (False, "sized"), (True, "sized-column"), (True, "sized-advance")]
 FEED_IDS = ["host", "device", "device-stream", "host-stream", "device-sized", "host-sized",
-            "device-sized-column"]
+            "device-sized-column", "device-sized-advance"]
 
 
 @pytest.fixture(scope="module", params=FEEDS, ids=FEED_IDS)
@@ -390,8 +390,8 @@ def test_step_jobs_equal_sequential_steps(hq):
             w.close()
 
 
-@pytest.mark.parametrize("stream", [True, False, "sized", "sized-column"],
-                         ids=["stream", "rows", "sized", "sized-column"])
+@pytest.mark.parametrize("stream", [True, False, "sized", "sized-column", "sized-advance"],
+                         ids=["stream", "rows", "sized", "sized-column", "sized-advance"])
 def test_chunked_device_step_equals_host_worker(hq, stream):
     """A step of >= 256 Ki groups runs in 4 chunks whose copies overlap the neighbouring chunks'
     passes (hq_dstep.hip); its lists equal the host worker's on the same events (the host
@@ -402,13 +402,16 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
     roles = bench.STEP_ROLES["step5"]
     g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
     nv = sum(r != "observer" for r in roles)
-    dev = hq.Worker(0, nv, on_device=True, commit_column=stream == "sized-column")
+    dev = hq.Worker(0, nv, on_device=True, commit_column=stream == "sized-column",
+                    commit_advance=stream == "sized-advance")
     host = hq.Worker(0, nv)
     try:
         dev.add_groups(g, m)
         host.add_groups(g, m)
         for s in range(3):
             e = bench.step_events(hq, G, s, roles)
+            prev_col = np.array([host.get_group(c)[0]["committed"] for c in range(1, G + 1)],
+                                np.uint64) if stream == "sized-advance" and s else None
             want = host.step(*e)
             if str(stream).startswith("sized"):   # byte chunks, each group's pass A in the
                 data, sizes = hq.encode_events_sized(e[1], e[2])   # chunk its bytes end in
@@ -419,6 +422,13 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
                     want_col[want["commits"]["cluster_id"].astype(np.int64) - 1] = \
                         want["commits"]["committed"]
                     np.testing.assert_array_equal(got["committed_column"], want_col)
+                    got["commits"] = want["commits"]
+                elif "committed_advance" in got:  # the advance over the previous step's
+                    assert s and stream == "sized-advance" and got["n_commits"] == G
+                    want_col = np.zeros(G, np.uint64)
+                    want_col[want["commits"]["cluster_id"].astype(np.int64) - 1] = \
+                        want["commits"]["committed"]
+                    np.testing.assert_array_equal(prev_col + got["committed_advance"], want_col)
                     got["commits"] = want["commits"]
                 else:
                     assert not s or stream == "sized"

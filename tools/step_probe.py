@@ -24,7 +24,8 @@ nm = len(roles)
 workers = []
 for i in range(W):
     w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True,
-                  commit_column=os.environ.get("COLUMN", "1") == "1")
+                  commit_column=os.environ.get("COLUMN", "1") == "1",
+                  commit_advance=os.environ.get("ADVANCE", "1") == "1")
     w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
     workers.append(w)
 pc = hq.Context(0)
@@ -43,8 +44,9 @@ for s in range(STEPS):
         p = tuple(pc.pinned(x.size, x.dtype) for x in e)
         for dst, src in zip(p, e):
             dst[:] = src
-        if feed == "sized":
-            p = hq.SizedStream(p[0], p[1], nev, p[2])
+        if feed == "sized":       # IMPLICIT=1 (default): groups = NULL, as the bench's legs
+            implicit = os.environ.get("IMPLICIT", "1") == "1"
+            p = hq.SizedStream(None if implicit else p[0], p[1], nev, p[2])
         inputs.append(p)
     jobs = hq.StepJobs(list(zip(workers, inputs)))
     t0 = time.perf_counter()
