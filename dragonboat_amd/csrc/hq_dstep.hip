@@ -60,8 +60,11 @@ struct StepK {
     const struct Layout *layout;  //   at layout->off[list]
 };
 
-struct PackSize {                 // per-group size word -> events << 32 | bytes
-    __host__ __device__ uint64_t operator()(uint32_t s) const {
+struct PackSize {                 // group i's size word -> events << 32 | bytes; i = n: 0 (the
+    const uint32_t *sizes;        // scan's last element is the totals; no memset on the copy
+    uint64_t n;                   // stream between the sizes' copy and the bytes')
+    __host__ __device__ uint64_t operator()(uint64_t i) const {
+        const uint32_t s = i < n ? sizes[i] : 0;
         return (uint64_t)(s & 0xFFFFu) << 32 | (s >> 16);
     }
 };
@@ -829,8 +832,9 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (!rc) d->host_out_cap = want;
     }
     size_t tmp = 0, tmp2 = 0;
-    const hipcub::TransformInputIterator<uint64_t, PackSize, const uint32_t *> packed_sizes(
-        reinterpret_cast<const uint32_t *>(din + o_off), PackSize{});
+    const hipcub::TransformInputIterator<uint64_t, PackSize, hipcub::CountingInputIterator<uint64_t>>
+        packed_sizes(hipcub::CountingInputIterator<uint64_t>(0),
+                     PackSize{reinterpret_cast<const uint32_t *>(din + o_off), n});
     uint64_t *prefix = reinterpret_cast<uint64_t *>(din + o_boff);
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
@@ -874,7 +878,6 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.wide = d->commit_column & kColumn32 ? d->bases + 1 : nullptr;   // likewise
     k.out = static_cast<char *>(d->host_out);
     k.layout = d->layout;
-    rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream), "memset");
     const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
     auto launch = [&](bool write, uint64_t i0, uint64_t i1) {
         k.i_begin = i0;
@@ -897,27 +900,29 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         rc = hq::post_launch(ctx, write ? "k_step<write>" : "k_step<count>");
     };
     if (sized) {
-        // handles and sizes (+ a zero: the scan's last element is the totals), their scan; then
+        // handles and sizes, their scan (PackSize adds the totals as element n); then
         // the bytes in equal byte chunks, each followed by pass A over the groups whose bytes end
         // inside what has landed
+        // every copy is queued before the first launch, event c behind chunk c's bytes; the
+        // scan waits for chunk 0's event too (an event between two copies leaves a 20-65-us
+        // hole in the copy stream, longer than the scan and pass A of chunk 0 take)
         if (in->groups) h2d(0, in->groups, n * 4);   // NULL: the step lists handles 0 .. n - 1
         h2d(o_off, in->sizes, n * 4);
-        if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(din + o_off + n * 4, 0, 4, cs), "memset");
-        if (chunks > 1) {
-            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[0], cs), "event");
-            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[0], 0), "wait");
+        for (int c = 0; c < chunks && !rc; ++c) {
+            const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
+            h2d(o_ev + lo, in->bytes + lo, hi - lo);
+            if (chunks > 1 && !rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
         }
+        if (chunks > 1 && !rc)
+            rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[0], 0), "wait");
         if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(
                                               d->scan_tmp, tmp2, packed_sizes, prefix, n + 1,
                                               ctx->stream),
                                     "hipcub scan");
         for (int c = 0; c < chunks && !rc; ++c) {
             const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
-            h2d(o_ev + lo, in->bytes + lo, hi - lo);
-            if (chunks > 1) {
-                if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
-                if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
-            }
+            if (chunks > 1 && c > 0)
+                rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
             k.own_lo = c == 0 ? 0 : lo + 1;
             k.own_hi = c + 1 == chunks ? UINT64_MAX : hi + 1;
             launch(false, 0, n);
@@ -945,6 +950,9 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         }
         launch(false, i0, i1);
     }
+    // (the counts' trailing zero: set after the copies are queued, which it does not gate)
+    if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->counts + kLists * n, 0, 4, ctx->stream),
+                                "memset");
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, d->counts,
                                                                        d->scan, cn, ctx->stream),
                                 "hipcub scan");
