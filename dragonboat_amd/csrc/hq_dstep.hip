@@ -835,10 +835,10 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     // one chunk: every copy on the compute stream (nothing to overlap, no cross-stream waits)
     hipStream_t cs = chunks > 1 ? d->copy : ctx->stream;
     char *din = static_cast<char *>(d->in);
-    auto h2d = [&](size_t off, const void *src, size_t bytes) {
+    auto h2d = [&](size_t off, const void *src, size_t bytes, hipStream_t s = nullptr) {
         if (!rc && bytes)
             rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
-                                                   cs), "hq_dstep H2D");
+                                                   s ? s : cs), "hq_dstep H2D");
     };
     // counts [kLists][n]; the scan buffer holds the per-wave sums [kLists][nw] + 1 (a zero: the
     // scan's last element is the grand total) and their scan (one size covers both)
@@ -938,24 +938,23 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         // the bytes in equal byte chunks, each followed by pass A over the groups whose bytes end
         // inside what has landed
         // every copy is queued before the first launch, event c behind chunk c's bytes; the
-        // scan waits for chunk 0's event too (an event between two copies leaves a 20-65-us
-        // hole in the copy stream, longer than the scan and pass A of chunk 0 take)
-        if (in->groups) h2d(0, in->groups, n * 4);   // NULL: the step lists handles 0 .. n - 1
-        h2d(o_off, in->sizes, n * 4);
+        // handles and sizes go on the compute stream ahead of their scan, the bytes on the copy
+        // stream beside them (behind the sizes on one stream the first bytes copy started
+        // 50-65 us after the sizes' copy ended)
+        if (in->groups) h2d(0, in->groups, n * 4, ctx->stream);   // NULL: handles 0 .. n - 1
+        h2d(o_off, in->sizes, n * 4, ctx->stream);
         for (int c = 0; c < chunks && !rc; ++c) {
             const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
             h2d(o_ev + lo, in->bytes + lo, hi - lo);
             if (chunks > 1 && !rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
         }
-        if (chunks > 1 && !rc)
-            rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[0], 0), "wait");
         if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(
                                               d->scan_tmp, tmp2, packed_sizes, prefix, n + 1,
                                               ctx->stream),
                                     "hipcub scan");
         for (int c = 0; c < chunks && !rc; ++c) {
             const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
-            if (chunks > 1 && c > 0)
+            if (chunks > 1)
                 rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
             k.own_lo = c == 0 ? 0 : lo + 1;
             k.own_hi = c + 1 == chunks ? UINT64_MAX : hi + 1;
