@@ -1,7 +1,8 @@
 /*
  * step_worker.c — a plain C host of the step worker (what a cgo execEngine.processSteps would
  * do, INTEGRATION.md §4, without Go): three Raft groups on one device worker
- * (HQ_WORKER_ON_DEVICE), two steps of events encoded as a sized event stream
+ * (HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_ADVANCE: commits as one 4-byte advance per listed
+ * group when more than a quarter of them commit), two steps of events encoded as a sized event stream
  * (hq_events_encode_sized), stepped with hq_worker_step_stream. The expected results follow the
  * reference by hand:
  *   cluster 100, leader of 3 remotes + 1 witness + 1 observer (4 voting, quorum 3), committed 5,
@@ -87,7 +88,7 @@ static int step(hq_worker *w, uint32_t n, const uint32_t *handles, const uint64_
 
 int main(void) {
     hq_worker *w = NULL;
-    if (hq_worker_open_ex(0, 8, HQ_WORKER_ON_DEVICE, &w) != HQ_OK) {
+    if (hq_worker_open_ex(0, 8, HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_ADVANCE, &w) != HQ_OK) {
         fprintf(stderr, "hq_worker_open_ex: %s\n", hq_worker_last_error(NULL));
         return 2;
     }
@@ -119,8 +120,11 @@ int main(void) {
     const uint64_t off1[4] = {0, 3, 5, 6};
     hq_step_output out;
     CHECK(step(w, 3, h, off1, ev1, &out));
-    EXPECT(out.n_commits == 1 && out.commits[0].cluster_id == 100 && out.commits[0].committed == 7,
-           "commit 100 -> 7 (witness ack, observer ack ignored)");
+    /* one of the three listed groups commits (> 1/4): the advance column, in listing order */
+    EXPECT(out.n_commits == 1 && out.commits == NULL && out.committed_advance != NULL &&
+               out.committed_advance[0] == 2 && out.committed_advance[1] == 0 &&
+               out.committed_advance[2] == 0,
+           "commit 100 -> 7 as advance 2 (witness ack, observer ack ignored)");
     EXPECT(out.n_ready == 1 && out.ready[0].cluster_id == 200 && out.ready[0].index == 10 &&
                out.ready[0].ctx_low == 77 && out.ready[0].ctx_high == 1,
            "ReadyToRead 200 at 10");
