@@ -22,6 +22,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -247,9 +248,75 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def gather_obj(self, o) -> list:
+        """Every rank's picklable object, in rank order (off the timed region)."""
+        if self.torch is None:
+            return [o]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, o)
+        return out
+
     def close(self):
         if self.torch is not None:
             self.dist.destroy_process_group()
+
+
+class ThreadGroup:
+    """State shared by the host threads of one launcher-free multi-GPU run."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.bar = threading.Barrier(n, timeout=1800)
+        self.slots = [None] * n
+
+
+class ThreadDist:
+    """`python bench.py --gpus N` without a launcher: one process, one host thread and one hq_ctx
+    (one HIP stream) per GPU, the way SURVEY.md §8e and the reference's step workers run
+    (execengine.go:675-690: one goroutine per worker, groups on worker clusterID % N,
+    partition.go:38). Same interface as Dist; the barrier and the max / sum over ranks are host
+    thread barriers, taken only at the start and end of a timed region. A GPU index beyond the
+    visible devices wraps (rehearsal of N ranks on fewer GPUs)."""
+
+    def __init__(self, group: ThreadGroup, rank: int, ngpu: int):
+        self.g = group
+        self.world, self.rank, self.local_rank = group.n, rank, rank
+        self.device = rank % max(1, ngpu)
+        self.backend = "threads"
+        self.torch = None
+
+    def barrier(self):
+        self.g.bar.wait()
+
+    def sync_device(self):
+        pass          # every leg syncs its own contexts before the barrier
+
+    def _all(self, x) -> list:
+        self.g.slots[self.rank] = x
+        self.g.bar.wait()
+        vals = list(self.g.slots)
+        self.g.bar.wait()             # nobody overwrites a slot before all have read it
+        return vals
+
+    def max(self, x: float) -> float:
+        return max(self._all(x))
+
+    def sum(self, x: float) -> float:
+        return float(sum(self._all(x)))
+
+    def gather(self, xs) -> list:
+        return [list(v) for v in self._all(list(xs))]
+
+    def gather_obj(self, o) -> list:
+        return self._all(o)
+
+    def gather_words(self, ctx, dev_words, nwords: int):
+        t0 = time.perf_counter()
+        words = self._all(ctx.download(dev_words)[:nwords].copy())
+        return np.stack(words).view(np.uint64), time.perf_counter() - t0
+
+    def close(self):
+        pass
 
 
 # ----------------------------------------------------------------------------- GPU legs -------
@@ -881,84 +948,44 @@ def _partition(ev_full, b0, b1):
 STEP_WARM = 2
 
 
-def _run_workers(hq, d: Dist, G, W, steps, cpu_steps, roles, on_device=False, stream=False,
-                 events=None):
-    """W workers (one native thread each, own HIP stream) over G groups split into W contiguous
-    partitions, stepping concurrently; returns (timed seconds, events, counter sums, committed
-    of the first 4096 groups after the last step, ..., encode seconds). on_device:
-    HQ_WORKER_ON_DEVICE workers, the step's input in pinned host memory (a step worker's receive
-    buffers) so that it crosses PCIe at the link's rate. stream: the input is the event stream
-    (hq_worker_step_stream), written by the producer — here hq_events_encode over the rows,
-    outside the timed region and timed on its own (encode seconds). events(s): the full step s
-    input (cached by the caller across modes)."""
-    rng = _shard_of(d, G)
-    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
-    nm = len(roles)
-    n_voting = sum(r != "observer" for r in roles)
-    bounds = [G * i // W for i in range(W + 1)]
-    workers = []
-    for i in range(W):
-        w = hq.Worker(d.device, n_voting, on_device=on_device, commit_column=stream == "sized",
-                      commit_advance=stream == "sized")
-        w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
-        workers.append(w)
-    pin_ctx = hq.Context(d.device) if on_device else None
-    pinned = [None] * W
-    acc = dict(handle_ns=0, pass_ns=0, pack_ns=0, device_ns=0, apply_ns=0, gpu_passes=0,
-               decisions=0)
-    t_total, n_events, committed, t_enc, nb_total = 0.0, 0, None, 0.0, 0
-    step_ms = []
-    warm = STEP_WARM   # untimed: allocations, first touch, and the first step with commits
-    for s in range(steps + warm):   # (its output lists size the pinned result buffers)
-        full = events(s) if events else step_events(hq, G, s, roles)
-        evs = [_partition(full, bounds[i], bounds[i + 1]) for i in range(W)]
-        n_step = sum(len(e[2]) for e in evs)
-        n_ev = [len(e[2]) for e in evs]
-        if stream:
-            t0 = time.perf_counter()
-            enc = [hq.encode_events_sized(e[1], e[2]) if stream == "sized" else
-                   hq.encode_events(e[1], e[2]) for e in evs]
-            if s >= warm:
-                t_enc += time.perf_counter() - t0
-                nb_total += sum(len(data) for data, _ in enc)
-            # sized: (groups, size words, bytes); else (groups, offsets, boffsets, bytes)
-            evs = [(e[0], z, data) if stream == "sized" else (e[0], e[1], z, data)
-                   for e, (data, z) in zip(evs, enc)]
-        if pin_ctx is not None:      # copied into pinned buffers outside the timed region
-            for i, e in enumerate(evs):
-                if pinned[i] is None or any(p.size < x.size for p, x in zip(pinned[i], e)):
-                    pinned[i] = tuple(pin_ctx.pinned(x.size + x.size // 4 + 1, x.dtype)
-                                      for x in e)
-                for dst, src in zip(pinned[i], e):
-                    dst[:src.size] = src
-            evs = [tuple(p[k][:e[k].size] for k in range(len(e))) for p, e in zip(pinned, evs)]
-        if stream == "sized":   # every group in handle order: the handles stay implicit
-            evs = [hq.SizedStream(None, e[1], ne, e[2]) for e, ne in zip(evs, n_ev)]
-        # the W workers stepped at once on native threads (hq_worker_step_jobs), as W step-
-        # worker goroutines each calling its own worker
-        jobs = hq.StepJobs(list(zip(workers, evs)))
-        t0 = time.perf_counter()
-        res = jobs.run(copy=False)
-        dt = time.perf_counter() - t0
-        if s < warm:
-            continue
-        step_ms.append(round(dt * 1e3, 3))
-        t_total += dt
-        n_events += n_step
-        for r in res:
-            for k in acc:
-                acc[k] += r[k]
-    # the state after the last step, checked against the CPU replay of the same steps (read
-    # after the timed steps: reading a device worker's state downloads all of it)
-    committed = [int(workers[0].get_group(int(c))[0]["committed"])
-                 for c in cids[:min(4096, bounds[1])]]
-    for w in workers:
-        w.close()
-    if pin_ctx is not None:
-        pin_ctx.close()
-    acc["stream_bytes"] = nb_total
-    acc["step_ms"] = step_ms
-    return t_total, n_events, acc, committed, (g, m), t_enc
+class StepRows:
+    """The steady-state step inputs of step_events(), kept in ONE row array and advanced in
+    place. Rows of step s + 1 differ from step s only in the ReplicateResp log index and the
+    ReadIndex ctx words, and the rows repeat with a period of 4 groups (group 4p serves the read),
+    so set(s) is a few strided column writes instead of a regeneration (equality with
+    step_events() is tested in tests/test_bench_host.py)."""
+
+    WORDS = 7     # hq_event = 56 bytes = 7 u64 words: kind|type, from, term, log_index, hint,
+    #               hint_high, reject|reserved
+
+    def __init__(self, hq, G, roles, last0=1000):
+        assert G % 4 == 0 and hq.EVENT_DTYPE.itemsize == 8 * self.WORDS
+        self.G, self.last0, self.s = G, last0, 0
+        self.groups, self.offsets, self.ev = step_events(hq, G, 0, roles, last0)
+        others = list(enumerate(roles))[1:]
+        k = len(others)
+        per = 2 * k + 1                      # ReplicateResps, HeartbeatResps, the proposal
+        self.period = 4 * per + 1
+        assert len(self.ev) == (G // 4) * self.period
+        self.u = self.ev.view(np.uint64).reshape(G // 4, self.period, self.WORDS)
+        starts = [1] + [per + 1 + j * per for j in range(3)]
+        self.repl = [st + j for st in starts for j in range(k)]
+        self.hb_ctx = [1 + k + j for j, (_, r) in enumerate(others) if r != "observer"]
+        self.read = 0
+        self.g0 = np.arange(0, G, 4, dtype=np.uint64)
+
+    def set(self, s):
+        """Make the rows those of step s."""
+        u, s1 = self.u, np.uint64(s + 1)
+        u[:, self.repl, 3] = np.uint64(self.last0 + s)
+        ctx = (s1 << np.uint64(32)) | self.g0
+        u[:, self.read, 4] = ctx
+        u[:, self.read, 5] = s1
+        for p in self.hb_ctx:
+            u[:, p, 4] = ctx
+            u[:, p, 5] = s1
+        self.s = s
+        return self.groups, self.offsets, self.ev
 
 
 def _shard_of(d, G):
@@ -967,117 +994,188 @@ def _shard_of(d, G):
     return shard.rank_shard(d.rank, d.world, G)
 
 
-def run_step_leg(d: Dist, G=1 << 20, steps=6, cpu_steps=3, with_cpu=True, name="step"):
-    """The step worker end to end (hq_worker_step): host bookkeeping of every event plus the
-    GPU passes, against the event-by-event C restatement of the reference (oracle, CPU) on the
-    same events; the committed indexes of both must agree. Run with one worker (one step-worker
-    thread), two (dragonboat's 16 step workers on an 8-GPU node: two per GPU) and T workers
-    stepping concurrently (dragonboat runs 16 step workers, internal/settings/hard.go:36), next
-    to the CPU replay on 1 and T threads."""
+def _median(xs):
+    return float(np.median(xs)) if xs else None
+
+
+def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
+    """The device step engine (hq_worker_step_stream, HQ_WORKER_ON_DEVICE: every event of the
+    step taken on the GPU) over G leader groups per GPU, W = 1, 2 and 16 workers (dragonboat runs
+    16 step workers, internal/settings/hard.go:35; each worker one native thread and one HIP
+    stream, stepped at once by hq_worker_step_jobs), in two timings over the same `steps` steps:
+
+      device_only  the step's event stream already encoded in pinned memory (the producer's
+                   encode outside the timed region);
+      end_to_end   the producer's encode inside: while the device takes step s, the W threads
+                   encode step s + 1's rows into the other pinned stream buffer
+                   (hq_events_encode_sized), and a step costs the longer of the two. The rows
+                   stand for the pb.Message values the reference's step worker holds
+                   (execengine.go:923-1000 -> node.go:1257-1287); making them (the messages
+                   arriving) is outside both timings.
+
+    Beside it the CPU event-by-event replay of the reference path (oracle/qref_step.c) over the
+    same rows of the same steps, on all usable host cores, 16 threads and 1 thread. Every step's
+    commit count, ReadyToRead count and the sum of the committed advances of all groups must
+    agree between every mode and the replay."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from dragonboat_amd import hipquorum as hq
 
-    assert cpu_steps <= steps
-    T = min(16, os.cpu_count() or 1)
     roles = STEP_ROLES[name]
-    nmsg = 2 * (len(roles) - 1)
-    members = ", ".join(f"{roles.count(r)} {r}" for r in ("remote", "witness", "observer")
-                        if roles.count(r))
-    out = {
-        "workload": f"{name}: hq_worker_step (device engine; host worker beside it) over {G} "
-                    f"leader groups per GPU ({members}); per group "
-                    f"and step {nmsg} messages ({nmsg // 2} ReplicateResp, {nmsg // 2} "
-                    f"HeartbeatResp), 1 proposal, 1/4 local ReadIndex",
-        "unit": "events/s",
-    }
-    committed = {}
-    cache = {}
+    n_voting = sum(r != "observer" for r in roles)
+    nm = len(roles)
+    rng = _shard_of(d, G)
+    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
+    rows = StepRows(hq, G, roles)
+    offsets = rows.offsets
+    pin = hq.Context(d.device)
+    Ws = (1, 2, 16)
+    modes = {}
+    for W in Ws:
+        bounds = [G * i // W for i in range(W + 1)]
+        parts = []
+        for i in range(W):
+            o = offsets[bounds[i]:bounds[i + 1] + 1]
+            parts.append((o - o[0], int(o[0]), int(o[-1])))
 
-    def events(s):            # one generation per step index, shared by every mode
-        if s not in cache:
-            cache[s] = step_events(hq, G, s, roles)
-        return cache[s]
+        def workers():
+            ws = []
+            for i in range(W):
+                wk = hq.Worker(d.device, n_voting, on_device=True, commit_column=True,
+                               commit_advance=True)
+                wk.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
+                ws.append(wk)
+            return ws
+        bufs = [[(pin.pinned((e1 - e0) * 5 + 64, np.uint8), pin.pinned(len(o) - 1, np.uint32))
+                 for o, e0, e1 in parts] for _ in range(2)]
+        modes[W] = dict(parts=parts, bufs=bufs, nbytes=[[0] * W, [0] * W], dev=workers(),
+                        e2e=workers(), t={"dev": [], "e2e": []}, bytes=0,
+                        check={"dev": [], "e2e": []})
+    pool = ThreadPoolExecutor(max(Ws) + 1)
 
-    modes = {"device_sized": "device worker (HQ_WORKER_ON_DEVICE: every event on the GPU), "
-                             "events as the event stream in the sized form (hq_worker_step_stream:"
-                             " 4-byte per-group size words, scanned on the device), commits as a "
-                             "column of 4-byte advances when > 1/4 of the groups commit "
-                             "(HQ_WORKER_COMMIT_ADVANCE | _COLUMN)",
-             "device_stream": "device worker, events as the event stream with the two 8-byte "
-                              "prefix arrays (hq_worker_step_stream)",
-             "device_rows": "device worker, events as 56-byte hq_event rows (hq_worker_step)",
-             "host": "host worker (events on the host, decisions in GPU passes), rows"}
-    all_modes = (("device_sized", 1), ("device_sized", 2), ("device_sized", T),
-                 ("device_stream", 1), ("device_stream", T), ("device_rows", 1),
-                 ("device_rows", T), ("host", 1), ("host", T))
-    # with several ranks (a node's GPUs, each with its own share) only the device engine's modes
-    # run: the comparison modes are host-bound and would share the node's cores
-    for mode, W in all_modes if d.world == 1 else all_modes[:3]:
-        if d.rank == 0:
-            log(f"  step leg {name}: {mode}, {W} worker(s)")
-        t, ne, acc, committed[mode], gm, t_enc = _run_workers(
-            hq, d, G, W, steps, cpu_steps, roles, mode != "host",
-            {"device_sized": "sized", "device_stream": True}.get(mode, False), events)
-        elapsed = d.max(t)
-        rec = {
-            "workers": W,
-            "mode": modes[mode],
-            "value": d.sum(float(ne)) / elapsed,
-            "decisions_per_s": d.sum(float(acc["decisions"])) / elapsed,
-            "ms_per_step": elapsed / steps * 1e3,
-            "step_ms": acc["step_ms"],
-            # the copy-engine paths see occasional multi-ms idle gaps on these boxes (DESIGN §9.3):
-            # the median step beside the mean
-            "median_ms_per_step": float(np.median(acc["step_ms"])) if acc["step_ms"] else None,
-            "gpu_passes_per_step": acc["gpu_passes"] / steps / W,
-            "host_ms_per_step_per_worker": acc["handle_ns"] / steps / W / 1e6,
-            "pass_split_ms_per_worker": {k: acc[k + "_ns"] / steps / W / 1e6
-                                         for k in ("pack", "device", "apply")},
-        }
-        if mode in ("device_sized", "device_stream"):
-            rec["stream_bytes_per_event"] = acc.get("stream_bytes", 0) / max(1, ne)
-            rec["producer_encode_ns_per_event"] = t_enc / max(1, ne) * 1e9
-        key = {("device_sized", 1): None, ("device_sized", T): "concurrent_workers",
-               ("device_sized", 2): "two_workers",
-               ("device_stream", 1): "device_stream", ("device_stream", T): "device_stream_concurrent",
-               ("device_rows", 1): "device_rows", ("device_rows", T): "device_rows_concurrent",
-               ("host", 1): "host_worker", ("host", T): "host_worker_concurrent"}[(mode, W)]
-        if key is None:
-            out.update(rec)
-        else:
-            out[key] = rec
+    def encode(W, i, slot):
+        mo = modes[W]
+        off, e0, e1 = mo["parts"][i]
+        out, sz = mo["bufs"][slot][i]
+        mo["nbytes"][slot][i] = hq.encode_events_sized_into(off, rows.ev[e0:e1], out, sz)
+
+    def jobs(W, slot, which):
+        mo = modes[W]
+        return hq.StepJobs([
+            (wk, hq.SizedStream(None, mo["bufs"][slot][i][1], mo["parts"][i][2] - mo["parts"][i][1],
+                                mo["bufs"][slot][i][0][:mo["nbytes"][slot][i]]))
+            for i, wk in enumerate(mo[which])])
+
+    def digest(res):     # (commits, ReadyToReads, sum of committed advances) of one step
+        c = sum(int(r.get("n_commits", len(r["commits"]))) for r in res)
+        adv = sum(int(r["committed_advance"].sum(dtype=np.uint64)) for r in res
+                  if "committed_advance" in r)
+        ok = all("committed_advance" in r or r.get("n_commits", 0) == 0 for r in res)
+        return (c, sum(len(r["ready"]) for r in res), adv if ok else None)
+
+    cpus = {}
     if with_cpu and d.rank == 0 and d.world == 1:
         from oracle import qref
 
-        g, m = gm
-        cpu = {}
-        for nt in (1, T):
-            b = qref.StepBatch(g, m)
-            tc, ne = 0.0, 0
-            for s in range(steps + STEP_WARM):   # timed: steps 1 .. cpu_steps; the rest
-                ev = events(s)                       # replayed for the final state
-                t0 = time.perf_counter()
-                b.step(*ev, nthreads=nt)
-                if 0 < s <= cpu_steps:
-                    tc += time.perf_counter() - t0
-                    ne += len(ev[2])
-            committed_cpu = [b.committed(i) for i in range(len(committed["host"]))]
+        _, counts = cpu_thread_counts()
+        cpus = {nt: [qref.StepBatch(g, m), [], []] for nt in counts}
+    prev_sum = int(g["committed"].sum(dtype=np.uint64))
+    rows.set(0)
+    for W in Ws:                       # step 0's streams (untimed)
+        for i in range(W):
+            encode(W, i, 0)
+    n_events = len(rows.ev)
+    timed = 0
+    for s in range(steps + STEP_WARM):
+        slot = s % 2
+        for nt, (b, ts, dg) in cpus.items():    # the CPU replay of the same rows
+            t0 = time.perf_counter()
+            tot = b.step(rows.groups, offsets, rows.ev, nthreads=nt)
+            dt = time.perf_counter() - t0
+            if s >= STEP_WARM:
+                ts.append(dt)
+            dg.append((tot["commits"], tot["ready"], tot["committed_sum"] - prev_sum))
+        if cpus:
+            prev_sum = tot["committed_sum"]
+        rows.set(s + 1)                # untimed: step s + 1's messages arrive
+        for W in Ws:
+            mo = modes[W]
+            if s >= STEP_WARM:
+                mo["bytes"] += sum(mo["nbytes"][slot])
+            j = jobs(W, slot, "dev")
+            d.barrier()
+            t0 = time.perf_counter()
+            res = j.run(copy=False)
+            dt = time.perf_counter() - t0
+            mo["check"]["dev"].append(digest(res))
+            j = jobs(W, slot, "e2e")
+            d.barrier()
+            t1 = time.perf_counter()
+            fut = pool.submit(j.run, False)
+            encs = [pool.submit(encode, W, i, 1 - slot) for i in range(W)]
+            for f in encs:
+                f.result()
+            res = fut.result()
+            dt2 = time.perf_counter() - t1
+            mo["check"]["e2e"].append(digest(res))
+            if s >= STEP_WARM:
+                mo["t"]["dev"].append(dt)
+                mo["t"]["e2e"].append(dt2)
+        if s >= STEP_WARM:
+            timed += 1
+    pool.shutdown()
+    committed = {}
+    for W in Ws:
+        for which in ("dev", "e2e"):
+            committed[(W, which)] = [int(modes[W][which][0].get_group(int(c))[0]["committed"])
+                                     for c in cids[:min(1024, G // W)]]
+            for wk in modes[W][which]:
+                wk.close()
+    pin.close()
+    ref = modes[1]["check"]["dev"]
+    same_modes = all(modes[W]["check"][k] == ref for W in Ws for k in ("dev", "e2e")) and \
+        len(set(map(tuple, committed.values()))) == 1
+    members = ", ".join(f"{roles.count(r)} {r}" for r in ("remote", "witness", "observer")
+                        if roles.count(r))
+    ev_total = n_events * timed
+
+    def rate(ts):
+        return d.sum(float(n_events * len(ts))) / d.max(sum(ts)) if ts else None
+
+    dev = {f"w{W}": rate(modes[W]["t"]["dev"]) for W in Ws}
+    e2e = {f"w{W}": rate(modes[W]["t"]["e2e"]) for W in Ws}
+    out = {
+        "workload": f"{name}: device step engine over {G} leader groups per GPU ({members}); per "
+                    f"group and step {nm - 1} ReplicateResp + {nm - 1} HeartbeatResp, 1 proposal, "
+                    f"1/4 local ReadIndex; {timed} timed steps",
+        "unit": "events/s",
+        "events_per_step": n_events,
+        "value": e2e["w16"], "ms_per_step": n_events / e2e["w16"] * 1e3 * d.world,
+        "median_ms_per_step": _median(modes[16]["t"]["e2e"]) * 1e3,
+        "end_to_end": e2e, "device_only": dev,
+        "ms_per_step_detail": {f"{k}_w{W}": {"mean": float(np.mean(modes[W]["t"][k]) * 1e3),
+                                             "median": _median(modes[W]["t"][k]) * 1e3,
+                                             "max": float(np.max(modes[W]["t"][k]) * 1e3)}
+                               for W in Ws for k in ("dev", "e2e")},
+        "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
+        "modes_agree": same_modes,
+        "note": "end_to_end: the producer's encode of step s + 1 (W threads) overlapped with the "
+                "device step s; device_only: the encoded stream given",
+    }
+    if cpus:
+        cpu = {str(nt): n_events * len(ts) / sum(ts) for nt, (_, ts, _) in cpus.items()}
+        best = max(cpu.values())
+        digs = [dg for _, _, dg in cpus.values()]
+        out["cpu_replay"] = dict(cpu, sample=f"the same rows of the same {timed} timed steps "
+                                             "replayed event by event (oracle/qref_step.c)")
+        out["parity_committed"] = bool(all(x == digs[0] for x in digs) and
+                                       [x[:2] for x in digs[0]] == [x[:2] for x in ref] and
+                                       all(a[2] == b[2] for a, b in zip(digs[0], ref)
+                                           if b[2] is not None) and same_modes)
+        out["vs_cpu_replay_end_to_end"] = {k: v / best for k, v in e2e.items()}
+        out["vs_cpu_replay_device_only"] = {k: v / best for k, v in dev.items()}
+        for b, _, _ in cpus.values():
             b.close()
-            cpu[nt] = ne / tc
-        out["cpu_reference"] = {
-            "value": cpu[T], "unit": "events/s", "threads": T, "single_thread_value": cpu[1],
-            "sample": f"the same events of the first {cpu_steps} steps, replayed event by "
-                      f"event (oracle/qref_step.c, C restatement of the reference path)",
-        }
-        # the same events left the same committed indexes
-        out["parity_committed"] = all(c == committed_cpu for c in committed.values())
-        for k in ("value", "two_workers", "concurrent_workers", "device_stream",
-                  "device_stream_concurrent",
-                  "device_rows", "device_rows_concurrent", "host_worker",
-                  "host_worker_concurrent"):
-            v = out.get(k)
-            v = v["value"] if isinstance(v, dict) else v
-            if v:
-                out.setdefault("vs_cpu_replay", {})[k] = v / cpu[T]
     return out
 
 
@@ -1194,13 +1292,40 @@ def full_size_parity(w, set0, nthreads):
     return res
 
 
-def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
-    """The oracle (C restatement of the reference path) on a bounded sample of the workload.
-    gpu_set0: the GPU's decisions of batch set 0 (run_gpu), compared bit for bit with the
-    oracle's on the same inputs at full size (full_size_parity)."""
+def host_cores():
+    """(CPUs the host shows, CPUs this process may run on, the cgroup CPU quota or None). On the
+    GPU box the first two show the whole machine while the quota is the box's share."""
+    visible = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = visible
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return visible, usable, quota
+
+
+def cpu_thread_counts():
+    """(all usable cores, the thread counts the CPU legs run at: all cores, 16 = the reference's
+    StepEngineWorkerCount (internal/settings/hard.go:35), 1)."""
+    _, usable, quota = host_cores()
+    allc = min(usable, quota) if quota else usable
+    return allc, sorted({allc, min(16, allc), 1}, reverse=True)
+
+
+def cpu_baseline(w, budget_s=9.0, gpu_set0=None):
+    """The oracle (C restatement of the reference path) on a bounded sample of the workload, on
+    all usable host cores, on 16 threads and on 1. gpu_set0: the GPU's decisions of batch set 0
+    (run_gpu), compared bit for bit with the oracle's on the same inputs at full size
+    (full_size_parity)."""
     from oracle import qref
 
-    host_threads = min(16, os.cpu_count() or 1)
+    host_threads, counts = cpu_thread_counts()
     G = min(w["G"], 1 << 20)
     s = qref.spec(SEED_BASE + w["cfg"], G, w["n"])
     out = {}
@@ -1215,16 +1340,17 @@ def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
         def one(nt):
             qref.readindex_batch(inp.ack, inp.n_voting, 0, nthreads=nt)
             qref.vote_batch(inp.granted, inp.rejected, inp.n_voting, 0, nthreads=nt)
-    for nt in (1, host_threads):
+    for nt in counts:
         passes, t0 = 0, time.perf_counter()
         while True:
             one(nt)
             passes += 1
             dt = time.perf_counter() - t0
-            if dt >= budget_s / 2:
+            if dt >= budget_s / len(counts):
                 break
         out[nt] = (passes * G * decisions_per_group(w) / dt, passes, dt)
-    rate, passes, dt = out[host_threads]
+    best = max(counts, key=lambda nt: out[nt][0])
+    rate, passes, dt = out[best]
     parity = full_size_parity(w, gpu_set0, host_threads) if gpu_set0 else None
     # BASELINE config C1: the reference's own CPU case, one group x 3 voters, tryCommit per step
     T = 4 << 20
@@ -1232,14 +1358,15 @@ def cpu_baseline(w, budget_s=8.0, gpu_set0=None):
     t0 = time.perf_counter()
     qref.c1_run(match, last, 1003, 1000)
     c1_s = time.perf_counter() - t0
+    visible, usable, quota = host_cores()
     return {
-        "value": rate, "unit": "decisions/s", "cores": host_threads, "kind": "port",
+        "value": rate, "unit": "decisions/s", "cores": best, "kind": "port",
         "sample": (f"{G} groups of the same workload and generator, {passes} passes in {dt:.1f} s "
-                   f"on {host_threads} host threads (oracle/qref.c -O3, C restatement of the "
-                   f"reference Go path; Go toolchain unavailable)"),
-        "single_thread_value": out[1][0],
+                   f"on {best} host threads (oracle/qref.c -O3, C restatement of the reference "
+                   f"Go path; Go toolchain unavailable)"),
+        "by_threads": {str(nt): out[nt][0] for nt in counts},
+        "host_cpus": {"visible": visible, "usable": usable, "cgroup_quota": quota},
         "c1_single_group_ns_per_trycommit": c1_s / T * 1e9,
-        "c1_sample": f"BASELINE config C1: 1 group x 3 voters, {T} sequential tryCommit steps",
         "parity_full_size": parity,
     }
 
@@ -1279,6 +1406,223 @@ def same_decisions(a, b):
                for p, q in zip(a, b))
 
 
+EXTRAS_MULTI = "c5tl,c5v5tl,c4p,cqp,rimt,ingo"
+
+
+def run_rank(args, d, progress):
+    """Everything one rank measures: the headline, the extra legs, and (rank 0 at N = 1) the CPU
+    baseline. Every rank runs the same legs in the same order (their collectives pair up)."""
+    w = WORKLOADS[args.workload]
+    progress(f"headline {args.workload}: {args.steps} steps, {args.warmup} warmup")
+    r = run_gpu(w, args.steps, args.warmup, d)
+    r["world"] = d.world
+    from dragonboat_amd import hipquorum as hq
+
+    devices = d.gather_obj({"rank": d.rank, "device": d.device,
+                            "pci_bus_id": hq.device_pci_bus_id(d.device)})
+    host_threads, _ = cpu_thread_counts()
+    oracle_here = d.rank == 0 and d.world == 1 and not args.no_cpu
+    extra_names = args.extra if args.extra is not None else (
+        DEFAULT_EXTRAS if d.world == 1 else EXTRAS_MULTI)
+    records, extra_runs = [], {}
+    for name in [x for x in extra_names.split(",") if x and x != args.workload]:
+        we = WORKLOADS.get(name)
+        if we is not None and we.get("mixed") and d.world % 3 == 0:
+            # voter-count buckets need gcd(3, world) == 1 (shard.rank_bucket); same on every rank
+            records.append({"name": name, "skipped": "world size divisible by 3"})
+            continue
+        progress(f"extra {name}")
+        try:
+            if name == "e2e":
+                rec = run_e2e(max(100, args.steps // 4), 5, d)   # >= 30 ms timed per variant
+            elif name == "wire":
+                rec = run_wire_leg(d)
+            elif name in STEP_ROLES:
+                rec = run_step_leg(d, G=args.step_groups, steps=args.step_steps,
+                                   with_cpu=not args.no_cpu, name=name)
+            elif name in ("rim", "rimt", "cq", "cqp", "ing", "ingo", "ingu"):
+                rec = run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d)
+            elif name == "sweep":
+                rec = run_size_sweep(args.workload, max(50, args.steps // 4),
+                                     max(5, args.warmup // 4), d)
+            elif name.startswith("w") and name[1:].isdigit():
+                rec = run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:]))
+            else:
+                re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
+                re_["world"] = d.world
+                par = None
+                if oracle_here and re_.get("set0") and not args.no_extra_parity:
+                    par = full_size_parity(we, re_["set0"], host_threads)
+                rec = extra_record(name, we, re_, par)
+                extra_runs[name] = re_
+        except Exception as e:   # an extra leg never costs the headline line
+            log(f"extra leg {name} failed: {e!r}")
+            rec = {"error": repr(e)}
+        rec = dict(name=name, **rec)
+        records.append(rec)
+        if d.rank == 0:     # each leg's record as it lands (the final line only summarises it)
+            log("extra " + json.dumps(rec)[:4000])
+    cpu = None
+    if oracle_here:
+        progress("cpu baseline")
+        cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
+    # the term check of the same groups in its other exact forms (the ring gathers the north
+    # star names, the mask the headline streams): rate and whether every decision is identical
+    forms = []
+    for name in SAME_DATA_FORMS.get(args.workload, ()):
+        if name in extra_runs:
+            re_ = extra_runs[name]
+            forms.append({
+                "workload": name, "form": {0: "term_start", 1: "ring_u64", 2: "term_mask",
+                                           3: "ring_u32"}[WORKLOADS[name]["form"]]
+                + (" tiles" if WORKLOADS[name].get("tiled") else ""),
+                "value": re_["decisions"] / re_["elapsed"],
+                "frac": re_["achieved_node_gbs"] / (HBM_PEAK_GBS * d.world),
+                "equal": same_decisions(r.get("set0"), re_.get("set0")),
+            })
+    r.pop("set0", None)
+    return dict(r=r, devices=devices, records=records, cpu=cpu, forms=forms)
+
+
+def _short(rec):
+    """The few numbers of one extra record that the final line carries."""
+    if "error" in rec or "skipped" in rec:
+        return {k: str(rec.get(k))[:120] for k in ("error", "skipped") if k in rec}
+    out = {}
+    for k in ("value", "unit", "roofline_frac", "kernel_avg_us", "ms_per_step",
+              "median_ms_per_step", "aggregate_frac_of_peak", "fit_t0_us",
+              "fit_stream_frac_of_peak"):
+        v = rec.get(k)
+        if v is not None:
+            out[k] = round(v, 4) if isinstance(v, float) and abs(v) < 1e4 else (
+                float(f"{v:.4g}") if isinstance(v, float) else v)
+    par = rec.get("parity_full_size")
+    if isinstance(par, dict):
+        out["parity_equal"] = par.get("equal")
+    for k in ("end_to_end", "device_only", "cpu_replay", "vs_cpu_replay_end_to_end",
+              "vs_cpu_replay_device_only", "parity_committed", "modes_agree"):
+        if k in rec:
+            v = rec[k]
+            if isinstance(v, dict):
+                v = {a: (float(f"{b:.4g}") if isinstance(b, float) else b)
+                     for a, b in v.items() if not isinstance(b, (dict, list))}
+            out[k] = v
+    return out
+
+
+def report(args, d, res, launcher):
+    """Rank 0: the full record to a side file, ONE compact JSON line (<= 8 KB) to stdout."""
+    w = WORKLOADS[args.workload]
+    r = res["r"]
+    traffic, traffic_src = pmc_traffic(args.workload)
+    peak = HBM_PEAK_GBS * d.world
+    achieved = r["achieved_node_gbs"]
+    devs = res["devices"]
+    line = {
+        "metric": "quorum-commit decisions/sec (whole node) + % HBM roofline at 1/2/4/8 GPUs",
+        "value": r["decisions"] / r["elapsed"],
+        "unit": "decisions/s",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["elapsed"] / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": f"synthetic: device-generated splitmix64 batches, {r['nsets']} distinct per GPU "
+                f"rotated (>= 1.1 GiB); timed steps start at batch {r['first_timed_set']}",
+        "config": {
+            "workload": args.workload,
+            "desc": w["desc"],
+            "groups_per_gpu": w["G"], "voters": w["n"],
+            "form": ({0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
+                     + ("_lag" if w["kind"] == "lag" else ""))
+            if w["kind"] in ("commit", "lag") else "bitmaps",
+            "layout": ("tiles_leader" if w.get("lead") else "tiles") if w.get("tiled")
+            else "columns",
+            "global_groups_per_step": groups_per_step(w) * d.world,
+            "parallelism": f"shard{d.world} (clusterID % {d.world}, partition.go:38)",
+            "launcher": launcher,
+            "devices_seen": len({x["pci_bus_id"] or x["device"] for x in devs}),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+            "frac": achieved / peak, "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel_avg_us": r["avg_kernel_s"] * 1e6,
+            "algorithmic_bytes_per_launch": r["bytes_per_launch"],
+            "kernel_time": "HIP events on the launch stream around the timed launches "
+                           "(back to back), / launches",
+            "achieved_scope": f"sum over {d.world} GPU(s) of bytes per launch / kernel time",
+        },
+        "per_gpu": [{"rank": i, "device": devs[i]["device"], "pci": devs[i]["pci_bus_id"],
+                     "value": float(f"{v:.5g}"), "kernel_us": round(k, 3),
+                     "frac": round(a / HBM_PEAK_GBS, 4)}
+                    for i, (v, k, a) in enumerate(r["per_gpu"])],
+        "cpu_baseline": res["cpu"],
+        "term_check_forms_same_data": res["forms"],
+    }
+    summary = {rec["name"]: _short(rec) for rec in res["records"]}
+    detail = dict(line, result_gather=r.get("gather"), extra=res["records"])
+    path = args.detail_out
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(detail, f, indent=1)
+        line["detail_file"] = os.path.relpath(os.path.abspath(path), ROOT)
+    except OSError as e:
+        log(f"detail file not written: {e!r}")
+    line["extra"] = summary
+    text = json.dumps(line, separators=(",", ":"))
+    if len(text) > 8000:       # the driver parses this line: never let the summary break it
+        line["extra"] = {k: {kk: v.get(kk) for kk in ("value", "roofline_frac") if kk in v}
+                         for k, v in summary.items()}
+        text = json.dumps(line, separators=(",", ":"))
+    if len(text) > 8000:
+        line.pop("extra")
+        text = json.dumps(line, separators=(",", ":"))
+    print(text, flush=True)
+
+
+def main_threads(args, t_start):
+    """--gpus N with no launcher: N host threads in this process, thread i opens its contexts on
+    GPU i (i % visible GPUs when fewer are visible: a rehearsal), groups sharded clusterID % N."""
+    from dragonboat_amd import hipquorum as hq
+
+    ngpu = hq.device_count()
+    if ngpu < 1:
+        log("no GPU visible")
+        sys.exit(1)
+    if ngpu < args.gpus:
+        log(f"--gpus {args.gpus} with {ngpu} GPU(s) visible: ranks share GPUs (rehearsal)")
+    grp = ThreadGroup(args.gpus)
+    ds = [ThreadDist(grp, i, ngpu) for i in range(args.gpus)]
+    results, errors = [None] * args.gpus, []
+
+    def progress(msg):
+        log(f"[bench {time.perf_counter() - t_start:7.1f} s] {msg}")
+
+    def body(i):
+        try:
+            results[i] = run_rank(args, ds[i], progress if i == 0 else (lambda m: None))
+        except BaseException as e:    # one failed rank releases the others' barriers
+            errors.append((i, e))
+            grp.bar.abort()
+
+    threads = [threading.Thread(target=body, args=(i,), name=f"rank{i}")
+               for i in range(args.gpus)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        i, e = errors[0]
+        raise RuntimeError(f"rank {i} failed") from e
+    report(args, ds[0], results[0], f"threads: 1 process, {args.gpus} host threads, one hq_ctx "
+                                    f"per GPU ({ngpu} visible)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1286,140 +1630,35 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
     ap.add_argument("--step-groups", type=int, default=1 << 20,
-                    help="groups per GPU of the step-worker leg (extra 'step')")
+                    help="groups per GPU of the step-worker legs (extras 'step', 'step5')")
+    ap.add_argument("--step-steps", type=int, default=50,
+                    help="timed steps of the step-worker legs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra-parity", action="store_true",
                     help="skip the full-size oracle check of the commit / lag extras")
-    ap.add_argument("--extra", default=DEFAULT_EXTRAS,
-                    help="comma list of extra workloads reported under 'extra' ('' for none)")
+    ap.add_argument("--extra", default=None,
+                    help="comma list of extra legs ('' for none; default: all at N = 1, "
+                         f"{EXTRAS_MULTI} at N > 1)")
+    ap.add_argument("--detail-out", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="where the full record (every extra leg) is written")
     args = ap.parse_args()
-
+    t_start = time.perf_counter()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1:
+        main_threads(args, t_start)
+        return
     d = Dist()
     if args.gpus != d.world:
-        log(f"--gpus {args.gpus} but WORLD_SIZE={d.world}: launch N>1 with torch.distributed.run")
-        if d.world == 1 and args.gpus > 1:
-            sys.exit(2)
-    w = WORKLOADS[args.workload]
-    t_start = time.perf_counter()
+        log(f"--gpus {args.gpus} but WORLD_SIZE={d.world}: measuring WORLD_SIZE ranks")
 
     def progress(msg):          # one line per phase (a long run must keep writing)
         if d.rank == 0:
             log(f"[bench {time.perf_counter() - t_start:7.1f} s] {msg}")
 
-    progress(f"headline {args.workload}: {args.steps} steps, {args.warmup} warmup")
-    r = run_gpu(w, args.steps, args.warmup, d)
-    r["world"] = d.world
-    host_threads = min(16, os.cpu_count() or 1)
-    oracle_here = d.rank == 0 and d.world == 1 and not args.no_cpu
-    extras, extra_runs = [], {}
-    e2e = None
-    steps_legs = []
-    conc, kern = [], []
-    failed = []
-    for name in [x for x in args.extra.split(",") if x and x != args.workload]:
-        we = WORKLOADS.get(name)
-        if we is not None and we.get("mixed") and d.world % 3 == 0:
-            # voter-count buckets need gcd(3, world) == 1 (shard.rank_bucket); same on every rank
-            failed.append({"workload": name, "skipped": "world size divisible by 3"})
-            continue
-        progress(f"extra {name}")
-        try:
-            if name == "e2e":
-                e2e = run_e2e(max(100, args.steps // 4), 5, d)   # >= 30 ms timed per variant
-            elif name == "wire":
-                steps_legs.append(run_wire_leg(d))
-            elif name in STEP_ROLES:
-                steps_legs.append(run_step_leg(d, G=args.step_groups, with_cpu=not args.no_cpu,
-                                               name=name))
-            elif name in ("rim", "rimt", "cq", "cqp", "ing", "ingo", "ingu"):
-                kern.append(run_kernel_leg(name, max(50, args.steps // 4),
-                                           max(5, args.warmup // 4), d))
-            elif name == "sweep":
-                conc.append(run_size_sweep(args.workload, max(50, args.steps // 4),
-                                           max(5, args.warmup // 4), d))
-            elif name.startswith("w") and name[1:].isdigit():
-                conc.append(run_concurrent(w, args.steps, args.warmup, d, W=int(name[1:])))
-            else:
-                re_ = run_gpu(we, max(50, args.steps // 4), max(5, args.warmup // 4), d)
-                re_["world"] = d.world
-                par = None
-                if oracle_here and re_.get("set0") and not args.no_extra_parity:
-                    par = full_size_parity(we, re_["set0"], host_threads)
-                extras.append(extra_record(name, we, re_, par))
-                extra_runs[name] = re_
-        except Exception as e:   # an extra leg never costs the headline line
-            log(f"extra leg {name} failed: {e!r}")
-            failed.append({"workload": name, "error": repr(e)})
-    cpu = None
-    if oracle_here:
-        progress("cpu baseline")
-        cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
-    # the term check of the same groups in its other exact forms (the ring gathers the north
-    # star names, the mask the headline streams): rate and whether every decision is identical
-    forms_same_data = []
-    for name in SAME_DATA_FORMS.get(args.workload, ()):
-        if name in extra_runs:
-            re_ = extra_runs[name]
-            forms_same_data.append({
-                "workload": name, "form": WORKLOADS[name]["desc"],
-                "value": re_["decisions"] / re_["elapsed"],
-                "roofline_frac": re_["achieved_node_gbs"] / (HBM_PEAK_GBS * d.world),
-                "decisions_equal_to_headline": same_decisions(r.get("set0"), re_.get("set0")),
-            })
+    res = run_rank(args, d, progress)
     if d.rank == 0:
-        traffic, traffic_src = pmc_traffic(args.workload)
-        peak = HBM_PEAK_GBS * d.world
-        achieved = r["achieved_node_gbs"]
-        line = {
-            "metric": "quorum-commit decisions/sec (whole node) + % HBM roofline at 1/2/4/8 GPUs",
-            "value": r["decisions"] / r["elapsed"],
-            "unit": "decisions/s",
-            "n_gpus": d.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": r["elapsed"] / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic: device-generated splitmix64 batches (DESIGN.md), "
-                    f"{r['nsets']} distinct batches per GPU rotated (>= 1.1 GiB); the timed "
-                    f"steps start at batch {r['first_timed_set']}, after the warm-up's",
-            "config": {
-                "workload": f"{args.workload}: {w['desc']}",
-                "groups_per_gpu": w["G"], "voters": w["n"],
-                "form": ({0: "term_start", 1: "ring", 2: "term_mask", 3: "ring32"}[w["form"]]
-                         + ("_lag" if w["kind"] == "lag" else ""))
-                if w["kind"] in ("commit", "lag") else "bitmaps",
-                "layout": ("tiles_leader" if w.get("lead") else "tiles") if w.get("tiled")
-                else "columns",
-                "global_groups_per_step": w["G"] * d.world,
-                "parallelism": f"shard{d.world} (clusterID % {d.world})",
-                "world_size": d.world,
-                "backend": d.backend or "none (one process)",
-            },
-            "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                "frac": achieved / peak, "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel_avg_us": r["avg_kernel_s"] * 1e6,
-                "kernel_time": "HIP events on the launch stream: a region opened behind the first "
-                               "timed launch and closed behind the last one, / the launches in "
-                               "it (back-to-back kernels: duration + dependent-launch boundary)",
-                "algorithmic_bytes_per_launch": r["bytes_per_launch"],
-                "achieved_scope": f"node: sum over {d.world} GPU(s) of bytes per launch / "
-                                  "kernel time; peak = 8 TB/s x GPUs",
-                "measured_copy_ceiling_gbs": HBM_MEASURED_COPY_GBS * d.world,
-            },
-            "per_gpu": [{"rank": i, "decisions_per_s": v, "kernel_avg_us": k,
-                         "achieved_gbs": a, "frac": a / HBM_PEAK_GBS}
-                        for i, (v, k, a) in enumerate(r["per_gpu"])],
-            "result_gather": r["gather"],
-            "cpu_baseline": cpu,
-            "term_check_forms_same_data": forms_same_data,
-            "extra": extras + kern + conc + ([e2e] if e2e else []) + steps_legs + failed,
-        }
-        print(json.dumps(line), flush=True)
+        report(args, d, res, "one process" if d.world == 1 else
+               f"torch.distributed.run: {d.world} processes, {d.backend}")
     d.close()
 
 

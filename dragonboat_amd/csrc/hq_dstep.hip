@@ -470,6 +470,11 @@ struct Engine {
                 defer(e);
             }
         }
+        // a group that took all its events must have used all its bytes: left-over bytes mean the
+        // sizes were split wrongly between groups, which the host decoder rejects as HQ_E_INVAL
+        // (hq_stream.cpp); pass A makes it an input error, so no state is written
+        if (STREAM && !WRITE && !(g.flags & kDSuspended) && br.p != br.end)
+            atomicOr(a.error, (uint32_t)kErrBoffsets);
         if (!WRITE && g.committed - committed0 > 0xFFFFFFFFull && a.wide)
             atomicOr(a.wide, 1u);                        // no 4-byte advance column this step
         if (WRITE && a.layout->commit_column == kColumn32) {   // every listed group's word
@@ -602,7 +607,6 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
     lay->commit_column = (allow_column & kColumn32) && !*wide && 4 * (uint64_t)commits > n
                              ? kColumn32
                          : (allow_column & kColumn64) && 2 * (uint64_t)commits > n ? kColumn64 : 0;
-    *wide = 0;
     for (int l = 0; l < kLists; ++l) {
         const uint32_t len = scan[(uint64_t)(l + 1) * nw] - scan[(uint64_t)l * nw];
         lay->off[l] = total;
@@ -615,7 +619,13 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
     lay->total = total;
     lay->error = *error;
     lay->overflow = total > cap;
-    *error = 0;
+    // pass A's flags are reset for the next step, except when the host will grow the region and
+    // run this layout again for the same step (overflow without an input error): the re-run must
+    // see the same flags, or it could choose the 4-byte advance column for a 2^32 advance
+    if (!(lay->overflow && !*error)) {
+        *error = 0;
+        *wide = 0;
+    }
 }
 
 uint64_t now_ns() {

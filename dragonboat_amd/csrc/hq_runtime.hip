@@ -74,6 +74,31 @@ int hq_device_count(int *out) {
     return HQ_OK;
 }
 
+int hq_device_pci_bus_id(int device, char *out, int len) {
+    if (!out || len < 13) return HQ_E_INVAL;   // "dddd:bb:dd.f" + NUL
+    out[0] = '\0';
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return HQ_E_DEVICE;
+    if (device < 0 || device >= n) return HQ_E_INVAL;
+    return hipDeviceGetPCIBusId(out, len, device) == hipSuccess ? HQ_OK : HQ_E_DEVICE;
+}
+
+int hq_pointer_kind(const void *p, int *kind) {
+    if (!kind) return HQ_E_INVAL;
+    *kind = HQ_PTR_UNREGISTERED;
+    if (!p) return HQ_OK;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable host memory reports an error: clear it
+        return HQ_OK;
+    }
+    if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged)
+        *kind = HQ_PTR_DEVICE;
+    else if (at.type == hipMemoryTypeHost)
+        *kind = HQ_PTR_PINNED_HOST;
+    return HQ_OK;
+}
+
 int hq_open(int device, uint32_t flags, hq_ctx **out) {
     (void)flags;
     if (!out) return hq::fail(nullptr, HQ_E_INVAL, "hq_open: out is NULL");

@@ -881,8 +881,9 @@ int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
         return fail(HQ_E_INVAL, e & 1 ? "hq_worker_step: unknown group handle"
                                 : e & 8 ? "hq_worker_step: a group is listed twice"
                                 : e & 2 ? "hq_worker_step: offsets decrease"
-                                        : "hq_worker_step_stream: boffsets decrease or out of range, or sizes "
-                                          "not summing to the totals");
+                                        : "hq_worker_step_stream: boffsets decrease or out of range, sizes "
+                                          "not summing to the totals, or a group's bytes not used up by its "
+                                          "events (malformed event stream)");
     }
     rc = hq(rc, "hq_dstep_run");
     if (rc) return rc;

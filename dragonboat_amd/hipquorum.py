@@ -40,7 +40,7 @@ HQ_INGEST_UNIQUE = 2         # hq_table_*: every key at most once in the batch
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 11
+HQ_ABI_VERSION = 12
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -225,6 +225,8 @@ class StepOutput(ctypes.Structure):
 SIGNATURES = {
     "hq_abi_version": (ctypes.c_int, []),
     "hq_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "hq_device_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "hq_pointer_kind": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "hq_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp)]),
     "hq_close": (None, [_vp]),
     "hq_last_error": (ctypes.c_char_p, [_vp]),
@@ -393,6 +395,25 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     lib.hq_device_count(ctypes.byref(n))
     return n.value
+
+
+HQ_PTR_UNREGISTERED, HQ_PTR_PINNED_HOST, HQ_PTR_DEVICE = 0, 1, 2
+
+
+def pointer_kind(a) -> int:
+    """hq_pointer_kind of a numpy array's data (or a raw address / DeviceArray)."""
+    p = a.ctypes.data if isinstance(a, np.ndarray) else getattr(a, "ptr", a)
+    k = ctypes.c_int(0)
+    _chk(lib.hq_pointer_kind(p, ctypes.byref(k)), "hq_pointer_kind")
+    return k.value
+
+
+def device_pci_bus_id(device: int) -> str:
+    """hq_device_pci_bus_id: the PCI bus id of visible GPU `device` ("" if it has none)."""
+    buf = ctypes.create_string_buffer(64)
+    if lib.hq_device_pci_bus_id(device, buf, len(buf)) != HQ_OK:
+        return ""
+    return buf.value.decode()
 
 
 @dataclass
@@ -1415,6 +1436,22 @@ def encode_events_sized(offsets, events):
                                     _p(out), len(out), _p(sizes), ctypes.byref(nb)),
          "hq_events_encode_sized")
     return out[:nb.value].copy(), sizes
+
+
+def encode_events_sized_into(offsets, events, out: np.ndarray, sizes: np.ndarray) -> int:
+    """hq_events_encode_sized into caller buffers (a producer writing the stream straight into
+    its pinned receive buffer): `out` uint8, `sizes` uint32 of len(offsets) - 1, both contiguous.
+    Returns the stream's byte count; raises HQError(HQ_E_STATE) when `out` cannot hold it (the
+    encoder wants HQ_EVENT_STREAM_MAX bytes free before each event)."""
+    n = len(offsets) - 1
+    assert offsets.dtype == np.uint64 and events.dtype == EVENT_DTYPE
+    assert out.dtype == np.uint8 and sizes.dtype == np.uint32 and len(sizes) >= n
+    assert offsets.flags.c_contiguous and events.flags.c_contiguous and out.flags.c_contiguous
+    nb = ctypes.c_uint64(0)
+    _chk(lib.hq_events_encode_sized(n, _p(offsets), _p(events) if len(events) else None,
+                                    _p(out), len(out), _p(sizes), ctypes.byref(nb)),
+         "hq_events_encode_sized")
+    return nb.value
 
 
 def decode_events(offsets, boffsets, data):

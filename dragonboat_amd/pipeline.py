@@ -50,7 +50,10 @@ class HostFedPipeline:
         zero_copy: no copies at all — the append / ingest kernels read the caller's pinned records
         over PCIe and the decision writes the changed / fallback bitmaps and the committed column
         straight into this slot's pinned result buffers (``depth`` result slots), every step on
-        one stream: no copy engine and no cross-stream wait is involved."""
+        one stream: no copy engine and no cross-stream wait is involved. The records must then be
+        pinned host (``Context.pinned``) or device memory (``step`` raises ValueError otherwise,
+        instead of letting a kernel fault on pageable memory), and they must stay unmodified until
+        that step's ``results`` / ``sync`` returns: the kernels read them asynchronously."""
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.zero_copy = zero_copy
@@ -154,6 +157,10 @@ class HostFedPipeline:
         if self.zero_copy:
             x = self.ctxs[0]
             app, upd = appends[:w * n_appends], updates[:w * n_updates]
+            for name, arr, cnt in (("appends", app, n_appends), ("updates", upd, n_updates)):
+                if cnt and hq.pointer_kind(arr) == hq.HQ_PTR_UNREGISTERED:
+                    raise ValueError(f"zero_copy: {name} must be pinned host or device memory "
+                                     "(Context.pinned), not pageable host memory")
             if self.compact:
                 if n_appends:
                     x.table_append_count_dev(app, n_appends, self.tiles, G, n, f, self.R,

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 11
+#define HQ_ABI_VERSION 12
 
 /* status codes */
 #define HQ_OK          0
@@ -93,6 +93,18 @@ typedef struct hq_ctx hq_ctx;
 int hq_abi_version(void);
 /* Number of visible GPUs. */
 int hq_device_count(int *out);
+/* PCI bus id ("dddd:bb:dd.f", NUL-terminated, len >= 13) of visible GPU `device`: lets a host
+ * that opens one context per GPU (partition.go:38 sharding) show which physical
+ * devices did the work. */
+int hq_device_pci_bus_id(int device, char *out, int len);
+/* What a pointer is to the GPU: HQ_PTR_PINNED_HOST (hq_alloc_pinned / hipHostMalloc memory, which
+ * kernels may read and write over PCIe), HQ_PTR_DEVICE, or HQ_PTR_UNREGISTERED (pageable host
+ * memory, NULL or unknown: a kernel touching it faults). Lets a zero-copy caller refuse ordinary
+ * host arrays with an error instead of a GPU memory fault. */
+#define HQ_PTR_UNREGISTERED 0
+#define HQ_PTR_PINNED_HOST 1
+#define HQ_PTR_DEVICE 2
+int hq_pointer_kind(const void *p, int *kind);
 /* Open a context (one HIP stream) on GPU `device`. flags: reserved, pass 0. */
 int hq_open(int device, uint32_t flags, hq_ctx **out);
 /* Destroy a context; waits for its stream. NULL is a no-op. */
@@ -913,7 +925,11 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
  *                     the followers of a steady leader ack the same index), 5 HeartbeatResp
  *                     whose hint / hint_high repeat the group's previous HeartbeatResp in the
  *                     stream (0 / 0 before the first: ctx-less acks and every follower's ack of
- *                     the same ctx), 7 another type (its varint follows)
+ *                     the same ctx), 7 another type (its varint follows). "Previous" counts
+ *                     only events written with codes 0 / 4 (ReplicateResp) and 2 / 5
+ *                     (HeartbeatResp): a ReplicateResp or HeartbeatResp written with code 7 does
+ *                     not set the index / ctx that a later code 4 / 5 repeats (the encoder never
+ *                     writes those two types with code 7)
  *           bit 6     reject
  *           bit 7     term repeats the group's previous message term in the stream (0 before
  *                     its first message): the term varint is left out

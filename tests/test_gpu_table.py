@@ -272,6 +272,31 @@ def test_host_fed_pipeline_matches_oracle(hq, depth, compact, grouped, zero_copy
     p.close()
 
 
+def test_zero_copy_pipeline_refuses_pageable_records(hq):
+    """zero_copy kernels read the records over PCIe: ordinary numpy (pageable) arrays are
+    refused with ValueError before any launch, pinned ones are accepted (hq_pointer_kind)."""
+    from dragonboat_amd.pipeline import HostFedPipeline
+
+    G, n = 4096, 3
+    p = HostFedPipeline(0, G, n, 16, 16, depth=1, compact=True, zero_copy=True)
+    try:
+        c = p.ctxs[0]
+        z = np.zeros(16, np.uint64)
+        assert hq.pointer_kind(z) == hq.HQ_PTR_UNREGISTERED
+        pz = c.pinned(16, np.uint64)
+        pz[:] = 0
+        assert hq.pointer_kind(pz) == hq.HQ_PTR_PINNED_HOST
+        assert hq.pointer_kind(p.tiles) == hq.HQ_PTR_DEVICE
+        with pytest.raises(ValueError, match="pinned"):
+            p.step(0, z, 1, pz, 0)
+        with pytest.raises(ValueError, match="pinned"):
+            p.step(0, pz, 0, z, 1)
+        p.step(0, pz, 0, pz, 0)     # no records: nothing to check, the decision still runs
+        p.results(0)
+    finally:
+        p.close()
+
+
 def test_pipeline_surfaces_fallback_groups(hq):
     """Appends that push lastIndex - committed past the mask's 16 indexes leave those groups
     undecided: the pipeline returns their fallback bits (equal to the oracle's), the caller

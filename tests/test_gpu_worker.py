@@ -301,7 +301,10 @@ def test_sized_input_errors_leave_state(hq, on_device):
                 ([1, 1], sizes, 2, data, "listed twice"),
                 ([0, 1], sizes, 3, data, "sizes"),                        # events total
                 ([0, 1], sizes, 2, np.concatenate([data, data[:1]]), "sizes"),   # bytes total
-                ([0, 1], [1 | 4 << 16, 1 | 5 << 16], 2, data, "sizes")):
+                ([0, 1], [1 | 4 << 16, 1 | 5 << 16], 2, data, "sizes"),
+                # totals right, split wrong: group 0 keeps a byte of group 1's event (the host
+                # decoder's p != end; the device engine's left-over-bytes check, pass A)
+                ([0, 1], [1 | 5 << 16, 1 | 3 << 16], 2, data, "malformed")):
             with pytest.raises(hq.HQError, match=msg):
                 w.step_sized(np.array(grp, np.uint32), np.array(z, np.uint32), ne, d)
             assert w.get_group(1)[0]["committed"] == 5 and w.get_group(2)[0]["committed"] == 5
@@ -337,6 +340,48 @@ def test_sized_stream_implicit_handles(hq, on_device):
         assert a.get_group(G)[0]["committed"] == b.get_group(G)[0]["committed"]
         with pytest.raises(hq.HQError):                  # more sizes than groups on the worker
             a.step_sized(None, np.zeros(G + 1, np.uint32), 0, np.zeros(0, np.uint8))
+    finally:
+        a.close()
+        b.close()
+
+
+def test_wide_advance_survives_output_regrow(hq):
+    """HQ_WORKER_COMMIT_ADVANCE with a committed index that moves by 2^33 in a step whose lists
+    overflow the pinned output region: the region is grown and the layout run again, and the
+    re-run must keep pass A's "wide" flag (the 4-byte advance column would truncate 2^33 to 0).
+    Worker a's region is sized by a first step listing one group; b's by a first step listing
+    all of them (no overflow). Both must return the same 8-byte commit column."""
+    import bench
+
+    G, big, special = 8192, 1 << 33, 5
+    roles = bench.STEP_ROLES["step"]
+    g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
+    g["committed"] -= np.uint64(10)                  # the step's acks of lastIndex commit
+    g["term_start"] = g["committed"]
+    m["match"][m["node_id"] != 1] -= np.uint64(10)
+    g["last_index"][special] = big                   # this group commits 2^33 - 990 at once
+    m["match"][len(roles) * special] = big           # the leader's own match = lastIndex
+    grp, off, ev = bench.step_events(hq, G, 0, roles)
+    rows = ev[int(off[special]):int(off[special + 1])]
+    rows["log_index"][(rows["kind"] == hq.EV_MESSAGE) & (rows["type"] == 13)] = big
+    ev[int(off[special]):int(off[special + 1])] = rows
+    data, sizes = hq.encode_events_sized(off, ev)
+    nv = sum(r != "observer" for r in roles)
+    a = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True)
+    b = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True)
+    try:
+        a.add_groups(g, m)
+        b.add_groups(g, m)
+        empty = np.zeros(0, np.uint8)
+        a.step_sized(np.array([0], np.uint32), np.zeros(1, np.uint32), 0, empty)
+        b.step_sized(grp, np.zeros(G, np.uint32), 0, empty)
+        got = a.step_sized(grp, sizes, len(ev), data)
+        want = b.step_sized(grp, sizes, len(ev), data)
+        assert len(got["ready"]) == G // 4 and 32 * (G // 4) > 1 << 16   # lists overflow a
+        assert "committed_advance" not in got and "committed_advance" not in want
+        np.testing.assert_array_equal(got["committed_column"], want["committed_column"])
+        assert int(got["committed_column"][special]) == big
+        assert a.get_group(int(cids[special]))[0]["committed"] == big
     finally:
         a.close()
         b.close()

@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU-box session of round 3: parity tests, smoke, the default bench line, then rocprofv3
+# evidence of the headline (kernel trace + one PMC pass per counter). Stops at the first
+# fault / timeout / abort; a plain test failure (pytest exit 1) still lets the bench run.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 3 "gpurun_out/$name.log" | cut -c1-400
+  return $rc
+}
+fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  rc=$?; if fatal $rc; then exit $rc; fi
+  step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
+  rc=$?; if fatal $rc; then exit $rc; fi
+fi
+if [ "${SKIP_BENCH:-0}" != 1 ]; then
+  step bench 600 python -u bench.py ${BENCH_ARGS:-}
+  rc=$?; if fatal $rc; then exit $rc; fi
+  tail -n 1 gpurun_out/bench.log | wc -c
+fi
+# launcher-free multi-GPU path, rehearsed with two host threads (two contexts on one GPU)
+if [ "${REHEARSE:-1}" = 1 ]; then
+  step bench_n2_threads 300 python -u bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu \
+    --extra c5v5tl,c4p,cqp --detail-out gpurun_out/bench_n2_detail.json
+  rc=$?; if fatal $rc; then exit $rc; fi
+fi
+for W in ${PROFILE:-}; do
+  step prof_$W 400 bash tools/profile_bench.sh $W || exit $?
+done
