@@ -33,6 +33,11 @@ struct hq_ctx {
     // device workspace for the host-pointer entry points
     void *ws = nullptr;
     size_t ws_bytes = 0;
+    // device workspace of the binned table ingest (hq_table.hip): the chunks' binned records
+    // and their per-bucket offsets; chunks per launch (HQ_BIN_LAUNCH_CHUNKS at hq_open: tests)
+    void *bin_ws = nullptr;
+    size_t bin_ws_bytes = 0;
+    uint32_t bin_launch_chunks = 4096;
     // host readback of the fallback count (hq_commit etc.)
 };
 

@@ -116,6 +116,10 @@ int hq_open(int device, uint32_t flags, hq_ctx **out) {
         if (v == 256 || v == 512 || v == 1024) ctx->bits_block = v;
     }
     if (const char *r = std::getenv("HQ_RI_PAIRS")) ctx->ri_pairs = std::atoi(r) != 0;
+    if (const char *c = std::getenv("HQ_BIN_LAUNCH_CHUNKS")) {
+        const int v = std::atoi(c);
+        if (v >= 1 && v <= 4096) ctx->bin_launch_chunks = (uint32_t)v;
+    }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -135,6 +139,7 @@ void hq_close(hq_ctx *ctx) {
     if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->bin_ws) (void)hipFree(ctx->bin_ws);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -222,6 +222,227 @@ __global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uin
     }
 }
 
+// ---------------------------------------------------------------- binned ingest ---------------
+// Records in any order, many per table slot (HQ_INGEST_BINNED, chosen by default for dense
+// batches): a random 8-byte read-modify-write or 64-bit atomic per record moves whole lines at
+// the memory side's random-access rate (one atomic per record: 10 % of HBM peak). Two streaming
+// passes instead, no global atomics:
+//   k_bin    each workgroup takes a chunk of kBinChunk records, counts them per bucket (a bucket =
+//            2^tpb_shift consecutive tiles) in LDS, and writes the chunk back bucket by bucket as
+//            8-byte entries (bucket-local key << 48 | index or lag), with each bucket's offset and
+//            count in the chunk (meta[chunk][bucket]);
+//   k_apply  one workgroup per bucket loads the bucket's match rows (and, for lags, its
+//            lastIndex row) into LDS, applies every chunk's entries of the bucket with LDS 64-bit
+//            max, and writes the rows back: every table line is read and written once per launch.
+// The max commutes, so the result equals the sequential application in any order. Indexes of 2^48
+// or more (never a real log index) do not fit an entry: k_bin applies those few with a global
+// atomic, which k_apply's later read of the row sees (kernel boundary).
+constexpr int kBinThreads = 1024;
+constexpr int kBinPer = 8;                                        // records per thread and chunk
+constexpr uint64_t kBinChunk = (uint64_t)kBinThreads * kBinPer;   // 8192 records per workgroup
+constexpr uint32_t kBinMaxBuckets = 8192;                         // k_bin: 64 KB + 8 B per bucket
+constexpr uint32_t kBinLds = 160 * 1024;                          // LDS a workgroup may declare
+
+struct BinK {
+    uint64_t *ent;       // [chunk][kBinChunk] entries, bucket order inside a chunk
+    uint32_t *meta;      // [chunk][B]: offset | count << 16 of the bucket in the chunk
+    uint64_t ntiles;
+    uint32_t B;          // buckets
+    uint32_t tpb_shift;  // tiles per bucket = 1 << tpb_shift
+    uint32_t rows;       // LDS rows per tile in k_apply: the match rows (+ lastIndex for lags)
+    uint32_t nchunks;    // chunks of this launch
+};
+
+// exclusive scan of n (<= 8192) u32 counts in LDS into out (may not alias), block-wide; returns
+// the total to every thread. Every thread must call it.
+template <int T>
+__device__ uint32_t block_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *wtot) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t per = (n + T - 1) / T, b0 = tid * per, b1 = min(b0 + per, n);
+    uint32_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += in[b];
+    uint32_t x = s;                              // inclusive scan over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0u;
+    }
+    if (lane == 63) wtot[wv] = x;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (uint32_t w = 0; w < T / 64; ++w) {
+        const uint32_t v = wtot[w];
+        wbase += w < wv ? v : 0u;
+        total += v;
+    }
+    uint32_t run = wbase + x - s;
+    for (uint32_t b = b0; b < b1; ++b) {
+        out[b] = run;
+        run += in[b];
+    }
+    __syncthreads();                             // wtot may be reused after the call
+    return total;
+}
+
+template <bool LAG>
+__global__ __launch_bounds__(kBinThreads) void k_bin(const uint64_t *u, uint64_t count, TableK t,
+                                                     BinK bk, uint64_t *n_skipped) {
+    extern __shared__ uint64_t lds[];
+    uint64_t *stage = lds;                                           // kBinChunk entries
+    uint32_t *hist = reinterpret_cast<uint32_t *>(lds + kBinChunk);  // [B]
+    uint32_t *hoff = hist + bk.B;                                    // [B]
+    uint32_t *wtot = hoff + bk.B;                                    // [16]
+    const uint32_t tid = threadIdx.x;
+    const uint64_t k = blockIdx.x, base = k * kBinChunk;
+    for (uint32_t b = tid; b < bk.B; b += kBinThreads) hist[b] = 0;
+    __syncthreads();
+    constexpr int SH = LAG ? 4 : 8;
+    uint64_t key[kBinPer], v[kBinPer];
+    uint32_t bb[kBinPer], rk[kBinPer];
+    // every record load first (kBinPer in flight per lane)
+#pragma unroll
+    for (int r = 0; r < kBinPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kBinThreads + tid;
+        key[r] = ~0ull;
+        v[r] = 0;
+        if (i < count) {
+            if constexpr (LAG) {
+                const uint64_t x = __builtin_nontemporal_load(u + i);
+                key[r] = x >> 28;                      // group << 4 | slot
+                v[r] = x & 0x0FFFFFFFull;              // lag
+            } else {
+                const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u) + i);
+                key[r] = x.x;
+                v[r] = x.y;                            // index
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kBinPer; ++r) {
+        const bool in = base + (uint64_t)r * kBinThreads + tid < count;
+        const uint64_t g = key[r] >> SH, s = key[r] & ((1u << SH) - 1);
+        const bool ok = in && g < t.G && s >= 1 && s <= t.nr;
+        count_skip(n_skipped, in && !ok);
+        bb[r] = 0xFFFFFFFFu;
+        rk[r] = 0;
+        if (!ok) continue;
+        if (!LAG && (v[r] >> 48)) {                    // no room in an entry: applied now
+            atomicMax(reinterpret_cast<unsigned long long *>(trow(t, g, (uint32_t)s - 1)),
+                      (unsigned long long)v[r]);
+            continue;
+        }
+        const uint32_t b = (uint32_t)((g >> 7) >> bk.tpb_shift);
+        const uint64_t lg = g - ((uint64_t)b << (7 + bk.tpb_shift));
+        v[r] |= (lg << 3 | (s - 1)) << 48;             // the entry
+        bb[r] = b;
+        rk[r] = atomicAdd(&hist[b], 1u);               // LDS
+    }
+    __syncthreads();
+    const uint32_t total = block_scan<kBinThreads>(hist, hoff, bk.B, wtot);
+    for (uint32_t b = tid; b < bk.B; b += kBinThreads)
+        bk.meta[k * bk.B + b] = hoff[b] | hist[b] << 16;
+#pragma unroll
+    for (int r = 0; r < kBinPer; ++r)
+        if (bb[r] != 0xFFFFFFFFu) stage[hoff[bb[r]] + rk[r]] = v[r];
+    __syncthreads();
+    uint64_t *dst = bk.ent + base;
+    for (uint32_t j = 2 * tid; j < total; j += 2 * kBinThreads) {
+        if (j + 1 < total) {
+            u64x2 x;
+            x.x = stage[j];
+            x.y = stage[j + 1];
+            *reinterpret_cast<u64x2 *>(dst + j) = x;
+        } else {
+            dst[j] = stage[j];
+        }
+    }
+}
+
+template <bool LAG>
+__global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64_t *n_skipped) {
+    extern __shared__ uint64_t lds[];
+    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    const uint64_t tile0 = (uint64_t)b << bk.tpb_shift;
+    const uint32_t nt = (uint32_t)min((uint64_t)1 << bk.tpb_shift, bk.ntiles - tile0);
+    const uint32_t R = bk.rows;
+    uint64_t *rows = lds;                                                    // [nt][R][128]
+    uint32_t *P = reinterpret_cast<uint32_t *>(lds + ((size_t)R << (7 + bk.tpb_shift)));
+    uint32_t *cnt = P + bk.nchunks + 1;                                      // [nchunks]
+    uint16_t *O = reinterpret_cast<uint16_t *>(cnt + bk.nchunks);           // [nchunks]
+    uint32_t *wtot = reinterpret_cast<uint32_t *>(O + ((bk.nchunks + 1) & ~1u));
+    // the bucket's rows: tile-major, row r < nr = match slot r + 1, row nr = lastIndex (lags)
+    const uint32_t pairs = nt * R * 64;
+    for (uint32_t w = tid; w < pairs; w += kBinThreads) {
+        const uint32_t tl = w / (R * 64), r = (w / 64) % R, x = 2 * (w % 64);
+        const uint32_t src = r < t.nr ? r : t.nr + 1;
+        const u64x2 v = *reinterpret_cast<const u64x2 *>(t.tiles + (tile0 + tl) * t.tw +
+                                                         (uint64_t)src * kT + x);
+        rows[(tl * R + r) * kT + x] = v.x;
+        rows[(tl * R + r) * kT + x + 1] = v.y;
+    }
+    for (uint32_t c = tid; c < bk.nchunks; c += kBinThreads) {
+        const uint32_t m = bk.meta[(uint64_t)c * bk.B + b];
+        cnt[c] = m >> 16;
+        O[c] = (uint16_t)(m & 0xFFFFu);
+    }
+    __syncthreads();
+    const uint32_t total = block_scan<kBinThreads>(cnt, P, bk.nchunks, wtot);
+    if (tid == 0) P[bk.nchunks] = total;
+    __syncthreads();
+    // kBinPer entries per thread and round: every entry load issued before the first LDS max
+    for (uint32_t j0 = 0; j0 < total; j0 += kBinThreads * 8) {
+        uint64_t ent[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint32_t j = j0 + (uint32_t)r * kBinThreads + tid;
+            ent[r] = ~0ull;
+            if (j < total) {
+                uint32_t lo = 0, hi = bk.nchunks;     // the chunk c with P[c] <= j < P[c + 1]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (P[mid] <= j) lo = mid;
+                    else hi = mid;
+                }
+                ent[r] = __builtin_nontemporal_load(bk.ent + (uint64_t)lo * kBinChunk + O[lo] +
+                                                    (j - P[lo]));
+            }
+        }
+        bool skip[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            skip[r] = false;
+            if (ent[r] == ~0ull) continue;
+            const uint32_t lk = (uint32_t)(ent[r] >> 48);
+            uint64_t v = ent[r] & 0xFFFFFFFFFFFFull;
+            const uint32_t gl = lk >> 3, s1 = lk & 7, tl = gl >> 7;
+            const uint32_t pos = (uint32_t)tpos(gl & 127);
+            if constexpr (LAG) {
+                const uint64_t last = rows[(tl * R + t.nr) * kT + pos];
+                if (v > last) {                         // an ack above lastIndex: skipped
+                    skip[r] = true;
+                    continue;
+                }
+                v = last - v;
+            }
+            atomicMax(reinterpret_cast<unsigned long long *>(rows + (tl * R + s1) * kT + pos),
+                      (unsigned long long)v);
+        }
+        if constexpr (LAG) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) count_skip(n_skipped, skip[r]);
+        }
+    }
+    __syncthreads();
+    const uint32_t mpairs = nt * t.nr * 64;          // the match rows back
+    for (uint32_t w = tid; w < mpairs; w += kBinThreads) {
+        const uint32_t tl = w / (t.nr * 64), r = (w / 64) % t.nr, x = 2 * (w % 64);
+        u64x2 v;
+        v.x = rows[(tl * R + r) * kT + x];
+        v.y = rows[(tl * R + r) * kT + x + 1];
+        *reinterpret_cast<u64x2 *>(t.tiles + (tile0 + tl) * t.tw + (uint64_t)r * kT + x) = v;
+    }
+}
+
 // one group's append of its run: lastIndex raised to new_last (16-byte form) or advanced by n
 // (count form); the term-mask bits of the new entries set
 template <bool COUNT>
@@ -326,7 +547,7 @@ int table_k(hq_ctx *ctx, const char *what, uint64_t *tiles, uint64_t G, uint32_t
     if (form == HQ_FORM_TERM_MASK &&
         (ring_len < 1 || ring_len > 16 || (ring_len & (ring_len - 1))))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": ring_len must be a power of two <= 16");
-    if (flags & ~(HQ_INGEST_GROUPED | HQ_INGEST_UNIQUE))
+    if (flags & ~(HQ_INGEST_GROUPED | HQ_INGEST_UNIQUE | HQ_INGEST_ATOMIC | HQ_INGEST_BINNED))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": unknown flags");
     t.tiles = tiles;
     t.G = G;
@@ -336,6 +557,111 @@ int table_k(hq_ctx *ctx, const char *what, uint64_t *tiles, uint64_t G, uint32_t
     t.mask = form == HQ_FORM_TERM_MASK;
     t.flags = flags;
     return HQ_OK;
+}
+
+// The binned ingest's geometry for this batch, or false when the table is too large for it
+// (more buckets than k_bin's LDS counts hold).
+bool bin_plan(const hq_ctx *ctx, const TableK &t, uint64_t count, bool lag, BinK &bk,
+              size_t &lds_bin, size_t &lds_apply, size_t &ws) {
+    bk.ntiles = (t.G + kT - 1) / kT;
+    bk.rows = t.nr + (lag ? 1u : 0u);
+    const uint64_t chunks = (count + kBinChunk - 1) / kBinChunk;
+    bk.nchunks = (uint32_t)std::min<uint64_t>(chunks, ctx->bin_launch_chunks);
+    // k_apply's LDS: the bucket's rows, then the chunks' prefix, count and offset arrays
+    const size_t meta_lds = 4 * ((size_t)bk.nchunks + 1) + 4 * bk.nchunks +
+                            2 * (((size_t)bk.nchunks + 1) & ~size_t(1)) + 64;
+    uint32_t sh = 6;                                   // at most 64 tiles (16-bit entry keys)
+    while (sh > 0 && ((size_t)bk.rows << (10 + sh)) + meta_lds > kBinLds) --sh;
+    if (((size_t)bk.rows << (10 + sh)) + meta_lds > kBinLds) return false;
+    bk.tpb_shift = sh;
+    const uint64_t B = (bk.ntiles + (1ull << sh) - 1) >> sh;
+    if (B > kBinMaxBuckets || B == 0) return false;
+    bk.B = (uint32_t)B;
+    lds_bin = kBinChunk * 8 + 8 * (size_t)bk.B + 64;
+    lds_apply = ((size_t)bk.rows << (10 + sh)) + meta_lds;
+    ws = (size_t)bk.nchunks * kBinChunk * 8 + (size_t)bk.nchunks * bk.B * 4;
+    return true;
+}
+
+// dense batches (>= 1 record per 8 table slots, >= 64 Ki records) in any order go binned
+bool bin_default(const TableK &t, uint64_t count) {
+    return count >= (1u << 16) && count * 8 >= t.G * t.nr;
+}
+
+template <bool LAG>
+int ingest_binned(hq_ctx *ctx, const char *what, const uint64_t *u, uint64_t count, TableK &t,
+                  BinK bk, size_t lds_bin, size_t lds_apply, size_t ws, uint64_t *n_skipped) {
+    if (ctx->bin_ws_bytes < ws) {
+        int rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+        if (rc) return rc;
+        if (ctx->bin_ws) (void)hipFree(ctx->bin_ws);
+        ctx->bin_ws = nullptr;
+        ctx->bin_ws_bytes = 0;
+        rc = hq::check_hip(ctx, hipMalloc(&ctx->bin_ws, ws), "hipMalloc(binned ingest)");
+        if (rc) return rc;
+        ctx->bin_ws_bytes = ws;
+    }
+    bk.ent = static_cast<uint64_t *>(ctx->bin_ws);
+    bk.meta = reinterpret_cast<uint32_t *>(bk.ent + (size_t)bk.nchunks * kBinChunk);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_bin<LAG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_apply<LAG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_apply);
+    const uint64_t per = (uint64_t)bk.nchunks * kBinChunk;   // records per launch pair
+    for (uint64_t r0 = 0; r0 < count; r0 += per) {
+        const uint64_t n = std::min(per, count - r0);
+        BinK b = bk;
+        b.nchunks = (uint32_t)((n + kBinChunk - 1) / kBinChunk);
+        hipLaunchKernelGGL(k_bin<LAG>, dim3(b.nchunks), dim3(kBinThreads), lds_bin, ctx->stream,
+                           u + r0 * (LAG ? 1 : 2), n, t, b, n_skipped);
+        int rc = hq::post_launch(ctx, what);
+        if (!rc) rc = hq::pre_launch(ctx);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_apply<LAG>, dim3(b.B), dim3(kBinThreads), lds_apply, ctx->stream, t, b,
+                           n_skipped);
+        rc = hq::post_launch(ctx, what);
+        if (rc) return rc;
+        if (r0 + per < count && (rc = hq::pre_launch(ctx))) return rc;
+    }
+    return HQ_OK;
+}
+
+// the ingest launch of any flags: binned (forced, or by default for a dense batch that is not
+// grouped), else the per-record kernel
+template <bool LAG>
+int table_ingest(hq_ctx *ctx, const char *what, const uint64_t *u, uint64_t count, TableK &t,
+                 uint32_t flags, uint64_t *n_skipped) {
+    if ((flags & HQ_INGEST_ATOMIC) && (flags & (HQ_INGEST_BINNED | HQ_INGEST_GROUPED |
+                                                HQ_INGEST_UNIQUE)))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": HQ_INGEST_ATOMIC excludes the "
+                                                              "other modes");
+    if ((flags & HQ_INGEST_BINNED) && (flags & HQ_INGEST_GROUPED))
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": HQ_INGEST_BINNED excludes "
+                                                              "HQ_INGEST_GROUPED");
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    const bool want_bin = (flags & HQ_INGEST_BINNED) ||
+                          (!(flags & (HQ_INGEST_ATOMIC | HQ_INGEST_GROUPED)) && bin_default(t, count));
+    if (want_bin) {
+        BinK bk{};
+        size_t l1 = 0, l2 = 0, ws = 0;
+        if (bin_plan(ctx, t, count, LAG, bk, l1, l2, ws))
+            return ingest_binned<LAG>(ctx, what, u, count, t, bk, l1, l2, ws, n_skipped);
+        if (flags & HQ_INGEST_BINNED)
+            return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": table too large for "
+                                                                  "HQ_INGEST_BINNED");
+    }
+    const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
+    if (flags & HQ_INGEST_UNIQUE)
+        hipLaunchKernelGGL((k_table_ingest<kUnique, LAG>), grid, blk, 0, ctx->stream, u, count, t,
+                           n_skipped);
+    else if (flags & HQ_INGEST_GROUPED)
+        hipLaunchKernelGGL((k_table_ingest<kGrouped, LAG>), grid, blk, 0, ctx->stream, u, count, t,
+                           n_skipped);
+    else
+        hipLaunchKernelGGL((k_table_ingest<kAtomic, LAG>), grid, blk, 0, ctx->stream, u, count, t,
+                           n_skipped);
+    return hq::post_launch(ctx, "k_table_ingest");
 }
 
 }  // namespace
@@ -352,19 +678,9 @@ int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint6
     if (rc) return rc;
     if (!updates || !hq::aligned16(updates))
         return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_match_dev: updates NULL or misaligned");
-    if ((rc = hq::pre_launch(ctx))) return rc;
-    const uint64_t *u = reinterpret_cast<const uint64_t *>(updates);
-    const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
-    if (flags & HQ_INGEST_UNIQUE)
-        hipLaunchKernelGGL((k_table_ingest<kUnique, false>), grid, blk, 0, ctx->stream, u, count,
-                           t, n_skipped);
-    else if (flags & HQ_INGEST_GROUPED)
-        hipLaunchKernelGGL((k_table_ingest<kGrouped, false>), grid, blk, 0, ctx->stream, u, count,
-                           t, n_skipped);
-    else
-        hipLaunchKernelGGL((k_table_ingest<kAtomic, false>), grid, blk, 0, ctx->stream, u, count,
-                           t, n_skipped);
-    return hq::post_launch(ctx, "k_table_ingest");
+    return table_ingest<false>(ctx, "hq_table_ingest_match_dev",
+                               reinterpret_cast<const uint64_t *>(updates), count, t, flags,
+                               n_skipped);
 }
 
 int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
@@ -376,18 +692,7 @@ int hq_table_ingest_lag_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count
     int rc = table_k(ctx, "hq_table_ingest_lag_dev", tiles, G, n_max, form, 16, flags, t);
     if (rc) return rc;
     if (!updates) return hq::fail(ctx, HQ_E_INVAL, "hq_table_ingest_lag_dev: updates NULL");
-    if ((rc = hq::pre_launch(ctx))) return rc;
-    const dim3 grid(tgrid((count + kIV - 1) / kIV)), blk(kTBlock);
-    if (flags & HQ_INGEST_UNIQUE)
-        hipLaunchKernelGGL((k_table_ingest<kUnique, true>), grid, blk, 0, ctx->stream, updates,
-                           count, t, n_skipped);
-    else if (flags & HQ_INGEST_GROUPED)
-        hipLaunchKernelGGL((k_table_ingest<kGrouped, true>), grid, blk, 0, ctx->stream, updates,
-                           count, t, n_skipped);
-    else
-        hipLaunchKernelGGL((k_table_ingest<kAtomic, true>), grid, blk, 0, ctx->stream, updates,
-                           count, t, n_skipped);
-    return hq::post_launch(ctx, "k_table_ingest");
+    return table_ingest<true>(ctx, "hq_table_ingest_lag_dev", updates, count, t, flags, n_skipped);
 }
 
 static int table_append(hq_ctx *ctx, const char *what, const uint64_t *updates, uint64_t count,
@@ -398,6 +703,8 @@ static int table_append(hq_ctx *ctx, const char *what, const uint64_t *updates, 
     TableK t;
     int rc = table_k(ctx, what, tiles, G, n_max, form, ring_len, flags, t);
     if (rc) return rc;
+    if (flags & HQ_INGEST_BINNED)
+        return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": HQ_INGEST_BINNED is for the ingests");
     if (!updates || (!counts && !hq::aligned16(updates)))
         return hq::fail(ctx, HQ_E_INVAL, std::string(what) + ": updates NULL or misaligned");
     if ((rc = hq::pre_launch(ctx))) return rc;

@@ -37,6 +37,8 @@ HQ_TILE_GROUPS = 128
 HQ_LAYOUT_IN_PLACE = 0x100   # | HQ_LAYOUT_TILES_LEADER: a device-resident table decided in place
 HQ_INGEST_GROUPED = 1        # hq_table_*: the records of one key are adjacent in the batch
 HQ_INGEST_UNIQUE = 2         # hq_table_*: every key at most once in the batch
+HQ_INGEST_ATOMIC = 4         # hq_table_ingest_*: the per-record atomic kernel, forced
+HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, forced
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit

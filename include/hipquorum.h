@@ -610,7 +610,8 @@ int hq_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
  *                              hq_append_update (16-byte aligned)
  *   hq_table_append_count_dev  the same from 8-byte records group << 32 | n: lastIndex += n
  *   hq_table_committed_dev     the committed row of every tile into committed[G], group order
- * flags: 0 = any batch (one 64-bit atomic per record); HQ_INGEST_GROUPED = the caller guarantees
+ * flags: 0 = any batch (one 64-bit atomic per record, or binned: below); HQ_INGEST_GROUPED = the
+ * caller guarantees
  * that the records of one key — (group, slot) for the ingests, group for the appends — are
  * adjacent in the batch (a step worker emitting node by node; a batch with unique keys is
  * grouped). Each wave then reduces its runs of equal keys with a segmented scan and applies a
@@ -620,9 +621,20 @@ int hq_append_count_dev(hq_ctx *ctx, const uint64_t *updates, uint64_t count,
  * guarantees every key at most once in the batch (a step's final ack per (group, slot); one
  * append per group): each record is one plain read-modify-write of its own table word, no scan
  * and no atomic, in any order.
+ * Ingests only (hq_table_ingest_match_dev / _lag_dev): HQ_INGEST_BINNED = records in any order
+ * applied in two streaming passes without global atomics: the records are binned by table region
+ * (2^k consecutive tiles) in LDS and written back bucket by bucket, then one workgroup per region
+ * loads its match rows into LDS, applies every record of the region with LDS max and writes the
+ * rows back (each table line read and written once). Chosen by default (flags 0 or
+ * HQ_INGEST_UNIQUE) for a dense batch — at least 64 Ki records and one per 8 table slots — when
+ * the table has at most 8192 regions (64 tiles each at n_max 3: 67 M groups); HQ_INGEST_BINNED
+ * forces it (HQ_E_INVAL if the table is too large), HQ_INGEST_ATOMIC forces the per-record path.
+ * Uses a device workspace of the context (8 bytes per record of a launch pair).
  */
 #define HQ_INGEST_GROUPED 1u
 #define HQ_INGEST_UNIQUE 2u
+#define HQ_INGEST_ATOMIC 4u
+#define HQ_INGEST_BINNED 8u
 int hq_table_ingest_match_dev(hq_ctx *ctx, const hq_match_update *updates, uint64_t count,
                               uint64_t *tiles, uint64_t G, uint32_t n_max, uint32_t form,
                               uint32_t flags, uint64_t *n_skipped);

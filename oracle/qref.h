@@ -254,6 +254,8 @@ typedef struct qref_event {
     uint32_t reserved;
 } qref_event;
 
+#define QREF_LOG_MAX_RUNS 64
+
 typedef struct qref_group {
     uint64_t cluster_id, node_id, term;
     int state;
@@ -262,6 +264,17 @@ typedef struct qref_group {
     qref_member members[QREF_STEP_MAX_MEMBERS];
     qref_read_index *ri;      /* allocated on the first ReadIndex; qref_group_free releases it */
     qref_votes votes;
+    /* The node's log as terms by index, the way inMemory.getTerm / logdb answer it
+     * (inmemory.go:87-105, logentry.go:143-160): runs of equal terms, run k covering
+     * [run_start[k], run_start[k + 1]) with term run_term[k] (starts and terms increasing,
+     * entryutils.go:44-47); indexes below first_minus_1 are compacted (term 0, ErrCompacted) and
+     * above last do not exist (term 0). The leader's no-op and proposals extend it at r.term
+     * (raft.go:911-922, 977-989). qref_group_init sets the two-run history {(0, term - 1),
+     * (term_start, term)}; qref_group_set_log replaces it with any history. term_start (the
+     * first current-term index) is only reported, never read by the oracle's term check. */
+    uint64_t first_minus_1;
+    int n_runs;
+    uint64_t run_start[QREF_LOG_MAX_RUNS], run_term[QREF_LOG_MAX_RUNS];
 } qref_group;
 
 typedef struct qref_step_out {
@@ -279,6 +292,10 @@ int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64
                     int state, uint64_t committed, uint64_t last, uint64_t term_start,
                     const qref_member *members, int n_members);
 void qref_group_free(qref_group *g);
+/* Replace the group's log history (see qref_group): starts strictly increasing with
+ * starts[0] <= first_minus_1, terms strictly increasing and <= the group's term. Returns 0 or -1. */
+int qref_group_set_log(qref_group *g, uint64_t first_minus_1, int n_runs, const uint64_t *starts,
+                       const uint64_t *terms);
 
 /* Many groups, one step (the CPU baseline of the step worker): list[i] is an index into
  * `groups` whose events are events[offsets[i] .. offsets[i + 1]) — the layout of hq_step_input

@@ -62,6 +62,7 @@ class Votes(ctypes.Structure):
 
 
 QREF_STEP_MAX_MEMBERS = 16
+QREF_LOG_MAX_RUNS = 64
 QREF_STEP_MAX_OUT = 64
 EV_READ, EV_MSG, EV_CHECK_QUORUM, EV_CAMPAIGN, EV_PROPOSE = 1, 2, 3, 4, 5
 
@@ -81,7 +82,9 @@ class Group(ctypes.Structure):
     _fields_ = [("cluster_id", _u64), ("node_id", _u64), ("term", _u64), ("state", ctypes.c_int),
                 ("n_members", ctypes.c_int), ("committed", _u64), ("last", _u64),
                 ("term_start", _u64), ("members", Member * QREF_STEP_MAX_MEMBERS),
-                ("ri", ctypes.POINTER(ReadIndex)), ("votes", Votes)]
+                ("ri", ctypes.POINTER(ReadIndex)), ("votes", Votes),
+                ("first_minus_1", _u64), ("n_runs", ctypes.c_int),
+                ("run_start", _u64 * QREF_LOG_MAX_RUNS), ("run_term", _u64 * QREF_LOG_MAX_RUNS)]
 
 
 class _Ready(ctypes.Structure):
@@ -164,6 +167,7 @@ def load() -> ctypes.CDLL:
         "qref_group_init": (ctypes.c_int, [_vp, _u64, _u64, _u64, ctypes.c_int, _u64, _u64, _u64,
                                            _vp, ctypes.c_int]),
         "qref_group_step": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
+        "qref_group_set_log": (ctypes.c_int, [_vp, _u64, ctypes.c_int, _vp, _vp]),
         "qref_group_free": (None, [_vp]),
         "qref_groups_new": (_vp, [_u64]),
         "qref_groups_free": (None, [_vp, _u64]),
@@ -449,14 +453,31 @@ class StepGroup:
     Events are tuples: ("read", low, high) | ("msg", type, from, term, log_index, hint,
     hint_high, reject) | ("check_quorum",) | ("campaign",) | ("propose", n)."""
 
-    def __init__(self, cluster_id, node_id, term, state, committed, last, term_start, members):
+    def __init__(self, cluster_id, node_id, term, state, committed, last, term_start, members,
+                 log=None):
+        """log: None (the two-run history {(0, term - 1), (term_start, term)}) or
+        (first_minus_1, [(start, term), ...]) — the node's log terms by index as runs
+        (qref_group_set_log)."""
         self.c = Group()
         m = (Member * len(members))(*[Member(int(a), int(b), int(c), int(d))
                                       for a, b, c, d in members])
         rc = lib.qref_group_init(ctypes.byref(self.c), cluster_id, node_id, term, state,
                                  committed, last, term_start, m, len(members))
         assert rc == 0, rc
+        if log is not None:
+            first_minus_1, runs = log
+            st = np.array([r[0] for r in runs], np.uint64)
+            tm = np.array([r[1] for r in runs], np.uint64)
+            rc = lib.qref_group_set_log(ctypes.byref(self.c), first_minus_1, len(runs),
+                                        st.ctypes.data, tm.ctypes.data)
+            assert rc == 0, (rc, log)
         self._out = StepOut()
+
+    def log_terms(self):
+        """(first_minus_1, [(start, term), ...]) of the group's log history now."""
+        c = self.c
+        return int(c.first_minus_1), [(int(c.run_start[k]), int(c.run_term[k]))
+                                      for k in range(c.n_runs)]
 
     def __del__(self):
         if lib is not None and getattr(self, "c", None) is not None:

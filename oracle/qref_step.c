@@ -43,24 +43,40 @@ static int n_voting(const qref_group *g) {      /* numVotingMembers, raft.go:368
 
 static int quorum(const qref_group *g) { return qref_quorum(n_voting(g)); }
 
-typedef struct { uint64_t term, term_start; } leader_log_ud;
-/* the leader's log: entries from its first current-term entry on carry r.term; older entries a
- * lower term (entryutils.go:44-47) */
-static uint64_t leader_term_at(const void *ud, uint64_t i) {
-    const leader_log_ud *l = (const leader_log_ud *)ud;
-    return i >= l->term_start ? l->term : l->term - 1;
+/* the term of index i in the group's log history (the run that holds it; inMemory.getTerm,
+ * inmemory.go:87-105, and logdb below it); qref_log_term applies the compacted / beyond-last
+ * bounds first (logentry.go:143-160) */
+static uint64_t history_term_at(const void *ud, uint64_t i) {
+    const qref_group *g = (const qref_group *)ud;
+    uint64_t t = 0;
+    for (int k = 0; k < g->n_runs && g->run_start[k] <= i; k++) t = g->run_term[k];
+    return t;
 }
 
-static qref_log log_view(qref_group *g, leader_log_ud *ud) {
-    ud->term = g->term;
-    ud->term_start = g->term_start;
+static qref_log log_view(qref_group *g) {
     qref_log l;
-    l.first_minus_1 = 0;
+    l.first_minus_1 = g->first_minus_1;
     l.last = g->last;
     l.committed = g->committed;
-    l.term_at = leader_term_at;
-    l.ud = ud;
+    l.term_at = history_term_at;
+    l.ud = g;
     return l;
+}
+
+/* entries appended at the group's term from index `from` on (the leader's no-op and proposals,
+ * raft.go:911-922): a new run unless the last run already has this term */
+static int log_extend(qref_group *g, uint64_t from) {
+    if (g->n_runs && g->run_term[g->n_runs - 1] == g->term) return QREF_OK;
+    if (g->n_runs && g->run_start[g->n_runs - 1] >= from) {   /* a run of no entries yet */
+        g->run_start[g->n_runs - 1] = from;
+        g->run_term[g->n_runs - 1] = g->term;
+        return QREF_OK;
+    }
+    if (g->n_runs >= QREF_LOG_MAX_RUNS) return QREF_PANIC;
+    g->run_start[g->n_runs] = from;
+    g->run_term[g->n_runs] = g->term;
+    g->n_runs++;
+    return QREF_OK;
 }
 
 /* raft.tryCommit (raft.go:888-909) over the group's remotes then witnesses */
@@ -71,8 +87,7 @@ static int try_commit(qref_group *g) {
         if (g->members[i].role == QREF_ROLE_REMOTE) rm[nr++] = g->members[i].match;
         else if (g->members[i].role == QREF_ROLE_WITNESS) wm[nw++] = g->members[i].match;
     }
-    leader_log_ud ud;
-    qref_log l = log_view(g, &ud);
+    qref_log l = log_view(g);
     int rc = qref_try_commit(rm, nr, wm, nw, &l, g->term, NULL);
     if (rc == QREF_PANIC) return rc;
     g->committed = l.committed;
@@ -109,6 +124,10 @@ static int become_follower(qref_group *g, uint64_t term, qref_step_out *o, int r
 /* raft.appendEntries (raft.go:911-922): entries get r.term and follow lastIndex; the node's own
  * remote follows the log; a single-node quorum commits at once */
 static int append_entries(qref_group *g, uint64_t n) {
+    if (n) {
+        int rc = log_extend(g, g->last + 1);
+        if (rc) return rc;
+    }
     g->last += n;
     int self = find_member(g, g->node_id);
     if (self >= 0 && g->members[self].match < g->last) g->members[self].match = g->last;
@@ -165,8 +184,7 @@ static int defer_event(qref_step_out *o, int i) {
 
 /* raft.hasCommittedEntryAtCurrentTerm (raft.go:1612-1621) */
 static int has_committed_entry_at_current_term(qref_group *g) {
-    leader_log_ud ud;
-    qref_log l = log_view(g, &ud);
+    qref_log l = log_view(g);
     return qref_log_term(&l, g->committed) == g->term;
 }
 
@@ -287,9 +305,33 @@ int qref_group_init(qref_group *g, uint64_t cluster_id, uint64_t node_id, uint64
     g->n_members = n_members;
     memcpy(g->members, members, (size_t)n_members * sizeof *members);
     g->ri = NULL;
+    /* the default history: term_start's run at the group's term, one older term below it */
+    g->first_minus_1 = 0;
+    g->n_runs = 0;
+    if (term > 0 && term_start > 0) {
+        g->run_start[g->n_runs] = 0;
+        g->run_term[g->n_runs++] = term - 1;
+    }
+    g->run_start[g->n_runs] = term_start;
+    g->run_term[g->n_runs++] = term;
     qref_votes_reset(&g->votes);
     /* a candidate holds its own vote (campaign, raft.go:1093) */
     if (state == QREF_CANDIDATE) qref_handle_vote_resp(&g->votes, node_id, 0);
+    return 0;
+}
+
+int qref_group_set_log(qref_group *g, uint64_t first_minus_1, int n_runs, const uint64_t *starts,
+                       const uint64_t *terms) {
+    if (!g || n_runs < 1 || n_runs > QREF_LOG_MAX_RUNS || !starts || !terms) return -1;
+    if (starts[0] > first_minus_1 || first_minus_1 > g->committed) return -1;
+    for (int k = 0; k < n_runs; k++) {
+        if (k && (starts[k] <= starts[k - 1] || terms[k] <= terms[k - 1])) return -1;
+        if (terms[k] > g->term) return -1;
+        g->run_start[k] = starts[k];
+        g->run_term[k] = terms[k];
+    }
+    g->n_runs = n_runs;
+    g->first_minus_1 = first_minus_1;
     return 0;
 }
 

@@ -42,9 +42,10 @@ class OracleBackend:
         self.qref = qref
         self.groups = {}
 
-    def add_group(self, cid, node, term, state, committed, last, term_start, members):
+    def add_group(self, cid, node, term, state, committed, last, term_start, members, log=None):
+        """log: the node's log terms by index (StepGroup), None for the two-run history."""
         self.groups[cid] = self.qref.StepGroup(cid, node, term, state, committed, last,
-                                               term_start, members)
+                                               term_start, members, log)
 
     def step(self, per_group):
         out = {}
@@ -80,7 +81,10 @@ class WorkerBackend:
     def close(self):
         self.w.close()
 
-    def add_group(self, cid, node, term, state, committed, last, term_start, members):
+    def add_group(self, cid, node, term, state, committed, last, term_start, members, log=None):
+        # the worker holds term_start only: its term check is term_start <= q <= last, exact
+        # because the leader's entries from its no-op on carry its term and earlier ones a lower
+        # one (raft.go:911-922, entryutils.go:44-47); the oracle checks the whole history
         self.w.add_group(cid, node, term, state, committed, last, term_start, members)
         self.cids.append(cid)
 

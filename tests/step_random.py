@@ -35,8 +35,30 @@ def random_groups(rng, G, cid0=1):
             mem.append((i, m, r, int(rng.random() < 0.5)))
         order = rng.permutation(len(mem))
         mem = [mem[k] for k in order]
-        groups.append((cid0 + j, node, term, state, committed, last, term_start, mem))
+        groups.append((cid0 + j, node, term, state, committed, last, term_start, mem,
+                       random_log(rng, term, state, committed, term_start)))
     return groups
+
+
+def random_log(rng, term, state, committed, term_start):
+    """A multi-term log history for the oracle (qref_group_set_log): 1-4 runs of older terms
+    below term_start (run 0 from index 0), then term_start's run at the group's term (a
+    candidate's at term - 1: it has no entries of the term it campaigns in), and a compaction
+    point at or below committed (term 0 below it, logentry.go:143-160)."""
+    top = term - 1 if state == sc.CANDIDATE else term
+    k = int(rng.integers(1, min(4, top - 1) + 1)) if top > 1 else 0
+    terms = sorted(int(t) for t in rng.choice(np.arange(1, top), k, replace=False)) if k else []
+    starts = [0] + sorted(int(x) for x in rng.choice(np.arange(1, max(2, term_start)),
+                                                     min(k - 1, max(0, term_start - 1)),
+                                                     replace=False)) if k else []
+    terms = terms[:len(starts)]
+    runs = list(zip(starts, terms))
+    if not runs:                 # a candidate at term 2: every entry at term 1
+        runs = [(0, top)]
+    elif term_start > starts[-1]:
+        runs.append((term_start, top))
+    first_minus_1 = max(0, committed - int(rng.integers(0, 40)))
+    return first_minus_1, runs
 
 
 def random_events(rng, state, step_no, ctx_seq):

@@ -39,14 +39,27 @@ def _match_updates(rng, G, n, count, last, grouped, dup=True):
     return np.stack([key, idx], axis=1).astype(np.uint64)
 
 
-@pytest.mark.parametrize("grouped", [False, True])
+# ingest modes: the per-record atomic kernel, the default (binned for these dense batches), the
+# binned two-pass kernels forced, the grouped segmented scan
+MODES = ["atomic", "default", "binned", "grouped"]
+
+
+def _flags(hq, mode):
+    return {"atomic": hq.HQ_INGEST_ATOMIC, "default": 0, "binned": hq.HQ_INGEST_BINNED,
+            "grouped": hq.HQ_INGEST_GROUPED}[mode]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("form", [2, 0])
-def test_table_ingest_match(gpu_ctx, hq, grouped, form):
-    rng = np.random.default_rng(SEED + grouped + 2 * form)
+def test_table_ingest_match(gpu_ctx, hq, mode, form):
+    grouped = mode == "grouped"
+    rng = np.random.default_rng(SEED + MODES.index(mode) + 7 * form)
     G, n = 70_001, 5
     inp = qref.CommitInputs(qref.spec(SEED + 1, G, n))
     dt = _table(gpu_ctx, hq, inp, form)
     upd = _match_updates(rng, G, n, 400_000, inp.last_index, grouped)
+    # indexes of 2^48 and more (the binned entries cannot hold them: applied with an atomic)
+    upd[[10, 20, 30], 1] = np.uint64(1 << 50) + np.arange(3, dtype=np.uint64)
     if grouped:   # long runs of one key across wave edges too
         upd = np.concatenate([upd[:1000], np.repeat(upd[1000:1003], 150, axis=0), upd[1003:]])
         o = np.argsort(upd[:, 0], kind="stable")
@@ -58,8 +71,7 @@ def test_table_ingest_match(gpu_ctx, hq, grouped, form):
     qref.ingest_match(upd[valid].copy(), want, G, G, n)
     du = gpu_ctx.upload(upd.reshape(-1))
     skip = gpu_ctx.upload(np.zeros(1, np.uint64))
-    gpu_ctx.table_ingest_match_dev(du, len(upd), dt, G, n, form,
-                                   hq.HQ_INGEST_GROUPED if grouped else 0, skip)
+    gpu_ctx.table_ingest_match_dev(du, len(upd), dt, G, n, form, _flags(hq, mode), skip)
     v = _view(gpu_ctx, hq, dt, G, n, form)
     np.testing.assert_array_equal(v.match().reshape(-1), want)
     np.testing.assert_array_equal(v.row("committed"), inp.committed_in)
@@ -68,9 +80,10 @@ def test_table_ingest_match(gpu_ctx, hq, grouped, form):
         gpu_ctx.free(x)
 
 
-@pytest.mark.parametrize("grouped", [False, True])
-def test_table_ingest_lag(gpu_ctx, hq, grouped):
-    rng = np.random.default_rng(SEED + 10 + grouped)
+@pytest.mark.parametrize("mode", MODES)
+def test_table_ingest_lag(gpu_ctx, hq, mode):
+    grouped = mode == "grouped"
+    rng = np.random.default_rng(SEED + 10 + MODES.index(mode))
     G, n = 50_003, 4
     form = hq.HQ_FORM_TERM_MASK
     inp = qref.CommitInputs(qref.spec(SEED + 2, G, n))
@@ -96,13 +109,60 @@ def test_table_ingest_lag(gpu_ctx, hq, grouped):
     qref.ingest_match(upd, want, G, G, n)
     du = gpu_ctx.upload(wire)
     skip = gpu_ctx.upload(np.zeros(1, np.uint64))
-    gpu_ctx.table_ingest_lag_dev(du, len(wire), dt, G, n, form,
-                                 hq.HQ_INGEST_GROUPED if grouped else 0, skip)
+    gpu_ctx.table_ingest_lag_dev(du, len(wire), dt, G, n, form, _flags(hq, mode), skip)
     v = _view(gpu_ctx, hq, dt, G, n, form)
     np.testing.assert_array_equal(v.match().reshape(-1), want)
     assert int(gpu_ctx.download(skip)[0]) == int((~valid).sum())
     for x in (dt, du, skip):
         gpu_ctx.free(x)
+
+
+@pytest.mark.parametrize("lag", [False, True])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_binned_ingest_many_launches_and_shapes(hq, monkeypatch, lag, n):
+    """The binned ingest split over several launch pairs (HQ_BIN_LAUNCH_CHUNKS = 3 chunks of
+    8192 records per pair), a ragged last tile, a batch that is not a multiple of the chunk, and
+    voter counts whose match rows shrink the regions (n = 8: 7 rows, 16 tiles per region):
+    equal to the oracle's sequential tryUpdate."""
+    monkeypatch.setenv("HQ_BIN_LAUNCH_CHUNKS", "3")
+    rng = np.random.default_rng(SEED + 50 + n + 10 * lag)
+    G, form = 30_011, hq.HQ_FORM_TERM_MASK
+    inp = qref.CommitInputs(qref.spec(SEED + 7, G, n))
+    with hq.Context(0) as ctx:
+        dt = _table(ctx, hq, inp, form)
+        cnt = 8192 * 7 + 4321
+        g = rng.integers(0, G, cnt, dtype=np.uint64)
+        s = rng.integers(1, n, cnt, dtype=np.uint64)
+        lagv = rng.integers(0, 30, cnt, dtype=np.uint64)
+        want = inp.match.copy()
+        if lag:
+            wire = hq.pack_lag_updates(g, s, lagv)
+            ok = lagv <= inp.last_index[g]
+            upd = np.stack([(g[ok] << np.uint64(8)) | s[ok], inp.last_index[g[ok]] - lagv[ok]],
+                           axis=1).astype(np.uint64)
+        else:
+            upd = np.stack([(g << np.uint64(8)) | s, inp.last_index[g] - lagv],
+                           axis=1).astype(np.uint64)
+            wire = upd.reshape(-1)
+            ok = np.ones(cnt, bool)
+        qref.ingest_match(upd.copy(), want, G, G, n)
+        du = ctx.upload(wire)
+        skip = ctx.upload(np.zeros(1, np.uint64))
+        if lag:
+            ctx.table_ingest_lag_dev(du, cnt, dt, G, n, form, hq.HQ_INGEST_BINNED, skip)
+        else:
+            ctx.table_ingest_match_dev(du, cnt, dt, G, n, form, hq.HQ_INGEST_BINNED, skip)
+        v = _view(ctx, hq, dt, G, n, form)
+        np.testing.assert_array_equal(v.match().reshape(-1), want)
+        np.testing.assert_array_equal(v.row("committed"), inp.committed_in)
+        np.testing.assert_array_equal(v.row("last_index"), inp.last_index)
+        assert int(ctx.download(skip)[0]) == int((~ok).sum())
+        with pytest.raises(hq.HQError):          # modes that exclude each other
+            ctx.table_ingest_match_dev(du, 4, dt, G, n, form,
+                                       hq.HQ_INGEST_BINNED | hq.HQ_INGEST_GROUPED)
+        with pytest.raises(hq.HQError):
+            ctx.table_ingest_match_dev(du, 4, dt, G, n, form,
+                                       hq.HQ_INGEST_ATOMIC | hq.HQ_INGEST_UNIQUE)
 
 
 @pytest.mark.parametrize("grouped", [False, True])

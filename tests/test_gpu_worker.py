@@ -377,7 +377,7 @@ def test_wide_advance_survives_output_regrow(hq):
         b.step_sized(grp, np.zeros(G, np.uint32), 0, empty)
         got = a.step_sized(grp, sizes, len(ev), data)
         want = b.step_sized(grp, sizes, len(ev), data)
-        assert len(got["ready"]) == G // 4 and 32 * (G // 4) > 1 << 16   # lists overflow a
+        assert len(got["ready"]) == G // 4 and 32 * (G // 4) + 8 * G > 1 << 16   # a overflows
         assert "committed_advance" not in got and "committed_advance" not in want
         np.testing.assert_array_equal(got["committed_column"], want["committed_column"])
         assert int(got["committed_column"][special]) == big

@@ -52,3 +52,65 @@ def test_follower_forwards_reads_and_proposals():
     b.add_group(1, 1, 3, sc.FOLLOWER, 5, 6, 5, sc.members(3))
     out = b.step({1: [("read", 1, 2), sc.msg(sc.READIDX, 2, 3, hint=4), ("propose", 2)]})[1]
     assert out["deferred"] == [0, 1, 2]
+
+
+@pytest.mark.parametrize("idx,want", [(1, 0), (2, 0), (3, 3)])
+def test_leader_only_commits_log_from_current_term_with_a_real_log(idx, want):
+    """TestLeaderOnlyCommitsLogFromCurrentTerm (raft_etcd_paper_test.go:854-885) over the log the
+    reference test builds, held as a term history: entries {1: t1, 2: t2}, the node at term 2
+    campaigns (term 3), wins its vote, appends the no-op at 3 (term 3) and a proposal at 4; a
+    ReplicateResp from node 2 at `idx` commits only an index of term 3."""
+    b = OracleBackend()
+    b.add_group(1, 1, 2, sc.FOLLOWER, 0, 2, 2, sc.members(3), log=(0, [(0, 0), (1, 1), (2, 2)]))
+    out = b.step({1: [sc.msg(sc.VRESP, 2, 0), ("campaign",)]})[1]
+    assert out["states"][-1][:2] == (3, sc.CANDIDATE)
+    out = b.step({1: [sc.msg(sc.VRESP, 2, 3), ("propose", 1)]})[1]
+    assert out["states"] == [(3, sc.LEADER, sc.R_VOTE)]
+    assert b.groups[1].log_terms() == (0, [(0, 0), (1, 1), (2, 2), (3, 3)])
+    out = b.step({1: [sc.msg(sc.RREP, 2, 3, idx)]})[1]
+    assert out["committed"] == want
+
+
+def test_term_check_reads_the_history_not_term_start():
+    """A leader at term 7 whose log holds terms 2, 4, 6 below its first term-7 entry (90): a
+    quorum at 85 (term 6) does not commit, at 95 it does; a ReadIndex needs a committed entry
+    at term 7 (raft.go:1612-1621), so it is dropped until the commit. Compacted indexes
+    (below first - 1 = 30) have term 0 (logentry.go:143-160)."""
+    b = OracleBackend()
+    hist = (30, [(0, 2), (40, 4), (70, 6), (90, 7)])
+    b.add_group(1, 1, 7, sc.LEADER, 80, 100, 90,
+                [(1, 100, 0, 0), (2, 80, 0, 0), (3, 80, 0, 0)], log=hist)
+    out = b.step({1: [("read", 11, 1), sc.msg(sc.RREP, 2, 7, 85)]})[1]
+    assert out["dropped"] == [(11, 1, 0, sc.D_NOT_READY)] and out["committed"] == 80
+    out = b.step({1: [sc.msg(sc.RREP, 3, 7, 95)]})[1]
+    assert out["committed"] == 95
+    out = b.step({1: [("read", 12, 1)]})[1]
+    assert out["dropped"] == [] and b.state(1)[6][0][0] == 95   # pending at index 95
+    # a history whose runs are not increasing, or compacted above committed, is refused
+    with pytest.raises(AssertionError):
+        OracleBackend().add_group(2, 1, 7, sc.LEADER, 80, 100, 90, sc.members(3),
+                                  log=(30, [(0, 4), (40, 2)]))
+    with pytest.raises(AssertionError):
+        OracleBackend().add_group(2, 1, 7, sc.LEADER, 80, 100, 90, sc.members(3),
+                                  log=(81, [(0, 4)]))
+
+
+def test_random_histories_are_valid_and_consistent_with_term_start():
+    """The differential tests' histories (tests/step_random.py): every leader's last run starts
+    at its term_start at its term, every earlier run is older — the invariant under which the
+    worker's term_start <= q <= last check is the history's term(q) == term."""
+    import numpy as np
+
+    import step_random as sr
+    from oracle import qref
+
+    rng = np.random.default_rng(7)
+    multi = 0
+    for g in sr.random_groups(rng, 4000):
+        qref.StepGroup(*g)                       # accepted by qref_group_set_log
+        fm, runs = g[8]
+        assert fm <= g[4] and runs[0][0] == 0
+        if g[3] == sc.LEADER:
+            assert runs[-1] == (g[6], g[2]) and all(t < g[2] for _, t in runs[:-1])
+            multi += len(runs) > 2
+    assert multi > 500
