@@ -93,3 +93,12 @@ tools/lib_rinet0/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_RI_NET=0)
 tools/lib_sw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_STEP_WAVES=$*)
+# binned-ingest A/B (tools/ab_bin.sh): kernel parts removed (HQ_BIN_AB) or smaller regions
+tools/lib_binab%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_BIN_AB=$*)
+tools/lib_bintpb%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_BIN_TPB_SHIFT=$*)
+# phase timestamps of the binned ingest (tools/binprof.hip includes hq_table.hip with HQ_BIN_PROF)
+tools/binprof: tools/binprof.hip $(SRCS) $(DEPS) $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -c -o tools/binprof.o tools/binprof.hip
+	$(HIPCC) $(HIPFLAGS) -pthread -o $@ tools/binprof.o $(filter-out $(LIBDIR)/hq_table.o,$(OBJS))

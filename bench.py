@@ -130,7 +130,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,cq,cqp,ing,ingo,ingu,w2,sweep,e2e,step,step5,wire")
+                  "rimt,cq,cqp,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -606,9 +606,11 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
       rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
       cq:  CheckQuorum (k_bits CHECKQ), 16M groups x 7 voters, active flags reset in place
       cqp: the same over active-flag planes (k_cq_planes)
-      ing: match-delta ingest (k_ingest_match), 4M ReplicateResp deltas into a 4M x 3 table
+      ing: match-delta ingest, 4M ReplicateResp deltas in random order into a 4M x 3 table
+           (binned: k_bin + k_apply)
       ingo: the same deltas in group order, the order a step worker emits them
-      ingu: distinct (group, slot) keys in random order (HQ_INGEST_UNIQUE)"""
+      ingu: distinct (group, slot) keys in random order (HQ_INGEST_UNIQUE)
+      inga: as ing with the per-record atomic path forced (HQ_INGEST_ATOMIC)"""
     from dragonboat_amd import hipquorum as hq
 
     ctx = hq.Context(d.device)
@@ -684,7 +686,7 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                 f"{n - 1} planes of 2048 groups; bit-sliced count, planes zeroed in place), "
                 f"{G} groups x {n} voters")
         units, unit = G, "decisions/s"
-    else:   # ing / ingo: the device table in the headline layout (leader-row tiles)
+    else:   # ing / ingo / ingu / inga: the device table in the headline layout (leader-row tiles)
         G, n, U = 4 << 20, 3, 4 << 20
         form = hq.HQ_FORM_TERM_MASK
         per = U * 16 + U * 16          # the update + the 8-byte read-modify-write of its match
@@ -708,7 +710,8 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                 # the order a step worker emits them: node by node (execengine.go:923-1000)
                 u = u[np.argsort(u[:, 0], kind="stable")]
             ups.append(ctx.upload(u.reshape(-1)))
-        flags = {"ingo": hq.HQ_INGEST_GROUPED, "ingu": hq.HQ_INGEST_UNIQUE}.get(name, 0)
+        flags = {"ingo": hq.HQ_INGEST_GROUPED, "ingu": hq.HQ_INGEST_UNIQUE,
+                 "inga": hq.HQ_INGEST_ATOMIC}.get(name, 0)
 
         def run(i):
             ctx.table_ingest_match_dev(ups[i % nsets], U, table, G, n, form, flags)
@@ -717,17 +720,25 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                 + {"ingo": "in group order (as a step worker emits them): runs reduced in "
                            "registers, plain read-modify-write, atomics only at wave edges "
                            "(HQ_INGEST_GROUPED)",
-                   "ingu": "with distinct (group, slot) keys in random order: one plain "
-                           "read-modify-write each (HQ_INGEST_UNIQUE)"}.get(
-                       name, "in random order: one 64-bit atomic max each"))
+                   "ingu": "with distinct (group, slot) keys in random order (HQ_INGEST_UNIQUE; "
+                           "a dense batch goes binned, as ing)",
+                   "inga": "in random order, one 64-bit atomic max each (HQ_INGEST_ATOMIC: the "
+                           "per-record path, forced)"}.get(
+                       name, "in random order: binned in two streaming passes without global "
+                             "atomics (k_bin + k_apply, the default for a dense batch)"))
         units, unit = U, "updates/s"
     elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
     ctx.close()
+    # the timed region opens behind the first launch: a step of L launches counts L * steps - 1
+    L = max(1, round((launches + 1) / max(1, steps)))
+    step_s = avg * L                     # the kernels of one step, back to back
     return {
         "workload": desc, "value": d.sum(float(units * steps)) / elapsed, "unit": unit,
-        "kernel_avg_us": avg * 1e6, "launches_per_step": launches / max(1, steps),
-        "roofline_achieved_gbs": per / avg / 1e9, "roofline_frac": per / avg / 1e9 / HBM_PEAK_GBS,
-        "algorithmic_bytes_per_launch": per,
+        "kernel_avg_us": avg * 1e6, "launches_per_step": L,
+        "kernel_us_per_step": step_s * 1e6,
+        "roofline_achieved_gbs": per / step_s / 1e9,
+        "roofline_frac": per / step_s / 1e9 / HBM_PEAK_GBS,
+        "algorithmic_bytes_per_step": per,
     }
 
 
@@ -1440,7 +1451,7 @@ def run_rank(args, d, progress):
             elif name in STEP_ROLES:
                 rec = run_step_leg(d, G=args.step_groups, steps=args.step_steps,
                                    with_cpu=not args.no_cpu, name=name)
-            elif name in ("rim", "rimt", "cq", "cqp", "ing", "ingo", "ingu"):
+            elif name in ("rim", "rimt", "cq", "cqp", "ing", "ingo", "ingu", "inga"):
                 rec = run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d)
             elif name == "sweep":
                 rec = run_size_sweep(args.workload, max(50, args.steps // 4),

@@ -38,6 +38,8 @@ struct hq_ctx {
     void *bin_ws = nullptr;
     size_t bin_ws_bytes = 0;
     uint32_t bin_launch_chunks = 4096;
+    uint32_t bin_grid = 256;      // persistent workgroups of the binned ingest (HQ_BIN_GRID)
+    uint32_t bin_tpb_shift = 6;   // its largest region, 2^shift tiles (HQ_BIN_TPB: A/B)
     // host readback of the fallback count (hq_commit etc.)
 };
 

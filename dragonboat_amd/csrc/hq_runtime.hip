@@ -116,6 +116,14 @@ int hq_open(int device, uint32_t flags, hq_ctx **out) {
         if (v == 256 || v == 512 || v == 1024) ctx->bits_block = v;
     }
     if (const char *r = std::getenv("HQ_RI_PAIRS")) ctx->ri_pairs = std::atoi(r) != 0;
+    if (const char *gd = std::getenv("HQ_BIN_GRID")) {
+        const int v = std::atoi(gd);
+        if (v >= 8 && v <= 4096) ctx->bin_grid = (uint32_t)(v & ~7);
+    }
+    if (const char *tp = std::getenv("HQ_BIN_TPB")) {
+        const int v = std::atoi(tp);
+        if (v >= 0 && v <= 6) ctx->bin_tpb_shift = (uint32_t)v;
+    }
     if (const char *c = std::getenv("HQ_BIN_LAUNCH_CHUNKS")) {
         const int v = std::atoi(c);
         if (v >= 1 && v <= 4096) ctx->bin_launch_chunks = (uint32_t)v;

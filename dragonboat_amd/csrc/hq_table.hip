@@ -237,11 +237,21 @@ __global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uin
 // The max commutes, so the result equals the sequential application in any order. Indexes of 2^48
 // or more (never a real log index) do not fit an entry: k_bin applies those few with a global
 // atomic, which k_apply's later read of the row sees (kernel boundary).
-constexpr int kBinThreads = 1024;
+constexpr int kBinThreads = 1024;                                 // k_apply's workgroup
+constexpr int kBinT = 1024;                                       // k_bin's workgroup
 constexpr int kBinPer = 8;                                        // records per thread and chunk
-constexpr uint64_t kBinChunk = (uint64_t)kBinThreads * kBinPer;   // 8192 records per workgroup
+constexpr uint64_t kBinChunk = (uint64_t)kBinT * kBinPer;         // 8192 records per chunk
 constexpr uint32_t kBinMaxBuckets = 8192;                         // k_bin: 64 KB + 8 B per bucket
-constexpr uint32_t kBinLds = 160 * 1024;                          // LDS a workgroup may declare
+
+// HQ_BIN_PROF (tools/binprof.hip only): per-workgroup phase timestamps (wall_clock64) of the
+// binned kernels' first loop iteration
+#ifdef HQ_BIN_PROF
+__device__ unsigned long long g_bin_prof[2][8192][4];
+#define BIN_T(K, P) \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_bin_prof[K][blockIdx.x][P] = wall_clock64()
+#else
+#define BIN_T(K, P)
+#endif
 
 struct BinK {
     uint64_t *ent;       // [chunk][kBinChunk] entries, bucket order inside a chunk
@@ -252,6 +262,15 @@ struct BinK {
     uint32_t rows;       // LDS rows per tile in k_apply: the match rows (+ lastIndex for lags)
     uint32_t nchunks;    // chunks of this launch
 };
+
+// A workgroup barrier for LDS only: this wave's LDS operations done, then s_barrier.
+// __syncthreads' release fence also waits for every outstanding global load and store of the
+// wave (one vmcnt on gfx9), which would turn a prefetch issued before the barrier into a stall.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 // exclusive scan of n (<= 8192) u32 counts in LDS into out (may not alias), block-wide; returns
 // the total to every thread. Every thread must call it.
@@ -268,7 +287,7 @@ __device__ uint32_t block_scan(const uint32_t *in, uint32_t *out, uint32_t n, ui
         x += lane >= (uint32_t)d ? y : 0u;
     }
     if (lane == 63) wtot[wv] = x;
-    __syncthreads();
+    lds_barrier();
     uint32_t wbase = 0, total = 0;
     for (uint32_t w = 0; w < T / 64; ++w) {
         const uint32_t v = wtot[w];
@@ -280,46 +299,53 @@ __device__ uint32_t block_scan(const uint32_t *in, uint32_t *out, uint32_t n, ui
         out[b] = run;
         run += in[b];
     }
-    __syncthreads();                             // wtot may be reused after the call
+    lds_barrier();                             // wtot may be reused after the call
     return total;
 }
 
+// a chunk's records into registers: every load issued at once, unconditionally (a load inside
+// `if (i < count)` is compiled as a branch that waits for it, one memory latency per record);
+// positions past the end load the last record (the decode masks them)
 template <bool LAG>
-__global__ __launch_bounds__(kBinThreads) void k_bin(const uint64_t *u, uint64_t count, TableK t,
-                                                     BinK bk, uint64_t *n_skipped) {
-    extern __shared__ uint64_t lds[];
+__device__ __forceinline__ void bin_load(const uint64_t *u, uint64_t count, uint64_t base,
+                                         uint64_t (&key)[kBinPer], uint64_t (&v)[kBinPer]) {
+#pragma unroll
+    for (int r = 0; r < kBinPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kBinT + threadIdx.x;
+        const uint64_t ic = i < count ? i : count - 1;
+        if constexpr (LAG) {
+            const uint64_t x = __builtin_nontemporal_load(u + ic);
+            key[r] = x >> 28;                          // group << 4 | slot
+            v[r] = x & 0x0FFFFFFFull;                  // lag
+        } else {
+            const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u) + ic);
+            key[r] = x.x;
+            v[r] = x.y;                                // index
+        }
+    }
+}
+
+// One chunk k of k_bin: count its records per bucket, scan, write its meta row, scatter the
+// entries into LDS bucket by bucket and write them out (key / v: its records, loaded earlier;
+// then the records at `next`, unless ~0, are loaded into them)
+template <bool LAG>
+__device__ __forceinline__ void bin_chunk(uint64_t k, uint64_t count, const TableK &t,
+                                          const BinK &bk, uint64_t *n_skipped, uint64_t *lds,
+                                          uint64_t (&key)[kBinPer], uint64_t (&v)[kBinPer],
+                                          uint64_t next, const uint64_t *u) {
     uint64_t *stage = lds;                                           // kBinChunk entries
     uint32_t *hist = reinterpret_cast<uint32_t *>(lds + kBinChunk);  // [B]
     uint32_t *hoff = hist + bk.B;                                    // [B]
     uint32_t *wtot = hoff + bk.B;                                    // [16]
     const uint32_t tid = threadIdx.x;
-    const uint64_t k = blockIdx.x, base = k * kBinChunk;
-    for (uint32_t b = tid; b < bk.B; b += kBinThreads) hist[b] = 0;
-    __syncthreads();
     constexpr int SH = LAG ? 4 : 8;
-    uint64_t key[kBinPer], v[kBinPer];
+    const uint64_t base = k * kBinChunk;
     uint32_t bb[kBinPer], rk[kBinPer];
-    // every record load first (kBinPer in flight per lane)
+    for (uint32_t b = tid; b < bk.B; b += kBinT) hist[b] = 0;
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < kBinPer; ++r) {
-        const uint64_t i = base + (uint64_t)r * kBinThreads + tid;
-        key[r] = ~0ull;
-        v[r] = 0;
-        if (i < count) {
-            if constexpr (LAG) {
-                const uint64_t x = __builtin_nontemporal_load(u + i);
-                key[r] = x >> 28;                      // group << 4 | slot
-                v[r] = x & 0x0FFFFFFFull;              // lag
-            } else {
-                const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(u) + i);
-                key[r] = x.x;
-                v[r] = x.y;                            // index
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < kBinPer; ++r) {
-        const bool in = base + (uint64_t)r * kBinThreads + tid < count;
+        const bool in = base + (uint64_t)r * kBinT + tid < count;
         const uint64_t g = key[r] >> SH, s = key[r] & ((1u << SH) - 1);
         const bool ok = in && g < t.G && s >= 1 && s <= t.nr;
         count_skip(n_skipped, in && !ok);
@@ -337,16 +363,19 @@ __global__ __launch_bounds__(kBinThreads) void k_bin(const uint64_t *u, uint64_t
         bb[r] = b;
         rk[r] = atomicAdd(&hist[b], 1u);               // LDS
     }
-    __syncthreads();
-    const uint32_t total = block_scan<kBinThreads>(hist, hoff, bk.B, wtot);
-    for (uint32_t b = tid; b < bk.B; b += kBinThreads)
+    lds_barrier();
+    if (k == blockIdx.x) BIN_T(0, 1);
+    const uint32_t total = block_scan<kBinT>(hist, hoff, bk.B, wtot);
+    for (uint32_t b = tid; b < bk.B; b += kBinT)
         bk.meta[k * bk.B + b] = hoff[b] | hist[b] << 16;
 #pragma unroll
     for (int r = 0; r < kBinPer; ++r)
         if (bb[r] != 0xFFFFFFFFu) stage[hoff[bb[r]] + rk[r]] = v[r];
-    __syncthreads();
+    if (next != ~0ull) bin_load<LAG>(u, count, next, key, v);   // in flight from here on
+    lds_barrier();
+    if (k == blockIdx.x) BIN_T(0, 2);
     uint64_t *dst = bk.ent + base;
-    for (uint32_t j = 2 * tid; j < total; j += 2 * kBinThreads) {
+    for (uint32_t j = 2 * tid; j < total; j += 2 * kBinT) {
         if (j + 1 < total) {
             u64x2 x;
             x.x = stage[j];
@@ -356,90 +385,168 @@ __global__ __launch_bounds__(kBinThreads) void k_bin(const uint64_t *u, uint64_t
             dst[j] = stage[j];
         }
     }
+    lds_barrier();                                     // stage and hist are reused next chunk
+    if (k == blockIdx.x) BIN_T(0, 3);
 }
 
+// Persistent over the chunks (k = blockIdx.x, + gridDim.x, ...): the next chunk's records are
+// loaded (into the registers this chunk's entries no longer need) before this chunk is written
+template <bool LAG>
+__global__ __launch_bounds__(kBinT) void k_bin(const uint64_t *u, uint64_t count, TableK t,
+                                               BinK bk, uint64_t *n_skipped) {
+    extern __shared__ uint64_t lds[];
+    uint64_t key[kBinPer], v[kBinPer];
+    BIN_T(0, 0);
+    uint64_t k = blockIdx.x;
+    if (k < bk.nchunks) bin_load<LAG>(u, count, k * kBinChunk, key, v);
+    for (; k < bk.nchunks; k += gridDim.x)
+        bin_chunk<LAG>(k, count, t, bk, n_skipped, lds, key, v,
+                       k + gridDim.x < bk.nchunks ? (k + gridDim.x) * kBinChunk : ~0ull, u);
+}
+
+// A/B builds (tools/): HQ_BIN_AB 1 = k_apply with plain LDS stores instead of the LDS max,
+// 2 = without the entry gather, 3 = the rows' read and write alone; HQ_BIN_TPB_SHIFT = the
+// largest region (2^shift tiles) tried
+#ifndef HQ_BIN_AB
+#define HQ_BIN_AB 0
+#endif
+#ifndef HQ_BIN_TPB_SHIFT
+#define HQ_BIN_TPB_SHIFT 6
+#endif
+// one entry applied to the bucket's rows in LDS (64-bit LDS max); returns true for an ack above
+// lastIndex (lags), which is skipped
+template <bool LAG>
+__device__ __forceinline__ bool bin_apply(const TableK &t, uint32_t R, uint64_t *rows, uint64_t e) {
+    if (e == ~0ull) return false;
+    const uint32_t lk = (uint32_t)(e >> 48);
+    uint64_t v = e & 0xFFFFFFFFFFFFull;
+    const uint32_t gl = lk >> 3, s1 = lk & 7, tl = gl >> 7;
+    const uint32_t pos = (uint32_t)tpos(gl & 127);
+    if constexpr (LAG) {
+        const uint64_t last = rows[(tl * R + t.nr) * kT + pos];
+        if (v > last) return true;
+        v = last - v;
+    }
+#if HQ_BIN_AB == 1
+    rows[(tl * R + s1) * kT + pos] = v;
+#else
+    atomicMax(reinterpret_cast<unsigned long long *>(rows + (tl * R + s1) * kT + pos),
+              (unsigned long long)v);
+#endif
+    return false;
+}
+
+constexpr int kApplyEnt = 6;                              // entries per thread and round
+constexpr uint32_t kApplyLds = 128 * 1024;                // a bucket's rows in k_apply's LDS
+constexpr int kApplyRows = (int)(kApplyLds / 16 / kBinThreads);  // row pairs per thread (8)
+
+// the rows of bucket b (tile-major; row r < nr = match slot r + 1, row nr = lastIndex for lags)
+// into registers, every load at once
+__device__ __forceinline__ void apply_load_rows(const TableK &t, const BinK &bk, uint32_t b,
+                                                u64x2 (&rv)[kApplyRows]) {
+    const uint64_t tile0 = (uint64_t)b << bk.tpb_shift;
+    const uint32_t nt = (uint32_t)min((uint64_t)1 << bk.tpb_shift, bk.ntiles - tile0);
+    const uint32_t R = bk.rows, pairs = nt * R * 64;
+#pragma unroll
+    for (int k = 0; k < kApplyRows; ++k) {   // unconditional loads (see bin_load), clamped
+        uint32_t w = threadIdx.x + (uint32_t)k * kBinThreads;
+        w = w < pairs ? w : pairs - 1;
+        const uint32_t tl = w / (R * 64), r = (w / 64) % R, x = 2 * (w % 64);
+        const uint32_t src = r < t.nr ? r : t.nr + 1;
+        rv[k] = *reinterpret_cast<const u64x2 *>(t.tiles + (tile0 + tl) * t.tw +
+                                                 (uint64_t)src * kT + x);
+    }
+}
+
+// Persistent over the buckets, XCD-aware: workgroup i runs on XCD i % 8 and takes the buckets
+// x * per + j, x * per + j + W, ... (x = i % 8, j = i / 8, W workgroups per XCD), so that the W
+// workgroups of an XCD work on consecutive buckets at any time (the lines two neighbouring
+// buckets share — an entry segment that straddles them, a meta row — are served by that XCD's L2
+// once); the next bucket's rows are loaded while this one's entries are applied and its rows
+// written back
 template <bool LAG>
 __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64_t *n_skipped) {
     extern __shared__ uint64_t lds[];
-    const uint32_t tid = threadIdx.x, b = blockIdx.x;
-    const uint64_t tile0 = (uint64_t)b << bk.tpb_shift;
-    const uint32_t nt = (uint32_t)min((uint64_t)1 << bk.tpb_shift, bk.ntiles - tile0);
-    const uint32_t R = bk.rows;
     uint64_t *rows = lds;                                                    // [nt][R][128]
-    uint32_t *P = reinterpret_cast<uint32_t *>(lds + ((size_t)R << (7 + bk.tpb_shift)));
-    uint32_t *cnt = P + bk.nchunks + 1;                                      // [nchunks]
-    uint16_t *O = reinterpret_cast<uint16_t *>(cnt + bk.nchunks);           // [nchunks]
-    uint32_t *wtot = reinterpret_cast<uint32_t *>(O + ((bk.nchunks + 1) & ~1u));
-    // the bucket's rows: tile-major, row r < nr = match slot r + 1, row nr = lastIndex (lags)
-    const uint32_t pairs = nt * R * 64;
-    for (uint32_t w = tid; w < pairs; w += kBinThreads) {
-        const uint32_t tl = w / (R * 64), r = (w / 64) % R, x = 2 * (w % 64);
-        const uint32_t src = r < t.nr ? r : t.nr + 1;
-        const u64x2 v = *reinterpret_cast<const u64x2 *>(t.tiles + (tile0 + tl) * t.tw +
-                                                         (uint64_t)src * kT + x);
-        rows[(tl * R + r) * kT + x] = v.x;
-        rows[(tl * R + r) * kT + x + 1] = v.y;
-    }
-    for (uint32_t c = tid; c < bk.nchunks; c += kBinThreads) {
-        const uint32_t m = bk.meta[(uint64_t)c * bk.B + b];
-        cnt[c] = m >> 16;
-        O[c] = (uint16_t)(m & 0xFFFFu);
-    }
-    __syncthreads();
-    const uint32_t total = block_scan<kBinThreads>(cnt, P, bk.nchunks, wtot);
-    if (tid == 0) P[bk.nchunks] = total;
-    __syncthreads();
-    // kBinPer entries per thread and round: every entry load issued before the first LDS max
-    for (uint32_t j0 = 0; j0 < total; j0 += kBinThreads * 8) {
-        uint64_t ent[8];
+    const uint32_t tid = threadIdx.x, R = bk.rows;
+    uint32_t *M = reinterpret_cast<uint32_t *>(lds + ((size_t)R << (7 + bk.tpb_shift)));
+    constexpr int NE = LAG ? 4 : kApplyEnt;    // (the lag form's extra row reads take registers)
+    const uint32_t per = (bk.B + 7) / 8, x = blockIdx.x % 8, W = gridDim.x / 8;
+    uint32_t j = blockIdx.x / 8;
+    u64x2 rv[kApplyRows];
+    BIN_T(1, 0);
+    if (j < per && x * per + j < bk.B) apply_load_rows(t, bk, x * per + j, rv);
+    for (; j < per && x * per + j < bk.B; j += W) {
+        const uint32_t b = x * per + j;
+        const uint64_t tile0 = (uint64_t)b << bk.tpb_shift;
+        const uint32_t nt = (uint32_t)min((uint64_t)1 << bk.tpb_shift, bk.ntiles - tile0);
+        const uint32_t pairs = nt * R * 64;
+        // every chunk's (offset, count) of this bucket into LDS: one load round for all of them
+        for (uint32_t c = tid; c < bk.nchunks; c += kBinThreads)
+            M[c] = HQ_BIN_AB >= 2 ? 0u : bk.meta[(uint64_t)c * bk.B + b];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const uint32_t j = j0 + (uint32_t)r * kBinThreads + tid;
-            ent[r] = ~0ull;
-            if (j < total) {
-                uint32_t lo = 0, hi = bk.nchunks;     // the chunk c with P[c] <= j < P[c + 1]
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (P[mid] <= j) lo = mid;
-                    else hi = mid;
-                }
-                ent[r] = __builtin_nontemporal_load(bk.ent + (uint64_t)lo * kBinChunk + O[lo] +
-                                                    (j - P[lo]));
+        for (int k = 0; k < kApplyRows; ++k) {
+            const uint32_t w = tid + (uint32_t)k * kBinThreads;
+            if (w < pairs) {
+                const uint32_t tl = w / (R * 64), r = (w / 64) % R, xx = 2 * (w % 64);
+                rows[(tl * R + r) * kT + xx] = rv[k].x;
+                rows[(tl * R + r) * kT + xx + 1] = rv[k].y;
             }
         }
-        bool skip[8];
+        __syncthreads();                               // (waits for the meta loads too)
+        if (j == blockIdx.x / 8) BIN_T(1, 1);
+        // the entries: each half-wave takes one chunk's segment of the bucket at a time (lane l
+        // its l-th entry; a segment averages kBinChunk / B entries), NE chunks per round with
+        // every entry load issued before the first LDS max; segments longer than 32 entries
+        // finish in a loop of their own
+        const uint32_t wv = tid >> 6, h = (tid >> 5) & 1, l = tid & 31;
+        constexpr uint32_t kHalves = 2 * kBinThreads / 64;      // half-waves per workgroup
+        for (uint32_t c0 = 0; c0 < bk.nchunks; c0 += kHalves * NE) {
+            uint32_t m[NE];
+            uint64_t ent[NE];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            skip[r] = false;
-            if (ent[r] == ~0ull) continue;
-            const uint32_t lk = (uint32_t)(ent[r] >> 48);
-            uint64_t v = ent[r] & 0xFFFFFFFFFFFFull;
-            const uint32_t gl = lk >> 3, s1 = lk & 7, tl = gl >> 7;
-            const uint32_t pos = (uint32_t)tpos(gl & 127);
+            for (int u = 0; u < NE; ++u) {           // unconditional loads (see bin_load)
+                const uint32_t c = c0 + (uint32_t)u * kHalves + 2 * wv + h;
+                const uint32_t cc = c < bk.nchunks ? c : 0;
+                m[u] = c < bk.nchunks ? M[c] : 0u;
+                ent[u] = __builtin_nontemporal_load(bk.ent + (uint64_t)cc * kBinChunk +
+                                                    (m[u] & 0xFFFFu) + l);
+            }
+            bool skip[NE];
+#pragma unroll
+            for (int u = 0; u < NE; ++u)
+                skip[u] = bin_apply<LAG>(t, R, rows, l < (m[u] >> 16) ? ent[u] : ~0ull);
             if constexpr (LAG) {
-                const uint64_t last = rows[(tl * R + t.nr) * kT + pos];
-                if (v > last) {                         // an ack above lastIndex: skipped
-                    skip[r] = true;
-                    continue;
-                }
-                v = last - v;
-            }
-            atomicMax(reinterpret_cast<unsigned long long *>(rows + (tl * R + s1) * kT + pos),
-                      (unsigned long long)v);
-        }
-        if constexpr (LAG) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) count_skip(n_skipped, skip[r]);
+                for (int u = 0; u < NE; ++u) count_skip(n_skipped, skip[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < NE; ++u) {           // the rare segments beyond 32 entries
+                const uint32_t c = c0 + (uint32_t)u * kHalves + 2 * wv + h;
+                for (uint32_t k = l + 32; k < (m[u] >> 16); k += 32) {
+                    const bool sk = bin_apply<LAG>(
+                        t, R, rows, bk.ent[(uint64_t)c * kBinChunk + (m[u] & 0xFFFFu) + k]);
+                    if (LAG && sk && n_skipped)
+                        atomicAdd(reinterpret_cast<unsigned long long *>(n_skipped), 1ull);
+                }
+            }
         }
-    }
-    __syncthreads();
-    const uint32_t mpairs = nt * t.nr * 64;          // the match rows back
-    for (uint32_t w = tid; w < mpairs; w += kBinThreads) {
-        const uint32_t tl = w / (t.nr * 64), r = (w / 64) % t.nr, x = 2 * (w % 64);
-        u64x2 v;
-        v.x = rows[(tl * R + r) * kT + x];
-        v.y = rows[(tl * R + r) * kT + x + 1];
-        *reinterpret_cast<u64x2 *>(t.tiles + (tile0 + tl) * t.tw + (uint64_t)r * kT + x) = v;
+        // the next bucket's rows, in flight while these are written back (issued after this
+        // bucket's entry loads: the in-order load counter would make those wait for them)
+        if (j + W < per && b + W < bk.B) apply_load_rows(t, bk, b + W, rv);
+        lds_barrier();
+        if (j == blockIdx.x / 8) BIN_T(1, 2);
+        // the match rows back
+        const uint32_t mpairs = nt * t.nr * 64;
+        for (uint32_t w = tid; w < mpairs; w += kBinThreads) {
+            const uint32_t tl = w / (t.nr * 64), r = (w / 64) % t.nr, xx = 2 * (w % 64);
+            u64x2 v;
+            v.x = rows[(tl * R + r) * kT + xx];
+            v.y = rows[(tl * R + r) * kT + xx + 1];
+            *reinterpret_cast<u64x2 *>(t.tiles + (tile0 + tl) * t.tw + (uint64_t)r * kT + xx) = v;
+        }
+        lds_barrier();                                 // the rows' LDS is reused next bucket
+        if (j == blockIdx.x / 8) BIN_T(1, 3);
     }
 }
 
@@ -567,12 +674,16 @@ bool bin_plan(const hq_ctx *ctx, const TableK &t, uint64_t count, bool lag, BinK
     bk.rows = t.nr + (lag ? 1u : 0u);
     const uint64_t chunks = (count + kBinChunk - 1) / kBinChunk;
     bk.nchunks = (uint32_t)std::min<uint64_t>(chunks, ctx->bin_launch_chunks);
-    // k_apply's LDS: the bucket's rows, then the chunks' prefix, count and offset arrays
-    const size_t meta_lds = 4 * ((size_t)bk.nchunks + 1) + 4 * bk.nchunks +
-                            2 * (((size_t)bk.nchunks + 1) & ~size_t(1)) + 64;
-    uint32_t sh = 6;                                   // at most 64 tiles (16-bit entry keys)
-    while (sh > 0 && ((size_t)bk.rows << (10 + sh)) + meta_lds > kBinLds) --sh;
-    if (((size_t)bk.rows << (10 + sh)) + meta_lds > kBinLds) return false;
+    // k_apply's LDS: the bucket's rows, then a meta word per chunk
+    const size_t meta_lds = 4 * (size_t)bk.nchunks;
+    uint32_t sh = std::min<uint32_t>(HQ_BIN_TPB_SHIFT, ctx->bin_tpb_shift);   // <= 64 tiles
+                                                       // (16-bit entry keys)
+    auto fits = [&](uint32_t sh) {
+        const size_t rows = (size_t)bk.rows << (10 + sh);
+        return rows <= kApplyLds && rows + meta_lds <= 160 * 1024;
+    };
+    while (sh > 0 && !fits(sh)) --sh;
+    if (!fits(sh)) return false;
     bk.tpb_shift = sh;
     const uint64_t B = (bk.ntiles + (1ull << sh) - 1) >> sh;
     if (B > kBinMaxBuckets || B == 0) return false;
@@ -612,13 +723,15 @@ int ingest_binned(hq_ctx *ctx, const char *what, const uint64_t *u, uint64_t cou
         const uint64_t n = std::min(per, count - r0);
         BinK b = bk;
         b.nchunks = (uint32_t)((n + kBinChunk - 1) / kBinChunk);
-        hipLaunchKernelGGL(k_bin<LAG>, dim3(b.nchunks), dim3(kBinThreads), lds_bin, ctx->stream,
-                           u + r0 * (LAG ? 1 : 2), n, t, b, n_skipped);
+        hipLaunchKernelGGL(k_bin<LAG>, dim3(std::min<uint32_t>(b.nchunks, ctx->bin_grid)),
+                           dim3(kBinT), lds_bin, ctx->stream, u + r0 * (LAG ? 1 : 2), n, t,
+                           b, n_skipped);
         int rc = hq::post_launch(ctx, what);
         if (!rc) rc = hq::pre_launch(ctx);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_apply<LAG>, dim3(b.B), dim3(kBinThreads), lds_apply, ctx->stream, t, b,
-                           n_skipped);
+        hipLaunchKernelGGL(k_apply<LAG>, dim3(8 * std::min<uint32_t>((b.B + 7) / 8,
+                                                                     ctx->bin_grid / 8)),
+                           dim3(kBinThreads), lds_apply, ctx->stream, t, b, n_skipped);
         rc = hq::post_launch(ctx, what);
         if (rc) return rc;
         if (r0 + per < count && (rc = hq::pre_launch(ctx))) return rc;
