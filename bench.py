@@ -130,7 +130,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,cq,cqp,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire")
+                  "rimt,cq,cqp,c4pq,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -606,6 +606,7 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
       rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
       cq:  CheckQuorum (k_bits CHECKQ), 16M groups x 7 voters, active flags reset in place
       cqp: the same over active-flag planes (k_cq_planes)
+      c4pq: c4p's ReadIndex + vote planes and CheckQuorum's active planes in one launch
       ing: match-delta ingest, 4M ReplicateResp deltas in random order into a 4M x 3 table
            (binned: k_bin + k_apply)
       ingo: the same deltas in group order, the order a step worker emits them
@@ -686,6 +687,35 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                 f"{n - 1} planes of 2048 groups; bit-sliced count, planes zeroed in place), "
                 f"{G} groups x {n} voters")
         units, unit = G, "decisions/s"
+    elif name == "c4pq":
+        G, n = 16 << 20, 7
+        T = hq.HQ_PLANE_TILE_GROUPS
+        pb, ab = hq.plane_tiles(G) * 3 * T, hq.cq_plane_bytes(G, 8)
+        # 24 vote / ack planes + 7 active planes read, the active planes zeroed, confirmed +
+        # has-quorum bits and the 2-bit outcome codes written
+        per = pb + 2 * ab + hq.words64(G) * 8 * 2 + hq.words32(G) * 8
+        nsets = max(4, int(np.ceil(ROTATE_BYTES / per)))
+        sets = []
+        for k in range(nsets):
+            arrs = [ctx.empty(G, np.uint8) for _ in range(4)]
+            ctx.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 3 + (k << 40), G, n), *arrs)
+            pl, apl = ctx.empty(pb, np.uint8), ctx.empty(ab, np.uint8)
+            ctx.tile_planes_dev(G, *arrs, 0, pl)
+            # the active flags: the same generator's ack bitmaps of another seed
+            ctx.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 5 + (k << 40), G, n), arrs[0])
+            ctx.tile_cq_planes_dev(G, arrs[0], None, 8, 0, apl)
+            ctx.sync()
+            for a in arrs:
+                ctx.free(a)
+            sets.append((pl, apl, ctx.empty(hq.words64(G), np.uint64),
+                         ctx.empty(hq.words32(G), np.uint64), ctx.empty(hq.words64(G), np.uint64)))
+
+        def run(i):
+            ctx.readindex_vote_cq_planes_dev(G, *sets[i % nsets])
+        desc = (f"c4pq: ReadIndex confirm + vote tally + CheckQuorum (setNotActive) in one pass "
+                f"over bit planes (24 vote / ack planes + 7 active planes per 2048 groups), {G} "
+                f"groups x {n} voters, 3 decisions per group")
+        units, unit = 3 * G, "decisions/s"
     else:   # ing / ingo / ingu / inga: the device table in the headline layout (leader-row tiles)
         G, n, U = 4 << 20, 3, 4 << 20
         form = hq.HQ_FORM_TERM_MASK
@@ -1417,7 +1447,7 @@ def same_decisions(a, b):
                for p, q in zip(a, b))
 
 
-EXTRAS_MULTI = "c5tl,c5v5tl,c4p,cqp,rimt,ingo"
+EXTRAS_MULTI = "c5tl,c5v5tl,c4p,cqp,c4pq,rimt,ingo"
 
 
 def run_rank(args, d, progress):
@@ -1451,7 +1481,7 @@ def run_rank(args, d, progress):
             elif name in STEP_ROLES:
                 rec = run_step_leg(d, G=args.step_groups, steps=args.step_steps,
                                    with_cpu=not args.no_cpu, name=name)
-            elif name in ("rim", "rimt", "cq", "cqp", "ing", "ingo", "ingu", "inga"):
+            elif name in ("rim", "rimt", "cq", "cqp", "c4pq", "ing", "ingo", "ingu", "inga"):
                 rec = run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d)
             elif name == "sweep":
                 rec = run_size_sweep(args.workload, max(50, args.steps // 4),

@@ -1088,8 +1088,12 @@ __device__ __forceinline__ uint32_t shuffle16(uint32_t x) {
     return x;
 }
 
-template <bool FULL>
-__device__ __forceinline__ void planes_slot(const BitsK &a, uint64_t g, const uint32_t *p) {
+// CQ: also decide CheckQuorum for the same 32 groups from `act`, this lane's dword of the tile's
+// 7 active-flag planes (plane k = the active flag of voting slot k + 1; the leader's slot 0
+// counts implicitly, raft.go:384), masked to the group's voting slots by the n planes of `p`.
+template <bool FULL, bool CQ = false>
+__device__ __forceinline__ void planes_slot(const BitsK &a, uint64_t g, const uint32_t *p,
+                                            const uint32_t *act = nullptr) {
 #ifdef HQ_PLANES_COPY   // tuning floor: the same loads and stores, no decision (wrong results)
     uint32_t x0 = 0, x1 = 0, x2 = 0;
     for (int q = 0; q < 8; ++q) {
@@ -1136,6 +1140,15 @@ __device__ __forceinline__ void planes_slot(const BitsK &a, uint64_t g, const ui
     const uint32_t foll = ~ge3(h0, h1, h2, r0, r1, r2) & inr & ~lead;
     const uint32_t cand = inr & ~lead & ~foll;
     reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = conf;
+    if constexpr (CQ) {
+        // leaderHasQuorum (raft.go:380-390): 1 + active voting slots >= n/2 + 1, the same
+        // threshold as the ReadIndex acks
+        uint32_t v[7], c0, c1, c2;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v[k] = act[k] & m[k];
+        count7(v, c0, c1, c2);
+        reinterpret_cast<uint32_t *>(a.has_quorum)[g >> 5] = ge3(c0, c1, c2, h0, h1, h2) & inr;
+    }
     const uint32_t w0 = shuffle16(__builtin_amdgcn_perm(lead, cand, 0x05010400u));
     const uint32_t w1 = shuffle16(__builtin_amdgcn_perm(lead, cand, 0x07030602u));
     *reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(a.outcome) + (g >> 4)) =
@@ -1175,6 +1188,42 @@ __global__ __launch_bounds__(BLK) void k_planes(const BitsK a) {
             else if (g < ((a.G + 63) & ~63ull))           // the rest of the last bitmap word
                 reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = 0;
         }
+    }
+}
+
+// ReadIndex + vote + CheckQuorum in one pass (hq_readindex_vote_cq_planes_dev): a step worker
+// decides all three for the same leader groups (readindex.go:77-116, raft.go:1968-1985,
+// raft.go:380-390), so one launch reads a tile's 24 vote / ack planes and its 7 active-flag
+// planes (a separate 1792-byte tile per 2048 groups, the layout hq_tile_cq_planes_dev builds with
+// n_uniform 8 and self slot 0), writes the confirmed, outcome and has-quorum words and zeroes
+// the active planes it read (setNotActive of every voting member, remote.go:196-198): one
+// launch boundary instead of two.
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_planes_cq(const BitsK a, uint8_t *active_planes) {
+    const uint64_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (BLK / 64);
+    const uint64_t ntiles = (a.G + kPlaneTile - 1) / kPlaneTile;
+    for (uint64_t t = wave; t < ntiles; t += nw) {
+        const uint32_t *base = reinterpret_cast<const uint32_t *>(a.tiles + t * (kPlaneTile * 3)) + lane;
+        uint32_t *abase = reinterpret_cast<uint32_t *>(active_planes + t * (7 * (kPlaneTile / 8))) + lane;
+        uint32_t p[24], q[7];
+#pragma unroll
+        for (int k = 0; k < 24; ++k) p[k] = __builtin_nontemporal_load(base + k * 64);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) q[k] = __builtin_nontemporal_load(abase + k * 64);
+        const uint64_t g = t * kPlaneTile + lane * 32;
+        if (t * kPlaneTile + kPlaneTile <= a.G) {
+            planes_slot<true, true>(a, g, p, q);
+        } else if (g < a.G) {
+            planes_slot<false, true>(a, g, p, q);
+        } else if (g < ((a.G + 63) & ~63ull)) {           // the rest of the last bitmap words
+            reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = 0;
+            reinterpret_cast<uint32_t *>(a.has_quorum)[g >> 5] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(0u, abase + k * 64);
     }
 }
 
@@ -2072,6 +2121,28 @@ extern "C" int hq_readindex_vote_planes_dev(hq_ctx *ctx, uint64_t G, const uint8
                        dim3(grid_for((ntiles + kPlTPW - 1) / kPlTPW * 64, HQ_PLANES_BLK)),
                        dim3(HQ_PLANES_BLK), 0, ctx->stream, k);
     return hq::post_launch(ctx, "hq_readindex_vote_planes");
+}
+
+extern "C" int hq_readindex_vote_cq_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *planes,
+                                               uint8_t *active_planes, uint64_t *confirmed,
+                                               uint64_t *outcome, uint64_t *has_quorum) {
+    if (!ctx) return HQ_E_INVAL;
+    if (G == 0) return HQ_OK;
+    if (!planes || !active_planes || !confirmed || !outcome || !has_quorum ||
+        !hq::aligned16(planes) || !hq::aligned16(active_planes))
+        return hq::fail(ctx, HQ_E_INVAL,
+                        "hq_readindex_vote_cq_planes: NULL argument or planes not 16-byte aligned");
+    BitsK k = bits_args(G, nullptr, 0, nullptr);
+    k.tiles = planes;
+    k.confirmed = confirmed;
+    k.outcome = outcome;
+    k.has_quorum = has_quorum;
+    int rc = hq::pre_launch(ctx);
+    if (rc) return rc;
+    const uint64_t ntiles = (G + kPlaneTile - 1) / kPlaneTile;
+    hipLaunchKernelGGL(k_planes_cq<HQ_PLANES_BLK>, dim3(grid_for(ntiles * 64, HQ_PLANES_BLK)),
+                       dim3(HQ_PLANES_BLK), 0, ctx->stream, k, active_planes);
+    return hq::post_launch(ctx, "hq_readindex_vote_cq_planes");
 }
 
 extern "C" int hq_tile_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack,

@@ -246,7 +246,7 @@ constexpr uint32_t kBinMaxBuckets = 8192;                         // k_bin: 64 K
 // HQ_BIN_PROF (tools/binprof.hip only): per-workgroup phase timestamps (wall_clock64) of the
 // binned kernels' first loop iteration
 #ifdef HQ_BIN_PROF
-__device__ unsigned long long g_bin_prof[2][8192][4];
+__device__ unsigned long long g_bin_prof[2][8192][8];
 #define BIN_T(K, P) \
     if (threadIdx.x == 0 && blockIdx.x < 8192) g_bin_prof[K][blockIdx.x][P] = wall_clock64()
 #else
@@ -402,6 +402,7 @@ __global__ __launch_bounds__(kBinT) void k_bin(const uint64_t *u, uint64_t count
     for (; k < bk.nchunks; k += gridDim.x)
         bin_chunk<LAG>(k, count, t, bk, n_skipped, lds, key, v,
                        k + gridDim.x < bk.nchunks ? (k + gridDim.x) * kBinChunk : ~0ull, u);
+    BIN_T(0, 7);
 }
 
 // A/B builds (tools/): HQ_BIN_AB 1 = k_apply with plain LDS stores instead of the LDS max,
@@ -548,6 +549,7 @@ __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64
         lds_barrier();                                 // the rows' LDS is reused next bucket
         if (j == blockIdx.x / 8) BIN_T(1, 3);
     }
+    BIN_T(1, 7);
 }
 
 // one group's append of its run: lastIndex raised to new_last (16-byte form) or advanced by n

@@ -42,7 +42,7 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 12
+HQ_ABI_VERSION = 13
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -270,6 +270,8 @@ SIGNATURES = {
     "hq_tile_bits3_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
                                          ctypes.c_uint32, _vp, _vp]),
     "hq_readindex_vote_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "hq_readindex_vote_cq_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp,
+                                                       _vp, _vp]),
     "hq_tile_planes_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
                                           ctypes.c_uint32, _vp, _vp]),
     "hq_tile_planes_host": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
@@ -612,6 +614,15 @@ class Context:
     def readindex_vote_planes_dev(self, G, planes, confirmed, outcome) -> None:
         self._check(lib.hq_readindex_vote_planes_dev(self.h, G, _p(planes), _p(confirmed),
                                                      _p(outcome)))
+
+    def readindex_vote_cq_planes_dev(self, G, planes, active_planes, confirmed, outcome,
+                                     has_quorum) -> None:
+        """ReadIndex + vote + CheckQuorum in one launch (hq_readindex_vote_cq_planes_dev):
+        active_planes as tile_cq_planes_dev(..., n_uniform=8, self_slot=0) builds them, zeroed
+        in place."""
+        self._check(lib.hq_readindex_vote_cq_planes_dev(self.h, G, _p(planes), _p(active_planes),
+                                                        _p(confirmed), _p(outcome),
+                                                        _p(has_quorum)))
 
     def tile_planes_dev(self, G, ack, granted, rejected, n_voting, n_uniform, planes,
                         fallback=None) -> None:

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 12
+#define HQ_ABI_VERSION 13
 
 /* status codes */
 #define HQ_OK          0
@@ -519,6 +519,18 @@ static inline uint64_t hq_cq_plane_bytes(uint64_t G, uint32_t n_uniform) {
 }
 int hq_check_quorum_planes_dev(hq_ctx *ctx, uint64_t G, uint8_t *planes, uint32_t n_uniform,
                                uint64_t *has_quorum);
+/*
+ * ReadIndex + vote + CheckQuorum in one pass (ABI 13): planes as hq_readindex_vote_planes_dev
+ * (the groups' n from its n bits), active_planes = the CheckQuorum planes built with
+ * n_uniform 8 and self_slot 0 (7 planes of HQ_PLANE_TILE_GROUPS / 8 bytes per tile, plane k = the
+ * active flag of voting slot k + 1; hq_cq_plane_bytes(G, 8) bytes). Writes the confirmed and
+ * outcome words of hq_readindex_vote_planes_dev and the has_quorum words of
+ * hq_check_quorum_planes_dev, then zeroes the active planes (remote.go:196-198). Both plane
+ * buffers 16-byte aligned. The ack / vote / active flags of slots >= n are ignored.
+ */
+int hq_readindex_vote_cq_planes_dev(hq_ctx *ctx, uint64_t G, const uint8_t *planes,
+                                    uint8_t *active_planes, uint64_t *confirmed,
+                                    uint64_t *outcome, uint64_t *has_quorum);
 /* Columns (active u8 bitmap per group, bit s = voting slot s; n_voting, or n_uniform when NULL;
  * self_slot = the leader's slot) -> CheckQuorum planes (padding zeroed, 8-byte aligned);
  * fallback (may be NULL) receives the contract violations. */
