@@ -102,3 +102,5 @@ tools/lib_bintpb%/libhipquorum.so: $(SRCS) $(DEPS)
 tools/binprof: tools/binprof.hip $(SRCS) $(DEPS) $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -c -o tools/binprof.o tools/binprof.hip
 	$(HIPCC) $(HIPFLAGS) -pthread -o $@ tools/binprof.o $(filter-out $(LIBDIR)/hq_table.o,$(OBJS))
+tools/lib_plcqtpw%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_PLCQ_TPW=$*)

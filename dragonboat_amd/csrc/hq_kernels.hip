@@ -1054,6 +1054,10 @@ constexpr uint32_t kPlaneTile = HQ_PLANE_TILE_GROUPS;   // 2048
 #define HQ_PLANES_BLK 256
 #endif
 constexpr int kPlTPW = HQ_PLANES_TPW;
+// tiles per wave of the fused ReadIndex + vote + CheckQuorum pass (one after the other)
+#ifndef HQ_PLCQ_TPW
+#define HQ_PLCQ_TPW 1
+#endif
 
 __device__ __forceinline__ void full_add(uint32_t a, uint32_t b, uint32_t c, uint32_t &s,
                                          uint32_t &co) {
@@ -2140,7 +2144,8 @@ extern "C" int hq_readindex_vote_cq_planes_dev(hq_ctx *ctx, uint64_t G, const ui
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     const uint64_t ntiles = (G + kPlaneTile - 1) / kPlaneTile;
-    hipLaunchKernelGGL(k_planes_cq<HQ_PLANES_BLK>, dim3(grid_for(ntiles * 64, HQ_PLANES_BLK)),
+    hipLaunchKernelGGL(k_planes_cq<HQ_PLANES_BLK>,
+                       dim3(grid_for((ntiles + HQ_PLCQ_TPW - 1) / HQ_PLCQ_TPW * 64, HQ_PLANES_BLK)),
                        dim3(HQ_PLANES_BLK), 0, ctx->stream, k, active_planes);
     return hq::post_launch(ctx, "hq_readindex_vote_cq_planes");
 }
