@@ -13,11 +13,14 @@
 // triggers it, so no event waits for another's decision and a step is one launch, whatever the
 // events (the host worker cuts runs at such barriers and needs several passes).
 //
-// The outputs are lists whose lengths are not known in advance: the kernel runs twice over the
-// same state, first counting each group's records (on a private copy of the state), then, after
-// an exclusive scan of the counts (per-wave sums scanned, the lanes of a wave by shuffles in
-// pass B), writing every record at its place — in input group order, as the host worker lists
-// them — and writing the new state back.
+// The outputs are lists whose lengths are not known in advance: the kernel runs twice. Pass A
+// takes every group's events, counts its records, saves the state it found and writes the new
+// state in place; after an exclusive scan of the counts (per-wave sums scanned, the lanes of a
+// wave by shuffles in pass B) pass B replays, from the saved state, only the groups that have
+// records other than their commit — with the commits as a column (k_step_lite writes every
+// group's word from the saved and the new committed index) that is the quarter of a steady step
+// with a ReadIndex — writing every record at its place, in input group order, as the host worker
+// lists them. A step with an input error writes no state: k_step_restore puts the saved state back.
 #include <algorithm>
 #include <chrono>
 #include <new>
@@ -30,7 +33,7 @@
 namespace {
 
 enum List { kCommits, kReady, kResps, kStates, kDropped, kDeferred, kFallback, kDecisions,
-            kLists };
+            kRerun, kLists };   // kRerun: 1 for a group with records other than its commit
 // the worker's input checks, taken by pass A (which writes no group state) before pass B runs
 enum InputError : uint32_t { kErrHandle = 1, kErrOffsets = 2, kErrBoffsets = 4, kErrTwice = 8 };
 
@@ -61,6 +64,19 @@ struct StepK {
     uint64_t nw;                  //   (+1; k_wave_sums): pass B input with the counts
     char *out;                    // pass B: the lists, written straight into pinned host memory
     const struct Layout *layout;  //   at layout->off[list]
+    // pass A writes each group's new state in place and its state before the step here (same
+    // indexing as groups / members / reads): pass B replays the step from it, and a step with an
+    // input error puts it back (k_step_restore)
+    hq_dgroup *groups_old;        // (pad1 holds the members' active flags, bit s = member s)
+    uint64_t *match_old;
+    hq_dread *reads_old;
+    // pass A also writes every group's 4-byte advance where the advance column goes (offset 0
+    // of the host region) when spec_col is set: those PCIe writes then overlap the later chunks'
+    // input copies, and k_step_lite skips them when the layout picks that column (spec_valid)
+    uint32_t spec_col, spec_valid;
+    uint8_t *rerun;               // [n] pass A: bit 0 the group has records other than its
+                                  //   commit, bit 1 pass A stepped it (0: an input error)
+    uint32_t *rerun_list;         // [n] k_step_lite: the positions of those groups, in order
 };
 
 struct PackSize {                 // group i's size word -> events << 32 | bytes; i = n: 0 (the
@@ -170,6 +186,8 @@ __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
 
 // One group's state and its output cursor. WRITE = false: counting pass on a private copy;
 // WRITE = true: the same sequence writing records and, at the end, the new state.
+constexpr uint32_t kStageReady = 64;   // ReadyToRead records staged per wave in pass B
+
 template <bool WRITE, int MC>   // MC: member slots held in registers (8 or MC)
 struct Engine {
     const StepK &a;
@@ -185,10 +203,18 @@ struct Engine {
     hq_dread *rd;                 // the pending reads: a separate local array (run-time indexed)
     uint32_t cnt[kLists];
     uint32_t base[kLists];
+    // pass B: the wave's ReadyToRead records are staged in LDS from record stage_lo on (the
+    // records of a wave's groups are consecutive) and written out by the wave as one contiguous
+    // run of 16-byte lane stores: a 32-byte record stored per lane leaves half-filled lines
+    // whose writes cross PCIe as small packets
+    hq_ready_to_read *stage = nullptr;
+    uint32_t stage_lo = 0;
 
     __device__ __forceinline__ Engine(const StepK &k, uint64_t idx, uint32_t h, hq_dread *reads)
         : a(k), i(idx), rd(reads) {
-        g = k.groups[h];
+        // pass A: the group's state (then saved, and overwritten by its new state); pass B: the
+        // state pass A saved (node ids and roles never change in a step: the live records)
+        g = WRITE ? k.groups_old[h] : k.groups[h];
         gm = k.members + g.mem;
         active = 0;
 #pragma unroll
@@ -196,12 +222,13 @@ struct Engine {
             match[s] = 0;
             ids[s] = 0;
             if (s < g.n_members) {
-                match[s] = gm[s].match;
+                match[s] = WRITE ? k.match_old[g.mem + s] : gm[s].match;
                 ids[s] = gm[s].node_id;
-                active |= (uint32_t)(gm[s].active != 0) << s;
+                active |= (uint32_t)(WRITE ? (g.pad1 >> s) & 1 : gm[s].active != 0) << s;
             }
         }
-        for (uint32_t r = 0; r < g.n_reads; ++r) rd[r] = k.reads[(uint64_t)h * kDReads + r];
+        const hq_dread *rs = (WRITE ? k.reads_old : k.reads) + (uint64_t)h * kDReads;
+        for (uint32_t r = 0; r < g.n_reads; ++r) rd[r] = rs[r];
         for (int l = 0; l < kLists; ++l) {
             cnt[l] = 0;           // pass B: the wave's base + the counts of the lanes before
             base[l] = WRITE ? k.scan[(uint64_t)l * k.nw + (idx >> 6)] - k.scan[(uint64_t)l * k.nw] +
@@ -237,7 +264,11 @@ struct Engine {
     // -- outputs ----------------------------------------------------------------------------
     __device__ __forceinline__ void ready(uint64_t index, uint64_t low, uint64_t high) {
         const uint32_t p = slot(kReady);
-        if (WRITE) list<hq_ready_to_read>(kReady)[p] = hq_ready_to_read{g.cluster_id, index, low, high};
+        if (WRITE) {
+            const hq_ready_to_read r{g.cluster_id, index, low, high};
+            if (p - stage_lo < kStageReady) stage[p - stage_lo] = r;
+            else list<hq_ready_to_read>(kReady)[p] = r;
+        }
     }
     __device__ __forceinline__ void resp(uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
         const uint32_t p = slot(kResps);
@@ -477,14 +508,25 @@ struct Engine {
             atomicOr(a.error, (uint32_t)kErrBoffsets);
         if (!WRITE && g.committed - committed0 > 0xFFFFFFFFull && a.wide)
             atomicOr(a.wide, 1u);                        // no 4-byte advance column this step
-        if (WRITE && a.layout->commit_column == kColumn32) {   // every listed group's word
-            list<uint32_t>(kCommits)[i] = (uint32_t)(g.committed - committed0);
-        } else if (WRITE && a.layout->commit_column) {
-            list<uint64_t>(kCommits)[i] = g.committed != committed0 ? g.committed : 0;
+        if (!WRITE && a.spec_col)                        // the advance column, ahead of the layout
+            reinterpret_cast<uint32_t *>(a.out)[i] = (uint32_t)(g.committed - committed0);
+        if (WRITE && a.layout->commit_column) {
+            // every listed group's word: k_step_lite wrote it (from the saved and the new state)
         } else if (g.committed != committed0) {
             const uint32_t p = slot(kCommits);
             if (WRITE) list<hq_commit_event>(kCommits)[p] = hq_commit_event{g.cluster_id, g.committed};
         }
+    }
+
+    // pass A, before the group's events: its state as the step found it
+    __device__ __forceinline__ void save_old(uint32_t h) {
+        hq_dgroup o = g;
+        o.pad1 = active;
+        a.groups_old[h] = o;
+#pragma unroll
+        for (uint32_t s = 0; s < MC; ++s)
+            if (s < g.n_members) a.match_old[g.mem + s] = match[s];
+        for (uint32_t r = 0; r < g.n_reads; ++r) a.reads_old[(uint64_t)h * kDReads + r] = rd[r];
     }
 
     __device__ __forceinline__ void store(uint32_t h) {
@@ -513,9 +555,16 @@ template <bool WRITE, bool STREAM, int MC>
 #define HQ_STEP_OCC
 #endif
 __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
-    const uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
-    if (i >= a.i_end) return;
+    if (WRITE && a.layout->commit_column) {
+        // the commits are a column (k_step_lite wrote it from pass A's state): pass B takes
+        // only the groups with other records, packed at the front of the grid
+        if (i >= a.layout->len[kRerun]) return;
+        i = a.rerun_list[i];
+    } else if (i >= a.i_end) {
+        return;
+    }
     uint64_t e0, e1, b0 = 0, b1 = 0;
     if (STREAM && a.prefix) {
         const uint64_t x0 = a.prefix[i], x1 = a.prefix[i + 1];
@@ -549,20 +598,83 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
         if (err) {
             atomicOr(a.error, err);
             for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = 0;
+            a.rerun[i] = 0;       // not stepped: nothing to restore
             return;
         }
     }
     hq_dread reads[kDReads];
     Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
+    if (!WRITE) eng.save_old(h);
+    __shared__ hq_ready_to_read stage[WRITE ? 256 / 64 : 1][WRITE ? kStageReady : 1];
+    if (WRITE) {                  // the wave's first record: its first active lane's (in order)
+        eng.stage = stage[threadIdx.x >> 6];
+        eng.stage_lo = __builtin_amdgcn_readfirstlane(eng.base[kReady]);
+    }
     if (STREAM)
         eng.template run<true>(e0, e1, a.bytes + b0, a.bytes + b1);
     else
         eng.template run<false>(e0, e1, nullptr, nullptr);
-    if (WRITE) {
-        eng.store(h);
-    } else {
-        for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
+    if (WRITE) {                  // the staged records out, 16 contiguous bytes per lane
+        const uint64_t act = __ballot(1);
+        const int last = 63 - __clzll((long long)act);
+        const uint32_t end = __shfl(eng.base[kReady] + eng.cnt[kReady], last);
+        const uint32_t nrec = min(end - eng.stage_lo, kStageReady);
+        const uint32_t rank = __popcll(act & ((1ull << (threadIdx.x & 63)) - 1));
+        const uint32_t nact = __popcll(act);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS stores landed
+        __builtin_amdgcn_wave_barrier();
+        const uint4 *src = reinterpret_cast<const uint4 *>(eng.stage);
+        uint4 *dst = reinterpret_cast<uint4 *>(eng.template list<hq_ready_to_read>(kReady) +
+                                               eng.stage_lo);
+        for (uint32_t q = rank; q < 2 * nrec; q += nact) dst[q] = src[q];
     }
+    if (!WRITE) {                 // the new state in place (pass B replays from the saved one)
+        const bool rerun = (eng.cnt[kReady] | eng.cnt[kResps] | eng.cnt[kStates] |
+                            eng.cnt[kDropped] | eng.cnt[kDeferred] | eng.cnt[kFallback]) != 0;
+        eng.cnt[kRerun] = rerun;
+        for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
+        a.rerun[i] = (uint8_t)(2 | rerun);
+        eng.store(h);
+    }
+}
+
+// Between the layout and pass B: with the commits as a column, every listed group's word from
+// the committed index pass A saved and the one it wrote (the advance, or the new index), and the
+// positions of the groups with other records packed in order for pass B; in list mode nothing
+__global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || (a.layout->error | a.layout->overflow) || !a.layout->commit_column) return;
+    const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
+    const uint64_t c0 = a.groups_old[h].committed, c1 = a.groups[h].committed;
+    char *col = a.out + a.layout->off[kCommits];
+    if (a.layout->commit_column == kColumn32) {
+        if (!a.spec_valid) reinterpret_cast<uint32_t *>(col)[i] = (uint32_t)(c1 - c0);
+    } else {
+        reinterpret_cast<uint64_t *>(col)[i] = c1 != c0 ? c1 : 0;
+    }
+    if (a.rerun[i] & 1) {         // the wave's base + the lanes before (k_wave_sums)
+        const uint64_t l = kRerun;
+        a.rerun_list[a.scan[l * a.nw + (i >> 6)] - a.scan[l * a.nw] + a.counts[l * a.n + i]] =
+            (uint32_t)i;
+    }
+}
+
+// A step with an input error writes no group state: the groups pass A stepped get back the
+// state it saved (the host launches this only when k_layout reported an error)
+__global__ __launch_bounds__(256) void k_step_restore(const StepK a) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || !(a.rerun[i] & 2)) return;
+    const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
+    hq_dgroup g = a.groups_old[h];
+    const uint32_t act = g.pad1;
+    g.pad1 = 0;
+    a.groups[h] = g;
+    for (uint32_t s = 0; s < g.n_members; ++s) {
+        a.members[g.mem + s].match = a.match_old[g.mem + s];
+        a.members[g.mem + s].active = (uint8_t)((act >> s) & 1);
+    }
+    for (uint32_t r = 0; r < g.n_reads; ++r)
+        a.reads[(uint64_t)h * kDReads + r] = a.reads_old[(uint64_t)h * kDReads + r];
 }
 
 // per-wave sums of pass A's counts, [kLists][nw] + a trailing 0 (its exclusive scan's last
@@ -598,7 +710,7 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
     if (threadIdx.x != 0) return;
     const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
                                   sizeof(hq_read_index_resp), sizeof(hq_state_change),
-                                  sizeof(hq_dropped_read), 8, 8, 0};
+                                  sizeof(hq_dropped_read), 8, 8, 0, 0};
     uint64_t total = 0;
     const uint32_t commits = scan[nw] - scan[0];
     // the commits as a column when that moves fewer bytes (16 per commit in the list against 8
@@ -641,6 +753,13 @@ struct hq_dstep {
     hq_dgroup *groups = nullptr;
     hq_dread *reads = nullptr;
     hq_dmember *members = nullptr;
+    // the state pass A saved (StepK::groups_old ...), as large as the state
+    hq_dgroup *groups_old = nullptr;
+    hq_dread *reads_old = nullptr;
+    uint64_t *match_old = nullptr;
+    uint8_t *rerun = nullptr;     // [rcap] per listed group
+    uint32_t *rerun_list = nullptr;
+    size_t rcap = 0;
     uint32_t *stamp = nullptr;    // [gcap] step stamps (duplicate handles)
     uint64_t gcap = 0, mcap = 0;
     uint64_t n_groups = 0;        // group records uploaded (valid handles)
@@ -737,7 +856,9 @@ void hq_dstep_close(hq_dstep *d) {
     (void)hipStreamSynchronize(d->ctx->stream);
     for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, (void *)d->stamp, d->in,
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp,
-                    (void *)d->layout})
+                    (void *)d->layout, (void *)d->groups_old, (void *)d->reads_old,
+                    (void *)d->match_old, (void *)d->rerun,
+                    (void *)d->rerun_list})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
     if (d->host_layout) (void)hipHostFree(d->host_layout);
@@ -768,8 +889,17 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
         if (!rc)
             rc = grow(ctx, reinterpret_cast<void **>(&d->stamp), &sc, (g0 + ng) * 4, true,
                       "hq_dstep stamps");
+        // the saved-state buffers only live within a step: grown without their contents
+        size_t gn = d->gcap * sizeof(hq_dgroup), rn = d->gcap * kDReads * sizeof(hq_dread);
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->groups_old), &gn,
+                      (g0 + ng) * sizeof(hq_dgroup), false, "hq_dstep saved groups");
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->reads_old), &rn,
+                      (g0 + ng) * kDReads * sizeof(hq_dread), false, "hq_dstep saved reads");
         if (!rc) d->gcap = std::min({gc / sizeof(hq_dgroup), rcap / (kDReads * sizeof(hq_dread)),
-                                     sc / 4});
+                                     sc / 4, gn / sizeof(hq_dgroup),
+                                     rn / (kDReads * sizeof(hq_dread))});
     }
     for (uint64_t i = 0; i < ng; ++i)
         if (g[i].n_members > d->max_members) d->max_members = g[i].n_members;
@@ -778,9 +908,13 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
         if (!rc && g0 + ng > d->n_groups) d->n_groups = g0 + ng;
     }
     if (!rc && (m0 + nm) > d->mcap) {
+        size_t xn = d->mcap * 8;
         rc = grow(ctx, reinterpret_cast<void **>(&d->members), &mc,
                   (m0 + nm) * sizeof(hq_dmember), true, "hq_dstep members");
-        if (!rc) d->mcap = mc / sizeof(hq_dmember);
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->match_old), &xn, (m0 + nm) * 8, false,
+                      "hq_dstep saved matches");
+        if (!rc) d->mcap = std::min(mc / sizeof(hq_dmember), xn / 8);
     }
     if (!rc && ng)
         rc = hq::check_hip(ctx, hipMemcpyAsync(d->groups + g0, g, ng * sizeof(hq_dgroup),
@@ -865,6 +999,14 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
     }
+    if (!rc && n > d->rcap) {
+        size_t fc = d->rcap, lc = d->rcap * 4;
+        rc = grow(ctx, reinterpret_cast<void **>(&d->rerun), &fc, n, false, "hq_dstep rerun");
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->rerun_list), &lc, n * 4, false,
+                      "hq_dstep rerun list");
+        if (!rc) d->rcap = std::min(fc, lc / 4);
+    }
     // the host region the lists go to: last step's size with room to spare (a step that needs
     // more runs pass B again after growing it)
     if (!rc && !d->host_out) {
@@ -922,6 +1064,15 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.wide = d->commit_column & kColumn32 ? d->bases + 1 : nullptr;   // likewise
     k.out = static_cast<char *>(d->host_out);
     k.layout = d->layout;
+    k.groups_old = d->groups_old;
+    k.match_old = d->match_old;
+    // pass A's advance words need the column allowed and the region to hold n of them (its
+    // offset 0 is the commits list's in every layout)
+    k.spec_col = (d->commit_column & kColumn32) && n * 4 <= d->host_out_cap;
+    k.spec_valid = k.spec_col;
+    k.reads_old = d->reads_old;
+    k.rerun = d->rerun;
+    k.rerun_list = d->rerun_list;
     const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
     auto launch = [&](bool write, uint64_t i0, uint64_t i1) {
         k.i_begin = i0;
@@ -1008,6 +1159,11 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
                                (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout);
             rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
         }
+        const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+        if (!rc) {
+            hipLaunchKernelGGL(k_step_lite, grid, blk, 0, ctx->stream, k);
+            rc = hq::check_hip(ctx, hipGetLastError(), "k_step_lite");
+        }
         launch(true, 0, n);
         if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(d->host_layout, d->layout, sizeof(Layout),
                                                         hipMemcpyDeviceToHost, ctx->stream), "D2H");
@@ -1017,7 +1173,12 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const uint64_t t1 = now_ns();
     if (rc) return rc;
     const Layout &lay = *d->host_layout;
-    if (lay.error) {              // no group state was written
+    if (lay.error) {              // no group state is written: pass A's is taken back
+        hipLaunchKernelGGL(k_step_restore, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           ctx->stream, k);
+        rc = hq::check_hip(ctx, hipGetLastError(), "k_step_restore");
+        if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep restore");
+        if (rc) return rc;
         out->input_error = lay.error;
         return HQ_E_INVAL;
     }
@@ -1031,6 +1192,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (rc) return rc;
         d->host_out_cap = want;
         k.out = static_cast<char *>(d->host_out);
+        k.spec_valid = 0;         // pass A's advance words went with the old region
         pass_b();
         if (rc) return rc;
         if (lay.overflow || lay.error) return hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout");

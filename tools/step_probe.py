@@ -56,6 +56,10 @@ for s in range(STEPS):
     if os.environ.get("PER_WORKER") and W > 1:
         print("  device ms per worker:", " ".join(f"{r['device_ns'] / 1e6:.2f}" for r in res),
               "| host ms:", " ".join(f"{r['handle_ns'] / 1e6:.2f}" for r in res), flush=True)
+    if os.environ.get("LISTS"):
+        print("  lists:", {k: sum(len(r[k]) for r in res if r.get(k) is not None)
+                           for k in ("ready", "read_resps", "state_changes", "dropped_reads",
+                                     "deferred", "fallback_groups")}, flush=True)
     print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, W={W}, "
           f"max device {dev:.2f} ms, input {sum(getattr(x, 'nbytes', 0) for p in inputs for x in p) / 1e6:.1f} MB",
           flush=True)
