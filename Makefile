@@ -104,3 +104,5 @@ tools/binprof: tools/binprof.hip $(SRCS) $(DEPS) $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -pthread -o $@ tools/binprof.o $(filter-out $(LIBDIR)/hq_table.o,$(OBJS))
 tools/lib_plcqtpw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLCQ_TPW=$*)
+tools/lib_stepchunks%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_STEP_CHUNKS=$*)

@@ -703,7 +703,13 @@ __global__ __launch_bounds__(256) void k_wave_sums(uint32_t *counts, uint64_t n,
 
 // the lists' place in the host output region (of cap bytes) from the scanned per-wave sums, and
 // the input errors of pass A (reset for the next step)
-constexpr int kMaxChunks = 4;
+// input chunks of a large step (at least kChunkGroups groups each): chunk c's copy overlaps pass A
+// of chunk c - 1, and the last chunk's pass A is the step's tail (8 chunks: no faster, profiles/r03e/ab_step_chunks.log)
+#ifndef HQ_STEP_CHUNKS
+#define HQ_STEP_CHUNKS 4
+#endif
+constexpr int kMaxChunks = HQ_STEP_CHUNKS;
+constexpr uint64_t kChunkGroups = 65536;
 __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t *error,
                          uint64_t cap, uint32_t allow_column, Layout *lay) {
     uint32_t *wide = error + 1;   // pass A: an advance of 2^32 or more
@@ -960,7 +966,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     const uint64_t t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     // chunks of groups (at least 64 Ki each): chunk c's input copy overlaps pass A of chunk c - 1
-    const int chunks = n >= 4 * 65536 ? 4 : n >= 2 * 65536 ? 2 : 1;
+    int chunks = 1;
+    while (chunks * 2 <= kMaxChunks && n >= (uint64_t)chunks * 2 * kChunkGroups) chunks *= 2;
     uint64_t bound[kMaxChunks + 1];
     for (int c = 0; c <= chunks; ++c) bound[c] = n * c / chunks;
     // the step's input in one device region: handles, offsets, [boffsets,] events or bytes, each
