@@ -12,11 +12,11 @@ mkdir -p $OUT
 set -o pipefail
 echo "== kernel trace ($W)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 bench.py $ARGS --no-cpu > $OUT/trace_stdout.log 2>&1 || exit $?
+  python3 bench.py $ARGS --no-cpu --detail-out $OUT/trace_detail.json > $OUT/trace_stdout.log 2>&1 || exit $?
 tail -n 1 $OUT/trace_stdout.log
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C ($W)"
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$C -o run -- \
-    python3 bench.py $ARGS --no-cpu --steps 40 --warmup 4 > $OUT/pmc_${C}_stdout.log 2>&1 || exit $?
+    python3 bench.py $ARGS --no-cpu --steps 40 --warmup 4 --detail-out $OUT/pmc_${C}_detail.json > $OUT/pmc_${C}_stdout.log 2>&1 || exit $?
 done
 find $OUT -name "*.csv" | sort

@@ -32,7 +32,7 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2,
           "c2ll": "k_commit_lag_big<3, 0, 4, false, 1>", "c5ll": "k_commit_lag_fused<2, 512, 1>",
           "c5l": "k_commit_lag_fused<2, 512, 0>", "rim": "k_ri_multi2<false, false, 4, false>", "rimt": "k_ri_multi2<false, false, 4, true>",
           "cq": "k_bits<4, false, 256, false, true>", "cqp": "k_cq_planes<6, false, 256>",
-          "ing": "k_table_ingest<false, false>",
+          "ing": ("k_bin<false>", "k_apply<false>"), "c4pq": "k_planes_cq<256>",
           "ingo": "k_table_ingest<true, false>", "rim2": "k_ri_multi2",
           "c4t3": "k_bits3<256>", "c4p": "k_planes<256>"}
 
@@ -51,13 +51,20 @@ def main():
     traffic = json.load(open(tj)) if os.path.exists(tj) else {}
     for w in workloads:
         src = os.path.join(ROOT, "gpurun_out", f"prof_{w}")
-        k = KERNEL[w]
+        ks = KERNEL[w] if isinstance(KERNEL[w], tuple) else (KERNEL[w],)   # a step's kernels
+        k = " + ".join(ks)
         shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                     os.path.join(dst, f"{w}_kernel_stats.csv"))
         stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, f"{w}_kernel_stats.csv")))}
-        row = next(v for n, v in stats.items() if k in n)
-        fetch, nf = counter(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"), k)
-        write, nw = counter(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), k)
+        rows = [next(v for n, v in stats.items() if kk in n) for kk in ks]
+        row = {"AverageNs": sum(float(r["AverageNs"]) for r in rows),
+               "Calls": min(int(r["Calls"]) for r in rows)}
+        fc = [counter(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"), kk)
+              for kk in ks]
+        wc = [counter(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), kk)
+              for kk in ks]
+        fetch, nf = sum(v for v, _ in fc), min(n for _, n in fc)
+        write, nw = sum(v for v, _ in wc), min(n for _, n in wc)
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             shutil.copy(os.path.join(src, f"pmc_{c}", "run_counter_collection.csv"),
                         os.path.join(dst, f"{w}_pmc_{c}.csv"))
