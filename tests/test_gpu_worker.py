@@ -491,3 +491,52 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
     finally:
         dev.close()
         host.close()
+
+
+@pytest.mark.parametrize("feed", ["sized", "sized-advance"])
+@pytest.mark.parametrize("seed", [11, 12])
+def test_rejected_steps_restore_state_on_device(hq, seed, feed):
+    """The device engine writes each group's new state in pass A and puts the saved state back
+    when the step turns out to have an input error (k_step_restore): before every good step of a
+    random multi-step run, the same step is offered with a group listed twice or with one byte
+    moved between two groups' sizes (the left-over-bytes check) and must be rejected whole —
+    every group's full state (members' match and active flags, pending reads, votes) equal to
+    the oracle's, which never saw the bad step — and the good step then matches the oracle."""
+    rng = np.random.default_rng(seed)
+    G, steps = 600, 8
+    groups = sr.random_groups(rng, G)
+    o = OracleBackend()
+    w = WorkerBackend(hq, n_max=8, seed=seed, on_device=True, stream=feed)
+    try:
+        for g in groups:
+            o.add_group(*g)
+            w.add_group(*g)
+        ctx_seq = [0]
+        rejected = 0
+        for s in range(steps):
+            per = {g[0]: sr.random_events(rng, o.state(g[0]), s + 1, ctx_seq)
+                   for g in groups if rng.random() < 0.9}
+            (grp, sizes, ne, data), _ = w.build_inputs(per)
+            bad = [(np.concatenate([grp[:1], grp[:1], grp[2:]]), sizes, "listed twice")]
+            nb = sizes >> 16                   # per-group bytes
+            k = int(np.nonzero(nb[1:] > 0)[0][0])
+            moved = sizes.copy()
+            moved[k] += np.uint32(1 << 16)     # group k keeps the first byte of group k + 1:
+            moved[k + 1] -= np.uint32(1 << 16)  # its events leave that byte over
+            bad.append((grp, moved, "malformed"))
+            for bg, bz, msg in bad:
+                with pytest.raises(hq.HQError, match=msg):
+                    w.w.step_sized(bg, bz, ne, data)
+                rejected += 1
+                for g in groups:
+                    assert w.state(g[0]) == o.state(g[0]), (s, msg, g[0])
+            want = o.step(per)
+            got = w.step(per)
+            assert got["_fallback"] == []
+            for cid in per:
+                same_step(want, got, cid)
+            for g in groups:
+                assert w.state(g[0]) == o.state(g[0]), (s, g[0])
+        assert rejected == 2 * steps
+    finally:
+        w.close()
