@@ -711,7 +711,7 @@ __global__ __launch_bounds__(256) void k_wave_sums(uint32_t *counts, uint64_t n,
 constexpr int kMaxChunks = HQ_STEP_CHUNKS;
 constexpr uint64_t kChunkGroups = 65536;
 __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t *error,
-                         uint64_t cap, uint32_t allow_column, Layout *lay) {
+                         uint64_t cap, uint32_t allow_column, Layout *lay, Layout *host_lay) {
     uint32_t *wide = error + 1;   // pass A: an advance of 2^32 or more
     if (threadIdx.x != 0) return;
     const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
@@ -744,6 +744,7 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
         *error = 0;
         *wide = 0;
     }
+    *host_lay = *lay;             // the host's copy, written into pinned memory (no copy launch)
 }
 
 uint64_t now_ns() {
@@ -1163,7 +1164,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     auto pass_b = [&]() {
         if (!rc) {
             hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, nw, k.error,
-                               (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout);
+                               (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout,
+                               d->host_layout);
             rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
         }
         const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
@@ -1172,8 +1174,6 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
             rc = hq::check_hip(ctx, hipGetLastError(), "k_step_lite");
         }
         launch(true, 0, n);
-        if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(d->host_layout, d->layout, sizeof(Layout),
-                                                        hipMemcpyDeviceToHost, ctx->stream), "D2H");
         if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
     };
     pass_b();
