@@ -106,3 +106,5 @@ tools/lib_plcqtpw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLCQ_TPW=$*)
 tools/lib_stepchunks%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_STEP_CHUNKS=$*)
+tools/lib_plcqzero%/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_PLCQ_ZERO_EARLY=$*)

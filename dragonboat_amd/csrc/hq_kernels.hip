@@ -1058,6 +1058,11 @@ constexpr int kPlTPW = HQ_PLANES_TPW;
 #ifndef HQ_PLCQ_TPW
 #define HQ_PLCQ_TPW 1
 #endif
+// the fused pass zeroes the active planes right behind their loads (1: 15.5-15.7 us per 16 M x 7
+// launch, 70-71 % of peak) or after the decision (0: 15.7-15.9 us; profiles/r03c/ab_c4pq_zero_early.log)
+#ifndef HQ_PLCQ_ZERO_EARLY
+#define HQ_PLCQ_ZERO_EARLY 1
+#endif
 
 __device__ __forceinline__ void full_add(uint32_t a, uint32_t b, uint32_t c, uint32_t &s,
                                          uint32_t &co) {
@@ -1217,6 +1222,11 @@ __global__ __launch_bounds__(BLK) void k_planes_cq(const BitsK a, uint8_t *activ
         for (int k = 0; k < 24; ++k) p[k] = __builtin_nontemporal_load(base + k * 64);
 #pragma unroll
         for (int k = 0; k < 7; ++k) q[k] = __builtin_nontemporal_load(abase + k * 64);
+#if HQ_PLCQ_ZERO_EARLY
+        // the zeroes go out right behind the loads of the same words (in order per wave)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(0u, abase + k * 64);
+#endif
         const uint64_t g = t * kPlaneTile + lane * 32;
         if (t * kPlaneTile + kPlaneTile <= a.G) {
             planes_slot<true, true>(a, g, p, q);
@@ -1226,8 +1236,10 @@ __global__ __launch_bounds__(BLK) void k_planes_cq(const BitsK a, uint8_t *activ
             reinterpret_cast<uint32_t *>(a.confirmed)[g >> 5] = 0;
             reinterpret_cast<uint32_t *>(a.has_quorum)[g >> 5] = 0;
         }
+#if !HQ_PLCQ_ZERO_EARLY
 #pragma unroll
         for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(0u, abase + k * 64);
+#endif
     }
 }
 

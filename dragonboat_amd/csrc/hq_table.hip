@@ -239,7 +239,13 @@ __global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uin
 // atomic, which k_apply's later read of the row sees (kernel boundary).
 constexpr int kBinThreads = 1024;                                 // k_apply's workgroup
 constexpr int kBinT = 1024;                                       // k_bin's workgroup
-constexpr int kBinPer = 8;                                        // records per thread and chunk
+// records per thread and chunk (HQ_BIN_PER 16, chunks of 16 Ki with whole-wave segments in
+// k_apply, HQ_APPLY_SEG 64: k_bin then holds 16 records' keys, values, buckets and ranks and
+// spills 103 VGPRs — not measured)
+#ifndef HQ_BIN_PER
+#define HQ_BIN_PER 8
+#endif
+constexpr int kBinPer = HQ_BIN_PER;
 constexpr uint64_t kBinChunk = (uint64_t)kBinT * kBinPer;         // 8192 records per chunk
 constexpr uint32_t kBinMaxBuckets = 8192;                         // k_bin: 64 KB + 8 B per bucket
 
@@ -437,6 +443,9 @@ __device__ __forceinline__ bool bin_apply(const TableK &t, uint32_t R, uint64_t 
     return false;
 }
 
+#ifndef HQ_APPLY_SEG
+#define HQ_APPLY_SEG 32
+#endif
 constexpr int kApplyEnt = 6;                              // entries per thread and round
 constexpr uint32_t kApplyLds = 128 * 1024;                // a bucket's rows in k_apply's LDS
 constexpr int kApplyRows = (int)(kApplyLds / 16 / kBinThreads);  // row pairs per thread (8)
@@ -500,14 +509,16 @@ __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64
         // its l-th entry; a segment averages kBinChunk / B entries), NE chunks per round with
         // every entry load issued before the first LDS max; segments longer than 32 entries
         // finish in a loop of their own
-        const uint32_t wv = tid >> 6, h = (tid >> 5) & 1, l = tid & 31;
-        constexpr uint32_t kHalves = 2 * kBinThreads / 64;      // half-waves per workgroup
+        // (HQ_APPLY_SEG = 64: a whole wave per segment, for chunks of 16 Ki records)
+        constexpr uint32_t kSeg = HQ_APPLY_SEG;
+        const uint32_t wv = tid >> 6, h = kSeg == 32 ? (tid >> 5) & 1 : 0, l = tid & (kSeg - 1);
+        constexpr uint32_t kHalves = (64 / kSeg) * kBinThreads / 64;   // segments in flight
         for (uint32_t c0 = 0; c0 < bk.nchunks; c0 += kHalves * NE) {
             uint32_t m[NE];
             uint64_t ent[NE];
 #pragma unroll
             for (int u = 0; u < NE; ++u) {           // unconditional loads (see bin_load)
-                const uint32_t c = c0 + (uint32_t)u * kHalves + 2 * wv + h;
+                const uint32_t c = c0 + (uint32_t)u * kHalves + (64 / kSeg) * wv + h;
                 const uint32_t cc = c < bk.nchunks ? c : 0;
                 m[u] = c < bk.nchunks ? M[c] : 0u;
                 ent[u] = __builtin_nontemporal_load(bk.ent + (uint64_t)cc * kBinChunk +
@@ -523,8 +534,8 @@ __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64
             }
 #pragma unroll
             for (int u = 0; u < NE; ++u) {           // the rare segments beyond 32 entries
-                const uint32_t c = c0 + (uint32_t)u * kHalves + 2 * wv + h;
-                for (uint32_t k = l + 32; k < (m[u] >> 16); k += 32) {
+                const uint32_t c = c0 + (uint32_t)u * kHalves + (64 / kSeg) * wv + h;
+                for (uint32_t k = l + kSeg; k < (m[u] >> 16); k += kSeg) {
                     const bool sk = bin_apply<LAG>(
                         t, R, rows, bk.ent[(uint64_t)c * kBinChunk + (m[u] & 0xFFFFu) + k]);
                     if (LAG && sk && n_skipped)

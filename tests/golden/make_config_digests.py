@@ -6,6 +6,7 @@ oracle still reproduces them; the GPU tests check the kernels produce the same b
 device generator's inputs, in the headline layouts.
 
 usage: python tests/golden/make_config_digests.py   (from the repo root; ~1 minute on 8 cores)
+       python tests/golden/make_config_digests.py --c5-node   (adds only the 8-GPU C5 shards)
 """
 import hashlib
 import json
@@ -63,10 +64,34 @@ def main():
         cases[f"C5_bucket{b}"] = commit_case(f"C5_bucket{b}", SEED + 4, rng.count,
                                              shard.MIXED_VOTERS[b], 2, rng.cid_base,
                                              rng.cid_stride)
+    cases.update(c5_node_cases())
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config_digests.json")
     json.dump(cases, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(cases, indent=1))
 
 
+def c5_node_cases():
+    """BASELINE config 5 whole: 64 Mi groups, n = 3 / 5 / 7 by clusterID % 3, sharded
+    clusterID % 8 over 8 GPUs (partition.go:38): 8 ranks x 3 buckets of (8 Mi / 3) groups, each
+    rank's buckets as bench.py builds them (shard.rank_bucket)."""
+    from dragonboat_amd import shard
+
+    per = (8 << 20) // 3
+    out = {}
+    for r in range(8):
+        for b in range(3):
+            rng = shard.rank_bucket(r, 8, b, per)
+            out[f"C5x8_rank{r}_bucket{b}"] = commit_case(
+                f"C5x8_rank{r}_bucket{b}", SEED + 4, rng.count, shard.MIXED_VOTERS[b], 2,
+                rng.cid_base, rng.cid_stride)
+    return out
+
+
 if __name__ == "__main__":
-    main()
+    if "--c5-node" in sys.argv:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config_digests.json")
+        cases = json.load(open(path))
+        cases.update(c5_node_cases())
+        json.dump(cases, open(path, "w"), indent=1, sort_keys=True)
+    else:
+        main()

@@ -106,3 +106,33 @@ def test_gpu_c4_digest(gpu_ctx, hq, path):
     assert digest(gpu_ctx.download(outc)) == c["outcome"]
     for x in cols + [conf, outc] + extra:
         gpu_ctx.free(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank", range(8))
+def test_gpu_c5_node_shard_digest(gpu_ctx, hq, rank):
+    """BASELINE config 5 whole — 64 Mi groups with 3 / 5 / 7 voters (clusterID % 3), sharded
+    clusterID % 8 over 8 GPUs (partition.go:38) — one GPU's share per case: its three buckets
+    generated on the device, decided in one fused launch over leader-row tiles, equal to the
+    oracle's digests of that shard (tests/golden/make_config_digests.py --c5-node). Together the
+    eight cases check every decision of the 8-GPU configuration on one GPU."""
+    cases = [GOLD[f"C5x8_rank{rank}_bucket{b}"] for b in range(3)]
+    got = _commit_on_gpu(gpu_ctx, hq, cases, hq.HQ_LAYOUT_TILES_LEADER)
+    for c, g in zip(cases, got):
+        assert g == (c["committed"], c["changed"], c["fallback"])
+
+
+def test_c5_node_digests_cover_the_config():
+    """The 24 shard-bucket cases are the 64 Mi-group config: 8 ranks x 3 buckets, disjoint
+    clusterID progressions covering cid % 24 == every residue."""
+    from dragonboat_amd import shard
+
+    keys = [f"C5x8_rank{r}_bucket{b}" for r in range(8) for b in range(3)]
+    assert all(k in GOLD for k in keys)
+    assert sum(GOLD[k]["G"] for k in keys) == 24 * ((8 << 20) // 3)
+    assert len({GOLD[k]["cid_base"] % 24 for k in keys}) == 24
+    for r in range(8):
+        for b in range(3):
+            c = GOLD[f"C5x8_rank{r}_bucket{b}"]
+            assert c["cid_base"] % 8 == r and c["cid_base"] % 3 == b and c["cid_stride"] == 24
+            assert c["n"] == shard.MIXED_VOTERS[b]
