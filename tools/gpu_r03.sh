@@ -31,6 +31,20 @@ if [ "${REHEARSE:-1}" = 1 ]; then
     --extra c5v5tl,c4p,cqp --detail-out gpurun_out/bench_n2_detail.json
   rc=$?; if fatal $rc; then exit $rc; fi
 fi
+# the driver's multi-GPU launch (torchrun, one rank per GPU), rehearsed with two ranks sharing
+# the one GPU (gloo for the timing collectives), and BASELINE config 5's 8-GPU share layout with
+# eight contexts on the one GPU
+if [ "${REHEARSE_TORCHRUN:-0}" = 1 ]; then
+  step bench_torchrun_n2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu \
+    --extra c5v5tl --detail-out gpurun_out/bench_torchrun_n2_detail.json
+  rc=$?; if fatal $rc; then exit $rc; fi
+fi
+if [ "${REHEARSE8:-0}" = 1 ]; then
+  step bench_c5tl_n8_threads 400 python -u bench.py --gpus 8 --workload c5tl --steps 20 \
+    --warmup 5 --no-cpu --extra= --detail-out gpurun_out/bench_c5tl_n8_detail.json
+  rc=$?; if fatal $rc; then exit $rc; fi
+fi
 for W in ${PROFILE:-}; do
   step prof_$W 400 bash tools/profile_bench.sh $W || exit $?
 done
