@@ -75,7 +75,10 @@ struct StepK {
     // input copies, and k_step_lite skips them when the layout picks that column (spec_valid)
     uint32_t spec_col, spec_valid;
     uint8_t *rerun;               // [n] pass A: bit 0 the group has records other than its
-                                  //   commit, bit 1 pass A stepped it (0: an input error)
+                                  //   commit (and not just one ReadyToRead), bit 1 pass A stepped
+                                  //   it (0: an input error), bit 2 its only record besides the
+                                  //   commit is one ReadyToRead, kept in ready_slot
+    hq_ready_to_read *ready_slot; // [n] pass A: a group's first ReadyToRead of the step
     uint32_t *rerun_list;         // [n] k_step_lite: the positions of those groups, in order
 };
 
@@ -264,10 +267,13 @@ struct Engine {
     // -- outputs ----------------------------------------------------------------------------
     __device__ __forceinline__ void ready(uint64_t index, uint64_t low, uint64_t high) {
         const uint32_t p = slot(kReady);
-        if (WRITE) {
-            const hq_ready_to_read r{g.cluster_id, index, low, high};
-            if (p - stage_lo < kStageReady) stage[p - stage_lo] = r;
-            else list<hq_ready_to_read>(kReady)[p] = r;
+        const hq_ready_to_read r{g.cluster_id, index, low, high};
+        if (!WRITE) {
+            if (p == 0) a.ready_slot[i] = r;              // k_step_lite copies it out
+        } else if (stage && p - stage_lo < kStageReady) {
+            stage[p - stage_lo] = r;
+        } else {
+            list<hq_ready_to_read>(kReady)[p] = r;
         }
     }
     __device__ __forceinline__ void resp(uint64_t to, uint64_t index, uint64_t hint, uint64_t high) {
@@ -606,7 +612,11 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
     Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
     if (!WRITE) eng.save_old(h);
     __shared__ hq_ready_to_read stage[WRITE ? 256 / 64 : 1][WRITE ? kStageReady : 1];
-    if (WRITE) {                  // the wave's first record: its first active lane's (in order)
+    // list mode: the wave's groups are consecutive and so are their records, staged from its
+    // first active lane's on; column mode: the groups replayed are a sparse subset whose records
+    // lie between k_step_lite's, so each is stored where it goes
+    const bool staged = WRITE && !a.layout->commit_column;
+    if (staged) {
         eng.stage = stage[threadIdx.x >> 6];
         eng.stage_lo = __builtin_amdgcn_readfirstlane(eng.base[kReady]);
     }
@@ -614,7 +624,7 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
         eng.template run<true>(e0, e1, a.bytes + b0, a.bytes + b1);
     else
         eng.template run<false>(e0, e1, nullptr, nullptr);
-    if (WRITE) {                  // the staged records out, 16 contiguous bytes per lane
+    if (staged) {                 // the staged records out, 16 contiguous bytes per lane
         const uint64_t act = __ballot(1);
         const int last = 63 - __clzll((long long)act);
         const uint32_t end = __shfl(eng.base[kReady] + eng.cnt[kReady], last);
@@ -629,11 +639,13 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
         for (uint32_t q = rank; q < 2 * nrec; q += nact) dst[q] = src[q];
     }
     if (!WRITE) {                 // the new state in place (pass B replays from the saved one)
-        const bool rerun = (eng.cnt[kReady] | eng.cnt[kResps] | eng.cnt[kStates] |
-                            eng.cnt[kDropped] | eng.cnt[kDeferred] | eng.cnt[kFallback]) != 0;
+        const bool others = (eng.cnt[kResps] | eng.cnt[kStates] | eng.cnt[kDropped] |
+                             eng.cnt[kDeferred] | eng.cnt[kFallback]) != 0;
+        const bool rerun = others || eng.cnt[kReady] > 1;
+        const bool one_ready = !rerun && eng.cnt[kReady] == 1;
         eng.cnt[kRerun] = rerun;
         for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
-        a.rerun[i] = (uint8_t)(2 | rerun);
+        a.rerun[i] = (uint8_t)(2 | rerun | (one_ready ? 4 : 0));
         eng.store(h);
     }
 }
@@ -644,6 +656,32 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
 __global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n || (a.layout->error | a.layout->overflow) || !a.layout->commit_column) return;
+    // the single ReadyToReads pass A kept: the wave's records are consecutive in the list (its
+    // groups are), staged in LDS at their places and stored as one contiguous run of 16-byte
+    // lane stores; the places of the replayed groups' records are holes pass B fills afterwards
+    __shared__ hq_ready_to_read stage[256 / 64][kStageReady];
+    {
+        constexpr uint64_t l = kReady;
+        const uint64_t w = i >> 6;
+        const uint32_t lo = a.scan[l * a.nw + w] - a.scan[l * a.nw];
+        const uint32_t cnt = a.scan[l * a.nw + w + 1] - a.scan[l * a.nw + w];   // the wave's
+        hq_ready_to_read *st = stage[threadIdx.x >> 6];
+        hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.layout->off[kReady]);
+        const uint32_t pos = a.scan[l * a.nw + w] - a.scan[l * a.nw] + a.counts[l * a.n + i];
+        if (a.rerun[i] & 4) {
+            if (pos - lo < kStageReady) st[pos - lo] = a.ready_slot[i];
+            else dst[pos] = a.ready_slot[i];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t act = __ballot(1);
+        const uint32_t rank = __popcll(act & ((1ull << (threadIdx.x & 63)) - 1));
+        const uint32_t nact = __popcll(act);
+        const uint32_t nrec = min(cnt, kStageReady);
+        const uint4 *src = reinterpret_cast<const uint4 *>(st);
+        uint4 *out = reinterpret_cast<uint4 *>(dst + lo);
+        for (uint32_t q = rank; q < 2 * nrec; q += nact) out[q] = src[q];
+    }
     const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
     const uint64_t c0 = a.groups_old[h].committed, c1 = a.groups[h].committed;
     char *col = a.out + a.layout->off[kCommits];
@@ -766,6 +804,7 @@ struct hq_dstep {
     uint64_t *match_old = nullptr;
     uint8_t *rerun = nullptr;     // [rcap] per listed group
     uint32_t *rerun_list = nullptr;
+    hq_ready_to_read *ready_slot = nullptr;
     size_t rcap = 0;
     uint32_t *stamp = nullptr;    // [gcap] step stamps (duplicate handles)
     uint64_t gcap = 0, mcap = 0;
@@ -864,7 +903,7 @@ void hq_dstep_close(hq_dstep *d) {
     for (void *p : {(void *)d->groups, (void *)d->reads, (void *)d->members, (void *)d->stamp, d->in,
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp,
                     (void *)d->layout, (void *)d->groups_old, (void *)d->reads_old,
-                    (void *)d->match_old, (void *)d->rerun,
+                    (void *)d->match_old, (void *)d->rerun, (void *)d->ready_slot,
                     (void *)d->rerun_list})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
@@ -1013,7 +1052,11 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (!rc)
             rc = grow(ctx, reinterpret_cast<void **>(&d->rerun_list), &lc, n * 4, false,
                       "hq_dstep rerun list");
-        if (!rc) d->rcap = std::min(fc, lc / 4);
+        size_t sc = d->rcap * sizeof(hq_ready_to_read);
+        if (!rc)
+            rc = grow(ctx, reinterpret_cast<void **>(&d->ready_slot), &sc,
+                      n * sizeof(hq_ready_to_read), false, "hq_dstep ready slots");
+        if (!rc) d->rcap = std::min({fc, lc / 4, sc / sizeof(hq_ready_to_read)});
     }
     // the host region the lists go to: last step's size with room to spare (a step that needs
     // more runs pass B again after growing it)
@@ -1081,6 +1124,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.reads_old = d->reads_old;
     k.rerun = d->rerun;
     k.rerun_list = d->rerun_list;
+    k.ready_slot = d->ready_slot;
     const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
     auto launch = [&](bool write, uint64_t i0, uint64_t i1) {
         k.i_begin = i0;
