@@ -68,21 +68,6 @@ tools/lib_tilecopy/libhipquorum.so: $(SRCS) $(DEPS)
 tools/lib_b3copy/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_BITS3_COPY)
 
-variants: grid cap (in 256-thread units) raised 2x / 4x / 8x
-tools/lib_mb%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)
-	@mkdir -p tools/lib_mb$*
-	$(HIPCC) $(HIPFLAGS) -DHQ_MAX_BLOCKS=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip
-
-# tuning variants: records per lane of the table ingest kernels
-tools/lib_iv%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)
-	@mkdir -p tools/lib_iv$*
-	$(HIPCC) $(HIPFLAGS) -DHQ_INGEST_V=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip
-
-# tuning variants: tiles per wave of the 3-byte bitmap kernel
-tools/lib_b3tpw%/libhipquorum.so: $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip $(DEPS)
-	@mkdir -p tools/lib_b3tpw$*
-	$(HIPCC) $(HIPFLAGS) -DHQ_BITS3_TPW=$* -shared -o $@ $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_dstep.hip
-
 variants: tools/lib_vec2/libhipquorum.so tools/lib_b512/libhipquorum.so
 
 clean:

@@ -493,6 +493,46 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
         host.close()
 
 
+def test_chunked_step_outgrows_the_pinned_region(hq):
+    """The pinned region a device worker writes its lists into is sized by its first step: after
+    a 20 000-group step, a chunked step with the advance column (pass A's speculative advance
+    words in the region, the single ReadyToReads copied out by k_step_lite) needs 3 MB, the layout
+    overflows, and the step's lists are written again into a larger region; the next steps fit.
+    Every step's lists equal the host worker's."""
+    import bench
+
+    G = 4 * 65536 + 5
+    roles = bench.STEP_ROLES["step5"]
+    g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
+    nv = sum(r != "observer" for r in roles)
+    dev = hq.Worker(0, nv, on_device=True, commit_advance=True)
+    host = hq.Worker(0, nv)
+    try:
+        dev.add_groups(g, m)
+        host.add_groups(g, m)
+        # (the full steps restart at step 0: a group's first step must be step 0's events)
+        for n, s in ((20000, 0), (G, 0), (G, 1), (G, 2)):
+            e = bench.step_events(hq, n, s, roles)
+            prev = np.array([host.get_group(c)[0]["committed"] for c in range(1, n + 1)], np.uint64)
+            want = host.step(*e)
+            data, sizes = hq.encode_events_sized(e[1], e[2])
+            got = dev.step_sized(e[0], sizes, len(e[2]), data)
+            if "committed_advance" in got:
+                col = prev.copy()
+                col[want["commits"]["cluster_id"].astype(np.int64) - 1] = want["commits"]["committed"]
+                np.testing.assert_array_equal(prev + got["committed_advance"], col)
+                got["commits"] = want["commits"]
+            for k in ("commits", "ready", "read_resps", "state_changes", "dropped_reads",
+                      "deferred", "fallback_groups"):
+                np.testing.assert_array_equal(got[k], want[k], err_msg=f"step {s} {k}")
+            assert len(want["ready"]) > n // 5    # (2 MB of records after the column's 1 MB)
+        for cid in (1, 20001, 131073, G):
+            assert dev.get_group(cid)[0]["committed"] == host.get_group(cid)[0]["committed"]
+    finally:
+        dev.close()
+        host.close()
+
+
 @pytest.mark.parametrize("feed", ["sized", "sized-advance"])
 @pytest.mark.parametrize("seed", [11, 12])
 def test_rejected_steps_restore_state_on_device(hq, seed, feed):
