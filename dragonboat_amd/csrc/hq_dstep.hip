@@ -58,10 +58,13 @@ struct StepK {
     // sizes); pass A of byte chunk c takes the groups whose bytes end in [own_lo, own_hi)
     const uint64_t *prefix;
     uint64_t own_lo, own_hi;
-    uint32_t *counts;             // [kLists][n]: pass A output; k_wave_sums turns them into the
-                                  // counts of the lanes before in the group's wave
-    const uint32_t *scan;         // exclusive scan of the per-wave sums of counts, [kLists][nw]
-    uint64_t nw;                  //   (+1; k_wave_sums): pass B input with the counts
+    uint32_t *counts;             // [kLists][n]: pass A output (the group's records per list)
+    uint32_t *wsum;               // [kLists][nw] + 1 zero: pass A adds each wave's counts (zero
+    uint64_t ws;                  //   between steps: k_step_lite clears the ws it used, after the scan)
+    const uint32_t *scan;         // exclusive scan of wsum: a wave's first record per list
+    uint64_t nw;
+    uint32_t *pre;                // [kLists][n] k_step_lite: the counts of the lanes before in the
+                                  //   wave, for the groups pass B replays (with scan: their places)
     char *out;                    // pass B: the lists, written straight into pinned host memory
     const struct Layout *layout;  //   at layout->off[list]
     // pass A writes each group's new state in place and its state before the step here (same
@@ -235,7 +238,7 @@ struct Engine {
         for (int l = 0; l < kLists; ++l) {
             cnt[l] = 0;           // pass B: the wave's base + the counts of the lanes before
             base[l] = WRITE ? k.scan[(uint64_t)l * k.nw + (idx >> 6)] - k.scan[(uint64_t)l * k.nw] +
-                                  k.counts[(uint64_t)l * k.n + idx]
+                                  k.pre[(uint64_t)l * k.n + idx]
                             : 0;
         }
     }
@@ -561,6 +564,10 @@ template <bool WRITE, bool STREAM, int MC>
 #define HQ_STEP_OCC
 #endif
 __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
+    // pass A: the wave's counts summed in LDS, added to wsum by one lane (i_begin is a multiple
+    // of 64: the wave's groups are one wave of the scan)
+    __shared__ uint32_t wtot[WRITE ? 1 : 256 / 64][kLists];
+    if (!WRITE && (threadIdx.x & 63) < kLists) wtot[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
     if (WRITE && a.layout->commit_column) {
@@ -647,6 +654,17 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
         for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
         a.rerun[i] = (uint8_t)(2 | rerun | (one_ready ? 4 : 0));
         eng.store(h);
+        uint32_t *wt = wtot[threadIdx.x >> 6];   // (the lanes that left early add nothing)
+        for (int l = 0; l < kLists; ++l)
+            if (eng.cnt[l]) atomicAdd(wt + l, eng.cnt[l]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+            for (int l = 0; l < kLists; ++l) {
+                const uint32_t v = wt[l];
+                if (v) atomicAdd(a.wsum + (uint64_t)l * a.nw + (i >> 6), v);
+            }
+        }
     }
 }
 
@@ -655,7 +673,33 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
 // positions of the groups with other records packed in order for pass B; in list mode nothing
 __global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n || (a.layout->error | a.layout->overflow) || !a.layout->commit_column) return;
+    if (i < a.ws) a.wsum[i] = 0;  // (scanned already; the grid covers ws: 9 n / 64 + 10 <= max(n, 256))
+    const bool in = i < a.n;
+    if ((a.layout->error | a.layout->overflow) || !__ballot(in)) return;   // (whole waves)
+    const uint32_t col = a.layout->commit_column;
+    const uint8_t rr = in ? a.rerun[i] : 0;
+    const int lane = threadIdx.x & 63;
+    // the counts of the lanes before in the wave (pass A's counts, scanned across the wave):
+    // stored for the groups pass B replays (with the column: those with other records; in list
+    // mode: all), kReady's and kRerun's kept for below; a wave with no replayed group scans those two
+    const bool replay = in && (!col || (rr & 1));
+    const bool any = __ballot(replay) != 0;
+    uint32_t pre_ready = 0, pre_rerun = 0;
+    for (int l = 0; l < kLists; ++l) {
+        if (!any && l != kReady && l != kRerun) continue;
+        const uint32_t c = in ? a.counts[(uint64_t)l * a.n + i] : 0;
+        uint32_t x = c;           // inclusive scan over the wave's lanes
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            x += lane >= d ? y : 0u;
+        }
+        if (replay) a.pre[(uint64_t)l * a.n + i] = x - c;
+        if (l == kReady) pre_ready = x - c;
+        if (l == kRerun) pre_rerun = x - c;
+    }
+    if (!col) return;
+    const bool col32 = col == kColumn32;
     // the single ReadyToReads pass A kept: the wave's records are consecutive in the list (its
     // groups are), staged in LDS at their places and stored as one contiguous run of 16-byte
     // lane stores; the places of the replayed groups' records are holes pass B fills afterwards
@@ -667,33 +711,31 @@ __global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
         const uint32_t cnt = a.scan[l * a.nw + w + 1] - a.scan[l * a.nw + w];   // the wave's
         hq_ready_to_read *st = stage[threadIdx.x >> 6];
         hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.layout->off[kReady]);
-        const uint32_t pos = a.scan[l * a.nw + w] - a.scan[l * a.nw] + a.counts[l * a.n + i];
-        if (a.rerun[i] & 4) {
+        const uint32_t pos = lo + pre_ready;
+        if (rr & 4) {
             if (pos - lo < kStageReady) st[pos - lo] = a.ready_slot[i];
             else dst[pos] = a.ready_slot[i];
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        const uint64_t act = __ballot(1);
-        const uint32_t rank = __popcll(act & ((1ull << (threadIdx.x & 63)) - 1));
-        const uint32_t nact = __popcll(act);
         const uint32_t nrec = min(cnt, kStageReady);
         const uint4 *src = reinterpret_cast<const uint4 *>(st);
         uint4 *out = reinterpret_cast<uint4 *>(dst + lo);
-        for (uint32_t q = rank; q < 2 * nrec; q += nact) out[q] = src[q];
+        for (uint32_t q = lane; q < 2 * nrec; q += 64) out[q] = src[q];
     }
-    const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
-    const uint64_t c0 = a.groups_old[h].committed, c1 = a.groups[h].committed;
-    char *col = a.out + a.layout->off[kCommits];
-    if (a.layout->commit_column == kColumn32) {
-        if (!a.spec_valid) reinterpret_cast<uint32_t *>(col)[i] = (uint32_t)(c1 - c0);
-    } else {
-        reinterpret_cast<uint64_t *>(col)[i] = c1 != c0 ? c1 : 0;
+    if (!in) return;
+    if (!(col32 && a.spec_valid)) {   // (pass A wrote the advance words)
+        const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
+        const uint64_t c0 = a.groups_old[h].committed, c1 = a.groups[h].committed;
+        char *cw = a.out + a.layout->off[kCommits];
+        if (col32)
+            reinterpret_cast<uint32_t *>(cw)[i] = (uint32_t)(c1 - c0);
+        else
+            reinterpret_cast<uint64_t *>(cw)[i] = c1 != c0 ? c1 : 0;
     }
-    if (a.rerun[i] & 1) {         // the wave's base + the lanes before (k_wave_sums)
+    if (rr & 1) {                 // the wave's base + the lanes before
         const uint64_t l = kRerun;
-        a.rerun_list[a.scan[l * a.nw + (i >> 6)] - a.scan[l * a.nw] + a.counts[l * a.n + i]] =
-            (uint32_t)i;
+        a.rerun_list[a.scan[l * a.nw + (i >> 6)] - a.scan[l * a.nw] + pre_rerun] = (uint32_t)i;
     }
 }
 
@@ -713,30 +755,6 @@ __global__ __launch_bounds__(256) void k_step_restore(const StepK a) {
     }
     for (uint32_t r = 0; r < g.n_reads; ++r)
         a.reads[(uint64_t)h * kDReads + r] = a.reads_old[(uint64_t)h * kDReads + r];
-}
-
-// per-wave sums of pass A's counts, [kLists][nw] + a trailing 0 (its exclusive scan's last
-// element is the grand total), and each count replaced by the sum of the lanes before it in its
-// wave: the scan pass B places its records by is 64 times shorter than the counts (8 lists x n,
-// mostly zeros: 44 us per 1 M groups scanned whole)
-__global__ __launch_bounds__(256) void k_wave_sums(uint32_t *counts, uint64_t n, uint64_t nw,
-                                                   uint32_t *wsum) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t w = i >> 6;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int l = 0; l < kLists; ++l) {
-        const uint32_t c = i < n ? counts[(uint64_t)l * n + i] : 0;
-        uint32_t x = c;           // inclusive scan over the wave's lanes
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            x += lane >= d ? y : 0u;
-        }
-        if (i < n) counts[(uint64_t)l * n + i] = x - c;
-        if (lane == 63 && w < nw) wsum[(uint64_t)l * nw + w] = x;
-    }
-    if (i == 0) wsum[(uint64_t)kLists * nw] = 0;
 }
 
 // the lists' place in the host output region (of cap bytes) from the scanned per-wave sums, and
@@ -817,6 +835,9 @@ struct hq_dstep {
     size_t in_cap = 0;
     uint32_t *counts = nullptr, *scan = nullptr, *bases = nullptr;
     size_t cnt_cap = 0;
+    uint32_t *wsum = nullptr;     // pass A's per-wave sums (StepK::wsum), zero between steps
+    size_t wsum_cap = 0;          //   (bytes)
+    bool wsum_dirty = true;
     void *scan_tmp = nullptr;
     size_t scan_tmp_cap = 0;
     void *host_out = nullptr;     // pinned host region pass B writes the lists into
@@ -904,7 +925,7 @@ void hq_dstep_close(hq_dstep *d) {
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp,
                     (void *)d->layout, (void *)d->groups_old, (void *)d->reads_old,
                     (void *)d->match_old, (void *)d->rerun, (void *)d->ready_slot,
-                    (void *)d->rerun_list})
+                    (void *)d->rerun_list, (void *)d->wsum})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
     if (d->host_layout) (void)hipHostFree(d->host_layout);
@@ -1009,7 +1030,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     int chunks = 1;
     while (chunks * 2 <= kMaxChunks && n >= (uint64_t)chunks * 2 * kChunkGroups) chunks *= 2;
     uint64_t bound[kMaxChunks + 1];
-    for (int c = 0; c <= chunks; ++c) bound[c] = n * c / chunks;
+    for (int c = 0; c <= chunks; ++c)   // (multiples of 64 inside: pass A's waves are the scan's)
+        bound[c] = c == chunks ? n : (n * c / chunks) & ~uint64_t(63);
     // the step's input in one device region: handles, offsets, [boffsets,] events or bytes, each
     // at the offsets it has on the host; a sized stream: handles, sizes (+ a zero), their scan,
     // bytes
@@ -1031,11 +1053,12 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
             rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
                                                    s ? s : cs), "hq_dstep H2D");
     };
-    // counts [kLists][n]; the scan buffer holds the per-wave sums [kLists][nw] + 1 (a zero: the
-    // scan's last element is the grand total) and their scan (one size covers both)
+    // counts [kLists][n] and the prefixes pass B reads, [kLists][n]; the scan buffer holds the
+    // per-wave sums [kLists][nw] + 1 (a zero: the scan's last element is the grand total) and
+    // their scan (one size covers both)
     const uint64_t nw = (n + 63) / 64;
     const size_t ws = (size_t)kLists * nw + 1;
-    const size_t cn = (size_t)kLists * n + 2 * ws;
+    const size_t cn = (size_t)2 * kLists * n + 2 * ws;
     size_t cc = d->cnt_cap * 4, sc = d->cnt_cap * 4, bc = d->cnt_cap ? 256 : 0;
     if (!rc && cn > d->cnt_cap) {
         rc = grow(ctx, reinterpret_cast<void **>(&d->counts), &cc, cn * 4, false, "hq_dstep counts");
@@ -1045,6 +1068,11 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
             if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 8, ctx->stream), "memset");
         }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
+    }
+    if (!rc && ws * 4 > d->wsum_cap) {
+        rc = grow(ctx, reinterpret_cast<void **>(&d->wsum), &d->wsum_cap, ws * 4, false,
+                  "hq_dstep wave sums");
+        d->wsum_dirty = true;
     }
     if (!rc && n > d->rcap) {
         size_t fc = d->rcap, lc = d->rcap * 4;
@@ -1071,7 +1099,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         packed_sizes(hipcub::CountingInputIterator<uint64_t>(0),
                      PackSize{reinterpret_cast<const uint32_t *>(din + o_off), n});
     uint64_t *prefix = reinterpret_cast<uint64_t *>(din + o_boff);
-    uint32_t *wsum = d->scan + ws;
+    uint32_t *wsum = d->wsum;
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, wsum, d->scan,
                                                                        ws, ctx->stream),
                                 "hipcub scan size");
@@ -1099,6 +1127,9 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         k.events = reinterpret_cast<const hq_event *>(din + o_ev);
     }
     k.counts = d->counts;
+    k.pre = d->counts + (size_t)kLists * n;
+    k.wsum = wsum;
+    k.ws = ws;
     k.scan = d->scan;
     k.nw = nw;
     k.n_handles = d->n_groups;
@@ -1111,6 +1142,13 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (rc) return rc;
     }
     k.step_no = d->step_no;
+    // pass A adds each wave's counts into wsum, which k_step_lite leaves zero; a step that
+    // stopped before it (or a new buffer) leaves it to clear here
+    if (d->wsum_dirty) {
+        rc = hq::check_hip(ctx, hipMemsetAsync(wsum, 0, d->wsum_cap, ctx->stream), "memset");
+        if (rc) return rc;
+    }
+    d->wsum_dirty = true;
     k.error = d->bases;           // zero here: reset by the previous step's k_layout
     k.wide = d->commit_column & kColumn32 ? d->bases + 1 : nullptr;   // likewise
     k.out = static_cast<char *>(d->host_out);
@@ -1196,11 +1234,6 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         }
         launch(false, i0, i1);
     }
-    if (!rc) {
-        hipLaunchKernelGGL(k_wave_sums, dim3((unsigned)((nw * 64 + 255) / 256)), dim3(256), 0,
-                           ctx->stream, d->counts, n, nw, wsum);
-        rc = hq::check_hip(ctx, hipGetLastError(), "k_wave_sums");
-    }
     if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, wsum,
                                                                        d->scan, ws, ctx->stream),
                                 "hipcub scan");
@@ -1216,6 +1249,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (!rc) {
             hipLaunchKernelGGL(k_step_lite, grid, blk, 0, ctx->stream, k);
             rc = hq::check_hip(ctx, hipGetLastError(), "k_step_lite");
+            if (!rc) d->wsum_dirty = false;
         }
         launch(true, 0, n);
         if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
