@@ -766,15 +766,15 @@ __global__ __launch_bounds__(256) void k_step_restore(const StepK a) {
 #endif
 constexpr int kMaxChunks = HQ_STEP_CHUNKS;
 constexpr uint64_t kChunkGroups = 65536;
-__global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t *error,
-                         uint64_t cap, uint32_t allow_column, Layout *lay, Layout *host_lay) {
+// bnd[l] = the scan at l * nw (list l's first record), l = 0 .. kLists
+__device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, uint64_t cap,
+                            uint32_t allow_column, Layout *lay, Layout *host_lay) {
     uint32_t *wide = error + 1;   // pass A: an advance of 2^32 or more
-    if (threadIdx.x != 0) return;
     const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
                                   sizeof(hq_read_index_resp), sizeof(hq_state_change),
                                   sizeof(hq_dropped_read), 8, 8, 0, 0};
     uint64_t total = 0;
-    const uint32_t commits = scan[nw] - scan[0];
+    const uint32_t commits = bnd[1] - bnd[0];
     // the commits as a column when that moves fewer bytes (16 per commit in the list against 8
     // per listed group, or 4 when every advance fits)
     // (allow_column: bit kColumn64 HQ_WORKER_COMMIT_COLUMN, bit kColumn32 _ADVANCE)
@@ -782,7 +782,7 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
                              ? kColumn32
                          : (allow_column & kColumn64) && 2 * (uint64_t)commits > n ? kColumn64 : 0;
     for (int l = 0; l < kLists; ++l) {
-        const uint32_t len = scan[(uint64_t)(l + 1) * nw] - scan[(uint64_t)l * nw];
+        const uint32_t len = bnd[l + 1] - bnd[l];
         lay->off[l] = total;
         lay->len[l] = len;
         const uint64_t bytes = l == kCommits && lay->commit_column
@@ -801,6 +801,74 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
         *wide = 0;
     }
     *host_lay = *lay;             // the host's copy, written into pinned memory (no copy launch)
+}
+
+__global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t *error,
+                         uint64_t cap, uint32_t allow_column, Layout *lay, Layout *host_lay) {
+    if (threadIdx.x != 0) return;
+    uint32_t bnd[kLists + 1];
+    for (int l = 0; l <= kLists; ++l) bnd[l] = scan[(uint64_t)l * nw];
+    layout_from(bnd, n, error, cap, allow_column, lay, host_lay);
+}
+
+// A small step's scan of the per-wave sums and its layout in one workgroup (hipcub's scan is two
+// launches, then k_layout a third: 16 workers pay 48 such launches per step): tiles of 11 Ki sums,
+// each thread scanning 11 consecutive ones from LDS (an odd stride: no bank conflicts), the
+// threads' totals scanned across the waves, with the carry of the tiles before
+constexpr int kScanT = 1024, kScanE = 11;
+constexpr uint64_t kScanSmall = 2 * kScanT * kScanE;   // sums taken this way (2 tiles)
+__global__ __launch_bounds__(kScanT) void k_scan_layout(const uint32_t *wsum, uint32_t *scan,
+                                                        uint64_t ws, uint64_t n, uint64_t nw,
+                                                        uint32_t *error, uint64_t cap,
+                                                        uint32_t allow_column, Layout *lay,
+                                                        Layout *host_lay) {
+    __shared__ uint32_t tile[kScanT * kScanE];
+    __shared__ uint32_t wtot[kScanT / 64];
+    __shared__ uint32_t bnd[kLists + 1];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t carry = 0;
+    for (uint64_t base = 0; base < ws; base += (uint64_t)kScanT * kScanE) {
+        for (int k = 0; k < kScanE; ++k) {
+            const uint64_t j = base + (uint64_t)k * kScanT + t;
+            tile[k * kScanT + t] = j < ws ? wsum[j] : 0u;
+        }
+        __syncthreads();
+        uint32_t v[kScanE], sum = 0;
+        for (int k = 0; k < kScanE; ++k) {
+            v[k] = tile[t * kScanE + k];
+            sum += v[k];
+        }
+        uint32_t x = sum;         // inclusive scan of the threads' totals over the wave
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            x += lane >= d ? y : 0u;
+        }
+        if (lane == 63) wtot[wv] = x;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < kScanT / 64; ++w) {
+            const uint32_t z = wtot[w];
+            before += w < wv ? z : 0u;
+            all += z;
+        }
+        uint32_t run = carry + before + x - sum;
+        for (int k = 0; k < kScanE; ++k) {
+            tile[t * kScanE + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        for (int k = 0; k < kScanE; ++k) {
+            const uint64_t j = base + (uint64_t)k * kScanT + t;
+            if (j < ws) {
+                const uint32_t e = tile[k * kScanT + t];
+                scan[j] = e;
+                if (j % nw == 0 && j / nw <= kLists) bnd[j / nw] = e;
+            }
+        }
+        carry += all;
+        __syncthreads();          // (the next tile overwrites tile and wtot)
+    }
+    if (t == 0) layout_from(bnd, n, error, cap, allow_column, lay, host_lay);
 }
 
 uint64_t now_ns() {
@@ -1234,17 +1302,28 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         }
         launch(false, i0, i1);
     }
-    if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, wsum,
-                                                                       d->scan, ws, ctx->stream),
-                                "hipcub scan");
+    // the wave sums' scan and the layout: one workgroup for a small step, else hipcub's scan and
+    // k_layout (a re-run after an overflow takes k_layout: k_step_lite has cleared the sums)
+    const bool small_scan = ws <= kScanSmall;
+    if (!rc && !small_scan)
+        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, wsum, d->scan,
+                                                                  ws, ctx->stream),
+                           "hipcub scan");
     // layout, pass B (straight into the pinned region), the layout back: one wait per step
+    bool first = true;
     auto pass_b = [&]() {
-        if (!rc) {
+        if (!rc && small_scan && first) {
+            hipLaunchKernelGGL(k_scan_layout, dim3(1), dim3(kScanT), 0, ctx->stream, wsum, d->scan,
+                               (uint64_t)ws, n, nw, k.error, (uint64_t)d->host_out_cap,
+                               (uint32_t)d->commit_column, d->layout, d->host_layout);
+            rc = hq::check_hip(ctx, hipGetLastError(), "k_scan_layout");
+        } else if (!rc) {
             hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, nw, k.error,
                                (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout,
                                d->host_layout);
             rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
         }
+        first = false;
         const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
         if (!rc) {
             hipLaunchKernelGGL(k_step_lite, grid, blk, 0, ctx->stream, k);
