@@ -14,13 +14,15 @@
 // events (the host worker cuts runs at such barriers and needs several passes).
 //
 // The outputs are lists whose lengths are not known in advance: the kernel runs twice. Pass A
-// takes every group's events, counts its records, saves the state it found and writes the new
-// state in place; after an exclusive scan of the counts (per-wave sums scanned, the lanes of a
-// wave by shuffles in pass B) pass B replays, from the saved state, only the groups that have
-// records other than their commit — with the commits as a column (k_step_lite writes every
-// group's word from the saved and the new committed index) that is the quarter of a steady step
-// with a ReadIndex — writing every record at its place, in input group order, as the host worker
-// lists them. A step with an input error writes no state: k_step_restore puts the saved state back.
+// takes every group's events, counts its records (and adds each wave's counts into per-wave
+// sums), saves the state it found and writes the new state in place; the per-wave sums are
+// scanned (hipcub, or k_scan_layout for a small step), k_step_lite scans the lanes of each wave
+// by shuffles, and pass B replays, from the saved state, only the groups that have records other
+// than their commit and one ReadyToRead — with the commits as a column (k_step_lite writes every
+// group's word from the saved and the new committed index, and copies out the single
+// ReadyToReads pass A kept) no group of a steady step is replayed — writing every record at its
+// place, in input group order, as the host worker lists them. A step with an input error writes
+// no state: k_step_restore puts the saved state back.
 #include <algorithm>
 #include <chrono>
 #include <new>
