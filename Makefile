@@ -6,9 +6,11 @@ CSRC := dragonboat_amd/csrc
 LIBDIR := dragonboat_amd/lib
 LIB := $(LIBDIR)/libhipquorum.so
 OBJS := $(LIBDIR)/hq_runtime.o $(LIBDIR)/hq_kernels.o $(LIBDIR)/hq_table.o $(LIBDIR)/hq_pack.o \
-        $(LIBDIR)/hq_worker.o $(LIBDIR)/hq_wire.o $(LIBDIR)/hq_stream.o $(LIBDIR)/hq_jobs.o $(LIBDIR)/hq_dstep.o
+        $(LIBDIR)/hq_worker.o $(LIBDIR)/hq_wire.o $(LIBDIR)/hq_stream.o $(LIBDIR)/hq_jobs.o $(LIBDIR)/hq_dstep.o \
+        $(LIBDIR)/hq_engine.o
 SRCS := $(CSRC)/hq_kernels.hip $(CSRC)/hq_table.hip $(CSRC)/hq_runtime.hip $(CSRC)/hq_pack.cpp \
-        $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_stream.cpp $(CSRC)/hq_jobs.cpp $(CSRC)/hq_dstep.hip
+        $(CSRC)/hq_worker.cpp $(CSRC)/hq_wire.cpp $(CSRC)/hq_stream.cpp $(CSRC)/hq_jobs.cpp $(CSRC)/hq_dstep.hip \
+        $(CSRC)/hq_engine.hip
 DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
 CXX ?= g++
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -pthread -Wall -Wextra
@@ -93,3 +95,6 @@ tools/lib_stepchunks%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_STEP_CHUNKS=$*)
 tools/lib_plcqzero%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLCQ_ZERO_EARLY=$*)
+# persistent-engine experiments (tools/ab_engine.py): multi-batch loop / flat kernels beside the engine
+tools/lib_engexp/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_ENGINE_EXP)

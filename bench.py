@@ -553,6 +553,155 @@ def run_gpu(w, steps, warmup, d: Dist):
     return res
 
 
+def engine_ok(w):
+    """The persistent commit engine serves uniform-n tiled batches in the term-start / mask form."""
+    return (w["kind"] == "commit" and not w["mixed"] and w.get("tiled")
+            and w["form"] in (0, 2))
+
+
+def run_engine(w, steps, warmup, d: Dist, windows=3):
+    """A commit workload stepped through the persistent commit engine (hq_engine_*,
+    dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps' batches are posted as K
+    descriptors and decided by ONE resident launch (no dependent-launch boundary between
+    steps), then drained. Beside each engine window, the same K batches as K back-to-back
+    launches (hq_commit_many_dev), so the line carries both on the same data. `windows` windows
+    of K = `steps` steps each continue the rotation (>= 1.1 GiB of distinct batches: no step
+    re-reads a batch the 256 MiB Infinity Cache could still hold); the median window is reported
+    (the median over repeated timings)."""
+    from dragonboat_amd import hipquorum as hq
+    from dragonboat_amd import shard
+
+    ctx = hq.Context(d.device)
+    sets, per_set = build_sets(ctx, hq, shard, w, d)
+    nsets = len(sets)
+    lay = hq.HQ_LAYOUT_TILES_LEADER if w.get("lead") else hq.HQ_LAYOUT_TILES
+    eng = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16)
+    # the same engine with per-step completion flags (what a step worker that applies each step's
+    # commits as soon as they are decided runs): its windows are reported beside the others
+    eng_sig = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16, signal=True)
+
+    def arr(i0, k):
+        return hq.commit_batch_array([batch_args(sets[(i0 + i) % nsets][0]) for i in range(k)])
+
+    W = max(1, warmup)
+    eng.post(arr(0, W))
+    eng.drain()
+    eng_sig.post(arr(0, W))
+    eng_sig.drain()
+    eng_sig.timing(reset=True)
+    ctx.commit_many_dev(arr(0, min(W, nsets)))
+    ctx.sync()
+    eng.timing(reset=True)
+    first = W % nsets
+    wins = []
+    for k in range(windows):
+        a = arr(first + k * steps, steps)
+        rec = {}
+        for mode in ("engine", "launches", "signal"):
+            ctx.sync()
+            d.sync_device()
+            d.barrier()
+            if mode == "launches":
+                ctx.timing_reset()
+                ctx.timing_begin_after(1 if steps > 1 else 0)
+            t0 = time.perf_counter()
+            if mode == "engine":
+                eng.post(a)
+                eng.drain()
+            elif mode == "signal":
+                q0 = eng_sig.post(a)
+                eng_sig.wait(q0 + steps - 1)       # the last step's flag: every step complete
+                sig_local = time.perf_counter() - t0
+                clocks = [eng_sig.done_clock(q0 + i) for i in range(steps)]
+                eng_sig.drain()
+            else:
+                ctx.commit_many_dev(a)
+                ctx.timing(False)
+                ctx.sync()
+            local = time.perf_counter() - t0
+            d.barrier()
+            if mode == "engine":
+                nl, ms = eng.timing(reset=True)
+                kernel_s = ms / 1e3 / max(1, steps)        # resident launch time per step
+            elif mode == "signal":
+                nl, ms = eng_sig.timing(reset=True)
+                local = sig_local
+                # device clock (100 MHz) between the first and the last step's completion
+                kernel_s = (clocks[-1] - clocks[0]) / 1e8 / max(1, steps - 1)
+            else:
+                ms, nl = ctx.timing_read()
+                kernel_s = ms / 1e3 / max(1, nl)           # back-to-back launch time
+            rec[mode] = {"elapsed": d.max(local), "local": local, "kernel_s": kernel_s,
+                         "launches": nl}
+        wins.append(rec)
+
+    def med(mode, key):
+        return float(np.median([x[mode][key] for x in wins]))
+
+    # set 0 once more through the engine, its outputs poisoned first: the full-size parity check
+    # of the cpu_baseline leg reads what the engine wrote; the launch path's decisions of the
+    # same batch must be identical
+    b0 = sets[0][0]
+    for x in (b0.committed_out, b0.changed, b0.fallback):
+        ctx.memset(x, 0xA5)
+    ctx.sync()
+    eng.post(arr(0, 1))
+    eng.drain()
+    outs = [ctx.download(x) for x in (b0.committed_out, b0.changed, b0.fallback)]
+    info = eng.info()
+    ctx.commit_dev(batch_args(b0))
+    ctx.sync()
+    launch_outs = [ctx.download(x) for x in (b0.committed_out, b0.changed, b0.fallback)]
+    rng = commit_buckets(shard, w, d)[0][1]
+    set0 = [dict(n=w["n"], cid_base=rng.cid_base, cid_stride=rng.cid_stride, count=rng.count,
+                 out=outs)]
+    engine_eq_launch = all(np.array_equal(x, y) for x, y in zip(outs, launch_outs))
+    eng.close()
+    eng_sig.close()
+    elapsed = med("engine", "elapsed")
+    kernel_s = med("engine", "kernel_s")
+    local = med("engine", "local")
+    achieved_local = per_set / kernel_s / 1e9
+    per_gpu = d.gather([groups_per_step(w) * steps / local, kernel_s * 1e6, achieved_local])
+    achieved_node = d.sum(achieved_local)
+    total_groups = d.sum(float(groups_per_step(w) * steps))
+    lk = med("launches", "kernel_s")
+    le = med("launches", "elapsed")
+    res = dict(
+        elapsed=elapsed, launches=steps, avg_kernel_s=kernel_s,
+        decisions=total_groups * decisions_per_group(w), nsets=nsets, first_timed_set=first,
+        bytes_per_launch=per_set, launches_per_step=1, steps=steps,
+        achieved_gbs=achieved_local, achieved_node_gbs=achieved_node, per_gpu=per_gpu,
+        set0=set0, gather=None, windows=len(wins),
+        engine={
+            "mode": "persistent commit engine (hq_engine): one resident launch per window of "
+                    f"{steps} posted steps", "grid": info.grid, "block": info.block,
+            "window_ms": [round(x["engine"]["elapsed"] * 1e3, 4) for x in wins],
+            "window_kernel_us_per_step": [round(x["engine"]["kernel_s"] * 1e6, 3) for x in wins],
+            "median_kernel_us_per_step": kernel_s * 1e6,
+            "engine_equals_launch_set0": engine_eq_launch,
+        },
+        engine_signal={
+            "mode": "the same engine with per-step completion flags (HQ_ENGINE_SIGNAL): the host "
+                    "waits for the last step's flag",
+            "window_ms": [round(x["signal"]["elapsed"] * 1e3, 4) for x in wins],
+            "median_ms_per_step": med("signal", "elapsed") / steps * 1e3,
+            "median_us_between_step_completions": med("signal", "kernel_s") * 1e6,
+            "value": total_groups * decisions_per_group(w) / med("signal", "elapsed"),
+        },
+        launch_per_step={
+            "mode": "the same batches as back-to-back launches (hq_commit_many_dev)",
+            "window_ms": [round(x["launches"]["elapsed"] * 1e3, 4) for x in wins],
+            "median_ms_per_step": le / steps * 1e3,
+            "median_kernel_us": lk * 1e6,
+            "value": total_groups * decisions_per_group(w) / le,
+            "frac": d.sum(per_set / lk / 1e9) / (HBM_PEAK_GBS * d.world),
+        },
+    )
+    ctx.close()
+    return res
+
+
 def run_size_sweep(name, steps, warmup, d: Dist, sizes=(1 << 18, 1 << 19, 1 << 20, 1 << 21,
                                                         1 << 22, 1 << 23)):
     """The headline kernel at batch sizes 256K..8M groups per GPU (same generator, same
@@ -1450,18 +1599,38 @@ def same_decisions(a, b):
 EXTRAS_MULTI = "c5tl,c5v5tl,c4p,cqp,c4pq,rimt,ingo"
 
 
+def rank_parity(w, r, d, no_cpu):
+    """Every rank checks its own shard's set 0 at full size against the oracle (the C
+    restatement, test infrastructure) on its share of the host cores, at any N: r["parity"] is
+    this rank's full record, r["parity_by_rank"] every rank's verdict in rank order (it travels
+    with per_gpu in the final line)."""
+    host_threads, _ = cpu_thread_counts()
+    r["parity"] = None
+    if not no_cpu and r.get("set0"):
+        r["parity"] = full_size_parity(w, r["set0"], max(1, host_threads // d.world))
+    mine = None if r["parity"] is None else {"equal": r["parity"]["equal"],
+                                             "groups": r["parity"]["groups"]}
+    r["parity_by_rank"] = d.gather_obj(mine)
+    return r
+
+
 def run_rank(args, d, progress):
     """Everything one rank measures: the headline, the extra legs, and (rank 0 at N = 1) the CPU
     baseline. Every rank runs the same legs in the same order (their collectives pair up)."""
     w = WORKLOADS[args.workload]
-    progress(f"headline {args.workload}: {args.steps} steps, {args.warmup} warmup")
-    r = run_gpu(w, args.steps, args.warmup, d)
+    use_engine = args.mode == "engine" and engine_ok(w)
+    progress(f"headline {args.workload}: {args.windows if use_engine else 1} x {args.steps} steps"
+             f" ({'persistent engine' if use_engine else 'launch per step'}), {args.warmup} warmup")
+    r = (run_engine(w, args.steps, args.warmup, d, windows=args.windows) if use_engine
+         else run_gpu(w, args.steps, args.warmup, d))
     r["world"] = d.world
     from dragonboat_amd import hipquorum as hq
 
     devices = d.gather_obj({"rank": d.rank, "device": d.device,
                             "pci_bus_id": hq.device_pci_bus_id(d.device)})
     host_threads, _ = cpu_thread_counts()
+    progress("full-size parity of every rank's set 0")
+    rank_parity(w, r, d, args.no_cpu)
     oracle_here = d.rank == 0 and d.world == 1 and not args.no_cpu
     extra_names = args.extra if args.extra is not None else (
         DEFAULT_EXTRAS if d.world == 1 else EXTRAS_MULTI)
@@ -1504,9 +1673,10 @@ def run_rank(args, d, progress):
         if d.rank == 0:     # each leg's record as it lands (the final line only summarises it)
             log("extra " + json.dumps(rec)[:4000])
     cpu = None
-    if oracle_here:
+    if d.rank == 0 and not args.no_cpu:    # once per run, on all usable host cores (any N)
         progress("cpu baseline")
-        cpu = cpu_baseline(w, gpu_set0=r.get("set0"))
+        cpu = cpu_baseline(w)
+        cpu["parity_full_size"] = r["parity"]
     # the term check of the same groups in its other exact forms (the ring gathers the north
     # star names, the mask the headline streams): rate and whether every decision is identical
     forms = []
@@ -1572,7 +1742,9 @@ def report(args, d, res, launcher):
         "vs_baseline": None,
         "dtype": "u64",
         "data": f"synthetic: device-generated splitmix64 batches, {r['nsets']} distinct per GPU "
-                f"rotated (>= 1.1 GiB); timed steps start at batch {r['first_timed_set']}",
+                f"rotated (>= 1.1 GiB); timed steps start at batch {r['first_timed_set']}"
+                + (f"; {r['windows']} timed windows of {args.steps} steps, the median window "
+                   f"reported (every window in engine.window_ms)" if r.get("windows") else ""),
         "config": {
             "workload": args.workload,
             "desc": w["desc"],
@@ -1593,17 +1765,25 @@ def report(args, d, res, launcher):
             "traffic_source": traffic_src,
             "kernel_avg_us": r["avg_kernel_s"] * 1e6,
             "algorithmic_bytes_per_launch": r["bytes_per_launch"],
-            "kernel_time": "HIP events on the launch stream around the timed launches "
-                           "(back to back), / launches",
+            "kernel_time": ("HIP events around the resident engine launch of the median "
+                            "window (posted steps + STOP), / steps" if r.get("engine") else
+                            "HIP events on the launch stream around the timed launches "
+                            "(back to back), / launches"),
             "achieved_scope": f"sum over {d.world} GPU(s) of bytes per launch / kernel time",
         },
         "per_gpu": [{"rank": i, "device": devs[i]["device"], "pci": devs[i]["pci_bus_id"],
                      "value": float(f"{v:.5g}"), "kernel_us": round(k, 3),
-                     "frac": round(a / HBM_PEAK_GBS, 4)}
+                     "frac": round(a / HBM_PEAK_GBS, 4),
+                     "parity_equal": ((r.get("parity_by_rank") or [None] * d.world)[i]
+                                      or {}).get("equal")}
                     for i, (v, k, a) in enumerate(r["per_gpu"])],
         "cpu_baseline": res["cpu"],
         "term_check_forms_same_data": res["forms"],
     }
+    if r.get("engine"):
+        line["engine"] = r["engine"]
+        line["launch_per_step"] = r["launch_per_step"]
+        line["engine_signal"] = r["engine_signal"]
     summary = {rec["name"]: _short(rec) for rec in res["records"]}
     detail = dict(line, result_gather=r.get("gather"), extra=res["records"])
     path = args.detail_out
@@ -1670,6 +1850,12 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
+    ap.add_argument("--mode", default="engine", choices=("engine", "launch"),
+                    help="headline commit steps through the persistent engine (one resident "
+                         "launch per window; uniform tiled term-start / mask workloads) or one "
+                         "launch per step")
+    ap.add_argument("--windows", type=int, default=3,
+                    help="timed windows of --steps steps (engine mode); the median is reported")
     ap.add_argument("--step-groups", type=int, default=1 << 20,
                     help="groups per GPU of the step-worker legs (extras 'step', 'step5')")
     ap.add_argument("--step-steps", type=int, default=50,

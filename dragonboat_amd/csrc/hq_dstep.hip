@@ -25,6 +25,7 @@
 // no state: k_step_restore puts the saved state back.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <new>
 
 #include <hipcub/hipcub.hpp>
@@ -883,6 +884,9 @@ uint64_t now_ns() {
 
 struct hq_dstep {
     hq_ctx *ctx = nullptr;
+    // HQ_TEST_FAIL_REGROW=1 in the environment at open: the output region's regrow fails (the
+    // failure path's test, tests/test_gpu_worker.py)
+    bool test_fail_regrow = false;
     hq_dgroup *groups = nullptr;
     hq_dread *reads = nullptr;
     hq_dmember *members = nullptr;
@@ -968,6 +972,7 @@ int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
     hq_dstep *d = *out;
     d->ctx = ctx;
     d->commit_column = commit_column;
+    if (const char *f = std::getenv("HQ_TEST_FAIL_REGROW")) d->test_fail_regrow = std::atoi(f) != 0;
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     if (!rc)
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming |
@@ -1335,33 +1340,52 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         launch(true, 0, n);
         if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
     };
-    pass_b();
-    const uint64_t t1 = now_ns();
-    if (rc) return rc;
-    const Layout &lay = *d->host_layout;
-    if (lay.error) {              // no group state is written: pass A's is taken back
+    // Pass A has written every listed group's new state in place (the state it found is saved).
+    // From here on a step that fails returns with that state taken back (k_step_restore), so a
+    // failed step leaves the groups as they were, whatever failed: an input error found by the
+    // kernels, a HIP error, the output region that could not grow, a second layout failure. (A
+    // pass A launch that itself fails leaves rc set before this point; the context is then
+    // unusable and the caller reloads the groups from the device, hq_worker.cpp.)
+    const bool stepped = !rc;
+    auto restore = [&](int code) {
+        if (!stepped) return code;
         hipLaunchKernelGGL(k_step_restore, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                            ctx->stream, k);
-        rc = hq::check_hip(ctx, hipGetLastError(), "k_step_restore");
-        if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep restore");
+        int r2 = hq::check_hip(ctx, hipGetLastError(), "k_step_restore");
+        if (!r2) r2 = wait_stream(d, ctx->stream, "hq_dstep restore");
+        return code ? code : r2;
+    };
+    pass_b();
+    const uint64_t t1 = now_ns();
+    if (rc) return restore(rc);
+    const Layout &lay = *d->host_layout;
+    if (lay.error) {              // no group state is written: pass A's is taken back
+        rc = restore(HQ_OK);
         if (rc) return rc;
         out->input_error = lay.error;
         return HQ_E_INVAL;
     }
     if (lay.overflow) {           // grow the region and write the lists again
-        if (d->host_out) (void)hipHostFree(d->host_out);
-        d->host_out = nullptr;
-        d->host_out_cap = 0;
+        // the new region first: if it cannot be had, the old one stays and the step is undone
         const size_t want = lay.total + lay.total / 2;
-        rc = hq::check_hip(ctx, hipHostMalloc(&d->host_out, want, hipHostMallocDefault),
+        void *grown = nullptr;
+        rc = hq::check_hip(ctx, hipHostMalloc(&grown, want, hipHostMallocDefault),
                            "hq_dstep pinned output");
-        if (rc) return rc;
+        if (d->test_fail_regrow) {   // tests: the allocation failure path
+            if (grown) (void)hipHostFree(grown);
+            grown = nullptr;
+            rc = hq::fail(ctx, HQ_E_NOMEM, "hq_dstep pinned output: injected failure");
+        }
+        if (rc) return restore(rc);
+        if (d->host_out) (void)hipHostFree(d->host_out);
+        d->host_out = grown;
         d->host_out_cap = want;
         k.out = static_cast<char *>(d->host_out);
         k.spec_valid = 0;         // pass A's advance words went with the old region
         pass_b();
-        if (rc) return rc;
-        if (lay.overflow || lay.error) return hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout");
+        if (rc) return restore(rc);
+        if (lay.overflow || lay.error)
+            return restore(hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout"));
     }
     const char *ho = static_cast<const char *>(d->host_out);
     out->commits = lay.commit_column ? nullptr

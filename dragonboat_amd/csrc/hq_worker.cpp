@@ -871,10 +871,13 @@ int hq_worker::sync_from_device() {
 int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     const uint64_t t0 = now_ns();
     // the per-group input checks (handles, offsets, a group listed twice) run in the engine's
-    // first kernel, before any group state is written
+    // first kernel, which writes each group's new state in place; a failed step takes that state
+    // back (k_step_restore). The device copy is the authoritative one from here on, whatever the
+    // outcome: the host copy is reloaded from it before the host reads a group.
     int rc = sync_to_device();
     if (rc) return rc;
     const uint64_t t1 = now_ns();
+    host_stale = true;
     rc = hq_dstep_run(dstep, &inp, &dout);
     if (rc == HQ_E_INVAL && dout.input_error) {
         const uint32_t e = dout.input_error;
@@ -887,7 +890,6 @@ int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     }
     rc = hq(rc, "hq_dstep_run");
     if (rc) return rc;
-    host_stale = true;
     const uint64_t t2 = now_ns();
     out->commits = dout.commits;
     out->n_commits = dout.n_commits;

@@ -42,7 +42,8 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 13
+HQ_ABI_VERSION = 14
+HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
 OUTCOME_CANDIDATE = 1
@@ -97,6 +98,22 @@ class LagArgs(ctypes.Structure):
         ("changed", _vp),
         ("fallback", _vp),
     ]
+
+
+class EngineConfig(ctypes.Structure):
+    """Mirror of ``hq_engine_config``."""
+
+    _fields_ = [(k, ctypes.c_uint32) for k in ("n_max", "form", "layout", "ring_len", "depth",
+                                                "flags", "idle_us", "max_workgroups")]
+
+
+class EngineStats(ctypes.Structure):
+    """Mirror of ``hq_engine_stats``."""
+
+    _fields_ = [("posted", ctypes.c_uint64), ("completed", ctypes.c_uint64),
+                ("relaunches", ctypes.c_uint64), ("grid", ctypes.c_uint32),
+                ("block", ctypes.c_uint32), ("depth", ctypes.c_uint32),
+                ("running", ctypes.c_uint32)]
 
 
 class SynthSpec(ctypes.Structure):
@@ -249,6 +266,15 @@ SIGNATURES = {
     "hq_commit_many_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
     "hq_commit_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32]),
     "hq_commit_lag_dev": (ctypes.c_int, [_vp, ctypes.POINTER(LagArgs)]),
+    "hq_engine_open": (ctypes.c_int, [_vp, ctypes.POINTER(EngineConfig), ctypes.POINTER(_vp)]),
+    "hq_engine_post": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32, _u64p]),
+    "hq_engine_wait": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+    "hq_engine_drain": (ctypes.c_int, [_vp]),
+    "hq_engine_timing": (ctypes.c_int, [_vp, _u64p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    "hq_engine_done_clock": (ctypes.c_int, [_vp, ctypes.c_uint64, _u64p]),
+    "hq_engine_info": (ctypes.c_int, [_vp, ctypes.POINTER(EngineStats)]),
+    "hq_engine_last_error": (ctypes.c_char_p, [_vp]),
+    "hq_engine_close": (None, [_vp]),
     "hq_commit_lag_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(LagArgs), ctypes.c_uint32]),
     "hq_pack_lags": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp,
                                     _vp, _vp, _vp, ctypes.POINTER(LagArgs)]),
@@ -852,6 +878,70 @@ def commit_batch_array(args_list) -> ctypes.Array:
     for i, a in enumerate(args_list):
         arr[i] = a
     return arr
+
+
+class Engine:
+    """hq_engine_*: the persistent commit engine. One resident launch decides every batch posted
+    to it (hq_commit_dev's decision bit for bit) with no launch boundary between steps; step
+    workers post the way execEngine wakes them (execengine.go:115-123, 860-882)."""
+
+    def __init__(self, ctx: Context, n_max: int, form: int, layout: int = HQ_LAYOUT_TILES_LEADER,
+                 ring_len: int = 16, depth: int = 0, signal: bool = False, idle_us: int = 0,
+                 max_workgroups: int = 0):
+        cfg = EngineConfig(n_max=n_max, form=form, layout=layout, ring_len=ring_len, depth=depth,
+                           flags=HQ_ENGINE_SIGNAL if signal else 0, idle_us=idle_us,
+                           max_workgroups=max_workgroups)
+        h = _vp()
+        ctx._check(lib.hq_engine_open(ctx.h, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.ctx = ctx
+
+    def _check(self, rc: int) -> None:
+        if rc != HQ_OK:
+            raise HQError(rc, lib.hq_engine_last_error(self.h).decode())
+
+    def post(self, batch) -> int:
+        """Post a ctypes array of CommitArgs (``commit_batch_array``) or one CommitArgs; returns
+        the sequence number of the first posted step."""
+        if isinstance(batch, CommitArgs):
+            batch = commit_batch_array([batch])
+        seq = ctypes.c_uint64(0)
+        self._check(lib.hq_engine_post(self.h, batch, len(batch), ctypes.byref(seq)))
+        return seq.value
+
+    def wait(self, seq: int) -> None:
+        self._check(lib.hq_engine_wait(self.h, seq))
+
+    def drain(self) -> None:
+        self._check(lib.hq_engine_drain(self.h))
+
+    def timing(self, reset: bool = False) -> tuple[int, float]:
+        """(finished resident launches, their total GPU ms) since the last reset."""
+        n = ctypes.c_uint64(0)
+        ms = ctypes.c_double(0)
+        self._check(lib.hq_engine_timing(self.h, ctypes.byref(n), ctypes.byref(ms), int(reset)))
+        return n.value, ms.value
+
+    def done_clock(self, seq: int) -> int:
+        t = ctypes.c_uint64(0)
+        self._check(lib.hq_engine_done_clock(self.h, seq, ctypes.byref(t)))
+        return t.value
+
+    def info(self) -> EngineStats:
+        st = EngineStats()
+        self._check(lib.hq_engine_info(self.h, ctypes.byref(st)))
+        return st
+
+    def close(self) -> None:
+        if self.h:
+            lib.hq_engine_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def pack_lag_updates(group, slot, lag) -> np.ndarray:

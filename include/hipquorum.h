@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 13
+#define HQ_ABI_VERSION 14
 
 /* status codes */
 #define HQ_OK          0
@@ -270,6 +270,67 @@ int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
  * owns its own workgroups; results are identical to hq_commit_many_dev, which is what runs
  * when the batches cannot share a launch. */
 int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
+
+/* ---------------------------------------------------------------- persistent commit engine -- */
+/*
+ * A resident commit engine: ONE kernel launch decides a stream of posted commit batches
+ * (hq_commit_dev's decision, bit for bit), so successive steps pay no dependent-launch boundary
+ * and no grid fill / drain (≈ 2 us of a 1M-group launch). Step workers post the
+ * batch of each step (raft.tryCommit over their leader groups, raft.go:888-909, logentry.go:378-393)
+ * the way execEngine wakes its step workers (workReady.clusterReady -> stepWorkerMain,
+ * execengine.go:115-123, 860-882): a 64-byte descriptor into a pinned ring, read by the resident
+ * kernel. Wave w of the engine's grid decides tiles w, w + W, ... of every batch in post order,
+ * so a device-resident table posted step after step (HQ_LAYOUT_IN_PLACE) is decided in order per
+ * group with no grid-wide barrier between steps.
+ *
+ * Served: uniform n (n_voting NULL), HQ_FORM_TERM_START or HQ_FORM_TERM_MASK, layout
+ * HQ_LAYOUT_TILES, HQ_LAYOUT_TILES_LEADER or HQ_LAYOUT_TILES_LEADER | HQ_LAYOUT_IN_PLACE, device
+ * pointers. Every posted batch must have the engine's n_max, form, layout (and ring_len for the
+ * mask form); its tiles and outputs must stay allocated until the step is complete.
+ *
+ * The engine has its own HIP stream and holds every CU of the GPU while it is resident (kernels
+ * on other streams wait for it): hq_engine_drain() ends the resident launch, the next post
+ * starts it again. A resident launch also ends by itself after idle_us without a post (every
+ * spin is bounded); steps posted meanwhile are run by a relaunch from hq_engine_wait().
+ */
+#define HQ_ENGINE_SIGNAL 1u   /* per-step completion: hq_engine_wait(seq) returns as soon as step
+                                 seq is done (else wait = drain: the steps complete as a whole) */
+typedef struct hq_engine hq_engine;
+typedef struct hq_engine_config {
+    uint32_t n_max;          /* voting slots of every posted batch, 1..HQ_MAX_VOTERS */
+    uint32_t form;           /* HQ_FORM_TERM_START or HQ_FORM_TERM_MASK */
+    uint32_t layout;         /* HQ_LAYOUT_TILES, _TILES_LEADER or _TILES_LEADER | HQ_LAYOUT_IN_PLACE */
+    uint32_t ring_len;       /* mask form: R (power of two <= 16); unused for term-start */
+    uint32_t depth;          /* posted steps in flight: power of two 2..64 (0 = 64) */
+    uint32_t flags;          /* HQ_ENGINE_SIGNAL */
+    uint32_t idle_us;        /* polling time without a post before the resident launch ends (0 = 20000) */
+    uint32_t max_workgroups; /* cap on the resident grid (0 = every CU at full occupancy) */
+} hq_engine_config;
+typedef struct hq_engine_stats {
+    uint64_t posted;         /* steps posted (STOP steps of drains included) */
+    uint64_t completed;      /* every step below this sequence number is known complete */
+    uint64_t relaunches;     /* launches started by a wait because the grid had gone idle */
+    uint32_t grid, block;    /* resident geometry */
+    uint32_t depth, running;
+} hq_engine_stats;
+int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out);
+/* Post `count` batches as the next steps; *first_seq (may be NULL) = the sequence number of the
+ * first. Blocks only when `depth` steps are in flight. Thread-safe (several step workers may
+ * share one engine per GPU). */
+int hq_engine_post(hq_engine *eng, const hq_commit_args *args, uint32_t count, uint64_t *first_seq);
+/* Return when step `seq` is complete: its outputs are in device memory, visible to the host and
+ * to every stream. */
+int hq_engine_wait(hq_engine *eng, uint64_t seq);
+/* Complete every posted step and end the resident launch (the CUs are free afterwards). */
+int hq_engine_drain(hq_engine *eng);
+/* GPU time of the finished resident launches (HIP events around each), since the last reset. */
+int hq_engine_timing(hq_engine *eng, uint64_t *launches, double *total_ms, int reset);
+/* The device clock (s_memrealtime, 100 MHz) when step seq completed (HQ_ENGINE_SIGNAL). */
+int hq_engine_done_clock(hq_engine *eng, uint64_t seq, uint64_t *ticks);
+int hq_engine_info(hq_engine *eng, hq_engine_stats *out);
+const char *hq_engine_last_error(const hq_engine *eng);
+/* Drain and destroy. NULL is a no-op. */
+void hq_engine_close(hq_engine *eng);
 
 /* ---------------------------------------------------------------- commit over lags --------- */
 /*

@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 13
+    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 14
 
 
 LAYOUT_C = r"""
@@ -82,6 +82,14 @@ int main(void) {
   printf("hq_wire_batch_info %zu\nhq_wire_stats %zu\nbin_ver %u\n", sizeof(hq_wire_batch_info),
          sizeof(hq_wire_stats), (unsigned)HQ_RPC_BIN_VERSION);
   printf("in_place %u\ngrouped %u\n", (unsigned)HQ_LAYOUT_IN_PLACE, (unsigned)HQ_INGEST_GROUPED);
+  printf("hq_engine_config %zu\nhq_engine_stats %zu\nengine_signal %u\n",
+         sizeof(hq_engine_config), sizeof(hq_engine_stats), (unsigned)HQ_ENGINE_SIGNAL);
+  F(hq_engine_config, n_max) F(hq_engine_config, form) F(hq_engine_config, layout)
+  F(hq_engine_config, ring_len) F(hq_engine_config, depth) F(hq_engine_config, flags)
+  F(hq_engine_config, idle_us) F(hq_engine_config, max_workgroups)
+  F(hq_engine_stats, posted) F(hq_engine_stats, completed) F(hq_engine_stats, relaunches)
+  F(hq_engine_stats, grid) F(hq_engine_stats, block) F(hq_engine_stats, depth)
+  F(hq_engine_stats, running)
   return 0;
 }
 """
@@ -98,6 +106,9 @@ def test_struct_layout_matches_c(hq, tmp_path):
     assert int(c["hq_commit_args"]) == ctypes.sizeof(hq.CommitArgs)
     assert int(c["hq_synth_spec"]) == ctypes.sizeof(hq.SynthSpec)
     assert int(c["hq_commit_lag_args"]) == ctypes.sizeof(hq.LagArgs)
+    assert int(c["hq_engine_config"]) == ctypes.sizeof(hq.EngineConfig)
+    assert int(c["hq_engine_stats"]) == ctypes.sizeof(hq.EngineStats)
+    assert int(c["engine_signal"]) == hq.HQ_ENGINE_SIGNAL
     dtypes = {"hq_member": hq.MEMBER_DTYPE, "hq_group_view": hq.GROUP_DTYPE,
               "hq_msg": hq.MSG_DTYPE, "hq_wire_message": hq.WIRE_MESSAGE_DTYPE}
     assert int(c["hq_wire_batch_info"]) == ctypes.sizeof(hq.WireBatchInfo)
@@ -123,7 +134,8 @@ def test_struct_layout_matches_c(hq, tmp_path):
                 assert dtypes[t].fields[m][1] == int(val), key
                 continue
             cls = {"hq_commit_args": hq.CommitArgs, "hq_synth_spec": hq.SynthSpec,
-                   "hq_commit_lag_args": hq.LagArgs}[t]
+                   "hq_commit_lag_args": hq.LagArgs, "hq_engine_config": hq.EngineConfig,
+                   "hq_engine_stats": hq.EngineStats}[t]
             assert getattr(cls, m).offset == int(val), key
 
 
@@ -138,6 +150,11 @@ def test_null_context_is_invalid(hq):
     assert hq.lib.hq_commit_lag_fused_dev(None, None, 0) == hq.HQ_E_INVAL
     assert hq.lib.hq_wait_for(None, None) == hq.HQ_E_INVAL
     hq.lib.hq_close(None)  # no-op
+    assert hq.lib.hq_engine_open(None, None, None) == hq.HQ_E_INVAL
+    assert hq.lib.hq_engine_post(None, None, 0, None) == hq.HQ_E_INVAL
+    assert hq.lib.hq_engine_wait(None, 0) == hq.HQ_E_INVAL
+    assert hq.lib.hq_engine_drain(None) == hq.HQ_E_INVAL
+    hq.lib.hq_engine_close(None)  # no-op
     assert hq.lib.hq_last_error(None) is not None
 
 

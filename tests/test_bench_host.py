@@ -76,7 +76,8 @@ def test_thread_dist_collectives(n):
 
 def _args(**kw):
     a = dict(gpus=2, steps=5, warmup=1, workload=bench.HEADLINE, step_groups=1 << 10,
-             step_steps=2, no_cpu=True, no_extra_parity=True, extra="", detail_out=None)
+             step_steps=2, no_cpu=True, no_extra_parity=True, extra="", detail_out=None,
+             mode="engine", windows=3)
     a.update(kw)
     return argparse.Namespace(**a)
 
@@ -130,6 +131,44 @@ def test_main_threads_rank_failure_releases_the_others(monkeypatch, tmp_path, hq
     monkeypatch.setattr(hq, "device_count", lambda: 1)
     with pytest.raises(RuntimeError, match="rank 1 failed"):
         bench.main_threads(_args(detail_out=str(tmp_path / "d.json")), 0.0)
+
+
+def _oracle_set0(w, d, corrupt=False):
+    """What run_engine / run_gpu hand to the parity check, made by the oracle itself on the CPU
+    (a small shard of the headline workload per rank)."""
+    from dragonboat_amd import shard
+    from oracle import qref
+
+    rng = shard.rank_shard(d.rank, d.world, w["G"])
+    s = qref.spec(bench.SEED_BASE + w["cfg"], rng.count, w["n"], cid_base=rng.cid_base,
+                  cid_stride=rng.cid_stride)
+    out, chg, fb, rc = qref.CommitInputs(s).run(w["form"], False, nthreads=2)
+    assert rc == 0
+    if corrupt:
+        out = out.copy()
+        out[7] += np.uint64(1)
+    return [dict(n=w["n"], cid_base=rng.cid_base, cid_stride=rng.cid_stride, count=rng.count,
+                 out=[out, chg, fb])]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_rank_parity_checks_every_rank(n):
+    """at N > 1 every rank's set 0 is checked against the oracle (no
+    world == 1 gate) and every rank's verdict reaches rank 0; a wrong decision on one rank
+    shows on that rank only."""
+    w = dict(bench.WORKLOADS[bench.HEADLINE], G=3 * 4096 + 5)
+
+    def fn(d):
+        r = {"set0": _oracle_set0(w, d, corrupt=(d.rank == 1))}
+        return bench.rank_parity(w, r, d, no_cpu=False)
+    ds, out = _in_threads(n, fn)
+    for rank, r in enumerate(out):
+        assert r["parity"]["equal"] == (rank != 1)
+        assert [p["equal"] for p in r["parity_by_rank"]] == [i != 1 for i in range(n)]
+        assert sum(p["groups"] for p in r["parity_by_rank"]) == n * w["G"]   # weak scaling
+    # --no-cpu: no check, and the line says so (None), never a silent "equal"
+    _, out = _in_threads(n, lambda d: bench.rank_parity(w, {"set0": None}, d, no_cpu=True))
+    assert all(r["parity_by_rank"] == [None] * n for r in out)
 
 
 def test_host_cores_reports_counts():

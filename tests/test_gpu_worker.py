@@ -580,3 +580,46 @@ def test_rejected_steps_restore_state_on_device(hq, seed, feed):
         assert rejected == 2 * steps
     finally:
         w.close()
+
+
+def test_failed_regrow_leaves_state(hq, monkeypatch):
+    """a device step whose output region cannot be grown fails with every
+    group's state as it was before the step (pass A's in-place state taken back by
+    k_step_restore). The allocation failure is injected (HQ_TEST_FAIL_REGROW at open); the same
+    step on a worker whose region grows does change the state compared."""
+    import bench
+
+    G = 16384                      # step 0's G/4 ReadyToReads (128 KB) overflow the 64 KB region
+    roles = bench.STEP_ROLES["step"]
+    g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
+    grp, off, ev = bench.step_events(hq, G, 0, roles)
+    data, sizes = hq.encode_events_sized(off, ev)
+    nv = sum(r != "observer" for r in roles)
+    empty = np.zeros(0, np.uint8)
+    b = hq.Worker(0, nv, on_device=True)
+    monkeypatch.setenv("HQ_TEST_FAIL_REGROW", "1")
+    a = hq.Worker(0, nv, on_device=True)
+    monkeypatch.delenv("HQ_TEST_FAIL_REGROW")
+    sample = [int(c) for c in cids[::97]]
+
+    def state(w):
+        return [w.get_group(c) for c in sample]
+
+    def same(x, y):
+        return all(np.array_equal(u, v) for p, q in zip(x, y) for u, v in zip(p, q))
+    try:
+        for w in (a, b):
+            w.add_groups(g, m)
+            # a first step listing one group sizes the output region for one group's lists
+            w.step_sized(np.array([0], np.uint32), np.zeros(1, np.uint32), 0, empty)
+        before = state(a)
+        assert same(before, state(b))
+        with pytest.raises(hq.HQError, match="injected"):
+            a.step_sized(grp, sizes, len(ev), data)
+        assert same(before, state(a))
+        res = b.step_sized(grp, sizes, len(ev), data)
+        assert len(res["ready"]) == G // 4
+        assert not same(before, state(b))
+    finally:
+        a.close()
+        b.close()
