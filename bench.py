@@ -597,13 +597,16 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
     for k in range(windows):
         a = arr(first + k * steps, steps)
         rec = {}
-        for mode in ("engine", "launches", "signal"):
+        for mode in ("engine", "launches", "signal", "fused"):
             ctx.sync()
             d.sync_device()
             d.barrier()
             if mode == "launches":
                 ctx.timing_reset()
                 ctx.timing_begin_after(1 if steps > 1 else 0)
+            elif mode == "fused":
+                ctx.timing_reset()
+                ctx.timing(True)
             t0 = time.perf_counter()
             if mode == "engine":
                 eng.post(a)
@@ -614,6 +617,10 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
                 sig_local = time.perf_counter() - t0
                 clocks = [eng_sig.done_clock(q0 + i) for i in range(steps)]
                 eng_sig.drain()
+            elif mode == "fused":
+                ctx.commit_fused_dev(a)
+                ctx.timing(False)
+                ctx.sync()
             else:
                 ctx.commit_many_dev(a)
                 ctx.timing(False)
@@ -628,6 +635,9 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
                 local = sig_local
                 # device clock (100 MHz) between the first and the last step's completion
                 kernel_s = (clocks[-1] - clocks[0]) / 1e8 / max(1, steps - 1)
+            elif mode == "fused":
+                ms, nl = ctx.timing_read()
+                kernel_s = ms / 1e3 / max(1, steps)        # one launch for the window's steps
             else:
                 ms, nl = ctx.timing_read()
                 kernel_s = ms / 1e3 / max(1, nl)           # back-to-back launch time
@@ -689,6 +699,15 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
             "median_us_between_step_completions": med("signal", "kernel_s") * 1e6,
             "value": total_groups * decisions_per_group(w) / med("signal", "elapsed"),
         },
+        fused_window={
+            "mode": f"the window's {steps} batches in ONE launch (hq_commit_fused_dev, one "
+                    "workgroup range per batch)",
+            "window_ms": [round(x["fused"]["elapsed"] * 1e3, 4) for x in wins],
+            "median_ms_per_step": med("fused", "elapsed") / steps * 1e3,
+            "median_kernel_us_per_step": med("fused", "kernel_s") * 1e6,
+            "value": total_groups * decisions_per_group(w) / med("fused", "elapsed"),
+            "frac": d.sum(per_set / med("fused", "kernel_s") / 1e9) / (HBM_PEAK_GBS * d.world),
+        },
         launch_per_step={
             "mode": "the same batches as back-to-back launches (hq_commit_many_dev)",
             "window_ms": [round(x["launches"]["elapsed"] * 1e3, 4) for x in wins],
@@ -749,7 +768,49 @@ def _timed(ctx, d, run, steps, warmup):
     return d.max(t1 - t0), ms / 1e3 / max(1, launches), launches
 
 
-def run_kernel_leg(name, steps, warmup, d: Dist):
+def rim_inputs(rank: int, G: int = 2 << 20, K: int = 4, n: int = 7):
+    """The multi-ctx ReadIndex legs' inputs (rim / rimt) of one rank: first-ack ordinals
+    uint16 [K][n][G] (~70 % of (ctx, voter) pairs acked, arrival order 1..K*n, 0xFFFF = no ack)
+    and the pending ctxs' indexes uint64 [K][G] (non-decreasing per group)."""
+    r = np.random.default_rng(SEED_BASE + rank)
+    ordn = r.integers(1, K * n + 1, (K, n, G)).astype(np.uint16)
+    ordn[r.random((K, n, G)) < 0.3] = 0xFFFF
+    idx = (np.uint64(1 << 30) + np.arange(K, dtype=np.uint64)[:, None] * np.uint64(3)
+           + r.integers(0, 1 << 20, G, dtype=np.uint64)[None, :])
+    return G, K, n, ordn, idx
+
+
+def rim_parity(inputs, got, nthreads):
+    """A multi-ctx ReadIndex batch's released indexes, counts and batch ends against the oracle
+    (oracle/qref.c's message replay, readindex.go:77-116) on the same inputs, at full size."""
+    from oracle import qref
+
+    G, K, n, ordn, idx = inputs
+    t0 = time.perf_counter()
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ordn.reshape(-1), idx.reshape(-1), None, None,
+                                                    n, K, n, nthreads=nthreads)
+    want = {"released_index": rel, "released_count": cnt, "batch_end": bend}
+    eq = {k: bool(np.array_equal(got[k], want[k])) for k in want}
+    return dict(groups=G, equal=all(eq.values()) and not fb.any(), oracle_fallback=int(fb.any()),
+                check_s=time.perf_counter() - t0, **eq)
+
+
+def c4pq_oracle(seed_votes, seed_active, G, n, nthreads):
+    """The fused ReadIndex + vote + CheckQuorum pass's expected outputs: the oracle's readindex /
+    vote / leaderHasQuorum batches (readindex.go:77-116, raft.go:1968-1985, raft.go:380-390) on the
+    generator's bitmaps (the active flags: the ack bitmaps of another seed, as the leg packs
+    them), the voter count of the vote bitmaps for all three."""
+    from oracle import qref
+
+    inp = qref.BitmapInputs(qref.spec(seed_votes, G, n))
+    act = qref.BitmapInputs(qref.spec(seed_active, G, n)).ack
+    conf = qref.readindex_batch(inp.ack, inp.n_voting, 0, nthreads=nthreads)[0]
+    outc = qref.vote_batch(inp.granted, inp.rejected, inp.n_voting, 0, nthreads=nthreads)[0]
+    hqb = qref.check_quorum_batch(act, inp.n_voting, 0, 0, nthreads=nthreads)[0]
+    return {"confirmed": conf, "outcome": outc, "has_quorum": hqb}
+
+
+def run_kernel_leg(name, steps, warmup, d: Dist, parity_threads=0):
     """The remaining decision kernels, each on its own BASELINE-shaped batch, device-resident and
     rotated past the Infinity Cache like the commit legs:
       rim: general multi-ctx ReadIndex (k_ri_multi), 2M groups x 4 pending ctxs x 7 voters
@@ -765,13 +826,10 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
 
     ctx = hq.Context(d.device)
     r = np.random.default_rng(SEED_BASE + d.rank)
+    parity = None
     if name in ("rim", "rimt"):
-        G, K, n = 2 << 20, 4, 7
-        # first-ack ordinals: ~70 % of (ctx, voter) pairs acked, in arrival order 1..K*n
-        ordn = r.integers(1, K * n + 1, (K, n, G)).astype(np.uint16)
-        ordn[r.random((K, n, G)) < 0.3] = 0xFFFF
-        idx = (np.uint64(1 << 30) + np.arange(K, dtype=np.uint64)[:, None] * np.uint64(3)
-               + r.integers(0, 1 << 20, G, dtype=np.uint64)[None, :])
+        rim_in = rim_inputs(d.rank)
+        G, K, n, ordn, idx = rim_in
         per = G * (2 * K * n + 8 * K + 8 * K + 2)      # ordinals + ctx index in; released out
         nsets = max(4, int(np.ceil(ROTATE_BYTES / per)))
         sets = [(ctx.upload(ordn.reshape(-1)), ctx.upload(idx.reshape(-1)),
@@ -907,6 +965,30 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
                              "atomics (k_bin + k_apply, the default for a dense batch)"))
         units, unit = U, "updates/s"
     elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
+    if parity_threads and name in ("rim", "rimt"):
+        # every set holds the same inputs: set 0's outputs as the timed runs left them
+        rel, cnt, bend = (tiled[0][1:] if name == "rimt" else sets[0][2:])
+        ctx.sync()
+        parity = rim_parity(rim_in, {"released_index": ctx.download(rel),
+                                     "released_count": ctx.download(cnt),
+                                     "batch_end": ctx.download(bend)}, parity_threads)
+    elif parity_threads and name == "c4pq":
+        # set 0 once more with its active planes packed afresh (the timed runs zeroed them, as
+        # setNotActive does), its outputs poisoned first
+        pl, apl, conf, outc, hqb = sets[0]
+        act = ctx.empty(G, np.uint8)
+        ctx.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 5, G, n), act)
+        ctx.tile_cq_planes_dev(G, act, None, 8, 0, apl)
+        for x in (conf, outc, hqb):
+            ctx.memset(x, 0xA5)
+        ctx.readindex_vote_cq_planes_dev(G, pl, apl, conf, outc, hqb)
+        ctx.sync()
+        got = {"confirmed": ctx.download(conf), "outcome": ctx.download(outc),
+               "has_quorum": ctx.download(hqb)}
+        t0 = time.perf_counter()
+        want = c4pq_oracle(SEED_BASE + 3, SEED_BASE + 5, G, n, parity_threads)
+        eq = {k: bool(np.array_equal(got[k], want[k])) for k in want}
+        parity = dict(groups=G, equal=all(eq.values()), check_s=time.perf_counter() - t0, **eq)
     ctx.close()
     # the timed region opens behind the first launch: a step of L launches counts L * steps - 1
     L = max(1, round((launches + 1) / max(1, steps)))
@@ -918,6 +1000,7 @@ def run_kernel_leg(name, steps, warmup, d: Dist):
         "roofline_achieved_gbs": per / step_s / 1e9,
         "roofline_frac": per / step_s / 1e9 / HBM_PEAK_GBS,
         "algorithmic_bytes_per_step": per,
+        **({"parity_full_size": parity} if parity is not None else {}),
     }
 
 
@@ -1651,7 +1734,9 @@ def run_rank(args, d, progress):
                 rec = run_step_leg(d, G=args.step_groups, steps=args.step_steps,
                                    with_cpu=not args.no_cpu, name=name)
             elif name in ("rim", "rimt", "cq", "cqp", "c4pq", "ing", "ingo", "ingu", "inga"):
-                rec = run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d)
+                pt = 0 if args.no_cpu or args.no_extra_parity else max(1, host_threads // d.world)
+                rec = run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d,
+                                     parity_threads=pt)
             elif name == "sweep":
                 rec = run_size_sweep(args.workload, max(50, args.steps // 4),
                                      max(5, args.warmup // 4), d)
@@ -1784,6 +1869,7 @@ def report(args, d, res, launcher):
         line["engine"] = r["engine"]
         line["launch_per_step"] = r["launch_per_step"]
         line["engine_signal"] = r["engine_signal"]
+        line["fused_window"] = r["fused_window"]
     summary = {rec["name"]: _short(rec) for rec in res["records"]}
     detail = dict(line, result_gather=r.get("gather"), extra=res["records"])
     path = args.detail_out

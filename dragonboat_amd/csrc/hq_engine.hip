@@ -172,38 +172,46 @@ __device__ void relay(const EngineK &e, uint32_t lane) {
 // takes `lock` and becomes the workgroup's poller: it polls the relayed count in device memory
 // (workgroup 0's poller relays from the host ring first), copies the new descriptors into LDS and
 // publishes `known`. `waiting` counts the waves at the end of what they know; the workgroup exits
-// idle only when all of them are (so they leave at one step). Per ring slot, `claim` hands out the
-// workgroup's tiles of the slot's step one by one and `fin` counts those decided; both carry the
-// step number in their high half, so a slot's next step starts them afresh and a late claim for
-// a step the slot has moved past reads as exhausted.
+// idle only when all of them are (so they leave at one step). Per ring slot, `claim` hands out
+// the workgroup's tiles of the slot's step one by one (a fetch-add per tile) and `fin` counts
+// those decided; `tag` is the step they serve. The first wave to reach a step re-arms its
+// slot's counters, once no wave of the workgroup is still on the slot's previous step
+// (`cur[w]`: the step wave w claims in).
 struct EngineLds {
     EngineDesc ring[kEngineMaxDepth];
-    uint64_t claim[kEngineMaxDepth];
-    uint64_t fin[kEngineMaxDepth];
+    uint64_t tag[kEngineMaxDepth];
+    uint32_t claim[kEngineMaxDepth];
+    uint32_t fin[kEngineMaxDepth];
+    uint64_t cur[16];
     uint64_t known;
     uint32_t waiting, lock, exit, pad;
 };
 
-// lane 0: take the next index of step s's counter at `w` (step << 32 | count); returns the
-// index, or 0xFFFFFFFF when the slot already serves a later step
-__device__ __forceinline__ uint32_t lds_take(uint64_t *w, uint64_t s) {
-    const uint32_t tag = (uint32_t)s;
-    uint64_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (;;) {
-        const uint32_t t = (uint32_t)(old >> 32);
-        if ((int32_t)(t - tag) > 0) return 0xFFFFFFFFu;
-        const uint64_t nw = t == tag ? old + 1 : ((uint64_t)tag << 32) | 1;
-        if (__hip_atomic_compare_exchange_weak(w, &old, nw, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP))
-            return t == tag ? (uint32_t)old : 0u;
-    }
-}
+constexpr uint64_t kTagBusy = ~0ull;   // a wave is re-arming the slot
 
-// the count of step s at `w` (0 if the slot still shows an earlier step, ~0 if a later one)
-__device__ __forceinline__ uint32_t lds_count(uint64_t *w, uint64_t s) {
-    const uint64_t v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t t = (uint32_t)(v >> 32), tag = (uint32_t)s;
-    return t == tag ? (uint32_t)v : (int32_t)(t - tag) > 0 ? 0xFFFFFFFFu : 0u;
+// lane 0: make slot `slot` serve step s (no-op when it does): the winner of the tag waits until
+// every wave of the workgroup has left the slot's previous step (s - depth), zeroes the
+// counters and publishes the tag; the others wait for it.
+template <int WPW>
+__device__ void arm_slot(EngineLds &l, uint64_t slot, uint64_t s, uint64_t depth) {
+    for (;;) {
+        uint64_t t = __hip_atomic_load(&l.tag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t == s) return;
+        if (t != kTagBusy && __hip_atomic_compare_exchange_strong(
+                                 &l.tag[slot], &t, kTagBusy, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+#pragma unroll 1
+            for (int w = 0; w < WPW; ++w)
+                while (__hip_atomic_load(&l.cur[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                           depth <= s)
+                    __builtin_amdgcn_s_sleep(1);
+            __hip_atomic_store(&l.claim[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&l.fin[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&l.tag[slot], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 __device__ __forceinline__ uint64_t lds_known(EngineLds &l) {
@@ -321,7 +329,8 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
     const bool relayer = blockIdx.x == 0;
     const uint64_t dmask = e.depth - 1;
     uint64_t s = uniform64(e.d_cursor[blockIdx.x]);   // written by the previous launch
-    for (uint32_t i = threadIdx.x; i < kEngineMaxDepth; i += BLK) l.claim[i] = l.fin[i] = 0;
+    for (uint32_t i = threadIdx.x; i < kEngineMaxDepth; i += BLK) l.tag[i] = kTagBusy - 1;
+    if (lane == 0) l.cur[wv] = s;
     // the descriptors handed over at launch (the host's oldest incomplete step <= the cursor)
     if (wv == 0 && lane < 6) {
 #pragma unroll
@@ -360,7 +369,11 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
             // the first wave here counts the workgroup's arrival at the STOP (every step before
             // it is complete once the grid has exited)
             uint32_t i = 0;
-            if (lane == 0) i = lds_take(&l.claim[slot], s);
+            if (lane == 0) {
+                arm_slot<WPW>(l, slot, s, e.depth);
+                i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             if (wave_u32(i) == 0 && lane == 0) {
                 if (blockIdx.x % 64 == 0) HQ_EPROBE_MAX(e, 10);   // workgroups at the STOP
                 arrive(e, s);
@@ -380,9 +393,12 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
         const uint64_t per = (tiles + gridDim.x - 1) / gridDim.x;
         const uint64_t b0 = (uint64_t)blockIdx.x * per;
         const uint32_t len = (uint32_t)(b0 >= tiles ? 0 : tiles - b0 < per ? tiles - b0 : per);
+        if (lane == 0) arm_slot<WPW>(l, slot, s, e.depth);
         for (;;) {
             uint32_t i = 0;
-            if (lane == 0) i = lds_take(&l.claim[slot], s);
+            if (lane == 0)
+                i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
             i = wave_u32(i);
             if (i >= len) {
                 // the first claim past the end of an empty range stands in for its last tile
@@ -393,7 +409,9 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
             if (e.signal || INPLACE) {
                 if (e.signal) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // WT drained
                 uint32_t f = 0;
-                if (lane == 0) f = lds_take(&l.fin[slot], s) + 1;
+                if (lane == 0)
+                    f = __hip_atomic_fetch_add(&l.fin[slot], 1u, __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
                 if (wave_u32(f) == len && e.signal && lane == 0) arrive(e, s);
             }
         }
@@ -408,9 +426,12 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
 #endif
         if constexpr (INPLACE) {
             // the table's tiles of step s + 1 are those of step s: wait until they are decided
-            while (lds_count(&l.fin[slot], s) < len) __builtin_amdgcn_s_sleep(2);
+            while (__hip_atomic_load(&l.fin[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                   len)
+                __builtin_amdgcn_s_sleep(2);
         }
         ++s;
+        if (lane == 0) __hip_atomic_store(&l.cur[wv], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (lane == 0 && wv == 0) e.d_cursor[blockIdx.x] = s;
 }
@@ -943,6 +964,40 @@ __global__ __launch_bounds__(BLK, OCC) void k_exp_claim(const MultiK m) {
         }
     }
 }
+// V6: every wave claims tiles one at a time from a device counter shared by the waves of
+// workgroups b and b + grid/2 (per batch), the next claim issued before the current tile is
+// decided: balance across the two workgroups of a CU, no LDS
+template <int N, int FORM, int LEAD, int BLK>
+__global__ __launch_bounds__(BLK, 8) void k_exp_gclaim(const MultiK m, uint32_t *ctr) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t half = gridDim.x / 2;
+    const uint32_t pair = blockIdx.x % half;
+    const uint64_t per = (m.ntiles + half - 1) / half;
+    const uint64_t b0 = pair * per;
+    const uint32_t len = (uint32_t)(b0 >= m.ntiles ? 0 : m.ntiles - b0 < per ? m.ntiles - b0 : per);
+    uint32_t c = 0;
+    uint32_t nxt = 0;
+    if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c * half + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (c < m.count) {
+        const uint32_t i = __builtin_amdgcn_readfirstlane(nxt);
+        if (i >= len) {
+            ++c;
+            if (c < m.count && lane == 0)
+                nxt = __hip_atomic_fetch_add(ctr + c * half + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c * half + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        CommitK k{};
+        k.G = m.G;
+        k.stride = m.stride;
+        k.match = m.tiles[c];
+        k.cout = m.cout[c];
+        k.changed = m.chg[c];
+        k.fallback = m.fb[c];
+        k.R = m.R;
+        commit_tile<N, FORM, false, LEAD, false>(k, (b0 + i) * HQ_TILE_GROUPS, lane);
+    }
+}
 }  // namespace
 
 extern "C" int hq_exp_engine_set(hq_engine *e, uint32_t bits) {
@@ -985,6 +1040,12 @@ extern "C" int hq_exp_multi(hq_ctx *ctx, const hq_commit_args *a, uint32_t count
         m.waves = grid * 16;
         hipLaunchKernelGGL((k_exp_loop<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid), dim3(1024), 0,
                            ctx->stream, m);
+    } else if (variant == 6) {
+        static uint32_t *ctr = nullptr;
+        if (!ctr && hipMalloc(&ctr, 4 * kExpMax * 1024) != hipSuccess) return HQ_E_NOMEM;
+        (void)hipMemsetAsync(ctr, 0, 4 * kExpMax * 1024, ctx->stream);
+        hipLaunchKernelGGL((k_exp_gclaim<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid ? grid : 512),
+                           dim3(1024), 0, ctx->stream, m, ctr);
     } else if (variant == 3) {
         hipLaunchKernelGGL((k_exp_claim<5, HQ_FORM_TERM_MASK, 1, 1024, 4>), dim3(grid ? grid : 256),
                            dim3(1024), 0, ctx->stream, m);

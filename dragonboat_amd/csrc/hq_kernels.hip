@@ -207,11 +207,15 @@ __global__ __launch_bounds__(HQ_COMMIT_BLOCK_BIG, 8) void k_commit_big(const Com
 // batch i owns workgroups [first[i], first[i+1]); the batch index and its n are uniform per
 // workgroup, so the switch costs no divergence. Saves the dependent-launch boundary and the
 // grid fill / drain between buckets (MI355X_MICROARCH.md "boundary": 1.7-1.9 us each).
-constexpr int kMaxFused = 8;
+constexpr int kMaxFused = 8;        // lag batches per fused launch
+// commit batches per fused launch: a step worker's voter-count buckets, or the independent
+// batches of several steps / step workers posted together (32 x 1M-group batches in one launch:
+// no boundary, fill or drain between them; 3.3 KB of kernel arguments)
+constexpr int kMaxFusedCommit = 32;
 struct FusedK {
-    CommitK b[kMaxFused];
-    uint32_t first[kMaxFused + 1];
-    uint32_t n[kMaxFused];   // dwords: a scalar load (a byte array is read with a vector load + wait)
+    CommitK b[kMaxFusedCommit];
+    uint32_t first[kMaxFusedCommit + 1];
+    uint32_t n[kMaxFusedCommit];   // dwords: a scalar load (a byte array is read with a vector load + wait)
     uint32_t count;
 };
 
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_fuse
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
 #pragma unroll
-    for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
+    for (int k = 1; k < kMaxFusedCommit; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
     const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
     switch (f.n[i]) {
     case 1: commit_blocks<1, FORM, 2, false, BLK, TILED>(f.b[i], b, nb); break;
@@ -475,7 +479,7 @@ __global__ __launch_bounds__(BLK, BLK > kCommitBlock ? 8 : 1) void k_commit_lag_
     const uint32_t blk = blockIdx.x;
     uint32_t i = 0;
 #pragma unroll
-    for (int k = 1; k < kMaxFused; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
+    for (int k = 1; k < kMaxFusedCommit; ++k) i += (k < (int)f.count && blk >= f.first[k]) ? 1u : 0u;
     const uint64_t b = blk - f.first[i], nb = f.first[i + 1] - f.first[i];
     switch (f.n[i]) {
     case 1: lag_blocks<1, FORM, kLagVec, false, BLK, LEAD>(f.b[i], b, nb); break;
@@ -1494,7 +1498,7 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
         if (rc) return rc;
     }
     // batches that can share the launch: uniform n, 16-byte aligned columns, one form
-    bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
+    bool fusable = count >= 2 && count <= (uint32_t)kMaxFusedCommit;
     for (uint32_t i = 0; fusable && i < count; ++i)
         fusable = args[i].G > 0 && !args[i].n_voting && commit_vec2(args + i) &&
                   args[i].form == args[0].form && args[i].layout == args[0].layout &&
@@ -1513,7 +1517,7 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
     // workgroup ranges in launch order, the widest batches first (their waves are dispatched
     // first, so the tail is made of the light ones: c5t 96-97 -> 93-94 us,
     // profiles/r01f/ab_heavy_first.log; HQ_FUSED_HEAVY_FIRST=0 keeps the argument order)
-    uint32_t order[kMaxFused];
+    uint32_t order[kMaxFusedCommit];
     for (uint32_t i = 0; i < count; ++i) order[i] = i;
 #if HQ_FUSED_HEAVY_FIRST
     for (uint32_t i = 1; i < count; ++i)
@@ -1531,7 +1535,7 @@ extern "C" int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint
         // the same lanes per batch as its own launch would get (grid-stride beyond that)
         blocks += grid_for((args[order[k]].G + 1) / 2, B, (uint64_t)kMaxBlocks * 256 / B);
     }
-    for (uint32_t i = count; i <= (uint32_t)kMaxFused; ++i) f.first[i] = (uint32_t)blocks;
+    for (uint32_t i = count; i <= (uint32_t)kMaxFusedCommit; ++i) f.first[i] = (uint32_t)blocks;
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
 #define HQ_FUSED(F, BLK)                                                                       \
@@ -1682,7 +1686,7 @@ extern "C" int hq_commit_lag_fused_dev(hq_ctx *ctx, const hq_commit_lag_args *ar
         int rc = validate_lag(ctx, args + i);
         if (rc) return rc;
     }
-    bool fusable = count >= 2 && count <= (uint32_t)kMaxFused;
+    bool fusable = count >= 2 && count <= (uint32_t)kMaxFusedCommit;
     for (uint32_t i = 0; fusable && i < count; ++i)
         fusable = args[i].G > 0 && !args[i].n_voting && lag_vec(args + i) &&
                   args[i].form == args[0].form && args[i].flags == args[0].flags;

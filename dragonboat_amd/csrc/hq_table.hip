@@ -703,7 +703,9 @@ bool bin_plan(const hq_ctx *ctx, const TableK &t, uint64_t count, bool lag, BinK
     bk.B = (uint32_t)B;
     lds_bin = kBinChunk * 8 + 8 * (size_t)bk.B + 64;
     lds_apply = ((size_t)bk.rows << (10 + sh)) + meta_lds;
-    ws = (size_t)bk.nchunks * kBinChunk * 8 + (size_t)bk.nchunks * bk.B * 4;
+    // + 64 entries of padding: k_apply's unconditional loads read up to 31 entries past the last
+    // chunk's last segment, which must stay inside the allocation
+    ws = (size_t)bk.nchunks * kBinChunk * 8 + (size_t)bk.nchunks * bk.B * 4 + 64 * 8;
     return true;
 }
 

@@ -264,11 +264,12 @@ int hq_tile_commit_as_host(const hq_commit_args *columns, uint64_t *tiles, uint3
 /* `count` independent batches back to back on the context's stream (e.g. a step worker's
  * per-voter-count buckets of one step, or successive steps). Stops at the first invalid batch. */
 int hq_commit_many_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
-/* The same `count` batches decided by ONE kernel launch when they can share it (2..8 batches,
- * uniform n (n_voting NULL), one form, 16-byte aligned columns, G > 0): a step worker's
- * voter-count buckets (groups bucketed by n for coalesced SoA, execengine.go:923 caller). Batch i
- * owns its own workgroups; results are identical to hq_commit_many_dev, which is what runs
- * when the batches cannot share a launch. */
+/* The same `count` batches decided by ONE kernel launch when they can share it (2..32 batches,
+ * uniform n (n_voting NULL), one form, 16-byte aligned columns, G > 0, not in place): a step
+ * worker's voter-count buckets (groups bucketed by n for coalesced SoA, execengine.go:923
+ * caller), or the independent batches that several step workers (or steps) have ready at once.
+ * Batch i owns its own workgroups; results are identical to hq_commit_many_dev, which is what
+ * runs when the batches cannot share a launch. */
 int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count);
 
 /* ---------------------------------------------------------------- persistent commit engine -- */

@@ -7,6 +7,7 @@ device generator's inputs, in the headline layouts.
 
 usage: python tests/golden/make_config_digests.py   (from the repo root; ~1 minute on 8 cores)
        python tests/golden/make_config_digests.py --c5-node   (adds only the 8-GPU C5 shards)
+       python tests/golden/make_config_digests.py --planes    (adds only RIM and C4PQ)
 """
 import hashlib
 import json
@@ -49,6 +50,32 @@ def bitmap_case(name, seed, G, n):
             "outcome": digest(outc), "n_confirmed": bits(conf, G)}
 
 
+def rim_case():
+    """The multi-ctx ReadIndex legs' batch (bench.py rim / rimt, rank 0: 2 Mi groups x 4 pending
+    ctxs x 7 voters) decided by the oracle's message replay."""
+    import bench
+
+    G, K, n, ordn, idx = bench.rim_inputs(0)
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ordn.reshape(-1), idx.reshape(-1), None, None,
+                                                    n, K, n, nthreads=THREADS)
+    assert not fb.any()
+    return {"kind": "readindex_multi", "G": G, "K": K, "n": n, "rank": 0,
+            "released_index": digest(rel), "released_count": digest(cnt),
+            "batch_end": digest(bend), "n_released": int(cnt.astype(np.int64).sum())}
+
+
+def c4pq_case():
+    """BASELINE config 4 with CheckQuorum (bench.py c4pq, set 0: 16 Mi groups x 7 voters, the
+    active flags the ack bitmaps of seed + 2) decided by the oracle's batches."""
+    import bench
+
+    G, n = 16 << 20, 7
+    want = bench.c4pq_oracle(SEED + 3, SEED + 5, G, n, THREADS)
+    return {"kind": "readindex_vote_checkquorum", "G": G, "n": n, "seed_votes": SEED + 3,
+            "seed_active": SEED + 5, **{k: digest(v) for k, v in want.items()},
+            "n_has_quorum": bits(want["has_quorum"], G)}
+
+
 def main():
     from dragonboat_amd import shard
 
@@ -65,6 +92,8 @@ def main():
                                              shard.MIXED_VOTERS[b], 2, rng.cid_base,
                                              rng.cid_stride)
     cases.update(c5_node_cases())
+    cases["RIM"] = rim_case()
+    cases["C4PQ"] = c4pq_case()
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config_digests.json")
     json.dump(cases, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(cases, indent=1))
@@ -88,10 +117,15 @@ def c5_node_cases():
 
 
 if __name__ == "__main__":
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config_digests.json")
     if "--c5-node" in sys.argv:
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config_digests.json")
         cases = json.load(open(path))
         cases.update(c5_node_cases())
+        json.dump(cases, open(path, "w"), indent=1, sort_keys=True)
+    elif "--planes" in sys.argv:       # adds only the multi-ctx ReadIndex and fused-planes cases
+        cases = json.load(open(path))
+        cases["RIM"] = rim_case()
+        cases["C4PQ"] = c4pq_case()
         json.dump(cases, open(path, "w"), indent=1, sort_keys=True)
     else:
         main()

@@ -111,11 +111,13 @@ def test_gpu_c4_digest(gpu_ctx, hq, path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("rank", range(8))
 def test_gpu_c5_node_shard_digest(gpu_ctx, hq, rank):
-    """BASELINE config 5 whole — 64 Mi groups with 3 / 5 / 7 voters (clusterID % 3), sharded
+    """BASELINE config 5 — 64 Mi groups with 3 / 5 / 7 voters (clusterID % 3), sharded
     clusterID % 8 over 8 GPUs (partition.go:38) — one GPU's share per case: its three buckets
     generated on the device, decided in one fused launch over leader-row tiles, equal to the
     oracle's digests of that shard (tests/golden/make_config_digests.py --c5-node). Together the
-    eight cases check every decision of the 8-GPU configuration on one GPU."""
+    eight cases check 24 x ((8 Mi) // 3) = 67,108,848 groups on one GPU: the configuration's
+    64 Mi groups less the 16 that 8 Mi per rank leaves over after three equal buckets (the
+    bench's per-rank shape, bench.py commit_buckets)."""
     cases = [GOLD[f"C5x8_rank{rank}_bucket{b}"] for b in range(3)]
     got = _commit_on_gpu(gpu_ctx, hq, cases, hq.HQ_LAYOUT_TILES_LEADER)
     for c, g in zip(cases, got):
@@ -136,3 +138,78 @@ def test_c5_node_digests_cover_the_config():
             c = GOLD[f"C5x8_rank{r}_bucket{b}"]
             assert c["cid_base"] % 8 == r and c["cid_base"] % 3 == b and c["cid_stride"] == 24
             assert c["n"] == shard.MIXED_VOTERS[b]
+
+
+def test_oracle_reproduces_rim_and_c4pq_digests():
+    """The multi-ctx ReadIndex batch the rim / rimt legs time (2 Mi x 4 ctxs x 7 voters) and the
+    fused ReadIndex + vote + CheckQuorum batch c4pq times (16 Mi x 7): the oracle still makes the
+    committed digests from bench.py's own input helpers."""
+    import bench
+
+    nt = os.cpu_count() or 1
+    c = GOLD["RIM"]
+    G, K, n, ordn, idx = bench.rim_inputs(c["rank"])
+    assert (G, K, n) == (c["G"], c["K"], c["n"])
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ordn.reshape(-1), idx.reshape(-1), None, None,
+                                                    n, K, n, nthreads=nt)
+    assert not fb.any()
+    assert (digest(rel), digest(cnt), digest(bend)) == (
+        c["released_index"], c["released_count"], c["batch_end"])
+    c = GOLD["C4PQ"]
+    want = bench.c4pq_oracle(c["seed_votes"], c["seed_active"], c["G"], c["n"], nt)
+    for k in ("confirmed", "outcome", "has_quorum"):
+        assert digest(want[k]) == c[k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["tiles", "columns"])
+def test_gpu_rim_digest(gpu_ctx, hq, path):
+    """rim / rimt at the bench's full size: the multi-ctx release (k_ri_multi2 over 128-group
+    tiles, and over columns) equals the oracle's replay digests."""
+    import bench
+
+    c = GOLD["RIM"]
+    G, K, n, ordn, idx = bench.rim_inputs(c["rank"])
+    o, x = gpu_ctx.upload(ordn.reshape(-1)), gpu_ctx.upload(idx.reshape(-1))
+    rel, cnt, bend = (gpu_ctx.empty(K * G, np.uint64), gpu_ctx.empty(G, np.uint8),
+                      gpu_ctx.empty(G, np.uint8))
+    extra = []
+    if path == "tiles":
+        t = gpu_ctx.empty((G // 128) * hq.ri_tile_bytes(K, n, 0), np.uint8)
+        gpu_ctx.tile_ri_multi_dev(G, K, n, o, x, None, None, t)
+        gpu_ctx.readindex_multi_tiles_dev(G, K, n, t, 0, n, rel, cnt, batch_end=bend)
+        extra = [t]
+    else:
+        gpu_ctx.readindex_multi_dev(G, K, n, o, x, None, None, n, rel, cnt, batch_end=bend)
+    gpu_ctx.sync()
+    assert (digest(gpu_ctx.download(rel)), digest(gpu_ctx.download(cnt)),
+            digest(gpu_ctx.download(bend))) == (c["released_index"], c["released_count"],
+                                                c["batch_end"])
+    for a in [o, x, rel, cnt, bend] + extra:
+        gpu_ctx.free(a)
+
+
+@pytest.mark.gpu
+def test_gpu_c4pq_digest(gpu_ctx, hq):
+    """c4pq at the bench's full size (16 Mi x 7): ReadIndex + vote + CheckQuorum in one pass over
+    the bit planes equals the oracle's three batches; the active planes are zeroed."""
+    c = GOLD["C4PQ"]
+    G, n = c["G"], c["n"]
+    T = hq.HQ_PLANE_TILE_GROUPS
+    arrs = [gpu_ctx.empty(G, np.uint8) for _ in range(4)]
+    gpu_ctx.synth_bitmaps_dev(hq.synth_spec(c["seed_votes"], G, n), *arrs)
+    pl, apl = gpu_ctx.empty(hq.plane_tiles(G) * 3 * T, np.uint8), gpu_ctx.empty(
+        hq.cq_plane_bytes(G, 8), np.uint8)
+    gpu_ctx.tile_planes_dev(G, *arrs, 0, pl)
+    gpu_ctx.synth_bitmaps_dev(hq.synth_spec(c["seed_active"], G, n), arrs[0])
+    gpu_ctx.tile_cq_planes_dev(G, arrs[0], None, 8, 0, apl)
+    conf, outc, hqb = (gpu_ctx.empty(hq.words64(G), np.uint64), gpu_ctx.empty(hq.words32(G), np.uint64),
+                       gpu_ctx.empty(hq.words64(G), np.uint64))
+    gpu_ctx.readindex_vote_cq_planes_dev(G, pl, apl, conf, outc, hqb)
+    gpu_ctx.sync()
+    assert digest(gpu_ctx.download(conf)) == c["confirmed"]
+    assert digest(gpu_ctx.download(outc)) == c["outcome"]
+    assert digest(gpu_ctx.download(hqb)) == c["has_quorum"]
+    assert not gpu_ctx.download(apl).any()
+    for a in arrs + [pl, apl, conf, outc, hqb]:
+        gpu_ctx.free(a)

@@ -54,6 +54,7 @@ def main():
         "claim256": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 3, 256)),
         "claim512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 4, 512)),
         "claim512x2": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 5, 1024)),
+        "gclaim512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 6, 512)),
         "engine": None,
     }
     only = os.environ.get("AB_ONLY")
@@ -95,7 +96,8 @@ def main():
                 res[name].append((ms * 1e3 / K, wall * 1e6 / K))
     # correctness of the experiment kernels: set 0 decided by each equals the launch path
     ref = None
-    for name in [x for x in ("launches", "loop512", "flat", "claim256", "claim512", "claim512x2")
+    for name in [x for x in ("launches", "loop512", "flat", "claim256", "claim512", "claim512x2",
+                             "gclaim512")
                  if x in variants]:
         b = sets[0][0]
         ctx.memset(b.committed_out, 0xA5)

@@ -1,7 +1,16 @@
 #!/bin/bash
-# One GPU-box session of round 3: parity tests, smoke, the default bench line, then rocprofv3
-# evidence of the headline (kernel trace + one PMC pass per counter). Stops at the first
-# fault / timeout / abort; a plain test failure (pytest exit 1) still lets the bench run.
+# One GPU-box session: parity tests, smoke, the default bench line, the multi-GPU rehearsals,
+# then rocprofv3 evidence (kernel trace + one PMC pass per counter) of the workloads in PROFILE.
+# Stops at the first fault / timeout / abort; a plain test failure (pytest exit 1) still lets the
+# bench run. Knobs (environment):
+#   TESTS="tests/test_x.py ..."  PYTEST_K="expr"   the GPU tests to run (default: all of -m gpu)
+#   SKIP_TESTS=1 SKIP_BENCH=1     skip those steps;  BENCH_ARGS="..." extra bench.py arguments
+#   REHEARSE=0                    skip the --gpus 2 threads rehearsal (default on)
+#   REHEARSE_TORCHRUN=1 REHEARSE8=1   the torchrun N = 2 and the --gpus 8 c5tl rehearsals
+#   AB="tools/ab_engine.py ..."   python scripts run after the bench (A/B drivers), one step each
+#   PROFILE="c3mtl c4pq ..."      tools/profile_bench.sh per workload
+# (replaces the round-2 gpu_r02.sh and the round-3 one-off g1.sh ... g17.sh, which git history
+# keeps as they were run)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -15,7 +24,8 @@ step() {  # step <name> <timeout> <cmd...>
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step gpu_tests 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 120 \
+    --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
   rc=$?; if fatal $rc; then exit $rc; fi
   step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
   rc=$?; if fatal $rc; then exit $rc; fi
@@ -45,6 +55,9 @@ if [ "${REHEARSE8:-0}" = 1 ]; then
     --warmup 5 --no-cpu --extra= --detail-out gpurun_out/bench_c5tl_n8_detail.json
   rc=$?; if fatal $rc; then exit $rc; fi
 fi
+for A in ${AB:-}; do
+  step ab_$(basename $A .py) 300 python -u $A || exit $?
+done
 for W in ${PROFILE:-}; do
   step prof_$W 400 bash tools/profile_bench.sh $W || exit $?
 done
