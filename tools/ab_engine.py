@@ -5,6 +5,7 @@ leader-row tiles, mask form) on one GPU, same data, alternated rounds:
   loop       ONE launch, every wave loops over the K batches (the engine's ownership, no doorbell)
   flat       ONE launch, one wave per (batch, tile), batch-major
   engine     the persistent engine (hq_engine): K posted descriptors, one resident launch
+             (engine: device pair claims; engine_lds: HQ_ENGINE_CLAIM=0, per-workgroup LDS ranges)
 Needs the experiment build: HQ_LIB_PATH=tools/lib_engexp/libhipquorum.so (make that target)."""
 import ctypes
 import os
@@ -42,9 +43,13 @@ def main():
     def arr(i0):
         return hq.commit_batch_array([bench.batch_args(sets[(i0 + i) % nsets][0]) for i in range(K)])
 
-    eng = hq.Engine(ctx, w["n"], w["form"], hq.HQ_LAYOUT_TILES_LEADER, ring_len=16)
+    engines = {}
     hq.lib.hq_exp_engine_set.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    hq.lib.hq_exp_engine_set(eng.h, int(os.environ.get("AB_ENGINE_EXP", "0")))
+    for name, claim in (("engine", "1"), ("engine_lds", "0")):
+        os.environ["HQ_ENGINE_CLAIM"] = claim
+        engines[name] = hq.Engine(ctx, w["n"], w["form"], hq.HQ_LAYOUT_TILES_LEADER, ring_len=16)
+        hq.lib.hq_exp_engine_set(engines[name].h, int(os.environ.get("AB_ENGINE_EXP", "0")))
+    os.environ.pop("HQ_ENGINE_CLAIM")
     variants = {
         "launches": lambda a: ctx.commit_many_dev(a),
         "loop512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 1, 512)),
@@ -56,6 +61,7 @@ def main():
         "claim512x2": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 5, 1024)),
         "gclaim512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 6, 512)),
         "engine": None,
+        "engine_lds": None,
     }
     only = os.environ.get("AB_ONLY")
     if only:
@@ -68,14 +74,15 @@ def main():
             i0 += K
             ctx.sync()
             t0 = time.perf_counter()
-            if name == "engine":
+            if name in engines:
+                eng = engines[name]
                 pr = (ctypes.c_uint64 * (64 + 16384))()
                 hq.lib.hq_exp_engine_probe(eng.h, pr)
                 eng.post(a)
                 eng.drain()
                 n, ms = eng.timing(reset=True)
                 hq.lib.hq_exp_engine_probe(eng.h, pr)
-                if r == ROUNDS:
+                if r == ROUNDS and name == "engine":
                     t0p = pr[0]
                     print("engine phases (us after the first sampled wave started): " + ", ".join(
                         f"{PROBES[i]} {(pr[i] - t0p) / 100:.2f}" for i in range(12)
@@ -112,7 +119,14 @@ def main():
         wl = np.array([x[1] for x in v])
         print(f"{name:9s} kernel us/step median {np.median(k):7.3f} (min {k.min():7.3f})  "
               f"frac {per_set / np.median(k) / 1e3 / 8000:.3f}   wall us/step {np.median(wl):7.3f}")
-    eng.close()
+    for name, eng in engines.items():
+        b = sets[0][0]
+        ctx.memset(b.committed_out, 0xA5)
+        eng.post(arr(0))
+        eng.drain()
+        out = ctx.download(b.committed_out)
+        print(f"{name}: set0 equal to launches: {ref is None or np.array_equal(out, ref)}")
+        eng.close()
     ctx.close()
 
 
