@@ -78,3 +78,14 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
 int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t nm, hq_dmember *m);
 // one step over the device state; the kernels check the input (out->input_error)
 int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out);
+// several engines' steps through shared launches (hq_worker_step_jobs): every input a sized
+// stream, every engine on ds[0]'s device, count <= 64; each job's result in rcs[j] and outs[j]
+// as hq_dstep_run gives it; returns the first failure
+int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out *outs, int *rcs,
+                      uint32_t count);
+constexpr uint32_t kDStepMaxJobs = 64;
+
+// hq_worker.cpp, for hq_worker_step_jobs (hq_jobs.cpp): the jobs stepped through shared device
+// launches when they allow it; kJobsNotFused (nothing done) when they do not
+constexpr int kJobsNotFused = 1 << 30;
+int hq_worker_step_jobs_fused(hq_step_job *jobs, uint32_t count);

@@ -86,6 +86,13 @@ struct StepK {
                                   //   commit is one ReadyToRead, kept in ready_slot
     hq_ready_to_read *ready_slot; // [n] pass A: a group's first ReadyToRead of the step
     uint32_t *rerun_list;         // [n] k_step_lite: the positions of those groups, in order
+    // the jobs path (hq_dstep_run_jobs: several workers' steps in shared launches): the layout's
+    // arguments, the sizes of a sized stream and the per-1024-group sums of their scan
+    uint64_t out_cap;
+    uint32_t allow_column, pad_j;
+    struct Layout *host_layout;
+    const uint32_t *sizes;
+    uint64_t *bsum;
 };
 
 struct PackSize {                 // group i's size word -> events << 32 | bytes; i = n: 0 (the
@@ -555,7 +562,6 @@ struct Engine {
     }
 };
 
-template <bool WRITE, bool STREAM, int MC>
 // HQ_STEP_WAVES: waves per SIMD asked of the compiler (0: its own choice, 2-3 waves at 157-177
 // VGPRs); a group's events are one serial dependency chain, so resident waves hide its latency
 #ifndef HQ_STEP_WAVES
@@ -566,12 +572,13 @@ template <bool WRITE, bool STREAM, int MC>
 #else
 #define HQ_STEP_OCC
 #endif
-__global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
+template <bool WRITE, bool STREAM, int MC>
+__device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
     // pass A: the wave's counts summed in LDS, added to wsum by one lane (i_begin is a multiple
     // of 64: the wave's groups are one wave of the scan)
     __shared__ uint32_t wtot[WRITE ? 1 : 256 / 64][kLists];
     if (!WRITE && (threadIdx.x & 63) < kLists) wtot[threadIdx.x >> 6][threadIdx.x & 63] = 0;
-    uint64_t i = a.i_begin + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t i = a.i_begin + blk * 256 + threadIdx.x;
     if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
     if (WRITE && a.layout->commit_column) {
         // the commits are a column (k_step_lite wrote it from pass A's state): pass B takes
@@ -671,11 +678,37 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
     }
 }
 
+template <bool WRITE, bool STREAM, int MC>
+__global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
+    step_groups<WRITE, STREAM, MC>(a, blockIdx.x);
+}
+
+// The jobs path: one launch over several workers' steps, each job's groups in consecutive
+// workgroups (blk0[j] .. blk0[j + 1]) and its StepK in device memory
+constexpr uint32_t kMaxJobs = 64;
+struct JobMap {
+    const StepK *ks;              // the jobs' StepK, job0 .. job0 + count - 1 in this launch
+    uint32_t job0, count;
+    uint32_t blk0[kMaxJobs + 1];  // relative to job0
+};
+
+__device__ __forceinline__ uint32_t job_of(const JobMap &m, uint32_t b) {
+    uint32_t j = 0;               // (uniform: kernel arguments and blockIdx)
+    while (j + 1 < m.count && b >= m.blk0[j + 1]) ++j;
+    return j;
+}
+
+template <bool WRITE, bool STREAM, int MC>
+__global__ __launch_bounds__(256) HQ_STEP_OCC void k_step_jobs(const JobMap m) {
+    const uint32_t j = job_of(m, blockIdx.x);
+    step_groups<WRITE, STREAM, MC>(m.ks[m.job0 + j], blockIdx.x - m.blk0[j]);
+}
+
 // Between the layout and pass B: with the commits as a column, every listed group's word from
 // the committed index pass A saved and the one it wrote (the advance, or the new index), and the
 // positions of the groups with other records packed in order for pass B; in list mode nothing
-__global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk) {
+    const uint64_t i = blk * 256 + threadIdx.x;
     if (i < a.ws) a.wsum[i] = 0;  // (scanned already; the grid covers ws: 9 n / 64 + 10 <= max(n, 256))
     const bool in = i < a.n;
     if ((a.layout->error | a.layout->overflow) || !__ballot(in)) return;   // (whole waves)
@@ -740,6 +773,13 @@ __global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
         const uint64_t l = kRerun;
         a.rerun_list[a.scan[l * a.nw + (i >> 6)] - a.scan[l * a.nw] + pre_rerun] = (uint32_t)i;
     }
+}
+
+__global__ __launch_bounds__(256) void k_step_lite(const StepK a) { lite_groups(a, blockIdx.x); }
+
+__global__ __launch_bounds__(256) void k_step_lite_jobs(const JobMap m) {
+    const uint32_t j = job_of(m, blockIdx.x);
+    lite_groups(m.ks[m.job0 + j], blockIdx.x - m.blk0[j]);
 }
 
 // A step with an input error writes no group state: the groups pass A stepped get back the
@@ -820,11 +860,9 @@ __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t
 // threads' totals scanned across the waves, with the carry of the tiles before
 constexpr int kScanT = 1024, kScanE = 11;
 constexpr uint64_t kScanSmall = 2 * kScanT * kScanE;   // sums taken this way (2 tiles)
-__global__ __launch_bounds__(kScanT) void k_scan_layout(const uint32_t *wsum, uint32_t *scan,
-                                                        uint64_t ws, uint64_t n, uint64_t nw,
-                                                        uint32_t *error, uint64_t cap,
-                                                        uint32_t allow_column, Layout *lay,
-                                                        Layout *host_lay) {
+__device__ __forceinline__ void scan_layout(const uint32_t *wsum, uint32_t *scan, uint64_t ws,
+                                            uint64_t n, uint64_t nw, uint32_t *error, uint64_t cap,
+                                            uint32_t allow_column, Layout *lay, Layout *host_lay) {
     __shared__ uint32_t tile[kScanT * kScanE];
     __shared__ uint32_t wtot[kScanT / 64];
     __shared__ uint32_t bnd[kLists + 1];
@@ -872,6 +910,99 @@ __global__ __launch_bounds__(kScanT) void k_scan_layout(const uint32_t *wsum, ui
         __syncthreads();          // (the next tile overwrites tile and wtot)
     }
     if (t == 0) layout_from(bnd, n, error, cap, allow_column, lay, host_lay);
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_layout(const uint32_t *wsum, uint32_t *scan,
+                                                        uint64_t ws, uint64_t n, uint64_t nw,
+                                                        uint32_t *error, uint64_t cap,
+                                                        uint32_t allow_column, Layout *lay,
+                                                        Layout *host_lay) {
+    scan_layout(wsum, scan, ws, n, nw, error, cap, allow_column, lay, host_lay);
+}
+
+// the jobs path: one workgroup per job (grid = the jobs)
+__global__ __launch_bounds__(kScanT) void k_scan_layout_jobs(const StepK *ks) {
+    const StepK &a = ks[blockIdx.x];
+    scan_layout(a.wsum, const_cast<uint32_t *>(a.scan), a.ws, a.n, a.nw, a.error, a.out_cap,
+                a.allow_column, const_cast<Layout *>(a.layout), a.host_layout);
+}
+
+// The jobs path's scan of a sized stream's sizes (the single path: hipcub over PackSize), in
+// three launches for all jobs: each 1024 groups' packed total (k_size_sums), those totals
+// scanned per job by one workgroup (k_bsum_scan), each 1024 groups scanned in a workgroup from
+// its total's place (k_size_apply); prefix[i] = events before group i << 32 | bytes before it,
+// prefix[n] the totals (n + 1 elements, as the single path's scan)
+constexpr uint32_t kSizeTile = 1024;   // groups per workgroup of 256 threads (4 each)
+__device__ __forceinline__ uint64_t packed_size(const StepK &a, uint64_t i) {
+    const uint32_t s = i < a.n ? a.sizes[i] : 0;
+    return (uint64_t)(s & 0xFFFFu) << 32 | (s >> 16);
+}
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total) {
+    __shared__ uint64_t wt[1024 / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        x += lane >= d ? y : 0ull;
+    }
+    if (lane == 63) wt[wv] = x;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+    for (int w = 0; w < (int)(blockDim.x / 64); ++w) {
+        before += w < wv ? wt[w] : 0ull;
+        all += wt[w];
+    }
+    __syncthreads();              // (wt is reused by the next call)
+    *total = all;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_size_sums(const JobMap m) {
+    const uint32_t j = job_of(m, blockIdx.x);
+    const StepK &a = m.ks[m.job0 + j];
+    const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += packed_size(a, i0 + k);
+    uint64_t tot;
+    (void)block_excl_scan(v, &tot);
+    if (threadIdx.x == 0) a.bsum[b] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_bsum_scan(const JobMap m) {
+    const StepK &a = m.ks[m.job0 + blockIdx.x];
+    const uint64_t nb = (a.n + 1 + kSizeTile - 1) / kSizeTile;
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += 1024) {
+        const uint64_t k = base + threadIdx.x;
+        const uint64_t v = k < nb ? a.bsum[k] : 0;
+        uint64_t tot;
+        const uint64_t e = block_excl_scan(v, &tot);
+        if (k < nb) a.bsum[k] = carry + e;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_size_apply(const JobMap m) {
+    const uint32_t j = job_of(m, blockIdx.x);
+    const StepK &a = m.ks[m.job0 + j];
+    const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
+    uint64_t v[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = packed_size(a, i0 + k);
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = a.bsum[b] + block_excl_scan(sum, &tot);
+    uint64_t *prefix = const_cast<uint64_t *>(a.prefix);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (i0 + k <= a.n) prefix[i0 + k] = run;
+        run += v[k];
+    }
 }
 
 uint64_t now_ns() {
@@ -924,6 +1055,9 @@ struct hq_dstep {
     hipStream_t copy = nullptr;
     hipEvent_t ev_in[kMaxChunks] = {};
     hipEvent_t ev_sync = nullptr;  // blocking-sync event: a waiting worker thread sleeps
+    // the jobs path (hq_dstep_run_jobs, this engine first): the jobs' StepK, pinned and on device
+    StepK *jobs_host = nullptr, *jobs_dev = nullptr;
+    uint32_t jobs_cap = 0;
 };
 
 namespace {
@@ -1000,9 +1134,10 @@ void hq_dstep_close(hq_dstep *d) {
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp,
                     (void *)d->layout, (void *)d->groups_old, (void *)d->reads_old,
                     (void *)d->match_old, (void *)d->rerun, (void *)d->ready_slot,
-                    (void *)d->rerun_list, (void *)d->wsum})
+                    (void *)d->rerun_list, (void *)d->wsum, (void *)d->jobs_dev})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
+    if (d->jobs_host) (void)hipHostFree(d->jobs_host);
     if (d->host_layout) (void)hipHostFree(d->host_layout);
     if (d->copy) {
         (void)hipStreamSynchronize(d->copy);
@@ -1088,51 +1223,60 @@ int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t n
     return rc;
 }
 
-int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
+namespace {
+
+// One worker's step from its preparation to its outputs (hq_dstep_run; hq_dstep_run_jobs runs
+// several of them through shared launches)
+struct Run {
+    hq_dstep *d = nullptr;
+    const hq_dstep_in *in = nullptr;
+    hq_dstep_out *out = nullptr;
+    StepK k{};
+    uint64_t n = 0, ne = 0, nb = 0, nw = 0;
+    size_t ws = 0, tmp = 0, tmp2 = 0;
+    size_t o_off = 0, o_boff = 0, o_ev = 0;
+    int chunks = 1;
+    bool stream = false, sized = false, small = false, small_scan = false;
+    bool stepped = false, first = true;
+    uint64_t t0 = 0, t1 = 0;
+    int rc = HQ_OK;
+};
+
+// The step's buffers (grown as needed) and its StepK, with the memsets it needs queued on s; no
+// launch. in->n > 0.
+int prepare(Run &r, hipStream_t s) {
+    hq_dstep *d = r.d;
     hq_ctx *ctx = d->ctx;
-    const uint64_t n = in->n;
-    const bool stream = in->bytes != nullptr;
-    const bool sized = stream && in->sizes != nullptr;   // per-group sizes, scanned here
-    const uint64_t ne = !n ? 0 : sized ? in->n_events : in->offsets[n];
-    const uint64_t nb = !n || !stream ? 0 : sized ? in->n_bytes : in->boffsets[n];
-    *out = hq_dstep_out{};
-    if (n == 0) return HQ_OK;
+    const hq_dstep_in *in = r.in;
+    const uint64_t n = r.n = in->n;
+    r.stream = in->bytes != nullptr;
+    r.sized = r.stream && in->sizes != nullptr;   // per-group sizes, scanned here
+    const bool stream = r.stream, sized = r.sized;
+    const uint64_t ne = r.ne = sized ? in->n_events : in->offsets[n];
+    const uint64_t nb = r.nb = !stream ? 0 : sized ? in->n_bytes : in->boffsets[n];
     if (sized && (ne >> 32 || nb >> 32))     // the scanned prefixes pack both totals in 64 bits
         return hq::fail(ctx, HQ_E_INVAL, "hq_dstep: a sized step holds < 2^32 events and bytes");
-    const uint64_t t0 = now_ns();
+    r.t0 = now_ns();
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     // chunks of groups (at least 64 Ki each): chunk c's input copy overlaps pass A of chunk c - 1
-    int chunks = 1;
-    while (chunks * 2 <= kMaxChunks && n >= (uint64_t)chunks * 2 * kChunkGroups) chunks *= 2;
-    uint64_t bound[kMaxChunks + 1];
-    for (int c = 0; c <= chunks; ++c)   // (multiples of 64 inside: pass A's waves are the scan's)
-        bound[c] = c == chunks ? n : (n * c / chunks) & ~uint64_t(63);
+    while (r.chunks * 2 <= kMaxChunks && n >= (uint64_t)r.chunks * 2 * kChunkGroups) r.chunks *= 2;
     // the step's input in one device region: handles, offsets, [boffsets,] events or bytes, each
     // at the offsets it has on the host; a sized stream: handles, sizes (+ a zero), their scan,
     // bytes
     auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t o_off = up(n * 4);
-    const size_t o_boff = o_off + up((n + 1) * 8);
-    const size_t o_ev = o_boff + (stream ? up((n + 1) * 8) : 0);   // (sized: prefix at o_boff)
+    r.o_off = up(n * 4);
+    r.o_boff = r.o_off + up((n + 1) * 8);
+    r.o_ev = r.o_boff + (stream ? up((n + 1) * 8) : 0);   // (sized: prefix at o_boff)
     // + 8: slack for ByteReader's aligned word past the last byte
-    const size_t in_bytes = o_ev + (stream ? nb : ne * sizeof(hq_event)) + 8;
+    const size_t in_bytes = r.o_ev + (stream ? nb : ne * sizeof(hq_event)) + 8;
     if (!rc) rc = grow(ctx, &d->in, &d->in_cap, in_bytes, false, "hq_dstep input");
-    if (!rc && chunks > 1 && !d->copy)       // the copy stream of the first chunked step
-        rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
-                           "hq_dstep copy stream");
-    // one chunk: every copy on the compute stream (nothing to overlap, no cross-stream waits)
-    hipStream_t cs = chunks > 1 ? d->copy : ctx->stream;
     char *din = static_cast<char *>(d->in);
-    auto h2d = [&](size_t off, const void *src, size_t bytes, hipStream_t s = nullptr) {
-        if (!rc && bytes)
-            rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
-                                                   s ? s : cs), "hq_dstep H2D");
-    };
     // counts [kLists][n] and the prefixes pass B reads, [kLists][n]; the scan buffer holds the
     // per-wave sums [kLists][nw] + 1 (a zero: the scan's last element is the grand total) and
     // their scan (one size covers both)
-    const uint64_t nw = (n + 63) / 64;
-    const size_t ws = (size_t)kLists * nw + 1;
+    const uint64_t nw = r.nw = (n + 63) / 64;
+    const size_t ws = r.ws = (size_t)kLists * nw + 1;
+    r.small_scan = ws <= kScanSmall;
     const size_t cn = (size_t)2 * kLists * n + 2 * ws;
     size_t cc = d->cnt_cap * 4, sc = d->cnt_cap * 4, bc = d->cnt_cap ? 256 : 0;
     if (!rc && cn > d->cnt_cap) {
@@ -1140,7 +1284,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->scan), &sc, cn * 4, false, "hq_dstep scan");
         if (!rc && !d->bases) {
             rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 256, false, "hq_dstep error");
-            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 8, ctx->stream), "memset");
+            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 8, s), "memset");
         }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
     }
@@ -1169,37 +1313,45 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
                            "hq_dstep pinned output");
         if (!rc) d->host_out_cap = want;
     }
-    size_t tmp = 0, tmp2 = 0;
     const hipcub::TransformInputIterator<uint64_t, PackSize, hipcub::CountingInputIterator<uint64_t>>
         packed_sizes(hipcub::CountingInputIterator<uint64_t>(0),
-                     PackSize{reinterpret_cast<const uint32_t *>(din + o_off), n});
-    uint64_t *prefix = reinterpret_cast<uint64_t *>(din + o_boff);
+                     PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n});
+    uint64_t *prefix = reinterpret_cast<uint64_t *>(din + r.o_boff);
     uint32_t *wsum = d->wsum;
-    if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, wsum, d->scan,
-                                                                       ws, ctx->stream),
+    if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, r.tmp, wsum, d->scan,
+                                                                       ws, s),
                                 "hipcub scan size");
     if (!rc && sized)
-        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, packed_sizes,
-                                                                  prefix, n + 1, ctx->stream),
+        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, r.tmp2, packed_sizes,
+                                                                  prefix, n + 1, s),
                            "hipcub scan size");
-    if (!rc) rc = grow(ctx, &d->scan_tmp, &d->scan_tmp_cap, std::max(tmp, tmp2), false,
-                       "hq_dstep scan tmp");
+    // (the jobs path's per-1024-group size totals live there too)
+    const size_t bsum_bytes = sized ? (n + 1 + kSizeTile - 1) / kSizeTile * 8 : 0;
+    if (!rc) rc = grow(ctx, &d->scan_tmp, &d->scan_tmp_cap, std::max({r.tmp, r.tmp2, bsum_bytes}),
+                       false, "hq_dstep scan tmp");
     if (rc) return rc;
-    StepK k{};
+    StepK &k = r.k;
+    k = StepK{};
     k.groups = d->groups;
     k.members = d->members;
     k.reads = d->reads;
     k.n = n;
+    k.i_begin = 0;
+    k.i_end = n;
+    k.own_lo = 0;
+    k.own_hi = UINT64_MAX;
     k.handles = sized && !in->groups ? nullptr : reinterpret_cast<const uint32_t *>(din);
-    k.offsets = reinterpret_cast<const uint64_t *>(din + o_off);
+    k.offsets = reinterpret_cast<const uint64_t *>(din + r.o_off);
     if (sized) {
         k.prefix = prefix;
-        k.bytes = reinterpret_cast<const uint8_t *>(din + o_ev);
+        k.bytes = reinterpret_cast<const uint8_t *>(din + r.o_ev);
+        k.sizes = reinterpret_cast<const uint32_t *>(din + r.o_off);
+        k.bsum = static_cast<uint64_t *>(d->scan_tmp);
     } else if (stream) {
-        k.boffsets = reinterpret_cast<const uint64_t *>(din + o_boff);
-        k.bytes = reinterpret_cast<const uint8_t *>(din + o_ev);
+        k.boffsets = reinterpret_cast<const uint64_t *>(din + r.o_boff);
+        k.bytes = reinterpret_cast<const uint8_t *>(din + r.o_ev);
     } else {
-        k.events = reinterpret_cast<const hq_event *>(din + o_ev);
+        k.events = reinterpret_cast<const hq_event *>(din + r.o_ev);
     }
     k.counts = d->counts;
     k.pre = d->counts + (size_t)kLists * n;
@@ -1212,7 +1364,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.n_bytes = nb;
     k.stamp = d->stamp;
     if (++d->step_no == 0) {      // stamps wrap: forget them
-        rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp, 0, d->gcap * 4, ctx->stream), "memset");
+        rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp, 0, d->gcap * 4, s), "memset");
         d->step_no = 1;
         if (rc) return rc;
     }
@@ -1220,7 +1372,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     // pass A adds each wave's counts into wsum, which k_step_lite leaves zero; a step that
     // stopped before it (or a new buffer) leaves it to clear here
     if (d->wsum_dirty) {
-        rc = hq::check_hip(ctx, hipMemsetAsync(wsum, 0, d->wsum_cap, ctx->stream), "memset");
+        rc = hq::check_hip(ctx, hipMemsetAsync(wsum, 0, d->wsum_cap, s), "memset");
         if (rc) return rc;
     }
     d->wsum_dirty = true;
@@ -1238,129 +1390,92 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     k.rerun = d->rerun;
     k.rerun_list = d->rerun_list;
     k.ready_slot = d->ready_slot;
-    const bool small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
-    auto launch = [&](bool write, uint64_t i0, uint64_t i1) {
-        k.i_begin = i0;
-        k.i_end = i1;
-        const dim3 grid((unsigned)((i1 - i0 + 255) / 256)), blk(256);
-        if (rc || i1 == i0) return;
-        rc = hq::pre_launch(ctx);
-        if (rc) return;
+    k.out_cap = d->host_out_cap;
+    k.allow_column = d->commit_column;
+    k.host_layout = d->host_layout;
+    r.small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
+    return HQ_OK;
+}
+
+// one pass over groups [i0, i1) of the step on its worker's stream
+void launch_pass(Run &r, bool write, uint64_t i0, uint64_t i1) {
+    hq_ctx *ctx = r.d->ctx;
+    StepK &k = r.k;
+    k.i_begin = i0;
+    k.i_end = i1;
+    const dim3 grid((unsigned)((i1 - i0 + 255) / 256)), blk(256);
+    if (r.rc || i1 == i0) return;
+    r.rc = hq::pre_launch(ctx);
+    if (r.rc) return;
+    const bool stream = r.stream, small = r.small;
 #define HQ_STEP_LAUNCH(W)                                                                        \
-        if (stream && small) hipLaunchKernelGGL((k_step<W, true, 8>), grid, blk, 0, ctx->stream, k); \
-        else if (stream) hipLaunchKernelGGL((k_step<W, true, kDMembers>), grid, blk, 0, ctx->stream, k); \
-        else if (small) hipLaunchKernelGGL((k_step<W, false, 8>), grid, blk, 0, ctx->stream, k); \
-        else hipLaunchKernelGGL((k_step<W, false, kDMembers>), grid, blk, 0, ctx->stream, k);
-        if (write) {
-            HQ_STEP_LAUNCH(true)
-        } else {
-            HQ_STEP_LAUNCH(false)
-        }
+    if (stream && small) hipLaunchKernelGGL((k_step<W, true, 8>), grid, blk, 0, ctx->stream, k); \
+    else if (stream) hipLaunchKernelGGL((k_step<W, true, kDMembers>), grid, blk, 0, ctx->stream, k); \
+    else if (small) hipLaunchKernelGGL((k_step<W, false, 8>), grid, blk, 0, ctx->stream, k); \
+    else hipLaunchKernelGGL((k_step<W, false, kDMembers>), grid, blk, 0, ctx->stream, k);
+    if (write) {
+        HQ_STEP_LAUNCH(true)
+    } else {
+        HQ_STEP_LAUNCH(false)
+    }
 #undef HQ_STEP_LAUNCH
-        rc = hq::post_launch(ctx, write ? "k_step<write>" : "k_step<count>");
-    };
-    if (sized) {
-        // handles and sizes, their scan (PackSize adds the totals as element n); then
-        // the bytes in equal byte chunks, each followed by pass A over the groups whose bytes end
-        // inside what has landed
-        // every copy is queued before the first launch, event c behind chunk c's bytes; the
-        // handles and sizes go on the compute stream ahead of their scan, the bytes on the copy
-        // stream beside them (behind the sizes on one stream the first bytes copy started
-        // 50-65 us after the sizes' copy ended)
-        if (in->groups) h2d(0, in->groups, n * 4, ctx->stream);   // NULL: handles 0 .. n - 1
-        h2d(o_off, in->sizes, n * 4, ctx->stream);
-        for (int c = 0; c < chunks && !rc; ++c) {
-            const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
-            h2d(o_ev + lo, in->bytes + lo, hi - lo);
-            if (chunks > 1 && !rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
-        }
-        if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(
-                                              d->scan_tmp, tmp2, packed_sizes, prefix, n + 1,
-                                              ctx->stream),
-                                    "hipcub scan");
-        for (int c = 0; c < chunks && !rc; ++c) {
-            const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
-            if (chunks > 1)
-                rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
-            k.own_lo = c == 0 ? 0 : lo + 1;
-            k.own_hi = c + 1 == chunks ? UINT64_MAX : hi + 1;
-            launch(false, 0, n);
-        }
+    r.rc = hq::post_launch(ctx, write ? "k_step<write>" : "k_step<count>");
+}
+
+// layout, pass B (straight into the pinned region), the layout back: one wait per step. The
+// first layout of a small step scans the wave sums in one workgroup; a re-run after an overflow
+// (or a step whose sums hipcub scanned) takes k_layout: k_step_lite has cleared the sums
+void pass_b(Run &r) {
+    hq_dstep *d = r.d;
+    hq_ctx *ctx = d->ctx;
+    StepK &k = r.k;
+    if (!r.rc && r.small_scan && r.first) {
+        hipLaunchKernelGGL(k_scan_layout, dim3(1), dim3(kScanT), 0, ctx->stream, d->wsum, d->scan,
+                           (uint64_t)r.ws, r.n, r.nw, k.error, (uint64_t)d->host_out_cap,
+                           (uint32_t)d->commit_column, d->layout, d->host_layout);
+        r.rc = hq::check_hip(ctx, hipGetLastError(), "k_scan_layout");
+    } else if (!r.rc) {
+        hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, r.n, r.nw, k.error,
+                           (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout,
+                           d->host_layout);
+        r.rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
     }
-    // inputs chunk by chunk, pass A of each chunk once it has landed
-    for (int c = 0; c < chunks && !rc && !sized; ++c) {
-        const uint64_t i0 = bound[c], i1 = bound[c + 1];
-        h2d(i0 * 4, in->groups + i0, (i1 - i0) * 4);
-        h2d(o_off + i0 * 8, in->offsets + i0, (i1 - i0 + 1) * 8);
-        if (stream) {
-            h2d(o_boff + i0 * 8, in->boffsets + i0, (i1 - i0 + 1) * 8);
-            // the chunk's bytes (garbage offsets are the kernel's to reject: clamp the copy)
-            const uint64_t lo = std::min(in->boffsets[i0], nb);
-            const uint64_t hi = std::min(std::max(in->boffsets[i1], lo), nb);
-            h2d(o_ev + lo, in->bytes + lo, hi - lo);
-        } else {
-            const uint64_t lo = std::min(in->offsets[i0], ne);
-            const uint64_t hi = std::min(std::max(in->offsets[i1], lo), ne);
-            h2d(o_ev + lo * sizeof(hq_event), in->events + lo, (hi - lo) * sizeof(hq_event));
-        }
-        if (chunks > 1) {
-            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
-            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
-        }
-        launch(false, i0, i1);
+    r.first = false;
+    const dim3 grid((unsigned)((r.n + 255) / 256)), blk(256);
+    if (!r.rc) {
+        hipLaunchKernelGGL(k_step_lite, grid, blk, 0, ctx->stream, k);
+        r.rc = hq::check_hip(ctx, hipGetLastError(), "k_step_lite");
+        if (!r.rc) d->wsum_dirty = false;
     }
-    // the wave sums' scan and the layout: one workgroup for a small step, else hipcub's scan and
-    // k_layout (a re-run after an overflow takes k_layout: k_step_lite has cleared the sums)
-    const bool small_scan = ws <= kScanSmall;
-    if (!rc && !small_scan)
-        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, tmp, wsum, d->scan,
-                                                                  ws, ctx->stream),
-                           "hipcub scan");
-    // layout, pass B (straight into the pinned region), the layout back: one wait per step
-    bool first = true;
-    auto pass_b = [&]() {
-        if (!rc && small_scan && first) {
-            hipLaunchKernelGGL(k_scan_layout, dim3(1), dim3(kScanT), 0, ctx->stream, wsum, d->scan,
-                               (uint64_t)ws, n, nw, k.error, (uint64_t)d->host_out_cap,
-                               (uint32_t)d->commit_column, d->layout, d->host_layout);
-            rc = hq::check_hip(ctx, hipGetLastError(), "k_scan_layout");
-        } else if (!rc) {
-            hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, n, nw, k.error,
-                               (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout,
-                               d->host_layout);
-            rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
-        }
-        first = false;
-        const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
-        if (!rc) {
-            hipLaunchKernelGGL(k_step_lite, grid, blk, 0, ctx->stream, k);
-            rc = hq::check_hip(ctx, hipGetLastError(), "k_step_lite");
-            if (!rc) d->wsum_dirty = false;
-        }
-        launch(true, 0, n);
-        if (!rc) rc = wait_stream(d, ctx->stream, "hq_dstep sync");
-    };
-    // Pass A has written every listed group's new state in place (the state it found is saved).
-    // From here on a step that fails returns with that state taken back (k_step_restore), so a
-    // failed step leaves the groups as they were, whatever failed: an input error found by the
-    // kernels, a HIP error, the output region that could not grow, a second layout failure. (A
-    // pass A launch that itself fails leaves rc set before this point; the context is then
-    // unusable and the caller reloads the groups from the device, hq_worker.cpp.)
-    const bool stepped = !rc;
-    auto restore = [&](int code) {
-        if (!stepped) return code;
-        hipLaunchKernelGGL(k_step_restore, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                           ctx->stream, k);
-        int r2 = hq::check_hip(ctx, hipGetLastError(), "k_step_restore");
-        if (!r2) r2 = wait_stream(d, ctx->stream, "hq_dstep restore");
-        return code ? code : r2;
-    };
-    pass_b();
-    const uint64_t t1 = now_ns();
-    if (rc) return restore(rc);
+    launch_pass(r, true, 0, r.n);
+    if (!r.rc) r.rc = wait_stream(d, ctx->stream, "hq_dstep sync");
+}
+
+// Pass A has written every listed group's new state in place (the state it found is saved).
+// From there on a step that fails returns with that state taken back (k_step_restore), so a
+// failed step leaves the groups as they were, whatever failed: an input error found by the
+// kernels, a HIP error, the output region that could not grow, a second layout failure. (A
+// pass A launch that itself fails leaves rc set before that point; the context is then
+// unusable and the caller reloads the groups from the device, hq_worker.cpp.)
+int restore(Run &r, int code) {
+    if (!r.stepped) return code;
+    hq_ctx *ctx = r.d->ctx;
+    hipLaunchKernelGGL(k_step_restore, dim3((unsigned)((r.n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, r.k);
+    int r2 = hq::check_hip(ctx, hipGetLastError(), "k_step_restore");
+    if (!r2) r2 = wait_stream(r.d, ctx->stream, "hq_dstep restore");
+    return code ? code : r2;
+}
+
+// after the first pass B and its wait: input errors, an output region too small, the outputs
+int finish(Run &r) {
+    hq_dstep *d = r.d;
+    hq_ctx *ctx = d->ctx;
+    hq_dstep_out *out = r.out;
+    if (r.rc) return restore(r, r.rc);
     const Layout &lay = *d->host_layout;
     if (lay.error) {              // no group state is written: pass A's is taken back
-        rc = restore(HQ_OK);
+        const int rc = restore(r, HQ_OK);
         if (rc) return rc;
         out->input_error = lay.error;
         return HQ_E_INVAL;
@@ -1369,23 +1484,24 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         // the new region first: if it cannot be had, the old one stays and the step is undone
         const size_t want = lay.total + lay.total / 2;
         void *grown = nullptr;
-        rc = hq::check_hip(ctx, hipHostMalloc(&grown, want, hipHostMallocDefault),
-                           "hq_dstep pinned output");
+        int rc = hq::check_hip(ctx, hipHostMalloc(&grown, want, hipHostMallocDefault),
+                               "hq_dstep pinned output");
         if (d->test_fail_regrow) {   // tests: the allocation failure path
             if (grown) (void)hipHostFree(grown);
             grown = nullptr;
             rc = hq::fail(ctx, HQ_E_NOMEM, "hq_dstep pinned output: injected failure");
         }
-        if (rc) return restore(rc);
+        if (rc) return restore(r, rc);
         if (d->host_out) (void)hipHostFree(d->host_out);
         d->host_out = grown;
         d->host_out_cap = want;
-        k.out = static_cast<char *>(d->host_out);
-        k.spec_valid = 0;         // pass A's advance words went with the old region
-        pass_b();
-        if (rc) return restore(rc);
+        r.k.out = static_cast<char *>(d->host_out);
+        r.k.out_cap = want;
+        r.k.spec_valid = 0;       // pass A's advance words went with the old region
+        pass_b(r);
+        if (r.rc) return restore(r, r.rc);
         if (lay.overflow || lay.error)
-            return restore(hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout"));
+            return restore(r, hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout"));
     }
     const char *ho = static_cast<const char *>(d->host_out);
     out->commits = lay.commit_column ? nullptr
@@ -1408,7 +1524,267 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     out->n_deferred = lay.len[kDeferred];
     out->n_fallback = lay.len[kFallback];
     out->decisions = lay.len[kDecisions];
-    out->kernel_ns = t1 - t0;
-    out->d2h_ns = now_ns() - t1;
+    out->kernel_ns = r.t1 - r.t0;
+    out->d2h_ns = now_ns() - r.t1;
     return HQ_OK;
+}
+
+}  // namespace
+
+int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
+    *out = hq_dstep_out{};
+    if (in->n == 0) return HQ_OK;
+    Run r;
+    r.d = d;
+    r.in = in;
+    r.out = out;
+    hq_ctx *ctx = d->ctx;
+    int rc = prepare(r, ctx->stream);
+    if (rc) return rc;
+    const uint64_t n = r.n, ne = r.ne, nb = r.nb;
+    const bool stream = r.stream, sized = r.sized;
+    const int chunks = r.chunks;
+    uint64_t bound[kMaxChunks + 1];
+    for (int c = 0; c <= chunks; ++c)   // (multiples of 64 inside: pass A's waves are the scan's)
+        bound[c] = c == chunks ? n : (n * c / chunks) & ~uint64_t(63);
+    if (chunks > 1 && !d->copy)       // the copy stream of the first chunked step
+        rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
+                           "hq_dstep copy stream");
+    // one chunk: every copy on the compute stream (nothing to overlap, no cross-stream waits)
+    hipStream_t cs = chunks > 1 ? d->copy : ctx->stream;
+    char *din = static_cast<char *>(d->in);
+    auto h2d = [&](size_t off, const void *src, size_t bytes, hipStream_t s = nullptr) {
+        if (!rc && bytes)
+            rc = hq::check_hip(ctx, hipMemcpyAsync(din + off, src, bytes, hipMemcpyHostToDevice,
+                                                   s ? s : cs), "hq_dstep H2D");
+    };
+    if (sized) {
+        // handles and sizes, their scan (PackSize adds the totals as element n); then
+        // the bytes in equal byte chunks, each followed by pass A over the groups whose bytes end
+        // inside what has landed
+        // every copy is queued before the first launch, event c behind chunk c's bytes; the
+        // handles and sizes go on the compute stream ahead of their scan, the bytes on the copy
+        // stream beside them (behind the sizes on one stream the first bytes copy started
+        // 50-65 us after the sizes' copy ended)
+        if (in->groups) h2d(0, in->groups, n * 4, ctx->stream);   // NULL: handles 0 .. n - 1
+        h2d(r.o_off, in->sizes, n * 4, ctx->stream);
+        for (int c = 0; c < chunks && !rc; ++c) {
+            const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
+            h2d(r.o_ev + lo, in->bytes + lo, hi - lo);
+            if (chunks > 1 && !rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
+        }
+        const hipcub::TransformInputIterator<uint64_t, PackSize,
+                                             hipcub::CountingInputIterator<uint64_t>>
+            packed_sizes(hipcub::CountingInputIterator<uint64_t>(0),
+                         PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n});
+        if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(
+                                              d->scan_tmp, r.tmp2, packed_sizes,
+                                              const_cast<uint64_t *>(r.k.prefix), n + 1,
+                                              ctx->stream),
+                                    "hipcub scan");
+        r.rc = rc;
+        for (int c = 0; c < chunks && !r.rc; ++c) {
+            const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
+            if (chunks > 1)
+                r.rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
+            r.k.own_lo = c == 0 ? 0 : lo + 1;
+            r.k.own_hi = c + 1 == chunks ? UINT64_MAX : hi + 1;
+            launch_pass(r, false, 0, n);
+        }
+        rc = r.rc;
+    }
+    // inputs chunk by chunk, pass A of each chunk once it has landed
+    for (int c = 0; c < chunks && !rc && !sized; ++c) {
+        const uint64_t i0 = bound[c], i1 = bound[c + 1];
+        h2d(i0 * 4, in->groups + i0, (i1 - i0) * 4);
+        h2d(r.o_off + i0 * 8, in->offsets + i0, (i1 - i0 + 1) * 8);
+        if (stream) {
+            h2d(r.o_boff + i0 * 8, in->boffsets + i0, (i1 - i0 + 1) * 8);
+            // the chunk's bytes (garbage offsets are the kernel's to reject: clamp the copy)
+            const uint64_t lo = std::min(in->boffsets[i0], nb);
+            const uint64_t hi = std::min(std::max(in->boffsets[i1], lo), nb);
+            h2d(r.o_ev + lo, in->bytes + lo, hi - lo);
+        } else {
+            const uint64_t lo = std::min(in->offsets[i0], ne);
+            const uint64_t hi = std::min(std::max(in->offsets[i1], lo), ne);
+            h2d(r.o_ev + lo * sizeof(hq_event), in->events + lo, (hi - lo) * sizeof(hq_event));
+        }
+        if (chunks > 1) {
+            if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_in[c], cs), "event");
+            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
+        }
+        r.rc = rc;
+        launch_pass(r, false, i0, i1);
+        rc = r.rc;
+    }
+    r.k.own_lo = 0;
+    r.k.own_hi = UINT64_MAX;
+    // the wave sums' scan (hipcub for a large step; a small one's is the layout's workgroup)
+    if (!rc && !r.small_scan)
+        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, r.tmp, d->wsum,
+                                                                  d->scan, r.ws, ctx->stream),
+                           "hipcub scan");
+    r.rc = rc;
+    r.stepped = !rc;
+    pass_b(r);
+    r.t1 = now_ns();
+    return finish(r);
+}
+
+int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out *outs, int *rcs,
+                      uint32_t count) {
+    if (count == 0) return HQ_OK;
+    if (count > kMaxJobs) return HQ_E_INVAL;
+    hq_dstep *d0 = ds[0];
+    hq_ctx *ctx = d0->ctx;
+    hipStream_t s = ctx->stream;
+    int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    Run runs[kMaxJobs];
+    uint32_t live[kMaxJobs], nl = 0;
+    for (uint32_t j = 0; j < count; ++j) {
+        outs[j] = hq_dstep_out{};
+        rcs[j] = HQ_OK;
+        if (ds[j]->ctx->device != ctx->device || !ins[j].sizes || !ins[j].bytes) {
+            rcs[j] = hq::fail(ds[j]->ctx, HQ_E_INVAL, "hq_dstep_run_jobs: a sized stream step "
+                                                      "on the first job's device");
+            continue;
+        }
+        if (rc || ins[j].n == 0) {
+            rcs[j] = rc;
+            continue;
+        }
+        Run &r = runs[j];
+        r.d = ds[j];
+        r.in = &ins[j];
+        r.out = &outs[j];
+        rcs[j] = prepare(r, s);
+        if (!rcs[j]) live[nl++] = j;
+    }
+    if (!nl) return rc;
+    // the jobs' StepK, pinned and copied to the device ahead of the launches
+    if (!rc && nl > d0->jobs_cap) {
+        if (d0->jobs_host) (void)hipHostFree(d0->jobs_host);
+        if (d0->jobs_dev) (void)hipFree(d0->jobs_dev);
+        d0->jobs_host = d0->jobs_dev = nullptr;
+        d0->jobs_cap = 0;
+        rc = hq::check_hip(ctx, hipHostMalloc(&d0->jobs_host, kMaxJobs * sizeof(StepK),
+                                              hipHostMallocDefault), "hq_dstep jobs");
+        if (!rc) rc = hq::check_hip(ctx, hipMalloc(&d0->jobs_dev, kMaxJobs * sizeof(StepK)),
+                                    "hq_dstep jobs");
+        if (!rc) d0->jobs_cap = kMaxJobs;
+    }
+    bool small = true;
+    uint64_t total_bytes = 0;
+    for (uint32_t x = 0; x < nl && !rc; ++x) {
+        const Run &r = runs[live[x]];
+        d0->jobs_host[x] = r.k;
+        small = small && r.small;
+        total_bytes += r.nb;
+    }
+    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
+                                                    hipMemcpyHostToDevice, s), "hq_dstep jobs");
+    // maps of jobs [x0, x1) onto workgroups of `per` groups (+ extra elements per job)
+    auto map = [&](uint32_t x0, uint32_t x1, uint64_t per, uint64_t extra) {
+        JobMap m{};
+        m.ks = d0->jobs_dev;
+        m.job0 = x0;
+        m.count = x1 - x0;
+        m.blk0[0] = 0;
+        for (uint32_t x = x0; x < x1; ++x)
+            m.blk0[x - x0 + 1] = m.blk0[x - x0] + (uint32_t)((runs[live[x]].n + extra + per - 1) / per);
+        return m;
+    };
+    auto launched = [&](const char *what) {
+        if (!rc) rc = hq::check_hip(ctx, hipGetLastError(), what);
+    };
+    auto h2d = [&](void *dst, const void *src, size_t bytes, hipStream_t st) {
+        if (!rc && bytes)
+            rc = hq::check_hip(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st),
+                               "hq_dstep H2D");
+    };
+    // handles and sizes on the compute stream, their scan; the bytes on the copy stream in up to
+    // kMaxChunks chunks of whole jobs, pass A of each chunk once its bytes have landed
+    for (uint32_t x = 0; x < nl; ++x) {
+        const Run &r = runs[live[x]];
+        char *din = static_cast<char *>(r.d->in);
+        if (r.in->groups) h2d(din, r.in->groups, r.n * 4, s);
+        h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
+    }
+    const JobMap sm = map(0, nl, kSizeTile, 1);
+    if (!rc) {
+        hipLaunchKernelGGL(k_size_sums, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
+        launched("k_size_sums");
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(k_bsum_scan, dim3(nl), dim3(1024), 0, s, sm);
+        launched("k_bsum_scan");
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(k_size_apply, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
+        launched("k_size_apply");
+    }
+    if (!rc && !d0->copy)
+        rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d0->copy, hipStreamNonBlocking),
+                           "hq_dstep copy stream");
+    uint32_t x0 = 0;
+    for (int c = 0; c < kMaxChunks && x0 < nl && !rc; ++c) {
+        // the chunk: jobs until its share of the bytes (the last chunk takes the rest)
+        uint32_t x1 = x0;
+        uint64_t acc = 0;
+        for (uint32_t x = 0; x < x0; ++x) acc += runs[live[x]].nb;
+        const uint64_t want = total_bytes * (uint64_t)(c + 1) / kMaxChunks;
+        do {
+            acc += runs[live[x1]].nb;
+            ++x1;
+        } while (x1 < nl && (c + 1 == kMaxChunks || acc < want));
+        for (uint32_t x = x0; x < x1; ++x) {
+            const Run &r = runs[live[x]];
+            h2d(static_cast<char *>(r.d->in) + r.o_ev, r.in->bytes, r.nb, d0->copy);
+        }
+        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in[c], d0->copy), "event");
+        if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(s, d0->ev_in[c], 0), "wait");
+        const JobMap m = map(x0, x1, 256, 0);
+        if (!rc) rc = hq::pre_launch(ctx);
+        if (!rc) {
+            if (small) hipLaunchKernelGGL((k_step_jobs<false, true, 8>), dim3(m.blk0[x1 - x0]),
+                                          dim3(256), 0, s, m);
+            else hipLaunchKernelGGL((k_step_jobs<false, true, kDMembers>), dim3(m.blk0[x1 - x0]),
+                                    dim3(256), 0, s, m);
+            rc = hq::post_launch(ctx, "k_step_jobs<count>");
+            for (uint32_t x = x0; x < x1 && !rc; ++x) runs[live[x]].stepped = true;
+        }
+        x0 = x1;
+    }
+    // every job's layout (one workgroup each), k_step_lite and pass B over all jobs, one wait
+    const JobMap am = map(0, nl, 256, 0);
+    if (!rc) {
+        hipLaunchKernelGGL(k_scan_layout_jobs, dim3(nl), dim3(kScanT), 0, s, d0->jobs_dev);
+        launched("k_scan_layout_jobs");
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(k_step_lite_jobs, dim3(am.blk0[nl]), dim3(256), 0, s, am);
+        launched("k_step_lite_jobs");
+        for (uint32_t x = 0; x < nl && !rc; ++x) runs[live[x]].d->wsum_dirty = false;
+    }
+    if (!rc) rc = hq::pre_launch(ctx);
+    if (!rc) {
+        if (small) hipLaunchKernelGGL((k_step_jobs<true, true, 8>), dim3(am.blk0[nl]), dim3(256),
+                                      0, s, am);
+        else hipLaunchKernelGGL((k_step_jobs<true, true, kDMembers>), dim3(am.blk0[nl]),
+                                dim3(256), 0, s, am);
+        rc = hq::post_launch(ctx, "k_step_jobs<write>");
+    }
+    if (!rc) rc = wait_stream(d0, s, "hq_dstep jobs sync");
+    else (void)hipStreamSynchronize(s);
+    const uint64_t t1 = now_ns();
+    int first_rc = HQ_OK;
+    for (uint32_t x = 0; x < nl; ++x) {
+        Run &r = runs[live[x]];
+        r.rc = rc;                // (restore: only the jobs whose pass A was launched)
+        r.first = false;
+        r.t1 = t1;
+        rcs[live[x]] = finish(r);
+        if (rcs[live[x]] && !first_rc) first_rc = rcs[live[x]];
+    }
+    return first_rc;
 }

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/hipquorum.h"
+#include "hq_dstep.h"
 
 namespace {
 
@@ -95,5 +96,7 @@ extern "C" int hq_worker_step_jobs(hq_step_job *jobs, uint32_t count) {
             if (jobs[k].worker == jobs[i].worker) return HQ_E_INVAL;
     }
     if (count == 1) return run_job(jobs[0]);
+    const int f = hq_worker_step_jobs_fused(jobs, count);
+    if (f != kJobsNotFused) return f;
     return pool().run(jobs, count);
 }

@@ -18,6 +18,7 @@
 // ReadIndex queues in a pool of fixed 8-entry blocks.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -91,6 +92,7 @@ bool is_response_type(uint32_t t) {       // isResponseMessageType (internal/raf
 
 struct hq_worker {
     hq_ctx *ctx = nullptr;
+    int device = -1;
     uint32_t n_max = 0;
     // HQ_WORKER_ON_DEVICE: the group state lives on the GPU (hq_dstep.hip) and a step is one
     // launch pair; the host records below are a mirror, refreshed from the device on demand
@@ -163,6 +165,8 @@ struct hq_worker {
     int sync_to_device();
     int sync_from_device();
     int step_on_device(const hq_dstep_in &in, hq_step_output *out);
+    int device_step_done(int rc, const hq_dstep_in &in, hq_step_output *out, uint64_t t0,
+                         uint64_t t1);
     int load_group(Group &g, const hq_worker_group *src, const hq_member *m, bool fresh);
     int step(const hq_step_input *in, hq_step_output *out);
     Verdict handle(Group &g, const hq_event &e, uint64_t ei);
@@ -879,6 +883,12 @@ int hq_worker::step_on_device(const hq_dstep_in &inp, hq_step_output *out) {
     const uint64_t t1 = now_ns();
     host_stale = true;
     rc = hq_dstep_run(dstep, &inp, &dout);
+    return device_step_done(rc, inp, out, t0, t1);
+}
+
+// the outputs of a device step (hq_dstep_run or hq_dstep_run_jobs) in the worker's terms
+int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *out, uint64_t t0,
+                                uint64_t t1) {
     if (rc == HQ_E_INVAL && dout.input_error) {
         const uint32_t e = dout.input_error;
         return fail(HQ_E_INVAL, e & 1 ? "hq_worker_step: unknown group handle"
@@ -938,6 +948,7 @@ int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **ou
         return rc;   // message: hq_last_error(NULL)
     }
     w->n_max = n_max;
+    w->device = device;
     if (flags & HQ_WORKER_ON_DEVICE) {
         rc = hq_dstep_open(w->ctx, &w->dstep,
                            ((flags & HQ_WORKER_COMMIT_COLUMN) ? 1u : 0u) |
@@ -1086,6 +1097,65 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
                                              nullptr, nullptr}, out);
     return w->step(in, out);
 }
+
+}  // extern "C"
+
+// hq_worker_step_jobs (hq_jobs.cpp): jobs that are all sized event streams for distinct device
+// workers on one GPU are stepped through shared launches (hq_dstep_run_jobs: one pass A per
+// input chunk, one layout, one k_step_lite and one pass B for all of them, one wait) instead of
+// one launch sequence per worker on its own thread. Returns kJobsNotFused, having done nothing,
+// for any other set of jobs; else the first job's failure (each job's in its rc).
+int hq_worker_step_jobs_fused(hq_step_job *jobs, uint32_t count) {
+    if (count < 2 || count > kDStepMaxJobs) return kJobsNotFused;
+    if (const char *v = std::getenv("HQ_STEP_JOBS_FUSED"))
+        if (std::atoi(v) == 0) return kJobsNotFused;
+    int device = -1;
+    for (uint32_t j = 0; j < count; ++j) {
+        const hq_step_job &b = jobs[j];
+        const hq_step_stream *in = b.stream;
+        if (!b.worker || !b.worker->dstep || !b.out || b.rows || !in || !in->sizes ||
+            (in->n_bytes && !in->bytes) || in->n_groups == 0)
+            return kJobsNotFused;
+        if (device >= 0 && b.worker->device != device) return kJobsNotFused;
+        device = b.worker->device;
+    }
+    static const uint8_t none = 0;
+    hq_dstep *ds[kDStepMaxJobs];
+    hq_dstep_in ins[kDStepMaxJobs];
+    hq_dstep_out outs[kDStepMaxJobs];
+    int rcs[kDStepMaxJobs];
+    uint32_t idx[kDStepMaxJobs], nl = 0;
+    const uint64_t t0 = now_ns();
+    for (uint32_t j = 0; j < count; ++j) {
+        hq_worker *w = jobs[j].worker;
+        const hq_step_stream *in = jobs[j].stream;
+        std::memset(jobs[j].out, 0, sizeof *jobs[j].out);
+        jobs[j].rc = w->sync_to_device();
+        if (jobs[j].rc) continue;
+        w->host_stale = true;
+        hq_dstep_in d{in->n_groups, in->groups, nullptr, nullptr, nullptr,
+                      in->bytes ? in->bytes : &none};
+        d.sizes = in->sizes;
+        d.n_events = in->n_events;
+        d.n_bytes = in->n_bytes;
+        ds[nl] = w->dstep;
+        ins[nl] = d;
+        idx[nl++] = j;
+    }
+    const uint64_t t1 = now_ns();
+    if (nl) (void)hq_dstep_run_jobs(ds, ins, outs, rcs, nl);
+    int first = HQ_OK;
+    for (uint32_t x = 0; x < nl; ++x) {
+        hq_step_job &b = jobs[idx[x]];
+        b.worker->dout = outs[x];
+        b.rc = b.worker->device_step_done(rcs[x], ins[x], b.out, t0, t1);
+    }
+    for (uint32_t j = 0; j < count; ++j)
+        if (jobs[j].rc && !first) first = jobs[j].rc;
+    return first;
+}
+
+extern "C" {
 
 int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output *out) {
     if (!w) return HQ_E_INVAL;

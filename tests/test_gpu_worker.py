@@ -435,6 +435,79 @@ def test_step_jobs_equal_sequential_steps(hq):
             w.close()
 
 
+@pytest.mark.parametrize("wide", [False, True], ids=["8-member-slots", "16-member-slots"])
+def test_fused_step_jobs_equal_single_steps(hq, wide):
+    """hq_worker_step_jobs over device workers that all take sized streams on one GPU steps them
+    through shared launches (hq_dstep_run_jobs: one pass A per input chunk, one layout, one
+    k_step_lite, one pass B). Every job's lists and its workers' state equal the same worker
+    stepped alone (its own launch sequence): ragged sizes (1, 63, 64, 4097 groups ...), implicit
+    handles, the list / column / advance forms of the commits, a job whose output region
+    overflows and is regrown, and a job with an input error (failed alone, state untouched)."""
+    import bench
+
+    sizes_g = [3000, 1, 64, 4097, 20000, 63, 700]
+    wide_roles = ("remote",) * 3 + ("observer",) * 7          # 10 members: 16 slots
+    specs = []
+    for i, G in enumerate(sizes_g):
+        roles = wide_roles if wide and i == 3 else bench.STEP_ROLES["step5" if i % 2 else "step"]
+        specs.append((G, roles, dict(commit_column=i % 3 == 1, commit_advance=i % 3 == 2),
+                      i in (1, 4)))                            # implicit handles
+    def make():
+        ws = []
+        for G, roles, flags, _ in specs:
+            g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
+            w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True, **flags)
+            w.add_groups(g, m)
+            ws.append(w)
+        return ws
+
+    def compare(got, want, what):
+        assert set(k for k in want if isinstance(want[k], np.ndarray)) == \
+            set(k for k in got if isinstance(got[k], np.ndarray)), what
+        for k, v in want.items():
+            if isinstance(v, np.ndarray):
+                np.testing.assert_array_equal(got[k], v, err_msg=f"{what} {k}")
+        assert got.get("n_commits") == want.get("n_commits"), what
+
+    a, b = make(), make()
+    empty = np.zeros(0, np.uint8)
+    try:
+        # step 0 lists one group with no events: every output region starts at its 64 KB minimum
+        jobs = [hq.SizedStream(np.zeros(1, np.uint32), np.zeros(1, np.uint32), 0, empty)
+                for _ in specs]
+        for i, (res, w) in enumerate(zip(hq.step_jobs(list(zip(a, jobs))), b)):
+            compare(res, w.step_sized(*jobs[i]), f"step 0 job {i}")
+        for s in range(3):
+            jobs = []
+            for G, roles, _, implicit in specs:
+                grp, off, ev = bench.step_events(hq, G, s, roles)
+                data, sz = hq.encode_events_sized(off, ev)
+                jobs.append(hq.SizedStream(None if implicit else grp, sz, len(ev), data))
+            got = hq.step_jobs(list(zip(a, jobs)))          # (the 20000-group job overflows at s 0)
+            for i, (res, w) in enumerate(zip(got, b)):
+                compare(res, w.step_sized(*jobs[i]), f"step {s + 1} job {i}")
+        # a job listing a group twice fails alone; the others step
+        G, roles, _, _ = specs[2]
+        grp, off, ev = bench.step_events(hq, G, 3, roles)
+        data, sz = hq.encode_events_sized(off, ev)
+        bad = grp.copy()
+        bad[1] = bad[0]
+        jobs[2] = hq.SizedStream(bad, sz, len(ev), data)
+        with pytest.raises(hq.HQError, match="listed twice"):
+            hq.step_jobs(list(zip(a, jobs)))
+        for i, w in enumerate(b):
+            if i != 2:
+                w.step_sized(*jobs[i])
+        for i, (G, _, _, _) in enumerate(specs):
+            for c in sorted({1, G // 2 + 1, G}):
+                ga, ma = a[i].get_group(c)[:2]
+                gb, mb = b[i].get_group(c)[:2]
+                assert ga.tobytes() == gb.tobytes() and ma.tobytes() == mb.tobytes(), (i, c)
+    finally:
+        for w in a + b:
+            w.close()
+
+
 @pytest.mark.parametrize("stream", [True, False, "sized", "sized-column", "sized-advance"],
                          ids=["stream", "rows", "sized", "sized-column", "sized-advance"])
 def test_chunked_device_step_equals_host_worker(hq, stream):
