@@ -1261,6 +1261,39 @@ class StepRows:
         return self.groups, self.offsets, self.ev
 
 
+class StepRows16:
+    """The producer's form of the same steps (step_events / StepRows): one 16-byte compact record
+    per message (hq_event16) instead of the 56-byte row, what a step worker's queue must hold of a
+    received pb.Message for this path (raft.proto:154-168); hq_events16_encode_sized turns them
+    into the same stream bytes. The steady-state step needs no escape, so record i is row i and
+    set(s) writes the same few strided columns as StepRows.set (equality with hq_events_to16 of
+    step_events() is tested in tests/test_bench_host.py)."""
+
+    def __init__(self, hq, G, roles, last0=1000):
+        assert G % 4 == 0
+        self.G, self.last0, self.s = G, last0, 0
+        _, off, ev = step_events(hq, G, 0, roles, last0)
+        self.recs, self.offsets = hq.events_to16(off, ev)
+        assert np.array_equal(self.offsets, off)
+        k = len(roles) - 1
+        per = 2 * k + 1
+        self.period = 4 * per + 1
+        self.r = self.recs.reshape(G // 4, self.period)
+        starts = [1] + [per + 1 + j * per for j in range(3)]
+        self.repl = [st + j for st in starts for j in range(k)]
+        self.g0 = np.arange(0, G, 4, dtype=np.uint64)
+
+    def set(self, s):
+        """Make the records those of step s (the heartbeat acks refer to the READ's ctx)."""
+        s1 = np.uint64(s + 1)
+        v = self.r["value"]
+        v[:, self.repl] = np.uint64(self.last0 + s)
+        v[:, 0] = (s1 << np.uint64(32)) | self.g0
+        self.r["term"][:, 0] = s + 1
+        self.s = s
+        return self.offsets, self.recs
+
+
 def _shard_of(d, G):
     from dragonboat_amd import shard
 
@@ -1300,7 +1333,10 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     rng = _shard_of(d, G)
     g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
     rows = StepRows(hq, G, roles)
+    recs = StepRows16(hq, G, roles)      # the producer's compact form of the same messages
     offsets = rows.offsets
+    # the producer's native encode threads per step, shared by the W workers' encodes
+    enc_threads = max(1, min(16, cpu_thread_counts()[0]))
     pin = hq.Context(d.device)
     Ws = (1, 2, 16)
     modes = {}
@@ -1327,10 +1363,15 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     pool = ThreadPoolExecutor(max(Ws) + 1)
 
     def encode(W, i, slot):
+        """Worker i's stream of the current step from the producer's compact records, on its
+        share of the encode threads, straight into its pinned receive buffer."""
         mo = modes[W]
         off, e0, e1 = mo["parts"][i]
         out, sz = mo["bufs"][slot][i]
-        mo["nbytes"][slot][i] = hq.encode_events_sized_into(off, rows.ev[e0:e1], out, sz)
+        ne, nb = hq.encode_events16_sized_into(off, recs.recs[e0:e1], out, sz,
+                                               max(1, enc_threads // W))
+        assert ne == e1 - e0
+        mo["nbytes"][slot][i] = nb
 
     def jobs(W, slot, which):
         mo = modes[W]
@@ -1354,9 +1395,16 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         cpus = {nt: [qref.StepBatch(g, m), [], []] for nt in counts}
     prev_sum = int(g["committed"].sum(dtype=np.uint64))
     rows.set(0)
+    recs.set(0)
     for W in Ws:                       # step 0's streams (untimed)
         for i in range(W):
             encode(W, i, 0)
+    # the compact producer writes the bytes the rows encode to (step 0, one worker)
+    want_data, want_sizes = hq.encode_events_sized(offsets, rows.ev)
+    producer_equal = bool(np.array_equal(modes[1]["bufs"][0][0][0][:modes[1]["nbytes"][0][0]],
+                                         want_data) and
+                          np.array_equal(modes[1]["bufs"][0][0][1], want_sizes))
+    del want_data, want_sizes
     n_events = len(rows.ev)
     timed = 0
     for s in range(steps + STEP_WARM):
@@ -1371,6 +1419,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         if cpus:
             prev_sum = tot["committed_sum"]
         rows.set(s + 1)                # untimed: step s + 1's messages arrive
+        recs.set(s + 1)
         for W in Ws:
             mo = modes[W]
             if s >= STEP_WARM:
@@ -1432,8 +1481,12 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                                for W in Ws for k in ("dev", "e2e")},
         "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
         "modes_agree": same_modes,
-        "note": "end_to_end: the producer's encode of step s + 1 (W threads) overlapped with the "
-                "device step s; device_only: the encoded stream given",
+        "producer": f"compact 16-byte message records (hq_event16) encoded by "
+                    f"hq_events16_encode_sized on {enc_threads} native threads per step "
+                    f"(max(1, {enc_threads} // W) per worker)",
+        "producer_equal_rows": producer_equal,
+        "note": "end_to_end: the producer's encode of step s + 1 overlapped with the device step "
+                "s; device_only: the encoded stream given",
     }
     if cpus:
         cpu = {str(nt): n_events * len(ts) / sum(ts) for nt, (_, ts, _) in cpus.items()}

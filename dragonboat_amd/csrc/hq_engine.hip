@@ -49,7 +49,6 @@ constexpr int kPollCopies = 16;            // copies of the relayed count, 256 B
                                            // workgroup 97 us after the launch, tools/ab_engine.py)
 constexpr int kPollStride = 32;            // u64 between copies
 constexpr int kInit = 32;                  // descriptors handed over in the kernel arguments
-constexpr uint32_t kClaimRing = 128;       // steps of device claim counters (>= 2 x depth)
 
 // A descriptor as the kernel arguments carry it (EngineDesc without seq / reserved).
 struct InitDesc {
@@ -89,9 +88,6 @@ struct EngineK {
     EngineDesc *d_ring;            // device [depth]
     uint64_t *dbg;                 // HQ_ENGINE_EXP phase clocks (tools/ab_engine.py), else NULL
     uint64_t *d_polled;            // device [kPollCopies * kPollStride]: copies of d_posted
-    uint32_t *d_claim;             // device [kClaimRing][npairs]: tiles taken per step and pair
-    uint32_t npairs;               // workgroup pairs (b, b + npairs) sharing a claim counter
-    uint32_t pad2;
     // the descriptors of steps [init_base, init_base + init_count), known when the grid was
     // launched: every workgroup starts with them in LDS (no relay, no poll at the start)
     uint64_t init_base;
@@ -187,7 +183,6 @@ struct EngineLds {
     uint64_t tag[kEngineMaxDepth];
     uint32_t claim[kEngineMaxDepth];
     uint32_t fin[kEngineMaxDepth];
-    uint32_t passed[kEngineMaxDepth];   // waves of the workgroup done with the slot's step
     uint64_t cur[16];
     uint64_t known;
     uint32_t waiting, lock, exit, pad;
@@ -213,7 +208,6 @@ __device__ void arm_slot(EngineLds &l, uint64_t slot, uint64_t s, uint64_t depth
                     __builtin_amdgcn_s_sleep(1);
             __hip_atomic_store(&l.claim[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_store(&l.fin[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&l.passed[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_store(&l.tag[slot], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
@@ -327,9 +321,8 @@ __device__ void arrive(const EngineK &e, uint64_t s) {
 // step s + 1 while the others finish theirs: no barrier between steps. In-place tables
 // (INPLACE) are the exception: a wave takes tiles of step s + 1 only when the workgroup has
 // decided all of step s, since the same table tiles come back at every step.
-template <int N, int FORM, int LEAD, bool INPLACE, int BLK, bool WT, bool DCLAIM>
+template <int N, int FORM, int LEAD, bool INPLACE, int BLK, bool WT>
 __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(const EngineK e) {
-    static_assert(!(INPLACE && DCLAIM), "an in-place table keeps every tile on one workgroup");
     constexpr int WPW = BLK / 64;   // waves per workgroup
     __shared__ EngineLds l;
     const uint32_t lane = threadIdx.x & 63;
@@ -373,19 +366,16 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
         }
         const uint64_t slot = s & dmask;
         const uint64_t *d = reinterpret_cast<const uint64_t *>(l.ring + slot);
-        if (lane == 0) arm_slot<WPW>(l, slot, s, e.depth);
         if (uniform64(d[6]) & kDescStop) {
-            // the last wave here counts the workgroup's arrival at the STOP (every step before it
-            // is complete once the grid has exited)
-            if constexpr (DCLAIM) {   // the STOP's counter is never claimed: re-arm ahead here
-                if (lane == 0)
-                    __hip_atomic_store(e.d_claim + ((s + kClaimRing / 2) & (kClaimRing - 1)) *
-                                                       e.npairs + blockIdx.x % e.npairs,
-                                       0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the first wave here counts the workgroup's arrival at the STOP (every step before
+            // it is complete once the grid has exited)
+            uint32_t i = 0;
+            if (lane == 0) {
+                arm_slot<WPW>(l, slot, s, e.depth);
+                i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (lane == 0 &&
-                __hip_atomic_fetch_add(&l.passed[slot], 1u, __ATOMIC_ACQ_REL,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP) + 1 == (uint32_t)WPW) {
+            if (wave_u32(i) == 0 && lane == 0) {
                 if (blockIdx.x % 64 == 0) HQ_EPROBE_MAX(e, 10);   // workgroups at the STOP
                 arrive(e, s);
             }
@@ -401,60 +391,29 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
         k.fallback = as_global<uint64_t>(uniform64(d[4]));
         k.R = e.R;
         const uint64_t tiles = (k.G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
-        if constexpr (DCLAIM) {
-            // workgroups b and b + npairs share a range and take its tiles one at a time from a
-            // device counter, the next claim issued before the current tile is decided. The
-            // first claim past the end (unique: every wave claims until it fails) re-arms the
-            // counter kClaimRing / 2 steps ahead, which no wave can still be using (the host
-            // keeps at most `depth` steps in flight, and a step is complete only when every
-            // wave has passed it, its failing claim included)
-            const uint32_t np = e.npairs, pair = blockIdx.x % np;
-            const uint64_t per = (tiles + np - 1) / np;
-            const uint64_t b0 = (uint64_t)pair * per;
-            const uint32_t len = (uint32_t)(b0 >= tiles ? 0 : tiles - b0 < per ? tiles - b0 : per);
-            uint32_t *ctr = e.d_claim + (s & (kClaimRing - 1)) * np + pair;
-            uint32_t nxt = 0;
+        const uint64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+        const uint64_t b0 = (uint64_t)blockIdx.x * per;
+        const uint32_t len = (uint32_t)(b0 >= tiles ? 0 : tiles - b0 < per ? tiles - b0 : per);
+        if (lane == 0) arm_slot<WPW>(l, slot, s, e.depth);
+        for (;;) {
+            uint32_t i = 0;
             if (lane == 0)
-                nxt = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (;;) {
-                const uint32_t i = wave_u32(nxt);
-                if (i >= len) {
-                    if (i == len && lane == 0)
-                        __hip_atomic_store(e.d_claim + ((s + kClaimRing / 2) & (kClaimRing - 1)) *
-                                                           np + pair,
-                                           0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                if (lane == 0)
-                    nxt = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                commit_tile<N, FORM, false, LEAD, INPLACE, WT>(k, (b0 + i) * HQ_TILE_GROUPS, lane);
+                i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            i = wave_u32(i);
+            if (i >= len) {
+                // the first claim past the end of an empty range stands in for its last tile
+                if (i == len && len == 0 && e.signal && lane == 0) arrive(e, s);
+                break;
             }
-        } else {
-            // workgroup b's own range, its tiles taken one at a time from the LDS counter
-            const uint64_t per = (tiles + gridDim.x - 1) / gridDim.x;
-            const uint64_t b0 = (uint64_t)blockIdx.x * per;
-            const uint32_t len = (uint32_t)(b0 >= tiles ? 0 : tiles - b0 < per ? tiles - b0 : per);
-            for (;;) {
-                uint32_t i = 0;
+            commit_tile<N, FORM, false, LEAD, INPLACE, WT>(k, (b0 + i) * HQ_TILE_GROUPS, lane);
+            if (e.signal || INPLACE) {
+                if (e.signal) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // WT drained
+                uint32_t f = 0;
                 if (lane == 0)
-                    i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                i = wave_u32(i);
-                if (i >= len) break;
-                commit_tile<N, FORM, false, LEAD, INPLACE, WT>(k, (b0 + i) * HQ_TILE_GROUPS, lane);
-                if constexpr (INPLACE) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0)
-                        __hip_atomic_fetch_add(&l.fin[slot], 1u, __ATOMIC_RELEASE,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            if constexpr (INPLACE) {
-                // the table's tiles of step s + 1 are those of step s: wait until the workgroup
-                // has decided all of them
-                while (__hip_atomic_load(&l.fin[slot], __ATOMIC_ACQUIRE,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP) < len)
-                    __builtin_amdgcn_s_sleep(2);
+                    f = __hip_atomic_fetch_add(&l.fin[slot], 1u, __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
+                if (wave_u32(f) == len && e.signal && lane == 0) arrive(e, s);
             }
         }
 #ifdef HQ_ENGINE_EXP
@@ -466,14 +425,11 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
             (uint64_t)blockIdx.x * 16 + wv < 16384)
             e.dbg[64 + (uint64_t)blockIdx.x * 16 + wv] = now_ticks();   // every wave's finish
 #endif
-        if (e.signal) {
-            // this wave is done with step s: its write-through stores drained, the last wave of
-            // the workgroup counts the workgroup's arrival
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0 &&
-                __hip_atomic_fetch_add(&l.passed[slot], 1u, __ATOMIC_ACQ_REL,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP) + 1 == (uint32_t)WPW)
-                arrive(e, s);
+        if constexpr (INPLACE) {
+            // the table's tiles of step s + 1 are those of step s: wait until they are decided
+            while (__hip_atomic_load(&l.fin[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                   len)
+                __builtin_amdgcn_s_sleep(2);
         }
         ++s;
         if (lane == 0) __hip_atomic_store(&l.cur[wv], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -483,39 +439,36 @@ __global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(cons
 
 typedef void (*EngineKernel)(const EngineK);
 
-template <int N, int FORM, int LEAD, bool INPLACE, int BLK>
-void engine_kernel_blk(bool wt, bool dclaim, EngineKernel *fn) {
-    if constexpr (INPLACE) {
-        *fn = wt ? k_commit_engine<N, FORM, LEAD, true, BLK, true, false>
-                 : k_commit_engine<N, FORM, LEAD, true, BLK, false, false>;
-    } else {
-        *fn = wt ? (dclaim ? k_commit_engine<N, FORM, LEAD, false, BLK, true, true>
-                           : k_commit_engine<N, FORM, LEAD, false, BLK, true, false>)
-                 : (dclaim ? k_commit_engine<N, FORM, LEAD, false, BLK, false, true>
-                           : k_commit_engine<N, FORM, LEAD, false, BLK, false, false>);
-    }
-}
-
 template <int N, int FORM, int LEAD, bool INPLACE>
-void engine_kernel_for(bool wt, bool dclaim, EngineKernel *fn, int *blk) {
+void engine_kernel_for(bool wt, EngineKernel *fn, int *blk) {
+#ifdef HQ_ENGINE_EXP   // A/B: HQ_ENGINE_BLOCK=512 takes 512-thread workgroups at any N
+    const char *eb = std::getenv("HQ_ENGINE_BLOCK");
+    if (N <= 5 && eb && std::atoi(eb) == 512) {
+        *fn = wt ? k_commit_engine<N, FORM, LEAD, INPLACE, 512, true>
+                 : k_commit_engine<N, FORM, LEAD, INPLACE, 512, false>;
+        *blk = 512;
+        return;
+    }
+#endif
     if constexpr (N <= 5) {
-        engine_kernel_blk<N, FORM, LEAD, INPLACE, 1024>(wt, dclaim, fn);
+        *fn = wt ? k_commit_engine<N, FORM, LEAD, INPLACE, 1024, true>
+                 : k_commit_engine<N, FORM, LEAD, INPLACE, 1024, false>;
         *blk = 1024;
     } else {
-        engine_kernel_blk<N, FORM, LEAD, INPLACE, 512>(wt, dclaim, fn);
+        *fn = wt ? k_commit_engine<N, FORM, LEAD, INPLACE, 512, true>
+                 : k_commit_engine<N, FORM, LEAD, INPLACE, 512, false>;
         *blk = 512;
     }
 }
 
 template <int N>
-int engine_kernel_n(uint32_t form, uint32_t layout, bool wt, bool dclaim, EngineKernel *fn,
-                    int *blk) {
+int engine_kernel_n(uint32_t form, uint32_t layout, bool wt, EngineKernel *fn, int *blk) {
     const bool lead = (layout & 0xFFu) == HQ_LAYOUT_TILES_LEADER;
     const bool inplace = (layout & HQ_LAYOUT_IN_PLACE) != 0;
 #define HQ_ENGINE_PICK(F)                                                                        \
-    if (inplace) engine_kernel_for<N, F, 1, true>(wt, dclaim, fn, blk);                          \
-    else if (lead) engine_kernel_for<N, F, 1, false>(wt, dclaim, fn, blk);                       \
-    else engine_kernel_for<N, F, 0, false>(wt, dclaim, fn, blk);
+    if (inplace) engine_kernel_for<N, F, 1, true>(wt, fn, blk);                                  \
+    else if (lead) engine_kernel_for<N, F, 1, false>(wt, fn, blk);                               \
+    else engine_kernel_for<N, F, 0, false>(wt, fn, blk);
     if (form == HQ_FORM_TERM_MASK) {
         HQ_ENGINE_PICK(HQ_FORM_TERM_MASK)
     } else {
@@ -527,17 +480,16 @@ int engine_kernel_n(uint32_t form, uint32_t layout, bool wt, bool dclaim, Engine
 
 // WT (write-through stores) for the per-step completion signals: a step's outputs are visible
 // once its waves' stores have drained
-int engine_kernel(uint32_t n, uint32_t form, uint32_t layout, bool wt, bool dclaim,
-                  EngineKernel *fn, int *blk) {
+int engine_kernel(uint32_t n, uint32_t form, uint32_t layout, bool wt, EngineKernel *fn, int *blk) {
     switch (n) {
-    case 1: return engine_kernel_n<1>(form, layout, wt, dclaim, fn, blk);
-    case 2: return engine_kernel_n<2>(form, layout, wt, dclaim, fn, blk);
-    case 3: return engine_kernel_n<3>(form, layout, wt, dclaim, fn, blk);
-    case 4: return engine_kernel_n<4>(form, layout, wt, dclaim, fn, blk);
-    case 5: return engine_kernel_n<5>(form, layout, wt, dclaim, fn, blk);
-    case 6: return engine_kernel_n<6>(form, layout, wt, dclaim, fn, blk);
-    case 7: return engine_kernel_n<7>(form, layout, wt, dclaim, fn, blk);
-    default: return engine_kernel_n<8>(form, layout, wt, dclaim, fn, blk);
+    case 1: return engine_kernel_n<1>(form, layout, wt, fn, blk);
+    case 2: return engine_kernel_n<2>(form, layout, wt, fn, blk);
+    case 3: return engine_kernel_n<3>(form, layout, wt, fn, blk);
+    case 4: return engine_kernel_n<4>(form, layout, wt, fn, blk);
+    case 5: return engine_kernel_n<5>(form, layout, wt, fn, blk);
+    case 6: return engine_kernel_n<6>(form, layout, wt, fn, blk);
+    case 7: return engine_kernel_n<7>(form, layout, wt, fn, blk);
+    default: return engine_kernel_n<8>(form, layout, wt, fn, blk);
     }
 }
 
@@ -774,12 +726,7 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     if (!e) return hq::fail(ctx, HQ_E_NOMEM, "hq_engine_open: out of host memory");
     e->ctx = ctx;
     e->cfg = c;
-    // device claims (workgroup pairs) unless HQ_ENGINE_CLAIM=0 (LDS ranges, A/B) or in place
-    bool dclaim = true;
-    if (const char *v = std::getenv("HQ_ENGINE_CLAIM")) dclaim = std::atoi(v) != 0;
-    dclaim = dclaim && !(c.layout & HQ_LAYOUT_IN_PLACE);
-    engine_kernel(c.n_max, c.form, c.layout, (c.flags & HQ_ENGINE_SIGNAL) != 0, dclaim, &e->fn,
-                  &e->block);
+    engine_kernel(c.n_max, c.form, c.layout, (c.flags & HQ_ENGINE_SIGNAL) != 0, &e->fn, &e->block);
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     int cus = 0, per_cu = 0;
     if (!rc) rc = hq::check_hip(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
@@ -801,9 +748,7 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     const size_t ring_off = (cur_off + 8 * (size_t)e->grid + 127) & ~(size_t)127;
     const size_t dbg_off = ring_off + sizeof(EngineDesc) * D;
     const size_t polled_off = dbg_off + 8 * (64 + 16384);
-    const size_t claim_off = polled_off + 8 * kPollCopies * kPollStride;
-    const uint32_t npairs = e->grid >= 2 && e->grid % 2 == 0 ? e->grid / 2 : e->grid;
-    const size_t dev_bytes = claim_off + 4 * (size_t)kClaimRing * npairs;
+    const size_t dev_bytes = polled_off + 8 * kPollCopies * kPollStride;
     void *hp = nullptr, *dp = nullptr;
     rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking),
                        "hipStreamCreateWithFlags");
@@ -837,8 +782,6 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     k.d_cursor = reinterpret_cast<uint64_t *>(e->dev + cur_off);
     k.d_ring = reinterpret_cast<EngineDesc *>(e->dev + ring_off);
     k.d_polled = reinterpret_cast<uint64_t *>(e->dev + polled_off);
-    k.d_claim = reinterpret_cast<uint32_t *>(e->dev + claim_off);
-    k.npairs = npairs;
 #ifdef HQ_ENGINE_EXP
     k.dbg = reinterpret_cast<uint64_t *>(e->dev + dbg_off);
 #endif

@@ -6,7 +6,11 @@
 // encoder a producer holding rows can call (the wire decoder and a caller's own producer can
 // write the stream directly) and the decoder the host worker uses for stream input; the device
 // twin of the decoder is in hq_dstep.hip.
+#include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/hipquorum.h"
 
@@ -93,9 +97,282 @@ inline uint8_t *encode(uint8_t *p, const hq_event &e, Prev &pv) {
     return p;
 }
 
+// The event a compact record stands for. rc: records taken (1, or 5 for an escape), 0 when a
+// record is malformed (an escape without its 4 records). ctx: the group's latest READ ctx.
+inline int from16(const hq_event16 *r, uint64_t left, uint64_t ctx[2], hq_event &e) {
+    if (r->kind & HQ_EV16_FULL) {
+        if (left < 5) return 0;
+        std::memcpy(&e, r + 1, sizeof e);
+        if (e.kind == HQ_EV_READ) {
+            ctx[0] = e.hint;
+            ctx[1] = e.hint_high;
+        }
+        return 5;
+    }
+    e = hq_event{};
+    e.kind = r->kind & 7;
+    e.reject = (r->kind >> 3) & 1;
+    if (e.kind == HQ_EV_READ) {
+        e.hint = ctx[0] = r->value;
+        e.hint_high = ctx[1] = r->term;
+    } else if (e.kind == HQ_EV_PROPOSE) {
+        e.log_index = r->value;
+    } else if (e.kind == HQ_EV_MESSAGE) {
+        e.type = r->type;
+        e.from = r->from;
+        e.term = r->term;
+        if (e.type == HQ_MSG_HEARTBEAT_RESP || e.type == HQ_MSG_READ_INDEX) {
+            if (r->kind & HQ_EV16_READ_CTX) {
+                e.hint = ctx[0];
+                e.hint_high = ctx[1];
+            } else {
+                e.hint = r->value;
+            }
+        } else {
+            e.log_index = r->value;
+        }
+    }
+    return 1;
+}
+
+__attribute__((always_inline)) inline uint8_t *put_fast(uint8_t *p, uint64_t v) {   // the 1- and 2-byte varints inline
+    if (v < 0x80) {
+        *p = (uint8_t)v;
+        return p + 1;
+    }
+    if (v < 0x4000) {
+        p[0] = (uint8_t)(v | 0x80);
+        p[1] = (uint8_t)(v >> 7);
+        return p + 2;
+    }
+    return put(p, v);
+}
+
+// type_code of the types below 32
+constexpr uint8_t kCode16[32] = {7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 0, 7, 1,
+                                 7, 7, 2, 3, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7};
+static_assert(HQ_MSG_REPLICATE_RESP == 13 && HQ_MSG_REQUEST_VOTE_RESP == 15 &&
+                  HQ_MSG_HEARTBEAT_RESP == 18 && HQ_MSG_READ_INDEX == 19,
+              "kCode16 follows the message type numbers");
+
+// one compact record (not an escape) straight into bytes: encode() of the event from16() makes
+// of it, without the row
+__attribute__((always_inline)) inline uint8_t *encode16(uint8_t *p, const hq_event16 &r, Prev &pv,
+                                                       uint64_t ctx[2]) {
+    const uint32_t k = r.kind & 7;
+    if (k != HQ_EV_MESSAGE) {
+        const uint32_t kind = k >= 1 && k <= 5 ? k : 0;
+        *p++ = (uint8_t)kind;
+        if (kind == HQ_EV_READ) {
+            ctx[0] = r.value;
+            ctx[1] = r.term;
+            p = put(p, r.value);
+            p = put_fast(p, r.term);
+        } else if (kind == HQ_EV_PROPOSE) {
+            p = put_fast(p, r.value);
+        }
+        return p;
+    }
+    uint32_t code = r.type < 32 ? kCode16[r.type] : 7u;
+    uint64_t hint = 0, high = 0;
+    if (code == 0) {
+        if (pv.have_index && r.value == pv.index) code = 4;
+        pv.index = r.value;
+        pv.have_index = true;
+    } else if (code == 2 || code == 3) {
+        if (r.kind & HQ_EV16_READ_CTX) {
+            hint = ctx[0];
+            high = ctx[1];
+        } else {
+            hint = r.value;
+        }
+        if (code == 2) {
+            if (hint == pv.hint && high == pv.high) code = 5;
+            pv.hint = hint;
+            pv.high = high;
+        }
+    }
+    const bool same = r.term == pv.term;
+    *p++ = (uint8_t)(HQ_EV_MESSAGE | code << 3 | ((r.kind & 8) ? 0x40 : 0) | (same ? 0x80 : 0));
+    if (code == 7) p = put(p, r.type);
+    p = put_fast(p, r.from);
+    if (!same) p = put(p, r.term);
+    pv.term = r.term;
+    if (code == 0 || code == 7) p = put_fast(p, r.value);
+    if (code == 2 || code == 3 || code == 7) {
+        p = put(p, hint);
+        p = put_fast(p, high);
+    }
+    return p;
+}
+
+// groups [g0, g1) encoded at p (room for HQ_EVENT_STREAM_MAX bytes before each event checked
+// against end; a growing scratch passes end = nullptr and grows itself)
+struct Enc16 {
+    const uint64_t *off;
+    const hq_event16 *recs;
+    uint32_t *sizes;
+    uint64_t events = 0;
+    int run(uint64_t g0, uint64_t g1, std::vector<uint8_t> *grow, uint8_t *out, uint64_t cap,
+            uint64_t *bytes) {
+        uint64_t pos = 0;
+        for (uint64_t i = g0; i < g1; ++i) {
+            if (off[i + 1] < off[i]) return HQ_E_INVAL;
+            const uint64_t p0 = pos;
+            uint64_t ne = 0, ctx[2] = {0, 0};
+            Prev pv;
+            // room for the group's records at HQ_EVENT_STREAM_MAX each: no check per event
+            const uint64_t need = (off[i + 1] - off[i]) * HQ_EVENT_STREAM_MAX;
+            if (grow && grow->size() < pos + need)
+                grow->resize(std::max<size_t>(2 * grow->size(), pos + need + (1 << 20)));
+            const bool roomy = grow || (cap >= pos && cap - pos >= need);
+            uint8_t *const base = grow ? grow->data() : out;
+            for (uint64_t k = off[i]; k < off[i + 1]; ++ne) {
+                if (!roomy && (cap < pos || cap - pos < HQ_EVENT_STREAM_MAX)) return HQ_E_STATE;
+                if (!(recs[k].kind & HQ_EV16_FULL)) {
+                    pos = (uint64_t)(encode16(base + pos, recs[k], pv, ctx) - base);
+                    ++k;
+                    continue;
+                }
+                hq_event e;
+                const int used = from16(recs + k, off[i + 1] - k, ctx, e);
+                if (!used) return HQ_E_INVAL;
+                k += used;
+                pos = (uint64_t)(encode(base + pos, e, pv) - base);
+            }
+            if (ne > 0xFFFF || pos - p0 > 0xFFFF) return HQ_E_INVAL;
+            sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
+            events += ne;
+        }
+        *bytes = pos;
+        return HQ_OK;
+    }
+};
+
+std::mutex g_enc16_mu;                           // one threaded encode at a time
+std::vector<std::vector<uint8_t>> g_enc16_scratch;
+
 }  // namespace
 
 extern "C" {
+
+int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const hq_event16 *recs,
+                             uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_events,
+                             uint64_t *n_bytes, uint32_t threads) {
+    if (!offsets16 || !n_events || !n_bytes || (n_groups && !sizes) ||
+        (n_groups && offsets16[n_groups] > offsets16[0] && !recs))
+        return HQ_E_INVAL;
+    *n_events = *n_bytes = 0;
+    if (n_groups && offsets16[n_groups] > offsets16[0] && !out) return HQ_E_STATE;
+    const uint64_t nrec = n_groups ? offsets16[n_groups] - offsets16[0] : 0;
+    const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(threads, 1u),
+                                                    std::max<uint64_t>(1, nrec / 4096));
+    if (T <= 1) {
+        Enc16 enc{offsets16, recs, sizes};
+        const int rc = enc.run(0, n_groups, nullptr, out, cap, n_bytes);
+        *n_events = enc.events;
+        return rc;
+    }
+    // T ranges of about equal records (group boundaries), each into its own scratch
+    std::lock_guard<std::mutex> lock(g_enc16_mu);
+    if (g_enc16_scratch.size() < T) g_enc16_scratch.resize(T);
+    std::vector<uint64_t> g(T + 1), bytes(T, 0);
+    std::vector<int> rcs(T, HQ_OK);
+    std::vector<Enc16> encs(T, Enc16{offsets16, recs, sizes});
+    g[0] = 0;
+    g[T] = n_groups;
+    for (uint32_t t = 1; t < T; ++t) {
+        const uint64_t want = offsets16[0] + nrec * t / T;
+        g[t] = std::max<uint64_t>(g[t - 1], (uint64_t)(std::lower_bound(offsets16, offsets16 + n_groups,
+                                                                         want) - offsets16));
+    }
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; ++t)
+        th.emplace_back([&, t] {
+            rcs[t] = encs[t].run(g[t], g[t + 1], &g_enc16_scratch[t], nullptr, 0, &bytes[t]);
+        });
+    rcs[0] = encs[0].run(g[0], g[1], &g_enc16_scratch[0], nullptr, 0, &bytes[0]);
+    for (auto &x : th) x.join();
+    uint64_t total = 0, events = 0;
+    for (uint32_t t = 0; t < T; ++t) {
+        if (rcs[t]) return rcs[t];
+        total += bytes[t];
+        events += encs[t].events;
+    }
+    if (total > cap) return HQ_E_STATE;
+    std::vector<uint64_t> at(T, 0);
+    for (uint32_t t = 1; t < T; ++t) at[t] = at[t - 1] + bytes[t - 1];
+    th.clear();
+    for (uint32_t t = 1; t < T; ++t)
+        th.emplace_back([&, t] {
+            if (bytes[t]) std::memcpy(out + at[t], g_enc16_scratch[t].data(), bytes[t]);
+        });
+    if (bytes[0]) std::memcpy(out, g_enc16_scratch[0].data(), bytes[0]);
+    for (auto &x : th) x.join();
+    *n_events = events;
+    *n_bytes = total;
+    return HQ_OK;
+}
+
+int hq_events_to16(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
+                   hq_event16 *out, uint64_t cap, uint64_t *offsets16) {
+    if (!offsets || !offsets16 || (n_groups && offsets[n_groups] > offsets[0] && !events))
+        return HQ_E_INVAL;
+    uint64_t k = 0;
+    offsets16[0] = 0;
+    for (uint64_t i = 0; i < n_groups; ++i) {
+        if (offsets[i + 1] < offsets[i]) return HQ_E_INVAL;
+        uint64_t ctx[2] = {0, 0};
+        for (uint64_t j = offsets[i]; j < offsets[i + 1]; ++j) {
+            const hq_event &e = events[j];
+            hq_event16 r{};
+            bool fits = e.kind >= 1 && e.kind <= 5 && e.reject <= 1;
+            r.kind = (uint8_t)(e.kind | (e.reject ? 8u : 0u));
+            if (fits && e.kind == HQ_EV_READ) {
+                fits = e.hint_high >> 32 == 0;
+                r.value = e.hint;
+                r.term = (uint32_t)e.hint_high;
+            } else if (fits && e.kind == HQ_EV_PROPOSE) {
+                r.value = e.log_index;
+            } else if (fits && e.kind == HQ_EV_MESSAGE) {
+                fits = e.type < 256 && e.from >> 16 == 0 && e.term >> 32 == 0;
+                r.type = (uint8_t)e.type;
+                r.from = (uint16_t)e.from;
+                r.term = (uint32_t)e.term;
+                if (e.type == HQ_MSG_HEARTBEAT_RESP || e.type == HQ_MSG_READ_INDEX) {
+                    if (e.hint == ctx[0] && e.hint_high == ctx[1] && (e.hint | e.hint_high)) {
+                        r.kind |= HQ_EV16_READ_CTX;
+                    } else {
+                        fits = fits && e.hint_high == 0;
+                        r.value = e.hint;
+                    }
+                } else if (e.type == HQ_MSG_REPLICATE_RESP || e.type == HQ_MSG_REQUEST_VOTE_RESP) {
+                    r.value = e.log_index;   // (a RequestVoteResp carries nothing more)
+                } else {                     // another type: log_index, hint, hint_high
+                    fits = fits && e.hint == 0 && e.hint_high == 0;
+                    r.value = e.log_index;
+                }
+            }
+            if (fits) {
+                if (k + 1 > cap) return HQ_E_STATE;
+                out[k++] = r;
+            } else {
+                if (k + 5 > cap) return HQ_E_STATE;
+                out[k] = hq_event16{};
+                out[k].kind = (uint8_t)HQ_EV16_FULL;
+                std::memset(out + k + 1, 0, 4 * sizeof(hq_event16));
+                std::memcpy(out + k + 1, &e, sizeof e);
+                k += 5;
+            }
+            if (e.kind == HQ_EV_READ) {
+                ctx[0] = e.hint;
+                ctx[1] = e.hint_high;
+            }
+        }
+        offsets16[i + 1] = k;
+    }
+    return HQ_OK;
+}
 
 int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
                      uint8_t *out, uint64_t cap, uint64_t *boffsets) {

@@ -42,7 +42,7 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 14
+HQ_ABI_VERSION = 15
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -152,6 +152,10 @@ DROP_WITNESS, DROP_NOT_READY = 1, 2
 EVENT_DTYPE = np.dtype([("kind", "<u4"), ("type", "<u4"), ("from", "<u8"), ("term", "<u8"),
                         ("log_index", "<u8"), ("hint", "<u8"), ("hint_high", "<u8"),
                         ("reject", "<u4"), ("reserved", "<u4")], align=True)
+# hq_event16: a compact message record (hq_events16_encode_sized)
+EVENT16_DTYPE = np.dtype([("kind", "u1"), ("type", "u1"), ("from", "<u2"), ("term", "<u4"),
+                          ("value", "<u8")])
+EV16_READ_CTX, EV16_FULL = 0x10, 0x80
 WORKER_GROUP_DTYPE = np.dtype([("cluster_id", "<u8"), ("node_id", "<u8"), ("term", "<u8"),
                                ("committed", "<u8"), ("last_index", "<u8"), ("term_start", "<u8"),
                                ("state", "<u4"), ("n_members", "<u4"),
@@ -377,6 +381,9 @@ SIGNATURES = {
     "hq_events_encode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "hq_events_encode_sized": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64,
                                               _vp, _vp]),
+    "hq_events16_encode_sized": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64,
+                                                _vp, _vp, _vp, ctypes.c_uint32]),
+    "hq_events_to16": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
                                            ctypes.POINTER(WireStats)]),
@@ -1539,6 +1546,46 @@ def encode_events_sized(offsets, events):
                                     _p(out), len(out), _p(sizes), ctypes.byref(nb)),
          "hq_events_encode_sized")
     return out[:nb.value].copy(), sizes
+
+
+def events_to16(offsets, events):
+    """hq_events_to16: (compact records as EVENT16_DTYPE, their per-group offsets) of rows
+    grouped by `offsets`."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    events = np.ascontiguousarray(events, EVENT_DTYPE)
+    n = len(offsets) - 1
+    ne = int(offsets[-1] - offsets[0]) if n > 0 else 0
+    out = np.zeros(max(1, 5 * ne), EVENT16_DTYPE)
+    off16 = np.zeros(n + 1, np.uint64)
+    _chk(lib.hq_events_to16(n, _p(offsets), _p(events) if len(events) else None, _p(out),
+                            len(out), _p(off16)), "hq_events_to16")
+    return out[:int(off16[-1])].copy(), off16
+
+
+def encode_events16_sized_into(offsets16, recs, out: np.ndarray, sizes: np.ndarray,
+                               threads: int = 1):
+    """hq_events16_encode_sized into caller buffers (`out` uint8, `sizes` uint32 of
+    len(offsets16) - 1, both contiguous): returns (n_events, n_bytes); `threads` native threads."""
+    n = len(offsets16) - 1
+    assert offsets16.dtype == np.uint64 and recs.dtype == EVENT16_DTYPE
+    assert out.dtype == np.uint8 and sizes.dtype == np.uint32 and len(sizes) >= n
+    assert offsets16.flags.c_contiguous and recs.flags.c_contiguous and out.flags.c_contiguous
+    ne, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _chk(lib.hq_events16_encode_sized(n, _p(offsets16), _p(recs) if len(recs) else None,
+                                      _p(out), len(out), _p(sizes), ctypes.byref(ne),
+                                      ctypes.byref(nb), threads), "hq_events16_encode_sized")
+    return ne.value, nb.value
+
+
+def encode_events16_sized(offsets16, recs, threads: int = 1):
+    """hq_events16_encode_sized: (stream bytes as uint8, per-group size words, n_events)."""
+    offsets16 = np.ascontiguousarray(offsets16, np.uint64)
+    recs = np.ascontiguousarray(recs, EVENT16_DTYPE)
+    n = len(offsets16) - 1
+    out = np.zeros(max(1, len(recs) * HQ_EVENT_STREAM_MAX), np.uint8)
+    sizes = np.zeros(max(0, n), np.uint32)
+    ne, nb = encode_events16_sized_into(offsets16, recs, out, sizes, threads)
+    return out[:nb].copy(), sizes, ne
 
 
 def encode_events_sized_into(offsets, events, out: np.ndarray, sizes: np.ndarray) -> int:

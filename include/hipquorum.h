@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 14
+#define HQ_ABI_VERSION 15
 
 /* status codes */
 #define HQ_OK          0
@@ -1054,6 +1054,40 @@ int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event 
  * or bytes (use boffsets for such a step). */
 int hq_events_encode_sized(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
                            uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_bytes);
+/* Compact messages. A producer that keeps a step's messages as 16-byte records instead of the
+ * 56-byte rows (what it must hold of a received pb.Message, raft.proto:154-168, for this path)
+ * hands them to hq_events16_encode_sized, which writes the same stream bytes as encoding the
+ * equivalent rows. A record is one event, or the escape HQ_EV16_FULL followed by the event as an
+ * hq_event row in the next 4 records (64 bytes; the last 8 unused) when a field does not fit. */
+typedef struct hq_event16 {
+    uint8_t kind;       /* bits 0-2 HQ_EV_*, bit 3 reject, HQ_EV16_READ_CTX, HQ_EV16_FULL */
+    uint8_t type;       /* HQ_EV_MESSAGE: HQ_MSG_* (< 256) */
+    uint16_t from;      /* sender node id (< 2^16) */
+    uint32_t term;      /* message term (< 2^32); HQ_EV_READ: SystemCtx.High (< 2^32) */
+    uint64_t value;     /* ReplicateResp, other types, HQ_EV_PROPOSE: log_index; HQ_EV_READ:
+                           SystemCtx.Low; HeartbeatResp / ReadIndex: SystemCtx.Low with High 0 */
+} hq_event16;
+/* a HeartbeatResp / ReadIndex whose ctx is that of the group's latest HQ_EV_READ record before it
+ * in the call (0 / 0 if none): the acks of the heartbeat a ReadIndex broadcast (raft.go:836-848);
+ * `value` is then not read */
+#define HQ_EV16_READ_CTX 0x10u
+#define HQ_EV16_FULL     0x80u   /* escape: the next 4 records hold the event as an hq_event */
+/* Encode compact records: group i's records are recs[offsets16[i] .. offsets16[i + 1]) (an
+ * escape and its 4 records are one event). Writes the sized form as hq_events_encode_sized does
+ * for the equivalent rows (the same bytes and size words) and the event and byte totals.
+ * threads > 1: that many native threads, each encoding a range of groups into its own scratch
+ * before the ranges are copied into place (one such call at a time per process; 0 or 1: the
+ * calling thread only). HQ_E_INVAL on a malformed escape or a group of 2^16 events or bytes;
+ * HQ_E_STATE when out (cap bytes) cannot hold the stream (one thread: as hq_events_encode_sized,
+ * fewer than HQ_EVENT_STREAM_MAX bytes left before an event). */
+int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const hq_event16 *recs,
+                             uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_events,
+                             uint64_t *n_bytes, uint32_t threads);
+/* Rows to compact records: group i's events (offsets as in hq_step_input) become records
+ * out[offsets16[i] .. offsets16[i + 1]) (an event that does not fit takes an escape: 5 records).
+ * HQ_E_STATE when cap records cannot hold them (5 per event always can). */
+int hq_events_to16(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
+                   hq_event16 *out, uint64_t cap, uint64_t *offsets16);
 /* Decode a stream back into rows events[offsets[0] .. offsets[n_groups]); HQ_E_INVAL when a
  * group's bytes do not hold exactly its events. */
 int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t *boffsets,

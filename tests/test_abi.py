@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 14
+    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 15
 
 
 LAYOUT_C = r"""
@@ -90,6 +90,10 @@ int main(void) {
   F(hq_engine_stats, posted) F(hq_engine_stats, completed) F(hq_engine_stats, relaunches)
   F(hq_engine_stats, grid) F(hq_engine_stats, block) F(hq_engine_stats, depth)
   F(hq_engine_stats, running)
+  printf("hq_event16 %zu\nhq_event %zu\nev16_flags %u\n", sizeof(hq_event16), sizeof(hq_event),
+         (unsigned)(HQ_EV16_READ_CTX | HQ_EV16_FULL << 8));
+  F(hq_event16, kind) F(hq_event16, type) F(hq_event16, from) F(hq_event16, term)
+  F(hq_event16, value)
   return 0;
 }
 """
@@ -110,7 +114,9 @@ def test_struct_layout_matches_c(hq, tmp_path):
     assert int(c["hq_engine_stats"]) == ctypes.sizeof(hq.EngineStats)
     assert int(c["engine_signal"]) == hq.HQ_ENGINE_SIGNAL
     dtypes = {"hq_member": hq.MEMBER_DTYPE, "hq_group_view": hq.GROUP_DTYPE,
-              "hq_msg": hq.MSG_DTYPE, "hq_wire_message": hq.WIRE_MESSAGE_DTYPE}
+              "hq_msg": hq.MSG_DTYPE, "hq_wire_message": hq.WIRE_MESSAGE_DTYPE,
+              "hq_event16": hq.EVENT16_DTYPE, "hq_event": hq.EVENT_DTYPE}
+    assert int(c["ev16_flags"]) == hq.EV16_READ_CTX | hq.EV16_FULL << 8
     assert int(c["hq_wire_batch_info"]) == ctypes.sizeof(hq.WireBatchInfo)
     assert int(c["hq_wire_stats"]) == ctypes.sizeof(hq.WireStats)
     assert int(c["bin_ver"]) == hq.HQ_RPC_BIN_VERSION

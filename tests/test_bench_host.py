@@ -25,6 +25,24 @@ def test_step_rows_advance_equals_generation(hq, name):
         assert rows.ev.tobytes() == want[2].tobytes(), (name, s)
 
 
+@pytest.mark.parametrize("name", ["step", "step5"])
+def test_step_rows16_follow_step_events(hq, name):
+    """The producer's compact records advanced in place (StepRows16.set) are hq_events_to16 of
+    step_events() of the same step, and encode (16 threads) to the rows' bytes."""
+    G = 1 << 10
+    roles = bench.STEP_ROLES[name]
+    recs = bench.StepRows16(hq, G, roles)
+    for s in (0, 5, 1, 2, 40):
+        off16, r = recs.set(s)
+        _, off, ev = bench.step_events(hq, G, s, roles)
+        want, woff = hq.events_to16(off, ev)
+        assert np.array_equal(off16, woff) and r.tobytes() == want.tobytes(), (name, s)
+        data, sizes, ne = hq.encode_events16_sized(off16, r, threads=16)
+        wdata, wsizes = hq.encode_events_sized(off, ev)
+        assert ne == len(ev) and data.tobytes() == wdata.tobytes()
+        assert np.array_equal(sizes, wsizes)
+
+
 def test_encode_into_matches_encode(hq):
     G = 1 << 9
     rows = bench.StepRows(hq, G, bench.STEP_ROLES["step5"])

@@ -208,3 +208,79 @@ def test_repeated_heartbeat_ctx(hq):
     off2 = np.array([0, 2, 3], np.uint64)
     d2, b2 = hq.encode_events(off2, ev[[0, 1, 3]])
     assert (int(d2[int(b2[1])]) >> 3) & 7 == 2
+
+
+# --- compact 16-byte records (hq_event16, hq_events16_encode_sized) ----------------------------
+
+def _random_groups(hq, seed, n=700, small=False):
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(0, 12, n)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    ev = random_rows(rng, int(off[-1]), small).view(hq.EVENT_DTYPE)
+    # ReadIndex acks: some groups read, then their heartbeats carry that ctx (READ_CTX records)
+    for i in range(0, n, 3):
+        a, b = int(off[i]), int(off[i + 1])
+        if b - a >= 2:
+            ev[a]["kind"], ev[a]["hint"], ev[a]["hint_high"] = hq.EV_READ, 1000 + i, 7
+            for j in range(a + 1, b, 2):
+                ev[j]["kind"], ev[j]["type"] = hq.EV_MESSAGE, HBRESP
+                ev[j]["hint"], ev[j]["hint_high"] = 1000 + i, 7
+    return off, ev
+
+
+@pytest.mark.parametrize("seed,small", [(11, False), (12, False), (13, True)])
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_compact_records_encode_like_rows(hq, seed, small, threads):
+    """Rows -> hq_events_to16 -> hq_events16_encode_sized writes the bytes and size words of
+    hq_events_encode_sized on the rows themselves, on any thread count: random rows with big
+    node ids / terms / ctxs (escapes), invalid kinds, other message types, ReadIndex acks."""
+    off, ev = _random_groups(hq, seed, small=small)
+    want_data, want_sizes = hq.encode_events_sized(off, ev)
+    recs, off16 = hq.events_to16(off, ev)
+    full = (recs["kind"] & hq.EV16_FULL) != 0
+    assert full.any() and (recs["kind"] & hq.EV16_READ_CTX).any() and (~full).sum() > len(ev) // 3
+    data, sizes, ne = hq.encode_events16_sized(off16, recs, threads=threads)
+    np.testing.assert_array_equal(data, want_data)
+    np.testing.assert_array_equal(sizes, want_sizes)
+    assert ne == len(ev)
+
+
+@pytest.mark.parametrize("name", ["step", "step5"])
+def test_compact_step_workload_has_no_escapes(hq, name):
+    """The bench's steady-state step (tests on bench.step_events): every event fits one 16-byte
+    record (no escape), the heartbeat acks of a ReadIndex refer to its READ, and the encoding
+    equals the rows' on 16 threads."""
+    import bench
+
+    roles = bench.STEP_ROLES[name]
+    grp, off, ev = bench.step_events(hq, 4096, 3, roles)
+    recs, off16 = hq.events_to16(off, ev)
+    np.testing.assert_array_equal(off16, off)
+    assert not (recs["kind"] & hq.EV16_FULL).any()
+    assert np.count_nonzero(recs["kind"] & hq.EV16_READ_CTX) == 1024 * sum(
+        r != "observer" for r in roles[1:])
+    want_data, want_sizes = hq.encode_events_sized(off, ev)
+    data, sizes, ne = hq.encode_events16_sized(off16, recs, threads=16)
+    np.testing.assert_array_equal(data, want_data)
+    np.testing.assert_array_equal(sizes, want_sizes)
+
+
+def test_compact_records_malformed(hq):
+    """An escape without its 4 records is HQ_E_INVAL; an output region too small is HQ_E_STATE
+    (single thread: room for HQ_EVENT_STREAM_MAX before each event; threads: the total)."""
+    recs = np.zeros(3, hq.EVENT16_DTYPE)
+    recs["kind"] = hq.EV16_FULL
+    with pytest.raises(hq.HQError):
+        hq.encode_events16_sized(np.array([0, 3], np.uint64), recs)
+    off, ev = _random_groups(hq, 21)
+    recs, off16 = hq.events_to16(off, ev)
+    _, want_sizes = hq.encode_events_sized(off, ev)
+    nb = int((want_sizes >> 16).sum())
+    for threads in (1, 4):
+        out = np.zeros(nb - 1, np.uint8)
+        sizes = np.zeros(len(off) - 1, np.uint32)
+        with pytest.raises(hq.HQError):
+            hq.encode_events16_sized_into(off16, recs, out, sizes, threads)
+    out = np.zeros(nb, np.uint8)                  # exactly the stream: enough for threads
+    assert hq.encode_events16_sized_into(off16, recs, out, np.zeros(len(off) - 1, np.uint32),
+                                         4) == (len(ev), nb)

@@ -5,7 +5,7 @@ leader-row tiles, mask form) on one GPU, same data, alternated rounds:
   loop       ONE launch, every wave loops over the K batches (the engine's ownership, no doorbell)
   flat       ONE launch, one wave per (batch, tile), batch-major
   engine     the persistent engine (hq_engine): K posted descriptors, one resident launch
-             (engine: device pair claims; engine_lds: HQ_ENGINE_CLAIM=0, per-workgroup LDS ranges)
+             (engine512: HQ_ENGINE_BLOCK=512, 512-thread workgroups; experiment build only)
 Needs the experiment build: HQ_LIB_PATH=tools/lib_engexp/libhipquorum.so (make that target)."""
 import ctypes
 import os
@@ -45,11 +45,11 @@ def main():
 
     engines = {}
     hq.lib.hq_exp_engine_set.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    for name, claim in (("engine", "1"), ("engine_lds", "0")):
-        os.environ["HQ_ENGINE_CLAIM"] = claim
+    for name, blk in (("engine", ""), ("engine512", "512")):
+        os.environ["HQ_ENGINE_BLOCK"] = blk
         engines[name] = hq.Engine(ctx, w["n"], w["form"], hq.HQ_LAYOUT_TILES_LEADER, ring_len=16)
         hq.lib.hq_exp_engine_set(engines[name].h, int(os.environ.get("AB_ENGINE_EXP", "0")))
-    os.environ.pop("HQ_ENGINE_CLAIM")
+    os.environ.pop("HQ_ENGINE_BLOCK")
     variants = {
         "launches": lambda a: ctx.commit_many_dev(a),
         "loop512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 1, 512)),
@@ -61,7 +61,7 @@ def main():
         "claim512x2": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 5, 1024)),
         "gclaim512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 6, 512)),
         "engine": None,
-        "engine_lds": None,
+        "engine512": None,
     }
     only = os.environ.get("AB_ONLY")
     if only:
