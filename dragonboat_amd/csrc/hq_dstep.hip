@@ -92,6 +92,8 @@ struct StepK {
     uint32_t allow_column, pad_j;
     struct Layout *host_layout;
     const uint32_t *sizes;
+    const uint32_t *sizes_src;    // the caller's sizes when in pinned host memory (read over the
+                                  //   link by k_size_sums, which writes `sizes`), else NULL
     uint64_t *bsum;
 };
 
@@ -964,8 +966,19 @@ __global__ __launch_bounds__(256) void k_size_sums(const JobMap m) {
     const StepK &a = m.ks[m.job0 + j];
     const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
     uint64_t v = 0;
+    if (a.sizes_src) {            // the sizes straight from pinned host memory, kept on device
+        uint32_t *dst = const_cast<uint32_t *>(a.sizes);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v += packed_size(a, i0 + k);
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t i = i0 + k;
+            const uint32_t z = i < a.n ? a.sizes_src[i] : 0;
+            if (i < a.n) dst[i] = z;
+            v += (uint64_t)(z & 0xFFFFu) << 32 | (z >> 16);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += packed_size(a, i0 + k);
+    }
     uint64_t tot;
     (void)block_excl_scan(v, &tot);
     if (threadIdx.x == 0) a.bsum[b] = tot;
@@ -1467,6 +1480,20 @@ int restore(Run &r, int code) {
     return code ? code : r2;
 }
 
+// the device's address of host memory it can read (pinned by hipHostMalloc / registered), or
+// NULL (pageable memory: copied instead)
+const uint32_t *pinned_on_device(const uint32_t *p) {
+    hipPointerAttribute_t at;
+    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable host memory reports an error: clear it
+        return nullptr;
+    }
+    if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+    const char *hp = static_cast<const char *>(at.hostPointer ? at.hostPointer : p);
+    return reinterpret_cast<const uint32_t *>(static_cast<const char *>(at.devicePointer) +
+                                              (reinterpret_cast<const char *>(p) - hp));
+}
+
 // after the first pass B and its wait: input errors, an output region too small, the outputs
 int finish(Run &r) {
     hq_dstep *d = r.d;
@@ -1676,7 +1703,10 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     bool small = true;
     uint64_t total_bytes = 0;
     for (uint32_t x = 0; x < nl && !rc; ++x) {
-        const Run &r = runs[live[x]];
+        Run &r = runs[live[x]];
+        // sizes in pinned host memory are read by k_size_sums over the link: no copy per job
+        // (16 workers' 256 KB size copies took 340 us one after another, with their gaps)
+        r.k.sizes_src = pinned_on_device(r.in->sizes);
         d0->jobs_host[x] = r.k;
         small = small && r.small;
         total_bytes += r.nb;
@@ -1708,7 +1738,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         const Run &r = runs[live[x]];
         char *din = static_cast<char *>(r.d->in);
         if (r.in->groups) h2d(din, r.in->groups, r.n * 4, s);
-        h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
+        if (!r.k.sizes_src) h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
     }
     const JobMap sm = map(0, nl, kSizeTile, 1);
     if (!rc) {

@@ -135,7 +135,8 @@ inline int from16(const hq_event16 *r, uint64_t left, uint64_t ctx[2], hq_event 
     return 1;
 }
 
-__attribute__((always_inline)) inline uint8_t *put_fast(uint8_t *p, uint64_t v) {   // the 1- and 2-byte varints inline
+// the 1- and 2-byte varints inline
+__attribute__((always_inline)) inline uint8_t *put_fast(uint8_t *p, uint64_t v) {
     if (v < 0x80) {
         *p = (uint8_t)v;
         return p + 1;
@@ -193,9 +194,17 @@ __attribute__((always_inline)) inline uint8_t *encode16(uint8_t *p, const hq_eve
         }
     }
     const bool same = r.term == pv.term;
-    *p++ = (uint8_t)(HQ_EV_MESSAGE | code << 3 | ((r.kind & 8) ? 0x40 : 0) | (same ? 0x80 : 0));
-    if (code == 7) p = put(p, r.type);
-    p = put_fast(p, r.from);
+    const uint32_t hdr =
+        HQ_EV_MESSAGE | code << 3 | ((r.kind & 8) ? 0x40u : 0u) | (same ? 0x80u : 0u);
+    if (code != 7 && r.from < 0x80) {   // header and a 1-byte sender in one store
+        const uint16_t w = (uint16_t)(hdr | (uint32_t)r.from << 8);
+        std::memcpy(p, &w, 2);
+        p += 2;
+    } else {
+        *p++ = (uint8_t)hdr;
+        if (code == 7) p = put(p, r.type);
+        p = put_fast(p, r.from);
+    }
     if (!same) p = put(p, r.term);
     pv.term = r.term;
     if (code == 0 || code == 7) p = put_fast(p, r.value);
@@ -206,51 +215,62 @@ __attribute__((always_inline)) inline uint8_t *encode16(uint8_t *p, const hq_eve
     return p;
 }
 
-// groups [g0, g1) encoded at p (room for HQ_EVENT_STREAM_MAX bytes before each event checked
-// against end; a growing scratch passes end = nullptr and grows itself)
-struct Enc16 {
-    const uint64_t *off;
-    const hq_event16 *recs;
-    uint32_t *sizes;
-    uint64_t events = 0;
-    int run(uint64_t g0, uint64_t g1, std::vector<uint8_t> *grow, uint8_t *out, uint64_t cap,
-            uint64_t *bytes) {
-        uint64_t pos = 0;
-        for (uint64_t i = g0; i < g1; ++i) {
-            if (off[i + 1] < off[i]) return HQ_E_INVAL;
-            const uint64_t p0 = pos;
-            uint64_t ne = 0, ctx[2] = {0, 0};
-            Prev pv;
-            // room for the group's records at HQ_EVENT_STREAM_MAX each: no check per event
-            const uint64_t need = (off[i + 1] - off[i]) * HQ_EVENT_STREAM_MAX;
-            if (grow && grow->size() < pos + need)
-                grow->resize(std::max<size_t>(2 * grow->size(), pos + need + (1 << 20)));
-            const bool roomy = grow || (cap >= pos && cap - pos >= need);
-            uint8_t *const base = grow ? grow->data() : out;
-            for (uint64_t k = off[i]; k < off[i + 1]; ++ne) {
-                if (!roomy && (cap < pos || cap - pos < HQ_EVENT_STREAM_MAX)) return HQ_E_STATE;
-                if (!(recs[k].kind & HQ_EV16_FULL)) {
-                    pos = (uint64_t)(encode16(base + pos, recs[k], pv, ctx) - base);
-                    ++k;
-                    continue;
-                }
-                hq_event e;
-                const int used = from16(recs + k, off[i + 1] - k, ctx, e);
-                if (!used) return HQ_E_INVAL;
-                k += used;
-                pos = (uint64_t)(encode(base + pos, e, pv) - base);
-            }
-            if (ne > 0xFFFF || pos - p0 > 0xFFFF) return HQ_E_INVAL;
-            sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
-            events += ne;
+// groups [g0, g1) encoded at out (cap bytes), or into a growing scratch (grow != nullptr); the
+// range's event count and byte count out (locals until the end: threads encoding neighbouring
+// ranges share no written cache line but their ends of `sizes`)
+int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, uint64_t g0,
+                uint64_t g1, std::vector<uint8_t> *grow, uint8_t *out, uint64_t cap,
+                uint64_t *n_events, uint64_t *n_bytes) {
+    uint64_t pos = 0, events = 0;
+    uint8_t *base = grow ? grow->data() : out;
+    for (uint64_t i = g0; i < g1; ++i) {
+        const uint64_t r0 = off[i], r1 = off[i + 1];
+        if (r1 < r0) return HQ_E_INVAL;
+        // room for the group's records at HQ_EVENT_STREAM_MAX each: no check per event
+        const uint64_t need = (r1 - r0) * HQ_EVENT_STREAM_MAX;
+        if (grow && grow->size() < pos + need) {
+            grow->resize(std::max<size_t>(2 * grow->size(), pos + need + (1 << 20)));
+            base = grow->data();
         }
-        *bytes = pos;
-        return HQ_OK;
+        const bool roomy = grow || (cap >= pos && cap - pos >= need);
+        const uint64_t p0 = pos;
+        uint64_t ne = 0, ctx[2] = {0, 0};
+        Prev pv;
+        uint8_t *p = base + pos;
+        for (uint64_t k = r0; k < r1; ++ne) {
+            if (!roomy && (cap < (uint64_t)(p - base) || cap - (uint64_t)(p - base) <
+                                                             HQ_EVENT_STREAM_MAX))
+                return HQ_E_STATE;
+            if (!(recs[k].kind & HQ_EV16_FULL)) {
+                p = encode16(p, recs[k], pv, ctx);
+                ++k;
+                continue;
+            }
+            hq_event e;
+            const int used = from16(recs + k, r1 - k, ctx, e);
+            if (!used) return HQ_E_INVAL;
+            k += used;
+            p = encode(p, e, pv);
+        }
+        pos = (uint64_t)(p - base);
+        if (ne > 0xFFFF || pos - p0 > 0xFFFF) return HQ_E_INVAL;
+        sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
+        events += ne;
     }
-};
+    *n_events = events;
+    *n_bytes = pos;
+    return HQ_OK;
+}
 
-std::mutex g_enc16_mu;                           // one threaded encode at a time
-std::vector<std::vector<uint8_t>> g_enc16_scratch;
+// per-thread scratch of threaded encodes, taken from a pool for the length of a call (calls on
+// several threads run side by side, each on scratch of its own)
+std::mutex g_scratch_mu;
+std::vector<std::vector<std::vector<uint8_t>>> g_scratch_free;
+
+struct alignas(64) RangeOut {   // one thread's results, a cache line each
+    uint64_t events = 0, bytes = 0;
+    int rc = HQ_OK;
+};
 
 }  // namespace
 
@@ -267,18 +287,21 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     const uint64_t nrec = n_groups ? offsets16[n_groups] - offsets16[0] : 0;
     const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(threads, 1u),
                                                     std::max<uint64_t>(1, nrec / 4096));
-    if (T <= 1) {
-        Enc16 enc{offsets16, recs, sizes};
-        const int rc = enc.run(0, n_groups, nullptr, out, cap, n_bytes);
-        *n_events = enc.events;
-        return rc;
-    }
+    if (T <= 1)
+        return enc16_range(offsets16, recs, sizes, 0, n_groups, nullptr, out, cap, n_events,
+                           n_bytes);
     // T ranges of about equal records (group boundaries), each into its own scratch
-    std::lock_guard<std::mutex> lock(g_enc16_mu);
-    if (g_enc16_scratch.size() < T) g_enc16_scratch.resize(T);
-    std::vector<uint64_t> g(T + 1), bytes(T, 0);
-    std::vector<int> rcs(T, HQ_OK);
-    std::vector<Enc16> encs(T, Enc16{offsets16, recs, sizes});
+    std::vector<std::vector<uint8_t>> scratch;
+    {
+        std::lock_guard<std::mutex> lock(g_scratch_mu);
+        if (!g_scratch_free.empty()) {
+            scratch = std::move(g_scratch_free.back());
+            g_scratch_free.pop_back();
+        }
+    }
+    if (scratch.size() < T) scratch.resize(T);
+    std::vector<uint64_t> g(T + 1);
+    std::vector<RangeOut> res(T);
     g[0] = 0;
     g[T] = n_groups;
     for (uint32_t t = 1; t < T; ++t) {
@@ -286,32 +309,38 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
         g[t] = std::max<uint64_t>(g[t - 1], (uint64_t)(std::lower_bound(offsets16, offsets16 + n_groups,
                                                                          want) - offsets16));
     }
+    auto run = [&](uint32_t t) {
+        res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch[t], nullptr, 0,
+                                &res[t].events, &res[t].bytes);
+    };
     std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; ++t)
-        th.emplace_back([&, t] {
-            rcs[t] = encs[t].run(g[t], g[t + 1], &g_enc16_scratch[t], nullptr, 0, &bytes[t]);
-        });
-    rcs[0] = encs[0].run(g[0], g[1], &g_enc16_scratch[0], nullptr, 0, &bytes[0]);
+    for (uint32_t t = 1; t < T; ++t) th.emplace_back(run, t);
+    run(0);
     for (auto &x : th) x.join();
     uint64_t total = 0, events = 0;
+    int rc = HQ_OK;
     for (uint32_t t = 0; t < T; ++t) {
-        if (rcs[t]) return rcs[t];
-        total += bytes[t];
-        events += encs[t].events;
+        if (res[t].rc && !rc) rc = res[t].rc;
+        total += res[t].bytes;
+        events += res[t].events;
     }
-    if (total > cap) return HQ_E_STATE;
-    std::vector<uint64_t> at(T, 0);
-    for (uint32_t t = 1; t < T; ++t) at[t] = at[t - 1] + bytes[t - 1];
-    th.clear();
-    for (uint32_t t = 1; t < T; ++t)
-        th.emplace_back([&, t] {
-            if (bytes[t]) std::memcpy(out + at[t], g_enc16_scratch[t].data(), bytes[t]);
-        });
-    if (bytes[0]) std::memcpy(out, g_enc16_scratch[0].data(), bytes[0]);
-    for (auto &x : th) x.join();
-    *n_events = events;
-    *n_bytes = total;
-    return HQ_OK;
+    if (!rc && total > cap) rc = HQ_E_STATE;
+    if (!rc) {
+        std::vector<uint64_t> at(T, 0);
+        for (uint32_t t = 1; t < T; ++t) at[t] = at[t - 1] + res[t - 1].bytes;
+        th.clear();
+        auto copy = [&](uint32_t t) {
+            if (res[t].bytes) std::memcpy(out + at[t], scratch[t].data(), res[t].bytes);
+        };
+        for (uint32_t t = 1; t < T; ++t) th.emplace_back(copy, t);
+        copy(0);
+        for (auto &x : th) x.join();
+        *n_events = events;
+        *n_bytes = total;
+    }
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
+    g_scratch_free.push_back(std::move(scratch));
+    return rc;
 }
 
 int hq_events_to16(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,

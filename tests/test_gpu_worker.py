@@ -471,6 +471,7 @@ def test_fused_step_jobs_equal_single_steps(hq, wide):
 
     a, b = make(), make()
     empty = np.zeros(0, np.uint8)
+    pin = hq.Context(0)       # sizes in pinned memory are read over the link (k_size_sums)
     try:
         # step 0 lists one group with no events: every output region starts at its 64 KB minimum
         jobs = [hq.SizedStream(np.zeros(1, np.uint32), np.zeros(1, np.uint32), 0, empty)
@@ -482,6 +483,10 @@ def test_fused_step_jobs_equal_single_steps(hq, wide):
             for G, roles, _, implicit in specs:
                 grp, off, ev = bench.step_events(hq, G, s, roles)
                 data, sz = hq.encode_events_sized(off, ev)
+                if s != 1:                                  # pinned sizes (s 1: pageable)
+                    p = pin.pinned(len(sz), np.uint32)
+                    p[:] = sz
+                    sz = p
                 jobs.append(hq.SizedStream(None if implicit else grp, sz, len(ev), data))
             got = hq.step_jobs(list(zip(a, jobs)))          # (the 20000-group job overflows at s 0)
             for i, (res, w) in enumerate(zip(got, b)):
@@ -506,6 +511,7 @@ def test_fused_step_jobs_equal_single_steps(hq, wide):
     finally:
         for w in a + b:
             w.close()
+        pin.close()
 
 
 @pytest.mark.parametrize("stream", [True, False, "sized", "sized-column", "sized-advance"],
