@@ -810,6 +810,8 @@ __global__ __launch_bounds__(256) void k_step_restore(const StepK a) {
 #define HQ_STEP_CHUNKS 4
 #endif
 constexpr int kMaxChunks = HQ_STEP_CHUNKS;
+constexpr int kMaxJobChunks = 8;   // the jobs path's chunks of whole jobs (events per copy stream)
+static_assert(kMaxChunks <= kMaxJobChunks, "the chunk events serve both paths");
 constexpr uint64_t kChunkGroups = 65536;
 // bnd[l] = the scan at l * nw (list l's first record), l = 0 .. kLists
 __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, uint64_t cap,
@@ -1066,7 +1068,11 @@ struct hq_dstep {
     // of chunk c - 1, and its result copy overlaps pass B of chunk c + 1 (compute stream); the
     // copy stream is created by the first such step
     hipStream_t copy = nullptr;
-    hipEvent_t ev_in[kMaxChunks] = {};
+    hipEvent_t ev_in[kMaxJobChunks] = {};
+    // the jobs path's second copy stream (jobs' byte copies alternate between the two, so that
+    // one copy's start-up gap overlaps the other's transfer) and its events
+    hipStream_t copy2 = nullptr;
+    hipEvent_t ev_in2[kMaxJobChunks] = {};
     hipEvent_t ev_sync = nullptr;  // blocking-sync event: a waiting worker thread sleeps
     // the jobs path (hq_dstep_run_jobs, this engine first): the jobs' StepK, pinned and on device
     StepK *jobs_host = nullptr, *jobs_dev = nullptr;
@@ -1125,8 +1131,11 @@ int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming |
                                                                           hipEventBlockingSync),
                            "event");
-    for (int c = 0; c < kMaxChunks && !rc; ++c) {
+    for (int c = 0; c < kMaxJobChunks && !rc; ++c) {
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_in[c], hipEventDisableTiming), "event");
+        if (!rc)
+            rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_in2[c], hipEventDisableTiming),
+                               "event");
     }
     if (!rc) rc = hq::check_hip(ctx, hipMalloc(&d->layout, sizeof(Layout)), "hq_dstep layout");
     if (!rc)
@@ -1152,13 +1161,16 @@ void hq_dstep_close(hq_dstep *d) {
     if (d->host_out) (void)hipHostFree(d->host_out);
     if (d->jobs_host) (void)hipHostFree(d->jobs_host);
     if (d->host_layout) (void)hipHostFree(d->host_layout);
-    if (d->copy) {
-        (void)hipStreamSynchronize(d->copy);
-        (void)hipStreamDestroy(d->copy);
+    for (hipStream_t cs : {d->copy, d->copy2}) {
+        if (cs) {
+            (void)hipStreamSynchronize(cs);
+            (void)hipStreamDestroy(cs);
+        }
     }
     if (d->ev_sync) (void)hipEventDestroy(d->ev_sync);
-    for (int c = 0; c < kMaxChunks; ++c) {
+    for (int c = 0; c < kMaxJobChunks; ++c) {
         if (d->ev_in[c]) (void)hipEventDestroy(d->ev_in[c]);
+        if (d->ev_in2[c]) (void)hipEventDestroy(d->ev_in2[c]);
     }
     delete d;
 }
@@ -1482,16 +1494,17 @@ int restore(Run &r, int code) {
 
 // the device's address of host memory it can read (pinned by hipHostMalloc / registered), or
 // NULL (pageable memory: copied instead)
-const uint32_t *pinned_on_device(const uint32_t *p) {
+template <class T>
+const T *pinned_on_device(const T *p) {
     hipPointerAttribute_t at;
     if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();  // pageable host memory reports an error: clear it
         return nullptr;
     }
     if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
-    const char *hp = static_cast<const char *>(at.hostPointer ? at.hostPointer : p);
-    return reinterpret_cast<const uint32_t *>(static_cast<const char *>(at.devicePointer) +
-                                              (reinterpret_cast<const char *>(p) - hp));
+    const char *hp = static_cast<const char *>(at.hostPointer ? at.hostPointer : (const void *)p);
+    return reinterpret_cast<const T *>(static_cast<const char *>(at.devicePointer) +
+                                       (reinterpret_cast<const char *>(p) - hp));
 }
 
 // after the first pass B and its wait: input errors, an output region too small, the outputs
@@ -1702,11 +1715,23 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     }
     bool small = true;
     uint64_t total_bytes = 0;
+    // every job's bytes in pinned host memory: pass A (and pass B) read them over the link, in
+    // one launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks as below).
+    // ByteReader's aligned 8-byte words never cross a page, so no read leaves the caller's pages;
+    // a kernel launch acquires at system scope, so the host's writes before the call are seen
+    bool zero_copy = true;
+    if (const char *v = std::getenv("HQ_STEP_ZERO_COPY")) zero_copy = std::atoi(v) != 0;
+    const uint8_t *zbytes[kMaxJobs] = {};
+    for (uint32_t x = 0; x < nl && zero_copy; ++x) {
+        zbytes[x] = pinned_on_device(runs[live[x]].in->bytes);
+        zero_copy = zbytes[x] != nullptr || runs[live[x]].nb == 0;
+    }
     for (uint32_t x = 0; x < nl && !rc; ++x) {
         Run &r = runs[live[x]];
         // sizes in pinned host memory are read by k_size_sums over the link: no copy per job
         // (16 workers' 256 KB size copies took 340 us one after another, with their gaps)
         r.k.sizes_src = pinned_on_device(r.in->sizes);
+        if (zero_copy && zbytes[x]) r.k.bytes = zbytes[x];
         d0->jobs_host[x] = r.k;
         small = small && r.small;
         total_bytes += r.nb;
@@ -1732,8 +1757,40 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
             rc = hq::check_hip(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st),
                                "hq_dstep H2D");
     };
-    // handles and sizes on the compute stream, their scan; the bytes on the copy stream in up to
-    // kMaxChunks chunks of whole jobs, pass A of each chunk once its bytes have landed
+    // The jobs' bytes in up to kMaxJobChunks chunks of whole jobs, copied on two copy streams
+    // (jobs alternating: one copy's start-up gap overlaps the other's transfer), event c behind
+    // chunk c on each. Queued in the order the device needs them, since each call takes the host
+    // microseconds: the sizes' scan first (it reads pinned sizes over the link), the copies of
+    // chunks 0 and 1, then pass A of chunk c (once its bytes have landed) before the copies of
+    // chunk c + 2.
+    for (hipStream_t *cs : {&d0->copy, &d0->copy2})
+        if (!rc && !*cs)
+            rc = hq::check_hip(ctx, hipStreamCreateWithFlags(cs, hipStreamNonBlocking),
+                               "hq_dstep copy stream");
+    uint32_t cend[kMaxJobChunks + 1] = {0};
+    int nchunks = 0;
+    if (zero_copy) {              // one chunk of all jobs, nothing to copy
+        cend[nchunks = 1] = nl;
+    } else {
+        uint64_t acc = 0;
+        uint32_t x = 0;
+        while (nchunks < kMaxJobChunks && x < nl) {
+            const uint64_t want = total_bytes * (uint64_t)(nchunks + 1) / kMaxJobChunks;
+            do acc += runs[live[x++]].nb;
+            while (x < nl && (nchunks + 1 == kMaxJobChunks || acc < want));
+            cend[++nchunks] = x;
+        }
+    }
+    auto copies = [&](int c) {
+        if (c >= nchunks || zero_copy) return;
+        for (uint32_t x = cend[c]; x < cend[c + 1]; ++x) {
+            const Run &r = runs[live[x]];
+            h2d(static_cast<char *>(r.d->in) + r.o_ev, r.in->bytes, r.nb,
+                x % 2 ? d0->copy2 : d0->copy);
+        }
+        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in[c], d0->copy), "event");
+        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in2[c], d0->copy2), "event");
+    };
     for (uint32_t x = 0; x < nl; ++x) {
         const Run &r = runs[live[x]];
         char *din = static_cast<char *>(r.d->in);
@@ -1745,6 +1802,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         hipLaunchKernelGGL(k_size_sums, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
         launched("k_size_sums");
     }
+    copies(0);
     if (!rc) {
         hipLaunchKernelGGL(k_bsum_scan, dim3(nl), dim3(1024), 0, s, sm);
         launched("k_bsum_scan");
@@ -1753,26 +1811,13 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         hipLaunchKernelGGL(k_size_apply, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
         launched("k_size_apply");
     }
-    if (!rc && !d0->copy)
-        rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d0->copy, hipStreamNonBlocking),
-                           "hq_dstep copy stream");
-    uint32_t x0 = 0;
-    for (int c = 0; c < kMaxChunks && x0 < nl && !rc; ++c) {
-        // the chunk: jobs until its share of the bytes (the last chunk takes the rest)
-        uint32_t x1 = x0;
-        uint64_t acc = 0;
-        for (uint32_t x = 0; x < x0; ++x) acc += runs[live[x]].nb;
-        const uint64_t want = total_bytes * (uint64_t)(c + 1) / kMaxChunks;
-        do {
-            acc += runs[live[x1]].nb;
-            ++x1;
-        } while (x1 < nl && (c + 1 == kMaxChunks || acc < want));
-        for (uint32_t x = x0; x < x1; ++x) {
-            const Run &r = runs[live[x]];
-            h2d(static_cast<char *>(r.d->in) + r.o_ev, r.in->bytes, r.nb, d0->copy);
+    copies(1);
+    for (int c = 0; c < nchunks && !rc; ++c) {
+        const uint32_t x0 = cend[c], x1 = cend[c + 1];
+        if (!zero_copy) {
+            rc = hq::check_hip(ctx, hipStreamWaitEvent(s, d0->ev_in[c], 0), "wait");
+            if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(s, d0->ev_in2[c], 0), "wait");
         }
-        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in[c], d0->copy), "event");
-        if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(s, d0->ev_in[c], 0), "wait");
         const JobMap m = map(x0, x1, 256, 0);
         if (!rc) rc = hq::pre_launch(ctx);
         if (!rc) {
@@ -1783,7 +1828,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
             rc = hq::post_launch(ctx, "k_step_jobs<count>");
             for (uint32_t x = x0; x < x1 && !rc; ++x) runs[live[x]].stepped = true;
         }
-        x0 = x1;
+        copies(c + 2);
     }
     // every job's layout (one workgroup each), k_step_lite and pass B over all jobs, one wait
     const JobMap am = map(0, nl, 256, 0);
@@ -1804,8 +1849,13 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                                 dim3(256), 0, s, am);
         rc = hq::post_launch(ctx, "k_step_jobs<write>");
     }
-    if (!rc) rc = wait_stream(d0, s, "hq_dstep jobs sync");
-    else (void)hipStreamSynchronize(s);
+    if (!rc) {
+        rc = wait_stream(d0, s, "hq_dstep jobs sync");
+    } else {                      // (a failed launch sequence leaves no copy behind either)
+        (void)hipStreamSynchronize(s);
+        for (hipStream_t cs : {d0->copy, d0->copy2})
+            if (cs) (void)hipStreamSynchronize(cs);
+    }
     const uint64_t t1 = now_ns();
     int first_rc = HQ_OK;
     for (uint32_t x = 0; x < nl; ++x) {

@@ -487,6 +487,10 @@ def test_fused_step_jobs_equal_single_steps(hq, wide):
                     p = pin.pinned(len(sz), np.uint32)
                     p[:] = sz
                     sz = p
+                if s == 2:                                  # pinned bytes: read in place
+                    p = pin.pinned(len(data), np.uint8)
+                    p[:] = data
+                    data = p
                 jobs.append(hq.SizedStream(None if implicit else grp, sz, len(ev), data))
             got = hq.step_jobs(list(zip(a, jobs)))          # (the 20000-group job overflows at s 0)
             for i, (res, w) in enumerate(zip(got, b)):
