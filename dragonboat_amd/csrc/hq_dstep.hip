@@ -205,6 +205,7 @@ __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
 // One group's state and its output cursor. WRITE = false: counting pass on a private copy;
 // WRITE = true: the same sequence writing records and, at the end, the new state.
 constexpr uint32_t kStageReady = 64;   // ReadyToRead records staged per wave in pass B
+constexpr uint32_t kStageBytes = 16384;  // pass A: a workgroup's stream bytes staged in LDS
 
 template <bool WRITE, int MC>   // MC: member slots held in registers (8 or MC)
 struct Engine {
@@ -581,6 +582,10 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
     __shared__ uint32_t wtot[WRITE ? 1 : 256 / 64][kLists];
     if (!WRITE && (threadIdx.x & 63) < kLists) wtot[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     uint64_t i = a.i_begin + blk * 256 + threadIdx.x;
+    // pass A over a stream stages the workgroup's bytes in LDS first (below): every thread takes
+    // part in that, so until then a thread with no group to step clears `act` instead of leaving
+    constexpr bool STAGE = !WRITE && STREAM;
+    bool act = true;
     if (WRITE && (a.layout->error | a.layout->overflow)) return;   // nothing written this time
     if (WRITE && a.layout->commit_column) {
         // the commits are a column (k_step_lite wrote it from pass A's state): pass B takes
@@ -588,10 +593,11 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
         if (i >= a.layout->len[kRerun]) return;
         i = a.rerun_list[i];
     } else if (i >= a.i_end) {
-        return;
+        if (!STAGE) return;
+        act = false;
     }
-    uint64_t e0, e1, b0 = 0, b1 = 0;
-    if (STREAM && a.prefix) {
+    uint64_t e0 = 0, e1 = 0, b0 = 0, b1 = 0;
+    if (act && STREAM && a.prefix) {
         const uint64_t x0 = a.prefix[i], x1 = a.prefix[i + 1];
         e0 = x0 >> 32;
         e1 = x1 >> 32;
@@ -601,9 +607,9 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
             // the sizes' totals must be the ones the copies were sized by (checked once)
             if (i + 1 == a.n && a.own_lo == 0 && (e1 != a.n_events || b1 != a.n_bytes))
                 atomicOr(a.error, (uint32_t)kErrBoffsets);
-            if (b1 < a.own_lo || b1 >= a.own_hi) return;   // another chunk's group
+            if (b1 < a.own_lo || b1 >= a.own_hi) act = false;   // another chunk's group
         }
-    } else {
+    } else if (act) {
         e0 = a.offsets[i];
         e1 = a.offsets[i + 1];
         if (STREAM) {
@@ -611,8 +617,9 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
             b1 = a.boffsets[i + 1];
         }
     }
-    const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;   // NULL: handles 0 .. n - 1
-    if (!WRITE) {                 // validate this group's entry; a bad one is not stepped
+    if (!STAGE && !act) return;
+    const uint32_t h = !act ? 0u : a.handles ? a.handles[i] : (uint32_t)i;   // NULL: 0 .. n - 1
+    if (!WRITE && act) {          // validate this group's entry; a bad one is not stepped
         uint32_t err = 0;
         if (h >= a.n_handles) err |= kErrHandle;
         if (e1 < e0 || (!STREAM && e1 > a.n_events) || (STREAM && a.prefix && e1 > a.n_events))
@@ -624,8 +631,38 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
             atomicOr(a.error, err);
             for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = 0;
             a.rerun[i] = 0;       // not stepped: nothing to restore
-            return;
+            act = false;
         }
+    }
+    // Pass A reads each group's bytes once, a thread per group: the workgroup's groups' bytes
+    // are one contiguous range, loaded into LDS by all its threads in coalesced 16-byte loads
+    // (a zero-copy stream in pinned host memory read lane by lane in 8-byte words crossed the
+    // link at 41 GB/s), each thread then decoding its own from LDS; a range larger than the
+    // buffer is read in place. The aligned 16-byte blocks around the range never leave the
+    // pages of its bytes.
+    const uint8_t *src0 = a.bytes + b0;
+    if constexpr (STAGE) {
+        __shared__ unsigned long long s_lo, s_hi;
+        __shared__ uint4 sbuf[kStageBytes / 16];
+        if (threadIdx.x == 0) {
+            s_lo = ~0ull;
+            s_hi = 0;
+        }
+        __syncthreads();
+        const uint64_t base = reinterpret_cast<uint64_t>(a.bytes);
+        if (act && b1 > b0) {
+            atomicMin(&s_lo, (unsigned long long)(base + b0));
+            atomicMax(&s_hi, (unsigned long long)(base + b1));
+        }
+        __syncthreads();
+        const uint64_t lo = s_lo & ~15ull, hi = (s_hi + 15) & ~15ull;
+        const bool fits = s_hi > s_lo && hi - lo <= kStageBytes;
+        if (fits)
+            for (uint64_t o = threadIdx.x * 16ull; o < hi - lo; o += 256 * 16)
+                sbuf[o / 16] = *reinterpret_cast<const uint4 *>(lo + o);
+        __syncthreads();
+        if (!act) return;
+        if (fits) src0 = reinterpret_cast<const uint8_t *>(sbuf) + (base + b0 - lo);
     }
     hq_dread reads[kDReads];
     Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
@@ -640,7 +677,7 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
         eng.stage_lo = __builtin_amdgcn_readfirstlane(eng.base[kReady]);
     }
     if (STREAM)
-        eng.template run<true>(e0, e1, a.bytes + b0, a.bytes + b1);
+        eng.template run<true>(e0, e1, src0, src0 + (b1 - b0));
     else
         eng.template run<false>(e0, e1, nullptr, nullptr);
     if (staged) {                 // the staged records out, 16 contiguous bytes per lane
