@@ -1544,6 +1544,15 @@ const T *pinned_on_device(const T *p) {
                                        (reinterpret_cast<const char *>(p) - hp));
 }
 
+// HQ_STEP_ZERO_COPY=0 in the environment: pinned streams are copied like pageable ones (A/B)
+bool zero_copy_allowed() {
+    static const bool on = [] {
+        const char *v = std::getenv("HQ_STEP_ZERO_COPY");
+        return !v || std::atoi(v) != 0;
+    }();
+    return on;
+}
+
 // after the first pass B and its wait: input errors, an output region too small, the outputs
 int finish(Run &r) {
     hq_dstep *d = r.d;
@@ -1611,6 +1620,9 @@ int finish(Run &r) {
 int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     *out = hq_dstep_out{};
     if (in->n == 0) return HQ_OK;
+    // (a single step copies its stream in chunks even from pinned memory: the copy engine moves
+    // ~55 GB/s where pass A reading in place over the link reached 45, 1.22 vs 1.35 ms for the
+    // 1 M-group step5; the jobs path reads in place, which spares its per-job copies)
     Run r;
     r.d = d;
     r.in = in;
@@ -1756,8 +1768,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     // one launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks as below).
     // ByteReader's aligned 8-byte words never cross a page, so no read leaves the caller's pages;
     // a kernel launch acquires at system scope, so the host's writes before the call are seen
-    bool zero_copy = true;
-    if (const char *v = std::getenv("HQ_STEP_ZERO_COPY")) zero_copy = std::atoi(v) != 0;
+    bool zero_copy = zero_copy_allowed();
     const uint8_t *zbytes[kMaxJobs] = {};
     for (uint32_t x = 0; x < nl && zero_copy; ++x) {
         zbytes[x] = pinned_on_device(runs[live[x]].in->bytes);

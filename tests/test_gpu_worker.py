@@ -518,6 +518,45 @@ def test_fused_step_jobs_equal_single_steps(hq, wide):
         pin.close()
 
 
+@pytest.mark.parametrize("flags", [{}, {"commit_column": True}, {"commit_advance": True}],
+                         ids=["list", "column", "advance"])
+def test_pinned_sized_stream_equals_pageable(hq, flags):
+    """A sized stream in pinned host memory (copied in chunks by the copy engine, or read in
+    place by the jobs path) decides as the same steps fed from pageable memory — at a size the
+    copy path chunks, with ragged groups from step_events."""
+    import bench
+
+    G = 4 * 65536 + 5
+    roles = bench.STEP_ROLES["step5"]
+    g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
+    nv = sum(r != "observer" for r in roles)
+    a = hq.Worker(0, nv, on_device=True, **flags)
+    b = hq.Worker(0, nv, on_device=True, **flags)
+    pin = hq.Context(0)
+    try:
+        a.add_groups(g, m)
+        b.add_groups(g, m)
+        for s in range(3):
+            grp, off, ev = bench.step_events(hq, G, s, roles)
+            data, sz = hq.encode_events_sized(off, ev)
+            pd, ps = pin.pinned(len(data), np.uint8), pin.pinned(len(sz), np.uint32)
+            pd[:], ps[:] = data, sz
+            got = a.step_sized(None, ps, len(ev), pd)
+            want = b.step_sized(None, sz, len(ev), data)
+            for k, v in want.items():
+                if isinstance(v, np.ndarray):
+                    np.testing.assert_array_equal(got[k], v, err_msg=f"step {s} {k}")
+            assert got.get("n_commits") == want.get("n_commits")
+        for c in (1, G // 2, G):
+            ga, ma = a.get_group(int(cids[c - 1]))[:2]
+            gb, mb = b.get_group(int(cids[c - 1]))[:2]
+            assert ga.tobytes() == gb.tobytes() and ma.tobytes() == mb.tobytes()
+    finally:
+        a.close()
+        b.close()
+        pin.close()
+
+
 @pytest.mark.parametrize("stream", [True, False, "sized", "sized-column", "sized-advance"],
                          ids=["stream", "rows", "sized", "sized-column", "sized-advance"])
 def test_chunked_device_step_equals_host_worker(hq, stream):
