@@ -559,7 +559,15 @@ def engine_ok(w):
             and w["form"] in (0, 2))
 
 
-def run_engine(w, steps, warmup, d: Dist, windows=3):
+def fused_chunks(steps):
+    """The window's batches split into hq_commit_fused_dev launches of at most 32 (the kernel's
+    batch limit), as even as possible: (first, count) per launch."""
+    n = max(1, -(-steps // 32))
+    bounds = [steps * i // n for i in range(n + 1)]
+    return [(bounds[i], bounds[i + 1] - bounds[i]) for i in range(n)]
+
+
+def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
     """A commit workload stepped through the persistent commit engine (hq_engine_*,
     dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps' batches are posted as K
     descriptors and decided by ONE resident launch (no dependent-launch boundary between
@@ -567,7 +575,13 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
     launches (hq_commit_many_dev), so the line carries both on the same data. `windows` windows
     of K = `steps` steps each continue the rotation (>= 1.1 GiB of distinct batches: no step
     re-reads a batch the 256 MiB Infinity Cache could still hold); the median window is reported
-    (the median over repeated timings)."""
+    (the median over repeated timings).
+
+    headline "fused": the line's value and roofline are the window's batches decided by fused
+    launches (hq_commit_fused_dev, up to 32 batches each). Each batch is one step worker's step of
+    1 M groups (the groups are disjoint between batches), so one launch decides the co-resident
+    workers' batches of a step (16 step workers in the reference, internal/settings/hard.go:35,
+    execengine.go:675-690). headline "engine": the resident engine's windows."""
     from dragonboat_amd import hipquorum as hq
     from dragonboat_amd import shard
 
@@ -596,6 +610,7 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
     wins = []
     for k in range(windows):
         a = arr(first + k * steps, steps)
+        fa = [arr(first + k * steps + c0, cn) for c0, cn in fused_chunks(steps)]
         rec = {}
         for mode in ("engine", "launches", "signal", "fused"):
             ctx.sync()
@@ -618,7 +633,8 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
                 clocks = [eng_sig.done_clock(q0 + i) for i in range(steps)]
                 eng_sig.drain()
             elif mode == "fused":
-                ctx.commit_fused_dev(a)
+                for x in fa:
+                    ctx.commit_fused_dev(x)
                 ctx.timing(False)
                 ctx.sync()
             else:
@@ -666,11 +682,21 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
     set0 = [dict(n=w["n"], cid_base=rng.cid_base, cid_stride=rng.cid_stride, count=rng.count,
                  out=outs)]
     engine_eq_launch = all(np.array_equal(x, y) for x, y in zip(outs, launch_outs))
+    # set 0 through a fused launch beside set 1, its outputs poisoned first
+    for x in (b0.committed_out, b0.changed, b0.fallback):
+        ctx.memset(x, 0xA5)
+    ctx.commit_fused_dev(arr(0, 2))
+    ctx.sync()
+    fused_outs = [ctx.download(x) for x in (b0.committed_out, b0.changed, b0.fallback)]
+    fused_eq_launch = all(np.array_equal(x, y) for x, y in zip(fused_outs, launch_outs))
+    if headline == "fused":
+        set0[0]["out"] = fused_outs
     eng.close()
     eng_sig.close()
-    elapsed = med("engine", "elapsed")
-    kernel_s = med("engine", "kernel_s")
-    local = med("engine", "local")
+    hm = "fused" if headline == "fused" else "engine"
+    elapsed = med(hm, "elapsed")
+    kernel_s = med(hm, "kernel_s")
+    local = med(hm, "local")
     achieved_local = per_set / kernel_s / 1e9
     per_gpu = d.gather([groups_per_step(w) * steps / local, kernel_s * 1e6, achieved_local])
     achieved_node = d.sum(achieved_local)
@@ -682,7 +708,7 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
         decisions=total_groups * decisions_per_group(w), nsets=nsets, first_timed_set=first,
         bytes_per_launch=per_set, launches_per_step=1, steps=steps,
         achieved_gbs=achieved_local, achieved_node_gbs=achieved_node, per_gpu=per_gpu,
-        set0=set0, gather=None, windows=len(wins),
+        set0=set0, gather=None, windows=len(wins), headline_mode=hm,
         engine={
             "mode": "persistent commit engine (hq_engine): one resident launch per window of "
                     f"{steps} posted steps", "grid": info.grid, "block": info.block,
@@ -700,8 +726,9 @@ def run_engine(w, steps, warmup, d: Dist, windows=3):
             "value": total_groups * decisions_per_group(w) / med("signal", "elapsed"),
         },
         fused_window={
-            "mode": f"the window's {steps} batches in ONE launch (hq_commit_fused_dev, one "
-                    "workgroup range per batch)",
+            "mode": f"the window's {steps} batches in {len(fused_chunks(steps))} fused launch(es) "
+                    "(hq_commit_fused_dev, one workgroup range per batch, <= 32 batches each)",
+            "fused_equals_launch_set0": fused_eq_launch,
             "window_ms": [round(x["fused"]["elapsed"] * 1e3, 4) for x in wins],
             "median_ms_per_step": med("fused", "elapsed") / steps * 1e3,
             "median_kernel_us_per_step": med("fused", "kernel_s") * 1e6,
@@ -1754,11 +1781,11 @@ def run_rank(args, d, progress):
     """Everything one rank measures: the headline, the extra legs, and (rank 0 at N = 1) the CPU
     baseline. Every rank runs the same legs in the same order (their collectives pair up)."""
     w = WORKLOADS[args.workload]
-    use_engine = args.mode == "engine" and engine_ok(w)
+    use_engine = args.mode in ("engine", "fused") and engine_ok(w)
     progress(f"headline {args.workload}: {args.windows if use_engine else 1} x {args.steps} steps"
-             f" ({'persistent engine' if use_engine else 'launch per step'}), {args.warmup} warmup")
-    r = (run_engine(w, args.steps, args.warmup, d, windows=args.windows) if use_engine
-         else run_gpu(w, args.steps, args.warmup, d))
+             f" ({args.mode if use_engine else 'launch per step'}), {args.warmup} warmup")
+    r = (run_engine(w, args.steps, args.warmup, d, windows=args.windows, headline=args.mode)
+         if use_engine else run_gpu(w, args.steps, args.warmup, d))
     r["world"] = d.world
     from dragonboat_amd import hipquorum as hq
 
@@ -1882,7 +1909,9 @@ def report(args, d, res, launcher):
         "data": f"synthetic: device-generated splitmix64 batches, {r['nsets']} distinct per GPU "
                 f"rotated (>= 1.1 GiB); timed steps start at batch {r['first_timed_set']}"
                 + (f"; {r['windows']} timed windows of {args.steps} steps, the median window "
-                   f"reported (every window in engine.window_ms)" if r.get("windows") else ""),
+                   f"reported (every window in "
+                   f"{'fused_window' if r.get('headline_mode') == 'fused' else 'engine'}"
+                   f".window_ms)" if r.get("windows") else ""),
         "config": {
             "workload": args.workload,
             "desc": w["desc"],
@@ -1903,7 +1932,9 @@ def report(args, d, res, launcher):
             "traffic_source": traffic_src,
             "kernel_avg_us": r["avg_kernel_s"] * 1e6,
             "algorithmic_bytes_per_launch": r["bytes_per_launch"],
-            "kernel_time": ("HIP events around the resident engine launch of the median "
+            "kernel_time": ("HIP events around the fused launch(es) of the median window, / "
+                            "steps" if r.get("headline_mode") == "fused" else
+                            "HIP events around the resident engine launch of the median "
                             "window (posted steps + STOP), / steps" if r.get("engine") else
                             "HIP events on the launch stream around the timed launches "
                             "(back to back), / launches"),
@@ -1989,10 +2020,12 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="engine", choices=("engine", "launch"),
-                    help="headline commit steps through the persistent engine (one resident "
-                         "launch per window; uniform tiled term-start / mask workloads) or one "
-                         "launch per step")
+    ap.add_argument("--mode", default="fused", choices=("fused", "engine", "launch"),
+                    help="headline commit steps: the co-resident step workers' batches fused "
+                         "into launches of up to 32 (fused), the persistent engine (one resident "
+                         "launch per window), or one launch per step; fused and engine apply to "
+                         "uniform tiled term-start / mask workloads, others take launches. All "
+                         "three are timed on the same windows and reported")
     ap.add_argument("--windows", type=int, default=3,
                     help="timed windows of --steps steps (engine mode); the median is reported")
     ap.add_argument("--step-groups", type=int, default=1 << 20,

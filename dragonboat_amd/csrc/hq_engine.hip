@@ -1025,6 +1025,47 @@ extern "C" int hq_exp_engine_probe(hq_engine *e, uint64_t *out) {
                                                                                          : HQ_E_DEVICE;
 }
 
+// V7: the claim512 shape plus a shared pool: per batch, the last `pool` tiles are claimed by
+// any wave of the grid from one device counter (the next claim issued before the current tile
+// is decided) once its workgroup's own range of the batch is exhausted; fast workgroups take
+// more of the pool, so the slowest one no longer sets the window
+template <int N, int FORM, int LEAD, int BLK>
+__global__ __launch_bounds__(BLK, 8) void k_exp_pool(const MultiK m, uint32_t *ctr, uint32_t pool) {
+    __shared__ uint32_t claim[kExpMax];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kExpMax; i += BLK) claim[i] = 0;
+    __syncthreads();
+    const uint64_t S = m.ntiles - pool;   // the static part
+    const uint64_t per = (S + gridDim.x - 1) / gridDim.x;
+    const uint64_t base = blockIdx.x * per;
+    const uint64_t end = base + per < S ? base + per : S;
+    for (uint32_t c = 0; c < m.count; ++c) {
+        CommitK k{};
+        k.G = m.G;
+        k.stride = m.stride;
+        k.match = m.tiles[c];
+        k.cout = m.cout[c];
+        k.changed = m.chg[c];
+        k.fallback = m.fb[c];
+        k.R = m.R;
+        for (;;) {
+            uint32_t t = 0;
+            if (lane == 0) t = __hip_atomic_fetch_add(&claim[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (base + t >= end) break;
+            commit_tile<N, FORM, false, LEAD, false>(k, (base + t) * HQ_TILE_GROUPS, lane);
+        }
+        uint32_t nxt = 0;
+        if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            const uint32_t i = __builtin_amdgcn_readfirstlane(nxt);
+            if (i >= pool) break;
+            if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            commit_tile<N, FORM, false, LEAD, false>(k, (S + i) * HQ_TILE_GROUPS, lane);
+        }
+    }
+}
+
 extern "C" int hq_exp_multi(hq_ctx *ctx, const hq_commit_args *a, uint32_t count, int variant,
                             uint32_t grid) {
     if (!ctx || !a || count == 0 || count > (uint32_t)kExpMax) return HQ_E_INVAL;
@@ -1050,6 +1091,14 @@ extern "C" int hq_exp_multi(hq_ctx *ctx, const hq_commit_args *a, uint32_t count
         m.waves = grid * 16;
         hipLaunchKernelGGL((k_exp_loop<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid), dim3(1024), 0,
                            ctx->stream, m);
+    } else if (variant == 7) {
+        static uint32_t *ctr = nullptr;
+        if (!ctr && hipMalloc(&ctr, 4 * kExpMax) != hipSuccess) return HQ_E_NOMEM;
+        (void)hipMemsetAsync(ctr, 0, 4 * kExpMax, ctx->stream);
+        const char *pv = std::getenv("AB_POOL");   // permille of a batch's tiles in the pool
+        const uint32_t pool = (uint32_t)((uint64_t)m.ntiles * (pv ? std::atoi(pv) : 250) / 1000);
+        hipLaunchKernelGGL((k_exp_pool<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid ? grid : 512),
+                           dim3(1024), 0, ctx->stream, m, ctr, pool);
     } else if (variant == 6) {
         static uint32_t *ctr = nullptr;
         if (!ctr && hipMalloc(&ctr, 4 * kExpMax * 1024) != hipSuccess) return HQ_E_NOMEM;

@@ -95,7 +95,7 @@ def test_thread_dist_collectives(n):
 def _args(**kw):
     a = dict(gpus=2, steps=5, warmup=1, workload=bench.HEADLINE, step_groups=1 << 10,
              step_steps=2, no_cpu=True, no_extra_parity=True, extra="", detail_out=None,
-             mode="engine", windows=3)
+             mode="fused", windows=3)
     a.update(kw)
     return argparse.Namespace(**a)
 
@@ -194,3 +194,14 @@ def test_host_cores_reports_counts():
     assert visible >= 1 and 1 <= usable <= visible
     allc, counts = bench.cpu_thread_counts()
     assert counts[0] == allc and counts[-1] == 1 and 1 <= allc <= usable
+
+
+def test_fused_chunks_cover_the_window():
+    """The fused headline's launches: at most 32 batches each (hq_commit_fused_dev's limit), as
+    even as possible, covering the window once in order."""
+    for steps in (1, 2, 20, 32, 33, 64, 400):
+        ch = bench.fused_chunks(steps)
+        assert ch[0][0] == 0 and all(n <= 32 for _, n in ch)
+        assert all(a + n == b for (a, n), (b, _) in zip(ch, ch[1:]))
+        assert ch[-1][0] + ch[-1][1] == steps and len(ch) == -(-steps // 32)
+        assert max(n for _, n in ch) - min(n for _, n in ch) <= 1

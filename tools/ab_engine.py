@@ -60,6 +60,8 @@ def main():
         "claim512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 4, 512)),
         "claim512x2": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 5, 1024)),
         "gclaim512": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 6, 512)),
+        # claim512 + a shared pool of the last AB_POOL permille tiles per batch (device claims)
+        "pool": lambda a: ctx._check(hq.lib.hq_exp_multi(ctx.h, a, K, 7, 512)),
         "engine": None,
         "engine512": None,
     }
@@ -104,7 +106,7 @@ def main():
     # correctness of the experiment kernels: set 0 decided by each equals the launch path
     ref = None
     for name in [x for x in ("launches", "loop512", "flat", "claim256", "claim512", "claim512x2",
-                             "gclaim512")
+                             "gclaim512", "pool")
                  if x in variants]:
         b = sets[0][0]
         ctx.memset(b.committed_out, 0xA5)
