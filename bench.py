@@ -630,7 +630,9 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
                 q0 = eng_sig.post(a)
                 eng_sig.wait(q0 + steps - 1)       # the last step's flag: every step complete
                 sig_local = time.perf_counter() - t0
-                clocks = [eng_sig.done_clock(q0 + i) for i in range(steps)]
+                # (the engine keeps the clocks of its last `depth` steps)
+                nclk = min(steps, eng_sig.info().depth)
+                clocks = [eng_sig.done_clock(q0 + i) for i in range(steps - nclk, steps)]
                 eng_sig.drain()
             elif mode == "fused":
                 for x in fa:
@@ -650,7 +652,7 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
                 nl, ms = eng_sig.timing(reset=True)
                 local = sig_local
                 # device clock (100 MHz) between the first and the last step's completion
-                kernel_s = (clocks[-1] - clocks[0]) / 1e8 / max(1, steps - 1)
+                kernel_s = (clocks[-1] - clocks[0]) / 1e8 / max(1, len(clocks) - 1)
             elif mode == "fused":
                 ms, nl = ctx.timing_read()
                 kernel_s = ms / 1e3 / max(1, steps)        # one launch for the window's steps

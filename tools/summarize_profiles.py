@@ -37,6 +37,19 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2,
           "c4t3": "k_bits3<256>", "c4p": "k_planes<256>"}
 
 
+# headline workloads decided by fused launches (bench.py --mode fused): a dispatch holds several
+# batches, grid threads per batch below; the kernel time and the counters are per batch (a step)
+FUSED_THREADS_PER_BATCH = {"c3mtl": 524288}
+KERNEL_FUSED = {"c3mtl": "k_commit_fused<2, 1024, 2>"}
+
+
+def per_batch(path, kernel, tpb, value_key, grid_key):
+    """sum over the kernel's dispatches of value / sum of their batches (grid / tpb)."""
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    batches = sum(int(r[grid_key]) // tpb for r in rows)
+    return sum(value_key(r) for r in rows) / batches, len(rows), batches
+
+
 def counter(path, kernel):
     rows = list(csv.DictReader(open(path)))
     vals = [float(r["Counter_Value"]) for r in rows if kernel in r["Kernel_Name"]]
@@ -51,6 +64,34 @@ def main():
     traffic = json.load(open(tj)) if os.path.exists(tj) else {}
     for w in workloads:
         src = os.path.join(ROOT, "gpurun_out", f"prof_{w}")
+        if w in FUSED_THREADS_PER_BATCH:
+            tpb, k = FUSED_THREADS_PER_BATCH[w], KERNEL_FUSED[w]
+            for f, name in (("trace/run_kernel_stats.csv", f"{w}_kernel_stats.csv"),
+                            ("trace/run_kernel_trace.csv", f"{w}_kernel_trace.csv"),
+                            ("pmc_FETCH_SIZE/run_counter_collection.csv", f"{w}_pmc_FETCH_SIZE.csv"),
+                            ("pmc_WRITE_SIZE/run_counter_collection.csv", f"{w}_pmc_WRITE_SIZE.csv")):
+                shutil.copy(os.path.join(src, f), os.path.join(dst, name))
+            ns, nd, nb = per_batch(os.path.join(dst, f"{w}_kernel_trace.csv"), k, tpb,
+                                   lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                   "Grid_Size_X")
+            fetch, nf, _ = per_batch(os.path.join(dst, f"{w}_pmc_FETCH_SIZE.csv"), k, tpb,
+                                     lambda r: float(r["Counter_Value"]), "Grid_Size")
+            write, nw, _ = per_batch(os.path.join(dst, f"{w}_pmc_WRITE_SIZE.csv"), k, tpb,
+                                     lambda r: float(r["Counter_Value"]), "Grid_Size")
+            traffic[w] = {
+                "kernel": k, "rocprof_avg_ns": ns, "rocprof_calls": nd, "rocprof_batches": nb,
+                "fetch_size_kb_median": fetch, "write_size_kb_median": write,
+                "dispatches": min(nf, nw),
+                "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+                "per": "batch (one step of 1 M groups; a fused dispatch decides several)",
+                "correction": "(2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE halves 16B/lane "
+                              "streams)",
+                "round": rnd,
+                "source": f"profiles/{rnd}/{w}_pmc_FETCH_SIZE.csv + {w}_pmc_WRITE_SIZE.csv "
+                          f"(kernel time: {w}_kernel_trace.csv, per batch)",
+            }
+            print(w, json.dumps(traffic[w]))
+            continue
         ks = KERNEL[w] if isinstance(KERNEL[w], tuple) else (KERNEL[w],)   # a step's kernels
         k = " + ".join(ks)
         shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
