@@ -716,7 +716,10 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
                     f"{steps} posted steps", "grid": info.grid, "block": info.block,
             "window_ms": [round(x["engine"]["elapsed"] * 1e3, 4) for x in wins],
             "window_kernel_us_per_step": [round(x["engine"]["kernel_s"] * 1e6, 3) for x in wins],
-            "median_kernel_us_per_step": kernel_s * 1e6,
+            "median_kernel_us_per_step": med("engine", "kernel_s") * 1e6,
+            "median_ms_per_step": med("engine", "elapsed") / steps * 1e3,
+            "value": total_groups * decisions_per_group(w) / med("engine", "elapsed"),
+            "frac": d.sum(per_set / med("engine", "kernel_s") / 1e9) / (HBM_PEAK_GBS * d.world),
             "engine_equals_launch_set0": engine_eq_launch,
         },
         engine_signal={
