@@ -25,6 +25,7 @@
 // no state: k_step_restore puts the saved state back.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <new>
 
@@ -657,9 +658,20 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
         __syncthreads();
         const uint64_t lo = s_lo & ~15ull, hi = (s_hi + 15) & ~15ull;
         const bool fits = s_hi > s_lo && hi - lo <= kStageBytes;
-        if (fits)
-            for (uint64_t o = threadIdx.x * 16ull; o < hi - lo; o += 256 * 16)
-                sbuf[o / 16] = *reinterpret_cast<const uint4 *>(lo + o);
+        if (fits) {               // every load issued before the first LDS store: one round
+            constexpr int kU = kStageBytes / (256 * 16);   // trip over the link, not kU
+            uint4 v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t o = (threadIdx.x + 256ull * u) * 16;
+                if (o < hi - lo) v[u] = *reinterpret_cast<const uint4 *>(lo + o);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t o = (threadIdx.x + 256ull * u) * 16;
+                if (o < hi - lo) sbuf[o / 16] = v[u];
+            }
+        }
         __syncthreads();
         if (!act) return;
         if (fits) src0 = reinterpret_cast<const uint8_t *>(sbuf) + (base + b0 - lo);
@@ -1727,6 +1739,12 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     hq_dstep *d0 = ds[0];
     hq_ctx *ctx = d0->ctx;
     hipStream_t s = ctx->stream;
+    // HQ_STEP_JOBS_TRACE=1: the host phases of each call to stderr (where a step's time goes)
+    static const bool trace = [] {
+        const char *v = std::getenv("HQ_STEP_JOBS_TRACE");
+        return v && std::atoi(v) != 0;
+    }();
+    uint64_t tp[6] = {now_ns(), 0, 0, 0, 0, 0};
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     Run runs[kMaxJobs];
     uint32_t live[kMaxJobs], nl = 0;
@@ -1750,6 +1768,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         if (!rcs[j]) live[nl++] = j;
     }
     if (!nl) return rc;
+    tp[1] = now_ns();
     // the jobs' StepK, pinned and copied to the device ahead of the launches
     if (!rc && nl > d0->jobs_cap) {
         if (d0->jobs_host) (void)hipHostFree(d0->jobs_host);
@@ -1786,6 +1805,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     }
     if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
                                                     hipMemcpyHostToDevice, s), "hq_dstep jobs");
+    tp[2] = now_ns();
     // maps of jobs [x0, x1) onto workgroups of `per` groups (+ extra elements per job)
     auto map = [&](uint32_t x0, uint32_t x1, uint64_t per, uint64_t extra) {
         JobMap m{};
@@ -1897,6 +1917,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                                 dim3(256), 0, s, am);
         rc = hq::post_launch(ctx, "k_step_jobs<write>");
     }
+    tp[3] = now_ns();
     if (!rc) {
         rc = wait_stream(d0, s, "hq_dstep jobs sync");
     } else {                      // (a failed launch sequence leaves no copy behind either)
@@ -1913,6 +1934,14 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         r.t1 = t1;
         rcs[live[x]] = finish(r);
         if (rcs[live[x]] && !first_rc) first_rc = rcs[live[x]];
+    }
+    if (trace) {
+        tp[4] = t1;
+        tp[5] = now_ns();
+        std::fprintf(stderr, "hq_dstep_run_jobs %u jobs: prepare %.1f us, pointers + table %.1f, "
+                             "submit %.1f, wait %.1f, outputs %.1f\n", nl,
+                     (tp[1] - tp[0]) / 1e3, (tp[2] - tp[1]) / 1e3, (tp[3] - tp[2]) / 1e3,
+                     (tp[4] - tp[3]) / 1e3, (tp[5] - tp[4]) / 1e3);
     }
     return first_rc;
 }

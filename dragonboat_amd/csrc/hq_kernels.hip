@@ -5,6 +5,8 @@
 // integer min/max networks and popcounts in registers, and bitmap outputs are assembled with
 // wave-wide __ballot (64-bit on wave64). No LDS and no MFMA: nothing here is reused or a
 // contraction (DESIGN.md "Kernels").
+#include <cstdlib>
+
 #include "hq_internal.h"
 #include "hq_commit_body.h"
 
@@ -2324,129 +2326,155 @@ __device__ __forceinline__ void ce_pk(uint32_t &a, uint32_t &b) {
 
 // KM >= K_max ctx slots in registers: every (ctx, voter) load of the lane is issued before the
 // first sorting network (K_max and n_max are uniform, so the guards are scalar branches; with the
-// loads inside the per-ctx branches each ctx waited for its own round trip)
+// loads inside the per-ctx branches each ctx waited for its own round trip). The lane's two
+// groups' loads (ri_load) and their decision (ri_decide) are written apart; a software-pipelined
+// form that issued the next tile's loads before deciding the current one (2, 4 or 8 tiles per
+// wave at 3 waves per SIMD) was no faster: 50.6-53.3 vs 50.3-51.5 us, profiles/r04b/ab_rimt.log.
+template <bool PERK, bool PERN, int KM>
+struct RiIn {
+    u64x2 idx[KM];
+    uint32_t ov[KM][8];
+    uint32_t kk, nn;              // PERK / PERN: the two groups' K / n bytes
+};
+
+template <bool PERK, bool PERN, int KM, bool TILED>
+__device__ __forceinline__ void ri_load(const RiMultiK &a, uint64_t wbase, int lane,
+                                        RiIn<PERK, PERN, KM> &in) {
+    const uint64_t g = wbase + 2 * (uint64_t)lane;
+    // TILED: the wave's 128 groups are one tile (wbase is a multiple of 128); rows of 128
+    // entries, this lane's two groups at entries 2 lane, 2 lane + 1
+    const uint8_t *tb = TILED ? a.tiles + (wbase >> 7) * a.tile_bytes : nullptr;
+    const uint64_t ord_bytes = (uint64_t)a.K_max * a.n_max * 256;
+    in.kk = in.nn = 0;
+    if (g >= a.G) return;         // columns: G is even, g + 1 < G too; tiles: padded rows
+    if constexpr (PERK)
+        in.kk = TILED ? *reinterpret_cast<const uint16_t *>(tb + ord_bytes + a.K_max * 1024ull +
+                                                           2 * lane)
+                      : *reinterpret_cast<const uint16_t *>(a.np + g);
+    if constexpr (PERN)
+        in.nn = TILED ? *reinterpret_cast<const uint16_t *>(tb + ord_bytes + a.K_max * 1024ull +
+                                                           (PERK ? 128 : 0) + 2 * lane)
+                      : *reinterpret_cast<const uint16_t *>(a.nv + g);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        in.idx[k] = (u64x2){0, 0};
+        if (k < (int)a.K_max) {
+            in.idx[k] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(
+                TILED ? tb + ord_bytes + k * 1024ull + 16 * lane
+                      : reinterpret_cast<const uint8_t *>(a.idx + (uint64_t)k * a.G + g)));
+#pragma unroll
+            for (int sl = 0; sl < 8; ++sl) {
+                in.ov[k][sl] = 0xFFFFFFFFu;
+                if (sl < (int)a.n_max)
+                    in.ov[k][sl] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
+                        TILED ? tb + ((uint64_t)k * a.n_max + sl) * 256 + 4 * lane
+                              : reinterpret_cast<const uint8_t *>(
+                                    a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g)));
+            }
+        }
+    }
+}
+
+template <bool PERK, bool PERN, int KM, bool TILED>
+__device__ __forceinline__ void ri_decide(const RiMultiK &a, uint64_t wbase, int lane,
+                                          const RiIn<PERK, PERN, KM> &in) {
+    const uint64_t g = wbase + 2 * (uint64_t)lane;
+    bool fb0 = false, fb1 = false;
+    if (g < a.G) {
+        uint32_t K0 = a.K_max, K1 = a.K_max, n0 = a.n_uniform, n1 = a.n_uniform;
+        if constexpr (PERK) {
+            K0 = in.kk & 0xFF;
+            K1 = in.kk >> 8;
+        }
+        if constexpr (PERN) {
+            n0 = in.nn & 0xFF;
+            n1 = in.nn >> 8;
+        }
+        fb0 = n0 < 1 || n0 > a.n_max || K0 > a.K_max;
+        fb1 = n1 < 1 || n1 > a.n_max || K1 > a.K_max;
+        // padding of the voters >= n, per half (0xFFFF = never acked)
+        const int r0 = n0 / 2 > 1 ? (int)(n0 / 2) : 1, r1 = n1 / 2 > 1 ? (int)(n1 / 2) : 1;
+        u64x2 idx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) idx[k] = k < KM ? in.idx[k < KM ? k : 0] : (u64x2){0, 0};
+        const uint32_t kmax = K0 > K1 ? K0 : K1;
+        uint32_t t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            t[k] = 0xFFFFFFFFu;
+            if (k < KM && k < (int)kmax && k < (int)a.K_max) {
+                if (k > 0) {   // addRequest: index moved backward
+                    fb0 |= k < (int)K0 && idx[k].x < idx[k - 1].x;
+                    fb1 |= k < (int)K1 && idx[k].y < idx[k - 1].y;
+                }
+                uint32_t v[8];
+#pragma unroll
+                for (int sl = 0; sl < 8; ++sl)
+                    v[sl] = in.ov[k < KM ? k : 0][sl] | (sl < (int)n0 ? 0u : 0xFFFFu) |
+                            (sl < (int)n1 ? 0u : 0xFFFF0000u);
+                sort8(v, [](uint32_t &x, uint32_t &y) { ce_pk(x, y); });
+                // reach time: the max(q-1, 1)-th smallest first-ack ordinal (readindex.go:84)
+                uint32_t tk = 0;
+#pragma unroll
+                for (int sl = 0; sl < 8; ++sl) {
+                    const uint32_t m = (sl == r0 - 1 ? 0xFFFFu : 0u) |
+                                       (sl == r1 - 1 ? 0xFFFF0000u : 0u);
+                    tk |= v[sl] & m;
+                }
+                t[k] = tk;
+            }
+        }
+        // suffix-min scan per group (ties go to the earlier ctx, as in k_ri_multi)
+        uint32_t bt0 = 0xFFFFu, bt1 = 0xFFFFu, rel0 = 0, rel1 = 0, be0 = 0, be1 = 0;
+        uint64_t bi0 = 0, bi1 = 0;
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {
+            const uint32_t t0 = t[k] & 0xFFFFu, t1 = t[k] >> 16;
+            const bool in0 = !fb0 && k < (int)K0, in1 = !fb1 && k < (int)K1;
+            bool own0 = false, own1 = false;
+            if (in0 && t0 != 0xFFFFu && t0 <= bt0) { bt0 = t0; bi0 = idx[k].x; own0 = true; }
+            if (in1 && t1 != 0xFFFFu && t1 <= bt1) { bt1 = t1; bi1 = idx[k].y; own1 = true; }
+            const bool rl0 = in0 && bt0 != 0xFFFFu, rl1 = in1 && bt1 != 0xFFFFu;
+            rel0 += rl0;
+            rel1 += rl1;
+            be0 |= (uint32_t)(rl0 && own0) << k;
+            be1 |= (uint32_t)(rl1 && own1) << k;
+            if (k < (int)a.K_max) {
+                uint64_t *r = a.rel + (uint64_t)k * a.G + g;
+                if (!TILED || g + 1 < a.G) {
+                    *reinterpret_cast<u64x2 *>(r) = (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
+                } else {
+                    r[0] = rl0 ? bi0 : ~0ull;   // odd G: the tile's padding group has no slot
+                }
+            }
+        }
+        if (!TILED || g + 1 < a.G) {
+            *reinterpret_cast<uint16_t *>(a.cnt + g) = (uint16_t)(rel0 | (rel1 << 8));
+            if (a.bend) *reinterpret_cast<uint16_t *>(a.bend + g) = (uint16_t)(be0 | (be1 << 8));
+        } else {
+            a.cnt[g] = (uint8_t)rel0;
+            if (a.bend) a.bend[g] = (uint8_t)be0;
+            fb1 = false;
+        }
+    }
+    const uint64_t f0 = __ballot(fb0), f1 = __ballot(fb1);
+    if (a.fallback && lane < 2) {
+        const uint32_t sh = 32 * lane;
+        const uint64_t w = (wbase >> 6) + lane;
+        if (w < (a.G + 63) >> 6)
+            a.fallback[w] = spread32((uint32_t)(f0 >> sh)) | (spread32((uint32_t)(f1 >> sh)) << 1);
+    }
+}
+
 template <bool PERK, bool PERN, int KM, bool TILED = false>
 __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint64_t step = (uint64_t)gridDim.x * kBlock * 2;
     for (uint64_t wbase = wave * 128; wbase < a.G; wbase += step) {
-        const uint64_t g = wbase + 2 * (uint64_t)lane;
-        // TILED: the wave's 128 groups are one tile (wbase is a multiple of 128); rows of 128
-        // entries, this lane's two groups at entries 2 lane, 2 lane + 1
-        const uint8_t *tb = TILED ? a.tiles + (wbase >> 7) * a.tile_bytes : nullptr;
-        const uint64_t ord_bytes = (uint64_t)a.K_max * a.n_max * 256;
-        bool fb0 = false, fb1 = false;
-        if (g < a.G) {   // columns: G is even, g + 1 < G too; tiles: padded rows
-            uint32_t K0 = a.K_max, K1 = a.K_max, n0 = a.n_uniform, n1 = a.n_uniform;
-            if constexpr (PERK) {
-                const uint32_t kk = TILED ? *reinterpret_cast<const uint16_t *>(
-                                                tb + ord_bytes + a.K_max * 1024ull + 2 * lane)
-                                          : *reinterpret_cast<const uint16_t *>(a.np + g);
-                K0 = kk & 0xFF;
-                K1 = kk >> 8;
-            }
-            if constexpr (PERN) {
-                const uint32_t nn =
-                    TILED ? *reinterpret_cast<const uint16_t *>(tb + ord_bytes + a.K_max * 1024ull +
-                                                               (PERK ? 128 : 0) + 2 * lane)
-                          : *reinterpret_cast<const uint16_t *>(a.nv + g);
-                n0 = nn & 0xFF;
-                n1 = nn >> 8;
-            }
-            fb0 = n0 < 1 || n0 > a.n_max || K0 > a.K_max;
-            fb1 = n1 < 1 || n1 > a.n_max || K1 > a.K_max;
-            // padding of the voters >= n, per half (0xFFFF = never acked)
-            const int r0 = n0 / 2 > 1 ? (int)(n0 / 2) : 1, r1 = n1 / 2 > 1 ? (int)(n1 / 2) : 1;
-            u64x2 idx[8];
-            uint32_t ov[KM][8];
-#pragma unroll
-            for (int k = 0; k < KM; ++k) {
-                idx[k] = (u64x2){0, 0};
-                if (k < (int)a.K_max) {
-                    idx[k] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(
-                        TILED ? tb + ord_bytes + k * 1024ull + 16 * lane
-                              : reinterpret_cast<const uint8_t *>(a.idx + (uint64_t)k * a.G + g)));
-#pragma unroll
-                    for (int sl = 0; sl < 8; ++sl) {
-                        ov[k][sl] = 0xFFFFFFFFu;
-                        if (sl < (int)a.n_max)
-                            ov[k][sl] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
-                                TILED ? tb + ((uint64_t)k * a.n_max + sl) * 256 + 4 * lane
-                                      : reinterpret_cast<const uint8_t *>(
-                                            a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g)));
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = KM; k < 8; ++k) idx[k] = (u64x2){0, 0};
-            const uint32_t kmax = K0 > K1 ? K0 : K1;
-            uint32_t t[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                t[k] = 0xFFFFFFFFu;
-                if (k < KM && k < (int)kmax && k < (int)a.K_max) {
-                    if (k > 0) {   // addRequest: index moved backward
-                        fb0 |= k < (int)K0 && idx[k].x < idx[k - 1].x;
-                        fb1 |= k < (int)K1 && idx[k].y < idx[k - 1].y;
-                    }
-                    uint32_t v[8];
-#pragma unroll
-                    for (int sl = 0; sl < 8; ++sl)
-                        v[sl] = ov[k < KM ? k : 0][sl] | (sl < (int)n0 ? 0u : 0xFFFFu) |
-                                (sl < (int)n1 ? 0u : 0xFFFF0000u);
-                    sort8(v, [](uint32_t &a, uint32_t &b) { ce_pk(a, b); });
-                    // reach time: the max(q-1, 1)-th smallest first-ack ordinal (readindex.go:84)
-                    uint32_t tk = 0;
-#pragma unroll
-                    for (int sl = 0; sl < 8; ++sl) {
-                        const uint32_t m = (sl == r0 - 1 ? 0xFFFFu : 0u) |
-                                           (sl == r1 - 1 ? 0xFFFF0000u : 0u);
-                        tk |= v[sl] & m;
-                    }
-                    t[k] = tk;
-                }
-            }
-            // suffix-min scan per group (ties go to the earlier ctx, as in k_ri_multi)
-            uint32_t bt0 = 0xFFFFu, bt1 = 0xFFFFu, rel0 = 0, rel1 = 0, be0 = 0, be1 = 0;
-            uint64_t bi0 = 0, bi1 = 0;
-#pragma unroll
-            for (int k = 7; k >= 0; --k) {
-                const uint32_t t0 = t[k] & 0xFFFFu, t1 = t[k] >> 16;
-                const bool in0 = !fb0 && k < (int)K0, in1 = !fb1 && k < (int)K1;
-                bool own0 = false, own1 = false;
-                if (in0 && t0 != 0xFFFFu && t0 <= bt0) { bt0 = t0; bi0 = idx[k].x; own0 = true; }
-                if (in1 && t1 != 0xFFFFu && t1 <= bt1) { bt1 = t1; bi1 = idx[k].y; own1 = true; }
-                const bool rl0 = in0 && bt0 != 0xFFFFu, rl1 = in1 && bt1 != 0xFFFFu;
-                rel0 += rl0;
-                rel1 += rl1;
-                be0 |= (uint32_t)(rl0 && own0) << k;
-                be1 |= (uint32_t)(rl1 && own1) << k;
-                if (k < (int)a.K_max) {
-                    uint64_t *r = a.rel + (uint64_t)k * a.G + g;
-                    if (!TILED || g + 1 < a.G) {
-                        *reinterpret_cast<u64x2 *>(r) = (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
-                    } else {
-                        r[0] = rl0 ? bi0 : ~0ull;   // odd G: the tile's padding group has no slot
-                    }
-                }
-            }
-            if (!TILED || g + 1 < a.G) {
-                *reinterpret_cast<uint16_t *>(a.cnt + g) = (uint16_t)(rel0 | (rel1 << 8));
-                if (a.bend) *reinterpret_cast<uint16_t *>(a.bend + g) = (uint16_t)(be0 | (be1 << 8));
-            } else {
-                a.cnt[g] = (uint8_t)rel0;
-                if (a.bend) a.bend[g] = (uint8_t)be0;
-                fb1 = false;
-            }
-        }
-        const uint64_t f0 = __ballot(fb0), f1 = __ballot(fb1);
-        if (a.fallback && lane < 2) {
-            const uint32_t sh = 32 * lane;
-            const uint64_t w = (wbase >> 6) + lane;
-            if (w < (a.G + 63) >> 6)
-                a.fallback[w] = spread32((uint32_t)(f0 >> sh)) | (spread32((uint32_t)(f1 >> sh)) << 1);
-        }
+        RiIn<PERK, PERN, KM> in;
+        ri_load<PERK, PERN, KM, TILED>(a, wbase, lane, in);
+        ri_decide<PERK, PERN, KM, TILED>(a, wbase, lane, in);
     }
 }
 

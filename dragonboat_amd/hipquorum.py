@@ -1492,15 +1492,23 @@ class StepJobs:
             self.arr[j].worker = w.h
             self.arr[j].out = ctypes.cast(ctypes.pointer(self.outs[j]), _vp)
 
-    def run(self, copy=True):
+    def execute(self):
+        """The native call alone (hq_worker_step_jobs); results() then reads the outputs."""
         rc = lib.hq_worker_step_jobs(self.arr, len(self.jobs))
         if rc != HQ_OK:
             bad = [j for j in range(len(self.jobs)) if self.arr[j].rc != HQ_OK]
             msg = lib.hq_worker_last_error(self.jobs[bad[0]][0].h).decode() if bad \
                 else "a worker listed twice"
             raise HQError(rc, f"hq_worker_step_jobs: {msg}")
+
+    def results(self, copy=True):
+        """One result dict per job (as Worker.step) of the last execute()."""
         return [Worker._results(o, copy, len(a[1]) if isinstance(a, SizedStream) else len(a[0]))
                 for o, (_, a) in zip(self.outs, self.jobs)]
+
+    def run(self, copy=True):
+        self.execute()
+        return self.results(copy)
 
 
 def step_jobs(jobs, copy=True):
