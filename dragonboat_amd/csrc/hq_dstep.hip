@@ -1318,7 +1318,7 @@ struct Run {
 
 // The step's buffers (grown as needed) and its StepK, with the memsets it needs queued on s; no
 // launch. in->n > 0.
-int prepare(Run &r, hipStream_t s) {
+int prepare(Run &r, hipStream_t s, bool jobs = false) {
     hq_dstep *d = r.d;
     hq_ctx *ctx = d->ctx;
     const hq_dstep_in *in = r.in;
@@ -1392,10 +1392,13 @@ int prepare(Run &r, hipStream_t s) {
                      PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n});
     uint64_t *prefix = reinterpret_cast<uint64_t *>(din + r.o_boff);
     uint32_t *wsum = d->wsum;
-    if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, r.tmp, wsum, d->scan,
-                                                                       ws, s),
-                                "hipcub scan size");
-    if (!rc && sized)
+    // (the jobs path scans with its own kernels: no hipcub temporary, whose size query costs
+    // microseconds of host time per job before the first launch)
+    if (!rc && !jobs)
+        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, r.tmp, wsum, d->scan,
+                                                                  ws, s),
+                           "hipcub scan size");
+    if (!rc && sized && !jobs)
         rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, r.tmp2, packed_sizes,
                                                                   prefix, n + 1, s),
                            "hipcub scan size");
@@ -1764,7 +1767,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         r.d = ds[j];
         r.in = &ins[j];
         r.out = &outs[j];
-        rcs[j] = prepare(r, s);
+        rcs[j] = prepare(r, s, true);
         if (!rcs[j]) live[nl++] = j;
     }
     if (!nl) return rc;
@@ -1783,22 +1786,16 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     }
     bool small = true;
     uint64_t total_bytes = 0;
-    // every job's bytes in pinned host memory: pass A (and pass B) read them over the link, in
-    // one launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks as below).
-    // ByteReader's aligned 8-byte words never cross a page, so no read leaves the caller's pages;
-    // a kernel launch acquires at system scope, so the host's writes before the call are seen
-    bool zero_copy = zero_copy_allowed();
-    const uint8_t *zbytes[kMaxJobs] = {};
-    for (uint32_t x = 0; x < nl && zero_copy; ++x) {
-        zbytes[x] = pinned_on_device(runs[live[x]].in->bytes);
-        zero_copy = zbytes[x] != nullptr || runs[live[x]].nb == 0;
-    }
+    // (a stream read in place: ByteReader's aligned 8-byte words and the staging's aligned 16-byte
+    // blocks never cross a page, so no read leaves the caller's pages; a kernel launch acquires
+    // at system scope, so the host's writes before the call are seen)
+    // (the streams' pointers are checked after the sizes' scan is queued: the checks cost the
+    // host ~1 us each, and the scan does not read the streams)
     for (uint32_t x = 0; x < nl && !rc; ++x) {
         Run &r = runs[live[x]];
         // sizes in pinned host memory are read by k_size_sums over the link: no copy per job
         // (16 workers' 256 KB size copies took 340 us one after another, with their gaps)
         r.k.sizes_src = pinned_on_device(r.in->sizes);
-        if (zero_copy && zbytes[x]) r.k.bytes = zbytes[x];
         d0->jobs_host[x] = r.k;
         small = small && r.small;
         total_bytes += r.nb;
@@ -1837,6 +1834,40 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                                "hq_dstep copy stream");
     uint32_t cend[kMaxJobChunks + 1] = {0};
     int nchunks = 0;
+    bool zero_copy = false;
+    // the sizes' first pass before anything else the device can start on
+    for (uint32_t x = 0; x < nl; ++x) {
+        const Run &r = runs[live[x]];
+        char *din = static_cast<char *>(r.d->in);
+        if (r.in->groups) h2d(din, r.in->groups, r.n * 4, s);
+        if (!r.k.sizes_src) h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
+    }
+    const JobMap sm = map(0, nl, kSizeTile, 1);
+    if (!rc) {
+        hipLaunchKernelGGL(k_size_sums, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
+        launched("k_size_sums");
+    }
+    if (!rc) {
+        // every job's stream in pinned host memory: pass A (and pass B) read it in place, in one
+        // launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks). The table
+        // is sent again with the streams' device addresses (ordered behind k_size_sums, which
+        // does not read them; the first copy may already carry them)
+        zero_copy = zero_copy_allowed();
+        const uint8_t *zbytes[kMaxJobs] = {};
+        for (uint32_t x = 0; x < nl && zero_copy; ++x) {
+            zbytes[x] = pinned_on_device(runs[live[x]].in->bytes);
+            zero_copy = zbytes[x] != nullptr || runs[live[x]].nb == 0;
+        }
+        if (zero_copy) {
+            for (uint32_t x = 0; x < nl; ++x) {
+                Run &r = runs[live[x]];
+                if (zbytes[x]) r.k.bytes = zbytes[x];
+                d0->jobs_host[x].bytes = r.k.bytes;
+            }
+            rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
+                                                   hipMemcpyHostToDevice, s), "hq_dstep jobs");
+        }
+    }
     if (zero_copy) {              // one chunk of all jobs, nothing to copy
         cend[nchunks = 1] = nl;
     } else {
@@ -1859,17 +1890,6 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in[c], d0->copy), "event");
         if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in2[c], d0->copy2), "event");
     };
-    for (uint32_t x = 0; x < nl; ++x) {
-        const Run &r = runs[live[x]];
-        char *din = static_cast<char *>(r.d->in);
-        if (r.in->groups) h2d(din, r.in->groups, r.n * 4, s);
-        if (!r.k.sizes_src) h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
-    }
-    const JobMap sm = map(0, nl, kSizeTile, 1);
-    if (!rc) {
-        hipLaunchKernelGGL(k_size_sums, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
-        launched("k_size_sums");
-    }
     copies(0);
     if (!rc) {
         hipLaunchKernelGGL(k_bsum_scan, dim3(nl), dim3(1024), 0, s, sm);
