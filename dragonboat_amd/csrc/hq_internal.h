@@ -40,6 +40,9 @@ struct hq_ctx {
     uint32_t bin_launch_chunks = 4096;
     uint32_t bin_grid = 256;      // persistent workgroups of the binned ingest (HQ_BIN_GRID)
     uint32_t bin_tpb_shift = 6;   // its largest region, 2^shift tiles (HQ_BIN_TPB: A/B)
+    // k_apply's workgroup: 1024 threads with up to 128 KB of rows (one per CU), or 512 with up to
+    // 64 KB (two per CU, HQ_BIN_APPLY_T=512: A/B)
+    uint32_t bin_apply_threads = 1024;
     // host readback of the fallback count (hq_commit etc.)
 };
 

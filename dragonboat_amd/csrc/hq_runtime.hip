@@ -124,6 +124,10 @@ int hq_open(int device, uint32_t flags, hq_ctx **out) {
         const int v = std::atoi(tp);
         if (v >= 0 && v <= 6) ctx->bin_tpb_shift = (uint32_t)v;
     }
+    if (const char *at = std::getenv("HQ_BIN_APPLY_T")) {
+        const int v = std::atoi(at);
+        if (v == 512 || v == 1024) ctx->bin_apply_threads = (uint32_t)v;
+    }
     if (const char *c = std::getenv("HQ_BIN_LAUNCH_CHUNKS")) {
         const int v = std::atoi(c);
         if (v >= 1 && v <= 4096) ctx->bin_launch_chunks = (uint32_t)v;

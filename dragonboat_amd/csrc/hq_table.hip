@@ -449,9 +449,15 @@ __device__ __forceinline__ bool bin_apply(const TableK &t, uint32_t R, uint64_t 
 constexpr int kApplyEnt = 6;                              // entries per thread and round
 constexpr uint32_t kApplyLds = 128 * 1024;                // a bucket's rows in k_apply's LDS
 constexpr int kApplyRows = (int)(kApplyLds / 16 / kBinThreads);  // row pairs per thread (8)
+// T threads per k_apply workgroup: a bucket's rows take up to kApplyRows * 16 * T bytes of LDS
+// (T = 1024: 128 KB, one workgroup per CU; T = 512: 64 KB, two per CU, so that one's latency
+// phases can overlap the other's streaming)
+template <int T>
+constexpr uint32_t apply_lds() { return (uint32_t)kApplyRows * 16 * T; }
 
 // the rows of bucket b (tile-major; row r < nr = match slot r + 1, row nr = lastIndex for lags)
 // into registers, every load at once
+template <int T>
 __device__ __forceinline__ void apply_load_rows(const TableK &t, const BinK &bk, uint32_t b,
                                                 u64x2 (&rv)[kApplyRows]) {
     const uint64_t tile0 = (uint64_t)b << bk.tpb_shift;
@@ -459,7 +465,7 @@ __device__ __forceinline__ void apply_load_rows(const TableK &t, const BinK &bk,
     const uint32_t R = bk.rows, pairs = nt * R * 64;
 #pragma unroll
     for (int k = 0; k < kApplyRows; ++k) {   // unconditional loads (see bin_load), clamped
-        uint32_t w = threadIdx.x + (uint32_t)k * kBinThreads;
+        uint32_t w = threadIdx.x + (uint32_t)k * T;
         w = w < pairs ? w : pairs - 1;
         const uint32_t tl = w / (R * 64), r = (w / 64) % R, x = 2 * (w % 64);
         const uint32_t src = r < t.nr ? r : t.nr + 1;
@@ -474,8 +480,8 @@ __device__ __forceinline__ void apply_load_rows(const TableK &t, const BinK &bk,
 // buckets share — an entry segment that straddles them, a meta row — are served by that XCD's L2
 // once); the next bucket's rows are loaded while this one's entries are applied and its rows
 // written back
-template <bool LAG>
-__global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64_t *n_skipped) {
+template <bool LAG, int T = kBinThreads>
+__global__ __launch_bounds__(T) void k_apply(TableK t, BinK bk, uint64_t *n_skipped) {
     extern __shared__ uint64_t lds[];
     uint64_t *rows = lds;                                                    // [nt][R][128]
     const uint32_t tid = threadIdx.x, R = bk.rows;
@@ -485,18 +491,18 @@ __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64
     uint32_t j = blockIdx.x / 8;
     u64x2 rv[kApplyRows];
     BIN_T(1, 0);
-    if (j < per && x * per + j < bk.B) apply_load_rows(t, bk, x * per + j, rv);
+    if (j < per && x * per + j < bk.B) apply_load_rows<T>(t, bk, x * per + j, rv);
     for (; j < per && x * per + j < bk.B; j += W) {
         const uint32_t b = x * per + j;
         const uint64_t tile0 = (uint64_t)b << bk.tpb_shift;
         const uint32_t nt = (uint32_t)min((uint64_t)1 << bk.tpb_shift, bk.ntiles - tile0);
         const uint32_t pairs = nt * R * 64;
         // every chunk's (offset, count) of this bucket into LDS: one load round for all of them
-        for (uint32_t c = tid; c < bk.nchunks; c += kBinThreads)
+        for (uint32_t c = tid; c < bk.nchunks; c += T)
             M[c] = HQ_BIN_AB >= 2 ? 0u : bk.meta[(uint64_t)c * bk.B + b];
 #pragma unroll
         for (int k = 0; k < kApplyRows; ++k) {
-            const uint32_t w = tid + (uint32_t)k * kBinThreads;
+            const uint32_t w = tid + (uint32_t)k * T;
             if (w < pairs) {
                 const uint32_t tl = w / (R * 64), r = (w / 64) % R, xx = 2 * (w % 64);
                 rows[(tl * R + r) * kT + xx] = rv[k].x;
@@ -512,7 +518,7 @@ __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64
         // (HQ_APPLY_SEG = 64: a whole wave per segment, for chunks of 16 Ki records)
         constexpr uint32_t kSeg = HQ_APPLY_SEG;
         const uint32_t wv = tid >> 6, h = kSeg == 32 ? (tid >> 5) & 1 : 0, l = tid & (kSeg - 1);
-        constexpr uint32_t kHalves = (64 / kSeg) * kBinThreads / 64;   // segments in flight
+        constexpr uint32_t kHalves = (64 / kSeg) * T / 64;   // segments in flight
         for (uint32_t c0 = 0; c0 < bk.nchunks; c0 += kHalves * NE) {
             uint32_t m[NE];
             uint64_t ent[NE];
@@ -545,12 +551,12 @@ __global__ __launch_bounds__(kBinThreads) void k_apply(TableK t, BinK bk, uint64
         }
         // the next bucket's rows, in flight while these are written back (issued after this
         // bucket's entry loads: the in-order load counter would make those wait for them)
-        if (j + W < per && b + W < bk.B) apply_load_rows(t, bk, b + W, rv);
+        if (j + W < per && b + W < bk.B) apply_load_rows<T>(t, bk, b + W, rv);
         lds_barrier();
         if (j == blockIdx.x / 8) BIN_T(1, 2);
         // the match rows back
         const uint32_t mpairs = nt * t.nr * 64;
-        for (uint32_t w = tid; w < mpairs; w += kBinThreads) {
+        for (uint32_t w = tid; w < mpairs; w += T) {
             const uint32_t tl = w / (t.nr * 64), r = (w / 64) % t.nr, xx = 2 * (w % 64);
             u64x2 v;
             v.x = rows[(tl * R + r) * kT + xx];
@@ -691,9 +697,11 @@ bool bin_plan(const hq_ctx *ctx, const TableK &t, uint64_t count, bool lag, BinK
     const size_t meta_lds = 4 * (size_t)bk.nchunks;
     uint32_t sh = std::min<uint32_t>(HQ_BIN_TPB_SHIFT, ctx->bin_tpb_shift);   // <= 64 tiles
                                                        // (16-bit entry keys)
+    const size_t cap = ctx->bin_apply_threads == 512 ? apply_lds<512>() : apply_lds<kBinThreads>();
+    const size_t per_cu = ctx->bin_apply_threads == 512 ? 80 * 1024 : 160 * 1024;
     auto fits = [&](uint32_t sh) {
         const size_t rows = (size_t)bk.rows << (10 + sh);
-        return rows <= kApplyLds && rows + meta_lds <= 160 * 1024;
+        return rows <= cap && rows + meta_lds <= per_cu;
     };
     while (sh > 0 && !fits(sh)) --sh;
     if (!fits(sh)) return false;
@@ -731,7 +739,9 @@ int ingest_binned(hq_ctx *ctx, const char *what, const uint64_t *u, uint64_t cou
     bk.meta = reinterpret_cast<uint32_t *>(bk.ent + (size_t)bk.nchunks * kBinChunk);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_bin<LAG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_apply<LAG>),
+    const bool half = ctx->bin_apply_threads == 512;
+    (void)hipFuncSetAttribute(half ? reinterpret_cast<const void *>(&k_apply<LAG, 512>)
+                                   : reinterpret_cast<const void *>(&k_apply<LAG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_apply);
     const uint64_t per = (uint64_t)bk.nchunks * kBinChunk;   // records per launch pair
     for (uint64_t r0 = 0; r0 < count; r0 += per) {
@@ -744,9 +754,13 @@ int ingest_binned(hq_ctx *ctx, const char *what, const uint64_t *u, uint64_t cou
         int rc = hq::post_launch(ctx, what);
         if (!rc) rc = hq::pre_launch(ctx);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_apply<LAG>, dim3(8 * std::min<uint32_t>((b.B + 7) / 8,
-                                                                     ctx->bin_grid / 8)),
-                           dim3(kBinThreads), lds_apply, ctx->stream, t, b, n_skipped);
+        const dim3 ag(8 * std::min<uint32_t>((b.B + 7) / 8, ctx->bin_grid / 8));
+        if (half)
+            hipLaunchKernelGGL((k_apply<LAG, 512>), ag, dim3(512), lds_apply, ctx->stream, t, b,
+                               n_skipped);
+        else
+            hipLaunchKernelGGL(k_apply<LAG>, ag, dim3(kBinThreads), lds_apply, ctx->stream, t, b,
+                               n_skipped);
         rc = hq::post_launch(ctx, what);
         if (rc) return rc;
         if (r0 + per < count && (rc = hq::pre_launch(ctx))) return rc;
