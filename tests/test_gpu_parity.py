@@ -320,15 +320,32 @@ def test_commit_fused_buckets(gpu_ctx, hq, form, sizes):
 
 
 def test_commit_fused_unfusable_batches(gpu_ctx, hq):
-    """Batches that cannot share a launch (per-group n, more than 8, one batch) are launched
-    separately with the same results."""
-    sizes = [(3, 5000), (5, 4000), (7, 3000)] * 3            # 9 batches
+    """Batches that cannot share a launch (per-group n, more than 32, one batch) are launched
+    separately with the same results; 32 still share one launch."""
+    sizes = [(3, 5000), (5, 4000), (7, 3000)] * 11           # 33 batches: one too many
     bs, want = _fused_buckets(gpu_ctx, hq, 2, sizes)
+    gpu_ctx.timing_reset()
+    gpu_ctx.timing(True)
     gpu_ctx.commit_fused_dev(hq.commit_batch_array([d["args"] for d in bs]))
     gpu_ctx.sync()
+    gpu_ctx.timing(False)
+    assert gpu_ctx.timing_read()[1] == 33                     # a launch per batch
     for d, (wo, wc, wf) in zip(bs, want):
         np.testing.assert_array_equal(gpu_ctx.download(d["out"])[:len(wo)], wo)
         np.testing.assert_array_equal(gpu_ctx.download(d["chg"]), wc)
+    for d in bs:                                              # 32 of them: one launch
+        for x in (d["out"], d["chg"]):
+            gpu_ctx.memset(x, 0xA5)
+    gpu_ctx.timing_reset()
+    gpu_ctx.timing(True)
+    gpu_ctx.commit_fused_dev(hq.commit_batch_array([d["args"] for d in bs[:32]]))
+    gpu_ctx.sync()
+    gpu_ctx.timing(False)
+    assert gpu_ctx.timing_read()[1] == 1
+    for d, (wo, wc, wf) in zip(bs[:32], want):
+        np.testing.assert_array_equal(gpu_ctx.download(d["out"])[:len(wo)], wo)
+        np.testing.assert_array_equal(gpu_ctx.download(d["chg"]), wc)
+    for d in bs:
         for b in d["bufs"]:
             gpu_ctx.free(b)
     inp = qref.CommitInputs(qref.spec(SEED + 50, 7777, 7, mixed_n=True, parity_extras=True))

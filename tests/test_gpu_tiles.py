@@ -128,6 +128,34 @@ def test_tiled_fused_buckets_equal_separate(gpu_ctx, hq, form, layout):
         hq.free_commit(gpu_ctx, b)
 
 
+def test_headline_window_in_one_fused_launch(gpu_ctx, hq):
+    """The bench headline's shape (bench.py --mode fused): 20 batches of 5-voter groups in the
+    mask form over leader-row tiles, disjoint groups per batch, decided by ONE launch; each batch
+    equals the oracle (at 1/16 of the bench's 1 M groups per batch)."""
+    n, form, lay, G = 5, hq.HQ_FORM_TERM_MASK, hq.HQ_LAYOUT_TILES_LEADER, 65_536
+    bufs = []
+    for k in range(20):
+        b = hq.alloc_commit(gpu_ctx, G, n, form, 16, tiled=True, tile_layout=lay)
+        gpu_ctx.synth_commit_dev(hq.synth_spec(SEED + 300 + k, G, n, parity_extras=True),
+                                 b.args())
+        gpu_ctx.tile_commit_dev(b.args(), b.tiles, lay)
+        bufs.append(b)
+    gpu_ctx.timing_reset()
+    gpu_ctx.timing(True)
+    gpu_ctx.commit_fused_dev(hq.commit_batch_array([b.tile_args() for b in bufs]))
+    gpu_ctx.sync()
+    gpu_ctx.timing(False)
+    assert gpu_ctx.timing_read()[1] == 1
+    for k, b in enumerate(bufs):
+        inp = qref.CommitInputs(qref.spec(SEED + 300 + k, G, n, parity_extras=True))
+        want_out, want_chg, want_fb, rc = inp.run(form, False, nthreads=8)
+        assert rc == 0
+        np.testing.assert_array_equal(gpu_ctx.download(b.committed_out), want_out)
+        np.testing.assert_array_equal(gpu_ctx.download(b.changed), want_chg)
+        np.testing.assert_array_equal(gpu_ctx.download(b.fallback), want_fb)
+        hq.free_commit(gpu_ctx, b)
+
+
 @pytest.mark.parametrize("layout", [1, 2])
 def test_tiled_host_entry_point(gpu_ctx, hq, layout):
     """hq_commit with host tiles: one H2D block, same decisions."""
