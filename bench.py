@@ -1336,6 +1336,66 @@ def _median(xs):
     return float(np.median(xs)) if xs else None
 
 
+_MIX_C1, _MIX_C2 = np.uint64(0xbf58476d1ce4e5b9), np.uint64(0x94d049bb133111eb)
+_READY_K = (np.uint64(0x9e3779b97f4a7c15), np.uint64(0xc2b2ae3d27d4eb4f),
+            np.uint64(0x165667b19e3779f9))
+
+
+def mix64(z):
+    """splitmix64's finalizer over a u64 array (qref_mix64, oracle/qref.h)."""
+    z = (z ^ (z >> np.uint64(30))) * _MIX_C1
+    z = (z ^ (z >> np.uint64(27))) * _MIX_C2
+    return z ^ (z >> np.uint64(31))
+
+
+def ready_digest(ready):
+    """Sum over ReadyToRead records (READY_DTYPE) of qref_digest_ready, mod 2^64."""
+    if len(ready) == 0:
+        return 0
+    k1, k2, k3 = _READY_K
+    t = mix64(mix64(ready["cluster_id"]) ^ (ready["index"] * k1 + ready["ctx_low"] * k2 +
+                                             ready["ctx_high"] * k3))
+    return int(t.sum(dtype=np.uint64))
+
+
+class CommitMirror:
+    """The committed index of every group of one step-leg mode, advanced from that mode's
+    results, so each step's commits reduce to (cluster, advance) pairs whatever form the worker
+    returned them in ('committed_advance', 'committed_column' or the 'commits' list); their
+    digest is qref_digest_commit's sum (oracle/qref.h)."""
+
+    def __init__(self, cids, committed, bounds):
+        assert np.all(cids[1:] > cids[:-1])         # sorted: the commits list maps by search
+        self.cids, self.bounds = cids, bounds
+        self.coef = mix64(cids) | np.uint64(1)
+        self.c = committed.astype(np.uint64).copy()
+
+    def step(self, res):
+        """(commits, ReadyToReads, sum of advances, ready digest, commit digest) of one step."""
+        n_c = n_r = adv_sum = rd = cd = 0
+        for i, r in enumerate(res):
+            lo, hi = self.bounds[i], self.bounds[i + 1]
+            if "committed_advance" in r:
+                ix = np.arange(lo, hi)
+                adv = r["committed_advance"][:hi - lo].astype(np.uint64)
+            elif "committed_column" in r:
+                ix = np.arange(lo, hi)
+                adv = r["committed_column"][:hi - lo] - self.c[lo:hi]
+            else:
+                cm = r["commits"]
+                ix = np.searchsorted(self.cids, cm["cluster_id"])
+                assert np.array_equal(self.cids[ix], cm["cluster_id"])
+                adv = cm["committed"] - self.c[ix]
+            self.c[ix] += adv
+            n_c += int(r.get("n_commits", len(r["commits"])))
+            adv_sum += int(adv.sum(dtype=np.uint64))
+            cd += int((self.coef[ix] * adv).sum(dtype=np.uint64))
+            n_r += len(r["ready"])
+            rd += ready_digest(r["ready"])
+        m = (1 << 64) - 1
+        return (n_c, n_r, adv_sum & m, rd & m, cd & m)
+
+
 def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     """The device step engine (hq_worker_step_stream, HQ_WORKER_ON_DEVICE: every event of the
     step taken on the GPU) over G leader groups per GPU, W = 1, 2 and 16 workers (dragonboat runs
@@ -1353,8 +1413,10 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
 
     Beside it the CPU event-by-event replay of the reference path (oracle/qref_step.c) over the
     same rows of the same steps, on all usable host cores, 16 threads and 1 thread. Every step's
-    commit count, ReadyToRead count and the sum of the committed advances of all groups must
-    agree between every mode and the replay."""
+    commit count, ReadyToRead count, sum of the committed advances and the content digests of
+    (cluster, advance) over the groups that committed and of the ReadyToRead records (cluster,
+    index, ctx) (CommitMirror; qref_step_totals, oracle/qref.h) must agree between every mode
+    and the replay."""
     from concurrent.futures import ThreadPoolExecutor
 
     from dragonboat_amd import hipquorum as hq
@@ -1391,7 +1453,9 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                  for o, e0, e1 in parts] for _ in range(2)]
         modes[W] = dict(parts=parts, bufs=bufs, nbytes=[[0] * W, [0] * W], dev=workers(),
                         e2e=workers(), t={"dev": [], "e2e": []}, bytes=0,
-                        check={"dev": [], "e2e": []})
+                        check={"dev": [], "e2e": []},
+                        mirror={k: CommitMirror(cids, g["committed"], bounds)
+                                for k in ("dev", "e2e")})
     pool = ThreadPoolExecutor(max(Ws) + 1)
 
     def encode(W, i, slot):
@@ -1411,13 +1475,6 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             (wk, hq.SizedStream(None, mo["bufs"][slot][i][1], mo["parts"][i][2] - mo["parts"][i][1],
                                 mo["bufs"][slot][i][0][:mo["nbytes"][slot][i]]))
             for i, wk in enumerate(mo[which])])
-
-    def digest(res):     # (commits, ReadyToReads, sum of committed advances) of one step
-        c = sum(int(r.get("n_commits", len(r["commits"]))) for r in res)
-        adv = sum(int(r["committed_advance"].sum(dtype=np.uint64)) for r in res
-                  if "committed_advance" in r)
-        ok = all("committed_advance" in r or r.get("n_commits", 0) == 0 for r in res)
-        return (c, sum(len(r["ready"]) for r in res), adv if ok else None)
 
     cpus = {}
     if with_cpu and d.rank == 0 and d.world == 1:
@@ -1447,7 +1504,9 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             dt = time.perf_counter() - t0
             if s >= STEP_WARM:
                 ts.append(dt)
-            dg.append((tot["commits"], tot["ready"], tot["committed_sum"] - prev_sum))
+            dg.append((tot["commits"], tot["ready"],
+                       (tot["committed_sum"] - prev_sum) & ((1 << 64) - 1),
+                       tot["ready_digest"], tot["commit_digest"]))
         if cpus:
             prev_sum = tot["committed_sum"]
         rows.set(s + 1)                # untimed: step s + 1's messages arrive
@@ -1462,7 +1521,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             t0 = time.perf_counter()
             j.execute()
             dt = time.perf_counter() - t0
-            mo["check"]["dev"].append(digest(j.results(copy=False)))
+            mo["check"]["dev"].append(mo["mirror"]["dev"].step(j.results(copy=False)))
             j = jobs(W, slot, "e2e")
             d.barrier()
             t1 = time.perf_counter()
@@ -1472,7 +1531,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                 f.result()
             fut.result()
             dt2 = time.perf_counter() - t1
-            mo["check"]["e2e"].append(digest(j.results(copy=False)))
+            mo["check"]["e2e"].append(mo["mirror"]["e2e"].step(j.results(copy=False)))
             if s >= STEP_WARM:
                 mo["t"]["dev"].append(dt)
                 mo["t"]["e2e"].append(dt2)
@@ -1483,13 +1542,28 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     for W in Ws:
         for which in ("dev", "e2e"):
             committed[(W, which)] = [int(modes[W][which][0].get_group(int(c))[0]["committed"])
-                                     for c in cids[:min(1024, G // W)]]
+                                     for c in cids[:min(1024, G // max(Ws))]]
             for wk in modes[W][which]:
                 wk.close()
     pin.close()
     ref = modes[1]["check"]["dev"]
     same_modes = all(modes[W]["check"][k] == ref for W in Ws for k in ("dev", "e2e")) and \
         len(set(map(tuple, committed.values()))) == 1
+    mismatch = []
+    if not same_modes:        # the first differing step of each mode, for the log
+        for W in Ws:
+            for k in ("dev", "e2e"):
+                got = modes[W]["check"][k]
+                bad = [i for i, (a, b) in enumerate(zip(got, ref)) if a != b]
+                if bad or len(got) != len(ref):
+                    i = bad[0] if bad else min(len(got), len(ref))
+                    mismatch.append({"mode": f"{k}_w{W}", "step": i,
+                                     "got": list(got[i]) if i < len(got) else None,
+                                     "want": list(ref[i]) if i < len(ref) else None})
+        c1 = committed[(1, "dev")]
+        mismatch += [{"mode": f"{k}_w{W}", "committed_differs_at": next(
+            (i for i, (a, b) in enumerate(zip(v, c1)) if a != b), len(v))}
+            for (W, k), v in committed.items() if v != c1]
     members = ", ".join(f"{roles.count(r)} {r}" for r in ("remote", "witness", "observer")
                         if roles.count(r))
     ev_total = n_events * timed
@@ -1514,6 +1588,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                                for W in Ws for k in ("dev", "e2e")},
         "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
         "modes_agree": same_modes,
+        **({"modes_mismatch": mismatch} if mismatch else {}),
         "producer": f"compact 16-byte message records (hq_event16) encoded by "
                     f"hq_events16_encode_sized on {enc_threads} native threads per step "
                     f"(max(1, {enc_threads} // W) per worker)",
@@ -1527,10 +1602,14 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         digs = [dg for _, _, dg in cpus.values()]
         out["cpu_replay"] = dict(cpu, sample=f"the same rows of the same {timed} timed steps "
                                              "replayed event by event (oracle/qref_step.c)")
-        out["parity_committed"] = bool(all(x == digs[0] for x in digs) and
-                                       [x[:2] for x in digs[0]] == [x[:2] for x in ref] and
-                                       all(a[2] == b[2] for a, b in zip(digs[0], ref)
-                                           if b[2] is not None) and same_modes)
+        # every step: commit and ReadyToRead counts, the sum of the committed advances and the
+        # content digests of (cluster, advance) and of the ReadyToRead records (cluster, index,
+        # ctx), equal between the replay at every thread count, and every device mode
+        out["parity_committed"] = bool(all(x == digs[0] for x in digs) and digs[0] == ref and
+                                       same_modes)
+        out["parity_checks"] = ("per step: commits, ReadyToReads, committed advance sum, "
+                                "digest of (cluster, advance) and of ReadyToRead (cluster, "
+                                "index, ctx)")
         out["vs_cpu_replay_end_to_end"] = {k: v / best for k, v in e2e.items()}
         out["vs_cpu_replay_device_only"] = {k: v / best for k, v in dev.items()}
         for b, _, _ in cpus.values():

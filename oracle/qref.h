@@ -303,7 +303,30 @@ int qref_group_set_log(qref_group *g, uint64_t first_minus_1, int n_runs, const 
  * qref_group_step; the list is split over nthreads threads. Totals of the outputs go to *tot. */
 typedef struct qref_step_totals {
     uint64_t commits, ready, resps, states, dropped, deferred, committed_sum;
+    /* order-free content digests (sums of qref_digest_* over the step's outputs, so any split
+     * of the list over threads, workers or GPUs adds up to the same value): every ReadyToRead
+     * record (cluster, index, ctx) and every group whose committed index moved (cluster,
+     * advance) */
+    uint64_t ready_digest, commit_digest;
 } qref_step_totals;
+
+/* splitmix64's finalizer; the digest terms bench.py recomputes from the device results */
+static inline uint64_t qref_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+static inline uint64_t qref_digest_ready(uint64_t cluster_id, uint64_t index, uint64_t low,
+                                         uint64_t high) {
+    return qref_mix64(qref_mix64(cluster_id) ^ (index * 0x9e3779b97f4a7c15ULL +
+                                                low * 0xc2b2ae3d27d4eb4fULL +
+                                                high * 0x165667b19e3779f9ULL));
+}
+/* linear in the advance: a random odd coefficient per cluster (mod 2^64), cheap to recompute
+ * over a whole column of advances */
+static inline uint64_t qref_digest_commit(uint64_t cluster_id, uint64_t advance) {
+    return (qref_mix64(cluster_id) | 1ULL) * advance;
+}
 
 /* hq_worker_group layout: a group's initial state; members of consecutive groups back to back */
 typedef struct qref_group_rec {
@@ -311,6 +334,8 @@ typedef struct qref_group_rec {
     uint32_t state, n_members, n_pending_reads, suspended;
 } qref_group_rec;
 
+uint64_t qref_digest_ready_term(uint64_t cluster_id, uint64_t index, uint64_t low, uint64_t high);
+uint64_t qref_digest_commit_term(uint64_t cluster_id, uint64_t advance);
 qref_group *qref_groups_new(uint64_t G);
 int qref_groups_init(qref_group *groups, uint64_t G, const qref_group_rec *recs,
                      const qref_member *members);

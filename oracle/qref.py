@@ -173,6 +173,8 @@ def load() -> ctypes.CDLL:
         "qref_groups_free": (None, [_vp, _u64]),
         "qref_groups_init": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
         "qref_step_batch": (ctypes.c_int, [_vp, _u64, _u64, _vp, _vp, _vp, ctypes.c_int, _vp]),
+        "qref_digest_ready_term": (_u64, [_u64, _u64, _u64, _u64]),
+        "qref_digest_commit_term": (_u64, [_u64, _u64]),
         "qref_c1_run": (ctypes.c_int, [_u64, _vp, _vp, _u64, _u64, _vp]),
         "qref_ingest_match": (_u64, [_vp, _u64, _vp, _u64, _u64, ctypes.c_uint32]),
         "qref_ingest_ack": (_u64, [_vp, _u64, _vp, _u64, ctypes.c_uint32]),
@@ -534,7 +536,7 @@ class StepGroup:
 
 class StepTotals(ctypes.Structure):
     _fields_ = [(k, _u64) for k in ("commits", "ready", "resps", "states", "dropped", "deferred",
-                                    "committed_sum")]
+                                    "committed_sum", "ready_digest", "commit_digest")]
 
 
 class StepBatch:

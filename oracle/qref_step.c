@@ -407,8 +407,15 @@ static void *step_run(void *p) {
     if (!o) { j->rc = QREF_PANIC; return NULL; }
     for (uint64_t i = j->i0; i < j->i1; i++) {
         uint64_t b = j->offsets[i], e = j->offsets[i + 1];
-        int rc = qref_group_step(&j->groups[j->list[i]], j->ev + b, (int)(e - b), o);
+        qref_group *g = &j->groups[j->list[i]];
+        const uint64_t committed0 = g->committed;
+        int rc = qref_group_step(g, j->ev + b, (int)(e - b), o);
         if (rc) { j->rc = rc; break; }
+        for (int r = 0; r < o->n_ready; r++)
+            j->tot.ready_digest += qref_digest_ready(g->cluster_id, o->ready[r].index,
+                                                     o->ready[r].low, o->ready[r].high);
+        if (o->commit_changed)
+            j->tot.commit_digest += qref_digest_commit(g->cluster_id, o->committed - committed0);
         j->tot.commits += (uint64_t)o->commit_changed;
         j->tot.ready += (uint64_t)o->n_ready;
         j->tot.resps += (uint64_t)o->n_resps;
@@ -460,8 +467,18 @@ int qref_step_batch(qref_group *groups, uint64_t G, uint64_t n_list, const uint3
         tot->dropped += jobs[t].tot.dropped;
         tot->deferred += jobs[t].tot.deferred;
         tot->committed_sum += jobs[t].tot.committed_sum;
+        tot->ready_digest += jobs[t].tot.ready_digest;
+        tot->commit_digest += jobs[t].tot.commit_digest;
     }
     return rc;
+}
+
+/* the digest terms, exported for tests/test_step_digest.py (bench.py restates them in numpy) */
+uint64_t qref_digest_ready_term(uint64_t cluster_id, uint64_t index, uint64_t low, uint64_t high) {
+    return qref_digest_ready(cluster_id, index, low, high);
+}
+uint64_t qref_digest_commit_term(uint64_t cluster_id, uint64_t advance) {
+    return qref_digest_commit(cluster_id, advance);
 }
 
 qref_group *qref_groups_new(uint64_t G) {
