@@ -130,7 +130,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,cq,cqp,c4pq,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire")
+                  "rimt,rimtc,cq,cqp,c4pq,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -859,15 +859,16 @@ def run_kernel_leg(name, steps, warmup, d: Dist, parity_threads=0):
     ctx = hq.Context(d.device)
     r = np.random.default_rng(SEED_BASE + d.rank)
     parity = None
-    if name in ("rim", "rimt"):
+    if name in ("rim", "rimt", "rimtc"):
         rim_in = rim_inputs(d.rank)
         G, K, n, ordn, idx = rim_in
-        per = G * (2 * K * n + 8 * K + 8 * K + 2)      # ordinals + ctx index in; released out
+        # ordinals + ctx index in; released index (not for rimtc), count and batch end out
+        per = G * (2 * K * n + 8 * K + (0 if name == "rimtc" else 8 * K) + 2)
         nsets = max(4, int(np.ceil(ROTATE_BYTES / per)))
         sets = [(ctx.upload(ordn.reshape(-1)), ctx.upload(idx.reshape(-1)),
                  ctx.empty(K * G, np.uint64), ctx.empty(G, np.uint8), ctx.empty(G, np.uint8))
                 for _ in range(nsets)]
-        if name == "rimt":     # the same inputs as 128-group tiles (one block per wave)
+        if name in ("rimt", "rimtc"):     # the same inputs as 128-group tiles (one per wave)
             tb = hq.ri_tile_bytes(K, n, 0)
             tiled = []
             for o, x, rel, cnt, bend in sets:
@@ -880,13 +881,17 @@ def run_kernel_leg(name, steps, warmup, d: Dist, parity_threads=0):
 
             def run(i):
                 t, rel, cnt, bend = tiled[i % nsets]
-                ctx.readindex_multi_tiles_dev(G, K, n, t, 0, n, rel, cnt, batch_end=bend)
+                ctx.readindex_multi_tiles_dev(G, K, n, t, 0, n, None if name == "rimtc" else rel,
+                                              cnt, batch_end=bend)
         else:
             def run(i):
                 o, x, rel, cnt, bend = sets[i % nsets]
                 ctx.readindex_multi_dev(G, K, n, o, x, None, None, n, rel, cnt, batch_end=bend)
         desc = (f"{name}: general multi-ctx ReadIndex release (suffix-min), {G} groups x {K} "
-                f"pending ctxs x {n} voters" + (", 128-group tiles" if name == "rimt" else ""))
+                f"pending ctxs x {n} voters" + (", 128-group tiles" if name != "rim" else "")
+                + (", compact outputs (released count + batch ends; the released index derived "
+                   "from ctx_index by the caller, hq_ri_released_host, outside the timed region)"
+                   if name == "rimtc" else ""))
         units, unit = G, "releases/s"
     elif name == "cq":
         G, n = 16 << 20, 7
@@ -997,13 +1002,15 @@ def run_kernel_leg(name, steps, warmup, d: Dist, parity_threads=0):
                              "atomics (k_bin + k_apply, the default for a dense batch)"))
         units, unit = U, "updates/s"
     elapsed, avg, launches = _timed(ctx, d, run, steps, warmup)
-    if parity_threads and name in ("rim", "rimt"):
+    if parity_threads and name in ("rim", "rimt", "rimtc"):
         # every set holds the same inputs: set 0's outputs as the timed runs left them
-        rel, cnt, bend = (tiled[0][1:] if name == "rimt" else sets[0][2:])
+        rel, cnt, bend = (tiled[0][1:] if name != "rim" else sets[0][2:])
         ctx.sync()
-        parity = rim_parity(rim_in, {"released_index": ctx.download(rel),
-                                     "released_count": ctx.download(cnt),
-                                     "batch_end": ctx.download(bend)}, parity_threads)
+        got = {"released_count": ctx.download(cnt), "batch_end": ctx.download(bend)}
+        got["released_index"] = (hq.ri_released_host(K, idx, got["released_count"],
+                                                     got["batch_end"])
+                                 if name == "rimtc" else ctx.download(rel))
+        parity = rim_parity(rim_in, got, parity_threads)
     elif parity_threads and name == "c4pq":
         # set 0 once more with its active planes packed afresh (the timed runs zeroed them, as
         # setNotActive does), its outputs poisoned first
@@ -1898,7 +1905,8 @@ def run_rank(args, d, progress):
             elif name in STEP_ROLES:
                 rec = run_step_leg(d, G=args.step_groups, steps=args.step_steps,
                                    with_cpu=not args.no_cpu, name=name)
-            elif name in ("rim", "rimt", "cq", "cqp", "c4pq", "ing", "ingo", "ingu", "inga"):
+            elif name in ("rim", "rimt", "rimtc", "cq", "cqp", "c4pq", "ing", "ingo", "ingu",
+                          "inga"):
                 pt = 0 if args.no_cpu or args.no_extra_parity else max(1, host_threads // d.world)
                 rec = run_kernel_leg(name, max(50, args.steps // 4), max(5, args.warmup // 4), d,
                                      parity_threads=pt)

@@ -28,6 +28,9 @@ struct hq_ctx {
     int bits_block = 256;
     // multi-ctx ReadIndex two groups per lane when the batch allows it (HQ_RI_PAIRS=0: off, A/B)
     bool ri_pairs = true;
+    // uniform multi-ctx tiles (K_max in {2, 4, 8}, n = n_max) on k_ri_tiles_u (HQ_RI_UNIFORM=0:
+    // on the general k_ri_multi2, A/B)
+    bool ri_uniform = true;
     // hq_wait_for: recorded on this context's stream when another context orders after it
     hipEvent_t ev_order = nullptr;
     // device workspace for the host-pointer entry points

@@ -2300,7 +2300,7 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi(const RiMultiK a) {
                 // entry k closes its release batch: it is the ctx whose confirm() released
                 // the batch (readindex.go:96), whose ctx the ReadIndexResp hints carry
                 bend |= (uint32_t)(rel && own) << k;
-                if (k < (int)a.K_max) a.rel[(uint64_t)k * a.G + g] = rel ? best_idx : ~0ull;
+                if (a.rel && k < (int)a.K_max) a.rel[(uint64_t)k * a.G + g] = rel ? best_idx : ~0ull;
             }
             a.cnt[g] = (uint8_t)released;
             if (a.bend) a.bend[g] = (uint8_t)bend;
@@ -2317,6 +2317,7 @@ __global__ __launch_bounds__(kBlock) void k_ri_multi(const RiMultiK a) {
 // v_pk_max_u16); the ctx indexes and released indexes move as 16-byte pairs. Same decisions as
 // k_ri_multi (the suffix-min release of readindex.go:77-116).
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void ce_pk(uint32_t &a, uint32_t &b) {
     const u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
@@ -2337,12 +2338,14 @@ struct RiIn {
     uint32_t kk, nn;              // PERK / PERN: the two groups' K / n bytes
 };
 
-template <bool PERK, bool PERN, int KM, bool TILED>
+// TILED: the voter-major tile (include/hipquorum.h): voter s's block of K_max * 256 bytes holds,
+// for lane l, the K_max ctx ordinal dwords of groups 2 l, 2 l + 1 back to back; EXACT (K_max ==
+// KM) reads them as vectors (one 16-byte load per voter at K_max = 4), otherwise dword by dword.
+template <bool PERK, bool PERN, int KM, bool TILED, bool EXACT = false>
 __device__ __forceinline__ void ri_load(const RiMultiK &a, uint64_t wbase, int lane,
                                         RiIn<PERK, PERN, KM> &in) {
     const uint64_t g = wbase + 2 * (uint64_t)lane;
-    // TILED: the wave's 128 groups are one tile (wbase is a multiple of 128); rows of 128
-    // entries, this lane's two groups at entries 2 lane, 2 lane + 1
+    // TILED: the wave's 128 groups are one tile (wbase is a multiple of 128)
     const uint8_t *tb = TILED ? a.tiles + (wbase >> 7) * a.tile_bytes : nullptr;
     const uint64_t ord_bytes = (uint64_t)a.K_max * a.n_max * 256;
     in.kk = in.nn = 0;
@@ -2358,19 +2361,45 @@ __device__ __forceinline__ void ri_load(const RiMultiK &a, uint64_t wbase, int l
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
         in.idx[k] = (u64x2){0, 0};
-        if (k < (int)a.K_max) {
+        if (k < (int)a.K_max)
             in.idx[k] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(
                 TILED ? tb + ord_bytes + k * 1024ull + 16 * lane
                       : reinterpret_cast<const uint8_t *>(a.idx + (uint64_t)k * a.G + g)));
+    }
 #pragma unroll
-            for (int sl = 0; sl < 8; ++sl) {
-                in.ov[k][sl] = 0xFFFFFFFFu;
-                if (sl < (int)a.n_max)
-                    in.ov[k][sl] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
-                        TILED ? tb + ((uint64_t)k * a.n_max + sl) * 256 + 4 * lane
-                              : reinterpret_cast<const uint8_t *>(
-                                    a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g)));
+    for (int sl = 0; sl < 8; ++sl) {
+#pragma unroll
+        for (int k = 0; k < KM; ++k) in.ov[k][sl] = 0xFFFFFFFFu;
+        if (sl >= (int)a.n_max) continue;
+        if constexpr (TILED) {
+            const uint8_t *p = tb + (uint64_t)sl * a.K_max * 256 + (uint64_t)lane * 4 * a.K_max;
+            if constexpr (EXACT && KM == 2) {
+                const u32x2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p));
+                in.ov[0][sl] = w.x;
+                in.ov[1][sl] = w.y;
+            } else if constexpr (EXACT) {
+#pragma unroll
+                for (int q = 0; q < KM / 4; ++q) {
+                    const u32x4 w = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4 *>(p + 16 * q));
+                    in.ov[4 * q + 0][sl] = w.x;
+                    in.ov[4 * q + 1][sl] = w.y;
+                    in.ov[4 * q + 2][sl] = w.z;
+                    in.ov[4 * q + 3][sl] = w.w;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < KM; ++k)
+                    if (k < (int)a.K_max)
+                        in.ov[k][sl] = __builtin_nontemporal_load(
+                            reinterpret_cast<const uint32_t *>(p + 4 * k));
             }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KM; ++k)
+                if (k < (int)a.K_max)
+                    in.ov[k][sl] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
+                        a.ord + ((uint64_t)k * a.n_max + sl) * a.G + g));
         }
     }
 }
@@ -2394,19 +2423,12 @@ __device__ __forceinline__ void ri_decide(const RiMultiK &a, uint64_t wbase, int
         fb1 = n1 < 1 || n1 > a.n_max || K1 > a.K_max;
         // padding of the voters >= n, per half (0xFFFF = never acked)
         const int r0 = n0 / 2 > 1 ? (int)(n0 / 2) : 1, r1 = n1 / 2 > 1 ? (int)(n1 / 2) : 1;
-        u64x2 idx[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) idx[k] = k < KM ? in.idx[k < KM ? k : 0] : (u64x2){0, 0};
         const uint32_t kmax = K0 > K1 ? K0 : K1;
         uint32_t t[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             t[k] = 0xFFFFFFFFu;
             if (k < KM && k < (int)kmax && k < (int)a.K_max) {
-                if (k > 0) {   // addRequest: index moved backward
-                    fb0 |= k < (int)K0 && idx[k].x < idx[k - 1].x;
-                    fb1 |= k < (int)K1 && idx[k].y < idx[k - 1].y;
-                }
                 uint32_t v[8];
 #pragma unroll
                 for (int sl = 0; sl < 8; ++sl)
@@ -2424,6 +2446,16 @@ __device__ __forceinline__ void ri_decide(const RiMultiK &a, uint64_t wbase, int
                 t[k] = tk;
             }
         }
+        u64x2 idx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) idx[k] = k < KM ? in.idx[k < KM ? k : 0] : (u64x2){0, 0};
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {   // addRequest: index moved backward
+            if (k < KM && k < (int)kmax && k < (int)a.K_max) {
+                fb0 |= k < (int)K0 && idx[k].x < idx[k - 1].x;
+                fb1 |= k < (int)K1 && idx[k].y < idx[k - 1].y;
+            }
+        }
         // suffix-min scan per group (ties go to the earlier ctx, as in k_ri_multi)
         uint32_t bt0 = 0xFFFFu, bt1 = 0xFFFFu, rel0 = 0, rel1 = 0, be0 = 0, be1 = 0;
         uint64_t bi0 = 0, bi1 = 0;
@@ -2439,7 +2471,7 @@ __device__ __forceinline__ void ri_decide(const RiMultiK &a, uint64_t wbase, int
             rel1 += rl1;
             be0 |= (uint32_t)(rl0 && own0) << k;
             be1 |= (uint32_t)(rl1 && own1) << k;
-            if (k < (int)a.K_max) {
+            if (a.rel && k < (int)a.K_max) {
                 uint64_t *r = a.rel + (uint64_t)k * a.G + g;
                 if (!TILED || g + 1 < a.G) {
                     *reinterpret_cast<u64x2 *>(r) = (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
@@ -2466,15 +2498,100 @@ __device__ __forceinline__ void ri_decide(const RiMultiK &a, uint64_t wbase, int
     }
 }
 
-template <bool PERK, bool PERN, int KM, bool TILED = false>
+template <bool PERK, bool PERN, int KM, bool TILED = false, bool EXACT = false>
 __global__ __launch_bounds__(kBlock) void k_ri_multi2(const RiMultiK a) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint64_t step = (uint64_t)gridDim.x * kBlock * 2;
     for (uint64_t wbase = wave * 128; wbase < a.G; wbase += step) {
         RiIn<PERK, PERN, KM> in;
-        ri_load<PERK, PERN, KM, TILED>(a, wbase, lane, in);
+        ri_load<PERK, PERN, KM, TILED, EXACT>(a, wbase, lane, in);
         ri_decide<PERK, PERN, KM, TILED>(a, wbase, lane, in);
+    }
+}
+
+// Uniform wide tiles (K_max == KM ctx slots and n_uniform == n_max == N voters in every group,
+// the voter-major ordinal layout): every bound is a constant, so the loads are N 16-byte reads
+// (KM = 4) plus KM ctx-index reads with no guards, the rank max(q - 1, 1) = max(N / 2, 1) is a
+// constant that prunes the network to the comparators that reach it, and no per-half masks or
+// SGPR-held exec masks remain. Same decisions as ri_decide (readindex.go:77-116).
+template <int KM, int N>
+__global__ __launch_bounds__(kBlock) void k_ri_tiles_u(const RiMultiK a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * 2;
+    constexpr int R = N / 2 > 1 ? N / 2 : 1;
+    for (uint64_t wbase = wave * 128; wbase < a.G; wbase += step) {
+        const uint64_t g = wbase + 2 * (uint64_t)lane;   // G even: g < G implies g + 1 < G
+        bool fb0 = false, fb1 = false;
+        if (g < a.G) {
+            const uint8_t *tb = a.tiles + (wbase >> 7) * a.tile_bytes;
+            uint32_t ov[KM][N];
+#pragma unroll
+            for (int sl = 0; sl < N; ++sl) {
+                const uint8_t *p = tb + sl * KM * 256 + lane * 4 * KM;
+                if constexpr (KM == 2) {
+                    const u32x2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p));
+                    ov[0][sl] = w.x;
+                    ov[1][sl] = w.y;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < KM / 4; ++q) {
+                        const u32x4 w = __builtin_nontemporal_load(
+                            reinterpret_cast<const u32x4 *>(p + 16 * q));
+                        ov[4 * q + 0][sl] = w.x;
+                        ov[4 * q + 1][sl] = w.y;
+                        ov[4 * q + 2][sl] = w.z;
+                        ov[4 * q + 3][sl] = w.w;
+                    }
+                }
+            }
+            u64x2 idx[KM];
+#pragma unroll
+            for (int k = 0; k < KM; ++k)
+                idx[k] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(
+                    tb + N * KM * 256 + k * 1024 + 16 * lane));
+            uint32_t t[KM];
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+                uint32_t v[8];
+#pragma unroll
+                for (int sl = 0; sl < 8; ++sl) v[sl] = sl < N ? ov[k][sl < N ? sl : 0] : 0xFFFFFFFFu;
+                sort8(v, [](uint32_t &x, uint32_t &y) { ce_pk(x, y); });
+                t[k] = v[R - 1];       // the R-th smallest first-ack ordinal of both groups
+            }
+#pragma unroll
+            for (int k = 1; k < KM; ++k) {   // addRequest: index moved backward
+                fb0 |= idx[k].x < idx[k - 1].x;
+                fb1 |= idx[k].y < idx[k - 1].y;
+            }
+            uint32_t bt0 = 0xFFFFu, bt1 = 0xFFFFu, rel0 = 0, rel1 = 0, be0 = 0, be1 = 0;
+            uint64_t bi0 = 0, bi1 = 0;
+#pragma unroll
+            for (int k = KM - 1; k >= 0; --k) {
+                const uint32_t t0 = t[k] & 0xFFFFu, t1 = t[k] >> 16;
+                bool own0 = false, own1 = false;
+                if (t0 != 0xFFFFu && t0 <= bt0) { bt0 = t0; bi0 = idx[k].x; own0 = true; }
+                if (t1 != 0xFFFFu && t1 <= bt1) { bt1 = t1; bi1 = idx[k].y; own1 = true; }
+                const bool rl0 = !fb0 && bt0 != 0xFFFFu, rl1 = !fb1 && bt1 != 0xFFFFu;
+                rel0 += rl0;
+                rel1 += rl1;
+                be0 |= (uint32_t)(rl0 && own0) << k;
+                be1 |= (uint32_t)(rl1 && own1) << k;
+                if (a.rel)
+                    *reinterpret_cast<u64x2 *>(a.rel + (uint64_t)k * a.G + g) =
+                        (u64x2){rl0 ? bi0 : ~0ull, rl1 ? bi1 : ~0ull};
+            }
+            *reinterpret_cast<uint16_t *>(a.cnt + g) = (uint16_t)(rel0 | (rel1 << 8));
+            if (a.bend) *reinterpret_cast<uint16_t *>(a.bend + g) = (uint16_t)(be0 | (be1 << 8));
+        }
+        const uint64_t f0 = __ballot(fb0), f1 = __ballot(fb1);
+        if (a.fallback && lane < 2) {
+            const uint32_t sh = 32 * lane;
+            const uint64_t w = (wbase >> 6) + lane;
+            if (w < (a.G + 63) >> 6)
+                a.fallback[w] = spread32((uint32_t)(f0 >> sh)) | (spread32((uint32_t)(f1 >> sh)) << 1);
+        }
     }
 }
 
@@ -2488,8 +2605,10 @@ extern "C" int hq_readindex_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, u
                                       uint64_t *fallback) {
     if (!ctx) return HQ_E_INVAL;
     if (G == 0) return HQ_OK;
-    if (!ack_ordinal || !ctx_index || !released_index || !released_count || K_max < 1 ||
-        K_max > 8 || n_max < 1 || n_max > 8 || (!n_voting && (n_uniform < 1 || n_uniform > 8)))
+    // released_index may be NULL when batch_end is given (the caller derives it from ctx_index)
+    if (!ack_ordinal || !ctx_index || (!released_index && !batch_end) || !released_count ||
+        K_max < 1 || K_max > 8 || n_max < 1 || n_max > 8 ||
+        (!n_voting && (n_uniform < 1 || n_uniform > 8)))
         return hq::fail(ctx, HQ_E_INVAL, "hq_readindex_multi_dev: bad arguments");
     RiMultiK k{G, K_max, n_max, n_uniform, nullptr, 0, ack_ordinal, ctx_index, n_pending,
                n_voting, released_index, released_count, batch_end, fallback};
@@ -2548,10 +2667,15 @@ __global__ __launch_bounds__(kBlock) void k_tile_ri_multi(uint64_t G, uint32_t K
         const uint64_t t = q / chunks, off = (q % chunks) * 16;
         const uint64_t g0 = t * HQ_RI_TILE_GROUPS;
         uint8_t v[16];
-        if (off < ord_bytes) {                           // 8 u16 entries of row off / 256
-            const uint64_t row = off / 256, j = (off % 256) / 2;
+        if (off < ord_bytes) {                           // 8 u16 ordinal entries
             for (int e = 0; e < 8; ++e) {
-                const uint64_t g = g0 + j + e;
+                // voter sl's block of K_max * 256 bytes: pair l's K_max dwords (groups 2 l and
+                // 2 l + 1 of ctx k at dword k)
+                const uint64_t b = off + 2 * e;
+                const uint64_t sl = b / (K_max * 256ull), r = b % (K_max * 256ull);
+                const uint64_t l = r / (4ull * K_max), w = r % (4ull * K_max);
+                const uint64_t row = (w / 4) * n_max + sl, j = 2 * l + (w % 4) / 2;
+                const uint64_t g = g0 + j;
                 const uint16_t x = g < G ? ord[row * G + g] : 0xFFFFu;
                 v[2 * e] = (uint8_t)x;
                 v[2 * e + 1] = (uint8_t)(x >> 8);
@@ -2588,8 +2712,8 @@ extern "C" int hq_readindex_multi_tiles_dev(hq_ctx *ctx, uint64_t G, uint32_t K_
     if (!ctx) return HQ_E_INVAL;
     if (G == 0) return HQ_OK;
     const bool perk = flags & HQ_RI_TILE_PER_K, pern = flags & HQ_RI_TILE_PER_N;
-    if (!tiles || !released_index || !released_count || K_max < 1 || K_max > 8 || n_max < 1 ||
-        n_max > 8 || (flags & ~(HQ_RI_TILE_PER_K | HQ_RI_TILE_PER_N)) ||
+    if (!tiles || (!released_index && !batch_end) || !released_count || K_max < 1 || K_max > 8 ||
+        n_max < 1 || n_max > 8 || (flags & ~(HQ_RI_TILE_PER_K | HQ_RI_TILE_PER_N)) ||
         (!pern && (n_uniform < 1 || n_uniform > 8)) || !hq::aligned16(tiles) ||
         (reinterpret_cast<uintptr_t>(released_index) & 15) ||
         (reinterpret_cast<uintptr_t>(released_count) & 1) ||
@@ -2605,23 +2729,48 @@ extern "C" int hq_readindex_multi_tiles_dev(hq_ctx *ctx, uint64_t G, uint32_t K_
     int rc = hq::pre_launch(ctx);
     if (rc) return rc;
     const int km = K_max <= 2 ? 2 : K_max <= 4 ? 4 : 8;
+    const bool exact = (uint32_t)km == K_max;
+    if (exact && ctx->ri_uniform && !perk && !pern && n_uniform == n_max) {
+#define HQ_RITU(KMV)                                                                            \
+        do {                                                                                    \
+            switch (n_max) {                                                                    \
+            case 1: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 1>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            case 2: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 2>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            case 3: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 3>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            case 4: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            case 5: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 5>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            case 6: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 6>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            case 7: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 7>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            default: hipLaunchKernelGGL((k_ri_tiles_u<KMV, 8>), dim3(grid), dim3(kBlock), 0, ctx->stream, k); break; \
+            }                                                                                   \
+        } while (0)
+        if (K_max == 2) HQ_RITU(2);
+        else if (K_max == 4) HQ_RITU(4);
+        else HQ_RITU(8);
+#undef HQ_RITU
+        return hq::post_launch(ctx, "k_ri_tiles_u");
+    }
+#define HQ_RIM2TK(PK, PN, KMV)                                                                  \
+    do {                                                                                        \
+        if (exact)                                                                              \
+            hipLaunchKernelGGL((k_ri_multi2<PK, PN, KMV, true, true>), dim3(grid),              \
+                               dim3(kBlock), 0, ctx->stream, k);                                \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_ri_multi2<PK, PN, KMV, true, false>), dim3(grid),             \
+                               dim3(kBlock), 0, ctx->stream, k);                                \
+    } while (0)
 #define HQ_RIM2T(PK, PN)                                                                        \
     do {                                                                                        \
-        if (km == 2)                                                                            \
-            hipLaunchKernelGGL((k_ri_multi2<PK, PN, 2, true>), dim3(grid), dim3(kBlock), 0,     \
-                               ctx->stream, k);                                                 \
-        else if (km == 4)                                                                       \
-            hipLaunchKernelGGL((k_ri_multi2<PK, PN, 4, true>), dim3(grid), dim3(kBlock), 0,     \
-                               ctx->stream, k);                                                 \
-        else                                                                                    \
-            hipLaunchKernelGGL((k_ri_multi2<PK, PN, 8, true>), dim3(grid), dim3(kBlock), 0,     \
-                               ctx->stream, k);                                                 \
+        if (km == 2) HQ_RIM2TK(PK, PN, 2);                                                      \
+        else if (km == 4) HQ_RIM2TK(PK, PN, 4);                                                 \
+        else HQ_RIM2TK(PK, PN, 8);                                                              \
     } while (0)
     if (perk && pern) HQ_RIM2T(true, true);
     else if (perk) HQ_RIM2T(true, false);
     else if (pern) HQ_RIM2T(false, true);
     else HQ_RIM2T(false, false);
 #undef HQ_RIM2T
+#undef HQ_RIM2TK
     return hq::post_launch(ctx, "k_ri_multi2<tiles>");
 }
 

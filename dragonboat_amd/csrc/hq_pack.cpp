@@ -384,10 +384,14 @@ extern "C" int hq_tile_ri_multi_host(uint64_t G, uint32_t K_max, uint32_t n_max,
         for (uint64_t j = 0; j < T; ++j) {
             const uint64_t g = t * T + j;
             const bool in = g < G;
-            for (uint64_t r = 0; r < rows; ++r) {
-                const uint16_t x = in ? ord[r * G + g] : 0xFFFFu;
-                std::memcpy(b + r * 256 + 2 * j, &x, 2);
-            }
+            // voter-major: voter s's block of K_max * 256 bytes, the pair j / 2's K_max dwords,
+            // ctx k's dword holding groups 2 (j / 2) and 2 (j / 2) + 1
+            for (uint64_t k = 0; k < K_max; ++k)
+                for (uint64_t s = 0; s < n_max; ++s) {
+                    const uint16_t x = in ? ord[(k * n_max + s) * G + g] : 0xFFFFu;
+                    std::memcpy(b + s * K_max * 256 + (j / 2) * 4 * K_max + 4 * k + 2 * (j % 2),
+                                &x, 2);
+                }
             for (uint64_t k = 0; k < K_max; ++k) {
                 const uint64_t x = in ? idx[k * G + g] : 0;
                 std::memcpy(b + rows * 256 + k * 1024 + 8 * j, &x, 8);
@@ -398,6 +402,31 @@ extern "C" int hq_tile_ri_multi_host(uint64_t G, uint32_t K_max, uint32_t n_max,
                 u += T;
             }
             if (nv) u[j] = in ? nv[g] : 0;
+        }
+    }
+    return HQ_OK;
+}
+
+// released_index from the compact ReadIndex outputs (include/hipquorum.h hq_ri_released_host): a
+// downward scan per group carries the index of the nearest closing ctx at or above entry k.
+extern "C" int hq_ri_released_host(uint64_t G, uint32_t K_max, const uint64_t *ctx_index,
+                                   const uint8_t *released_count, const uint8_t *batch_end,
+                                   uint64_t *released_index) {
+    if (G && (!ctx_index || !released_count || !batch_end || !released_index)) return HQ_E_INVAL;
+    if (K_max < 1 || K_max > 8) return HQ_E_INVAL;
+    for (uint64_t g = 0; g < G; ++g) {
+        const uint32_t cnt = released_count[g], be = batch_end[g];
+        if (cnt > K_max) return HQ_E_INVAL;
+        uint64_t cur = ~0ull;
+        bool closed = false;
+        for (int k = (int)K_max - 1; k >= 0; --k) {
+            if ((be >> k) & 1) {
+                cur = ctx_index[(uint64_t)k * G + g];
+                closed = true;
+            }
+            const bool rel = (uint32_t)k < cnt;
+            if (rel && !closed) return HQ_E_INVAL;
+            released_index[(uint64_t)k * G + g] = rel ? cur : ~0ull;
         }
     }
     return HQ_OK;

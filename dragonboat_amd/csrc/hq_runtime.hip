@@ -116,6 +116,7 @@ int hq_open(int device, uint32_t flags, hq_ctx **out) {
         if (v == 256 || v == 512 || v == 1024) ctx->bits_block = v;
     }
     if (const char *r = std::getenv("HQ_RI_PAIRS")) ctx->ri_pairs = std::atoi(r) != 0;
+    if (const char *r = std::getenv("HQ_RI_UNIFORM")) ctx->ri_uniform = std::atoi(r) != 0;
     if (const char *gd = std::getenv("HQ_BIN_GRID")) {
         const int v = std::atoi(gd);
         if (v >= 8 && v <= 4096) ctx->bin_grid = (uint32_t)(v & ~7);

@@ -42,7 +42,7 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 15
+HQ_ABI_VERSION = 16
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -327,6 +327,7 @@ SIGNATURES = {
                                                     ctypes.c_uint32, _vp, _vp, _vp, _vp]),
     "hq_tile_ri_multi_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                             _vp, _vp, _vp, _vp, _vp]),
+    "hq_ri_released_host": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, _vp, _vp, _vp, _vp]),
     "hq_tile_ri_multi_host": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                              _vp, _vp, _vp, _vp, _vp]),
     "hq_ingest_match_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
@@ -1111,6 +1112,21 @@ def tile_ri_multi_host(G, K_max, n_max, ack_ordinal, ctx_index, n_pending=None, 
     _chk(lib.hq_tile_ri_multi_host(G, K_max, n_max, *[_p(c) for c in cols], _p(out)),
          "hq_tile_ri_multi_host")
     return out, flags
+
+
+def ri_released_host(K_max, ctx_index, released_count, batch_end):
+    """hq_ri_released_host: released_index uint64 [K_max][G] from the compact outputs of
+    readindex_multi(_tiles)_dev with released_index None, and the caller's ctx_index."""
+    cnt = np.ascontiguousarray(released_count, np.uint8)
+    G = len(cnt)
+    idx = np.ascontiguousarray(ctx_index, np.uint64).reshape(-1)
+    be = np.ascontiguousarray(batch_end, np.uint8)
+    if len(idx) != K_max * G or len(be) != G:
+        raise ValueError("ri_released_host: ctx_index [K_max][G], batch_end [G]")
+    out = np.empty(K_max * G, np.uint64)
+    _chk(lib.hq_ri_released_host(G, K_max, _p(idx), _p(cnt), _p(be), _p(out)),
+         "hq_ri_released_host")
+    return out
 
 
 def plane_tiles(G: int) -> int:

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 15
+#define HQ_ABI_VERSION 16
 
 /* status codes */
 #define HQ_OK          0
@@ -440,7 +440,9 @@ int hq_vote(hq_ctx *ctx, uint64_t G, const uint8_t *granted, const uint8_t *reje
  * released_count[g] = released prefix length; batch_end[g] (may be NULL) bit k = entry k is the
  * ctx whose confirm() released its batch — every released entry i belongs to the batch closed by
  * the first k >= i with bit k set, and the ReadIndexResp messages of that batch carry ctx k as
- * their hint (handleReadIndexLeaderConfirmation, raft.go:1740-1760). n outside [1, n_max],
+ * their hint (handleReadIndexLeaderConfirmation, raft.go:1740-1760). released_index may be NULL
+ * when batch_end is not: it is then not written (32 of a K = 4 group's 34 output bytes), and the
+ * caller, which holds ctx_index, derives it with hq_ri_released_host. n outside [1, n_max],
  * K > K_max or a decreasing ctx_index give fallback (nothing released). K_max <= 8, n_max <= 8;
  * ordinals distinct per group except 0 (ties at equal ordinals resolve in queue order).
  */
@@ -478,6 +480,14 @@ int hq_tile_ri_multi_dev(hq_ctx *ctx, uint64_t G, uint32_t K_max, uint32_t n_max
 int hq_tile_ri_multi_host(uint64_t G, uint32_t K_max, uint32_t n_max,
                           const uint16_t *ack_ordinal, const uint64_t *ctx_index,
                           const uint8_t *n_pending, const uint8_t *n_voting, uint8_t *tiles);
+/* released_index [K_max][G] from the compact outputs (released_count, batch_end) and the
+ * caller's ctx_index [K_max][G]: entry k < released_count[g] gets ctx_index[k'][g] of the first
+ * k' >= k with batch_end bit k' set (the index confirm() rewrote it to, readindex.go:96-104), the
+ * other entries ~0 — the released_index the kernels write. Host pointers; HQ_E_INVAL when a
+ * released entry has no closing ctx (batch_end not from the same call). */
+int hq_ri_released_host(uint64_t G, uint32_t K_max, const uint64_t *ctx_index,
+                        const uint8_t *released_count, const uint8_t *batch_end,
+                        uint64_t *released_index);
 
 /* ReadIndex confirmation and vote tally of the same groups in one pass over the shared n. */
 int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uint8_t *granted,

@@ -85,7 +85,8 @@ def test_decreasing_index_is_fallback():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K_max,n_max,G", [(8, 8, 20_011), (3, 5, 4097), (1, 3, 65)])
-def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G):
+@pytest.mark.parametrize("compact", [False, True])
+def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G, compact):
     rng = np.random.default_rng(K_max * 100 + n_max)
     ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
     n[::97] = 0                                   # invalid n -> fallback
@@ -97,11 +98,11 @@ def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G):
     cnt = gpu_ctx.empty(G, np.uint8)
     bend = gpu_ctx.empty(G, np.uint8)
     fb = gpu_ctx.empty(hq.words64(G), np.uint64)
-    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], 0, rel, cnt, fb, bend)
-    np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
-    np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
-    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
-    np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
+    gpu_ctx.memset(rel, 0x5A)
+    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], 0,
+                                None if compact else rel, cnt, fb, bend)
+    _check_outputs(gpu_ctx, hq, K_max, idx, rel, cnt, fb, bend, compact,
+                   (want_rel, want_cnt, want_fb, want_bend))
     for x in d + [rel, cnt, bend, fb]:
         gpu_ctx.free(x)
 
@@ -113,7 +114,8 @@ def test_kernel_matches_oracle(gpu_ctx, hq, K_max, n_max, G):
                                                      (3, 5, 130, False, True),
                                                      (2, 3, 2, True, True),
                                                      (1, 1, 64, False, False)])
-def test_kernel_pairs_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
+@pytest.mark.parametrize("compact", [False, True])
+def test_kernel_pairs_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern, compact):
     """Even G with aligned columns takes the two-groups-per-lane kernel (packed u16 sorting):
     every combination of per-group / uniform pending count and voter count, bit-exact."""
     rng = np.random.default_rng(K_max * 1000 + n_max + G)
@@ -133,11 +135,11 @@ def test_kernel_pairs_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
     bend = gpu_ctx.empty(G, np.uint8)
     fb = gpu_ctx.empty(hq.words64(G), np.uint64)
     gpu_ctx.memset(fb, 0xFF)
-    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], nu, rel, cnt, fb, bend)
-    np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
-    np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
-    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
-    np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
+    gpu_ctx.memset(rel, 0x5A)
+    gpu_ctx.readindex_multi_dev(G, K_max, n_max, d[0], d[1], d[2], d[3], nu,
+                                None if compact else rel, cnt, fb, bend)
+    _check_outputs(gpu_ctx, hq, K_max, idx, rel, cnt, fb, bend, compact,
+                   (want_rel, want_cnt, want_fb, want_bend))
     for x in [x for x in d if x is not None] + [rel, cnt, bend, fb]:
         gpu_ctx.free(x)
 
@@ -146,11 +148,13 @@ def tiles_reference(ord_, idx, Kp, nv, K_max, n_max, G):
     """numpy restatement of the 128-group tile layout (include/hipquorum.h)."""
     T = 128
     nt = (G + T - 1) // T
-    o = np.full((K_max * n_max, nt * T), NONE, np.uint16)
-    o[:, :G] = ord_.reshape(K_max * n_max, G)
+    o = np.full((K_max, n_max, nt * T), NONE, np.uint16)
+    o[:, :, :G] = ord_.reshape(K_max, n_max, G)
     x = np.zeros((K_max, nt * T), np.uint64)
     x[:, :G] = idx.reshape(K_max, G)
-    parts = [o.reshape(K_max * n_max, nt, T).transpose(1, 0, 2).reshape(nt, -1).view(np.uint8),
+    # ordinals voter-major: [tile][voter][pair of groups][ctx][2 groups]
+    o = o.reshape(K_max, n_max, nt, T // 2, 2).transpose(2, 1, 3, 0, 4)
+    parts = [np.ascontiguousarray(o).reshape(nt, -1).view(np.uint8),
              x.reshape(K_max, nt, T).transpose(1, 0, 2).reshape(nt, -1).view(np.uint8)]
     for c in (Kp, nv):
         if c is not None:
@@ -173,16 +177,20 @@ def test_tile_packer_layout(hq, K_max, n_max, G, perk, pern):
     np.testing.assert_array_equal(tiles, tiles_reference(ord_, idx, Kp, nv, K_max, n_max, G))
 
 
+TILE_CASES = [(8, 8, 20_010, True, True), (4, 7, 4096, False, False), (4, 7, 4098, True, False),
+              (3, 5, 130, False, True), (2, 3, 2, True, True), (1, 1, 64, False, False),
+              # uniform K_max in {2, 4, 8} and n = n_max: k_ri_tiles_u; K_max = 3: dword loads
+              (8, 5, 2050, False, False), (2, 3, 258, False, False), (4, 1, 128, False, False),
+              (3, 4, 514, False, False)]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("K_max,n_max,G,perk,pern", [(8, 8, 20_010, True, True),
-                                                     (4, 7, 4096, False, False),
-                                                     (4, 7, 4098, True, False),
-                                                     (3, 5, 130, False, True),
-                                                     (2, 3, 2, True, True),
-                                                     (1, 1, 64, False, False)])
-def test_kernel_tiles_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("K_max,n_max,G,perk,pern", TILE_CASES)
+def test_kernel_tiles_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern, compact):
     """The 128-group tile layout: the device packer equals the host packer, and the kernel over
-    tiles is bit-exact with the oracle (every per-group / uniform combination)."""
+    tiles is bit-exact with the oracle (every per-group / uniform combination). compact: no
+    released_index written; hq_ri_released_host rebuilds it from the counts and batch ends."""
     rng = np.random.default_rng(K_max * 1000 + n_max + G + 7)
     ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
     if pern:
@@ -205,10 +213,71 @@ def test_kernel_tiles_match_oracle(gpu_ctx, hq, K_max, n_max, G, perk, pern):
     bend = gpu_ctx.empty(G, np.uint8)
     fb = gpu_ctx.empty(hq.words64(G), np.uint64)
     gpu_ctx.memset(fb, 0xFF)
-    gpu_ctx.readindex_multi_tiles_dev(G, K_max, n_max, dt, flags, nu, rel, cnt, fb, bend)
-    np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
-    np.testing.assert_array_equal(gpu_ctx.download(cnt), want_cnt)
-    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
-    np.testing.assert_array_equal(gpu_ctx.download(bend), want_bend)
+    gpu_ctx.memset(rel, 0x5A)
+    gpu_ctx.readindex_multi_tiles_dev(G, K_max, n_max, dt, flags, nu, None if compact else rel,
+                                      cnt, fb, bend)
+    _check_outputs(gpu_ctx, hq, K_max, idx, rel, cnt, fb, bend, compact,
+                   (want_rel, want_cnt, want_fb, want_bend))
     for x in [x for x in d if x is not None] + [dt, rel, cnt, bend, fb]:
         gpu_ctx.free(x)
+
+
+def _check_outputs(gpu_ctx, hq, K_max, idx, rel, cnt, fb, bend, compact, want):
+    want_rel, want_cnt, want_fb, want_bend = want
+    c, b = gpu_ctx.download(cnt), gpu_ctx.download(bend)
+    np.testing.assert_array_equal(c, want_cnt)
+    np.testing.assert_array_equal(gpu_ctx.download(fb), want_fb)
+    np.testing.assert_array_equal(b, want_bend)
+    if compact:     # not written: still the poison; the host rebuild equals the kernels' output
+        assert (gpu_ctx.download(rel).view(np.uint8) == 0x5A).all()
+        np.testing.assert_array_equal(hq.ri_released_host(K_max, idx, c, b), want_rel)
+    else:
+        np.testing.assert_array_equal(gpu_ctx.download(rel), want_rel)
+
+
+@pytest.mark.gpu
+def test_uniform_tiles_on_the_general_kernel(hq):
+    """HQ_RI_UNIFORM=0 (read at hq_open) sends uniform tiles through k_ri_multi2: same outputs."""
+    import os
+    K_max, n_max, G = 4, 7, 4098
+    rng = np.random.default_rng(77)
+    ord_, idx, K, n = random_batch(rng, G, K_max, n_max)
+    want = qref.readindex_multi_batch(ord_, idx, None, None, n_max, K_max, n_max)
+    tiles_h, flags = hq.tile_ri_multi_host(G, K_max, n_max, ord_, idx, None, None)
+    os.environ["HQ_RI_UNIFORM"] = "0"
+    try:
+        ctx = hq.Context(0)
+    finally:
+        del os.environ["HQ_RI_UNIFORM"]
+    try:
+        dt = ctx.upload(tiles_h)
+        rel, cnt = ctx.empty(K_max * G, np.uint64), ctx.empty(G, np.uint8)
+        bend, fb = ctx.empty(G, np.uint8), ctx.empty(hq.words64(G), np.uint64)
+        ctx.readindex_multi_tiles_dev(G, K_max, n_max, dt, flags, n_max, rel, cnt, fb, bend)
+        _check_outputs(ctx, hq, K_max, idx, rel, cnt, fb, bend, False, want)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("K_max,n", [(1, 3), (4, 7), (8, 5)])
+def test_released_index_from_compact_outputs(K_max, n):
+    """hq_ri_released_host rebuilds the released index the kernels write from the compact outputs
+    (released count, batch ends) and the caller's ctx indexes: on the oracle's own outputs it
+    gives the oracle's released index; a released entry without a closing ctx is refused."""
+    from dragonboat_amd import hipquorum as hq
+
+    rng = np.random.default_rng(11 + K_max)
+    G = 5003
+    ordn = rng.integers(1, K_max * n + 1, (K_max, n, G)).astype(np.uint16)
+    ordn[rng.random((K_max, n, G)) < 0.3] = 0xFFFF
+    idx = np.uint64(1000) + np.cumsum(rng.integers(0, 3, (K_max, G)), axis=0).astype(np.uint64)
+    rel, cnt, fb, bend = qref.readindex_multi_batch(ordn.reshape(-1), idx.reshape(-1), None, None,
+                                                    n, K_max, n, nthreads=2)
+    assert not fb.any() and cnt.any()
+    got = hq.ri_released_host(K_max, idx, cnt, bend)
+    assert np.array_equal(got, rel)
+    bad = bend.copy()
+    g = int(np.flatnonzero(cnt)[0])
+    bad[g] = 0                               # released entries, no closing ctx
+    with pytest.raises(hq.HQError):
+        hq.ri_released_host(K_max, idx, cnt, bad)
