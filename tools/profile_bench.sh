@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 W=${1:-c2}
 OUT=gpurun_out/prof_$W
 # kernel legs (bench extras) ride along the headline workload
-case $W in rim|rimt|cq|cqp|c4pq|ing|ingo|ingu) ARGS="--workload c2tl --extra $W" ;; *) ARGS="--workload $W --extra=" ;; esac
+case $W in rim|rimt|rimtc|cq|cqp|c4pq|ing|ingo|ingu) ARGS="--workload c2tl --extra $W" ;; *) ARGS="--workload $W --extra=" ;; esac
 mkdir -p $OUT
 set -o pipefail
 echo "== kernel trace ($W)"

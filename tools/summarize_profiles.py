@@ -30,7 +30,9 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2,
           "c5t": "k_commit_fused<2, 512, 1>", "c5s": "k_commit<7, 2, 2, false, 0>",
           "c2l": "k_commit_lag_big<3, 0, 4, false, 0>", "c3l": "k_commit_lag<5, 2, 4, false, 0>",
           "c2ll": "k_commit_lag_big<3, 0, 4, false, 1>", "c5ll": "k_commit_lag_fused<2, 512, 1>",
-          "c5l": "k_commit_lag_fused<2, 512, 0>", "rim": "k_ri_multi2<false, false, 4, false>", "rimt": "k_ri_multi2<false, false, 4, true>",
+          "c5l": "k_commit_lag_fused<2, 512, 0>", "rim": "k_ri_multi2<false, false, 4, false>",
+          # uniform tiles (K = 4, n = 7): k_ri_tiles_u since r04d; rimtc without released_index
+          "rimt": "k_ri_tiles_u<4, 7>", "rimtc": "k_ri_tiles_u<4, 7>",
           "cq": "k_bits<4, false, 256, false, true>", "cqp": "k_cq_planes<6, false, 256>",
           "ing": ("k_bin<false>", "k_apply<false>"), "c4pq": "k_planes_cq<256>",
           "ingo": "k_table_ingest<true, false>", "rim2": "k_ri_multi2",
