@@ -8,7 +8,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || exit $?
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
-timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --detail-out $O/bench_detail.json > $O/bench.log 2> $O/bench.err || exit $?
+T0=$(date +%s); timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --detail-out $O/bench_detail.json > $O/bench.log 2> $O/bench.err || exit $?; echo "bench wall $(( $(date +%s) - T0 )) s" > $O/bench_wall.txt
 timeout -k 10 400 python -u bench.py --gpus 2 --steps 20 --warmup 5 --extra= --detail-out $O/n2_detail.json > $O/bench_n2_threads.log 2>&1 || exit $?
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 --extra= --detail-out $O/tr2_detail.json > $O/bench_torchrun_n2.log 2>&1 || exit $?
 echo all ok
