@@ -43,6 +43,7 @@ oracle:
 #   lib_rinet0 multi-ctx ReadIndex with the 28-CE transposition sort instead of Batcher's 19-CE network
 #   lib_tilecopy / lib_b3copy / lib_plcopy the commit tile / 3-byte / bit-plane kernel's loads and stores without the
 #              decision (their floors)
+#   lib_ingnostore / lib_ingnoload the grouped table ingest without its table stores / loads (timing probes: wrong output)
 define variant
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(1) -shared -o $@ $(SRCS)
@@ -76,6 +77,10 @@ clean:
 	rm -rf $(LIBDIR) oracle/build
 
 .PHONY: all oracle clean variants
+tools/lib_ingnostore/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_INGEST_NOSTORE)
+tools/lib_ingnoload/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_INGEST_NOLOAD)
 tools/lib_rinet0/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_RI_NET=0)
 tools/lib_sw%/libhipquorum.so: $(SRCS) $(DEPS)

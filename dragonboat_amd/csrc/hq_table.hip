@@ -190,14 +190,22 @@ __global__ __launch_bounds__(kTBlock) void k_table_ingest(const uint64_t *u, uin
 #pragma unroll
             for (int c = 0; c < kIV; ++c) {
                 p[c] = trow(t, key[c] >> SH, (uint32_t)(key[c] & ((1u << SH) - 1)) - 1);
+#ifdef HQ_INGEST_NOLOAD      // timing probe (tools/lib_ingnoload): no table loads, wrong output
+                old[c] = 0;
+#else
                 old[c] = tail[c] && !edge[c] ? *p[c] : 0;
+#endif
             }
 #pragma unroll
             for (int c = 0; c < kIV; ++c) {
                 if (!tail[c]) continue;
+#ifdef HQ_INGEST_NOSTORE     // timing probe (tools/lib_ingnostore): no table stores, wrong output
+                if (v[c] == 0x5A5A5A5A5A5A5A5Aull) *p[c] = old[c];   // (keeps the loads live)
+#else
                 if (edge[c]) atomicMax(reinterpret_cast<unsigned long long *>(p[c]),
                                        (unsigned long long)v[c]);
                 else if (v[c] > old[c]) *p[c] = v[c];
+#endif
             }
         } else if constexpr (MODE == kUnique) {
             uint64_t *p[kIV], old[kIV];
