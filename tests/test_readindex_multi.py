@@ -281,3 +281,24 @@ def test_released_index_from_compact_outputs(K_max, n):
     bad[g] = 0                               # released entries, no closing ctx
     with pytest.raises(hq.HQError):
         hq.ri_released_host(K_max, idx, cnt, bad)
+
+
+def test_released_index_host_edges():
+    """hq_ri_released_host on the edges: an empty batch, K_max outside 1..8, a released count
+    above K_max and mismatched column lengths are refused or empty, never a write past the end."""
+    from dragonboat_amd import hipquorum as hq
+
+    assert hq.ri_released_host(4, np.zeros(0, np.uint64), np.zeros(0, np.uint8),
+                               np.zeros(0, np.uint8)).size == 0
+    idx = np.arange(8, dtype=np.uint64)
+    for K in (0, 9):
+        with pytest.raises((hq.HQError, ValueError)):
+            hq.ri_released_host(K, np.zeros(K * 2, np.uint64), np.zeros(2, np.uint8),
+                                np.zeros(2, np.uint8))
+    with pytest.raises(hq.HQError):                       # count 5 > K_max 4
+        hq.ri_released_host(4, idx, np.array([5, 0], np.uint8), np.array([0x10, 0], np.uint8))
+    with pytest.raises(ValueError):                       # ctx_index is not [K_max][G]
+        hq.ri_released_host(4, idx[:6], np.zeros(2, np.uint8), np.zeros(2, np.uint8))
+    # nothing released: every entry ~0, whatever the batch ends say
+    out = hq.ri_released_host(4, idx, np.zeros(2, np.uint8), np.array([0xF, 0x1], np.uint8))
+    assert (out == np.uint64(2**64 - 1)).all()
