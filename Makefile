@@ -44,6 +44,7 @@ oracle:
 #   lib_tilecopy / lib_b3copy / lib_plcopy the commit tile / 3-byte / bit-plane kernel's loads and stores without the
 #              decision (their floors)
 #   lib_ingnostore / lib_ingnoload the grouped table ingest without its table stores / loads (timing probes: wrong output)
+#   lib_encspawn the threaded event encoder spawning its threads per call (before the task pool)
 define variant
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(1) -shared -o $@ $(SRCS)
@@ -77,6 +78,8 @@ clean:
 	rm -rf $(LIBDIR) oracle/build
 
 .PHONY: all oracle clean variants
+tools/lib_encspawn/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_ENCODE_SPAWN)
 tools/lib_ingnostore/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_INGEST_NOSTORE)
 tools/lib_ingnoload/libhipquorum.so: $(SRCS) $(DEPS)

@@ -7,7 +7,11 @@
 // write the stream directly) and the decoder the host worker uses for stream input; the device
 // twin of the decoder is in hq_dstep.hip.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -272,6 +276,97 @@ struct alignas(64) RangeOut {   // one thread's results, a cache line each
     int rc = HQ_OK;
 };
 
+// The threaded encodes' workers: created once and kept, shared by calls made side by side (a
+// call spawning its T - 1 threads for each of its two phases paid tens of microseconds per
+// thread in a process holding the GPU runtime's mappings). A call queues T - 1 tasks, runs task
+// 0 itself, then runs queued tasks (its own or another call's) until its own are done.
+class TaskPool {
+public:
+    ~TaskPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void parallel_for(uint32_t T, const std::function<void(uint32_t)> &fn) {
+        if (T <= 1) {
+            if (T) fn(0);
+            return;
+        }
+#ifdef HQ_ENCODE_SPAWN          // A/B (tools/lib_encspawn): fresh threads for every phase
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < T; ++t) th.emplace_back(fn, t);
+        fn(0);
+        for (auto &x : th) x.join();
+        return;
+#endif
+        std::atomic<uint32_t> left(T - 1);
+        std::mutex dm;
+        std::condition_variable dcv;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            demand_ += T - 1;
+            while (th_.size() < demand_) th_.emplace_back([this] { loop(); });
+            for (uint32_t t = 1; t < T; ++t)
+                q_.emplace_back([&, t] {
+                    fn(t);
+                    if (left.fetch_sub(1) == 1) {
+                        std::lock_guard<std::mutex> l2(dm);
+                        dcv.notify_all();
+                    }
+                });
+        }
+        cv_.notify_all();
+        fn(0);
+        while (left.load() > 0) {
+            std::function<void()> f;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!q_.empty()) {
+                    f = std::move(q_.front());
+                    q_.pop_front();
+                }
+            }
+            if (f) {
+                f();
+                continue;
+            }
+            std::unique_lock<std::mutex> l2(dm);
+            dcv.wait(l2, [&] { return left.load() == 0; });
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        demand_ -= T - 1;
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;          // stop_ and nothing left
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::vector<std::thread> th_;
+    size_t demand_ = 0;
+    bool stop_ = false;
+};
+
+TaskPool &task_pool() {
+    static TaskPool p;
+    return p;
+}
+
 }  // namespace
 
 extern "C" {
@@ -309,14 +404,10 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
         g[t] = std::max<uint64_t>(g[t - 1], (uint64_t)(std::lower_bound(offsets16, offsets16 + n_groups,
                                                                          want) - offsets16));
     }
-    auto run = [&](uint32_t t) {
+    task_pool().parallel_for(T, [&](uint32_t t) {
         res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch[t], nullptr, 0,
                                 &res[t].events, &res[t].bytes);
-    };
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; ++t) th.emplace_back(run, t);
-    run(0);
-    for (auto &x : th) x.join();
+    });
     uint64_t total = 0, events = 0;
     int rc = HQ_OK;
     for (uint32_t t = 0; t < T; ++t) {
@@ -328,13 +419,9 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     if (!rc) {
         std::vector<uint64_t> at(T, 0);
         for (uint32_t t = 1; t < T; ++t) at[t] = at[t - 1] + res[t - 1].bytes;
-        th.clear();
-        auto copy = [&](uint32_t t) {
+        task_pool().parallel_for(T, [&](uint32_t t) {
             if (res[t].bytes) std::memcpy(out + at[t], scratch[t].data(), res[t].bytes);
-        };
-        for (uint32_t t = 1; t < T; ++t) th.emplace_back(copy, t);
-        copy(0);
-        for (auto &x : th) x.join();
+        });
         *n_events = events;
         *n_bytes = total;
     }
