@@ -284,3 +284,34 @@ def test_compact_records_malformed(hq):
     out = np.zeros(nb, np.uint8)                  # exactly the stream: enough for threads
     assert hq.encode_events16_sized_into(off16, recs, out, np.zeros(len(off) - 1, np.uint32),
                                          4) == (len(ev), nb)
+
+
+def test_threaded_encodes_side_by_side(hq):
+    """Threaded encodes called from several threads at once share the encoder's task pool: each
+    call's bytes and size words equal its single-thread encode."""
+    import threading
+
+    import bench
+    G, W = 1 << 14, 4
+    recs = bench.StepRows16(hq, G, bench.STEP_ROLES["step5"])
+    off16, r = recs.set(3)
+    b = [G * i // W for i in range(W + 1)]
+    parts = [(off16[b[i]:b[i + 1] + 1] - off16[b[i]], int(off16[b[i]]), int(off16[b[i + 1]]))
+             for i in range(W)]
+    want = [hq.encode_events16_sized(o, r[e0:e1], 1) for o, e0, e1 in parts]
+    bad = []
+
+    def one(i, T):
+        o, e0, e1 = parts[i]
+        out = np.zeros((e1 - e0) * 5 + 64, np.uint8)
+        sz = np.zeros(len(o) - 1, np.uint32)
+        ne, nb = hq.encode_events16_sized_into(o, r[e0:e1], out, sz, T)
+        if out[:nb].tobytes() != want[i][0].tobytes() or not np.array_equal(sz, want[i][1]):
+            bad.append((i, T))
+    for _ in range(5):
+        th = [threading.Thread(target=one, args=(i, (2, 3, 4, 8)[i])) for i in range(W)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert not bad
