@@ -162,10 +162,11 @@ def test_oracle_reproduces_rim_and_c4pq_digests():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["tiles", "columns"])
+@pytest.mark.parametrize("path", ["tiles", "columns", "tiles_compact"])
 def test_gpu_rim_digest(gpu_ctx, hq, path):
-    """rim / rimt at the bench's full size: the multi-ctx release (k_ri_multi2 over 128-group
-    tiles, and over columns) equals the oracle's replay digests."""
+    """rim / rimt / rimtc at the bench's full size: the multi-ctx release (the uniform tile
+    kernel over 128-group tiles, k_ri_multi2 over columns, and the tiles with released_index
+    NULL, rebuilt by hq_ri_released_host) equals the oracle's replay digests."""
     import bench
 
     c = GOLD["RIM"]
@@ -174,17 +175,21 @@ def test_gpu_rim_digest(gpu_ctx, hq, path):
     rel, cnt, bend = (gpu_ctx.empty(K * G, np.uint64), gpu_ctx.empty(G, np.uint8),
                       gpu_ctx.empty(G, np.uint8))
     extra = []
-    if path == "tiles":
+    if path.startswith("tiles"):
         t = gpu_ctx.empty((G // 128) * hq.ri_tile_bytes(K, n, 0), np.uint8)
         gpu_ctx.tile_ri_multi_dev(G, K, n, o, x, None, None, t)
-        gpu_ctx.readindex_multi_tiles_dev(G, K, n, t, 0, n, rel, cnt, batch_end=bend)
+        gpu_ctx.readindex_multi_tiles_dev(G, K, n, t, 0, n,
+                                          None if path == "tiles_compact" else rel, cnt,
+                                          batch_end=bend)
         extra = [t]
     else:
         gpu_ctx.readindex_multi_dev(G, K, n, o, x, None, None, n, rel, cnt, batch_end=bend)
     gpu_ctx.sync()
-    assert (digest(gpu_ctx.download(rel)), digest(gpu_ctx.download(cnt)),
-            digest(gpu_ctx.download(bend))) == (c["released_index"], c["released_count"],
-                                                c["batch_end"])
+    got_cnt, got_bend = gpu_ctx.download(cnt), gpu_ctx.download(bend)
+    got_rel = (hq.ri_released_host(K, idx, got_cnt, got_bend) if path == "tiles_compact"
+               else gpu_ctx.download(rel))
+    assert (digest(got_rel), digest(got_cnt), digest(got_bend)) == (
+        c["released_index"], c["released_count"], c["batch_end"])
     for a in [o, x, rel, cnt, bend] + extra:
         gpu_ctx.free(a)
 
