@@ -479,8 +479,9 @@ int hq_worker::run_pass() {
     // outputs
     const size_t c_out = L.take(8 * Gc), c_chg = L.take(8 * ((Gc + 63) / 64)),
                  c_fb = L.take(8 * ((Gc + 63) / 64));
-    const size_t r_rel = L.take(8 * (size_t)K * Gr), r_cnt = L.take(Gr), r_be = L.take(Gr),
-                 r_fb = L.take(8 * ((Gr + 63) / 64));
+    // (the released indexes are not read back: the compact release, each released entry's index
+    // taken from its closing ctx below)
+    const size_t r_cnt = L.take(Gr), r_be = L.take(Gr), r_fb = L.take(8 * ((Gr + 63) / 64));
     const size_t v_out = L.take(8 * ((Gv + 31) / 32)), v_fb = L.take(8 * ((Gv + 63) / 64));
     const size_t q_hq = L.take(8 * ((Gq + 63) / 64)), q_fb = L.take(8 * ((Gq + 63) / 64));
     const size_t total = L.off;
@@ -565,8 +566,8 @@ int hq_worker::run_pass() {
     if (!rc && Gr)
         rc = hq(hq_readindex_multi_dev(ctx, Gr, K, N, reinterpret_cast<const uint16_t *>(D(r_ord)),
                                        reinterpret_cast<const uint64_t *>(D(r_idx)), D(r_np),
-                                       D(r_nv), 0, reinterpret_cast<uint64_t *>(D(r_rel)),
-                                       D(r_cnt), D(r_be), reinterpret_cast<uint64_t *>(D(r_fb))),
+                                       D(r_nv), 0, nullptr, D(r_cnt), D(r_be),
+                                       reinterpret_cast<uint64_t *>(D(r_fb))),
                 "hq_readindex_multi_dev");
     if (!rc && Gv)
         rc = hq(hq_vote_dev(ctx, Gv, D(v_gr), D(v_rj), D(v_nv), 0,
@@ -603,7 +604,6 @@ int hq_worker::run_pass() {
         g.committed = cout[j];                      // commitTo (logentry.go:323-332)
         g.clear(kCommitDue);
     }
-    const uint64_t *rel = reinterpret_cast<const uint64_t *>(H(r_rel));
     const uint8_t *cnt = H(r_cnt), *be = H(r_be);
     for (uint64_t j = 0; j < Gr; ++j) {
         Group &g = groups[l_ri[j]];
@@ -614,7 +614,9 @@ int hq_worker::run_pass() {
             while (k < c && !((be[j] >> k) & 1)) ++k;
             if (k >= c) return fail(HQ_E_STATE, "ReadIndex release without a closing ctx");
             const ReadStatus &s = q.r[i];
-            const uint64_t index = rel[(uint64_t)i * Gr + j];
+            // confirm() rewrites every released entry's index to the closing ctx's
+            // (readindex.go:96-104): what the kernel's released_index column would hold
+            const uint64_t index = q.r[k].index;
             if (s.from == 0 || s.from == g.node_id)
                 ready.push_back({g.cluster_id, index, s.low, s.high});
             else
