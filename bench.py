@@ -1851,7 +1851,7 @@ def same_decisions(a, b):
                for p, q in zip(a, b))
 
 
-EXTRAS_MULTI = "c5tl,c5v5tl,c4p,cqp,c4pq,rimt,ingo"
+EXTRAS_MULTI = "c5tl,c5v5tl,c4p,cqp,c4pq,rimt,rimtc,ingo"
 
 
 def rank_parity(w, r, d, no_cpu):
