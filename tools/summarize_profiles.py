@@ -35,7 +35,7 @@ KERNEL = {"c2": "k_commit_big<3, 0, 2, false, 0>", "c2t": "k_commit_big<3, 0, 2,
           "rimt": "k_ri_tiles_u<4, 7>", "rimtc": "k_ri_tiles_u<4, 7>",
           "cq": "k_bits<4, false, 256, false, true>", "cqp": "k_cq_planes<6, false, 256>",
           "ing": ("k_bin<false>", "k_apply<false>"), "c4pq": "k_planes_cq<256>",
-          "ingo": "k_table_ingest<true, false>", "rim2": "k_ri_multi2",
+          "ingo": "k_table_ingest<1, false>", "rim2": "k_ri_multi2",
           "c4t3": "k_bits3<256>", "c4p": "k_planes<256>"}
 
 
