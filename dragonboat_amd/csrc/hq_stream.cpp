@@ -8,10 +8,12 @@
 // twin of the decoder is in hq_dstep.hip.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -224,8 +226,8 @@ __attribute__((always_inline)) inline uint8_t *encode16(uint8_t *p, const hq_eve
 // ranges share no written cache line but their ends of `sizes`)
 int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, uint64_t g0,
                 uint64_t g1, std::vector<uint8_t> *grow, uint8_t *out, uint64_t cap,
-                uint64_t *n_events, uint64_t *n_bytes) {
-    uint64_t pos = 0, events = 0;
+                uint64_t *n_events, uint64_t *n_bytes, uint64_t *last_start = nullptr) {
+    uint64_t pos = 0, events = 0, ls = ~0ull;
     uint8_t *base = grow ? grow->data() : out;
     for (uint64_t i = g0; i < g1; ++i) {
         const uint64_t r0 = off[i], r1 = off[i + 1];
@@ -241,10 +243,12 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
         uint64_t ne = 0, ctx[2] = {0, 0};
         Prev pv;
         uint8_t *p = base + pos;
+        uint8_t *lp = nullptr;
         for (uint64_t k = r0; k < r1; ++ne) {
             if (!roomy && (cap < (uint64_t)(p - base) || cap - (uint64_t)(p - base) <
                                                              HQ_EVENT_STREAM_MAX))
                 return HQ_E_STATE;
+            lp = p;
             if (!(recs[k].kind & HQ_EV16_FULL)) {
                 p = encode16(p, recs[k], pv, ctx);
                 ++k;
@@ -257,12 +261,14 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
             p = encode(p, e, pv);
         }
         pos = (uint64_t)(p - base);
+        if (lp) ls = (uint64_t)(lp - base);
         if (ne > 0xFFFF || pos - p0 > 0xFFFF) return HQ_E_INVAL;
         sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
         events += ne;
     }
     *n_events = events;
     *n_bytes = pos;
+    if (last_start) *last_start = ls;
     return HQ_OK;
 }
 
@@ -273,13 +279,36 @@ std::vector<std::vector<std::vector<uint8_t>>> g_scratch_free;
 
 struct alignas(64) RangeOut {   // one thread's results, a cache line each
     uint64_t events = 0, bytes = 0;
+    uint64_t last_start = ~0ull;   // offset of the range's last event in its bytes (none: ~0)
     int rc = HQ_OK;
 };
 
-// The threaded encodes' workers: created once and kept, shared by calls made side by side (a
-// call spawning its T - 1 threads for each of its two phases paid tens of microseconds per
-// thread in a process holding the GPU runtime's mappings). A call queues T - 1 tasks, runs task
-// 0 itself, then runs queued tasks (its own or another call's) until its own are done.
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// phase clocks of the threaded encodes (hq_encode_stats_read)
+struct EncodeClocks {
+    std::atomic<uint64_t> calls{0}, tasks{0}, helped{0}, wall_ns{0}, encode_ns{0}, copy_ns{0},
+        lag_ns{0}, max_lag_ns{0}, run_ns{0};
+    void max_lag(uint64_t v) {
+        uint64_t m = max_lag_ns.load(std::memory_order_relaxed);
+        while (v > m && !max_lag_ns.compare_exchange_weak(m, v, std::memory_order_relaxed)) {
+        }
+    }
+};
+EncodeClocks g_clk;
+
+// The threaded encodes' workers: created once and kept (a call spawning its T - 1 threads for
+// each of its two phases paid tens of microseconds per thread in a process holding the GPU
+// runtime's mappings). A call is one Job: indexes 1..T-1 are queued for the pool, the caller runs
+// index 0 and then takes its own job's remaining indexes from the job's counter — never another
+// call's tasks, so concurrent callers (one per step worker, execengine.go:675-690) do not wait
+// behind each other's work. The Job is shared with every queue entry, so a pool thread that
+// finishes the last index signals through memory the caller no longer owns alone (the caller
+// returns only once every index has finished; an entry popped after that finds no index left).
 class TaskPool {
 public:
     ~TaskPool() {
@@ -302,61 +331,71 @@ public:
         for (auto &x : th) x.join();
         return;
 #endif
-        std::atomic<uint32_t> left(T - 1);
-        std::mutex dm;
-        std::condition_variable dcv;
+        auto job = std::make_shared<Job>();
+        job->fn = &fn;
+        job->T = T;
+        job->queued = now_ns();
         {
             std::lock_guard<std::mutex> lk(mu_);
             demand_ += T - 1;
             while (th_.size() < demand_) th_.emplace_back([this] { loop(); });
-            for (uint32_t t = 1; t < T; ++t)
-                q_.emplace_back([&, t] {
-                    fn(t);
-                    if (left.fetch_sub(1) == 1) {
-                        std::lock_guard<std::mutex> l2(dm);
-                        dcv.notify_all();
-                    }
-                });
+            for (uint32_t t = 1; t < T; ++t) q_.push_back(job);
         }
         cv_.notify_all();
-        fn(0);
-        while (left.load() > 0) {
-            std::function<void()> f;
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                if (!q_.empty()) {
-                    f = std::move(q_.front());
-                    q_.pop_front();
-                }
-            }
-            if (f) {
-                f();
-                continue;
-            }
-            std::unique_lock<std::mutex> l2(dm);
-            dcv.wait(l2, [&] { return left.load() == 0; });
+        run(*job, 0);
+        for (;;) {
+            const uint32_t i = job->next.fetch_add(1);
+            if (i >= T) break;
+            run(*job, i);
+        }
+        {
+            std::unique_lock<std::mutex> l(job->m);
+            job->cv.wait(l, [&] { return job->done == job->T; });
         }
         std::lock_guard<std::mutex> lk(mu_);
         demand_ -= T - 1;
     }
 
 private:
+    struct Job {
+        const std::function<void(uint32_t)> *fn = nullptr;
+        uint32_t T = 0;
+        std::atomic<uint32_t> next{1};
+        uint64_t queued = 0;
+        std::mutex m;
+        std::condition_variable cv;
+        uint32_t done = 0;
+    };
+    static void run(Job &j, uint32_t i) {
+        const uint64_t t0 = now_ns();
+        (*j.fn)(i);
+        g_clk.run_ns += now_ns() - t0;
+        g_clk.tasks++;
+        std::lock_guard<std::mutex> l(j.m);
+        if (++j.done == j.T) j.cv.notify_all();
+    }
     void loop() {
         for (;;) {
-            std::function<void()> f;
+            std::shared_ptr<Job> job;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
                 if (q_.empty()) return;          // stop_ and nothing left
-                f = std::move(q_.front());
+                job = std::move(q_.front());
                 q_.pop_front();
             }
-            f();
+            const uint32_t i = job->next.fetch_add(1);
+            if (i >= job->T) continue;           // the caller took it
+            const uint64_t lag = now_ns() - job->queued;
+            g_clk.lag_ns += lag;
+            g_clk.max_lag(lag);
+            g_clk.helped++;
+            run(*job, i);
         }
     }
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<std::function<void()>> q_;
+    std::deque<std::shared_ptr<Job>> q_;
     std::vector<std::thread> th_;
     size_t demand_ = 0;
     bool stop_ = false;
@@ -385,6 +424,7 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     if (T <= 1)
         return enc16_range(offsets16, recs, sizes, 0, n_groups, nullptr, out, cap, n_events,
                            n_bytes);
+    const uint64_t c0 = now_ns();
     // T ranges of about equal records (group boundaries), each into its own scratch
     std::vector<std::vector<uint8_t>> scratch;
     {
@@ -406,16 +446,20 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     }
     task_pool().parallel_for(T, [&](uint32_t t) {
         res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch[t], nullptr, 0,
-                                &res[t].events, &res[t].bytes);
+                                &res[t].events, &res[t].bytes, &res[t].last_start);
     });
-    uint64_t total = 0, events = 0;
+    const uint64_t c1 = now_ns();
+    uint64_t total = 0, events = 0, last = ~0ull;
     int rc = HQ_OK;
     for (uint32_t t = 0; t < T; ++t) {
         if (res[t].rc && !rc) rc = res[t].rc;
+        if (res[t].last_start != ~0ull) last = total + res[t].last_start;
         total += res[t].bytes;
         events += res[t].events;
     }
-    if (!rc && total > cap) rc = HQ_E_STATE;
+    // the one-thread rule: HQ_EVENT_STREAM_MAX bytes free before every event, i.e. before the
+    // last one (event starts only grow)
+    if (!rc && last != ~0ull && (cap < last || cap - last < HQ_EVENT_STREAM_MAX)) rc = HQ_E_STATE;
     if (!rc) {
         std::vector<uint64_t> at(T, 0);
         for (uint32_t t = 1; t < T; ++t) at[t] = at[t - 1] + res[t - 1].bytes;
@@ -425,9 +469,31 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
         *n_events = events;
         *n_bytes = total;
     }
-    std::lock_guard<std::mutex> lock(g_scratch_mu);
-    g_scratch_free.push_back(std::move(scratch));
+    {
+        std::lock_guard<std::mutex> lock(g_scratch_mu);
+        g_scratch_free.push_back(std::move(scratch));
+    }
+    const uint64_t c2 = now_ns();
+    g_clk.calls++;
+    g_clk.encode_ns += c1 - c0;
+    g_clk.copy_ns += c2 - c1;
+    g_clk.wall_ns += c2 - c0;
     return rc;
+}
+
+int hq_encode_stats_read(hq_encode_stats *out, int reset) {
+    if (!out) return HQ_E_INVAL;
+    auto take = [&](std::atomic<uint64_t> &a) { return reset ? a.exchange(0) : a.load(); };
+    out->calls = take(g_clk.calls);
+    out->tasks = take(g_clk.tasks);
+    out->helped = take(g_clk.helped);
+    out->wall_ns = take(g_clk.wall_ns);
+    out->encode_ns = take(g_clk.encode_ns);
+    out->copy_ns = take(g_clk.copy_ns);
+    out->lag_ns = take(g_clk.lag_ns);
+    out->max_lag_ns = take(g_clk.max_lag_ns);
+    out->run_ns = take(g_clk.run_ns);
+    return HQ_OK;
 }
 
 int hq_events_to16(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,

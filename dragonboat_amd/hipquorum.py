@@ -384,6 +384,7 @@ SIGNATURES = {
                                               _vp, _vp]),
     "hq_events16_encode_sized": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64,
                                                 _vp, _vp, _vp, ctypes.c_uint32]),
+    "hq_encode_stats_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hq_events_to16": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
@@ -1599,6 +1600,18 @@ def encode_events16_sized_into(offsets16, recs, out: np.ndarray, sizes: np.ndarr
                                       _p(out), len(out), _p(sizes), ctypes.byref(ne),
                                       ctypes.byref(nb), threads), "hq_events16_encode_sized")
     return ne.value, nb.value
+
+
+ENCODE_STATS_FIELDS = ("calls", "tasks", "helped", "wall_ns", "encode_ns", "copy_ns", "lag_ns",
+                       "max_lag_ns", "run_ns")
+
+
+def encode_stats(reset: bool = False) -> dict:
+    """hq_encode_stats_read: the threaded encodes' phase clocks (process-wide sums)."""
+    buf = (ctypes.c_uint64 * len(ENCODE_STATS_FIELDS))()
+    _chk(lib.hq_encode_stats_read(ctypes.addressof(buf), 1 if reset else 0),
+         "hq_encode_stats_read")
+    return dict(zip(ENCODE_STATS_FIELDS, (int(x) for x in buf)))
 
 
 def encode_events16_sized(offsets16, recs, threads: int = 1):

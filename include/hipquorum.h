@@ -1085,14 +1085,25 @@ typedef struct hq_event16 {
 /* Encode compact records: group i's records are recs[offsets16[i] .. offsets16[i + 1]) (an
  * escape and its 4 records are one event). Writes the sized form as hq_events_encode_sized does
  * for the equivalent rows (the same bytes and size words) and the event and byte totals.
- * threads > 1: that many native threads, each encoding a range of groups into its own scratch
- * before the ranges are copied into place (one such call at a time per process; 0 or 1: the
- * calling thread only). HQ_E_INVAL on a malformed escape or a group of 2^16 events or bytes;
- * HQ_E_STATE when out (cap bytes) cannot hold the stream (one thread: as hq_events_encode_sized,
- * fewer than HQ_EVENT_STREAM_MAX bytes left before an event). */
+ * threads > 1: that many native threads (a persistent pool shared by concurrent calls; a caller
+ * runs only its own call's ranges), each encoding a range of groups into its own scratch before
+ * the ranges are copied into place (0 or 1: the calling thread only). HQ_E_INVAL on a malformed
+ * escape or a group of 2^16 events or bytes; HQ_E_STATE when fewer than HQ_EVENT_STREAM_MAX bytes
+ * of out (cap bytes) are left before an event — the same rule at every thread count, as
+ * hq_events_encode_sized (size out for HQ_EVENT_STREAM_MAX per event to never hit it). */
 int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const hq_event16 *recs,
                              uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_events,
                              uint64_t *n_bytes, uint32_t threads);
+/* Phase clocks of the threaded hq_events16_encode_sized calls (diagnostic; process-wide sums
+ * since the last reset): wall = encode + copy phase per call; a range ("task") queued for the
+ * pool waits `lag` from the call's queueing until a pool thread starts it (`helped` such starts;
+ * the others ran on the caller); `run` = the tasks' own time. */
+typedef struct hq_encode_stats {
+    uint64_t calls, tasks, helped;
+    uint64_t wall_ns, encode_ns, copy_ns;
+    uint64_t lag_ns, max_lag_ns, run_ns;
+} hq_encode_stats;
+int hq_encode_stats_read(hq_encode_stats *out, int reset);
 /* Rows to compact records: group i's events (offsets as in hq_step_input) become records
  * out[offsets16[i] .. offsets16[i + 1]) (an event that does not fit takes an escape: 5 records).
  * HQ_E_STATE when cap records cannot hold them (5 per event always can). */

@@ -266,8 +266,7 @@ def test_compact_step_workload_has_no_escapes(hq, name):
 
 
 def test_compact_records_malformed(hq):
-    """An escape without its 4 records is HQ_E_INVAL; an output region too small is HQ_E_STATE
-    (single thread: room for HQ_EVENT_STREAM_MAX before each event; threads: the total)."""
+    """An escape without its 4 records is HQ_E_INVAL; an output region too small is HQ_E_STATE."""
     recs = np.zeros(3, hq.EVENT16_DTYPE)
     recs["kind"] = hq.EV16_FULL
     with pytest.raises(hq.HQError):
@@ -281,9 +280,48 @@ def test_compact_records_malformed(hq):
         sizes = np.zeros(len(off) - 1, np.uint32)
         with pytest.raises(hq.HQError):
             hq.encode_events16_sized_into(off16, recs, out, sizes, threads)
-    out = np.zeros(nb, np.uint8)                  # exactly the stream: enough for threads
-    assert hq.encode_events16_sized_into(off16, recs, out, np.zeros(len(off) - 1, np.uint32),
-                                         4) == (len(ev), nb)
+
+
+def test_compact_capacity_rule_same_on_every_thread_count(hq):
+    """The capacity rule does not depend on the thread count: HQ_EVENT_STREAM_MAX
+    bytes free before every event, as hq_events_encode_sized. Every cap from just below the
+    stream's length to HQ_EVENT_STREAM_MAX past it succeeds or fails alike on 1, 4 and 8 threads,
+    with the same bytes when it succeeds."""
+    off, ev = _random_groups(hq, 22)
+    recs, off16 = hq.events_to16(off, ev)
+    want_data, want_sizes = hq.encode_events_sized(off, ev)
+    nb = len(want_data)
+    outcomes = set()
+    for cap in range(nb - 2, nb + hq.HQ_EVENT_STREAM_MAX + 2):
+        got = []
+        for threads in (1, 4, 8):
+            out = np.zeros(cap, np.uint8)
+            sizes = np.zeros(len(off) - 1, np.uint32)
+            try:
+                ne, n = hq.encode_events16_sized_into(off16, recs, out, sizes, threads)
+                assert (ne, n) == (len(ev), nb)
+                np.testing.assert_array_equal(out[:n], want_data)
+                np.testing.assert_array_equal(sizes, want_sizes)
+                got.append("ok")
+            except hq.HQError as e:
+                assert e.code == hq.HQ_E_STATE
+                got.append("state")
+        assert len(set(got)) == 1, (cap, got)
+        outcomes.add(got[0])
+    assert outcomes == {"ok", "state"}   # the boundary lies inside the swept caps
+
+
+def test_encode_stats_count_threaded_calls(hq):
+    """hq_encode_stats_read: a threaded call is counted with its tasks and phase clocks."""
+    off, ev = _random_groups(hq, 23, n=4000)
+    recs, off16 = hq.events_to16(off, ev)
+    hq.encode_stats(reset=True)
+    hq.encode_events16_sized(off16, recs, threads=4)
+    st = hq.encode_stats(reset=True)
+    assert st["calls"] == 1 and st["tasks"] == 8          # 4 ranges, 2 phases
+    assert st["wall_ns"] >= st["encode_ns"] > 0 and st["run_ns"] > 0
+    assert st["helped"] <= st["tasks"] and st["max_lag_ns"] <= st["lag_ns"]
+    assert hq.encode_stats()["calls"] == 0
 
 
 def test_threaded_encodes_side_by_side(hq):
