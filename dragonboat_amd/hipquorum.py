@@ -42,7 +42,7 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 16
+HQ_ABI_VERSION = 17
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -278,6 +278,7 @@ SIGNATURES = {
     "hq_engine_done_clock": (ctypes.c_int, [_vp, ctypes.c_uint64, _u64p]),
     "hq_engine_info": (ctypes.c_int, [_vp, ctypes.POINTER(EngineStats)]),
     "hq_engine_last_error": (ctypes.c_char_p, [_vp]),
+    "hq_engine_dump": (ctypes.c_int, [_vp, ctypes.c_void_p, ctypes.c_uint32]),
     "hq_engine_close": (None, [_vp]),
     "hq_commit_lag_fused_dev": (ctypes.c_int, [_vp, ctypes.POINTER(LagArgs), ctypes.c_uint32]),
     "hq_pack_lags": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp,
@@ -920,6 +921,17 @@ class Engine:
 
     def wait(self, seq: int) -> None:
         self._check(lib.hq_engine_wait(self.h, seq))
+
+    def dump(self) -> dict:
+        """hq_engine_dump: the device-side state (diagnostic)."""
+        n = 8 + 16384
+        buf = (ctypes.c_uint64 * n)()
+        self._check(lib.hq_engine_dump(self.h, buf, n))
+        head = ("posted", "relayed", "polled", "exit_epoch", "launches", "grid", "completed",
+                "running")
+        out = {k: int(buf[i]) for i, k in enumerate(head)}
+        out["cursor"] = np.frombuffer(buf, np.uint64, out["grid"], 8 * 8).copy()
+        return out
 
     def drain(self) -> None:
         self._check(lib.hq_engine_drain(self.h))

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 16
+#define HQ_ABI_VERSION 17
 
 /* status codes */
 #define HQ_OK          0
@@ -186,7 +186,7 @@ int hq_timing_reset(hq_ctx *ctx);
  *
  * Layout HQ_LAYOUT_TILES: the per-group input columns of 128 consecutive groups are stored as
  * one contiguous tile, so a wave reads its groups as ONE stream instead of n + 3 column streams
- * (6 % less time for the same bytes at 1 M groups x 3 voters, tools/kexp5.hip). `match` points
+ * (6 % less time for the same bytes at 1 M groups x 3 voters, tools/kexp5.hip, git history). `match` points
  * to tile 0 (16-byte aligned); tile t = match + t * hq_commit_tile_words(n_max, form) holds
  * groups [128 t, 128 t + 128), each row 128 entries of one field, position 2i holding group
  * 128 t + i and position 2i + 1 group 128 t + 64 + i (lane i of a wave reads both with one
@@ -329,6 +329,11 @@ int hq_engine_timing(hq_engine *eng, uint64_t *launches, double *total_ms, int r
 /* The device clock (s_memrealtime, 100 MHz) when step seq completed (HQ_ENGINE_SIGNAL). */
 int hq_engine_done_clock(hq_engine *eng, uint64_t seq, uint64_t *ticks);
 int hq_engine_info(hq_engine *eng, hq_engine_stats *out);
+/* Diagnostic: the engine's state as the device holds it (readable while the grid runs): out[0]
+ * posted (host ring), [1] relayed, [2] the relayed count the workgroups poll, [3] the exit
+ * epoch, [4] launches, [5] grid, [6] completed, [7] running, then every workgroup's cursor (the
+ * next step it takes at a launch). n_words >= 8 + grid. */
+int hq_engine_dump(hq_engine *eng, uint64_t *out, uint32_t n_words);
 const char *hq_engine_last_error(const hq_engine *eng);
 /* Drain and destroy. NULL is a no-op. */
 void hq_engine_close(hq_engine *eng);
@@ -498,7 +503,7 @@ int hq_readindex_vote_dev(hq_ctx *ctx, uint64_t G, const uint8_t *ack, const uin
  * The same fused pass over a tiled bitmap layout: the bitmaps of 1024 consecutive groups (one
  * wave, 16 groups per lane) stored as one contiguous block of 1024-byte rows
  *   [n_voting (per_group_n only)] [ack] [granted] [rejected]
- * so a wave reads ONE stream instead of 3-4 columns (tools/kexp8.hip: 14.5 vs 15.5 us per
+ * so a wave reads ONE stream instead of 3-4 columns (tools/kexp8.hip, git history: 14.5 vs 15.5 us per
  * 16M x 7 launch, 11.1 vs 11.9 us with uniform n). Tile t starts at tiles + t * rows * 1024,
  * byte (g & 1023) of each row is group g; the last tile is padded to 1024 groups (padding is
  * never decided). Outputs are the columns of hq_readindex_vote_dev. Same decisions as
