@@ -103,6 +103,9 @@ tools/lib_stepchunks%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_STEP_CHUNKS=$*)
 tools/lib_plcqzero%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_PLCQ_ZERO_EARLY=$*)
-# persistent-engine experiments (tools/ab_engine.py): multi-batch loop / flat kernels beside the engine
-tools/lib_engexp/libhipquorum.so: $(SRCS) $(DEPS)
-	$(call variant,-DHQ_ENGINE_EXP)
+# persistent-engine experiments (tools/ab_engine.py): multi-batch loop / flat / claim kernels beside
+# the engine, in a library of their own linked against the product library
+tools/lib_engexp/libengexp.so: tools/engine_exp.hip $(LIB) $(DEPS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ tools/engine_exp.hip -L$(LIBDIR) -lhipquorum -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+

@@ -3,6 +3,8 @@
 // forms and the body that decides one 128-group tile (HQ_LAYOUT_TILES / _TILES_LEADER).
 #pragma once
 
+#include <type_traits>
+
 #include "hq_internal.h"
 
 namespace {
@@ -11,8 +13,8 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Streaming columns are read once: nontemporal loads (measured ~6 % faster than plain ones on
-// the 1M x 3 commit stream, tools/kexp.hip). The committed column is stored with plain stores:
-// 11.10 vs 11.45 us per 1M x 3 launch against nontemporal ones (tools/kexp3.hip; sc1
+// the 1M x 3 commit stream, tools/kexp.hip, git history). The committed column is stored with plain stores:
+// 11.10 vs 11.45 us per 1M x 3 launch against nontemporal ones (tools/kexp3.hip, git history; sc1
 // write-through 11.19, nt sc1 12.36).
 __device__ __forceinline__ u64x2 ld_stream2(const uint64_t *p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
@@ -23,7 +25,7 @@ __device__ __forceinline__ void st_stream2(uint64_t *p, u64x2 v) {
 
 // The decision kernels' argument: only what one form reads, 96 bytes. Kernel arguments past
 // that cost the 1M-group launch 0.25 us (a 160-byte twin of the same kernel: 10.55 vs 10.30 us,
-// tools/kexp6.hip), so the form-specific columns share the `aux` and `ring` slots.
+// tools/kexp6.hip, git history), so the form-specific columns share the `aux` and `ring` slots.
 struct CommitK {
     uint64_t G;
     uint64_t stride;        // columns: elements between match rows; tiles: u64 words per tile
@@ -168,7 +170,17 @@ __device__ __forceinline__ void st8(uint64_t *p, uint64_t v) {
     else *p = v;
 }
 
-template <int N, int FORM, bool PERN, int LEAD, bool INPLACE, bool WT = false>
+// SOFF: the full-tile path addresses every row and output as a uniform (SGPR) base plus this
+// lane's 32-bit byte offset (global_load saddr + voffset), so no 64-bit per-lane address lives in
+// VGPRs across the caller's loop (the persistent engine, hq_engine.hip: its step loop otherwise
+// kept `match + 16 * lane` as a u64 pair and spilled it)
+template <class T>
+__device__ __forceinline__ T *byte_off(T *p, uint32_t off) {
+    return reinterpret_cast<T *>(reinterpret_cast<
+        typename std::conditional<std::is_const<T>::value, const char, char>::type *>(p) + off);
+}
+
+template <int N, int FORM, bool PERN, int LEAD, bool INPLACE, bool WT = false, bool SOFF = false>
 __device__ __forceinline__ void commit_tile(const CommitK &a, uint64_t wbase, uint64_t lane) {
     constexpr uint64_t T = HQ_TILE_GROUPS, H = T / 2;
     constexpr int NR = N - LEAD;   // match rows in the tile
@@ -176,25 +188,35 @@ __device__ __forceinline__ void commit_tile(const CommitK &a, uint64_t wbase, ui
     const uint64_t ga = wbase + lane, gb = ga + H;
     bool ca = false, cb = false, fa = false, fb = false;
     if (wbase + T <= a.G) {
+        // row r of the tile at lane's 16 bytes
+        const uint64_t *tb = a.match + (wbase / T) * a.stride;   // uniform
+        const uint32_t lo = (uint32_t)lane * 16u;
+        auto row = [&](int r) -> const uint64_t * {
+            if constexpr (SOFF) return byte_off(tb + r * T, lo);
+            return t + r * T;
+        };
         uint64_t m0[N], m1[N];
 #pragma unroll
         for (int s = LEAD; s < N; ++s) {
-            const u64x2 v = ld_stream2(t + (s - LEAD) * T);
+            const u64x2 v = ld_stream2(row(s - LEAD));
             m0[s] = v.x;
             m1[s] = v.y;
         }
-        const u64x2 ci = ld_stream2(t + NR * T), la = ld_stream2(t + (NR + 1) * T);
+        const u64x2 ci = ld_stream2(row(NR)), la = ld_stream2(row(NR + 1));
         if constexpr (LEAD) {
             m0[0] = la.x;
             m1[0] = la.y;
         }
         u64x2 ax;
         if constexpr (FORM == HQ_FORM_TERM_MASK) {
-            const uint32_t mm = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(
-                reinterpret_cast<const uint16_t *>(t - lane * 2 + (NR + 2) * T) + lane * 2));
+            const uint32_t *mp =
+                SOFF ? byte_off(reinterpret_cast<const uint32_t *>(tb + (NR + 2) * T), lo / 4)
+                     : reinterpret_cast<const uint32_t *>(
+                           reinterpret_cast<const uint16_t *>(t - lane * 2 + (NR + 2) * T) + lane * 2);
+            const uint32_t mm = __builtin_nontemporal_load(mp);
             ax = (u64x2){mm & 0xFFFFu, mm >> 16};
         } else {
-            ax = ld_stream2(t + (NR + 2) * T);
+            ax = ld_stream2(row(NR + 2));
         }
 #if HQ_TILE_SCHED_BARRIER
         // every row load of the tile is issued before the first compare: otherwise the
@@ -223,12 +245,17 @@ __device__ __forceinline__ void commit_tile(const CommitK &a, uint64_t wbase, ui
 #endif
         if constexpr (INPLACE) {
             // the lane's 16 bytes of the committed row it has just read (groups ga, gb)
+            uint64_t *cr = const_cast<uint64_t *>(row(NR));
             if constexpr (WT) {
-                st8<true>(const_cast<uint64_t *>(t) + NR * T, coa);
-                st8<true>(const_cast<uint64_t *>(t) + NR * T + 1, cob);
+                st8<true>(cr, coa);
+                st8<true>(cr + 1, cob);
             } else {
-                st_stream2(const_cast<uint64_t *>(t) + NR * T, (u64x2){coa, cob});
+                st_stream2(cr, (u64x2){coa, cob});
             }
+        } else if constexpr (SOFF) {
+            uint64_t *cb0 = a.cout + wbase;   // uniform
+            st8<WT>(byte_off(cb0, lo / 2), coa);
+            st8<WT>(byte_off(cb0 + H, lo / 2), cob);
         } else {
             st8<WT>(a.cout + ga, coa);
             st8<WT>(a.cout + gb, cob);

@@ -9,30 +9,38 @@
 // own launch (MI355X_MICROARCH.md "boundary": 1.7-1.9 us between streaming kernels, ~18 % of a
 // 1M-group step; DESIGN.md §7 size sweep).
 //
-// Ownership: wave w of the grid decides tiles w, w + W, w + 2W, ... of EVERY posted batch, in
-// post order. A group's step s + 1 depends only on its own step s (the in-place table's
-// committed row, raft.go:888-909 run per ReplicateResp on that group's state), so the waves need
-// no grid barrier between steps: a wave that finishes its tiles of step s starts step s + 1 while
-// the others still stream step s (every wave runs its own step sequence: no barrier, no LDS).
+// Ownership: workgroup b owns tiles [b * per, b * per + per) of every posted batch (per =
+// ceil(tiles / grid), computed by the host). Its waves take those tiles through ONE monotone LDS
+// ticket counter: ticket t is tile t - end(s - 1) of the first step s with t < end(s), where
+// end(s) is the workgroup's cumulative tile count through step s. The waves balance each other
+// inside the workgroup, a wave moves from step s to s + 1 with no barrier, re-arm or failing claim
+// (a ticket is always a tile of some step), and a step transition costs a few LDS reads.
+// A group's step s + 1 depends only on its own step s (the in-place table's committed row,
+// raft.go:888-909 run per ReplicateResp on that group's state); with HQ_LAYOUT_IN_PLACE the
+// posted steps keep one G, so a tile stays with its workgroup and a wave starts step s + 1 only
+// when the workgroup has decided all of step s.
 //
 // Doorbell: the host writes a 64-byte descriptor into the pinned ring and then bumps `posted`
-// (both fine-grained host memory). The first wave of workgroup 0 relays new descriptors into a
-// device copy of the ring and publishes the relayed count in device memory; a wave at the end of
-// what it knows polls that count (relaxed agent-scope load + s_sleep, MI355X_MICROARCH.md
-// "polling-cost") and reads each step's descriptor one step ahead. Completion
-// (HQ_ENGINE_SIGNAL): a wave counts its arrival on one of 64 shard counters, the last wave of a
-// shard on the step's top counter, and the last of those writes the step's sequence number into
-// the pinned done array (one PCIe write per step).
+// (both fine-grained host memory). The poller of workgroup 0 relays new descriptors into a
+// device copy of the ring and publishes the relayed count in 16 device copies; a workgroup whose
+// waves have run out of known steps polls one copy (relaxed agent-scope load + s_sleep,
+// MI355X_MICROARCH.md "polling-cost"). Completion (HQ_ENGINE_SIGNAL): a workgroup counts its
+// arrival on one of 8 shard counters, the last workgroup of a shard on the step's top counter,
+// and the last of those writes the step's sequence number into the pinned done array (one PCIe
+// write per step).
 //
-// Every spin is bounded: a wave that polls without news for idle_us exits (its next step is kept
-// in a device cursor, and the next post or wait relaunches the grid, which resumes every wave at
-// its cursor), so a host that dies never leaves waves spinning on the GPU.
+// Every spin is bounded: workgroup 0 ends the launch after idle_us without a post by publishing
+// the launch's epoch in `d_exit` (after relaying everything it saw); every workgroup leaves once
+// its waves have caught up with the relayed steps, so the grid exits as a whole and the next post
+// or wait relaunches it (each workgroup resumes at its cursor). A host that dies never leaves
+// waves spinning on the GPU.
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 
 #include "hq_commit_body.h"
@@ -46,17 +54,9 @@ constexpr int kShards = 8;                 // workgroup arrival counters per ste
 constexpr int kPollCopies = 16;            // copies of the relayed count, 256 B apart: 512
                                            // workgroups polling ONE word queue on its channel
                                            // (the first descriptors reached the last sampled
-                                           // workgroup 97 us after the launch, tools/ab_engine.py)
+                                           // workgroup 97 us after the launch, round-4 probes)
 constexpr int kPollStride = 32;            // u64 between copies
 constexpr int kInit = 32;                  // descriptors handed over in the kernel arguments
-
-// A descriptor as the kernel arguments carry it (EngineDesc without seq / reserved).
-struct InitDesc {
-    uint64_t G;
-    const uint64_t *tiles;
-    uint64_t *cout, *changed, *fallback;
-    uint64_t flags;
-};
 
 struct EngineDesc {   // one posted step, 64 bytes = 8 u64 words (one per relay lane)
     uint64_t G;
@@ -66,7 +66,7 @@ struct EngineDesc {   // one posted step, 64 bytes = 8 u64 words (one per relay 
     uint64_t *fallback;
     uint64_t seq;
     uint64_t flags;
-    uint64_t reserved;
+    uint64_t per;       // tiles per workgroup: ceil(ceil(G / 128) / grid), set by the host
 };
 static_assert(sizeof(EngineDesc) == 64, "a descriptor is 8 relay lanes of u64");
 
@@ -75,8 +75,8 @@ struct EngineK {
     uint64_t idle_ticks;    // s_memrealtime ticks (100 MHz) of polling without news before exit
     uint32_t R;             // term-mask window
     uint32_t depth;         // ring slots (power of two <= kEngineMaxDepth)
-    uint32_t waves;         // worker waves in the grid
     uint32_t signal;        // per-step completion into the pinned done array
+    uint32_t epoch;         // this launch's number (d_exit == epoch: the grid ends)
     const uint64_t *h_posted;      // pinned: descriptors written by the host
     uint64_t *h_done;              // pinned [depth]: seq + 1 of the last step completed per slot
     uint64_t *h_clock;             // pinned [depth]: s_memrealtime at that completion
@@ -86,23 +86,14 @@ struct EngineK {
     uint64_t *d_top;               // device [depth]
     uint64_t *d_cursor;            // device [grid]: the next step of each workgroup
     EngineDesc *d_ring;            // device [depth]
-    uint64_t *dbg;                 // HQ_ENGINE_EXP phase clocks (tools/ab_engine.py), else NULL
     uint64_t *d_polled;            // device [kPollCopies * kPollStride]: copies of d_posted
+    uint64_t *d_exit;              // device: the epoch of the launch that is ending
     // the descriptors of steps [init_base, init_base + init_count), known when the grid was
     // launched: every workgroup starts with them in LDS (no relay, no poll at the start)
     uint64_t init_base;
-    uint32_t init_count, exp;   // exp: HQ_ENGINE_EXP variant bits (0 in the product)
-    InitDesc init[kInit];
+    uint32_t init_count, pad;
+    EngineDesc init[kInit];
 };
-
-#ifdef HQ_ENGINE_EXP
-// phase clocks of the experiment build: min (i even) / max (i odd) or plain store
-#define HQ_EPROBE_MIN(e, i) __hip_atomic_fetch_min((e).dbg + (i), now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#define HQ_EPROBE_MAX(e, i) __hip_atomic_fetch_max((e).dbg + (i), now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#else
-#define HQ_EPROBE_MIN(e, i) ((void)0)
-#define HQ_EPROBE_MAX(e, i) ((void)0)
-#endif
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
@@ -114,7 +105,7 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 
 // A pointer read from memory (a posted descriptor) is generic to the compiler, and generic
 // pointers compile to FLAT loads and stores (counted in both vmcnt and lgkmcnt: every wait drains
-// everything; 13.1 vs 10.2 us per 1M-group step, tools/ab_engine.py). Descriptors hold device
+// everything; 13.1 vs 10.2 us per 1M-group step, round-4 probes). Descriptors hold device
 // (global) addresses by contract, so the value is cast into the global address space and back:
 // the compiler then infers global for every access through it.
 template <class T>
@@ -123,13 +114,25 @@ __device__ __forceinline__ T *as_global(uint64_t v) {
     return (T *)(GT *)v;
 }
 
-// Workgroup 0, first wave: copy the descriptors the host has posted since the last relay into
-// the device ring and publish their count. Lane l moves u64 word l & 7 of descriptor l >> 3 (+8i).
+// The kernel's argument as the rare paths (poll, relay, arrival) read it: volatile loads from the
+// kernarg segment at each use, so the compiler keeps none of those fields live across the tile
+// loop (held in SGPRs, they pushed the loop's own values into VGPR lanes and scratch)
+typedef __attribute__((address_space(1))) const volatile EngineK GlobalEngineK;
+__device__ __forceinline__ GlobalEngineK &kargs() {
+    return *(GlobalEngineK *)reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+// a pointer field of the engine's argument as a global-address-space pointer (no FLAT access)
+template <class T>
+__device__ __forceinline__ T *gp(T *p) { return as_global<T>(reinterpret_cast<uint64_t>(p)); }
+
+// Workgroup 0's poller: copy the descriptors the host has posted since the last relay into the
+// device ring and publish their count. Lane l moves u64 word l & 7 of descriptor l >> 3 (+8i).
 // The host never posts more than `depth` steps beyond the last completed one, so the slots
 // written here are no longer read by any workgroup.
-__device__ void relay(const EngineK &e, uint32_t lane) {
-    const uint64_t have = __hip_atomic_load(e.d_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t hp = __hip_atomic_load(e.h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ void relay(GlobalEngineK &e, uint32_t lane) {
+    const uint64_t have = __hip_atomic_load(gp(e.d_posted), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hp = __hip_atomic_load(gp(e.h_posted), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (hp <= have) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: the ring entries behind posted
     const uint64_t n = hp - have < e.depth ? hp - have : e.depth;
@@ -142,7 +145,7 @@ __device__ void relay(const EngineK &e, uint32_t lane) {
         for (int j = 0; j < 4; ++j) {
             const uint64_t i = base + (lane >> 3) + 8 * j;
             v[j] = i < n ? __hip_atomic_load(
-                               reinterpret_cast<const uint64_t *>(e.h_ring + ((have + i) & dmask)) +
+                               reinterpret_cast<const uint64_t *>(gp(e.h_ring) + ((have + i) & dmask)) +
                                    (lane & 7),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                          : 0;
@@ -151,68 +154,91 @@ __device__ void relay(const EngineK &e, uint32_t lane) {
         for (int j = 0; j < 4; ++j) {
             const uint64_t i = base + (lane >> 3) + 8 * j;
             if (i < n)
-                __hip_atomic_store(reinterpret_cast<uint64_t *>(e.d_ring + ((have + i) & dmask)) +
+                __hip_atomic_store(reinterpret_cast<uint64_t *>(gp(e.d_ring) + ((have + i) & dmask)) +
                                        (lane & 7),
                                    v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0)
-        __hip_atomic_store(e.d_posted, have + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gp(e.d_posted), have + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane < (uint32_t)kPollCopies)
-        __hip_atomic_store(e.d_polled + lane * kPollStride, have + n, __ATOMIC_RELAXED,
+        __hip_atomic_store(gp(e.d_polled) + lane * kPollStride, have + n, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == 0) {
-        HQ_EPROBE_MIN(e, 2);   // first relay published
-        HQ_EPROBE_MAX(e, 3);   // last relay published
-    }
+}
+
+// The workgroup is done with step s (called once per workgroup and step). In signal mode the
+// tiles' stores were write-through (WT) and every deciding wave drained them before counting its
+// tile, so they are visible device-wide with no release fence (Guideline 16 R1; a release fence
+// per workgroup and step, an L2 write-back each, took 26 us per step). The workgroup counts on
+// the step's shard counter (blockIdx % 8), the last workgroup of a shard on the step's top
+// counter, and the last of those publishes the step to the host. The last arriver of a counter
+// resets it for the slot's next step: the host posts that step only after it has seen this one's
+// done flag, which is written after the resets.
+__device__ void arrive(GlobalEngineK &e, uint64_t s) {
+    const uint64_t slot = s & (e.depth - 1);
+    const uint32_t shard = blockIdx.x % kShards;
+    const uint32_t nshard = gridDim.x < (uint32_t)kShards ? gridDim.x : (uint32_t)kShards;
+    const uint64_t per = (gridDim.x - shard + kShards - 1) / kShards;   // workgroups in the shard
+    uint64_t *ctr = gp(e.d_arrive) + slot * kShards + shard;
+    if (__hip_atomic_fetch_add(ctr, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 !=
+        per)
+        return;
+    __hip_atomic_store(ctr, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(gp(e.d_top) + slot, (uint64_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) + 1 != nshard)
+        return;
+    __hip_atomic_store(gp(e.d_top) + slot, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gp(e.h_clock) + slot, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(gp(e.h_done) + slot, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Per-workgroup state in LDS. The descriptors of steps [.., known) sit in `ring` (slot = step &
-// (depth - 1)); a wave that has run out of them waits for `known` to grow. The first such wave
-// takes `lock` and becomes the workgroup's poller: it polls the relayed count in device memory
-// (workgroup 0's poller relays from the host ring first), copies the new descriptors into LDS and
-// publishes `known`. `waiting` counts the waves at the end of what they know; the workgroup exits
-// idle only when all of them are (so they leave at one step). Per ring slot, `claim` hands out
-// the workgroup's tiles of the slot's step one by one (a fetch-add per tile) and `fin` counts
-// those decided; `tag` is the step they serve. The first wave to reach a step re-arms its
-// slot's counters, once no wave of the workgroup is still on the slot's previous step
-// (`cur[w]`: the step wave w claims in).
+// (depth - 1)) with `end` (the workgroup's cumulative tile count through the slot's step, counted
+// from this launch's cursor, mod 2^32) and `tgt` (the value of the slot's `fin` counter at which
+// the workgroup has decided the slot's step: signal mode). `ticket` hands out the workgroup's
+// tiles of all its steps in order; `done` counts decided tiles (in-place mode). Tickets, ends and
+// counters are u32 compared by differences: only values within a few ring lengths of steps are
+// ever compared. A wave whose ticket is beyond the known steps waits for `known` to grow: the
+// first such wave takes `lock` and becomes the workgroup's poller (workgroup 0's poller relays
+// from the host ring first), copies the new descriptors into LDS, extends `end` / `tgt` and
+// publishes `known`. `waiting` counts the waves at the end of what they know; the workgroup
+// exits only when all of them are (at one step).
 struct EngineLds {
     EngineDesc ring[kEngineMaxDepth];
-    uint64_t tag[kEngineMaxDepth];
-    uint32_t claim[kEngineMaxDepth];
+    uint32_t end[kEngineMaxDepth];
     uint32_t fin[kEngineMaxDepth];
-    uint64_t cur[16];
+    uint32_t tgt[kEngineMaxDepth];
     uint64_t known;
-    uint32_t waiting, lock, exit, pad;
+    uint32_t ticket;
+    uint32_t top_end;     // end of the last installed step
+    uint32_t done;
+    uint32_t waiting, lock, exit;
 };
 
-constexpr uint64_t kTagBusy = ~0ull;   // a wave is re-arming the slot
+__device__ __forceinline__ bool before(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
 
-// lane 0: make slot `slot` serve step s (no-op when it does): the winner of the tag waits until
-// every wave of the workgroup has left the slot's previous step (s - depth), zeroes the
-// counters and publishes the tag; the others wait for it.
-template <int WPW>
-__device__ void arm_slot(EngineLds &l, uint64_t slot, uint64_t s, uint64_t depth) {
-    for (;;) {
-        uint64_t t = __hip_atomic_load(&l.tag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (t == s) return;
-        if (t != kTagBusy && __hip_atomic_compare_exchange_strong(
-                                 &l.tag[slot], &t, kTagBusy, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
-#pragma unroll 1
-            for (int w = 0; w < WPW; ++w)
-                while (__hip_atomic_load(&l.cur[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) +
-                           depth <= s)
-                    __builtin_amdgcn_s_sleep(1);
-            __hip_atomic_store(&l.claim[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&l.fin[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&l.tag[slot], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
+// the workgroup's tiles of a step
+__device__ __forceinline__ uint64_t wg_len(uint64_t G, uint64_t per) {
+    const uint64_t tiles = (G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per;
+    return b0 >= tiles ? 0 : (tiles - b0 < per ? tiles - b0 : per);
+}
+
+// One thread: extend end / tgt over the descriptors of steps [from, to) now in the LDS ring. A
+// step in which the workgroup owns no tile is complete for it at once (signal: arrive now).
+__device__ void install(GlobalEngineK &e, EngineLds &l, uint64_t from, uint64_t to) {
+    const uint64_t dmask = e.depth - 1;
+    uint32_t top = l.top_end;
+    for (uint64_t s = from; s < to; ++s) {
+        const EngineDesc &d = l.ring[s & dmask];
+        const uint32_t len = (d.flags & kDescStop) ? 0u : (uint32_t)wg_len(d.G, d.per);
+        top += len;
+        l.end[s & dmask] = top;
+        l.tgt[s & dmask] += len;
+        if (len == 0 && e.signal && !(d.flags & kDescStop)) arrive(e, s);
     }
+    l.top_end = top;
 }
 
 __device__ __forceinline__ uint64_t lds_known(EngineLds &l) {
@@ -223,17 +249,18 @@ __device__ __forceinline__ uint64_t lds_known(EngineLds &l) {
 __device__ __forceinline__ uint32_t wave_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // A wave at step s with no descriptor beyond it (s == the workgroup's known count): returns the
-// new known count, or s when the workgroup exits idle (the wave then exits at s).
+// new known count, or s when the workgroup exits (the wave then exits at s).
 template <int WPW>
-__device__ uint64_t frontier(const EngineK &e, EngineLds &l, uint64_t s, uint32_t lane,
-                             bool relayer) {
+__device__ uint64_t frontier(GlobalEngineK &e, EngineLds &l, uint64_t s, uint32_t lane) {
     uint64_t k = lds_known(l);
     if (k > s) return k;
+    const bool relayer = blockIdx.x == 0;
     if (lane == 0) __hip_atomic_fetch_add(&l.waiting, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (;;) {
-        k = lds_known(l);
+        k = uniform64(lds_known(l));
         if (k > s) break;
-        if (__hip_atomic_load(&l.exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return s;
+        if (wave_u32(__hip_atomic_load(&l.exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+            return s;
         uint32_t got = 0;
         if (lane == 0)
             got = __hip_atomic_exchange(&l.lock, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
@@ -241,33 +268,54 @@ __device__ uint64_t frontier(const EngineK &e, EngineLds &l, uint64_t s, uint32_
             // the workgroup's poller
             const uint64_t t0 = now_ticks();
             uint32_t backoff = 1;
+            bool leave = false;
             for (;;) {
                 if (relayer) relay(e, lane);
-                const uint64_t p =
-                    __hip_atomic_load(e.d_polled + (blockIdx.x % kPollCopies) * kPollStride,
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t p = uniform64(
+                    __hip_atomic_load(gp(e.d_polled) + (blockIdx.x % kPollCopies) * kPollStride,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 if (p > s) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     const uint64_t dmask = e.depth - 1;
                     for (uint64_t i = lane >> 3; i < p - s; i += 8) {
                         const uint64_t slot = (s + i) & dmask;
                         reinterpret_cast<uint64_t *>(l.ring + slot)[lane & 7] = __hip_atomic_load(
-                            reinterpret_cast<const uint64_t *>(e.d_ring + slot) + (lane & 7),
+                            reinterpret_cast<const uint64_t *>(gp(e.d_ring) + slot) + (lane & 7),
                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     if (lane == 0) {
+                        install(e, l, s, p);
                         __hip_atomic_store(&l.known, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (blockIdx.x % 64 == 0) {
-                            HQ_EPROBE_MIN(e, 4);   // a sampled workgroup's first descriptors
-                            HQ_EPROBE_MAX(e, 5);   // a sampled workgroup's last descriptors
-                        }
                     }
                     k = p;
                     break;
                 }
-                if (now_ticks() - t0 > e.idle_ticks &&
-                    __hip_atomic_load(&l.waiting, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-                        (uint32_t)WPW) {
+                const bool all_waiting =
+                    wave_u32(__hip_atomic_load(&l.waiting, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) == (uint32_t)WPW;
+                if (relayer) {
+                    // the grid's exit: after idle_ticks without news, once every relayed step is
+                    // this workgroup's too (p == s) and its waves all wait
+                    if (all_waiting && now_ticks() - t0 > e.idle_ticks) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                        if (lane == 0)
+                            __hip_atomic_store(gp(e.d_exit), (uint64_t)e.epoch, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        leave = true;
+                    }
+                } else if (all_waiting) {
+                    // workgroup 0 has ended the launch and every step it relayed is here
+                    // (re-read after the exit word: nothing relayed is left behind); or, as a
+                    // backstop, 64 idle limits without news
+                    const bool ended = uniform64(__hip_atomic_load(gp(e.d_exit), __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT)) == e.epoch;
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const uint64_t p2 = uniform64(
+                        __hip_atomic_load(gp(e.d_polled) + (blockIdx.x % kPollCopies) * kPollStride,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if ((ended && p2 <= s) || now_ticks() - t0 > 64 * e.idle_ticks) leave = true;
+                }
+                if (leave) {
                     if (lane == 0)
                         __hip_atomic_store(&l.exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     k = s;
@@ -286,189 +334,136 @@ __device__ uint64_t frontier(const EngineK &e, EngineLds &l, uint64_t s, uint32_
     return k;
 }
 
-// The workgroup is done with step s (called once per workgroup and step, by lane 0 of the wave
-// that decided its last tile). The tiles' stores were write-through (WT) and every deciding wave
-// drained them before counting its tile, so they are visible device-wide with no release fence
-// (Guideline 16 R1; a release fence per workgroup and step, an L2 write-back each, took 26 us per
-// step). The workgroup counts on the step's shard counter (blockIdx % 8), the last workgroup of
-// a shard on the step's top counter, and the last of those publishes the step to the host. The
-// last arriver of a counter resets it for the slot's next step: the host posts that step only
-// after it has seen this one's done flag, which is written after the resets.
-__device__ void arrive(const EngineK &e, uint64_t s) {
-    const uint64_t slot = s & (e.depth - 1);
-    const uint32_t shard = blockIdx.x % kShards;
-    const uint32_t nshard = gridDim.x < (uint32_t)kShards ? gridDim.x : (uint32_t)kShards;
-    const uint64_t per = (gridDim.x - shard + kShards - 1) / kShards;   // workgroups in the shard
-    uint64_t *ctr = e.d_arrive + slot * kShards + shard;
-    if (__hip_atomic_fetch_add(ctr, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 !=
-        per)
-        return;
-    __hip_atomic_store(ctr, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(e.d_top + slot, (uint64_t)1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT) + 1 != nshard)
-        return;
-    __hip_atomic_store(e.d_top + slot, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(e.h_clock + slot, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(e.h_done + slot, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    HQ_EPROBE_MAX(e, 11);   // a step (or STOP) published to the host
+// the next ticket of the workgroup, for the whole wave
+__device__ __forceinline__ uint32_t claim(EngineLds &l, uint32_t lane) {
+    uint32_t t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(&l.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return wave_u32(t);
 }
 
-// Workgroup b owns tiles [b * per, b * per + per) of every step (per = ceil(tiles / grid)); its
-// waves take them one at a time from the slot's LDS claim counter, so the waves of a workgroup
-// balance each other (older waves are served first by the memory pipeline: with a fixed tile
-// per wave the youngest finished a 20-step window 2.8 x later than the oldest, 236 vs 83 us,
-// tools/ab_engine.py). A wave that finds the workgroup's tiles of step s all taken moves on to
-// step s + 1 while the others finish theirs: no barrier between steps. In-place tables
-// (INPLACE) are the exception: a wave takes tiles of step s + 1 only when the workgroup has
-// decided all of step s, since the same table tiles come back at every step.
-template <int N, int FORM, int LEAD, bool INPLACE, int BLK, bool WT>
-__global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_commit_engine(const EngineK e) {
+// SIG: per-step completion signals (write-through stores, drained before a tile is counted).
+// INPLACE: the device-resident table decided in place (committed' into the tile's row).
+template <int N, int FORM, int LEAD, bool INPLACE, int BLK, bool SIG>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(BLK >= 1024 ? 8 : 1, 8)))
+void k_commit_engine(const EngineK e) {
     constexpr int WPW = BLK / 64;   // waves per workgroup
     __shared__ EngineLds l;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool relayer = blockIdx.x == 0;
     const uint64_t dmask = e.depth - 1;
-    uint64_t s = uniform64(e.d_cursor[blockIdx.x]);   // written by the previous launch
-    for (uint32_t i = threadIdx.x; i < kEngineMaxDepth; i += BLK) l.tag[i] = kTagBusy - 1;
-    if (lane == 0) l.cur[wv] = s;
+    const uint64_t s0 = uniform64(gp(e.d_cursor)[blockIdx.x]);   // written by the previous launch
     // the descriptors handed over at launch (the host's oldest incomplete step <= the cursor)
-    if (wv == 0 && lane < 6) {
-#pragma unroll
-        for (int i = 0; i < kInit; ++i) {
-            if ((uint32_t)i < e.init_count) {
-                const InitDesc &x = e.init[i];
-                const uint64_t v = lane == 0 ? x.G
-                                 : lane == 1 ? reinterpret_cast<uint64_t>(x.tiles)
-                                 : lane == 2 ? reinterpret_cast<uint64_t>(x.cout)
-                                 : lane == 3 ? reinterpret_cast<uint64_t>(x.changed)
-                                 : lane == 4 ? reinterpret_cast<uint64_t>(x.fallback)
-                                             : x.flags;
-                reinterpret_cast<uint64_t *>(l.ring + ((e.init_base + i) & dmask))[lane < 5 ? lane : 6] = v;
-            }
-        }
+    for (uint32_t i = threadIdx.x; i < kEngineMaxDepth; i += BLK) {
+        l.fin[i] = 0;
+        l.tgt[i] = 0;
     }
+    for (uint32_t i = threadIdx.x; i < e.init_count * 8; i += BLK)
+        reinterpret_cast<uint64_t *>(l.ring + ((e.init_base + (i >> 3)) & dmask))[i & 7] =
+            reinterpret_cast<const uint64_t *>(e.init)[i];
+    __syncthreads();
     if (threadIdx.x == 0) {
         const uint64_t top = e.init_base + e.init_count;
-        l.known = top > s ? top : s;
+        l.ticket = 0;
+        l.done = 0;
+        l.top_end = 0;
         l.waiting = l.lock = l.exit = 0;
-    }
-    if (threadIdx.x == 0 && blockIdx.x % 64 == 0) {
-        HQ_EPROBE_MIN(e, 0);   // kernel start (sampled)
-        HQ_EPROBE_MAX(e, 1);
+        if (top > s0) install(kargs(), l, s0, top);
+        l.known = top > s0 ? top : s0;
     }
     __syncthreads();
-    uint64_t known = s;
+    uint64_t s = s0;          // the step of the wave's ticket (or the first it may be in)
+    uint64_t known = s0;      // descriptors the wave has seen as known
+    uint32_t e_prev = 0;      // the workgroup's tickets before step s
+    uint32_t t = claim(l, lane);
     for (;;) {
+        // the step of ticket t
         if (s >= known) {
-            known = frontier<WPW>(e, l, s, lane, relayer);
+            known = frontier<WPW>(kargs(), l, s, lane);
             if (known <= s) break;   // idle: resume here at the next launch
         }
         const uint64_t slot = s & dmask;
         const uint64_t *d = reinterpret_cast<const uint64_t *>(l.ring + slot);
         if (uniform64(d[6]) & kDescStop) {
-            // the first wave here counts the workgroup's arrival at the STOP (every step before
-            // it is complete once the grid has exited)
-            uint32_t i = 0;
-            if (lane == 0) {
-                arm_slot<WPW>(l, slot, s, e.depth);
-                i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            if (wave_u32(i) == 0 && lane == 0) {
-                if (blockIdx.x % 64 == 0) HQ_EPROBE_MAX(e, 10);   // workgroups at the STOP
-                arrive(e, s);
-            }
+            // the wave holding the first ticket past the workgroup's last tile counts the
+            // workgroup's arrival at the STOP (every step before it is complete once the grid
+            // has exited)
+            if (t == e_prev && lane == 0) arrive(kargs(), s);
             ++s;
             break;
         }
-        CommitK k{};
-        k.G = uniform64(d[0]);
-        k.stride = e.stride;
-        k.match = as_global<const uint64_t>(uniform64(d[1]));
-        k.cout = as_global<uint64_t>(uniform64(d[2]));
-        k.changed = as_global<uint64_t>(uniform64(d[3]));
-        k.fallback = as_global<uint64_t>(uniform64(d[4]));
-        k.R = e.R;
-        const uint64_t tiles = (k.G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
-        const uint64_t per = (tiles + gridDim.x - 1) / gridDim.x;
-        const uint64_t b0 = (uint64_t)blockIdx.x * per;
-        const uint32_t len = (uint32_t)(b0 >= tiles ? 0 : tiles - b0 < per ? tiles - b0 : per);
-        if (lane == 0) arm_slot<WPW>(l, slot, s, e.depth);
-        for (;;) {
-            uint32_t i = 0;
-            if (lane == 0)
-                i = __hip_atomic_fetch_add(&l.claim[slot], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-            i = wave_u32(i);
-            if (i >= len) {
-                // the first claim past the end of an empty range stands in for its last tile
-                if (i == len && len == 0 && e.signal && lane == 0) arrive(e, s);
-                break;
+        const uint32_t e_cur = wave_u32(l.end[slot]);
+        if (before(t, e_cur)) {
+            CommitK k{};
+            k.stride = e.stride;
+            k.R = e.R;
+            k.G = uniform64(d[0]);
+            k.match = as_global<const uint64_t>(uniform64(d[1]));
+            k.cout = as_global<uint64_t>(uniform64(d[2]));
+            k.changed = as_global<uint64_t>(uniform64(d[3]));
+            k.fallback = as_global<uint64_t>(uniform64(d[4]));
+            const uint64_t b0 = (uint64_t)blockIdx.x * uniform64(d[7]);
+            uint32_t tgt = 0;
+            if constexpr (SIG) tgt = wave_u32(l.tgt[slot]);
+            if constexpr (INPLACE) {
+                // the table's tiles of step s are those of step s - 1: wait until the workgroup
+                // has decided every tile before this step (no tile of step s is decided before)
+                while (before(wave_u32(__hip_atomic_load(&l.done, __ATOMIC_ACQUIRE,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP)),
+                              e_prev))
+                    __builtin_amdgcn_s_sleep(2);
             }
-            commit_tile<N, FORM, false, LEAD, INPLACE, WT>(k, (b0 + i) * HQ_TILE_GROUPS, lane);
-            if (e.signal || INPLACE) {
-                if (e.signal) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // WT drained
-                uint32_t f = 0;
-                if (lane == 0)
-                    f = __hip_atomic_fetch_add(&l.fin[slot], 1u, __ATOMIC_RELEASE,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
-                if (wave_u32(f) == len && e.signal && lane == 0) arrive(e, s);
-            }
+            // the workgroup's tiles of step s, one ticket at a time
+            do {
+                const uint64_t wbase = uniform64((b0 + (uint32_t)(t - e_prev)) * HQ_TILE_GROUPS);
+                // the lane index laundered per tile: nothing derived from it is loop-invariant, so
+                // no per-lane 64-bit address is hoisted and kept (spilled) across the loop
+                uint32_t ln;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+                commit_tile<N, FORM, false, LEAD, INPLACE, SIG, true>(k, wbase, ln);
+                if constexpr (SIG || INPLACE) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tile's stores drained
+                    if constexpr (INPLACE) {
+                        if (lane == 0)
+                            __hip_atomic_fetch_add(&l.done, 1u, __ATOMIC_RELEASE,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    if constexpr (SIG) {
+                        uint32_t f = 0;
+                        if (lane == 0)
+                            f = __hip_atomic_fetch_add(&l.fin[slot], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
+                        if (wave_u32(f) == tgt && lane == 0) arrive(kargs(), s);
+                    }
+                }
+                t = claim(l, lane);
+            } while (before(t, e_cur));
         }
-#ifdef HQ_ENGINE_EXP
-        if (lane == 0 && blockIdx.x % 64 == 0) {
-            HQ_EPROBE_MIN(e, 6);   // first step done (sampled)
-            HQ_EPROBE_MAX(e, 7);   // last step done (sampled)
-        }
-        if (lane == 0 && s + 1 == e.init_base + e.init_count && wave_u32(wv) < 16 &&
-            (uint64_t)blockIdx.x * 16 + wv < 16384)
-            e.dbg[64 + (uint64_t)blockIdx.x * 16 + wv] = now_ticks();   // every wave's finish
-#endif
-        if constexpr (INPLACE) {
-            // the table's tiles of step s + 1 are those of step s: wait until they are decided
-            while (__hip_atomic_load(&l.fin[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                   len)
-                __builtin_amdgcn_s_sleep(2);
-        }
+        e_prev = e_cur;
         ++s;
-        if (lane == 0) __hip_atomic_store(&l.cur[wv], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (lane == 0 && wv == 0) e.d_cursor[blockIdx.x] = s;
+    if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
 }
 
 typedef void (*EngineKernel)(const EngineK);
 
+// 1024-thread workgroups (two per CU) where the tile loop fits 64 VGPRs with no scratch (n <= 5;
+// some n = 7, 8 bodies spill at that size), 512 otherwise
 template <int N, int FORM, int LEAD, bool INPLACE>
-void engine_kernel_for(bool wt, EngineKernel *fn, int *blk) {
-#ifdef HQ_ENGINE_EXP   // A/B: HQ_ENGINE_BLOCK=512 takes 512-thread workgroups at any N
-    const char *eb = std::getenv("HQ_ENGINE_BLOCK");
-    if (N <= 5 && eb && std::atoi(eb) == 512) {
-        *fn = wt ? k_commit_engine<N, FORM, LEAD, INPLACE, 512, true>
-                 : k_commit_engine<N, FORM, LEAD, INPLACE, 512, false>;
-        *blk = 512;
-        return;
-    }
-#endif
-    if constexpr (N <= 5) {
-        *fn = wt ? k_commit_engine<N, FORM, LEAD, INPLACE, 1024, true>
-                 : k_commit_engine<N, FORM, LEAD, INPLACE, 1024, false>;
-        *blk = 1024;
-    } else {
-        *fn = wt ? k_commit_engine<N, FORM, LEAD, INPLACE, 512, true>
-                 : k_commit_engine<N, FORM, LEAD, INPLACE, 512, false>;
-        *blk = 512;
-    }
+void engine_kernel_for(bool sig, EngineKernel *fn, int *blk) {
+    constexpr int B = N <= 5 ? 1024 : 512;
+    *fn = sig ? k_commit_engine<N, FORM, LEAD, INPLACE, B, true>
+              : k_commit_engine<N, FORM, LEAD, INPLACE, B, false>;
+    *blk = B;
 }
 
 template <int N>
-int engine_kernel_n(uint32_t form, uint32_t layout, bool wt, EngineKernel *fn, int *blk) {
+int engine_kernel_n(uint32_t form, uint32_t layout, bool sig, EngineKernel *fn, int *blk) {
     const bool lead = (layout & 0xFFu) == HQ_LAYOUT_TILES_LEADER;
     const bool inplace = (layout & HQ_LAYOUT_IN_PLACE) != 0;
 #define HQ_ENGINE_PICK(F)                                                                        \
-    if (inplace) engine_kernel_for<N, F, 1, true>(wt, fn, blk);                                  \
-    else if (lead) engine_kernel_for<N, F, 1, false>(wt, fn, blk);                               \
-    else engine_kernel_for<N, F, 0, false>(wt, fn, blk);
+    if (inplace) engine_kernel_for<N, F, 1, true>(sig, fn, blk);                                 \
+    else if (lead) engine_kernel_for<N, F, 1, false>(sig, fn, blk);                              \
+    else engine_kernel_for<N, F, 0, false>(sig, fn, blk);
     if (form == HQ_FORM_TERM_MASK) {
         HQ_ENGINE_PICK(HQ_FORM_TERM_MASK)
     } else {
@@ -478,18 +473,18 @@ int engine_kernel_n(uint32_t form, uint32_t layout, bool wt, EngineKernel *fn, i
     return HQ_OK;
 }
 
-// WT (write-through stores) for the per-step completion signals: a step's outputs are visible
-// once its waves' stores have drained
-int engine_kernel(uint32_t n, uint32_t form, uint32_t layout, bool wt, EngineKernel *fn, int *blk) {
+// sig: per-step completion signals (write-through stores: a step's outputs are visible once its
+// waves' stores have drained)
+int engine_kernel(uint32_t n, uint32_t form, uint32_t layout, bool sig, EngineKernel *fn, int *blk) {
     switch (n) {
-    case 1: return engine_kernel_n<1>(form, layout, wt, fn, blk);
-    case 2: return engine_kernel_n<2>(form, layout, wt, fn, blk);
-    case 3: return engine_kernel_n<3>(form, layout, wt, fn, blk);
-    case 4: return engine_kernel_n<4>(form, layout, wt, fn, blk);
-    case 5: return engine_kernel_n<5>(form, layout, wt, fn, blk);
-    case 6: return engine_kernel_n<6>(form, layout, wt, fn, blk);
-    case 7: return engine_kernel_n<7>(form, layout, wt, fn, blk);
-    default: return engine_kernel_n<8>(form, layout, wt, fn, blk);
+    case 1: return engine_kernel_n<1>(form, layout, sig, fn, blk);
+    case 2: return engine_kernel_n<2>(form, layout, sig, fn, blk);
+    case 3: return engine_kernel_n<3>(form, layout, sig, fn, blk);
+    case 4: return engine_kernel_n<4>(form, layout, sig, fn, blk);
+    case 5: return engine_kernel_n<5>(form, layout, sig, fn, blk);
+    case 6: return engine_kernel_n<6>(form, layout, sig, fn, blk);
+    case 7: return engine_kernel_n<7>(form, layout, sig, fn, blk);
+    default: return engine_kernel_n<8>(form, layout, sig, fn, blk);
     }
 }
 
@@ -514,6 +509,10 @@ struct hq_engine {
     uint64_t launches = 0;       // finished launches since the last timing reset
     double launch_ms = 0.0;
     uint64_t relaunches = 0;
+    uint32_t epoch = 0;          // launches so far (the kernel's exit word names its launch)
+    uint64_t wait_limit_ms = 60000;   // a wait that sees no completion this long fails (HQ_ENGINE_WAIT_MS)
+    size_t cur_off = 0, exit_off = 0, polled_off = 0;   // device state (hq_engine_dump)
+    uint64_t inplace_G = 0;      // HQ_LAYOUT_IN_PLACE: the table's G (every post keeps it)
 };
 
 namespace {
@@ -556,10 +555,8 @@ int launch(hq_engine *e) {
     const uint64_t n = std::min<uint64_t>(e->posted - e->completed, kInit);
     e->k.init_base = e->completed;
     e->k.init_count = (uint32_t)n;
-    for (uint64_t i = 0; i < n; ++i) {
-        const EngineDesc &d = ring[(e->completed + i) & (e->cfg.depth - 1)];
-        e->k.init[i] = InitDesc{d.G, d.tiles, d.cout, d.changed, d.fallback, d.flags};
-    }
+    for (uint64_t i = 0; i < n; ++i) e->k.init[i] = ring[(e->completed + i) & (e->cfg.depth - 1)];
+    e->k.epoch = ++e->epoch;
     int rc = echeck(e, hipSetDevice(e->ctx->device), "hipSetDevice");
     if (!rc) rc = echeck(e, hipEventRecord(e->ev_start, e->stream), "hipEventRecord");
     if (rc) return rc;
@@ -603,8 +600,10 @@ int wait_step(hq_engine *e, uint64_t seq) {
         if (++spins > 256) {
             std::this_thread::yield();
             spins = 0;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
-                return efail(e, HQ_E_DEVICE, "hq_engine: step not completed within 60 s");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(e->wait_limit_ms))
+                return efail(e, HQ_E_DEVICE, "hq_engine: step " + std::to_string(seq) +
+                                                 " not completed within the wait limit (" +
+                                                 std::to_string(e->wait_limit_ms) + " ms)");
         }
     }
     while (e->completed < e->posted && step_done(e, e->completed)) e->completed++;
@@ -691,6 +690,11 @@ int validate_post(hq_engine *e, const hq_commit_args *a) {
         return efail(e, HQ_E_INVAL, "hq_engine_post: NULL tiles (match) / committed_out");
     if (!hq::aligned16(a->match) || (!in_place && !hq::aligned16(a->committed_out)))
         return efail(e, HQ_E_INVAL, "hq_engine_post: tiles and committed_out must be 16-byte aligned");
+    // an in-place table keeps its G: a tile then belongs to the same workgroup at every step,
+    // which is what orders a group's steps (the kernel orders steps inside a workgroup only)
+    if (in_place && e->inplace_G && a->G != e->inplace_G)
+        return efail(e, HQ_E_INVAL, "hq_engine_post: an in-place table's steps must keep one G (the "
+                                    "engine's first in-place post set it)");
     return HQ_OK;
 }
 
@@ -744,11 +748,15 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     if (c.max_workgroups && c.max_workgroups < e->grid) e->grid = c.max_workgroups;
     const size_t D = c.depth;
     const size_t host_bytes = 128 + 16 * D + sizeof(EngineDesc) * D;
+    if (const char *w = std::getenv("HQ_ENGINE_WAIT_MS")) e->wait_limit_ms = std::max(1, std::atoi(w));
     const size_t arrive_off = 128, top_off = arrive_off + 8 * kShards * D, cur_off = top_off + 8 * D;
     const size_t ring_off = (cur_off + 8 * (size_t)e->grid + 127) & ~(size_t)127;
-    const size_t dbg_off = ring_off + sizeof(EngineDesc) * D;
-    const size_t polled_off = dbg_off + 8 * (64 + 16384);
+    const size_t exit_off = ring_off + sizeof(EngineDesc) * D;
+    const size_t polled_off = exit_off + 256;
     const size_t dev_bytes = polled_off + 8 * kPollCopies * kPollStride;
+    e->cur_off = cur_off;
+    e->exit_off = exit_off;
+    e->polled_off = polled_off;
     void *hp = nullptr, *dp = nullptr;
     rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking),
                        "hipStreamCreateWithFlags");
@@ -770,7 +778,6 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     k.idle_ticks = (uint64_t)c.idle_us * 100;   // s_memrealtime runs at 100 MHz
     k.R = c.form == HQ_FORM_TERM_MASK ? c.ring_len : 16;
     k.depth = c.depth;
-    k.waves = e->grid * (uint32_t)(e->block / 64);
     k.signal = (c.flags & HQ_ENGINE_SIGNAL) ? 1u : 0u;
     k.h_posted = reinterpret_cast<const uint64_t *>(e->host);
     k.h_done = reinterpret_cast<uint64_t *>(e->host + 128);
@@ -782,9 +789,7 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     k.d_cursor = reinterpret_cast<uint64_t *>(e->dev + cur_off);
     k.d_ring = reinterpret_cast<EngineDesc *>(e->dev + ring_off);
     k.d_polled = reinterpret_cast<uint64_t *>(e->dev + polled_off);
-#ifdef HQ_ENGINE_EXP
-    k.dbg = reinterpret_cast<uint64_t *>(e->dev + dbg_off);
-#endif
+    k.d_exit = reinterpret_cast<uint64_t *>(e->dev + exit_off);
     *out = e;
     return HQ_OK;
 }
@@ -793,10 +798,16 @@ int hq_engine_post(hq_engine *e, const hq_commit_args *args, uint32_t count, uin
     if (!e) return HQ_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
     if (count && !args) return efail(e, HQ_E_INVAL, "hq_engine_post: args is NULL");
+    const uint64_t keep_G = e->inplace_G;
     for (uint32_t i = 0; i < count; ++i) {
         int rc = validate_post(e, args + i);
-        if (rc) return rc;
+        if (!rc && (e->cfg.layout & HQ_LAYOUT_IN_PLACE) && args[i].G) e->inplace_G = args[i].G;
+        if (rc) {
+            e->inplace_G = keep_G;
+            return rc;
+        }
     }
+    e->inplace_G = keep_G;
     if (first_seq) *first_seq = e->posted;
     int rc = echeck(e, hipSetDevice(e->ctx->device), "hipSetDevice");
     for (uint32_t i = 0; i < count && !rc; ++i) {
@@ -812,6 +823,9 @@ int hq_engine_post(hq_engine *e, const hq_commit_args *args, uint32_t count, uin
         d.changed = args[i].changed;
         d.fallback = args[i].fallback;
         d.seq = e->posted;
+        const uint64_t tiles = (d.G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
+        d.per = (tiles + e->grid - 1) / e->grid;
+        if ((e->cfg.layout & HQ_LAYOUT_IN_PLACE) && d.G) e->inplace_G = d.G;
         rc = write_desc(e, d);
     }
     if (!rc && count) rc = ensure_running(e);
@@ -877,6 +891,35 @@ int hq_engine_done_clock(hq_engine *e, uint64_t seq, uint64_t *ticks) {
     return HQ_OK;
 }
 
+int hq_engine_dump(hq_engine *e, uint64_t *out, uint32_t n_words) {
+    if (!e || !out) return HQ_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    const uint32_t head = 8;
+    if (n_words < head + e->grid)
+        return efail(e, HQ_E_INVAL, "hq_engine_dump: needs 8 + grid words");
+    hipStream_t st = nullptr;
+    int rc = echeck(e, hipSetDevice(e->ctx->device), "hipSetDevice");
+    if (!rc) rc = echeck(e, hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    uint64_t dp = 0, polled = 0, ex = 0;
+    if (!rc) rc = echeck(e, hipMemcpyAsync(&dp, e->dev, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    if (!rc) rc = echeck(e, hipMemcpyAsync(&polled, e->dev + e->polled_off, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    if (!rc) rc = echeck(e, hipMemcpyAsync(&ex, e->dev + e->exit_off, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    if (!rc) rc = echeck(e, hipMemcpyAsync(out + head, e->dev + e->cur_off, 8 * (size_t)e->grid,
+                                           hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    if (!rc) rc = echeck(e, hipStreamSynchronize(st), "hipStreamSynchronize");
+    if (st) (void)hipStreamDestroy(st);
+    if (rc) return rc;
+    out[0] = host_load(reinterpret_cast<const uint64_t *>(e->host));   // posted (host ring)
+    out[1] = dp;                                                      // relayed
+    out[2] = polled;                                                  // relayed count, copy 0
+    out[3] = ex;                                                      // exit epoch
+    out[4] = e->epoch;
+    out[5] = e->grid;
+    out[6] = e->completed;
+    out[7] = e->running ? 1 : 0;
+    return HQ_OK;
+}
+
 const char *hq_engine_last_error(const hq_engine *e) { return e ? e->err.c_str() : ""; }
 
 void hq_engine_close(hq_engine *e) {
@@ -897,229 +940,3 @@ void hq_engine_close(hq_engine *e) {
 
 }  // extern "C"
 
-#ifdef HQ_ENGINE_EXP
-// ---- tuning experiments (tools/lib_engexp, tools/ab_engine.py): never in the product build ----
-namespace {
-constexpr int kExpMax = 32;
-struct MultiK {
-    uint64_t stride, G;
-    uint32_t R, count, waves, ntiles;
-    const uint64_t *tiles[kExpMax];
-    uint64_t *cout[kExpMax];
-    uint64_t *chg[kExpMax];
-    uint64_t *fb[kExpMax];
-};
-// V1: each wave loops over the `count` batches (the engine's ownership, no doorbell)
-template <int N, int FORM, int LEAD, int BLK>
-__global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_exp_loop(const MultiK m) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t c = 0; c < m.count; ++c) {
-        CommitK k{};
-        k.G = m.G;
-        k.stride = m.stride;
-        k.match = m.tiles[c];
-        k.cout = m.cout[c];
-        k.changed = m.chg[c];
-        k.fallback = m.fb[c];
-        k.R = m.R;
-        for (uint64_t t = wave; t < m.ntiles; t += m.waves)
-            commit_tile<N, FORM, false, LEAD, false>(k, t * HQ_TILE_GROUPS, lane);
-    }
-}
-// V2: one wave per (batch, tile), batch-major: the launches' waves in one grid
-template <int N, int FORM, int LEAD, int BLK>
-__global__ __launch_bounds__(BLK, BLK >= 1024 ? 8 : 1) void k_exp_flat(const MultiK m) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * (BLK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t c = (uint32_t)(wave / m.ntiles);
-    const uint64_t t = wave % m.ntiles;
-    if (c >= m.count) return;
-    CommitK k{};
-    k.G = m.G;
-    k.stride = m.stride;
-    k.match = m.tiles[c];
-    k.cout = m.cout[c];
-    k.changed = m.chg[c];
-    k.fallback = m.fb[c];
-    k.R = m.R;
-    commit_tile<N, FORM, false, LEAD, false>(k, t * HQ_TILE_GROUPS, lane);
-}
-// V3: each workgroup owns a contiguous range of every batch's tiles; its waves claim them one by
-// one from an LDS counter per batch (the waves of one workgroup balance each other)
-template <int N, int FORM, int LEAD, int BLK, int OCC>
-__global__ __launch_bounds__(BLK, OCC) void k_exp_claim(const MultiK m) {
-    __shared__ uint32_t claim[kExpMax];
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)kExpMax; i += BLK) claim[i] = 0;
-    __syncthreads();
-    const uint64_t per = (m.ntiles + gridDim.x - 1) / gridDim.x;
-    const uint64_t base = blockIdx.x * per;
-    const uint64_t end = base + per < m.ntiles ? base + per : m.ntiles;
-    for (uint32_t c = 0; c < m.count; ++c) {
-        CommitK k{};
-        k.G = m.G;
-        k.stride = m.stride;
-        k.match = m.tiles[c];
-        k.cout = m.cout[c];
-        k.changed = m.chg[c];
-        k.fallback = m.fb[c];
-        k.R = m.R;
-        for (;;) {
-            uint32_t t = 0;
-            if (lane == 0) t = __hip_atomic_fetch_add(&claim[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            t = __builtin_amdgcn_readfirstlane(t);
-            if (base + t >= end) break;
-            commit_tile<N, FORM, false, LEAD, false>(k, (base + t) * HQ_TILE_GROUPS, lane);
-        }
-    }
-}
-// V6: every wave claims tiles one at a time from a device counter shared by the waves of
-// workgroups b and b + grid/2 (per batch), the next claim issued before the current tile is
-// decided: balance across the two workgroups of a CU, no LDS
-template <int N, int FORM, int LEAD, int BLK>
-__global__ __launch_bounds__(BLK, 8) void k_exp_gclaim(const MultiK m, uint32_t *ctr) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t half = gridDim.x / 2;
-    const uint32_t pair = blockIdx.x % half;
-    const uint64_t per = (m.ntiles + half - 1) / half;
-    const uint64_t b0 = pair * per;
-    const uint32_t len = (uint32_t)(b0 >= m.ntiles ? 0 : m.ntiles - b0 < per ? m.ntiles - b0 : per);
-    uint32_t c = 0;
-    uint32_t nxt = 0;
-    if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c * half + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (c < m.count) {
-        const uint32_t i = __builtin_amdgcn_readfirstlane(nxt);
-        if (i >= len) {
-            ++c;
-            if (c < m.count && lane == 0)
-                nxt = __hip_atomic_fetch_add(ctr + c * half + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c * half + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        CommitK k{};
-        k.G = m.G;
-        k.stride = m.stride;
-        k.match = m.tiles[c];
-        k.cout = m.cout[c];
-        k.changed = m.chg[c];
-        k.fallback = m.fb[c];
-        k.R = m.R;
-        commit_tile<N, FORM, false, LEAD, false>(k, (b0 + i) * HQ_TILE_GROUPS, lane);
-    }
-}
-}  // namespace
-
-extern "C" int hq_exp_engine_set(hq_engine *e, uint32_t bits) {
-    e->k.exp = bits;
-    return HQ_OK;
-}
-
-extern "C" int hq_exp_engine_probe(hq_engine *e, uint64_t *out) {
-    // read and re-arm the phase clocks (even slots min, odd max)
-    if (hipMemcpy(out, e->k.dbg, (64 + 16384) * 8, hipMemcpyDeviceToHost) != hipSuccess)
-        return HQ_E_DEVICE;
-    uint64_t init[32];
-    for (int i = 0; i < 32; ++i) init[i] = (i & 1) ? 0 : ~0ull;
-    return hipMemcpy(e->k.dbg, init, sizeof init, hipMemcpyHostToDevice) == hipSuccess ? HQ_OK
-                                                                                         : HQ_E_DEVICE;
-}
-
-// V7: the claim512 shape plus a shared pool: per batch, the last `pool` tiles are claimed by
-// any wave of the grid from one device counter (the next claim issued before the current tile
-// is decided) once its workgroup's own range of the batch is exhausted; fast workgroups take
-// more of the pool, so the slowest one no longer sets the window
-template <int N, int FORM, int LEAD, int BLK>
-__global__ __launch_bounds__(BLK, 8) void k_exp_pool(const MultiK m, uint32_t *ctr, uint32_t pool) {
-    __shared__ uint32_t claim[kExpMax];
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)kExpMax; i += BLK) claim[i] = 0;
-    __syncthreads();
-    const uint64_t S = m.ntiles - pool;   // the static part
-    const uint64_t per = (S + gridDim.x - 1) / gridDim.x;
-    const uint64_t base = blockIdx.x * per;
-    const uint64_t end = base + per < S ? base + per : S;
-    for (uint32_t c = 0; c < m.count; ++c) {
-        CommitK k{};
-        k.G = m.G;
-        k.stride = m.stride;
-        k.match = m.tiles[c];
-        k.cout = m.cout[c];
-        k.changed = m.chg[c];
-        k.fallback = m.fb[c];
-        k.R = m.R;
-        for (;;) {
-            uint32_t t = 0;
-            if (lane == 0) t = __hip_atomic_fetch_add(&claim[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            t = __builtin_amdgcn_readfirstlane(t);
-            if (base + t >= end) break;
-            commit_tile<N, FORM, false, LEAD, false>(k, (base + t) * HQ_TILE_GROUPS, lane);
-        }
-        uint32_t nxt = 0;
-        if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-            const uint32_t i = __builtin_amdgcn_readfirstlane(nxt);
-            if (i >= pool) break;
-            if (lane == 0) nxt = __hip_atomic_fetch_add(ctr + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            commit_tile<N, FORM, false, LEAD, false>(k, (S + i) * HQ_TILE_GROUPS, lane);
-        }
-    }
-}
-
-extern "C" int hq_exp_multi(hq_ctx *ctx, const hq_commit_args *a, uint32_t count, int variant,
-                            uint32_t grid) {
-    if (!ctx || !a || count == 0 || count > (uint32_t)kExpMax) return HQ_E_INVAL;
-    if (a[0].n_max != 5 || a[0].form != HQ_FORM_TERM_MASK || a[0].layout != HQ_LAYOUT_TILES_LEADER)
-        return HQ_E_INVAL;
-    MultiK m{};
-    m.stride = hq_commit_tile_words_for(5, HQ_FORM_TERM_MASK, HQ_LAYOUT_TILES_LEADER);
-    m.G = a[0].G;
-    m.R = a[0].ring_len;
-    m.count = count;
-    m.ntiles = (uint32_t)((m.G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS);
-    for (uint32_t i = 0; i < count; ++i) {
-        if (a[i].G != m.G) return HQ_E_INVAL;
-        m.tiles[i] = a[i].match;
-        m.cout[i] = a[i].committed_out;
-        m.chg[i] = a[i].changed;
-        m.fb[i] = a[i].fallback;
-    }
-    int rc = hq::pre_launch(ctx);
-    if (rc) return rc;
-    if (variant == 1) {
-        if (!grid) grid = 512;
-        m.waves = grid * 16;
-        hipLaunchKernelGGL((k_exp_loop<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid), dim3(1024), 0,
-                           ctx->stream, m);
-    } else if (variant == 7) {
-        static uint32_t *ctr = nullptr;
-        if (!ctr && hipMalloc(&ctr, 4 * kExpMax) != hipSuccess) return HQ_E_NOMEM;
-        (void)hipMemsetAsync(ctr, 0, 4 * kExpMax, ctx->stream);
-        const char *pv = std::getenv("AB_POOL");   // permille of a batch's tiles in the pool
-        const uint32_t pool = (uint32_t)((uint64_t)m.ntiles * (pv ? std::atoi(pv) : 250) / 1000);
-        hipLaunchKernelGGL((k_exp_pool<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid ? grid : 512),
-                           dim3(1024), 0, ctx->stream, m, ctr, pool);
-    } else if (variant == 6) {
-        static uint32_t *ctr = nullptr;
-        if (!ctr && hipMalloc(&ctr, 4 * kExpMax * 1024) != hipSuccess) return HQ_E_NOMEM;
-        (void)hipMemsetAsync(ctr, 0, 4 * kExpMax * 1024, ctx->stream);
-        hipLaunchKernelGGL((k_exp_gclaim<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3(grid ? grid : 512),
-                           dim3(1024), 0, ctx->stream, m, ctr);
-    } else if (variant == 3) {
-        hipLaunchKernelGGL((k_exp_claim<5, HQ_FORM_TERM_MASK, 1, 1024, 4>), dim3(grid ? grid : 256),
-                           dim3(1024), 0, ctx->stream, m);
-    } else if (variant == 4) {
-        hipLaunchKernelGGL((k_exp_claim<5, HQ_FORM_TERM_MASK, 1, 1024, 8>), dim3(grid ? grid : 512),
-                           dim3(1024), 0, ctx->stream, m);
-    } else if (variant == 5) {
-        hipLaunchKernelGGL((k_exp_claim<5, HQ_FORM_TERM_MASK, 1, 512, 8>), dim3(grid ? grid : 1024),
-                           dim3(512), 0, ctx->stream, m);
-    } else {
-        const uint64_t waves = (uint64_t)m.ntiles * count;
-        m.waves = 0;
-        hipLaunchKernelGGL((k_exp_flat<5, HQ_FORM_TERM_MASK, 1, 1024>), dim3((waves + 15) / 16),
-                           dim3(1024), 0, ctx->stream, m);
-    }
-    return hq::post_launch(ctx, "k_exp");
-}
-#endif

@@ -14,10 +14,10 @@ namespace {
 
 constexpr int kBlock = 256;           // 4 waves of 64
 // The commit stream runs 512-thread blocks: ~5 % shorter than 256 on the 1M x 3 launch under
-// rocprofv3 (11.7 vs 12.4 us, tools/kexp2.hip); 4 groups per lane was slower.
+// rocprofv3 (11.7 vs 12.4 us, tools/kexp2.hip, git history); 4 groups per lane was slower.
 constexpr int kCommitBlock = 512;
 // Kernels that fit 64 VGPRs (occupancy 8) run 1024-thread blocks: 10.57 vs 11.1 us per 1M x 3
-// launch (tools/kexp3.hip: fewer workgroups to dispatch for the same waves); the others keep
+// launch (tools/kexp3.hip, git history: fewer workgroups to dispatch for the same waves); the others keep
 // 512 so that two or more blocks still fit a CU. HQ_COMMIT_BLOCK_BIG=512 restores one size.
 #ifndef HQ_COMMIT_BLOCK_BIG
 #define HQ_COMMIT_BLOCK_BIG 1024

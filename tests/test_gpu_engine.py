@@ -171,6 +171,115 @@ def test_engine_in_place_table_steps(gpu_ctx, hq):
     hq.free_commit(gpu_ctx, b)
 
 
+@pytest.mark.parametrize("signal", [False, True])
+def test_engine_in_place_dependent_steps(gpu_ctx, hq, signal):
+    """HQ_LAYOUT_IN_PLACE with an ordering the result depends on: two steps over one
+    undecided 1 M-group table (every workgroup of the grid owns tiles), each with its own
+    `changed` bitmap. Step 1 must see the table as posted (its bitmap = the launch path's), step 2
+    the table step 1 left (nothing changes any more: an all-zero bitmap). A step 2 tile decided
+    before step 1's would re-set its changed bits."""
+    G, n, form = 1 << 20, 5, hq.HQ_FORM_TERM_MASK
+    lay = hq.HQ_LAYOUT_TILES_LEADER
+    b = make_batch(gpu_ctx, hq, G, n, form, lay, SEED + 650)
+    words = b.tiles.count
+    ref = gpu_ctx.empty(words, np.uint64)
+    gpu_ctx.copy_to_ptr(ref.ptr, b.tiles, words * 8)
+    chg = [gpu_ctx.empty(hq.words64(G), np.uint64) for _ in range(3)]
+
+    def table_args(tiles, changed):
+        a = b.tile_args()
+        a.layout = lay | hq.HQ_LAYOUT_IN_PLACE
+        a.match = tiles.ptr
+        a.committed_out = None
+        a.changed = changed.ptr
+        a.fallback = None
+        return a
+
+    gpu_ctx.commit_dev(table_args(ref, chg[0]))          # the launch path, one step
+    gpu_ctx.sync()
+    want1 = gpu_ctx.download(chg[0])
+    assert want1.any()                                    # the table was undecided
+    for c in chg[1:]:
+        gpu_ctx.memset(c, 0xA5)
+    gpu_ctx.sync()
+    with hq.Engine(gpu_ctx, n, form, lay | hq.HQ_LAYOUT_IN_PLACE, signal=signal) as eng:
+        eng.post(hq.commit_batch_array([table_args(b.tiles, chg[1]), table_args(b.tiles, chg[2])]))
+        eng.drain()
+    np.testing.assert_array_equal(gpu_ctx.download(chg[1]), want1)
+    assert not gpu_ctx.download(chg[2]).any()
+    np.testing.assert_array_equal(gpu_ctx.download(b.tiles), gpu_ctx.download(ref))
+    hq.free_commit(gpu_ctx, b)
+
+
+def test_engine_in_place_keeps_one_G(gpu_ctx, hq):
+    """An in-place table's steps keep the G of the engine's first in-place post: a tile then stays
+    with its workgroup, which is what orders a group's steps; another G is HQ_E_INVAL."""
+    G, n, form = 20_000, 3, hq.HQ_FORM_TERM_START
+    lay = hq.HQ_LAYOUT_TILES_LEADER
+    b = make_batch(gpu_ctx, hq, G, n, form, lay, SEED + 660)
+    a = b.tile_args()
+    a.layout = lay | hq.HQ_LAYOUT_IN_PLACE
+    a.committed_out = None
+    with hq.Engine(gpu_ctx, n, form, lay | hq.HQ_LAYOUT_IN_PLACE) as eng:
+        eng.post(a)
+        a2 = b.tile_args()
+        a2.layout, a2.committed_out, a2.G = a.layout, None, G - 128
+        with pytest.raises(hq.HQError) as e:
+            eng.post(a2)
+        assert e.value.code == hq.HQ_E_INVAL and "one G" in str(e.value)
+        with pytest.raises(hq.HQError):            # also inside one post call
+            eng.post(hq.commit_batch_array([a, a2]))
+        eng.post(a)                                 # the same G still posts
+        eng.drain()
+    hq.free_commit(gpu_ctx, b)
+
+
+def test_engine_wait_near_the_idle_limit(gpu_ctx, hq):
+    """Posts that land around the idle limit: the grid ends as a whole (workgroup 0
+    publishes the exit, the others follow once they hold every relayed step), so a post that
+    arrives as it ends waits for a relaunch, never for another idle limit. idle_us = 20 ms; every
+    wait must be well below it."""
+    n, form, lay = 3, hq.HQ_FORM_TERM_START, hq.HQ_LAYOUT_TILES_LEADER
+    b = make_batch(gpu_ctx, hq, 65_536, n, form, lay, SEED + 520)
+    want = launch_reference(gpu_ctx, b)
+    worst = 0.0
+    with hq.Engine(gpu_ctx, n, form, lay, signal=True, idle_us=20_000) as eng:
+        eng.wait(eng.post(b.tile_args()))
+        for gap_ms in (19.0, 19.5, 19.8, 20.0, 20.2, 20.5, 21.0, 22.0, 25.0):
+            time.sleep(gap_ms / 1e3)
+            t0 = time.perf_counter()
+            eng.wait(eng.post(b.tile_args()))
+            worst = max(worst, time.perf_counter() - t0)
+        launches, _ = eng.timing()
+    assert worst < 0.010, worst
+    for x, y in zip(outputs(gpu_ctx, b), want):
+        np.testing.assert_array_equal(x, y)
+    hq.free_commit(gpu_ctx, b)
+
+
+def test_engine_many_steps_one_post_each(gpu_ctx, hq):
+    """200 steps posted one call each into a 64-slot engine without signals (drains keep a slot
+    for the STOP): the workgroups' tickets run across many ring wraps and relaunches; the last
+    batch's outputs are the launch path's."""
+    n, form, lay = 5, hq.HQ_FORM_TERM_MASK, hq.HQ_LAYOUT_TILES_LEADER
+    bufs = [make_batch(gpu_ctx, hq, 30_000 + 4_000 * k, n, form, lay, SEED + 900 + k)
+            for k in range(3)]
+    want = [launch_reference(gpu_ctx, b) for b in bufs]
+    for b in bufs:
+        poison(gpu_ctx, b)
+    gpu_ctx.sync()
+    with hq.Engine(gpu_ctx, n, form, lay) as eng:
+        for s in range(200):
+            eng.post(bufs[s % 3].tile_args())
+        eng.drain()
+        st = eng.info()
+        assert st.completed == st.posted >= 200
+    for b, w in zip(bufs, want):
+        for x, y in zip(outputs(gpu_ctx, b), w):
+            np.testing.assert_array_equal(x, y)
+        hq.free_commit(gpu_ctx, b)
+
+
 def test_engine_threads_post_together(gpu_ctx, hq):
     """Four step workers (host threads) share one engine: 4 x 8 steps, all decided exactly."""
     n, form, lay = 5, hq.HQ_FORM_TERM_MASK, hq.HQ_LAYOUT_TILES_LEADER
