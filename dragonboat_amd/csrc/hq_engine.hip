@@ -265,7 +265,14 @@ __device__ uint64_t frontier(GlobalEngineK &e, EngineLds &l, uint64_t s, uint32_
         if (lane == 0)
             got = __hip_atomic_exchange(&l.lock, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
         if (wave_u32(got)) {
-            // the workgroup's poller
+            // the workgroup's poller. Another poller may have published news between this
+            // wave's look at `known` and its lock: look again under the lock, or the steps it
+            // installed would be installed twice (their ends counted twice)
+            k = uniform64(lds_known(l));
+            if (k > s) {
+                if (lane == 0) __hip_atomic_store(&l.lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
             const uint64_t t0 = now_ticks();
             uint32_t backoff = 1;
             bool leave = false;
@@ -895,8 +902,9 @@ int hq_engine_dump(hq_engine *e, uint64_t *out, uint32_t n_words) {
     if (!e || !out) return HQ_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
     const uint32_t head = 8;
-    if (n_words < head + e->grid)
-        return efail(e, HQ_E_INVAL, "hq_engine_dump: needs 8 + grid words");
+    const size_t D = e->cfg.depth;
+    if (n_words < head + e->grid + (kShards + 1) * D)
+        return efail(e, HQ_E_INVAL, "hq_engine_dump: needs 8 + grid + 9 * depth words");
     hipStream_t st = nullptr;
     int rc = echeck(e, hipSetDevice(e->ctx->device), "hipSetDevice");
     if (!rc) rc = echeck(e, hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
@@ -906,6 +914,10 @@ int hq_engine_dump(hq_engine *e, uint64_t *out, uint32_t n_words) {
     if (!rc) rc = echeck(e, hipMemcpyAsync(&ex, e->dev + e->exit_off, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     if (!rc) rc = echeck(e, hipMemcpyAsync(out + head, e->dev + e->cur_off, 8 * (size_t)e->grid,
                                            hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    // the arrival counters: [depth][kShards] then the top counters [depth]
+    if (!rc) rc = echeck(e, hipMemcpyAsync(out + head + e->grid, e->dev + 128,
+                                           8 * (kShards + 1) * D, hipMemcpyDeviceToHost, st),
+                         "hipMemcpyAsync");
     if (!rc) rc = echeck(e, hipStreamSynchronize(st), "hipStreamSynchronize");
     if (st) (void)hipStreamDestroy(st);
     if (rc) return rc;

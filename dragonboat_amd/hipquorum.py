@@ -931,6 +931,10 @@ class Engine:
                 "running")
         out = {k: int(buf[i]) for i, k in enumerate(head)}
         out["cursor"] = np.frombuffer(buf, np.uint64, out["grid"], 8 * 8).copy()
+        depth = self.info().depth
+        arr = np.frombuffer(buf, np.uint64, 9 * depth, 8 * (8 + out["grid"])).copy()
+        out["arrive"] = arr[:8 * depth].reshape(depth, 8)
+        out["top"] = arr[8 * depth:]
         return out
 
     def drain(self) -> None:

@@ -332,7 +332,8 @@ int hq_engine_info(hq_engine *eng, hq_engine_stats *out);
 /* Diagnostic: the engine's state as the device holds it (readable while the grid runs): out[0]
  * posted (host ring), [1] relayed, [2] the relayed count the workgroups poll, [3] the exit
  * epoch, [4] launches, [5] grid, [6] completed, [7] running, then every workgroup's cursor (the
- * next step it takes at a launch). n_words >= 8 + grid. */
+ * next step it takes at a launch), then the arrival counters ([depth][8] per shard, then [depth]
+ * top). n_words >= 8 + grid + 9 * depth. */
 int hq_engine_dump(hq_engine *eng, uint64_t *out, uint32_t n_words);
 const char *hq_engine_last_error(const hq_engine *eng);
 /* Drain and destroy. NULL is a no-op. */

@@ -1,4 +1,6 @@
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/engine_probe.py > gpurun_out/r05_probe.log 2>&1; rc=$?
-tail -30 gpurun_out/r05_probe.log; exit $rc
+PROBE_QUIET=1 PROBE_STEPS=37 timeout -k 10 60 python -u tools/engine_probe.py > gpurun_out/r05_probe_fast.log 2>&1; rc=$?
+tail -8 gpurun_out/r05_probe_fast.log
+PROBE_QUIET=1 PROBE_STEPS=37 PROBE_G=100000 timeout -k 10 60 python -u tools/engine_probe.py > gpurun_out/r05_probe_fast2.log 2>&1; rc2=$?
+tail -8 gpurun_out/r05_probe_fast2.log; exit $((rc+rc2))
