@@ -1403,6 +1403,34 @@ class CommitMirror:
         return (n_c, n_r, adv_sum & m, rd & m, cd & m)
 
 
+def _latency(ts):
+    """p50 / p99 / max (ms) of per-step wall times (s)."""
+    if not ts:
+        return None
+    a = np.asarray(ts) * 1e3
+    return {"p50": round(float(np.percentile(a, 50)), 4), "p99": round(float(np.percentile(a, 99)), 4),
+            "max": round(float(a.max()), 4), "n": len(a)}
+
+
+def _phase_summary(ph):
+    """The end-to-end steps' phases: medians, and the three slowest steps in full."""
+    if not ph:
+        return None
+    keys = ("e2e_ms", "encode_max_ms", "execute_ms", "dev_ms", "enc_wall_ms", "enc_task_lag_max_ms",
+            "cgroup_throttled_ms")
+    med = {k: round(float(np.median([p[k] for p in ph])), 4) for k in keys
+           if all(p.get(k) is not None for p in ph)}
+    th = [p["cgroup_throttled_ms"] for p in ph if p.get("cgroup_throttled_ms") is not None]
+    if th:
+        med["steps_throttled"] = int(sum(1 for x in th if x > 0))
+        med["throttled_ms_total"] = round(float(sum(th)), 3)
+    slow = sorted(ph, key=lambda p: -p["e2e_ms"])[:3]
+    slow_dev = sorted(ph, key=lambda p: -p["dev_ms"])[:2]
+    rnd = lambda p: {k: (round(v, 4) if isinstance(v, float) else v) for k, v in p.items()}
+    return {"median": med, "slowest": [rnd(p) for p in slow],
+            "slowest_device_only": [rnd(p) for p in slow_dev]}
+
+
 def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     """The device step engine (hq_worker_step_stream, HQ_WORKER_ON_DEVICE: every event of the
     step taken on the GPU) over G leader groups per GPU, W = 1, 2 and 16 workers (dragonboat runs
@@ -1437,7 +1465,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     recs = StepRows16(hq, G, roles)      # the producer's compact form of the same messages
     offsets = rows.offsets
     # the producer's native encode threads per step, shared by the W workers' encodes
-    enc_threads = max(1, min(16, cpu_thread_counts()[0]))
+    enc_threads = encode_threads()
     pin = hq.Context(d.device)
     Ws = (1, 2, 16)
     modes = {}
@@ -1459,15 +1487,19 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         bufs = [[(pin.pinned((e1 - e0) * 5 + 64, np.uint8), pin.pinned(len(o) - 1, np.uint32))
                  for o, e0, e1 in parts] for _ in range(2)]
         modes[W] = dict(parts=parts, bufs=bufs, nbytes=[[0] * W, [0] * W], dev=workers(),
-                        e2e=workers(), t={"dev": [], "e2e": []}, bytes=0,
+                        e2e=workers(), t={"dev": [], "e2e": []}, bytes=0, phases=[],
                         check={"dev": [], "e2e": []},
                         mirror={k: CommitMirror(cids, g["committed"], bounds)
                                 for k in ("dev", "e2e")})
     pool = ThreadPoolExecutor(max(Ws) + 1)
+    # the encodes of a step run on at most enc_threads threads in all (W > enc_threads: queued)
+    enc_pool = ThreadPoolExecutor(enc_threads)
 
     def encode(W, i, slot):
         """Worker i's stream of the current step from the producer's compact records, on its
-        share of the encode threads, straight into its pinned receive buffer."""
+        share of the encode threads, straight into its pinned receive buffer. Returns its wall
+        time (s)."""
+        t0 = time.perf_counter()
         mo = modes[W]
         off, e0, e1 = mo["parts"][i]
         out, sz = mo["bufs"][slot][i]
@@ -1475,6 +1507,12 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                                                max(1, enc_threads // W))
         assert ne == e1 - e0
         mo["nbytes"][slot][i] = nb
+        return time.perf_counter() - t0
+
+    def timed_execute(j):
+        t0 = time.perf_counter()
+        j.execute()
+        return time.perf_counter() - t0
 
     def jobs(W, slot, which):
         mo = modes[W]
@@ -1525,26 +1563,43 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             # (timed: the native step of the W workers; their result views are built after)
             j = jobs(W, slot, "dev")
             d.barrier()
+            tq0 = cgroup_throttled_us()
             t0 = time.perf_counter()
             j.execute()
             dt = time.perf_counter() - t0
+            tq1 = cgroup_throttled_us()
             mo["check"]["dev"].append(mo["mirror"]["dev"].step(j.results(copy=False)))
             j = jobs(W, slot, "e2e")
             d.barrier()
+            hq.encode_stats(reset=True)
+            th0 = cgroup_throttled_us()
             t1 = time.perf_counter()
-            fut = pool.submit(j.execute)
-            encs = [pool.submit(encode, W, i, 1 - slot) for i in range(W)]
-            for f in encs:
-                f.result()
-            fut.result()
+            fut = pool.submit(timed_execute, j)
+            encs = [enc_pool.submit(encode, W, i, 1 - slot) for i in range(W)]
+            enc_s = [f.result() for f in encs]
+            exe_s = fut.result()
             dt2 = time.perf_counter() - t1
+            th1 = cgroup_throttled_us()
+            es = hq.encode_stats(reset=True)
             mo["check"]["e2e"].append(mo["mirror"]["e2e"].step(j.results(copy=False)))
             if s >= STEP_WARM:
                 mo["t"]["dev"].append(dt)
                 mo["t"]["e2e"].append(dt2)
+                # where the end-to-end step went: the encodes (the slowest call), the device
+                # step beside them, the encoder's task-start lag (hq_encode_stats)
+                mo["phases"].append({"step": s - STEP_WARM, "e2e_ms": dt2 * 1e3,
+                                     "encode_max_ms": max(enc_s) * 1e3,
+                                     "execute_ms": exe_s * 1e3, "dev_ms": dt * 1e3,
+                                     "dev_throttled_ms": (None if tq0 is None or tq1 is None
+                                                          else (tq1 - tq0) / 1e3),
+                                     "enc_wall_ms": es["wall_ns"] / 1e6 / max(1, es["calls"]),
+                                     "enc_task_lag_max_ms": es["max_lag_ns"] / 1e6,
+                                     "cgroup_throttled_ms": (None if th0 is None or th1 is None
+                                                             else (th1 - th0) / 1e3)})
         if s >= STEP_WARM:
             timed += 1
     pool.shutdown()
+    enc_pool.shutdown()
     committed = {}
     for W in Ws:
         for which in ("dev", "e2e"):
@@ -1593,12 +1648,17 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                                              "median": _median(modes[W]["t"][k]) * 1e3,
                                              "max": float(np.max(modes[W]["t"][k]) * 1e3)}
                                for W in Ws for k in ("dev", "e2e")},
+        # step latency as the reference reports it (README.md:55-62: P99 / P99.9): per mode the
+        # p50 / p99 / max of the timed steps, and the slowest end-to-end steps with their phases
+        "latency_ms": {f"{k}_w{W}": _latency(modes[W]["t"][k]) for W in Ws for k in ("dev", "e2e")},
+        "e2e_phases": {f"w{W}": _phase_summary(modes[W]["phases"]) for W in Ws},
         "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
         "modes_agree": same_modes,
         **({"modes_mismatch": mismatch} if mismatch else {}),
         "producer": f"compact 16-byte message records (hq_event16) encoded by "
                     f"hq_events16_encode_sized on {enc_threads} native threads per step "
-                    f"(max(1, {enc_threads} // W) per worker)",
+                    f"(max(1, {enc_threads} // W) per worker, at most {enc_threads} encodes at "
+                    f"once; the usable CPUs less two, capped by the cgroup quota)",
         "producer_equal_rows": producer_equal,
         "note": "end_to_end: the producer's encode of step s + 1 overlapped with the device step "
                 "s; device_only: the encoded stream given",
@@ -1753,6 +1813,35 @@ def host_cores():
     except (OSError, ValueError):
         pass
     return visible, usable, quota
+
+
+def cgroup_throttled_us():
+    """CPU time (us) this process's cgroup has been throttled by its CPU quota so far (cgroup v2
+    cpu.stat throttled_usec, v1 throttled_time), or None where it cannot be read. A box whose
+    share of a large host is a quota of 16 CPUs stops every thread of the cgroup for the rest of
+    a quota period once its threads have used the period's CPU time."""
+    for path, key, scale in (("/sys/fs/cgroup/cpu.stat", "throttled_usec", 1.0),
+                             ("/sys/fs/cgroup/cpu/cpu.stat", "throttled_time", 1e-3),
+                             ("/sys/fs/cgroup/cpu,cpuacct/cpu.stat", "throttled_time", 1e-3)):
+        try:
+            for ln in open(path):
+                k, v = ln.split()
+                if k == key:
+                    return int(v) * scale
+        except (OSError, ValueError):
+            continue
+    return None
+
+
+def encode_threads():
+    """The producer's native encode threads: the usable CPUs (capped by the cgroup quota) less
+    two (the step's own thread and the GPU runtime's), at most 16 — so that the encodes, the step
+    and the runtime never ask for more CPU than the quota gives (BENCH_HQ_ENCODE_THREADS
+    overrides)."""
+    v = os.environ.get("BENCH_HQ_ENCODE_THREADS")
+    if v:
+        return max(1, int(v))
+    return max(1, min(16, cpu_thread_counts()[0] - 2))
 
 
 def cpu_thread_counts():
@@ -1958,8 +2047,8 @@ def _short(rec):
     if "error" in rec or "skipped" in rec:
         return {k: str(rec.get(k))[:120] for k in ("error", "skipped") if k in rec}
     out = {}
-    for k in ("value", "unit", "roofline_frac", "kernel_avg_us", "ms_per_step",
-              "median_ms_per_step", "aggregate_frac_of_peak", "fit_t0_us",
+    # (kernel times, units and the rest stay in the detail file: the line must stay < 8 KB)
+    for k in ("value", "roofline_frac", "aggregate_frac_of_peak", "fit_t0_us",
               "fit_stream_frac_of_peak"):
         v = rec.get(k)
         if v is not None:
@@ -1968,8 +2057,10 @@ def _short(rec):
     par = rec.get("parity_full_size")
     if isinstance(par, dict):
         out["parity_equal"] = par.get("equal")
-    for k in ("end_to_end", "device_only", "cpu_replay", "vs_cpu_replay_end_to_end",
-              "vs_cpu_replay_device_only", "parity_committed", "modes_agree"):
+    lat = rec.get("latency_ms")
+    if isinstance(lat, dict):
+        out["p99_ms"] = {k: v["p99"] for k, v in lat.items() if v}
+    for k in ("end_to_end", "device_only", "vs_cpu_replay_end_to_end", "parity_committed"):
         if k in rec:
             v = rec[k]
             if isinstance(v, dict):

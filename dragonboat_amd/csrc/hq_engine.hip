@@ -382,9 +382,40 @@ void k_commit_engine(const EngineK e) {
     uint64_t known = s0;      // descriptors the wave has seen as known
     uint32_t e_prev = 0;      // the workgroup's tickets before step s
     uint32_t t = claim(l, lane);
+    // SIG / INPLACE: a decided tile is counted (fin / done) only once its stores are complete.
+    // The count of tile k is taken after tile k + 1's loads have returned (vector memory
+    // operations complete in issue order on the VM counter, so tile k's stores are done by then):
+    // the wave issues the next tile's loads without waiting for its stores' acknowledgements.
+    // Before the wave waits (a step barrier, the frontier) or leaves, it drains and counts.
+    bool pend = false;        // a decided tile not yet counted
+    uint64_t p_s = 0;         // its step
+    uint32_t p_tgt = 0;       // SIG: fin value at which its step is decided
+    auto count = [&]() {
+        if constexpr (INPLACE) {
+            if (lane == 0)
+                __hip_atomic_fetch_add(&l.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (SIG) {
+            uint32_t f = 0;
+            if (lane == 0)
+                f = __hip_atomic_fetch_add(&l.fin[p_s & dmask], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
+            if (wave_u32(f) == p_tgt && lane == 0) arrive(kargs(), p_s);
+        }
+        pend = false;
+    };
+    auto drain = [&]() {
+        if constexpr (SIG || INPLACE) {
+            if (pend) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                count();
+            }
+        }
+    };
     for (;;) {
         // the step of ticket t
         if (s >= known) {
+            drain();
             known = frontier<WPW>(kargs(), l, s, lane);
             if (known <= s) break;   // idle: resume here at the next launch
         }
@@ -394,6 +425,7 @@ void k_commit_engine(const EngineK e) {
             // the wave holding the first ticket past the workgroup's last tile counts the
             // workgroup's arrival at the STOP (every step before it is complete once the grid
             // has exited)
+            drain();
             if (t == e_prev && lane == 0) arrive(kargs(), s);
             ++s;
             break;
@@ -414,6 +446,7 @@ void k_commit_engine(const EngineK e) {
             if constexpr (INPLACE) {
                 // the table's tiles of step s are those of step s - 1: wait until the workgroup
                 // has decided every tile before this step (no tile of step s is decided before)
+                drain();
                 while (before(wave_u32(__hip_atomic_load(&l.done, __ATOMIC_ACQUIRE,
                                                          __HIP_MEMORY_SCOPE_WORKGROUP)),
                               e_prev))
@@ -428,19 +461,14 @@ void k_commit_engine(const EngineK e) {
                 asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
                 commit_tile<N, FORM, false, LEAD, INPLACE, SIG, true>(k, wbase, ln);
                 if constexpr (SIG || INPLACE) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tile's stores drained
-                    if constexpr (INPLACE) {
-                        if (lane == 0)
-                            __hip_atomic_fetch_add(&l.done, 1u, __ATOMIC_RELEASE,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    if constexpr (SIG) {
-                        uint32_t f = 0;
-                        if (lane == 0)
-                            f = __hip_atomic_fetch_add(&l.fin[slot], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
-                        if (wave_u32(f) == tgt && lane == 0) arrive(kargs(), s);
-                    }
+                    // this tile's loads have returned (its decision used them; the compiler
+                    // barrier keeps the count below that wait): the previous tile's stores are
+                    // complete
+                    asm volatile("" ::: "memory");
+                    if (pend) count();
+                    pend = true;
+                    p_s = s;
+                    p_tgt = tgt;
                 }
                 t = claim(l, lane);
             } while (before(t, e_cur));
@@ -448,6 +476,7 @@ void k_commit_engine(const EngineK e) {
         e_prev = e_cur;
         ++s;
     }
+    drain();
     if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
 }
 
