@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -272,11 +273,6 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
     return HQ_OK;
 }
 
-// per-thread scratch of threaded encodes, taken from a pool for the length of a call (calls on
-// several threads run side by side, each on scratch of its own)
-std::mutex g_scratch_mu;
-std::vector<std::vector<std::vector<uint8_t>>> g_scratch_free;
-
 struct alignas(64) RangeOut {   // one thread's results, a cache line each
     uint64_t events = 0, bytes = 0;
     uint64_t last_start = ~0ull;   // offset of the range's last event in its bytes (none: ~0)
@@ -319,7 +315,10 @@ public:
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
-    void parallel_for(uint32_t T, const std::function<void(uint32_t)> &fn) {
+    // gang: the T indexes run at the same time (each may wait for the others: a barrier inside
+    // fn); the caller runs index 0 only and every other index gets a pool thread of its own (the
+    // pool holds a thread per queued index of every live call, so the gang always assembles)
+    void parallel_for(uint32_t T, const std::function<void(uint32_t)> &fn, bool gang = false) {
         if (T <= 1) {
             if (T) fn(0);
             return;
@@ -343,7 +342,7 @@ public:
         }
         cv_.notify_all();
         run(*job, 0);
-        for (;;) {
+        for (; !gang;) {
             const uint32_t i = job->next.fetch_add(1);
             if (i >= T) break;
             run(*job, i);
@@ -421,20 +420,18 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     const uint64_t nrec = n_groups ? offsets16[n_groups] - offsets16[0] : 0;
     const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(threads, 1u),
                                                     std::max<uint64_t>(1, nrec / 4096));
+    // one thread encodes straight into out (through a scratch of its own it was slower: 59
+    // against 38 ms for the step5 producer on one fresh thread, profiles/r05b/enc_probe.log)
     if (T <= 1)
         return enc16_range(offsets16, recs, sizes, 0, n_groups, nullptr, out, cap, n_events,
                            n_bytes);
     const uint64_t c0 = now_ns();
-    // T ranges of about equal records (group boundaries), each into its own scratch
-    std::vector<std::vector<uint8_t>> scratch;
-    {
-        std::lock_guard<std::mutex> lock(g_scratch_mu);
-        if (!g_scratch_free.empty()) {
-            scratch = std::move(g_scratch_free.back());
-            g_scratch_free.pop_back();
-        }
-    }
-    if (scratch.size() < T) scratch.resize(T);
+    // T ranges of about equal records (group boundaries). Each range is encoded by one pool
+    // thread into that thread's own scratch (first touched, so held on its memory node, and
+    // reused by later calls), the threads meet once every range's byte count is known, and each
+    // copies its range into place: one pass, no scratch shared between threads (scratch handed
+    // from thread to thread ran the encode 2.5 x slower per record on a 256-CPU host,
+    // profiles/r05b/enc_probe.log)
     std::vector<uint64_t> g(T + 1);
     std::vector<RangeOut> res(T);
     g[0] = 0;
@@ -444,34 +441,44 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
         g[t] = std::max<uint64_t>(g[t - 1], (uint64_t)(std::lower_bound(offsets16, offsets16 + n_groups,
                                                                          want) - offsets16));
     }
-    task_pool().parallel_for(T, [&](uint32_t t) {
-        res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch[t], nullptr, 0,
-                                &res[t].events, &res[t].bytes, &res[t].last_start);
-    });
-    const uint64_t c1 = now_ns();
-    uint64_t total = 0, events = 0, last = ~0ull;
+    std::mutex bm;
+    std::condition_variable bcv;
+    uint32_t arrived = 0;
+    uint64_t c1 = 0, total = 0, events = 0;
     int rc = HQ_OK;
-    for (uint32_t t = 0; t < T; ++t) {
-        if (res[t].rc && !rc) rc = res[t].rc;
-        if (res[t].last_start != ~0ull) last = total + res[t].last_start;
-        total += res[t].bytes;
-        events += res[t].events;
-    }
-    // the one-thread rule: HQ_EVENT_STREAM_MAX bytes free before every event, i.e. before the
-    // last one (event starts only grow)
-    if (!rc && last != ~0ull && (cap < last || cap - last < HQ_EVENT_STREAM_MAX)) rc = HQ_E_STATE;
+    bool fits = true;
+    std::vector<uint64_t> at(T, 0);
+    task_pool().parallel_for(T, [&](uint32_t t) {
+        thread_local std::vector<uint8_t> scratch;
+        res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch, nullptr, 0,
+                                &res[t].events, &res[t].bytes, &res[t].last_start);
+        {
+            std::unique_lock<std::mutex> lk(bm);
+            if (++arrived == T) {
+                // the last range in: totals, the capacity rule (HQ_EVENT_STREAM_MAX bytes free
+                // before every event, i.e. before the last one: event starts only grow) and
+                // every range's place
+                c1 = now_ns();
+                uint64_t last = ~0ull;
+                for (uint32_t i = 0; i < T; ++i) {
+                    if (res[i].rc && !rc) rc = res[i].rc;
+                    if (res[i].last_start != ~0ull) last = total + res[i].last_start;
+                    at[i] = total;
+                    total += res[i].bytes;
+                    events += res[i].events;
+                }
+                fits = last == ~0ull || (cap >= last && cap - last >= HQ_EVENT_STREAM_MAX);
+                bcv.notify_all();
+            } else {
+                bcv.wait(lk, [&] { return arrived == T; });
+            }
+        }
+        if (!rc && fits && res[t].bytes) std::memcpy(out + at[t], scratch.data(), res[t].bytes);
+    }, true);
+    if (!rc && !fits) rc = HQ_E_STATE;
     if (!rc) {
-        std::vector<uint64_t> at(T, 0);
-        for (uint32_t t = 1; t < T; ++t) at[t] = at[t - 1] + res[t - 1].bytes;
-        task_pool().parallel_for(T, [&](uint32_t t) {
-            if (res[t].bytes) std::memcpy(out + at[t], scratch[t].data(), res[t].bytes);
-        });
         *n_events = events;
         *n_bytes = total;
-    }
-    {
-        std::lock_guard<std::mutex> lock(g_scratch_mu);
-        g_scratch_free.push_back(std::move(scratch));
     }
     const uint64_t c2 = now_ns();
     g_clk.calls++;

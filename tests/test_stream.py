@@ -318,7 +318,7 @@ def test_encode_stats_count_threaded_calls(hq):
     hq.encode_stats(reset=True)
     hq.encode_events16_sized(off16, recs, threads=4)
     st = hq.encode_stats(reset=True)
-    assert st["calls"] == 1 and st["tasks"] == 8          # 4 ranges, 2 phases
+    assert st["calls"] == 1 and st["tasks"] == 4          # 4 ranges, encoded and copied by one task each
     assert st["wall_ns"] >= st["encode_ns"] > 0 and st["run_ns"] > 0
     assert st["helped"] <= st["tasks"] and st["max_lag_ns"] <= st["lag_ns"]
     assert hq.encode_stats()["calls"] == 0

@@ -24,12 +24,24 @@ def run(W, T, reps=5):
         o, e0, e1 = parts[i]
         hq.encode_events16_sized_into(o, r[e0:e1], outs[i][0], outs[i][1], T)
     ts = []
+    hq.encode_stats(reset=True)
     for _ in range(reps):
         th = [threading.Thread(target=one, args=(i,)) for i in range(W)]
         t0 = time.perf_counter()
         for t in th: t.start()
         for t in th: t.join()
         ts.append(time.perf_counter() - t0)
-    return min(ts) * 1e3, np.median(ts) * 1e3
-for W, T in ((1, 16), (2, 8), (16, 1), (1, 8), (2, 4)):
-    print(W, T, ["%.2f" % x for x in run(W, T)])
+    st = hq.encode_stats(reset=True)
+    c = max(1, st["calls"])
+    ph = (f"per call: encode {st['encode_ns'] / c / 1e6:.2f} copy {st['copy_ns'] / c / 1e6:.2f} ms, "
+          f"task run sum {st['run_ns'] / c / 1e6:.2f} ms, helped {st['helped'] / c:.1f}, "
+          f"lag max {st['max_lag_ns'] / 1e6:.3f} ms") if st["calls"] else ""
+    return min(ts) * 1e3, np.median(ts) * 1e3, ph
+import os
+for W, T in ((1, 16), (1, 14), (2, 8), (2, 7), (16, 1), (14, 1), (1, 8), (1, 1)):
+    mn, md, ph = run(W, T)
+    print(W, T, "%.2f %.2f" % (mn, md), ph, flush=True)
+os.environ["HQ_ENCODE_DIRECT"] = "1"
+for W, T in ((16, 1), (1, 1)):
+    mn, md, ph = run(W, T)
+    print("direct", W, T, "%.2f %.2f" % (mn, md), ph, flush=True)
