@@ -712,8 +712,12 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
         achieved_gbs=achieved_local, achieved_node_gbs=achieved_node, per_gpu=per_gpu,
         set0=set0, gather=None, windows=len(wins), headline_mode=hm,
         engine={
-            "mode": "persistent commit engine (hq_engine): one resident launch per window of "
-                    f"{steps} posted steps", "grid": info.grid, "block": info.block,
+            "mode": "persistent commit engine (hq_engine): the window's steps posted (one "
+                    f"descriptor per {groups_per_step(w)}-group step, {steps} steps in one "
+                    "hq_engine_post call) and decided step after step by one resident launch "
+                    "(started by the first post, ended by the drain's STOP)",
+            "groups_per_step": groups_per_step(w), "steps_per_window": steps,
+            "grid": info.grid, "block": info.block,
             "window_ms": [round(x["engine"]["elapsed"] * 1e3, 4) for x in wins],
             "window_kernel_us_per_step": [round(x["engine"]["kernel_s"] * 1e6, 3) for x in wins],
             "median_kernel_us_per_step": med("engine", "kernel_s") * 1e6,
@@ -733,6 +737,8 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
         fused_window={
             "mode": f"the window's {steps} batches in {len(fused_chunks(steps))} fused launch(es) "
                     "(hq_commit_fused_dev, one workgroup range per batch, <= 32 batches each)",
+            "batches_per_launch": [cn for _, cn in fused_chunks(steps)],
+            "groups_per_launch": [cn * groups_per_step(w) for _, cn in fused_chunks(steps)],
             "fused_equals_launch_set0": fused_eq_launch,
             "window_ms": [round(x["fused"]["elapsed"] * 1e3, 4) for x in wins],
             "median_ms_per_step": med("fused", "elapsed") / steps * 1e3,
@@ -742,6 +748,7 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
         },
         launch_per_step={
             "mode": "the same batches as back-to-back launches (hq_commit_many_dev)",
+            "groups_per_launch": groups_per_step(w),
             "window_ms": [round(x["launches"]["elapsed"] * 1e3, 4) for x in wins],
             "median_ms_per_step": le / steps * 1e3,
             "median_kernel_us": lk * 1e6,
@@ -2106,6 +2113,11 @@ def report(args, d, res, launcher):
             "layout": ("tiles_leader" if w.get("lead") else "tiles") if w.get("tiled")
             else "columns",
             "global_groups_per_step": groups_per_step(w) * d.world,
+            **({"headline_mode": r["headline_mode"], "steps_per_window": args.steps,
+                "groups_per_launch": (r["fused_window"]["groups_per_launch"]
+                                      if r["headline_mode"] == "fused" else
+                                      "one resident launch per window")}
+               if r.get("headline_mode") else {}),
             "parallelism": f"shard{d.world} (clusterID % {d.world}, partition.go:38)",
             "launcher": launcher,
             "devices_seen": len({x["pci_bus_id"] or x["device"] for x in devs}),
@@ -2204,7 +2216,7 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="fused", choices=("fused", "engine", "launch"),
+    ap.add_argument("--mode", default="engine", choices=("fused", "engine", "launch"),
                     help="headline commit steps: the co-resident step workers' batches fused "
                          "into launches of up to 32 (fused), the persistent engine (one resident "
                          "launch per window), or one launch per step; fused and engine apply to "
