@@ -157,16 +157,48 @@ __device__ __forceinline__ bool dvar(ByteReader &r, uint64_t &v) {
 }
 
 // a group's stream state the codes refer back to (hq_stream.cpp's Prev): its previous message
-// term, its previous ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code 5)
+// term, its previous ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code
+// 5), the previous message a run repeats (code 6; last 1 ReplicateResp, 2 HeartbeatResp, bit 2
+// its reject) and the run's events still to come
 struct DPrev {
     uint64_t term = 0, index = 0, hint = 0, high = 0;
     bool have_index = false;
+    uint32_t last = 0, run = 0;
 };
 
 // one event of a group's stream
 __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
     v = hq_event{};
     if (!r.more()) return false;
+    if (pv.run == 0) {
+        // (peek: a run header is taken here, any other header below)
+        const uintptr_t a = reinterpret_cast<uintptr_t>(r.p);
+        if ((a & ~uintptr_t(7)) != r.wa) {
+            r.wa = a & ~uintptr_t(7);
+            r.w = *reinterpret_cast<const uint64_t *>(r.wa);
+        }
+        const uint32_t h0 = (uint32_t)(r.w >> (8 * (a & 7))) & 0xFF;
+        if ((h0 & 7) == HQ_EV_MESSAGE && ((h0 >> 3) & 7) == 6) {
+            (void)r.next();
+            uint64_t m;
+            if (!(pv.last & 3) || !dvar(r, m) || m == 0 || m > 0xFFFF) return false;
+            pv.run = (uint32_t)m;
+        }
+    }
+    if (pv.run) {                  // a run member: the previous message with another sender
+        --pv.run;
+        v.kind = HQ_EV_MESSAGE;
+        v.type = (pv.last & 3) == 1 ? HQ_MSG_REPLICATE_RESP : HQ_MSG_HEARTBEAT_RESP;
+        v.reject = (pv.last >> 2) & 1;
+        v.term = pv.term;
+        if ((pv.last & 3) == 1) {
+            v.log_index = pv.index;
+        } else {
+            v.hint = pv.hint;
+            v.hint_high = pv.high;
+        }
+        return dvar(r, v.from);
+    }
     const uint32_t h = r.next();
     v.kind = h & 7;
     if (v.kind == HQ_EV_READ) return dvar(r, v.hint) && dvar(r, v.hint_high);
@@ -200,6 +232,7 @@ __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
         pv.hint = v.hint;
         pv.high = v.hint_high;
     }
+    pv.last = (code == 0 || code == 4 ? 1u : code == 2 || code == 5 ? 2u : 0u) | v.reject << 2;
     return true;
 }
 
@@ -527,7 +560,7 @@ struct Engine {
         // a group that took all its events must have used all its bytes: left-over bytes mean the
         // sizes were split wrongly between groups, which the host decoder rejects as HQ_E_INVAL
         // (hq_stream.cpp); pass A makes it an input error, so no state is written
-        if (STREAM && !WRITE && !(g.flags & kDSuspended) && br.p != br.end)
+        if (STREAM && !WRITE && !(g.flags & kDSuspended) && (br.p != br.end || pv.run))
             atomicOr(a.error, (uint32_t)kErrBoffsets);
         if (!WRITE && g.committed - committed0 > 0xFFFFFFFFull && a.wide)
             atomicOr(a.wide, 1u);                        // no 4-byte advance column this step

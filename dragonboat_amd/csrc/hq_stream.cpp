@@ -61,11 +61,45 @@ inline bool get(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
 }
 
 // a group's stream state the codes refer back to: its previous message term, its previous
-// ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code 5; 0 / 0 at first)
+// ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code 5; 0 / 0 at first),
+// and the previous message a run (code 6) repeats: last 1 = a ReplicateResp, 2 = a HeartbeatResp
+// (written with codes 0 / 4 / 2 / 5 or in a run), 0 = none or another type; last_reject its bit
 struct Prev {
     uint64_t term = 0, index = 0, hint = 0, high = 0;
     bool have_index = false;
+    uint8_t last = 0, last_reject = 0;
 };
+
+// Runs (code 6): the acks of a steady leader's followers repeat one another but for the sender
+// (every follower acks the same index, every follower's heartbeat ack carries the same ctx). A
+// run of 3..kRunMax messages that repeat the group's previous message (its type, term, reject
+// and index / ctx) is one header, a count and the senders: 2 + m bytes for 1-byte senders
+// instead of 2 m. At most kRunMax events per run, so that a run with 10-byte senders still fits
+// the HQ_EVENT_STREAM_MAX bytes the encoder asks for before each unit.
+constexpr uint32_t kRunMin = 3, kRunMax = 6;
+constexpr uint32_t kCodeRun = 6;
+
+inline uint8_t last_of(uint32_t code) {
+    return code == 0 || code == 4 ? 1 : code == 2 || code == 5 ? 2 : 0;
+}
+
+// does row e repeat the group's previous message (a run member)?
+inline bool repeats(const hq_event &e, const Prev &pv) {
+    if (!pv.last || e.kind != HQ_EV_MESSAGE || (e.reject != 0) != (pv.last_reject != 0) ||
+        e.term != pv.term)
+        return false;
+    if (pv.last == 1) return e.type == HQ_MSG_REPLICATE_RESP && e.log_index == pv.index;
+    return e.type == HQ_MSG_HEARTBEAT_RESP && e.hint == pv.hint && e.hint_high == pv.high;
+}
+
+// a run of m messages repeating the previous one, senders from[0..m)
+template <class From>
+inline uint8_t *put_run(uint8_t *p, uint32_t m, From from) {
+    *p++ = (uint8_t)(HQ_EV_MESSAGE | kCodeRun << 3);
+    *p++ = (uint8_t)m;                  // m <= kRunMax: one byte
+    for (uint32_t j = 0; j < m; ++j) p = put(p, from(j));
+    return p;
+}
 
 // one event; returns the write position
 inline uint8_t *encode(uint8_t *p, const hq_event &e, Prev &pv) {
@@ -91,6 +125,8 @@ inline uint8_t *encode(uint8_t *p, const hq_event &e, Prev &pv) {
         pv.high = e.hint_high;
     }
     const bool same = e.term == pv.term;
+    pv.last = last_of(code);
+    pv.last_reject = e.reject ? 1 : 0;
     *p++ = (uint8_t)(HQ_EV_MESSAGE | code << 3 | (e.reject ? 0x40 : 0) | (same ? 0x80 : 0));
     if (code == 7) p = put(p, e.type);
     p = put(p, e.from);
@@ -201,6 +237,8 @@ __attribute__((always_inline)) inline uint8_t *encode16(uint8_t *p, const hq_eve
         }
     }
     const bool same = r.term == pv.term;
+    pv.last = last_of(code);
+    pv.last_reject = (r.kind & 8) ? 1 : 0;
     const uint32_t hdr =
         HQ_EV_MESSAGE | code << 3 | ((r.kind & 8) ? 0x40u : 0u) | (same ? 0x80u : 0u);
     if (code != 7 && r.from < 0x80) {   // header and a 1-byte sender in one store
@@ -220,6 +258,65 @@ __attribute__((always_inline)) inline uint8_t *encode16(uint8_t *p, const hq_eve
         p = put_fast(p, high);
     }
     return p;
+}
+
+// does record r (not an escape) repeat the group's previous message? (repeats() of the event
+// from16 makes of it, without the row)
+__attribute__((always_inline)) inline bool repeats16(const hq_event16 &r, const Prev &pv,
+                                                    const uint64_t ctx[2]) {
+    if (!pv.last || (r.kind & 7) != HQ_EV_MESSAGE || ((r.kind >> 3) & 1) != pv.last_reject ||
+        r.term != pv.term)
+        return false;
+    if (pv.last == 1) return r.type == HQ_MSG_REPLICATE_RESP && r.value == pv.index;
+    if (r.type != HQ_MSG_HEARTBEAT_RESP) return false;
+    return (r.kind & HQ_EV16_READ_CTX) ? ctx[0] == pv.hint && ctx[1] == pv.high
+                                       : r.value == pv.hint && pv.high == 0;
+}
+
+// the records recs[k .. r1) that open with a run: its length (0 below kRunMin), the senders in
+// from[] and the records it takes in *used (an escaped event is 5 records)
+inline uint32_t run16(const hq_event16 *recs, uint64_t k, uint64_t r1, const Prev &pv,
+                      const uint64_t ctx[2], uint64_t from[kRunMax], uint64_t *used) {
+    uint32_t m = 0;
+    uint64_t q = k;
+    while (m < kRunMax && q < r1) {
+        const hq_event16 &r = recs[q];
+        if (r.kind & HQ_EV16_FULL) {      // an escaped event: its row
+            if (r1 - q < 5) break;
+            hq_event e;
+            std::memcpy(&e, &r + 1, sizeof e);
+            if (!repeats(e, pv)) break;
+            from[m++] = e.from;
+            q += 5;
+            continue;
+        }
+        if (!repeats16(r, pv, ctx)) break;
+        from[m++] = r.from;
+        ++q;
+    }
+    *used = q - k;
+    return m >= kRunMin ? m : 0;
+}
+
+// the rows events[e .. e1) that open with a run: its length (0 below kRunMin)
+inline uint32_t run_rows(const hq_event *events, uint64_t e, uint64_t e1, const Prev &pv) {
+    uint32_t m = 0;
+    while (m < kRunMax && e + m < e1 && repeats(events[e + m], pv)) ++m;
+    return m >= kRunMin ? m : 0;
+}
+
+// the unit at row e of a group's rows [.., e1): a run of repeats of the previous message, or
+// row e alone; returns the next row
+inline uint64_t encode_unit(uint8_t *&p, const hq_event *events, uint64_t e, uint64_t e1, Prev &pv) {
+    if (pv.last) {
+        const uint32_t m = run_rows(events, e, e1, pv);
+        if (m) {
+            p = put_run(p, m, [&](uint32_t j) { return events[e + j].from; });
+            return e + m;
+        }
+    }
+    p = encode(p, events[e], pv);
+    return e + 1;
 }
 
 // groups [g0, g1) encoded at out (cap bytes), or into a growing scratch (grow != nullptr); the
@@ -250,6 +347,16 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
                                                              HQ_EVENT_STREAM_MAX))
                 return HQ_E_STATE;
             lp = p;
+            if (pv.last) {                  // the next events repeat the previous message: a run
+                uint64_t from[kRunMax], used = 0;
+                const uint32_t m = run16(recs, k, r1, pv, ctx, from, &used);
+                if (m) {
+                    p = put_run(p, m, [&](uint32_t j) { return from[j]; });
+                    k += used;
+                    ne += m - 1;
+                    continue;
+                }
+            }
             if (!(recs[k].kind & HQ_EV16_FULL)) {
                 p = encode16(p, recs[k], pv, ctx);
                 ++k;
@@ -571,9 +678,9 @@ int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event 
     boffsets[0] = 0;
     for (uint64_t i = 0; i < n_groups; ++i) {
         Prev pv;
-        for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
+        for (uint64_t e = offsets[i]; e < offsets[i + 1];) {
             if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
-            p = encode(p, events[e], pv);
+            e = encode_unit(p, events, e, offsets[i + 1], pv);
         }
         boffsets[i + 1] = (uint64_t)(p - out);
     }
@@ -589,9 +696,9 @@ int hq_events_encode_sized(uint64_t n_groups, const uint64_t *offsets, const hq_
         if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 0xFFFF) return HQ_E_INVAL;
         uint8_t *const g0 = p;
         Prev pv;
-        for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
+        for (uint64_t e = offsets[i]; e < offsets[i + 1];) {
             if (!out || (uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return HQ_E_STATE;
-            p = encode(p, events[e], pv);
+            e = encode_unit(p, events, e, offsets[i + 1], pv);
         }
         if (p - g0 > 0xFFFF) return HQ_E_INVAL;
         sizes[i] = (uint32_t)(offsets[i + 1] - offsets[i]) | (uint32_t)(p - g0) << 16;
@@ -606,11 +713,33 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
     for (uint64_t i = 0; i < n_groups; ++i) {
         const uint8_t *p = bytes + boffsets[i], *const end = bytes + boffsets[i + 1];
         Prev pv;
+        uint64_t run_left = 0;          // events still to come in the current run
         for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
             hq_event &v = events[e];
             std::memset(&v, 0, sizeof v);
             if (p >= end) return HQ_E_INVAL;
-            const uint8_t h = *p++;
+            const uint8_t h = run_left ? (uint8_t)0 : *p;
+            if (run_left || ((h & 7) == HQ_EV_MESSAGE && ((h >> 3) & 7) == kCodeRun)) {
+                // a run member: the group's previous message with another sender
+                if (!run_left) {
+                    ++p;
+                    if (!pv.last || !get(p, end, run_left) || run_left == 0) return HQ_E_INVAL;
+                }
+                --run_left;
+                v.kind = HQ_EV_MESSAGE;
+                v.type = pv.last == 1 ? HQ_MSG_REPLICATE_RESP : HQ_MSG_HEARTBEAT_RESP;
+                v.reject = pv.last_reject;
+                v.term = pv.term;
+                if (pv.last == 1) {
+                    v.log_index = pv.index;
+                } else {
+                    v.hint = pv.hint;
+                    v.hint_high = pv.high;
+                }
+                if (!get(p, end, v.from)) return HQ_E_INVAL;
+                continue;
+            }
+            ++p;
             v.kind = h & 7;
             bool ok = true;
             if (v.kind == HQ_EV_READ) {
@@ -643,10 +772,12 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
                     pv.hint = v.hint;
                     pv.high = v.hint_high;
                 }
+                pv.last = last_of(code);
+                pv.last_reject = (uint8_t)v.reject;
             }
             if (!ok) return HQ_E_INVAL;
         }
-        if (p != end) return HQ_E_INVAL;
+        if (p != end || run_left) return HQ_E_INVAL;
     }
     return HQ_OK;
 }

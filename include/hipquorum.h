@@ -1031,7 +1031,14 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
  *                     only events written with codes 0 / 4 (ReplicateResp) and 2 / 5
  *                     (HeartbeatResp): a ReplicateResp or HeartbeatResp written with code 7 does
  *                     not set the index / ctx that a later code 4 / 5 repeats (the encoder never
- *                     writes those two types with code 7)
+ *                     writes those two types with code 7); 6 a run (ABI 17): the next m events
+ *                     repeat the group's previous message — a ReplicateResp or HeartbeatResp
+ *                     written with codes 0 / 4 / 2 / 5 or in a run: its type, term, reject and
+ *                     log_index / ctx — with other senders; a varint m >= 1, then m sender
+ *                     varints (bits 6-7 of a run's header are 0). The acks of a steady leader's
+ *                     followers come as runs: 2 + m bytes for m one-byte senders instead of 2 m.
+ *                     The encoders write a run for 3 to 6 such events (6: a run with 10-byte
+ *                     senders still fits HQ_EVENT_STREAM_MAX)
  *           bit 6     reject
  *           bit 7     term repeats the group's previous message term in the stream (0 before
  *                     its first message): the term varint is left out
@@ -1042,7 +1049,7 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
  * Fields a handler does not read are not carried (hq_events_decode returns them as 0). Event
  * indexes (offsets, deferred) count events as in hq_step_input.
  */
-#define HQ_EVENT_STREAM_MAX 64u   /* bytes one event takes at most */
+#define HQ_EVENT_STREAM_MAX 64u   /* bytes one event (or one run) takes at most */
 
 typedef struct hq_step_stream {
     uint64_t n_groups;

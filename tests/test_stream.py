@@ -353,3 +353,94 @@ def test_threaded_encodes_side_by_side(hq):
         for t in th:
             t.join()
     assert not bad
+
+
+# --- runs (code 6): acks repeating the group's previous message but for the sender --------------
+
+def runny_rows(hq, rng, groups=300):
+    """Groups whose steps a steady leader sees: runs of ReplicateResp / HeartbeatResp acks with one
+    index / ctx, term and reject, senders random (some >= 2^16: escapes in the compact form),
+    broken now and then by another index, a reject, another type, a READ or a proposal."""
+    rows, off = [], [0]
+    for _ in range(groups):
+        term = int(rng.choice([7, 7, 7, 9, 1 << 40]))
+        for _ in range(int(rng.integers(0, 5))):
+            typ = int(rng.choice([RREP, RREP, HBRESP, HBRESP, VRESP]))
+            idx, ctx = int(rng.choice([10, 11, 1 << 50])), int(rng.choice([0, 0, 5, 1 << 33]))
+            rej = int(rng.random() < 0.15)
+            for _ in range(int(rng.integers(1, 10))):
+                frm = int(rng.choice([2, 3, 4, 5, 6, 7, 100, 300, 1 << 20]))
+                r = (hq.EV_MESSAGE, typ, frm, term, idx if typ == RREP else 0,
+                     ctx if typ == HBRESP else 0, 0, rej, 0)
+                if rng.random() < 0.08:
+                    r = (hq.EV_MESSAGE, typ, frm, term, idx + 1 if typ == RREP else 0,
+                         ctx + 1 if typ == HBRESP else 0, 0, rej, 0)
+                rows.append(r)
+            if rng.random() < 0.3:
+                rows.append((hq.EV_READ, 0, 0, 0, 0, int(rng.integers(1, 99)), 0, 0, 0))
+            if rng.random() < 0.3:
+                rows.append((hq.EV_PROPOSE, 0, 0, 0, 3, 0, 0, 0, 0))
+        off.append(len(rows))
+    return np.array(rows, dtype=hq.EVENT_DTYPE), np.array(off, np.uint64)
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33])
+@pytest.mark.parametrize("threads", [1, 4])
+def test_runs_round_trip(hq, seed, threads):
+    """Runs are written by the row encoder and the compact-record encoder alike (escaped senders
+    included), never longer than 6 events, and decode back to the rows."""
+    ev, off = runny_rows(hq, np.random.default_rng(seed))
+    data, boff = hq.encode_events(off, ev)
+    hdr_run = 2 | 6 << 3
+    assert (data == hdr_run).sum() > 50
+    np.testing.assert_array_equal(hq.decode_events(off, boff, data), carried(hq, ev))
+    want, want_sizes = hq.encode_events_sized(off, ev)
+    np.testing.assert_array_equal(want, data)
+    recs, off16 = hq.events_to16(off, ev)
+    assert (recs["kind"] & hq.EV16_FULL).any()
+    got, sizes, ne = hq.encode_events16_sized(off16, recs, threads=threads)
+    np.testing.assert_array_equal(got, data)
+    np.testing.assert_array_equal(sizes, want_sizes)
+    assert ne == len(ev)
+
+
+def _one_group(hq, rows):
+    ev = np.array(rows, dtype=hq.EVENT_DTYPE)
+    return ev, np.array([0, len(ev)], np.uint64)
+
+
+def test_run_length_and_split(hq):
+    """A ReplicateResp and 8 repeats: the first in full, a run of 6, then two code-4 events (a run
+    needs 3); the same message with another term, index or reject breaks a run."""
+    rows = [(hq.EV_MESSAGE, RREP, 2 + i, 41, 1000, 0, 0, 0, 0) for i in range(9)]
+    ev, off = _one_group(hq, rows)
+    data, _ = hq.encode_events(off, ev)
+    # code 0: header, from, term (41), index (1000: 2 bytes) = 5; run: header, 6, six senders = 8;
+    # two code-4 events of 2 bytes
+    assert len(data) == 5 + 8 + 4
+    assert data[5] == (2 | 6 << 3) and data[6] == 6 and list(data[7:13]) == list(range(3, 9))
+    np.testing.assert_array_equal(hq.decode_events(off, np.array([0, len(data)], np.uint64), data),
+                                  carried(hq, ev))
+    for k, v in (("term", 42), ("log_index", 1001), ("reject", 1)):
+        ev2 = ev.copy()
+        ev2[3][k] = v
+        d2, _ = hq.encode_events(off, ev2)
+        assert (d2 == (2 | 6 << 3)).sum() <= 1 and len(d2) > len(data)
+        np.testing.assert_array_equal(
+            hq.decode_events(off, np.array([0, len(d2)], np.uint64), d2), carried(hq, ev2))
+
+
+def test_run_malformed(hq):
+    """A run with nothing to repeat (first in the group, or after a RequestVoteResp), a count of
+    0, or a count past the group's events is HQ_E_INVAL."""
+    run = 2 | 6 << 3
+    bad = [
+        (np.array([run, 1, 5], np.uint8), 1),                       # nothing before it
+        (np.array([2 | 1 << 3, 5, 7, run, 1, 6], np.uint8), 2),     # after a RequestVoteResp
+        (np.array([2 | 0 << 3, 5, 7, 9, run, 0], np.uint8), 2),     # count 0
+        (np.array([2 | 0 << 3, 5, 7, 9, run, 3, 6, 7, 8], np.uint8), 3),   # 3 announced, 2 left
+    ]
+    for data, n in bad:
+        with pytest.raises(hq.HQError):
+            hq.decode_events(np.array([0, n], np.uint64), np.array([0, len(data)], np.uint64),
+                             data)
