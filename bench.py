@@ -1419,12 +1419,23 @@ def _latency(ts):
             "max": round(float(a.max()), 4), "n": len(a)}
 
 
+def _device_split(rs):
+    """One jobs step's device time split (ms) from its workers' outputs (hq_step_output): the
+    host's submit, the GPU's time between the step's timing events, the outputs' mapping, and the
+    rest of the wait (the waiting thread's wake-up and queueing ahead of the step's work)."""
+    r = max(rs, key=lambda x: x["pass_ns"])
+    rest = r["pass_ns"] - r["pack_ns"] - r["device_ns"] - r["apply_ns"]
+    return {"submit_ms": r["pack_ns"] / 1e6, "gpu_ms": r["device_ns"] / 1e6,
+            "outputs_ms": r["apply_ns"] / 1e6, "wait_rest_ms": rest / 1e6}
+
+
 def _phase_summary(ph):
     """The end-to-end steps' phases: medians, and the three slowest steps in full."""
     if not ph:
         return None
     keys = ("e2e_ms", "encode_max_ms", "execute_ms", "dev_ms", "enc_wall_ms", "enc_task_lag_max_ms",
-            "cgroup_throttled_ms")
+            "cgroup_throttled_ms", "exe_gpu_ms", "exe_wait_rest_ms", "dev_gpu_ms",
+            "dev_wait_rest_ms")
     med = {k: round(float(np.median([p[k] for p in ph])), 4) for k in keys
            if all(p.get(k) is not None for p in ph)}
     th = [p["cgroup_throttled_ms"] for p in ph if p.get("cgroup_throttled_ms") is not None]
@@ -1446,9 +1457,10 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
 
       device_only  the step's event stream already encoded in pinned memory (the producer's
                    encode outside the timed region);
-      end_to_end   the producer's encode inside: while the device takes step s, the W threads
-                   encode step s + 1's rows into the other pinned stream buffer
-                   (hq_events_encode_sized), and a step costs the longer of the two. The rows
+      end_to_end   the producer's encode inside: while the device takes step s, the producer
+                   encodes step s + 1's messages for all W workers into their other pinned
+                   stream buffers (one hq_events16_encode_sized_multi call on the encode
+                   threads), and a step costs the longer of the two. The rows
                    stand for the pb.Message values the reference's step worker holds
                    (execengine.go:923-1000 -> node.go:1257-1287); making them (the messages
                    arriving) is outside both timings.
@@ -1499,21 +1511,22 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                         mirror={k: CommitMirror(cids, g["committed"], bounds)
                                 for k in ("dev", "e2e")})
     pool = ThreadPoolExecutor(max(Ws) + 1)
-    # the encodes of a step run on at most enc_threads threads in all (W > enc_threads: queued)
-    enc_pool = ThreadPoolExecutor(enc_threads)
 
-    def encode(W, i, slot):
-        """Worker i's stream of the current step from the producer's compact records, on its
-        share of the encode threads, straight into its pinned receive buffer. Returns its wall
-        time (s)."""
+    def encode(W, slot):
+        """The W workers' streams of the current step from the producer's compact records, in
+        one call on the encode threads (hq_events16_encode_sized_multi: the threads split the
+        records of all workers evenly), each straight into its worker's pinned receive buffer.
+        Returns its wall time (s)."""
         t0 = time.perf_counter()
         mo = modes[W]
-        off, e0, e1 = mo["parts"][i]
-        out, sz = mo["bufs"][slot][i]
-        ne, nb = hq.encode_events16_sized_into(off, recs.recs[e0:e1], out, sz,
-                                               max(1, enc_threads // W))
-        assert ne == e1 - e0
-        mo["nbytes"][slot][i] = nb
+        jobs = []
+        for i in range(W):
+            off, e0, e1 = mo["parts"][i]
+            out, sz = mo["bufs"][slot][i]
+            jobs.append((off, recs.recs[e0:e1], out, sz))
+        for i, (ne, nb) in enumerate(hq.encode_events16_sized_multi(jobs, enc_threads)):
+            assert ne == mo["parts"][i][2] - mo["parts"][i][1]
+            mo["nbytes"][slot][i] = nb
         return time.perf_counter() - t0
 
     def timed_execute(j):
@@ -1538,8 +1551,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     rows.set(0)
     recs.set(0)
     for W in Ws:                       # step 0's streams (untimed)
-        for i in range(W):
-            encode(W, i, 0)
+        encode(W, 0)
     # the compact producer writes the bytes the rows encode to (step 0, one worker)
     want_data, want_sizes = hq.encode_events_sized(offsets, rows.ev)
     producer_equal = bool(np.array_equal(modes[1]["bufs"][0][0][0][:modes[1]["nbytes"][0][0]],
@@ -1575,20 +1587,23 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             j.execute()
             dt = time.perf_counter() - t0
             tq1 = cgroup_throttled_us()
-            mo["check"]["dev"].append(mo["mirror"]["dev"].step(j.results(copy=False)))
+            rs = j.results(copy=False)
+            dev_split = _device_split(rs)
+            mo["check"]["dev"].append(mo["mirror"]["dev"].step(rs))
             j = jobs(W, slot, "e2e")
             d.barrier()
             hq.encode_stats(reset=True)
             th0 = cgroup_throttled_us()
             t1 = time.perf_counter()
             fut = pool.submit(timed_execute, j)
-            encs = [enc_pool.submit(encode, W, i, 1 - slot) for i in range(W)]
-            enc_s = [f.result() for f in encs]
+            enc_s = [encode(W, 1 - slot)]      # (the producer's thread: this one)
             exe_s = fut.result()
             dt2 = time.perf_counter() - t1
             th1 = cgroup_throttled_us()
             es = hq.encode_stats(reset=True)
-            mo["check"]["e2e"].append(mo["mirror"]["e2e"].step(j.results(copy=False)))
+            rs = j.results(copy=False)
+            e2e_split = _device_split(rs)
+            mo["check"]["e2e"].append(mo["mirror"]["e2e"].step(rs))
             if s >= STEP_WARM:
                 mo["t"]["dev"].append(dt)
                 mo["t"]["e2e"].append(dt2)
@@ -1597,6 +1612,8 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                 mo["phases"].append({"step": s - STEP_WARM, "e2e_ms": dt2 * 1e3,
                                      "encode_max_ms": max(enc_s) * 1e3,
                                      "execute_ms": exe_s * 1e3, "dev_ms": dt * 1e3,
+                                     **{f"exe_{k}": v for k, v in e2e_split.items()},
+                                     **{f"dev_{k}": v for k, v in dev_split.items()},
                                      "dev_throttled_ms": (None if tq0 is None or tq1 is None
                                                           else (tq1 - tq0) / 1e3),
                                      "enc_wall_ms": es["wall_ns"] / 1e6 / max(1, es["calls"]),
@@ -1606,7 +1623,6 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         if s >= STEP_WARM:
             timed += 1
     pool.shutdown()
-    enc_pool.shutdown()
     committed = {}
     for W in Ws:
         for which in ("dev", "e2e"):
@@ -1662,10 +1678,10 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
         "modes_agree": same_modes,
         **({"modes_mismatch": mismatch} if mismatch else {}),
-        "producer": f"compact 16-byte message records (hq_event16) encoded by "
-                    f"hq_events16_encode_sized on {enc_threads} native threads per step "
-                    f"(max(1, {enc_threads} // W) per worker, at most {enc_threads} encodes at "
-                    f"once; the usable CPUs less two, capped by the cgroup quota)",
+        "producer": f"compact 16-byte message records (hq_event16), the W workers' streams "
+                    f"encoded by one hq_events16_encode_sized_multi call per step on "
+                    f"{enc_threads} native threads (the usable CPUs less two, capped by the "
+                    f"cgroup quota) splitting the records of all workers evenly",
         "producer_equal_rows": producer_equal,
         "note": "end_to_end: the producer's encode of step s + 1 overlapped with the device step "
                 "s; device_only: the encoded stream given",

@@ -51,6 +51,9 @@ struct hq_dstep_out {                 // the lists of one step, in input group o
     uint32_t input_error;             // HQ_E_INVAL: bit 1 unknown handle, 2 offsets, 4 boffsets,
                                       // 8 a group listed twice (no group state written)
     uint64_t kernel_ns, d2h_ns;       // wall time: H2D + pass A + scan + bases; pass B + D2H
+    uint64_t submit_ns;               // host time from the call to the last queued operation
+    uint64_t gpu_ns;                  // GPU time from the step's first queued operation on the
+                                      // compute stream to its last (HIP events; 0: not timed)
 };
 
 // one step's input: rows (events), an event stream (bytes + boffsets), or an event stream with

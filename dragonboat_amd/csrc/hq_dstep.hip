@@ -38,8 +38,12 @@ namespace {
 
 enum List { kCommits, kReady, kResps, kStates, kDropped, kDeferred, kFallback, kDecisions,
             kRerun, kLists };   // kRerun: 1 for a group with records other than its commit
-// the worker's input checks, taken by pass A (which writes no group state) before pass B runs
-enum InputError : uint32_t { kErrHandle = 1, kErrOffsets = 2, kErrBoffsets = 4, kErrTwice = 8 };
+// the worker's input checks, taken by pass A (which writes no group state) before pass B runs;
+// kErrScan: pass A's chained scan of the ReadyToRead places found a tile's word missing (an
+// internal fault, reported instead of waiting for ever)
+enum InputError : uint32_t { kErrHandle = 1, kErrOffsets = 2, kErrBoffsets = 4, kErrTwice = 8,
+                             kErrScan = 16 };
+constexpr uint32_t kTickets = 8;  // pass A launches per step (chunks) with their own ticket word
 
 struct StepK {
     hq_dgroup *groups;
@@ -96,6 +100,15 @@ struct StepK {
     const uint32_t *sizes_src;    // the caller's sizes when in pinned host memory (read over the
                                   //   link by k_size_sums, which writes `sizes`), else NULL
     uint64_t *bsum;
+    // pass A over a stream with the advance column speculated (spec_ready): the ReadyToRead
+    // records of the groups pass B does not replay go straight to their places in the host region
+    // (ready_off: the list's offset when the commits are the 4-byte column), each tile of 256
+    // groups finding its first place by a chained scan over `tiles` in start order (`tickets`,
+    // one word per pass A launch `chunk`; k_step_lite zeroes them)
+    uint32_t spec_ready, chunk;
+    uint64_t ready_off;
+    uint64_t *tiles;              // per tile: step_no << 32 | chunk << 29 | inclusive << 28 | count
+    uint32_t *tickets;            // [kTickets]
 };
 
 struct PackSize {                 // group i's size word -> events << 32 | bytes; i = n: 0 (the
@@ -240,6 +253,31 @@ __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
 // WRITE = true: the same sequence writing records and, at the end, the new state.
 constexpr uint32_t kStageReady = 64;   // ReadyToRead records staged per wave in pass B
 constexpr uint32_t kStageBytes = 16384;  // pass A: a workgroup's stream bytes staged in LDS
+
+// pass A's chained scan of the ReadyToRead places (StepK::tiles): a tile publishes its count
+// (aggregate) and then its inclusive prefix, tagged with the step and the launch's chunk so that
+// words of earlier launches and steps are never taken for this one's
+constexpr uint32_t kTileVal = (1u << 28) - 1;
+constexpr uint32_t kSpinMax = 1u << 22;   // ~0.1 s of polling before kErrScan
+__device__ __forceinline__ uint64_t tile_word(uint32_t step, uint32_t chunk, bool incl, uint32_t v) {
+    return (uint64_t)step << 32 | (uint64_t)(chunk & 7) << 29 | (uint64_t)incl << 28 | (v & kTileVal);
+}
+__device__ __forceinline__ uint64_t tile_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tile_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A workgroup's place in its launch: a ticket drawn at its start, so that a tile's predecessor in
+// the chained scan has always started before it (resident or done: no wait on a workgroup not yet
+// dispatched)
+__device__ __forceinline__ uint32_t draw_ticket(uint32_t *ctr) {
+    __shared__ uint32_t t;
+    if (threadIdx.x == 0) t = atomicAdd(ctr, 1u);
+    __syncthreads();
+    return t;
+}
 
 template <bool WRITE, int MC>   // MC: member slots held in registers (8 or MC)
 struct Engine {
@@ -609,8 +647,125 @@ struct Engine {
 #else
 #define HQ_STEP_OCC
 #endif
+// Pass A over a stream, the advance column speculated (StepK::spec_ready): the ReadyToRead records
+// of the tile's groups that pass B does not replay (one record, kept in ready_slot), written at
+// their final places in the host region during pass A — their PCIe writes then overlap the step's
+// input reads instead of following pass A as k_step_lite's. A record's place is the count of
+// records of the groups before it in input order: the tile's first place comes from a chained
+// scan over the launch's tiles in start order (a tile publishes its count, looks back over its
+// predecessors' words until an inclusive one, publishes its own inclusive prefix); the launch's
+// first tile takes the inclusive prefix an earlier launch of the step left in the tile of the
+// group before its first (0 for group 0). The records are staged in LDS at their places (the
+// holes, the places of groups pass B replays, are written by pass B afterwards) and stored as
+// one contiguous run of 16-byte stores. All threads of the workgroup call this.
+__device__ void ready_tail(const StepK &a, uint64_t tile, uint32_t chunk, bool member, bool first,
+                          uint64_t i, uint32_t cnt, bool one, uint4 *sbuf) {
+    __shared__ uint32_t s_w[256 / 64], s_excl, s_any, s_first, s_ok;
+    __shared__ unsigned long long s_first_i;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        s_any = 0;
+        s_first = 0;
+    }
+    uint32_t x = cnt;             // inclusive scan over the wave's lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= d ? y : 0u;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();              // (also: every thread is done with the staged bytes in sbuf)
+    if (member) s_any = 1;
+    if (first) {                  // (one group of the launch is its first)
+        s_first = 1;
+        s_first_i = i;
+    }
+    uint32_t before = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < 256 / 64; ++w) {
+        before += w < wv ? s_w[w] : 0u;
+        agg += s_w[w];
+    }
+    __syncthreads();
+    if (!s_any) return;           // no group of this launch: no tile waits for this one
+    if (wv == 0) {                // the first wave looks back, 64 tiles per round trip
+        const uint32_t step = a.step_no;
+        uint32_t excl = 0;
+        bool ok = true;
+        if (s_first) {
+            if (s_first_i > 0) {  // written by an earlier launch of this step
+                const uint64_t w = tile_load(a.tiles + (s_first_i - 1) / 256);
+                ok = (uint32_t)(w >> 32) == step && ((w >> 28) & 1) &&
+                     (uint32_t)((w >> 29) & 7) < chunk;
+                excl = (uint32_t)w & kTileVal;
+            }
+        } else if (tile == 0) {
+            ok = false;
+        } else {
+            if (lane == 0) tile_store(a.tiles + tile, tile_word(step, chunk, false, agg));
+            // lane k reads tile hi - k; a window is taken once every tile up to the nearest
+            // inclusive word (or all 64) has published for this launch
+            int64_t hi = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t p = hi - lane;
+                const uint64_t w = p >= 0 ? tile_load(a.tiles + p) : 0;
+                const bool ready = p >= 0 && (uint32_t)(w >> 32) == step &&
+                                   (uint32_t)((w >> 29) & 7) == (chunk & 7);
+                const uint64_t rdy = __ballot(ready), inc = __ballot(ready && ((w >> 28) & 1));
+                const uint64_t need = inc ? (inc & (0 - inc)) * 2 - 1 : ~0ull;   // lanes 0 .. k
+                if ((rdy & need) == need) {
+                    uint32_t v = (lane < 64 - __clzll((long long)need) || !inc) && ready
+                                     ? (uint32_t)w & kTileVal : 0u;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+                    excl += v;
+                    if (inc) break;
+                    hi -= 64;
+                    if (hi < 0) {     // no inclusive word before: cannot be
+                        ok = false;
+                        break;
+                    }
+                    continue;
+                }
+                if (++spins > kSpinMax) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (lane == 0) {
+            if (!ok) atomicOr(a.error, (uint32_t)kErrScan);
+            tile_store(a.tiles + tile, tile_word(step, chunk, true, excl + agg));
+            s_excl = excl;
+            s_ok = ok;
+        }
+    }
+    __syncthreads();
+    const uint32_t lo = s_excl;
+    // (a region too small: the layout reports the overflow and the regrown step's k_step_lite
+    // writes every record)
+    if (!s_ok || agg == 0 || a.ready_off + (uint64_t)(lo + agg) * sizeof(hq_ready_to_read) > a.out_cap)
+        return;
+    constexpr uint32_t kCap = kStageBytes / sizeof(hq_ready_to_read);
+    hq_ready_to_read *stage = reinterpret_cast<hq_ready_to_read *>(sbuf);
+    hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.ready_off) + lo;
+    const uint32_t pos = before + x - cnt;   // the tile's records before this group's
+    if (one) {
+        const hq_ready_to_read r = a.ready_slot[i];
+        if (pos < kCap) stage[pos] = r;
+        else dst[pos] = r;
+    }
+    __syncthreads();
+    const uint32_t nq = 2 * min(agg, kCap);
+    const uint4 *src = reinterpret_cast<const uint4 *>(stage);
+    uint4 *out = reinterpret_cast<uint4 *>(dst);
+    for (uint32_t q = threadIdx.x; q < nq; q += 256) out[q] = src[q];
+}
+
 template <bool WRITE, bool STREAM, int MC>
-__device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
+__device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32_t chunk = 0) {
     // pass A: the wave's counts summed in LDS, added to wsum by one lane (i_begin is a multiple
     // of 64: the wave's groups are one wave of the scan)
     __shared__ uint32_t wtot[WRITE ? 1 : 256 / 64][kLists];
@@ -652,6 +807,9 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
         }
     }
     if (!STAGE && !act) return;
+    // (pass A over a stream: a group of this launch, input errors or not, and the launch's first)
+    const bool member = act;
+    const bool first = member && (a.prefix ? i == 0 || b0 < a.own_lo : i == a.i_begin);
     const uint32_t h = !act ? 0u : a.handles ? a.handles[i] : (uint32_t)i;   // NULL: 0 .. n - 1
     if (!WRITE && act) {          // validate this group's entry; a bad one is not stepped
         uint32_t err = 0;
@@ -675,9 +833,9 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
     // buffer is read in place. The aligned 16-byte blocks around the range never leave the
     // pages of its bytes.
     const uint8_t *src0 = a.bytes + b0;
+    __shared__ uint4 sbuf[STAGE ? kStageBytes / 16 : 1];
     if constexpr (STAGE) {
         __shared__ unsigned long long s_lo, s_hi;
-        __shared__ uint4 sbuf[kStageBytes / 16];
         if (threadIdx.x == 0) {
             s_lo = ~0ull;
             s_hi = 0;
@@ -706,65 +864,82 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk) {
             }
         }
         __syncthreads();
-        if (!act) return;
-        if (fits) src0 = reinterpret_cast<const uint8_t *>(sbuf) + (base + b0 - lo);
+        if (act && fits) src0 = reinterpret_cast<const uint8_t *>(sbuf) + (base + b0 - lo);
     }
-    hq_dread reads[kDReads];
-    Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
-    if (!WRITE) eng.save_old(h);
-    __shared__ hq_ready_to_read stage[WRITE ? 256 / 64 : 1][WRITE ? kStageReady : 1];
-    // list mode: the wave's groups are consecutive and so are their records, staged from its
-    // first active lane's on; column mode: the groups replayed are a sparse subset whose records
-    // lie between k_step_lite's, so each is stored where it goes
-    const bool staged = WRITE && !a.layout->commit_column;
-    if (staged) {
-        eng.stage = stage[threadIdx.x >> 6];
-        eng.stage_lo = __builtin_amdgcn_readfirstlane(eng.base[kReady]);
-    }
-    if (STREAM)
-        eng.template run<true>(e0, e1, src0, src0 + (b1 - b0));
-    else
-        eng.template run<false>(e0, e1, nullptr, nullptr);
-    if (staged) {                 // the staged records out, 16 contiguous bytes per lane
-        const uint64_t act = __ballot(1);
-        const int last = 63 - __clzll((long long)act);
-        const uint32_t end = __shfl(eng.base[kReady] + eng.cnt[kReady], last);
-        const uint32_t nrec = min(end - eng.stage_lo, kStageReady);
-        const uint32_t rank = __popcll(act & ((1ull << (threadIdx.x & 63)) - 1));
-        const uint32_t nact = __popcll(act);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS stores landed
-        __builtin_amdgcn_wave_barrier();
-        const uint4 *src = reinterpret_cast<const uint4 *>(eng.stage);
-        uint4 *dst = reinterpret_cast<uint4 *>(eng.template list<hq_ready_to_read>(kReady) +
-                                               eng.stage_lo);
-        for (uint32_t q = rank; q < 2 * nrec; q += nact) dst[q] = src[q];
-    }
-    if (!WRITE) {                 // the new state in place (pass B replays from the saved one)
-        const bool others = (eng.cnt[kResps] | eng.cnt[kStates] | eng.cnt[kDropped] |
-                             eng.cnt[kDeferred] | eng.cnt[kFallback]) != 0;
-        const bool rerun = others || eng.cnt[kReady] > 1;
-        const bool one_ready = !rerun && eng.cnt[kReady] == 1;
-        eng.cnt[kRerun] = rerun;
-        for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
-        a.rerun[i] = (uint8_t)(2 | rerun | (one_ready ? 4 : 0));
-        eng.store(h);
-        uint32_t *wt = wtot[threadIdx.x >> 6];   // (the lanes that left early add nothing)
-        for (int l = 0; l < kLists; ++l)
-            if (eng.cnt[l]) atomicAdd(wt + l, eng.cnt[l]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
-            for (int l = 0; l < kLists; ++l) {
-                const uint32_t v = wt[l];
-                if (v) atomicAdd(a.wsum + (uint64_t)l * a.nw + (i >> 6), v);
+    uint32_t n_ready = 0;
+    bool one_ready = false;
+    if (act) {
+        hq_dread reads[kDReads];
+        Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
+        if (!WRITE) eng.save_old(h);
+        __shared__ hq_ready_to_read stage[WRITE ? 256 / 64 : 1][WRITE ? kStageReady : 1];
+        // list mode: the wave's groups are consecutive and so are their records, staged from its
+        // first active lane's on; column mode: the groups replayed are a sparse subset whose records
+        // lie between k_step_lite's, so each is stored where it goes
+        const bool staged = WRITE && !a.layout->commit_column;
+        if (staged) {
+            eng.stage = stage[threadIdx.x >> 6];
+            eng.stage_lo = __builtin_amdgcn_readfirstlane(eng.base[kReady]);
+        }
+        if (STREAM)
+            eng.template run<true>(e0, e1, src0, src0 + (b1 - b0));
+        else
+            eng.template run<false>(e0, e1, nullptr, nullptr);
+        if (staged) {                 // the staged records out, 16 contiguous bytes per lane
+            const uint64_t act = __ballot(1);
+            const int last = 63 - __clzll((long long)act);
+            const uint32_t end = __shfl(eng.base[kReady] + eng.cnt[kReady], last);
+            const uint32_t nrec = min(end - eng.stage_lo, kStageReady);
+            const uint32_t rank = __popcll(act & ((1ull << (threadIdx.x & 63)) - 1));
+            const uint32_t nact = __popcll(act);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS stores landed
+            __builtin_amdgcn_wave_barrier();
+            const uint4 *src = reinterpret_cast<const uint4 *>(eng.stage);
+            uint4 *dst = reinterpret_cast<uint4 *>(eng.template list<hq_ready_to_read>(kReady) +
+                                                   eng.stage_lo);
+            for (uint32_t q = rank; q < 2 * nrec; q += nact) dst[q] = src[q];
+        }
+        if (!WRITE) {                 // the new state in place (pass B replays from the saved one)
+            const bool others = (eng.cnt[kResps] | eng.cnt[kStates] | eng.cnt[kDropped] |
+                                 eng.cnt[kDeferred] | eng.cnt[kFallback]) != 0;
+            const bool rerun = others || eng.cnt[kReady] > 1;
+            one_ready = !rerun && eng.cnt[kReady] == 1;
+            n_ready = eng.cnt[kReady];
+            eng.cnt[kRerun] = rerun;
+            for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
+            a.rerun[i] = (uint8_t)(2 | rerun | (one_ready ? 4 : 0));
+            eng.store(h);
+            uint32_t *wt = wtot[threadIdx.x >> 6];   // (the lanes that left early add nothing)
+            for (int l = 0; l < kLists; ++l)
+                if (eng.cnt[l]) atomicAdd(wt + l, eng.cnt[l]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+                for (int l = 0; l < kLists; ++l) {
+                    const uint32_t v = wt[l];
+                    if (v) atomicAdd(a.wsum + (uint64_t)l * a.nw + (i >> 6), v);
+                }
             }
         }
+    }
+    if constexpr (STAGE) {
+        if (a.spec_ready)
+            ready_tail(a, (a.i_begin >> 8) + blk, chunk, member, first, i, n_ready, one_ready, sbuf);
     }
 }
 
 template <bool WRITE, bool STREAM, int MC>
 __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
-    step_groups<WRITE, STREAM, MC>(a, blockIdx.x);
+    if constexpr (!WRITE && STREAM) {   // tiles in start order (ready_tail's chained scan)
+        const uint32_t b = draw_ticket(a.tickets + a.chunk);
+        if (b >= gridDim.x) {     // tickets not zeroed: report, step nothing
+            if (threadIdx.x == 0) atomicOr(a.error, (uint32_t)kErrScan);
+            return;
+        }
+        step_groups<WRITE, STREAM, MC>(a, b, a.chunk);
+    } else {
+        step_groups<WRITE, STREAM, MC>(a, blockIdx.x);
+    }
 }
 
 // The jobs path: one launch over several workers' steps, each job's groups in consecutive
@@ -774,6 +949,8 @@ struct JobMap {
     const StepK *ks;              // the jobs' StepK, job0 .. job0 + count - 1 in this launch
     uint32_t job0, count;
     uint32_t blk0[kMaxJobs + 1];  // relative to job0
+    uint32_t *tickets;            // pass A: the launch's ticket word is tickets[chunk]; k_step_lite_jobs
+    uint32_t chunk;               //   zeroes them
 };
 
 __device__ __forceinline__ uint32_t job_of(const JobMap &m, uint32_t b) {
@@ -784,15 +961,24 @@ __device__ __forceinline__ uint32_t job_of(const JobMap &m, uint32_t b) {
 
 template <bool WRITE, bool STREAM, int MC>
 __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step_jobs(const JobMap m) {
-    const uint32_t j = job_of(m, blockIdx.x);
-    step_groups<WRITE, STREAM, MC>(m.ks[m.job0 + j], blockIdx.x - m.blk0[j]);
+    uint32_t b = blockIdx.x;
+    if constexpr (!WRITE && STREAM) {
+        b = draw_ticket(m.tickets + m.chunk);
+        if (b >= gridDim.x) {
+            if (threadIdx.x == 0) atomicOr(m.ks[m.job0].error, (uint32_t)kErrScan);
+            return;
+        }
+    }
+    const uint32_t j = job_of(m, b);
+    step_groups<WRITE, STREAM, MC>(m.ks[m.job0 + j], b - m.blk0[j], m.chunk);
 }
 
 // Between the layout and pass B: with the commits as a column, every listed group's word from
 // the committed index pass A saved and the one it wrote (the advance, or the new index), and the
 // positions of the groups with other records packed in order for pass B; in list mode nothing
-__device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk) {
+__device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk, uint32_t *tickets) {
     const uint64_t i = blk * 256 + threadIdx.x;
+    if (tickets && threadIdx.x < kTickets) tickets[threadIdx.x] = 0;   // (pass A's are done)
     if (i < a.ws) a.wsum[i] = 0;  // (scanned already; the grid covers ws: 9 n / 64 + 10 <= max(n, 256))
     const bool in = i < a.n;
     if ((a.layout->error | a.layout->overflow) || !__ballot(in)) return;   // (whole waves)
@@ -824,7 +1010,7 @@ __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk) {
     // groups are), staged in LDS at their places and stored as one contiguous run of 16-byte
     // lane stores; the places of the replayed groups' records are holes pass B fills afterwards
     __shared__ hq_ready_to_read stage[256 / 64][kStageReady];
-    {
+    if (!(col32 && a.spec_valid && a.spec_ready)) {   // (else pass A wrote them: ready_tail)
         constexpr uint64_t l = kReady;
         const uint64_t w = i >> 6;
         const uint32_t lo = a.scan[l * a.nw + w] - a.scan[l * a.nw];
@@ -859,11 +1045,13 @@ __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_step_lite(const StepK a) { lite_groups(a, blockIdx.x); }
+__global__ __launch_bounds__(256) void k_step_lite(const StepK a) {
+    lite_groups(a, blockIdx.x, blockIdx.x == 0 ? a.tickets : nullptr);
+}
 
 __global__ __launch_bounds__(256) void k_step_lite_jobs(const JobMap m) {
     const uint32_t j = job_of(m, blockIdx.x);
-    lite_groups(m.ks[m.job0 + j], blockIdx.x - m.blk0[j]);
+    lite_groups(m.ks[m.job0 + j], blockIdx.x - m.blk0[j], blockIdx.x == 0 ? m.tickets : nullptr);
 }
 
 // A step with an input error writes no group state: the groups pass A stepped get back the
@@ -894,6 +1082,7 @@ __global__ __launch_bounds__(256) void k_step_restore(const StepK a) {
 constexpr int kMaxChunks = HQ_STEP_CHUNKS;
 constexpr int kMaxJobChunks = 8;   // the jobs path's chunks of whole jobs (events per copy stream)
 static_assert(kMaxChunks <= kMaxJobChunks, "the chunk events serve both paths");
+static_assert(kMaxJobChunks <= kTickets, "a ticket word per pass A launch");
 constexpr uint64_t kChunkGroups = 65536;
 // bnd[l] = the scan at l * nw (list l's first record), l = 0 .. kLists
 __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, uint64_t cap,
@@ -1156,9 +1345,18 @@ struct hq_dstep {
     hipStream_t copy2 = nullptr;
     hipEvent_t ev_in2[kMaxJobChunks] = {};
     hipEvent_t ev_sync = nullptr;  // blocking-sync event: a waiting worker thread sleeps
+    // timing events around a step's device work (hq_dstep_out::gpu_ns): the host's wait for a
+    // step, less the GPU's time, is its wake-up and queueing delay
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
     // the jobs path (hq_dstep_run_jobs, this engine first): the jobs' StepK, pinned and on device
     StepK *jobs_host = nullptr, *jobs_dev = nullptr;
     uint32_t jobs_cap = 0;
+    // pass A's ticket words (StepK::tickets), zeroed by k_step_lite; a step that stopped before
+    // it leaves them to clear (dirty), and pass A's chained-scan words per tile of 256 groups
+    uint32_t *tickets = nullptr;
+    bool tickets_dirty = false;
+    uint64_t *tiles = nullptr;
+    size_t tiles_cap = 0;         // (bytes)
 };
 
 namespace {
@@ -1213,6 +1411,8 @@ int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming |
                                                                           hipEventBlockingSync),
                            "event");
+    for (hipEvent_t *e : {&d->ev_t0, &d->ev_t1})
+        if (!rc) rc = hq::check_hip(ctx, hipEventCreate(e), "event");
     for (int c = 0; c < kMaxJobChunks && !rc; ++c) {
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_in[c], hipEventDisableTiming), "event");
         if (!rc)
@@ -1220,6 +1420,8 @@ int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
                                "event");
     }
     if (!rc) rc = hq::check_hip(ctx, hipMalloc(&d->layout, sizeof(Layout)), "hq_dstep layout");
+    if (!rc) rc = hq::check_hip(ctx, hipMalloc(&d->tickets, kTickets * 4), "hq_dstep tickets");
+    if (!rc) rc = hq::check_hip(ctx, hipMemset(d->tickets, 0, kTickets * 4), "hq_dstep tickets");
     if (!rc)
         rc = hq::check_hip(ctx, hipHostMalloc(&d->host_layout, sizeof(Layout), hipHostMallocDefault),
                            "hq_dstep layout");
@@ -1238,7 +1440,8 @@ void hq_dstep_close(hq_dstep *d) {
                     (void *)d->counts, (void *)d->scan, (void *)d->bases, d->scan_tmp,
                     (void *)d->layout, (void *)d->groups_old, (void *)d->reads_old,
                     (void *)d->match_old, (void *)d->rerun, (void *)d->ready_slot,
-                    (void *)d->rerun_list, (void *)d->wsum, (void *)d->jobs_dev})
+                    (void *)d->rerun_list, (void *)d->wsum, (void *)d->jobs_dev,
+                    (void *)d->tickets, (void *)d->tiles})
         if (p) (void)hipFree(p);
     if (d->host_out) (void)hipHostFree(d->host_out);
     if (d->jobs_host) (void)hipHostFree(d->jobs_host);
@@ -1249,7 +1452,8 @@ void hq_dstep_close(hq_dstep *d) {
             (void)hipStreamDestroy(cs);
         }
     }
-    if (d->ev_sync) (void)hipEventDestroy(d->ev_sync);
+    for (hipEvent_t e : {d->ev_sync, d->ev_t0, d->ev_t1})
+        if (e) (void)hipEventDestroy(e);
     for (int c = 0; c < kMaxJobChunks; ++c) {
         if (d->ev_in[c]) (void)hipEventDestroy(d->ev_in[c]);
         if (d->ev_in2[c]) (void)hipEventDestroy(d->ev_in2[c]);
@@ -1345,9 +1549,29 @@ struct Run {
     int chunks = 1;
     bool stream = false, sized = false, small = false, small_scan = false;
     bool stepped = false, first = true;
-    uint64_t t0 = 0, t1 = 0;
+    bool timing = false;          // ev_t0 recorded: pass B records ev_t1 before its wait
+    uint64_t t0 = 0, t1 = 0, t_sub = 0, gpu_ns = 0;
     int rc = HQ_OK;
 };
+
+// GPU time between two completed events (0 if it cannot be read)
+uint64_t elapsed_ns(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return (uint64_t)((double)ms * 1e6);
+}
+
+// HQ_STEP_SPEC_READY=0 in the environment: pass A leaves the ReadyToReads to k_step_lite (A/B)
+bool spec_ready_allowed() {
+    static const bool on = [] {
+        const char *v = std::getenv("HQ_STEP_SPEC_READY");
+        return !v || std::atoi(v) != 0;
+    }();
+    return on;
+}
 
 // The step's buffers (grown as needed) and its StepK, with the memsets it needs queued on s; no
 // launch. in->n > 0.
@@ -1394,6 +1618,13 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
             if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 8, s), "memset");
         }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
+    }
+    // pass A's chained-scan words: zeroed when allocated (their tags then never match a step)
+    const size_t tiles_bytes = ((n + 255) / 256 + 1) * 8;
+    if (!rc && tiles_bytes > d->tiles_cap) {
+        rc = grow(ctx, reinterpret_cast<void **>(&d->tiles), &d->tiles_cap, tiles_bytes, false,
+                  "hq_dstep tiles");
+        if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->tiles, 0, d->tiles_cap, s), "memset");
     }
     if (!rc && ws * 4 > d->wsum_cap) {
         rc = grow(ctx, reinterpret_cast<void **>(&d->wsum), &d->wsum_cap, ws * 4, false,
@@ -1496,6 +1727,16 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
     // offset 0 is the commits list's in every layout)
     k.spec_col = (d->commit_column & kColumn32) && n * 4 <= d->host_out_cap;
     k.spec_valid = k.spec_col;
+    // pass A writes the single ReadyToReads at their places too (ready_tail): stream input, the
+    // column speculated, the counts within a tile word (HQ_STEP_SPEC_READY=0: k_step_lite, A/B)
+    // (not the jobs path: there pass A reads the streams over the link in place, and these
+    // writes beside its reads slowed it by more than k_step_lite's copy takes, 981 vs 693 + 158
+    // us for the 16-worker step5, profiles/r05e)
+    k.spec_ready = !jobs && stream && k.spec_col && ne < kTileVal && spec_ready_allowed();
+    k.ready_off = (n * 4 + 255) & ~uint64_t(255);   // layout_from's offset of the list after the column
+    k.tiles = d->tiles;
+    k.tickets = d->tickets;
+    k.chunk = 0;
     k.reads_old = d->reads_old;
     k.rerun = d->rerun;
     k.rerun_list = d->rerun_list;
@@ -1555,10 +1796,16 @@ void pass_b(Run &r) {
     if (!r.rc) {
         hipLaunchKernelGGL(k_step_lite, grid, blk, 0, ctx->stream, k);
         r.rc = hq::check_hip(ctx, hipGetLastError(), "k_step_lite");
-        if (!r.rc) d->wsum_dirty = false;
+        if (!r.rc) d->wsum_dirty = d->tickets_dirty = false;
     }
     launch_pass(r, true, 0, r.n);
+    if (!r.rc && r.timing) {
+        r.rc = hq::check_hip(ctx, hipEventRecord(d->ev_t1, ctx->stream), "event");
+        r.t_sub = now_ns();
+    }
     if (!r.rc) r.rc = wait_stream(d, ctx->stream, "hq_dstep sync");
+    if (!r.rc && r.timing) r.gpu_ns = elapsed_ns(d->ev_t0, d->ev_t1);
+    r.timing = false;             // (a second pass B, after the output region grew: untimed)
 }
 
 // Pass A has written every listed group's new state in place (the state it found is saved).
@@ -1590,6 +1837,15 @@ const T *pinned_on_device(const T *p) {
     const char *hp = static_cast<const char *>(at.hostPointer ? at.hostPointer : (const void *)p);
     return reinterpret_cast<const T *>(static_cast<const char *>(at.devicePointer) +
                                        (reinterpret_cast<const char *>(p) - hp));
+}
+
+// HQ_STEP_SINGLE_JOBS=0 in the environment: a single pinned sized step takes the copy path (A/B)
+bool single_as_job_allowed() {
+    static const bool on = [] {
+        const char *v = std::getenv("HQ_STEP_SINGLE_JOBS");
+        return !v || std::atoi(v) != 0;
+    }();
+    return on;
 }
 
 // HQ_STEP_ZERO_COPY=0 in the environment: pinned streams are copied like pageable ones (A/B)
@@ -1660,6 +1916,8 @@ int finish(Run &r) {
     out->decisions = lay.len[kDecisions];
     out->kernel_ns = r.t1 - r.t0;
     out->d2h_ns = now_ns() - r.t1;
+    out->submit_ns = r.t_sub > r.t0 ? r.t_sub - r.t0 : 0;
+    out->gpu_ns = r.gpu_ns;
     return HQ_OK;
 }
 
@@ -1668,9 +1926,15 @@ int finish(Run &r) {
 int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     *out = hq_dstep_out{};
     if (in->n == 0) return HQ_OK;
-    // (a single step copies its stream in chunks even from pinned memory: the copy engine moves
-    // ~55 GB/s where pass A reading in place over the link reached 45, 1.22 vs 1.35 ms for the
-    // 1 M-group step5; the jobs path reads in place, which spares its per-job copies)
+    // A sized stream in pinned memory takes the jobs path as one job: pass A reads it in place in
+    // one launch (the stream staged through LDS), where this path's chunked copies put the
+    // first chunk's copy ahead of pass A and the last chunk's pass A behind the copies
+    // (HQ_STEP_SINGLE_JOBS=0: this path, A/B)
+    if (in->sizes && in->bytes && single_as_job_allowed() && pinned_on_device(in->bytes)) {
+        int rc1 = HQ_OK;
+        const int rc = hq_dstep_run_jobs(&d, in, out, &rc1, 1);
+        return rc1 ? rc1 : rc;
+    }
     Run r;
     r.d = d;
     r.in = in;
@@ -1678,12 +1942,19 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     hq_ctx *ctx = d->ctx;
     int rc = prepare(r, ctx->stream);
     if (rc) return rc;
+    rc = hq::check_hip(ctx, hipEventRecord(d->ev_t0, ctx->stream), "event");
+    if (!rc && d->tickets_dirty)
+        rc = hq::check_hip(ctx, hipMemsetAsync(d->tickets, 0, kTickets * 4, ctx->stream), "memset");
+    if (rc) return rc;
+    d->tickets_dirty = true;
+    r.timing = true;
     const uint64_t n = r.n, ne = r.ne, nb = r.nb;
     const bool stream = r.stream, sized = r.sized;
     const int chunks = r.chunks;
     uint64_t bound[kMaxChunks + 1];
-    for (int c = 0; c <= chunks; ++c)   // (multiples of 64 inside: pass A's waves are the scan's)
-        bound[c] = c == chunks ? n : (n * c / chunks) & ~uint64_t(63);
+    // (multiples of 256 inside: pass A's waves are the scan's, its tiles ready_tail's)
+    for (int c = 0; c <= chunks; ++c)
+        bound[c] = c == chunks ? n : (n * c / chunks) & ~uint64_t(255);
     if (chunks > 1 && !d->copy)       // the copy stream of the first chunked step
         rc = hq::check_hip(ctx, hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking),
                            "hq_dstep copy stream");
@@ -1726,6 +1997,7 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
                 r.rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
             r.k.own_lo = c == 0 ? 0 : lo + 1;
             r.k.own_hi = c + 1 == chunks ? UINT64_MAX : hi + 1;
+            r.k.chunk = (uint32_t)c;
             launch_pass(r, false, 0, n);
         }
         rc = r.rc;
@@ -1751,11 +2023,13 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
             if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(ctx->stream, d->ev_in[c], 0), "wait");
         }
         r.rc = rc;
+        r.k.chunk = (uint32_t)c;
         launch_pass(r, false, i0, i1);
         rc = r.rc;
     }
     r.k.own_lo = 0;
     r.k.own_hi = UINT64_MAX;
+    r.k.chunk = 0;
     // the wave sums' scan (hipcub for a large step; a small one's is the layout's workgroup)
     if (!rc && !r.small_scan)
         rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(d->scan_tmp, r.tmp, d->wsum,
@@ -1805,6 +2079,10 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     }
     if (!nl) return rc;
     tp[1] = now_ns();
+    if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_t0, s), "event");
+    if (!rc && d0->tickets_dirty)
+        rc = hq::check_hip(ctx, hipMemsetAsync(d0->tickets, 0, kTickets * 4, s), "memset");
+    d0->tickets_dirty = true;
     // the jobs' StepK, pinned and copied to the device ahead of the launches
     if (!rc && nl > d0->jobs_cap) {
         if (d0->jobs_host) (void)hipHostFree(d0->jobs_host);
@@ -1842,6 +2120,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         m.ks = d0->jobs_dev;
         m.job0 = x0;
         m.count = x1 - x0;
+        m.tickets = d0->tickets;
         m.blk0[0] = 0;
         for (uint32_t x = x0; x < x1; ++x)
             m.blk0[x - x0 + 1] = m.blk0[x - x0] + (uint32_t)((runs[live[x]].n + extra + per - 1) / per);
@@ -1939,7 +2218,8 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
             rc = hq::check_hip(ctx, hipStreamWaitEvent(s, d0->ev_in[c], 0), "wait");
             if (!rc) rc = hq::check_hip(ctx, hipStreamWaitEvent(s, d0->ev_in2[c], 0), "wait");
         }
-        const JobMap m = map(x0, x1, 256, 0);
+        JobMap m = map(x0, x1, 256, 0);
+        m.chunk = (uint32_t)c;
         if (!rc) rc = hq::pre_launch(ctx);
         if (!rc) {
             if (small) hipLaunchKernelGGL((k_step_jobs<false, true, 8>), dim3(m.blk0[x1 - x0]),
@@ -1951,9 +2231,29 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         }
         copies(c + 2);
     }
-    // every job's layout (one workgroup each), k_step_lite and pass B over all jobs, one wait
+    // every job's layout (one workgroup each), k_step_lite and pass B over all jobs, one wait;
+    // one large job (a single worker's step) scans its wave sums with hipcub, whose two launches
+    // take ~14 us where the one workgroup took 117 for 1 M groups (147 Ki sums, profiles/r05e)
     const JobMap am = map(0, nl, 256, 0);
-    if (!rc) {
+    Run &r0 = runs[live[0]];
+    hq_dstep *dj = r0.d;          // (the one job's engine: not d0 when job 0 listed no group)
+    if (!rc && nl == 1 && !r0.small_scan) {
+        size_t tmp = 0;
+        rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, dj->wsum, dj->scan,
+                                                                  r0.ws, s), "hipcub scan size");
+        // (scan_tmp holds the sizes' block totals, done with once pass A has its prefixes)
+        if (!rc) rc = grow(ctx, &dj->scan_tmp, &dj->scan_tmp_cap, tmp, false, "hq_dstep scan tmp");
+        if (!rc)
+            rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(dj->scan_tmp, tmp, dj->wsum,
+                                                                      dj->scan, r0.ws, s),
+                               "hipcub scan");
+        if (!rc) {
+            hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, s, dj->scan, r0.n, r0.nw, r0.k.error,
+                               (uint64_t)dj->host_out_cap, (uint32_t)dj->commit_column, dj->layout,
+                               dj->host_layout);
+            launched("k_layout");
+        }
+    } else if (!rc) {
         hipLaunchKernelGGL(k_scan_layout_jobs, dim3(nl), dim3(kScanT), 0, s, d0->jobs_dev);
         launched("k_scan_layout_jobs");
     }
@@ -1961,6 +2261,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         hipLaunchKernelGGL(k_step_lite_jobs, dim3(am.blk0[nl]), dim3(256), 0, s, am);
         launched("k_step_lite_jobs");
         for (uint32_t x = 0; x < nl && !rc; ++x) runs[live[x]].d->wsum_dirty = false;
+        if (!rc) d0->tickets_dirty = false;
     }
     if (!rc) rc = hq::pre_launch(ctx);
     if (!rc) {
@@ -1970,9 +2271,12 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                                 dim3(256), 0, s, am);
         rc = hq::post_launch(ctx, "k_step_jobs<write>");
     }
+    if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_t1, s), "event");
     tp[3] = now_ns();
+    uint64_t gpu_ns = 0;
     if (!rc) {
         rc = wait_stream(d0, s, "hq_dstep jobs sync");
+        if (!rc) gpu_ns = elapsed_ns(d0->ev_t0, d0->ev_t1);
     } else {                      // (a failed launch sequence leaves no copy behind either)
         (void)hipStreamSynchronize(s);
         for (hipStream_t cs : {d0->copy, d0->copy2})
@@ -1985,6 +2289,8 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         r.rc = rc;                // (restore: only the jobs whose pass A was launched)
         r.first = false;
         r.t1 = t1;
+        r.t_sub = tp[3];
+        r.gpu_ns = gpu_ns;
         rcs[live[x]] = finish(r);
         if (rcs[live[x]] && !first_rc) first_rc = rcs[live[x]];
     }

@@ -595,6 +595,132 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     return rc;
 }
 
+int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32_t threads) {
+    if (count && !jobs) return HQ_E_INVAL;
+    // each job checked as its own call would; the records of the valid ones laid end to end
+    std::vector<uint64_t> rec0(count + 1, 0);
+    std::vector<uint32_t> live;
+    int first = HQ_OK;
+    for (uint32_t j = 0; j < count; ++j) {
+        hq_encode16_job &b = jobs[j];
+        b.n_events = b.n_bytes = 0;
+        b.rc = HQ_OK;
+        const uint64_t n = b.n_groups;
+        if (!b.offsets16 || (n && !b.sizes) || (n && b.offsets16[n] > b.offsets16[0] && !b.recs))
+            b.rc = HQ_E_INVAL;
+        else if (n && b.offsets16[n] > b.offsets16[0] && !b.out)
+            b.rc = HQ_E_STATE;
+        else if (n && b.offsets16[n] < b.offsets16[0])
+            b.rc = HQ_E_INVAL;
+        rec0[j + 1] = rec0[j] + (b.rc || !n ? 0 : b.offsets16[n] - b.offsets16[0]);
+        if (!b.rc && n) live.push_back(j);
+        if (b.rc && !first) first = b.rc;
+    }
+    const uint64_t R = rec0[count];
+    const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(threads, 1u), std::max<uint64_t>(1, R / 4096));
+    if (live.empty()) return first;
+    const uint64_t c0 = now_ns();
+    // job j's groups split at the global record cuts R t / T (group boundaries): range t of the
+    // job is groups [gc[j][t], gc[j][t + 1]), empty unless the job's records meet cut range t
+    std::vector<std::vector<uint64_t>> gc(count);
+    for (uint32_t j : live) {
+        const hq_encode16_job &b = jobs[j];
+        std::vector<uint64_t> &c = gc[j];
+        c.assign(T + 1, 0);
+        c[T] = b.n_groups;
+        for (uint32_t t = 1; t < T; ++t) {
+            const uint64_t cut = R * t / T;
+            const uint64_t rel = cut <= rec0[j] ? 0 : std::min(cut - rec0[j], rec0[j + 1] - rec0[j]);
+            const uint64_t want = b.offsets16[0] + rel;
+            const uint64_t g = (uint64_t)(std::lower_bound(b.offsets16, b.offsets16 + b.n_groups, want) -
+                                          b.offsets16);
+            c[t] = std::min<uint64_t>(std::max<uint64_t>(c[t - 1], g), b.n_groups);
+        }
+    }
+    struct Piece {
+        uint32_t job;
+        uint64_t at, events, bytes, last_start;   // at: offset in the thread's scratch
+        int rc;
+    };
+    std::vector<std::vector<Piece>> pieces(T);
+    std::mutex bm;
+    std::condition_variable bcv;
+    uint32_t arrived = 0;
+    uint64_t c1 = 0;
+    // per job, per thread: where the thread's piece goes in the job's bytes
+    std::vector<uint64_t> place((size_t)count * T, 0);
+    std::vector<uint8_t> fits(count, 1);
+    task_pool().parallel_for(T, [&](uint32_t t) {
+        thread_local std::vector<uint8_t> scratch;
+        std::vector<Piece> &ps = pieces[t];
+        uint64_t pos = 0;
+        std::vector<uint8_t> part;
+        for (uint32_t j : live) {
+            const uint64_t g0 = gc[j][t], g1 = gc[j][t + 1];
+            if (g0 >= g1) continue;
+            const hq_encode16_job &b = jobs[j];
+            Piece pc{j, pos, 0, 0, ~0ull, HQ_OK};
+            // (the piece is encoded after the thread's earlier pieces: into a scratch of its
+            // own, then appended)
+            if (ps.empty()) {
+                pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &scratch, nullptr, 0,
+                                    &pc.events, &pc.bytes, &pc.last_start);
+            } else {
+                pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &part, nullptr, 0,
+                                    &pc.events, &pc.bytes, &pc.last_start);
+                if (!pc.rc) {
+                    if (scratch.size() < pos + pc.bytes) scratch.resize(pos + pc.bytes);
+                    std::memcpy(scratch.data() + pos, part.data(), pc.bytes);
+                }
+            }
+            pos += pc.bytes;
+            ps.push_back(pc);
+        }
+        {
+            std::unique_lock<std::mutex> lk(bm);
+            if (++arrived == T) {
+                // every piece in: each job's totals, its capacity rule and its pieces' places
+                c1 = now_ns();
+                std::vector<uint64_t> total(count, 0), last(count, ~0ull);
+                for (uint32_t u = 0; u < T; ++u) {
+                    for (const Piece &pc : pieces[u]) {
+                        hq_encode16_job &b = jobs[pc.job];
+                        if (pc.rc && !b.rc) b.rc = pc.rc;
+                        if (pc.last_start != ~0ull) last[pc.job] = total[pc.job] + pc.last_start;
+                        place[(size_t)pc.job * T + u] = total[pc.job];
+                        total[pc.job] += pc.bytes;
+                        b.n_events += pc.events;
+                    }
+                }
+                for (uint32_t j : live) {
+                    hq_encode16_job &b = jobs[j];
+                    fits[j] = last[j] == ~0ull ||
+                              (b.cap >= last[j] && b.cap - last[j] >= HQ_EVENT_STREAM_MAX);
+                    if (!b.rc && !fits[j]) b.rc = HQ_E_STATE;
+                    b.n_bytes = b.rc ? 0 : total[j];
+                    if (b.rc) b.n_events = 0;
+                }
+                bcv.notify_all();
+            } else {
+                bcv.wait(lk, [&] { return arrived == T; });
+            }
+        }
+        for (const Piece &pc : ps) {
+            const hq_encode16_job &b = jobs[pc.job];
+            if (!b.rc && pc.bytes)
+                std::memcpy(b.out + place[(size_t)pc.job * T + t], scratch.data() + pc.at, pc.bytes);
+        }
+    }, true);
+    first = HQ_OK;
+    for (uint32_t j = 0; j < count && !first; ++j) first = jobs[j].rc;
+    const uint64_t c2 = now_ns();
+    g_clk.calls++;
+    g_clk.encode_ns += c1 - c0;
+    g_clk.copy_ns += c2 - c1;
+    g_clk.wall_ns += c2 - c0;
+    return first;
+}
+
 int hq_encode_stats_read(hq_encode_stats *out, int reset) {
     if (!out) return HQ_E_INVAL;
     auto take = [&](std::atomic<uint64_t> &a) { return reset ? a.exchange(0) : a.load(); };

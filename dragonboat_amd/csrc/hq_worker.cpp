@@ -893,6 +893,9 @@ int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *
                                 uint64_t t1) {
     if (rc == HQ_E_INVAL && dout.input_error) {
         const uint32_t e = dout.input_error;
+        if (e & 16)               // (hq_dstep.hip kErrScan: not the input's fault)
+            return fail(HQ_E_STATE, "hq_worker_step: the device step's scan of the ReadyToRead "
+                                    "places failed (internal); no group state was written");
         return fail(HQ_E_INVAL, e & 1 ? "hq_worker_step: unknown group handle"
                                 : e & 8 ? "hq_worker_step: a group is listed twice"
                                 : e & 2 ? "hq_worker_step: offsets decrease"
@@ -921,10 +924,13 @@ int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *
     out->n_fallback_groups = dout.n_fallback;
     out->gpu_passes = inp.n ? 1 : 0;
     out->decisions = dout.decisions;
+    // (device path: pack = the host's submit, device = the GPU's time between its events, apply
+    // = the outputs mapped after the wait; pass less the three is the wait the GPU does not
+    // explain: queueing ahead of the step's work and the waiting thread's wake-up)
     out->pass_ns = t2 - t1;
-    out->pack_ns = 0;
-    out->device_ns = t2 - t1;
-    out->apply_ns = 0;
+    out->pack_ns = dout.submit_ns;
+    out->device_ns = dout.gpu_ns;
+    out->apply_ns = dout.d2h_ns;
     out->handle_ns = t1 - t0;
     return HQ_OK;
 }

@@ -42,7 +42,7 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 17
+HQ_ABI_VERSION = 18
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -386,6 +386,7 @@ SIGNATURES = {
     "hq_events16_encode_sized": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64,
                                                 _vp, _vp, _vp, ctypes.c_uint32]),
     "hq_encode_stats_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hq_events16_encode_sized_multi": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "hq_events_to16": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
@@ -1616,6 +1617,34 @@ def encode_events16_sized_into(offsets16, recs, out: np.ndarray, sizes: np.ndarr
                                       _p(out), len(out), _p(sizes), ctypes.byref(ne),
                                       ctypes.byref(nb), threads), "hq_events16_encode_sized")
     return ne.value, nb.value
+
+
+class Encode16Job(ctypes.Structure):
+    """hq_encode16_job (include/hipquorum.h)."""
+    _fields_ = [("n_groups", ctypes.c_uint64), ("offsets16", _vp), ("recs", _vp), ("out", _vp),
+                ("cap", ctypes.c_uint64), ("sizes", _vp), ("n_events", ctypes.c_uint64),
+                ("n_bytes", ctypes.c_uint64), ("rc", ctypes.c_int)]
+
+
+def encode_events16_sized_multi(jobs, threads: int = 1):
+    """hq_events16_encode_sized_multi: jobs = [(offsets16, recs, out, sizes)] as
+    encode_events16_sized_into's arguments, encoded in one call whose `threads` native threads
+    split the records of all jobs evenly; returns [(n_events, n_bytes)] per job."""
+    arr = (Encode16Job * max(1, len(jobs)))()
+    for b, (off, recs, out, sizes) in zip(arr, jobs):
+        n = len(off) - 1
+        assert off.dtype == np.uint64 and recs.dtype == EVENT16_DTYPE
+        assert out.dtype == np.uint8 and sizes.dtype == np.uint32 and len(sizes) >= n
+        assert off.flags.c_contiguous and recs.flags.c_contiguous and out.flags.c_contiguous
+        b.n_groups, b.offsets16 = n, _p(off)
+        b.recs = _p(recs) if len(recs) else None
+        b.out, b.cap, b.sizes = _p(out), len(out), _p(sizes)
+    rc = lib.hq_events16_encode_sized_multi(ctypes.addressof(arr), len(jobs), threads)
+    for j, b in enumerate(arr[:len(jobs)]):
+        if b.rc:
+            raise HQError(b.rc, f"hq_events16_encode_sized_multi job {j}")
+    _chk(rc, "hq_events16_encode_sized_multi")
+    return [(b.n_events, b.n_bytes) for b in arr[:len(jobs)]]
 
 
 ENCODE_STATS_FIELDS = ("calls", "tasks", "helped", "wall_ns", "encode_ns", "copy_ns", "lag_ns",

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 17
+#define HQ_ABI_VERSION 18
 
 /* status codes */
 #define HQ_OK          0
@@ -954,6 +954,11 @@ typedef struct hq_step_output {
     uint64_t pack_ns;           /*   of which packing the kernels' SoA inputs */
     uint64_t device_ns;         /*   of which H2D + kernels + D2H + sync */
     uint64_t apply_ns;          /*   of which applying the decisions */
+    /* (HQ_WORKER_ON_DEVICE workers: pack_ns = the host's time to queue the step's copies and
+     * launches, device_ns = the GPU's time from the step's first queued operation to its last
+     * (HIP timing events; a jobs step's is the shared launches' time), apply_ns = mapping the
+     * outputs after the wait; pass_ns - pack_ns - device_ns - apply_ns is the wait the GPU's
+     * time does not explain, the waiting thread's wake-up and any queueing ahead of the step) */
     /* HQ_WORKER_COMMIT_COLUMN workers only, else NULL: the step's commits as one word per
      * listed group (input order), its new committed index or 0 (no commit: a commit never sets
      * 0); `commits` is then NULL and n_commits counts the nonzero words */
@@ -1107,6 +1112,24 @@ typedef struct hq_event16 {
 int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const hq_event16 *recs,
                              uint8_t *out, uint64_t cap, uint32_t *sizes, uint64_t *n_events,
                              uint64_t *n_bytes, uint32_t threads);
+/* Several streams at once — the steps of a GPU's step workers (execengine.go:675-690), one
+ * stream each: hq_events16_encode_sized for every job, the groups of all jobs split into
+ * `threads` ranges of about equal records (a range may cross from one job into the next), so
+ * that the threads stay evenly loaded whatever the number of jobs (one call per job on a shared
+ * pool queues the jobs past the threads' count: 16 workers on 14 threads took two rounds).
+ * Every job's bytes, sizes and totals equal its own hq_events16_encode_sized call's; each job's
+ * rc is its own (HQ_E_INVAL / HQ_E_STATE as there), the call returns the first job's failure. */
+typedef struct hq_encode16_job {
+    uint64_t n_groups;
+    const uint64_t *offsets16;
+    const hq_event16 *recs;
+    uint8_t *out;
+    uint64_t cap;
+    uint32_t *sizes;
+    uint64_t n_events, n_bytes;  /* out */
+    int rc;                      /* out */
+} hq_encode16_job;
+int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32_t threads);
 /* Phase clocks of the threaded hq_events16_encode_sized calls (diagnostic; process-wide sums
  * since the last reset): wall = encode + copy phase per call; a range ("task") queued for the
  * pool waits `lag` from the call's queueing until a pool thread starts it (`helped` such starts;

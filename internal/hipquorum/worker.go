@@ -10,6 +10,7 @@ import (
 	"encoding/binary"
 	"errors"
 	"fmt"
+	"runtime"
 	"unsafe"
 
 	pb "github.com/lni/dragonboat/v3/raftpb"
@@ -386,5 +387,56 @@ func Encode16(offsets []uint64, recs []C.hq_event16, b *StreamBuf, threads int) 
 	b.Bytes = b.Bytes[:int(nBytes)]
 	b.Sizes = b.Sizes[:nGroups]
 	b.NEvents = uint64(nEvents)
+	return nil
+}
+
+// Encode16Job is one step worker's step for EncodeMany: its compact records and stream buffer.
+type Encode16Job struct {
+	Offsets []uint64
+	Recs    []C.hq_event16
+	Buf     *StreamBuf
+}
+
+// EncodeMany encodes the steps of several step workers in one call whose `threads` native
+// threads split the records of all of them evenly (hq_events16_encode_sized_multi); each
+// buffer ends as its own Encode16 would leave it. The Go slices the C array points at are
+// pinned for the call (cgo: Go pointers stored in C memory must be pinned).
+func EncodeMany(jobs []Encode16Job, threads int) error {
+	if len(jobs) == 0 {
+		return nil
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	mem := C.malloc(C.size_t(len(jobs)) * C.size_t(unsafe.Sizeof(C.hq_encode16_job{})))
+	defer C.free(mem)
+	cj := unsafe.Slice((*C.hq_encode16_job)(mem), len(jobs))
+	for i, j := range jobs {
+		b := j.Buf
+		pin.Pin(&j.Offsets[0])
+		bytes := b.Bytes[:cap(b.Bytes)]
+		sizes := b.Sizes[:cap(b.Sizes)]
+		pin.Pin(&bytes[0])
+		pin.Pin(&sizes[0])
+		cj[i] = C.hq_encode16_job{n_groups: C.uint64_t(len(j.Offsets) - 1),
+			offsets16: (*C.uint64_t)(unsafe.Pointer(&j.Offsets[0])),
+			out:       (*C.uint8_t)(unsafe.Pointer(&bytes[0])), cap: C.uint64_t(len(bytes)),
+			sizes: (*C.uint32_t)(unsafe.Pointer(&sizes[0]))}
+		if len(j.Recs) > 0 {
+			pin.Pin(&j.Recs[0])
+			cj[i].recs = &j.Recs[0]
+		}
+	}
+	rc := C.hq_events16_encode_sized_multi(&cj[0], C.uint32_t(len(jobs)), C.uint32_t(threads))
+	for i, j := range jobs {
+		if cj[i].rc != C.HQ_OK {
+			return fmt.Errorf("hq_events16_encode_sized_multi: job %d: %d", i, int(cj[i].rc))
+		}
+		j.Buf.Bytes = j.Buf.Bytes[:int(cj[i].n_bytes)]
+		j.Buf.Sizes = j.Buf.Sizes[:len(j.Offsets)-1]
+		j.Buf.NEvents = uint64(cj[i].n_events)
+	}
+	if rc != C.HQ_OK {
+		return fmt.Errorf("hq_events16_encode_sized_multi: %d", int(rc))
+	}
 	return nil
 }

@@ -557,12 +557,17 @@ def test_pinned_sized_stream_equals_pageable(hq, flags):
         pin.close()
 
 
-@pytest.mark.parametrize("stream", [True, False, "sized", "sized-column", "sized-advance"],
-                         ids=["stream", "rows", "sized", "sized-column", "sized-advance"])
+@pytest.mark.parametrize("stream", [True, False, "sized", "sized-column", "sized-advance",
+                                    "stream-advance"],
+                         ids=["stream", "rows", "sized", "sized-column", "sized-advance",
+                              "stream-advance"])
 def test_chunked_device_step_equals_host_worker(hq, stream):
     """A step of >= 256 Ki groups runs in 4 chunks whose copies overlap the neighbouring chunks'
     passes (hq_dstep.hip); its lists equal the host worker's on the same events (the host
-    worker is checked against the oracle above), in the same order."""
+    worker is checked against the oracle above), in the same order. With the advance column a
+    stream's pass A also writes the single ReadyToReads at their places (ready_tail's chained
+    scan across the chunks' launches: byte chunks for a sized stream, group chunks for one with
+    offsets)."""
     import bench
 
     G = 4 * 65536 + 5
@@ -570,7 +575,7 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
     g, m, _ = bench.step_groups(hq, G, 1, 1, roles)
     nv = sum(r != "observer" for r in roles)
     dev = hq.Worker(0, nv, on_device=True, commit_column=stream == "sized-column",
-                    commit_advance=stream == "sized-advance")
+                    commit_advance=str(stream).endswith("advance"))
     host = hq.Worker(0, nv)
     try:
         dev.add_groups(g, m)
@@ -578,7 +583,7 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
         for s in range(3):
             e = bench.step_events(hq, G, s, roles)
             prev_col = np.array([host.get_group(c)[0]["committed"] for c in range(1, G + 1)],
-                                np.uint64) if stream == "sized-advance" and s else None
+                                np.uint64) if str(stream).endswith("advance") and s else None
             want = host.step(*e)
             if str(stream).startswith("sized"):   # byte chunks, each group's pass A in the
                 data, sizes = hq.encode_events_sized(e[1], e[2])   # chunk its bytes end in
@@ -602,6 +607,13 @@ def test_chunked_device_step_equals_host_worker(hq, stream):
             elif stream:
                 data, boff = hq.encode_events(e[1], e[2])
                 got = dev.step_stream(e[0], e[1], boff, data)
+                if "committed_advance" in got:
+                    assert s and stream == "stream-advance" and got["n_commits"] == G
+                    want_col = np.zeros(G, np.uint64)
+                    want_col[want["commits"]["cluster_id"].astype(np.int64) - 1] = \
+                        want["commits"]["committed"]
+                    np.testing.assert_array_equal(prev_col + got["committed_advance"], want_col)
+                    got["commits"] = want["commits"]
             else:
                 got = dev.step(*e)
             for k in ("commits", "ready", "read_resps", "state_changes", "dropped_reads",

@@ -355,6 +355,58 @@ def test_threaded_encodes_side_by_side(hq):
     assert not bad
 
 
+@pytest.mark.parametrize("threads", [1, 3, 14])
+def test_multi_encode_equals_one_call_per_job(hq, threads):
+    """hq_events16_encode_sized_multi: 16 workers' streams (ragged: a worker with no groups, one
+    with groups but no records, others of unequal size) encoded in one call whose thread ranges
+    cross job boundaries; every job's bytes, size words and totals equal its own single call's."""
+    import bench
+    G = 1 << 13
+    recs = bench.StepRows16(hq, G, bench.STEP_ROLES["step5"])
+    off16, r = recs.set(2)
+    b = sorted({0, G} | {int(x) for x in np.random.default_rng(5).integers(0, G, 14)})
+    b = [0, 0] + b[1:]                       # worker 0: no groups
+    parts = [(off16[b[i]:b[i + 1] + 1] - off16[b[i]], int(off16[b[i]]), int(off16[b[i + 1]]))
+             for i in range(len(b) - 1)]
+    empty = (np.zeros(4, np.uint64), 0, 0)   # 3 groups without records
+    parts.insert(3, empty)
+    want = [hq.encode_events16_sized(o, r[e0:e1], 1) for o, e0, e1 in parts]
+    jobs = [(o, r[e0:e1], np.zeros((e1 - e0) * 5 + 64, np.uint8), np.zeros(len(o) - 1, np.uint32))
+            for o, e0, e1 in parts]
+    hq.encode_stats(reset=True)
+    got = hq.encode_events16_sized_multi(jobs, threads)
+    assert hq.encode_stats(reset=True)["calls"] == 1
+    for (o, rr, out, sz), (ne, nb), (wd, ws, wne) in zip(jobs, got, want):
+        assert ne == wne and nb == len(wd)
+        np.testing.assert_array_equal(out[:nb], wd)
+        np.testing.assert_array_equal(sz, ws)
+
+
+def test_multi_encode_errors_per_job(hq):
+    """A job whose region is too small fails with HQ_E_STATE and one with a malformed escape with
+    HQ_E_INVAL, each in its own rc; the other jobs are encoded as alone."""
+    off, ev = _random_groups(hq, 24, n=3000)
+    recs, off16 = hq.events_to16(off, ev)
+    wd, ws, wne = hq.encode_events16_sized(off16, recs, 1)
+    bad = np.zeros(3, hq.EVENT16_DTYPE)
+    bad["kind"] = hq.EV16_FULL
+    for T in (1, 4):
+        jobs = [(off16, recs, np.zeros(len(wd) + 64 * 8, np.uint8), np.zeros(len(off) - 1, np.uint32)),
+                (off16, recs, np.zeros(len(wd) - 1, np.uint8), np.zeros(len(off) - 1, np.uint32)),
+                (np.array([0, 3], np.uint64), bad, np.zeros(256, np.uint8), np.zeros(1, np.uint32))]
+        arr = (hq.Encode16Job * 3)()
+        for a, (o, rr, out, sz) in zip(arr, jobs):
+            a.n_groups, a.offsets16, a.recs = len(o) - 1, o.ctypes.data, rr.ctypes.data
+            a.out, a.cap, a.sizes = out.ctypes.data, len(out), sz.ctypes.data
+        rc = hq.lib.hq_events16_encode_sized_multi(hq.ctypes.addressof(arr), 3, T)
+        assert rc == hq.HQ_E_STATE            # the first failing job's
+        assert [a.rc for a in arr] == [hq.HQ_OK, hq.HQ_E_STATE, hq.HQ_E_INVAL]
+        assert arr[0].n_events == wne and arr[0].n_bytes == len(wd)
+        np.testing.assert_array_equal(jobs[0][2][:len(wd)], wd)
+        np.testing.assert_array_equal(jobs[0][3], ws)
+        assert arr[1].n_bytes == 0 and arr[2].n_bytes == 0
+
+
 # --- runs (code 6): acks repeating the group's previous message but for the sender --------------
 
 def runny_rows(hq, rng, groups=300):

@@ -51,9 +51,9 @@ def main(d, steps, W=1):
     in_mb = float(os.environ.get("INPUT_MB", 0))    # the trace has no copy sizes: the step's input
     # pass B launches (k_step<true, ...>) end each worker's step: the last step's window opens
     # after the previous step's last pass B of every worker
-    pb = sorted(e for a, e, n in ks if "k_step<true" in n)
-    if len(pb) < W * steps:
-        print(f"expected {W * steps} pass-B launches, found {len(pb)}")
+    pb = sorted(e for a, e, n in ks if "k_step<true" in n or "k_step_jobs<true" in n)
+    if len(pb) < steps:
+        print(f"expected >= {steps} pass-B launches, found {len(pb)}")
     # the host builds the next step's events between steps (milliseconds with no device
     # activity): the window opens at the first copy or kernel after the last such gap
     t_close = pb[-1]
