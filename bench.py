@@ -569,9 +569,9 @@ def fused_chunks(steps):
 
 def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
     """A commit workload stepped through the persistent commit engine (hq_engine_*,
-    dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps' batches are posted as K
-    descriptors and decided by ONE resident launch (no dependent-launch boundary between
-    steps), then drained. Beside each engine window, the same K batches as K back-to-back
+    dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps' batches are handed over as K
+    descriptors and a STOP (hq_engine_run) and decided by ONE resident launch (no
+    dependent-launch boundary between steps) that ends at the STOP. Beside each engine window, the same K batches as K back-to-back
     launches (hq_commit_many_dev), so the line carries both on the same data. `windows` windows
     of K = `steps` steps each continue the rotation (>= 1.1 GiB of distinct batches: no step
     re-reads a batch the 256 MiB Infinity Cache could still hold); the median window is reported
@@ -598,8 +598,7 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
         return hq.commit_batch_array([batch_args(sets[(i0 + i) % nsets][0]) for i in range(k)])
 
     W = max(1, warmup)
-    eng.post(arr(0, W))
-    eng.drain()
+    eng.run(arr(0, W))
     eng_sig.post(arr(0, W))
     eng_sig.drain()
     eng_sig.timing(reset=True)
@@ -624,13 +623,16 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
                 ctx.timing(True)
             t0 = time.perf_counter()
             if mode == "engine":
-                eng.post(a)
-                eng.drain()
+                eng.run(a)
             elif mode == "signal":
                 q0 = eng_sig.post(a)
-                eng_sig.wait(q0 + steps - 1)       # the last step's flag: every step complete
+                eng_sig.wait(q0 + steps - 1)       # the last step's flag: every step decided
                 sig_local = time.perf_counter() - t0
-                # (the engine keeps the clocks of its last `depth` steps)
+                # (each step's flag is written by its own last arriving workgroup: an earlier
+                # step's may land just after a later one's, so every flag is awaited before its
+                # clock is read; the engine keeps the clocks of its last `depth` steps)
+                for i in range(steps):
+                    eng_sig.wait(q0 + i)
                 nclk = min(steps, eng_sig.info().depth)
                 clocks = [eng_sig.done_clock(q0 + i) for i in range(steps - nclk, steps)]
                 eng_sig.drain()
@@ -712,10 +714,10 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
         achieved_gbs=achieved_local, achieved_node_gbs=achieved_node, per_gpu=per_gpu,
         set0=set0, gather=None, windows=len(wins), headline_mode=hm,
         engine={
-            "mode": "persistent commit engine (hq_engine): the window's steps posted (one "
-                    f"descriptor per {groups_per_step(w)}-group step, {steps} steps in one "
-                    "hq_engine_post call) and decided step after step by one resident launch "
-                    "(started by the first post, ended by the drain's STOP)",
+            "mode": "persistent commit engine (hq_engine): the window's steps (one descriptor "
+                    f"per {groups_per_step(w)}-group step, {steps} steps) and a STOP handed to one "
+                    "launch (hq_engine_run), decided step after step by the resident grid, which "
+                    "ends at the STOP",
             "groups_per_step": groups_per_step(w), "steps_per_window": steps,
             "grid": info.grid, "block": info.block,
             "window_ms": [round(x["engine"]["elapsed"] * 1e3, 4) for x in wins],
@@ -2147,7 +2149,7 @@ def report(args, d, res, launcher):
             "kernel_time": ("HIP events around the fused launch(es) of the median window, / "
                             "steps" if r.get("headline_mode") == "fused" else
                             "HIP events around the resident engine launch of the median "
-                            "window (posted steps + STOP), / steps" if r.get("engine") else
+                            "window (its steps + STOP, hq_engine_run), / steps" if r.get("engine") else
                             "HIP events on the launch stream around the timed launches "
                             "(back to back), / launches"),
             "achieved_scope": f"sum over {d.world} GPU(s) of bytes per launch / kernel time",
@@ -2232,7 +2234,7 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="engine", choices=("fused", "engine", "launch"),
+    ap.add_argument("--mode", default="fused", choices=("fused", "engine", "launch"),
                     help="headline commit steps: the co-resident step workers' batches fused "
                          "into launches of up to 32 (fused), the persistent engine (one resident "
                          "launch per window), or one launch per step; fused and engine apply to "

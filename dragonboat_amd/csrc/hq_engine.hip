@@ -830,9 +830,12 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     return HQ_OK;
 }
 
-int hq_engine_post(hq_engine *e, const hq_commit_args *args, uint32_t count, uint64_t *first_seq) {
-    if (!e) return HQ_E_INVAL;
-    std::lock_guard<std::mutex> g(e->mu);
+namespace {
+
+// hq_engine_post under the lock; start: launch the grid if none is resident (hq_engine_run
+// leaves that to its drain, so that the launch carries the STOP too)
+int post_locked(hq_engine *e, const hq_commit_args *args, uint32_t count, uint64_t *first_seq,
+                bool start) {
     if (count && !args) return efail(e, HQ_E_INVAL, "hq_engine_post: args is NULL");
     const uint64_t keep_G = e->inplace_G;
     for (uint32_t i = 0; i < count; ++i) {
@@ -864,8 +867,27 @@ int hq_engine_post(hq_engine *e, const hq_commit_args *args, uint32_t count, uin
         if ((e->cfg.layout & HQ_LAYOUT_IN_PLACE) && d.G) e->inplace_G = d.G;
         rc = write_desc(e, d);
     }
-    if (!rc && count) rc = ensure_running(e);
+    if (!rc && count && start) rc = ensure_running(e);
     return rc;
+}
+
+}  // namespace
+
+int hq_engine_post(hq_engine *e, const hq_commit_args *args, uint32_t count, uint64_t *first_seq) {
+    if (!e) return HQ_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    return post_locked(e, args, count, first_seq, true);
+}
+
+int hq_engine_run(hq_engine *e, const hq_commit_args *args, uint32_t count, uint64_t *first_seq) {
+    if (!e) return HQ_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    int rc = post_locked(e, args, count, first_seq, false);
+    // no grid resident: the drain launches one whose arguments carry the steps and the STOP (no
+    // relay: the grid ends as soon as its last step is decided); a resident grid gets the STOP
+    // through the ring as in hq_engine_drain
+    if (!rc) rc = echeck(e, hipSetDevice(e->ctx->device), "hipSetDevice");
+    return rc ? rc : drain_locked(e);
 }
 
 int hq_engine_wait(hq_engine *e, uint64_t seq) {

@@ -42,7 +42,7 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 18
+HQ_ABI_VERSION = 19
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -274,6 +274,7 @@ SIGNATURES = {
     "hq_engine_post": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32, _u64p]),
     "hq_engine_wait": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "hq_engine_drain": (ctypes.c_int, [_vp]),
+    "hq_engine_run": (ctypes.c_int, [_vp, ctypes.POINTER(CommitArgs), ctypes.c_uint32, _u64p]),
     "hq_engine_timing": (ctypes.c_int, [_vp, _u64p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "hq_engine_done_clock": (ctypes.c_int, [_vp, ctypes.c_uint64, _u64p]),
     "hq_engine_info": (ctypes.c_int, [_vp, ctypes.POINTER(EngineStats)]),
@@ -940,6 +941,13 @@ class Engine:
 
     def drain(self) -> None:
         self._check(lib.hq_engine_drain(self.h))
+
+    def run(self, batch) -> int:
+        """hq_engine_run: post the batches and drain, the STOP handed over with the steps when
+        no grid is resident (one launch that ends at its last step); returns the first seq."""
+        seq = ctypes.c_uint64(0)
+        self._check(lib.hq_engine_run(self.h, batch, len(batch), ctypes.byref(seq)))
+        return seq.value
 
     def timing(self, reset: bool = False) -> tuple[int, float]:
         """(finished resident launches, their total GPU ms) since the last reset."""

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 18
+#define HQ_ABI_VERSION 19
 
 /* status codes */
 #define HQ_OK          0
@@ -324,6 +324,11 @@ int hq_engine_post(hq_engine *eng, const hq_commit_args *args, uint32_t count, u
 int hq_engine_wait(hq_engine *eng, uint64_t seq);
 /* Complete every posted step and end the resident launch (the CUs are free afterwards). */
 int hq_engine_drain(hq_engine *eng);
+/* A bounded run: post `count` batches, then drain. With no grid resident the launch's arguments
+ * carry the steps and the STOP together (up to 32), so the grid ends as soon as the last step is
+ * decided — a post followed by a drain launches on the post and the STOP reaches the running grid
+ * through the ring (~20 us of relay and polling per launch, tools/engine_overhead.py). */
+int hq_engine_run(hq_engine *eng, const hq_commit_args *args, uint32_t count, uint64_t *first_seq);
 /* GPU time of the finished resident launches (HIP events around each), since the last reset. */
 int hq_engine_timing(hq_engine *eng, uint64_t *launches, double *total_ms, int reset);
 /* The device clock (s_memrealtime, 100 MHz) when step seq completed (HQ_ENGINE_SIGNAL). */

@@ -103,6 +103,26 @@ func (g *Engine) Step(t *TileBatch) error {
 // Drain completes every posted step and ends the resident launch (the CUs are free afterwards).
 func (g *Engine) Drain() error { return g.err(C.hq_engine_drain(g.e)) }
 
+// Run posts the batches as the next steps and drains: with no launch resident, one launch
+// carries the steps and the STOP and ends at the last step (hq_engine_run).
+func (g *Engine) Run(ts []*TileBatch) (uint64, error) {
+	if len(ts) == 0 {
+		return 0, errors.New("hipquorum: no batch to run")
+	}
+	n := len(ts)
+	mem := C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.hq_commit_args{})))
+	defer C.free(mem)
+	as := unsafe.Slice((*C.hq_commit_args)(mem), n)
+	for i, t := range ts {
+		as[i] = t.Args()
+	}
+	var seq C.uint64_t
+	if rc := C.hq_engine_run(g.e, &as[0], C.uint32_t(n), &seq); rc != C.HQ_OK {
+		return 0, g.err(rc)
+	}
+	return uint64(seq), nil
+}
+
 // Stats reports the engine's counters.
 func (g *Engine) Stats() (posted, completed, relaunches uint64, err error) {
 	var s C.hq_engine_stats

@@ -107,12 +107,44 @@ def test_engine_ring_wraps(gpu_ctx, hq, signal):
         st = eng.info()
         assert st.completed >= seqs[-1] or not signal
         if signal:
+            # (a step's flag is written by its own last workgroup: an earlier step's may land
+            # just after a later one's, so each is awaited before its clock is read)
+            for q in seqs[-4:]:
+                eng.wait(q)
             clocks = [eng.done_clock(q) for q in seqs[-4:]]
             assert clocks == sorted(clocks)
         eng.drain()
     for b, w in zip(bufs, want):
         for x, y in zip(outputs(gpu_ctx, b), w):
             np.testing.assert_array_equal(x, y)
+        hq.free_commit(gpu_ctx, b)
+
+
+@pytest.mark.parametrize("signal", [False, True])
+@pytest.mark.parametrize("steps", [6, 45])
+def test_engine_run_bounded(gpu_ctx, hq, signal, steps):
+    """hq_engine_run: the steps and the STOP in one launch (45 > the 32 descriptors a launch's
+    arguments carry: the rest arrive through the ring); then, with a grid left resident by a
+    signalled post, a run whose STOP reaches the running grid. Every step's outputs are the
+    launch path's and no launch is left running."""
+    n, form, lay = 5, hq.HQ_FORM_TERM_MASK, hq.HQ_LAYOUT_TILES_LEADER
+    bufs = [make_batch(gpu_ctx, hq, 3_000 + 131 * k, n, form, lay, SEED + 700 + k) for k in range(5)]
+    want = [launch_reference(gpu_ctx, b) for b in bufs]
+    with hq.Engine(gpu_ctx, n, form, lay, signal=signal) as eng:
+        for rnd in range(2):
+            for b in bufs:
+                poison(gpu_ctx, b)
+            gpu_ctx.sync()
+            if rnd == 1 and signal:          # a grid resident when the run posts
+                eng.wait(eng.post(bufs[0].tile_args()))
+                assert eng.info().running
+            first = eng.run(hq.commit_batch_array([bufs[s % 5].tile_args() for s in range(steps)]))
+            st = eng.info()
+            assert not st.running and st.completed == st.posted and first + steps < st.posted + 1
+            for b, w in zip(bufs, want):
+                for x, y in zip(outputs(gpu_ctx, b), w):
+                    np.testing.assert_array_equal(x, y)
+    for b in bufs:
         hq.free_commit(gpu_ctx, b)
 
 

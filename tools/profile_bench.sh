@@ -1,7 +1,8 @@
 #!/bin/bash
 # rocprofv3 evidence for bench.py: kernel-trace stats of the bench command, then one PMC pass per
 # counter group (FETCH_SIZE and WRITE_SIZE do not fit one pass). Each step has its own time limit;
-# the script stops at the first failure.
+# the script stops at the first failure. The trace runs the driver's command (--steps 20 --warmup 5
+# unless STEPS / WARMUP say otherwise).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 W=${1:-c2}
@@ -12,7 +13,7 @@ mkdir -p $OUT
 set -o pipefail
 echo "== kernel trace ($W)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 bench.py $ARGS --no-cpu --detail-out $OUT/trace_detail.json > $OUT/trace_stdout.log 2>&1 || exit $?
+  python3 bench.py $ARGS --no-cpu --steps ${STEPS:-20} --warmup ${WARMUP:-5} --detail-out $OUT/trace_detail.json > $OUT/trace_stdout.log 2>&1 || exit $?
 tail -n 1 $OUT/trace_stdout.log
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C ($W)"

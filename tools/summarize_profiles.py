@@ -45,6 +45,22 @@ FUSED_THREADS_PER_BATCH = {"c3mtl": 524288}
 KERNEL_FUSED = {"c3mtl": "k_commit_fused<2, 1024, 2>"}
 
 
+# the default line's headline mode "engine" (bench.py run_engine): the persistent engine's launch
+# per timed window of --steps steps; its dispatches are the warm-up (warmup steps), the timed
+# windows (steps each, in order) and the parity launch (1 step). Per step: a window dispatch's
+# duration or counter over its steps.
+KERNEL_ENGINE = {"c3mtl-engine": ("c3mtl", "k_commit_engine<5, 2, 1, false, 1024, false>")}
+ENGINE_STEPS, ENGINE_WARMUP, ENGINE_WINDOWS = 20, 5, 3
+
+
+def engine_windows(path, kernel, value_key):
+    """per-step values of the timed-window dispatches (2nd .. windows + 1st of the kernel's)."""
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0))
+    wins = rows[1:1 + ENGINE_WINDOWS]
+    return [value_key(r) / ENGINE_STEPS for r in wins], len(rows)
+
+
 def per_batch(path, kernel, tpb, value_key, grid_key):
     """sum over the kernel's dispatches of value / sum of their batches (grid / tpb)."""
     rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
@@ -66,6 +82,38 @@ def main():
     traffic = json.load(open(tj)) if os.path.exists(tj) else {}
     for w in workloads:
         src = os.path.join(ROOT, "gpurun_out", f"prof_{w}")
+        if w in KERNEL_ENGINE:
+            base, k = KERNEL_ENGINE[w]
+            for f, name in (("trace/run_kernel_stats.csv", f"{w}_kernel_stats.csv"),
+                            ("trace/run_kernel_trace.csv", f"{w}_kernel_trace.csv"),
+                            ("pmc_FETCH_SIZE/run_counter_collection.csv", f"{w}_pmc_FETCH_SIZE.csv"),
+                            ("pmc_WRITE_SIZE/run_counter_collection.csv", f"{w}_pmc_WRITE_SIZE.csv"),
+                            ("trace_stdout.log", f"{w}_bench_line.log")):
+                shutil.copy(os.path.join(src, f), os.path.join(dst, name))
+            ns, nd = engine_windows(os.path.join(dst, f"{w}_kernel_trace.csv"), k,
+                                    lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            fetch, nf = engine_windows(os.path.join(dst, f"{w}_pmc_FETCH_SIZE.csv"), k,
+                                       lambda r: float(r["Counter_Value"]))
+            write, nw = engine_windows(os.path.join(dst, f"{w}_pmc_WRITE_SIZE.csv"), k,
+                                       lambda r: float(r["Counter_Value"]))
+            f_med, w_med = statistics.median(fetch), statistics.median(write)
+            traffic[w] = {
+                "kernel": k, "mode": "engine",
+                "rocprof_window_ns_per_step": ns, "rocprof_avg_ns": statistics.median(ns),
+                "rocprof_calls": nd, "steps_per_window": ENGINE_STEPS,
+                "fetch_size_kb_median": f_med, "write_size_kb_median": w_med,
+                "dispatches": min(nf, nw),
+                "hbm_bytes_per_launch": (2 * f_med + w_med) * 1024,
+                "per": f"step (one step of 1 M groups; a window launch decides {ENGINE_STEPS})",
+                "correction": "(2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE halves 16B/lane "
+                              "streams)",
+                "round": rnd,
+                "source": f"profiles/{rnd}/{w}_pmc_FETCH_SIZE.csv + {w}_pmc_WRITE_SIZE.csv "
+                          f"(kernel time: {w}_kernel_trace.csv, the timed windows' launches / "
+                          f"{ENGINE_STEPS} steps)",
+            }
+            print(w, json.dumps(traffic[w]))
+            continue
         if w in FUSED_THREADS_PER_BATCH:
             tpb, k = FUSED_THREADS_PER_BATCH[w], KERNEL_FUSED[w]
             for f, name in (("trace/run_kernel_stats.csv", f"{w}_kernel_stats.csv"),
