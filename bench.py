@@ -569,9 +569,9 @@ def fused_chunks(steps):
 
 def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
     """A commit workload stepped through the persistent commit engine (hq_engine_*,
-    dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps' batches are handed over as K
-    descriptors and a STOP (hq_engine_run) and decided by ONE resident launch (no
-    dependent-launch boundary between steps) that ends at the STOP. Beside each engine window, the same K batches as K back-to-back
+    dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps are posted one hq_engine_post call each
+    (post-as-ready, the reference's step-worker shape) and decided by ONE resident launch (no
+    dependent-launch boundary between steps) that the drain's STOP ends. Beside each engine window, the same K batches as K back-to-back
     launches (hq_commit_many_dev), so the line carries both on the same data. `windows` windows
     of K = `steps` steps each continue the rotation (>= 1.1 GiB of distinct batches: no step
     re-reads a batch the 256 MiB Infinity Cache could still hold); the median window is reported
@@ -609,6 +609,7 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
     wins = []
     for k in range(windows):
         a = arr(first + k * steps, steps)
+        a1 = [arr(first + k * steps + i, 1) for i in range(steps)]
         fa = [arr(first + k * steps + c0, cn) for c0, cn in fused_chunks(steps)]
         rec = {}
         for mode in ("engine", "launches", "signal", "fused"):
@@ -623,7 +624,12 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
                 ctx.timing(True)
             t0 = time.perf_counter()
             if mode == "engine":
-                eng.run(a)
+                # post-as-ready: one hq_engine_post per step, as each step worker posts its own
+                # step when it is ready (execengine.go:860-882); the first post launches the
+                # grid, the later ones reach it through the ring; the drain's STOP ends it
+                for one in a1:
+                    eng.post(one)
+                eng.drain()
             elif mode == "signal":
                 q0 = eng_sig.post(a)
                 eng_sig.wait(q0 + steps - 1)       # the last step's flag: every step decided
@@ -714,10 +720,10 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
         achieved_gbs=achieved_local, achieved_node_gbs=achieved_node, per_gpu=per_gpu,
         set0=set0, gather=None, windows=len(wins), headline_mode=hm,
         engine={
-            "mode": "persistent commit engine (hq_engine): the window's steps (one descriptor "
-                    f"per {groups_per_step(w)}-group step, {steps} steps) and a STOP handed to one "
-                    "launch (hq_engine_run), decided step after step by the resident grid, which "
-                    "ends at the STOP",
+            "mode": "persistent commit engine (hq_engine), post-as-ready: the window's "
+                    f"{steps} steps ({groups_per_step(w)} groups each) posted one hq_engine_post "
+                    "call per step as the step workers would; the first post launches the grid, "
+                    "the others reach it through the pinned ring, and the drain's STOP ends it",
             "groups_per_step": groups_per_step(w), "steps_per_window": steps,
             "grid": info.grid, "block": info.block,
             "window_ms": [round(x["engine"]["elapsed"] * 1e3, 4) for x in wins],
@@ -2149,7 +2155,7 @@ def report(args, d, res, launcher):
             "kernel_time": ("HIP events around the fused launch(es) of the median window, / "
                             "steps" if r.get("headline_mode") == "fused" else
                             "HIP events around the resident engine launch of the median "
-                            "window (its steps + STOP, hq_engine_run), / steps" if r.get("engine") else
+                            "window (steps posted one by one, then STOP), / steps" if r.get("engine") else
                             "HIP events on the launch stream around the timed launches "
                             "(back to back), / launches"),
             "achieved_scope": f"sum over {d.world} GPU(s) of bytes per launch / kernel time",

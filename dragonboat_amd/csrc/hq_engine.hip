@@ -341,6 +341,37 @@ __device__ uint64_t frontier(GlobalEngineK &e, EngineLds &l, uint64_t s, uint32_
     return k;
 }
 
+// The workgroup's look-ahead (one wave, at its step transition to step s): when no step beyond s
+// is known, workgroup 0 relays what the host has posted, and the workgroup installs what has been
+// relayed — the frontier's work, done while the other waves still decide tiles. Skipped while the
+// workgroup's poller holds the lock (it is doing the same).
+__device__ void refresh(GlobalEngineK &e, EngineLds &l, uint64_t s, uint32_t lane) {
+    if (uniform64(lds_known(l)) > s + 1) return;
+    uint32_t got = 0;
+    if (lane == 0)
+        got = __hip_atomic_exchange(&l.lock, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+    if (!wave_u32(got)) return;
+    const uint64_t k = uniform64(lds_known(l));
+    if (blockIdx.x == 0) relay(e, lane);
+    const uint64_t p = uniform64(__hip_atomic_load(gp(e.d_polled) + (blockIdx.x % kPollCopies) * kPollStride,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (p > k) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint64_t dmask = e.depth - 1;
+        for (uint64_t i = lane >> 3; i < p - k; i += 8) {
+            const uint64_t slot = (k + i) & dmask;
+            reinterpret_cast<uint64_t *>(l.ring + slot)[lane & 7] = __hip_atomic_load(
+                reinterpret_cast<const uint64_t *>(gp(e.d_ring) + slot) + (lane & 7),
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            install(e, l, k, p);
+            __hip_atomic_store(&l.known, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    if (lane == 0) __hip_atomic_store(&l.lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // the next ticket of the workgroup, for the whole wave
 __device__ __forceinline__ uint32_t claim(EngineLds &l, uint32_t lane) {
     uint32_t t = 0;
@@ -378,6 +409,9 @@ void k_commit_engine(const EngineK e) {
         l.known = top > s0 ? top : s0;
     }
     __syncthreads();
+    // (workgroup 0 relays once at the start: steps posted one call each right after the launch
+    // are then in the device ring when the other workgroups first look ahead)
+    if (blockIdx.x == 0 && wv == 0) refresh(kargs(), l, s0, lane);
     uint64_t s = s0;          // the step of the wave's ticket (or the first it may be in)
     uint64_t known = s0;      // descriptors the wave has seen as known
     uint32_t e_prev = 0;      // the workgroup's tickets before step s
@@ -475,6 +509,11 @@ void k_commit_engine(const EngineK e) {
         }
         e_prev = e_cur;
         ++s;
+        // Steps posted one at a time reach a working grid one relay at a time: the first wave
+        // of each workgroup looks ahead at its step transitions, while its other waves work on
+        // (refresh), so that the workgroup seldom runs out of known steps and stalls at its
+        // frontier for a relay round trip and a polling sleep (post-as-ready windows)
+        if (wv == 0) refresh(kargs(), l, s, lane);
     }
     drain();
     if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
