@@ -1394,9 +1394,14 @@ class CommitMirror:
 
     def step(self, res):
         """(commits, ReadyToReads, sum of advances, ready digest, commit digest) of one step."""
+        from dragonboat_amd import hipquorum as hq
         n_c = n_r = adv_sum = rd = cd = 0
         for i, r in enumerate(res):
             lo, hi = self.bounds[i], self.bounds[i + 1]
+            # ReadyToReads as 24-byte records (HQ_WORKER_READY_COMPACT): the cluster id and the
+            # index rebuilt from the group's position and its committed index before the step
+            ready = (hq.expand_ready(r["ready_compact"], self.cids[lo:hi], self.c[lo:hi])
+                     if "ready_compact" in r else r["ready"])
             if "committed_advance" in r:
                 ix = np.arange(lo, hi)
                 adv = r["committed_advance"][:hi - lo].astype(np.uint64)
@@ -1412,8 +1417,8 @@ class CommitMirror:
             n_c += int(r.get("n_commits", len(r["commits"])))
             adv_sum += int(adv.sum(dtype=np.uint64))
             cd += int((self.coef[ix] * adv).sum(dtype=np.uint64))
-            n_r += len(r["ready"])
-            rd += ready_digest(r["ready"])
+            n_r += len(ready)
+            rd += ready_digest(ready)
         m = (1 << 64) - 1
         return (n_c, n_r, adv_sum & m, rd & m, cd & m)
 
@@ -1507,7 +1512,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             ws = []
             for i in range(W):
                 wk = hq.Worker(d.device, n_voting, on_device=True, commit_column=True,
-                               commit_advance=True)
+                               commit_advance=True, ready_compact=True)
                 wk.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
                 ws.append(wk)
             return ws

@@ -37,7 +37,8 @@ struct hq_dstep;                      // device buffers of one worker
 
 struct hq_dstep_out {                 // the lists of one step, in input group order, in the
     const hq_commit_event *commits;   // engine's pinned host buffer (valid until its next step)
-    const hq_ready_to_read *ready;
+    const hq_ready_to_read *ready;    // (NULL when the records are compact)
+    const hq_ready_compact *ready_compact;
     const hq_read_index_resp *resps;
     const hq_state_change *states;
     const hq_dropped_read *dropped;
@@ -70,7 +71,8 @@ struct hq_dstep_in {
 };
 
 // commit_column: bit 1 a step may return its commits as a column (HQ_WORKER_COMMIT_COLUMN), bit 2
-// as a column of advances (HQ_WORKER_COMMIT_ADVANCE)
+// as a column of advances (HQ_WORKER_COMMIT_ADVANCE), bit 4 its ReadyToReads as 24-byte records
+// (HQ_WORKER_READY_COMPACT)
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column = 0);
 void hq_dstep_close(hq_dstep *d);
 // copy group records [g0, g0 + ng) with their reads (kDReads per group) and member records

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <new>
+#include <thread>
 
 #include <hipcub/hipcub.hpp>
 
@@ -107,6 +108,9 @@ struct StepK {
     // one word per pass A launch `chunk`; k_step_lite zeroes them)
     uint32_t spec_ready, chunk;
     uint64_t ready_off;
+    // HQ_WORKER_READY_COMPACT: pass A flags a ReadyToRead whose index - the group's committed
+    // index before the step does not fit 32 bits (the step then keeps the 32-byte records)
+    uint32_t *ready_wide;
     uint64_t *tiles;              // per tile: step_no << 32 | chunk << 29 | inclusive << 28 | count
     uint32_t *tickets;            // [kTickets]
 };
@@ -129,8 +133,10 @@ struct Layout {
     uint32_t error, overflow;
     uint32_t commit_column;       // the commits list is a column: one word per listed group
                                   // (kColumn64: the committed index, kColumn32: its advance)
+    uint32_t ready_compact;       // the ReadyToReads are hq_ready_compact records
 };
 constexpr uint32_t kColumn64 = 1, kColumn32 = 2;
+constexpr uint32_t kReadyCompact = 4;   // allow_column bit: HQ_WORKER_READY_COMPACT
 
 __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
     return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
@@ -300,6 +306,7 @@ struct Engine {
     // whose writes cross PCIe as small packets
     hq_ready_to_read *stage = nullptr;
     uint32_t stage_lo = 0;
+    uint64_t c0 = 0;              // the group's committed index before the step
 
     __device__ __forceinline__ Engine(const StepK &k, uint64_t idx, uint32_t h, hq_dread *reads)
         : a(k), i(idx), rd(reads) {
@@ -356,8 +363,13 @@ struct Engine {
     __device__ __forceinline__ void ready(uint64_t index, uint64_t low, uint64_t high) {
         const uint32_t p = slot(kReady);
         const hq_ready_to_read r{g.cluster_id, index, low, high};
+        const int64_t delta = (int64_t)(index - c0);
         if (!WRITE) {
             if (p == 0) a.ready_slot[i] = r;              // k_step_lite copies it out
+            if (a.ready_wide && delta != (int64_t)(int32_t)delta) atomicOr(a.ready_wide, 1u);
+        } else if (a.layout->ready_compact) {
+            list<hq_ready_compact>(kReady)[p] =
+                hq_ready_compact{low, high, (uint32_t)i, (int32_t)delta};
         } else if (stage && p - stage_lo < kStageReady) {
             stage[p - stage_lo] = r;
         } else {
@@ -572,7 +584,7 @@ struct Engine {
     // that does not decode is a fallback like one the path does not take
     template <bool STREAM>
     __device__ __forceinline__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
-        const uint64_t committed0 = g.committed;
+        const uint64_t committed0 = c0 = g.committed;
         DPrev pv;
         ByteReader br{p, end};
         for (uint64_t e = e0; e < e1; ++e) {
@@ -876,7 +888,7 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
         // list mode: the wave's groups are consecutive and so are their records, staged from its
         // first active lane's on; column mode: the groups replayed are a sparse subset whose records
         // lie between k_step_lite's, so each is stored where it goes
-        const bool staged = WRITE && !a.layout->commit_column;
+        const bool staged = WRITE && !a.layout->commit_column && !a.layout->ready_compact;
         if (staged) {
             eng.stage = stage[threadIdx.x >> 6];
             eng.stage_lo = __builtin_amdgcn_readfirstlane(eng.base[kReady]);
@@ -1016,18 +1028,38 @@ __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk, uint32
         const uint32_t lo = a.scan[l * a.nw + w] - a.scan[l * a.nw];
         const uint32_t cnt = a.scan[l * a.nw + w + 1] - a.scan[l * a.nw + w];   // the wave's
         hq_ready_to_read *st = stage[threadIdx.x >> 6];
-        hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.layout->off[kReady]);
         const uint32_t pos = lo + pre_ready;
-        if (rr & 4) {
-            if (pos - lo < kStageReady) st[pos - lo] = a.ready_slot[i];
-            else dst[pos] = a.ready_slot[i];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
         const uint32_t nrec = min(cnt, kStageReady);
-        const uint4 *src = reinterpret_cast<const uint4 *>(st);
-        uint4 *out = reinterpret_cast<uint4 *>(dst + lo);
-        for (uint32_t q = lane; q < 2 * nrec; q += 64) out[q] = src[q];
+        if (a.layout->ready_compact) {
+            // 24-byte records (the group's position and index - its committed index before the
+            // step, which pass A saved), stored as 8-byte lane words
+            hq_ready_compact *stc = reinterpret_cast<hq_ready_compact *>(st);
+            hq_ready_compact *dst = reinterpret_cast<hq_ready_compact *>(a.out + a.layout->off[kReady]);
+            if (rr & 4) {
+                const hq_ready_to_read r = a.ready_slot[i];
+                const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
+                const hq_ready_compact c{r.ctx_low, r.ctx_high, (uint32_t)i,
+                                         (int32_t)(int64_t)(r.index - a.groups_old[h].committed)};
+                if (pos - lo < kStageReady) stc[pos - lo] = c;
+                else dst[pos] = c;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const uint2 *src = reinterpret_cast<const uint2 *>(stc);
+            uint2 *out = reinterpret_cast<uint2 *>(dst + lo);
+            for (uint32_t q = lane; q < 3 * nrec; q += 64) out[q] = src[q];
+        } else {
+            hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.layout->off[kReady]);
+            if (rr & 4) {
+                if (pos - lo < kStageReady) st[pos - lo] = a.ready_slot[i];
+                else dst[pos] = a.ready_slot[i];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const uint4 *src = reinterpret_cast<const uint4 *>(st);
+            uint4 *out = reinterpret_cast<uint4 *>(dst + lo);
+            for (uint32_t q = lane; q < 2 * nrec; q += 64) out[q] = src[q];
+        }
     }
     if (!in) return;
     if (!(col32 && a.spec_valid)) {   // (pass A wrote the advance words)
@@ -1088,7 +1120,10 @@ constexpr uint64_t kChunkGroups = 65536;
 __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, uint64_t cap,
                             uint32_t allow_column, Layout *lay, Layout *host_lay) {
     uint32_t *wide = error + 1;   // pass A: an advance of 2^32 or more
-    const uint64_t rec[kLists] = {sizeof(hq_commit_event), sizeof(hq_ready_to_read),
+    uint32_t *ready_wide = error + 2;   // pass A: a ReadyToRead delta beyond 32 bits
+    lay->ready_compact = (allow_column & kReadyCompact) && !*ready_wide;
+    const uint64_t rec[kLists] = {sizeof(hq_commit_event),
+                                  lay->ready_compact ? sizeof(hq_ready_compact) : sizeof(hq_ready_to_read),
                                   sizeof(hq_read_index_resp), sizeof(hq_state_change),
                                   sizeof(hq_dropped_read), 8, 8, 0, 0};
     uint64_t total = 0;
@@ -1117,6 +1152,7 @@ __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, ui
     if (!(lay->overflow && !*error)) {
         *error = 0;
         *wide = 0;
+        *ready_wide = 0;
     }
     *host_lay = *lay;             // the host's copy, written into pinned memory (no copy launch)
 }
@@ -1382,17 +1418,19 @@ namespace {
 
 // Wait for a stream: poll briefly (a one-worker step's sync is short), then sleep on a
 // blocking-sync event, so that 16 workers waiting at once do not spin 16 host cores (a spinning
-// wait under a CPU quota stalls every thread of the process for the rest of the period)
-int wait_stream(hq_dstep *d, hipStream_t s, const char *what) {
+// wait under a CPU quota stalls every thread of the process for the rest of the period). spin_us
+// above 50: the poll yields now and then (the jobs path's one waiter, HQ_STEP_JOBS_SPIN_US)
+int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us = 50) {
     hq_ctx *ctx = d->ctx;
     int rc = hq::check_hip(ctx, hipEventRecord(d->ev_sync, s), what);
     if (rc) return rc;
     const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
+    for (uint32_t k = 0;; ++k) {
         const hipError_t q = hipEventQuery(d->ev_sync);
         if (q == hipSuccess) return HQ_OK;
         if (q != hipErrorNotReady) return hq::check_hip(ctx, q, what);
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
+        if (spin_us > 50 && (k & 15) == 15) std::this_thread::yield();
     }
     return hq::check_hip(ctx, hipEventSynchronize(d->ev_sync), what);
 }
@@ -1615,7 +1653,7 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
         if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&d->scan), &sc, cn * 4, false, "hq_dstep scan");
         if (!rc && !d->bases) {
             rc = grow(ctx, reinterpret_cast<void **>(&d->bases), &bc, 256, false, "hq_dstep error");
-            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 8, s), "memset");
+            if (!rc) rc = hq::check_hip(ctx, hipMemsetAsync(d->bases, 0, 256, s), "memset");
         }
         if (!rc) d->cnt_cap = std::min(cc, sc) / 4;
     }
@@ -1732,7 +1770,10 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
     // (not the jobs path: there pass A reads the streams over the link in place, and these
     // writes beside its reads slowed it by more than k_step_lite's copy takes, 981 vs 693 + 158
     // us for the 16-worker step5, profiles/r05e)
-    k.spec_ready = !jobs && stream && k.spec_col && ne < kTileVal && spec_ready_allowed();
+    // (nor with compact ReadyToReads, whose record size the layout picks after pass A)
+    k.spec_ready = !jobs && stream && k.spec_col && ne < kTileVal && spec_ready_allowed() &&
+                   !(d->commit_column & kReadyCompact);
+    k.ready_wide = (d->commit_column & kReadyCompact) ? d->bases + 2 : nullptr;   // (zero: k_layout)
     k.ready_off = (n * 4 + 255) & ~uint64_t(255);   // layout_from's offset of the list after the column
     k.tiles = d->tiles;
     k.tickets = d->tickets;
@@ -1839,6 +1880,18 @@ const T *pinned_on_device(const T *p) {
                                        (reinterpret_cast<const char *>(p) - hp));
 }
 
+// HQ_STEP_JOBS_SPIN_US: how long the jobs path's one waiting thread polls before it sleeps on the
+// blocking event (default 50 us, as the per-worker waits). Polling through the whole step
+// (5000) gained nothing device-only and cost end to end: the poller takes a core from the
+// producer's encode (tools/ab_spin.sh, step5 e2e 5.16 -> 5.37 ms)
+uint32_t jobs_spin_us() {
+    static const uint32_t us = [] {
+        const char *v = std::getenv("HQ_STEP_JOBS_SPIN_US");
+        return v ? (uint32_t)std::atoi(v) : 50u;
+    }();
+    return us;
+}
+
 // HQ_STEP_SINGLE_JOBS=0 in the environment: a single pinned sized step takes the copy path (A/B)
 bool single_as_job_allowed() {
     static const bool on = [] {
@@ -1900,7 +1953,11 @@ int finish(Run &r) {
                           ? reinterpret_cast<const uint64_t *>(ho + lay.off[kCommits]) : nullptr;
     out->commit_adv = lay.commit_column == kColumn32
                           ? reinterpret_cast<const uint32_t *>(ho + lay.off[kCommits]) : nullptr;
-    out->ready = reinterpret_cast<const hq_ready_to_read *>(ho + lay.off[kReady]);
+    out->ready = lay.ready_compact ? nullptr
+                                   : reinterpret_cast<const hq_ready_to_read *>(ho + lay.off[kReady]);
+    out->ready_compact = lay.ready_compact
+                             ? reinterpret_cast<const hq_ready_compact *>(ho + lay.off[kReady])
+                             : nullptr;
     out->resps = reinterpret_cast<const hq_read_index_resp *>(ho + lay.off[kResps]);
     out->states = reinterpret_cast<const hq_state_change *>(ho + lay.off[kStates]);
     out->dropped = reinterpret_cast<const hq_dropped_read *>(ho + lay.off[kDropped]);
@@ -2275,7 +2332,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     tp[3] = now_ns();
     uint64_t gpu_ns = 0;
     if (!rc) {
-        rc = wait_stream(d0, s, "hq_dstep jobs sync");
+        rc = wait_stream(d0, s, "hq_dstep jobs sync", jobs_spin_us());
         if (!rc) gpu_ns = elapsed_ns(d0->ev_t0, d0->ev_t1);
     } else {                      // (a failed launch sequence leaves no copy behind either)
         (void)hipStreamSynchronize(s);

@@ -97,7 +97,11 @@ template <class From>
 inline uint8_t *put_run(uint8_t *p, uint32_t m, From from) {
     *p++ = (uint8_t)(HQ_EV_MESSAGE | kCodeRun << 3);
     *p++ = (uint8_t)m;                  // m <= kRunMax: one byte
-    for (uint32_t j = 0; j < m; ++j) p = put(p, from(j));
+    for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t f = from(j);
+        if (f < 0x80) *p++ = (uint8_t)f;   // (a node id: one byte in the steady state)
+        else p = put(p, f);
+    }
     return p;
 }
 

@@ -911,6 +911,7 @@ int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *
     out->committed_column = dout.commit_col;
     out->committed_advance = dout.commit_adv;
     out->ready = dout.ready;
+    out->ready_compact = dout.ready_compact;
     out->n_ready = dout.n_ready;
     out->read_resps = dout.resps;
     out->n_read_resps = dout.n_resps;
@@ -944,8 +945,11 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
 
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out) {
     if (!out) return HQ_E_INVAL;
-    if (flags & ~(HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_COLUMN | HQ_WORKER_COMMIT_ADVANCE))
+    if (flags & ~(HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_COLUMN | HQ_WORKER_COMMIT_ADVANCE |
+                  HQ_WORKER_READY_COMPACT))
         return HQ_E_INVAL;
+    if ((flags & HQ_WORKER_READY_COMPACT) && !(flags & HQ_WORKER_ON_DEVICE))
+        return HQ_E_INVAL;            // (the compact records are the device step's form)
     *out = nullptr;
     if (n_max < 1 || n_max > HQ_MAX_VOTERS) return HQ_E_INVAL;
     hq_worker *w = new (std::nothrow) hq_worker();
@@ -960,7 +964,8 @@ int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **ou
     if (flags & HQ_WORKER_ON_DEVICE) {
         rc = hq_dstep_open(w->ctx, &w->dstep,
                            ((flags & HQ_WORKER_COMMIT_COLUMN) ? 1u : 0u) |
-                               ((flags & HQ_WORKER_COMMIT_ADVANCE) ? 2u : 0u));
+                               ((flags & HQ_WORKER_COMMIT_ADVANCE) ? 2u : 0u) |
+                               ((flags & HQ_WORKER_READY_COMPACT) ? 4u : 0u));
         if (rc) {
             hq_close(w->ctx);
             delete w;

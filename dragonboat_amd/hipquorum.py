@@ -42,7 +42,8 @@ HQ_INGEST_BINNED = 8         # hq_table_ingest_*: the two-pass binned kernels, f
 HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and events on the GPU
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
-HQ_ABI_VERSION = 19
+HQ_WORKER_READY_COMPACT = 8  # with it: ReadyToReads as 24-byte records (position, delta, ctx)
+HQ_ABI_VERSION = 20
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -166,6 +167,9 @@ READ_STATUS_DTYPE = np.dtype([("index", "<u8"), ("from", "<u8"), ("ctx_low", "<u
 COMMIT_EVENT_DTYPE = np.dtype([("cluster_id", "<u8"), ("committed", "<u8")], align=True)
 READY_DTYPE = np.dtype([("cluster_id", "<u8"), ("index", "<u8"), ("ctx_low", "<u8"),
                         ("ctx_high", "<u8")], align=True)
+READY_COMPACT_DTYPE = np.dtype([("ctx_low", "<u8"), ("ctx_high", "<u8"), ("pos", "<u4"),
+                                ("delta", "<i4")], align=True)
+assert READY_COMPACT_DTYPE.itemsize == 24
 READ_RESP_DTYPE = np.dtype([("cluster_id", "<u8"), ("to", "<u8"), ("log_index", "<u8"),
                             ("hint", "<u8"), ("hint_high", "<u8")], align=True)
 STATE_CHANGE_DTYPE = np.dtype([("cluster_id", "<u8"), ("term", "<u8"), ("state", "<u4"),
@@ -232,6 +236,21 @@ STEP_OUTPUT_LISTS = [("commits", COMMIT_EVENT_DTYPE), ("ready", READY_DTYPE),
                      ("fallback_groups", np.dtype("<u8"))]
 
 
+def expand_ready(compact, cluster_ids, committed_before):
+    """HQ_WORKER_READY_COMPACT records -> READY_DTYPE records: cluster_ids[pos] and
+    committed_before[pos] + delta (the listed groups' cluster ids and committed indexes before
+    the step, in list order)."""
+    out = np.zeros(len(compact), READY_DTYPE)
+    pos = compact["pos"].astype(np.int64)
+    out["cluster_id"] = np.asarray(cluster_ids, np.uint64)[pos]
+    # (mod 2^64, as the device computed index - committed)
+    out["index"] = np.asarray(committed_before, np.uint64)[pos] + \
+        compact["delta"].astype(np.int64).astype(np.uint64)
+    out["ctx_low"] = compact["ctx_low"]
+    out["ctx_high"] = compact["ctx_high"]
+    return out
+
+
 class StepOutput(ctypes.Structure):
     """Mirror of ``hq_step_output``."""
 
@@ -241,7 +260,7 @@ class StepOutput(ctypes.Structure):
                 ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64),
                 ("pack_ns", ctypes.c_uint64), ("device_ns", ctypes.c_uint64),
                 ("apply_ns", ctypes.c_uint64), ("committed_column", _vp),
-                ("committed_advance", _vp)]
+                ("committed_advance", _vp), ("ready_compact", _vp)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -1356,17 +1375,21 @@ class Worker:
     every quorum decision taken by the kernels."""
 
     def __init__(self, device: int = 0, n_max: int = 8, on_device: bool = False,
-                 commit_column: bool = False, commit_advance: bool = False):
+                 commit_column: bool = False, commit_advance: bool = False,
+                 ready_compact: bool = False):
         """on_device: HQ_WORKER_ON_DEVICE, the group state resident on the GPU and every event
         taken there (hq_dstep.hip); otherwise the host worker (events on the host, decisions
         in GPU passes). commit_column: HQ_WORKER_COMMIT_COLUMN (results carry
         'committed_column' instead of 'commits' when most listed groups commit);
         commit_advance: HQ_WORKER_COMMIT_ADVANCE ('committed_advance', u32 per listed group,
-        when more than a quarter of them commit)."""
+        when more than a quarter of them commit); ready_compact: HQ_WORKER_READY_COMPACT (results
+        carry 'ready_compact', READY_COMPACT_DTYPE, instead of 'ready'; expand_ready rebuilds
+        the records)."""
         self.h = _vp()
         flags = (HQ_WORKER_ON_DEVICE if on_device else 0) | \
             (HQ_WORKER_COMMIT_COLUMN if commit_column else 0) | \
-            (HQ_WORKER_COMMIT_ADVANCE if commit_advance else 0)
+            (HQ_WORKER_COMMIT_ADVANCE if commit_advance else 0) | \
+            (HQ_WORKER_READY_COMPACT if ready_compact else 0)
         rc = lib.hq_worker_open_ex(device, n_max, flags, ctypes.byref(self.h))
         if rc != HQ_OK:
             raise HQError(rc, "hq_worker_open: " + lib.hq_last_error(None).decode())
@@ -1473,7 +1496,8 @@ class Worker:
         for name, dt in STEP_OUTPUT_LISTS:
             n = getattr(out, "n_" + name)
             ptr = getattr(out, name)
-            if n == 0 or (name == "commits" and (out.committed_column or out.committed_advance)):
+            if n == 0 or (name == "commits" and (out.committed_column or out.committed_advance)) \
+                    or (name == "ready" and out.ready_compact):
                 res[name] = np.zeros(0, dt)
                 continue
             buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
@@ -1491,6 +1515,11 @@ class Worker:
             col = np.frombuffer(buf, np.uint32)
             res["committed_advance"] = col.copy() if copy else col
             res["n_commits"] = out.n_commits
+        if out.ready_compact:
+            n = out.n_ready
+            buf = (ctypes.c_char * (n * READY_COMPACT_DTYPE.itemsize)).from_address(out.ready_compact)
+            rc = np.frombuffer(buf, READY_COMPACT_DTYPE)
+            res["ready_compact"] = rc.copy() if copy else rc
         return res
 
     def add_groups(self, groups: np.ndarray, members: np.ndarray) -> None:

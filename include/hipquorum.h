@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 19
+#define HQ_ABI_VERSION 20
 
 /* status codes */
 #define HQ_OK          0
@@ -929,6 +929,15 @@ typedef struct hq_commit_event { uint64_t cluster_id, committed; } hq_commit_eve
 typedef struct hq_ready_to_read {   /* pb.ReadyToRead (raftpb/raft.go:54-57) */
     uint64_t cluster_id, index, ctx_low, ctx_high;
 } hq_ready_to_read;
+/* HQ_WORKER_READY_COMPACT: a ReadyToRead in 24 bytes. The host holds the rest: the group is the
+ * pos-th of the step's list (its cluster id is the worker's), and the index is the group's
+ * committed index before the step plus delta (a ReadIndex records the committed index when it
+ * is received, raft.go:1636-1669; the host holds that committed index to apply entries) */
+typedef struct hq_ready_compact {
+    uint64_t ctx_low, ctx_high;
+    uint32_t pos;
+    int32_t delta;
+} hq_ready_compact;
 typedef struct hq_read_index_resp { /* ReadIndexResp to a remote requester (raft.go:1751-1757) */
     uint64_t cluster_id, to, log_index, hint, hint_high;
 } hq_read_index_resp;
@@ -974,6 +983,10 @@ typedef struct hq_step_output {
      * advance] are committed); `commits` and `committed_column` are then NULL and n_commits
      * counts the nonzero words */
     const uint32_t *committed_advance;
+    /* HQ_WORKER_READY_COMPACT workers only, else NULL: the step's ReadyToReads as 24-byte
+     * records (hq_ready_compact, in the order of `ready`); `ready` is then NULL and n_ready
+     * counts them. A step in which some record's delta does not fit 32 bits keeps `ready` */
+    const hq_ready_compact *ready_compact;
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;
@@ -997,6 +1010,9 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
  * returns its commits as hq_step_output.committed_advance (4 bytes per listed group); other steps,
  * and a step in which some group's committed index advances by 2^32 or more, keep the list */
 #define HQ_WORKER_COMMIT_ADVANCE 4u
+/* with HQ_WORKER_ON_DEVICE: the ReadyToReads as hq_step_output.ready_compact (24 bytes each
+ * across PCIe instead of 32: the cluster id and the index are the host's already) */
+#define HQ_WORKER_READY_COMPACT 8u
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out);
 void hq_worker_close(hq_worker *w);
 const char *hq_worker_last_error(const hq_worker *w);

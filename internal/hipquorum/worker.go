@@ -51,13 +51,15 @@ func OpenWorker(device, nMax int) (*Worker, error) {
 // OpenDeviceWorker opens a worker whose groups' quorum state is resident in HBM: one GPU thread
 // per group takes its events in order, every decision at the event that triggers it
 // (hq_dstep.hip); commits come back as 4-byte advances when a quarter of the listed groups
-// commit, else as one word per listed group or as records.
+// commit, else as one word per listed group or as records; ReadyToReads as 24-byte records
+// (EachReady).
 func OpenDeviceWorker(device, nMax int) (*Worker, error) {
 	if err := checkABI(); err != nil {
 		return nil, err
 	}
 	var w *C.hq_worker
-	flags := C.uint32_t(C.HQ_WORKER_ON_DEVICE | C.HQ_WORKER_COMMIT_ADVANCE | C.HQ_WORKER_COMMIT_COLUMN)
+	flags := C.uint32_t(C.HQ_WORKER_ON_DEVICE | C.HQ_WORKER_COMMIT_ADVANCE | C.HQ_WORKER_COMMIT_COLUMN |
+		C.HQ_WORKER_READY_COMPACT)
 	if rc := C.hq_worker_open_ex(C.int(device), C.uint32_t(nMax), flags, &w); rc != C.HQ_OK {
 		return nil, errors.New(C.GoString(C.hq_last_error(nil)))
 	}
@@ -317,12 +319,37 @@ func (o *Output) EachCommit(committedOf func(i int) uint64, listedOf func(cluste
 	}
 }
 
-// ReadyToRead lists the step's released reads (pb.ReadyToRead, raftpb/raft.go:54-57).
+// ReadyToRead lists the step's released reads (pb.ReadyToRead, raftpb/raft.go:54-57) when the
+// step returned them as full records (nil when they are compact: EachReady reads both).
 func (o *Output) ReadyToRead() []C.hq_ready_to_read {
-	if o.c.n_ready == 0 {
+	if o.c.n_ready == 0 || o.c.ready == nil {
 		return nil
 	}
 	return unsafe.Slice(o.c.ready, int(o.c.n_ready))
+}
+
+// EachReady calls fn(listed index, pb.ReadyToRead) for every released read of the step, in the
+// reference's order, whichever form the step returned: the 24-byte records (HQ_WORKER_READY_COMPACT:
+// the index is the group's committed index before the step, committedBefore, plus the record's
+// delta) or the full records (listedOf maps a cluster id to its listed index).
+func (o *Output) EachReady(committedBefore func(i int) uint64, listedOf func(clusterID uint64) int,
+	fn func(i int, r pb.ReadyToRead)) {
+	if o.c.n_ready == 0 {
+		return
+	}
+	if o.c.ready_compact != nil {
+		recs := unsafe.Slice(o.c.ready_compact, int(o.c.n_ready))
+		for _, r := range recs {
+			i := int(r.pos)
+			fn(i, pb.ReadyToRead{Index: committedBefore(i) + uint64(int64(r.delta)),
+				SystemCtx: pb.SystemCtx{Low: uint64(r.ctx_low), High: uint64(r.ctx_high)}})
+		}
+		return
+	}
+	for _, r := range unsafe.Slice(o.c.ready, int(o.c.n_ready)) {
+		fn(listedOf(uint64(r.cluster_id)), pb.ReadyToRead{Index: uint64(r.index),
+			SystemCtx: pb.SystemCtx{Low: uint64(r.ctx_low), High: uint64(r.ctx_high)}})
+	}
 }
 
 // StateChanges lists the step's leader / follower / candidate transitions.

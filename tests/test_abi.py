@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 19
+    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 20
 
 
 LAYOUT_C = r"""

@@ -757,3 +757,126 @@ def test_failed_regrow_leaves_state(hq, monkeypatch):
     finally:
         a.close()
         b.close()
+
+
+def _expand(hq, got, cids, committed_before):
+    """A compact step's ReadyToReads as full records (hq.expand_ready over the listed groups)."""
+    if "ready_compact" not in got:
+        return got["ready"]
+    assert len(got["ready"]) == 0
+    return hq.expand_ready(got["ready_compact"], cids, committed_before)
+
+
+@pytest.mark.parametrize("G,pinned", [(5000, False), (4 * 65536 + 5, False),
+                                      (4 * 65536 + 5, True)],
+                         ids=["small", "chunked-copy", "pinned-job"])
+def test_ready_compact_equals_records(hq, G, pinned):
+    """HQ_WORKER_READY_COMPACT: the 24-byte ReadyToReads (the group's position, index - its
+    committed index before the step, the ctx) rebuild exactly the 32-byte records of a worker
+    without the flag, step after step (the single-ReadyToRead groups copied out by k_step_lite,
+    pass B's replayed groups, the copy path and the pinned one-job path); every other list and
+    the commits are unchanged."""
+    import bench
+
+    roles = bench.STEP_ROLES["step5"]
+    g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
+    nv = sum(r != "observer" for r in roles)
+    a = hq.Worker(0, nv, on_device=True, commit_advance=True, ready_compact=True)
+    b = hq.Worker(0, nv, on_device=True, commit_advance=True)
+    pin = hq.Context(0) if pinned else None
+    committed = g["committed"].astype(np.uint64).copy()
+    try:
+        a.add_groups(g, m)
+        b.add_groups(g, m)
+        for s in range(3):
+            grp, off, ev = bench.step_events(hq, G, s, roles)
+            if s == 2:
+                # group 8 gets a follower's ReadIndex ahead of its local read: the heartbeat
+                # acks release both, so the group has a ReadIndexResp besides its ReadyToRead
+                # and pass B replays it (its compact record written by pass B itself)
+                lo = int(off[8])
+                assert ev["kind"][lo] == hq.EV_READ and ev["type"][lo + 1] == 13
+                fwd = ev[lo + 1].copy()
+                fwd["type"], fwd["hint"], fwd["hint_high"], fwd["log_index"] = 19, 99, 0, 0
+                ev[lo + 1] = ev[lo]
+                ev[lo] = fwd
+            data, sz = hq.encode_events_sized(off, ev)
+            if pinned:
+                pd, ps = pin.pinned(len(data), np.uint8), pin.pinned(len(sz), np.uint32)
+                pd[:], ps[:] = data, sz
+                data, sz = pd, ps
+            got = a.step_sized(None, sz, len(ev), data)
+            want = b.step_sized(None, sz, len(ev), data)
+            assert "ready_compact" in got and len(want["ready"]) > G // 5
+            if s == 2:
+                assert len(want["read_resps"]) == 1
+            np.testing.assert_array_equal(_expand(hq, got, cids, committed), want["ready"],
+                                          err_msg=f"step {s}")
+            for k in ("read_resps", "state_changes", "dropped_reads", "deferred", "fallback_groups"):
+                np.testing.assert_array_equal(got[k], want[k], err_msg=f"step {s} {k}")
+            for k in ("committed_advance", "commits"):
+                if k in want:
+                    np.testing.assert_array_equal(got[k], want[k], err_msg=f"step {s} {k}")
+            if "committed_advance" in want:
+                committed += want["committed_advance"].astype(np.uint64)
+            else:
+                ix = want["commits"]["cluster_id"].astype(np.int64) - 1
+                committed[ix] = want["commits"]["committed"]
+    finally:
+        a.close()
+        b.close()
+        if pin:
+            pin.close()
+
+
+def test_ready_compact_wide_delta_keeps_records(hq):
+    """A ReadyToRead whose index lies 2^33 above its group's committed index before the step (the
+    group commits 2^33 entries in the step and then receives a ReadIndex): the delta does not fit
+    the compact record, so the step returns the 32-byte records — equal to a worker's without the
+    flag — and the next steps are compact again."""
+    import bench
+
+    G, big, special = 8192, 1 << 33, 4               # group 4 serves a read (every 4th)
+    roles = bench.STEP_ROLES["step"]
+    g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
+    g["committed"] -= np.uint64(10)
+    g["term_start"] = g["committed"]
+    m["match"][m["node_id"] != 1] -= np.uint64(10)
+    g["last_index"][special] = big
+    m["match"][len(roles) * special] = big
+    grp, off, ev = bench.step_events(hq, G, 0, roles)
+    lo, hi = int(off[special]), int(off[special + 1])
+    rows = ev[lo:hi].copy()
+    assert rows["kind"][0] == hq.EV_READ
+    rows["log_index"][(rows["kind"] == hq.EV_MESSAGE) & (rows["type"] == 13)] = big
+    k = len(roles) - 1                                # the ReplicateResps, then the READ
+    ev[lo:hi] = np.concatenate([rows[1:1 + k], rows[:1], rows[1 + k:]])
+    data, sizes = hq.encode_events_sized(off, ev)
+    nv = sum(r != "observer" for r in roles)
+    a = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True, ready_compact=True)
+    b = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True)
+    try:
+        a.add_groups(g, m)
+        b.add_groups(g, m)
+        got = a.step_sized(grp, sizes, len(ev), data)
+        want = b.step_sized(grp, sizes, len(ev), data)
+        assert "ready_compact" not in got
+        np.testing.assert_array_equal(got["ready"], want["ready"])
+        r4 = got["ready"][got["ready"]["cluster_id"] == cids[special]]
+        assert len(r4) == 1 and int(r4["index"][0]) == big
+        before = np.array([a.get_group(int(c))[0]["committed"] for c in cids], np.uint64)
+        grp, off, ev = bench.step_events(hq, G, 1, roles)
+        ev["log_index"][(ev["kind"] == hq.EV_MESSAGE) & (ev["type"] == 13)] = 0   # no commits
+        data, sizes = hq.encode_events_sized(off, ev)
+        got = a.step_sized(grp, sizes, len(ev), data)
+        want = b.step_sized(grp, sizes, len(ev), data)
+        assert "ready_compact" in got
+        np.testing.assert_array_equal(_expand(hq, got, cids, before), want["ready"])
+    finally:
+        a.close()
+        b.close()
+
+
+def test_ready_compact_needs_the_device_worker(hq):
+    with pytest.raises(hq.HQError):
+        hq.Worker(0, 3, on_device=False, ready_compact=True)
