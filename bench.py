@@ -2181,6 +2181,10 @@ def report(args, d, res, launcher):
         line["fused_window"] = r["fused_window"]
     summary = {rec["name"]: _short(rec) for rec in res["records"]}
     detail = dict(line, result_gather=r.get("gather"), extra=res["records"])
+    # (the modes' descriptions stay in the detail file; the line keeps their figures)
+    for k in ("engine", "launch_per_step", "engine_signal", "fused_window"):
+        if k in line:
+            line[k] = {kk: v for kk, v in line[k].items() if kk != "mode"}
     path = args.detail_out
     try:
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
