@@ -424,17 +424,32 @@ struct Engine {
     // raft.tryCommit (raft.go:888-909): the quorum-th largest match of the voting members, then
     // entryLog.tryCommit (logentry.go:378-393) with term(q) == term <=> term_start <= q <= last
     // (the leader's entries carry its term and terms never decrease, entryutils.go:44-47)
+    // The quorum-th largest by an 8-input sorting network (19 compare-exchanges; the slots past
+    // n_voting enter as 0, below or tied with every voting match, so the q-th largest of the 8
+    // is that of the n, q <= n) instead of counting, for every slot, the slots at or above it
+    // (64 compares): the same value, a third of the instructions on every updating ack.
     __device__ __forceinline__ void try_commit() {
+        static_assert(HQ_MAX_VOTERS == 8, "the network sorts 8 voting slots");
         cnt[kDecisions]++;
         const uint32_t n = g.n_voting, q = quorum();
+        uint64_t v[8];
+#pragma unroll
+        for (uint32_t s = 0; s < 8; ++s) v[s] = s < n ? match[s] : 0;
+        auto cx = [&](int i, int j) {                    // v[i] >= v[j] afterwards
+            const uint64_t a = v[i], b = v[j];
+            const bool gt = a > b;
+            v[i] = gt ? a : b;
+            v[j] = gt ? b : a;
+        };
+        cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
+        cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
+        cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
+        cx(2, 4); cx(3, 5);
+        cx(1, 4); cx(3, 6);
+        cx(1, 2); cx(3, 4); cx(5, 6);
         uint64_t best = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < HQ_MAX_VOTERS; ++s) {
-            uint32_t ge = 0;
-#pragma unroll
-            for (uint32_t t = 0; t < HQ_MAX_VOTERS; ++t) ge += t < n && match[t] >= match[s];
-            if (s < n && ge >= q && match[s] > best) best = match[s];
-        }
+        for (uint32_t s = 0; s < 8; ++s) best = s + 1 == q ? v[s] : best;
         if (best > g.committed && best >= g.term_start && best <= g.last)
             g.committed = best;                          // commitTo (logentry.go:323-332)
     }
