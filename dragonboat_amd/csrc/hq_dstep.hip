@@ -1401,6 +1401,7 @@ struct hq_dstep {
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
     // the jobs path (hq_dstep_run_jobs, this engine first): the jobs' StepK, pinned and on device
     StepK *jobs_host = nullptr, *jobs_dev = nullptr;
+    const StepK *jobs_host_dev = nullptr;   // jobs_host's device address (k_size_sums reads it)
     uint32_t jobs_cap = 0;
     // pass A's ticket words (StepK::tickets), zeroed by k_step_lite; a step that stopped before
     // it leaves them to clear (dirty), and pass A's chained-scan words per tile of 256 groups
@@ -2160,12 +2161,16 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         if (d0->jobs_host) (void)hipHostFree(d0->jobs_host);
         if (d0->jobs_dev) (void)hipFree(d0->jobs_dev);
         d0->jobs_host = d0->jobs_dev = nullptr;
+        d0->jobs_host_dev = nullptr;
         d0->jobs_cap = 0;
         rc = hq::check_hip(ctx, hipHostMalloc(&d0->jobs_host, kMaxJobs * sizeof(StepK),
                                               hipHostMallocDefault), "hq_dstep jobs");
         if (!rc) rc = hq::check_hip(ctx, hipMalloc(&d0->jobs_dev, kMaxJobs * sizeof(StepK)),
                                     "hq_dstep jobs");
-        if (!rc) d0->jobs_cap = kMaxJobs;
+        if (!rc) {
+            d0->jobs_cap = kMaxJobs;
+            d0->jobs_host_dev = pinned_on_device(d0->jobs_host);
+        }
     }
     bool small = true;
     uint64_t total_bytes = 0;
@@ -2183,8 +2188,13 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         small = small && r.small;
         total_bytes += r.nb;
     }
-    if (!rc) rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
-                                                    hipMemcpyHostToDevice, s), "hq_dstep jobs");
+    // (the table goes to the device once k_size_sums is queued, which reads it from the pinned
+    // copy: the device starts on the sizes without waiting for the table's copy to be submitted,
+    // ~25 us of host time for a one-worker step)
+    const bool table_first = !d0->jobs_host_dev;
+    if (!rc && table_first)
+        rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
+                                               hipMemcpyHostToDevice, s), "hq_dstep jobs");
     tp[2] = now_ns();
     // maps of jobs [x0, x1) onto workgroups of `per` groups (+ extra elements per job)
     auto map = [&](uint32_t x0, uint32_t x1, uint64_t per, uint64_t extra) {
@@ -2228,14 +2238,16 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     }
     const JobMap sm = map(0, nl, kSizeTile, 1);
     if (!rc) {
-        hipLaunchKernelGGL(k_size_sums, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
+        JobMap pm = sm;
+        if (!table_first) pm.ks = d0->jobs_host_dev;
+        hipLaunchKernelGGL(k_size_sums, dim3(pm.blk0[nl]), dim3(256), 0, s, pm);
         launched("k_size_sums");
     }
     if (!rc) {
         // every job's stream in pinned host memory: pass A (and pass B) read it in place, in one
         // launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks). The table
-        // is sent again with the streams' device addresses (ordered behind k_size_sums, which
-        // does not read them; the first copy may already carry them)
+        // goes to the device with the streams' device addresses (k_size_sums reads none of the
+        // fields written here)
         zero_copy = zero_copy_allowed();
         const uint8_t *zbytes[kMaxJobs] = {};
         for (uint32_t x = 0; x < nl && zero_copy; ++x) {
@@ -2248,9 +2260,10 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                 if (zbytes[x]) r.k.bytes = zbytes[x];
                 d0->jobs_host[x].bytes = r.k.bytes;
             }
+        }
+        if (zero_copy || !table_first)
             rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
                                                    hipMemcpyHostToDevice, s), "hq_dstep jobs");
-        }
     }
     if (zero_copy) {              // one chunk of all jobs, nothing to copy
         cend[nchunks = 1] = nl;
