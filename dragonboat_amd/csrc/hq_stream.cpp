@@ -323,13 +323,16 @@ inline uint64_t encode_unit(uint8_t *&p, const hq_event *events, uint64_t e, uin
     return e + 1;
 }
 
-// groups [g0, g1) encoded at out (cap bytes), or into a growing scratch (grow != nullptr); the
-// range's event count and byte count out (locals until the end: threads encoding neighbouring
-// ranges share no written cache line but their ends of `sizes`)
+// groups [g0, g1) encoded at out (cap bytes), or into a growing scratch (grow != nullptr) from
+// its byte pos0 on (a thread's later pieces follow its earlier ones there); the range's event
+// count and byte count out, its last event's start relative to the range's first byte (locals
+// until the end: threads encoding neighbouring ranges share no written cache line but their ends
+// of `sizes`)
 int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, uint64_t g0,
                 uint64_t g1, std::vector<uint8_t> *grow, uint8_t *out, uint64_t cap,
-                uint64_t *n_events, uint64_t *n_bytes, uint64_t *last_start = nullptr) {
-    uint64_t pos = 0, events = 0, ls = ~0ull;
+                uint64_t *n_events, uint64_t *n_bytes, uint64_t *last_start = nullptr,
+                uint64_t pos0 = 0) {
+    uint64_t pos = pos0, events = 0, ls = ~0ull;
     uint8_t *base = grow ? grow->data() : out;
     for (uint64_t i = g0; i < g1; ++i) {
         const uint64_t r0 = off[i], r1 = off[i + 1];
@@ -373,13 +376,13 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
             p = encode(p, e, pv);
         }
         pos = (uint64_t)(p - base);
-        if (lp) ls = (uint64_t)(lp - base);
+        if (lp) ls = (uint64_t)(lp - base) - pos0;
         if (ne > 0xFFFF || pos - p0 > 0xFFFF) return HQ_E_INVAL;
         sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
         events += ne;
     }
     *n_events = events;
-    *n_bytes = pos;
+    *n_bytes = pos - pos0;
     if (last_start) *last_start = ls;
     return HQ_OK;
 }
@@ -658,25 +661,15 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
         thread_local std::vector<uint8_t> scratch;
         std::vector<Piece> &ps = pieces[t];
         uint64_t pos = 0;
-        std::vector<uint8_t> part;
         for (uint32_t j : live) {
             const uint64_t g0 = gc[j][t], g1 = gc[j][t + 1];
             if (g0 >= g1) continue;
             const hq_encode16_job &b = jobs[j];
             Piece pc{j, pos, 0, 0, ~0ull, HQ_OK};
-            // (the piece is encoded after the thread's earlier pieces: into a scratch of its
-            // own, then appended)
-            if (ps.empty()) {
-                pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &scratch, nullptr, 0,
-                                    &pc.events, &pc.bytes, &pc.last_start);
-            } else {
-                pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &part, nullptr, 0,
-                                    &pc.events, &pc.bytes, &pc.last_start);
-                if (!pc.rc) {
-                    if (scratch.size() < pos + pc.bytes) scratch.resize(pos + pc.bytes);
-                    std::memcpy(scratch.data() + pos, part.data(), pc.bytes);
-                }
-            }
+            // (the piece follows the thread's earlier pieces in its scratch)
+            pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &scratch, nullptr, 0,
+                                &pc.events, &pc.bytes, &pc.last_start, pos);
+            if (pc.rc) pc.bytes = 0;
             pos += pc.bytes;
             ps.push_back(pc);
         }
