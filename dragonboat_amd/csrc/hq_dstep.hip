@@ -1062,7 +1062,12 @@ __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk, uint32
             __builtin_amdgcn_wave_barrier();
             const uint2 *src = reinterpret_cast<const uint2 *>(stc);
             uint2 *out = reinterpret_cast<uint2 *>(dst + lo);
+#ifndef HQ_LITE_NOSTORE       // (timing probe: the records not written, wrong output)
             for (uint32_t q = lane; q < 3 * nrec; q += 64) out[q] = src[q];
+#else
+            (void)src;
+            (void)out;
+#endif
         } else {
             hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.layout->off[kReady]);
             if (rr & 4) {

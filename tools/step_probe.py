@@ -25,7 +25,8 @@ workers = []
 for i in range(W):
     w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True,
                   commit_column=os.environ.get("COLUMN", "1") == "1",
-                  commit_advance=os.environ.get("ADVANCE", "1") == "1")
+                  commit_advance=os.environ.get("ADVANCE", "1") == "1",
+                  ready_compact=os.environ.get("COMPACT", "0") == "1")
     w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
     workers.append(w)
 pc = hq.Context(0)
