@@ -1290,10 +1290,10 @@ __global__ __launch_bounds__(kScanT) void k_scan_layout_jobs(const StepK *ks) {
 }
 
 // The jobs path's scan of a sized stream's sizes (the single path: hipcub over PackSize), in
-// three launches for all jobs: each 1024 groups' packed total (k_size_sums), those totals
-// scanned per job by one workgroup (k_bsum_scan), each 1024 groups scanned in a workgroup from
-// its total's place (k_size_apply); prefix[i] = events before group i << 32 | bytes before it,
-// prefix[n] the totals (n + 1 elements, as the single path's scan)
+// two launches for all jobs: each 1024 groups' packed total (k_size_sums), then each 1024 groups
+// scanned in a workgroup from the sum of the totals before it (k_size_apply); prefix[i] = events
+// before group i << 32 | bytes before it, prefix[n] the totals (n + 1 elements, as the single
+// path's scan)
 constexpr uint32_t kSizeTile = 1024;   // groups per workgroup of 256 threads (4 each)
 __device__ __forceinline__ uint64_t packed_size(const StepK &a, uint64_t i) {
     const uint32_t s = i < a.n ? a.sizes[i] : 0;
@@ -1344,24 +1344,16 @@ __global__ __launch_bounds__(256) void k_size_sums(const JobMap m) {
     if (threadIdx.x == 0) a.bsum[b] = tot;
 }
 
-__global__ __launch_bounds__(1024) void k_bsum_scan(const JobMap m) {
-    const StepK &a = m.ks[m.job0 + blockIdx.x];
-    const uint64_t nb = (a.n + 1 + kSizeTile - 1) / kSizeTile;
-    uint64_t carry = 0;
-    for (uint64_t base = 0; base < nb; base += 1024) {
-        const uint64_t k = base + threadIdx.x;
-        const uint64_t v = k < nb ? a.bsum[k] : 0;
-        uint64_t tot;
-        const uint64_t e = block_excl_scan(v, &tot);
-        if (k < nb) a.bsum[k] = carry + e;
-        carry += tot;
-    }
-}
-
+// (each workgroup sums the totals of the blocks before its own: at most a few thousand words
+// from L2, in place of a scan launch between the two passes)
 __global__ __launch_bounds__(256) void k_size_apply(const JobMap m) {
     const uint32_t j = job_of(m, blockIdx.x);
     const StepK &a = m.ks[m.job0 + j];
     const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
+    uint64_t before = 0;
+    for (uint64_t k = threadIdx.x; k < b; k += 256) before += a.bsum[k];
+    uint64_t base;
+    (void)block_excl_scan(before, &base);
     uint64_t v[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1369,7 +1361,7 @@ __global__ __launch_bounds__(256) void k_size_apply(const JobMap m) {
         sum += v[k];
     }
     uint64_t tot;
-    uint64_t run = a.bsum[b] + block_excl_scan(sum, &tot);
+    uint64_t run = base + block_excl_scan(sum, &tot);
     uint64_t *prefix = const_cast<uint64_t *>(a.prefix);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -2324,10 +2316,6 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in2[c], d0->copy2), "event");
     };
     copies(0);
-    if (!rc) {
-        hipLaunchKernelGGL(k_bsum_scan, dim3(nl), dim3(1024), 0, s, sm);
-        launched("k_bsum_scan");
-    }
     if (!rc) {
         hipLaunchKernelGGL(k_size_apply, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
         launched("k_size_apply");
