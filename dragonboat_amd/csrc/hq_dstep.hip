@@ -1009,7 +1009,10 @@ struct JobMap {
     uint32_t blk0[kMaxJobs + 1];  // relative to job0
     uint32_t *tickets;            // pass A: the launch's ticket word is tickets[chunk]; k_step_lite_jobs
     uint32_t chunk;               //   zeroes them
+    StepK *table_out;             // k_size_sums (reading `ks` from its pinned copy): workgroup 0
+                                  //   writes the jobs' StepK there for the later launches
 };
+static_assert(sizeof(StepK) % 8 == 0, "k_size_sums copies the table in 8-byte words");
 
 __device__ __forceinline__ uint32_t job_of(const JobMap &m, uint32_t b) {
     uint32_t j = 0;               // (uniform: kernel arguments and blockIdx)
@@ -1322,6 +1325,12 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total)
 }
 
 __global__ __launch_bounds__(256) void k_size_sums(const JobMap m) {
+    if (m.table_out && blockIdx.x == 0) {   // the table for the launches behind this one
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(m.ks + m.job0);
+        uint64_t *dst = reinterpret_cast<uint64_t *>(m.table_out + m.job0);
+        for (uint32_t q = threadIdx.x; q < m.count * (uint32_t)(sizeof(StepK) / 8); q += 256)
+            dst[q] = src[q];
+    }
     const uint32_t j = job_of(m, blockIdx.x);
     const StepK &a = m.ks[m.job0 + j];
     const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
@@ -2216,9 +2225,8 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         small = small && r.small;
         total_bytes += r.nb;
     }
-    // (the table goes to the device once k_size_sums is queued, which reads it from the pinned
-    // copy: the device starts on the sizes without waiting for the table's copy to be submitted,
-    // ~25 us of host time for a one-worker step)
+    // (k_size_sums reads the table from the pinned copy and writes it to the device: no copy is
+    // queued ahead of the first launch, ~25 us of host time for a one-worker step)
     const bool table_first = !d0->jobs_host_dev;
     if (!rc && table_first)
         rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
@@ -2264,18 +2272,11 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         if (r.in->groups) h2d(din, r.in->groups, r.n * 4, s);
         if (!r.k.sizes_src) h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
     }
-    const JobMap sm = map(0, nl, kSizeTile, 1);
-    if (!rc) {
-        JobMap pm = sm;
-        if (!table_first) pm.ks = d0->jobs_host_dev;
-        hipLaunchKernelGGL(k_size_sums, dim3(pm.blk0[nl]), dim3(256), 0, s, pm);
-        launched("k_size_sums");
-    }
     if (!rc) {
         // every job's stream in pinned host memory: pass A (and pass B) read it in place, in one
-        // launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks). The table
-        // goes to the device with the streams' device addresses (k_size_sums reads none of the
-        // fields written here)
+        // launch for all jobs, with no copy (HQ_STEP_ZERO_COPY=0: copied in chunks). The
+        // streams' device addresses go into the table before the first launch, which carries it
+        // to the device
         zero_copy = zero_copy_allowed();
         const uint8_t *zbytes[kMaxJobs] = {};
         for (uint32_t x = 0; x < nl && zero_copy; ++x) {
@@ -2289,9 +2290,21 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                 d0->jobs_host[x].bytes = r.k.bytes;
             }
         }
-        if (zero_copy || !table_first)
+        if (zero_copy && table_first)   // (no device alias of the pinned table: copied again)
             rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
                                                    hipMemcpyHostToDevice, s), "hq_dstep jobs");
+    }
+    const JobMap sm = map(0, nl, kSizeTile, 1);
+    if (!rc) {
+        // k_size_sums reads the table from its pinned copy and writes it to the device for the
+        // launches behind it: no copy of its own (a blit launch and ~10 us of host time)
+        JobMap pm = sm;
+        if (!table_first) {
+            pm.ks = d0->jobs_host_dev;
+            pm.table_out = d0->jobs_dev;
+        }
+        hipLaunchKernelGGL(k_size_sums, dim3(pm.blk0[nl]), dim3(256), 0, s, pm);
+        launched("k_size_sums");
     }
     if (zero_copy) {              // one chunk of all jobs, nothing to copy
         cend[nchunks = 1] = nl;
