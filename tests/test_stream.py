@@ -496,3 +496,29 @@ def test_run_malformed(hq):
         with pytest.raises(hq.HQError):
             hq.decode_events(np.array([0, n], np.uint64), np.array([0, len(data)], np.uint64),
                              data)
+
+
+@pytest.mark.parametrize("threads", [1, 2, 5])
+def test_multi_encode_bad_job_before_good_ones(hq, threads):
+    """A malformed job ahead of good ones in the same thread's pieces: the good jobs' bytes land
+    where their own calls put them (a thread's pieces follow each other in its scratch, and a
+    failed piece takes no room)."""
+    off, ev = _random_groups(hq, 25, n=2000)
+    recs, off16 = hq.events_to16(off, ev)
+    wd, ws, wne = hq.encode_events16_sized(off16, recs, 1)
+    bad = np.zeros(3, hq.EVENT16_DTYPE)
+    bad["kind"] = hq.EV16_FULL
+    jobs = [(np.array([0, 3], np.uint64), bad, np.zeros(256, np.uint8), np.zeros(1, np.uint32))]
+    jobs += [(off16, recs, np.zeros(len(wd) + 64 * 8, np.uint8), np.zeros(len(off) - 1, np.uint32))
+             for _ in range(2)]
+    arr = (hq.Encode16Job * 3)()
+    for a, (o, rr, out, sz) in zip(arr, jobs):
+        a.n_groups, a.offsets16, a.recs = len(o) - 1, o.ctypes.data, rr.ctypes.data
+        a.out, a.cap, a.sizes = out.ctypes.data, len(out), sz.ctypes.data
+    rc = hq.lib.hq_events16_encode_sized_multi(hq.ctypes.addressof(arr), 3, threads)
+    assert rc == hq.HQ_E_INVAL
+    assert [a.rc for a in arr] == [hq.HQ_E_INVAL, hq.HQ_OK, hq.HQ_OK]
+    for a, (o, rr, out, sz) in zip(arr[1:], jobs[1:]):
+        assert a.n_events == wne and a.n_bytes == len(wd)
+        np.testing.assert_array_equal(out[:len(wd)], wd)
+        np.testing.assert_array_equal(sz, ws)
