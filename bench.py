@@ -1525,6 +1525,13 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                                 for k in ("dev", "e2e")})
     pool = ThreadPoolExecutor(max(Ws) + 1)
 
+    # the producer's encode calls, one per (W, buffer slot): the records and the receive buffers
+    # stay in place from step to step (StepRows16.set rewrites the records in place), so each
+    # call's job table is built once (hq.Encode16Batch)
+    batches = {(W, slot): hq.Encode16Batch([
+        (off, recs.recs[e0:e1], modes[W]["bufs"][slot][i][0], modes[W]["bufs"][slot][i][1])
+        for i, (off, e0, e1) in enumerate(modes[W]["parts"])]) for W in Ws for slot in (0, 1)}
+
     def encode(W, slot):
         """The W workers' streams of the current step from the producer's compact records, in
         one call on the encode threads (hq_events16_encode_sized_multi: the threads split the
@@ -1532,12 +1539,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         Returns its wall time (s)."""
         t0 = time.perf_counter()
         mo = modes[W]
-        jobs = []
-        for i in range(W):
-            off, e0, e1 = mo["parts"][i]
-            out, sz = mo["bufs"][slot][i]
-            jobs.append((off, recs.recs[e0:e1], out, sz))
-        for i, (ne, nb) in enumerate(hq.encode_events16_sized_multi(jobs, enc_threads)):
+        for i, (ne, nb) in enumerate(batches[(W, slot)].run(enc_threads)):
             assert ne == mo["parts"][i][2] - mo["parts"][i][1]
             mo["nbytes"][slot][i] = nb
         return time.perf_counter() - t0
