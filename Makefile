@@ -109,9 +109,3 @@ tools/lib_engexp/libengexp.so: tools/engine_exp.hip $(LIB) $(DEPS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ tools/engine_exp.hip -L$(LIBDIR) -lhipquorum -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
-# the device step's k_step_lite without its ReadyToRead stores (timing probe: wrong output)
-tools/lib_litenostore/libhipquorum.so: $(SRCS) $(DEPS)
-	$(call variant,-DHQ_LITE_NOSTORE)
-# pass A also writing the single ReadyToReads into per-tile slots of the host region (timing probe)
-tools/lib_passaslots/libhipquorum.so: $(SRCS) $(DEPS)
-	$(call variant,-DHQ_PASSA_SLOTS_PROBE)

@@ -952,37 +952,6 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
     if constexpr (STAGE) {
         if (a.spec_ready)
             ready_tail(a, (a.i_begin >> 8) + blk, chunk, member, first, i, n_ready, one_ready, sbuf);
-#ifdef HQ_PASSA_SLOTS_PROBE
-        // timing probe (tools/lib_passaslots): the tile's single ReadyToReads as compact records,
-        // written during pass A into fixed per-tile slots at the end of the host region (past
-        // every list; the step's outputs are unchanged: k_step_lite still writes the list)
-        const uint64_t slots = ((a.n + 255) / 256) * 256 * sizeof(hq_ready_compact);
-        if (a.out_cap >= (uint64_t)a.n * 32 + slots) {
-            __shared__ uint32_t s_pw[256 / 64];
-            const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-            const uint64_t bal = __ballot(one_ready);
-            const uint32_t rank = __popcll(bal & ((1ull << lane) - 1));
-            if (lane == 0) s_pw[wv] = __popcll(bal);
-            __syncthreads();      // (also: every thread is done with the staged bytes in sbuf)
-            uint32_t before = 0, agg = 0;
-            for (int w = 0; w < 256 / 64; ++w) {
-                before += w < wv ? s_pw[w] : 0u;
-                agg += s_pw[w];
-            }
-            hq_ready_compact *stage = reinterpret_cast<hq_ready_compact *>(sbuf);
-            if (one_ready) {
-                const hq_ready_to_read r = a.ready_slot[i];
-                stage[before + rank] = hq_ready_compact{r.ctx_low, r.ctx_high, (uint32_t)i,
-                                                        (int32_t)(int64_t)(r.index - a.groups_old[h].committed)};
-            }
-            __syncthreads();
-            const uint64_t tile = (a.i_begin >> 8) + blk;
-            uint2 *dst = reinterpret_cast<uint2 *>(a.out + a.out_cap - slots +
-                                                   tile * 256 * sizeof(hq_ready_compact));
-            const uint2 *src = reinterpret_cast<const uint2 *>(stage);
-            for (uint32_t q = threadIdx.x; q < 3 * agg; q += 256) dst[q] = src[q];
-        }
-#endif
     }
 }
 
@@ -1096,12 +1065,7 @@ __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk, uint32
             __builtin_amdgcn_wave_barrier();
             const uint2 *src = reinterpret_cast<const uint2 *>(stc);
             uint2 *out = reinterpret_cast<uint2 *>(dst + lo);
-#ifndef HQ_LITE_NOSTORE       // (timing probe: the records not written, wrong output)
             for (uint32_t q = lane; q < 3 * nrec; q += 64) out[q] = src[q];
-#else
-            (void)src;
-            (void)out;
-#endif
         } else {
             hq_ready_to_read *dst = reinterpret_cast<hq_ready_to_read *>(a.out + a.layout->off[kReady]);
             if (rr & 4) {

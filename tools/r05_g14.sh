@@ -1,5 +1,6 @@
 # r05t: step5 device-step timelines with compact ReadyToReads, the product library against a
 # build whose k_step_lite skips its ReadyToRead stores (timing probe)
+# (the nostore / slots libraries are builds of profiles/r05n/device_step_probes.patch)
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
