@@ -522,3 +522,26 @@ def test_multi_encode_bad_job_before_good_ones(hq, threads):
         assert a.n_events == wne and a.n_bytes == len(wd)
         np.testing.assert_array_equal(out[:len(wd)], wd)
         np.testing.assert_array_equal(sz, ws)
+
+
+def test_encode_batch_reuses_its_buffers(hq):
+    """hq.Encode16Batch: one job table, called step after step while the records change in place
+    (StepRows16.set): every call's bytes and sizes equal a fresh call's."""
+    import bench
+    G = 1 << 12
+    recs = bench.StepRows16(hq, G, bench.STEP_ROLES["step5"])
+    off16, r = recs.set(0)
+    bounds = [0, G // 3, G // 2, G]
+    parts = [(off16[b0:b1 + 1] - off16[b0], int(off16[b0]), int(off16[b1]))
+             for b0, b1 in zip(bounds, bounds[1:])]
+    bufs = [(np.zeros((e1 - e0) * 5 + 64, np.uint8), np.zeros(len(o) - 1, np.uint32))
+            for o, e0, e1 in parts]
+    batch = hq.Encode16Batch([(o, r[e0:e1], out, sz) for (o, e0, e1), (out, sz) in zip(parts, bufs)])
+    for s in range(3):
+        recs.set(s)
+        got = batch.run(4)
+        for (o, e0, e1), (out, sz), (ne, nb) in zip(parts, bufs, got):
+            wd, ws, wne = hq.encode_events16_sized(o, r[e0:e1], 1)
+            assert ne == wne and nb == len(wd)
+            np.testing.assert_array_equal(out[:nb], wd)
+            np.testing.assert_array_equal(sz, ws)
