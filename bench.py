@@ -1370,14 +1370,27 @@ def mix64(z):
     return z ^ (z >> np.uint64(31))
 
 
+def ready_terms(ready):
+    """qref_digest_ready of each ReadyToRead record (READY_DTYPE), as uint64."""
+    k1, k2, k3 = _READY_K
+    return mix64(mix64(ready["cluster_id"]) ^ (ready["index"] * k1 + ready["ctx_low"] * k2 +
+                                                ready["ctx_high"] * k3))
+
+
 def ready_digest(ready):
     """Sum over ReadyToRead records (READY_DTYPE) of qref_digest_ready, mod 2^64."""
     if len(ready) == 0:
         return 0
-    k1, k2, k3 = _READY_K
-    t = mix64(mix64(ready["cluster_id"]) ^ (ready["index"] * k1 + ready["ctx_low"] * k2 +
-                                             ready["ctx_high"] * k3))
-    return int(t.sum(dtype=np.uint64))
+    return int(ready_terms(ready).sum(dtype=np.uint64))
+
+
+def ready_order_digest(ready, pos0=0):
+    """qref_step_totals.ready_order_digest's terms for records at positions pos0, pos0 + 1, ...:
+    the sum of (position + 1) * qref_digest_ready, mod 2^64 (a reordered list changes it)."""
+    if len(ready) == 0:
+        return 0
+    w = np.arange(pos0 + 1, pos0 + 1 + len(ready), dtype=np.uint64)
+    return int((ready_terms(ready) * w).sum(dtype=np.uint64))
 
 
 class CommitMirror:
@@ -1393,9 +1406,10 @@ class CommitMirror:
         self.c = committed.astype(np.uint64).copy()
 
     def step(self, res):
-        """(commits, ReadyToReads, sum of advances, ready digest, commit digest) of one step."""
+        """(commits, ReadyToReads, sum of advances, ready digest, commit digest, ordered ready
+        digest) of one step; the workers' lists in worker order make the step's list."""
         from dragonboat_amd import hipquorum as hq
-        n_c = n_r = adv_sum = rd = cd = 0
+        n_c = n_r = adv_sum = rd = cd = od = 0
         for i, r in enumerate(res):
             lo, hi = self.bounds[i], self.bounds[i + 1]
             # ReadyToReads as 24-byte records (HQ_WORKER_READY_COMPACT): the cluster id and the
@@ -1417,10 +1431,11 @@ class CommitMirror:
             n_c += int(r.get("n_commits", len(r["commits"])))
             adv_sum += int(adv.sum(dtype=np.uint64))
             cd += int((self.coef[ix] * adv).sum(dtype=np.uint64))
+            od += ready_order_digest(ready, n_r)
             n_r += len(ready)
             rd += ready_digest(ready)
         m = (1 << 64) - 1
-        return (n_c, n_r, adv_sum & m, rd & m, cd & m)
+        return (n_c, n_r, adv_sum & m, rd & m, cd & m, od & m)
 
 
 def _latency(ts):
@@ -1585,7 +1600,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                 ts.append(dt)
             dg.append((tot["commits"], tot["ready"],
                        (tot["committed_sum"] - prev_sum) & ((1 << 64) - 1),
-                       tot["ready_digest"], tot["commit_digest"]))
+                       tot["ready_digest"], tot["commit_digest"], tot["ready_order_digest"]))
         if cpus:
             prev_sum = tot["committed_sum"]
         rows.set(s + 1)                # untimed: step s + 1's messages arrive
@@ -1714,7 +1729,8 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                                        same_modes)
         out["parity_checks"] = ("per step: commits, ReadyToReads, committed advance sum, "
                                 "digest of (cluster, advance) and of ReadyToRead (cluster, "
-                                "index, ctx)")
+                                "index, ctx), and a position-weighted ReadyToRead digest "
+                                "(the list's order)")
         out["vs_cpu_replay_end_to_end"] = {k: v / best for k, v in e2e.items()}
         out["vs_cpu_replay_device_only"] = {k: v / best for k, v in dev.items()}
         for b, _, _ in cpus.values():

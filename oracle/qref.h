@@ -308,6 +308,10 @@ typedef struct qref_step_totals {
      * record (cluster, index, ctx) and every group whose committed index moved (cluster,
      * advance) */
     uint64_t ready_digest, commit_digest;
+    /* order-sensitive: the sum over the step's ReadyToRead records, in output order (the list's
+     * groups in order, each group's records in order), of (position + 1) * qref_digest_ready —
+     * a reordered list changes it. Threads combine their sums by their records' offsets. */
+    uint64_t ready_order_digest;
 } qref_step_totals;
 
 /* splitmix64's finalizer; the digest terms bench.py recomputes from the device results */

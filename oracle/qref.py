@@ -536,7 +536,8 @@ class StepGroup:
 
 class StepTotals(ctypes.Structure):
     _fields_ = [(k, _u64) for k in ("commits", "ready", "resps", "states", "dropped", "deferred",
-                                    "committed_sum", "ready_digest", "commit_digest")]
+                                    "committed_sum", "ready_digest", "commit_digest",
+                                    "ready_order_digest")]
 
 
 class StepBatch:

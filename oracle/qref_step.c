@@ -411,9 +411,13 @@ static void *step_run(void *p) {
         const uint64_t committed0 = g->committed;
         int rc = qref_group_step(g, j->ev + b, (int)(e - b), o);
         if (rc) { j->rc = rc; break; }
-        for (int r = 0; r < o->n_ready; r++)
-            j->tot.ready_digest += qref_digest_ready(g->cluster_id, o->ready[r].index,
-                                                     o->ready[r].low, o->ready[r].high);
+        for (int r = 0; r < o->n_ready; r++) {
+            const uint64_t d = qref_digest_ready(g->cluster_id, o->ready[r].index,
+                                                 o->ready[r].low, o->ready[r].high);
+            j->tot.ready_digest += d;
+            /* (the thread's own positions from 0; qref_step_batch adds its offset) */
+            j->tot.ready_order_digest += j->tot.ready * d + (uint64_t)r * d;
+        }
         if (o->commit_changed)
             j->tot.commit_digest += qref_digest_commit(g->cluster_id, o->committed - committed0);
         j->tot.commits += (uint64_t)o->commit_changed;
@@ -467,6 +471,10 @@ int qref_step_batch(qref_group *groups, uint64_t G, uint64_t n_list, const uint3
         tot->dropped += jobs[t].tot.dropped;
         tot->deferred += jobs[t].tot.deferred;
         tot->committed_sum += jobs[t].tot.committed_sum;
+        /* position p of the thread's records is offset + its own position: (p + 1) d summed =
+         * own-position sum + (offset + 1) * the thread's digest (tot->ready so far = offset) */
+        tot->ready_order_digest += jobs[t].tot.ready_order_digest +
+                                   (tot->ready - jobs[t].tot.ready + 1) * jobs[t].tot.ready_digest;
         tot->ready_digest += jobs[t].tot.ready_digest;
         tot->commit_digest += jobs[t].tot.commit_digest;
     }

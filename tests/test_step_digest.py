@@ -112,7 +112,7 @@ def test_commit_forms_reduce_to_one_digest():
     got = {f: bench.CommitMirror(cids, committed, bounds).step(results(f))
            for f in ("advance", "column", "list")}
     assert len(set(got.values())) == 1, got
-    n_c, n_r, s, rd, cd = got["advance"]
+    n_c, n_r, s, rd, cd, od = got["advance"]
     assert n_c == np.count_nonzero(adv) and n_r == len(ready) and s == int(adv.sum())
     # the replay's terms, summed in any order
     want_cd = sum(qref.lib.qref_digest_commit_term(int(c), int(a))
@@ -132,3 +132,25 @@ def test_commit_forms_reduce_to_one_digest():
     r2 = ready.copy()
     r2["ctx_high"][0] ^= 1
     assert bench.CommitMirror(cids, committed, bounds).step(results("advance", ready=r2))[3] != rd
+    # order: two records swapped leave the order-free digest and change the ordered one
+    wk = np.searchsorted(np.array([cids[b] for b in bounds[1:-1]]), ready["cluster_id"], "right")
+    i, j = next((i, j) for i in range(len(ready)) for j in range(i + 1, len(ready))
+                if wk[i] == wk[j])           # two records of one worker's list
+    r3 = ready.copy()
+    r3[[i, j]] = r3[[j, i]]
+    got3 = bench.CommitMirror(cids, committed, bounds).step(results("advance", ready=r3))
+    assert got3[3] == rd and got3[5] != od
+
+
+def test_ordered_digest_terms():
+    """bench.ready_order_digest is the sum of (position + 1) * qref_digest_ready, positions
+    continuing across workers' lists (pos0)."""
+    rng = np.random.default_rng(11)
+    r = np.zeros(40, bench_ready_dtype())
+    for f in ("cluster_id", "index", "ctx_low", "ctx_high"):
+        r[f] = _rng_u64(rng, 40)
+    terms = [qref.lib.qref_digest_ready_term(int(x["cluster_id"]), int(x["index"]),
+                                             int(x["ctx_low"]), int(x["ctx_high"])) for x in r]
+    want = sum((k + 1) * t for k, t in enumerate(terms)) & U64
+    assert bench.ready_order_digest(r) == want
+    assert (bench.ready_order_digest(r[:17]) + bench.ready_order_digest(r[17:], 17)) & U64 == want
