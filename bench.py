@@ -1273,6 +1273,7 @@ def _partition(ev_full, b0, b1):
 
 
 STEP_WARM = 2
+STEP_WAIT_DEFAULT = "block"      # the step legs' wait policy (run_step_leg, BENCH_STEP_WAIT)
 
 
 class StepRows:
@@ -1412,10 +1413,11 @@ class CommitMirror:
         n_c = n_r = adv_sum = rd = cd = od = 0
         for i, r in enumerate(res):
             lo, hi = self.bounds[i], self.bounds[i + 1]
-            # ReadyToReads as 24-byte records (HQ_WORKER_READY_COMPACT): the cluster id and the
-            # index rebuilt from the group's position and its committed index before the step
-            ready = (hq.expand_ready(r["ready_compact"], self.cids[lo:hi], self.c[lo:hi])
-                     if "ready_compact" in r else r["ready"])
+            # ReadyToReads as 24-byte records (HQ_WORKER_READY_COMPACT) in the list and the
+            # per-tile slots (HQ_WORKER_READY_SLOTS): the cluster id and the index rebuilt from
+            # the group's position and its committed index before the step, the two merged in
+            # group order (the reference's)
+            ready = hq.merge_ready(r, self.cids[lo:hi], self.c[lo:hi])
             if "committed_advance" in r:
                 ix = np.arange(lo, hi)
                 adv = r["committed_advance"][:hi - lo].astype(np.uint64)
@@ -1450,11 +1452,31 @@ def _latency(ts):
 def _device_split(rs):
     """One jobs step's device time split (ms) from its workers' outputs (hq_step_output): the
     host's submit, the GPU's time between the step's timing events, the outputs' mapping, and the
-    rest of the wait (the waiting thread's wake-up and queueing ahead of the step's work)."""
+    rest of the wait (the waiting thread's wake-up and queueing ahead of the step's work); the
+    wait itself (its poll and sleep), and the raw clocks of its end for _wake_lag: the host's
+    steady clock at the wait's return and the device's 100-MHz stamp after the step
+    (HQ_WAIT_CLOCK)."""
     r = max(rs, key=lambda x: x["pass_ns"])
-    rest = r["pass_ns"] - r["pack_ns"] - r["device_ns"] - r["apply_ns"]
-    return {"submit_ms": r["pack_ns"] / 1e6, "gpu_ms": r["device_ns"] / 1e6,
-            "outputs_ms": r["apply_ns"] / 1e6, "wait_rest_ms": rest / 1e6}
+    rest = r["pass_ns"] - r["pack_ns"] - r["gpu_ns"] - r["apply_ns"]
+    return {"submit_ms": r["pack_ns"] / 1e6, "gpu_ms": r["gpu_ns"] / 1e6,
+            "outputs_ms": r["apply_ns"] / 1e6, "wait_rest_ms": rest / 1e6,
+            "wait_ms": r["device_ns"] / 1e6, "wait_poll_ms": r["wait_poll_ns"] / 1e6,
+            "wait_sleep_ms": r["wait_sleep_ns"] / 1e6, "wait_sleeps": r["wait_sleeps"],
+            "_end_ns": r["wait_end_ns"], "_end_ticks": r["device_end_ticks"]}
+
+
+def _wake_lag(phases, prefix):
+    """Each step's wake-up lateness (ms) from the clocks of its wait's end: the host's return
+    time less the device's end stamp (10 ns per tick), each against the run's smallest such
+    difference (the two clocks' offset: the best wake-up of the run counts as 0; the clocks
+    drift by far less than a microsecond over a run). Written into the phases as
+    <prefix>wake_lag_ms; the raw clocks are dropped."""
+    d = [p[prefix + "_end_ns"] - 10 * p[prefix + "_end_ticks"] for p in phases
+         if p.get(prefix + "_end_ticks")]
+    base = min(d) if d else None
+    for p in phases:
+        t, k = p.pop(prefix + "_end_ns", 0), p.pop(prefix + "_end_ticks", 0)
+        p[prefix + "wake_lag_ms"] = (t - 10 * k - base) / 1e6 if (k and base is not None) else None
 
 
 def _phase_summary(ph):
@@ -1463,7 +1485,8 @@ def _phase_summary(ph):
         return None
     keys = ("e2e_ms", "encode_max_ms", "execute_ms", "dev_ms", "enc_wall_ms", "enc_task_lag_max_ms",
             "cgroup_throttled_ms", "exe_gpu_ms", "exe_wait_rest_ms", "dev_gpu_ms",
-            "dev_wait_rest_ms")
+            "dev_wait_rest_ms", "exe_wake_lag_ms", "dev_wake_lag_ms", "exe_wait_sleep_ms",
+            "dev_wait_sleep_ms")
     med = {k: round(float(np.median([p[k] for p in ph])), 4) for k in keys
            if all(p.get(k) is not None for p in ph)}
     th = [p["cgroup_throttled_ms"] for p in ph if p.get("cgroup_throttled_ms") is not None]
@@ -1513,6 +1536,10 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     offsets = rows.offsets
     # the producer's native encode threads per step, shared by the W workers' encodes
     enc_threads = encode_threads()
+    # the step thread's wait (hq_worker_set_wait; BENCH_STEP_WAIT=block|sleep|spin[:poll:sleep])
+    wait_name, *wv = os.environ.get("BENCH_STEP_WAIT", STEP_WAIT_DEFAULT).split(":")
+    wait = ({"block": hq.HQ_WAIT_BLOCK, "sleep": hq.HQ_WAIT_SLEEP, "spin": hq.HQ_WAIT_SPIN}[wait_name],
+            int(wv[0]) if wv else 50, int(wv[1]) if len(wv) > 1 else 20)
     pin = hq.Context(d.device)
     Ws = (1, 2, 16)
     modes = {}
@@ -1527,11 +1554,13 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             ws = []
             for i in range(W):
                 wk = hq.Worker(d.device, n_voting, on_device=True, commit_column=True,
-                               commit_advance=True, ready_compact=True)
+                               commit_advance=True, ready_compact=True, ready_slots=True)
+                wk.set_wait(wait[0], wait[1], wait[2], clock=True)
                 wk.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
                 ws.append(wk)
             return ws
-        bufs = [[(pin.pinned((e1 - e0) * 5 + 64, np.uint8), pin.pinned(len(o) - 1, np.uint32))
+        # the receive buffers: the stream bytes and the 2-byte size words (hq_step_stream.sizes16)
+        bufs = [[(pin.pinned((e1 - e0) * 5 + 64, np.uint8), pin.pinned(len(o) - 1, np.uint16))
                  for o, e0, e1 in parts] for _ in range(2)]
         modes[W] = dict(parts=parts, bufs=bufs, nbytes=[[0] * W, [0] * W], dev=workers(),
                         e2e=workers(), t={"dev": [], "e2e": []}, bytes=0, phases=[],
@@ -1586,7 +1615,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     want_data, want_sizes = hq.encode_events_sized(offsets, rows.ev)
     producer_equal = bool(np.array_equal(modes[1]["bufs"][0][0][0][:modes[1]["nbytes"][0][0]],
                                          want_data) and
-                          np.array_equal(modes[1]["bufs"][0][0][1], want_sizes))
+                          np.array_equal(modes[1]["bufs"][0][0][1], hq.sizes16_of(want_sizes)))
     del want_data, want_sizes
     n_events = len(rows.ev)
     timed = 0
@@ -1679,6 +1708,9 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         mismatch += [{"mode": f"{k}_w{W}", "committed_differs_at": next(
             (i for i, (a, b) in enumerate(zip(v, c1)) if a != b), len(v))}
             for (W, k), v in committed.items() if v != c1]
+    for W in Ws:
+        _wake_lag(modes[W]["phases"], "exe_")
+        _wake_lag(modes[W]["phases"], "dev_")
     members = ", ".join(f"{roles.count(r)} {r}" for r in ("remote", "witness", "observer")
                         if roles.count(r))
     ev_total = n_events * timed
@@ -1705,6 +1737,8 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         # p50 / p99 / max of the timed steps, and the slowest end-to-end steps with their phases
         "latency_ms": {f"{k}_w{W}": _latency(modes[W]["t"][k]) for W in Ws for k in ("dev", "e2e")},
         "e2e_phases": {f"w{W}": _phase_summary(modes[W]["phases"]) for W in Ws},
+        "wait_policy": {"mode": wait_name, "poll_us": wait[1], "sleep_us": wait[2],
+                        "clock": "HQ_WAIT_CLOCK: the device's end stamp beside the host's return"},
         "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
         "modes_agree": same_modes,
         **({"modes_mismatch": mismatch} if mismatch else {}),

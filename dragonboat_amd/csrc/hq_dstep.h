@@ -35,6 +35,13 @@ constexpr uint8_t kDSuspended = 1;
 
 struct hq_dstep;                      // device buffers of one worker
 
+struct hq_wait_clock {                // one wait of a step's thread (host steady clock, ns)
+    uint64_t t_begin_ns, t_end_ns;    // the wait's start (all queued) and return
+    uint64_t poll_ns, sleep_ns;       // polling, then asleep (blocking event or timed sleeps)
+    uint64_t sleeps;                  // the sleeps (HQ_WAIT_SLEEP) or 1 (a blocking wait)
+    uint64_t device_end_ticks;        // HQ_WAIT_CLOCK: the device's 100-MHz clock after the step
+};
+
 struct hq_dstep_out {                 // the lists of one step, in input group order, in the
     const hq_commit_event *commits;   // engine's pinned host buffer (valid until its next step)
     const hq_ready_to_read *ready;    // (NULL when the records are compact)
@@ -55,6 +62,13 @@ struct hq_dstep_out {                 // the lists of one step, in input group o
     uint64_t submit_ns;               // host time from the call to the last queued operation
     uint64_t gpu_ns;                  // GPU time from the step's first queued operation on the
                                       // compute stream to its last (HIP events; 0: not timed)
+    uint32_t gpu_jobs;                // the jobs whose steps shared those launches (1: its own)
+    hq_wait_clock wait;               // the step's thread waiting for the device
+    // HQ_WORKER_READY_SLOTS (a step that wrote them; else NULL / 0): tile t's single ReadyToReads
+    // at ready_slots[256 t ..], slot_counts[t] of them, n_slotted in all
+    const hq_ready_compact *ready_slots;
+    const uint32_t *slot_counts;
+    uint64_t n_tiles, n_slotted;
 };
 
 // one step's input: rows (events), an event stream (bytes + boffsets), or an event stream with
@@ -68,12 +82,15 @@ struct hq_dstep_in {
     const uint8_t *bytes;
     const uint32_t *sizes = nullptr;   // per group: events | bytes << 16
     uint64_t n_events = 0, n_bytes = 0;
+    const uint16_t *sizes16 = nullptr; // or per group: bytes (the engine counts the events)
 };
 
 // commit_column: bit 1 a step may return its commits as a column (HQ_WORKER_COMMIT_COLUMN), bit 2
 // as a column of advances (HQ_WORKER_COMMIT_ADVANCE), bit 4 its ReadyToReads as 24-byte records
-// (HQ_WORKER_READY_COMPACT)
+// (HQ_WORKER_READY_COMPACT), bit 8 the single ReadyToReads in per-tile slots (HQ_WORKER_READY_SLOTS)
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column = 0);
+// the step thread's wait (HQ_WAIT_* of include/hipquorum.h, | HQ_WAIT_CLOCK)
+int hq_dstep_set_wait(hq_dstep *d, uint32_t mode, uint32_t poll_us, uint32_t sleep_us);
 void hq_dstep_close(hq_dstep *d);
 // copy group records [g0, g0 + ng) with their reads (kDReads per group) and member records
 // [m0, m0 + nm) to the device, growing the device arrays to hold them

@@ -37,13 +37,17 @@
 
 namespace {
 
+// kRerun: 1 for a group with records other than its commit; kEvents: the group's events (pass A
+// counts them as it decodes: with 2-byte size words the event prefix pass B needs is their scan);
+// kSlotted: 1 for a group whose single ReadyToRead went to its tile's slot (HQ_WORKER_READY_SLOTS)
 enum List { kCommits, kReady, kResps, kStates, kDropped, kDeferred, kFallback, kDecisions,
-            kRerun, kLists };   // kRerun: 1 for a group with records other than its commit
+            kRerun, kEvents, kSlotted, kLists };
 // the worker's input checks, taken by pass A (which writes no group state) before pass B runs;
-// kErrScan: pass A's chained scan of the ReadyToRead places found a tile's word missing (an
-// internal fault, reported instead of waiting for ever)
+// kErrScan: pass A's chained scan of the ReadyToRead places gave up on a tile's word (a stalled
+// predecessor: the step re-runs the copy-out through k_step_lite, finish()); kErrTicket: a pass A
+// launch found its ticket word not zeroed (an internal fault: nothing of that launch stepped)
 enum InputError : uint32_t { kErrHandle = 1, kErrOffsets = 2, kErrBoffsets = 4, kErrTwice = 8,
-                             kErrScan = 16 };
+                             kErrScan = 16, kErrTicket = 32 };
 constexpr uint32_t kTickets = 8;  // pass A launches per step (chunks) with their own ticket word
 
 struct StepK {
@@ -113,12 +117,32 @@ struct StepK {
     uint32_t *ready_wide;
     uint64_t *tiles;              // per tile: step_no << 32 | chunk << 29 | inclusive << 28 | count
     uint32_t *tickets;            // [kTickets]
+    // 2-byte size words (hq_step_stream.sizes16: a group's byte count only): the prefixes hold
+    // bytes alone, pass A counts each group's events as it decodes them (kEvents) and a group's
+    // bytes that do not decode are an input error (kErrBoffsets); sizes16_src as sizes_src
+    const uint16_t *sizes16;
+    const uint16_t *sizes16_src;
+    uint32_t bytes_only;
+    // HQ_WORKER_READY_SLOTS: pass A writes the single ReadyToRead of every group that has no other
+    // record (and whose index - committed fits 32 bits) as an hq_ready_compact into its tile's slot
+    // in the host region — tile t (256 groups) at out + slot_off + 6144 t, in group order, its
+    // count at out + cnt_off + 4 t — in the link's write direction while pass A reads the stream;
+    // those groups leave the list (kSlotted instead of kReady)
+    uint32_t slots;
+    uint64_t slot_off, cnt_off;
+    uint32_t test_scan_fail, pad_t;   // HQ_TEST_SCAN_FAIL at open: every look-back gives up (tests)
 };
+
+constexpr uint32_t kSlotTile = 256;   // groups per slot tile (pass A's workgroup)
+constexpr uint64_t kSlotTileBytes = kSlotTile * sizeof(hq_ready_compact);
+static_assert(kSlotTileBytes % 256 == 0, "slot tiles keep the region's 256-byte alignment");
 
 struct PackSize {                 // group i's size word -> events << 32 | bytes; i = n: 0 (the
     const uint32_t *sizes;        // scan's last element is the totals; no memset on the copy
     uint64_t n;                   // stream between the sizes' copy and the bytes')
+    const uint16_t *sizes16 = nullptr;   // 2-byte words: bytes only
     __host__ __device__ uint64_t operator()(uint64_t i) const {
+        if (sizes16) return i < n ? sizes16[i] : 0;
         const uint32_t s = i < n ? sizes[i] : 0;
         return (uint64_t)(s & 0xFFFFu) << 32 | (s >> 16);
     }
@@ -134,9 +158,12 @@ struct Layout {
     uint32_t commit_column;       // the commits list is a column: one word per listed group
                                   // (kColumn64: the committed index, kColumn32: its advance)
     uint32_t ready_compact;       // the ReadyToReads are hq_ready_compact records
+    uint32_t pad;
+    uint64_t reserve;             // bytes ahead of the lists (the slot form's column + slots)
 };
 constexpr uint32_t kColumn64 = 1, kColumn32 = 2;
 constexpr uint32_t kReadyCompact = 4;   // allow_column bit: HQ_WORKER_READY_COMPACT
+constexpr uint32_t kReadySlots = 8;     // allow_column bit: this step writes slots (ready slots)
 
 __device__ __forceinline__ bool is_response(uint32_t t) {   // internal/raft/utils.go
     return t == HQ_MSG_REPLICATE_RESP || t == HQ_MSG_REQUEST_VOTE_RESP ||
@@ -264,7 +291,10 @@ constexpr uint32_t kStageBytes = 16384;  // pass A: a workgroup's stream bytes s
 // (aggregate) and then its inclusive prefix, tagged with the step and the launch's chunk so that
 // words of earlier launches and steps are never taken for this one's
 constexpr uint32_t kTileVal = (1u << 28) - 1;
-constexpr uint32_t kSpinMax = 1u << 22;   // ~0.1 s of polling before kErrScan
+// how long a tile waits for a predecessor's word before it gives up (kErrScan; the host then
+// re-runs the copy-out without pass A's records): 0.1 s of the device's 100-MHz constant clock
+// (wall_clock64, hipDeviceAttributeWallClockRate), whatever each poll costs
+constexpr uint64_t kScanWaitTicks = 10000000;
 __device__ __forceinline__ uint64_t tile_word(uint32_t step, uint32_t chunk, bool incl, uint32_t v) {
     return (uint64_t)step << 32 | (uint64_t)(chunk & 7) << 29 | (uint64_t)incl << 28 | (v & kTileVal);
 }
@@ -597,22 +627,34 @@ struct Engine {
 
     // the group's events: rows (STREAM = false) or its bytes [p, end) of the stream; an event
     // that does not decode is a fallback like one the path does not take
+    // (2-byte size words, a.bytes_only: the events are the group's bytes decoded to their end —
+    // e1 is not known and a suspended group's events are still decoded to be counted; bytes that
+    // do not decode are an input error, as the host worker's decoder makes them, not a fallback)
     template <bool STREAM>
     __device__ __forceinline__ void run(uint64_t e0, uint64_t e1, const uint8_t *p, const uint8_t *end) {
         const uint64_t committed0 = c0 = g.committed;
         DPrev pv;
         ByteReader br{p, end};
-        for (uint64_t e = e0; e < e1; ++e) {
+        const bool by_bytes = STREAM && a.bytes_only;
+        uint64_t e = e0;
+        for (;; ++e) {
+            if (by_bytes ? !(br.more() || pv.run) : e >= e1) break;
+            hq_event ev;
+            bool dec = true;
+            if (STREAM && (by_bytes || !(g.flags & kDSuspended))) dec = decode_event(br, pv, ev);
+            if (by_bytes && !dec) {
+                if (!WRITE) atomicOr(a.error, (uint32_t)kErrBoffsets);
+                break;
+            }
             if (g.flags & kDSuspended) {
                 defer(e);
                 continue;
             }
             bool ok;
             if (STREAM) {
-                hq_event ev;
-                ok = decode_event(br, pv, ev) && handle(ev, e);
+                ok = dec && handle(ev, e);
             } else {
-                const hq_event ev = a.events[e];
+                ev = a.events[e];
                 ok = handle(ev, e);
             }
             if (!ok) {                                   // this event and the rest are deferred
@@ -622,10 +664,11 @@ struct Engine {
                 defer(e);
             }
         }
+        cnt[kEvents] = (uint32_t)(e - e0);
         // a group that took all its events must have used all its bytes: left-over bytes mean the
         // sizes were split wrongly between groups, which the host decoder rejects as HQ_E_INVAL
         // (hq_stream.cpp); pass A makes it an input error, so no state is written
-        if (STREAM && !WRITE && !(g.flags & kDSuspended) && (br.p != br.end || pv.run))
+        if (STREAM && !WRITE && !by_bytes && !(g.flags & kDSuspended) && (br.p != br.end || pv.run))
             atomicOr(a.error, (uint32_t)kErrBoffsets);
         if (!WRITE && g.committed - committed0 > 0xFFFFFFFFull && a.wide)
             atomicOr(a.wide, 1u);                        // no 4-byte advance column this step
@@ -726,14 +769,14 @@ __device__ void ready_tail(const StepK &a, uint64_t tile, uint32_t chunk, bool m
                      (uint32_t)((w >> 29) & 7) < chunk;
                 excl = (uint32_t)w & kTileVal;
             }
-        } else if (tile == 0) {
+        } else if (tile == 0 || a.test_scan_fail) {
             ok = false;
         } else {
             if (lane == 0) tile_store(a.tiles + tile, tile_word(step, chunk, false, agg));
             // lane k reads tile hi - k; a window is taken once every tile up to the nearest
             // inclusive word (or all 64) has published for this launch
             int64_t hi = (int64_t)tile - 1;
-            uint32_t spins = 0;
+            const uint64_t t_wait = wall_clock64();
             for (;;) {
                 const int64_t p = hi - lane;
                 const uint64_t w = p >= 0 ? tile_load(a.tiles + p) : 0;
@@ -755,7 +798,7 @@ __device__ void ready_tail(const StepK &a, uint64_t tile, uint32_t chunk, bool m
                     }
                     continue;
                 }
-                if (++spins > kSpinMax) {
+                if (wall_clock64() - t_wait > kScanWaitTicks) {
                     ok = false;
                     break;
                 }
@@ -791,6 +834,40 @@ __device__ void ready_tail(const StepK &a, uint64_t tile, uint32_t chunk, bool m
     for (uint32_t q = threadIdx.x; q < nq; q += 256) out[q] = src[q];
 }
 
+// HQ_WORKER_READY_SLOTS: tile `tile`'s slotted records (one per slotted thread, the thread's
+// group = the tile's 256-group block in order) staged in LDS in group order and stored as one
+// contiguous run of 16-byte stores at the tile's slot, the count beside it. No place depends on
+// another tile, so pass A writes them while it still reads the stream (the link's other
+// direction). buf: >= kSlotTileBytes of LDS no thread still reads. All threads of the workgroup
+// call this.
+__device__ void slot_store(const StepK &a, uint64_t tile, bool slotted, const hq_ready_compact &rec,
+                           uint4 *buf) {
+    __shared__ uint32_t s_w[256 / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t bal = __ballot(slotted);
+    if (lane == 0) s_w[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();              // (also: every thread is done with what buf held)
+    uint32_t before = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < 256 / 64; ++w) {
+        before += w < wv ? s_w[w] : 0u;
+        agg += s_w[w];
+    }
+    hq_ready_compact *stage = reinterpret_cast<hq_ready_compact *>(buf);
+    if (slotted) stage[before + __popcll(bal & ((1ull << lane) - 1))] = rec;
+    __syncthreads();
+    char *dst = a.out + a.slot_off + tile * kSlotTileBytes;
+    const uint32_t nbytes = agg * (uint32_t)sizeof(hq_ready_compact);
+    for (uint32_t q = threadIdx.x; q < nbytes / 16; q += 256)
+        reinterpret_cast<uint4 *>(dst)[q] = buf[q];
+    if (threadIdx.x == 0) {
+        if (nbytes & 8)           // (an odd record count: the last 8 bytes)
+            reinterpret_cast<uint2 *>(dst)[nbytes / 8 - 1] =
+                reinterpret_cast<const uint2 *>(buf)[nbytes / 8 - 1];
+        reinterpret_cast<uint32_t *>(a.out + a.cnt_off)[tile] = agg;
+    }
+}
+
 template <bool WRITE, bool STREAM, int MC>
 __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32_t chunk = 0) {
     // pass A: the wave's counts summed in LDS, added to wsum by one lane (i_begin is a multiple
@@ -821,7 +898,9 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
         b1 = x1 & 0xFFFFFFFFu;
         if (!WRITE) {
             // the sizes' totals must be the ones the copies were sized by (checked once)
-            if (i + 1 == a.n && a.own_lo == 0 && (e1 != a.n_events || b1 != a.n_bytes))
+            // (2-byte words carry no events: the layout checks the events pass A counted)
+            if (i + 1 == a.n && a.own_lo == 0 &&
+                ((!a.bytes_only && e1 != a.n_events) || b1 != a.n_bytes))
                 atomicOr(a.error, (uint32_t)kErrBoffsets);
             if (b1 < a.own_lo || b1 >= a.own_hi) act = false;   // another chunk's group
         }
@@ -894,11 +973,13 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
         if (act && fits) src0 = reinterpret_cast<const uint8_t *>(sbuf) + (base + b0 - lo);
     }
     uint32_t n_ready = 0;
-    bool one_ready = false;
+    bool one_ready = false, slotted = false;
+    hq_ready_compact srec{};
     if (act) {
         hq_dread reads[kDReads];
         Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
         if (!WRITE) eng.save_old(h);
+        if (WRITE && STREAM && a.bytes_only) e0 = eng.base[kEvents];   // (the events' scan)
         __shared__ hq_ready_to_read stage[WRITE ? 256 / 64 : 1][WRITE ? kStageReady : 1];
         // list mode: the wave's groups are consecutive and so are their records, staged from its
         // first active lane's on; column mode: the groups replayed are a sparse subset whose records
@@ -931,10 +1012,21 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
                                  eng.cnt[kDeferred] | eng.cnt[kFallback]) != 0;
             const bool rerun = others || eng.cnt[kReady] > 1;
             one_ready = !rerun && eng.cnt[kReady] == 1;
+            if (a.slots && one_ready) {   // the record goes to the tile's slot, out of the list
+                const hq_ready_to_read r = a.ready_slot[i];
+                const int64_t delta = (int64_t)(r.index - eng.c0);
+                if (delta == (int64_t)(int32_t)delta) {
+                    slotted = true;
+                    one_ready = false;
+                    srec = hq_ready_compact{r.ctx_low, r.ctx_high, (uint32_t)i, (int32_t)delta};
+                    eng.cnt[kReady] = 0;
+                    eng.cnt[kSlotted] = 1;
+                }
+            }
             n_ready = eng.cnt[kReady];
             eng.cnt[kRerun] = rerun;
             for (int l = 0; l < kLists; ++l) a.counts[(uint64_t)l * a.n + i] = eng.cnt[l];
-            a.rerun[i] = (uint8_t)(2 | rerun | (one_ready ? 4 : 0));
+            a.rerun[i] = (uint8_t)(2 | rerun | (one_ready ? 4 : 0) | (slotted ? 8 : 0));
             eng.store(h);
             uint32_t *wt = wtot[threadIdx.x >> 6];   // (the lanes that left early add nothing)
             for (int l = 0; l < kLists; ++l)
@@ -952,6 +1044,8 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
     if constexpr (STAGE) {
         if (a.spec_ready)
             ready_tail(a, (a.i_begin >> 8) + blk, chunk, member, first, i, n_ready, one_ready, sbuf);
+        else if (a.slots)
+            slot_store(a, (a.i_begin >> 8) + blk, slotted, srec, sbuf);
     }
 }
 
@@ -960,7 +1054,7 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step(const StepK a) {
     if constexpr (!WRITE && STREAM) {   // tiles in start order (ready_tail's chained scan)
         const uint32_t b = draw_ticket(a.tickets + a.chunk);
         if (b >= gridDim.x) {     // tickets not zeroed: report, step nothing
-            if (threadIdx.x == 0) atomicOr(a.error, (uint32_t)kErrScan);
+            if (threadIdx.x == 0) atomicOr(a.error, (uint32_t)kErrTicket);
             return;
         }
         step_groups<WRITE, STREAM, MC>(a, b, a.chunk);
@@ -980,6 +1074,7 @@ struct JobMap {
     uint32_t chunk;               //   zeroes them
     StepK *table_out;             // k_size_sums (reading `ks` from its pinned copy): workgroup 0
                                   //   writes the jobs' StepK there for the later launches
+    uint32_t bsum_scanned, pad;   // k_size_apply: the tiles' totals were scanned (k_bsum_scan_jobs)
 };
 static_assert(sizeof(StepK) % 8 == 0, "k_size_sums copies the table in 8-byte words");
 
@@ -995,7 +1090,7 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step_jobs(const JobMap m) {
     if constexpr (!WRITE && STREAM) {
         b = draw_ticket(m.tickets + m.chunk);
         if (b >= gridDim.x) {
-            if (threadIdx.x == 0) atomicOr(m.ks[m.job0].error, (uint32_t)kErrScan);
+            if (threadIdx.x == 0) atomicOr(m.ks[m.job0].error, (uint32_t)kErrTicket);
             return;
         }
     }
@@ -1009,7 +1104,23 @@ __global__ __launch_bounds__(256) HQ_STEP_OCC void k_step_jobs(const JobMap m) {
 __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk, uint32_t *tickets) {
     const uint64_t i = blk * 256 + threadIdx.x;
     if (tickets && threadIdx.x < kTickets) tickets[threadIdx.x] = 0;   // (pass A's are done)
-    if (i < a.ws) a.wsum[i] = 0;  // (scanned already; the grid covers ws: 9 n / 64 + 10 <= max(n, 256))
+    if (i < a.ws) a.wsum[i] = 0;  // (scanned already; the grid covers ws: 11 n / 64 + 12 <= max(n, 256))
+    __shared__ __align__(16) hq_ready_to_read stage[256 / 64][kStageReady];
+    static_assert(sizeof(stage) >= kSlotTileBytes, "the slot staging fits the list's");
+    if (a.slots && !a.spec_valid && !(a.layout->error | a.layout->overflow)) {
+        // the output region grew after pass A wrote the slots into the old one: this tile's
+        // slots again, from the records pass A kept (whole workgroup; the tiles are pass A's)
+        const bool s = i < a.n && (a.rerun[i] & 8);
+        hq_ready_compact rec{};
+        if (s) {
+            const hq_ready_to_read r = a.ready_slot[i];
+            const uint32_t h = a.handles ? a.handles[i] : (uint32_t)i;
+            rec = hq_ready_compact{r.ctx_low, r.ctx_high, (uint32_t)i,
+                                   (int32_t)(int64_t)(r.index - a.groups_old[h].committed)};
+        }
+        slot_store(a, blk, s, rec, reinterpret_cast<uint4 *>(&stage[0][0]));
+        __syncthreads();          // (stage is the list's staging below)
+    }
     const bool in = i < a.n;
     if ((a.layout->error | a.layout->overflow) || !__ballot(in)) return;   // (whole waves)
     const uint32_t col = a.layout->commit_column;
@@ -1039,7 +1150,7 @@ __device__ __forceinline__ void lite_groups(const StepK &a, uint64_t blk, uint32
     // the single ReadyToReads pass A kept: the wave's records are consecutive in the list (its
     // groups are), staged in LDS at their places and stored as one contiguous run of 16-byte
     // lane stores; the places of the replayed groups' records are holes pass B fills afterwards
-    __shared__ hq_ready_to_read stage[256 / 64][kStageReady];
+    // (stage: declared above)
     if (!(col32 && a.spec_valid && a.spec_ready)) {   // (else pass A wrote them: ready_tail)
         constexpr uint64_t l = kReady;
         const uint64_t w = i >> 6;
@@ -1134,17 +1245,31 @@ constexpr int kMaxJobChunks = 8;   // the jobs path's chunks of whole jobs (even
 static_assert(kMaxChunks <= kMaxJobChunks, "the chunk events serve both paths");
 static_assert(kMaxJobChunks <= kTickets, "a ticket word per pass A launch");
 constexpr uint64_t kChunkGroups = 65536;
-// bnd[l] = the scan at l * nw (list l's first record), l = 0 .. kLists
+// the slot form's part of the host region ahead of the lists: the 4-byte column at 0, tile t's
+// slots at slot_off + 6144 t, the tiles' counts at cnt_off; returns its size (the lists' start)
+__host__ __device__ inline uint64_t slot_layout(uint64_t n, uint64_t *slot_off, uint64_t *cnt_off) {
+    const uint64_t tiles = (n + kSlotTile - 1) / kSlotTile;
+    const uint64_t so = (n * 4 + 255) & ~uint64_t(255);
+    const uint64_t co = so + tiles * kSlotTileBytes;
+    if (slot_off) *slot_off = so;
+    if (cnt_off) *cnt_off = co;
+    return co + ((tiles * 4 + 255) & ~uint64_t(255));
+}
+
+// bnd[l] = the scan at l * nw (list l's first record), l = 0 .. kLists; want_events: the step's
+// event total when pass A counted the events (2-byte size words), else ~0
 __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, uint64_t cap,
-                            uint32_t allow_column, Layout *lay, Layout *host_lay) {
+                            uint32_t allow_column, uint64_t want_events, Layout *lay,
+                            Layout *host_lay) {
     uint32_t *wide = error + 1;   // pass A: an advance of 2^32 or more
     uint32_t *ready_wide = error + 2;   // pass A: a ReadyToRead delta beyond 32 bits
+    if (want_events != ~uint64_t(0) && (uint64_t)(bnd[kEvents + 1] - bnd[kEvents]) != want_events)
+        *error |= kErrBoffsets;   // (the events decoded are not the totals the caller gave)
     lay->ready_compact = (allow_column & kReadyCompact) && !*ready_wide;
     const uint64_t rec[kLists] = {sizeof(hq_commit_event),
                                   lay->ready_compact ? sizeof(hq_ready_compact) : sizeof(hq_ready_to_read),
                                   sizeof(hq_read_index_resp), sizeof(hq_state_change),
-                                  sizeof(hq_dropped_read), 8, 8, 0, 0};
-    uint64_t total = 0;
+                                  sizeof(hq_dropped_read), 8, 8, 0, 0, 0, 0};
     const uint32_t commits = bnd[1] - bnd[0];
     // the commits as a column when that moves fewer bytes (16 per commit in the list against 8
     // per listed group, or 4 when every advance fits)
@@ -1152,22 +1277,32 @@ __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, ui
     lay->commit_column = (allow_column & kColumn32) && !*wide && 4 * (uint64_t)commits > n
                              ? kColumn32
                          : (allow_column & kColumn64) && 2 * (uint64_t)commits > n ? kColumn64 : 0;
+    // the slot form: the column and the slots pass A wrote come first, the lists after them
+    const bool slots = (allow_column & kReadySlots) != 0;
+    const uint64_t reserve = slots ? slot_layout(n, nullptr, nullptr) : 0;
+    uint64_t total = reserve;
     for (int l = 0; l < kLists; ++l) {
         const uint32_t len = bnd[l + 1] - bnd[l];
-        lay->off[l] = total;
         lay->len[l] = len;
+        if (l == kCommits && slots && lay->commit_column == kColumn32) {
+            lay->off[l] = 0;      // (where pass A wrote the advance words)
+            continue;
+        }
+        lay->off[l] = total;
         const uint64_t bytes = l == kCommits && lay->commit_column
                                    ? n * (lay->commit_column == kColumn32 ? 4 : 8)
                                    : len * rec[l];
         total += (bytes + 255) & ~uint64_t(255);
     }
     lay->total = total;
+    lay->reserve = reserve;
     lay->error = *error;
     lay->overflow = total > cap;
-    // pass A's flags are reset for the next step, except when the host will grow the region and
-    // run this layout again for the same step (overflow without an input error): the re-run must
-    // see the same flags, or it could choose the 4-byte advance column for a 2^32 advance
-    if (!(lay->overflow && !*error)) {
+    // pass A's flags are reset for the next step, except when the host will run this layout again
+    // for the same step and the re-run must see the same flags (or it could choose the 4-byte
+    // advance column for a 2^32 advance): an overflow without an input error (the region grows),
+    // or kErrScan alone (the copy-out runs again without pass A's records; the host clears it)
+    if (!((lay->overflow && !*error) || *error == kErrScan)) {
         *error = 0;
         *wide = 0;
         *ready_wide = 0;
@@ -1176,11 +1311,12 @@ __device__ void layout_from(const uint32_t *bnd, uint64_t n, uint32_t *error, ui
 }
 
 __global__ void k_layout(const uint32_t *scan, uint64_t n, uint64_t nw, uint32_t *error,
-                         uint64_t cap, uint32_t allow_column, Layout *lay, Layout *host_lay) {
+                         uint64_t cap, uint32_t allow_column, uint64_t want_events, Layout *lay,
+                         Layout *host_lay) {
     if (threadIdx.x != 0) return;
     uint32_t bnd[kLists + 1];
     for (int l = 0; l <= kLists; ++l) bnd[l] = scan[(uint64_t)l * nw];
-    layout_from(bnd, n, error, cap, allow_column, lay, host_lay);
+    layout_from(bnd, n, error, cap, allow_column, want_events, lay, host_lay);
 }
 
 // A small step's scan of the per-wave sums and its layout in one workgroup (hipcub's scan is two
@@ -1191,7 +1327,8 @@ constexpr int kScanT = 1024, kScanE = 11;
 constexpr uint64_t kScanSmall = 2 * kScanT * kScanE;   // sums taken this way (2 tiles)
 __device__ __forceinline__ void scan_layout(const uint32_t *wsum, uint32_t *scan, uint64_t ws,
                                             uint64_t n, uint64_t nw, uint32_t *error, uint64_t cap,
-                                            uint32_t allow_column, Layout *lay, Layout *host_lay) {
+                                            uint32_t allow_column, uint64_t want_events, Layout *lay,
+                                            Layout *host_lay) {
     __shared__ uint32_t tile[kScanT * kScanE];
     __shared__ uint32_t wtot[kScanT / 64];
     __shared__ uint32_t bnd[kLists + 1];
@@ -1238,22 +1375,26 @@ __device__ __forceinline__ void scan_layout(const uint32_t *wsum, uint32_t *scan
         carry += all;
         __syncthreads();          // (the next tile overwrites tile and wtot)
     }
-    if (t == 0) layout_from(bnd, n, error, cap, allow_column, lay, host_lay);
+    if (t == 0) layout_from(bnd, n, error, cap, allow_column, want_events, lay, host_lay);
 }
 
 __global__ __launch_bounds__(kScanT) void k_scan_layout(const uint32_t *wsum, uint32_t *scan,
                                                         uint64_t ws, uint64_t n, uint64_t nw,
                                                         uint32_t *error, uint64_t cap,
-                                                        uint32_t allow_column, Layout *lay,
-                                                        Layout *host_lay) {
-    scan_layout(wsum, scan, ws, n, nw, error, cap, allow_column, lay, host_lay);
+                                                        uint32_t allow_column, uint64_t want_events,
+                                                        Layout *lay, Layout *host_lay) {
+    scan_layout(wsum, scan, ws, n, nw, error, cap, allow_column, want_events, lay, host_lay);
+}
+
+__host__ __device__ inline uint64_t want_events_of(const StepK &a) {
+    return a.bytes_only ? a.n_events : ~uint64_t(0);
 }
 
 // the jobs path: one workgroup per job (grid = the jobs)
 __global__ __launch_bounds__(kScanT) void k_scan_layout_jobs(const StepK *ks) {
     const StepK &a = ks[blockIdx.x];
     scan_layout(a.wsum, const_cast<uint32_t *>(a.scan), a.ws, a.n, a.nw, a.error, a.out_cap,
-                a.allow_column, const_cast<Layout *>(a.layout), a.host_layout);
+                a.allow_column, want_events_of(a), const_cast<Layout *>(a.layout), a.host_layout);
 }
 
 // The jobs path's scan of a sized stream's sizes (the single path: hipcub over PackSize), in
@@ -1262,8 +1403,14 @@ __global__ __launch_bounds__(kScanT) void k_scan_layout_jobs(const StepK *ks) {
 // before group i << 32 | bytes before it, prefix[n] the totals (n + 1 elements, as the single
 // path's scan)
 constexpr uint32_t kSizeTile = 1024;   // groups per workgroup of 256 threads (4 each)
+// a job of more size tiles than this has its tiles' totals scanned by a launch of their own
+// (k_bsum_scan_jobs) instead of each k_size_apply workgroup summing the totals before it (the
+// sum's work grows with the square of the tiles: ~134 M L2 loads at 16 M groups)
+constexpr uint64_t kSizeApplyDirect = 2048;
 __device__ __forceinline__ uint64_t packed_size(const StepK &a, uint64_t i) {
-    const uint32_t s = i < a.n ? a.sizes[i] : 0;
+    if (i >= a.n) return 0;
+    if (a.bytes_only) return a.sizes16[i];
+    const uint32_t s = a.sizes[i];
     return (uint64_t)(s & 0xFFFFu) << 32 | (s >> 16);
 }
 
@@ -1299,7 +1446,27 @@ __global__ __launch_bounds__(256) void k_size_sums(const JobMap m) {
     const StepK &a = m.ks[m.job0 + j];
     const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
     uint64_t v = 0;
-    if (a.sizes_src) {            // the sizes straight from pinned host memory, kept on device
+    if (a.bytes_only && a.sizes16_src) {
+        // 2-byte words straight from pinned host memory (one 8-byte load of a thread's 4 where
+        // aligned and whole), kept on device for k_size_apply
+        uint16_t *dst = const_cast<uint16_t *>(a.sizes16);
+        uint16_t z[4];
+        if (i0 + 4 <= a.n && !(reinterpret_cast<uintptr_t>(a.sizes16_src) & 7)) {
+            const uint64_t w = *reinterpret_cast<const uint64_t *>(a.sizes16_src + i0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = (uint16_t)(w >> (16 * k));
+            *reinterpret_cast<uint64_t *>(dst + i0) = w;   // (dst: a 256-byte aligned region)
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t i = i0 + k;
+                z[k] = i < a.n ? a.sizes16_src[i] : 0;
+                if (i < a.n) dst[i] = z[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += z[k];
+    } else if (!a.bytes_only && a.sizes_src) {   // the sizes straight from pinned host memory
         uint32_t *dst = const_cast<uint32_t *>(a.sizes);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1317,16 +1484,36 @@ __global__ __launch_bounds__(256) void k_size_sums(const JobMap m) {
     if (threadIdx.x == 0) a.bsum[b] = tot;
 }
 
-// (each workgroup sums the totals of the blocks before its own: at most a few thousand words
-// from L2, in place of a scan launch between the two passes)
+// the size tiles' totals of every job scanned in place (exclusive), one workgroup per job: the
+// large steps' form (k_size_apply then reads its tile's prefix)
+__global__ __launch_bounds__(1024) void k_bsum_scan_jobs(const JobMap m) {
+    const StepK &a = m.ks[m.job0 + blockIdx.x];
+    const uint64_t nb = (a.n + 1 + kSizeTile - 1) / kSizeTile;
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += 1024) {
+        const uint64_t k = base + threadIdx.x;
+        const uint64_t v = k < nb ? a.bsum[k] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan(v, &tot);
+        if (k < nb) a.bsum[k] = carry + ex;
+        carry += tot;
+    }
+}
+
+// (a small job's workgroups each sum the totals of the tiles before their own: at most a few
+// thousand words from L2, in place of a scan launch between the two passes)
 __global__ __launch_bounds__(256) void k_size_apply(const JobMap m) {
     const uint32_t j = job_of(m, blockIdx.x);
     const StepK &a = m.ks[m.job0 + j];
     const uint64_t b = blockIdx.x - m.blk0[j], i0 = b * kSizeTile + threadIdx.x * 4;
-    uint64_t before = 0;
-    for (uint64_t k = threadIdx.x; k < b; k += 256) before += a.bsum[k];
     uint64_t base;
-    (void)block_excl_scan(before, &base);
+    if (m.bsum_scanned) {
+        base = a.bsum[b];
+    } else {
+        uint64_t before = 0;
+        for (uint64_t k = threadIdx.x; k < b; k += 256) before += a.bsum[k];
+        (void)block_excl_scan(before, &base);
+    }
     uint64_t v[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1356,6 +1543,7 @@ struct hq_dstep {
     // HQ_TEST_FAIL_REGROW=1 in the environment at open: the output region's regrow fails (the
     // failure path's test, tests/test_gpu_worker.py)
     bool test_fail_regrow = false;
+    bool test_scan_fail = false;  // HQ_TEST_SCAN_FAIL=1 at open: pass A's look-backs give up
     hq_dgroup *groups = nullptr;
     hq_dread *reads = nullptr;
     hq_dmember *members = nullptr;
@@ -1410,6 +1598,13 @@ struct hq_dstep {
     bool tickets_dirty = false;
     uint64_t *tiles = nullptr;
     size_t tiles_cap = 0;         // (bytes)
+    // how the step's thread waits for the device (hq_dstep_set_wait; HQ_WAIT_*) and the clock of
+    // the last wait: the device's 100-MHz stamp after the step's last kernel (HQ_WAIT_CLOCK), in
+    // pinned memory
+    uint32_t wait_mode = HQ_WAIT_BLOCK, wait_poll_us = 50, wait_sleep_us = 20;
+    bool wait_clock = false;
+    uint64_t *clock_host = nullptr;
+    hq_wait_clock last_wait{};
 };
 
 namespace {
@@ -1433,26 +1628,90 @@ int grow(hq_ctx *ctx, void **p, size_t *cap, size_t need, bool keep, const char 
 
 namespace {
 
-// Wait for a stream: poll briefly (a one-worker step's sync is short), then sleep on a
-// blocking-sync event, so that 16 workers waiting at once do not spin 16 host cores (a spinning
-// wait under a CPU quota stalls every thread of the process for the rest of the period). spin_us
-// above 50: the poll yields now and then (the jobs path's one waiter, HQ_STEP_JOBS_SPIN_US)
-int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us = 50) {
+// Wait for a stream on the step's thread, as d's policy says (hq_dstep_set_wait), its clock in
+// d->last_wait:
+//   HQ_WAIT_BLOCK  poll for poll_us, then sleep on a blocking-sync event (the runtime's interrupt
+//                  wait): 16 workers waiting at once do not spin 16 host cores (a spinning wait
+//                  under a CPU quota stalls every thread of the process for the rest of the
+//                  period); spin_us > 50 (the jobs path's one waiter, HQ_STEP_JOBS_SPIN_US) polls
+//                  longer, yielding now and then
+//   HQ_WAIT_SLEEP  poll for poll_us, then query the event every sleep_us, asleep in between (a
+//                  timer wake-up: its lateness is bounded by the timer's slack, not by the
+//                  runtime's interrupt path)
+//   HQ_WAIT_SPIN   poll with yields until done (a core held for the step)
+// With HQ_WAIT_CLOCK a one-thread kernel behind the step writes the device's constant clock into
+// pinned memory: the step's end on the device's clock, against which the host's wake-up is read
+__global__ void k_clock_stamp(uint64_t *dst) {
+    if (threadIdx.x == 0) *dst = wall_clock64();
+}
+
+int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us = 0) {
     hq_ctx *ctx = d->ctx;
-    int rc = hq::check_hip(ctx, hipEventRecord(d->ev_sync, s), what);
+    hq_wait_clock &wc = d->last_wait;
+    wc = hq_wait_clock{};
+    int rc = HQ_OK;
+    if (d->wait_clock) {
+        d->clock_host[0] = 0;
+        hipLaunchKernelGGL(k_clock_stamp, dim3(1), dim3(64), 0, s, d->clock_host);
+        rc = hq::check_hip(ctx, hipGetLastError(), "k_clock_stamp");
+    }
+    if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->ev_sync, s), what);
     if (rc) return rc;
-    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t mode = d->wait_mode;
+    const uint32_t poll_us = spin_us ? spin_us : d->wait_poll_us;
+    const uint64_t t0 = now_ns();
+    wc.t_begin_ns = t0;
+    auto done = [&](int r) {
+        wc.t_end_ns = now_ns();
+        if (d->wait_clock && !r) wc.device_end_ticks = d->clock_host[0];
+        return r;
+    };
     for (uint32_t k = 0;; ++k) {
         const hipError_t q = hipEventQuery(d->ev_sync);
-        if (q == hipSuccess) return HQ_OK;
-        if (q != hipErrorNotReady) return hq::check_hip(ctx, q, what);
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
-        if (spin_us > 50 && (k & 15) == 15) std::this_thread::yield();
+        if (q == hipSuccess) {
+            wc.poll_ns = now_ns() - t0;
+            return done(HQ_OK);
+        }
+        if (q != hipErrorNotReady) return done(hq::check_hip(ctx, q, what));
+        if (mode != HQ_WAIT_SPIN && now_ns() - t0 > (uint64_t)poll_us * 1000) break;
+        if ((mode == HQ_WAIT_SPIN || poll_us > 50) && (k & 15) == 15) std::this_thread::yield();
     }
-    return hq::check_hip(ctx, hipEventSynchronize(d->ev_sync), what);
+    const uint64_t t1 = now_ns();
+    wc.poll_ns = t1 - t0;
+    if (mode == HQ_WAIT_SLEEP) {
+        for (;;) {
+            std::this_thread::sleep_for(std::chrono::microseconds(d->wait_sleep_us));
+            ++wc.sleeps;
+            const hipError_t q = hipEventQuery(d->ev_sync);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return done(hq::check_hip(ctx, q, what));
+        }
+        wc.sleep_ns = now_ns() - t1;
+        return done(HQ_OK);
+    }
+    wc.sleeps = 1;
+    rc = hq::check_hip(ctx, hipEventSynchronize(d->ev_sync), what);
+    wc.sleep_ns = now_ns() - t1;
+    return done(rc);
 }
 
 }  // namespace
+
+int hq_dstep_set_wait(hq_dstep *d, uint32_t mode, uint32_t poll_us, uint32_t sleep_us) {
+    const uint32_t m = mode & ~HQ_WAIT_CLOCK;
+    if (m != HQ_WAIT_BLOCK && m != HQ_WAIT_SLEEP && m != HQ_WAIT_SPIN) return HQ_E_INVAL;
+    if (m == HQ_WAIT_SLEEP && sleep_us == 0) return HQ_E_INVAL;
+    if ((mode & HQ_WAIT_CLOCK) && !d->clock_host) {
+        int rc = hq::check_hip(d->ctx, hipHostMalloc(&d->clock_host, 64, hipHostMallocDefault),
+                               "hq_dstep clock");
+        if (rc) return rc;
+    }
+    d->wait_mode = m;
+    d->wait_poll_us = poll_us;
+    d->wait_sleep_us = sleep_us;
+    d->wait_clock = (mode & HQ_WAIT_CLOCK) != 0;
+    return HQ_OK;
+}
 
 int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
     *out = new (std::nothrow) hq_dstep();
@@ -1461,6 +1720,7 @@ int hq_dstep_open(hq_ctx *ctx, hq_dstep **out, uint32_t commit_column) {
     d->ctx = ctx;
     d->commit_column = commit_column;
     if (const char *f = std::getenv("HQ_TEST_FAIL_REGROW")) d->test_fail_regrow = std::atoi(f) != 0;
+    if (const char *f = std::getenv("HQ_TEST_SCAN_FAIL")) d->test_scan_fail = std::atoi(f) != 0;
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     if (!rc)
         rc = hq::check_hip(ctx, hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming |
@@ -1501,6 +1761,7 @@ void hq_dstep_close(hq_dstep *d) {
     if (d->host_out) (void)hipHostFree(d->host_out);
     if (d->jobs_host) (void)hipHostFree(d->jobs_host);
     if (d->host_layout) (void)hipHostFree(d->host_layout);
+    if (d->clock_host) (void)hipHostFree(d->clock_host);
     for (hipStream_t cs : {d->copy, d->copy2}) {
         if (cs) {
             (void)hipStreamSynchronize(cs);
@@ -1636,8 +1897,9 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
     const hq_dstep_in *in = r.in;
     const uint64_t n = r.n = in->n;
     r.stream = in->bytes != nullptr;
-    r.sized = r.stream && in->sizes != nullptr;   // per-group sizes, scanned here
+    r.sized = r.stream && (in->sizes != nullptr || in->sizes16 != nullptr);   // scanned here
     const bool stream = r.stream, sized = r.sized;
+    const bool s16 = sized && in->sizes16 != nullptr;   // 2-byte words: bytes only
     const uint64_t ne = r.ne = sized ? in->n_events : in->offsets[n];
     const uint64_t nb = r.nb = !stream ? 0 : sized ? in->n_bytes : in->boffsets[n];
     if (sized && (ne >> 32 || nb >> 32))     // the scanned prefixes pack both totals in 64 bits
@@ -1708,7 +1970,8 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
     }
     const hipcub::TransformInputIterator<uint64_t, PackSize, hipcub::CountingInputIterator<uint64_t>>
         packed_sizes(hipcub::CountingInputIterator<uint64_t>(0),
-                     PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n});
+                     PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n,
+                              s16 ? reinterpret_cast<const uint16_t *>(din + r.o_off) : nullptr});
     uint64_t *prefix = reinterpret_cast<uint64_t *>(din + r.o_boff);
     uint32_t *wsum = d->wsum;
     // (the jobs path scans with its own kernels: no hipcub temporary, whose size query costs
@@ -1742,6 +2005,8 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
         k.prefix = prefix;
         k.bytes = reinterpret_cast<const uint8_t *>(din + r.o_ev);
         k.sizes = reinterpret_cast<const uint32_t *>(din + r.o_off);
+        k.sizes16 = reinterpret_cast<const uint16_t *>(din + r.o_off);   // (one of the two)
+        k.bytes_only = s16;
         k.bsum = static_cast<uint64_t *>(d->scan_tmp);
     } else if (stream) {
         k.boffsets = reinterpret_cast<const uint64_t *>(din + r.o_boff);
@@ -1759,8 +2024,10 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
     k.n_events = ne;
     k.n_bytes = nb;
     k.stamp = d->stamp;
-    if (++d->step_no == 0) {      // stamps wrap: forget them
-        rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp, 0, d->gcap * 4, s), "memset");
+    if (++d->step_no == 0) {      // stamps wrap: forget them, and the chained-scan words
+        rc = hq::check_hip(ctx, hipMemsetAsync(d->stamp, 0, d->gcap * 4, s), "memset");   // (tagged
+        if (!rc && d->tiles)                                                               // with it)
+            rc = hq::check_hip(ctx, hipMemsetAsync(d->tiles, 0, d->tiles_cap, s), "memset");
         d->step_no = 1;
         if (rc) return rc;
     }
@@ -1800,9 +2067,32 @@ int prepare(Run &r, hipStream_t s, bool jobs = false) {
     k.rerun_list = d->rerun_list;
     k.ready_slot = d->ready_slot;
     k.out_cap = d->host_out_cap;
-    k.allow_column = d->commit_column;
+    k.test_scan_fail = d->test_scan_fail;
+    k.allow_column = d->commit_column & ~kReadySlots;
     k.host_layout = d->host_layout;
     r.small = d->max_members <= 8;   // member slots in registers: 8 or kDMembers
+    // HQ_WORKER_READY_SLOTS: a stream step of the jobs path (pass A's tiles are whole 256-group
+    // blocks of one launch there) with the advance column allowed writes the slots; the host region
+    // is grown ahead of pass A to hold the column, the slots and room for the lists
+    if (jobs && stream && (d->commit_column & kReadySlots) && (d->commit_column & kColumn32)) {
+        const uint64_t reserve = slot_layout(n, &k.slot_off, &k.cnt_off);
+        const size_t want = reserve + std::max<size_t>(n * 16, 1 << 16);
+        if (d->host_out_cap < want) {
+            void *grown = nullptr;
+            rc = hq::check_hip(ctx, hipHostMalloc(&grown, want, hipHostMallocDefault),
+                               "hq_dstep pinned output");
+            if (rc) return rc;
+            if (d->host_out) (void)hipHostFree(d->host_out);
+            d->host_out = grown;
+            d->host_out_cap = want;
+            k.out = static_cast<char *>(d->host_out);
+            k.out_cap = want;
+            k.spec_col = n * 4 <= want;
+            k.spec_valid = k.spec_col;
+        }
+        k.slots = 1;
+        k.allow_column |= kReadySlots;
+    }
     return HQ_OK;
 }
 
@@ -1841,11 +2131,11 @@ void pass_b(Run &r) {
     if (!r.rc && r.small_scan && r.first) {
         hipLaunchKernelGGL(k_scan_layout, dim3(1), dim3(kScanT), 0, ctx->stream, d->wsum, d->scan,
                            (uint64_t)r.ws, r.n, r.nw, k.error, (uint64_t)d->host_out_cap,
-                           (uint32_t)d->commit_column, d->layout, d->host_layout);
+                           k.allow_column, want_events_of(k), d->layout, d->host_layout);
         r.rc = hq::check_hip(ctx, hipGetLastError(), "k_scan_layout");
     } else if (!r.rc) {
         hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, ctx->stream, d->scan, r.n, r.nw, k.error,
-                           (uint64_t)d->host_out_cap, (uint32_t)d->commit_column, d->layout,
+                           (uint64_t)d->host_out_cap, k.allow_column, want_events_of(k), d->layout,
                            d->host_layout);
         r.rc = hq::check_hip(ctx, hipGetLastError(), "k_layout");
     }
@@ -1897,14 +2187,14 @@ const T *pinned_on_device(const T *p) {
                                        (reinterpret_cast<const char *>(p) - hp));
 }
 
-// HQ_STEP_JOBS_SPIN_US: how long the jobs path's one waiting thread polls before it sleeps on the
-// blocking event (default 50 us, as the per-worker waits). Polling through the whole step
+// HQ_STEP_JOBS_SPIN_US: how long the jobs path's one waiting thread polls before it waits as the
+// policy says (unset: the policy's poll, hq_worker_set_wait). Polling through the whole step
 // (5000) gained nothing device-only and cost end to end: the poller takes a core from the
 // producer's encode (tools/ab_spin.sh, step5 e2e 5.16 -> 5.37 ms)
 uint32_t jobs_spin_us() {
     static const uint32_t us = [] {
         const char *v = std::getenv("HQ_STEP_JOBS_SPIN_US");
-        return v ? (uint32_t)std::atoi(v) : 50u;
+        return v ? (uint32_t)std::atoi(v) : 0u;
     }();
     return us;
 }
@@ -1934,6 +2224,17 @@ int finish(Run &r) {
     hq_dstep_out *out = r.out;
     if (r.rc) return restore(r, r.rc);
     const Layout &lay = *d->host_layout;
+    if (lay.error == kErrScan) {
+        // pass A's chained scan of the ReadyToRead places gave up on a stalled predecessor
+        // (only the copy-out is affected, not a group's step): the layout again, and k_step_lite
+        // writes every single ReadyToRead, as when pass A does not (spec_ready off). The layout
+        // kept pass A's flags for this; its error word is cleared here
+        r.k.spec_ready = 0;
+        int rc = hq::check_hip(ctx, hipMemsetAsync(r.k.error, 0, 4, ctx->stream), "memset");
+        if (rc) return restore(r, rc);
+        pass_b(r);
+        if (r.rc) return restore(r, r.rc);
+    }
     if (lay.error) {              // no group state is written: pass A's is taken back
         const int rc = restore(r, HQ_OK);
         if (rc) return rc;
@@ -1964,6 +2265,13 @@ int finish(Run &r) {
             return restore(r, hq::fail(ctx, HQ_E_STATE, "hq_dstep: output layout"));
     }
     const char *ho = static_cast<const char *>(d->host_out);
+    if (lay.reserve) {            // the slot form (pass A's, or k_step_lite's after a regrow)
+        out->ready_slots = reinterpret_cast<const hq_ready_compact *>(ho + r.k.slot_off);
+        out->slot_counts = reinterpret_cast<const uint32_t *>(ho + r.k.cnt_off);
+        out->n_tiles = (r.n + kSlotTile - 1) / kSlotTile;
+        out->n_slotted = lay.len[kSlotted];
+    }
+    out->wait = d->last_wait;
     out->commits = lay.commit_column ? nullptr
                                      : reinterpret_cast<const hq_commit_event *>(ho + lay.off[kCommits]);
     out->commit_col = lay.commit_column == kColumn64
@@ -1992,6 +2300,7 @@ int finish(Run &r) {
     out->d2h_ns = now_ns() - r.t1;
     out->submit_ns = r.t_sub > r.t0 ? r.t_sub - r.t0 : 0;
     out->gpu_ns = r.gpu_ns;
+    out->gpu_jobs = 1;
     return HQ_OK;
 }
 
@@ -2004,7 +2313,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
     // one launch (the stream staged through LDS), where this path's chunked copies put the
     // first chunk's copy ahead of pass A and the last chunk's pass A behind the copies
     // (HQ_STEP_SINGLE_JOBS=0: this path, A/B)
-    if (in->sizes && in->bytes && single_as_job_allowed() && pinned_on_device(in->bytes)) {
+    if ((in->sizes || in->sizes16) && in->bytes && single_as_job_allowed() &&
+        pinned_on_device(in->bytes)) {
         int rc1 = HQ_OK;
         const int rc = hq_dstep_run_jobs(&d, in, out, &rc1, 1);
         return rc1 ? rc1 : rc;
@@ -2049,7 +2359,8 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         // stream beside them (behind the sizes on one stream the first bytes copy started
         // 50-65 us after the sizes' copy ended)
         if (in->groups) h2d(0, in->groups, n * 4, ctx->stream);   // NULL: handles 0 .. n - 1
-        h2d(r.o_off, in->sizes, n * 4, ctx->stream);
+        if (in->sizes16) h2d(r.o_off, in->sizes16, n * 2, ctx->stream);
+        else h2d(r.o_off, in->sizes, n * 4, ctx->stream);
         for (int c = 0; c < chunks && !rc; ++c) {
             const uint64_t lo = nb * c / chunks, hi = nb * (c + 1) / chunks;
             h2d(r.o_ev + lo, in->bytes + lo, hi - lo);
@@ -2058,7 +2369,9 @@ int hq_dstep_run(hq_dstep *d, const hq_dstep_in *in, hq_dstep_out *out) {
         const hipcub::TransformInputIterator<uint64_t, PackSize,
                                              hipcub::CountingInputIterator<uint64_t>>
             packed_sizes(hipcub::CountingInputIterator<uint64_t>(0),
-                         PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n});
+                         PackSize{reinterpret_cast<const uint32_t *>(din + r.o_off), n,
+                                  in->sizes16 ? reinterpret_cast<const uint16_t *>(din + r.o_off)
+                                              : nullptr});
         if (!rc) rc = hq::check_hip(ctx, hipcub::DeviceScan::ExclusiveSum(
                                               d->scan_tmp, r.tmp2, packed_sizes,
                                               const_cast<uint64_t *>(r.k.prefix), n + 1,
@@ -2135,7 +2448,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     for (uint32_t j = 0; j < count; ++j) {
         outs[j] = hq_dstep_out{};
         rcs[j] = HQ_OK;
-        if (ds[j]->ctx->device != ctx->device || !ins[j].sizes || !ins[j].bytes) {
+        if (ds[j]->ctx->device != ctx->device || !(ins[j].sizes || ins[j].sizes16) || !ins[j].bytes) {
             rcs[j] = hq::fail(ds[j]->ctx, HQ_E_INVAL, "hq_dstep_run_jobs: a sized stream step "
                                                       "on the first job's device");
             continue;
@@ -2184,7 +2497,8 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         Run &r = runs[live[x]];
         // sizes in pinned host memory are read by k_size_sums over the link: no copy per job
         // (16 workers' 256 KB size copies took 340 us one after another, with their gaps)
-        r.k.sizes_src = pinned_on_device(r.in->sizes);
+        if (r.in->sizes16) r.k.sizes16_src = pinned_on_device(r.in->sizes16);
+        else r.k.sizes_src = pinned_on_device(r.in->sizes);
         d0->jobs_host[x] = r.k;
         small = small && r.small;
         total_bytes += r.nb;
@@ -2234,7 +2548,11 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         const Run &r = runs[live[x]];
         char *din = static_cast<char *>(r.d->in);
         if (r.in->groups) h2d(din, r.in->groups, r.n * 4, s);
-        if (!r.k.sizes_src) h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
+        if (r.in->sizes16) {
+            if (!r.k.sizes16_src) h2d(din + r.o_off, r.in->sizes16, r.n * 2, s);
+        } else if (!r.k.sizes_src) {
+            h2d(din + r.o_off, r.in->sizes, r.n * 4, s);
+        }
     }
     if (!rc) {
         // every job's stream in pinned host memory: pass A (and pass B) read it in place, in one
@@ -2258,7 +2576,9 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
             rc = hq::check_hip(ctx, hipMemcpyAsync(d0->jobs_dev, d0->jobs_host, nl * sizeof(StepK),
                                                    hipMemcpyHostToDevice, s), "hq_dstep jobs");
     }
-    const JobMap sm = map(0, nl, kSizeTile, 1);
+    JobMap sm = map(0, nl, kSizeTile, 1);
+    for (uint32_t x = 0; x < nl; ++x)   // (a large job: its size tiles' totals get their own scan)
+        if ((runs[live[x]].n + kSizeTile) / kSizeTile > kSizeApplyDirect) sm.bsum_scanned = 1;
     if (!rc) {
         // k_size_sums reads the table from its pinned copy and writes it to the device for the
         // launches behind it: no copy of its own (a blit launch and ~10 us of host time)
@@ -2293,6 +2613,10 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_in2[c], d0->copy2), "event");
     };
     copies(0);
+    if (!rc && sm.bsum_scanned) {
+        hipLaunchKernelGGL(k_bsum_scan_jobs, dim3(nl), dim3(1024), 0, s, sm);
+        launched("k_bsum_scan_jobs");
+    }
     if (!rc) {
         hipLaunchKernelGGL(k_size_apply, dim3(sm.blk0[nl]), dim3(256), 0, s, sm);
         launched("k_size_apply");
@@ -2335,8 +2659,8 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
                                "hipcub scan");
         if (!rc) {
             hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, s, dj->scan, r0.n, r0.nw, r0.k.error,
-                               (uint64_t)dj->host_out_cap, (uint32_t)dj->commit_column, dj->layout,
-                               dj->host_layout);
+                               (uint64_t)dj->host_out_cap, r0.k.allow_column, want_events_of(r0.k),
+                               dj->layout, dj->host_layout);
             launched("k_layout");
         }
     } else if (!rc) {
@@ -2369,6 +2693,7 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
             if (cs) (void)hipStreamSynchronize(cs);
     }
     const uint64_t t1 = now_ns();
+    const hq_wait_clock w = d0->last_wait;   // (the one wait, before any job's own re-run)
     int first_rc = HQ_OK;
     for (uint32_t x = 0; x < nl; ++x) {
         Run &r = runs[live[x]];
@@ -2378,6 +2703,8 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
         r.t_sub = tp[3];
         r.gpu_ns = gpu_ns;
         rcs[live[x]] = finish(r);
+        outs[live[x]].wait = w;
+        outs[live[x]].gpu_jobs = nl;
         if (rcs[live[x]] && !first_rc) first_rc = rcs[live[x]];
     }
     if (trace) {

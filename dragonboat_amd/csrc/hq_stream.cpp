@@ -16,6 +16,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -331,7 +332,7 @@ inline uint64_t encode_unit(uint8_t *&p, const hq_event *events, uint64_t e, uin
 int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, uint64_t g0,
                 uint64_t g1, std::vector<uint8_t> *grow, uint8_t *out, uint64_t cap,
                 uint64_t *n_events, uint64_t *n_bytes, uint64_t *last_start = nullptr,
-                uint64_t pos0 = 0) {
+                uint64_t pos0 = 0, uint16_t *sizes16 = nullptr) {
     uint64_t pos = pos0, events = 0, ls = ~0ull;
     uint8_t *base = grow ? grow->data() : out;
     for (uint64_t i = g0; i < g1; ++i) {
@@ -378,7 +379,8 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
         pos = (uint64_t)(p - base);
         if (lp) ls = (uint64_t)(lp - base) - pos0;
         if (ne > 0xFFFF || pos - p0 > 0xFFFF) return HQ_E_INVAL;
-        sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
+        if (sizes16) sizes16[i] = (uint16_t)(pos - p0);   // (2-byte words: bytes only)
+        else sizes[i] = (uint32_t)ne | (uint32_t)(pos - p0) << 16;
         events += ne;
     }
     *n_events = events;
@@ -431,27 +433,39 @@ public:
     }
     // gang: the T indexes run at the same time (each may wait for the others: a barrier inside
     // fn); the caller runs index 0 only and every other index gets a pool thread of its own (the
-    // pool holds a thread per queued index of every live call, so the gang always assembles)
-    void parallel_for(uint32_t T, const std::function<void(uint32_t)> &fn, bool gang = false) {
+    // pool holds a thread per queued index of every live call, so the gang always assembles).
+    // The pool holds at most kMaxThreads threads: a call whose indexes would need more waits
+    // until earlier calls have finished (T - 1 <= kMaxThreads: callers clamp T). HQ_E_NOMEM when
+    // a thread cannot be started (nothing of the call run).
+    static constexpr uint32_t kMaxThreads = 256;
+    int parallel_for(uint32_t T, const std::function<void(uint32_t)> &fn, bool gang = false) {
         if (T <= 1) {
             if (T) fn(0);
-            return;
+            return HQ_OK;
         }
+        if (T - 1 > kMaxThreads) return HQ_E_INVAL;
 #ifdef HQ_ENCODE_SPAWN          // A/B (tools/lib_encspawn): fresh threads for every phase
         std::vector<std::thread> th;
         for (uint32_t t = 1; t < T; ++t) th.emplace_back(fn, t);
         fn(0);
         for (auto &x : th) x.join();
-        return;
+        return HQ_OK;
 #endif
         auto job = std::make_shared<Job>();
         job->fn = &fn;
         job->T = T;
-        job->queued = now_ns();
         {
-            std::lock_guard<std::mutex> lk(mu_);
+            std::unique_lock<std::mutex> lk(mu_);
+            room_.wait(lk, [&] { return demand_ + (T - 1) <= kMaxThreads; });
             demand_ += T - 1;
-            while (th_.size() < demand_) th_.emplace_back([this] { loop(); });
+            try {
+                while (th_.size() < demand_) th_.emplace_back([this] { loop(); });
+            } catch (const std::system_error &) {   // (no thread: the call does not start)
+                demand_ -= T - 1;
+                room_.notify_all();
+                return HQ_E_NOMEM;
+            }
+            job->queued = now_ns();
             for (uint32_t t = 1; t < T; ++t) q_.push_back(job);
         }
         cv_.notify_all();
@@ -467,6 +481,8 @@ public:
         }
         std::lock_guard<std::mutex> lk(mu_);
         demand_ -= T - 1;
+        room_.notify_all();
+        return HQ_OK;
     }
 
 private:
@@ -507,12 +523,83 @@ private:
         }
     }
     std::mutex mu_;
-    std::condition_variable cv_;
+    std::condition_variable cv_, room_;
     std::deque<std::shared_ptr<Job>> q_;
     std::vector<std::thread> th_;
     size_t demand_ = 0;
     bool stop_ = false;
 };
+
+// One event of a group's bytes at p (pv, run_left: the group's decoder state, as the encoder
+// left it); false when the bytes do not hold a whole event
+bool decode_one(const uint8_t *&p, const uint8_t *end, Prev &pv, uint64_t &run_left, hq_event &v) {
+    std::memset(&v, 0, sizeof v);
+    if (p >= end && !run_left) return false;
+    const uint8_t h = run_left ? (uint8_t)0 : *p;
+    if (run_left || ((h & 7) == HQ_EV_MESSAGE && ((h >> 3) & 7) == kCodeRun)) {
+        // a run member: the group's previous message with another sender
+        if (!run_left) {
+            ++p;
+            if (!pv.last || !get(p, end, run_left) || run_left == 0) return false;
+        }
+        --run_left;
+        v.kind = HQ_EV_MESSAGE;
+        v.type = pv.last == 1 ? HQ_MSG_REPLICATE_RESP : HQ_MSG_HEARTBEAT_RESP;
+        v.reject = pv.last_reject;
+        v.term = pv.term;
+        if (pv.last == 1) {
+            v.log_index = pv.index;
+        } else {
+            v.hint = pv.hint;
+            v.hint_high = pv.high;
+        }
+        return get(p, end, v.from);
+    }
+    ++p;
+    v.kind = h & 7;
+    bool ok = true;
+    if (v.kind == HQ_EV_READ) {
+        ok = get(p, end, v.hint) && get(p, end, v.hint_high);
+    } else if (v.kind == HQ_EV_PROPOSE) {
+        ok = get(p, end, v.log_index);
+    } else if (v.kind == HQ_EV_MESSAGE) {
+        const uint32_t code = (h >> 3) & 7;
+        uint64_t t = code_type(code);
+        if (code == 7) ok = get(p, end, t);
+        if (code == 4) ok = pv.have_index;  // repeats an index the group has not sent
+        v.type = (uint32_t)t;
+        v.reject = (h >> 6) & 1;
+        ok = ok && get(p, end, v.from);
+        if (ok && !(h & 0x80)) ok = get(p, end, pv.term);
+        v.term = pv.term;
+        if (ok && (code == 0 || code == 7)) ok = get(p, end, v.log_index);
+        if (code == 4) v.log_index = pv.index;
+        if (ok && (code == 2 || code == 3 || code == 7))
+            ok = get(p, end, v.hint) && get(p, end, v.hint_high);
+        if (code == 5) {
+            v.hint = pv.hint;
+            v.hint_high = pv.high;
+        }
+        if (ok && (code == 0 || code == 4)) {
+            pv.index = v.log_index;
+            pv.have_index = true;
+        }
+        if (ok && (code == 2 || code == 5)) {
+            pv.hint = v.hint;
+            pv.high = v.hint_high;
+        }
+        pv.last = last_of(code);
+        pv.last_reject = (uint8_t)v.reject;
+    }
+    return ok;
+}
+
+// a pool thread's encode scratch is kept for its next call (first touched on its memory node),
+// unless a call grew it past kKeepScratch: then it is released
+constexpr size_t kKeepScratch = size_t(256) << 20;
+inline void shrink_scratch(std::vector<uint8_t> &v) {
+    if (v.capacity() > kKeepScratch) std::vector<uint8_t>().swap(v);
+}
 
 TaskPool &task_pool() {
     static TaskPool p;
@@ -532,8 +619,8 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     *n_events = *n_bytes = 0;
     if (n_groups && offsets16[n_groups] > offsets16[0] && !out) return HQ_E_STATE;
     const uint64_t nrec = n_groups ? offsets16[n_groups] - offsets16[0] : 0;
-    const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(threads, 1u),
-                                                    std::max<uint64_t>(1, nrec / 4096));
+    const uint32_t T = (uint32_t)std::min<uint64_t>(
+        {std::max(threads, 1u), std::max<uint64_t>(1, nrec / 4096), TaskPool::kMaxThreads + 1});
     // one thread encodes straight into out (through a scratch of its own it was slower: 59
     // against 38 ms for the step5 producer on one fresh thread, profiles/r05b/enc_probe.log)
     if (T <= 1)
@@ -562,7 +649,7 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     int rc = HQ_OK;
     bool fits = true;
     std::vector<uint64_t> at(T, 0);
-    task_pool().parallel_for(T, [&](uint32_t t) {
+    const int prc = task_pool().parallel_for(T, [&](uint32_t t) {
         thread_local std::vector<uint8_t> scratch;
         res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch, nullptr, 0,
                                 &res[t].events, &res[t].bytes, &res[t].last_start);
@@ -588,7 +675,9 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
             }
         }
         if (!rc && fits && res[t].bytes) std::memcpy(out + at[t], scratch.data(), res[t].bytes);
+        shrink_scratch(scratch);
     }, true);
+    if (prc) return prc;
     if (!rc && !fits) rc = HQ_E_STATE;
     if (!rc) {
         *n_events = events;
@@ -613,7 +702,8 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
         b.n_events = b.n_bytes = 0;
         b.rc = HQ_OK;
         const uint64_t n = b.n_groups;
-        if (!b.offsets16 || (n && !b.sizes) || (n && b.offsets16[n] > b.offsets16[0] && !b.recs))
+        if (!b.offsets16 || (n && !b.sizes && !b.sizes16) ||
+            (n && b.offsets16[n] > b.offsets16[0] && !b.recs))
             b.rc = HQ_E_INVAL;
         else if (n && b.offsets16[n] > b.offsets16[0] && !b.out)
             b.rc = HQ_E_STATE;
@@ -624,7 +714,8 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
         if (b.rc && !first) first = b.rc;
     }
     const uint64_t R = rec0[count];
-    const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(threads, 1u), std::max<uint64_t>(1, R / 4096));
+    const uint32_t T = (uint32_t)std::min<uint64_t>(
+        {std::max(threads, 1u), std::max<uint64_t>(1, R / 4096), TaskPool::kMaxThreads + 1});
     if (live.empty()) return first;
     const uint64_t c0 = now_ns();
     // job j's groups split at the global record cuts R t / T (group boundaries): range t of the
@@ -657,7 +748,7 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
     // per job, per thread: where the thread's piece goes in the job's bytes
     std::vector<uint64_t> place((size_t)count * T, 0);
     std::vector<uint8_t> fits(count, 1);
-    task_pool().parallel_for(T, [&](uint32_t t) {
+    const int prc = task_pool().parallel_for(T, [&](uint32_t t) {
         thread_local std::vector<uint8_t> scratch;
         std::vector<Piece> &ps = pieces[t];
         uint64_t pos = 0;
@@ -668,7 +759,7 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
             Piece pc{j, pos, 0, 0, ~0ull, HQ_OK};
             // (the piece follows the thread's earlier pieces in its scratch)
             pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &scratch, nullptr, 0,
-                                &pc.events, &pc.bytes, &pc.last_start, pos);
+                                &pc.events, &pc.bytes, &pc.last_start, pos, b.sizes16);
             if (pc.rc) pc.bytes = 0;
             pos += pc.bytes;
             ps.push_back(pc);
@@ -707,7 +798,12 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
             if (!b.rc && pc.bytes)
                 std::memcpy(b.out + place[(size_t)pc.job * T + t], scratch.data() + pc.at, pc.bytes);
         }
+        shrink_scratch(scratch);
     }, true);
+    if (prc) {                    // (nothing encoded)
+        for (uint32_t j : live) jobs[j].rc = prc;
+        return prc;
+    }
     first = HQ_OK;
     for (uint32_t j = 0; j < count && !first; ++j) first = jobs[j].rc;
     const uint64_t c2 = now_ns();
@@ -837,70 +933,29 @@ int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t 
         const uint8_t *p = bytes + boffsets[i], *const end = bytes + boffsets[i + 1];
         Prev pv;
         uint64_t run_left = 0;          // events still to come in the current run
-        for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e) {
-            hq_event &v = events[e];
-            std::memset(&v, 0, sizeof v);
-            if (p >= end) return HQ_E_INVAL;
-            const uint8_t h = run_left ? (uint8_t)0 : *p;
-            if (run_left || ((h & 7) == HQ_EV_MESSAGE && ((h >> 3) & 7) == kCodeRun)) {
-                // a run member: the group's previous message with another sender
-                if (!run_left) {
-                    ++p;
-                    if (!pv.last || !get(p, end, run_left) || run_left == 0) return HQ_E_INVAL;
-                }
-                --run_left;
-                v.kind = HQ_EV_MESSAGE;
-                v.type = pv.last == 1 ? HQ_MSG_REPLICATE_RESP : HQ_MSG_HEARTBEAT_RESP;
-                v.reject = pv.last_reject;
-                v.term = pv.term;
-                if (pv.last == 1) {
-                    v.log_index = pv.index;
-                } else {
-                    v.hint = pv.hint;
-                    v.hint_high = pv.high;
-                }
-                if (!get(p, end, v.from)) return HQ_E_INVAL;
-                continue;
-            }
-            ++p;
-            v.kind = h & 7;
-            bool ok = true;
-            if (v.kind == HQ_EV_READ) {
-                ok = get(p, end, v.hint) && get(p, end, v.hint_high);
-            } else if (v.kind == HQ_EV_PROPOSE) {
-                ok = get(p, end, v.log_index);
-            } else if (v.kind == HQ_EV_MESSAGE) {
-                const uint32_t code = (h >> 3) & 7;
-                uint64_t t = code_type(code);
-                if (code == 7) ok = get(p, end, t);
-                if (code == 4) ok = pv.have_index;  // repeats an index the group has not sent
-                v.type = (uint32_t)t;
-                v.reject = (h >> 6) & 1;
-                ok = ok && get(p, end, v.from);
-                if (ok && !(h & 0x80)) ok = get(p, end, pv.term);
-                v.term = pv.term;
-                if (ok && (code == 0 || code == 7)) ok = get(p, end, v.log_index);
-                if (code == 4) v.log_index = pv.index;
-                if (ok && (code == 2 || code == 3 || code == 7))
-                    ok = get(p, end, v.hint) && get(p, end, v.hint_high);
-                if (code == 5) {
-                    v.hint = pv.hint;
-                    v.hint_high = pv.high;
-                }
-                if (ok && (code == 0 || code == 4)) {
-                    pv.index = v.log_index;
-                    pv.have_index = true;
-                }
-                if (ok && (code == 2 || code == 5)) {
-                    pv.hint = v.hint;
-                    pv.high = v.hint_high;
-                }
-                pv.last = last_of(code);
-                pv.last_reject = (uint8_t)v.reject;
-            }
-            if (!ok) return HQ_E_INVAL;
-        }
+        for (uint64_t e = offsets[i]; e < offsets[i + 1]; ++e)
+            if (!decode_one(p, end, pv, run_left, events[e])) return HQ_E_INVAL;
         if (p != end || run_left) return HQ_E_INVAL;
+    }
+    return HQ_OK;
+}
+
+int hq_events_count(uint64_t n_groups, const uint64_t *boffsets, const uint8_t *bytes,
+                    uint64_t *offsets) {
+    if (!boffsets || !offsets || (n_groups && boffsets[n_groups] > boffsets[0] && !bytes))
+        return HQ_E_INVAL;
+    offsets[0] = 0;
+    for (uint64_t i = 0; i < n_groups; ++i) {
+        if (boffsets[i + 1] < boffsets[i]) return HQ_E_INVAL;
+        const uint8_t *p = bytes + boffsets[i], *const end = bytes + boffsets[i + 1];
+        Prev pv;
+        uint64_t run_left = 0, n = 0;
+        hq_event v;
+        while (p < end || run_left) {
+            if (!decode_one(p, end, pv, run_left, v)) return HQ_E_INVAL;
+            ++n;
+        }
+        offsets[i + 1] = offsets[i] + n;
     }
     return HQ_OK;
 }

@@ -893,9 +893,10 @@ int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *
                                 uint64_t t1) {
     if (rc == HQ_E_INVAL && dout.input_error) {
         const uint32_t e = dout.input_error;
-        if (e & 16)               // (hq_dstep.hip kErrScan: not the input's fault)
+        if (e & (16 | 32))        // (hq_dstep.hip kErrScan / kErrTicket: not the input's fault)
             return fail(HQ_E_STATE, "hq_worker_step: the device step's scan of the ReadyToRead "
-                                    "places failed (internal); no group state was written");
+                                    "places or its launch order failed (internal); no group "
+                                    "state was written");
         return fail(HQ_E_INVAL, e & 1 ? "hq_worker_step: unknown group handle"
                                 : e & 8 ? "hq_worker_step: a group is listed twice"
                                 : e & 2 ? "hq_worker_step: offsets decrease"
@@ -928,11 +929,25 @@ int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *
     // (device path: pack = the host's submit, device = the GPU's time between its events, apply
     // = the outputs mapped after the wait; pass less the three is the wait the GPU does not
     // explain: queueing ahead of the step's work and the waiting thread's wake-up)
+    out->ready_slots = dout.ready_slots;
+    out->ready_slot_counts = dout.slot_counts;
+    out->n_ready_tiles = dout.n_tiles;
+    out->n_ready_slotted = dout.n_slotted;
+    // (device path: pack = the host's submit, device = the thread's wait for the device, apply =
+    // the outputs mapped after the wait, gpu = the GPU's time between the step's events)
     out->pass_ns = t2 - t1;
     out->pack_ns = dout.submit_ns;
-    out->device_ns = dout.gpu_ns;
+    out->device_ns = dout.wait.t_end_ns > dout.wait.t_begin_ns
+                         ? dout.wait.t_end_ns - dout.wait.t_begin_ns : 0;
     out->apply_ns = dout.d2h_ns;
     out->handle_ns = t1 - t0;
+    out->gpu_ns = dout.gpu_ns;
+    out->gpu_jobs = dout.gpu_jobs;
+    out->wait_sleeps = (uint32_t)dout.wait.sleeps;
+    out->wait_poll_ns = dout.wait.poll_ns;
+    out->wait_sleep_ns = dout.wait.sleep_ns;
+    out->wait_end_ns = dout.wait.t_end_ns;
+    out->device_end_ticks = dout.wait.device_end_ticks;
     return HQ_OK;
 }
 
@@ -946,10 +961,12 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out) {
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out) {
     if (!out) return HQ_E_INVAL;
     if (flags & ~(HQ_WORKER_ON_DEVICE | HQ_WORKER_COMMIT_COLUMN | HQ_WORKER_COMMIT_ADVANCE |
-                  HQ_WORKER_READY_COMPACT))
+                  HQ_WORKER_READY_COMPACT | HQ_WORKER_READY_SLOTS))
         return HQ_E_INVAL;
-    if ((flags & HQ_WORKER_READY_COMPACT) && !(flags & HQ_WORKER_ON_DEVICE))
+    if ((flags & (HQ_WORKER_READY_COMPACT | HQ_WORKER_READY_SLOTS)) && !(flags & HQ_WORKER_ON_DEVICE))
         return HQ_E_INVAL;            // (the compact records are the device step's form)
+    if ((flags & HQ_WORKER_READY_SLOTS) && !(flags & HQ_WORKER_COMMIT_ADVANCE))
+        return HQ_E_INVAL;            // (the slots follow the advance column in the region)
     *out = nullptr;
     if (n_max < 1 || n_max > HQ_MAX_VOTERS) return HQ_E_INVAL;
     hq_worker *w = new (std::nothrow) hq_worker();
@@ -965,7 +982,8 @@ int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **ou
         rc = hq_dstep_open(w->ctx, &w->dstep,
                            ((flags & HQ_WORKER_COMMIT_COLUMN) ? 1u : 0u) |
                                ((flags & HQ_WORKER_COMMIT_ADVANCE) ? 2u : 0u) |
-                               ((flags & HQ_WORKER_READY_COMPACT) ? 4u : 0u));
+                               ((flags & HQ_WORKER_READY_COMPACT) ? 4u : 0u) |
+                               ((flags & HQ_WORKER_READY_SLOTS) ? 8u : 0u));
         if (rc) {
             hq_close(w->ctx);
             delete w;
@@ -1097,6 +1115,14 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *out,
     return HQ_OK;
 }
 
+int hq_worker_set_wait(hq_worker *w, uint32_t mode, uint32_t poll_us, uint32_t sleep_us) {
+    if (!w) return HQ_E_INVAL;
+    if (!w->dstep) return w->fail(HQ_E_INVAL, "hq_worker_set_wait: not a device worker");
+    const int rc = hq_dstep_set_wait(w->dstep, mode, poll_us, sleep_us);
+    if (rc == HQ_E_INVAL) return w->fail(rc, "hq_worker_set_wait: unknown mode (or sleep_us 0)");
+    return w->hq(rc, "hq_worker_set_wait");
+}
+
 int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out) {
     if (!w) return HQ_E_INVAL;
     if (!in || !out) return w->fail(HQ_E_INVAL, "hq_worker_step: NULL argument");
@@ -1126,7 +1152,7 @@ int hq_worker_step_jobs_fused(hq_step_job *jobs, uint32_t count) {
     for (uint32_t j = 0; j < count; ++j) {
         const hq_step_job &b = jobs[j];
         const hq_step_stream *in = b.stream;
-        if (!b.worker || !b.worker->dstep || !b.out || b.rows || !in || !in->sizes ||
+        if (!b.worker || !b.worker->dstep || !b.out || b.rows || !in || !(in->sizes || in->sizes16) ||
             (in->n_bytes && !in->bytes) || in->n_groups == 0)
             return kJobsNotFused;
         if (device >= 0 && b.worker->device != device) return kJobsNotFused;
@@ -1148,7 +1174,8 @@ int hq_worker_step_jobs_fused(hq_step_job *jobs, uint32_t count) {
         w->host_stale = true;
         hq_dstep_in d{in->n_groups, in->groups, nullptr, nullptr, nullptr,
                       in->bytes ? in->bytes : &none};
-        d.sizes = in->sizes;
+        d.sizes = in->sizes16 ? nullptr : in->sizes;
+        d.sizes16 = in->sizes16;
         d.n_events = in->n_events;
         d.n_bytes = in->n_bytes;
         ds[nl] = w->dstep;
@@ -1173,10 +1200,10 @@ extern "C" {
 int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output *out) {
     if (!w) return HQ_E_INVAL;
     if (!in || !out) return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL argument");
-    if (in->sizes || (in->n_groups && !in->offsets && !in->boffsets)) {
+    if (in->sizes || in->sizes16 || (in->n_groups && !in->offsets && !in->boffsets)) {
         // the sized form: the device engine scans the sizes; a host worker (or a check) makes
         // the prefix arrays here
-        if (in->n_groups && !in->sizes)
+        if (in->n_groups && !in->sizes && !in->sizes16)
             return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL sizes");
         if (in->n_bytes && !in->bytes)
             return w->fail(HQ_E_INVAL, "hq_worker_step_stream: NULL bytes");
@@ -1185,7 +1212,8 @@ int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output
         if (w->dstep) {
             hq_dstep_in d{in->n_groups, in->groups, nullptr, nullptr, nullptr,
                           in->bytes ? in->bytes : &none};
-            d.sizes = in->sizes;
+            d.sizes = in->sizes16 ? nullptr : in->sizes;
+            d.sizes16 = in->sizes16;
             d.n_events = in->n_events;
             d.n_bytes = in->n_bytes;
             return w->step_on_device(d, out);
@@ -1199,15 +1227,25 @@ int hq_worker_step_stream(hq_worker *w, const hq_step_stream *in, hq_step_output
         w->sized_off.resize(in->n_groups + 1);
         w->sized_boff.resize(in->n_groups + 1);
         w->sized_off[0] = w->sized_boff[0] = 0;
-        for (uint64_t i = 0; i < in->n_groups; ++i) {
-            w->sized_off[i + 1] = w->sized_off[i] + (in->sizes[i] & 0xFFFFu);
-            w->sized_boff[i + 1] = w->sized_boff[i] + (in->sizes[i] >> 16);
+        if (in->sizes16) {        // bytes only: the events counted from the bytes
+            for (uint64_t i = 0; i < in->n_groups; ++i)
+                w->sized_boff[i + 1] = w->sized_boff[i] + in->sizes16[i];
+            if (w->sized_boff[in->n_groups] != in->n_bytes)
+                return w->fail(HQ_E_INVAL, "hq_worker_step_stream: sizes do not sum to the totals");
+            if (hq_events_count(in->n_groups, w->sized_boff.data(), in->bytes ? in->bytes : &none,
+                                w->sized_off.data()) != HQ_OK)
+                return w->fail(HQ_E_INVAL, "hq_worker_step_stream: malformed event stream");
+        } else {
+            for (uint64_t i = 0; i < in->n_groups; ++i) {
+                w->sized_off[i + 1] = w->sized_off[i] + (in->sizes[i] & 0xFFFFu);
+                w->sized_boff[i + 1] = w->sized_boff[i] + (in->sizes[i] >> 16);
+            }
         }
         if (w->sized_off[in->n_groups] != in->n_events || w->sized_boff[in->n_groups] != in->n_bytes)
             return w->fail(HQ_E_INVAL, "hq_worker_step_stream: sizes do not sum to the totals");
         const hq_step_stream full{in->n_groups, groups, w->sized_off.data(),
                                   w->sized_boff.data(), in->bytes ? in->bytes : &none,
-                                  nullptr, 0, 0};
+                                  nullptr, 0, 0, nullptr};
         return hq_worker_step_stream(w, &full, out);
     }
     if (in->n_groups && (!in->groups || !in->offsets || !in->boffsets))

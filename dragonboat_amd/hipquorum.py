@@ -43,7 +43,10 @@ HQ_WORKER_ON_DEVICE = 1      # hq_worker_open_ex: the step worker's state and ev
 HQ_WORKER_COMMIT_COLUMN = 2  # with it: a step's commits as a column when most groups commit
 HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 of groups commit
 HQ_WORKER_READY_COMPACT = 8  # with it: ReadyToReads as 24-byte records (position, delta, ctx)
-HQ_ABI_VERSION = 20
+HQ_WORKER_READY_SLOTS = 16   # with it (+ COMMIT_ADVANCE): single ReadyToReads in per-tile slots
+HQ_WAIT_BLOCK, HQ_WAIT_SLEEP, HQ_WAIT_SPIN, HQ_WAIT_CLOCK = 0, 1, 2, 0x100   # hq_worker_set_wait
+SLOT_TILE = 256              # groups per ReadyToRead slot tile
+HQ_ABI_VERSION = 21
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags
 
 OUTCOME_FOLLOWER = 0
@@ -210,12 +213,13 @@ class StepStream(ctypes.Structure):
 
     _fields_ = [("n_groups", ctypes.c_uint64), ("groups", _vp), ("offsets", _vp),
                 ("boffsets", _vp), ("bytes", _vp), ("sizes", _vp), ("n_events", ctypes.c_uint64),
-                ("n_bytes", ctypes.c_uint64)]
+                ("n_bytes", ctypes.c_uint64), ("sizes16", _vp)]
 
 
 class SizedStream(tuple):
     """A step's event stream in the sized form of ``hq_step_stream``: (groups, sizes, n_events,
-    bytes), sizes[i] = events | bytes << 16 of group i (encode_events_sized)."""
+    bytes), sizes[i] = events | bytes << 16 of group i (encode_events_sized) as uint32, or its
+    byte count alone as uint16 (the 2-byte words, ``sizes16``)."""
 
     def __new__(cls, groups, sizes, n_events, data):
         return super().__new__(cls, (groups, sizes, n_events, data))
@@ -260,7 +264,13 @@ class StepOutput(ctypes.Structure):
                 ("handle_ns", ctypes.c_uint64), ("pass_ns", ctypes.c_uint64),
                 ("pack_ns", ctypes.c_uint64), ("device_ns", ctypes.c_uint64),
                 ("apply_ns", ctypes.c_uint64), ("committed_column", _vp),
-                ("committed_advance", _vp), ("ready_compact", _vp)]
+                ("committed_advance", _vp), ("ready_compact", _vp),
+                ("gpu_ns", ctypes.c_uint64), ("gpu_jobs", ctypes.c_uint32),
+                ("wait_sleeps", ctypes.c_uint32), ("wait_poll_ns", ctypes.c_uint64),
+                ("wait_sleep_ns", ctypes.c_uint64), ("wait_end_ns", ctypes.c_uint64),
+                ("device_end_ticks", ctypes.c_uint64), ("ready_slots", _vp),
+                ("ready_slot_counts", _vp), ("n_ready_tiles", ctypes.c_uint64),
+                ("n_ready_slotted", ctypes.c_uint64)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -409,6 +419,8 @@ SIGNATURES = {
     "hq_events16_encode_sized_multi": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "hq_events_to16": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "hq_events_decode": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp, _vp]),
+    "hq_events_count": (ctypes.c_int, [ctypes.c_uint64, _vp, _vp, _vp]),
+    "hq_worker_set_wait": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "hq_wire_step_stream": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepStream),
                                            ctypes.POINTER(WireStats)]),
     "hq_wire_decode_batch": (ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_uint64, _u64p,
@@ -1376,7 +1388,7 @@ class Worker:
 
     def __init__(self, device: int = 0, n_max: int = 8, on_device: bool = False,
                  commit_column: bool = False, commit_advance: bool = False,
-                 ready_compact: bool = False):
+                 ready_compact: bool = False, ready_slots: bool = False):
         """on_device: HQ_WORKER_ON_DEVICE, the group state resident on the GPU and every event
         taken there (hq_dstep.hip); otherwise the host worker (events on the host, decisions
         in GPU passes). commit_column: HQ_WORKER_COMMIT_COLUMN (results carry
@@ -1384,12 +1396,15 @@ class Worker:
         commit_advance: HQ_WORKER_COMMIT_ADVANCE ('committed_advance', u32 per listed group,
         when more than a quarter of them commit); ready_compact: HQ_WORKER_READY_COMPACT (results
         carry 'ready_compact', READY_COMPACT_DTYPE, instead of 'ready'; expand_ready rebuilds
-        the records)."""
+        the records); ready_slots: HQ_WORKER_READY_SLOTS (with commit_advance: a sized stream
+        step's single ReadyToReads come as 'ready_slots', READY_COMPACT_DTYPE in group order,
+        out of the list; merge_ready rebuilds the step's whole list)."""
         self.h = _vp()
         flags = (HQ_WORKER_ON_DEVICE if on_device else 0) | \
             (HQ_WORKER_COMMIT_COLUMN if commit_column else 0) | \
             (HQ_WORKER_COMMIT_ADVANCE if commit_advance else 0) | \
-            (HQ_WORKER_READY_COMPACT if ready_compact else 0)
+            (HQ_WORKER_READY_COMPACT if ready_compact else 0) | \
+            (HQ_WORKER_READY_SLOTS if ready_slots else 0)
         rc = lib.hq_worker_open_ex(device, n_max, flags, ctypes.byref(self.h))
         if rc != HQ_OK:
             raise HQError(rc, "hq_worker_open: " + lib.hq_last_error(None).decode())
@@ -1400,6 +1415,12 @@ class Worker:
         if self.h:
             lib.hq_worker_close(self.h)
             self.h = _vp()
+
+    def set_wait(self, mode: int = HQ_WAIT_BLOCK, poll_us: int = 50, sleep_us: int = 20,
+                 clock: bool = False) -> None:
+        """hq_worker_set_wait: how the worker's thread waits for its device step."""
+        self._check(lib.hq_worker_set_wait(self.h, mode | (HQ_WAIT_CLOCK if clock else 0),
+                                           poll_us, sleep_us), "hq_worker_set_wait")
 
     def __enter__(self):
         return self
@@ -1503,8 +1524,21 @@ class Worker:
             buf = (ctypes.c_char * (n * dt.itemsize)).from_address(ptr)
             res[name] = np.frombuffer(buf, dt).copy() if copy else np.frombuffer(buf, dt)
         for k in ("gpu_passes", "decisions", "handle_ns", "pass_ns", "pack_ns", "device_ns",
-                  "apply_ns"):
+                  "apply_ns", "gpu_ns", "gpu_jobs", "wait_sleeps", "wait_poll_ns",
+                  "wait_sleep_ns", "wait_end_ns", "device_end_ticks"):
             res[k] = getattr(out, k)
+        if out.ready_slots:
+            # tile t's records at slots[256 t ..], counts[t] of them: gathered in tile order (=
+            # group order)
+            nt = out.n_ready_tiles
+            cnt = np.frombuffer((ctypes.c_char * (4 * nt)).from_address(out.ready_slot_counts),
+                                np.uint32).astype(np.int64)
+            allr = np.frombuffer((ctypes.c_char * (nt * SLOT_TILE * READY_COMPACT_DTYPE.itemsize))
+                                 .from_address(out.ready_slots), READY_COMPACT_DTYPE)
+            ix = np.repeat(np.arange(nt, dtype=np.int64) * SLOT_TILE, cnt) + \
+                (np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+            res["ready_slots"] = allr[ix]          # (a fancy index: a copy)
+            assert len(res["ready_slots"]) == out.n_ready_slotted
         if out.committed_column:
             buf = (ctypes.c_char * (n_listed * 8)).from_address(out.committed_column)
             col = np.frombuffer(buf, np.uint64)
@@ -1601,14 +1635,62 @@ def encode_events(offsets, events):
 
 
 def _sized_input(groups, sizes, n_events, data):
-    """groups None: the step lists the worker's handles 0 .. len(sizes) - 1."""
-    z = np.ascontiguousarray(sizes, np.uint32)
+    """groups None: the step lists the worker's handles 0 .. len(sizes) - 1; uint16 sizes are the
+    2-byte words (bytes only), any other dtype the 4-byte words."""
+    s16 = getattr(sizes, "dtype", None) == np.uint16
+    z = np.ascontiguousarray(sizes, np.uint16 if s16 else np.uint32)
     g = None if groups is None else np.ascontiguousarray(groups, np.uint32)
     d = np.ascontiguousarray(data, np.uint8)
     assert g is None or len(g) == len(z)
-    inp = StepStream(len(z), _p(g), None, None, _p(d) if len(d) else None, _p(z),
-                     int(n_events), len(d))
+    inp = StepStream(len(z), _p(g), None, None, _p(d) if len(d) else None,
+                     None if s16 else _p(z), int(n_events), len(d), _p(z) if s16 else None)
     return inp, [g, z, d]
+
+
+def sizes16_of(sizes):
+    """The 2-byte words (bytes only) of 4-byte size words."""
+    return (np.asarray(sizes, np.uint32) >> np.uint32(16)).astype(np.uint16)
+
+
+def count_events(boffsets, data):
+    """hq_events_count: the event prefix (uint64, len(boffsets)) of a stream's groups."""
+    boffsets = np.ascontiguousarray(boffsets, np.uint64)
+    data = np.ascontiguousarray(data, np.uint8)
+    n = len(boffsets) - 1
+    off = np.zeros(n + 1, np.uint64)
+    _chk(lib.hq_events_count(n, _p(boffsets), _p(data) if len(data) else None, _p(off)),
+         "hq_events_count")
+    return off
+
+
+def merge_ready(res, cluster_ids, committed_before):
+    """A step's ReadyToReads (READY_DTYPE) in the reference's order (group order), whatever form
+    the worker returned them in: the list ('ready' or 'ready_compact') and, with
+    HQ_WORKER_READY_SLOTS, the slots ('ready_slots'), merged by group position as the Go
+    EachReady walks them: each slot record goes before the first list record of a later group,
+    so both sequences keep their own order (a misordered list stays misordered). cluster_ids and
+    committed_before: the listed groups' in list order; a 32-byte list record's position is found
+    from its cluster id."""
+    cids = np.asarray(cluster_ids, np.uint64)
+    lst, lpos = np.zeros(0, READY_DTYPE), np.zeros(0, np.int64)
+    if "ready_compact" in res:
+        rc = res["ready_compact"]
+        lst, lpos = expand_ready(rc, cids, committed_before), rc["pos"].astype(np.int64)
+    elif len(res.get("ready", ())):
+        lst = res["ready"]
+        order = np.argsort(cids, kind="stable")
+        lpos = order[np.searchsorted(cids, lst["cluster_id"], sorter=order)].astype(np.int64)
+        assert np.array_equal(cids[lpos], lst["cluster_id"])
+    if "ready_slots" not in res or len(res["ready_slots"]) == 0:
+        return np.asarray(lst)
+    rs = res["ready_slots"]
+    slots = expand_ready(rs, cids, committed_before)
+    if len(lst) == 0:
+        return slots
+    # (the first list record past a slot's group: past the running maximum of the list's
+    # positions, which is non-decreasing)
+    at = np.searchsorted(np.maximum.accumulate(lpos), rs["pos"].astype(np.int64), "right")
+    return np.insert(np.asarray(lst), at, slots)
 
 
 def encode_events_sized(offsets, events):
@@ -1660,7 +1742,8 @@ class Encode16Job(ctypes.Structure):
     """hq_encode16_job (include/hipquorum.h)."""
     _fields_ = [("n_groups", ctypes.c_uint64), ("offsets16", _vp), ("recs", _vp), ("out", _vp),
                 ("cap", ctypes.c_uint64), ("sizes", _vp), ("n_events", ctypes.c_uint64),
-                ("n_bytes", ctypes.c_uint64), ("rc", ctypes.c_int)]
+                ("n_bytes", ctypes.c_uint64), ("rc", ctypes.c_int), ("reserved", ctypes.c_int),
+                ("sizes16", _vp)]
 
 
 class Encode16Batch:
@@ -1677,11 +1760,16 @@ class Encode16Batch:
         for b, (off, recs, out, sizes) in zip(self.arr, self._jobs):
             n = len(off) - 1
             assert off.dtype == np.uint64 and recs.dtype == EVENT16_DTYPE
-            assert out.dtype == np.uint8 and sizes.dtype == np.uint32 and len(sizes) >= n
+            assert out.dtype == np.uint8 and sizes.dtype in (np.uint32, np.uint16)
+            assert len(sizes) >= n
             assert off.flags.c_contiguous and recs.flags.c_contiguous and out.flags.c_contiguous
             b.n_groups, b.offsets16 = n, _p(off)
             b.recs = _p(recs) if len(recs) else None
-            b.out, b.cap, b.sizes = _p(out), len(out), _p(sizes)
+            b.out, b.cap = _p(out), len(out)
+            if sizes.dtype == np.uint16:     # the 2-byte words (hq_step_stream.sizes16)
+                b.sizes16 = _p(sizes)
+            else:
+                b.sizes = _p(sizes)
         self._addr = ctypes.addressof(self.arr)
 
     def run(self, threads: int = 1):

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HQ_ABI_VERSION 20
+#define HQ_ABI_VERSION 21
 
 /* status codes */
 #define HQ_OK          0
@@ -969,10 +969,11 @@ typedef struct hq_step_output {
     uint64_t device_ns;         /*   of which H2D + kernels + D2H + sync */
     uint64_t apply_ns;          /*   of which applying the decisions */
     /* (HQ_WORKER_ON_DEVICE workers: pack_ns = the host's time to queue the step's copies and
-     * launches, device_ns = the GPU's time from the step's first queued operation to its last
-     * (HIP timing events; a jobs step's is the shared launches' time), apply_ns = mapping the
-     * outputs after the wait; pass_ns - pack_ns - device_ns - apply_ns is the wait the GPU's
-     * time does not explain, the waiting thread's wake-up and any queueing ahead of the step) */
+     * launches, device_ns = the thread's wait for the device after that (as for host workers:
+     * the device's share of the pass, seen from the host), apply_ns = mapping the outputs after
+     * the wait; gpu_ns below is the GPU's own time, so pass_ns - pack_ns - gpu_ns - apply_ns is
+     * the wait the GPU's time does not explain: the waiting thread's wake-up and any queueing
+     * ahead of the step) */
     /* HQ_WORKER_COMMIT_COLUMN workers only, else NULL: the step's commits as one word per
      * listed group (input order), its new committed index or 0 (no commit: a commit never sets
      * 0); `commits` is then NULL and n_commits counts the nonzero words */
@@ -987,6 +988,28 @@ typedef struct hq_step_output {
      * records (hq_ready_compact, in the order of `ready`); `ready` is then NULL and n_ready
      * counts them. A step in which some record's delta does not fit 32 bits keeps `ready` */
     const hq_ready_compact *ready_compact;
+    /* ABI 21. Device workers (0 otherwise): the step's clocks. device_ns above is the thread's
+     * wait for the device (the time from the last queued operation to the wait's return);
+     * gpu_ns the GPU's time between the step's timing events — with hq_worker_step_jobs the
+     * shared launches' time, the same in each of the gpu_jobs workers' outputs (count it once).
+     * The wait polled for wait_poll_ns, then slept wait_sleep_ns (wait_sleeps times: a blocking
+     * wait is one); wait_end_ns is the host's steady clock at its return and, with HQ_WAIT_CLOCK,
+     * device_end_ticks the device's 100-MHz constant clock after the step's last kernel (the
+     * difference between the two over steps is the wake-up's lateness, hq_worker_set_wait). */
+    uint64_t gpu_ns;
+    uint32_t gpu_jobs;
+    uint32_t wait_sleeps;
+    uint64_t wait_poll_ns, wait_sleep_ns, wait_end_ns, device_end_ticks;
+    /* HQ_WORKER_READY_SLOTS workers, a step that wrote slots (else NULL / 0): the single ReadyToRead
+     * of every listed group whose only other record is its commit, as hq_ready_compact records in
+     * per-tile slots — tile t (listed groups 256 t .. 256 t + 255) holds ready_slot_counts[t]
+     * records at ready_slots[256 t ..], in group order; n_ready_slotted in all. They are not in
+     * `ready` / `ready_compact` (n_ready counts the list only). A group's records are all in one
+     * of the two; the step's ReadyToReads in the reference's order (group order) are the two merged
+     * by the record's group position (`pos`; a 32-byte list record's group is its cluster id). */
+    const hq_ready_compact *ready_slots;
+    const uint32_t *ready_slot_counts;
+    uint64_t n_ready_tiles, n_ready_slotted;
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;
@@ -1013,6 +1036,13 @@ int hq_worker_open(int device, uint32_t n_max, hq_worker **out);
 /* with HQ_WORKER_ON_DEVICE: the ReadyToReads as hq_step_output.ready_compact (24 bytes each
  * across PCIe instead of 32: the cluster id and the index are the host's already) */
 #define HQ_WORKER_READY_COMPACT 8u
+/* with HQ_WORKER_ON_DEVICE and HQ_WORKER_COMMIT_ADVANCE: the single ReadyToReads in per-tile slots
+ * (hq_step_output.ready_slots): the engine's first pass writes them while it still reads the
+ * step's stream (the host link's other direction) instead of a pass after it. Taken by sized
+ * stream steps (hq_worker_step_stream / _step_jobs with sizes or sizes16; other inputs keep the
+ * list); a record whose index - the group's committed index before the step does not fit 32
+ * bits stays in the list */
+#define HQ_WORKER_READY_SLOTS 16u
 int hq_worker_open_ex(int device, uint32_t n_max, uint32_t flags, hq_worker **out);
 void hq_worker_close(hq_worker *w);
 const char *hq_worker_last_error(const hq_worker *w);
@@ -1036,6 +1066,20 @@ int hq_worker_get_group(hq_worker *w, uint64_t cluster_id, hq_worker_group *g,
                         hq_member *members, uint32_t cap, hq_read_status *reads,
                         uint32_t reads_cap);
 int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
+/* How a device worker's thread waits for its step (ABI 21):
+ *   HQ_WAIT_BLOCK  poll for poll_us, then sleep on a blocking-sync HIP event (the runtime's
+ *                  interrupt wait) — the default, poll_us 50
+ *   HQ_WAIT_SLEEP  poll for poll_us, then check every sleep_us microseconds, asleep in between
+ *                  (a timer wake-up)
+ *   HQ_WAIT_SPIN   poll (yielding) until the step is done: one host core per waiting worker
+ * | HQ_WAIT_CLOCK: a one-thread kernel behind each step stamps the device's constant clock
+ *   (hq_step_output.device_end_ticks). The jobs path (hq_worker_step_jobs) waits with the first
+ *   job's worker's policy. HQ_E_INVAL for a host worker or an unknown mode. */
+#define HQ_WAIT_BLOCK 0u
+#define HQ_WAIT_SLEEP 1u
+#define HQ_WAIT_SPIN  2u
+#define HQ_WAIT_CLOCK 0x100u
+int hq_worker_set_wait(hq_worker *w, uint32_t mode, uint32_t poll_us, uint32_t sleep_us);
 
 /* ---------------------------------------------------------------- event streams ------------- */
 /*
@@ -1091,6 +1135,12 @@ typedef struct hq_step_stream {
      * that steps all its groups every time; a group without events has size 0). */
     const uint32_t *sizes;
     uint64_t n_events, n_bytes;
+    /* ABI 21, the sized form with 2-byte words (sizes NULL): per group its byte count (< 2^16)
+     * only — 2 bytes per group cross the link instead of 4. The events are the group's bytes
+     * decoded to their end, counted by the engine (n_events must still be their total); a
+     * group's bytes that do not decode make the step HQ_E_INVAL (as a host worker's decoder
+     * does), not a fallback of the group. */
+    const uint16_t *sizes16;
 } hq_step_stream;
 
 /* Encode rows (offsets as in hq_step_input) into out[0 .. cap) and boffsets[0 .. n_groups];
@@ -1149,6 +1199,9 @@ typedef struct hq_encode16_job {
     uint32_t *sizes;
     uint64_t n_events, n_bytes;  /* out */
     int rc;                      /* out */
+    int reserved;
+    uint16_t *sizes16;           /* ABI 21: when not NULL, the 2-byte words (hq_step_stream.sizes16)
+                                    are written here instead (sizes may then be NULL) */
 } hq_encode16_job;
 int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32_t threads);
 /* Phase clocks of the threaded hq_events16_encode_sized calls (diagnostic; process-wide sums
@@ -1166,6 +1219,11 @@ int hq_encode_stats_read(hq_encode_stats *out, int reset);
  * HQ_E_STATE when cap records cannot hold them (5 per event always can). */
 int hq_events_to16(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
                    hq_event16 *out, uint64_t cap, uint64_t *offsets16);
+/* Count each group's events in a stream (group i's bytes: bytes[boffsets[i] .. boffsets[i + 1])):
+ * offsets[0] = 0, offsets[i + 1] = offsets[i] + its events — the event prefix of a stream given
+ * with 2-byte size words. HQ_E_INVAL when a group's bytes do not decode to whole events. */
+int hq_events_count(uint64_t n_groups, const uint64_t *boffsets, const uint8_t *bytes,
+                    uint64_t *offsets);
 /* Decode a stream back into rows events[offsets[0] .. offsets[n_groups]); HQ_E_INVAL when a
  * group's bytes do not hold exactly its events. */
 int hq_events_decode(uint64_t n_groups, const uint64_t *offsets, const uint64_t *boffsets,

@@ -59,7 +59,7 @@ func OpenDeviceWorker(device, nMax int) (*Worker, error) {
 	}
 	var w *C.hq_worker
 	flags := C.uint32_t(C.HQ_WORKER_ON_DEVICE | C.HQ_WORKER_COMMIT_ADVANCE | C.HQ_WORKER_COMMIT_COLUMN |
-		C.HQ_WORKER_READY_COMPACT)
+		C.HQ_WORKER_READY_COMPACT | C.HQ_WORKER_READY_SLOTS)
 	if rc := C.hq_worker_open_ex(C.int(device), C.uint32_t(nMax), flags, &w); rc != C.HQ_OK {
 		return nil, errors.New(C.GoString(C.hq_last_error(nil)))
 	}
@@ -74,6 +74,12 @@ func (x *Worker) err(rc C.int) error {
 }
 
 // Close frees the worker.
+// SetWait sets how the worker's goroutine waits for its device step (hq_worker_set_wait:
+// C.HQ_WAIT_BLOCK / C.HQ_WAIT_SLEEP / C.HQ_WAIT_SPIN, | C.HQ_WAIT_CLOCK).
+func (x *Worker) SetWait(mode, pollUs, sleepUs uint32) error {
+	return x.err(C.hq_worker_set_wait(x.w, C.uint32_t(mode), C.uint32_t(pollUs), C.uint32_t(sleepUs)))
+}
+
 func (x *Worker) Close() {
 	C.hq_worker_close(x.w)
 	C.free(unsafe.Pointer(x.rows))
@@ -138,7 +144,7 @@ func (x *Worker) Step(groups []uint32, offsets []uint64, events []C.hq_event) (*
 // per node one size word (events | bytes << 16; the sized form of hq_step_stream).
 type StreamBuf struct {
 	Groups  []uint32 // worker handles, or nil: every handle 0 .. len(Sizes)-1 in order
-	Sizes   []uint32
+	Sizes   []uint16 // per node its byte count (hq_step_stream.sizes16: the engine counts events)
 	NEvents uint64
 	Bytes   []byte // a pinned region; len = bytes written so far
 	start   int
@@ -165,7 +171,7 @@ func (b *StreamBuf) EndNode(handle uint32) {
 	if b.Groups != nil {
 		b.Groups = append(b.Groups, handle)
 	}
-	b.Sizes = append(b.Sizes, uint32(b.events)|uint32(len(b.Bytes)-b.start)<<16)
+	b.Sizes = append(b.Sizes, uint16(len(b.Bytes)-b.start))
 	b.NEvents += uint64(b.events)
 }
 
@@ -241,7 +247,7 @@ func (x *Worker) setStream(b *StreamBuf) {
 	*x.strm = C.hq_step_stream{
 		n_groups: C.uint64_t(len(b.Sizes)),
 		bytes:    (*C.uint8_t)(unsafe.Pointer(&b.Bytes[0])),
-		sizes:    (*C.uint32_t)(unsafe.Pointer(&b.Sizes[0])),
+		sizes16:  (*C.uint16_t)(unsafe.Pointer(&b.Sizes[0])),
 		n_events: C.uint64_t(b.NEvents),
 		n_bytes:  C.uint64_t(len(b.Bytes)),
 	}
@@ -329,26 +335,48 @@ func (o *Output) ReadyToRead() []C.hq_ready_to_read {
 }
 
 // EachReady calls fn(listed index, pb.ReadyToRead) for every released read of the step, in the
-// reference's order, whichever form the step returned: the 24-byte records (HQ_WORKER_READY_COMPACT:
-// the index is the group's committed index before the step, committedBefore, plus the record's
-// delta) or the full records (listedOf maps a cluster id to its listed index).
+// reference's order (listed order), whichever form the step returned: the per-tile slots
+// (HQ_WORKER_READY_SLOTS) and the list — 24-byte records (HQ_WORKER_READY_COMPACT: the index is
+// the group's committed index before the step, committedBefore, plus the record's delta) or full
+// records (listedOf maps a cluster id to its listed index) — merged by listed index (a group's
+// reads are all in one of the two). The node then calls processReadyToRead (node.go:1026-1031).
 func (o *Output) EachReady(committedBefore func(i int) uint64, listedOf func(clusterID uint64) int,
 	fn func(i int, r pb.ReadyToRead)) {
-	if o.c.n_ready == 0 {
-		return
+	compact := func(r C.hq_ready_compact) (int, pb.ReadyToRead) {
+		i := int(r.pos)
+		return i, pb.ReadyToRead{Index: committedBefore(i) + uint64(int64(r.delta)),
+			SystemCtx: pb.SystemCtx{Low: uint64(r.ctx_low), High: uint64(r.ctx_high)}}
 	}
-	if o.c.ready_compact != nil {
-		recs := unsafe.Slice(o.c.ready_compact, int(o.c.n_ready))
-		for _, r := range recs {
-			i := int(r.pos)
-			fn(i, pb.ReadyToRead{Index: committedBefore(i) + uint64(int64(r.delta)),
-				SystemCtx: pb.SystemCtx{Low: uint64(r.ctx_low), High: uint64(r.ctx_high)}})
+	// the list, one record at a time with its listed index
+	k, n := 0, int(o.c.n_ready)
+	listAt := func(k int) (int, pb.ReadyToRead) {
+		if o.c.ready_compact != nil {
+			return compact(unsafe.Slice(o.c.ready_compact, n)[k])
 		}
-		return
+		var f C.hq_ready_to_read = unsafe.Slice(o.c.ready, n)[k]
+		return listedOf(uint64(f.cluster_id)), pb.ReadyToRead{Index: uint64(f.index),
+			SystemCtx: pb.SystemCtx{Low: uint64(f.ctx_low), High: uint64(f.ctx_high)}}
 	}
-	for _, r := range unsafe.Slice(o.c.ready, int(o.c.n_ready)) {
-		fn(listedOf(uint64(r.cluster_id)), pb.ReadyToRead{Index: uint64(r.index),
-			SystemCtx: pb.SystemCtx{Low: uint64(r.ctx_low), High: uint64(r.ctx_high)}})
+	if o.c.ready_slots != nil {
+		tiles := int(o.c.n_ready_tiles)
+		counts := unsafe.Slice((*uint32)(unsafe.Pointer(o.c.ready_slot_counts)), tiles)
+		slots := unsafe.Slice(o.c.ready_slots, tiles*256)
+		for t, c := range counts {
+			for _, r := range slots[t*256 : t*256+int(c)] {
+				i, rr := compact(r)
+				for ; k < n; k++ { // the list's reads of the groups before this one
+					j, lr := listAt(k)
+					if j > i {
+						break
+					}
+					fn(j, lr)
+				}
+				fn(i, rr)
+			}
+		}
+	}
+	for ; k < n; k++ {
+		fn(listAt(k))
 	}
 }
 
@@ -447,7 +475,7 @@ func EncodeMany(jobs []Encode16Job, threads int) error {
 		cj[i] = C.hq_encode16_job{n_groups: C.uint64_t(len(j.Offsets) - 1),
 			offsets16: (*C.uint64_t)(unsafe.Pointer(&j.Offsets[0])),
 			out:       (*C.uint8_t)(unsafe.Pointer(&bytes[0])), cap: C.uint64_t(len(bytes)),
-			sizes: (*C.uint32_t)(unsafe.Pointer(&sizes[0]))}
+			sizes16: (*C.uint16_t)(unsafe.Pointer(&sizes[0]))}
 		if len(j.Recs) > 0 {
 			pin.Pin(&j.Recs[0])
 			cj[i].recs = &j.Recs[0]

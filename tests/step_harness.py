@@ -66,13 +66,20 @@ class WorkerBackend:
 
     def __init__(self, hq, n_max=8, seed=0, worker=None, on_device=False, stream=False):
         """stream: False (rows), True (stream with prefix arrays), "sized" (size words),
-        "sized-column" (size words in, commits as a column out: HQ_WORKER_COMMIT_COLUMN) or
-        "sized-advance" (commits as 4-byte advances: HQ_WORKER_COMMIT_ADVANCE)."""
+        "sized-column" (size words in, commits as a column out: HQ_WORKER_COMMIT_COLUMN),
+        "sized-advance" (commits as 4-byte advances: HQ_WORKER_COMMIT_ADVANCE), "sized16" (2-byte
+        size words, bytes only) or "sized16-slots" (2-byte words and the stream in pinned memory:
+        the jobs path, commits as advances, ReadyToReads compact and in per-tile slots,
+        HQ_WORKER_READY_SLOTS)."""
         self.hq = hq
         self.stream = stream
+        slots = stream == "sized16-slots"
         self.w = worker if worker is not None else hq.Worker(
             0, n_max, on_device=on_device, commit_column=stream == "sized-column",
-            commit_advance=stream == "sized-advance")
+            commit_advance=stream in ("sized-advance", "sized16-slots"), ready_compact=slots,
+            ready_slots=slots)
+        self.pin = hq.Context(0) if slots else None
+        self.pinned = {}
         self.rng = np.random.default_rng(seed)
         self.cids = []
         self.last_passes = 0
@@ -80,6 +87,24 @@ class WorkerBackend:
 
     def close(self):
         self.w.close()
+        if self.pin:
+            self.pin.close()
+
+    def _pinned(self, key, a):
+        """a copied into a pinned buffer kept for the next steps (grown when too small)."""
+        buf = self.pinned.get(key)
+        if buf is None or len(buf) < len(a):
+            buf = self.pinned[key] = self.pin.pinned(max(len(a), 1) * 2, a.dtype)
+        buf[:len(a)] = a
+        return buf[:len(a)]
+
+    def _sized(self, grp, sizes, n_events, data):
+        """The SizedStream of this backend's form (4-byte words -> 2-byte ones, pinned)."""
+        if str(self.stream).startswith("sized16"):
+            sizes = self.hq.sizes16_of(sizes)
+        if self.pin:
+            sizes, data = self._pinned("sizes", sizes), self._pinned("data", data)
+        return self.hq.SizedStream(grp, sizes, n_events, data)
 
     def add_group(self, cid, node, term, state, committed, last, term_start, members, log=None):
         # the worker holds term_start only: its term check is term_start <= q <= last, exact
@@ -108,7 +133,7 @@ class WorkerBackend:
         ev = np.array(recs, hq.EVENT_DTYPE)
         if str(self.stream).startswith("sized"):
             data, sizes = hq.encode_events_sized(off, ev)
-            return hq.SizedStream(grp, sizes, len(ev), data), refs
+            return self._sized(grp, sizes, len(ev), data), refs
         if self.stream:
             data, boff = hq.encode_events(off, ev)
             return (grp, off, boff, data), refs
@@ -117,7 +142,7 @@ class WorkerBackend:
     def step(self, per_group):
         arrs, refs = self.build_inputs(per_group)
         prev = {}                       # the committed indexes the advances add to
-        if self.stream == "sized-advance":
+        if self.stream in ("sized-advance", "sized16-slots"):
             prev = {cid: int(self.w.get_group(cid)[0]["committed"]) for cid in self.last_cids}
         if isinstance(arrs, self.hq.SizedStream):
             res = self.w.step_sized(*arrs)
@@ -127,7 +152,13 @@ class WorkerBackend:
         self.last_raw = res
         out = {cid: {"ready": [], "resps": [], "states": [], "dropped": [], "deferred": [],
                      "commit_changed": False} for cid in per_group}
-        for r in res["ready"]:
+        ready = res["ready"]
+        if "ready_compact" in res or "ready_slots" in res:
+            # the compact list and the slots, merged in list order (the reference's)
+            lc = np.array(self.last_cids, np.uint64)
+            ready = self.hq.merge_ready(res, lc, np.array([prev[c] for c in self.last_cids],
+                                                          np.uint64))
+        for r in ready:
             out[int(r["cluster_id"])]["ready"].append(
                 (int(r["index"]), int(r["ctx_low"]), int(r["ctx_high"])))
         for r in res["read_resps"]:
@@ -261,5 +292,5 @@ class WireBackend(WorkerBackend):
         self.last_cids = [handle_cid[int(h)] for h in grp]
         if str(self.stream).startswith("sized"):
             sizes = (np.diff(off) | (np.diff(boff) << np.uint64(16))).astype(np.uint32)
-            return self.hq.SizedStream(grp, sizes, int(off[-1]), data), refs
+            return self._sized(grp, sizes, int(off[-1]), data), refs
         return ((grp, off, boff, data) if self.stream else (grp, off, ev)), refs

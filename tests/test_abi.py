@@ -29,7 +29,7 @@ def test_exports_match_header(hq):
 
 
 def test_abi_version(hq):
-    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 20
+    assert hq.lib.hq_abi_version() == hq.HQ_ABI_VERSION == 21
 
 
 LAYOUT_C = r"""
@@ -94,6 +94,15 @@ int main(void) {
          (unsigned)(HQ_EV16_READ_CTX | HQ_EV16_FULL << 8));
   F(hq_event16, kind) F(hq_event16, type) F(hq_event16, from) F(hq_event16, term)
   F(hq_event16, value)
+  printf("hq_step_output %zu\nhq_step_stream %zu\nhq_encode16_job %zu\n", sizeof(hq_step_output),
+         sizeof(hq_step_stream), sizeof(hq_encode16_job));
+  F(hq_step_output, ready_compact) F(hq_step_output, gpu_ns) F(hq_step_output, gpu_jobs)
+  F(hq_step_output, wait_sleeps) F(hq_step_output, wait_end_ns) F(hq_step_output, device_end_ticks)
+  F(hq_step_output, ready_slots) F(hq_step_output, n_ready_slotted)
+  F(hq_step_stream, sizes16) F(hq_encode16_job, sizes16)
+  printf("wait_modes %u,%u,%u,%u\nready_slots_flag %u\n", (unsigned)HQ_WAIT_BLOCK,
+         (unsigned)HQ_WAIT_SLEEP, (unsigned)HQ_WAIT_SPIN, (unsigned)HQ_WAIT_CLOCK,
+         (unsigned)HQ_WORKER_READY_SLOTS);
   return 0;
 }
 """
@@ -121,6 +130,15 @@ def test_struct_layout_matches_c(hq, tmp_path):
     assert int(c["hq_wire_stats"]) == ctypes.sizeof(hq.WireStats)
     assert int(c["bin_ver"]) == hq.HQ_RPC_BIN_VERSION
     assert int(c["in_place"]) == hq.HQ_LAYOUT_IN_PLACE
+    # the step worker's structs (ABI 21: wait clocks, ReadyToRead slots, 2-byte size words)
+    for t, py in (("hq_step_output", hq.StepOutput), ("hq_step_stream", hq.StepStream),
+                  ("hq_encode16_job", hq.Encode16Job)):
+        assert int(c[t]) == ctypes.sizeof(py), t
+        for f in [k for k in c if k.startswith(t + ".")]:
+            assert int(c[f]) == getattr(py, f.split(".", 1)[1]).offset, f
+    assert c["wait_modes"] == ",".join(map(str, (hq.HQ_WAIT_BLOCK, hq.HQ_WAIT_SLEEP, hq.HQ_WAIT_SPIN,
+                                                 hq.HQ_WAIT_CLOCK)))
+    assert int(c["ready_slots_flag"]) == hq.HQ_WORKER_READY_SLOTS
     assert int(c["grouped"]) == hq.HQ_INGEST_GROUPED
     for name, dt in dtypes.items():
         assert int(c[name]) == dt.itemsize, name
@@ -141,7 +159,8 @@ def test_struct_layout_matches_c(hq, tmp_path):
                 continue
             cls = {"hq_commit_args": hq.CommitArgs, "hq_synth_spec": hq.SynthSpec,
                    "hq_commit_lag_args": hq.LagArgs, "hq_engine_config": hq.EngineConfig,
-                   "hq_engine_stats": hq.EngineStats}[t]
+                   "hq_engine_stats": hq.EngineStats, "hq_step_output": hq.StepOutput,
+                   "hq_step_stream": hq.StepStream, "hq_encode16_job": hq.Encode16Job}[t]
             assert getattr(cls, m).offset == int(val), key
 
 

@@ -175,7 +175,8 @@ def test_every_call_matches_the_header(header):
     for need in ("hq_open", "hq_commit", "hq_commit_dev", "hq_commit_fused_dev", "hq_engine_post",
                  "hq_engine_wait", "hq_readindex_multi_tiles_dev",
                  "hq_readindex_vote_cq_planes_dev", "hq_worker_step_stream",
-                 "hq_worker_step_jobs", "hq_events16_encode_sized", "hq_abi_version"):
+                 "hq_worker_step_jobs", "hq_events16_encode_sized_multi", "hq_worker_set_wait",
+                 "hq_abi_version"):
         assert need in seen, need
 
 

@@ -18,9 +18,11 @@ MODES = [False, True]
 MODE_IDS = ["host", "device"]      # the host worker / HQ_WORKER_ON_DEVICE (hq_dstep.hip)
 # (on_device, stream): events as rows or as an event stream (hq_worker_step_stream)
 FEEDS = [(False, False), (True, False), (True, True), (False, True), (True, "sized"),
-         (False, "sized"), (True, "sized-column"), (True, "sized-advance")]
+         (False, "sized"), (True, "sized-column"), (True, "sized-advance"), (True, "sized16"),
+         (False, "sized16"), (True, "sized16-slots")]
 FEED_IDS = ["host", "device", "device-stream", "host-stream", "device-sized", "host-sized",
-            "device-sized-column", "device-sized-advance"]
+            "device-sized-column", "device-sized-advance", "device-sized16", "host-sized16",
+            "device-sized16-slots"]
 
 
 @pytest.fixture(scope="module", params=FEEDS, ids=FEED_IDS)

@@ -26,7 +26,12 @@ for i in range(W):
     w = hq.Worker(0, sum(r != "observer" for r in roles), on_device=True,
                   commit_column=os.environ.get("COLUMN", "1") == "1",
                   commit_advance=os.environ.get("ADVANCE", "1") == "1",
-                  ready_compact=os.environ.get("COMPACT", "0") == "1")
+                  ready_compact=os.environ.get("COMPACT", "0") == "1" or
+                  os.environ.get("SLOTS", "0") == "1",
+                  ready_slots=os.environ.get("SLOTS", "0") == "1")
+    if os.environ.get("WAIT"):             # WAIT=block|sleep|spin (hq_worker_set_wait)
+        w.set_wait({"block": 0, "sleep": 1, "spin": 2}[os.environ["WAIT"]],
+                   int(os.environ.get("POLL_US", 50)), int(os.environ.get("SLEEP_US", 20)))
     w.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
     workers.append(w)
 pc = hq.Context(0)
@@ -38,6 +43,8 @@ for s in range(STEPS):
         nev = len(e[2])
         if feed == "sized":
             data, sizes = hq.encode_events_sized(e[1], e[2])
+            if os.environ.get("S16", "0") == "1":     # 2-byte size words
+                sizes = hq.sizes16_of(sizes)
             e = (e[0], sizes, data)
         elif stream:
             data, boff = hq.encode_events(e[1], e[2])
@@ -53,7 +60,8 @@ for s in range(STEPS):
     t0 = time.perf_counter()
     res = jobs.run(copy=False)
     dt = time.perf_counter() - t0
-    dev = max(r["device_ns"] for r in res) / 1e6
+    dev = max(r["gpu_ns"] for r in res) / 1e6
+    slotted = sum(len(r.get("ready_slots", ())) for r in res)
     if os.environ.get("PER_WORKER") and W > 1:
         print("  device ms per worker:", " ".join(f"{r['device_ns'] / 1e6:.2f}" for r in res),
               "| host ms:", " ".join(f"{r['handle_ns'] / 1e6:.2f}" for r in res), flush=True)
@@ -62,7 +70,7 @@ for s in range(STEPS):
                            for k in ("ready", "read_resps", "state_changes", "dropped_reads",
                                      "deferred", "fallback_groups")}, flush=True)
     print(f"step {s}: {dt * 1e3:.2f} ms, {ne} events, {ne / dt:.3e} events/s, W={W}, "
-          f"max device {dev:.2f} ms, input {sum(getattr(x, 'nbytes', 0) for p in inputs for x in p) / 1e6:.1f} MB",
+          f"gpu {dev:.3f} ms, slotted {slotted}, input {sum(getattr(x, 'nbytes', 0) for p in inputs for x in p) / 1e6:.1f} MB",
           flush=True)
 for w in workers:
     w.close()
