@@ -130,7 +130,7 @@ WORKLOADS = {
 HEADLINE = "c3mtl"
 DEFAULT_EXTRAS = ("c2tl,c2t,c2,c2l,c3,c3r32,c3r32t,c3m,c3mt,c3l,c5v5t,c5v5tl,c5v5r32t,"
                   "c4,c4t,c4t3,c4p,c4u,c4ut,c5,c5t,c5tl,c5s,c5l,c2ll,c5ll,c5r,c5r32,rim,"
-                  "rimt,rimtc,cq,cqp,c4pq,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire")
+                  "rimt,rimtc,cq,cqp,c4pq,ing,ingo,ingu,inga,w2,sweep,e2e,step,step5,wire,wire_step")
 # the same generated groups decided with the other exact term-check forms (same cfg, n, G)
 SAME_DATA_FORMS = {"c3mtl": ("c3", "c3r32", "c3r32t", "c3m", "c3mt"),
                    "c3mt": ("c3", "c3r32", "c3r32t", "c3m", "c3mtl")}
@@ -1772,17 +1772,58 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     return out
 
 
+HQ_MSG_REPLICATE_RESP, HQ_MSG_HEARTBEAT_RESP = 13, 18
+
+
+def _wire_arrivals(hq, ev, off, cids, roles, bounds, dep):
+    """The step's received messages (a step_events() input) for the workers owning groups
+    [bounds[i], bounds[i + 1]) as MessageBatch bytes, per worker, in the arrival order that keeps
+    every group's messages in the rows' order (step_events: the ReplicateResps of the other
+    members, then their HeartbeatResps): one batch per (message type, sender), the
+    ReplicateResps' batches first — the senders' batches of one tick, marshalled by
+    hq_wire_encode_batch (MessageBatch.MarshalTo) — and the worker's local events (ReadIndex,
+    proposals) as (cluster ids, offsets, rows) for hq_wire_add_locals."""
+    per = np.diff(off).astype(np.int64)
+    grp = np.repeat(np.arange(len(off) - 1), per)
+    is_msg = ev["kind"] == hq.EV_MESSAGE
+    out = [([], None) for _ in range(len(bounds) - 1)]
+    for typ in (HQ_MSG_REPLICATE_RESP, HQ_MSG_HEARTBEAT_RESP):
+        for k in range(2, len(roles) + 1):
+            sel = np.nonzero(is_msg & (ev["type"] == typ) & (ev["from"] == k))[0]
+            gs = grp[sel]                                # (in group order)
+            m = np.zeros(len(sel), hq.WIRE_MESSAGE_DTYPE)
+            m["ev"] = ev[sel]
+            m["cluster_id"] = cids[gs]
+            m["to"] = 1
+            cut = np.searchsorted(gs, bounds)
+            for i in range(len(bounds) - 1):
+                out[i][0].append(hq.encode_wire_batch(m[cut[i]:cut[i + 1]], deployment_id=dep,
+                                                      source_address=b"n%d:63000" % k).copy())
+    loc = np.nonzero(~is_msg)[0]
+    gl = grp[loc]
+    cnt = np.bincount(gl, minlength=len(off) - 1)
+    res = []
+    for i in range(len(bounds) - 1):
+        lo, hi = bounds[i], bounds[i + 1]
+        o = np.zeros(hi - lo + 1, np.uint64)
+        o[1:] = np.cumsum(cnt[lo:hi])
+        a, b = np.searchsorted(gl, [lo, hi])
+        res.append((out[i][0], (cids[lo:hi].copy(), o, ev[loc[a:b]].copy())))
+    return res
+
+
 def run_wire_leg(d: Dist, G=1 << 14, reps=20):
     """The step worker's input from the wire (hq_wire.cpp), host side: the received messages of
     a steady-state step of G leader groups (3 voters: a ReplicateResp and a HeartbeatResp from
-    each follower) marshalled as raftpb.MessageBatch bytes, one batch per sending node
-    (tests/wire_encode.py, the gogo layout), then per step: hq_wire_reset + hq_wire_add_batch of
-    every batch (protobuf decode, deployment / version check, per-cluster queues) +
-    hq_wire_step_stream (the step's event stream for the worker). One host thread; the bytes are
-    built outside the timed region. The stream it produces is then stepped on the device engine,
-    and its commits are checked against the same step fed as rows."""
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
-    import wire_encode as we
+    each follower) marshalled as raftpb.MessageBatch bytes (one batch per message type and sending
+    node), then per step, on one host thread: the production feed — hq_wire_reset +
+    hq_wire_add_batch of every batch (protobuf decode with the Message.MarshalTo fast path,
+    deployment / version check, each message's cluster resolved to the attached worker's handle)
+    + hq_wire_add_locals + hq_wire_step_sized (the step's sized stream with 2-byte words, in
+    handle order, straight into pinned buffers) — and, beside it, the first-appearance form
+    (hq_wire_step_stream: clusters in order of first appearance, prefix arrays). The bytes are
+    built outside the timed region. Both streams are stepped on the device engine and decide
+    like the same step fed as rows."""
     from dragonboat_amd import hipquorum as hq
 
     roles = STEP_ROLES["step"]
@@ -1792,64 +1833,386 @@ def run_wire_leg(d: Dist, G=1 << 14, reps=20):
     m["match"][m["node_id"] != 1] -= np.uint64(10)
     dep = 0x5EED
     _, off, ev = step_events(hq, G, 0, roles)
-    msgs = {}
-    cols = {k: ev[k].tolist() for k in ("kind", "type", "from", "term", "log_index", "hint",
-                                        "hint_high")}
-    offl, cidl = off.tolist(), cids.tolist()
-    for i in range(G):
-        for j in range(offl[i], offl[i + 1]):
-            if cols["kind"][j] == hq.EV_MESSAGE:
-                msgs.setdefault(cols["from"][j], []).append(
-                    we.message(type=cols["type"][j], to=1, frm=cols["from"][j],
-                               cluster_id=cidl[i], term=cols["term"][j],
-                               log_index=cols["log_index"][j], hint=cols["hint"][j],
-                               hint_high=cols["hint_high"][j]))
-    batches = [we.batch(v, deployment_id=dep, source_address=b"n%d:63000" % k)
-               for k, v in sorted(msgs.items())]
-    n_msg = sum(len(v) for v in msgs.values())
-    n_bytes = sum(len(b) for b in batches)
-    w = hq.Worker(d.device, sum(r != "observer" for r in roles), on_device=True)
+    [(bufs, (lc, lo_, lev))] = _wire_arrivals(hq, ev, off, cids, roles, [0, G], dep)
+    n_msg = int((ev["kind"] == hq.EV_MESSAGE).sum())
+    n_bytes = sum(len(b) for b in bufs)
+    nv = sum(r != "observer" for r in roles)
+    w = hq.Worker(d.device, nv, on_device=True, commit_advance=True)
     w.add_groups(g, m)
-    wire = hq.Wire(dep)
-    bufs = [np.frombuffer(b, np.uint8) for b in batches]
-    times = []
+    wa = hq.Worker(d.device, nv, on_device=True, commit_advance=True, ready_compact=True,
+                   ready_slots=True)
+    wa.add_groups(g, m)
+    pin = hq.Context(d.device)
+    pdata = pin.pinned(len(ev) * hq.HQ_EVENT_STREAM_MAX + 64, np.uint8)
+    psizes = pin.pinned(G, np.uint16)
+    wire, wire_a = hq.Wire(dep), hq.Wire(dep)
+    wire_a.attach(wa)
+    times, times_a = [], []
     for r in range(reps + 2):
         t0 = time.perf_counter()
+        wire_a.reset()
+        for b in bufs:
+            wire_a.add_batch_at(b.ctypes.data, len(b))
+        wire_a.add_locals(lc, lo_, lev)
+        ss, st_a = wire_a.step_sized(pdata, psizes)
+        t1 = time.perf_counter()
         wire.reset()
         for b in bufs:
-            wire.add_batch(b)
+            wire.add_batch_at(b.ctypes.data, len(b))
+        wire.add_locals(lc, lo_, lev)
         grp, o, bo, data, st = wire.step_stream(w)
-        dt = time.perf_counter() - t0
+        t2 = time.perf_counter()
         if r >= 2:
-            times.append(dt)
-    assert st.messages == n_msg and st.dropped_messages == 0
-    # the stream from the wire decides like the same messages fed as rows
+            times_a.append(t1 - t0)
+            times.append(t2 - t1)
+    assert st.messages == n_msg and st.dropped_messages == 0 and st_a.messages == n_msg
+    # both streams from the wire decide like the same step fed as rows
+    res_a = wa.step_sized(*ss)
     res = w.step_stream(grp, o, bo, data)
-    w2 = hq.Worker(d.device, sum(r != "observer" for r in roles), on_device=True)
+    w2 = hq.Worker(d.device, nv, on_device=True, commit_advance=True)
     w2.add_groups(g, m)
-    msg_only = ev[ev["kind"] == hq.EV_MESSAGE]
-    per = np.array([int(((ev["kind"][int(off[i]):int(off[i + 1])]) == hq.EV_MESSAGE).sum())
-                    for i in range(G)], np.int64)
-    moff = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
-    ref = w2.step(np.arange(G, dtype=np.uint32), moff, msg_only)
-    same = bool(np.array_equal(np.sort(res["commits"]["cluster_id"]),
-                               np.sort(ref["commits"]["cluster_id"])) and
-                np.array_equal(res["commits"]["committed"][np.argsort(res["commits"]["cluster_id"])],
-                               ref["commits"]["committed"][np.argsort(ref["commits"]["cluster_id"])]))
-    w.close()
-    w2.close()
-    wire.close()
-    t = float(np.median(times))
+    ref = w2.step(np.arange(G, dtype=np.uint32), off, ev)
+    same = all(np.array_equal(x.get("committed_advance"), ref.get("committed_advance"))
+               for x in (res, res_a))
+    same = same and np.array_equal(res["ready"], ref["ready"]) and np.array_equal(
+        hq.merge_ready(res_a, cids, g["committed"]), ref["ready"])
+    for x in (w, w2, wa, wire, wire_a, pin):
+        x.close()
+    t, ta = float(np.median(times)), float(np.median(times_a))
     return {
         "workload": f"wire: the received messages of one steady-state step of {G} leader groups "
-                    f"(3 voters), {n_msg} raftpb.Message in {len(batches)} MessageBatch "
-                    f"({n_bytes} bytes), decoded and assembled into the step's event stream "
-                    f"(hq_wire_add_batch + hq_wire_step_stream), one host thread",
-        "unit": "messages/s", "value": n_msg / t, "ms_per_step": t * 1e3,
-        "ns_per_message": t / n_msg * 1e9, "wire_mb_per_s": n_bytes / t / 1e6,
-        "stream_bytes_per_message": len(data) / n_msg,
-        "commits_equal_rows_path": same and len(res["commits"]) == G,
-        "commits": int(len(res["commits"])),
+                    f"(3 voters), {n_msg} raftpb.Message in {len(bufs)} MessageBatch "
+                    f"({n_bytes} bytes) + the local ReadIndex / proposals, decoded and assembled "
+                    f"into the worker's sized stream (hq_wire_attach: handles resolved as the "
+                    f"batches decode; hq_wire_step_sized), one host thread",
+        "unit": "messages/s", "value": n_msg / ta, "ms_per_step": ta * 1e3,
+        "ns_per_message": ta / n_msg * 1e9, "wire_mb_per_s": n_bytes / ta / 1e6,
+        "stream_bytes_per_message": int(ss[3].nbytes) / n_msg,
+        "first_appearance_form": {"ns_per_message": t / n_msg * 1e9,
+                                  "api": "hq_wire_step_stream (clusters in order of first "
+                                         "appearance, prefix arrays)"},
+        "decisions_equal_rows_path": bool(same),
+        "commits": int((res_a["committed_advance"] != 0).sum()),
+    }
+
+
+def run_wire_step_leg(d: Dist, G=1 << 20, steps=6, name="step5", with_cpu=True):
+    """The device step fed from the wire at step size: every step's received messages of G
+    leader groups (BENCH step5's membership: 4 full members, a witness, 2 observers: 12 messages
+    per group) arrive as MessageBatch bytes (one batch per message type and sending node, per
+    step worker; marshalled outside the timed region, hq_wire_encode_batch), W = 1 and 16 step
+    workers each with its own hq_wire attached to its worker. A step: on each worker's own thread
+    hq_wire_reset + hq_wire_add_batch of its batches + hq_wire_add_locals (its nodes' ReadIndex
+    and proposals) + hq_wire_step_sized straight into its pinned receive buffers (2-byte size
+    words); then the W workers' device step (hq_worker_step_jobs: ReadyToRead slots, advance
+    column). Pipelined as a host would run it: while the device takes step s the workers decode
+    step s + 1 into their other buffers. Every step's commits and ReadyToReads (order included)
+    match the CPU replay of the same rows (oracle/qref_step.c)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from dragonboat_amd import hipquorum as hq
+
+    roles = STEP_ROLES[name]
+    nv, nm = sum(r != "observer" for r in roles), len(roles)
+    rng = _shard_of(d, G)
+    g, m, cids = step_groups(hq, G, rng.cid_base, rng.cid_stride, roles)
+    dep = 0x5EED
+    Ws = (1, 16)
+    pin = hq.Context(d.device)
+    nsteps = steps + STEP_WARM
+
+    # every step's arrivals per W (the rows advanced in place, StepRows; outside the timed
+    # region), and the CPU replay of the same rows (its digests are the parity reference)
+    rows = StepRows(hq, G, roles)
+    n_events, n_msg = len(rows.ev), int((rows.ev["kind"] == hq.EV_MESSAGE).sum())
+    arrivals = {W: [] for W in Ws}
+    cpu = None
+    if with_cpu and d.rank == 0 and d.world == 1:
+        from oracle import qref
+
+        _, counts = cpu_thread_counts()
+        nt = 16 if 16 in counts else max(counts)
+        rb = qref.StepBatch(g, m)
+        cpu = {"threads": nt, "digests": [], "t": []}
+        prev = int(g["committed"].sum(dtype=np.uint64))
+    for s in range(nsteps + 1):
+        rows.set(s)
+        if cpu is not None and s < nsteps:
+            t0 = time.perf_counter()
+            tot = rb.step(rows.groups, rows.offsets, rows.ev, nthreads=cpu["threads"])
+            cpu["t"].append(time.perf_counter() - t0)
+            cpu["digests"].append((tot["commits"], tot["ready"],
+                                   (tot["committed_sum"] - prev) & ((1 << 64) - 1),
+                                   tot["ready_digest"], tot["commit_digest"],
+                                   tot["ready_order_digest"]))
+            prev = tot["committed_sum"]
+        for W in Ws:
+            bounds = [G * i // W for i in range(W + 1)]
+            arrivals[W].append(_wire_arrivals(hq, rows.ev, rows.offsets, cids, roles, bounds, dep))
+    if cpu is not None:
+        rb.close()
+        cpu["events_per_s"] = n_events * steps / sum(cpu["t"][STEP_WARM:])
+    ev0 = int(rows.offsets[-1])
+    out = {}
+    for W in Ws:
+        bounds = [G * i // W for i in range(W + 1)]
+        workers, wires, bufs = [], [], []
+        for i in range(W):
+            wk = hq.Worker(d.device, nv, on_device=True, commit_column=True, commit_advance=True,
+                           ready_compact=True, ready_slots=True)
+            wk.add_groups(g[bounds[i]:bounds[i + 1]], m[nm * bounds[i]:nm * bounds[i + 1]])
+            wr = hq.Wire(dep)
+            wr.attach(wk)
+            n_i = bounds[i + 1] - bounds[i]
+            ev_i = int(rows.offsets[bounds[i + 1]] - rows.offsets[bounds[i]])
+            bufs.append([(pin.pinned(ev_i * 5 + 4096, np.uint8), pin.pinned(n_i, np.uint16))
+                         for _ in range(2)])
+            workers.append(wk)
+            wires.append(wr)
+        pool = ThreadPoolExecutor(W + 1)
+        mirror = CommitMirror(cids, g["committed"], bounds)
+
+        def decode(i, s, slot):
+            """Worker i's thread: step s's arrivals into its pinned buffers; (stream, seconds)."""
+            t0 = time.perf_counter()
+            wr = wires[i]
+            wr.reset()
+            batches, (lc, lo_, lev) = arrivals[W][s][i]
+            for b in batches:
+                wr.add_batch_at(b.ctypes.data, len(b))
+            wr.add_locals(lc, lo_, lev)
+            ss, _ = wr.step_sized(*bufs[i][slot])
+            return ss, time.perf_counter() - t0
+
+        def decode_all(s, slot):
+            t0 = time.perf_counter()
+            rs = list(pool.map(lambda i: decode(i, s, slot), range(W)))
+            return [x for x, _ in rs], max(t for _, t in rs), time.perf_counter() - t0
+
+        def device(streams):
+            j = hq.StepJobs(list(zip(workers, streams)))
+            t0 = time.perf_counter()
+            j.execute()
+            return j, time.perf_counter() - t0
+
+        checks, t_e2e, t_dec, t_dev = [], [], [], []
+        streams, _, _ = decode_all(0, 0)
+        for s in range(nsteps):
+            slot = s % 2
+            t0 = time.perf_counter()
+            fut = pool.submit(device, streams)           # step s on the device
+            nxt, dec_max, dec_wall = decode_all(s + 1, 1 - slot)   # step s + 1 from the wire
+            j, dt_dev = fut.result()
+            dt = time.perf_counter() - t0
+            checks.append(mirror.step(j.results(copy=False)))
+            streams = nxt
+            if s >= STEP_WARM:
+                t_e2e.append(dt)
+                t_dec.append(dec_wall)
+                t_dev.append(dt_dev)
+        pool.shutdown()
+        for x in workers + wires:
+            x.close()
+        arrivals[W] = None
+        parity = cpu is not None and checks == cpu["digests"]
+        out[f"w{W}"] = {
+            "events_per_s": n_events / float(np.median(t_e2e)),
+            "latency_ms": _latency(t_e2e),
+            "decode_ms_p50": float(np.median(t_dec)) * 1e3,
+            "device_ms_p50": float(np.median(t_dev)) * 1e3,
+            "decode_ns_per_message_per_thread": float(np.median(t_dec)) * W / n_msg * 1e9,
+            "parity_committed": bool(parity) if cpu is not None else None,
+        }
+    pin.close()
+    rec = {
+        "workload": f"wire_step: {name}'s step of {G} leader groups from MessageBatch bytes "
+                    f"({n_msg} messages + {n_events - n_msg} local events per step), decoded on "
+                    f"each step worker's thread straight into its sized stream, then the device "
+                    f"step; decode of step s + 1 overlapped with the device's step s; {steps} "
+                    f"timed steps",
+        "unit": "events/s", "value": out["w16"]["events_per_s"],
+        "events_per_step": n_events, "messages_per_step": n_msg,
+        "end_to_end": {k: v["events_per_s"] for k, v in out.items()}, "modes": out,
+    }
+    if cpu is not None:
+        rec["cpu_replay"] = {"threads": cpu["threads"], "events_per_s": cpu["events_per_s"],
+                             "sample": "the same rows of the same steps replayed event by event "
+                                       "(oracle/qref_step.c)"}
+        rec["vs_cpu_replay_end_to_end"] = {k: v["events_per_s"] / cpu["events_per_s"]
+                                           for k, v in out.items()}
+        rec["parity_committed"] = all(v["parity_committed"] for v in out.values())
+    return rec
+
+
+def run_share_leg(d: Dist, steps=20, step_steps=8, variants=None):
+    """One GPU shared by three of the path's kernels, in one process: the persistent commit engine
+    (hq_engine, post-as-ready windows of `steps` c3mtl steps, BASELINE config 3), the fused
+    ReadIndex + vote + CheckQuorum plane pass (c4pq, 16 M x 7, back-to-back launches on its own
+    context) and a device step worker (step5, 1 M groups, sized stream with ReadyToRead slots) —
+    what a node's 16 step workers run at once (execengine.go:675-690, 860-882). Each is timed
+    alone and then all three together (each on its own thread and stream, the engine and the
+    plane pass looping until the step worker's steps are done), for each engine policy in
+    `variants`: (max_workgroups, idle_us) — the full grid or a capped one, the 20 ms idle exit or
+    a short one. Every output of the shared run equals the solo run's: the engine's batches
+    (against a launch of the same batch), the plane pass's outputs on a freshly packed set, the
+    step worker's per-step digests."""
+    import threading
+
+    from dragonboat_amd import hipquorum as hq
+    from dragonboat_amd import shard
+
+    w = WORKLOADS["c3mtl"]
+    variants = variants or [(0, 20000), (0, 500), (-2, 500)]
+    ctx_e, ctx_q = hq.Context(d.device), hq.Context(d.device)
+    sets, per_set = build_sets(ctx_e, hq, shard, w, d)
+    nsets = len(sets)
+    lay = hq.HQ_LAYOUT_TILES_LEADER
+    arr1 = [hq.commit_batch_array([batch_args(sets[i % nsets][0])]) for i in range(nsets)]
+    # c4pq: rotating plane sets (as run_kernel_leg), one more kept for the equality check
+    G4, n4, T = 16 << 20, 7, hq.HQ_PLANE_TILE_GROUPS
+    pb, ab = hq.plane_tiles(G4) * 3 * T, hq.cq_plane_bytes(G4, 8)
+
+    def plane_set(k):
+        arrs = [ctx_q.empty(G4, np.uint8) for _ in range(4)]
+        ctx_q.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 3 + (k << 40), G4, n4), *arrs)
+        pl, apl = ctx_q.empty(pb, np.uint8), ctx_q.empty(ab, np.uint8)
+        ctx_q.tile_planes_dev(G4, *arrs, 0, pl)
+        ctx_q.synth_bitmaps_dev(hq.synth_spec(SEED_BASE + 5 + (k << 40), G4, n4), arrs[0])
+        ctx_q.tile_cq_planes_dev(G4, arrs[0], None, 8, 0, apl)
+        ctx_q.sync()
+        act = arrs[0]
+        for a in arrs[1:]:
+            ctx_q.free(a)
+        return [pl, apl, ctx_q.empty(hq.words64(G4), np.uint64), ctx_q.empty(hq.words32(G4), np.uint64),
+                ctx_q.empty(hq.words64(G4), np.uint64), act]
+    qsets = [plane_set(k) for k in range(4)]
+
+    def q_repack(x):
+        ctx_q.tile_cq_planes_dev(G4, x[5], None, 8, 0, x[1])
+
+    def q_outputs(x):
+        ctx_q.sync()
+        return [ctx_q.download(y) for y in x[2:5]]
+    # the step worker: step5's groups, every step's sized stream pre-encoded into pinned memory
+    roles = STEP_ROLES["step5"]
+    Gs = 1 << 20
+    rng = _shard_of(d, Gs)
+    g, m, cids = step_groups(hq, Gs, rng.cid_base, rng.cid_stride, roles)
+    nv = sum(r != "observer" for r in roles)
+    pin = hq.Context(d.device)
+    rows = StepRows(hq, Gs, roles)
+    streams = []
+    for s_ in range(step_steps):
+        rows.set(s_)
+        data, sz = hq.encode_events_sized(rows.offsets, rows.ev)
+        pd, ps = pin.pinned(len(data), np.uint8), pin.pinned(Gs, np.uint16)
+        pd[:], ps[:] = data, hq.sizes16_of(sz)
+        streams.append(hq.SizedStream(None, ps, len(rows.ev), pd))
+
+    def step_run(stop=None):
+        """step_steps steps of a fresh worker: (ms per step, digests)."""
+        wk = hq.Worker(d.device, nv, on_device=True, commit_column=True, commit_advance=True,
+                       ready_compact=True, ready_slots=True)
+        wk.add_groups(g, m)
+        mir = CommitMirror(cids, g["committed"], [0, Gs])
+        ts, dg = [], []
+        for ss in streams:
+            j = hq.StepJobs([(wk, ss)])
+            t0 = time.perf_counter()
+            j.execute()
+            ts.append(time.perf_counter() - t0)
+            dg.append(mir.step(j.results(copy=False)))
+        wk.close()
+        if stop is not None:
+            stop.set()
+        return float(np.median(ts)) * 1e3, dg
+
+    def engine_run(eng, stop=None, windows=3):
+        """post-as-ready windows (one post per step, the drain's STOP): us per step (median)."""
+        out, k = [], 0
+        while True:
+            t0 = time.perf_counter()
+            for i in range(steps):
+                eng.post(arr1[(k * steps + i) % nsets])
+            eng.drain()
+            out.append((time.perf_counter() - t0) / steps * 1e6)
+            k += 1
+            if (stop is None and k >= windows) or (stop is not None and stop.is_set()):
+                return float(np.median(out)), k
+
+    def q_run(stop=None, launches=100):
+        """back-to-back plane passes: us per launch, launches."""
+        k, t0 = 0, time.perf_counter()
+        while True:
+            for _ in range(10):
+                ctx_q.readindex_vote_cq_planes_dev(G4, *qsets[k % 3][:5])
+                k += 1
+            ctx_q.sync()
+            if (stop is None and k >= launches) or (stop is not None and stop.is_set()):
+                return (time.perf_counter() - t0) / k * 1e6, k
+
+    # solo: the plane pass and the step worker; the engine per policy
+    q_run(launches=20)
+    q_solo, _ = q_run()
+    q_repack(qsets[3])
+    ctx_q.readindex_vote_cq_planes_dev(G4, *qsets[3][:5])
+    q_ref = q_outputs(qsets[3])
+    st_solo, st_dg = step_run()
+    # the engine's decisions of set 0 against a launch of the same batch
+    b0 = sets[0][0]
+    ctx_e.commit_dev(batch_args(b0))
+    ctx_e.sync()
+    e_ref = [ctx_e.download(x) for x in (b0.committed_out, b0.changed, b0.fallback)]
+    out = {"solo": {"c4pq_us_per_launch": q_solo, "step5_ms_per_step": st_solo}, "policies": []}
+    info = None
+    for cap, idle in variants:
+        eng0 = hq.Engine(ctx_e, w["n"], w["form"], lay, ring_len=16)
+        grid = eng0.info().grid
+        eng0.close()
+        mw = grid // -cap if cap < 0 else cap
+        eng = hq.Engine(ctx_e, w["n"], w["form"], lay, ring_len=16, idle_us=idle, max_workgroups=mw)
+        engine_run(eng, windows=1)                       # (warm)
+        e_solo, _ = engine_run(eng)
+        stop = threading.Event()
+        res = {}
+        th = [threading.Thread(target=lambda: res.__setitem__("e", engine_run(eng, stop))),
+              threading.Thread(target=lambda: res.__setitem__("q", q_run(stop)))]
+        for t in th:
+            t.start()
+        st_shared, dg = step_run(stop)
+        for t in th:
+            t.join()
+        # outputs of the shared run: the engine's set 0 (poisoned, decided by the engine after
+        # the shared phase ran through it), a freshly packed plane set, the step digests
+        for x in (b0.committed_out, b0.changed, b0.fallback):
+            ctx_e.memset(x, 0xA5)
+        ctx_e.sync()
+        eng.post(arr1[0])
+        eng.drain()
+        e_out = [ctx_e.download(x) for x in (b0.committed_out, b0.changed, b0.fallback)]
+        q_repack(qsets[3])
+        ctx_q.readindex_vote_cq_planes_dev(G4, *qsets[3][:5])
+        q_out = q_outputs(qsets[3])
+        info = eng.info()
+        eng.close()
+        out["policies"].append({
+            "engine_max_workgroups": mw or grid, "engine_grid": grid, "engine_idle_us": idle,
+            "alone": {"engine_us_per_step": e_solo},
+            "together": {"engine_us_per_step": res["e"][0], "engine_windows": res["e"][1],
+                         "c4pq_us_per_launch": res["q"][0], "c4pq_launches": res["q"][1],
+                         "step5_ms_per_step": st_shared},
+            "outputs_equal": {"engine": all(np.array_equal(a, b) for a, b in zip(e_out, e_ref)),
+                              "c4pq": all(np.array_equal(a, b) for a, b in zip(q_out, q_ref)),
+                              "step5": dg == st_dg},
+        })
+    for c in (ctx_e, ctx_q, pin):
+        c.close()
+    return {
+        "workload": f"share: the commit engine (c3mtl, {steps}-step post-as-ready windows), the "
+                    f"c4pq plane pass (16 M x 7, back to back) and a step5 device step worker "
+                    f"(1 M groups, {step_steps} steps) on one GPU, alone and together, per engine "
+                    f"policy (max_workgroups, idle_us)",
+        "unit": "us", "value": None, **out,
     }
 
 
@@ -2079,6 +2442,11 @@ def run_rank(args, d, progress):
                 rec = run_e2e(max(100, args.steps // 4), 5, d)   # >= 30 ms timed per variant
             elif name == "wire":
                 rec = run_wire_leg(d)
+            elif name == "share":
+                rec = run_share_leg(d)
+            elif name == "wire_step":
+                rec = run_wire_step_leg(d, G=args.step_groups, steps=min(args.step_steps, 8),
+                                        with_cpu=not args.no_cpu)
             elif name in STEP_ROLES:
                 rec = run_step_leg(d, G=args.step_groups, steps=args.step_steps,
                                    with_cpu=not args.no_cpu, name=name)

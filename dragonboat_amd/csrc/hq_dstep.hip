@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <new>
 #include <thread>
+#include <vector>
 
 #include <hipcub/hipcub.hpp>
 
@@ -337,6 +338,9 @@ struct Engine {
     hq_ready_to_read *stage = nullptr;
     uint32_t stage_lo = 0;
     uint64_t c0 = 0;              // the group's committed index before the step
+    // pass B over a group whose single ReadyToRead pass A put in its tile's slot (a step in list
+    // mode replays every group): the record is not written again nor counted in the list
+    bool slotted = false;
 
     __device__ __forceinline__ Engine(const StepK &k, uint64_t idx, uint32_t h, hq_dread *reads)
         : a(k), i(idx), rd(reads) {
@@ -391,6 +395,7 @@ struct Engine {
 
     // -- outputs ----------------------------------------------------------------------------
     __device__ __forceinline__ void ready(uint64_t index, uint64_t low, uint64_t high) {
+        if (WRITE && slotted) return;
         const uint32_t p = slot(kReady);
         const hq_ready_to_read r{g.cluster_id, index, low, high};
         const int64_t delta = (int64_t)(index - c0);
@@ -980,6 +985,7 @@ __device__ __forceinline__ void step_groups(const StepK &a, uint64_t blk, uint32
         Engine<WRITE, MC> eng(a, i, h, reads);   // (pass B: i_begin = 0, i / 64 is its wave)
         if (!WRITE) eng.save_old(h);
         if (WRITE && STREAM && a.bytes_only) e0 = eng.base[kEvents];   // (the events' scan)
+        if (WRITE && a.slots) eng.slotted = (a.rerun[i] & 8) != 0;
         __shared__ hq_ready_to_read stage[WRITE ? 256 / 64 : 1][WRITE ? kStageReady : 1];
         // list mode: the wave's groups are consecutive and so are their records, staged from its
         // first active lane's on; column mode: the groups replayed are a sparse subset whose records

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/hipquorum.h"
+#include "hq_stream.h"
 
 namespace {
 
@@ -85,7 +86,8 @@ inline uint8_t last_of(uint32_t code) {
 }
 
 // does row e repeat the group's previous message (a run member)?
-inline bool repeats(const hq_event &e, const Prev &pv) {
+template <class Ev>
+inline bool repeats(const Ev &e, const Prev &pv) {
     if (!pv.last || e.kind != HQ_EV_MESSAGE || (e.reject != 0) != (pv.last_reject != 0) ||
         e.term != pv.term)
         return false;
@@ -107,7 +109,8 @@ inline uint8_t *put_run(uint8_t *p, uint32_t m, From from) {
 }
 
 // one event; returns the write position
-inline uint8_t *encode(uint8_t *p, const hq_event &e, Prev &pv) {
+template <class Ev>
+inline uint8_t *encode(uint8_t *p, const Ev &e, Prev &pv) {
     const uint32_t kind = e.kind >= 1 && e.kind <= 5 ? e.kind : 0;   // 0: not a valid kind
     if (kind != HQ_EV_MESSAGE) {
         *p++ = (uint8_t)kind;
@@ -304,7 +307,8 @@ inline uint32_t run16(const hq_event16 *recs, uint64_t k, uint64_t r1, const Pre
 }
 
 // the rows events[e .. e1) that open with a run: its length (0 below kRunMin)
-inline uint32_t run_rows(const hq_event *events, uint64_t e, uint64_t e1, const Prev &pv) {
+template <class Ev>
+inline uint32_t run_rows(const Ev *events, uint64_t e, uint64_t e1, const Prev &pv) {
     uint32_t m = 0;
     while (m < kRunMax && e + m < e1 && repeats(events[e + m], pv)) ++m;
     return m >= kRunMin ? m : 0;
@@ -312,7 +316,8 @@ inline uint32_t run_rows(const hq_event *events, uint64_t e, uint64_t e1, const 
 
 // the unit at row e of a group's rows [.., e1): a run of repeats of the previous message, or
 // row e alone; returns the next row
-inline uint64_t encode_unit(uint8_t *&p, const hq_event *events, uint64_t e, uint64_t e1, Prev &pv) {
+template <class Ev>
+inline uint64_t encode_unit(uint8_t *&p, const Ev *events, uint64_t e, uint64_t e1, Prev &pv) {
     if (pv.last) {
         const uint32_t m = run_rows(events, e, e1, pv);
         if (m) {
@@ -888,6 +893,30 @@ int hq_events_to16(uint64_t n_groups, const uint64_t *offsets, const hq_event *e
     }
     return HQ_OK;
 }
+
+}  // extern "C"
+
+namespace hqs {
+namespace {
+template <class Ev>
+uint8_t *encode_events_of(uint8_t *p, const uint8_t *end, const Ev *ev, uint64_t n) {
+    Prev pv;
+    for (uint64_t e = 0; e < n;) {
+        if ((uint64_t)(end - p) < HQ_EVENT_STREAM_MAX) return nullptr;
+        e = encode_unit(p, ev, e, n, pv);
+    }
+    return p;
+}
+}  // namespace
+uint8_t *encode_group(uint8_t *p, const uint8_t *end, const hq_event *ev, uint64_t n) {
+    return encode_events_of(p, end, ev, n);
+}
+uint8_t *encode_group(uint8_t *p, const uint8_t *end, const WireEvent *ev, uint64_t n) {
+    return encode_events_of(p, end, ev, n);
+}
+}  // namespace hqs
+
+extern "C" {
 
 int hq_events_encode(uint64_t n_groups, const uint64_t *offsets, const hq_event *events,
                      uint8_t *out, uint64_t cap, uint64_t *boffsets) {

@@ -15,9 +15,11 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/hipquorum.h"
+#include "hq_stream.h"
 
 namespace {
 
@@ -138,6 +140,76 @@ int decode_message(const uint8_t *b, size_t len, hq_wire_message *m, std::string
     return HQ_OK;
 }
 
+// one event of the step as the wire keeps it (hq_stream.h): a decoded message's fields, or a
+// local event's
+struct Rec : hqs::WireEvent {
+    hq_event event() const {
+        hq_event e{};
+        e.kind = kind;
+        e.type = type;
+        e.from = from;
+        e.term = term;
+        e.log_index = log_index;
+        e.hint = hint;
+        e.hint_high = hint_high;
+        e.reject = reject;
+        return e;
+    }
+};
+static_assert(sizeof(Rec) == 56, "56-byte wire records");
+
+// the one-byte varint, else the loop; p < end on entry
+inline bool varint_at(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
+    if (*p < 0x80) {
+        v = *p++;
+        return true;
+    }
+    v = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+        if (p >= end) return false;
+        const uint8_t b = *p++;
+        v |= (uint64_t)(b & 0x7F) << shift;
+        if (b < 0x80) return true;
+    }
+    return false;
+}
+
+// A Message in the field order raft.pb.go Message.MarshalTo writes (:2232-2296): every field of
+// 1-10 with its tag in order, entries (11) repeated, the snapshot (12, always: nullable=false),
+// hint_high (13), nothing else. false: not that layout (the general decoder takes it from the
+// start, any field order); *entries counts field 11
+inline bool decode_marshal_order(const uint8_t *p, const uint8_t *end, Rec &r, uint64_t &cluster,
+                                 uint32_t &entries) {
+    uint64_t v[10];
+    for (uint32_t f = 0; f < 10; ++f) {            // fields 1-10: tag (f + 1) << 3, a varint
+        if (p >= end || *p != (uint8_t)((f + 1) << 3)) return false;
+        if (++p >= end || !varint_at(p, end, v[f])) return false;
+    }
+    entries = 0;
+    while (p < end && *p == 0x5a) {                // entries: counted, not decoded
+        uint64_t n;
+        if (++p >= end || !varint_at(p, end, n) || (uint64_t)(end - p) < n) return false;
+        p += n;
+        ++entries;
+    }
+    uint64_t n, high;
+    if (p >= end || *p != 0x62) return false;      // the snapshot
+    if (++p >= end || !varint_at(p, end, n) || (uint64_t)(end - p) < n) return false;
+    p += n;
+    if (p >= end || *p != 0x68) return false;      // hint_high, the last field
+    if (++p >= end || !varint_at(p, end, high) || p != end) return false;
+    r.kind = HQ_EV_MESSAGE;
+    r.type = (uint32_t)v[0];
+    r.from = v[2];
+    cluster = v[3];
+    r.term = v[4];
+    r.log_index = v[6];
+    r.reject = v[8] != 0;
+    r.hint = v[9];
+    r.hint_high = high;
+    return true;
+}
+
 // MessageBatch (raft.proto:191-196): every Message handed to sink(bytes, len) in order (sink
 // returns an HQ_ status), the other fields into *bi. Any field order; unknown fields skipped.
 template <class Sink>
@@ -192,6 +264,26 @@ class ClusterIndex {
         used_.clear();
         has_empty_ = false;
     }
+    // the value of id, or false
+    bool find(uint64_t id, uint32_t *v) const {
+        if (id == kEmpty) {
+            if (has_empty_) *v = empty_val_;
+            return has_empty_;
+        }
+        if (keys_.empty()) return false;
+        const uint64_t mask = keys_.size() - 1;
+        for (uint64_t i = hash(id) & mask;; i = (i + 1) & mask) {
+            if (keys_[i] == id) {
+                *v = vals_[i];
+                return true;
+            }
+            if (keys_[i] == kEmpty) return false;
+        }
+    }
+    void prefetch(uint64_t id) const {
+        if (!keys_.empty()) __builtin_prefetch(&keys_[hash(id) & (keys_.size() - 1)]);
+    }
+    size_t size() const { return used_.size() + has_empty_; }
     // the index of id, inserting next if new (*fresh = true)
     uint32_t find_or_add(uint64_t id, uint32_t next, bool *fresh) {
         if ((used_.size() + 1) * 2 > keys_.size()) rehash(keys_.empty() ? 1024 : keys_.size() * 2);
@@ -256,15 +348,15 @@ class ClusterIndex {
 struct hq_wire {
     uint64_t deployment_id = 0;
     std::string err;
-    struct Rec {
-        uint32_t cluster;   // index into clusters (order of first appearance)
-        uint32_t cat;       // 0 local ReadIndex, 1 received message, 2 tick, 3 proposal
-        hq_event ev;
-    };
     std::vector<Rec> recs;
     std::vector<uint64_t> clusters;
     ClusterIndex cluster_index;
-    std::vector<hq_wire_message> scratch;
+    // attached (hq_wire_attach): a record's key is the worker's handle, resolved as it is
+    // decoded through handle_of (cluster id -> handle, kept across steps: handles never change;
+    // only clusters the worker runs are kept in it)
+    hq_worker *worker = nullptr;
+    ClusterIndex handle_of;
+    std::vector<uint64_t> pending;     // the cluster ids of a batch's records, before their keys
     hq_wire_stats stats{};
     // the assembled step input (valid until the next reset)
     std::vector<uint32_t> groups;
@@ -272,6 +364,8 @@ struct hq_wire {
     std::vector<hq_event> events;
     std::vector<uint64_t> boffsets;    // hq_wire_step_stream
     std::vector<uint8_t> bytes;
+    std::vector<uint32_t> cnt, perm, pos;   // hq_wire_step_sized's counting sort
+    std::vector<Rec> grp;              //   and one group's events
 
     int fail(int code, const std::string &m) {
         err = m;
@@ -282,6 +376,44 @@ struct hq_wire {
         const uint32_t k = cluster_index.find_or_add(id, (uint32_t)clusters.size(), &fresh);
         if (fresh) clusters.push_back(id);
         return k;
+    }
+    // the key of a cluster: its handle when attached (false: the worker does not run it), else
+    // its index of first appearance
+    bool key(uint64_t id, uint32_t *k) {
+        if (!worker) {
+            *k = cluster(id);
+            return true;
+        }
+        if (handle_of.find(id, k)) return true;
+        uint32_t h;
+        if (hq_worker_find(worker, id, &h) != HQ_OK) return false;
+        bool fresh;
+        handle_of.find_or_add(id, h, &fresh);
+        *k = h;
+        return true;
+    }
+    // the records from r0 on got their cluster ids in `pending`: their keys, dropping (in place)
+    // those of clusters the attached worker does not run; the handle table prefetched 8 ahead
+    void resolve(size_t r0) {
+        const size_t n = recs.size() - r0;
+        size_t i = 0;
+        for (; i < n; ++i) {                   // (no record dropped: keys set in place)
+            if (worker && i + 8 < n) handle_of.prefetch(pending[i + 8]);
+            if (!key(pending[i], &recs[r0 + i].key)) break;
+        }
+        if (i == n) return;
+        size_t o = r0 + i;
+        for (; i < n; ++i) {
+            if (worker && i + 8 < n) handle_of.prefetch(pending[i + 8]);
+            uint32_t k;
+            if (!key(pending[i], &k)) {
+                stats.dropped_no_cluster++;
+                continue;
+            }
+            recs[o] = recs[r0 + i];
+            recs[o++].key = k;
+        }
+        recs.resize(o);
     }
 };
 
@@ -304,6 +436,66 @@ int hq_wire_decode_batch(const uint8_t *bytes, size_t len, hq_wire_message *out,
     return *count > cap && out ? HQ_E_STATE : HQ_OK;
 }
 
+// The sending node's side (bench and tests): MessageBatch.MarshalTo (raft.pb.go:2417-2445) over
+// Message.MarshalTo (:2232-2296) of the fields hq_wire_message carries, every nullable=false
+// field written, the empty Snapshot's 24 bytes (Snapshot.MarshalTo :2142, Membership :2019)
+int hq_wire_encode_batch(const hq_wire_message *msgs, uint64_t n, uint64_t deployment_id,
+                         const uint8_t *source, size_t source_len, uint8_t *out, uint64_t cap,
+                         uint64_t *len) {
+    if ((n && !msgs) || !len || (source_len && !source) || (cap && !out)) return HQ_E_INVAL;
+    static const uint8_t kSnap[24] = {0x12, 0, 0x18, 0, 0x20, 0, 0x28, 0, 0x32, 2, 0x08, 0,
+                                      0x48, 0, 0x50, 0, 0x58, 0, 0x60, 0, 0x68, 0, 0x70, 0};
+    auto vlen = [](uint64_t v) {
+        uint32_t k = 1;
+        while (v >= 0x80) {
+            v >>= 7;
+            ++k;
+        }
+        return k;
+    };
+    auto put = [](uint8_t *p, uint64_t v) {
+        while (v >= 0x80) {
+            *p++ = (uint8_t)(v | 0x80);
+            v >>= 7;
+        }
+        *p++ = (uint8_t)v;
+        return p;
+    };
+    uint8_t *p = out, *const end = out + cap;
+    for (uint64_t i = 0; i < n; ++i) {
+        const hq_wire_message &m = msgs[i];
+        if (m.n_entries) return HQ_E_INVAL;      // (entries are not marshalled here)
+        const uint64_t f[10] = {m.ev.type, m.to, m.ev.from, m.cluster_id, m.ev.term, m.log_term,
+                                m.ev.log_index, m.commit, m.ev.reject ? 1u : 0u, m.ev.hint};
+        uint64_t size = 2 + sizeof kSnap + 1 + vlen(m.ev.hint_high);
+        for (uint64_t v : f) size += 1 + vlen(v);
+        if ((uint64_t)(end - p) < size + 1 + vlen(size)) return HQ_E_STATE;
+        *p++ = 0x0a;                              // requests (1), length-delimited
+        p = put(p, size);
+        for (uint32_t k = 0; k < 10; ++k) {
+            *p++ = (uint8_t)((k + 1) << 3);
+            p = put(p, f[k]);
+        }
+        *p++ = 0x62;
+        *p++ = (uint8_t)sizeof kSnap;
+        std::memcpy(p, kSnap, sizeof kSnap);
+        p += sizeof kSnap;
+        *p++ = 0x68;
+        p = put(p, m.ev.hint_high);
+    }
+    if ((uint64_t)(end - p) < 1 + 10 + 1 + 10 + source_len + 1 + 10) return HQ_E_STATE;
+    *p++ = 0x10;                                  // deployment_id (2)
+    p = put(p, deployment_id);
+    *p++ = 0x1a;                                  // source_address (3)
+    p = put(p, source_len);
+    if (source_len) std::memcpy(p, source, source_len);
+    p += source_len;
+    *p++ = 0x20;                                  // bin_ver (4)
+    p = put(p, HQ_RPC_BIN_VERSION);
+    *len = (uint64_t)(p - out);
+    return HQ_OK;
+}
+
 int hq_wire_open(uint64_t deployment_id, hq_wire **out) {
     if (!out) return HQ_E_INVAL;
     *out = new (std::nothrow) hq_wire();
@@ -316,6 +508,14 @@ void hq_wire_close(hq_wire *w) { delete w; }
 
 const char *hq_wire_last_error(const hq_wire *w) { return w ? w->err.c_str() : ""; }
 
+int hq_wire_attach(hq_wire *w, hq_worker *worker) {
+    if (!w) return HQ_E_INVAL;
+    if (!w->recs.empty()) return w->fail(HQ_E_STATE, "hq_wire_attach: events queued (reset first)");
+    w->worker = worker;
+    w->handle_of = ClusterIndex();
+    return HQ_OK;
+}
+
 int hq_wire_reset(hq_wire *w) {
     if (!w) return HQ_E_INVAL;
     w->recs.clear();
@@ -327,18 +527,45 @@ int hq_wire_reset(hq_wire *w) {
 
 int hq_wire_add_local(hq_wire *w, uint64_t cluster_id, const hq_event *events, uint64_t count) {
     if (!w || (count && !events)) return HQ_E_INVAL;
-    const uint32_t k = w->cluster(cluster_id);
-    for (uint64_t i = 0; i < count; ++i) {
-        const hq_event &e = events[i];
-        uint32_t cat;
-        switch (e.kind) {
-        case HQ_EV_READ: cat = 0; break;
-        case HQ_EV_CHECK_QUORUM:
-        case HQ_EV_ELECTION: cat = 2; break;
-        case HQ_EV_PROPOSE: cat = 3; break;
-        default: return w->fail(HQ_E_INVAL, "hq_wire_add_local: kind must be a local event");
+    const uint64_t off[2] = {0, count};
+    return hq_wire_add_locals(w, 1, &cluster_id, off, events);
+}
+
+int hq_wire_add_locals(hq_wire *w, uint64_t n, const uint64_t *cluster_ids, const uint64_t *offsets,
+                       const hq_event *events) {
+    if (!w || (n && (!cluster_ids || !offsets))) return HQ_E_INVAL;
+    if (n && offsets[n] > offsets[0] && !events) return HQ_E_INVAL;
+    for (uint64_t c = 0; c < n; ++c) {
+        if (offsets[c + 1] < offsets[c]) return w->fail(HQ_E_INVAL, "hq_wire_add_locals: offsets decrease");
+        for (uint64_t i = offsets[c]; i < offsets[c + 1]; ++i) {
+            switch (events[i].kind) {
+            case HQ_EV_READ: case HQ_EV_CHECK_QUORUM: case HQ_EV_ELECTION: case HQ_EV_PROPOSE: break;
+            default: return w->fail(HQ_E_INVAL, "hq_wire_add_local: kind must be a local event");
+            }
         }
-        w->recs.push_back({k, cat, e});
+    }
+    for (uint64_t c = 0; c < n; ++c) {
+        if (offsets[c + 1] == offsets[c]) continue;
+        uint32_t k;
+        if (!w->key(cluster_ids[c], &k)) {      // (a cluster the attached worker does not run)
+            w->stats.dropped_no_cluster += offsets[c + 1] - offsets[c];
+            continue;
+        }
+        for (uint64_t i = offsets[c]; i < offsets[c + 1]; ++i) {
+            const hq_event &e = events[i];
+            Rec r{};
+            r.key = k;
+            r.cat = e.kind == HQ_EV_READ ? 0 : e.kind == HQ_EV_PROPOSE ? 3 : 2;
+            r.kind = (uint8_t)e.kind;
+            r.reject = e.reject != 0;
+            r.type = e.type;
+            r.from = e.from;
+            r.term = e.term;
+            r.log_index = e.log_index;
+            r.hint = e.hint;
+            r.hint_high = e.hint_high;
+            w->recs.push_back(r);
+        }
     }
     return HQ_OK;
 }
@@ -346,43 +573,74 @@ int hq_wire_add_local(hq_wire *w, uint64_t cluster_id, const hq_event *events, u
 int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
     if (!w) return HQ_E_INVAL;
     if (!bytes && len) return w->fail(HQ_E_INVAL, "hq_wire_add_batch: NULL bytes");
-    // one pass: every message decoded into the scratch list; the batch's own fields (they follow
-    // the messages in the marshalled order) decide afterwards whether it is kept
-    w->scratch.clear();
+    // one pass: every message straight into a record (Message.MarshalTo's field order on the fast
+    // path, any order on the general one) with its cluster id aside; the batch's own fields
+    // (they follow the messages in the marshalled order) then decide whether the records stay
+    // and their clusters are resolved to keys
+    const size_t r0 = w->recs.size();
+    w->pending.clear();
+    uint64_t entries = 0, snap = 0;
     std::string err;
     hq_wire_batch_info bi;
     uint64_t n = 0;
     const int rc = parse_batch(bytes, len, &bi, &n, [&](const uint8_t *m, size_t k) {
-        w->scratch.emplace_back();
-        return decode_message(m, k, &w->scratch.back(), err);
+        Rec r;
+        r.key = 0;
+        r.pad = 0;
+        r.pad2 = 0;
+        uint64_t cid;
+        uint32_t ent;
+        if (!decode_marshal_order(m, m + k, r, cid, ent)) {
+            hq_wire_message x;
+            const int e = decode_message(m, k, &x, err);
+            if (e) return e;
+            r.kind = HQ_EV_MESSAGE;
+            r.type = x.ev.type;
+            r.from = x.ev.from;
+            r.term = x.ev.term;
+            r.log_index = x.ev.log_index;
+            r.hint = x.ev.hint;
+            r.hint_high = x.ev.hint_high;
+            r.reject = x.ev.reject != 0;
+            cid = x.cluster_id;
+            ent = x.n_entries;
+        }
+        entries += ent;
+        // HandleMessageBatch (nodehost.go:2039-2044): snapshot confirmations go aside
+        if (r.type == kSnapshotReceived) {
+            ++snap;
+            return HQ_OK;
+        }
+        r.cat = 1;
+        w->recs.push_back(r);
+        w->pending.push_back(cid);
+        return HQ_OK;
     });
-    if (rc) return w->fail(HQ_E_INVAL, "hq_wire_add_batch: malformed MessageBatch" +
-                                           (err.empty() ? std::string() : ": " + err));
+    if (rc) {
+        w->recs.resize(r0);
+        return w->fail(HQ_E_INVAL, "hq_wire_add_batch: malformed MessageBatch" +
+                                       (err.empty() ? std::string() : ": " + err));
+    }
     w->stats.batches++;
     w->stats.bytes += len;
     // Transport.handleRequest (transport.go:289-300): the whole batch is dropped on a foreign
-    // deployment id or binary version
+    // deployment id or binary version (none of its clusters is looked at)
     if (bi.deployment_id != w->deployment_id || bi.bin_ver != HQ_RPC_BIN_VERSION) {
+        w->recs.resize(r0);
         w->stats.dropped_batches++;
         w->stats.dropped_messages += n;
         return HQ_OK;
     }
-    w->recs.reserve(w->recs.size() + n);
-    for (const hq_wire_message &x : w->scratch) {
-        w->stats.messages++;
-        w->stats.entries += x.n_entries;
-        // HandleMessageBatch (nodehost.go:2039-2044): snapshot confirmations go aside
-        if (x.ev.type == kSnapshotReceived) {
-            w->stats.snapshot_received++;
-            continue;
-        }
-        w->recs.push_back({w->cluster(x.cluster_id), 1, x.ev});
-    }
+    w->stats.messages += n;
+    w->stats.entries += entries;
+    w->stats.snapshot_received += snap;
+    w->resolve(r0);
     return HQ_OK;
 }
 
 int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wire_stats *stats) {
     if (!w || !worker || !out) return HQ_E_INVAL;
+    if (w->worker) return w->fail(HQ_E_STATE, "hq_wire_step_input: attached (hq_wire_step_sized)");
     const uint32_t nc = (uint32_t)w->clusters.size();
     // handles; clusters this worker does not run are dropped (nodehost.go:2045-2046)
     std::vector<uint32_t> handle(nc);
@@ -390,11 +648,14 @@ int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wir
     for (uint32_t k = 0; k < nc; ++k)
         if (hq_worker_find(worker, w->clusters[k], &handle[k]) != HQ_OK) handle[k] = UINT32_MAX;
     // counting sort by (cluster order of first appearance, category), stable in arrival order
-    for (const auto &r : w->recs) cnt[(size_t)r.cluster * 4 + r.cat + 1]++;
+    for (const auto &r : w->recs) cnt[(size_t)r.key * 4 + r.cat + 1]++;
     for (size_t i = 1; i < cnt.size(); ++i) cnt[i] += cnt[i - 1];
-    std::vector<hq_event> sorted(w->recs.size());
+    std::vector<uint32_t> perm(w->recs.size());
     std::vector<uint64_t> pos(cnt.begin(), cnt.end() - 1);
-    for (const auto &r : w->recs) sorted[pos[(size_t)r.cluster * 4 + r.cat]++] = r.ev;
+    for (uint32_t i = 0; i < (uint32_t)w->recs.size(); ++i) {
+        const Rec &r = w->recs[i];
+        perm[pos[(size_t)r.key * 4 + r.cat]++] = i;
+    }
     w->groups.clear();
     w->offsets.assign(1, 0);
     w->events.clear();
@@ -406,7 +667,7 @@ int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wir
         }
         if (b == e) continue;
         w->groups.push_back(handle[k]);
-        w->events.insert(w->events.end(), sorted.begin() + b, sorted.begin() + e);
+        for (uint64_t j = b; j < e; ++j) w->events.push_back(w->recs[perm[j]].event());
         w->offsets.push_back(w->events.size());
     }
     out->n_groups = w->groups.size();
@@ -434,6 +695,61 @@ int hq_wire_step_stream(hq_wire *w, hq_worker *worker, hq_step_stream *out, hq_w
     out->bytes = w->bytes.data();
     out->sizes = nullptr;
     out->n_events = out->n_bytes = 0;
+    out->sizes16 = nullptr;
+    return HQ_OK;
+}
+
+int hq_wire_step_sized(hq_wire *w, uint8_t *bytes, uint64_t cap, uint16_t *sizes16, uint64_t n_cap,
+                       hq_step_stream *out, hq_wire_stats *stats) {
+    if (!w || !out || (cap && !bytes)) return HQ_E_INVAL;
+    if (!w->worker) return w->fail(HQ_E_STATE, "hq_wire_step_sized: no worker attached");
+    uint64_t n = 0;
+    if (hq_worker_group_count(w->worker, &n) != HQ_OK) return HQ_E_INVAL;
+    if (n > n_cap || (n && !sizes16))
+        return w->fail(HQ_E_INVAL, "hq_wire_step_sized: sizes16 holds fewer words than the worker's groups");
+    // counting sort of the records by handle, stable in arrival order; each handle's records
+    // then taken category by category (node.handleEvents: local ReadIndex, received messages,
+    // ticks, proposals)
+    const uint32_t nr = (uint32_t)w->recs.size();
+    w->cnt.assign(n + 1, 0);
+    for (const Rec &r : w->recs) w->cnt[r.key + 1]++;
+    for (uint64_t h = 0; h < n; ++h) w->cnt[h + 1] += w->cnt[h];
+    w->perm.resize(nr);
+    w->pos.assign(w->cnt.begin(), w->cnt.end() - 1);
+    for (uint32_t i = 0; i < nr; ++i) w->perm[w->pos[w->recs[i].key]++] = i;
+    uint8_t *p = bytes, *const end = bytes + cap;
+    uint64_t events = 0;
+    for (uint64_t h = 0; h < n; ++h) {
+        const uint32_t b = w->cnt[h], e = w->cnt[h + 1];
+        uint8_t *const g0 = p;
+        if (e > b) {
+            // the group's events gathered in arrival order; put in category order (a stable
+            // insertion sort of the few out of place) when they are not already
+            w->grp.resize(e - b);
+            Rec *g = w->grp.data();
+            bool sorted = true;
+            for (uint32_t j = b; j < e; ++j) {
+                g[j - b] = w->recs[w->perm[j]];
+                sorted = sorted && (j == b || g[j - b - 1].cat <= g[j - b].cat);
+            }
+            if (!sorted)
+                for (uint32_t x = 1; x < e - b; ++x)
+                    for (uint32_t y = x; y > 0 && g[y - 1].cat > g[y].cat; --y) std::swap(g[y - 1], g[y]);
+            p = hqs::encode_group(p, end, static_cast<const hqs::WireEvent *>(g), e - b);
+            if (!p) return w->fail(HQ_E_STATE, "hq_wire_step_sized: the stream does not fit cap");
+            if (p - g0 > 0xFFFF || e - b > 0xFFFF)
+                return w->fail(HQ_E_INVAL, "hq_wire_step_sized: a group of 2^16 events or bytes");
+            events += e - b;
+        }
+        sizes16[h] = (uint16_t)(p - g0);
+    }
+    *out = hq_step_stream{};
+    out->n_groups = n;
+    out->bytes = bytes;
+    out->sizes16 = sizes16;
+    out->n_events = events;
+    out->n_bytes = (uint64_t)(p - bytes);
+    if (stats) *stats = w->stats;
     return HQ_OK;
 }
 

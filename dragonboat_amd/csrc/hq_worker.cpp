@@ -1053,6 +1053,12 @@ int hq_worker_add_groups(hq_worker *w, const hq_worker_group *groups, uint64_t c
     return HQ_OK;
 }
 
+int hq_worker_group_count(hq_worker *w, uint64_t *n) {
+    if (!w || !n) return HQ_E_INVAL;
+    *n = w->groups.size();
+    return HQ_OK;
+}
+
 int hq_worker_find(hq_worker *w, uint64_t cluster_id, uint32_t *handle) {
     if (!w) return HQ_E_INVAL;
     auto it = w->index.find(cluster_id);

@@ -433,6 +433,13 @@ SIGNATURES = {
     "hq_wire_add_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
     "hq_wire_step_input": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(StepInput),
                                           ctypes.POINTER(WireStats)]),
+    "hq_wire_attach": (ctypes.c_int, [_vp, _vp]),
+    "hq_wire_encode_batch": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp,
+                                            ctypes.c_size_t, _vp, ctypes.c_uint64, _u64p]),
+    "hq_wire_add_locals": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "hq_wire_step_sized": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                          ctypes.POINTER(StepStream), ctypes.POINTER(WireStats)]),
+    "hq_worker_group_count": (ctypes.c_int, [_vp, _u64p]),
     "hq_synth_commit_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec), ctypes.POINTER(CommitArgs)]),
     "hq_synth_commit_lag_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthSpec),
                                                ctypes.POINTER(LagArgs), _vp]),
@@ -1535,9 +1542,8 @@ class Worker:
                                 np.uint32).astype(np.int64)
             allr = np.frombuffer((ctypes.c_char * (nt * SLOT_TILE * READY_COMPACT_DTYPE.itemsize))
                                  .from_address(out.ready_slots), READY_COMPACT_DTYPE)
-            ix = np.repeat(np.arange(nt, dtype=np.int64) * SLOT_TILE, cnt) + \
-                (np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt))
-            res["ready_slots"] = allr[ix]          # (a fancy index: a copy)
+            keep = np.arange(SLOT_TILE)[None, :] < cnt[:, None]
+            res["ready_slots"] = allr.reshape(nt, SLOT_TILE)[keep]   # (a copy, tile order)
             assert len(res["ready_slots"]) == out.n_ready_slotted
         if out.committed_column:
             buf = (ctypes.c_char * (n_listed * 8)).from_address(out.committed_column)
@@ -1856,6 +1862,21 @@ def decode_batch(data: bytes):
     return out[:n.value], info
 
 
+def encode_wire_batch(msgs, deployment_id=0, source_address=b"", out=None):
+    """hq_wire_encode_batch: one MessageBatch of WIRE_MESSAGE_DTYPE messages (no entries), as
+    the sending node marshals it. Into `out` (uint8, e.g. pinned) when given: returns the bytes
+    written as a view of it; else a new array."""
+    m = np.ascontiguousarray(msgs, WIRE_MESSAGE_DTYPE)
+    src = np.frombuffer(source_address, np.uint8) if source_address else np.zeros(1, np.uint8)
+    if out is None:
+        out = np.empty(len(m) * 160 + len(source_address) + 24, np.uint8)
+    n = ctypes.c_uint64(0)
+    _chk(lib.hq_wire_encode_batch(_p(m) if len(m) else None, len(m), deployment_id, _p(src),
+                                  len(source_address), _p(out), len(out), ctypes.byref(n)),
+         "hq_wire_encode_batch")
+    return out[:n.value]
+
+
 class Wire:
     """hq_wire: a step's input assembled from received MessageBatch bytes and local events."""
 
@@ -1884,6 +1905,34 @@ class Wire:
     def add_batch(self, data: bytes) -> None:
         buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
         self._check(lib.hq_wire_add_batch(self.h, _p(buf), len(data)), "hq_wire_add_batch")
+
+    def add_batch_at(self, addr: int, n: int) -> None:
+        """hq_wire_add_batch of n bytes at a raw address (a prepared buffer; no copy)."""
+        self._check(lib.hq_wire_add_batch(self.h, _vp(addr), n), "hq_wire_add_batch")
+
+    def add_locals(self, cluster_ids, offsets, events) -> None:
+        """hq_wire_add_locals: cluster c's local events are events[offsets[c]:offsets[c + 1]]."""
+        c = np.ascontiguousarray(cluster_ids, np.uint64)
+        o = np.ascontiguousarray(offsets, np.uint64)
+        e = np.ascontiguousarray(events, EVENT_DTYPE)
+        assert len(o) == len(c) + 1
+        self._check(lib.hq_wire_add_locals(self.h, len(c), _p(c), _p(o), _p(e) if len(e) else None),
+                    "hq_wire_add_locals")
+
+    def attach(self, worker: "Worker") -> None:
+        """hq_wire_attach: messages resolved to the worker's handles as they are decoded."""
+        self._check(lib.hq_wire_attach(self.h, worker.h if worker else None), "hq_wire_attach")
+
+    def step_sized(self, data: np.ndarray, sizes16: np.ndarray):
+        """hq_wire_step_sized into the caller's buffers (uint8 `data`, uint16 `sizes16`, e.g.
+        pinned): returns (SizedStream over them, WireStats)."""
+        assert data.dtype == np.uint8 and sizes16.dtype == np.uint16
+        st, out = WireStats(), StepStream()
+        self._check(lib.hq_wire_step_sized(self.h, _p(data), len(data), _p(sizes16), len(sizes16),
+                                           ctypes.byref(out), ctypes.byref(st)),
+                    "hq_wire_step_sized")
+        n = out.n_groups
+        return SizedStream(None, sizes16[:n], out.n_events, data[:out.n_bytes]), st
 
     def step_input(self, worker: "Worker"):
         """(groups, offsets, events) numpy views of the assembled hq_step_input (owned by the

@@ -1057,6 +1057,8 @@ int hq_worker_add_groups(hq_worker *w, const hq_worker_group *groups, uint64_t c
                          const hq_member *members);
 /* The handle of a cluster. */
 int hq_worker_find(hq_worker *w, uint64_t cluster_id, uint32_t *handle);
+/* The worker's groups (handles 0 .. *n - 1; ABI 21). */
+int hq_worker_group_count(hq_worker *w, uint64_t *n);
 /* Overwrite a group's state (re-sync after fallback); clears its read queue and votes and
  * resumes it. */
 int hq_worker_set_group(hq_worker *w, const hq_worker_group *g, const hq_member *members);
@@ -1302,6 +1304,15 @@ typedef struct hq_wire_stats {    /* counters since the last hq_wire_reset */
 int hq_wire_decode_batch(const uint8_t *bytes, size_t len, hq_wire_message *out, uint64_t cap,
                          uint64_t *count, hq_wire_batch_info *info);
 
+/* The sending side (ABI 21; benchmarks and tests): msgs[0 .. n) marshalled as one MessageBatch
+ * exactly as MessageBatch.MarshalTo / Message.MarshalTo write it (raft.pb.go:2417-2445,
+ * :2232-2296: every nullable=false field in field order, the empty Snapshot), then deployment_id,
+ * source_address and HQ_RPC_BIN_VERSION. Messages with entries are HQ_E_INVAL (not marshalled);
+ * HQ_E_STATE when cap is short (160 bytes per message and source_len + 24 always suffice). */
+int hq_wire_encode_batch(const hq_wire_message *msgs, uint64_t n, uint64_t deployment_id,
+                         const uint8_t *source, size_t source_len, uint8_t *out, uint64_t cap,
+                         uint64_t *len);
+
 typedef struct hq_wire hq_wire;
 int hq_wire_open(uint64_t deployment_id, hq_wire **out);
 void hq_wire_close(hq_wire *w);
@@ -1318,6 +1329,25 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len);
 int hq_wire_step_input(hq_wire *w, hq_worker *worker, hq_step_input *out, hq_wire_stats *stats);
 /* The same step as an event stream (see "event streams" above); arrays owned by w likewise. */
 int hq_wire_step_stream(hq_wire *w, hq_worker *worker, hq_step_stream *out, hq_wire_stats *stats);
+/* Local events of many clusters at once: cluster c's are events[offsets[c] .. offsets[c + 1]). */
+int hq_wire_add_locals(hq_wire *w, uint64_t n, const uint64_t *cluster_ids, const uint64_t *offsets,
+                       const hq_event *events);
+/* ABI 21, the step worker's production feed: the step in the worker's handle order, straight into
+ * a sized stream. hq_wire_attach binds a worker (before events are queued): from then on every
+ * message's cluster is resolved to the worker's handle as its batch is decoded (through a table
+ * the wire keeps across steps — handles never change), messages of clusters the worker does not
+ * run are dropped at once, and hq_wire_step_input / _step_stream are HQ_E_STATE. Each step:
+ * hq_wire_reset, hq_wire_add_batch / hq_wire_add_locals, then hq_wire_step_sized writes every
+ * handle h in 0 .. n - 1 (n = hq_worker_group_count) — its events in node.handleEvents order as
+ * stream bytes into bytes[0 .. cap) and their byte count into sizes16[h] (0: no event) — and fills
+ * *out as hq_step_stream's sized form with 2-byte words and groups = NULL, ready for
+ * hq_worker_step_stream / hq_worker_step_jobs (bytes and sizes16 in pinned memory are read by
+ * the device in place). HQ_E_STATE when cap runs short (HQ_EVENT_STREAM_MAX bytes per event
+ * always suffice), HQ_E_INVAL when sizes16 has fewer than n words (n_cap) or a group reaches 2^16
+ * events or bytes. The batch acceptance and per-cluster order are hq_wire_step_input's. */
+int hq_wire_attach(hq_wire *w, hq_worker *worker);
+int hq_wire_step_sized(hq_wire *w, uint8_t *bytes, uint64_t cap, uint16_t *sizes16, uint64_t n_cap,
+                       hq_step_stream *out, hq_wire_stats *stats);
 
 /* ---------------------------------------------------------------- synthetic inputs ---------- */
 

@@ -228,6 +228,11 @@ class WireBackend(WorkerBackend):
         super().__init__(hq, n_max, seed, worker, on_device, stream)
         self.wire = hq.Wire(self.DEPLOYMENT)
         self.last_stats = None
+        # "sized16-slots": the production feed — the wire attached to the worker, the step in
+        # handle order straight into pinned stream buffers (hq_wire_step_sized)
+        self.attached = stream == "sized16-slots"
+        if self.attached:
+            self.wire.attach(self.w)
 
     def close(self):
         self.wire.close()
@@ -273,6 +278,22 @@ class WireBackend(WorkerBackend):
             wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT, source_address=b"n2:1"))
             if i == 0:   # a foreign deployment's batch: dropped whole (transport.go:291-295)
                 wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT + 1))
+        if self.attached:
+            # every handle in order (a group without events has size 0); handles are the order
+            # the groups were added in
+            ne = sum(len(v) for v in per_group.values())
+            data = self._pinned("wdata", np.zeros(ne * hq.HQ_EVENT_STREAM_MAX + 64, np.uint8))
+            sizes = self._pinned("wsizes", np.zeros(len(self.cids), np.uint16))
+            ss, st = wire.step_sized(data, sizes)
+            self.last_stats = st
+            refs, k = {}, 0
+            for cid in self.cids:
+                for pos in range(len(per_group.get(cid, ()))):
+                    refs[k] = (cid, pos)
+                    k += 1
+            assert k == ss[2] and len(ss[1]) == len(self.cids)
+            self.last_cids = list(self.cids)
+            return ss, refs
         if self.stream:                       # hq_wire_step_stream
             grp, off, boff, data, st = wire.step_stream(self.w)
         else:

@@ -98,3 +98,37 @@ def test_cap_too_small_is_reported(hq):
     n = ctypes.c_uint64(0)
     rc = hq.lib.hq_wire_decode_batch(hq._p(buf), len(data), hq._p(out), 2, ctypes.byref(n), None)
     assert rc == hq.HQ_E_STATE and n.value == 3
+
+
+def test_encode_batch_matches_the_marshaller(hq):
+    """hq_wire_encode_batch (the sending node's MessageBatch.MarshalTo, bench infrastructure)
+    writes exactly the bytes of the Python restatement (tests/wire_encode.py, pinned by the
+    hand-derived fixtures), for messages with small and 10-byte varints; they decode back."""
+    rng = np.random.default_rng(21)
+    n = 300
+    m = np.zeros(n, hq.WIRE_MESSAGE_DTYPE)
+    big = lambda k: rng.integers(0, 1 << 63, k, dtype=np.uint64) * np.uint64(2) + \
+        rng.integers(0, 2, k, dtype=np.uint64)
+    for f in ("from", "term", "log_index", "hint", "hint_high"):
+        m["ev"][f] = np.where(rng.random(n) < 0.5, rng.integers(0, 300, n).astype(np.uint64), big(n))
+    m["ev"]["type"] = rng.integers(0, 30, n)
+    m["ev"]["reject"] = rng.integers(0, 2, n)
+    m["ev"]["kind"] = hq.EV_MESSAGE
+    for f in ("cluster_id", "to", "log_term", "commit"):
+        m[f] = np.where(rng.random(n) < 0.5, rng.integers(0, 300, n).astype(np.uint64), big(n))
+    got = hq.encode_wire_batch(m, deployment_id=77, source_address=b"n9:1")
+    want = we.batch([we.message(type=int(x["ev"]["type"]), to=int(x["to"]), frm=int(x["ev"]["from"]),
+                                cluster_id=int(x["cluster_id"]), term=int(x["ev"]["term"]),
+                                log_term=int(x["log_term"]), log_index=int(x["ev"]["log_index"]),
+                                commit=int(x["commit"]), reject=bool(x["ev"]["reject"]),
+                                hint=int(x["ev"]["hint"]), hint_high=int(x["ev"]["hint_high"]))
+                     for x in m], deployment_id=77, source_address=b"n9:1")
+    assert bytes(got) == want
+    dec, info = hq.decode_batch(bytes(got))
+    assert info.deployment_id == 77 and len(dec) == n
+    for f in ("cluster_id", "to", "log_term", "commit"):
+        np.testing.assert_array_equal(dec[f], m[f])
+    for f in ("type", "from", "term", "log_index", "hint", "hint_high", "reject"):
+        np.testing.assert_array_equal(dec["ev"][f], m["ev"][f])
+    with pytest.raises(hq.HQError):
+        hq.encode_wire_batch(m, out=np.zeros(100, np.uint8))
