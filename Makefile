@@ -15,7 +15,11 @@ DEPS := $(wildcard $(CSRC)/*.h) include/hipquorum.h
 CXX ?= g++
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -pthread -Wall -Wextra
 
-all: $(LIB) oracle
+all: $(LIB) oracle tools/link_probe
+
+# the host-link probe bench.py's step legs run beside them (their link roofline)
+tools/link_probe: tools/link_probe.cpp
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 
 $(LIBDIR)/%.o: $(CSRC)/%.hip $(DEPS)
 	@mkdir -p $(LIBDIR)

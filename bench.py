@@ -567,7 +567,7 @@ def fused_chunks(steps):
     return [(bounds[i], bounds[i + 1] - bounds[i]) for i in range(n)]
 
 
-def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
+def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused", share=1):
     """A commit workload stepped through the persistent commit engine (hq_engine_*,
     dragonboat_amd/csrc/hq_engine.hip): per timed window the K steps are posted one hq_engine_post call each
     (post-as-ready, the reference's step-worker shape) and decided by ONE resident launch (no
@@ -581,7 +581,9 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
     launches (hq_commit_fused_dev, up to 32 batches each). Each batch is one step worker's step of
     1 M groups (the groups are disjoint between batches), so one launch decides the co-resident
     workers' batches of a step (16 step workers in the reference, internal/settings/hard.go:35,
-    execengine.go:675-690). headline "engine": the resident engine's windows."""
+    execengine.go:675-690). headline "engine": the resident engine's windows. share: the ranks
+    on this GPU; above 1 each engine is capped at its share of the full grid (max_workgroups), so
+    that the co-located engines are all resident."""
     from dragonboat_amd import hipquorum as hq
     from dragonboat_amd import shard
 
@@ -589,10 +591,15 @@ def run_engine(w, steps, warmup, d: Dist, windows=3, headline="fused"):
     sets, per_set = build_sets(ctx, hq, shard, w, d)
     nsets = len(sets)
     lay = hq.HQ_LAYOUT_TILES_LEADER if w.get("lead") else hq.HQ_LAYOUT_TILES
-    eng = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16)
+    mw = 0
+    if share > 1:
+        e0 = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16)
+        mw = max(1, e0.info().grid // share)
+        e0.close()
+    eng = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16, max_workgroups=mw)
     # the same engine with per-step completion flags (what a step worker that applies each step's
     # commits as soon as they are decided runs): its windows are reported beside the others
-    eng_sig = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16, signal=True)
+    eng_sig = hq.Engine(ctx, w["n"], w["form"], lay, ring_len=16, signal=True, max_workgroups=mw)
 
     def arr(i0, k):
         return hq.commit_batch_array([batch_args(sets[(i0 + i) % nsets][0]) for i in range(k)])
@@ -1465,6 +1472,67 @@ def _device_split(rs):
             "_end_ns": r["wait_end_ns"], "_end_ticks": r["device_end_ticks"]}
 
 
+_LINK = {}
+
+
+def _link_probe(d):
+    """The host link's measured rates for kernels that read / write pinned host memory in place
+    (tools/link_probe --json, 64 MiB per direction, best of its grids; built by `make all`):
+    one direction at a time and both at once. Run once per process, on rank 0 (None elsewhere
+    or when the probe is missing or fails)."""
+    if "v" in _LINK:
+        return _LINK["v"]
+    v = None
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "link_probe")
+    if d.rank == 0 and os.path.exists(exe):
+        import subprocess
+        try:
+            r = subprocess.run([exe, "64", str(d.device), "--json"], capture_output=True,
+                               text=True, timeout=90)
+            if r.returncode == 0:
+                v = json.loads(r.stdout.strip().splitlines()[-1])
+        except (subprocess.SubprocessError, ValueError, IndexError):
+            v = None
+    _LINK["v"] = v
+    return v
+
+
+def _out_bytes(rs):
+    """The bytes one jobs step's kernels wrote into the workers' pinned output (the host link's
+    write direction): every list and column the results view, the ReadyToRead slots by their
+    records and count words (the rest of each tile's slot is not written)."""
+    n = 0
+    for r in rs:
+        for k, v in r.items():
+            if k == "ready_slots":
+                continue
+            if isinstance(v, np.ndarray):
+                n += v.nbytes
+        if "ready_slots" in r:
+            n += len(r["ready_slots"]) * 24 + 4 * ((len(r.get("committed_advance", ())) + 255) // 256)
+    return n
+
+
+def _link_block(d, bytes_in, bytes_out, gpu_ms):
+    """The step's host-link roofline: bytes read from pinned memory (the stream and its size
+    words) and written to it (the outputs) per step, over the GPU time of the step (median of
+    the W = 1 device-only steps), against the probe's rates. frac = both directions' bytes per
+    second over the probe's both-at-once total; frac_serial = the time the two directions
+    would take one after the other at the probe's one-direction rates, over the GPU time."""
+    lk = _link_probe(d)
+    t = gpu_ms / 1e3
+    out = {"bytes_in": int(bytes_in), "bytes_out": int(bytes_out), "gpu_ms": round(gpu_ms, 4),
+           "in_GBps": round(bytes_in / t / 1e9, 2), "out_GBps": round(bytes_out / t / 1e9, 2),
+           "both_GBps": round((bytes_in + bytes_out) / t / 1e9, 2), "probe": lk}
+    if lk:
+        out["frac"] = round((bytes_in + bytes_out) / t / 1e9 / lk["both_GBps"], 3)
+        out["frac_serial"] = round((bytes_in / lk["read_GBps"] + bytes_out / lk["write_GBps"])
+                                   / 1e9 / t, 3)
+    else:
+        out["frac"] = None
+    return out
+
+
 def _wake_lag(phases, prefix):
     """Each step's wake-up lateness (ms) from the clocks of its wait's end: the host's return
     time less the device's end stamp (10 ns per tick), each against the run's smallest such
@@ -1564,7 +1632,7 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
                  for o, e0, e1 in parts] for _ in range(2)]
         modes[W] = dict(parts=parts, bufs=bufs, nbytes=[[0] * W, [0] * W], dev=workers(),
                         e2e=workers(), t={"dev": [], "e2e": []}, bytes=0, phases=[],
-                        check={"dev": [], "e2e": []},
+                        check={"dev": [], "e2e": []}, link=[],
                         mirror={k: CommitMirror(cids, g["committed"], bounds)
                                 for k in ("dev", "e2e")})
     pool = ThreadPoolExecutor(max(Ws) + 1)
@@ -1648,6 +1716,9 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             tq1 = cgroup_throttled_us()
             rs = j.results(copy=False)
             dev_split = _device_split(rs)
+            if W == 1 and s >= STEP_WARM:
+                mo["link"].append((sum(mo["nbytes"][slot]) + 2 * G, _out_bytes(rs),
+                                   dev_split["gpu_ms"]))
             mo["check"]["dev"].append(mo["mirror"]["dev"].step(rs))
             j = jobs(W, slot, "e2e")
             d.barrier()
@@ -1740,6 +1811,9 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
         "wait_policy": {"mode": wait_name, "poll_us": wait[1], "sleep_us": wait[2],
                         "clock": "HQ_WAIT_CLOCK: the device's end stamp beside the host's return"},
         "stream_bytes_per_event": modes[1]["bytes"] / max(1, ev_total),
+        # the host-link roofline of the W = 1 device-only steps (medians over the timed steps)
+        "link": (_link_block(d, *(float(np.median([x[i] for x in modes[1]["link"]]))
+                                  for i in range(3))) if modes[1]["link"] else None),
         "modes_agree": same_modes,
         **({"modes_mismatch": mismatch} if mismatch else {}),
         "producer": f"compact 16-byte message records (hq_event16), the W workers' streams "
@@ -2416,13 +2490,17 @@ def run_rank(args, d, progress):
     use_engine = args.mode in ("engine", "fused") and engine_ok(w)
     progress(f"headline {args.workload}: {args.windows if use_engine else 1} x {args.steps} steps"
              f" ({args.mode if use_engine else 'launch per step'}), {args.warmup} warmup")
-    r = (run_engine(w, args.steps, args.warmup, d, windows=args.windows, headline=args.mode)
-         if use_engine else run_gpu(w, args.steps, args.warmup, d))
-    r["world"] = d.world
     from dragonboat_amd import hipquorum as hq
 
     devices = d.gather_obj({"rank": d.rank, "device": d.device,
                             "pci_bus_id": hq.device_pci_bus_id(d.device)})
+    # ranks sharing one GPU (a rehearsal of N ranks on fewer devices) split its CUs between their
+    # engines, so that every engine's grid is resident at once
+    per_device = max(1, d.world // max(1, len({x["pci_bus_id"] or x["device"] for x in devices})))
+    r = (run_engine(w, args.steps, args.warmup, d, windows=args.windows, headline=args.mode,
+                    share=per_device)
+         if use_engine else run_gpu(w, args.steps, args.warmup, d))
+    r["world"] = d.world
     host_threads, _ = cpu_thread_counts()
     progress("full-size parity of every rank's set 0")
     rank_parity(w, r, d, args.no_cpu)
@@ -2513,6 +2591,11 @@ def _short(rec):
     par = rec.get("parity_full_size")
     if isinstance(par, dict):
         out["parity_equal"] = par.get("equal")
+    lk = rec.get("link")
+    if isinstance(lk, dict):
+        out["link"] = {k: lk.get(k) for k in ("frac", "frac_serial", "both_GBps", "gpu_ms")}
+        if lk.get("probe"):
+            out["link"]["peak_both_GBps"] = lk["probe"].get("both_GBps")
     lat = rec.get("latency_ms")
     if isinstance(lat, dict):
         out["p99_ms"] = {k: v["p99"] for k, v in lat.items() if v}
@@ -2619,7 +2702,7 @@ def report(args, d, res, launcher):
         # the step legs keep their p99 per mode and their replay ratios; the others their value
         # and roofline fraction
         line["extra"] = {k: ({kk: v[kk] for kk in ("value", "p99_ms", "vs_cpu_replay_end_to_end",
-                                                     "parity_committed") if kk in v}
+                                                     "parity_committed", "link") if kk in v}
                              if k in ("step", "step5") else
                              {kk: v.get(kk) for kk in ("value", "roofline_frac") if kk in v})
                          for k, v in summary.items()}

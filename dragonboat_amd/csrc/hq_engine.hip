@@ -57,6 +57,9 @@ constexpr int kPollCopies = 16;            // copies of the relayed count, 256 B
                                            // workgroup 97 us after the launch, round-4 probes)
 constexpr int kPollStride = 32;            // u64 between copies
 constexpr int kInit = 32;                  // descriptors handed over in the kernel arguments
+constexpr int kPools = 8;                  // balanced mode: one tile pool per XCD (blockIdx % 8)
+constexpr int kPoolStride = 16;            // u64 between pool counters (one 128-B line each)
+constexpr int kChunkQ = 32;                // balanced mode: claimed chunks a workgroup keeps
 
 struct EngineDesc {   // one posted step, 64 bytes = 8 u64 words (one per relay lane)
     uint64_t G;
@@ -88,6 +91,12 @@ struct EngineK {
     EngineDesc *d_ring;            // device [depth]
     uint64_t *d_polled;            // device [kPollCopies * kPollStride]: copies of d_posted
     uint64_t *d_exit;              // device: the epoch of the launch that is ending
+    // balanced mode (BAL): each step's tiles split into `pools` contiguous pools, pool x taken
+    // by the workgroups with blockIdx % pools == x (one XCD under round-robin dispatch) in chunks
+    // of `chunk` tiles through a device ticket counter per pool
+    uint64_t *d_claim;             // device [kPools * kPoolStride]: tickets taken this launch
+    uint64_t *d_pdone;             // device [depth][kPools * kPoolStride]: tiles decided per pool
+    uint32_t chunk, pools;
     // the descriptors of steps [init_base, init_base + init_count), known when the grid was
     // launched: every workgroup starts with them in LDS (no relay, no poll at the start)
     uint64_t init_base;
@@ -175,6 +184,12 @@ __device__ void relay(GlobalEngineK &e, uint32_t lane) {
 // counter, and the last of those publishes the step to the host. The last arriver of a counter
 // resets it for the slot's next step: the host posts that step only after it has seen this one's
 // done flag, which is written after the resets.
+__device__ void publish(GlobalEngineK &e, uint64_t s) {
+    const uint64_t slot = s & (e.depth - 1);
+    __hip_atomic_store(gp(e.h_clock) + slot, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(gp(e.h_done) + slot, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ void arrive(GlobalEngineK &e, uint64_t s) {
     const uint64_t slot = s & (e.depth - 1);
     const uint32_t shard = blockIdx.x % kShards;
@@ -189,8 +204,44 @@ __device__ void arrive(GlobalEngineK &e, uint64_t s) {
                                __HIP_MEMORY_SCOPE_AGENT) + 1 != nshard)
         return;
     __hip_atomic_store(gp(e.d_top) + slot, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(gp(e.h_clock) + slot, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(gp(e.h_done) + slot, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    publish(e, s);
+}
+
+// Balanced mode: tiles [*b, *b + *n) of a step of G groups form pool x
+__device__ __forceinline__ void pool_range(uint64_t G, uint32_t pools, uint32_t x, uint64_t *b,
+                                           uint64_t *n) {
+    const uint64_t tiles = (G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
+    *b = tiles * x / pools;
+    *n = tiles * (x + 1) / pools - *b;
+}
+
+// Balanced mode, one lane: `n` tiles of pool x of step s decided (their stores complete) — the
+// add, issued (pool_add) one chunk before its returned value is looked at (pool_settle), so no
+// wave waits for an atomic's round trip. The adder that completes the pool counts it on the
+// step's top counter, and the one that completes the last non-empty pool publishes the step (the
+// counters reset by their last adder, as in arrive)
+__device__ __forceinline__ uint64_t *pool_ctr(GlobalEngineK &e, uint64_t s, uint32_t x) {
+    return gp(e.d_pdone) + ((s & (e.depth - 1)) * kPools + x) * kPoolStride;
+}
+
+__device__ __forceinline__ uint64_t pool_add(GlobalEngineK &e, uint64_t s, uint32_t x, uint32_t n) {
+    return __hip_atomic_fetch_add(pool_ctr(e, s, x), (uint64_t)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void pool_settle(GlobalEngineK &e, uint64_t s, uint64_t G, uint32_t x, uint32_t n,
+                            uint64_t before_add) {
+    const uint64_t slot = s & (e.depth - 1);
+    uint64_t b, len;
+    pool_range(G, e.pools, x, &b, &len);
+    if (before_add + n != len) return;
+    __hip_atomic_store(pool_ctr(e, s, x), (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t tiles = (G + HQ_TILE_GROUPS - 1) / HQ_TILE_GROUPS;
+    const uint64_t busy = tiles < e.pools ? tiles : e.pools;     // the pools with a tile
+    if (__hip_atomic_fetch_add(gp(e.d_top) + slot, (uint64_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) + 1 != busy)
+        return;
+    __hip_atomic_store(gp(e.d_top) + slot, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish(e, s);
 }
 
 // Per-workgroup state in LDS. The descriptors of steps [.., known) sit in `ring` (slot = step &
@@ -214,6 +265,12 @@ struct EngineLds {
     uint32_t top_end;     // end of the last installed step
     uint32_t done;
     uint32_t waiting, lock, exit;
+    uint32_t stopc;       // balanced mode: waves at the STOP
+    // balanced mode: the workgroup's claimed chunks (pool tickets), chunk q at q % kChunkQ;
+    // cq_have = chunks published; cq_done = tiles of the chunk counted
+    uint32_t cq_have;
+    uint32_t cq_T[kChunkQ];
+    uint32_t cq_done[kChunkQ];
 };
 
 __device__ __forceinline__ bool before(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
@@ -230,6 +287,25 @@ __device__ __forceinline__ uint64_t wg_len(uint64_t G, uint64_t per) {
 __device__ void install(GlobalEngineK &e, EngineLds &l, uint64_t from, uint64_t to) {
     const uint64_t dmask = e.depth - 1;
     uint32_t top = l.top_end;
+    if (e.chunk) {
+        // balanced: `end` counts the tickets (chunks) of this workgroup's pool; a step with no
+        // tile at all is published by workgroup 0 at once
+        const uint32_t pools = e.pools, x = blockIdx.x % pools, chunk = e.chunk;
+        for (uint64_t s = from; s < to; ++s) {
+            const EngineDesc &d = l.ring[s & dmask];
+            uint32_t len = 0;
+            if (!(d.flags & kDescStop)) {
+                uint64_t b, n;
+                pool_range(d.G, pools, x, &b, &n);
+                len = (uint32_t)((n + chunk - 1) / chunk);
+                if (d.G == 0 && e.signal && blockIdx.x == 0) publish(e, s);
+            }
+            top += len;
+            l.end[s & dmask] = top;
+        }
+        l.top_end = top;
+        return;
+    }
     for (uint64_t s = from; s < to; ++s) {
         const EngineDesc &d = l.ring[s & dmask];
         const uint32_t len = (d.flags & kDescStop) ? 0u : (uint32_t)wg_len(d.G, d.per);
@@ -381,15 +457,19 @@ __device__ __forceinline__ uint32_t claim(EngineLds &l, uint32_t lane) {
 
 // SIG: per-step completion signals (write-through stores, drained before a tile is counted).
 // INPLACE: the device-resident table decided in place (committed' into the tile's row).
-template <int N, int FORM, int LEAD, bool INPLACE, int BLK, bool SIG>
+// BAL: balanced mode (tiles taken from per-XCD pools through device tickets; not with INPLACE).
+template <int N, int FORM, int LEAD, bool INPLACE, int BLK, bool SIG, bool BAL>
 __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(BLK >= 1024 ? 8 : 1, 8)))
 void k_commit_engine(const EngineK e) {
+    static_assert(!(BAL && INPLACE), "an in-place table keeps each tile with one workgroup");
     constexpr int WPW = BLK / 64;   // waves per workgroup
     __shared__ EngineLds l;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t dmask = e.depth - 1;
-    const uint64_t s0 = uniform64(gp(e.d_cursor)[blockIdx.x]);   // written by the previous launch
+    // written by the previous launch (balanced: every workgroup resumes where workgroup 0 did,
+    // so that all map the pools' tickets to the same steps)
+    const uint64_t s0 = uniform64(gp(e.d_cursor)[BAL ? 0 : blockIdx.x]);
     // the descriptors handed over at launch (the host's oldest incomplete step <= the cursor)
     for (uint32_t i = threadIdx.x; i < kEngineMaxDepth; i += BLK) {
         l.fin[i] = 0;
@@ -404,7 +484,14 @@ void k_commit_engine(const EngineK e) {
         l.ticket = 0;
         l.done = 0;
         l.top_end = 0;
-        l.waiting = l.lock = l.exit = 0;
+        l.waiting = l.lock = l.exit = l.stopc = 0;
+        if constexpr (BAL) {
+            // the workgroup's first chunk
+            l.cq_T[0] = (uint32_t)__hip_atomic_fetch_add(gp(e.d_claim) + (blockIdx.x % e.pools) * kPoolStride,
+                                                        (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            l.cq_have = 1;
+            for (int i = 0; i < kChunkQ; ++i) l.cq_done[i] = 0;
+        }
         if (top > s0) install(kargs(), l, s0, top);
         l.known = top > s0 ? top : s0;
     }
@@ -415,6 +502,139 @@ void k_commit_engine(const EngineK e) {
     uint64_t s = s0;          // the step of the wave's ticket (or the first it may be in)
     uint64_t known = s0;      // descriptors the wave has seen as known
     uint32_t e_prev = 0;      // the workgroup's tickets before step s
+    if constexpr (BAL) {
+        // Balanced: the workgroup takes the tiles of its pool (x = blockIdx % pools) a chunk of
+        // `chunk` tiles at a time through the pool's device ticket counter (zeroed before the
+        // launch): pool ticket T is chunk T - end(s - 1) of the pool's tiles of the first step s
+        // with T < end(s), and every workgroup of the pool computes the same ends from the same
+        // descriptors. Inside the workgroup the waves share the claimed chunks through the LDS
+        // ticket: LDS ticket u is tile u % chunk of the workgroup's chunk u / chunk. The wave
+        // holding the first ticket of chunk q claims chunk q + 1 and publishes it (no wait in
+        // between, so a wave waiting for a chunk never waits on a frontier), while the other
+        // waves decide chunk q. A chunk is counted on its pool's step counter when its last tile
+        // is counted (a tile once its stores are complete: after the wave's next tile's loads
+        // have returned, or at a drain).
+        const uint32_t x = blockIdx.x % e.pools, K = e.chunk;
+        uint64_t *const tickets = gp(e.d_claim) + x * kPoolStride;
+        uint32_t u = claim(l, lane);
+        bool pend = false;
+        uint64_t p_s = 0, p_G = 0;
+        uint32_t p_q = 0, p_n = 0;
+        // the pool count in flight (its add issued, its return not yet looked at)
+        bool c_fly = false;
+        uint64_t c_s = 0, c_G = 0, c_ret = 0;
+        uint32_t c_n = 0;
+        auto settle = [&]() {
+            if (c_fly && lane == 0) pool_settle(kargs(), c_s, c_G, x, c_n, c_ret);
+            c_fly = false;
+        };
+        auto count = [&]() {
+            uint32_t f = 0;
+            if (lane == 0)
+                f = __hip_atomic_fetch_add(&l.cq_done[p_q % kChunkQ], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
+            if (wave_u32(f) == p_n) {           // the chunk's last tile
+                settle();
+                if (lane == 0) {
+                    __hip_atomic_store(&l.cq_done[p_q % kChunkQ], 0u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                    c_ret = pool_add(kargs(), p_s, x, p_n);
+                }
+                c_fly = true;
+                c_s = p_s;
+                c_G = p_G;
+                c_n = p_n;
+            }
+            pend = false;
+        };
+        auto drain = [&]() {
+            if constexpr (SIG) {
+                if (pend) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    count();
+                }
+                settle();
+            }
+        };
+        for (;;) {
+            const uint32_t q = u / K, i = u % K;
+            // chunk q is published by the wave holding the first ticket of chunk q - 1
+            while (before(wave_u32(__hip_atomic_load(&l.cq_have, __ATOMIC_ACQUIRE,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)), q + 1))
+                __builtin_amdgcn_s_sleep(1);
+            const uint32_t T = wave_u32(l.cq_T[q % kChunkQ]);
+            if (i == 0) {
+                uint32_t tn = 0;
+                if (lane == 0) {
+                    tn = (uint32_t)__hip_atomic_fetch_add(tickets, (uint64_t)1, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    l.cq_T[(q + 1) % kChunkQ] = tn;
+                    __hip_atomic_store(&l.cq_have, q + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            // the step of pool ticket T
+            bool out = false;
+            for (;;) {
+                if (s >= known) {
+                    drain();
+                    known = frontier<WPW>(kargs(), l, s, lane);
+                    if (known <= s) {        // idle: the next launch resumes at workgroup 0's step
+                        out = true;
+                        break;
+                    }
+                }
+                const uint64_t *d = reinterpret_cast<const uint64_t *>(l.ring + (s & dmask));
+                if (uniform64(d[6]) & kDescStop) {
+                    // the workgroup arrives at the STOP when its last wave does
+                    drain();
+                    if (lane == 0 && __hip_atomic_fetch_add(&l.stopc, 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP) + 1 == (uint32_t)WPW)
+                        arrive(kargs(), s);
+                    ++s;
+                    out = true;
+                    break;
+                }
+                const uint32_t e_cur = wave_u32(l.end[s & dmask]);
+                if (before(T, e_cur)) break;
+                e_prev = e_cur;
+                ++s;
+                if (wv == 0) refresh(kargs(), l, s, lane);
+            }
+            if (out) break;
+            const uint64_t *d = reinterpret_cast<const uint64_t *>(l.ring + (s & dmask));
+            CommitK k{};
+            k.stride = e.stride;
+            k.R = e.R;
+            k.G = uniform64(d[0]);
+            k.match = as_global<const uint64_t>(uniform64(d[1]));
+            k.cout = as_global<uint64_t>(uniform64(d[2]));
+            k.changed = as_global<uint64_t>(uniform64(d[3]));
+            k.fallback = as_global<uint64_t>(uniform64(d[4]));
+            uint64_t pb, pn;
+            pool_range(k.G, e.pools, x, &pb, &pn);
+            const uint64_t tile0 = pb + (uint64_t)(T - e_prev) * K;
+            const uint32_t n = (uint32_t)(tile0 + K < pb + pn ? K : pb + pn - tile0);
+            if (i < n) {
+                const uint64_t wbase = uniform64((tile0 + i) * HQ_TILE_GROUPS);
+                uint32_t ln;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+                commit_tile<N, FORM, false, LEAD, false, SIG, true>(k, wbase, ln);
+                if constexpr (SIG) {
+                    asm volatile("" ::: "memory");
+                    if (pend) count();
+                    pend = true;
+                    p_s = s;
+                    p_G = k.G;
+                    p_q = q;
+                    p_n = n;
+                }
+            }
+            u = claim(l, lane);
+        }
+        drain();
+        if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
+        return;
+    }
     uint32_t t = claim(l, lane);
     // SIG / INPLACE: a decided tile is counted (fin / done) only once its stores are complete.
     // The count of tile k is taken after tile k + 1's loads have returned (vector memory
@@ -524,21 +744,29 @@ typedef void (*EngineKernel)(const EngineK);
 // 1024-thread workgroups (two per CU) where the tile loop fits 64 VGPRs with no scratch (n <= 5;
 // some n = 7, 8 bodies spill at that size), 512 otherwise
 template <int N, int FORM, int LEAD, bool INPLACE>
-void engine_kernel_for(bool sig, EngineKernel *fn, int *blk) {
+void engine_kernel_for(bool sig, bool bal, EngineKernel *fn, int *blk) {
     constexpr int B = N <= 5 ? 1024 : 512;
-    *fn = sig ? k_commit_engine<N, FORM, LEAD, INPLACE, B, true>
-              : k_commit_engine<N, FORM, LEAD, INPLACE, B, false>;
+    if constexpr (!INPLACE) {
+        if (bal) {
+            *fn = sig ? k_commit_engine<N, FORM, LEAD, false, B, true, true>
+                      : k_commit_engine<N, FORM, LEAD, false, B, false, true>;
+            *blk = B;
+            return;
+        }
+    }
+    *fn = sig ? k_commit_engine<N, FORM, LEAD, INPLACE, B, true, false>
+              : k_commit_engine<N, FORM, LEAD, INPLACE, B, false, false>;
     *blk = B;
 }
 
 template <int N>
-int engine_kernel_n(uint32_t form, uint32_t layout, bool sig, EngineKernel *fn, int *blk) {
+int engine_kernel_n(uint32_t form, uint32_t layout, bool sig, bool bal, EngineKernel *fn, int *blk) {
     const bool lead = (layout & 0xFFu) == HQ_LAYOUT_TILES_LEADER;
     const bool inplace = (layout & HQ_LAYOUT_IN_PLACE) != 0;
 #define HQ_ENGINE_PICK(F)                                                                        \
-    if (inplace) engine_kernel_for<N, F, 1, true>(sig, fn, blk);                                 \
-    else if (lead) engine_kernel_for<N, F, 1, false>(sig, fn, blk);                              \
-    else engine_kernel_for<N, F, 0, false>(sig, fn, blk);
+    if (inplace) engine_kernel_for<N, F, 1, true>(sig, false, fn, blk);                          \
+    else if (lead) engine_kernel_for<N, F, 1, false>(sig, bal, fn, blk);                         \
+    else engine_kernel_for<N, F, 0, false>(sig, bal, fn, blk);
     if (form == HQ_FORM_TERM_MASK) {
         HQ_ENGINE_PICK(HQ_FORM_TERM_MASK)
     } else {
@@ -550,16 +778,17 @@ int engine_kernel_n(uint32_t form, uint32_t layout, bool sig, EngineKernel *fn, 
 
 // sig: per-step completion signals (write-through stores: a step's outputs are visible once its
 // waves' stores have drained)
-int engine_kernel(uint32_t n, uint32_t form, uint32_t layout, bool sig, EngineKernel *fn, int *blk) {
+int engine_kernel(uint32_t n, uint32_t form, uint32_t layout, bool sig, bool bal, EngineKernel *fn,
+                  int *blk) {
     switch (n) {
-    case 1: return engine_kernel_n<1>(form, layout, sig, fn, blk);
-    case 2: return engine_kernel_n<2>(form, layout, sig, fn, blk);
-    case 3: return engine_kernel_n<3>(form, layout, sig, fn, blk);
-    case 4: return engine_kernel_n<4>(form, layout, sig, fn, blk);
-    case 5: return engine_kernel_n<5>(form, layout, sig, fn, blk);
-    case 6: return engine_kernel_n<6>(form, layout, sig, fn, blk);
-    case 7: return engine_kernel_n<7>(form, layout, sig, fn, blk);
-    default: return engine_kernel_n<8>(form, layout, sig, fn, blk);
+    case 1: return engine_kernel_n<1>(form, layout, sig, bal, fn, blk);
+    case 2: return engine_kernel_n<2>(form, layout, sig, bal, fn, blk);
+    case 3: return engine_kernel_n<3>(form, layout, sig, bal, fn, blk);
+    case 4: return engine_kernel_n<4>(form, layout, sig, bal, fn, blk);
+    case 5: return engine_kernel_n<5>(form, layout, sig, bal, fn, blk);
+    case 6: return engine_kernel_n<6>(form, layout, sig, bal, fn, blk);
+    case 7: return engine_kernel_n<7>(form, layout, sig, bal, fn, blk);
+    default: return engine_kernel_n<8>(form, layout, sig, bal, fn, blk);
     }
 }
 
@@ -588,6 +817,8 @@ struct hq_engine {
     uint64_t wait_limit_ms = 60000;   // a wait that sees no completion this long fails (HQ_ENGINE_WAIT_MS)
     size_t cur_off = 0, exit_off = 0, polled_off = 0;   // device state (hq_engine_dump)
     uint64_t inplace_G = 0;      // HQ_LAYOUT_IN_PLACE: the table's G (every post keeps it)
+    bool balanced = false;       // per-XCD tile pools (not with HQ_LAYOUT_IN_PLACE)
+    size_t claim_off = 0;        // the pools' ticket counters (zeroed before each launch)
 };
 
 namespace {
@@ -633,6 +864,10 @@ int launch(hq_engine *e) {
     for (uint64_t i = 0; i < n; ++i) e->k.init[i] = ring[(e->completed + i) & (e->cfg.depth - 1)];
     e->k.epoch = ++e->epoch;
     int rc = echeck(e, hipSetDevice(e->ctx->device), "hipSetDevice");
+    // (balanced: the pools' tickets restart with the launch; the previous launch has ended)
+    if (!rc && e->balanced)
+        rc = echeck(e, hipMemsetAsync(e->dev + e->claim_off, 0, 8 * kPools * kPoolStride, e->stream),
+                    "hipMemsetAsync(engine tickets)");
     if (!rc) rc = echeck(e, hipEventRecord(e->ev_start, e->stream), "hipEventRecord");
     if (rc) return rc;
     hipLaunchKernelGGL(e->fn, dim3(e->grid), dim3(e->block), 0, e->stream, e->k);
@@ -782,7 +1017,7 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     *out = nullptr;
     hq_engine_config c = *cfg;
     if (c.depth == 0) c.depth = kEngineMaxDepth;
-    if (c.idle_us == 0) c.idle_us = 20000;
+    if (c.idle_us == 0) c.idle_us = 1000;     // (the sharing policy)
     if (c.n_max < 1 || c.n_max > HQ_MAX_VOTERS)
         return hq::fail(ctx, HQ_E_INVAL, "hq_engine_open: n_max must be 1..8");
     if (c.form != HQ_FORM_TERM_START && c.form != HQ_FORM_TERM_MASK)
@@ -805,7 +1040,17 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     if (!e) return hq::fail(ctx, HQ_E_NOMEM, "hq_engine_open: out of host memory");
     e->ctx = ctx;
     e->cfg = c;
-    engine_kernel(c.n_max, c.form, c.layout, (c.flags & HQ_ENGINE_SIGNAL) != 0, &e->fn, &e->block);
+    // balanced mode (per-XCD pools of each step's tiles, HQ_ENGINE_BALANCE=1; not with an
+    // in-place table): measured slower than the static ownership on the headline windows at every
+    // chunk size, so it is off unless asked for
+    e->balanced = false;
+    if (const char *b = std::getenv("HQ_ENGINE_BALANCE"))
+        e->balanced = !(c.layout & HQ_LAYOUT_IN_PLACE) && std::atoi(b) != 0;
+    engine_kernel(c.n_max, c.form, c.layout, (c.flags & HQ_ENGINE_SIGNAL) != 0, e->balanced, &e->fn,
+                  &e->block);
+    // tiles per claimed chunk: one per wave of the workgroup unless HQ_ENGINE_CHUNK says
+    uint32_t chunk = (uint32_t)e->block / 64;
+    if (const char *ch = std::getenv("HQ_ENGINE_CHUNK")) chunk = (uint32_t)std::max(1, std::atoi(ch));
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     int cus = 0, per_cu = 0;
     if (!rc) rc = hq::check_hip(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
@@ -828,7 +1073,10 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     const size_t ring_off = (cur_off + 8 * (size_t)e->grid + 127) & ~(size_t)127;
     const size_t exit_off = ring_off + sizeof(EngineDesc) * D;
     const size_t polled_off = exit_off + 256;
-    const size_t dev_bytes = polled_off + 8 * kPollCopies * kPollStride;
+    const size_t claim_off = polled_off + 8 * kPollCopies * kPollStride;
+    const size_t pdone_off = claim_off + 8 * kPools * kPoolStride;
+    const size_t dev_bytes = pdone_off + 8 * kPools * kPoolStride * D;
+    e->claim_off = claim_off;
     e->cur_off = cur_off;
     e->exit_off = exit_off;
     e->polled_off = polled_off;
@@ -865,6 +1113,10 @@ int hq_engine_open(hq_ctx *ctx, const hq_engine_config *cfg, hq_engine **out) {
     k.d_ring = reinterpret_cast<EngineDesc *>(e->dev + ring_off);
     k.d_polled = reinterpret_cast<uint64_t *>(e->dev + polled_off);
     k.d_exit = reinterpret_cast<uint64_t *>(e->dev + exit_off);
+    k.d_claim = reinterpret_cast<uint64_t *>(e->dev + claim_off);
+    k.d_pdone = reinterpret_cast<uint64_t *>(e->dev + pdone_off);
+    k.chunk = e->balanced ? chunk : 0;
+    k.pools = std::min<uint32_t>(e->grid, kPools);
     *out = e;
     return HQ_OK;
 }

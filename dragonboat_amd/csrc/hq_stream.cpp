@@ -108,6 +108,20 @@ inline uint8_t *put_run(uint8_t *p, uint32_t m, From from) {
     return p;
 }
 
+// the 1- and 2-byte varints inline
+__attribute__((always_inline)) inline uint8_t *put_fast(uint8_t *p, uint64_t v) {
+    if (v < 0x80) {
+        *p = (uint8_t)v;
+        return p + 1;
+    }
+    if (v < 0x4000) {
+        p[0] = (uint8_t)(v | 0x80);
+        p[1] = (uint8_t)(v >> 7);
+        return p + 2;
+    }
+    return put(p, v);
+}
+
 // one event; returns the write position
 template <class Ev>
 inline uint8_t *encode(uint8_t *p, const Ev &e, Prev &pv) {
@@ -116,9 +130,9 @@ inline uint8_t *encode(uint8_t *p, const Ev &e, Prev &pv) {
         *p++ = (uint8_t)kind;
         if (kind == HQ_EV_READ) {
             p = put(p, e.hint);
-            p = put(p, e.hint_high);
+            p = put_fast(p, e.hint_high);
         } else if (kind == HQ_EV_PROPOSE) {
-            p = put(p, e.log_index);
+            p = put_fast(p, e.log_index);
         }
         return p;
     }
@@ -137,13 +151,13 @@ inline uint8_t *encode(uint8_t *p, const Ev &e, Prev &pv) {
     pv.last_reject = e.reject ? 1 : 0;
     *p++ = (uint8_t)(HQ_EV_MESSAGE | code << 3 | (e.reject ? 0x40 : 0) | (same ? 0x80 : 0));
     if (code == 7) p = put(p, e.type);
-    p = put(p, e.from);
+    p = put_fast(p, e.from);
     if (!same) p = put(p, e.term);
     pv.term = e.term;
-    if (code == 0 || code == 7) p = put(p, e.log_index);
+    if (code == 0 || code == 7) p = put_fast(p, e.log_index);
     if (code == 2 || code == 3 || code == 7) {
         p = put(p, e.hint);
-        p = put(p, e.hint_high);
+        p = put_fast(p, e.hint_high);
     }
     return p;
 }
@@ -184,20 +198,6 @@ inline int from16(const hq_event16 *r, uint64_t left, uint64_t ctx[2], hq_event 
         }
     }
     return 1;
-}
-
-// the 1- and 2-byte varints inline
-__attribute__((always_inline)) inline uint8_t *put_fast(uint8_t *p, uint64_t v) {
-    if (v < 0x80) {
-        *p = (uint8_t)v;
-        return p + 1;
-    }
-    if (v < 0x4000) {
-        p[0] = (uint8_t)(v | 0x80);
-        p[1] = (uint8_t)(v >> 7);
-        return p + 2;
-    }
-    return put(p, v);
 }
 
 // type_code of the types below 32

@@ -260,7 +260,7 @@ int parse_batch(const uint8_t *bytes, size_t len, hq_wire_batch_info *bi, uint64
 class ClusterIndex {
   public:
     void clear() {
-        for (uint32_t i : used_) keys_[i] = kEmpty;
+        for (uint32_t i : used_) slots_[i].key = kEmpty;
         used_.clear();
         has_empty_ = false;
     }
@@ -270,30 +270,30 @@ class ClusterIndex {
             if (has_empty_) *v = empty_val_;
             return has_empty_;
         }
-        if (keys_.empty()) return false;
-        const uint64_t mask = keys_.size() - 1;
+        if (slots_.empty()) return false;
+        const uint64_t mask = slots_.size() - 1;
         for (uint64_t i = hash(id) & mask;; i = (i + 1) & mask) {
-            if (keys_[i] == id) {
-                *v = vals_[i];
+            if (slots_[i].key == id) {
+                *v = slots_[i].val;
                 return true;
             }
-            if (keys_[i] == kEmpty) return false;
+            if (slots_[i].key == kEmpty) return false;
         }
     }
     void prefetch(uint64_t id) const {
-        if (!keys_.empty()) __builtin_prefetch(&keys_[hash(id) & (keys_.size() - 1)]);
+        if (!slots_.empty()) __builtin_prefetch(&slots_[hash(id) & (slots_.size() - 1)]);
     }
     size_t size() const { return used_.size() + has_empty_; }
     // the index of id, inserting next if new (*fresh = true)
     uint32_t find_or_add(uint64_t id, uint32_t next, bool *fresh) {
-        if ((used_.size() + 1) * 2 > keys_.size()) rehash(keys_.empty() ? 1024 : keys_.size() * 2);
-        const uint64_t mask = keys_.size() - 1;
+        if ((used_.size() + 1) * 2 > slots_.size()) rehash(slots_.empty() ? 1024 : slots_.size() * 2);
+        const uint64_t mask = slots_.size() - 1;
         for (uint64_t i = hash(id) & mask;; i = (i + 1) & mask) {
-            if (keys_[i] == id && id != kEmpty) {
+            if (slots_[i].key == id && id != kEmpty) {
                 *fresh = false;
-                return vals_[i];
+                return slots_[i].val;
             }
-            if (keys_[i] == kEmpty) {
+            if (slots_[i].key == kEmpty) {
                 if (id == kEmpty) {                   // the one key the table cannot hold
                     if (!has_empty_) {
                         has_empty_ = true;
@@ -304,8 +304,8 @@ class ClusterIndex {
                     *fresh = false;
                     return empty_val_;
                 }
-                keys_[i] = id;
-                vals_[i] = next;
+                slots_[i].key = id;
+                slots_[i].val = next;
                 used_.push_back((uint32_t)i);
                 *fresh = true;
                 return next;
@@ -319,25 +319,26 @@ class ClusterIndex {
         x *= 0xff51afd7ed558ccdull;
         return x ^ (x >> 33);
     }
+    // key and value side by side: a lookup touches one 16-byte slot
+    struct Slot {
+        uint64_t key;
+        uint32_t val, pad;
+    };
     void rehash(size_t cap) {
-        std::vector<uint64_t> k(cap, kEmpty);
-        std::vector<uint32_t> v(cap);
+        std::vector<Slot> k(cap, Slot{kEmpty, 0, 0});
         std::vector<uint32_t> u;
         u.reserve(used_.size());
         for (uint32_t i : used_) {
-            const uint64_t id = keys_[i];
+            const uint64_t id = slots_[i].key;
             uint64_t j = hash(id) & (cap - 1);
-            while (k[j] != kEmpty) j = (j + 1) & (cap - 1);
-            k[j] = id;
-            v[j] = vals_[i];
+            while (k[j].key != kEmpty) j = (j + 1) & (cap - 1);
+            k[j] = slots_[i];
             u.push_back((uint32_t)j);
         }
-        keys_.swap(k);
-        vals_.swap(v);
+        slots_.swap(k);
         used_.swap(u);
     }
-    std::vector<uint64_t> keys_;
-    std::vector<uint32_t> vals_;
+    std::vector<Slot> slots_;
     std::vector<uint32_t> used_;
     bool has_empty_ = false;
     uint32_t empty_val_ = 0;
@@ -365,6 +366,20 @@ struct hq_wire {
     std::vector<uint64_t> boffsets;    // hq_wire_step_stream
     std::vector<uint8_t> bytes;
     std::vector<uint32_t> cnt, perm, pos;   // hq_wire_step_sized's counting sort
+    std::vector<uint32_t> kcnt;        // attached: the records queued per handle (at h + 1)
+
+    void count_key(uint32_t k) {
+        if ((size_t)k + 2 > kcnt.size()) kcnt.resize(std::max<size_t>((size_t)k + 2, 2 * kcnt.size()), 0);
+        kcnt[(size_t)k + 1]++;
+    }
+    static constexpr uint32_t kNoKey = UINT32_MAX;   // a record of a cluster the worker does not run
+    // records r0.. leave the queue (a batch dropped after its decode)
+    void drop_from(size_t r0) {
+        if (worker)
+            for (size_t i = r0; i < recs.size(); ++i)
+                if (recs[i].key != kNoKey) kcnt[(size_t)recs[i].key + 1]--;
+        recs.resize(r0);
+    }
     std::vector<Rec> grp;              //   and one group's events
 
     int fail(int code, const std::string &m) {
@@ -513,12 +528,14 @@ int hq_wire_attach(hq_wire *w, hq_worker *worker) {
     if (!w->recs.empty()) return w->fail(HQ_E_STATE, "hq_wire_attach: events queued (reset first)");
     w->worker = worker;
     w->handle_of = ClusterIndex();
+    w->kcnt.clear();
     return HQ_OK;
 }
 
 int hq_wire_reset(hq_wire *w) {
     if (!w) return HQ_E_INVAL;
     w->recs.clear();
+    std::fill(w->kcnt.begin(), w->kcnt.end(), 0u);
     w->clusters.clear();
     w->cluster_index.clear();
     w->stats = hq_wire_stats{};
@@ -565,6 +582,7 @@ int hq_wire_add_locals(hq_wire *w, uint64_t n, const uint64_t *cluster_ids, cons
             r.hint = e.hint;
             r.hint_high = e.hint_high;
             w->recs.push_back(r);
+            if (w->worker) w->count_key(k);
         }
     }
     return HQ_OK;
@@ -579,7 +597,25 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
     // and their clusters are resolved to keys
     const size_t r0 = w->recs.size();
     w->pending.clear();
-    uint64_t entries = 0, snap = 0;
+    uint64_t entries = 0, snap = 0, no_cluster = 0;
+    // attached: each record's key (the worker's handle) looked up while the batch decodes, kAhead
+    // messages behind the decode (the handle table's slot prefetched when the message is decoded;
+    // a batch the deployment check drops afterwards only leaves its clusters' handles cached);
+    // else the keys wait for that check (an index of first appearance must not see a dropped
+    // batch)
+    const bool now = w->worker != nullptr;
+    constexpr size_t kAhead = 8;
+    size_t looked = 0;
+    auto look_up = [&]() {
+        Rec &x = w->recs[r0 + looked];
+        const uint64_t id = w->pending[looked++];
+        if (w->handle_of.find(id, &x.key) || w->key(id, &x.key)) {
+            w->count_key(x.key);
+        } else {
+            x.key = hq_wire::kNoKey;
+            ++no_cluster;
+        }
+    };
     std::string err;
     hq_wire_batch_info bi;
     uint64_t n = 0;
@@ -614,10 +650,23 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
         r.cat = 1;
         w->recs.push_back(r);
         w->pending.push_back(cid);
+        if (now) {
+            w->handle_of.prefetch(cid);
+            if (w->pending.size() - looked > kAhead) look_up();
+        }
         return HQ_OK;
     });
+    if (now) {
+        while (looked < w->pending.size()) look_up();
+        if (no_cluster && !rc) {       // the records of clusters the worker does not run leave
+            size_t o = r0;
+            for (size_t i = r0; i < w->recs.size(); ++i)
+                if (w->recs[i].key != hq_wire::kNoKey) w->recs[o++] = w->recs[i];
+            w->recs.resize(o);
+        }
+    }
     if (rc) {
-        w->recs.resize(r0);
+        w->drop_from(r0);
         return w->fail(HQ_E_INVAL, "hq_wire_add_batch: malformed MessageBatch" +
                                        (err.empty() ? std::string() : ": " + err));
     }
@@ -626,7 +675,7 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
     // Transport.handleRequest (transport.go:289-300): the whole batch is dropped on a foreign
     // deployment id or binary version (none of its clusters is looked at)
     if (bi.deployment_id != w->deployment_id || bi.bin_ver != HQ_RPC_BIN_VERSION) {
-        w->recs.resize(r0);
+        w->drop_from(r0);
         w->stats.dropped_batches++;
         w->stats.dropped_messages += n;
         return HQ_OK;
@@ -634,7 +683,8 @@ int hq_wire_add_batch(hq_wire *w, const uint8_t *bytes, size_t len) {
     w->stats.messages += n;
     w->stats.entries += entries;
     w->stats.snapshot_received += snap;
-    w->resolve(r0);
+    w->stats.dropped_no_cluster += no_cluster;
+    if (!now) w->resolve(r0);
     return HQ_OK;
 }
 
@@ -711,9 +761,12 @@ int hq_wire_step_sized(hq_wire *w, uint8_t *bytes, uint64_t cap, uint16_t *sizes
     // then taken category by category (node.handleEvents: local ReadIndex, received messages,
     // ticks, proposals)
     const uint32_t nr = (uint32_t)w->recs.size();
+    // (the counts per handle were kept as the records were queued; handles only grow, so every
+    // queued key is below n)
     w->cnt.assign(n + 1, 0);
-    for (const Rec &r : w->recs) w->cnt[r.key + 1]++;
+    std::copy(w->kcnt.begin(), w->kcnt.begin() + std::min<size_t>(w->kcnt.size(), n + 1), w->cnt.begin());
     for (uint64_t h = 0; h < n; ++h) w->cnt[h + 1] += w->cnt[h];
+    if (w->cnt[n] != nr) return w->fail(HQ_E_STATE, "hq_wire_step_sized: a queued record's handle is past the worker's groups");
     w->perm.resize(nr);
     w->pos.assign(w->cnt.begin(), w->cnt.end() - 1);
     for (uint32_t i = 0; i < nr; ++i) w->perm[w->pos[w->recs[i].key]++] = i;

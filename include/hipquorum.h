@@ -304,7 +304,7 @@ typedef struct hq_engine_config {
     uint32_t ring_len;       /* mask form: R (power of two <= 16); unused for term-start */
     uint32_t depth;          /* posted steps in flight: power of two 2..64 (0 = 64) */
     uint32_t flags;          /* HQ_ENGINE_SIGNAL */
-    uint32_t idle_us;        /* polling time without a post before the resident launch ends (0 = 20000) */
+    uint32_t idle_us;        /* polling time without a post before the resident launch ends (0 = 1000) */
     uint32_t max_workgroups; /* cap on the resident grid (0 = every CU at full occupancy) */
 } hq_engine_config;
 typedef struct hq_engine_stats {

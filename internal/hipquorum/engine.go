@@ -25,7 +25,7 @@ type EngineConfig struct {
 	InPlace bool // batches are device-resident tables decided in place (every post keeps one G)
 	Signal  bool // per-step completion (Wait returns when that step is done)
 	Depth   int  // steps in flight (power of two 2..64; 0 = 64)
-	IdleUs  int  // polling time without a post before the resident launch ends (0 = 20 ms)
+	IdleUs  int  // polling time without a post before the resident launch ends (0 = 1 ms)
 }
 
 // OpenEngine opens the engine on the context's GPU (leader-row tiles, term-mask form).

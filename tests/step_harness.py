@@ -278,6 +278,15 @@ class WireBackend(WorkerBackend):
             wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT, source_address=b"n2:1"))
             if i == 0:   # a foreign deployment's batch: dropped whole (transport.go:291-295)
                 wire.add_batch(we.batch(p, deployment_id=self.DEPLOYMENT + 1))
+                if p:    # a truncated batch: rejected, none of its messages queued
+                    b = we.batch(p, deployment_id=self.DEPLOYMENT, source_address=b"n2:1")
+                    tail = len(we.batch([], deployment_id=self.DEPLOYMENT, source_address=b"n2:1"))
+                    try:       # (the last message one byte short of its length)
+                        wire.add_batch(b[:len(b) - tail - 1])
+                    except hq.HQError:
+                        pass
+                    else:
+                        raise AssertionError("a truncated MessageBatch was accepted")
         if self.attached:
             # every handle in order (a group without events has size 0); handles are the order
             # the groups were added in

@@ -94,3 +94,22 @@ def test_wake_lag_from_clocks():
     lags = [p["dev_wake_lag_ms"] for p in ph]
     assert lags[:4] == pytest.approx([0.02, 0.0, 1.99, 0.0]) and lags[4] is None
     assert all("dev__end_ns" not in p for p in ph)
+
+
+def test_link_block_bytes():
+    """The step legs' link roofline: output bytes counted from the results (slots by records and
+    count words), rates over the GPU time, frac against the probe's both-ways total."""
+    rs = [{"committed_advance": np.zeros(600, np.uint32),
+           "ready_compact": np.zeros(5, hq.READY_COMPACT_DTYPE),
+           "ready_slots": np.zeros(40, hq.READY_COMPACT_DTYPE), "gpu_ns": 7}]
+    assert bench._out_bytes(rs) == 600 * 4 + 5 * 24 + 40 * 24 + 4 * 3
+
+    class D:
+        rank, device = 1, 0
+    bench._LINK["v"] = {"read_GBps": 50.0, "write_GBps": 40.0, "both_GBps": 80.0}
+    try:
+        b = bench._link_block(D(), 40e6, 10e6, 1.0)
+    finally:
+        bench._LINK.clear()
+    assert b["both_GBps"] == 50.0 and b["frac"] == 0.625
+    assert b["frac_serial"] == pytest.approx((40e6 / 50e9 + 10e6 / 40e9) / 1e-3, abs=1e-3)

@@ -2,11 +2,13 @@
 // place (the device step's zero-copy pass A reads, k_step_lite's ReadyToRead writes): one
 // direction at a time and both at once (two kernels on two streams). Build:
 //   hipcc -O3 --offload-arch=gfx950 -o tools/link_probe tools/link_probe.cpp
-// Run: tools/link_probe [MiB per direction, default 64]
+// Run: tools/link_probe [MiB per direction, default 64] [device] [--json]
+// --json: one line, the best of the grids per figure (bench.py's step legs read it)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #define CHECK(x)                                                                         \
     do {                                                                                 \
@@ -33,6 +35,10 @@ __global__ __launch_bounds__(256) void k_write(uint4 *dst, size_t n, unsigned ta
 
 int main(int argc, char **argv) {
     const size_t mib = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 64;
+    const int device = argc > 2 ? std::atoi(argv[2]) : 0;
+    const bool json = argc > 3 && std::string(argv[3]) == "--json";
+    CHECK(hipSetDevice(device));
+    double top[5] = {0, 0, 0, 0, 0};   // read, write, read and write together, their sum
     const size_t bytes = mib << 20, n = bytes / 16;
     void *hr = nullptr, *hw = nullptr;
     unsigned *sink = nullptr;
@@ -80,11 +86,18 @@ int main(int argc, char **argv) {
             }
         }
         const double gb = bytes / 1e9;
-        std::printf("grid %5u x 256: read %.1f GB/s, write %.1f GB/s; together read %.1f GB/s "
+        const double f[5] = {gb / (best_r * 1e-3), gb / (best_w * 1e-3), gb / (best_rb * 1e-3),
+                             gb / (best_wb * 1e-3), gb / (best_rb * 1e-3) + gb / (best_wb * 1e-3)};
+        for (int i = 0; i < 5; ++i) top[i] = f[i] > top[i] ? f[i] : top[i];
+        if (!json) std::printf("grid %5u x 256: read %.1f GB/s, write %.1f GB/s; together read %.1f GB/s "
                     "+ write %.1f GB/s (%.0f / %.0f us for %zu MiB each)\n",
                     grid, gb / (best_r * 1e-3), gb / (best_w * 1e-3), gb / (best_rb * 1e-3),
                     gb / (best_wb * 1e-3), best_rb * 1e3, best_wb * 1e3, mib);
     }
+    if (json)
+        std::printf("{\"read_GBps\": %.2f, \"write_GBps\": %.2f, \"both_read_GBps\": %.2f, "
+                    "\"both_write_GBps\": %.2f, \"both_GBps\": %.2f, \"MiB\": %zu}\n",
+                    top[0], top[1], top[2], top[3], top[4], mib);
     CHECK(hipHostFree(hr));
     CHECK(hipHostFree(hw));
     CHECK(hipFree(sink));
