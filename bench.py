@@ -1606,7 +1606,8 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     enc_threads = encode_threads()
     # the step thread's wait (hq_worker_set_wait; BENCH_STEP_WAIT=block|sleep|spin[:poll:sleep])
     wait_name, *wv = os.environ.get("BENCH_STEP_WAIT", STEP_WAIT_DEFAULT).split(":")
-    wait = ({"block": hq.HQ_WAIT_BLOCK, "sleep": hq.HQ_WAIT_SLEEP, "spin": hq.HQ_WAIT_SPIN}[wait_name],
+    wait = ({"block": hq.HQ_WAIT_BLOCK, "sleep": hq.HQ_WAIT_SLEEP, "spin": hq.HQ_WAIT_SPIN,
+             "adapt": hq.HQ_WAIT_ADAPT}[wait_name],
             int(wv[0]) if wv else 50, int(wv[1]) if len(wv) > 1 else 20)
     pin = hq.Context(d.device)
     Ws = (1, 2, 16)

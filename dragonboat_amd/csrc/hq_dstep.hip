@@ -206,18 +206,19 @@ __device__ __forceinline__ bool dvar(ByteReader &r, uint64_t &v) {
 // a group's stream state the codes refer back to (hq_stream.cpp's Prev): its previous message
 // term, its previous ReplicateResp's log_index (code 4), its previous HeartbeatResp's ctx (code
 // 5), the previous message a run repeats (code 6; last 1 ReplicateResp, 2 HeartbeatResp, bit 2
-// its reject) and the run's events still to come
+// its reject, bit 3 a run in the consecutive form) and the run's events still to come (and, in
+// the consecutive form, the next member's sender)
 struct DPrev {
     uint64_t term = 0, index = 0, hint = 0, high = 0;
     bool have_index = false;
-    uint32_t last = 0, run = 0;
+    uint32_t last = 0, run = 0, run_from = 0;
 };
 
 // one event of a group's stream
 __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
     v = hq_event{};
-    if (!r.more()) return false;
     if (pv.run == 0) {
+        if (!r.more()) return false;
         // (peek: a run header is taken here, any other header below)
         const uintptr_t a = reinterpret_cast<uintptr_t>(r.p);
         if ((a & ~uintptr_t(7)) != r.wa) {
@@ -230,6 +231,13 @@ __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
             uint64_t m;
             if (!(pv.last & 3) || !dvar(r, m) || m == 0 || m > 0xFFFF) return false;
             pv.run = (uint32_t)m;
+            pv.last &= 7u;
+            if (h0 & 0x80) {       // the consecutive form: the first sender, the rest follow
+                uint64_t f0;
+                if (!dvar(r, f0) || f0 + m > 0xFFFFFFFFull) return false;
+                pv.run_from = (uint32_t)f0;
+                pv.last |= 8u;
+            }
         }
     }
     if (pv.run) {                  // a run member: the previous message with another sender
@@ -243,6 +251,10 @@ __device__ bool decode_event(ByteReader &r, DPrev &pv, hq_event &v) {
         } else {
             v.hint = pv.hint;
             v.hint_high = pv.high;
+        }
+        if (pv.last & 8u) {
+            v.from = pv.run_from++;
+            return true;
         }
         return dvar(r, v.from);
     }
@@ -1608,6 +1620,7 @@ struct hq_dstep {
     // the last wait: the device's 100-MHz stamp after the step's last kernel (HQ_WAIT_CLOCK), in
     // pinned memory
     uint32_t wait_mode = HQ_WAIT_BLOCK, wait_poll_us = 50, wait_sleep_us = 20;
+    uint64_t wait_pred_ns = 0;    // HQ_WAIT_ADAPT: the last step's wait, start to seen done
     bool wait_clock = false;
     uint64_t *clock_host = nullptr;
     hq_wait_clock last_wait{};
@@ -1645,6 +1658,10 @@ namespace {
 //                  timer wake-up: its lateness is bounded by the timer's slack, not by the
 //                  runtime's interrupt path)
 //   HQ_WAIT_SPIN   poll with yields until done (a core held for the step)
+//   HQ_WAIT_ADAPT  one timed sleep until max(poll_us, 100) before the end the last step's wait
+//                  predicts (its length from the wait's start to the step seen done), then poll
+//                  with yields: a spinning wait's lateness for ~100 us of a core per step; past
+//                  twice the prediction (+ 1 ms) it sleeps on the blocking-sync event
 // With HQ_WAIT_CLOCK a one-thread kernel behind the step writes the device's constant clock into
 // pinned memory: the step's end on the device's clock, against which the host's wake-up is read
 __global__ void k_clock_stamp(uint64_t *dst) {
@@ -1672,6 +1689,34 @@ int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us =
         if (d->wait_clock && !r) wc.device_end_ticks = d->clock_host[0];
         return r;
     };
+    if (mode == HQ_WAIT_ADAPT && d->wait_pred_ns) {
+        const uint64_t pred = d->wait_pred_ns;
+        const uint64_t margin = (uint64_t)std::max<uint32_t>(poll_us, 100) * 1000;
+        if (pred > margin) {
+            std::this_thread::sleep_for(std::chrono::nanoseconds(pred - margin));
+            wc.sleeps = 1;
+            wc.sleep_ns = now_ns() - t0;
+        }
+        const uint64_t t1 = now_ns();
+        for (uint32_t k = 0;; ++k) {
+            const hipError_t q = hipEventQuery(d->ev_sync);
+            if (q == hipSuccess) {
+                wc.poll_ns = now_ns() - t1;
+                d->wait_pred_ns = now_ns() - t0;
+                return done(HQ_OK);
+            }
+            if (q != hipErrorNotReady) return done(hq::check_hip(ctx, q, what));
+            if (now_ns() - t0 > 2 * pred + 1000000) break;    // far past the prediction
+            if ((k & 15) == 15) std::this_thread::yield();
+        }
+        const uint64_t t2 = now_ns();
+        wc.poll_ns = t2 - t1;
+        ++wc.sleeps;
+        rc = hq::check_hip(ctx, hipEventSynchronize(d->ev_sync), what);
+        wc.sleep_ns += now_ns() - t2;
+        if (!rc) d->wait_pred_ns = now_ns() - t0;
+        return done(rc);
+    }
     for (uint32_t k = 0;; ++k) {
         const hipError_t q = hipEventQuery(d->ev_sync);
         if (q == hipSuccess) {
@@ -1698,6 +1743,7 @@ int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us =
     wc.sleeps = 1;
     rc = hq::check_hip(ctx, hipEventSynchronize(d->ev_sync), what);
     wc.sleep_ns = now_ns() - t1;
+    if (!rc) d->wait_pred_ns = now_ns() - t0;   // (HQ_WAIT_ADAPT's first step)
     return done(rc);
 }
 
@@ -1705,7 +1751,8 @@ int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us =
 
 int hq_dstep_set_wait(hq_dstep *d, uint32_t mode, uint32_t poll_us, uint32_t sleep_us) {
     const uint32_t m = mode & ~HQ_WAIT_CLOCK;
-    if (m != HQ_WAIT_BLOCK && m != HQ_WAIT_SLEEP && m != HQ_WAIT_SPIN) return HQ_E_INVAL;
+    if (m != HQ_WAIT_BLOCK && m != HQ_WAIT_SLEEP && m != HQ_WAIT_SPIN && m != HQ_WAIT_ADAPT)
+        return HQ_E_INVAL;
     if (m == HQ_WAIT_SLEEP && sleep_us == 0) return HQ_E_INVAL;
     if ((mode & HQ_WAIT_CLOCK) && !d->clock_host) {
         int rc = hq::check_hip(d->ctx, hipHostMalloc(&d->clock_host, 64, hipHostMallocDefault),

@@ -70,6 +70,8 @@ struct Prev {
     uint64_t term = 0, index = 0, hint = 0, high = 0;
     bool have_index = false;
     uint8_t last = 0, last_reject = 0;
+    bool run_seq = false;          // (decoder) the current run's senders are run_from, + 1, ..
+    uint32_t run_from = 0;
 };
 
 // Runs (code 6): the acks of a steady leader's followers repeat one another but for the sender
@@ -95,9 +97,20 @@ inline bool repeats(const Ev &e, const Prev &pv) {
     return e.type == HQ_MSG_HEARTBEAT_RESP && e.hint == pv.hint && e.hint_high == pv.high;
 }
 
-// a run of m messages repeating the previous one, senders from[0..m)
+// a run of m messages repeating the previous one, senders from[0..m); senders s0, s0 + 1, ..
+// (a leader's followers acking in node order) as the consecutive form: header bit 7, m, s0
 template <class From>
 inline uint8_t *put_run(uint8_t *p, uint32_t m, From from) {
+    const uint64_t f0 = from(0);
+    bool seq = f0 + m <= 0xFFFFFFFFull;
+    for (uint32_t j = 1; j < m && seq; ++j) seq = from(j) == f0 + j;
+    if (seq) {
+        *p++ = (uint8_t)(HQ_EV_MESSAGE | kCodeRun << 3 | 0x80);
+        *p++ = (uint8_t)m;
+        if (f0 < 0x80) *p++ = (uint8_t)f0;
+        else p = put(p, f0);
+        return p;
+    }
     *p++ = (uint8_t)(HQ_EV_MESSAGE | kCodeRun << 3);
     *p++ = (uint8_t)m;                  // m <= kRunMax: one byte
     for (uint32_t j = 0; j < m; ++j) {
@@ -546,6 +559,12 @@ bool decode_one(const uint8_t *&p, const uint8_t *end, Prev &pv, uint64_t &run_l
         if (!run_left) {
             ++p;
             if (!pv.last || !get(p, end, run_left) || run_left == 0) return false;
+            pv.run_seq = (h & 0x80) != 0;
+            if (pv.run_seq) {          // the consecutive form: the first sender, the rest follow
+                uint64_t f0;
+                if (!get(p, end, f0) || f0 + run_left > 0xFFFFFFFFull) return false;
+                pv.run_from = (uint32_t)f0;
+            }
         }
         --run_left;
         v.kind = HQ_EV_MESSAGE;
@@ -557,6 +576,10 @@ bool decode_one(const uint8_t *&p, const uint8_t *end, Prev &pv, uint64_t &run_l
         } else {
             v.hint = pv.hint;
             v.hint_high = pv.high;
+        }
+        if (pv.run_seq) {
+            v.from = pv.run_from++;
+            return true;
         }
         return get(p, end, v.from);
     }

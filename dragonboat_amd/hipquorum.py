@@ -45,6 +45,7 @@ HQ_WORKER_COMMIT_ADVANCE = 4  # with it: commits as 4-byte advances when > 1/4 o
 HQ_WORKER_READY_COMPACT = 8  # with it: ReadyToReads as 24-byte records (position, delta, ctx)
 HQ_WORKER_READY_SLOTS = 16   # with it (+ COMMIT_ADVANCE): single ReadyToReads in per-tile slots
 HQ_WAIT_BLOCK, HQ_WAIT_SLEEP, HQ_WAIT_SPIN, HQ_WAIT_CLOCK = 0, 1, 2, 0x100   # hq_worker_set_wait
+HQ_WAIT_ADAPT = 3
 SLOT_TILE = 256              # groups per ReadyToRead slot tile
 HQ_ABI_VERSION = 21
 HQ_ENGINE_SIGNAL = 1         # hq_engine_config.flags: per-step completion flags

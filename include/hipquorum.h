@@ -291,8 +291,11 @@ int hq_commit_fused_dev(hq_ctx *ctx, const hq_commit_args *args, uint32_t count)
  *
  * The engine has its own HIP stream and holds every CU of the GPU while it is resident (kernels
  * on other streams wait for it): hq_engine_drain() ends the resident launch, the next post
- * starts it again. A resident launch also ends by itself after idle_us without a post (every
- * spin is bounded); steps posted meanwhile are run by a relaunch from hq_engine_wait().
+ * starts it again. A resident launch also ends by itself after idle_us without a post (1 ms by
+ * default; every spin is bounded); steps posted meanwhile are run by a relaunch from
+ * hq_engine_wait(). Engines of several processes on one GPU: give each max_workgroups = the
+ * full grid / the processes, so that every grid is resident at once (a grid partly resident
+ * beside another waits for its missing workgroups until one of them exits idle).
  */
 #define HQ_ENGINE_SIGNAL 1u   /* per-step completion: hq_engine_wait(seq) returns as soon as step
                                  seq is done (else wait = drain: the steps complete as a whole) */
@@ -1074,12 +1077,16 @@ int hq_worker_step(hq_worker *w, const hq_step_input *in, hq_step_output *out);
  *   HQ_WAIT_SLEEP  poll for poll_us, then check every sleep_us microseconds, asleep in between
  *                  (a timer wake-up)
  *   HQ_WAIT_SPIN   poll (yielding) until the step is done: one host core per waiting worker
+ *   HQ_WAIT_ADAPT  sleep once until poll_us (at least 100) before the end the previous step's wait
+ *                  predicts, then poll (yielding); a step running past twice the prediction
+ *                  sleeps on the blocking-sync event (the first step waits as HQ_WAIT_BLOCK)
  * | HQ_WAIT_CLOCK: a one-thread kernel behind each step stamps the device's constant clock
  *   (hq_step_output.device_end_ticks). The jobs path (hq_worker_step_jobs) waits with the first
  *   job's worker's policy. HQ_E_INVAL for a host worker or an unknown mode. */
 #define HQ_WAIT_BLOCK 0u
 #define HQ_WAIT_SLEEP 1u
 #define HQ_WAIT_SPIN  2u
+#define HQ_WAIT_ADAPT 3u
 #define HQ_WAIT_CLOCK 0x100u
 int hq_worker_set_wait(hq_worker *w, uint32_t mode, uint32_t poll_us, uint32_t sleep_us);
 
@@ -1107,8 +1114,11 @@ int hq_worker_set_wait(hq_worker *w, uint32_t mode, uint32_t poll_us, uint32_t s
  *                     repeat the group's previous message — a ReplicateResp or HeartbeatResp
  *                     written with codes 0 / 4 / 2 / 5 or in a run: its type, term, reject and
  *                     log_index / ctx — with other senders; a varint m >= 1, then m sender
- *                     varints (bits 6-7 of a run's header are 0). The acks of a steady leader's
- *                     followers come as runs: 2 + m bytes for m one-byte senders instead of 2 m.
+ *                     varints (bit 6 of a run's header is 0; bit 7 0). Bit 7 set (ABI 21): the
+ *                     consecutive form, senders s0, s0 + 1, .., s0 + m - 1 — a varint m, then s0
+ *                     alone (s0 + m < 2^32). The acks of a steady leader's followers come as
+ *                     runs: 2 + m bytes for m one-byte senders instead of 2 m, 3 bytes when the
+ *                     followers' node ids are consecutive.
  *                     The encoders write a run for 3 to 6 such events (6: a run with 10-byte
  *                     senders still fits HQ_EVENT_STREAM_MAX)
  *           bit 6     reject

@@ -75,7 +75,7 @@ func (x *Worker) err(rc C.int) error {
 
 // Close frees the worker.
 // SetWait sets how the worker's goroutine waits for its device step (hq_worker_set_wait:
-// C.HQ_WAIT_BLOCK / C.HQ_WAIT_SLEEP / C.HQ_WAIT_SPIN, | C.HQ_WAIT_CLOCK).
+// C.HQ_WAIT_BLOCK / C.HQ_WAIT_SLEEP / C.HQ_WAIT_SPIN / C.HQ_WAIT_ADAPT, | C.HQ_WAIT_CLOCK).
 func (x *Worker) SetWait(mode, pollUs, sleepUs uint32) error {
 	return x.err(C.hq_worker_set_wait(x.w, C.uint32_t(mode), C.uint32_t(pollUs), C.uint32_t(sleepUs)))
 }

@@ -100,8 +100,9 @@ int main(void) {
   F(hq_step_output, wait_sleeps) F(hq_step_output, wait_end_ns) F(hq_step_output, device_end_ticks)
   F(hq_step_output, ready_slots) F(hq_step_output, n_ready_slotted)
   F(hq_step_stream, sizes16) F(hq_encode16_job, sizes16)
-  printf("wait_modes %u,%u,%u,%u\nready_slots_flag %u\n", (unsigned)HQ_WAIT_BLOCK,
+  printf("wait_modes %u,%u,%u,%u,%u\nready_slots_flag %u\n", (unsigned)HQ_WAIT_BLOCK,
          (unsigned)HQ_WAIT_SLEEP, (unsigned)HQ_WAIT_SPIN, (unsigned)HQ_WAIT_CLOCK,
+         (unsigned)HQ_WAIT_ADAPT,
          (unsigned)HQ_WORKER_READY_SLOTS);
   return 0;
 }
@@ -137,7 +138,7 @@ def test_struct_layout_matches_c(hq, tmp_path):
         for f in [k for k in c if k.startswith(t + ".")]:
             assert int(c[f]) == getattr(py, f.split(".", 1)[1]).offset, f
     assert c["wait_modes"] == ",".join(map(str, (hq.HQ_WAIT_BLOCK, hq.HQ_WAIT_SLEEP, hq.HQ_WAIT_SPIN,
-                                                 hq.HQ_WAIT_CLOCK)))
+                                                 hq.HQ_WAIT_CLOCK, hq.HQ_WAIT_ADAPT)))
     assert int(c["ready_slots_flag"]) == hq.HQ_WORKER_READY_SLOTS
     assert int(c["grouped"]) == hq.HQ_INGEST_GROUPED
     for name, dt in dtypes.items():

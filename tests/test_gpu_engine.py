@@ -4,6 +4,7 @@ to the oracle (the first test re-checks that anchor through the engine). Covers 
 both served term forms, the three served layouts (leader-row tiles, tiles, the in-place table),
 ragged and empty batches, the ring wrapping many times, per-step completion signals with device
 clocks, an idle exit followed by a relaunch, and several threads posting into one engine."""
+import os
 import threading
 import time
 
@@ -112,7 +113,10 @@ def test_engine_ring_wraps(gpu_ctx, hq, signal):
             for q in seqs[-4:]:
                 eng.wait(q)
             clocks = [eng.done_clock(q) for q in seqs[-4:]]
-            assert clocks == sorted(clocks)
+            # (static ownership completes steps in post order; the balanced mode's pools can
+            # finish an older step after a newer one, each step's flag still its own)
+            if os.environ.get("HQ_ENGINE_BALANCE", "0") == "0":
+                assert clocks == sorted(clocks)
         eng.drain()
     for b, w in zip(bufs, want):
         for x, y in zip(outputs(gpu_ctx, b), w):

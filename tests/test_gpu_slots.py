@@ -273,7 +273,7 @@ def test_sizes16_rejects_bad_input(hq, where):
         pin.close()
 
 
-@pytest.mark.parametrize("mode", ["block", "sleep", "spin"])
+@pytest.mark.parametrize("mode", ["block", "sleep", "spin", "adapt"])
 def test_wait_policies_same_results(hq, mode):
     """Every wait policy steps the same: outputs equal, the wait's clock filled in (a blocking
     wait is one sleep), the device's end stamp taken with HQ_WAIT_CLOCK."""
@@ -283,7 +283,8 @@ def test_wait_policies_same_results(hq, mode):
     roles = bench.STEP_ROLES["step"]
     g, m, cids = bench.step_groups(hq, G, 1, 1, roles)
     nv = sum(r != "observer" for r in roles)
-    code = {"block": hq.HQ_WAIT_BLOCK, "sleep": hq.HQ_WAIT_SLEEP, "spin": hq.HQ_WAIT_SPIN}[mode]
+    code = {"block": hq.HQ_WAIT_BLOCK, "sleep": hq.HQ_WAIT_SLEEP, "spin": hq.HQ_WAIT_SPIN,
+            "adapt": hq.HQ_WAIT_ADAPT}[mode]
     a = hq.Worker(0, nv, on_device=True, commit_advance=True)
     b = hq.Worker(0, nv, on_device=True, commit_advance=True)
     pin = hq.Context(0)
@@ -305,8 +306,8 @@ def test_wait_policies_same_results(hq, mode):
             assert want["device_end_ticks"] == 0
             if mode == "spin":
                 assert got["wait_sleeps"] == 0 and got["wait_sleep_ns"] == 0
-            elif mode == "block":
-                assert got["wait_sleeps"] in (0, 1)
+            elif mode in ("block", "adapt"):
+                assert got["wait_sleeps"] in (0, 1, 2)
             ticks.append(got["device_end_ticks"])
         assert ticks == sorted(ticks) and len(set(ticks)) == 3   # the device's clock advances
     finally:

@@ -463,14 +463,26 @@ def _one_group(hq, rows):
 
 def test_run_length_and_split(hq):
     """A ReplicateResp and 8 repeats: the first in full, a run of 6, then two code-4 events (a run
-    needs 3); the same message with another term, index or reject breaks a run."""
-    rows = [(hq.EV_MESSAGE, RREP, 2 + i, 41, 1000, 0, 0, 0, 0) for i in range(9)]
+    needs 3); the same message with another term, index or reject breaks a run. Senders in node
+    order make the run's consecutive form (header bit 7, the count, the first sender)."""
+    senders = [2, 5, 3, 9, 4, 7, 6, 8, 10]
+    rows = [(hq.EV_MESSAGE, RREP, senders[i], 41, 1000, 0, 0, 0, 0) for i in range(9)]
     ev, off = _one_group(hq, rows)
     data, _ = hq.encode_events(off, ev)
     # code 0: header, from, term (41), index (1000: 2 bytes) = 5; run: header, 6, six senders = 8;
     # two code-4 events of 2 bytes
     assert len(data) == 5 + 8 + 4
-    assert data[5] == (2 | 6 << 3) and data[6] == 6 and list(data[7:13]) == list(range(3, 9))
+    assert data[5] == (2 | 6 << 3) and data[6] == 6 and list(data[7:13]) == senders[1:7]
+    seq = ev.copy()
+    seq["from"] = np.arange(2, 11)
+    d_seq, _ = hq.encode_events(off, seq)
+    assert len(d_seq) == 5 + 3 + 4
+    assert d_seq[5] == (2 | 6 << 3 | 0x80) and d_seq[6] == 6 and d_seq[7] == 3
+    np.testing.assert_array_equal(
+        hq.decode_events(off, np.array([0, len(d_seq)], np.uint64), d_seq), carried(hq, seq))
+    recs, off16 = hq.events_to16(off, seq)
+    got, _, _ = hq.encode_events16_sized(off16, recs)
+    np.testing.assert_array_equal(got, d_seq)
     np.testing.assert_array_equal(hq.decode_events(off, np.array([0, len(data)], np.uint64), data),
                                   carried(hq, ev))
     for k, v in (("term", 42), ("log_index", 1001), ("reject", 1)):
@@ -491,6 +503,9 @@ def test_run_malformed(hq):
         (np.array([2 | 1 << 3, 5, 7, run, 1, 6], np.uint8), 2),     # after a RequestVoteResp
         (np.array([2 | 0 << 3, 5, 7, 9, run, 0], np.uint8), 2),     # count 0
         (np.array([2 | 0 << 3, 5, 7, 9, run, 3, 6, 7, 8], np.uint8), 3),   # 3 announced, 2 left
+        (np.array([2 | 0 << 3, 5, 7, 9, run | 0x80, 3], np.uint8), 4),      # consecutive, no s0
+        # consecutive senders past 2^32 - 1
+        (np.array([2 | 0 << 3, 5, 7, 9, run | 0x80, 3, 0xFE, 0xFF, 0xFF, 0xFF, 0x0F], np.uint8), 4),
     ]
     for data, n in bad:
         with pytest.raises(hq.HQError):
