@@ -1469,7 +1469,11 @@ def _device_split(rs):
             "outputs_ms": r["apply_ns"] / 1e6, "wait_rest_ms": rest / 1e6,
             "wait_ms": r["device_ns"] / 1e6, "wait_poll_ms": r["wait_poll_ns"] / 1e6,
             "wait_sleep_ms": r["wait_sleep_ns"] / 1e6, "wait_sleeps": r["wait_sleeps"],
-            "_end_ns": r["wait_end_ns"], "_end_ticks": r["device_end_ticks"]}
+            "_end_ns": r["wait_end_ns"], "_end_ticks": r["device_end_ticks"],
+            # the device's own span of the step, first stamp to last (HQ_WAIT_CLOCK): far above
+            # gpu_ms, the step waited in the device's queue or behind its last kernel
+            "span_ms": ((r["device_end_ticks"] - r["device_start_ticks"]) / 1e5
+                        if r["device_start_ticks"] and r["device_end_ticks"] else None)}
 
 
 _LINK = {}
@@ -1554,7 +1558,7 @@ def _phase_summary(ph):
     keys = ("e2e_ms", "encode_max_ms", "execute_ms", "dev_ms", "enc_wall_ms", "enc_task_lag_max_ms",
             "cgroup_throttled_ms", "exe_gpu_ms", "exe_wait_rest_ms", "dev_gpu_ms",
             "dev_wait_rest_ms", "exe_wake_lag_ms", "dev_wake_lag_ms", "exe_wait_sleep_ms",
-            "dev_wait_sleep_ms")
+            "dev_wait_sleep_ms", "exe_span_ms", "dev_span_ms")
     med = {k: round(float(np.median([p[k] for p in ph])), 4) for k in keys
            if all(p.get(k) is not None for p in ph)}
     th = [p["cgroup_throttled_ms"] for p in ph if p.get("cgroup_throttled_ms") is not None]
@@ -2598,9 +2602,10 @@ def _short(rec):
         if lk.get("probe"):
             out["link"]["peak_both_GBps"] = lk["probe"].get("both_GBps")
     lat = rec.get("latency_ms")
-    if isinstance(lat, dict):
-        out["p99_ms"] = {k: v["p99"] for k, v in lat.items() if v}
-    for k in ("end_to_end", "device_only", "vs_cpu_replay_end_to_end", "parity_committed"):
+    if isinstance(lat, dict):          # per mode [p50, p99] (ms)
+        out["lat_ms"] = {k: [round(v["p50"], 3), round(v["p99"], 3)] for k, v in lat.items() if v}
+    for k in (("end_to_end", "vs_cpu_replay_end_to_end", "parity_committed") if lat else
+              ("end_to_end", "device_only", "vs_cpu_replay_end_to_end", "parity_committed")):
         if k in rec:
             v = rec[k]
             if isinstance(v, dict):
@@ -2702,7 +2707,7 @@ def report(args, d, res, launcher):
     if len(text) > 8000:       # the driver parses this line: never let the summary break it
         # the step legs keep their p99 per mode and their replay ratios; the others their value
         # and roofline fraction
-        line["extra"] = {k: ({kk: v[kk] for kk in ("value", "p99_ms", "vs_cpu_replay_end_to_end",
+        line["extra"] = {k: ({kk: v[kk] for kk in ("value", "lat_ms", "vs_cpu_replay_end_to_end",
                                                      "parity_committed", "link") if kk in v}
                              if k in ("step", "step5") else
                              {kk: v.get(kk) for kk in ("value", "roofline_frac") if kk in v})

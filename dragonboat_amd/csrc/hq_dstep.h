@@ -40,6 +40,7 @@ struct hq_wait_clock {                // one wait of a step's thread (host stead
     uint64_t poll_ns, sleep_ns;       // polling, then asleep (blocking event or timed sleeps)
     uint64_t sleeps;                  // the sleeps (HQ_WAIT_SLEEP) or 1 (a blocking wait)
     uint64_t device_end_ticks;        // HQ_WAIT_CLOCK: the device's 100-MHz clock after the step
+    uint64_t device_start_ticks;      //   and before its first kernel (the jobs path)
 };
 
 struct hq_dstep_out {                 // the lists of one step, in input group order, in the

@@ -1686,7 +1686,10 @@ int wait_stream(hq_dstep *d, hipStream_t s, const char *what, uint32_t spin_us =
     wc.t_begin_ns = t0;
     auto done = [&](int r) {
         wc.t_end_ns = now_ns();
-        if (d->wait_clock && !r) wc.device_end_ticks = d->clock_host[0];
+        if (d->wait_clock && !r) {
+            wc.device_end_ticks = d->clock_host[0];
+            wc.device_start_ticks = d->clock_host[1];
+        }
         return r;
     };
     if (mode == HQ_WAIT_ADAPT && d->wait_pred_ns) {
@@ -2519,6 +2522,11 @@ int hq_dstep_run_jobs(hq_dstep *const *ds, const hq_dstep_in *ins, hq_dstep_out 
     }
     if (!nl) return rc;
     tp[1] = now_ns();
+    if (!rc && d0->wait_clock) {  // (HQ_WAIT_CLOCK: the device's clock ahead of the step)
+        d0->clock_host[1] = 0;
+        hipLaunchKernelGGL(k_clock_stamp, dim3(1), dim3(64), 0, s, d0->clock_host + 1);
+        rc = hq::check_hip(ctx, hipGetLastError(), "k_clock_stamp");
+    }
     if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d0->ev_t0, s), "event");
     if (!rc && d0->tickets_dirty)
         rc = hq::check_hip(ctx, hipMemsetAsync(d0->tickets, 0, kTickets * 4, s), "memset");

@@ -948,6 +948,7 @@ int hq_worker::device_step_done(int rc, const hq_dstep_in &inp, hq_step_output *
     out->wait_sleep_ns = dout.wait.sleep_ns;
     out->wait_end_ns = dout.wait.t_end_ns;
     out->device_end_ticks = dout.wait.device_end_ticks;
+    out->device_start_ticks = dout.wait.device_start_ticks;
     return HQ_OK;
 }
 

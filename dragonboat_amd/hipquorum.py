@@ -271,7 +271,7 @@ class StepOutput(ctypes.Structure):
                 ("wait_sleep_ns", ctypes.c_uint64), ("wait_end_ns", ctypes.c_uint64),
                 ("device_end_ticks", ctypes.c_uint64), ("ready_slots", _vp),
                 ("ready_slot_counts", _vp), ("n_ready_tiles", ctypes.c_uint64),
-                ("n_ready_slotted", ctypes.c_uint64)]
+                ("n_ready_slotted", ctypes.c_uint64), ("device_start_ticks", ctypes.c_uint64)]
 
 
 # name -> (restype, argtypes); the complete export list of include/hipquorum.h
@@ -1533,7 +1533,7 @@ class Worker:
             res[name] = np.frombuffer(buf, dt).copy() if copy else np.frombuffer(buf, dt)
         for k in ("gpu_passes", "decisions", "handle_ns", "pass_ns", "pack_ns", "device_ns",
                   "apply_ns", "gpu_ns", "gpu_jobs", "wait_sleeps", "wait_poll_ns",
-                  "wait_sleep_ns", "wait_end_ns", "device_end_ticks"):
+                  "wait_sleep_ns", "wait_end_ns", "device_end_ticks", "device_start_ticks"):
             res[k] = getattr(out, k)
         if out.ready_slots:
             # tile t's records at slots[256 t ..], counts[t] of them: gathered in tile order (=

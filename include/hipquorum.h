@@ -1013,6 +1013,10 @@ typedef struct hq_step_output {
     const hq_ready_compact *ready_slots;
     const uint32_t *ready_slot_counts;
     uint64_t n_ready_tiles, n_ready_slotted;
+    /* HQ_WAIT_CLOCK, the jobs path: the device's 100-MHz clock before the step's first kernel (a
+     * one-thread kernel ahead of it): (device_end_ticks - device_start_ticks) x 10 ns against
+     * gpu_ns tells a step that waited in the device's queue from one whose kernels ran late */
+    uint64_t device_start_ticks;
 } hq_step_output;
 
 typedef struct hq_worker hq_worker;

@@ -99,6 +99,7 @@ int main(void) {
   F(hq_step_output, ready_compact) F(hq_step_output, gpu_ns) F(hq_step_output, gpu_jobs)
   F(hq_step_output, wait_sleeps) F(hq_step_output, wait_end_ns) F(hq_step_output, device_end_ticks)
   F(hq_step_output, ready_slots) F(hq_step_output, n_ready_slotted)
+  F(hq_step_output, device_start_ticks)
   F(hq_step_stream, sizes16) F(hq_encode16_job, sizes16)
   printf("wait_modes %u,%u,%u,%u,%u\nready_slots_flag %u\n", (unsigned)HQ_WAIT_BLOCK,
          (unsigned)HQ_WAIT_SLEEP, (unsigned)HQ_WAIT_SPIN, (unsigned)HQ_WAIT_CLOCK,

@@ -303,6 +303,9 @@ def test_wait_policies_same_results(hq, mode):
             _same_lists(got, want)
             np.testing.assert_array_equal(got["ready"], want["ready"])
             assert got["device_end_ticks"] > 0 and got["wait_end_ns"] > 0 and got["gpu_ns"] > 0
+            # the device's span of the step covers the GPU's time between its timing events
+            assert 0 < got["device_start_ticks"] < got["device_end_ticks"]
+            assert (got["device_end_ticks"] - got["device_start_ticks"]) * 10 >= got["gpu_ns"] * 0.9
             assert want["device_end_ticks"] == 0
             if mode == "spin":
                 assert got["wait_sleeps"] == 0 and got["wait_sleep_ns"] == 0
