@@ -49,7 +49,7 @@ KERNEL_FUSED = {"c3mtl": "k_commit_fused<2, 1024, 2>"}
 # per timed window of --steps steps; its dispatches are the warm-up (warmup steps), the timed
 # windows (steps each, in order) and the parity launch (1 step). Per step: a window dispatch's
 # duration or counter over its steps.
-KERNEL_ENGINE = {"c3mtl-engine": ("c3mtl", "k_commit_engine<5, 2, 1, false, 1024, false>")}
+KERNEL_ENGINE = {"c3mtl-engine": ("c3mtl", "k_commit_engine<5, 2, 1, false, 1024, false, false>")}
 ENGINE_STEPS, ENGINE_WARMUP, ENGINE_WINDOWS = 20, 5, 3
 
 
