@@ -49,6 +49,7 @@ oracle:
 #              decision (their floors)
 #   lib_ingnostore / lib_ingnoload the grouped table ingest without its table stores / loads (timing probes: wrong output)
 #   lib_encspawn the threaded event encoder spawning its threads per call (before the task pool)
+#   lib_notakerun the device step taking every run member one event at a time (no take_run; A/B)
 define variant
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(1) -shared -o $@ $(SRCS)
@@ -90,6 +91,8 @@ tools/lib_ingnoload/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_INGEST_NOLOAD)
 tools/lib_rinet0/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_RI_NET=0)
+tools/lib_notakerun/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_NO_TAKE_RUN)
 tools/lib_sw%/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_STEP_WAVES=$*)
 # binned-ingest A/B (tools/ab_bin.sh): kernel parts removed (HQ_BIN_AB) or smaller regions

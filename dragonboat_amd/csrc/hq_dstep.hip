@@ -679,6 +679,10 @@ struct Engine {
                 const uint32_t p = slot(kFallback);
                 if (WRITE) list<uint64_t>(kFallback)[p] = g.cluster_id;
                 defer(e);
+            } else if (STREAM && pv.run) {               // the run's other members at once
+#ifndef HQ_NO_TAKE_RUN
+                e += take_run(pv, by_bytes ? ~0ull : e1 - e - 1);
+#endif
             }
         }
         cnt[kEvents] = (uint32_t)(e - e0);
@@ -697,6 +701,42 @@ struct Engine {
             const uint32_t p = slot(kCommits);
             if (WRITE) list<hq_commit_event>(kCommits)[p] = hq_commit_event{g.cluster_id, g.committed};
         }
+    }
+
+    // The rest of a run whose members are consecutive node ids (the event just handled was its
+    // first or an earlier member) taken at once where each member could only raise its match
+    // (ReplicateResp) and mark its member active: a leader at the run's term, a ReplicateResp
+    // run within the log (or rejecting) or a HeartbeatResp run without a ctx. Each member that
+    // raises its match is a tryCommit decision; tryCommit runs once after the last: the quorum-th
+    // largest match only rises as matches rise, so it ends where the member-by-member calls end
+    // (and the run holds no event that reads the committed index). Returns the members taken;
+    // otherwise (0) the loop takes them one at a time (also when the run claims more events than
+    // the group has left, `room`: the loop then reports the bad sizes).
+    __device__ __forceinline__ uint32_t take_run(DPrev &pv, uint64_t room) {
+        const uint32_t kind = pv.last & 3;
+        const bool rej = (pv.last >> 2) & 1;
+        if (!(pv.last & 8u) || pv.run > room || g.state != HQ_STATE_LEADER || (g.flags & kDSuspended) ||
+            (pv.term != 0 && pv.term != g.term) ||
+            !(kind == 2 ? pv.hint == 0 : (rej || pv.index <= g.last)))
+            return 0;
+        const uint32_t m = pv.run;
+        uint32_t upd = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            const int mi = member_of(pv.run_from + j);
+            if (mi < 0) continue;                        // Peer.Handle drop (peer.go:191-197)
+            if (kind == 1 && !rej && match_of(mi) < pv.index) {
+                set_match(mi, pv.index);                 // remote.tryUpdate
+                ++upd;
+            }
+            active |= 1u << mi;
+        }
+        pv.run_from += m;
+        pv.run = 0;
+        if (upd) {
+            try_commit();
+            cnt[kDecisions] += upd - 1;
+        }
+        return m;
     }
 
     // pass A, before the group's events: its state as the step found it

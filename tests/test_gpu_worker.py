@@ -882,3 +882,98 @@ def test_ready_compact_wide_delta_keeps_records(hq):
 def test_ready_compact_needs_the_device_worker(hq):
     with pytest.raises(hq.HQError):
         hq.Worker(0, 3, on_device=False, ready_compact=True)
+
+
+def _consecutive_groups(rng, G):
+    """Groups whose members are node ids 1..n (the leader node 1), in a random member order: the
+    followers' acks then arrive as runs of consecutive senders (the stream's consecutive form)."""
+    groups = []
+    for j in range(G):
+        n = int(rng.integers(3, 9))
+        n_wit = int(rng.integers(0, 2)) if n >= 4 else 0
+        n_obs = int(rng.integers(0, 3)) if n - n_wit >= 3 else 0
+        roles = [sc.REMOTE] * (n - n_wit - n_obs) + [sc.WITNESS] * n_wit + [sc.OBSERVER] * n_obs
+        state = int(rng.choice([sc.LEADER] * 7 + [sc.CANDIDATE, sc.FOLLOWER]))
+        term = int(rng.integers(2, 9))
+        last = 100 + int(rng.integers(0, 50))
+        term_start = last - int(rng.integers(0, 6))
+        committed = last - int(rng.integers(0, 9))
+        mem = []
+        for i, r in zip(range(1, n + 1), roles):
+            m = last if i == 1 else (int(rng.integers(max(0, committed - 3), last + 1))
+                                     if state == sc.LEADER else 0)
+            mem.append((i, m, r, int(rng.random() < 0.5)))
+        order = rng.permutation(n)
+        groups.append((1 + j, 1, term, state, committed, last, term_start,
+                       [mem[k] for k in order]))
+    return groups
+
+
+def _run_events(rng, state, ctx_seq):
+    """One step of a group inside the worker's contract: maybe a ReadIndex, then runs of
+    ReplicateResps and HeartbeatResps from consecutive node ids (some past the members, some from
+    the node itself) at the group's term or another, rejecting now and then, at or below
+    lastIndex, HeartbeatResps without a ctx from anyone and with a pending ctx from voting members
+    only (an observer acking a ctx is the worker's fallback); maybe CheckQuorum and a proposal."""
+    term, st, committed, last, ts, mem, reads = state
+    ev = []
+    ctxs = [r[2] for r in reads]
+    if rng.random() < 0.3 and len(ctxs) < 8:
+        ctx_seq[0] += 1
+        c = (ctx_seq[0], 7)
+        ctxs.append(c)
+        ev.append(("read", c[0], c[1]))
+    n = len(mem)
+    n_vote = sum(1 for m in mem if m[2] != sc.OBSERVER)     # (observers hold the top ids)
+    for _ in range(int(rng.integers(1, 4))):
+        t = int(rng.choice([term] * 17 + [0, term - 1, term + 1]))
+        if rng.random() < 0.5:
+            s0, k = int(rng.integers(1, 4)), int(rng.integers(3, n + 3))
+            idx = int(rng.choice([last, last, last - 1, committed]))
+            rej = int(rng.random() < 0.1)
+            ev += [sc.msg(sc.RREP, s0 + i, t, idx, reject=rej) for i in range(k)]
+        elif ctxs and rng.random() < 0.4 and n_vote >= 3:
+            c = ctxs[int(rng.integers(len(ctxs)))]
+            s0 = int(rng.integers(1, n_vote - 1))
+            k = int(rng.integers(3, n_vote - s0 + 2))
+            ev += [sc.msg(sc.HBRESP, s0 + i, t, hint=c[0], high=c[1]) for i in range(k)]
+        else:
+            s0, k = int(rng.integers(1, 4)), int(rng.integers(3, n + 3))
+            ev += [sc.msg(sc.HBRESP, s0 + i, t) for i in range(k)]
+    if rng.random() < 0.2:
+        ev.append(("check_quorum",))
+    if rng.random() < 0.5:
+        ev.append(("propose", 1))
+    return ev
+
+
+@pytest.mark.parametrize("stream", [True, "sized16", "sized16-slots"])
+@pytest.mark.parametrize("seed", [31, 32])
+def test_consecutive_runs_device_equals_reference(hq, seed, stream):
+    """Runs of acks from consecutive node ids, which the device takes a run at a time where each
+    member can only raise its match and mark itself active (hq_dstep.hip take_run), against the
+    reference replay (oracle/qref_step.c) taking the same events one at a time: every output list
+    and every group's state equal, no fallback."""
+    rng = np.random.default_rng(seed)
+    o = OracleBackend()
+    dev = WorkerBackend(hq, n_max=8, seed=seed, on_device=True, stream=stream)
+    try:
+        groups = _consecutive_groups(rng, 2000)
+        for g in groups:
+            o.add_group(*g)
+            dev.add_group(*g)
+        ctx_seq = [0]
+        events = 0
+        for s in range(5):
+            per = {g[0]: _run_events(rng, o.state(g[0]), ctx_seq) for g in groups
+                   if rng.random() < 0.9}
+            events += sum(len(e) for e in per.values())
+            want, got = o.step(per), dev.step(per)
+            assert got["_fallback"] == []
+            for cid in per:
+                same_step(want, got, cid)
+            for g in groups:
+                assert dev.state(g[0]) == o.state(g[0]), (s, g[0])
+        assert events > 20000
+    finally:
+        dev.close()
