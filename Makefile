@@ -49,6 +49,7 @@ oracle:
 #              decision (their floors)
 #   lib_ingnostore / lib_ingnoload the grouped table ingest without its table stores / loads (timing probes: wrong output)
 #   lib_encspawn the threaded event encoder spawning its threads per call (before the task pool)
+#   lib_engprof the engine's per-workgroup clocks and tile counts (hq_engine_wgprof; tools/engine_wgprof.py)
 #   lib_notakerun the device step taking every run member one event at a time (no take_run; A/B)
 define variant
 	@mkdir -p $(dir $@)
@@ -91,6 +92,8 @@ tools/lib_ingnoload/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_INGEST_NOLOAD)
 tools/lib_rinet0/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_RI_NET=0)
+tools/lib_engprof/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_ENGINE_WGPROF)
 tools/lib_notakerun/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_NO_TAKE_RUN)
 tools/lib_sw%/libhipquorum.so: $(SRCS) $(DEPS)

@@ -455,6 +455,15 @@ __device__ __forceinline__ uint32_t claim(EngineLds &l, uint32_t lane) {
     return wave_u32(t);
 }
 
+#ifdef HQ_ENGINE_WGPROF
+// probe builds only (-DHQ_ENGINE_WGPROF, tools/engine_wgprof.py): per workgroup of the static
+// path, 8 words — the device clock at its start, its XCC id, its HW_ID register, the ticks its
+// waves spent in their tile loops (summed), the tiles it decided, the clock when its last wave
+// left — read and reset by hq_engine_wgprof
+constexpr uint32_t kWgProfMax = 2048;
+__device__ uint64_t g_wgprof[kWgProfMax * 8];
+#endif
+
 // SIG: per-step completion signals (write-through stores, drained before a tile is counted).
 // INPLACE: the device-resident table decided in place (committed' into the tile's row).
 // BAL: balanced mode (tiles taken from per-XCD pools through device tickets; not with INPLACE).
@@ -635,6 +644,17 @@ void k_commit_engine(const EngineK e) {
         if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
         return;
     }
+#ifdef HQ_ENGINE_WGPROF
+    uint64_t *const prof = blockIdx.x < kWgProfMax ? g_wgprof + (size_t)blockIdx.x * 8 : nullptr;
+    uint64_t p_busy = 0, p_tiles = 0;
+    if (prof && threadIdx.x == 0) {
+        __hip_atomic_store(prof + 0, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(prof + 1, (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // HW_REG_XCC_ID [3:0]
+        __hip_atomic_store(prof + 2, (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // HW_REG_HW_ID
+    }
+#endif
     uint32_t t = claim(l, lane);
     // SIG / INPLACE: a decided tile is counted (fin / done) only once its stores are complete.
     // The count of tile k is taken after tile k + 1's loads have returned (vector memory
@@ -707,6 +727,9 @@ void k_commit_engine(const EngineK e) {
                     __builtin_amdgcn_s_sleep(2);
             }
             // the workgroup's tiles of step s, one ticket at a time
+#ifdef HQ_ENGINE_WGPROF
+            const uint64_t p_t0 = now_ticks();
+#endif
             do {
                 const uint64_t wbase = uniform64((b0 + (uint32_t)(t - e_prev)) * HQ_TILE_GROUPS);
                 // the lane index laundered per tile: nothing derived from it is loop-invariant, so
@@ -724,8 +747,14 @@ void k_commit_engine(const EngineK e) {
                     p_s = s;
                     p_tgt = tgt;
                 }
+#ifdef HQ_ENGINE_WGPROF
+                ++p_tiles;
+#endif
                 t = claim(l, lane);
             } while (before(t, e_cur));
+#ifdef HQ_ENGINE_WGPROF
+            p_busy += now_ticks() - p_t0;
+#endif
         }
         e_prev = e_cur;
         ++s;
@@ -737,6 +766,13 @@ void k_commit_engine(const EngineK e) {
     }
     drain();
     if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
+#ifdef HQ_ENGINE_WGPROF
+    if (prof && lane == 0) {
+        __hip_atomic_fetch_add(prof + 3, p_busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(prof + 4, p_tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(prof + 5, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
 }
 
 typedef void (*EngineKernel)(const EngineK);
@@ -1275,6 +1311,24 @@ int hq_engine_dump(hq_engine *e, uint64_t *out, uint32_t n_words) {
 }
 
 const char *hq_engine_last_error(const hq_engine *e) { return e ? e->err.c_str() : ""; }
+
+#ifdef HQ_ENGINE_WGPROF
+// probe builds only: the per-workgroup words of the launches since the last reset (8 per
+// workgroup, kWgProfMax workgroups), then zeroed when reset is set. Call with no grid resident.
+int hq_engine_wgprof(uint64_t *out, uint32_t n_words, int reset) {
+    const size_t bytes = sizeof(uint64_t) * 8 * kWgProfMax;
+    if (out && n_words < 8 * kWgProfMax) return HQ_E_INVAL;
+    if (hipDeviceSynchronize() != hipSuccess) return HQ_E_DEVICE;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wgprof), bytes) != hipSuccess) return HQ_E_DEVICE;
+    if (reset) {
+        void *z = nullptr;
+        if (hipGetSymbolAddress(&z, HIP_SYMBOL(g_wgprof)) != hipSuccess ||
+            hipMemset(z, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return HQ_E_DEVICE;
+    }
+    return HQ_OK;
+}
+#endif
 
 void hq_engine_close(hq_engine *e) {
     if (!e) return;
