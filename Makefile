@@ -49,6 +49,7 @@ oracle:
 #              decision (their floors)
 #   lib_ingnostore / lib_ingnoload the grouped table ingest without its table stores / loads (timing probes: wrong output)
 #   lib_encspawn the threaded event encoder spawning its threads per call (before the task pool)
+#   lib_encprof the threaded encoder's per-range start / barrier arrival per call (stderr)
 #   lib_engprof the engine's per-workgroup clocks and tile counts (hq_engine_wgprof; tools/engine_wgprof.py)
 #   lib_notakerun the device step taking every run member one event at a time (no take_run; A/B)
 define variant
@@ -92,6 +93,8 @@ tools/lib_ingnoload/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_INGEST_NOLOAD)
 tools/lib_rinet0/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_RI_NET=0)
+tools/lib_encprof/libhipquorum.so: $(SRCS) $(DEPS)
+	$(call variant,-DHQ_ENC_PROF)
 tools/lib_engprof/libhipquorum.so: $(SRCS) $(DEPS)
 	$(call variant,-DHQ_ENGINE_WGPROF)
 tools/lib_notakerun/libhipquorum.so: $(SRCS) $(DEPS)

@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -625,6 +626,20 @@ bool decode_one(const uint8_t *&p, const uint8_t *end, Prev &pv, uint64_t &run_l
 // a pool thread's encode scratch is kept for its next call (first touched on its memory node),
 // unless a call grew it past kKeepScratch: then it is released
 constexpr size_t kKeepScratch = size_t(256) << 20;
+// hq_events16_encode_sized_multi: chunks per encode thread (taken from a shared counter);
+// HQ_ENC_CHUNKS overrides (1: one range per thread, the static split of round 5, for A/B)
+uint64_t chunks_per_thread() {
+    auto read = [] {
+        const char *v = std::getenv("HQ_ENC_CHUNKS");
+        return v && std::atoi(v) > 0 ? (uint64_t)std::atoi(v) : uint64_t(8);
+    };
+#ifdef HQ_ENC_PROF
+    return read();                  // (probe builds: read at every call, for step-by-step A/B)
+#else
+    static const uint64_t k = read();
+    return k;
+#endif
+}
 inline void shrink_scratch(std::vector<uint8_t> &v) {
     if (v.capacity() > kKeepScratch) std::vector<uint8_t>().swap(v);
 }
@@ -746,16 +761,21 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
         {std::max(threads, 1u), std::max<uint64_t>(1, R / 4096), TaskPool::kMaxThreads + 1});
     if (live.empty()) return first;
     const uint64_t c0 = now_ns();
-    // job j's groups split at the global record cuts R t / T (group boundaries): range t of the
-    // job is groups [gc[j][t], gc[j][t + 1]), empty unless the job's records meet cut range t
+    // C chunks of about equal records, taken by the T threads from a shared counter: a thread
+    // slowed by its core (a busy SMT sibling or a crowded host) takes fewer chunks instead of
+    // holding the call back by a whole 1/T share
+    const uint32_t C = (uint32_t)std::min<uint64_t>((uint64_t)T * chunks_per_thread(),
+                                                    std::max<uint64_t>(T, R / 4096));
+    // job j's groups split at the global record cuts R c / C (group boundaries): chunk c of the
+    // job is groups [gc[j][c], gc[j][c + 1]), empty unless the job's records meet chunk c
     std::vector<std::vector<uint64_t>> gc(count);
     for (uint32_t j : live) {
         const hq_encode16_job &b = jobs[j];
         std::vector<uint64_t> &c = gc[j];
-        c.assign(T + 1, 0);
-        c[T] = b.n_groups;
-        for (uint32_t t = 1; t < T; ++t) {
-            const uint64_t cut = R * t / T;
+        c.assign(C + 1, 0);
+        c[C] = b.n_groups;
+        for (uint32_t t = 1; t < C; ++t) {
+            const uint64_t cut = R * t / C;
             const uint64_t rel = cut <= rec0[j] ? 0 : std::min(cut - rec0[j], rec0[j + 1] - rec0[j]);
             const uint64_t want = b.offsets16[0] + rel;
             const uint64_t g = (uint64_t)(std::lower_bound(b.offsets16, b.offsets16 + b.n_groups, want) -
@@ -764,46 +784,58 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
         }
     }
     struct Piece {
-        uint32_t job;
-        uint64_t at, events, bytes, last_start;   // at: offset in the thread's scratch
+        uint32_t job, thread;                          // thread: whose scratch holds it
+        uint64_t at, events, bytes, last_start, dst;   // at: offset in that scratch; dst: in out
         int rc;
     };
-    std::vector<std::vector<Piece>> pieces(T);
+    std::vector<std::vector<Piece>> pieces(C);         // per chunk, one per job it meets
+    std::atomic<uint32_t> next{0};
     std::mutex bm;
     std::condition_variable bcv;
     uint32_t arrived = 0;
     uint64_t c1 = 0;
-    // per job, per thread: where the thread's piece goes in the job's bytes
-    std::vector<uint64_t> place((size_t)count * T, 0);
     std::vector<uint8_t> fits(count, 1);
+#ifdef HQ_ENC_PROF   // probe builds only: each range's start and arrival at the barrier (stderr)
+    std::vector<uint64_t> p_start(T, 0), p_arrive(T, 0);
+#endif
     const int prc = task_pool().parallel_for(T, [&](uint32_t t) {
         thread_local std::vector<uint8_t> scratch;
-        std::vector<Piece> &ps = pieces[t];
         uint64_t pos = 0;
-        for (uint32_t j : live) {
-            const uint64_t g0 = gc[j][t], g1 = gc[j][t + 1];
-            if (g0 >= g1) continue;
-            const hq_encode16_job &b = jobs[j];
-            Piece pc{j, pos, 0, 0, ~0ull, HQ_OK};
-            // (the piece follows the thread's earlier pieces in its scratch)
-            pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &scratch, nullptr, 0,
-                                &pc.events, &pc.bytes, &pc.last_start, pos, b.sizes16);
-            if (pc.rc) pc.bytes = 0;
-            pos += pc.bytes;
-            ps.push_back(pc);
+#ifdef HQ_ENC_PROF
+        p_start[t] = now_ns();
+#endif
+        for (;;) {
+            const uint32_t c = next.fetch_add(1, std::memory_order_relaxed);
+            if (c >= C) break;
+            std::vector<Piece> &ps = pieces[c];
+            for (uint32_t j : live) {
+                const uint64_t g0 = gc[j][c], g1 = gc[j][c + 1];
+                if (g0 >= g1) continue;
+                const hq_encode16_job &b = jobs[j];
+                Piece pc{j, t, pos, 0, 0, ~0ull, 0, HQ_OK};
+                // (the piece follows the thread's earlier pieces in its scratch)
+                pc.rc = enc16_range(b.offsets16, b.recs, b.sizes, g0, g1, &scratch, nullptr, 0,
+                                    &pc.events, &pc.bytes, &pc.last_start, pos, b.sizes16);
+                if (pc.rc) pc.bytes = 0;
+                pos += pc.bytes;
+                ps.push_back(pc);
+            }
         }
+#ifdef HQ_ENC_PROF
+        p_arrive[t] = now_ns();
+#endif
         {
             std::unique_lock<std::mutex> lk(bm);
             if (++arrived == T) {
                 // every piece in: each job's totals, its capacity rule and its pieces' places
                 c1 = now_ns();
                 std::vector<uint64_t> total(count, 0), last(count, ~0ull);
-                for (uint32_t u = 0; u < T; ++u) {
-                    for (const Piece &pc : pieces[u]) {
+                for (uint32_t u = 0; u < C; ++u) {       // (chunk order: each job's byte order)
+                    for (Piece &pc : pieces[u]) {
                         hq_encode16_job &b = jobs[pc.job];
                         if (pc.rc && !b.rc) b.rc = pc.rc;
                         if (pc.last_start != ~0ull) last[pc.job] = total[pc.job] + pc.last_start;
-                        place[(size_t)pc.job * T + u] = total[pc.job];
+                        pc.dst = total[pc.job];
                         total[pc.job] += pc.bytes;
                         b.n_events += pc.events;
                     }
@@ -821,11 +853,12 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
                 bcv.wait(lk, [&] { return arrived == T; });
             }
         }
-        for (const Piece &pc : ps) {
-            const hq_encode16_job &b = jobs[pc.job];
-            if (!b.rc && pc.bytes)
-                std::memcpy(b.out + place[(size_t)pc.job * T + t], scratch.data() + pc.at, pc.bytes);
-        }
+        for (uint32_t c = 0; c < C; ++c)                // the pieces this thread encoded
+            for (const Piece &pc : pieces[c]) {
+                const hq_encode16_job &b = jobs[pc.job];
+                if (pc.thread == t && !b.rc && pc.bytes)
+                    std::memcpy(b.out + pc.dst, scratch.data() + pc.at, pc.bytes);
+            }
         shrink_scratch(scratch);
     }, true);
     if (prc) {                    // (nothing encoded)
@@ -835,6 +868,22 @@ int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32
     first = HQ_OK;
     for (uint32_t j = 0; j < count && !first; ++j) first = jobs[j].rc;
     const uint64_t c2 = now_ns();
+#ifdef HQ_ENC_PROF
+    {   // per call: wall, phase 1, the ranges' latest start and earliest / latest arrival (us
+        // after the call's start), and the slowest range's own encode time
+        uint64_t s_max = 0, a_min = ~0ull, a_max = 0, d_max = 0, d_min = ~0ull;
+        for (uint32_t t = 0; t < T; ++t) {
+            s_max = std::max(s_max, p_start[t] - c0);
+            a_min = std::min(a_min, p_arrive[t] - c0);
+            a_max = std::max(a_max, p_arrive[t] - c0);
+            d_max = std::max(d_max, p_arrive[t] - p_start[t]);
+            d_min = std::min(d_min, p_arrive[t] - p_start[t]);
+        }
+        std::fprintf(stderr, "encprof T=%u wall=%.1f phase1=%.1f start_max=%.1f arrive=%.1f..%.1f "
+                             "range_us=%.1f..%.1f\n", T, (c2 - c0) / 1e3, (c1 - c0) / 1e3,
+                     s_max / 1e3, a_min / 1e3, a_max / 1e3, d_min / 1e3, d_max / 1e3);
+    }
+#endif
     g_clk.calls++;
     g_clk.encode_ns += c1 - c0;
     g_clk.copy_ns += c2 - c1;

@@ -355,13 +355,13 @@ def test_threaded_encodes_side_by_side(hq):
     assert not bad
 
 
-@pytest.mark.parametrize("threads", [1, 3, 14])
-def test_multi_encode_equals_one_call_per_job(hq, threads):
+@pytest.mark.parametrize("threads,G", [(1, 1 << 13), (3, 1 << 13), (14, 1 << 13), (14, 1 << 16)])
+def test_multi_encode_equals_one_call_per_job(hq, threads, G):
     """hq_events16_encode_sized_multi: 16 workers' streams (ragged: a worker with no groups, one
-    with groups but no records, others of unequal size) encoded in one call whose thread ranges
-    cross job boundaries; every job's bytes, size words and totals equal its own single call's."""
+    with groups but no records, others of unequal size) encoded in one call whose chunks (taken
+    by the threads from a shared counter: 26 and 112 chunks here) cross job boundaries; every
+    job's bytes, size words and totals equal its own single call's."""
     import bench
-    G = 1 << 13
     recs = bench.StepRows16(hq, G, bench.STEP_ROLES["step5"])
     off16, r = recs.set(2)
     b = sorted({0, G} | {int(x) for x in np.random.default_rng(5).integers(0, G, 14)})

@@ -31,6 +31,9 @@ G = int(os.environ.get("G", 1 << 20))
 STEPS = int(os.environ.get("STEPS", 100))
 GAP = float(os.environ.get("GAP", 1.0))
 GAP_STEPS = int(os.environ.get("GAP_STEPS", 30))
+# AB=8,1: the conc modes alternate HQ_ENC_CHUNKS over these values step by step (the encode
+# profiling build reads it at every call); each row records the value its encode ran with
+AB = [x for x in os.environ.get("AB", "").split(",") if x]
 MODES = os.environ.get("MODES", "dev,seq,conc,plain,sleep").split(",")
 roles = bench.STEP_ROLES["step5"]
 nv = sum(r != "observer" for r in roles)
@@ -107,6 +110,8 @@ def run_mode(mode):
                 enc = encode(1 - slot, "plain")
                 encode(1 - slot)           # (the next step's real stream, after the timed part)
             else:
+                if AB:                     # alternate the encoder's chunking step by step
+                    os.environ["HQ_ENC_CHUNKS"] = AB[s % len(AB)]
                 enc = encode(1 - slot)
             fut.result()
             dt = time.perf_counter() - t0
@@ -115,7 +120,8 @@ def run_mode(mode):
             if r["device_start_ticks"] and r["device_end_ticks"] else None
         wait = (r["wait_poll_ns"] + r["wait_sleep_ns"]) / 1e6
         if s >= 3:
-            rows.append({"s": s - 3, "e2e": dt * 1e3, "enc": enc * 1e3, "gpu": r["gpu_ns"] / 1e6,
+            rows.append({"s": s - 3, "k": AB[s % len(AB)] if AB else None,
+                         "e2e": dt * 1e3, "enc": enc * 1e3, "gpu": r["gpu_ns"] / 1e6,
                          "span": span, "wait": wait, "submit": r["pack_ns"] / 1e6,
                          "lag": (wait - span) if span is not None else None})
     wk.close()
@@ -131,6 +137,9 @@ def run_mode(mode):
            "gpu_p50": round(float(np.median([x["gpu"] for x in rows])), 4),
            "late": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in x.items()}
                     for x in late[:8]]}
+    if os.environ.get("ROWS"):
+        out["rows"] = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in x.items()}
+                       for x in rows]
     print(json.dumps(out), flush=True)
 
 

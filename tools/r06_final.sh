@@ -3,7 +3,7 @@
 # the --gpus 2 threads and torchrun rehearsals; each step under its own time limit, stopping at
 # the first failure. Outputs under gpurun_out/r06final/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r06final
+O=${OUT:-gpurun_out/r06final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 380 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || exit $?
