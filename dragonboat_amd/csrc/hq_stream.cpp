@@ -408,12 +408,6 @@ int enc16_range(const uint64_t *off, const hq_event16 *recs, uint32_t *sizes, ui
     return HQ_OK;
 }
 
-struct alignas(64) RangeOut {   // one thread's results, a cache line each
-    uint64_t events = 0, bytes = 0;
-    uint64_t last_start = ~0ull;   // offset of the range's last event in its bytes (none: ~0)
-    int rc = HQ_OK;
-};
-
 uint64_t now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::steady_clock::now().time_since_epoch())
@@ -669,69 +663,23 @@ int hq_events16_encode_sized(uint64_t n_groups, const uint64_t *offsets16, const
     if (T <= 1)
         return enc16_range(offsets16, recs, sizes, 0, n_groups, nullptr, out, cap, n_events,
                            n_bytes);
-    const uint64_t c0 = now_ns();
-    // T ranges of about equal records (group boundaries). Each range is encoded by one pool
-    // thread into that thread's own scratch (first touched, so held on its memory node, and
-    // reused by later calls), the threads meet once every range's byte count is known, and each
-    // copies its range into place: one pass, no scratch shared between threads (scratch handed
-    // from thread to thread ran the encode 2.5 x slower per record on a 256-CPU host,
-    // profiles/r05b/enc_probe.log)
-    std::vector<uint64_t> g(T + 1);
-    std::vector<RangeOut> res(T);
-    g[0] = 0;
-    g[T] = n_groups;
-    for (uint32_t t = 1; t < T; ++t) {
-        const uint64_t want = offsets16[0] + nrec * t / T;
-        g[t] = std::max<uint64_t>(g[t - 1], (uint64_t)(std::lower_bound(offsets16, offsets16 + n_groups,
-                                                                         want) - offsets16));
-    }
-    std::mutex bm;
-    std::condition_variable bcv;
-    uint32_t arrived = 0;
-    uint64_t c1 = 0, total = 0, events = 0;
-    int rc = HQ_OK;
-    bool fits = true;
-    std::vector<uint64_t> at(T, 0);
-    const int prc = task_pool().parallel_for(T, [&](uint32_t t) {
-        thread_local std::vector<uint8_t> scratch;
-        res[t].rc = enc16_range(offsets16, recs, sizes, g[t], g[t + 1], &scratch, nullptr, 0,
-                                &res[t].events, &res[t].bytes, &res[t].last_start);
-        {
-            std::unique_lock<std::mutex> lk(bm);
-            if (++arrived == T) {
-                // the last range in: totals, the capacity rule (HQ_EVENT_STREAM_MAX bytes free
-                // before every event, i.e. before the last one: event starts only grow) and
-                // every range's place
-                c1 = now_ns();
-                uint64_t last = ~0ull;
-                for (uint32_t i = 0; i < T; ++i) {
-                    if (res[i].rc && !rc) rc = res[i].rc;
-                    if (res[i].last_start != ~0ull) last = total + res[i].last_start;
-                    at[i] = total;
-                    total += res[i].bytes;
-                    events += res[i].events;
-                }
-                fits = last == ~0ull || (cap >= last && cap - last >= HQ_EVENT_STREAM_MAX);
-                bcv.notify_all();
-            } else {
-                bcv.wait(lk, [&] { return arrived == T; });
-            }
-        }
-        if (!rc && fits && res[t].bytes) std::memcpy(out + at[t], scratch.data(), res[t].bytes);
-        shrink_scratch(scratch);
-    }, true);
-    if (prc) return prc;
-    if (!rc && !fits) rc = HQ_E_STATE;
-    if (!rc) {
-        *n_events = events;
-        *n_bytes = total;
-    }
-    const uint64_t c2 = now_ns();
-    g_clk.calls++;
-    g_clk.encode_ns += c1 - c0;
-    g_clk.copy_ns += c2 - c1;
-    g_clk.wall_ns += c2 - c0;
-    return rc;
+    // the threads take chunks of the records as hq_events16_encode_sized_multi does (one job):
+    // each chunk encoded into the taking thread's own scratch (first touched, so held on its
+    // memory node, and reused by later calls), then copied into place once every chunk's byte
+    // count is known (scratch handed from thread to thread ran the encode 2.5 x slower per record
+    // on a 256-CPU host, profiles/r05b/enc_probe.log)
+    hq_encode16_job job{};
+    job.n_groups = n_groups;
+    job.offsets16 = offsets16;
+    job.recs = recs;
+    job.out = out;
+    job.cap = cap;
+    job.sizes = sizes;
+    const int rc = hq_events16_encode_sized_multi(&job, 1, T);
+    if (rc) return rc;
+    *n_events = job.n_events;
+    *n_bytes = job.n_bytes;
+    return HQ_OK;
 }
 
 int hq_events16_encode_sized_multi(hq_encode16_job *jobs, uint32_t count, uint32_t threads) {
