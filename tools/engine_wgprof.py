@@ -10,6 +10,7 @@ import ctypes
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -53,8 +54,13 @@ eng.timing(reset=True)
 prev = None
 for k in range(WINDOWS):
     a1 = [arr(5 + k * STEPS + i, 1) for i in range(STEPS)]
-    for one in a1:
-        eng.post(one)
+    tp0 = time.perf_counter()
+    if os.environ.get("ONEPOST"):          # the window's steps in one hq_engine_post call
+        eng.post(arr(5 + k * STEPS, STEPS))
+    else:
+        for one in a1:
+            eng.post(one)
+    post_us = (time.perf_counter() - tp0) * 1e6
     eng.drain()
     nl, ms = eng.timing(reset=True)
     p = wgprof(True)[:grid]
@@ -69,7 +75,11 @@ for k in range(WINDOWS):
     rank = np.argsort(np.argsort(per_tile))
     corr = None if prev is None else float(np.corrcoef(rank, prev)[0, 1])
     prev = rank
-    out = {"window": k, "launches": nl, "event_ms": round(ms, 4),
+    busy_frac = busy / np.maximum(end - start, 1) / (eng.info().block // 64)
+    half = grid // 2
+    out = {"window": k, "launches": nl, "event_ms": round(ms, 4), "post_us": round(post_us, 1),
+           "busy_frac_first_half_second_half": [round(float(busy_frac[:half].mean()), 3),
+                                                round(float(busy_frac[half:].mean()), 3)],
            "event_us_per_step": round(ms * 1e3 / STEPS, 3),
            "device_span_us": round(float(end.max() - t0) / 100, 2),
            "start_spread_us": round(float(start.max() - t0) / 100, 2),
