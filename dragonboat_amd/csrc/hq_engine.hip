@@ -459,7 +459,8 @@ __device__ __forceinline__ uint32_t claim(EngineLds &l, uint32_t lane) {
 // probe builds only (-DHQ_ENGINE_WGPROF, tools/engine_wgprof.py): per workgroup of the static
 // path, 8 words — the device clock at its start, its XCC id, its HW_ID register, the ticks its
 // waves spent in their tile loops (summed), the tiles it decided, the clock when its last wave
-// left — read and reset by hq_engine_wgprof
+// left, the ticks its waves spent at the frontier (bits 0-39) and their entries there (40-63),
+// and the ticks its first wave spent in the look-ahead — read and reset by hq_engine_wgprof
 constexpr uint32_t kWgProfMax = 2048;
 __device__ uint64_t g_wgprof[kWgProfMax * 8];
 #endif
@@ -646,7 +647,7 @@ void k_commit_engine(const EngineK e) {
     }
 #ifdef HQ_ENGINE_WGPROF
     uint64_t *const prof = blockIdx.x < kWgProfMax ? g_wgprof + (size_t)blockIdx.x * 8 : nullptr;
-    uint64_t p_busy = 0, p_tiles = 0;
+    uint64_t p_busy = 0, p_tiles = 0, p_front = 0, p_nfront = 0, p_refr = 0;
     if (prof && threadIdx.x == 0) {
         __hip_atomic_store(prof + 0, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(prof + 1, (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20),
@@ -690,7 +691,14 @@ void k_commit_engine(const EngineK e) {
         // the step of ticket t
         if (s >= known) {
             drain();
+            #ifdef HQ_ENGINE_WGPROF
+            const uint64_t p_f0 = now_ticks();
+            #endif
             known = frontier<WPW>(kargs(), l, s, lane);
+            #ifdef HQ_ENGINE_WGPROF
+            p_front += now_ticks() - p_f0;
+            ++p_nfront;
+            #endif
             if (known <= s) break;   // idle: resume here at the next launch
         }
         const uint64_t slot = s & dmask;
@@ -762,7 +770,13 @@ void k_commit_engine(const EngineK e) {
         // of each workgroup looks ahead at its step transitions, while its other waves work on
         // (refresh), so that the workgroup seldom runs out of known steps and stalls at its
         // frontier for a relay round trip and a polling sleep (post-as-ready windows)
+        #ifdef HQ_ENGINE_WGPROF
+        const uint64_t p_r0 = now_ticks();
+        #endif
         if (wv == 0) refresh(kargs(), l, s, lane);
+        #ifdef HQ_ENGINE_WGPROF
+        if (wv == 0) p_refr += now_ticks() - p_r0;
+        #endif
     }
     drain();
     if (lane == 0 && wv == 0) gp(e.d_cursor)[blockIdx.x] = s;
@@ -771,6 +785,9 @@ void k_commit_engine(const EngineK e) {
         __hip_atomic_fetch_add(prof + 3, p_busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(prof + 4, p_tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_max(prof + 5, now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(prof + 6, p_front | (p_nfront << 40), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);   // frontier ticks | entries << 40
+        __hip_atomic_fetch_add(prof + 7, p_refr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
 }

@@ -65,6 +65,9 @@ for k in range(WINDOWS):
     nl, ms = eng.timing(reset=True)
     p = wgprof(True)[:grid]
     start, xcc, hwid, busy, tiles, end = (p[:, i].astype(np.int64) for i in range(6))
+    front = (p[:, 6] & np.uint64((1 << 40) - 1)).astype(np.int64)
+    nfront = (p[:, 6] >> np.uint64(40)).astype(np.int64)
+    refr = p[:, 7].astype(np.int64)
     t0 = start.min()
     per_tile = busy / np.maximum(tiles, 1)      # wave-ticks per tile (10 ns)
     by_xcc = {int(x): {"wgs": int((xcc == x).sum()),
@@ -77,7 +80,15 @@ for k in range(WINDOWS):
     prev = rank
     busy_frac = busy / np.maximum(end - start, 1) / (eng.info().block // 64)
     half = grid // 2
+    wps = eng.info().block // 64
+    life = np.maximum(end - start, 1) * wps             # wave-ticks of each workgroup's life
     out = {"window": k, "launches": nl, "event_ms": round(ms, 4), "post_us": round(post_us, 1),
+           "frontier_frac_halves": [round(float((front / life)[:grid // 2].mean()), 4),
+                                    round(float((front / life)[grid // 2:].mean()), 4)],
+           "frontier_entries_per_wg_halves": [round(float(nfront[:grid // 2].mean()), 1),
+                                              round(float(nfront[grid // 2:].mean()), 1)],
+           "lookahead_us_per_wg_halves": [round(float(refr[:grid // 2].mean()) / 100, 2),
+                                          round(float(refr[grid // 2:].mean()) / 100, 2)],
            "busy_frac_first_half_second_half": [round(float(busy_frac[:half].mean()), 3),
                                                 round(float(busy_frac[half:].mean()), 3)],
            "event_us_per_step": round(ms * 1e3 / STEPS, 3),
