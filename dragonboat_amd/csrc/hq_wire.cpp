@@ -181,7 +181,11 @@ inline bool varint_at(const uint8_t *&p, const uint8_t *end, uint64_t &v) {
 inline bool decode_marshal_order(const uint8_t *p, const uint8_t *end, Rec &r, uint64_t &cluster,
                                  uint32_t &entries) {
     uint64_t v[10];
-    for (uint32_t f = 0; f < 10; ++f) {            // fields 1-10: tag (f + 1) << 3, a varint
+    // fields 1-10: tag (f + 1) << 3, a varint — unrolled, so that each field's tag is a constant
+    // and each field's varint length has a branch of its own to predict (the lengths differ by
+    // field and repeat from message to message)
+#pragma GCC unroll 10
+    for (uint32_t f = 0; f < 10; ++f) {
         if (p >= end || *p != (uint8_t)((f + 1) << 3)) return false;
         if (++p >= end || !varint_at(p, end, v[f])) return false;
     }
@@ -219,6 +223,20 @@ int parse_batch(const uint8_t *bytes, size_t len, hq_wire_batch_info *bi, uint64
     *count = 0;
     Reader r{bytes, bytes + len};
     while (r.p < r.end) {
+        // the common case first: a Message (tag 0x0a) shorter than 128 bytes
+        if (r.end - r.p >= 2 && r.p[0] == 0x0a && r.p[1] < 0x80) {
+            const uint64_t n = r.p[1];
+            if ((uint64_t)(r.end - r.p - 2) < n) {
+                r.err = "unexpected end of data in a length-delimited field";
+                break;
+            }
+            const uint8_t *m = r.p + 2;
+            r.p = m + n;
+            const int rc = sink(m, (size_t)n);
+            if (rc) return rc;
+            ++*count;
+            continue;
+        }
         uint64_t tag;
         if (!r.varint(tag)) break;
         const uint32_t field = (uint32_t)(tag >> 3), wt = (uint32_t)(tag & 7);
