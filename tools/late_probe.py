@@ -11,6 +11,9 @@ host had queued it). One step5-shaped worker (W = 1, 1 M leader groups), STEPS s
          time), then the step alone (dev) and then the step beside the encode (conc) — the row
          is the conc step's
   busy   as gap, the GPU idle for GAP s while the encode threads run (the replays' CPU load)
+  churn  as the bench's second step leg: CHURN workers opened, stepped once together and closed
+         (the first leg's teardown), then fresh workers stepped alone and beside the encode as in
+         `gap` without the gap; CHURN_ROUNDS times
 
 Per mode: the start lag of every step (the wait beyond the device's own span: poll + sleep -
 span), how many steps started > 0.5 ms late, the worst, and the e2e p50 / p99. Prints one JSON
@@ -53,6 +56,25 @@ print(json.dumps({"G": G, "steps": STEPS, "encode_threads": enc_threads,
                   "cpus": bench.host_cores()}), flush=True)
 
 
+def churn():
+    """CHURN workers of the same groups opened, stepped once as one jobs call (each its own
+    pinned stream copy) and closed."""
+    recs.set(0)                            # (slot 0 holds a fresh step-0 stream)
+    NB0[0] = batch["p0"].run(enc_threads)[0][1]
+    ws = []
+    for _ in range(int(os.environ.get("CHURN", 18))):
+        x = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True,
+                      ready_compact=True, ready_slots=True)
+        x.add_groups(g, m)
+        ws.append(x)
+    hq.StepJobs([(x, hq.SizedStream(None, bufs[0][1], ne, bufs[0][0][:NB0[0]])) for x in ws]).execute()
+    for x in ws:
+        x.close()
+
+
+NB0 = [0]
+
+
 def run_mode(mode):
     wk = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True,
                    ready_compact=True, ready_slots=True)
@@ -60,7 +82,7 @@ def run_mode(mode):
     wk.set_wait(pol, 50, 20, clock=True)
     wk.add_groups(g, m)
     wk2 = None
-    if mode in ("gap", "busy"):
+    if mode in ("gap", "busy", "churn"):
         wk2 = hq.Worker(0, nv, on_device=True, commit_column=True, commit_advance=True,
                         ready_compact=True, ready_slots=True)
         wk2.set_wait(pol, 50, 20, clock=True)
@@ -79,14 +101,17 @@ def run_mode(mode):
 
     recs.set(0)
     encode(0)
+    NB0[0] = nbytes[0]
     rows = []
-    for s in range((GAP_STEPS if mode in ("gap", "busy") else STEPS) + 3):
+    for s in range((GAP_STEPS if mode in ("gap", "busy", "churn") else STEPS) + 3):
         slot = s % 2
         recs.set(s + 1)
         j = job(slot)
-        if mode in ("gap", "busy"):
+        if mode in ("gap", "busy", "churn"):
             tg = time.perf_counter()
-            if mode == "gap":
+            if mode == "churn":
+                pass
+            elif mode == "gap":
                 time.sleep(GAP)
             else:
                 while time.perf_counter() - tg < GAP:
@@ -119,7 +144,7 @@ def run_mode(mode):
         span = (r["device_end_ticks"] - r["device_start_ticks"]) / 1e5 \
             if r["device_start_ticks"] and r["device_end_ticks"] else None
         wait = (r["wait_poll_ns"] + r["wait_sleep_ns"]) / 1e6
-        if s >= 3:
+        if s >= 3 or mode == "churn":      # (churn: the first steps after the teardown too)
             rows.append({"s": s - 3, "k": AB[s % len(AB)] if AB else None,
                          "e2e": dt * 1e3, "enc": enc * 1e3, "gpu": r["gpu_ns"] / 1e6,
                          "span": span, "wait": wait, "submit": r["pack_ns"] / 1e6,
@@ -144,6 +169,11 @@ def run_mode(mode):
 
 
 for md in MODES:
-    run_mode(md)
+    if md == "churn":
+        for _ in range(int(os.environ.get("CHURN_ROUNDS", 3))):
+            churn()
+            run_mode(md)
+    else:
+        run_mode(md)
 pool.shutdown()
 pin.close()
