@@ -1692,8 +1692,12 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
     del want_data, want_sizes
     n_events = len(rows.ev)
     timed = 0
-    for s in range(steps + STEP_WARM):
-        slot = s % 2
+    # The CPU replay of every step's rows first, then the device steps: the replay (GBs of host
+    # memory touched per step on up to all host cores) run between the device steps was followed,
+    # about once per full run, by a device step whose first kernel started 5-18 ms after it was
+    # queued (profiles/r06q/, r06l2/: never without the replay); a step worker has no replay
+    # beside it. The replay's own timing and digests are the same work in the same order.
+    for s in range(steps + STEP_WARM if cpus else 0):
         for nt, (b, ts, dg) in cpus.items():    # the CPU replay of the same rows
             t0 = time.perf_counter()
             tot = b.step(rows.groups, offsets, rows.ev, nthreads=nt)
@@ -1703,10 +1707,11 @@ def run_step_leg(d, G=1 << 20, steps=50, with_cpu=True, name="step"):
             dg.append((tot["commits"], tot["ready"],
                        (tot["committed_sum"] - prev_sum) & ((1 << 64) - 1),
                        tot["ready_digest"], tot["commit_digest"], tot["ready_order_digest"]))
-        if cpus:
-            prev_sum = tot["committed_sum"]
-        rows.set(s + 1)                # untimed: step s + 1's messages arrive
-        recs.set(s + 1)
+        prev_sum = tot["committed_sum"]
+        rows.set(s + 1)
+    for s in range(steps + STEP_WARM):
+        slot = s % 2
+        recs.set(s + 1)                # untimed: step s + 1's messages arrive
         for W in Ws:
             mo = modes[W]
             if s >= STEP_WARM:

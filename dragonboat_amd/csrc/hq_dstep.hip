@@ -1671,6 +1671,15 @@ namespace {
 int grow(hq_ctx *ctx, void **p, size_t *cap, size_t need, bool keep, const char *what) {
     if (need <= *cap) return HQ_OK;
     size_t want = need + need / 2;
+    // HQ_GROW_TRACE=1: each device regrowth on stderr (a hipMalloc + hipFree in a step's
+    // submission: the device synchronizes for the free)
+    static const bool trace = [] {
+        const char *v = std::getenv("HQ_GROW_TRACE");
+        return v && std::atoi(v) != 0;
+    }();
+    if (trace)
+        std::fprintf(stderr, "[hq grow] %s %zu -> %zu bytes at %.3f ms\n", what, *cap, want,
+                     now_ns() / 1e6);
     void *n = nullptr;
     int rc = hq::check_hip(ctx, hipMalloc(&n, want), what);
     if (rc) return rc;
