@@ -1642,6 +1642,9 @@ struct hq_dstep {
     // one copy's start-up gap overlaps the other's transfer) and its events
     hipStream_t copy2 = nullptr;
     hipEvent_t ev_in2[kMaxJobChunks] = {};
+    // the pinned bounce buffer of hq_dstep_put / _get (two halves) and each half's last copy
+    char *bounce = nullptr;
+    hipEvent_t bounce_ev[2] = {nullptr, nullptr};
     hipEvent_t ev_sync = nullptr;  // blocking-sync event: a waiting worker thread sleeps
     // timing events around a step's device work (hq_dstep_out::gpu_ns): the host's wait for a
     // step, less the GPU's time, is its wake-up and queueing delay
@@ -1867,6 +1870,9 @@ void hq_dstep_close(hq_dstep *d) {
     if (d->jobs_host) (void)hipHostFree(d->jobs_host);
     if (d->host_layout) (void)hipHostFree(d->host_layout);
     if (d->clock_host) (void)hipHostFree(d->clock_host);
+    if (d->bounce) (void)hipHostFree(d->bounce);
+    for (hipEvent_t e : d->bounce_ev)
+        if (e) (void)hipEventDestroy(e);
     for (hipStream_t cs : {d->copy, d->copy2}) {
         if (cs) {
             (void)hipStreamSynchronize(cs);
@@ -1881,6 +1887,58 @@ void hq_dstep_close(hq_dstep *d) {
     }
     delete d;
 }
+
+namespace {
+
+// The groups' state moves between the worker's own (pageable) vectors and the device through a
+// pinned bounce buffer, in halves of kBounce bytes: for a large pageable copy the HIP runtime pins
+// the caller's pages in place, and when those pages' mappings later change (the allocator handing
+// them back) the driver evicts and restores the process's queues — a device step queued meanwhile
+// started 5-24 ms late (profiles/r06l/)
+constexpr size_t kBounce = size_t(8) << 20;
+
+int bounce_ready(hq_dstep *d) {
+    if (d->bounce) return HQ_OK;
+    hq_ctx *ctx = d->ctx;
+    int rc = hq::check_hip(ctx, hipHostMalloc(reinterpret_cast<void **>(&d->bounce), 2 * kBounce,
+                                              hipHostMallocDefault), "hq_dstep bounce");
+    for (hipEvent_t &e : d->bounce_ev)
+        if (!rc) rc = hq::check_hip(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    return rc;
+}
+
+int put_staged(hq_dstep *d, void *dst, const void *src, size_t bytes, uint64_t *half) {
+    hq_ctx *ctx = d->ctx;
+    int rc = bounce_ready(d);
+    for (size_t off = 0; !rc && off < bytes; off += kBounce, ++*half) {
+        const size_t n = std::min(kBounce, bytes - off);
+        const int h = (int)(*half & 1);
+        char *b = d->bounce + h * kBounce;
+        // (the half's previous copy must have read it: its event, recorded behind that copy)
+        if (*half >= 2) rc = hq::check_hip(ctx, hipEventSynchronize(d->bounce_ev[h]), "hq_dstep_put");
+        if (rc) break;
+        std::memcpy(b, static_cast<const char *>(src) + off, n);
+        rc = hq::check_hip(ctx, hipMemcpyAsync(static_cast<char *>(dst) + off, b, n,
+                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
+        if (!rc) rc = hq::check_hip(ctx, hipEventRecord(d->bounce_ev[h], ctx->stream), "hq_dstep_put");
+    }
+    return rc;
+}
+
+int get_staged(hq_dstep *d, void *dst, const void *src, size_t bytes) {
+    hq_ctx *ctx = d->ctx;
+    int rc = bounce_ready(d);
+    for (size_t off = 0; !rc && off < bytes; off += kBounce) {
+        const size_t n = std::min(kBounce, bytes - off);
+        rc = hq::check_hip(ctx, hipMemcpyAsync(d->bounce, static_cast<const char *>(src) + off, n,
+                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
+        if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep_get");
+        if (!rc) std::memcpy(static_cast<char *>(dst) + off, d->bounce, n);
+    }
+    return rc;
+}
+
+}  // namespace
 
 int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, const hq_dread *r,
                  uint64_t m0, uint64_t nm, const hq_dmember *m) {
@@ -1925,16 +1983,10 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
                       "hq_dstep saved matches");
         if (!rc) d->mcap = std::min(mc / sizeof(hq_dmember), xn / 8);
     }
-    if (!rc && ng)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(d->groups + g0, g, ng * sizeof(hq_dgroup),
-                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
-    if (!rc && ng)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(d->reads + g0 * kDReads, r,
-                                               ng * kDReads * sizeof(hq_dread),
-                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
-    if (!rc && nm)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(d->members + m0, m, nm * sizeof(hq_dmember),
-                                               hipMemcpyHostToDevice, ctx->stream), "hq_dstep_put");
+    uint64_t half = 0;
+    if (!rc && ng) rc = put_staged(d, d->groups + g0, g, ng * sizeof(hq_dgroup), &half);
+    if (!rc && ng) rc = put_staged(d, d->reads + g0 * kDReads, r, ng * kDReads * sizeof(hq_dread), &half);
+    if (!rc && nm) rc = put_staged(d, d->members + m0, m, nm * sizeof(hq_dmember), &half);
     if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep_put");
     return rc;
 }
@@ -1942,16 +1994,9 @@ int hq_dstep_put(hq_dstep *d, uint64_t g0, uint64_t ng, const hq_dgroup *g, cons
 int hq_dstep_get(hq_dstep *d, uint64_t ng, hq_dgroup *g, hq_dread *r, uint64_t nm, hq_dmember *m) {
     hq_ctx *ctx = d->ctx;
     int rc = hq::check_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    if (!rc && ng)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(g, d->groups, ng * sizeof(hq_dgroup),
-                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
-    if (!rc && ng)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(r, d->reads, ng * kDReads * sizeof(hq_dread),
-                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
-    if (!rc && nm)
-        rc = hq::check_hip(ctx, hipMemcpyAsync(m, d->members, nm * sizeof(hq_dmember),
-                                               hipMemcpyDeviceToHost, ctx->stream), "hq_dstep_get");
-    if (!rc) rc = hq::check_hip(ctx, hipStreamSynchronize(ctx->stream), "hq_dstep_get");
+    if (!rc && ng) rc = get_staged(d, g, d->groups, ng * sizeof(hq_dgroup));
+    if (!rc && ng) rc = get_staged(d, r, d->reads, ng * kDReads * sizeof(hq_dread));
+    if (!rc && nm) rc = get_staged(d, m, d->members, nm * sizeof(hq_dmember));
     return rc;
 }
 
